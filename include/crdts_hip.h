@@ -1,0 +1,240 @@
+/*
+ * crdts_hip.h — C ABI of the MI355X batched CRDT merge engine.
+ *
+ * This is the drop-in boundary for ONE path of etsangsplk/rust-crdt (crate
+ * `crdts` 1.3.0): the state-based join
+ *
+ *     pub trait CvRDT { fn merge(&mut self, other: &Self); }   // src/traits.rs:9-12
+ *
+ * for VClock (src/vclock.rs:131-137), GCounter (src/gcounter.rs:58-62),
+ * PNCounter (src/pncounter.rs:90-95) and Orswot incl. deferred removes
+ * (src/orswot.rs:87-157, 195-211, 235-243). The reference merges ONE pair per
+ * call; every entry point here merges a BATCH of independent pairs
+ * (self[i] ⊔= other[i]) on one MI355X, with per-object results bit-exact with
+ * calling the reference `merge` on each pair.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only. Pointers named `d_*` are DEVICE pointers
+ *    (hipMalloc'd or torch tensors' data_ptr), `h_*` are host pointers.
+ *  - `stream` is a hipStream_t passed as void* (NULL = default stream).
+ *  - Return 0 on success, a negative CRDT_E* code otherwise. Nothing aborts.
+ *    Launches are asynchronous: argument errors are returned immediately,
+ *    record-level errors found by a kernel (non-canonical / oversized input)
+ *    are latched in the context and returned by crdt_ctx_status().
+ *  - The caller owns every buffer. A crdt_ctx owns only a small device status
+ *    word; distinct contexts may be used from distinct threads concurrently.
+ *  - Orientation is fixed and matters (Orswot merge is structurally
+ *    non-commutative, src/orswot.rs:98-103 vs :132-137):
+ *    output = self.merge(&other), exactly.
+ *
+ * Actors are interned by the caller to dense u32 ids in the same order as the
+ * reference's `Ord` on actors (BTreeMap order, src/vclock.rs:54-57); members
+ * are interned to u64 keys bijectively (the caller's intern table).
+ */
+#ifndef CRDTS_HIP_H
+#define CRDTS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CRDT_ABI_VERSION 1
+
+#define CRDT_OK 0
+#define CRDT_EINVAL (-1)     /* bad argument (null pointer, zero actors, misaligned) */
+#define CRDT_ENONCANON (-2)  /* an input record is not canonical / inconsistent     */
+#define CRDT_EHIP (-3)       /* HIP runtime error                                  */
+#define CRDT_ECAPACITY (-4)  /* output capacity too small                          */
+#define CRDT_ECOMM (-5)      /* RCCL / communicator error                          */
+#define CRDT_ENODEV (-6)     /* no usable gfx950 device                            */
+
+typedef struct crdt_ctx crdt_ctx;
+
+/* Context: binds a device and owns a device-side status word. */
+int crdt_ctx_create(crdt_ctx** out, int device);
+int crdt_ctx_destroy(crdt_ctx* ctx);
+/* Synchronizes `stream`, returns the first record-level error latched by any
+ * kernel launched through ctx since the last call (and clears it). */
+int crdt_ctx_status(crdt_ctx* ctx, void* stream);
+/* Number of objects rejected by the last kernels (cleared by ctx_status). */
+const char* crdt_strerror(int code);
+int crdt_abi_version(void);
+
+/* ------------------------------------------------------------------------ *
+ * Dense clocks and counters.
+ *
+ * Layout: row-major u64[n_obj][n_actors]; row i is one VClock / GCounter, slot
+ * a holds the counter of interned actor a, 0 = absent (canonical: the
+ * reference never stores a 0, `witness` src/vclock.rs:159-163).
+ *
+ * self[i] := pointwise max(self[i], other[i]), in place.
+ *   VClock::merge   src/vclock.rs:131-137   (witness loop == pointwise max)
+ *   GCounter::merge src/gcounter.rs:58-62   (delegates to VClock::merge)
+ *   PNCounter::merge src/pncounter.rs:90-95 (P and N rows: pass the [P|N]
+ *                    row of 2*n_actors slots, see crdt_pncounter_merge)
+ * ------------------------------------------------------------------------ */
+int crdt_vclock_dense_merge(crdt_ctx* ctx, uint64_t* d_self, const uint64_t* d_other,
+                            size_t n_obj, uint32_t n_actors, void* stream);
+int crdt_gcounter_merge(crdt_ctx* ctx, uint64_t* d_self, const uint64_t* d_other,
+                        size_t n_obj, uint32_t n_actors, void* stream);
+/* PNCounter row = P slots [0, n_actors) then N slots [n_actors, 2*n_actors). */
+int crdt_pncounter_merge(crdt_ctx* ctx, uint64_t* d_self, const uint64_t* d_other,
+                         size_t n_obj, uint32_t n_actors, void* stream);
+
+/* ------------------------------------------------------------------------ *
+ * Orswot canonical record (one object = one contiguous, self-describing
+ * record; a batch = a byte buffer + a u64 byte offset per object).
+ *
+ * The reference state is (src/orswot.rs:26-30)
+ *     clock:    VClock<A>
+ *     entries:  HashMap<M, VClock<A>>
+ *     deferred: HashMap<VClock<A>, HashSet<M>>
+ * and equality is structural (`#[derive(PartialEq)]`, src/orswot.rs:25). The
+ * record is the canonical form of that state: hash-map order is replaced by
+ * sorted order, so two states are equal iff their records are byte-equal.
+ *
+ * Record = header (32 B) followed by a MEMBER block and a DEFERRED block.
+ * Every section is densely packed; the member block is zero-padded to a
+ * multiple of 8 bytes and the record to a multiple of 16 bytes:
+ *   u64 clk_ctr [n_clk]      top clock, DENSE: n_clk == n_actors, 0 = absent
+ *   -- member block (entries: HashMap<M, VClock<A>>) --
+ *   u64 mem_key [n_mem]      member keys, strictly increasing
+ *   u64 dot_ctr [n_dot]      member clocks' counters, member-major
+ *   u32 dot_act [n_dot]      member clocks' actors, strictly increasing per member
+ *   u32 mem_dend[n_mem]      cumulative end of member m's dots (member m owns
+ *                            dots [mem_dend[m-1], mem_dend[m]), mem_dend[-1]=0)
+ *   (pad to 8)
+ *   -- deferred block (deferred: HashMap<VClock<A>, HashSet<M>>) --
+ *   u64 def_ctr [n_def_dot]  deferred clocks' counters, clock-major
+ *   u64 def_key [n_def_mem]  deferred member sets, clock-major, each strictly increasing
+ *   u32 def_act [n_def_dot]  deferred clocks' actors, strictly increasing per clock
+ *   u32 def_dend[n_def]      cumulative end of deferred clock d's dots
+ *   u32 def_mend[n_def]      cumulative end of deferred clock d's member keys
+ *   (pad to 16)
+ * Canonical: every counter stored in a run is > 0, every member clock, every
+ * deferred clock and every deferred member set is non-empty, and deferred
+ * clocks are strictly increasing in CLOCK ORDER = lexicographic order of their
+ * (actor, counter) sequences, a proper prefix ordering first.
+ * ------------------------------------------------------------------------ */
+typedef struct crdt_orswot_hdr {
+  uint32_t size;      /* record bytes (header included), multiple of 16 */
+  uint32_t n_clk;     /* dense top clock slots (== batch n_actors)      */
+  uint32_t n_mem;
+  uint32_t n_dot;
+  uint32_t n_def;
+  uint32_t n_def_dot;
+  uint32_t n_def_mem;
+  uint32_t flags;     /* must be 0 in ABI v1                              */
+} crdt_orswot_hdr;
+
+#define CRDT_ORSWOT_HDR_BYTES 32u
+#define CRDT_RECORD_ALIGN 16u
+
+/* Bytes of a record with these counts (header and padding included). */
+size_t crdt_orswot_record_bytes(uint32_t n_clk, uint32_t n_mem, uint32_t n_dot,
+                                uint32_t n_def, uint32_t n_def_dot, uint32_t n_def_mem);
+
+/* A batch of records: record i starts at d_base + d_off[i] (16-B aligned). */
+typedef struct crdt_orswot_batch {
+  const uint8_t* base;   /* device */
+  const uint64_t* off;   /* device, n_obj entries */
+  size_t n_obj;
+  size_t bytes;          /* extent of base, for bounds checks */
+} crdt_orswot_batch;
+
+/*
+ * out[i] := self[i].merge(&other[i])   — src/orswot.rs:87-157 incl.
+ * apply_deferred (:235-243) / apply_remove (:195-211).
+ *
+ * The output record i is written at d_out_base + d_out_off[i] where
+ * d_out_off[i] := self.off[i] + other.off[i] (written by the kernel). Because a
+ * merged record is never larger than the two inputs together, the output
+ * needs at most self.bytes + other.bytes bytes and no prefix scan: the output
+ * batch (d_out_base, d_out_off) is itself a valid input batch (it may have
+ * gaps between records; crdt_orswot_compact removes them).
+ * `n_actors` is the dense top-clock width shared by every record.
+ */
+int crdt_orswot_merge(crdt_ctx* ctx, const crdt_orswot_batch* self,
+                      const crdt_orswot_batch* other, uint8_t* d_out_base,
+                      uint64_t* d_out_off, size_t out_bytes, uint32_t n_actors,
+                      void* stream);
+
+/* Same with host buffers: H2D, merge, D2H, synchronous (PCIe-inclusive path
+ * used by a host `merge_batch(&mut [T], &[T])`). h_out_off receives offsets
+ * into h_out_base (compacted, so h_out_bytes >= sum of merged record sizes
+ * suffices; worst case h_self_bytes + h_other_bytes). */
+int crdt_orswot_merge_host(crdt_ctx* ctx, const uint8_t* h_self_base,
+                           const uint64_t* h_self_off, size_t self_bytes,
+                           const uint8_t* h_other_base, const uint64_t* h_other_off,
+                           size_t other_bytes, size_t n_obj, uint32_t n_actors,
+                           uint8_t* h_out_base, uint64_t* h_out_off, size_t h_out_bytes,
+                           size_t* h_out_used);
+
+/* Deep canonical-form check of a batch on the device (sortedness, non-zero
+ * counters, non-empty runs, section sizes). Result via crdt_ctx_status. */
+int crdt_orswot_validate(crdt_ctx* ctx, const crdt_orswot_batch* batch,
+                         uint32_t n_actors, void* stream);
+
+/* Remove gaps: copies records into d_dst contiguously; d_dst_off receives the
+ * new offsets. d_scratch needs crdt_orswot_compact_scratch_bytes(n_obj). */
+size_t crdt_orswot_compact_scratch_bytes(size_t n_obj);
+int crdt_orswot_compact(crdt_ctx* ctx, const crdt_orswot_batch* src, uint8_t* d_dst,
+                        uint64_t* d_dst_off, size_t dst_bytes, void* d_scratch,
+                        void* stream);
+
+/* ------------------------------------------------------------------------ *
+ * Host-side helpers (no device work).
+ * ------------------------------------------------------------------------ */
+
+/* Synthetic Orswot pair batches by op simulation (Orswot::apply,
+ * src/orswot.rs:61-85), identical for any sharding: object i uses the
+ * SplitMix64 stream seeded with (seed ^ i). Records for objects
+ * [first_obj, first_obj + n_obj) are produced by n_threads host threads.
+ * Two calls: first with h_*_base == NULL to get the byte totals, then with
+ * buffers of at least those sizes. */
+typedef struct crdt_orswot_gen_params {
+  uint32_t n_actors;         /* dense top-clock width (config 3: 16)            */
+  uint32_t member_universe;  /* distinct member keys per object (config 3: 64)  */
+  uint32_t ancestor_adds;    /* shared-history adds (config 3: 32)              */
+  uint32_t min_div_ops;      /* divergent ops per side, uniform in [min, max]   */
+  uint32_t max_div_ops;      /* (config 3: 4..16)                               */
+  uint32_t pct_add;          /* % of divergent ops that are adds (60)           */
+  uint32_t pct_rm_ctx;       /* % removes with a read ctx (30); rest = future ctx (10) */
+  uint32_t pct_shared_actor; /* % of objects where both sides add with one actor (5) */
+} crdt_orswot_gen_params;
+
+int crdt_orswot_generate(uint64_t seed, size_t first_obj, size_t n_obj,
+                         const crdt_orswot_gen_params* params, int n_threads,
+                         uint8_t* h_self_base, uint64_t* h_self_off, size_t* self_bytes,
+                         uint8_t* h_other_base, uint64_t* h_other_off, size_t* other_bytes);
+
+/* Dense synthetic counters: u64[n_obj][n_actors] rows for objects
+ * [first_obj, first_obj+n_obj), counter U[0, 2^bits) with `pct_zero` % zeros. */
+int crdt_dense_generate(uint64_t seed, size_t first_obj, size_t n_obj, uint32_t n_actors,
+                        uint32_t bits, uint32_t pct_zero, int n_threads, uint64_t* h_rows);
+
+/* Host op-path builder used to construct states (tests, KAT scripts): an
+ * opaque host Orswot with the reference's op semantics (src/orswot.rs:61-85,
+ * 195-211, 235-243), encoded to / decoded from canonical records. */
+typedef struct crdt_host_orswot crdt_host_orswot;
+crdt_host_orswot* crdt_host_orswot_new(void);
+crdt_host_orswot* crdt_host_orswot_clone(const crdt_host_orswot* o);
+void crdt_host_orswot_free(crdt_host_orswot* o);
+/* Op::Add { dot: (actor, counter), member }  (src/orswot.rs:66-79) */
+int crdt_host_orswot_apply_add(crdt_host_orswot* o, uint32_t actor, uint64_t counter,
+                               uint64_t member);
+/* Op::Rm { clock, member }  (src/orswot.rs:80-82) — clock as sorted runs */
+int crdt_host_orswot_apply_rm(crdt_host_orswot* o, uint64_t member, const uint32_t* actors,
+                              const uint64_t* counters, uint32_t n);
+/* Encode into h_rec (capacity cap); returns bytes written or a negative code. */
+long crdt_host_orswot_encode(const crdt_host_orswot* o, uint32_t n_actors, uint8_t* h_rec,
+                             size_t cap);
+crdt_host_orswot* crdt_host_orswot_decode(const uint8_t* h_rec, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CRDTS_HIP_H */

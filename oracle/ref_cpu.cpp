@@ -1,0 +1,586 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY.
+//
+// CPU restatement of the etsangsplk/rust-crdt (crate `crdts` 1.3.0) state-based
+// join for VClock, GCounter, PNCounter and Orswot (incl. deferred removes).
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+// load this library, and only as the checker / CPU baseline — the product
+// path (rust-crdt_amd/) never links or calls it.
+//
+// It mirrors the reference's data structures so that it is also a fair CPU
+// baseline ("kind": "port"):
+//   BTreeMap<A,u64>            -> std::map<uint32_t,uint64_t>     (src/vclock.rs:54-57)
+//   HashMap<M,VClock>          -> std::unordered_map<uint64_t,VClock> (src/orswot.rs:28)
+//   HashMap<VClock,HashSet<M>> -> std::unordered_map<VClock,std::unordered_set<uint64_t>>
+//                                                                 (src/orswot.rs:29)
+// and the reference's clone pattern in Orswot::merge (src/orswot.rs:90-93).
+//
+// Parity pinning: the reference cannot be compiled in this image (no
+// cargo/rustc), so this restatement is pinned by the reference's own
+// known-answer tests and properties, transcribed into tests/golden/*.json and
+// run by tests/test_oracle_kat.py, and cross-checked against a second,
+// independent pure-Python restatement (oracle/crdts_ref.py).
+//
+// Canonical record encoding follows include/crdts_hip.h (the boundary spec);
+// this file has its own encoder/decoder, independent of the product's.
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "../include/crdts_hip.h"
+
+namespace oracle {
+
+typedef uint32_t Actor;
+typedef uint64_t Counter;  // src/vclock.rs:23
+typedef uint64_t Member;
+
+// ---------------------------------------------------------------- VClock
+// src/vclock.rs:54-57
+struct VClock {
+  std::map<Actor, Counter> dots;
+
+  bool operator==(const VClock& o) const { return dots == o.dots; }  // derive(PartialEq) :53
+
+  // get — src/vclock.rs:206-210
+  Counter get(Actor a) const {
+    auto it = dots.find(a);
+    return it == dots.end() ? 0 : it->second;
+  }
+  // witness — src/vclock.rs:159-163
+  void witness(Actor a, Counter c) {
+    if (!(get(a) >= c)) dots[a] = c;
+  }
+  // CvRDT::merge — src/vclock.rs:131-137
+  void merge(const VClock& other) {
+    for (const auto& kv : other.dots) witness(kv.first, kv.second);
+  }
+  // PartialOrd::partial_cmp — src/vclock.rs:59-71.
+  // Returns 0 Equal, 1 Greater, -1 Less, 2 None.
+  int partial_cmp(const VClock& other) const {
+    if (*this == other) return 0;
+    bool all = true;
+    for (const auto& kv : other.dots)
+      if (!(get(kv.first) >= kv.second)) { all = false; break; }
+    if (all) return 1;
+    all = true;
+    for (const auto& kv : dots)
+      if (!(other.get(kv.first) >= kv.second)) { all = false; break; }
+    if (all) return -1;
+    return 2;
+  }
+  // `a <= b` on PartialOrd: Some(Less) | Some(Equal)
+  bool le(const VClock& other) const {
+    int c = partial_cmp(other);
+    return c == 0 || c == -1;
+  }
+  bool is_empty() const { return dots.empty(); }  // :213-215
+  // intersection — src/vclock.rs:219-228
+  VClock intersection(const VClock& other) const {
+    VClock r;
+    for (const auto& kv : dots)
+      if (other.get(kv.first) == kv.second) r.dots.emplace(kv.first, kv.second);
+    return r;
+  }
+  // subtract — src/vclock.rs:236-242
+  void subtract(const VClock& other) {
+    for (const auto& kv : other.dots)
+      if (kv.second >= get(kv.first)) dots.erase(kv.first);
+  }
+  // inc — src/vclock.rs:182-185
+  Counter inc(Actor a) const { return get(a) + 1; }
+};
+
+struct VClockHash {
+  size_t operator()(const VClock& v) const {
+    uint64_t h = 1469598103934665603ull;
+    for (const auto& kv : v.dots) {
+      h ^= kv.first; h *= 1099511628211ull;
+      h ^= kv.second; h *= 1099511628211ull;
+    }
+    return (size_t)h;
+  }
+};
+
+// ---------------------------------------------------------------- Orswot
+// src/orswot.rs:26-30
+struct Orswot {
+  VClock clock;
+  std::unordered_map<Member, VClock> entries;
+  std::unordered_map<VClock, std::unordered_set<Member>, VClockHash> deferred;
+
+  // CmRDT::apply, Op::Add — src/orswot.rs:66-79
+  void apply_add(Actor actor, Counter counter, Member member) {
+    if (clock.get(actor) >= counter) return;  // already seen
+    entries[member].witness(actor, counter);  // entry().or_insert_with(VClock::new).apply(dot)
+    clock.witness(actor, counter);
+    apply_deferred();
+  }
+  // CmRDT::apply, Op::Rm — src/orswot.rs:80-82
+  void apply_rm(Member member, const VClock& rm_clock) { apply_remove(member, rm_clock); }
+
+  // apply_remove — src/orswot.rs:195-211
+  void apply_remove(Member member, const VClock& rm_clock) {
+    if (!rm_clock.le(clock)) {
+      std::unordered_set<Member> drops;
+      auto it = deferred.find(rm_clock);
+      if (it != deferred.end()) { drops = std::move(it->second); deferred.erase(it); }
+      drops.insert(member);
+      deferred.emplace(rm_clock, std::move(drops));
+    }
+    auto it = entries.find(member);
+    if (it != entries.end()) {
+      VClock existing = std::move(it->second);
+      entries.erase(it);
+      existing.subtract(rm_clock);
+      if (!existing.is_empty()) entries.emplace(member, std::move(existing));
+    }
+  }
+
+  // apply_deferred — src/orswot.rs:235-243
+  void apply_deferred() {
+    auto d = deferred;  // clone
+    deferred.clear();
+    for (const auto& kv : d)
+      for (Member m : kv.second) apply_remove(m, kv.first);
+  }
+
+  // CvRDT::merge — src/orswot.rs:87-157 (clone pattern of :90, :92, :93 kept)
+  void merge(const Orswot& other) {
+    auto other_remaining = other.entries;                 // :90
+    std::unordered_map<Member, VClock> keep;              // :91
+    auto self_entries = entries;                          // :92
+    for (auto& kv : self_entries) {
+      const Member entry = kv.first;
+      VClock& eclock = kv.second;
+      auto oit = other.entries.find(entry);
+      if (oit == other.entries.end()) {                   // :94-104
+        if (eclock.le(other.clock)) {
+          // other has seen this entry and dropped it
+        } else {
+          keep.emplace(entry, eclock);
+        }
+      } else {                                            // :105-128
+        VClock other_entry_clock = oit->second;           // .cloned() :93
+        VClock common = eclock.intersection(other_entry_clock);  // :109
+        eclock.subtract(common);                          // :110
+        other_entry_clock.subtract(common);               // :111
+        eclock.subtract(other.clock);                     // :112
+        other_entry_clock.subtract(clock);                // :113 (pre-merge self.clock)
+        common.merge(eclock);                             // :115
+        common.merge(other_entry_clock);                  // :116
+        if (!common.is_empty()) keep.emplace(entry, std::move(common));  // :120-125
+        other_remaining.erase(entry);                     // :127
+      }
+    }
+    for (auto& kv : other_remaining) {                    // :132-138
+      VClock c = kv.second;
+      c.subtract(clock);
+      if (!c.is_empty()) keep.emplace(kv.first, std::move(c));
+    }
+    for (const auto& kv : other.deferred) {               // :141-148
+      std::unordered_set<Member> ours;
+      auto it = deferred.find(kv.first);
+      if (it != deferred.end()) { ours = std::move(it->second); deferred.erase(it); }
+      for (Member e : kv.second) ours.insert(e);
+      deferred.emplace(kv.first, std::move(ours));
+    }
+    entries = std::move(keep);                            // :150
+    clock.merge(other.clock);                             // :153
+    apply_deferred();                                     // :155
+  }
+};
+
+// GCounter — src/gcounter.rs:26-28; merge :58-62
+struct GCounter {
+  VClock inner;
+  void merge(const GCounter& o) { inner.merge(o.inner); }
+  uint64_t value() const {  // :76-78 (wrapping like release-mode Rust u64 add)
+    uint64_t s = 0;
+    for (const auto& kv : inner.dots) s += kv.second;
+    return s;
+  }
+};
+// PNCounter — src/pncounter.rs:33-36; merge :90-95
+struct PNCounter {
+  GCounter p, n;
+  void merge(const PNCounter& o) { p.merge(o.p); n.merge(o.n); }
+  int64_t value() const { return (int64_t)p.value() - (int64_t)n.value(); }  // :117-119
+};
+
+// ------------------------------------------------- canonical record codec
+static inline size_t pad16(size_t x) { return (x + 15) & ~size_t(15); }
+
+size_t record_bytes(uint32_t n_clk, uint32_t n_mem, uint32_t n_dot, uint32_t n_def,
+                    uint32_t n_def_dot, uint32_t n_def_mem) {
+  size_t b = CRDT_ORSWOT_HDR_BYTES + 8ull * n_clk;
+  b += 12ull * ((size_t)n_mem + n_dot);                 // member block
+  b = (b + 7) & ~size_t(7);
+  b += 12ull * n_def_dot + 8ull * n_def_mem + 8ull * n_def;  // deferred block
+  return pad16(b);
+}
+
+// Section pointers of a record (layout: include/crdts_hip.h).
+struct Sections {
+  uint64_t *clk, *key, *dctr, *fctr, *fkey;
+  uint32_t *dact, *mdend, *fact, *fdend, *fmend;
+};
+static Sections sections(uint8_t* rec, const crdt_orswot_hdr& h) {
+  Sections s;
+  s.clk = (uint64_t*)(rec + CRDT_ORSWOT_HDR_BYTES);
+  s.key = s.clk + h.n_clk;
+  s.dctr = s.key + h.n_mem;
+  s.dact = (uint32_t*)(s.dctr + h.n_dot);
+  s.mdend = s.dact + h.n_dot;
+  size_t mb = (size_t)((uint8_t*)(s.mdend + h.n_mem) - rec);
+  mb = (mb + 7) & ~size_t(7);
+  s.fctr = (uint64_t*)(rec + mb);
+  s.fkey = s.fctr + h.n_def_dot;
+  s.fact = (uint32_t*)(s.fkey + h.n_def_mem);
+  s.fdend = s.fact + h.n_def_dot;
+  s.fmend = s.fdend + h.n_def;
+  return s;
+}
+
+static bool clock_less(const VClock& a, const VClock& b) {
+  // CLOCK ORDER: lexicographic over the (actor, counter) sequence, prefix first.
+  auto ia = a.dots.begin(), ib = b.dots.begin();
+  for (; ia != a.dots.end() && ib != b.dots.end(); ++ia, ++ib) {
+    if (ia->first != ib->first) return ia->first < ib->first;
+    if (ia->second != ib->second) return ia->second < ib->second;
+  }
+  return ia == a.dots.end() && ib != b.dots.end();
+}
+
+// Encode; returns bytes or negative code. Dense clock of n_actors slots.
+long encode(const Orswot& o, uint32_t n_actors, uint8_t* out, size_t cap) {
+  std::vector<std::pair<Member, const VClock*>> ents;
+  for (const auto& kv : o.entries) ents.emplace_back(kv.first, &kv.second);
+  std::sort(ents.begin(), ents.end(),
+            [](const auto& x, const auto& y) { return x.first < y.first; });
+  std::vector<std::pair<const VClock*, std::vector<Member>>> defs;
+  for (const auto& kv : o.deferred) {
+    std::vector<Member> ms(kv.second.begin(), kv.second.end());
+    std::sort(ms.begin(), ms.end());
+    defs.emplace_back(&kv.first, std::move(ms));
+  }
+  std::sort(defs.begin(), defs.end(),
+            [](const auto& x, const auto& y) { return clock_less(*x.first, *y.first); });
+  uint32_t n_mem = (uint32_t)ents.size(), n_dot = 0, n_def = (uint32_t)defs.size(),
+           n_def_dot = 0, n_def_mem = 0;
+  for (auto& e : ents) n_dot += (uint32_t)e.second->dots.size();
+  for (auto& d : defs) {
+    n_def_dot += (uint32_t)d.first->dots.size();
+    n_def_mem += (uint32_t)d.second.size();
+  }
+  // Dense top clock: every interned actor id (top clock, member clocks,
+  // deferred clocks) must be < n_actors.
+  for (auto& kv : o.clock.dots)
+    if (kv.first >= n_actors) return CRDT_EINVAL;
+  for (auto& e : ents)
+    for (auto& kv : e.second->dots)
+      if (kv.first >= n_actors) return CRDT_EINVAL;
+  for (auto& d : defs)
+    for (auto& kv : d.first->dots)
+      if (kv.first >= n_actors) return CRDT_EINVAL;
+  size_t bytes = record_bytes(n_actors, n_mem, n_dot, n_def, n_def_dot, n_def_mem);
+  if (bytes > cap) return CRDT_ECAPACITY;
+  std::memset(out, 0, bytes);
+  crdt_orswot_hdr h = {(uint32_t)bytes, n_actors, n_mem, n_dot, n_def, n_def_dot, n_def_mem, 0};
+  std::memcpy(out, &h, sizeof h);
+  Sections S = sections(out, h);
+  uint64_t *clk = S.clk, *key = S.key, *dctr = S.dctr, *fctr = S.fctr, *fkey = S.fkey;
+  uint32_t *dact = S.dact, *mdend = S.mdend, *fact = S.fact, *fdend = S.fdend, *fmend = S.fmend;
+  for (auto& kv : o.clock.dots) clk[kv.first] = kv.second;
+  uint32_t d = 0;
+  for (uint32_t m = 0; m < n_mem; ++m) {
+    key[m] = ents[m].first;
+    for (auto& kv : ents[m].second->dots) { dact[d] = kv.first; dctr[d] = kv.second; ++d; }
+    mdend[m] = d;
+  }
+  uint32_t fd = 0, fm = 0;
+  for (uint32_t k = 0; k < n_def; ++k) {
+    for (auto& kv : defs[k].first->dots) { fact[fd] = kv.first; fctr[fd] = kv.second; ++fd; }
+    for (Member mm : defs[k].second) fkey[fm++] = mm;
+    fdend[k] = fd;
+    fmend[k] = fm;
+  }
+  return (long)bytes;
+}
+
+bool decode(const uint8_t* rec, size_t avail, Orswot& o) {
+  if (avail < CRDT_ORSWOT_HDR_BYTES) return false;
+  crdt_orswot_hdr h;
+  std::memcpy(&h, rec, sizeof h);
+  size_t bytes = record_bytes(h.n_clk, h.n_mem, h.n_dot, h.n_def, h.n_def_dot, h.n_def_mem);
+  if (bytes != h.size || bytes > avail || h.flags != 0) return false;
+  Sections S = sections(const_cast<uint8_t*>(rec), h);
+  const uint64_t *clk = S.clk, *key = S.key, *dctr = S.dctr, *fctr = S.fctr, *fkey = S.fkey;
+  const uint32_t *dact = S.dact, *mdend = S.mdend, *fact = S.fact, *fdend = S.fdend,
+                 *fmend = S.fmend;
+  o = Orswot();
+  for (uint32_t a = 0; a < h.n_clk; ++a)
+    if (clk[a]) o.clock.dots.emplace(a, clk[a]);
+  uint32_t d0 = 0;
+  for (uint32_t m = 0; m < h.n_mem; ++m) {
+    if (mdend[m] < d0 || mdend[m] > h.n_dot) return false;
+    VClock c;
+    for (uint32_t d = d0; d < mdend[m]; ++d) c.dots[dact[d]] = dctr[d];
+    o.entries[key[m]] = std::move(c);
+    d0 = mdend[m];
+  }
+  uint32_t f0 = 0, k0 = 0;
+  for (uint32_t k = 0; k < h.n_def; ++k) {
+    if (fdend[k] < f0 || fdend[k] > h.n_def_dot || fmend[k] < k0 || fmend[k] > h.n_def_mem)
+      return false;
+    VClock c;
+    for (uint32_t d = f0; d < fdend[k]; ++d) c.dots[fact[d]] = fctr[d];
+    auto& s = o.deferred[c];
+    for (uint32_t j = k0; j < fmend[k]; ++j) s.insert(fkey[j]);
+    f0 = fdend[k];
+    k0 = fmend[k];
+  }
+  return true;
+}
+
+template <class F>
+static void parallel_for(size_t n, int threads, F f) {
+  if (threads <= 1 || n < 2) {
+    f(0, n);
+    return;
+  }
+  std::vector<std::thread> ts;
+  size_t chunk = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; ++t) {
+    size_t b = t * chunk, e = std::min(n, b + chunk);
+    if (b >= e) break;
+    ts.emplace_back(f, b, e);
+  }
+  for (auto& t : ts) t.join();
+}
+
+static VClock row_to_vclock(const uint64_t* row, uint32_t n) {
+  VClock v;
+  for (uint32_t a = 0; a < n; ++a)
+    if (row[a]) v.dots.emplace(a, row[a]);
+  return v;
+}
+static void vclock_to_row(const VClock& v, uint64_t* row, uint32_t n) {
+  std::memset(row, 0, 8ull * n);
+  for (auto& kv : v.dots) row[kv.first] = kv.second;
+}
+
+}  // namespace oracle
+
+using namespace oracle;
+
+extern "C" {
+
+size_t orc_record_bytes(uint32_t n_clk, uint32_t n_mem, uint32_t n_dot, uint32_t n_def,
+                        uint32_t n_def_dot, uint32_t n_def_mem) {
+  return record_bytes(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem);
+}
+
+// Merge a batch of record pairs; output compacted (out_off computed here).
+// Returns 0, or a negative code (first failing object index in *bad).
+int orc_orswot_merge_batch(const uint8_t* lb, const uint64_t* loff, size_t lbytes,
+                           const uint8_t* rb, const uint64_t* roff, size_t rbytes, size_t n,
+                           uint32_t n_actors, uint8_t* ob, uint64_t* ooff, size_t ocap,
+                           int threads, int64_t* bad) {
+  std::vector<std::vector<uint8_t>> outs(n);
+  std::vector<int> err(n, 0);
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) {
+      Orswot L, R;
+      if (!decode(lb + loff[i], lbytes - loff[i], L) || !decode(rb + roff[i], rbytes - roff[i], R)) {
+        err[i] = CRDT_ENONCANON;
+        continue;
+      }
+      L.merge(R);
+      std::vector<uint8_t> buf(record_bytes(n_actors, L.entries.size(), 0, 0, 0, 0) + 65536);
+      long got;
+      while ((got = encode(L, n_actors, buf.data(), buf.size())) == CRDT_ECAPACITY)
+        buf.resize(buf.size() * 2);
+      if (got < 0) { err[i] = (int)got; continue; }
+      buf.resize(got);
+      outs[i] = std::move(buf);
+    }
+  });
+  size_t pos = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (err[i]) { if (bad) *bad = (int64_t)i; return err[i]; }
+    if (pos + outs[i].size() > ocap) { if (bad) *bad = (int64_t)i; return CRDT_ECAPACITY; }
+    std::memcpy(ob + pos, outs[i].data(), outs[i].size());
+    ooff[i] = pos;
+    pos += outs[i].size();
+  }
+  return 0;
+}
+
+// CPU baseline: decode untimed, time only L[i].merge(&R[i]) for i in [0, n)
+// over `threads` std::threads (static partition, standing in for rayon
+// par_iter over objects). Returns seconds of the merge loop.
+double orc_orswot_bench(const uint8_t* lb, const uint64_t* loff, size_t lbytes,
+                        const uint8_t* rb, const uint64_t* roff, size_t rbytes, size_t n,
+                        int threads) {
+  std::vector<Orswot> L(n), R(n);
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) {
+      decode(lb + loff[i], lbytes - loff[i], L[i]);
+      decode(rb + roff[i], rbytes - roff[i], R[i]);
+    }
+  });
+  auto t0 = std::chrono::steady_clock::now();
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) L[i].merge(R[i]);
+  });
+  auto t1 = std::chrono::steady_clock::now();
+  // keep results alive so the loop is not elided
+  volatile size_t sink = 0;
+  for (size_t i = 0; i < n; i += 997) sink += L[i].entries.size();
+  (void)sink;
+  std::vector<Orswot>().swap(L);
+  return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// Dense VClock/GCounter rows, through the BTreeMap-style VClock::merge.
+int orc_dense_merge(uint64_t* self, const uint64_t* other, size_t n, uint32_t n_actors,
+                    int threads) {
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) {
+      VClock a = row_to_vclock(self + i * n_actors, n_actors);
+      VClock o = row_to_vclock(other + i * n_actors, n_actors);
+      a.merge(o);
+      vclock_to_row(a, self + i * n_actors, n_actors);
+    }
+  });
+  return 0;
+}
+// PNCounter rows [P|N], 2*n_actors slots; via PNCounter::merge.
+int orc_pncounter_merge(uint64_t* self, const uint64_t* other, size_t n, uint32_t n_actors,
+                        int threads) {
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) {
+      uint64_t* s = self + i * 2ull * n_actors;
+      const uint64_t* o = other + i * 2ull * n_actors;
+      PNCounter a, c;
+      a.p.inner = row_to_vclock(s, n_actors);
+      a.n.inner = row_to_vclock(s + n_actors, n_actors);
+      c.p.inner = row_to_vclock(o, n_actors);
+      c.n.inner = row_to_vclock(o + n_actors, n_actors);
+      a.merge(c);
+      vclock_to_row(a.p.inner, s, n_actors);
+      vclock_to_row(a.n.inner, s + n_actors, n_actors);
+    }
+  });
+  return 0;
+}
+double orc_dense_bench(const uint64_t* self, const uint64_t* other, size_t n, uint32_t n_actors,
+                       int threads) {
+  std::vector<GCounter> A(n), B(n);
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) {
+      A[i].inner = row_to_vclock(self + i * n_actors, n_actors);
+      B[i].inner = row_to_vclock(other + i * n_actors, n_actors);
+    }
+  });
+  auto t0 = std::chrono::steady_clock::now();
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) A[i].merge(B[i]);
+  });
+  auto t1 = std::chrono::steady_clock::now();
+  return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// --------------------------------------- object handles for KAT scripts
+void* orc_obj_new() { return new Orswot(); }
+void* orc_obj_clone(const void* h) { return new Orswot(*(const Orswot*)h); }
+void orc_obj_free(void* h) { delete (Orswot*)h; }
+void orc_obj_apply_add(void* h, uint32_t actor, uint64_t counter, uint64_t member) {
+  ((Orswot*)h)->apply_add(actor, counter, member);
+}
+void orc_obj_apply_rm(void* h, uint64_t member, const uint32_t* act, const uint64_t* ctr,
+                      uint32_t n) {
+  VClock c;
+  for (uint32_t i = 0; i < n; ++i) c.witness(act[i], ctr[i]);  // From<Vec<(A,u64)>>, :267-271
+  ((Orswot*)h)->apply_rm(member, c);
+}
+void orc_obj_merge(void* dst, const void* src) { ((Orswot*)dst)->merge(*(const Orswot*)src); }
+long orc_obj_encode(const void* h, uint32_t n_actors, uint8_t* out, size_t cap) {
+  return encode(*(const Orswot*)h, n_actors, out, cap);
+}
+void* orc_obj_decode(const uint8_t* rec, size_t bytes) {
+  Orswot* o = new Orswot();
+  if (!decode(rec, bytes, *o)) { delete o; return nullptr; }
+  return o;
+}
+long orc_obj_deferred_len(const void* h) { return (long)((const Orswot*)h)->deferred.size(); }
+// value(): sorted member keys; returns count (writes up to cap).
+long orc_obj_value(const void* h, uint64_t* out, size_t cap) {
+  const Orswot* o = (const Orswot*)h;
+  std::vector<uint64_t> ks;
+  for (auto& kv : o->entries) ks.push_back(kv.first);
+  std::sort(ks.begin(), ks.end());
+  for (size_t i = 0; i < ks.size() && i < cap; ++i) out[i] = ks[i];
+  return (long)ks.size();
+}
+// contains(m).rm_clock: entry clock dots; returns n or -1 if absent.
+long orc_obj_entry(const void* h, uint64_t member, uint32_t* act, uint64_t* ctr, size_t cap) {
+  const Orswot* o = (const Orswot*)h;
+  auto it = o->entries.find(member);
+  if (it == o->entries.end()) return -1;
+  size_t i = 0;
+  for (auto& kv : it->second.dots) {
+    if (i < cap) { act[i] = kv.first; ctr[i] = kv.second; }
+    ++i;
+  }
+  return (long)i;
+}
+long orc_obj_clock(const void* h, uint32_t* act, uint64_t* ctr, size_t cap) {
+  const Orswot* o = (const Orswot*)h;
+  size_t i = 0;
+  for (auto& kv : o->clock.dots) {
+    if (i < cap) { act[i] = kv.first; ctr[i] = kv.second; }
+    ++i;
+  }
+  return (long)i;
+}
+
+// --------------------------------------- VClock primitives for KATs
+// Clocks passed as (actor[], counter[], n) built with witness (From<Vec>).
+static VClock mk(const uint32_t* a, const uint64_t* c, uint32_t n) {
+  VClock v;
+  for (uint32_t i = 0; i < n; ++i) v.witness(a[i], c[i]);
+  return v;
+}
+static long dump(const VClock& v, uint32_t* a, uint64_t* c, size_t cap) {
+  size_t i = 0;
+  for (auto& kv : v.dots) {
+    if (i < cap) { a[i] = kv.first; c[i] = kv.second; }
+    ++i;
+  }
+  return (long)i;
+}
+// op: 0 merge, 1 subtract, 2 intersection. Result written to (ra, rc).
+long orc_vclock_binop(int op, const uint32_t* aa, const uint64_t* ac, uint32_t an,
+                      const uint32_t* ba, const uint64_t* bc, uint32_t bn, uint32_t* ra,
+                      uint64_t* rc, size_t cap) {
+  VClock a = mk(aa, ac, an), b = mk(ba, bc, bn);
+  if (op == 0) a.merge(b);
+  else if (op == 1) a.subtract(b);
+  else if (op == 2) a = a.intersection(b);
+  else return CRDT_EINVAL;
+  return dump(a, ra, rc, cap);
+}
+int orc_vclock_partial_cmp(const uint32_t* aa, const uint64_t* ac, uint32_t an,
+                           const uint32_t* ba, const uint64_t* bc, uint32_t bn) {
+  return mk(aa, ac, an).partial_cmp(mk(ba, bc, bn));
+}
+
+}  // extern "C"

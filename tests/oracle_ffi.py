@@ -1,0 +1,213 @@
+"""ctypes binding of the CPU oracle (oracle/ref_cpu.cpp) — test infrastructure.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "_build", "liboracle.so")
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    src = os.path.join(ORACLE_DIR, "ref_cpu.cpp")
+    if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < os.path.getmtime(src):
+        build()
+    L = C.CDLL(ORACLE_SO)
+    P, U8P, U64P, U32P = C.c_void_p, C.POINTER(C.c_uint8), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)
+    L.orc_record_bytes.restype = C.c_size_t
+    L.orc_record_bytes.argtypes = [C.c_uint32] * 6
+    L.orc_orswot_merge_batch.restype = C.c_int
+    L.orc_orswot_merge_batch.argtypes = [P, P, C.c_size_t, P, P, C.c_size_t, C.c_size_t, C.c_uint32,
+                                         P, P, C.c_size_t, C.c_int, C.POINTER(C.c_int64)]
+    L.orc_orswot_bench.restype = C.c_double
+    L.orc_orswot_bench.argtypes = [P, P, C.c_size_t, P, P, C.c_size_t, C.c_size_t, C.c_int]
+    L.orc_dense_merge.restype = C.c_int
+    L.orc_dense_merge.argtypes = [P, P, C.c_size_t, C.c_uint32, C.c_int]
+    L.orc_pncounter_merge.restype = C.c_int
+    L.orc_pncounter_merge.argtypes = [P, P, C.c_size_t, C.c_uint32, C.c_int]
+    L.orc_dense_bench.restype = C.c_double
+    L.orc_dense_bench.argtypes = [P, P, C.c_size_t, C.c_uint32, C.c_int]
+    L.orc_obj_new.restype = P
+    L.orc_obj_clone.restype = P
+    L.orc_obj_clone.argtypes = [P]
+    L.orc_obj_free.argtypes = [P]
+    L.orc_obj_apply_add.argtypes = [P, C.c_uint32, C.c_uint64, C.c_uint64]
+    L.orc_obj_apply_rm.argtypes = [P, C.c_uint64, U32P, U64P, C.c_uint32]
+    L.orc_obj_merge.argtypes = [P, P]
+    L.orc_obj_encode.restype = C.c_long
+    L.orc_obj_encode.argtypes = [P, C.c_uint32, P, C.c_size_t]
+    L.orc_obj_decode.restype = P
+    L.orc_obj_decode.argtypes = [P, C.c_size_t]
+    L.orc_obj_deferred_len.restype = C.c_long
+    L.orc_obj_deferred_len.argtypes = [P]
+    L.orc_obj_value.restype = C.c_long
+    L.orc_obj_value.argtypes = [P, U64P, C.c_size_t]
+    L.orc_obj_entry.restype = C.c_long
+    L.orc_obj_entry.argtypes = [P, C.c_uint64, U32P, U64P, C.c_size_t]
+    L.orc_obj_clock.restype = C.c_long
+    L.orc_obj_clock.argtypes = [P, U32P, U64P, C.c_size_t]
+    L.orc_vclock_binop.restype = C.c_long
+    L.orc_vclock_binop.argtypes = [C.c_int, U32P, U64P, C.c_uint32, U32P, U64P, C.c_uint32, U32P, U64P,
+                                   C.c_size_t]
+    L.orc_vclock_partial_cmp.restype = C.c_int
+    L.orc_vclock_partial_cmp.argtypes = [U32P, U64P, C.c_uint32, U32P, U64P, C.c_uint32]
+    _lib = L
+    return L
+
+
+def _ptr(a):
+    return C.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def _clock_arrays(pairs):
+    a = (C.c_uint32 * max(1, len(pairs)))(*[int(x) for x, _ in pairs])
+    c = (C.c_uint64 * max(1, len(pairs)))(*[int(y) for _, y in pairs])
+    return a, c, len(pairs)
+
+
+def _dump(fn, *args):
+    cap = 4096
+    a = (C.c_uint32 * cap)()
+    c = (C.c_uint64 * cap)()
+    n = fn(*args, a, c, cap)
+    if n < 0:
+        return None
+    return [(int(a[i]), int(c[i])) for i in range(n)]
+
+
+# ------------------------------------------------------------- VClock KATs
+def vclock_binop(op, a, b):
+    code = {"merge": 0, "subtract": 1, "intersection": 2}[op]
+    aa, ac, an = _clock_arrays(a)
+    ba, bc, bn = _clock_arrays(b)
+    return _dump(lambda *r: lib().orc_vclock_binop(code, aa, ac, an, ba, bc, bn, *r))
+
+
+def vclock_partial_cmp(a, b):
+    aa, ac, an = _clock_arrays(a)
+    ba, bc, bn = _clock_arrays(b)
+    r = lib().orc_vclock_partial_cmp(aa, ac, an, ba, bc, bn)
+    return {0: "Equal", 1: "Greater", -1: "Less", 2: "None"}[r]
+
+
+# ------------------------------------------------------------- Orswot objects
+class OracleOrswot:
+    """Handle to an oracle Orswot (reference-like std::map/unordered_map)."""
+
+    def __init__(self, handle=None):
+        self.h = handle if handle is not None else lib().orc_obj_new()
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_obj_free(self.h)
+            self.h = None
+
+    def clone(self):
+        return OracleOrswot(lib().orc_obj_clone(self.h))
+
+    def apply_add(self, actor, counter, member):
+        lib().orc_obj_apply_add(self.h, actor, counter, member)
+
+    def apply_rm(self, member, clock_pairs):
+        a, c, n = _clock_arrays(clock_pairs)
+        lib().orc_obj_apply_rm(self.h, member, a, c, n)
+
+    def merge(self, other):
+        lib().orc_obj_merge(self.h, other.h)
+
+    def clock(self):
+        return _dump(lambda *r: lib().orc_obj_clock(self.h, *r))
+
+    def entry(self, member):
+        return _dump(lambda *r: lib().orc_obj_entry(self.h, member, *r))
+
+    def value(self):
+        cap = 1 << 16
+        buf = (C.c_uint64 * cap)()
+        n = lib().orc_obj_value(self.h, buf, cap)
+        return [int(buf[i]) for i in range(n)]
+
+    def deferred_len(self):
+        return int(lib().orc_obj_deferred_len(self.h))
+
+    def encode(self, n_actors):
+        cap = 1 << 16
+        while True:
+            buf = np.zeros(cap, dtype=np.uint8)
+            n = lib().orc_obj_encode(self.h, n_actors, _ptr(buf), cap)
+            if n == -4:
+                cap *= 4
+                continue
+            if n < 0:
+                raise ValueError(f"encode failed: {n}")
+            return buf[:n].tobytes()
+
+    @staticmethod
+    def decode(rec: bytes):
+        arr = np.frombuffer(rec, dtype=np.uint8).copy()
+        h = lib().orc_obj_decode(_ptr(arr), len(rec))
+        if not h:
+            raise ValueError("decode failed")
+        return OracleOrswot(h)
+
+
+# ------------------------------------------------------------- batches
+def orswot_merge_batch(lbase, loff, rbase, roff, n_actors, threads=8):
+    """Merge record batches (numpy u8 bases, u64 offsets). Returns (base, off)."""
+    n = len(loff)
+    cap = int(lbase.nbytes + rbase.nbytes) + 64
+    obase = np.zeros(cap, dtype=np.uint8)
+    ooff = np.zeros(n, dtype=np.uint64)
+    bad = C.c_int64(-1)
+    rc = lib().orc_orswot_merge_batch(_ptr(lbase), _ptr(loff), lbase.nbytes, _ptr(rbase), _ptr(roff),
+                                      rbase.nbytes, n, n_actors, _ptr(obase), _ptr(ooff), cap, threads,
+                                      C.byref(bad))
+    if rc != 0:
+        raise ValueError(f"oracle merge failed rc={rc} at object {bad.value}")
+    return obase, ooff
+
+
+def orswot_bench(lbase, loff, rbase, roff, threads):
+    return lib().orc_orswot_bench(_ptr(lbase), _ptr(loff), lbase.nbytes, _ptr(rbase), _ptr(roff),
+                                  rbase.nbytes, len(loff), threads)
+
+
+def dense_merge(self_rows, other_rows, n_actors, threads=8):
+    out = np.ascontiguousarray(self_rows, dtype=np.uint64).copy()
+    o = np.ascontiguousarray(other_rows, dtype=np.uint64)
+    n = out.size // n_actors
+    lib().orc_dense_merge(_ptr(out), _ptr(o), n, n_actors, threads)
+    return out
+
+
+def pncounter_merge(self_rows, other_rows, n_actors, threads=8):
+    out = np.ascontiguousarray(self_rows, dtype=np.uint64).copy()
+    o = np.ascontiguousarray(other_rows, dtype=np.uint64)
+    n = out.size // (2 * n_actors)
+    lib().orc_pncounter_merge(_ptr(out), _ptr(o), n, n_actors, threads)
+    return out
+
+
+def dense_bench(self_rows, other_rows, n_actors, threads):
+    n = self_rows.size // n_actors
+    return lib().orc_dense_bench(_ptr(self_rows), _ptr(other_rows), n, n_actors, threads)
+
+
+def record_bytes(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem):
+    return int(lib().orc_record_bytes(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem))
