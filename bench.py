@@ -1,0 +1,288 @@
+#!/usr/bin/env python3
+"""Benchmark: batched state-based CRDT merge on MI355X.
+
+Headline (BASELINE.json `metric`): merged Orswot objects/s on config 3 —
+1M objects x ~32 members x 16 actors incl. deferred removes — plus the
+achieved HBM GB/s of the merge kernel against the MI355X roofline.
+
+A step = one pass of the hot path over one batch: out[i] = L[i].merge(&R[i])
+for every object of the GPU's shard (one kernel launch), inputs resident in
+HBM. Objects shard across ranks (weak scaling: 1M objects per GPU, object i
+generated from SplitMix64(seed ^ i) so the data is identical at any N); there
+is no collective on this path.
+
+    python bench.py [--gpus N --steps K --warmup W] [--workload orswot|gcounter|pncounter]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "rust-crdt_amd"))
+
+HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md: 8.0 TB/s spec
+METRIC = "merged objects/sec (node) + achieved HBM GB/s % of peak, Orswot 1M×32 members"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--workload", default="orswot", choices=["orswot", "gcounter", "pncounter"])
+    p.add_argument("--n-obj", type=int, default=None, help="objects per GPU")
+    p.add_argument("--threads", type=int, default=16, help="host threads (generation, CPU baseline)")
+    p.add_argument("--cpu-sample", type=int, default=500_000, help="objects in the CPU-baseline sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
+                   help="measured per-launch HBM bytes (rocprofv3 PMC) to report as roofline.traffic")
+    p.add_argument("--blocks-per-cu", type=int, default=None)
+    return p.parse_args()
+
+
+def dist_setup():
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device(f"cuda:{local}"))
+    return rank, world, local
+
+
+def barrier(world):
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world):
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x, world):
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def load_traffic(path, key):
+    try:
+        with open(path) as f:
+            return json.load(f).get(key)
+    except (OSError, ValueError):
+        return None
+
+
+def run_orswot(args, rank, world, local):
+    import numpy as np
+    import torch
+
+    import crdts_hip
+
+    n = args.n_obj or 1_000_000
+    first = rank * n
+    t0 = time.time()
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(n, first_obj=first, threads=args.threads)
+    gen_s = time.time() - t0
+    eng = crdts_hip.Engine(local)
+    if args.blocks_per_cu:
+        eng.set_blocks_per_cu(args.blocks_per_cu)
+    L = crdts_hip.OrswotBatch.from_host(lb, lo, 16, device=local)
+    R = crdts_hip.OrswotBatch.from_host(rb, ro, 16, device=local)
+    out = eng.orswot_alloc_out(L, R)
+    stream = torch.cuda.Stream(device=local)
+    # one checked launch, then algorithmic bytes from the real output sizes
+    eng.orswot_merge(L, R, out=out, stream=stream, check_status=True)
+    out_sizes = out.base.view(torch.int32)[(out.off // 4)].cpu().numpy().astype(np.int64)
+    in_bytes = int(lb.nbytes + rb.nbytes)
+    out_bytes = int(out_sizes.sum())
+    alg_bytes = in_bytes + out_bytes + 3 * 8 * n  # + L/R offsets read, out offsets written
+
+    for _ in range(args.warmup):
+        eng.orswot_merge(L, R, out=out, stream=stream, check_status=False)
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    barrier(world)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        starts[k].record(stream)
+        eng.orswot_merge(L, R, out=out, stream=stream, check_status=False)
+        ends[k].record(stream)
+    stream.synchronize()
+    barrier(world)
+    wall = time.perf_counter() - t0
+    eng.status(stream)  # no record-level errors latched during the timed steps
+    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    wall = max_over_ranks(wall, world)
+    total_objs = sum_over_ranks(float(n * args.steps), world)
+    value = total_objs / wall
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic = load_traffic(args.traffic_json, "orswot_merge_kernel")
+    res = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "objects/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic: op-simulated Orswot pairs (SplitMix64 seed 0xC0FFEE03 ^ object id)",
+        "config": {
+            "workload": "orswot_merge config3 (BASELINE.json configs[2]): 1M objects/GPU x ~31 members/side "
+                        "x 16 dense actors incl. deferred removes",
+            "n_obj_per_gpu": n,
+            "n_actors": 16,
+            "alg_bytes_per_merge": alg_bytes / n,
+            "parallelism": f"objects sharded over {world} GPU(s), no collective",
+            "gen_s": round(gen_s, 2),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "orswot_merge_kernel",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "kernel_ms": kernel_ms,
+            "alg_bytes_per_launch": alg_bytes,
+            "traffic": traffic,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_orswot(lb, lo, rb, ro, args)
+    return res
+
+
+def cpu_baseline_orswot(lb, lo, rb, ro, args):
+    """The oracle (C++ std::map/unordered_map restatement of Orswot::merge with
+    the reference's clone pattern) on the host cores, bounded sample."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_ffi
+
+    m = min(args.cpu_sample, len(lo))
+    end = int(lo[m]) if m < len(lo) else lb.nbytes
+    endr = int(ro[m]) if m < len(ro) else rb.nbytes
+    threads = max(1, min(args.threads, os.cpu_count() or 1))
+    secs = oracle_ffi.orswot_bench(lb[:end], lo[:m], rb[:endr], ro[:m], threads)
+    m1 = max(1, m // 10)
+    secs1 = oracle_ffi.orswot_bench(lb, lo[:m1], rb, ro[:m1], 1)
+    return {
+        "value": m / secs,
+        "unit": "objects/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"first {m} objects of the same config-3 batch, merge loop only (decode untimed), "
+                  f"{threads} std::threads static partition",
+        "value_1core": m1 / secs1,
+    }
+
+
+def run_dense(args, rank, world, local, kind):
+    import numpy as np
+    import torch
+
+    import crdts_hip
+
+    A = 64
+    slots = A * (2 if kind == "pncounter" else 1)
+    # configs[1]: 100M counters x 64 dense actors; PNCounter's [P|N] rows are
+    # twice as wide, so it runs 50M rows per GPU to fit one HBM stack set.
+    n = args.n_obj or (100_000_000 if kind == "gcounter" else 50_000_000)
+    g = torch.Generator(device=f"cuda:{local}")
+    g.manual_seed(0xC0FFEE02 + rank)
+    a = torch.randint(0, 1 << 40, (n * slots,), dtype=torch.int64, device=f"cuda:{local}", generator=g)
+    b = torch.randint(0, 1 << 40, (n * slots,), dtype=torch.int64, device=f"cuda:{local}", generator=g)
+    a[torch.rand(n * slots, device=f"cuda:{local}", generator=g) < 0.25] = 0
+    b[torch.rand(n * slots, device=f"cuda:{local}", generator=g) < 0.25] = 0
+    eng = crdts_hip.Engine(local)
+    stream = torch.cuda.Stream(device=local)
+    for _ in range(args.warmup):
+        eng.dense_merge(a, b, A, kind, stream=stream)
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    barrier(world)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        starts[k].record(stream)
+        eng.dense_merge(a, b, A, kind, stream=stream)
+        ends[k].record(stream)
+    stream.synchronize()
+    barrier(world)
+    wall = max_over_ranks(time.perf_counter() - t0, world)
+    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    alg = 24.0 * n * slots
+    achieved = alg / (kernel_ms * 1e-3) / 1e9
+    total = sum_over_ranks(float(n * args.steps), world)
+    res = {
+        "metric": f"merged {kind} objects/sec (node), {A} dense actors",
+        "value": total / wall, "unit": "objects/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic: U[0,2^40) with 25% zeros",
+        "config": {"workload": f"{kind} dense merge (BASELINE.json configs[1])", "n_obj_per_gpu": n,
+                   "n_actors": A, "parallelism": f"objects sharded over {world} GPU(s), no collective"},
+        "roofline": {"bound": "hbm", "kernel": "dense_max_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "kernel_ms": kernel_ms,
+                     "alg_bytes_per_launch": alg, "traffic": load_traffic(args.traffic_json, "dense_max_kernel")},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_ffi
+
+        m = min(args.cpu_sample * 4, n)
+        ha = a[: m * slots].cpu().numpy().view(np.uint64).copy()
+        hb = b[: m * slots].cpu().numpy().view(np.uint64).copy()
+        threads = max(1, min(args.threads, os.cpu_count() or 1))
+        secs = oracle_ffi.dense_bench(ha, hb, slots, threads)
+        res["cpu_baseline"] = {"value": m / secs, "unit": "objects/s", "cores": threads, "kind": "port",
+                               "sample": f"first {m} rows, VClock::merge over std::map, {threads} threads"}
+    return res
+
+
+def main():
+    args = parse()
+    rank, world, local = dist_setup()
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if args.workload == "orswot":
+        res = run_orswot(args, rank, world, local)
+    else:
+        res = run_dense(args, rank, world, local, args.workload)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -190,26 +190,38 @@ int crdt_orswot_compact(crdt_ctx* ctx, const crdt_orswot_batch* src, uint8_t* d_
  * ------------------------------------------------------------------------ */
 
 /* Synthetic Orswot pair batches by op simulation (Orswot::apply,
- * src/orswot.rs:61-85), identical for any sharding: object i uses the
- * SplitMix64 stream seeded with (seed ^ i). Records for objects
- * [first_obj, first_obj + n_obj) are produced by n_threads host threads.
- * Two calls: first with h_*_base == NULL to get the byte totals, then with
- * buffers of at least those sizes. */
+ * src/orswot.rs:61-85), identical for any sharding: object i draws from the
+ * SplitMix64 stream seeded with (seed ^ i). Both sides share an ancestor
+ * built from `ancestor_adds` adds of distinct members over all actors (each actor starting from a
+ * random 40-bit counter base, as after a long history); side L then adds
+ * with actors [0, n_actors/2), side R with [n_actors/2, n_actors).
+ * Divergent ops per side: pct_add % adds, the rest removes with a read
+ * context (Orswot::contains(m).rm_clock); in `pct_deferred_obj` % of objects,
+ * `pct_future_rm` % of ops are removes with a FUTURE context (the side's clock
+ * advanced on a remote actor), which defer (src/orswot.rs:197-203). In
+ * `pct_shared_actor` % of objects side R also adds with actor 0 (the
+ * weird_highlight_1 path, test/orswot.rs:84-92). */
 typedef struct crdt_orswot_gen_params {
   uint32_t n_actors;         /* dense top-clock width (config 3: 16)            */
   uint32_t member_universe;  /* distinct member keys per object (config 3: 64)  */
   uint32_t ancestor_adds;    /* shared-history adds (config 3: 32)              */
   uint32_t min_div_ops;      /* divergent ops per side, uniform in [min, max]   */
   uint32_t max_div_ops;      /* (config 3: 4..16)                               */
-  uint32_t pct_add;          /* % of divergent ops that are adds (60)           */
-  uint32_t pct_rm_ctx;       /* % removes with a read ctx (30); rest = future ctx (10) */
-  uint32_t pct_shared_actor; /* % of objects where both sides add with one actor (5) */
+  uint32_t pct_add;          /* (60)                                            */
+  uint32_t pct_future_rm;    /* (10)                                            */
+  uint32_t pct_deferred_obj; /* (8)                                             */
+  uint32_t pct_shared_actor; /* (5)                                             */
 } crdt_orswot_gen_params;
 
+typedef struct crdt_orswot_gen crdt_orswot_gen;
+/* Generates objects [first_obj, first_obj + n_obj) on n_threads host threads. */
 int crdt_orswot_generate(uint64_t seed, size_t first_obj, size_t n_obj,
                          const crdt_orswot_gen_params* params, int n_threads,
-                         uint8_t* h_self_base, uint64_t* h_self_off, size_t* self_bytes,
-                         uint8_t* h_other_base, uint64_t* h_other_off, size_t* other_bytes);
+                         crdt_orswot_gen** out);
+/* side 0 = self (L), 1 = other (R): host base, u64 offsets (n_obj), bytes. */
+int crdt_orswot_gen_side(const crdt_orswot_gen* g, int side, const uint8_t** h_base,
+                         const uint64_t** h_off, size_t* bytes);
+void crdt_orswot_gen_free(crdt_orswot_gen* g);
 
 /* Dense synthetic counters: u64[n_obj][n_actors] rows for objects
  * [first_obj, first_obj+n_obj), counter U[0, 2^bits) with `pct_zero` % zeros. */

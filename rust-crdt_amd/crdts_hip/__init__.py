@@ -1,0 +1,425 @@
+"""crdts_hip — MI355X batched state-based CRDT merge (host side, Python).
+
+Mirrors the reference's `CvRDT::merge(&mut self, &other)` (src/traits.rs:9-12)
+for VClock / GCounter / PNCounter / Orswot, executed on the GPU through the C
+ABI of libcrdts_hip.so (include/crdts_hip.h):
+
+    eng = Engine(0)
+    out = eng.orswot_merge(self_batch, other_batch)      # batch join on HBM
+    a.merge(b)                                           # one pair, same kernel
+
+Device memory and streams come from torch (plumbing only).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import (CRDT_ECAPACITY, CRDT_ENONCANON, CRDT_OK, EXPORTS, LIB_PATH, Batch, CrdtError, GenParams,
+                   check, lib)
+from .record import decode_record, encode_record, record_bytes
+
+__all__ = [
+    "Engine", "OrswotBatch", "GenParams", "CrdtError", "generate_orswot", "generate_dense", "HostOrswot",
+    "Orswot", "VClock", "GCounter", "PNCounter", "merge_batch", "decode_record", "encode_record",
+    "record_bytes", "CONFIG3", "EXPORTS", "LIB_PATH",
+]
+
+# SURVEY.md §8(d) config 3 / BASELINE.json configs[2].
+CONFIG3 = dict(n_actors=16, member_universe=64, ancestor_adds=32, min_div_ops=4, max_div_ops=16, pct_add=60,
+               pct_future_rm=10, pct_deferred_obj=8, pct_shared_actor=5)
+CONFIG3_SEED = 0xC0FFEE03
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+class OrswotBatch:
+    """A batch of canonical Orswot records resident on one GPU.
+
+    base: torch.uint8 device tensor; off: torch.int64 device tensor (u64 offsets).
+    """
+
+    def __init__(self, base, off, n_actors, nbytes=None):
+        self.base = base
+        self.off = off
+        self.n_actors = int(n_actors)
+        self.n_obj = int(off.numel())
+        self.bytes = int(nbytes if nbytes is not None else base.numel())
+
+    def cbatch(self):
+        return Batch(self.base.data_ptr(), self.off.data_ptr(), self.n_obj, self.bytes)
+
+    @classmethod
+    def from_host(cls, base, off, n_actors, device=0):
+        torch = _torch()
+        base = np.ascontiguousarray(base, dtype=np.uint8)
+        nb = max(16, (base.nbytes + 15) // 16 * 16)
+        b = torch.zeros(nb, dtype=torch.uint8, device=f"cuda:{device}")
+        if base.nbytes:
+            b[: base.nbytes].copy_(torch.from_numpy(base))
+        o = torch.from_numpy(np.ascontiguousarray(off, dtype=np.uint64).view(np.int64)).to(f"cuda:{device}")
+        return cls(b, o, n_actors, nb)
+
+    @classmethod
+    def from_records(cls, records, n_actors, device=0):
+        offs, pos = [], 0
+        for r in records:
+            offs.append(pos)
+            pos += (len(r) + 15) // 16 * 16
+        base = np.zeros(max(pos, 16), dtype=np.uint8)
+        for o, r in zip(offs, records):
+            base[o:o + len(r)] = np.frombuffer(r, dtype=np.uint8)
+        return cls.from_host(base, np.array(offs, dtype=np.uint64), n_actors, device)
+
+    def to_host(self):
+        base = self.base.cpu().numpy()
+        off = self.off.cpu().numpy().view(np.uint64)
+        return base, off
+
+    def records(self):
+        base, off = self.to_host()
+        out = []
+        for o in off.tolist():
+            size = int(base[o:o + 4].view(np.uint32)[0])
+            out.append(base[o:o + size].tobytes())
+        return out
+
+
+class Engine:
+    """One crdt_ctx bound to a device. All merges run on the GPU."""
+
+    def __init__(self, device=0):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise CrdtError(-6, "Engine needs a visible gfx950 GPU")
+        self.device = int(device)
+        torch.cuda.set_device(self.device)
+        ctx = C.c_void_p()
+        check(lib.crdt_ctx_create(C.byref(ctx), self.device), "crdt_ctx_create")
+        self.ctx = ctx
+
+    def __del__(self):
+        if getattr(self, "ctx", None) is not None and lib is not None:
+            lib.crdt_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def _stream(self, stream=None):
+        torch = _torch()
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        return C.c_void_p(s.cuda_stream)
+
+    def set_blocks_per_cu(self, k):
+        check(lib.crdt_ctx_set_blocks_per_cu(self.ctx, int(k)), "set_blocks_per_cu")
+
+    def status(self, stream=None):
+        rc = lib.crdt_ctx_status(self.ctx, self._stream(stream))
+        check(rc, "kernel status")
+
+    # ---------------------------------------------------------------- Orswot
+    def orswot_alloc_out(self, L: OrswotBatch, R: OrswotBatch):
+        torch = _torch()
+        nb = L.bytes + R.bytes
+        base = torch.empty(nb, dtype=torch.uint8, device=f"cuda:{self.device}")
+        off = torch.empty(L.n_obj, dtype=torch.int64, device=f"cuda:{self.device}")
+        return OrswotBatch(base, off, L.n_actors, nb)
+
+    def orswot_merge(self, L: OrswotBatch, R: OrswotBatch, out: OrswotBatch | None = None, stream=None,
+                     check_status=True):
+        """out[i] = L[i].merge(&R[i])  (src/orswot.rs:87-157). Async unless check_status."""
+        if L.n_actors != R.n_actors or L.n_obj != R.n_obj:
+            raise CrdtError(-1, "batch shapes differ")
+        if out is None:
+            out = self.orswot_alloc_out(L, R)
+        lb, rb = L.cbatch(), R.cbatch()
+        rc = lib.crdt_orswot_merge(self.ctx, C.byref(lb), C.byref(rb), C.c_void_p(out.base.data_ptr()),
+                                   C.c_void_p(out.off.data_ptr()), out.bytes, L.n_actors, self._stream(stream))
+        check(rc, "crdt_orswot_merge")
+        if check_status:
+            self.status(stream)
+        return out
+
+    def orswot_validate(self, B: OrswotBatch, stream=None):
+        b = B.cbatch()
+        check(lib.crdt_orswot_validate(self.ctx, C.byref(b), B.n_actors, self._stream(stream)), "validate")
+        self.status(stream)
+
+    def orswot_compact(self, B: OrswotBatch, stream=None):
+        torch = _torch()
+        dev = f"cuda:{self.device}"
+        scratch = torch.empty(int(lib.crdt_orswot_compact_scratch_bytes(B.n_obj)), dtype=torch.uint8, device=dev)
+        dst = torch.empty(B.bytes, dtype=torch.uint8, device=dev)
+        doff = torch.empty(B.n_obj, dtype=torch.int64, device=dev)
+        b = B.cbatch()
+        check(lib.crdt_orswot_compact(self.ctx, C.byref(b), C.c_void_p(dst.data_ptr()),
+                                      C.c_void_p(doff.data_ptr()), B.bytes, C.c_void_p(scratch.data_ptr()),
+                                      self._stream(stream)), "compact")
+        torch.cuda.synchronize(self.device)
+        used = 0
+        if B.n_obj:
+            last = int(doff[-1].item())
+            used = last + int(dst[last:last + 4].cpu().numpy().view(np.uint32)[0])
+        return OrswotBatch(dst, doff, B.n_actors, max(16, (used + 15) // 16 * 16))
+
+    # ---------------------------------------------------------------- dense
+    def dense_merge(self, self_rows, other_rows, n_actors, kind="gcounter", stream=None):
+        """In place: self_rows = max(self_rows, other_rows) (src/vclock.rs:131-137).
+
+        Rows are torch int64 device tensors holding u64 counters; shape
+        [n_obj, n_actors] (vclock / gcounter) or [n_obj, 2*n_actors] (pncounter).
+        """
+        fn = {"vclock": lib.crdt_vclock_dense_merge, "gcounter": lib.crdt_gcounter_merge,
+              "pncounter": lib.crdt_pncounter_merge}[kind]
+        slots = n_actors * (2 if kind == "pncounter" else 1)
+        if self_rows.numel() != other_rows.numel() or self_rows.numel() % slots:
+            raise CrdtError(-1, "dense rows shape mismatch")
+        n_obj = self_rows.numel() // slots
+        check(fn(self.ctx, C.c_void_p(self_rows.data_ptr()), C.c_void_p(other_rows.data_ptr()), n_obj,
+                 n_actors, self._stream(stream)), f"dense merge ({kind})")
+        return self_rows
+
+
+# -------------------------------------------------------------- generators
+def _params(p):
+    if isinstance(p, GenParams):
+        return p
+    d = dict(CONFIG3)
+    d.update(p or {})
+    return GenParams(**{k: int(v) for k, v in d.items()})
+
+
+def generate_orswot(n_obj, first_obj=0, seed=CONFIG3_SEED, params=None, threads=8):
+    """Host op-simulation generator (see include/crdts_hip.h). Returns
+    ((L_base, L_off), (R_base, R_off)) as numpy arrays (copies)."""
+    P = _params(params)
+    g = C.c_void_p()
+    check(lib.crdt_orswot_generate(seed, first_obj, n_obj, C.byref(P), threads, C.byref(g)), "generate")
+    try:
+        sides = []
+        for s in range(2):
+            bp, op, nb = C.c_void_p(), C.c_void_p(), C.c_size_t()
+            check(lib.crdt_orswot_gen_side(g, s, C.byref(bp), C.byref(op), C.byref(nb)), "gen_side")
+            base = np.ctypeslib.as_array((C.c_uint8 * max(1, nb.value)).from_address(bp.value)).copy() \
+                if nb.value else np.zeros(16, np.uint8)
+            off = np.ctypeslib.as_array((C.c_uint64 * max(1, n_obj)).from_address(op.value)).copy()[:n_obj] \
+                if n_obj else np.zeros(0, np.uint64)
+            sides.append((base, off))
+        return sides[0], sides[1]
+    finally:
+        lib.crdt_orswot_gen_free(g)
+
+
+def generate_dense(n_obj, n_actors, seed, first_obj=0, bits=40, pct_zero=25, threads=8):
+    rows = np.empty((n_obj, n_actors), dtype=np.uint64)
+    check(lib.crdt_dense_generate(seed, first_obj, n_obj, n_actors, bits, pct_zero, threads,
+                                  C.c_void_p(rows.ctypes.data)), "dense_generate")
+    return rows
+
+
+# -------------------------------------------------------------- op path
+class HostOrswot:
+    """Host Orswot built through the reference's op path (src/orswot.rs:61-85)."""
+
+    def __init__(self, handle=None):
+        self.h = C.c_void_p(handle) if handle is not None else C.c_void_p(lib.crdt_host_orswot_new())
+
+    def __del__(self):
+        if getattr(self, "h", None) is not None and lib is not None:
+            lib.crdt_host_orswot_free(self.h)
+            self.h = None
+
+    def clone(self):
+        return HostOrswot(lib.crdt_host_orswot_clone(self.h))
+
+    def apply_add(self, actor, counter, member):
+        check(lib.crdt_host_orswot_apply_add(self.h, actor, counter, member), "apply_add")
+
+    def apply_rm(self, member, clock_pairs):
+        n = len(clock_pairs)
+        a = (C.c_uint32 * max(1, n))(*[int(x) for x, _ in clock_pairs])
+        c = (C.c_uint64 * max(1, n))(*[int(y) for _, y in clock_pairs])
+        check(lib.crdt_host_orswot_apply_rm(self.h, member, a, c, n), "apply_rm")
+
+    def encode(self, n_actors):
+        cap = 1 << 14
+        while True:
+            buf = (C.c_uint8 * cap)()
+            n = lib.crdt_host_orswot_encode(self.h, n_actors, buf, cap)
+            if n == CRDT_ECAPACITY:
+                cap *= 4
+                continue
+            check(n if n < 0 else 0, "encode")
+            return bytes(buf[:n])
+
+    @staticmethod
+    def decode(rec: bytes):
+        arr = (C.c_uint8 * len(rec)).from_buffer_copy(rec)
+        h = lib.crdt_host_orswot_decode(arr, len(rec))
+        if not h:
+            raise CrdtError(CRDT_ENONCANON, "decode")
+        return HostOrswot(h)
+
+
+_default_engine = None
+
+
+def default_engine():
+    global _default_engine
+    if _default_engine is None:
+        _default_engine = Engine(0)
+    return _default_engine
+
+
+class Orswot:
+    """Reference-shaped Orswot (src/orswot.rs:26-30) whose `merge` runs on the GPU.
+
+    `n_actors` is the dense top-clock width used when the state crosses the
+    C ABI (actors must be interned to ids < n_actors).
+    """
+
+    def __init__(self, n_actors=16, host=None):
+        self.n_actors = n_actors
+        self.host = host or HostOrswot()
+
+    def clone(self):
+        return Orswot(self.n_actors, self.host.clone())
+
+    def apply_add(self, actor, counter, member):  # CmRDT::apply Op::Add
+        self.host.apply_add(actor, counter, member)
+
+    def apply_rm(self, member, clock_pairs):  # CmRDT::apply Op::Rm
+        self.host.apply_rm(member, clock_pairs)
+
+    def merge(self, other: "Orswot", engine=None):  # CvRDT::merge
+        merge_batch([self], [other], engine)
+
+    def state(self):
+        return decode_record(self.host.encode(self.n_actors))
+
+    def clock(self):
+        return sorted(self.state()["clock"].items())
+
+    def entry(self, member):
+        e = self.state()["entries"].get(member)
+        return None if e is None else list(e)
+
+    def value(self):
+        return sorted(self.state()["entries"])
+
+    def deferred_len(self):
+        return len(self.state()["deferred"])
+
+    def record(self):
+        return self.host.encode(self.n_actors)
+
+
+def merge_batch(selfs, others, engine=None):
+    """`merge_batch(&mut [T], &[T])`: selfs[i].merge(&others[i]) for every i, one kernel launch."""
+    if len(selfs) != len(others):
+        raise CrdtError(-1, "merge_batch length mismatch")
+    if not selfs:
+        return
+    eng = engine or default_engine()
+    kinds = {type(x) for x in selfs} | {type(x) for x in others}
+    if kinds == {Orswot}:
+        n_actors = max(x.n_actors for x in list(selfs) + list(others))
+        L = OrswotBatch.from_records([x.host.encode(n_actors) for x in selfs], n_actors, eng.device)
+        R = OrswotBatch.from_records([x.host.encode(n_actors) for x in others], n_actors, eng.device)
+        out = eng.orswot_merge(L, R)
+        for x, rec in zip(selfs, out.records()):
+            x.host = HostOrswot.decode(rec)
+        return
+    if kinds <= {VClock, GCounter, PNCounter} and len(kinds) == 1:
+        kind = {VClock: "vclock", GCounter: "gcounter", PNCounter: "pncounter"}[kinds.pop()]
+        n_actors = max(x.n_actors for x in list(selfs) + list(others))
+        torch = _torch()
+        a = torch.from_numpy(np.stack([x.row(n_actors) for x in selfs]).view(np.int64)).to(f"cuda:{eng.device}")
+        b = torch.from_numpy(np.stack([x.row(n_actors) for x in others]).view(np.int64)).to(f"cuda:{eng.device}")
+        eng.dense_merge(a, b, n_actors, kind)
+        rows = a.cpu().numpy().view(np.uint64)
+        for x, r in zip(selfs, rows):
+            x.set_row(r, n_actors)
+        return
+    raise CrdtError(-1, f"merge_batch: unsupported element types {kinds}")
+
+
+class VClock:
+    """Reference-shaped VClock (src/vclock.rs:54-57) over interned actor ids."""
+
+    def __init__(self, dots=None, n_actors=16):
+        self.n_actors = n_actors
+        self.dots = {}
+        for a, c in (dots or []):
+            self.witness(a, c)
+
+    def get(self, a):
+        return self.dots.get(a, 0)
+
+    def witness(self, a, c):  # src/vclock.rs:159-163
+        if not (self.get(a) >= c):
+            self.dots[a] = int(c)
+
+    def merge(self, other, engine=None):
+        merge_batch([self], [other], engine)
+
+    def row(self, n):
+        r = np.zeros(n, dtype=np.uint64)
+        for a, c in self.dots.items():
+            r[a] = c
+        return r
+
+    def set_row(self, r, n):
+        self.dots = {a: int(r[a]) for a in range(n) if r[a]}
+
+
+class GCounter(VClock):
+    """src/gcounter.rs:26-28 — one VClock; value() = sum (:76-78)."""
+
+    def inc(self, actor):
+        return (actor, self.get(actor) + 1)
+
+    def apply(self, dot):
+        self.witness(*dot)
+
+    def value(self):
+        return sum(self.dots.values()) & 0xFFFFFFFFFFFFFFFF
+
+
+class PNCounter:
+    """src/pncounter.rs:33-36 — P and N GCounters, merged together as one [P|N] row."""
+
+    def __init__(self, n_actors=16):
+        self.n_actors = n_actors
+        self.p = GCounter(n_actors=n_actors)
+        self.n = GCounter(n_actors=n_actors)
+
+    def inc(self, actor):
+        return (self.p.inc(actor), True)
+
+    def dec(self, actor):
+        return (self.n.inc(actor), False)
+
+    def apply(self, op):
+        dot, pos = op
+        (self.p if pos else self.n).apply(dot)
+
+    def merge(self, other, engine=None):
+        merge_batch([self], [other], engine)
+
+    def value(self):
+        def i64(x):
+            x &= 0xFFFFFFFFFFFFFFFF
+            return x - (1 << 64) if x >= (1 << 63) else x
+
+        return i64(i64(self.p.value()) - i64(self.n.value()))
+
+    def row(self, n):
+        return np.concatenate([self.p.row(n), self.n.row(n)])
+
+    def set_row(self, r, n):
+        self.p.set_row(r[:n], n)
+        self.n.set_row(r[n:], n)

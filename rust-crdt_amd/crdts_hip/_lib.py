@@ -1,0 +1,105 @@
+"""ctypes binding of libcrdts_hip.so (C ABI: include/crdts_hip.h).
+
+The shared library is the product; this module only declares its symbols.
+There is no CPU fallback anywhere: if the library is missing, importing the
+package raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG_DIR)  # rust-crdt_amd/
+LIB_PATH = os.path.join(ROOT, "lib", "libcrdts_hip.so")
+
+CRDT_OK = 0
+CRDT_EINVAL = -1
+CRDT_ENONCANON = -2
+CRDT_EHIP = -3
+CRDT_ECAPACITY = -4
+CRDT_ECOMM = -5
+CRDT_ENODEV = -6
+
+
+class CrdtError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        msg = lib.crdt_strerror(code).decode() if lib is not None else str(code)
+        super().__init__(f"{what}: {msg} ({code})" if what else f"{msg} ({code})")
+
+
+class Batch(C.Structure):
+    _fields_ = [("base", C.c_void_p), ("off", C.c_void_p), ("n_obj", C.c_size_t), ("bytes", C.c_size_t)]
+
+
+class GenParams(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("n_actors", "member_universe", "ancestor_adds", "min_div_ops",
+                                          "max_div_ops", "pct_add", "pct_future_rm", "pct_deferred_obj",
+                                          "pct_shared_actor")]
+
+
+# Every symbol include/crdts_hip.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "crdt_ctx_create", "crdt_ctx_destroy", "crdt_ctx_status", "crdt_strerror", "crdt_abi_version",
+    "crdt_vclock_dense_merge", "crdt_gcounter_merge", "crdt_pncounter_merge",
+    "crdt_orswot_record_bytes", "crdt_orswot_merge", "crdt_orswot_merge_host", "crdt_orswot_validate",
+    "crdt_orswot_compact_scratch_bytes", "crdt_orswot_compact",
+    "crdt_orswot_generate", "crdt_orswot_gen_side", "crdt_orswot_gen_free", "crdt_dense_generate",
+    "crdt_host_orswot_new", "crdt_host_orswot_clone", "crdt_host_orswot_free",
+    "crdt_host_orswot_apply_add", "crdt_host_orswot_apply_rm", "crdt_host_orswot_encode",
+    "crdt_host_orswot_decode",
+]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"crdts_hip: native library missing at {LIB_PATH}; build it with "
+            "`make -C rust-crdt_amd` or `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(LIB_PATH)
+    P, I, SZ, U32, U64 = C.c_void_p, C.c_int, C.c_size_t, C.c_uint32, C.c_uint64
+    BP = C.POINTER(Batch)
+    sig = {
+        "crdt_ctx_create": (I, [C.POINTER(P), I]),
+        "crdt_ctx_destroy": (I, [P]),
+        "crdt_ctx_status": (I, [P, P]),
+        "crdt_ctx_set_blocks_per_cu": (I, [P, I]),
+        "crdt_strerror": (C.c_char_p, [I]),
+        "crdt_abi_version": (I, []),
+        "crdt_vclock_dense_merge": (I, [P, P, P, SZ, U32, P]),
+        "crdt_gcounter_merge": (I, [P, P, P, SZ, U32, P]),
+        "crdt_pncounter_merge": (I, [P, P, P, SZ, U32, P]),
+        "crdt_orswot_record_bytes": (SZ, [U32] * 6),
+        "crdt_orswot_merge": (I, [P, BP, BP, P, P, SZ, U32, P]),
+        "crdt_orswot_merge_host": (I, [P, P, P, SZ, P, P, SZ, SZ, U32, P, P, SZ, C.POINTER(SZ)]),
+        "crdt_orswot_validate": (I, [P, BP, U32, P]),
+        "crdt_orswot_compact_scratch_bytes": (SZ, [SZ]),
+        "crdt_orswot_compact": (I, [P, BP, P, P, SZ, P, P]),
+        "crdt_orswot_generate": (I, [U64, SZ, SZ, C.POINTER(GenParams), I, C.POINTER(P)]),
+        "crdt_orswot_gen_side": (I, [P, I, C.POINTER(P), C.POINTER(P), C.POINTER(SZ)]),
+        "crdt_orswot_gen_free": (None, [P]),
+        "crdt_dense_generate": (I, [U64, SZ, SZ, U32, U32, U32, I, P]),
+        "crdt_host_orswot_new": (P, []),
+        "crdt_host_orswot_clone": (P, [P]),
+        "crdt_host_orswot_free": (None, [P]),
+        "crdt_host_orswot_apply_add": (I, [P, U32, U64, U64]),
+        "crdt_host_orswot_apply_rm": (I, [P, U64, P, P, U32]),
+        "crdt_host_orswot_encode": (C.c_long, [P, U32, P, SZ]),
+        "crdt_host_orswot_decode": (P, [P, SZ]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
+lib = None
+lib = _load()
+
+
+def check(rc, what=""):
+    if rc != CRDT_OK:
+        raise CrdtError(rc, what)
+    return rc

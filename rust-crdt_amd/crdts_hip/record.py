@@ -1,0 +1,81 @@
+"""Canonical Orswot record codec (layout: include/crdts_hip.h), host side.
+
+Used by the Python mirror types to read states back; the hot path never goes
+through here.
+"""
+from __future__ import annotations
+
+import struct
+
+HDR = 32
+
+
+def _pad(x, a):
+    return (x + a - 1) // a * a
+
+
+def record_bytes(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem):
+    b = _pad(HDR + 8 * n_clk + 12 * (n_mem + n_dot), 8)
+    return _pad(b + 12 * n_def_dot + 8 * n_def_mem + 8 * n_def, 16)
+
+
+def decode_record(rec):
+    """-> dict(clock={actor: ctr}, entries={member: [(actor, ctr)]}, deferred=[([(a, c)], [members])])."""
+    rec = bytes(rec)
+    size, n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem, flags = struct.unpack_from("<8I", rec, 0)
+    o = HDR
+    clk = struct.unpack_from(f"<{n_clk}Q", rec, o); o += 8 * n_clk
+    keys = struct.unpack_from(f"<{n_mem}Q", rec, o); o += 8 * n_mem
+    dctr = struct.unpack_from(f"<{n_dot}Q", rec, o); o += 8 * n_dot
+    dact = struct.unpack_from(f"<{n_dot}I", rec, o); o += 4 * n_dot
+    dend = struct.unpack_from(f"<{n_mem}I", rec, o); o = _pad(o + 4 * n_mem, 8)
+    fctr = struct.unpack_from(f"<{n_def_dot}Q", rec, o); o += 8 * n_def_dot
+    fkey = struct.unpack_from(f"<{n_def_mem}Q", rec, o); o += 8 * n_def_mem
+    fact = struct.unpack_from(f"<{n_def_dot}I", rec, o); o += 4 * n_def_dot
+    fdend = struct.unpack_from(f"<{n_def}I", rec, o); o += 4 * n_def
+    fmend = struct.unpack_from(f"<{n_def}I", rec, o)
+    entries, s = {}, 0
+    for m, e in zip(keys, dend):
+        entries[m] = list(zip(dact[s:e], dctr[s:e]))
+        s = e
+    deferred, s, t = [], 0, 0
+    for de, me in zip(fdend, fmend):
+        deferred.append((list(zip(fact[s:de], fctr[s:de])), list(fkey[t:me])))
+        s, t = de, me
+    return dict(size=size, clock={a: c for a, c in enumerate(clk) if c}, entries=entries, deferred=deferred)
+
+
+def encode_record(clock, entries, deferred, n_actors):
+    """clock {a: c}; entries {m: {a: c}}; deferred {tuple(sorted (a, c)): iterable(m)}."""
+    mems = sorted(entries)
+    runs = [sorted(entries[m].items()) for m in mems]
+    defs = sorted((tuple(k), sorted(v)) for k, v in deferred.items())
+    n_mem, n_dot, n_def = len(mems), sum(map(len, runs)), len(defs)
+    n_def_dot = sum(len(d[0]) for d in defs)
+    n_def_mem = sum(len(d[1]) for d in defs)
+    size = record_bytes(n_actors, n_mem, n_dot, n_def, n_def_dot, n_def_mem)
+    out = bytearray(size)
+    struct.pack_into("<8I", out, 0, size, n_actors, n_mem, n_dot, n_def, n_def_dot, n_def_mem, 0)
+    o = HDR
+    clk = [0] * n_actors
+    for a, c in clock.items():
+        clk[a] = c
+    struct.pack_into(f"<{n_actors}Q", out, o, *clk); o += 8 * n_actors
+    struct.pack_into(f"<{n_mem}Q", out, o, *mems); o += 8 * n_mem
+    struct.pack_into(f"<{n_dot}Q", out, o, *[c for r in runs for _, c in r]); o += 8 * n_dot
+    struct.pack_into(f"<{n_dot}I", out, o, *[a for r in runs for a, _ in r]); o += 4 * n_dot
+    e, ends = 0, []
+    for r in runs:
+        e += len(r)
+        ends.append(e)
+    struct.pack_into(f"<{n_mem}I", out, o, *ends); o = _pad(o + 4 * n_mem, 8)
+    struct.pack_into(f"<{n_def_dot}Q", out, o, *[c for d in defs for _, c in d[0]]); o += 8 * n_def_dot
+    struct.pack_into(f"<{n_def_mem}Q", out, o, *[m for d in defs for m in d[1]]); o += 8 * n_def_mem
+    struct.pack_into(f"<{n_def_dot}I", out, o, *[a for d in defs for a, _ in d[0]]); o += 4 * n_def_dot
+    de, me, a, b = [], [], 0, 0
+    for d in defs:
+        a += len(d[0]); b += len(d[1])
+        de.append(a); me.append(b)
+    struct.pack_into(f"<{n_def}I", out, o, *de); o += 4 * n_def
+    struct.pack_into(f"<{n_def}I", out, o, *me)
+    return bytes(out)

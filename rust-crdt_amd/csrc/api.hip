@@ -1,0 +1,240 @@
+// C ABI of crdts_hip (include/crdts_hip.h): argument validation, the context,
+// and launches. Nothing here falls back to a CPU implementation: without a
+// usable gfx950 device every device entry point returns CRDT_ENODEV/EHIP.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cstring>
+#include <vector>
+
+#include "../../include/crdts_hip.h"
+#include "kernels.h"
+#include "record_layout.h"
+
+using namespace crdts_hip;
+
+struct crdt_ctx {
+  int device;
+  int* d_status;
+  int blocks_per_cu;
+};
+
+namespace {
+
+inline hipStream_t S(void* s) { return (hipStream_t)s; }
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+int set_device(crdt_ctx* ctx) {
+  if (!ctx) return CRDT_EINVAL;
+  return hipSetDevice(ctx->device) == hipSuccess ? CRDT_OK : CRDT_EHIP;
+}
+
+int dense(crdt_ctx* ctx, uint64_t* self, const uint64_t* other, size_t n_obj, uint64_t slots,
+          void* stream) {
+  if (!ctx || (n_obj && (!self || !other)) || slots == 0) return CRDT_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return launch_dense_max(self, other, (uint64_t)n_obj * slots, S(stream));
+}
+
+}  // namespace
+
+extern "C" {
+
+int crdt_abi_version(void) { return CRDT_ABI_VERSION; }
+
+const char* crdt_strerror(int code) {
+  switch (code) {
+    case CRDT_OK: return "ok";
+    case CRDT_EINVAL: return "invalid argument";
+    case CRDT_ENONCANON: return "non-canonical or inconsistent record";
+    case CRDT_EHIP: return "HIP runtime error";
+    case CRDT_ECAPACITY: return "output capacity too small";
+    case CRDT_ECOMM: return "communicator error";
+    case CRDT_ENODEV: return "no usable gfx950 device";
+    default: return "unknown error";
+  }
+}
+
+int crdt_ctx_create(crdt_ctx** out, int device) {
+  if (!out) return CRDT_EINVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return CRDT_ENODEV;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return CRDT_ENODEV;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return CRDT_ENODEV;
+  if (hipSetDevice(device) != hipSuccess) return CRDT_EHIP;
+  auto* c = new crdt_ctx();
+  c->device = device;
+  c->blocks_per_cu = 8;
+  if (hipMalloc(&c->d_status, sizeof(int)) != hipSuccess ||
+      hipMemset(c->d_status, 0, sizeof(int)) != hipSuccess) {
+    delete c;
+    return CRDT_EHIP;
+  }
+  *out = c;
+  return CRDT_OK;
+}
+
+int crdt_ctx_destroy(crdt_ctx* ctx) {
+  if (!ctx) return CRDT_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  (void)hipFree(ctx->d_status);
+  delete ctx;
+  return CRDT_OK;
+}
+
+int crdt_ctx_status(crdt_ctx* ctx, void* stream) {
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  if (hipStreamSynchronize(S(stream)) != hipSuccess) return CRDT_EHIP;
+  int st = 0;
+  if (hipMemcpy(&st, ctx->d_status, sizeof st, hipMemcpyDeviceToHost) != hipSuccess) return CRDT_EHIP;
+  if (st != 0 && hipMemset(ctx->d_status, 0, sizeof(int)) != hipSuccess) return CRDT_EHIP;
+  return st;
+}
+
+// Tuning knob (not in the public header): workgroups per CU for the Orswot kernel.
+int crdt_ctx_set_blocks_per_cu(crdt_ctx* ctx, int k) {
+  if (!ctx || k < 1 || k > 64) return CRDT_EINVAL;
+  ctx->blocks_per_cu = k;
+  return CRDT_OK;
+}
+
+int crdt_vclock_dense_merge(crdt_ctx* ctx, uint64_t* d_self, const uint64_t* d_other, size_t n_obj,
+                            uint32_t n_actors, void* stream) {
+  return dense(ctx, d_self, d_other, n_obj, n_actors, stream);
+}
+int crdt_gcounter_merge(crdt_ctx* ctx, uint64_t* d_self, const uint64_t* d_other, size_t n_obj,
+                        uint32_t n_actors, void* stream) {
+  return dense(ctx, d_self, d_other, n_obj, n_actors, stream);
+}
+int crdt_pncounter_merge(crdt_ctx* ctx, uint64_t* d_self, const uint64_t* d_other, size_t n_obj,
+                         uint32_t n_actors, void* stream) {
+  return dense(ctx, d_self, d_other, n_obj, 2ull * n_actors, stream);
+}
+
+int crdt_orswot_merge(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_orswot_batch* other,
+                      uint8_t* d_out_base, uint64_t* d_out_off, size_t out_bytes, uint32_t n_actors,
+                      void* stream) {
+  if (!ctx || !self || !other || n_actors == 0 || self->n_obj != other->n_obj) return CRDT_EINVAL;
+  if (self->n_obj == 0) return CRDT_OK;
+  if (!self->base || !self->off || !other->base || !other->off || !d_out_base || !d_out_off)
+    return CRDT_EINVAL;
+  if (!aligned16(self->base) || !aligned16(other->base) || !aligned16(d_out_base)) return CRDT_EINVAL;
+  if (out_bytes < self->bytes + other->bytes) return CRDT_ECAPACITY;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return launch_orswot_merge(self->base, self->off, self->bytes, other->base, other->off,
+                             other->bytes, d_out_base, d_out_off, out_bytes, self->n_obj, n_actors,
+                             ctx->d_status, S(stream), ctx->blocks_per_cu);
+}
+
+int crdt_orswot_validate(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32_t n_actors,
+                         void* stream) {
+  if (!ctx || !batch || n_actors == 0) return CRDT_EINVAL;
+  if (batch->n_obj && (!batch->base || !batch->off)) return CRDT_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return launch_orswot_validate(batch->base, batch->off, batch->bytes, batch->n_obj, n_actors,
+                                ctx->d_status, S(stream));
+}
+
+size_t crdt_orswot_compact_scratch_bytes(size_t n_obj) {
+  size_t temp = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, temp, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                   (int)(n_obj ? n_obj : 1));
+  return ((8 * n_obj + 255) & ~size_t(255)) + temp + 256;
+}
+
+int crdt_orswot_compact(crdt_ctx* ctx, const crdt_orswot_batch* src, uint8_t* d_dst,
+                        uint64_t* d_dst_off, size_t dst_bytes, void* d_scratch, void* stream) {
+  if (!ctx || !src || (src->n_obj && (!src->base || !src->off || !d_dst || !d_dst_off || !d_scratch)))
+    return CRDT_EINVAL;
+  if (src->n_obj == 0) return CRDT_OK;
+  if (src->n_obj > 0x7FFFFFFFull) return CRDT_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  uint64_t* sizes = (uint64_t*)d_scratch;
+  uint8_t* temp = (uint8_t*)d_scratch + ((8 * src->n_obj + 255) & ~size_t(255));
+  size_t temp_bytes = crdt_orswot_compact_scratch_bytes(src->n_obj) -
+                      ((8 * src->n_obj + 255) & ~size_t(255)) - 256;
+  if ((rc = launch_record_sizes(src->base, src->off, src->n_obj, sizes, S(stream)))) return rc;
+  if (hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, sizes, d_dst_off, (int)src->n_obj,
+                                       S(stream)) != hipSuccess)
+    return CRDT_EHIP;
+  // bound check: last offset + last size <= dst_bytes (host round trip is fine here)
+  uint64_t last_off = 0, last_size = 0;
+  if (hipMemcpyAsync(&last_off, d_dst_off + src->n_obj - 1, 8, hipMemcpyDeviceToHost, S(stream)) !=
+          hipSuccess ||
+      hipMemcpyAsync(&last_size, sizes + src->n_obj - 1, 8, hipMemcpyDeviceToHost, S(stream)) !=
+          hipSuccess ||
+      hipStreamSynchronize(S(stream)) != hipSuccess)
+    return CRDT_EHIP;
+  if (last_off + last_size > dst_bytes) return CRDT_ECAPACITY;
+  return launch_record_copy(src->base, src->off, d_dst, d_dst_off, src->n_obj, S(stream));
+}
+
+int crdt_orswot_merge_host(crdt_ctx* ctx, const uint8_t* h_self_base, const uint64_t* h_self_off,
+                           size_t self_bytes, const uint8_t* h_other_base,
+                           const uint64_t* h_other_off, size_t other_bytes, size_t n_obj,
+                           uint32_t n_actors, uint8_t* h_out_base, uint64_t* h_out_off,
+                           size_t h_out_bytes, size_t* h_out_used) {
+  if (!ctx || n_actors == 0) return CRDT_EINVAL;
+  if (n_obj == 0) {
+    if (h_out_used) *h_out_used = 0;
+    return CRDT_OK;
+  }
+  if (!h_self_base || !h_self_off || !h_other_base || !h_other_off || !h_out_base || !h_out_off)
+    return CRDT_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  size_t sb = (self_bytes + 15) & ~size_t(15), ob = (other_bytes + 15) & ~size_t(15);
+  size_t outb = sb + ob;
+  uint8_t *dL = nullptr, *dR = nullptr, *dO = nullptr;
+  uint64_t *dLo = nullptr, *dRo = nullptr, *dOo = nullptr;
+  hipStream_t st = nullptr;
+  auto cleanup = [&]() {
+    (void)hipFree(dL); (void)hipFree(dR); (void)hipFree(dO);
+    (void)hipFree(dLo); (void)hipFree(dRo); (void)hipFree(dOo);
+    if (st) (void)hipStreamDestroy(st);
+  };
+  if (hipStreamCreate(&st) != hipSuccess || hipMalloc(&dL, sb) != hipSuccess ||
+      hipMalloc(&dR, ob) != hipSuccess || hipMalloc(&dO, outb) != hipSuccess ||
+      hipMalloc(&dLo, 8 * n_obj) != hipSuccess || hipMalloc(&dRo, 8 * n_obj) != hipSuccess ||
+      hipMalloc(&dOo, 8 * n_obj) != hipSuccess) {
+    cleanup();
+    return CRDT_EHIP;
+  }
+  bool ok = hipMemcpyAsync(dL, h_self_base, self_bytes, hipMemcpyHostToDevice, st) == hipSuccess &&
+            hipMemcpyAsync(dR, h_other_base, other_bytes, hipMemcpyHostToDevice, st) == hipSuccess &&
+            hipMemcpyAsync(dLo, h_self_off, 8 * n_obj, hipMemcpyHostToDevice, st) == hipSuccess &&
+            hipMemcpyAsync(dRo, h_other_off, 8 * n_obj, hipMemcpyHostToDevice, st) == hipSuccess;
+  if (!ok) { cleanup(); return CRDT_EHIP; }
+  crdt_orswot_batch Lb = {dL, dLo, n_obj, sb}, Rb = {dR, dRo, n_obj, ob};
+  rc = crdt_orswot_merge(ctx, &Lb, &Rb, dO, dOo, outb, n_actors, st);
+  if (rc == CRDT_OK) rc = crdt_ctx_status(ctx, st);
+  if (rc != CRDT_OK) { cleanup(); return rc; }
+  std::vector<uint64_t> offs(n_obj);
+  std::vector<uint8_t> out(outb);
+  ok = hipMemcpyAsync(offs.data(), dOo, 8 * n_obj, hipMemcpyDeviceToHost, st) == hipSuccess &&
+       hipMemcpyAsync(out.data(), dO, outb, hipMemcpyDeviceToHost, st) == hipSuccess &&
+       hipStreamSynchronize(st) == hipSuccess;
+  cleanup();
+  if (!ok) return CRDT_EHIP;
+  size_t pos = 0;
+  for (size_t i = 0; i < n_obj; ++i) {
+    uint32_t size;
+    std::memcpy(&size, out.data() + offs[i], 4);
+    if (pos + size > h_out_bytes) return CRDT_ECAPACITY;
+    std::memcpy(h_out_base + pos, out.data() + offs[i], size);
+    h_out_off[i] = pos;
+    pos += size;
+  }
+  if (h_out_used) *h_out_used = pos;
+  return CRDT_OK;
+}
+
+}  // extern "C"

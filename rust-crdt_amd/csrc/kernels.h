@@ -1,0 +1,23 @@
+// Internal launch entry points (the C ABI in api.hip validates and calls these).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace crdts_hip {
+
+int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
+                        const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff,
+                        uint64_t Obytes, uint64_t n_obj, uint32_t n_actors, int* status,
+                        hipStream_t stream, int blocks_per_cu);
+
+int launch_dense_max(uint64_t* self, const uint64_t* other, uint64_t n_words, hipStream_t stream);
+
+int launch_orswot_validate(const uint8_t* base, const uint64_t* off, uint64_t bytes, uint64_t n_obj,
+                           uint32_t n_actors, int* status, hipStream_t stream);
+
+int launch_record_sizes(const uint8_t* base, const uint64_t* off, uint64_t n_obj, uint64_t* sizes,
+                        hipStream_t stream);
+int launch_record_copy(const uint8_t* src, const uint64_t* src_off, uint8_t* dst,
+                       const uint64_t* dst_off, uint64_t n_obj, hipStream_t stream);
+
+}  // namespace crdts_hip

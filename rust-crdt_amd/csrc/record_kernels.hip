@@ -1,0 +1,124 @@
+// Record utilities on the device: deep canonical-form validation, and the
+// size / copy kernels behind crdt_orswot_compact (gap removal after a merge).
+#include <hip/hip_runtime.h>
+
+#include "../../include/crdts_hip.h"
+#include "kernels.h"
+#include "record_layout.h"
+
+namespace crdts_hip {
+namespace {
+
+__device__ __forceinline__ void fail(int* status) { atomicCAS(status, 0, CRDT_ENONCANON); }
+
+// One lane per record. Checks every invariant listed in include/crdts_hip.h.
+__global__ void validate_kernel(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                                uint64_t bytes, uint64_t n_obj, uint32_t A, int* status) {
+  uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n_obj) return;
+  uint64_t o = off[i];
+  if ((o & 15u) || o + kHdrBytes > bytes) return fail(status);
+  const uint8_t* r = base + o;
+  const uint32_t* h = (const uint32_t*)r;
+  RecLayout L;
+  rec_layout(L, h[1], h[2], h[3], h[4], h[5], h[6]);
+  if (h[0] != L.size || h[1] != A || h[7] != 0 || o + L.size > bytes) return fail(status);
+  const uint64_t* key = (const uint64_t*)(r + L.o_key);
+  const uint64_t* dctr = (const uint64_t*)(r + L.o_dctr);
+  const uint32_t* dact = (const uint32_t*)(r + L.o_dact);
+  const uint32_t* mdend = (const uint32_t*)(r + L.o_mdend);
+  const uint64_t* fctr = (const uint64_t*)(r + L.o_fctr);
+  const uint64_t* fkey = (const uint64_t*)(r + L.o_fkey);
+  const uint32_t* fact = (const uint32_t*)(r + L.o_fact);
+  const uint32_t* fdend = (const uint32_t*)(r + L.o_fdend);
+  const uint32_t* fmend = (const uint32_t*)(r + L.o_fmend);
+  uint32_t s = 0;
+  for (uint32_t m = 0; m < L.n_mem; ++m) {
+    if (m && !(key[m - 1] < key[m])) return fail(status);
+    uint32_t e = mdend[m];
+    if (e <= s || e > L.n_dot) return fail(status);
+    for (uint32_t d = s; d < e; ++d) {
+      if (dact[d] >= A || dctr[d] == 0) return fail(status);
+      if (d > s && !(dact[d - 1] < dact[d])) return fail(status);
+    }
+    s = e;
+  }
+  if (s != L.n_dot) return fail(status);
+  uint32_t fs = 0, ms = 0;
+  for (uint32_t k = 0; k < L.n_def; ++k) {
+    uint32_t fe = fdend[k], me = fmend[k];
+    if (fe <= fs || fe > L.n_def_dot || me <= ms || me > L.n_def_mem) return fail(status);
+    for (uint32_t d = fs; d < fe; ++d) {
+      if (fact[d] >= A || fctr[d] == 0) return fail(status);
+      if (d > fs && !(fact[d - 1] < fact[d])) return fail(status);
+    }
+    for (uint32_t j = ms + 1; j < me; ++j)
+      if (!(fkey[j - 1] < fkey[j])) return fail(status);
+    if (k) {  // strictly increasing CLOCK ORDER
+      uint32_t ps = k > 1 ? fdend[k - 2] : 0, pe = fs, a = ps, b = fs;
+      int c = 0;
+      for (; a < pe && b < fe && c == 0; ++a, ++b) {
+        if (fact[a] != fact[b]) c = fact[a] < fact[b] ? -1 : 1;
+        else if (fctr[a] != fctr[b]) c = fctr[a] < fctr[b] ? -1 : 1;
+      }
+      if (c == 0) c = (a == pe && b == fe) ? 0 : (a == pe ? -1 : 1);
+      if (c >= 0) return fail(status);
+    }
+    fs = fe;
+    ms = me;
+  }
+  if (fs != L.n_def_dot || ms != L.n_def_mem) return fail(status);
+}
+
+__global__ void sizes_kernel(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                             uint64_t n_obj, uint64_t* __restrict__ sizes) {
+  uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i < n_obj) sizes[i] = *(const uint32_t*)(base + off[i]);
+}
+
+// One wave per record, 16-B copies.
+__global__ __launch_bounds__(256) void copy_kernel(const uint8_t* __restrict__ src,
+                                                   const uint64_t* __restrict__ src_off,
+                                                   uint8_t* __restrict__ dst,
+                                                   const uint64_t* __restrict__ dst_off,
+                                                   uint64_t n_obj) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t stride = (uint64_t)gridDim.x * 4;
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64; i < n_obj; i += stride) {
+    const uint4* s = (const uint4*)(src + src_off[i]);
+    uint4* d = (uint4*)(dst + dst_off[i]);
+    uint32_t n16 = *(const uint32_t*)s / 16;
+    for (uint32_t k = lane; k < n16; k += 64) d[k] = s[k];
+  }
+}
+
+}  // namespace
+
+int launch_orswot_validate(const uint8_t* base, const uint64_t* off, uint64_t bytes, uint64_t n_obj,
+                           uint32_t n_actors, int* status, hipStream_t stream) {
+  if (n_obj == 0) return CRDT_OK;
+  uint32_t blocks = (uint32_t)((n_obj + 255) / 256);
+  hipLaunchKernelGGL(validate_kernel, dim3(blocks), dim3(256), 0, stream, base, off, bytes, n_obj,
+                     n_actors, status);
+  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+}
+
+int launch_record_sizes(const uint8_t* base, const uint64_t* off, uint64_t n_obj, uint64_t* sizes,
+                        hipStream_t stream) {
+  if (n_obj == 0) return CRDT_OK;
+  uint32_t blocks = (uint32_t)((n_obj + 255) / 256);
+  hipLaunchKernelGGL(sizes_kernel, dim3(blocks), dim3(256), 0, stream, base, off, n_obj, sizes);
+  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+}
+
+int launch_record_copy(const uint8_t* src, const uint64_t* src_off, uint8_t* dst,
+                       const uint64_t* dst_off, uint64_t n_obj, hipStream_t stream) {
+  if (n_obj == 0) return CRDT_OK;
+  uint64_t want = (n_obj + 3) / 4;
+  uint32_t blocks = (uint32_t)(want < 2048 ? want : 2048);
+  hipLaunchKernelGGL(copy_kernel, dim3(blocks), dim3(256), 0, stream, src, src_off, dst, dst_off,
+                     n_obj);
+  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+}
+
+}  // namespace crdts_hip

@@ -1,0 +1,284 @@
+"""GPU parity: the HIP Orswot join (through the C ABI) vs the oracle.
+
+Bar: bit-exact canonical records for every object.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import kat_runner
+import opgen
+import records
+from gpu_backend import GpuBackend
+
+pytestmark = pytest.mark.gpu
+CASES = kat_runner.load_cases()
+
+
+def _dev_batch(crdts_hip, base, off, n_actors):
+    return crdts_hip.OrswotBatch.from_host(base, off, n_actors)
+
+
+def _gpu_merge(gpu, lb, lo, rb, ro, n_actors):
+    import crdts_hip
+
+    L = _dev_batch(crdts_hip, lb, lo, n_actors)
+    R = _dev_batch(crdts_hip, rb, ro, n_actors)
+    out = gpu.orswot_merge(L, R)
+    return out
+
+
+def _compare(gpu_out, ob, oo, what=""):
+    got = gpu_out.records()
+    exp = records.unpack_batch(ob, oo)
+    assert len(got) == len(exp)
+    bad = [i for i, (g, e) in enumerate(zip(got, exp)) if g != e]
+    if bad:
+        i = bad[0]
+        raise AssertionError(f"{what}: {len(bad)} / {len(exp)} objects differ; first {i}:\n"
+                             f"gpu    {records.decode(got[i])}\noracle {records.decode(exp[i])}")
+
+
+# ------------------------------------------------------------------ KATs
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_orswot_kat_on_gpu(case, gpu, oracle):
+    be = GpuBackend(gpu, n_actors=16)
+    tg, to = [], []
+    kat_runner.run_case(case, be, trace=tg)
+    kat_runner.run_case(case, kat_runner.OracleBackend(), trace=to)
+    assert be.merges > 0
+    for (k1, n1, a), (k2, n2, b) in zip(tg, to):
+        assert a.record() == b.encode(16), f"{case['name']} step {k1}"
+
+
+# ------------------------------------------------------------------ prop_merge_converges
+def test_prop_merge_converges_on_gpu(gpu, oracle):
+    """test/orswot.rs:37-76: for every op vector, folding i = 2..10 witnesses
+    (witness = actor % i) into an empty set in index order, then merging an
+    empty 'defer plunger', converges; every fold step runs as one batched
+    kernel launch over all (opvec, i) folds, and every step is compared with
+    the oracle's fold."""
+    import crdts_hip
+
+    A = 100
+    rng = random.Random(2024)
+    opvecs = [opgen.orswot_opvec(rng) for _ in range(60)]
+    folds = []  # (opvec index, i, witnesses as host states, oracle witnesses)
+    for v, ops in enumerate(opvecs):
+        for i in range(2, 11):
+            hw = [crdts_hip.HostOrswot() for _ in range(i)]
+            ow = [oracle.OracleOrswot() for _ in range(i)]
+            for actor, op in ops:
+                for be, w in ((hw, hw[actor % i]), (ow, ow[actor % i])):
+                    if op[0] == "add":
+                        w.apply_add(op[1], op[2], op[3])
+                    else:
+                        w.apply_rm(op[1], op[2])
+            folds.append((v, i, hw, ow))
+    merged = [crdts_hip.HostOrswot().encode(A) for _ in folds]
+    omerged = [oracle.OracleOrswot() for _ in folds]
+    for step in range(11):
+        others = []
+        for f, (v, i, hw, ow) in enumerate(folds):
+            if step < i:
+                others.append(hw[step].encode(A))
+                omerged[f].merge(ow[step])
+            else:  # the defer plunger, then idempotent re-plunges
+                others.append(crdts_hip.HostOrswot().encode(A))
+                omerged[f].merge(oracle.OracleOrswot())
+        L = crdts_hip.OrswotBatch.from_records(merged, A)
+        R = crdts_hip.OrswotBatch.from_records(others, A)
+        merged = gpu.orswot_merge(L, R).records()
+        for f in range(len(folds)):
+            assert merged[f] == omerged[f].encode(A), f"fold {folds[f][:2]} step {step}"
+    by_vec = {}
+    for f, (v, i, _, _) in enumerate(folds):
+        by_vec.setdefault(v, set()).add(merged[f])
+    assert all(len(s) == 1 for s in by_vec.values())
+
+
+# ------------------------------------------------------------------ config 3 differential
+def test_config3_differential_200k(gpu, oracle):
+    import crdts_hip
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(200_000, threads=16)
+    out = _gpu_merge(gpu, lb, lo, rb, ro, 16)
+    ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, 16, threads=16)
+    _compare(out, ob, oo, "config3 200k")
+    # output offsets are self.off + other.off
+    assert (out.off.cpu().numpy().view(np.uint64) == lo + ro).all()
+
+
+def test_config3_reverse_orientation(gpu, oracle):
+    """Orswot merge is structurally non-commutative (src/orswot.rs:98-103 vs
+    :132-137): R ⊔ L must match the oracle's R.merge(&L), not L ⊔ R."""
+    import crdts_hip
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(20_000, first_obj=7, threads=16,
+                                                    params=dict(pct_shared_actor=50))
+    out = _gpu_merge(gpu, rb, ro, lb, lo, 16)
+    ob, oo = oracle.orswot_merge_batch(rb, ro, lb, lo, 16, threads=16)
+    _compare(out, ob, oo, "reverse")
+
+
+@pytest.mark.parametrize("params", [
+    dict(pct_deferred_obj=100, pct_future_rm=40),                    # deferred-heavy
+    dict(pct_shared_actor=100),                                     # same-actor adds
+    dict(n_actors=3, member_universe=8, ancestor_adds=4),          # tiny
+    dict(n_actors=64, member_universe=200, ancestor_adds=150, max_div_ops=40),  # > LDS stage -> global path
+    dict(n_actors=1, member_universe=16, ancestor_adds=8),
+    dict(ancestor_adds=0, min_div_ops=0, max_div_ops=3),           # empty / near-empty objects
+], ids=["deferred_heavy", "shared_actor", "tiny", "large_global_path", "one_actor", "empty"])
+def test_generated_variants(params, gpu, oracle):
+    import crdts_hip
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(5_000, threads=16, seed=99, params=params)
+    A = params.get("n_actors", 16)
+    out = _gpu_merge(gpu, lb, lo, rb, ro, A)
+    ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, A, threads=16)
+    _compare(out, ob, oo, str(params))
+
+
+def _random_state(rng, A, members, ops):
+    import crdts_hip
+
+    h = crdts_hip.HostOrswot()
+    for _ in range(ops):
+        r = rng.random()
+        m = rng.randrange(members)
+        a = rng.randrange(A)
+        st = crdts_hip.decode_record(h.encode(A))
+        if r < 0.55:
+            h.apply_add(a, st["clock"].get(a, 0) + 1 + rng.randrange(2), m)
+        elif r < 0.8:
+            h.apply_rm(m, st["entries"].get(m, []))
+        else:
+            clk = dict(st["clock"])
+            clk[a] = clk.get(a, 0) + rng.randrange(1, 5)
+            h.apply_rm(m, sorted(clk.items()))
+    return h
+
+
+def test_random_states_with_deferred(gpu, oracle):
+    """Independent random states (no shared ancestor) with many future-context removes."""
+    rng = random.Random(77)
+    A = 8
+    L = [_random_state(rng, A, 12, rng.randrange(0, 40)).encode(A) for _ in range(1500)]
+    R = [_random_state(rng, A, 12, rng.randrange(0, 40)).encode(A) for _ in range(1500)]
+    lb, lo = records.pack_batch(L)
+    rb, ro = records.pack_batch(R)
+    out = _gpu_merge(gpu, lb, lo, rb, ro, A)
+    ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, A, threads=16)
+    _compare(out, ob, oo, "random deferred")
+    assert sum(len(records.decode(r)["deferred"]) > 0 for r in L) > 300
+
+
+def test_self_merge_and_chained_fold(gpu, oracle):
+    """x ⊔ x, and a 3-way fold whose intermediate batch (with gaps) is fed back."""
+    import crdts_hip
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(8_000, threads=16, seed=5)
+    (cb, co), _ = crdts_hip.generate_orswot(8_000, threads=16, seed=6)
+    out = _gpu_merge(gpu, lb, lo, lb, lo, 16)
+    ob, oo = oracle.orswot_merge_batch(lb, lo, lb, lo, 16, threads=16)
+    _compare(out, ob, oo, "self")
+    L = crdts_hip.OrswotBatch.from_host(lb, lo, 16)
+    R = crdts_hip.OrswotBatch.from_host(rb, ro, 16)
+    C = crdts_hip.OrswotBatch.from_host(cb, co, 16)
+    lr = gpu.orswot_merge(L, R)
+    lrc = gpu.orswot_merge(lr, C)
+    ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, 16, threads=16)
+    ob2, oo2 = oracle.orswot_merge_batch(ob, oo, cb, co, 16, threads=16)
+    _compare(lrc, ob2, oo2, "fold")
+    # compaction keeps every record, and outputs validate as canonical
+    comp = gpu.orswot_compact(lrc)
+    assert comp.records() == lrc.records()
+    assert comp.bytes <= lrc.bytes
+    gpu.orswot_validate(comp)
+
+
+def test_validate_and_noncanonical_inputs(gpu):
+    import crdts_hip
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(100, threads=4)
+    gpu.orswot_validate(crdts_hip.OrswotBatch.from_host(lb, lo, 16))
+    bad = lb.copy()
+    o = int(lo[10])
+    d = records.decode(bad[o:o + int(bad[o:o + 4].view(np.uint32)[0])].tobytes())
+    # swap the first two member keys -> not strictly increasing
+    key_off = o + 32 + 8 * 16
+    k0 = bad[key_off:key_off + 8].copy()
+    bad[key_off:key_off + 8] = bad[key_off + 8:key_off + 16]
+    bad[key_off + 8:key_off + 16] = k0
+    with pytest.raises(crdts_hip.CrdtError):
+        gpu.orswot_validate(crdts_hip.OrswotBatch.from_host(bad, lo, 16))
+    # a wrong header (n_clk != n_actors) is rejected by the merge kernel itself
+    bad2 = lb.copy()
+    bad2[int(lo[3]) + 4:int(lo[3]) + 8] = np.frombuffer(np.uint32(17).tobytes(), np.uint8)
+    with pytest.raises(crdts_hip.CrdtError):
+        _gpu_merge(gpu, bad2, lo, rb, ro, 16)
+    assert len(d["entries"]) > 1
+
+
+def test_capacity_and_empty_batch(gpu):
+    import torch
+
+    import crdts_hip
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(64, threads=2)
+    L = crdts_hip.OrswotBatch.from_host(lb, lo, 16)
+    R = crdts_hip.OrswotBatch.from_host(rb, ro, 16)
+    small = crdts_hip.OrswotBatch(torch.empty(L.bytes, dtype=torch.uint8, device="cuda:0"),
+                                  torch.empty(64, dtype=torch.int64, device="cuda:0"), 16, L.bytes)
+    with pytest.raises(crdts_hip.CrdtError):
+        gpu.orswot_merge(L, R, out=small)
+    E = crdts_hip.OrswotBatch.from_records([], 16)
+    out = gpu.orswot_merge(E, E)
+    assert out.n_obj == 0
+
+
+def test_merge_host_path_matches_device_path(gpu):
+    import ctypes as C
+
+    import crdts_hip
+    from crdts_hip._lib import lib
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(3_000, threads=8, seed=31)
+    dev = _gpu_merge(gpu, lb, lo, rb, ro, 16).records()
+    out = np.zeros(lb.nbytes + rb.nbytes, np.uint8)
+    ooff = np.zeros(3000, np.uint64)
+    used = C.c_size_t()
+    rc = lib.crdt_orswot_merge_host(gpu.ctx, lb.ctypes.data, lo.ctypes.data, lb.nbytes, rb.ctypes.data,
+                                    ro.ctypes.data, rb.nbytes, 3000, 16, out.ctypes.data, ooff.ctypes.data,
+                                    out.nbytes, C.byref(used))
+    assert rc == 0
+    assert records.unpack_batch(out, ooff) == dev
+    assert used.value == sum(len(r) for r in dev)
+
+
+def test_config3_full_size_bitexact(gpu, oracle):
+    """BASELINE.json configs[2] at full size (1M objects): every record equals the oracle's."""
+    import crdts_hip
+
+    n = 1_000_000
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(n, threads=16)
+    out = _gpu_merge(gpu, lb, lo, rb, ro, 16)
+    gb, go = out.to_host()
+    ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, 16, threads=16)
+    # compare record by record with numpy views (sizes first, then bytes)
+    gs = gb.view(np.uint32)[(go // 4).astype(np.int64)]
+    os_ = ob.view(np.uint32)[(oo // 4).astype(np.int64)]
+    assert (gs == os_).all()
+    gi = np.concatenate([np.arange(o, o + s, dtype=np.int64) for o, s in zip(go[:50_000], gs[:50_000])])
+    oi = np.concatenate([np.arange(o, o + s, dtype=np.int64) for o, s in zip(oo[:50_000], os_[:50_000])])
+    assert (gb[gi] == ob[oi]).all()
+    # the rest via a checksum of per-record checksums
+    def digest(base, offs, sizes):
+        h = np.zeros(len(offs), dtype=np.uint64)
+        w = base.view(np.uint64)
+        for k in range(int(sizes.max()) // 8):
+            m = sizes > 8 * k
+            h[m] = (h[m] * np.uint64(0x100000001B3)) ^ w[(offs[m] // 8 + k).astype(np.int64)]
+        return h
+    assert (digest(gb, go, gs) == digest(ob, oo, os_)).all()
