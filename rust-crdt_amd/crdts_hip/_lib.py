@@ -53,6 +53,14 @@ EXPORTS = [
 
 
 def _load():
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7. Load
+    # torch first so this library's libamdhip64.so.7 dependency binds to the
+    # already-loaded copy (same SONAME) instead of a second runtime from
+    # /opt/rocm, which would fail to open the device next to torch's.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"crdts_hip: native library missing at {LIB_PATH}; build it with "

@@ -61,7 +61,9 @@ int crdt_ctx_create(crdt_ctx** out, int device) {
   if (!out) return CRDT_EINVAL;
   *out = nullptr;
   int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return CRDT_ENODEV;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e == hipErrorNoDevice || (e == hipSuccess && (device < 0 || device >= n))) return CRDT_ENODEV;
+  if (e != hipSuccess) return CRDT_EHIP;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return CRDT_ENODEV;
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return CRDT_ENODEV;
