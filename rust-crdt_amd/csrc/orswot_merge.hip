@@ -3,21 +3,28 @@
 // out[i] = self[i].merge(&other[i]) — CvRDT for Orswot, src/orswot.rs:87-157,
 // including apply_deferred (:235-243) / apply_remove (:195-211).
 //
-// Per object (one wave64):
-//  1. both input records are copied HBM -> LDS with 16-B loads (records are
-//     16-B aligned and padded) — the only HBM reads of the object;
-//  2. members: the two sorted key lists are merged by MERGE PATH, one union
-//     position per lane (ties put self first, so a key present on both sides
-//     is handled by the self lane and its twin lane idles). Per position the
-//     lane computes the joined dot run with the reference's case rules
-//     (self-only :94-104, both :105-128, other-only :132-138) and the
-//     deferred-remove subtraction (:195-211), in two passes: a count pass
-//     (fixes the output section offsets) and a write pass (wave ballot /
-//     prefix sums give each kept member its slot and dot offset);
-//  3. deferred: the union of both deferred maps keyed by clock (:141-148),
-//     kept iff !(D <= merged clock) (:197); rare, done by lane 0;
-//  4. the top clock is the pointwise max (:153), written by lanes < n_actors.
-// The output record is written straight to its final place in HBM.
+// Work assignment: each wave owns chunks of 64 consecutive objects. Per chunk
+// lane k loads object k's two offsets and two record headers in one
+// coalesced step (2 dependent HBM round trips per 64 objects), and writes the
+// chunk's 64 output offsets in one store. Per object, the wave then
+//  1. copies both input records HBM -> registers -> LDS with 16-B loads; the
+//     loads for object t+1 are issued before object t is computed, so their
+//     HBM latency hides behind the join (software pipeline, 1 object deep);
+//  2. merges the two sorted member-key lists by MERGE PATH, one union
+//     position per lane (self first on ties: a key present on both sides is
+//     handled by the self lane, its twin lane idles), and per position runs
+//     one join loop over the two actor-sorted dot runs implementing the
+//     reference's rules — self-only :94-104, both :105-128, other-only
+//     :132-138 — followed by the deferred subtraction (:195-211);
+//  3. a count pass fixes the output section offsets (wave ballot + prefix
+//     sum), a write pass stores keys / dots / ends straight to the final
+//     place of the output record in HBM;
+//  4. deferred maps: union keyed by clock (:141-148), kept iff
+//     !(D <= merged clock) (:197); rare, done by lane 0;
+//  5. top clock = pointwise max (:153), written by lanes < n_actors.
+// Records larger than the LDS stage (kStageBytes) are flagged in the output
+// offset (bit 63) and joined by orswot_merge_big_kernel with the same code
+// (staged through a larger LDS buffer, or straight from HBM).
 //
 // Canonical record layout: include/crdts_hip.h, record_layout.h.
 #include <hip/hip_runtime.h>
@@ -31,8 +38,9 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
-constexpr uint32_t kStageBytes = 2048;  // LDS staging per input record per wave
-constexpr uint32_t kCache = 128;        // cached union positions per wave
+constexpr uint32_t kStageBytes = 2048;                     // LDS stage per input record per wave
+constexpr uint32_t kPer = kStageBytes / 16 / kWave;        // 16-B pieces per lane per record
+constexpr uint64_t kPending = 1ull << 63;                   // Ooff flag: record left for the big kernel
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -44,7 +52,12 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t lane_of(uint32_t v, uint32_t t) { return __builtin_amdgcn_readlane(v, t); }
+__device__ __forceinline__ uint64_t lane_of64(uint64_t v, uint32_t t) {
+  return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), t) << 32) |
+         __builtin_amdgcn_readlane((uint32_t)v, t);
+}
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
@@ -61,59 +74,55 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
   return v;
 }
 
-// Read-only view of one record (generic pointers; the staged path points
-// into LDS and the compiler's address-space inference keeps ds_* loads).
-struct View {
-  const uint64_t* clk;
-  const uint64_t* key;
-  const uint64_t* dctr;
-  const uint32_t* dact;
-  const uint32_t* mdend;
-  const uint64_t* fctr;
-  const uint64_t* fkey;
-  const uint32_t* fact;
-  const uint32_t* fdend;
-  const uint32_t* fmend;
-  uint32_t n_mem, n_dot, n_def, n_def_dot, n_def_mem;
+// Byte offsets of one record's sections (wave-uniform), relative to its base.
+struct RV {
+  uint32_t clk, key, dctr, dact, mdend, fctr, fkey, fact, fdend, fmend;
+  uint32_t n_mem, n_def;
 };
 
-__device__ __forceinline__ View make_view(const uint8_t* rec, const RecLayout& L) {
-  View v;
-  v.clk = (const uint64_t*)(rec + L.o_clk);
-  v.key = (const uint64_t*)(rec + L.o_key);
-  v.dctr = (const uint64_t*)(rec + L.o_dctr);
-  v.dact = (const uint32_t*)(rec + L.o_dact);
-  v.mdend = (const uint32_t*)(rec + L.o_mdend);
-  v.fctr = (const uint64_t*)(rec + L.o_fctr);
-  v.fkey = (const uint64_t*)(rec + L.o_fkey);
-  v.fact = (const uint32_t*)(rec + L.o_fact);
-  v.fdend = (const uint32_t*)(rec + L.o_fdend);
-  v.fmend = (const uint32_t*)(rec + L.o_fmend);
-  v.n_mem = L.n_mem; v.n_dot = L.n_dot; v.n_def = L.n_def;
-  v.n_def_dot = L.n_def_dot; v.n_def_mem = L.n_def_mem;
+__device__ __forceinline__ RV make_rv(const RecLayout& L) {
+  RV v;
+  v.clk = L.o_clk; v.key = L.o_key; v.dctr = L.o_dctr; v.dact = L.o_dact; v.mdend = L.o_mdend;
+  v.fctr = L.o_fctr; v.fkey = L.o_fkey; v.fact = L.o_fact; v.fdend = L.o_fdend; v.fmend = L.o_fmend;
+  v.n_mem = L.n_mem; v.n_def = L.n_def;
   return v;
 }
 
-__device__ __forceinline__ uint64_t top(const View& v, uint32_t a, uint32_t n_actors) {
-  return a < n_actors ? v.clk[a] : 0ull;  // VClock::get, absent = 0 (src/vclock.rs:206-210)
+// Record accessors (base = LDS stage or HBM record; offsets in bytes).
+__device__ __forceinline__ uint64_t g64(const uint8_t* b, uint32_t off, uint32_t i) {
+  return *(const uint64_t*)(b + off + 8u * i);
+}
+__device__ __forceinline__ uint32_t g32(const uint8_t* b, uint32_t off, uint32_t i) {
+  return *(const uint32_t*)(b + off + 4u * i);
+}
+// VClock::get on a dense top clock, absent = 0 (src/vclock.rs:206-210)
+__device__ __forceinline__ uint64_t top(const uint8_t* b, const RV& v, uint32_t a, uint32_t A) {
+  return a < A ? g64(b, v.clk, a) : 0ull;
+}
+__device__ __forceinline__ uint32_t run_begin(const uint8_t* b, uint32_t off, uint32_t k) {
+  return k ? g32(b, off, k - 1) : 0u;
 }
 
-// D[x] for deferred clock k of side v (sorted run), 0 if absent.
-__device__ __forceinline__ uint64_t def_get(const View& v, uint32_t k, uint32_t x) {
-  uint32_t s = k ? v.fdend[k - 1] : 0, e = v.fdend[k];
-  for (uint32_t d = s; d < e; ++d) {
-    uint32_t a = v.fact[d];
-    if (a == x) return v.fctr[d];
-    if (a > x) break;
+struct Side {
+  const uint8_t* b;
+  RV v;
+};
+
+// D[x] for deferred clock k (actor-sorted run), 0 if absent.
+__device__ __forceinline__ uint64_t def_get(const Side& s, uint32_t k, uint32_t x) {
+  uint32_t e = g32(s.b, s.v.fdend, k);
+  for (uint32_t d = run_begin(s.b, s.v.fdend, k); d < e; ++d) {
+    uint32_t a = g32(s.b, s.v.fact, d);
+    if (a >= x) return a == x ? g64(s.b, s.v.fctr, d) : 0ull;
   }
-  return 0;
+  return 0ull;
 }
 
-__device__ __forceinline__ bool def_has_member(const View& v, uint32_t k, uint64_t m) {
-  uint32_t lo = k ? v.fmend[k - 1] : 0, hi = v.fmend[k];
+__device__ __forceinline__ bool def_has_member(const Side& s, uint32_t k, uint64_t m) {
+  uint32_t lo = run_begin(s.b, s.v.fmend, k), hi = g32(s.b, s.v.fmend, k);
   while (lo < hi) {
     uint32_t mid = (lo + hi) >> 1;
-    uint64_t km = v.fkey[mid];
+    uint64_t km = g64(s.b, s.v.fkey, mid);
     if (km == m) return true;
     if (km < m) lo = mid + 1; else hi = mid;
   }
@@ -121,108 +130,101 @@ __device__ __forceinline__ bool def_has_member(const View& v, uint32_t k, uint64
 }
 
 // apply_deferred over the union of both deferred maps (src/orswot.rs:235-243):
-// apply_remove subtracts D from entries[m] for every (D, m) — regardless of
-// whether D is re-deferred — dropping dot (x, v) iff D[x] >= v
-// (VClock::subtract, src/vclock.rs:236-242). Order-independent.
-__device__ __forceinline__ bool killed_by_deferred(const View& L, const View& R, uint64_t m,
-                                                   uint32_t x, uint64_t v) {
-  for (uint32_t k = 0; k < L.n_def; ++k)
+// apply_remove subtracts D from entries[m] for every (D, m) — whether or not
+// D is re-deferred — dropping dot (x, v) iff D[x] >= v (VClock::subtract,
+// src/vclock.rs:236-242). Order-independent, and duplicates are harmless.
+__device__ __forceinline__ bool killed(const Side& L, const Side& R, uint64_t m, uint32_t x, uint64_t v) {
+  for (uint32_t k = 0; k < L.v.n_def; ++k)
     if (def_has_member(L, k, m) && def_get(L, k, x) >= v) return true;
-  for (uint32_t k = 0; k < R.n_def; ++k)
+  for (uint32_t k = 0; k < R.v.n_def; ++k)
     if (def_has_member(R, k, m) && def_get(R, k, x) >= v) return true;
   return false;
 }
 
-// Merge path: candidate at union position p of the two sorted key lists
-// (self first on ties). Returns type, self index i, other index j.
-__device__ __forceinline__ uint32_t merge_path(const View& L, const View& R, uint32_t p,
-                                               uint32_t& i, uint32_t& j) {
-  uint32_t nL = L.n_mem, nR = R.n_mem;
-  uint32_t lo = p > nR ? p - nR : 0, hi = p < nL ? p : nL;
-  while (lo < hi) {
-    uint32_t mid = (lo + hi) >> 1;
-    if (L.key[mid] <= R.key[p - 1 - mid]) lo = mid + 1; else hi = mid;
+// Merge path: the candidate at union position p (self first on ties).
+// Branch-free binary search with a fixed trip count (no per-lane loop
+// control): i = number of self keys among the first p union positions.
+__device__ __forceinline__ uint32_t merge_path(const Side& L, const Side& R, uint32_t p, uint32_t& i,
+                                               uint32_t& j) {
+  const uint32_t nL = L.v.n_mem, nR = R.v.n_mem;
+  uint32_t lo = p > nR ? p - nR : 0, len = (p < nL ? p : nL) - lo;
+  const uint32_t steps = 32u - __builtin_clz(uni(nL < nR ? nL : nR) | 1u);  // >= log2(len + 1)
+  for (uint32_t s = 0; s <= steps; ++s) {
+    const uint32_t half = len >> 1, mid = lo + half;
+    const bool go = len != 0 && g64(L.b, L.v.key, mid) <= g64(R.b, R.v.key, p - 1 - mid);
+    lo = go ? mid + 1 : lo;
+    len = len == 0 ? 0 : (go ? len - half - 1 : half);
   }
   i = lo;
   j = p - lo;
-  if (i < nL && (j >= nR || L.key[i] <= R.key[j])) {
-    return (j < nR && L.key[i] == R.key[j]) ? kBoth : kSelf;
-  }
-  if (i > 0 && L.key[i - 1] == R.key[j]) return kNone;  // twin of a kBoth at p-1
+  const uint64_t kl = i < nL ? g64(L.b, L.v.key, i) : ~0ull;
+  const uint64_t kr = j < nR ? g64(R.b, R.v.key, j) : ~0ull;
+  if (i < nL && (j >= nR || kl <= kr)) return (j < nR && kl == kr) ? kBoth : kSelf;
+  if (i > 0 && g64(L.b, L.v.key, i - 1) == kr) return kNone;  // twin of a kBoth at p-1
   return kOther;
 }
 
-// Joined dot run of one member, emitted in actor order: emit(actor, counter).
-// Rules: src/orswot.rs:94-104 (self-only), :105-128 (both), :132-138 (other-only);
-// then the deferred subtraction. Lc/Rc are the PRE-merge top clocks.
-template <class Emit>
-__device__ __forceinline__ void join_member(uint32_t type, uint32_t i, uint32_t j, const View& L,
-                                            const View& R, uint32_t n_actors, bool has_def,
-                                            Emit&& emit) {
-  uint64_t m = type == kOther ? R.key[j] : L.key[i];
-  auto out = [&](uint32_t x, uint64_t v) {
-    if (!has_def || !killed_by_deferred(L, R, m, x, v)) emit(x, v);
-  };
+// The joined dot run of one member; returns its length. MODE 0 counts and
+// captures the first output dot in (x0, v0); MODE 1 also stores the run at
+// oact/octr[d0..]. Lc/Rc are the PRE-merge top clocks. One loop step per
+// actor of the union of both runs, branch-free inside.
+template <int MODE>
+__device__ __forceinline__ uint32_t join(const Side& L, const Side& R, uint32_t type, uint32_t i,
+                                         uint32_t j, uint32_t A, bool has_def, uint32_t& x0, uint64_t& v0,
+                                         uint32_t* oact, uint64_t* octr, uint32_t d0) {
+  uint32_t a = 0, ae = 0, b = 0, be = 0;
+  if (type & kSelf) { a = run_begin(L.b, L.v.mdend, i); ae = g32(L.b, L.v.mdend, i); }
+  if (type & kOther) { b = run_begin(R.b, R.v.mdend, j); be = g32(R.b, R.v.mdend, j); }
   if (type == kSelf) {
-    // keep the entry UNCHANGED iff !(clock <= other.clock)  (:98-103)
-    uint32_t s = i ? L.mdend[i - 1] : 0, e = L.mdend[i];
-    bool le = true;
-    for (uint32_t d = s; d < e; ++d)
-      if (L.dctr[d] > top(R, L.dact[d], n_actors)) { le = false; break; }
-    if (!le)
-      for (uint32_t d = s; d < e; ++d) out(L.dact[d], L.dctr[d]);
-  } else if (type == kOther) {
-    // clock.subtract(&self.clock); keep dots with R[x] > Lc[x]  (:133)
-    uint32_t s = j ? R.mdend[j - 1] : 0, e = R.mdend[j];
-    for (uint32_t d = s; d < e; ++d) {
-      uint32_t x = R.dact[d];
-      uint64_t v = R.dctr[d];
-      if (v > top(L, x, n_actors)) out(x, v);
-    }
-  } else {
-    // common = intersection; (L - common) - Rc; (R - common) - Lc; max of all (:109-116)
-    uint32_t a = i ? L.mdend[i - 1] : 0, ae = L.mdend[i];
-    uint32_t b = j ? R.mdend[j - 1] : 0, be = R.mdend[j];
-    while (a < ae || b < be) {
-      uint32_t xa = a < ae ? L.dact[a] : 0xFFFFFFFFu;
-      uint32_t xb = b < be ? R.dact[b] : 0xFFFFFFFFu;
-      if (xa < xb) {
-        uint64_t v = L.dctr[a++];
-        if (v > top(R, xa, n_actors)) out(xa, v);
-      } else if (xb < xa) {
-        uint64_t v = R.dctr[b++];
-        if (v > top(L, xb, n_actors)) out(xb, v);
-      } else {
-        uint64_t va = L.dctr[a++], vb = R.dctr[b++];
-        if (va == vb) {
-          out(xa, va);
-        } else {
-          uint64_t lp = va > top(R, xa, n_actors) ? va : 0;
-          uint64_t rp = vb > top(L, xa, n_actors) ? vb : 0;
-          uint64_t mx = lp > rp ? lp : rp;
-          if (mx) out(xa, mx);
-        }
+    // a self-only entry is kept UNCHANGED iff !(clock <= other.clock) (:98-103)
+    bool any = false;
+    for (uint32_t d = a; d < ae && !any; ++d)
+      any = g64(L.b, L.v.dctr, d) > top(R.b, R.v, g32(L.b, L.v.dact, d), A);
+    if (!any) ae = a;
+  }
+  uint64_t m = 0;
+  if (has_def) m = (type & kSelf) ? g64(L.b, L.v.key, i) : g64(R.b, R.v.key, j);
+  uint32_t c = 0;
+  while (a < ae || b < be) {
+    const bool ha = a < ae, hb = b < be;
+    const uint32_t xa = ha ? g32(L.b, L.v.dact, a) : 0xFFFFFFFFu;
+    const uint32_t xb = hb ? g32(R.b, R.v.dact, b) : 0xFFFFFFFFu;
+    const bool ta = xa <= xb, tb = xb <= xa;  // which run(s) hold actor x
+    const uint32_t x = ta ? xa : xb;
+    const uint64_t va = ta ? g64(L.b, L.v.dctr, a) : 0ull;
+    const uint64_t vb = tb ? g64(R.b, R.v.dctr, b) : 0ull;
+    const uint64_t rc = top(R.b, R.v, x, A), lc = top(L.b, L.v, x, A);
+    // self-only: the whole run (kept); otherwise L[x] survives iff > Rc[x]
+    // (:112, :133 analogue), R[x] iff > Lc[x] (:113, :133); a dot equal on
+    // both sides is common (:109) and survives as is; result = max (:115-116)
+    const uint64_t lp = (ta && (type == kSelf || va > rc)) ? va : 0ull;
+    const uint64_t rp = (tb && vb > lc) ? vb : 0ull;
+    uint64_t v = (ta && tb && va == vb) ? va : (lp > rp ? lp : rp);
+    a += ta ? 1u : 0u;
+    b += tb ? 1u : 0u;
+    if (v != 0 && has_def && killed(L, R, m, x, v)) v = 0;
+    if (v != 0) {
+      if (MODE == 1) {
+        oact[d0 + c] = x;
+        octr[d0 + c] = v;
+      } else if (c == 0) {
+        x0 = x;
+        v0 = v;
       }
+      ++c;
     }
   }
-}
-
-__device__ __forceinline__ uint32_t count_member(uint32_t type, uint32_t i, uint32_t j, const View& L,
-                                                 const View& R, uint32_t n_actors, bool has_def) {
-  if (type == kNone) return 0;
-  uint32_t c = 0;
-  join_member(type, i, j, L, R, n_actors, has_def, [&](uint32_t, uint64_t) { ++c; });
   return c;
 }
 
 // CLOCK ORDER compare of deferred clock k of X with deferred clock l of Y.
-__device__ __forceinline__ int clock_cmp(const View& X, uint32_t k, const View& Y, uint32_t l) {
-  uint32_t a = k ? X.fdend[k - 1] : 0, ae = X.fdend[k];
-  uint32_t b = l ? Y.fdend[l - 1] : 0, be = Y.fdend[l];
+__device__ __forceinline__ int clock_cmp(const Side& X, uint32_t k, const Side& Y, uint32_t l) {
+  uint32_t a = run_begin(X.b, X.v.fdend, k), ae = g32(X.b, X.v.fdend, k);
+  uint32_t b = run_begin(Y.b, Y.v.fdend, l), be = g32(Y.b, Y.v.fdend, l);
   for (; a < ae && b < be; ++a, ++b) {
-    uint32_t xa = X.fact[a], xb = Y.fact[b];
+    uint32_t xa = g32(X.b, X.v.fact, a), xb = g32(Y.b, Y.v.fact, b);
     if (xa != xb) return xa < xb ? -1 : 1;
-    uint64_t va = X.fctr[a], vb = Y.fctr[b];
+    uint64_t va = g64(X.b, X.v.fctr, a), vb = g64(Y.b, Y.v.fctr, b);
     if (va != vb) return va < vb ? -1 : 1;
   }
   if (a == ae && b == be) return 0;
@@ -230,13 +232,13 @@ __device__ __forceinline__ int clock_cmp(const View& X, uint32_t k, const View& 
 }
 
 // !(D <= merged clock): some dot of D exceeds max(Lc, Rc)  (src/orswot.rs:197)
-__device__ __forceinline__ bool def_survives(const View& X, uint32_t k, const View& L, const View& R,
-                                             uint32_t n_actors) {
-  uint32_t s = k ? X.fdend[k - 1] : 0, e = X.fdend[k];
-  for (uint32_t d = s; d < e; ++d) {
-    uint32_t x = X.fact[d];
-    uint64_t lc = top(L, x, n_actors), rc = top(R, x, n_actors);
-    if (X.fctr[d] > (lc > rc ? lc : rc)) return true;
+__device__ __forceinline__ bool def_survives(const Side& X, uint32_t k, const Side& L, const Side& R,
+                                             uint32_t A) {
+  uint32_t e = g32(X.b, X.v.fdend, k);
+  for (uint32_t d = run_begin(X.b, X.v.fdend, k); d < e; ++d) {
+    uint32_t x = g32(X.b, X.v.fact, d);
+    uint64_t lc = top(L.b, L.v, x, A), rc = top(R.b, R.v, x, A);
+    if (g64(X.b, X.v.fctr, d) > (lc > rc ? lc : rc)) return true;
   }
   return false;
 }
@@ -250,27 +252,28 @@ struct DefOut {
 };
 
 // Deferred union + filter (src/orswot.rs:141-148, then :155 -> :197-203),
-// single lane. If `w` is null only counts.
-__device__ void deferred_pass(const View& L, const View& R, uint32_t n_actors, uint32_t& nd,
-                              uint32_t& ndd, uint32_t& ndm, const DefOut* w) {
+// single lane. With w == nullptr only counts.
+__device__ void deferred_pass(const Side& L, const Side& R, uint32_t A, uint32_t& nd, uint32_t& ndd,
+                              uint32_t& ndm, const DefOut* w) {
   uint32_t k = 0, l = 0;
   nd = ndd = ndm = 0;
-  while (k < L.n_def || l < R.n_def) {
-    int c = k >= L.n_def ? 1 : (l >= R.n_def ? -1 : clock_cmp(L, k, R, l));
-    const View& X = c <= 0 ? L : R;
-    uint32_t kx = c <= 0 ? k : l;
-    if (def_survives(X, kx, L, R, n_actors)) {
-      uint32_t s = kx ? X.fdend[kx - 1] : 0, e = X.fdend[kx];
-      for (uint32_t d = s; d < e; ++d) {
-        if (w) { w->fact[ndd] = X.fact[d]; w->fctr[ndd] = X.fctr[d]; }
+  while (k < L.v.n_def || l < R.v.n_def) {
+    const int c = k >= L.v.n_def ? 1 : (l >= R.v.n_def ? -1 : clock_cmp(L, k, R, l));
+    const Side& X = c <= 0 ? L : R;
+    const uint32_t kx = c <= 0 ? k : l;
+    if (def_survives(X, kx, L, R, A)) {
+      uint32_t e = g32(X.b, X.v.fdend, kx);
+      for (uint32_t d = run_begin(X.b, X.v.fdend, kx); d < e; ++d) {
+        if (w) { w->fact[ndd] = g32(X.b, X.v.fact, d); w->fctr[ndd] = g64(X.b, X.v.fctr, d); }
         ++ndd;
       }
       // member set: self's, other's, or the sorted union of both (c == 0)
       uint32_t a = 0, ae = 0, b = 0, be = 0;
-      if (c <= 0) { a = k ? L.fmend[k - 1] : 0; ae = L.fmend[k]; }
-      if (c >= 0) { b = l ? R.fmend[l - 1] : 0; be = R.fmend[l]; }
+      if (c <= 0) { a = run_begin(L.b, L.v.fmend, k); ae = g32(L.b, L.v.fmend, k); }
+      if (c >= 0) { b = run_begin(R.b, R.v.fmend, l); be = g32(R.b, R.v.fmend, l); }
       while (a < ae || b < be) {
-        uint64_t ka = a < ae ? L.fkey[a] : ~0ull, kb = b < be ? R.fkey[b] : ~0ull;
+        const uint64_t ka = a < ae ? g64(L.b, L.v.fkey, a) : ~0ull;
+        const uint64_t kb = b < be ? g64(R.b, R.v.fkey, b) : ~0ull;
         uint64_t km;
         if (a < ae && (b >= be || ka < kb)) { km = ka; ++a; }
         else if (b < be && (a >= ae || kb < ka)) { km = kb; ++b; }
@@ -286,122 +289,141 @@ __device__ void deferred_pass(const View& L, const View& R, uint32_t n_actors, u
   }
 }
 
-// Merge one pair; Lr/Rr point at the (staged or global) input records.
-__device__ __forceinline__ void merge_pair(const uint8_t* Lr, const RecLayout& LL, const uint8_t* Rr,
-                                           const RecLayout& RL, uint8_t* O, uint32_t n_actors,
-                                           uint32_t* cid, uint16_t* ccnt, uint32_t lane) {
-  const View L = make_view(Lr, LL);
-  const View R = make_view(Rr, RL);
-  const bool has_def = (L.n_def | R.n_def) != 0;
-  const uint32_t P = L.n_mem + R.n_mem;
+__device__ __forceinline__ RecLayout layout_at(const uint8_t* rec) {
+  const uint32_t* h = (const uint32_t*)rec;
+  RecLayout L;
+  rec_layout(L, uni(h[1]), uni(h[2]), uni(h[3]), uni(h[4]), uni(h[5]), uni(h[6]));
+  return L;
+}
 
-  // ---- pass 1: per-position join counts -> output member/dot totals
+// Join one object pair whose records sit at Ls / Rs (LDS stage or HBM) into
+// the output record at O (HBM).
+__device__ __forceinline__ void merge_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* O, uint32_t A,
+                                             uint32_t lane) {
+  const RecLayout LL = layout_at(Ls), RL = layout_at(Rs);
+  const Side L{Ls, make_rv(LL)}, R{Rs, make_rv(RL)};
+  const bool has_def = (L.v.n_def | R.v.n_def) != 0;
+  const uint32_t P = L.v.n_mem + R.v.n_mem;
+
+  // ---- pass 1: per-position join -> member / dot totals. For the first
+  // two 64-wide chunks each lane keeps its candidate, count and first output
+  // dot in registers for pass 2; later chunks are recomputed.
+  uint32_t q0 = 0, c0 = 0, x0 = 0, q1 = 0, c1 = 0, x1 = 0;
+  uint64_t v0 = 0, v1 = 0;
   uint32_t tot_mem = 0, tot_dot = 0;
   for (uint32_t base = 0; base < P; base += kWave) {
-    uint32_t p = base + lane;
-    uint32_t cnt = 0, type = kNone, i = 0, j = 0;
+    const uint32_t p = base + lane;
+    uint32_t type = kNone, i = 0, j = 0, cnt = 0, x = 0;
+    uint64_t v = 0;
     if (p < P) {
       type = merge_path(L, R, p, i, j);
-      cnt = count_member(type, i, j, L, R, n_actors, has_def);
-      if (p < kCache) { cid[p] = (type << 30) | (i << 15) | j; ccnt[p] = (uint16_t)cnt; }
+      if (type != kNone) cnt = join<0>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0);
     }
-    tot_mem += (uint32_t)__popcll(__ballot(cnt > 0));
+    const uint32_t q = (type << 30) | (i << 15) | j;
+    if (base == 0) { q0 = q; c0 = cnt; x0 = x; v0 = v; }
+    else if (base == kWave) { q1 = q; c1 = cnt; x1 = x; v1 = v; }
+    tot_mem += (uint32_t)__popcll(__ballot(cnt != 0));
     tot_dot += wave_sum(cnt);
   }
+  tot_mem = uni(tot_mem);
+  tot_dot = uni(tot_dot);
 
-  // ---- deferred counts (lane 0, rare) and output layout
-  uint32_t nd = 0, ndd = 0, ndm = 0;
-  if (has_def) {
-    if (lane == 0) deferred_pass(L, R, n_actors, nd, ndd, ndm, nullptr);
-    nd = __shfl(nd, 0, kWave);
-    ndd = __shfl(ndd, 0, kWave);
-    ndm = __shfl(ndm, 0, kWave);
-  }
-  RecLayout OL;
-  rec_layout(OL, n_actors, tot_mem, tot_dot, nd, ndd, ndm);
-  uint64_t* okey = (uint64_t*)(O + OL.o_key);
-  uint64_t* odctr = (uint64_t*)(O + OL.o_dctr);
-  uint32_t* odact = (uint32_t*)(O + OL.o_dact);
-  uint32_t* omdend = (uint32_t*)(O + OL.o_mdend);
+  // ---- output member block (its offsets depend on the member totals only)
+  const uint32_t o_key = kHdrBytes + 8u * A;
+  const uint32_t o_dctr = o_key + 8u * tot_mem;
+  const uint32_t o_dact = o_dctr + 8u * tot_dot;
+  const uint32_t o_mdend = o_dact + 4u * tot_dot;
+  const uint32_t o_mpad = o_mdend + 4u * tot_mem;
+  const uint32_t o_def = (o_mpad + 7u) & ~7u;
+  uint64_t* okey = (uint64_t*)(O + o_key);
+  uint64_t* odctr = (uint64_t*)(O + o_dctr);
+  uint32_t* odact = (uint32_t*)(O + o_dact);
+  uint32_t* omdend = (uint32_t*)(O + o_mdend);
 
-  // ---- top clock: pointwise max (src/orswot.rs:153, src/vclock.rs:131-137)
-  uint64_t* oclk = (uint64_t*)(O + OL.o_clk);
-  for (uint32_t a = lane; a < n_actors; a += kWave) {
-    uint64_t x = L.clk[a], y = R.clk[a];
-    oclk[a] = x > y ? x : y;
+  // top clock: pointwise max (src/orswot.rs:153 -> src/vclock.rs:131-137)
+  for (uint32_t a = lane; a < A; a += kWave) {
+    const uint64_t x = g64(Ls, L.v.clk, a), y = g64(Rs, R.v.clk, a);
+    ((uint64_t*)(O + kHdrBytes))[a] = x > y ? x : y;
   }
 
-  // ---- pass 2: write kept members and their joined dots
+  // ---- pass 2: write kept members and their joined dot runs
   uint32_t mem_base = 0, dot_base = 0;
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   for (uint32_t base = 0; base < P; base += kWave) {
-    uint32_t p = base + lane;
-    uint32_t cnt = 0, type = kNone, i = 0, j = 0;
-    if (p < P) {
-      if (p < kCache) {
-        uint32_t c = cid[p];
-        type = c >> 30; i = (c >> 15) & 0x7FFFu; j = c & 0x7FFFu;
-        cnt = ccnt[p];
-      } else {
+    const uint32_t p = base + lane;
+    uint32_t q, cnt, x;
+    uint64_t v;
+    if (base == 0) { q = q0; cnt = c0; x = x0; v = v0; }
+    else if (base == kWave) { q = q1; cnt = c1; x = x1; v = v1; }
+    else {
+      uint32_t type = kNone, i = 0, j = 0;
+      cnt = 0; x = 0; v = 0;
+      if (p < P) {
         type = merge_path(L, R, p, i, j);
-        cnt = count_member(type, i, j, L, R, n_actors, has_def);
+        if (type != kNone) cnt = join<0>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0);
       }
+      q = (type << 30) | (i << 15) | j;
     }
-    uint64_t keep = __ballot(cnt > 0);
-    uint32_t incl = wave_incl_scan(cnt, lane);
-    if (cnt > 0) {
-      uint32_t midx = mem_base + (uint32_t)__popcll(keep & lt_mask);
-      uint32_t d = dot_base + incl - cnt;
-      okey[midx] = type == kOther ? R.key[j] : L.key[i];
-      join_member(type, i, j, L, R, n_actors, has_def, [&](uint32_t x, uint64_t v) {
-        odact[d] = x;
-        odctr[d] = v;
-        ++d;
-      });
-      omdend[midx] = d;
+    const uint64_t keep = __ballot(cnt != 0);
+    const uint32_t incl = wave_incl_scan(cnt, lane);
+    if (cnt != 0) {
+      const uint32_t type = q >> 30, i = (q >> 15) & 0x7FFFu, j = q & 0x7FFFu;
+      const uint32_t midx = mem_base + (uint32_t)__popcll(keep & lt_mask);
+      const uint32_t d0 = dot_base + incl - cnt;
+      okey[midx] = (type & kSelf) ? g64(Ls, L.v.key, i) : g64(Rs, R.v.key, j);
+      if (cnt == 1) {
+        odact[d0] = x;
+        odctr[d0] = v;
+      } else {
+        join<1>(L, R, type, i, j, A, has_def, x, v, odact, odctr, d0);
+      }
+      omdend[midx] = d0 + cnt;
     }
     mem_base += (uint32_t)__popcll(keep);
     dot_base += __shfl(incl, kWave - 1, kWave);
   }
 
+  // ---- deferred block + header + padding (lane 0)
   if (lane == 0) {
-    if (OL.o_def != OL.o_mpad) *(uint32_t*)(O + OL.o_mpad) = 0u;  // member-block pad
+    uint32_t nd = 0, ndd = 0, ndm = 0;
+    if (o_def != o_mpad) *(uint32_t*)(O + o_mpad) = 0u;
     if (has_def) {
-      DefOut w;
-      w.fctr = (uint64_t*)(O + OL.o_fctr);
-      w.fkey = (uint64_t*)(O + OL.o_fkey);
-      w.fact = (uint32_t*)(O + OL.o_fact);
-      w.fdend = (uint32_t*)(O + OL.o_fdend);
-      w.fmend = (uint32_t*)(O + OL.o_fmend);
-      deferred_pass(L, R, n_actors, nd, ndd, ndm, &w);
+      deferred_pass(L, R, A, nd, ndd, ndm, nullptr);
+      RecLayout OL;
+      rec_layout(OL, A, tot_mem, tot_dot, nd, ndd, ndm);
+      DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
+               (uint32_t*)(O + OL.o_fdend), (uint32_t*)(O + OL.o_fmend)};
+      deferred_pass(L, R, A, nd, ndd, ndm, &w);
     }
-    for (uint32_t b = OL.o_end; b < OL.size; b += 4) *(uint32_t*)(O + b) = 0u;  // record pad
-    uint4* h = (uint4*)O;
-    h[0] = make_uint4(OL.size, n_actors, tot_mem, tot_dot);
-    h[1] = make_uint4(nd, ndd, ndm, 0u);
+    RecLayout OL;
+    rec_layout(OL, A, tot_mem, tot_dot, nd, ndd, ndm);
+    for (uint32_t b = OL.o_end; b < OL.size; b += 4) *(uint32_t*)(O + b) = 0u;
+    u32x4* h = (u32x4*)O;
+    h[0] = u32x4{OL.size, A, tot_mem, tot_dot};
+    h[1] = u32x4{nd, ndd, ndm, 0u};
   }
 }
 
-__device__ __forceinline__ bool read_layout(const uint8_t* rec, uint64_t avail, uint32_t n_actors,
-                                            RecLayout& L) {
-  const uint4* h = (const uint4*)rec;
-  uint4 a = h[0], b = h[1];
-  rec_layout(L, a.y, a.z, a.w, b.x, b.y, b.z);
-  return a.x == L.size && a.y == n_actors && b.w == 0u && (uint64_t)L.size <= avail;
+// Header sanity for a record of the batch: size matches the counts, the
+// top-clock width is the batch's, flags are clear, it lies in the buffer.
+__device__ __forceinline__ bool header_ok(u32x4 h0, u32x4 h1, uint64_t off, uint64_t bytes, uint32_t A) {
+  const uint64_t sz = record_size64(h0.y, h0.z, h0.w, h1.x, h1.y, h1.z);
+  return (off & 15u) == 0 && off + kHdrBytes <= bytes && sz == h0.x && h0.y == A && h1.w == 0u &&
+         off + sz <= bytes;
 }
 
-// Copy one record (size multiple of 16) into LDS: loads first, then stores.
-__device__ __forceinline__ void stage_record(u32x4* dst, const u32x4* src, uint32_t n16, uint32_t lane) {
-  constexpr uint32_t kPer = kStageBytes / 16 / kWave;  // 16-B chunks per lane
-  u32x4 r[kPer];
+__device__ __forceinline__ void prefetch(u32x4 (&r)[kPer], const uint8_t* src, uint32_t n16, uint32_t lane) {
 #pragma unroll
   for (uint32_t k = 0; k < kPer; ++k) {
-    uint32_t idx = lane + k * kWave;
-    if (idx < n16) r[k] = __builtin_nontemporal_load(src + idx);
+    const uint32_t idx = lane + k * kWave;
+    if (idx < n16) r[k] = __builtin_nontemporal_load((const u32x4*)src + idx);
   }
+}
+
+__device__ __forceinline__ void stage(u32x4* dst, const u32x4 (&r)[kPer], uint32_t n16, uint32_t lane) {
 #pragma unroll
   for (uint32_t k = 0; k < kPer; ++k) {
-    uint32_t idx = lane + k * kWave;
+    const uint32_t idx = lane + k * kWave;
     if (idx < n16) dst[idx] = r[k];
   }
 }
@@ -409,37 +431,100 @@ __device__ __forceinline__ void stage_record(u32x4* dst, const u32x4* src, uint3
 __global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
-    uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj,
-    uint32_t n_actors, int* __restrict__ status) {
-  __shared__ u32x4 stage[kWavesPerBlock][2][kStageBytes / 16];
-  __shared__ uint32_t cid_s[kWavesPerBlock][kCache];
-  __shared__ uint16_t ccnt_s[kWavesPerBlock][kCache];
+    uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
+    int* __restrict__ status) {
+  __shared__ u32x4 stage_s[kWavesPerBlock][2][kStageBytes / 16];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wave = threadIdx.x / kWave;
-  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
-  for (uint64_t obj = (uint64_t)blockIdx.x * kWavesPerBlock + wave; obj < n_obj; obj += stride) {
-    const uint64_t lo = Loff[obj], ro = Roff[obj];
-    const uint64_t oo = lo + ro;
-    if (lane == 0) Ooff[obj] = oo;
-    RecLayout LL, RL;
-    bool ok = lo + kHdrBytes <= Lbytes && ro + kHdrBytes <= Rbytes && ((lo | ro) & 15u) == 0;
-    ok = ok && read_layout(Lb + lo, Lbytes - lo, n_actors, LL) &&
-         read_layout(Rb + ro, Rbytes - ro, n_actors, RL);
-    ok = ok && oo + (uint64_t)LL.size + RL.size <= Obytes;
-    if (!ok) {
-      if (lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
-      continue;
+  u32x4* const sL = stage_s[wave][0];
+  u32x4* const sR = stage_s[wave][1];
+  const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
+  const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
+
+  for (uint64_t chunk = wave_id; chunk < n_chunks; chunk += n_waves) {
+    // ---- chunk state: lane k <-> object chunk*64 + k
+    const uint64_t obj = chunk * kWave + lane;
+    const bool valid = obj < n_obj;
+    uint64_t lo = 0, ro = 0;
+    if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
+    u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
+    bool ok = valid && (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes &&
+              ro + kHdrBytes <= Rbytes;
+    if (ok) {
+      hl0 = ((const u32x4*)(Lb + lo))[0]; hl1 = ((const u32x4*)(Lb + lo))[1];
+      hr0 = ((const u32x4*)(Rb + ro))[0]; hr1 = ((const u32x4*)(Rb + ro))[1];
     }
-    if (LL.size <= kStageBytes && RL.size <= kStageBytes) {
-      stage_record(stage[wave][0], (const u32x4*)(Lb + lo), LL.size / 16, lane);
-      stage_record(stage[wave][1], (const u32x4*)(Rb + ro), RL.size / 16, lane);
+    ok = ok && header_ok(hl0, hl1, lo, Lbytes, A) && header_ok(hr0, hr1, ro, Rbytes, A) &&
+         lo + ro + (uint64_t)hl0.x + hr0.x <= Obytes;
+    const bool big = ok && (hl0.x > kStageBytes || hr0.x > kStageBytes);
+    const bool run = ok && !big;  // joined by this kernel
+    if (valid) Ooff[obj] = (lo + ro) | (big ? kPending : 0ull);
+    if (__ballot(valid && !ok) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
+    const uint64_t runs = __ballot(run);
+    if (runs == 0ull) continue;
+    const uint32_t n16L = run ? hl0.x / 16u : 0u, n16R = run ? hr0.x / 16u : 0u;
+
+    // ---- software pipeline: records of the next runnable object are in
+    // flight while the current one is joined from LDS.
+    uint64_t pend = runs;
+    uint32_t t = (uint32_t)__builtin_ctzll(pend);
+    u32x4 pl[kPer], pr[kPer];
+    prefetch(pl, Lb + lane_of64(lo, t), lane_of(n16L, t), lane);
+    prefetch(pr, Rb + lane_of64(ro, t), lane_of(n16R, t), lane);
+    while (pend) {
+      t = (uint32_t)__builtin_ctzll(pend);
+      pend &= pend - 1;
+      wave_sync();  // previous object's LDS reads are done
+      stage(sL, pl, lane_of(n16L, t), lane);
+      stage(sR, pr, lane_of(n16R, t), lane);
       wave_sync();
-      merge_pair((const uint8_t*)stage[wave][0], LL, (const uint8_t*)stage[wave][1], RL, Ob + oo,
-                 n_actors, cid_s[wave], ccnt_s[wave], lane);
-      wave_sync();
-    } else {
-      merge_pair(Lb + lo, LL, Rb + ro, RL, Ob + oo, n_actors, cid_s[wave], ccnt_s[wave], lane);
-      wave_sync();
+      const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
+      if (pend) {
+        const uint32_t u = (uint32_t)__builtin_ctzll(pend);
+        prefetch(pl, Lb + lane_of64(lo, u), lane_of(n16L, u), lane);
+        prefetch(pr, Rb + lane_of64(ro, u), lane_of(n16R, u), lane);
+      }
+      merge_object((const uint8_t*)sL, (const uint8_t*)sR, Ob + oo, A, lane);
+    }
+  }
+}
+
+// Records larger than the LDS stage: one wave per block walks 64-object
+// chunks of the output offsets and joins every flagged object, staging records
+// of up to kBigStage bytes through LDS (plain 16-B copies) and joining larger
+// ones straight from HBM. Clears the flag it consumes.
+constexpr uint32_t kBigStage = 16384;
+
+__global__ __launch_bounds__(kWave) void orswot_merge_big_kernel(
+    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, const uint8_t* __restrict__ Rb,
+    const uint64_t* __restrict__ Roff, uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t n_obj,
+    uint32_t A) {
+  __shared__ u32x4 big_s[2][kBigStage / 16];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
+  for (uint64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
+    const uint64_t obj = chunk * kWave + lane;
+    const uint64_t oo = obj < n_obj ? Ooff[obj] : 0ull;
+    uint64_t pend = __ballot((oo & kPending) != 0ull);
+    while (pend) {
+      const uint32_t t = (uint32_t)__builtin_ctzll(pend);
+      pend &= pend - 1;
+      const uint64_t o = chunk * kWave + t;
+      const uint8_t* lr = Lb + Loff[o];
+      const uint8_t* rr = Rb + Roff[o];
+      uint8_t* out = Ob + (lane_of64(oo, t) & ~kPending);
+      const uint32_t szl = uni(*(const uint32_t*)lr), szr = uni(*(const uint32_t*)rr);
+      if (szl <= kBigStage && szr <= kBigStage) {
+        wave_sync();
+        for (uint32_t k = lane; k < szl / 16; k += kWave) big_s[0][k] = ((const u32x4*)lr)[k];
+        for (uint32_t k = lane; k < szr / 16; k += kWave) big_s[1][k] = ((const u32x4*)rr)[k];
+        wave_sync();
+        merge_object((const uint8_t*)big_s[0], (const uint8_t*)big_s[1], out, A, lane);
+      } else {
+        merge_object(lr, rr, out, A, lane);
+      }
+      if (lane == 0) Ooff[o] = lane_of64(oo, t) & ~kPending;
     }
   }
 }
@@ -452,14 +537,17 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
                         hipStream_t stream, int blocks_per_cu) {
   if (n_obj == 0) return CRDT_OK;
   int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) {
+  if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  }
-  uint64_t want = (n_obj + kWavesPerBlock - 1) / kWavesPerBlock;
-  uint64_t cap = (uint64_t)cus * (blocks_per_cu > 0 ? blocks_per_cu : 8);
-  uint32_t blocks = (uint32_t)(want < cap ? want : cap);
-  hipLaunchKernelGGL(orswot_merge_kernel, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, stream,
-                     Lb, Loff, Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors, status);
+  const uint64_t chunks = (n_obj + kWave - 1) / kWave;
+  const uint64_t want = (chunks + kWavesPerBlock - 1) / kWavesPerBlock;
+  const uint64_t cap = (uint64_t)cus * (blocks_per_cu > 0 ? blocks_per_cu : 8);
+  const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
+  hipLaunchKernelGGL(orswot_merge_kernel, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, stream, Lb, Loff,
+                     Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors, status);
+  const uint32_t big_blocks = (uint32_t)(chunks < (uint64_t)cus * 4 ? chunks : (uint64_t)cus * 4);
+  hipLaunchKernelGGL(orswot_merge_big_kernel, dim3(big_blocks), dim3(kWave), 0, stream, Lb,
+                     Loff, Rb, Roff, Ob, Ooff, n_obj, n_actors);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 

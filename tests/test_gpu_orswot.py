@@ -126,14 +126,16 @@ def test_config3_reverse_orientation(gpu, oracle):
     dict(pct_deferred_obj=100, pct_future_rm=40),                    # deferred-heavy
     dict(pct_shared_actor=100),                                     # same-actor adds
     dict(n_actors=3, member_universe=8, ancestor_adds=4),          # tiny
-    dict(n_actors=64, member_universe=200, ancestor_adds=150, max_div_ops=40),  # > LDS stage -> global path
+    dict(n_actors=64, member_universe=200, ancestor_adds=150, max_div_ops=40),  # > 2 KB stage -> big kernel (LDS)
+    dict(n_actors=32, member_universe=2000, ancestor_adds=1500, max_div_ops=60),  # > 16 KB -> big kernel (HBM)
     dict(n_actors=1, member_universe=16, ancestor_adds=8),
     dict(ancestor_adds=0, min_div_ops=0, max_div_ops=3),           # empty / near-empty objects
-], ids=["deferred_heavy", "shared_actor", "tiny", "large_global_path", "one_actor", "empty"])
+], ids=["deferred_heavy", "shared_actor", "tiny", "big_lds", "big_hbm", "one_actor", "empty"])
 def test_generated_variants(params, gpu, oracle):
     import crdts_hip
 
-    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(5_000, threads=16, seed=99, params=params)
+    n = 300 if params.get("member_universe", 0) >= 2000 else 5_000
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(n, threads=16, seed=99, params=params)
     A = params.get("n_actors", 16)
     out = _gpu_merge(gpu, lb, lo, rb, ro, A)
     ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, A, threads=16)
