@@ -38,9 +38,6 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
-constexpr uint32_t kStageBytes = 2048;                     // LDS stage per input record per wave
-constexpr uint32_t kPer = kStageBytes / 16 / kWave;        // 16-B pieces per lane per record
-constexpr uint64_t kPending = 1ull << 63;                   // Ooff flag: record left for the big kernel
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -412,6 +409,197 @@ __device__ __forceinline__ bool header_ok(u32x4 h0, u32x4 h1, uint64_t off, uint
          off + sz <= bytes;
 }
 
+// ======================================================================
+// Fast path: objects without deferred removes whose records fit the LDS
+// stage and whose merge has at most 128 union positions (two 64-wide
+// chunks) — ~95 % of config-3 objects. Same rules as merge_object, written
+// for the issue rate: every LDS load is unconditional (indices clamped or
+// garbage-then-selected: LDS reads never fault), selects instead of branches,
+// DPP wave scans, and all per-position state stays in registers between the
+// count and the write pass.
+// ======================================================================
+constexpr uint32_t kFastStage = 2048;                 // LDS stage per input record per wave
+constexpr uint32_t kPer = kFastStage / 16 / kWave;    // 16-B pieces per lane per record
+constexpr uint64_t kPending = 1ull << 63;             // Ooff flag: object left for the general kernel
+
+// Wave-wide inclusive prefix sum: DPP row shifts then row broadcasts (gfx9).
+__device__ __forceinline__ uint32_t scan_incl(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+
+__device__ __forceinline__ uint64_t ld64(const uint8_t* b, uint32_t off) { return *(const uint64_t*)(b + off); }
+__device__ __forceinline__ uint32_t ld32(const uint8_t* b, uint32_t off) { return *(const uint32_t*)(b + off); }
+
+// One staged record: LDS base and (wave-uniform) section offsets.
+struct FSide {
+  const uint8_t* b;
+  uint32_t n, key, ctr, act, end;
+};
+
+__device__ __forceinline__ FSide fside(const uint8_t* b, uint32_t A, uint32_t n_mem, uint32_t n_dot) {
+  FSide s;
+  s.b = b;
+  s.n = n_mem;
+  s.key = kHdrBytes + 8u * A;
+  s.ctr = s.key + 8u * n_mem;
+  s.act = s.ctr + 8u * n_dot;
+  s.end = s.act + 4u * n_dot;
+  return s;
+}
+
+// Merge path at union position p (p <= nL + nR), branch-free.
+__device__ __forceinline__ uint32_t fpath(const FSide& L, const FSide& R, uint32_t p, uint32_t steps, uint32_t& i,
+                                          uint32_t& j) {
+  uint32_t lo = p > R.n ? p - R.n : 0u;
+  uint32_t len = (p < L.n ? p : L.n) - lo;
+  for (uint32_t s = 0; s <= steps; ++s) {
+    const uint32_t half = len >> 1, mid = lo + half;
+    const uint64_t kl = ld64(L.b, L.key + 8u * mid), kr = ld64(R.b, R.key + 8u * (p - 1u - mid));
+    const bool go = len != 0u && kl <= kr;
+    lo = go ? mid + 1u : lo;
+    len = len == 0u ? 0u : (go ? len - half - 1u : half);
+  }
+  i = lo;
+  j = p - lo;
+  const uint64_t kl = ld64(L.b, L.key + 8u * i), kr = ld64(R.b, R.key + 8u * j);
+  const uint64_t kp = ld64(L.b, L.key + 8u * i - 8u);
+  const bool hl = i < L.n, hr = j < R.n;
+  if (hl && (!hr || kl <= kr)) return (hr && kl == kr) ? kBoth : kSelf;
+  return (i > 0u && hr && kp == kr) ? kNone : kOther;
+}
+
+// Joined dot run of one member (rules of join<> above / src/orswot.rs:94-138).
+// COUNT: returns the run length and captures the first dot in (x0, v0);
+// WRITE: stores the run at oact/octr[d0..] (the entry is known to survive).
+template <bool WRITE>
+__device__ __forceinline__ uint32_t fjoin(const FSide& L, const FSide& R, uint32_t A, uint32_t type, uint32_t i,
+                                          uint32_t j, uint32_t& x0, uint64_t& v0, uint32_t* oact, uint64_t* octr,
+                                          uint32_t d0) {
+  const bool hs = (type & kSelf) != 0u, ho = (type & kOther) != 0u, self_only = type == kSelf;
+  const uint32_t ab = ld32(L.b, L.end + 4u * i - 4u), ae_ = ld32(L.b, L.end + 4u * i);
+  const uint32_t bb = ld32(R.b, R.end + 4u * j - 4u), be_ = ld32(R.b, R.end + 4u * j);
+  uint32_t a = hs && i ? ab : 0u, ae = hs ? ae_ : 0u;
+  uint32_t b = ho && j ? bb : 0u, be = ho ? be_ : 0u;
+  bool any = false;
+  uint32_t c = 0;
+  while (a < ae || b < be) {
+    const uint32_t xa_ = ld32(L.b, L.act + 4u * a), xb_ = ld32(R.b, R.act + 4u * b);
+    const uint64_t va = ld64(L.b, L.ctr + 8u * a), vb = ld64(R.b, R.ctr + 8u * b);
+    const uint32_t xa = a < ae ? xa_ : 0xFFFFFFFFu, xb = b < be ? xb_ : 0xFFFFFFFFu;
+    const bool ta = xa <= xb, tb = xb <= xa;
+    const uint32_t x = ta ? xa : xb;
+    const bool in = x < A;
+    const uint32_t xo = kHdrBytes + 8u * (in ? x : 0u);
+    const uint64_t rc_ = ld64(R.b, xo), lc_ = ld64(L.b, xo);
+    const uint64_t rc = in ? rc_ : 0ull, lc = in ? lc_ : 0ull;
+    any = any || (self_only && ta && va > rc);
+    const uint64_t lp = (ta && (self_only || va > rc)) ? va : 0ull;
+    const uint64_t rp = (tb && vb > lc) ? vb : 0ull;
+    const uint64_t v = (ta && tb && va == vb) ? va : (lp > rp ? lp : rp);
+    a += ta ? 1u : 0u;
+    b += tb ? 1u : 0u;
+    const bool keep = v != 0ull;
+    if (WRITE) {
+      if (keep) {
+        oact[d0 + c] = x;
+        octr[d0 + c] = v;
+      }
+    } else {
+      const bool first = keep && c == 0u;
+      x0 = first ? x : x0;
+      v0 = first ? v : v0;
+    }
+    c += keep ? 1u : 0u;
+  }
+  if (!WRITE && self_only && !any) c = 0u;  // self-only entry dropped as a whole (:98-100)
+  return c;
+}
+
+__device__ __forceinline__ void fwrite_member(const FSide& L, const FSide& R, uint32_t A, uint32_t q, uint32_t cnt,
+                                              uint32_t x, uint64_t v, uint32_t midx, uint32_t d0, uint64_t* okey,
+                                              uint32_t* odact, uint64_t* odctr, uint32_t* omdend) {
+  const uint32_t type = q >> 30, i = (q >> 15) & 0x7FFFu, j = q & 0x7FFFu;
+  const uint64_t kl = ld64(L.b, L.key + 8u * i), kr = ld64(R.b, R.key + 8u * j);
+  okey[midx] = (type & kSelf) ? kl : kr;
+  if (cnt == 1u) {
+    odact[d0] = x;
+    odctr[d0] = v;
+  } else {
+    fjoin<true>(L, R, A, type, i, j, x, v, odact, odctr, d0);
+  }
+  omdend[midx] = d0 + cnt;
+}
+
+__device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* O, uint32_t A,
+                                            uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane) {
+  const FSide L = fside(Ls, A, nL, dL), R = fside(Rs, A, nR, dR);
+  const uint32_t P = nL + nR;
+  const uint32_t steps = 32u - __builtin_clz((nL < nR ? nL : nR) | 1u);
+  // chunk 0: positions 0..63
+  uint32_t i = 0, j = 0, x0 = 0, c0 = 0, q0 = 0;
+  uint64_t v0 = 0;
+  {
+    const uint32_t p = lane < P ? lane : P;
+    uint32_t type = fpath(L, R, p, steps, i, j);
+    type = lane < P ? type : kNone;
+    c0 = fjoin<false>(L, R, A, type, i, j, x0, v0, nullptr, nullptr, 0u);
+    q0 = (type << 30) | (i << 15) | j;
+  }
+  // chunk 1: positions 64..127 (P <= 128 on this path)
+  uint32_t x1 = 0, c1 = 0, q1 = 0;
+  uint64_t v1 = 0;
+  if (P > (uint32_t)kWave) {
+    const uint32_t p = lane + kWave < P ? lane + kWave : P;
+    uint32_t type = fpath(L, R, p, steps, i, j);
+    type = lane + kWave < P ? type : kNone;
+    c1 = fjoin<false>(L, R, A, type, i, j, x1, v1, nullptr, nullptr, 0u);
+    q1 = (type << 30) | (i << 15) | j;
+  }
+  const uint32_t inc0 = scan_incl(c0), inc1 = scan_incl(c1);
+  const uint64_t k0 = __ballot(c0 != 0u), k1 = __ballot(c1 != 0u);
+  const uint32_t tot0 = lane_of(inc0, kWave - 1), tot1 = lane_of(inc1, kWave - 1);
+  const uint32_t m0 = (uint32_t)__popcll(k0);
+  const uint32_t tot_mem = m0 + (uint32_t)__popcll(k1), tot_dot = tot0 + tot1;
+
+  // output member block (no deferred block on this path)
+  const uint32_t o_key = kHdrBytes + 8u * A;
+  const uint32_t o_dctr = o_key + 8u * tot_mem;
+  const uint32_t o_dact = o_dctr + 8u * tot_dot;
+  const uint32_t o_mdend = o_dact + 4u * tot_dot;
+  const uint32_t o_mpad = o_mdend + 4u * tot_mem;
+  const uint32_t o_def = (o_mpad + 7u) & ~7u;
+  const uint32_t size = (o_def + 15u) & ~15u;
+  uint64_t* okey = (uint64_t*)(O + o_key);
+  uint64_t* odctr = (uint64_t*)(O + o_dctr);
+  uint32_t* odact = (uint32_t*)(O + o_dact);
+  uint32_t* omdend = (uint32_t*)(O + o_mdend);
+
+  // top clock: pointwise max (src/orswot.rs:153 -> src/vclock.rs:131-137)
+  for (uint32_t a = lane; a < A; a += kWave) {
+    const uint64_t x = ld64(Ls, kHdrBytes + 8u * a), y = ld64(Rs, kHdrBytes + 8u * a);
+    ((uint64_t*)(O + kHdrBytes))[a] = x > y ? x : y;
+  }
+  const uint64_t lt = (1ull << lane) - 1ull;
+  if (c0 != 0u)
+    fwrite_member(L, R, A, q0, c0, x0, v0, (uint32_t)__popcll(k0 & lt), inc0 - c0, okey, odact, odctr, omdend);
+  if (c1 != 0u)
+    fwrite_member(L, R, A, q1, c1, x1, v1, m0 + (uint32_t)__popcll(k1 & lt), tot0 + inc1 - c1, okey, odact, odctr,
+                  omdend);
+  if (lane == 0u) {
+    if (o_def != o_mpad) *(uint32_t*)(O + o_mpad) = 0u;
+    if (size != o_def) *(uint64_t*)(O + o_def) = 0ull;
+    u32x4* h = (u32x4*)O;
+    h[0] = u32x4{size, A, tot_mem, tot_dot};
+    h[1] = u32x4{0u, 0u, 0u, 0u};
+  }
+}
+
 __device__ __forceinline__ void prefetch(u32x4 (&r)[kPer], const uint8_t* src, uint32_t n16, uint32_t lane) {
 #pragma unroll
   for (uint32_t k = 0; k < kPer; ++k) {
@@ -433,7 +621,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_kernel(
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
     uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
     int* __restrict__ status) {
-  __shared__ u32x4 stage_s[kWavesPerBlock][2][kStageBytes / 16];
+  __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wave = threadIdx.x / kWave;
   u32x4* const sL = stage_s[wave][0];
@@ -457,53 +645,64 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_kernel(
     }
     ok = ok && header_ok(hl0, hl1, lo, Lbytes, A) && header_ok(hr0, hr1, ro, Rbytes, A) &&
          lo + ro + (uint64_t)hl0.x + hr0.x <= Obytes;
-    const bool big = ok && (hl0.x > kStageBytes || hr0.x > kStageBytes);
-    const bool run = ok && !big;  // joined by this kernel
-    if (valid) Ooff[obj] = (lo + ro) | (big ? kPending : 0ull);
+    const bool fast = ok && hl0.x <= kFastStage && hr0.x <= kFastStage && hl1.x == 0u && hr1.x == 0u &&
+                      hl0.z + hr0.z <= 2u * kWave;
+    if (valid) Ooff[obj] = (lo + ro) | ((ok && !fast) ? kPending : 0ull);
     if (__ballot(valid && !ok) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
-    const uint64_t runs = __ballot(run);
+    const uint64_t runs = __ballot(fast);
     if (runs == 0ull) continue;
-    const uint32_t n16L = run ? hl0.x / 16u : 0u, n16R = run ? hr0.x / 16u : 0u;
+    const uint32_t n16 = fast ? (hl0.x / 16u) | ((hr0.x / 16u) << 16) : 0u;
+    const uint32_t nm = hl0.z | (hr0.z << 16), nd = hl0.w | (hr0.w << 16);
 
-    // ---- software pipeline: records of the next runnable object are in
-    // flight while the current one is joined from LDS.
+    // ---- software pipeline: the next fast object's records are in flight
+    // while the current one is joined from LDS.
     uint64_t pend = runs;
     uint32_t t = (uint32_t)__builtin_ctzll(pend);
     u32x4 pl[kPer], pr[kPer];
-    prefetch(pl, Lb + lane_of64(lo, t), lane_of(n16L, t), lane);
-    prefetch(pr, Rb + lane_of64(ro, t), lane_of(n16R, t), lane);
+    uint32_t nn = lane_of(n16, t);
+    prefetch(pl, Lb + lane_of64(lo, t), nn & 0xFFFFu, lane);
+    prefetch(pr, Rb + lane_of64(ro, t), nn >> 16, lane);
     while (pend) {
       t = (uint32_t)__builtin_ctzll(pend);
       pend &= pend - 1;
+      nn = lane_of(n16, t);
       wave_sync();  // previous object's LDS reads are done
-      stage(sL, pl, lane_of(n16L, t), lane);
-      stage(sR, pr, lane_of(n16R, t), lane);
+      stage(sL, pl, nn & 0xFFFFu, lane);
+      stage(sR, pr, nn >> 16, lane);
       wave_sync();
       const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
+      const uint32_t m = lane_of(nm, t), d = lane_of(nd, t);
       if (pend) {
         const uint32_t u = (uint32_t)__builtin_ctzll(pend);
-        prefetch(pl, Lb + lane_of64(lo, u), lane_of(n16L, u), lane);
-        prefetch(pr, Rb + lane_of64(ro, u), lane_of(n16R, u), lane);
+        const uint32_t nu = lane_of(n16, u);
+        prefetch(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
+        prefetch(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
       }
-      merge_object((const uint8_t*)sL, (const uint8_t*)sR, Ob + oo, A, lane);
+      fast_object((const uint8_t*)sL, (const uint8_t*)sR, Ob + oo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16,
+                  d >> 16, lane);
     }
   }
 }
 
-// Records larger than the LDS stage: one wave per block walks 64-object
-// chunks of the output offsets and joins every flagged object, staging records
-// of up to kBigStage bytes through LDS (plain 16-B copies) and joining larger
-// ones straight from HBM. Clears the flag it consumes.
-constexpr uint32_t kBigStage = 16384;
+// ======================================================================
+// General path: objects the fast kernel flagged (deferred removes, records
+// larger than its stage, > 128 union positions). One wave per 64-object chunk
+// (a coalesced scan of the chunk's output offsets); every flagged object is
+// staged through LDS when both records fit kGenStage, else joined straight
+// from HBM. Clears the flag it consumes.
+// ======================================================================
+constexpr uint32_t kGenStage = 4096;
 
-__global__ __launch_bounds__(kWave) void orswot_merge_big_kernel(
+__global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_general_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, const uint8_t* __restrict__ Rb,
     const uint64_t* __restrict__ Roff, uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t n_obj,
     uint32_t A) {
-  __shared__ u32x4 big_s[2][kBigStage / 16];
-  const uint32_t lane = threadIdx.x;
+  __shared__ u32x4 gen_s[kWavesPerBlock][2][kGenStage / 16];
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t wave = threadIdx.x / kWave;
   const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
-  for (uint64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
+  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t chunk = (uint64_t)blockIdx.x * kWavesPerBlock + wave; chunk < n_chunks; chunk += n_waves) {
     const uint64_t obj = chunk * kWave + lane;
     const uint64_t oo = obj < n_obj ? Ooff[obj] : 0ull;
     uint64_t pend = __ballot((oo & kPending) != 0ull);
@@ -515,12 +714,12 @@ __global__ __launch_bounds__(kWave) void orswot_merge_big_kernel(
       const uint8_t* rr = Rb + Roff[o];
       uint8_t* out = Ob + (lane_of64(oo, t) & ~kPending);
       const uint32_t szl = uni(*(const uint32_t*)lr), szr = uni(*(const uint32_t*)rr);
-      if (szl <= kBigStage && szr <= kBigStage) {
+      if (szl <= kGenStage && szr <= kGenStage) {
         wave_sync();
-        for (uint32_t k = lane; k < szl / 16; k += kWave) big_s[0][k] = ((const u32x4*)lr)[k];
-        for (uint32_t k = lane; k < szr / 16; k += kWave) big_s[1][k] = ((const u32x4*)rr)[k];
+        for (uint32_t k = lane; k < szl / 16; k += kWave) gen_s[wave][0][k] = ((const u32x4*)lr)[k];
+        for (uint32_t k = lane; k < szr / 16; k += kWave) gen_s[wave][1][k] = ((const u32x4*)rr)[k];
         wave_sync();
-        merge_object((const uint8_t*)big_s[0], (const uint8_t*)big_s[1], out, A, lane);
+        merge_object((const uint8_t*)gen_s[wave][0], (const uint8_t*)gen_s[wave][1], out, A, lane);
       } else {
         merge_object(lr, rr, out, A, lane);
       }
@@ -545,9 +744,10 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
   hipLaunchKernelGGL(orswot_merge_kernel, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, stream, Lb, Loff,
                      Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors, status);
-  const uint32_t big_blocks = (uint32_t)(chunks < (uint64_t)cus * 4 ? chunks : (uint64_t)cus * 4);
-  hipLaunchKernelGGL(orswot_merge_big_kernel, dim3(big_blocks), dim3(kWave), 0, stream, Lb,
-                     Loff, Rb, Roff, Ob, Ooff, n_obj, n_actors);
+  const uint64_t gen_blocks = (chunks + kWavesPerBlock - 1) / kWavesPerBlock;
+  hipLaunchKernelGGL(orswot_merge_general_kernel,
+                     dim3((uint32_t)(gen_blocks < 0x7FFFFFFFull ? gen_blocks : 0x7FFFFFFFull)),
+                     dim3(kWave * kWavesPerBlock), 0, stream, Lb, Loff, Rb, Roff, Ob, Ooff, n_obj, n_actors);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 
