@@ -410,9 +410,9 @@ __device__ __forceinline__ bool header_ok(u32x4 h0, u32x4 h1, uint64_t off, uint
 }
 
 // ======================================================================
-// Fast path: objects without deferred removes whose records fit the LDS
-// stage and whose merge has at most 128 union positions (two 64-wide
-// chunks) — ~95 % of config-3 objects. Same rules as merge_object, written
+// Fast path: objects whose records fit the LDS stage, with at most 32
+// deferred clocks per side, and whose merge has at most 128 union positions
+// (two 64-wide chunks) — all of config 3. Same rules as merge_object, written
 // for the issue rate: every LDS load is unconditional (indices clamped or
 // garbage-then-selected: LDS reads never fault), selects instead of branches,
 // DPP wave scans, and all per-position state stays in registers between the
@@ -474,13 +474,32 @@ __device__ __forceinline__ uint32_t fpath(const FSide& L, const FSide& R, uint32
   return (i > 0u && hr && kp == kr) ? kNone : kOther;
 }
 
+// Deferred removes on the fast path (objects with any, ~10 % in config 3):
+// bit k (k < 32) / 32+k of the mask says deferred clock k of self / other
+// lists this member, so each output dot is checked only against those
+// clocks (apply_remove via apply_deferred, src/orswot.rs:195-211, 235-243).
+__device__ __forceinline__ uint64_t dmask_of(const Side& DL, const Side& DR, uint64_t m) {
+  uint64_t mask = 0;
+  for (uint32_t k = 0; k < DL.v.n_def; ++k) mask |= def_has_member(DL, k, m) ? (1ull << k) : 0ull;
+  for (uint32_t k = 0; k < DR.v.n_def; ++k) mask |= def_has_member(DR, k, m) ? (1ull << (32 + k)) : 0ull;
+  return mask;
+}
+
+__device__ __forceinline__ bool dkilled(const Side& DL, const Side& DR, uint64_t mask, uint32_t x, uint64_t v) {
+  for (; mask; mask &= mask - 1) {
+    const uint32_t k = (uint32_t)__builtin_ctzll(mask);
+    if ((k < 32 ? def_get(DL, k, x) : def_get(DR, k - 32, x)) >= v) return true;
+  }
+  return false;
+}
+
 // Joined dot run of one member (rules of join<> above / src/orswot.rs:94-138).
 // COUNT: returns the run length and captures the first dot in (x0, v0);
 // WRITE: stores the run at oact/octr[d0..] (the entry is known to survive).
-template <bool WRITE>
+template <bool WRITE, bool HD>
 __device__ __forceinline__ uint32_t fjoin(const FSide& L, const FSide& R, uint32_t A, uint32_t type, uint32_t i,
                                           uint32_t j, uint32_t& x0, uint64_t& v0, uint32_t* oact, uint64_t* octr,
-                                          uint32_t d0) {
+                                          uint32_t d0, uint64_t dmask, const Side& DL, const Side& DR) {
   const bool hs = (type & kSelf) != 0u, ho = (type & kOther) != 0u, self_only = type == kSelf;
   const uint32_t ab = ld32(L.b, L.end + 4u * i - 4u), ae_ = ld32(L.b, L.end + 4u * i);
   const uint32_t bb = ld32(R.b, R.end + 4u * j - 4u), be_ = ld32(R.b, R.end + 4u * j);
@@ -501,9 +520,10 @@ __device__ __forceinline__ uint32_t fjoin(const FSide& L, const FSide& R, uint32
     any = any || (self_only && ta && va > rc);
     const uint64_t lp = (ta && (self_only || va > rc)) ? va : 0ull;
     const uint64_t rp = (tb && vb > lc) ? vb : 0ull;
-    const uint64_t v = (ta && tb && va == vb) ? va : (lp > rp ? lp : rp);
+    uint64_t v = (ta && tb && va == vb) ? va : (lp > rp ? lp : rp);
     a += ta ? 1u : 0u;
     b += tb ? 1u : 0u;
+    if (HD && v != 0ull && dmask != 0ull && dkilled(DL, DR, dmask, x, v)) v = 0ull;
     const bool keep = v != 0ull;
     if (WRITE) {
       if (keep) {
@@ -521,9 +541,11 @@ __device__ __forceinline__ uint32_t fjoin(const FSide& L, const FSide& R, uint32
   return c;
 }
 
+template <bool HD>
 __device__ __forceinline__ void fwrite_member(const FSide& L, const FSide& R, uint32_t A, uint32_t q, uint32_t cnt,
                                               uint32_t x, uint64_t v, uint32_t midx, uint32_t d0, uint64_t* okey,
-                                              uint32_t* odact, uint64_t* odctr, uint32_t* omdend) {
+                                              uint32_t* odact, uint64_t* odctr, uint32_t* omdend, uint64_t dmask,
+                                              const Side& DL, const Side& DR) {
   const uint32_t type = q >> 30, i = (q >> 15) & 0x7FFFu, j = q & 0x7FFFu;
   const uint64_t kl = ld64(L.b, L.key + 8u * i), kr = ld64(R.b, R.key + 8u * j);
   okey[midx] = (type & kSelf) ? kl : kr;
@@ -531,34 +553,44 @@ __device__ __forceinline__ void fwrite_member(const FSide& L, const FSide& R, ui
     odact[d0] = x;
     odctr[d0] = v;
   } else {
-    fjoin<true>(L, R, A, type, i, j, x, v, odact, odctr, d0);
+    fjoin<true, HD>(L, R, A, type, i, j, x, v, odact, odctr, d0, dmask, DL, DR);
   }
   omdend[midx] = d0 + cnt;
 }
 
+// Record-wide section offsets of a staged record (general accessor form),
+// used for its deferred block.
+__device__ __forceinline__ Side side_of(const uint8_t* b) { return Side{b, make_rv(layout_at(b))}; }
+
+// HD: the object has deferred removes (either side; <= 32 clocks per side).
+template <bool HD>
 __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* O, uint32_t A,
                                             uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane) {
   const FSide L = fside(Ls, A, nL, dL), R = fside(Rs, A, nR, dR);
+  Side DL{Ls, RV{}}, DR{Rs, RV{}};
+  if (HD) { DL = side_of(Ls); DR = side_of(Rs); }
   const uint32_t P = nL + nR;
   const uint32_t steps = 32u - __builtin_clz((nL < nR ? nL : nR) | 1u);
   // chunk 0: positions 0..63
   uint32_t i = 0, j = 0, x0 = 0, c0 = 0, q0 = 0;
-  uint64_t v0 = 0;
+  uint64_t v0 = 0, m0k = 0;
   {
     const uint32_t p = lane < P ? lane : P;
     uint32_t type = fpath(L, R, p, steps, i, j);
     type = lane < P ? type : kNone;
-    c0 = fjoin<false>(L, R, A, type, i, j, x0, v0, nullptr, nullptr, 0u);
+    if (HD && type != kNone) m0k = dmask_of(DL, DR, (type & kSelf) ? ld64(Ls, L.key + 8u * i) : ld64(Rs, R.key + 8u * j));
+    c0 = fjoin<false, HD>(L, R, A, type, i, j, x0, v0, nullptr, nullptr, 0u, m0k, DL, DR);
     q0 = (type << 30) | (i << 15) | j;
   }
   // chunk 1: positions 64..127 (P <= 128 on this path)
   uint32_t x1 = 0, c1 = 0, q1 = 0;
-  uint64_t v1 = 0;
+  uint64_t v1 = 0, m1k = 0;
   if (P > (uint32_t)kWave) {
     const uint32_t p = lane + kWave < P ? lane + kWave : P;
     uint32_t type = fpath(L, R, p, steps, i, j);
     type = lane + kWave < P ? type : kNone;
-    c1 = fjoin<false>(L, R, A, type, i, j, x1, v1, nullptr, nullptr, 0u);
+    if (HD && type != kNone) m1k = dmask_of(DL, DR, (type & kSelf) ? ld64(Ls, L.key + 8u * i) : ld64(Rs, R.key + 8u * j));
+    c1 = fjoin<false, HD>(L, R, A, type, i, j, x1, v1, nullptr, nullptr, 0u, m1k, DL, DR);
     q1 = (type << 30) | (i << 15) | j;
   }
   const uint32_t inc0 = scan_incl(c0), inc1 = scan_incl(c1);
@@ -567,14 +599,13 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
   const uint32_t m0 = (uint32_t)__popcll(k0);
   const uint32_t tot_mem = m0 + (uint32_t)__popcll(k1), tot_dot = tot0 + tot1;
 
-  // output member block (no deferred block on this path)
+  // output member block; the deferred block (if any) follows it
   const uint32_t o_key = kHdrBytes + 8u * A;
   const uint32_t o_dctr = o_key + 8u * tot_mem;
   const uint32_t o_dact = o_dctr + 8u * tot_dot;
   const uint32_t o_mdend = o_dact + 4u * tot_dot;
   const uint32_t o_mpad = o_mdend + 4u * tot_mem;
   const uint32_t o_def = (o_mpad + 7u) & ~7u;
-  const uint32_t size = (o_def + 15u) & ~15u;
   uint64_t* okey = (uint64_t*)(O + o_key);
   uint64_t* odctr = (uint64_t*)(O + o_dctr);
   uint32_t* odact = (uint32_t*)(O + o_dact);
@@ -587,16 +618,29 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
   }
   const uint64_t lt = (1ull << lane) - 1ull;
   if (c0 != 0u)
-    fwrite_member(L, R, A, q0, c0, x0, v0, (uint32_t)__popcll(k0 & lt), inc0 - c0, okey, odact, odctr, omdend);
+    fwrite_member<HD>(L, R, A, q0, c0, x0, v0, (uint32_t)__popcll(k0 & lt), inc0 - c0, okey, odact, odctr, omdend,
+                      m0k, DL, DR);
   if (c1 != 0u)
-    fwrite_member(L, R, A, q1, c1, x1, v1, m0 + (uint32_t)__popcll(k1 & lt), tot0 + inc1 - c1, okey, odact, odctr,
-                  omdend);
+    fwrite_member<HD>(L, R, A, q1, c1, x1, v1, m0 + (uint32_t)__popcll(k1 & lt), tot0 + inc1 - c1, okey, odact,
+                      odctr, omdend, m1k, DL, DR);
   if (lane == 0u) {
+    uint32_t nd = 0, ndd = 0, ndm = 0, end = o_def;
     if (o_def != o_mpad) *(uint32_t*)(O + o_mpad) = 0u;
-    if (size != o_def) *(uint64_t*)(O + o_def) = 0ull;
+    if (HD) {
+      // deferred union keyed by clock (:141-148), kept iff !(D <= clock) (:197)
+      deferred_pass(DL, DR, A, nd, ndd, ndm, nullptr);
+      RecLayout OL;
+      rec_layout(OL, A, tot_mem, tot_dot, nd, ndd, ndm);
+      DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
+               (uint32_t*)(O + OL.o_fdend), (uint32_t*)(O + OL.o_fmend)};
+      deferred_pass(DL, DR, A, nd, ndd, ndm, &w);
+      end = OL.o_end;
+    }
+    const uint32_t size = (end + 15u) & ~15u;
+    for (uint32_t b = end; b < size; b += 4) *(uint32_t*)(O + b) = 0u;
     u32x4* h = (u32x4*)O;
     h[0] = u32x4{size, A, tot_mem, tot_dot};
-    h[1] = u32x4{0u, 0u, 0u, 0u};
+    h[1] = u32x4{nd, ndd, ndm, 0u};
   }
 }
 
@@ -645,7 +689,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_kernel(
     }
     ok = ok && header_ok(hl0, hl1, lo, Lbytes, A) && header_ok(hr0, hr1, ro, Rbytes, A) &&
          lo + ro + (uint64_t)hl0.x + hr0.x <= Obytes;
-    const bool fast = ok && hl0.x <= kFastStage && hr0.x <= kFastStage && hl1.x == 0u && hr1.x == 0u &&
+    const bool fast = ok && hl0.x <= kFastStage && hr0.x <= kFastStage && hl1.x <= 32u && hr1.x <= 32u &&
                       hl0.z + hr0.z <= 2u * kWave;
     if (valid) Ooff[obj] = (lo + ro) | ((ok && !fast) ? kPending : 0ull);
     if (__ballot(valid && !ok) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
@@ -653,6 +697,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_kernel(
     if (runs == 0ull) continue;
     const uint32_t n16 = fast ? (hl0.x / 16u) | ((hr0.x / 16u) << 16) : 0u;
     const uint32_t nm = hl0.z | (hr0.z << 16), nd = hl0.w | (hr0.w << 16);
+    const uint64_t defs = __ballot(fast && (hl1.x | hr1.x) != 0u);  // objects with deferred removes
 
     // ---- software pipeline: the next fast object's records are in flight
     // while the current one is joined from LDS.
@@ -678,15 +723,19 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_kernel(
         prefetch(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
         prefetch(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
       }
-      fast_object((const uint8_t*)sL, (const uint8_t*)sR, Ob + oo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16,
-                  d >> 16, lane);
+      if ((defs >> t) & 1ull)
+        fast_object<true>((const uint8_t*)sL, (const uint8_t*)sR, Ob + oo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16,
+                          d >> 16, lane);
+      else
+        fast_object<false>((const uint8_t*)sL, (const uint8_t*)sR, Ob + oo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16,
+                           d >> 16, lane);
     }
   }
 }
 
 // ======================================================================
-// General path: objects the fast kernel flagged (deferred removes, records
-// larger than its stage, > 128 union positions). One wave per 64-object chunk
+// General path: objects the fast kernel flagged (records larger than its
+// stage, > 128 union positions, > 32 deferred clocks on a side). One wave per 64-object chunk
 // (a coalesced scan of the chunk's output offsets); every flagged object is
 // staged through LDS when both records fit kGenStage, else joined straight
 // from HBM. Clears the flag it consumes.
