@@ -13,9 +13,16 @@
 
 using namespace crdts_hip;
 
+// Device scratch of a context: status word, the general-path object list
+// and its control words. A context serves one stream at a time.
+constexpr uint32_t kDefaultListCap = 1u << 16;
+
 struct crdt_ctx {
   int device;
-  int* d_status;
+  int* d_status;        // d_scratch + 0
+  uint32_t* d_ctl;      // d_scratch + 16: [list count, finished-block ticket]
+  uint64_t* d_list;     // d_scratch + 64
+  uint32_t list_cap;
   int blocks_per_cu;
 };
 
@@ -71,11 +78,17 @@ int crdt_ctx_create(crdt_ctx** out, int device) {
   auto* c = new crdt_ctx();
   c->device = device;
   c->blocks_per_cu = 8;
-  if (hipMalloc(&c->d_status, sizeof(int)) != hipSuccess ||
-      hipMemset(c->d_status, 0, sizeof(int)) != hipSuccess) {
+  c->list_cap = kDefaultListCap;
+  const size_t bytes = 64 + 8ull * kDefaultListCap;
+  uint8_t* scratch = nullptr;
+  if (hipMalloc(&scratch, bytes) != hipSuccess || hipMemset(scratch, 0, bytes) != hipSuccess) {
+    (void)hipFree(scratch);
     delete c;
     return CRDT_EHIP;
   }
+  c->d_status = (int*)scratch;
+  c->d_ctl = (uint32_t*)(scratch + 16);
+  c->d_list = (uint64_t*)(scratch + 64);
   *out = c;
   return CRDT_OK;
 }
@@ -96,6 +109,14 @@ int crdt_ctx_status(crdt_ctx* ctx, void* stream) {
   if (hipMemcpy(&st, ctx->d_status, sizeof st, hipMemcpyDeviceToHost) != hipSuccess) return CRDT_EHIP;
   if (st != 0 && hipMemset(ctx->d_status, 0, sizeof(int)) != hipSuccess) return CRDT_EHIP;
   return st;
+}
+
+// Test knob (not in the public header): shrink the general-path list so the
+// overflow scan is exercised.
+int crdt_ctx_set_list_cap(crdt_ctx* ctx, uint32_t cap) {
+  if (!ctx || cap > kDefaultListCap) return CRDT_EINVAL;
+  ctx->list_cap = cap;
+  return CRDT_OK;
 }
 
 // Tuning knob (not in the public header): workgroups per CU for the Orswot kernel.
@@ -131,7 +152,8 @@ int crdt_orswot_merge(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_o
   if (rc) return rc;
   return launch_orswot_merge(self->base, self->off, self->bytes, other->base, other->off,
                              other->bytes, d_out_base, d_out_off, out_bytes, self->n_obj, n_actors,
-                             ctx->d_status, S(stream), ctx->blocks_per_cu);
+                             ctx->d_status, ctx->d_ctl, ctx->d_list, ctx->list_cap, S(stream),
+                             ctx->blocks_per_cu);
 }
 
 int crdt_orswot_validate(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32_t n_actors,

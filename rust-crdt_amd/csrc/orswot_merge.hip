@@ -664,7 +664,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
     uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
-    int* __restrict__ status) {
+    int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
   __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wave = threadIdx.x / kWave;
@@ -692,6 +692,10 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_kernel(
     const bool fast = ok && hl0.x <= kFastStage && hr0.x <= kFastStage && hl1.x <= 32u && hr1.x <= 32u &&
                       hl0.z + hr0.z <= 2u * kWave;
     if (valid) Ooff[obj] = (lo + ro) | ((ok && !fast) ? kPending : 0ull);
+    if (ok && !fast) {  // hand the object to the general kernel
+      const uint32_t e = atomicAdd(&ctl[0], 1u);
+      if (e < list_cap) list[e] = obj;
+    }
     if (__ballot(valid && !ok) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
     const uint64_t runs = __ballot(fast);
     if (runs == 0ull) continue;
@@ -735,44 +739,61 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_kernel(
 
 // ======================================================================
 // General path: objects the fast kernel flagged (records larger than its
-// stage, > 128 union positions, > 32 deferred clocks on a side). One wave per 64-object chunk
-// (a coalesced scan of the chunk's output offsets); every flagged object is
-// staged through LDS when both records fit kGenStage, else joined straight
-// from HBM. Clears the flag it consumes.
+// stage, > 128 union positions, > 32 deferred clocks on a side). The fast
+// kernel appends them to a list; a small fixed grid of single-wave blocks
+// joins each one, staged through LDS when both records fit kGenStage, else
+// straight from HBM, and clears its flag. If the list overflowed, the blocks
+// scan every output offset for flags instead. The last block to finish
+// (atomic ticket) resets the list for the next launch on this context.
 // ======================================================================
-constexpr uint32_t kGenStage = 4096;
+constexpr uint32_t kGenStage = 8192;
+constexpr uint32_t kGenBlocks = 512;
 
-__global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_general_kernel(
+__device__ __forceinline__ void general_one(const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb,
+                                            const uint64_t* Roff, uint8_t* Ob, uint64_t* Ooff, uint64_t o, uint32_t A,
+                                            u32x4* sl, u32x4* sr, uint32_t lane) {
+  const uint64_t oo = Ooff[o] & ~kPending;
+  const uint8_t* lr = Lb + Loff[o];
+  const uint8_t* rr = Rb + Roff[o];
+  const uint32_t szl = uni(*(const uint32_t*)lr), szr = uni(*(const uint32_t*)rr);
+  if (szl <= kGenStage && szr <= kGenStage) {
+    wave_sync();
+    for (uint32_t k = lane; k < szl / 16; k += kWave) sl[k] = ((const u32x4*)lr)[k];
+    for (uint32_t k = lane; k < szr / 16; k += kWave) sr[k] = ((const u32x4*)rr)[k];
+    wave_sync();
+    merge_object((const uint8_t*)sl, (const uint8_t*)sr, Ob + oo, A, lane);
+  } else {
+    merge_object(lr, rr, Ob + oo, A, lane);
+  }
+  if (lane == 0) Ooff[o] = oo;
+}
+
+__global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, const uint8_t* __restrict__ Rb,
     const uint64_t* __restrict__ Roff, uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t n_obj,
-    uint32_t A) {
-  __shared__ u32x4 gen_s[kWavesPerBlock][2][kGenStage / 16];
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint32_t wave = threadIdx.x / kWave;
-  const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
-  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
-  for (uint64_t chunk = (uint64_t)blockIdx.x * kWavesPerBlock + wave; chunk < n_chunks; chunk += n_waves) {
-    const uint64_t obj = chunk * kWave + lane;
-    const uint64_t oo = obj < n_obj ? Ooff[obj] : 0ull;
-    uint64_t pend = __ballot((oo & kPending) != 0ull);
-    while (pend) {
-      const uint32_t t = (uint32_t)__builtin_ctzll(pend);
-      pend &= pend - 1;
-      const uint64_t o = chunk * kWave + t;
-      const uint8_t* lr = Lb + Loff[o];
-      const uint8_t* rr = Rb + Roff[o];
-      uint8_t* out = Ob + (lane_of64(oo, t) & ~kPending);
-      const uint32_t szl = uni(*(const uint32_t*)lr), szr = uni(*(const uint32_t*)rr);
-      if (szl <= kGenStage && szr <= kGenStage) {
-        wave_sync();
-        for (uint32_t k = lane; k < szl / 16; k += kWave) gen_s[wave][0][k] = ((const u32x4*)lr)[k];
-        for (uint32_t k = lane; k < szr / 16; k += kWave) gen_s[wave][1][k] = ((const u32x4*)rr)[k];
-        wave_sync();
-        merge_object((const uint8_t*)gen_s[wave][0], (const uint8_t*)gen_s[wave][1], out, A, lane);
-      } else {
-        merge_object(lr, rr, out, A, lane);
-      }
-      if (lane == 0) Ooff[o] = lane_of64(oo, t) & ~kPending;
+    uint32_t A, uint32_t* __restrict__ ctl, const uint64_t* __restrict__ list, uint32_t list_cap) {
+  __shared__ u32x4 gen_s[2][kGenStage / 16];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (n <= list_cap) {
+    for (uint32_t e = blockIdx.x; e < n; e += gridDim.x)
+      general_one(Lb, Loff, Rb, Roff, Ob, Ooff, list[e], A, gen_s[0], gen_s[1], lane);
+  } else {
+    const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
+    for (uint64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
+      const uint64_t obj = chunk * kWave + lane;
+      const uint64_t oo = obj < n_obj ? Ooff[obj] : 0ull;
+      for (uint64_t pend = __ballot((oo & kPending) != 0ull); pend; pend &= pend - 1)
+        general_one(Lb, Loff, Rb, Roff, Ob, Ooff, chunk * kWave + (uint32_t)__builtin_ctzll(pend), A, gen_s[0],
+                    gen_s[1], lane);
+    }
+  }
+  if (lane == 0) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const uint32_t ticket = atomicAdd(&ctl[1], 1u);
+    if (ticket == gridDim.x - 1) {  // every block has read ctl[0]
+      __hip_atomic_store(&ctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -781,8 +802,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_general_k
 
 int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                         const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff,
-                        uint64_t Obytes, uint64_t n_obj, uint32_t n_actors, int* status,
-                        hipStream_t stream, int blocks_per_cu) {
+                        uint64_t Obytes, uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl,
+                        uint64_t* list, uint32_t list_cap, hipStream_t stream, int blocks_per_cu) {
   if (n_obj == 0) return CRDT_OK;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess)
@@ -792,11 +813,9 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   const uint64_t cap = (uint64_t)cus * (blocks_per_cu > 0 ? blocks_per_cu : 8);
   const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
   hipLaunchKernelGGL(orswot_merge_kernel, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, stream, Lb, Loff,
-                     Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors, status);
-  const uint64_t gen_blocks = (chunks + kWavesPerBlock - 1) / kWavesPerBlock;
-  hipLaunchKernelGGL(orswot_merge_general_kernel,
-                     dim3((uint32_t)(gen_blocks < 0x7FFFFFFFull ? gen_blocks : 0x7FFFFFFFull)),
-                     dim3(kWave * kWavesPerBlock), 0, stream, Lb, Loff, Rb, Roff, Ob, Ooff, n_obj, n_actors);
+                     Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors, status, ctl, list, list_cap);
+  hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
+                     Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 

@@ -284,3 +284,23 @@ def test_config3_full_size_bitexact(gpu, oracle):
             h[m] = (h[m] * np.uint64(0x100000001B3)) ^ w[(offs[m] // 8 + k).astype(np.int64)]
         return h
     assert (digest(gb, go, gs) == digest(ob, oo, os_)).all()
+
+
+def test_general_path_list_overflow_and_reset(gpu, oracle):
+    """Objects the fast kernel cannot take go through the general kernel's
+    list; with a tiny list it falls back to scanning every output offset.
+    Launches alternate so the list counter reset between launches is exercised."""
+    import crdts_hip
+
+    params = dict(n_actors=64, member_universe=200, ancestor_adds=150, max_div_ops=40)
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(700, threads=16, seed=4, params=params)
+    (cb, co), (db, do) = crdts_hip.generate_orswot(3000, threads=16, seed=8)  # fast path only
+    ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, 64, threads=16)
+    ob2, oo2 = oracle.orswot_merge_batch(cb, co, db, do, 16, threads=16)
+    try:
+        for cap in (8, 0, 65536, 8):
+            gpu.set_list_cap(cap)
+            _compare(_gpu_merge(gpu, lb, lo, rb, ro, 64), ob, oo, f"cap {cap}")
+            _compare(_gpu_merge(gpu, cb, co, db, do, 16), ob2, oo2, f"fast after cap {cap}")
+    finally:
+        gpu.set_list_cap(65536)
