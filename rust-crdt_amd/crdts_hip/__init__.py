@@ -116,6 +116,10 @@ class Engine:
     def set_blocks_per_cu(self, k):
         check(lib.crdt_ctx_set_blocks_per_cu(self.ctx, int(k)), "set_blocks_per_cu")
 
+    def set_variant(self, v):
+        """Tuning knob: Orswot fast-kernel variant (0 = default)."""
+        check(lib.crdt_ctx_set_variant(self.ctx, int(v)), "set_variant")
+
     def set_list_cap(self, cap):
         """Test knob: capacity of the general-path object list (overflow -> full scan)."""
         check(lib.crdt_ctx_set_list_cap(self.ctx, int(cap)), "set_list_cap")

@@ -24,6 +24,7 @@ struct crdt_ctx {
   uint64_t* d_list;     // d_scratch + 64
   uint32_t list_cap;
   int blocks_per_cu;
+  int variant;  // fast-kernel register budget (min waves per SIMD); 0 = default
 };
 
 namespace {
@@ -79,6 +80,7 @@ int crdt_ctx_create(crdt_ctx** out, int device) {
   c->device = device;
   c->blocks_per_cu = 8;
   c->list_cap = kDefaultListCap;
+  c->variant = 0;
   const size_t bytes = 64 + 8ull * kDefaultListCap;
   uint8_t* scratch = nullptr;
   if (hipMalloc(&scratch, bytes) != hipSuccess || hipMemset(scratch, 0, bytes) != hipSuccess) {
@@ -119,6 +121,13 @@ int crdt_ctx_set_list_cap(crdt_ctx* ctx, uint32_t cap) {
   return CRDT_OK;
 }
 
+// Tuning knob (not in the public header): Orswot fast-kernel variant.
+int crdt_ctx_set_variant(crdt_ctx* ctx, int v) {
+  if (!ctx || v < 0) return CRDT_EINVAL;
+  ctx->variant = v;
+  return CRDT_OK;
+}
+
 // Tuning knob (not in the public header): workgroups per CU for the Orswot kernel.
 int crdt_ctx_set_blocks_per_cu(crdt_ctx* ctx, int k) {
   if (!ctx || k < 1 || k > 64) return CRDT_EINVAL;
@@ -153,7 +162,7 @@ int crdt_orswot_merge(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_o
   return launch_orswot_merge(self->base, self->off, self->bytes, other->base, other->off,
                              other->bytes, d_out_base, d_out_off, out_bytes, self->n_obj, n_actors,
                              ctx->d_status, ctx->d_ctl, ctx->d_list, ctx->list_cap, S(stream),
-                             ctx->blocks_per_cu);
+                             ctx->blocks_per_cu, ctx->variant);
 }
 
 int crdt_orswot_validate(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32_t n_actors,

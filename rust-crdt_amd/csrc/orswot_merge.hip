@@ -453,20 +453,22 @@ __device__ __forceinline__ FSide fside(const uint8_t* b, uint32_t A, uint32_t n_
   return s;
 }
 
-// Merge path at union position p (p <= nL + nR), branch-free.
-__device__ __forceinline__ uint32_t fpath(const FSide& L, const FSide& R, uint32_t p, uint32_t steps, uint32_t& i,
+// Merge path at union position p (p <= nL + nR), branch-free: i = the
+// number of self keys among the first p union positions = the first mid in
+// [lo, hi] with !(L[mid] <= R[p-1-mid]); found with wave-uniform power-of-two
+// steps (`top` = the largest power of two <= min(nL, nR), or 0).
+__device__ __forceinline__ uint32_t fpath(const FSide& L, const FSide& R, uint32_t p, uint32_t top, uint32_t& i,
                                           uint32_t& j) {
-  uint32_t lo = p > R.n ? p - R.n : 0u;
-  uint32_t len = (p < L.n ? p : L.n) - lo;
-  for (uint32_t s = 0; s <= steps; ++s) {
-    const uint32_t half = len >> 1, mid = lo + half;
-    const uint64_t kl = ld64(L.b, L.key + 8u * mid), kr = ld64(R.b, R.key + 8u * (p - 1u - mid));
-    const bool go = len != 0u && kl <= kr;
-    lo = go ? mid + 1u : lo;
-    len = len == 0u ? 0u : (go ? len - half - 1u : half);
+  const uint32_t lo = p > R.n ? p - R.n : 0u;
+  const uint32_t hi = p < L.n ? p : L.n;
+  uint32_t base = lo;
+  for (uint32_t step = top; step != 0u; step >>= 1) {
+    const uint32_t cand = base + step;  // test mid = cand - 1
+    const uint64_t kl = ld64(L.b, L.key + 8u * cand - 8u), kr = ld64(R.b, R.key + 8u * (p - cand));
+    base = (cand <= hi && kl <= kr) ? cand : base;
   }
-  i = lo;
-  j = p - lo;
+  i = base;
+  j = p - base;
   const uint64_t kl = ld64(L.b, L.key + 8u * i), kr = ld64(R.b, R.key + 8u * j);
   const uint64_t kp = ld64(L.b, L.key + 8u * i - 8u);
   const bool hl = i < L.n, hr = j < R.n;
@@ -570,13 +572,14 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
   Side DL{Ls, RV{}}, DR{Rs, RV{}};
   if (HD) { DL = side_of(Ls); DR = side_of(Rs); }
   const uint32_t P = nL + nR;
-  const uint32_t steps = 32u - __builtin_clz((nL < nR ? nL : nR) | 1u);
+  const uint32_t mn = nL < nR ? nL : nR;
+  const uint32_t top = mn ? 1u << (31u - __builtin_clz(mn)) : 0u;
   // chunk 0: positions 0..63
   uint32_t i = 0, j = 0, x0 = 0, c0 = 0, q0 = 0;
   uint64_t v0 = 0, m0k = 0;
   {
     const uint32_t p = lane < P ? lane : P;
-    uint32_t type = fpath(L, R, p, steps, i, j);
+    uint32_t type = fpath(L, R, p, top, i, j);
     type = lane < P ? type : kNone;
     if (HD && type != kNone) m0k = dmask_of(DL, DR, (type & kSelf) ? ld64(Ls, L.key + 8u * i) : ld64(Rs, R.key + 8u * j));
     c0 = fjoin<false, HD>(L, R, A, type, i, j, x0, v0, nullptr, nullptr, 0u, m0k, DL, DR);
@@ -587,7 +590,7 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
   uint64_t v1 = 0, m1k = 0;
   if (P > (uint32_t)kWave) {
     const uint32_t p = lane + kWave < P ? lane + kWave : P;
-    uint32_t type = fpath(L, R, p, steps, i, j);
+    uint32_t type = fpath(L, R, p, top, i, j);
     type = lane + kWave < P ? type : kNone;
     if (HD && type != kNone) m1k = dmask_of(DL, DR, (type & kSelf) ? ld64(Ls, L.key + 8u * i) : ld64(Rs, R.key + 8u * j));
     c1 = fjoin<false, HD>(L, R, A, type, i, j, x1, v1, nullptr, nullptr, 0u, m1k, DL, DR);
@@ -660,7 +663,8 @@ __device__ __forceinline__ void stage(u32x4* dst, const u32x4 (&r)[kPer], uint32
   }
 }
 
-__global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_kernel(
+template <int MINW>
+__global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
     uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
@@ -803,7 +807,7 @@ __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
 int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                         const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff,
                         uint64_t Obytes, uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl,
-                        uint64_t* list, uint32_t list_cap, hipStream_t stream, int blocks_per_cu) {
+                        uint64_t* list, uint32_t list_cap, hipStream_t stream, int blocks_per_cu, int variant) {
   if (n_obj == 0) return CRDT_OK;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess)
@@ -812,8 +816,13 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   const uint64_t want = (chunks + kWavesPerBlock - 1) / kWavesPerBlock;
   const uint64_t cap = (uint64_t)cus * (blocks_per_cu > 0 ? blocks_per_cu : 8);
   const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
-  hipLaunchKernelGGL(orswot_merge_kernel, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, stream, Lb, Loff,
-                     Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors, status, ctl, list, list_cap);
+  // variant = the fast kernel's minimum waves per SIMD (register budget)
+  if (variant == 6)
+    hipLaunchKernelGGL(orswot_merge_kernel<6>, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, stream, Lb, Loff,
+                       Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors, status, ctl, list, list_cap);
+  else
+    hipLaunchKernelGGL(orswot_merge_kernel<1>, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, stream, Lb, Loff,
+                       Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors, status, ctl, list, list_cap);
   hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
                      Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;

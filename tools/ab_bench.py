@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of Orswot merge kernel variants in ONE process
+(config 3, 1M objects): N rounds x each variant, HIP-event timing of the
+merge launch(es); prints median/min ms per variant as one JSON line."""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "rust-crdt_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="0,6")
+    ap.add_argument("--bpc", default="8", help="blocks per CU values to sweep")
+    ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--n-obj", type=int, default=1_000_000)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import crdts_hip
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(a.n_obj, threads=16)
+    eng = crdts_hip.Engine(0)
+    L = crdts_hip.OrswotBatch.from_host(lb, lo, 16)
+    R = crdts_hip.OrswotBatch.from_host(rb, ro, 16)
+    out = eng.orswot_alloc_out(L, R)
+    s = torch.cuda.Stream()
+    configs = [(int(v), int(b)) for v in a.variants.split(",") for b in a.bpc.split(",")]
+    res = {c: [] for c in configs}
+    ref = None
+    for r in range(a.rounds + 1):
+        for c in configs:
+            eng.set_variant(c[0])
+            eng.set_blocks_per_cu(c[1])
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            eng.orswot_merge(L, R, out=out, stream=s, check_status=False)
+            e1.record(s)
+            s.synchronize()
+            eng.status(s)
+            if r > 0:
+                res[c].append(e0.elapsed_time(e1))
+            if r == 0:
+                h = out.base.sum().item()
+                ref = h if ref is None else ref
+                assert h == ref, f"variant {c} output differs"
+    print(json.dumps({f"v{c[0]}_bpc{c[1]}": {"median_ms": float(np.median(v)), "min_ms": float(np.min(v))}
+                      for c, v in res.items()}))
+
+
+if __name__ == "__main__":
+    main()
