@@ -78,7 +78,7 @@ int crdt_ctx_create(crdt_ctx** out, int device) {
   if (hipSetDevice(device) != hipSuccess) return CRDT_EHIP;
   auto* c = new crdt_ctx();
   c->device = device;
-  c->blocks_per_cu = 8;
+  c->blocks_per_cu = 0;
   c->list_cap = kDefaultListCap;
   c->variant = 0;
   const size_t bytes = 64 + 8ull * kDefaultListCap;
@@ -130,7 +130,7 @@ int crdt_ctx_set_variant(crdt_ctx* ctx, int v) {
 
 // Tuning knob (not in the public header): workgroups per CU for the Orswot kernel.
 int crdt_ctx_set_blocks_per_cu(crdt_ctx* ctx, int k) {
-  if (!ctx || k < 1 || k > 64) return CRDT_EINVAL;
+  if (!ctx || k < 0 || k > 64) return CRDT_EINVAL;  // 0 = the variant's occupancy
   ctx->blocks_per_cu = k;
   return CRDT_OK;
 }
