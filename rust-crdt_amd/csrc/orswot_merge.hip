@@ -674,18 +674,18 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
   const uint32_t wave = threadIdx.x / kWave;
   u32x4* const sL = stage_s[wave][0];
   u32x4* const sR = stage_s[wave][1];
-  // Each wave owns one contiguous range of objects of equal length (the grid
-  // is sized to residency), walked in 64-object chunks: no tail imbalance.
+  // Rounds of chunks: in round r wave w takes chunk r * n_waves + w of `cs`
+  // consecutive objects, cs <= 64 chosen so every wave gets the same number
+  // of rounds (no tail) while concurrent waves read neighbouring memory.
   const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
   const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint64_t per = (n_obj + n_waves - 1) / n_waves;
-  const uint64_t r_begin = wave_id * per < n_obj ? wave_id * per : n_obj;
-  const uint64_t r_end = r_begin + per < n_obj ? r_begin + per : n_obj;
+  const uint64_t rounds = (n_obj + n_waves * kWave - 1) / (n_waves * kWave);
+  const uint64_t cs = (n_obj + n_waves * rounds - 1) / (n_waves * rounds);
 
-  for (uint64_t cbase = r_begin; cbase < r_end; cbase += kWave) {
+  for (uint64_t cbase = wave_id * cs; cbase < n_obj; cbase += n_waves * cs) {
     // ---- chunk state: lane k <-> object cbase + k
     const uint64_t obj = cbase + lane;
-    const bool valid = obj < r_end;
+    const bool valid = lane < cs && obj < n_obj;
     uint64_t lo = 0, ro = 0;
     if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
     u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
@@ -816,9 +816,8 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  // Resident grid: one 4-wave block per SIMD-wave slot of the variant's
-  // occupancy (blocks_per_cu overrides), but no more 4-wave blocks than needed
-  // to give every wave at least 64 objects.
+  // Resident grid: the variant's occupancy in 4-wave blocks per CU
+  // (blocks_per_cu overrides), no more blocks than 64-object chunks need.
   const int occ = variant == 6 ? 6 : 5;
   const uint64_t chunks = (n_obj + kWave - 1) / kWave;
   const uint64_t want = (chunks + kWavesPerBlock - 1) / kWavesPerBlock;
