@@ -29,6 +29,8 @@
 // Canonical record layout: include/crdts_hip.h, record_layout.h.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "../../include/crdts_hip.h"
 #include "kernels.h"
 #include "record_layout.h"
@@ -419,6 +421,7 @@ __device__ __forceinline__ bool header_ok(u32x4 h0, u32x4 h1, uint64_t off, uint
 // count and the write pass.
 // ======================================================================
 constexpr uint32_t kFastStage = 2048;                 // LDS stage per input record per wave
+constexpr uint32_t kOutStage = 2048;                  // LDS stage for the output record per wave
 constexpr uint32_t kPer = kFastStage / 16 / kWave;    // 16-B pieces per lane per record
 constexpr uint64_t kPending = 1ull << 63;             // Ooff flag: object left for the general kernel
 
@@ -567,11 +570,24 @@ __device__ __forceinline__ Side side_of(const uint8_t* b) { return Side{b, make_
 // HD: the object has deferred removes (either side; <= 32 clocks per side).
 // ABL (ablation builds for timing only; outputs are NOT valid): 1 = stage
 // only, 2 = + merge path, 3 = + counting join, 0 = the real kernel.
+// Where a fast-path object's output goes: built in the wave's LDS output
+// stage `Os`, then copied to `Og` in HBM with 16-B coalesced stores. An
+// output larger than the stage is handed to the general kernel instead.
+struct FOut {
+  u32x4* Os;
+  uint8_t* Og;
+  uint64_t obj;
+  uint64_t* Ooff;
+  uint32_t* ctl;
+  uint64_t* list;
+  uint32_t list_cap;
+};
+
 template <bool HD, int ABL>
-__device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* O, uint32_t A,
+__device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs, const FOut& fo, uint32_t A,
                                             uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane) {
   if (ABL == 1) {
-    if (lane == 0) *(u32x4*)O = u32x4{ld32(Ls, 4), ld32(Rs, 4), nL, nR};
+    if (lane == 0) *(u32x4*)fo.Og = u32x4{ld32(Ls, 4), ld32(Rs, 4), nL, nR};
     return;
   }
   const FSide L = fside(Ls, A, nL, dL), R = fside(Rs, A, nR, dR);
@@ -604,8 +620,8 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
   }
   if (ABL == 2 || ABL == 3) {  // keep the phase's results live, skip the writes
     const uint32_t k = q0 + q1 + c0 + c1 + x0 + x1 + (uint32_t)(v0 ^ v1);
-    if (__ballot(k == 0x12345u) != 0ull && lane == 0) *(uint32_t*)O = k;
-    if (lane == 0) *(u32x4*)O = u32x4{nL, nR, 0u, 0u};
+    if (__ballot(k == 0x12345u) != 0ull && lane == 0) *(uint32_t*)fo.Og = k;
+    if (lane == 0) *(u32x4*)fo.Og = u32x4{nL, nR, 0u, 0u};
     return;
   }
   const uint32_t inc0 = scan_incl(c0), inc1 = scan_incl(c1);
@@ -614,18 +630,31 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
   const uint32_t m0 = (uint32_t)__popcll(k0);
   const uint32_t tot_mem = m0 + (uint32_t)__popcll(k1), tot_dot = tot0 + tot1;
 
-  // output member block; the deferred block (if any) follows it
-  const uint32_t o_key = kHdrBytes + 8u * A;
-  const uint32_t o_dctr = o_key + 8u * tot_mem;
-  const uint32_t o_dact = o_dctr + 8u * tot_dot;
-  const uint32_t o_mdend = o_dact + 4u * tot_dot;
-  const uint32_t o_mpad = o_mdend + 4u * tot_mem;
-  const uint32_t o_def = (o_mpad + 7u) & ~7u;
-  uint64_t* okey = (uint64_t*)(O + o_key);
-  uint64_t* odctr = (uint64_t*)(O + o_dctr);
-  uint32_t* odact = (uint32_t*)(O + o_dact);
-  uint32_t* omdend = (uint32_t*)(O + o_mdend);
+  // deferred counts first (lane 0), so the output size is known up front
+  uint32_t nd = 0, ndd = 0, ndm = 0;
+  if (HD) {
+    if (lane == 0u) deferred_pass(DL, DR, A, nd, ndd, ndm, nullptr);
+    nd = lane_of(nd, 0);
+    ndd = lane_of(ndd, 0);
+    ndm = lane_of(ndm, 0);
+  }
+  RecLayout OL;
+  rec_layout(OL, A, tot_mem, tot_dot, nd, ndd, ndm);
+  if (OL.size > kOutStage) {  // rare: let the general kernel write it
+    if (lane == 0u) {
+      fo.Ooff[fo.obj] |= kPending;
+      const uint32_t e = atomicAdd(&fo.ctl[0], 1u);
+      if (e < fo.list_cap) fo.list[e] = fo.obj;
+    }
+    return;
+  }
+  uint8_t* O = (uint8_t*)fo.Os;
+  uint64_t* okey = (uint64_t*)(O + OL.o_key);
+  uint64_t* odctr = (uint64_t*)(O + OL.o_dctr);
+  uint32_t* odact = (uint32_t*)(O + OL.o_dact);
+  uint32_t* omdend = (uint32_t*)(O + OL.o_mdend);
 
+  wave_sync();  // the previous object's copy-out has read the stage
   // top clock: pointwise max (src/orswot.rs:153 -> src/vclock.rs:131-137)
   for (uint32_t a = lane; a < A; a += kWave) {
     const uint64_t x = ld64(Ls, kHdrBytes + 8u * a), y = ld64(Rs, kHdrBytes + 8u * a);
@@ -639,24 +668,22 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
     fwrite_member<HD>(L, R, A, q1, c1, x1, v1, m0 + (uint32_t)__popcll(k1 & lt), tot0 + inc1 - c1, okey, odact,
                       odctr, omdend, m1k, DL, DR);
   if (lane == 0u) {
-    uint32_t nd = 0, ndd = 0, ndm = 0, end = o_def;
-    if (o_def != o_mpad) *(uint32_t*)(O + o_mpad) = 0u;
+    if (OL.o_def != OL.o_mpad) *(uint32_t*)(O + OL.o_mpad) = 0u;
     if (HD) {
       // deferred union keyed by clock (:141-148), kept iff !(D <= clock) (:197)
-      deferred_pass(DL, DR, A, nd, ndd, ndm, nullptr);
-      RecLayout OL;
-      rec_layout(OL, A, tot_mem, tot_dot, nd, ndd, ndm);
       DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
                (uint32_t*)(O + OL.o_fdend), (uint32_t*)(O + OL.o_fmend)};
       deferred_pass(DL, DR, A, nd, ndd, ndm, &w);
-      end = OL.o_end;
     }
-    const uint32_t size = (end + 15u) & ~15u;
-    for (uint32_t b = end; b < size; b += 4) *(uint32_t*)(O + b) = 0u;
+    for (uint32_t b = OL.o_end; b < OL.size; b += 4) *(uint32_t*)(O + b) = 0u;
     u32x4* h = (u32x4*)O;
-    h[0] = u32x4{size, A, tot_mem, tot_dot};
+    h[0] = u32x4{OL.size, A, tot_mem, tot_dot};
     h[1] = u32x4{nd, ndd, ndm, 0u};
   }
+  wave_sync();
+  // copy-out: 16-B coalesced, non-temporal (the output is not re-read here)
+  const uint32_t n16 = OL.size / 16u;
+  for (uint32_t k = lane; k < n16; k += kWave) __builtin_nontemporal_store(fo.Os[k], (u32x4*)fo.Og + k);
 }
 
 __device__ __forceinline__ void prefetch(u32x4 (&r)[kPer], const uint8_t* src, uint32_t n16, uint32_t lane) {
@@ -682,6 +709,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
     uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
     int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
   __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
+  __shared__ u32x4 out_s[kWavesPerBlock][kOutStage / 16];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wave = threadIdx.x / kWave;
   u32x4* const sL = stage_s[wave][0];
@@ -747,12 +775,13 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
         prefetch(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
         prefetch(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
       }
+      const FOut fo{out_s[wave], Ob + oo, cbase + t, Ooff, ctl, list, list_cap};
       if ((defs >> t) & 1ull)
-        fast_object<true, ABL>((const uint8_t*)sL, (const uint8_t*)sR, Ob + oo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16,
-                          d >> 16, lane);
+        fast_object<true, ABL>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16,
+                               d >> 16, lane);
       else
-        fast_object<false, ABL>((const uint8_t*)sL, (const uint8_t*)sR, Ob + oo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16,
-                           d >> 16, lane);
+        fast_object<false, ABL>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16,
+                                d >> 16, lane);
     }
   }
 }
@@ -828,27 +857,35 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  // Resident grid: the variant's occupancy in 4-wave blocks per CU
+  // variant: the fast kernel's minimum waves per SIMD (register budget);
+  // 101..103 are timing-only ablation builds (invalid output).
+  const void* fn;
+  switch (variant) {
+    case 5: fn = (const void*)orswot_merge_kernel<5, 0>; break;
+    case 6: fn = (const void*)orswot_merge_kernel<6, 0>; break;
+    case 101: fn = (const void*)orswot_merge_kernel<6, 1>; break;
+    case 102: fn = (const void*)orswot_merge_kernel<6, 2>; break;
+    case 103: fn = (const void*)orswot_merge_kernel<6, 3>; break;
+    default: fn = (const void*)orswot_merge_kernel<1, 0>; break;
+  }
+  // Resident grid: the kernel's occupancy in 4-wave blocks per CU
   // (blocks_per_cu overrides), no more blocks than 64-object chunks need.
-  const int occ = variant == 0 ? 5 : 6;
+  static std::atomic<int> occ_cache[8];  // per variant slot, 0 = not yet queried
+  const int slot = variant == 5 ? 1 : variant == 6 ? 2 : variant >= 101 && variant <= 103 ? variant - 98 : 0;
+  int occ = occ_cache[slot].load(std::memory_order_relaxed);
+  if (occ == 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)
+      occ = 4;
+    occ_cache[slot].store(occ, std::memory_order_relaxed);
+  }
   const uint64_t chunks = (n_obj + kWave - 1) / kWave;
   const uint64_t want = (chunks + kWavesPerBlock - 1) / kWavesPerBlock;
   const uint64_t cap = (uint64_t)cus * (blocks_per_cu > 0 ? blocks_per_cu : occ);
   const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
-  // variant: the fast kernel's minimum waves per SIMD (register budget);
-  // 101..103 are timing-only ablation builds (invalid output).
-#define CRDT_LAUNCH_FAST(MINW, ABL)                                                                          \
-  hipLaunchKernelGGL((orswot_merge_kernel<MINW, ABL>), dim3(blocks), dim3(kWave * kWavesPerBlock), 0, stream, \
-                     Lb, Loff, Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors, status, ctl, list,  \
-                     list_cap)
-  switch (variant) {
-    case 6: CRDT_LAUNCH_FAST(6, 0); break;
-    case 101: CRDT_LAUNCH_FAST(6, 1); break;
-    case 102: CRDT_LAUNCH_FAST(6, 2); break;
-    case 103: CRDT_LAUNCH_FAST(6, 3); break;
-    default: CRDT_LAUNCH_FAST(1, 0); break;
-  }
-#undef CRDT_LAUNCH_FAST
+  void* args[] = {&Lb, &Loff, &Lbytes, &Rb, &Roff, &Rbytes, &Ob, &Ooff, &Obytes, &n_obj, &n_actors, &status,
+                  &ctl, &list, &list_cap};
+  if (hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) != hipSuccess)
+    return CRDT_EHIP;
   hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
                      Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
