@@ -75,6 +75,7 @@ def _load():
         "crdt_ctx_set_blocks_per_cu": (I, [P, I]),
         "crdt_ctx_set_list_cap": (I, [P, U32]),
         "crdt_ctx_set_variant": (I, [P, I]),
+        "crdt_ctx_debug_read": (I, [P, P, SZ, P]),
         "crdt_strerror": (C.c_char_p, [I]),
         "crdt_abi_version": (I, []),
         "crdt_vclock_dense_merge": (I, [P, P, P, SZ, U32, P]),

@@ -121,6 +121,16 @@ int crdt_ctx_set_list_cap(crdt_ctx* ctx, uint32_t cap) {
   return CRDT_OK;
 }
 
+// Diagnostics (not in the public header): copy the context's list buffer
+// (holds per-wave phase stamps after a variant-109 launch).
+int crdt_ctx_debug_read(crdt_ctx* ctx, uint64_t* h_out, size_t n, void* stream) {
+  if (!ctx || !h_out || n > 8ull * kDefaultListCap / 8) return CRDT_EINVAL;
+  if (hipMemcpyAsync(h_out, ctx->d_list, 8 * n, hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
+      hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+    return CRDT_EHIP;
+  return CRDT_OK;
+}
+
 // Tuning knob (not in the public header): Orswot fast-kernel variant.
 int crdt_ctx_set_variant(crdt_ctx* ctx, int v) {
   if (!ctx || v < 0) return CRDT_EINVAL;

@@ -51,6 +51,28 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Diagnostic in-kernel stamps (ABL == 9 builds only; never in the real
+// kernel): s_memtime with its own lgkmcnt wait, fenced by sched barriers.
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+struct Stamps {
+  uint64_t acc[8];
+  uint64_t last;
+};
+template <int ABL>
+__device__ __forceinline__ void mark(Stamps& st, int k) {
+  if (ABL == 9) {
+    const uint64_t t = stamp();
+    st.acc[k] += t - st.last;
+    st.last = t;
+  }
+}
+
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint32_t lane_of(uint32_t v, uint32_t t) { return __builtin_amdgcn_readlane(v, t); }
 __device__ __forceinline__ uint64_t lane_of64(uint64_t v, uint32_t t) {
@@ -585,7 +607,8 @@ struct FOut {
 
 template <bool HD, int ABL>
 __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs, const FOut& fo, uint32_t A,
-                                            uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane) {
+                                            uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane,
+                                            Stamps& st) {
   if (ABL == 1) {
     if (lane == 0) *(u32x4*)fo.Og = u32x4{ld32(Ls, 4), ld32(Rs, 4), nL, nR};
     return;
@@ -604,8 +627,10 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
     uint32_t type = fpath(L, R, p, top, i, j);
     type = lane < P ? type : kNone;
     if (HD && type != kNone) m0k = dmask_of(DL, DR, (type & kSelf) ? ld64(Ls, L.key + 8u * i) : ld64(Rs, R.key + 8u * j));
+    mark<ABL>(st, 2);
     if (ABL != 2) c0 = fjoin<false, HD>(L, R, A, type, i, j, x0, v0, nullptr, nullptr, 0u, m0k, DL, DR);
     q0 = (type << 30) | (i << 15) | j;
+    mark<ABL>(st, 3);
   }
   // chunk 1: positions 64..127 (P <= 128 on this path)
   uint32_t x1 = 0, c1 = 0, q1 = 0;
@@ -615,8 +640,10 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
     uint32_t type = fpath(L, R, p, top, i, j);
     type = lane + kWave < P ? type : kNone;
     if (HD && type != kNone) m1k = dmask_of(DL, DR, (type & kSelf) ? ld64(Ls, L.key + 8u * i) : ld64(Rs, R.key + 8u * j));
+    mark<ABL>(st, 2);
     if (ABL != 2) c1 = fjoin<false, HD>(L, R, A, type, i, j, x1, v1, nullptr, nullptr, 0u, m1k, DL, DR);
     q1 = (type << 30) | (i << 15) | j;
+    mark<ABL>(st, 3);
   }
   if (ABL == 2 || ABL == 3) {  // keep the phase's results live, skip the writes
     const uint32_t k = q0 + q1 + c0 + c1 + x0 + x1 + (uint32_t)(v0 ^ v1);
@@ -640,6 +667,7 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
   }
   RecLayout OL;
   rec_layout(OL, A, tot_mem, tot_dot, nd, ndd, ndm);
+  mark<ABL>(st, 4);
   if (OL.size > kOutStage) {  // rare: let the general kernel write it
     if (lane == 0u) {
       fo.Ooff[fo.obj] |= kPending;
@@ -681,9 +709,11 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
     h[1] = u32x4{nd, ndd, ndm, 0u};
   }
   wave_sync();
+  mark<ABL>(st, 5);
   // copy-out: 16-B coalesced, non-temporal (the output is not re-read here)
   const uint32_t n16 = OL.size / 16u;
   for (uint32_t k = lane; k < n16; k += kWave) __builtin_nontemporal_store(fo.Os[k], (u32x4*)fo.Og + k);
+  mark<ABL>(st, 6);
 }
 
 __device__ __forceinline__ void prefetch(u32x4 (&r)[kPer], const uint8_t* src, uint32_t n16, uint32_t lane) {
@@ -722,6 +752,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
   const uint64_t rounds = (n_obj + n_waves * kWave - 1) / (n_waves * kWave);
   const uint64_t cs = (n_obj + n_waves * rounds - 1) / (n_waves * rounds);
 
+  Stamps st{};
+  if (ABL == 9) st.last = stamp();
   for (uint64_t cbase = wave_id * cs; cbase < n_obj; cbase += n_waves * cs) {
     // ---- chunk state: lane k <-> object cbase + k
     const uint64_t obj = cbase + lane;
@@ -759,6 +791,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
     uint32_t nn = lane_of(n16, t);
     prefetch(pl, Lb + lane_of64(lo, t), nn & 0xFFFFu, lane);
     prefetch(pr, Rb + lane_of64(ro, t), nn >> 16, lane);
+    mark<ABL>(st, 7);  // chunk state
     while (pend) {
       t = (uint32_t)__builtin_ctzll(pend);
       pend &= pend - 1;
@@ -767,6 +800,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
       stage(sL, pl, nn & 0xFFFFu, lane);
       stage(sR, pr, nn >> 16, lane);
       wave_sync();
+      mark<ABL>(st, 0);  // wait for the prefetched records + stage them
       const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
       const uint32_t m = lane_of(nm, t), d = lane_of(nd, t);
       if (pend) {
@@ -775,14 +809,21 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
         prefetch(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
         prefetch(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
       }
+      mark<ABL>(st, 1);  // issue the next prefetch
       const FOut fo{out_s[wave], Ob + oo, cbase + t, Ooff, ctl, list, list_cap};
       if ((defs >> t) & 1ull)
         fast_object<true, ABL>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16,
-                               d >> 16, lane);
+                               d >> 16, lane, st);
       else
         fast_object<false, ABL>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16,
-                                d >> 16, lane);
+                                d >> 16, lane, st);
     }
+  }
+  if (ABL == 9 && lane < 8u) {  // per-wave phase sums -> the context's list buffer
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v = lane == (uint32_t)k ? st.acc[k] : v;
+    list[wave_id * 8u + lane] = v;
   }
 }
 
@@ -866,12 +907,13 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
     case 101: fn = (const void*)orswot_merge_kernel<6, 1>; break;
     case 102: fn = (const void*)orswot_merge_kernel<6, 2>; break;
     case 103: fn = (const void*)orswot_merge_kernel<6, 3>; break;
+    case 109: fn = (const void*)orswot_merge_kernel<5, 9>; break;
     default: fn = (const void*)orswot_merge_kernel<1, 0>; break;
   }
   // Resident grid: the kernel's occupancy in 4-wave blocks per CU
   // (blocks_per_cu overrides), no more blocks than 64-object chunks need.
   static std::atomic<int> occ_cache[8];  // per variant slot, 0 = not yet queried
-  const int slot = variant == 5 ? 1 : variant == 6 ? 2 : variant >= 101 && variant <= 103 ? variant - 98 : 0;
+  const int slot = variant == 5 ? 1 : variant == 6 ? 2 : variant >= 101 && variant <= 103 ? variant - 98 : variant == 109 ? 6 : 0;
   int occ = occ_cache[slot].load(std::memory_order_relaxed);
   if (occ == 0) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)
