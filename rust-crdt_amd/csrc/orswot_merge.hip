@@ -310,6 +310,91 @@ __device__ void deferred_pass(const Side& L, const Side& R, uint32_t A, uint32_t
   }
 }
 
+// Wave-cooperative deferred union + filter (same semantics as deferred_pass:
+// src/orswot.rs:141-148, then :155 -> :197-203). Entries are walked in CLOCK
+// ORDER by a wave-uniform loop; per entry the dot-level work (clock compare,
+// survival test, copies) is spread over the lanes. With w == nullptr only
+// counts. Every lane returns the same counts.
+__device__ __forceinline__ int clock_cmp_wave(const Side& X, uint32_t k, const Side& Y, uint32_t l, uint32_t lane) {
+  const uint32_t a0 = uni(run_begin(X.b, X.v.fdend, k)), na = uni(g32(X.b, X.v.fdend, k)) - a0;
+  const uint32_t b0 = uni(run_begin(Y.b, Y.v.fdend, l)), nb = uni(g32(Y.b, Y.v.fdend, l)) - b0;
+  const uint32_t n = na < nb ? na : nb;
+  for (uint32_t base = 0; base < n; base += kWave) {
+    const uint32_t d = base + lane;
+    int c = 0;
+    if (d < n) {
+      const uint32_t xa = g32(X.b, X.v.fact, a0 + d), xb = g32(Y.b, Y.v.fact, b0 + d);
+      const uint64_t va = g64(X.b, X.v.fctr, a0 + d), vb = g64(Y.b, Y.v.fctr, b0 + d);
+      c = xa != xb ? (xa < xb ? -1 : 1) : (va != vb ? (va < vb ? -1 : 1) : 0);
+    }
+    const uint64_t diff = __ballot(c != 0);
+    if (diff) return (int)__builtin_amdgcn_readlane((uint32_t)c, (uint32_t)__builtin_ctzll(diff));
+  }
+  return na == nb ? 0 : (na < nb ? -1 : 1);
+}
+
+__device__ __forceinline__ bool def_survives_wave(const Side& X, uint32_t k, const Side& L, const Side& R, uint32_t A,
+                                                  uint32_t lane) {
+  const uint32_t s = uni(run_begin(X.b, X.v.fdend, k)), e = uni(g32(X.b, X.v.fdend, k));
+  bool any = false;
+  for (uint32_t d = s + lane; d < e; d += kWave) {
+    const uint32_t x = g32(X.b, X.v.fact, d);
+    const uint64_t lc = top(L.b, L.v, x, A), rc = top(R.b, R.v, x, A);
+    any = any || g64(X.b, X.v.fctr, d) > (lc > rc ? lc : rc);
+  }
+  return __ballot(any) != 0ull;
+}
+
+__device__ void deferred_pass_wave(const Side& L, const Side& R, uint32_t A, uint32_t lane, uint32_t& nd,
+                                   uint32_t& ndd, uint32_t& ndm, const DefOut* w) {
+  uint32_t k = 0, l = 0;
+  nd = ndd = ndm = 0;
+  const uint32_t nfL = uni(L.v.n_def), nfR = uni(R.v.n_def);
+  while (k < nfL || l < nfR) {
+    const int c = k >= nfL ? 1 : (l >= nfR ? -1 : clock_cmp_wave(L, k, R, l, lane));
+    const Side& X = c <= 0 ? L : R;
+    const uint32_t kx = c <= 0 ? k : l;
+    if (def_survives_wave(X, kx, L, R, A, lane)) {
+      const uint32_t s = uni(run_begin(X.b, X.v.fdend, kx)), e = uni(g32(X.b, X.v.fdend, kx));
+      if (w)
+        for (uint32_t d = s + lane; d < e; d += kWave) {
+          w->fact[ndd + d - s] = g32(X.b, X.v.fact, d);
+          w->fctr[ndd + d - s] = g64(X.b, X.v.fctr, d);
+        }
+      ndd += e - s;
+      // member set: self's, other's (copied by the lanes), or — for a clock
+      // present on both sides — the sorted union of both (lane 0, rare)
+      if (c != 0) {
+        const uint32_t ms = uni(run_begin(X.b, X.v.fmend, kx)), me = uni(g32(X.b, X.v.fmend, kx));
+        if (w)
+          for (uint32_t j = ms + lane; j < me; j += kWave) w->fkey[ndm + j - ms] = g64(X.b, X.v.fkey, j);
+        ndm += me - ms;
+      } else {
+        uint32_t cnt = 0;
+        if (lane == 0u) {
+          uint32_t a = run_begin(L.b, L.v.fmend, k), ae = g32(L.b, L.v.fmend, k);
+          uint32_t b = run_begin(R.b, R.v.fmend, l), be = g32(R.b, R.v.fmend, l);
+          while (a < ae || b < be) {
+            const uint64_t ka = a < ae ? g64(L.b, L.v.fkey, a) : ~0ull;
+            const uint64_t kb = b < be ? g64(R.b, R.v.fkey, b) : ~0ull;
+            uint64_t km;
+            if (a < ae && (b >= be || ka < kb)) { km = ka; ++a; }
+            else if (b < be && (a >= ae || kb < ka)) { km = kb; ++b; }
+            else { km = ka; ++a; ++b; }
+            if (w) w->fkey[ndm + cnt] = km;
+            ++cnt;
+          }
+        }
+        ndm += lane_of(cnt, 0);
+      }
+      if (w && lane == 0u) { w->fdend[nd] = ndd; w->fmend[nd] = ndm; }
+      ++nd;
+    }
+    if (c <= 0) ++k;
+    if (c >= 0) ++l;
+  }
+}
+
 __device__ __forceinline__ RecLayout layout_at(const uint8_t* rec) {
   const uint32_t* h = (const uint32_t*)rec;
   RecLayout L;
@@ -659,12 +744,7 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
 
   // deferred counts first (lane 0), so the output size is known up front
   uint32_t nd = 0, ndd = 0, ndm = 0;
-  if (HD) {
-    if (lane == 0u) deferred_pass(DL, DR, A, nd, ndd, ndm, nullptr);
-    nd = lane_of(nd, 0);
-    ndd = lane_of(ndd, 0);
-    ndm = lane_of(ndm, 0);
-  }
+  if (HD) deferred_pass_wave(DL, DR, A, lane, nd, ndd, ndm, nullptr);
   RecLayout OL;
   rec_layout(OL, A, tot_mem, tot_dot, nd, ndd, ndm);
   mark<ABL>(st, 4);
@@ -695,14 +775,14 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
   if (c1 != 0u)
     fwrite_member<HD>(L, R, A, q1, c1, x1, v1, m0 + (uint32_t)__popcll(k1 & lt), tot0 + inc1 - c1, okey, odact,
                       odctr, omdend, m1k, DL, DR);
+  if (HD) {
+    // deferred union keyed by clock (:141-148), kept iff !(D <= clock) (:197)
+    DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
+             (uint32_t*)(O + OL.o_fdend), (uint32_t*)(O + OL.o_fmend)};
+    deferred_pass_wave(DL, DR, A, lane, nd, ndd, ndm, &w);
+  }
   if (lane == 0u) {
     if (OL.o_def != OL.o_mpad) *(uint32_t*)(O + OL.o_mpad) = 0u;
-    if (HD) {
-      // deferred union keyed by clock (:141-148), kept iff !(D <= clock) (:197)
-      DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
-               (uint32_t*)(O + OL.o_fdend), (uint32_t*)(O + OL.o_fmend)};
-      deferred_pass(DL, DR, A, nd, ndd, ndm, &w);
-    }
     for (uint32_t b = OL.o_end; b < OL.size; b += 4) *(uint32_t*)(O + b) = 0u;
     u32x4* h = (u32x4*)O;
     h[0] = u32x4{OL.size, A, tot_mem, tot_dot};
