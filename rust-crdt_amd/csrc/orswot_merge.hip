@@ -606,12 +606,14 @@ __device__ __forceinline__ bool dkilled(const Side& DL, const Side& DR, uint64_t
 }
 
 // Joined dot run of one member (rules of join<> above / src/orswot.rs:94-138).
-// COUNT: returns the run length and captures the first dot in (x0, v0);
+// COUNT: returns the run length and captures the first two dots in (x0, v0),
+// (x1, v1);
 // WRITE: stores the run at oact/octr[d0..] (the entry is known to survive).
 template <bool WRITE, bool HD>
 __device__ __forceinline__ uint32_t fjoin(const FSide& L, const FSide& R, uint32_t A, uint32_t type, uint32_t i,
-                                          uint32_t j, uint32_t& x0, uint64_t& v0, uint32_t* oact, uint64_t* octr,
-                                          uint32_t d0, uint64_t dmask, const Side& DL, const Side& DR) {
+                                          uint32_t j, uint32_t& x0, uint64_t& v0, uint32_t& x1, uint64_t& v1,
+                                          uint32_t* oact, uint64_t* octr, uint32_t d0, uint64_t dmask, const Side& DL,
+                                          const Side& DR) {
   const bool hs = (type & kSelf) != 0u, ho = (type & kOther) != 0u, self_only = type == kSelf;
   const uint32_t ab = ld32(L.b, L.end + 4u * i - 4u), ae_ = ld32(L.b, L.end + 4u * i);
   const uint32_t bb = ld32(R.b, R.end + 4u * j - 4u), be_ = ld32(R.b, R.end + 4u * j);
@@ -643,9 +645,11 @@ __device__ __forceinline__ uint32_t fjoin(const FSide& L, const FSide& R, uint32
         octr[d0 + c] = v;
       }
     } else {
-      const bool first = keep && c == 0u;
+      const bool first = keep && c == 0u, second = keep && c == 1u;
       x0 = first ? x : x0;
       v0 = first ? v : v0;
+      x1 = second ? x : x1;
+      v1 = second ? v : v1;
     }
     c += keep ? 1u : 0u;
   }
@@ -655,17 +659,21 @@ __device__ __forceinline__ uint32_t fjoin(const FSide& L, const FSide& R, uint32
 
 template <bool HD>
 __device__ __forceinline__ void fwrite_member(const FSide& L, const FSide& R, uint32_t A, uint32_t q, uint32_t cnt,
-                                              uint32_t x, uint64_t v, uint32_t midx, uint32_t d0, uint64_t* okey,
-                                              uint32_t* odact, uint64_t* odctr, uint32_t* omdend, uint64_t dmask,
-                                              const Side& DL, const Side& DR) {
+                                              uint32_t x, uint64_t v, uint32_t xb, uint64_t vb, uint32_t midx,
+                                              uint32_t d0, uint64_t* okey, uint32_t* odact, uint64_t* odctr,
+                                              uint32_t* omdend, uint64_t dmask, const Side& DL, const Side& DR) {
   const uint32_t type = q >> 30, i = (q >> 15) & 0x7FFFu, j = q & 0x7FFFu;
   const uint64_t kl = ld64(L.b, L.key + 8u * i), kr = ld64(R.b, R.key + 8u * j);
   okey[midx] = (type & kSelf) ? kl : kr;
-  if (cnt == 1u) {
+  if (cnt <= 2u) {
     odact[d0] = x;
     odctr[d0] = v;
+    if (cnt == 2u) {
+      odact[d0 + 1] = xb;
+      odctr[d0 + 1] = vb;
+    }
   } else {
-    fjoin<true, HD>(L, R, A, type, i, j, x, v, odact, odctr, d0, dmask, DL, DR);
+    fjoin<true, HD>(L, R, A, type, i, j, x, v, xb, vb, odact, odctr, d0, dmask, DL, DR);
   }
   omdend[midx] = d0 + cnt;
 }
@@ -705,33 +713,33 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
   const uint32_t mn = nL < nR ? nL : nR;
   const uint32_t top = mn ? 1u << (31u - __builtin_clz(mn)) : 0u;
   // chunk 0: positions 0..63
-  uint32_t i = 0, j = 0, x0 = 0, c0 = 0, q0 = 0;
-  uint64_t v0 = 0, m0k = 0;
+  uint32_t i = 0, j = 0, x0 = 0, y0 = 0, c0 = 0, q0 = 0;
+  uint64_t v0 = 0, w0 = 0, m0k = 0;
   {
     const uint32_t p = lane < P ? lane : P;
     uint32_t type = fpath(L, R, p, top, i, j);
     type = lane < P ? type : kNone;
     if (HD && type != kNone) m0k = dmask_of(DL, DR, (type & kSelf) ? ld64(Ls, L.key + 8u * i) : ld64(Rs, R.key + 8u * j));
     mark<ABL>(st, 2);
-    if (ABL != 2) c0 = fjoin<false, HD>(L, R, A, type, i, j, x0, v0, nullptr, nullptr, 0u, m0k, DL, DR);
+    if (ABL != 2) c0 = fjoin<false, HD>(L, R, A, type, i, j, x0, v0, y0, w0, nullptr, nullptr, 0u, m0k, DL, DR);
     q0 = (type << 30) | (i << 15) | j;
     mark<ABL>(st, 3);
   }
   // chunk 1: positions 64..127 (P <= 128 on this path)
-  uint32_t x1 = 0, c1 = 0, q1 = 0;
-  uint64_t v1 = 0, m1k = 0;
+  uint32_t x1 = 0, y1 = 0, c1 = 0, q1 = 0;
+  uint64_t v1 = 0, w1 = 0, m1k = 0;
   if (P > (uint32_t)kWave) {
     const uint32_t p = lane + kWave < P ? lane + kWave : P;
     uint32_t type = fpath(L, R, p, top, i, j);
     type = lane + kWave < P ? type : kNone;
     if (HD && type != kNone) m1k = dmask_of(DL, DR, (type & kSelf) ? ld64(Ls, L.key + 8u * i) : ld64(Rs, R.key + 8u * j));
     mark<ABL>(st, 2);
-    if (ABL != 2) c1 = fjoin<false, HD>(L, R, A, type, i, j, x1, v1, nullptr, nullptr, 0u, m1k, DL, DR);
+    if (ABL != 2) c1 = fjoin<false, HD>(L, R, A, type, i, j, x1, v1, y1, w1, nullptr, nullptr, 0u, m1k, DL, DR);
     q1 = (type << 30) | (i << 15) | j;
     mark<ABL>(st, 3);
   }
   if (ABL == 2 || ABL == 3) {  // keep the phase's results live, skip the writes
-    const uint32_t k = q0 + q1 + c0 + c1 + x0 + x1 + (uint32_t)(v0 ^ v1);
+    const uint32_t k = q0 + q1 + c0 + c1 + x0 + x1 + y0 + y1 + (uint32_t)(v0 ^ v1 ^ w0 ^ w1);
     if (__ballot(k == 0x12345u) != 0ull && lane == 0) *(uint32_t*)fo.Og = k;
     if (lane == 0) *(u32x4*)fo.Og = u32x4{nL, nR, 0u, 0u};
     return;
@@ -770,11 +778,11 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
   }
   const uint64_t lt = (1ull << lane) - 1ull;
   if (c0 != 0u)
-    fwrite_member<HD>(L, R, A, q0, c0, x0, v0, (uint32_t)__popcll(k0 & lt), inc0 - c0, okey, odact, odctr, omdend,
-                      m0k, DL, DR);
+    fwrite_member<HD>(L, R, A, q0, c0, x0, v0, y0, w0, (uint32_t)__popcll(k0 & lt), inc0 - c0, okey, odact, odctr,
+                      omdend, m0k, DL, DR);
   if (c1 != 0u)
-    fwrite_member<HD>(L, R, A, q1, c1, x1, v1, m0 + (uint32_t)__popcll(k1 & lt), tot0 + inc1 - c1, okey, odact,
-                      odctr, omdend, m1k, DL, DR);
+    fwrite_member<HD>(L, R, A, q1, c1, x1, v1, y1, w1, m0 + (uint32_t)__popcll(k1 & lt), tot0 + inc1 - c1, okey,
+                      odact, odctr, omdend, m1k, DL, DR);
   if (HD) {
     // deferred union keyed by clock (:141-148), kept iff !(D <= clock) (:197)
     DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
