@@ -698,13 +698,15 @@ struct FOut {
   uint32_t list_cap;
 };
 
+// Returns the output record's size in 16-B pieces (built in fo.Os; the caller
+// copies it to fo.Og later), or 0 if nothing is left to copy.
 template <bool HD, int ABL>
-__device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs, const FOut& fo, uint32_t A,
+__device__ __forceinline__ uint32_t fast_object(const uint8_t* Ls, const uint8_t* Rs, const FOut& fo, uint32_t A,
                                             uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane,
                                             Stamps& st) {
   if (ABL == 1) {
     if (lane == 0) *(u32x4*)fo.Og = u32x4{ld32(Ls, 4), ld32(Rs, 4), nL, nR};
-    return;
+    return 0u;
   }
   const FSide L = fside(Ls, A, nL, dL), R = fside(Rs, A, nR, dR);
   Side DL{Ls, RV{}}, DR{Rs, RV{}};
@@ -742,7 +744,7 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
     const uint32_t k = q0 + q1 + c0 + c1 + x0 + x1 + y0 + y1 + (uint32_t)(v0 ^ v1 ^ w0 ^ w1);
     if (__ballot(k == 0x12345u) != 0ull && lane == 0) *(uint32_t*)fo.Og = k;
     if (lane == 0) *(u32x4*)fo.Og = u32x4{nL, nR, 0u, 0u};
-    return;
+    return 0u;
   }
   const uint32_t inc0 = scan_incl(c0), inc1 = scan_incl(c1);
   const uint64_t k0 = __ballot(c0 != 0u), k1 = __ballot(c1 != 0u);
@@ -762,7 +764,7 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
       const uint32_t e = atomicAdd(&fo.ctl[0], 1u);
       if (e < fo.list_cap) fo.list[e] = fo.obj;
     }
-    return;
+    return 0u;
   }
   uint8_t* O = (uint8_t*)fo.Os;
   uint64_t* okey = (uint64_t*)(O + OL.o_key);
@@ -770,7 +772,7 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
   uint32_t* odact = (uint32_t*)(O + OL.o_dact);
   uint32_t* omdend = (uint32_t*)(O + OL.o_mdend);
 
-  wave_sync();  // the previous object's copy-out has read the stage
+  wave_sync();  // the copy-out of the object that last used this stage has read it
   // top clock: pointwise max (src/orswot.rs:153 -> src/vclock.rs:131-137)
   for (uint32_t a = lane; a < A; a += kWave) {
     const uint64_t x = ld64(Ls, kHdrBytes + 8u * a), y = ld64(Rs, kHdrBytes + 8u * a);
@@ -796,12 +798,15 @@ __device__ __forceinline__ void fast_object(const uint8_t* Ls, const uint8_t* Rs
     h[0] = u32x4{OL.size, A, tot_mem, tot_dot};
     h[1] = u32x4{nd, ndd, ndm, 0u};
   }
-  wave_sync();
   mark<ABL>(st, 5);
-  // copy-out: 16-B coalesced, non-temporal (the output is not re-read here)
-  const uint32_t n16 = OL.size / 16u;
-  for (uint32_t k = lane; k < n16; k += kWave) __builtin_nontemporal_store(fo.Os[k], (u32x4*)fo.Og + k);
-  mark<ABL>(st, 6);
+  return OL.size / 16u;
+}
+
+// Copy an output record from its LDS stage to HBM: 16-B coalesced,
+// non-temporal stores (the output is not re-read by this kernel).
+__device__ __forceinline__ void copy_out(const u32x4* src, uint8_t* dst, uint32_t n16, uint32_t lane) {
+  wave_sync();
+  for (uint32_t k = lane; k < n16; k += kWave) __builtin_nontemporal_store(src[k], (u32x4*)dst + k);
 }
 
 __device__ __forceinline__ void prefetch(u32x4 (&r)[kPer], const uint8_t* src, uint32_t n16, uint32_t lane) {
@@ -827,7 +832,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
     uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
     int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
   __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
-  __shared__ u32x4 out_s[kWavesPerBlock][kOutStage / 16];
+  __shared__ u32x4 out_s[kWavesPerBlock][2][kOutStage / 16];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wave = threadIdx.x / kWave;
   u32x4* const sL = stage_s[wave][0];
@@ -880,6 +885,10 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
     prefetch(pl, Lb + lane_of64(lo, t), nn & 0xFFFFu, lane);
     prefetch(pr, Rb + lane_of64(ro, t), nn >> 16, lane);
     mark<ABL>(st, 7);  // chunk state
+    // output stages alternate; object t-1's copy-out is issued right after
+    // object t is staged, so its stores drain while object t is joined
+    uint32_t par = 0, out_n16 = 0;
+    uint8_t* out_dst = Ob;
     while (pend) {
       t = (uint32_t)__builtin_ctzll(pend);
       pend &= pend - 1;
@@ -889,6 +898,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
       stage(sR, pr, nn >> 16, lane);
       wave_sync();
       mark<ABL>(st, 0);  // wait for the prefetched records + stage them
+      copy_out(out_s[wave][par ^ 1u], out_dst, out_n16, lane);
+      mark<ABL>(st, 6);
       const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
       const uint32_t m = lane_of(nm, t), d = lane_of(nd, t);
       if (pend) {
@@ -898,14 +909,17 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
         prefetch(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
       }
       mark<ABL>(st, 1);  // issue the next prefetch
-      const FOut fo{out_s[wave], Ob + oo, cbase + t, Ooff, ctl, list, list_cap};
+      const FOut fo{out_s[wave][par], Ob + oo, cbase + t, Ooff, ctl, list, list_cap};
       if ((defs >> t) & 1ull)
-        fast_object<true, ABL>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16,
-                               d >> 16, lane, st);
+        out_n16 = fast_object<true, ABL>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, m & 0xFFFFu, d & 0xFFFFu,
+                                         m >> 16, d >> 16, lane, st);
       else
-        fast_object<false, ABL>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16,
-                                d >> 16, lane, st);
+        out_n16 = fast_object<false, ABL>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, m & 0xFFFFu, d & 0xFFFFu,
+                                          m >> 16, d >> 16, lane, st);
+      out_dst = Ob + oo;
+      par ^= 1u;
     }
+    copy_out(out_s[wave][par ^ 1u], out_dst, out_n16, lane);  // drain the chunk's last object
   }
   if (ABL == 9 && lane < 8u) {  // per-wave phase sums -> the context's list buffer
     uint64_t v = 0;
@@ -990,18 +1004,17 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // 101..103 are timing-only ablation builds (invalid output).
   const void* fn;
   switch (variant) {
-    case 5: fn = (const void*)orswot_merge_kernel<5, 0>; break;
-    case 6: fn = (const void*)orswot_merge_kernel<6, 0>; break;
-    case 101: fn = (const void*)orswot_merge_kernel<6, 1>; break;
-    case 102: fn = (const void*)orswot_merge_kernel<6, 2>; break;
-    case 103: fn = (const void*)orswot_merge_kernel<6, 3>; break;
+    case 1: fn = (const void*)orswot_merge_kernel<1, 0>; break;
+    case 101: fn = (const void*)orswot_merge_kernel<5, 1>; break;
+    case 102: fn = (const void*)orswot_merge_kernel<5, 2>; break;
+    case 103: fn = (const void*)orswot_merge_kernel<5, 3>; break;
     case 109: fn = (const void*)orswot_merge_kernel<5, 9>; break;
-    default: fn = (const void*)orswot_merge_kernel<1, 0>; break;
+    default: fn = (const void*)orswot_merge_kernel<5, 0>; break;  // measured best (tools/ab_bench.py)
   }
   // Resident grid: the kernel's occupancy in 4-wave blocks per CU
   // (blocks_per_cu overrides), no more blocks than 64-object chunks need.
   static std::atomic<int> occ_cache[8];  // per variant slot, 0 = not yet queried
-  const int slot = variant == 5 ? 1 : variant == 6 ? 2 : variant >= 101 && variant <= 103 ? variant - 98 : variant == 109 ? 6 : 0;
+  const int slot = variant == 1 ? 1 : variant >= 101 && variant <= 103 ? variant - 98 : variant == 109 ? 6 : 0;
   int occ = occ_cache[slot].load(std::memory_order_relaxed);
   if (occ == 0) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)

@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.join(REPO, "rust-crdt_amd"))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,6")
+    ap.add_argument("--variants", default="0,1")
     ap.add_argument("--bpc", default="8", help="blocks per CU values to sweep")
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--n-obj", type=int, default=1_000_000)
