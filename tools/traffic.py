@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run into profiles/: per-kernel average
+duration (rocprofv3 --kernel-trace --stats) and per-launch HBM traffic from
+the separate FETCH_SIZE / WRITE_SIZE PMC passes, plus the SQ counters.
+
+Corrections (/opt/skills/guides/MI355X_MICROARCH.md, HBM / rocprofv3
+section): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports
+half the bytes of a wide (16 B/lane) coalesced streaming read, so it is
+doubled; WRITE_SIZE reads exactly for 16-B-per-lane streaming stores.
+
+    python tools/traffic.py gpurun_out/prof_r01 profiles/r01
+writes profiles/r01_kernel_stats.csv, profiles/r01_pmc.json and
+profiles/traffic_r01.json (the file bench.py reads for roofline.traffic).
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+KERNELS = {"orswot_merge_kernel": "orswot_merge_kernel<", "orswot_merge_general_kernel": "orswot_merge_general_kernel",
+           "dense_max_kernel": "dense_max_kernel"}
+
+
+def short(name):
+    for k, pat in KERNELS.items():
+        if pat in name:
+            return k
+    return None
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    tag = os.path.basename(dst)
+    os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
+    shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), dst + "_kernel_stats.csv")
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    for d in sorted(os.listdir(src)):
+        f = os.path.join(src, d, "run_counter_collection.csv")
+        if not d.startswith("pmc_") or not os.path.exists(f):
+            continue
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            if k:
+                per[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    pmc = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in per.items()}
+    traffic = {}
+    for k, cs in pmc.items():
+        if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
+            rd = 2.0 * cs["FETCH_SIZE"] * 1024.0
+            wr = cs["WRITE_SIZE"] * 1024.0
+            traffic[k] = {"read_bytes": rd, "write_bytes": wr, "total_bytes": rd + wr,
+                          "note": "per launch; FETCH_SIZE x2 (gfx950 16-B streaming-read correction), KiB->B"}
+    json.dump({"pmc_avg_per_launch": pmc, "source": src}, open(dst + "_pmc.json", "w"), indent=1)
+    tdir = os.path.dirname(dst) or "."
+    json.dump({k: v["total_bytes"] for k, v in traffic.items()} | {"detail": traffic},
+              open(os.path.join(tdir, f"traffic_{tag}.json"), "w"), indent=1)
+    print(json.dumps(traffic, indent=1))
+
+
+if __name__ == "__main__":
+    main()
