@@ -42,6 +42,7 @@ def parse():
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
                    help="measured per-launch HBM bytes (rocprofv3 PMC) to report as roofline.traffic")
     p.add_argument("--blocks-per-cu", type=int, default=None)
+    p.add_argument("--variant", type=int, default=None, help="Orswot kernel variant (tuning/diagnostics)")
     return p.parse_args()
 
 
@@ -112,6 +113,8 @@ def run_orswot(args, rank, world, local):
     eng = crdts_hip.Engine(local)
     if args.blocks_per_cu:
         eng.set_blocks_per_cu(args.blocks_per_cu)
+    if args.variant is not None:
+        eng.set_variant(args.variant)
     L = crdts_hip.OrswotBatch.from_host(lb, lo, 16, device=local)
     R = crdts_hip.OrswotBatch.from_host(rb, ro, 16, device=local)
     out = eng.orswot_alloc_out(L, R)

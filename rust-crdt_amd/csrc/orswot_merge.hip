@@ -528,7 +528,7 @@ __device__ __forceinline__ bool header_ok(u32x4 h0, u32x4 h1, uint64_t off, uint
 // count and the write pass.
 // ======================================================================
 constexpr uint32_t kFastStage = 2048;                 // LDS stage per input record per wave
-constexpr uint32_t kOutStage = 2048;                  // LDS stage for the output record per wave
+constexpr uint32_t kOutStage = 3072;                  // LDS stage for the output record per wave (4 blocks/CU at 40 KB)
 constexpr uint32_t kPer = kFastStage / 16 / kWave;    // 16-B pieces per lane per record
 constexpr uint64_t kPending = 1ull << 63;             // Ooff flag: object left for the general kernel
 
@@ -700,7 +700,9 @@ struct FOut {
 
 // Returns the output record's size in 16-B pieces (built in fo.Os; the caller
 // copies it to fo.Og later), or 0 if nothing is left to copy.
-template <bool HD, int ABL>
+// OUTCAP: bytes of the output stage. GEN (general kernel): an output larger
+// than the stage returns ~0u instead of flagging the object.
+template <bool HD, int ABL, uint32_t OUTCAP = kOutStage, bool GEN = false>
 __device__ __forceinline__ uint32_t fast_object(const uint8_t* Ls, const uint8_t* Rs, const FOut& fo, uint32_t A,
                                             uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane,
                                             Stamps& st) {
@@ -758,7 +760,8 @@ __device__ __forceinline__ uint32_t fast_object(const uint8_t* Ls, const uint8_t
   RecLayout OL;
   rec_layout(OL, A, tot_mem, tot_dot, nd, ndd, ndm);
   mark<ABL>(st, 4);
-  if (OL.size > kOutStage) {  // rare: let the general kernel write it
+  if (OL.size > OUTCAP) {  // rare: let the general kernel write it
+    if (GEN) return ~0u;
     if (lane == 0u) {
       fo.Ooff[fo.obj] |= kPending;
       const uint32_t e = atomicAdd(&fo.ctl[0], 1u);
@@ -802,6 +805,206 @@ __device__ __forceinline__ uint32_t fast_object(const uint8_t* Ls, const uint8_t
   return OL.size / 16u;
 }
 
+
+// ======================================================================
+// Lean path (v5): objects without deferred removes whose union has at most
+// 64 members and nL + nR <= 128 — ~93 % of config 3. Same rules as
+// fast_object / merge_object, restructured for VALU economy:
+//  1. merge path over the diagonal 2*lane only; the lane then settles union
+//     positions 2*lane and 2*lane+1 with one extra compare (no second
+//     64-position round for nL + nR > 64);
+//  2. the (up to 2) union members per lane are compacted through LDS so that
+//     lane u owns union member u (twins of keys present on both sides vanish);
+//  3. one dot-parallel pass precomputes, for every dot, whether it is above
+//     the OTHER side's pre-merge top clock (L[x] > Rc[x], R[x] > Lc[x]) and
+//     keeps it in bit 31 of the staged actor id — the join loop then reads
+//     no top clock at all;
+//  4. the per-member join loop (src/orswot.rs:94-138) is branch-free per
+//     step and captures the first two output dots in registers.
+// Returns the output size in 16-B pieces, or kLeanFallback when the union
+// has more than 64 members (the caller then runs fast_object on the
+// untouched stage).
+// ======================================================================
+constexpr uint32_t kLeanFallback = 0xFFFFFFFFu;
+constexpr uint32_t kFlag = 0x80000000u;
+
+template <bool WRITE>
+__device__ __forceinline__ uint32_t lean_join(const uint8_t* Ls, const uint8_t* Rs, uint32_t actL, uint32_t ctrL,
+                                              uint32_t actR, uint32_t ctrR, uint32_t a, uint32_t ae, uint32_t b,
+                                              uint32_t be, bool self_only, uint32_t& x0, uint64_t& v0, uint32_t& x1,
+                                              uint64_t& v1, uint32_t* oact, uint64_t* octr, uint32_t d0) {
+  uint32_t c = 0;
+  bool any = false;
+  while (a < ae || b < be) {
+    const uint32_t xa2 = ld32(Ls, actL + 4u * a), xb2 = ld32(Rs, actR + 4u * b);
+    const uint64_t va = ld64(Ls, ctrL + 8u * a), vb = ld64(Rs, ctrR + 8u * b);
+    const uint32_t xa = a < ae ? (xa2 & ~kFlag) : 0xFFFFFFFFu;
+    const uint32_t xb = b < be ? (xb2 & ~kFlag) : 0xFFFFFFFFu;
+    const bool ta = xa <= xb, tb = xb <= xa;
+    const bool fa = (int32_t)xa2 < 0, fb = (int32_t)xb2 < 0;
+    // both present and equal: common dot (:109); else L[x] survives iff
+    // > Rc[x] (self-only: the whole run, :98-103), R[x] iff > Lc[x]; max.
+    const bool lp = ta && (self_only || fa), rp = tb && fb;
+    const bool useA = (ta && tb && va == vb) || (lp && (!rp || va >= vb));
+    const bool keep = useA || rp;
+    const uint64_t v = useA ? va : vb;
+    const uint32_t x = ta ? xa : xb;
+    any = any || (ta && fa);
+    if (WRITE) {
+      if (keep) {
+        oact[d0 + c] = x;
+        octr[d0 + c] = v;
+      }
+    } else {
+      const bool first = keep && c == 0u, second = keep && c == 1u;
+      x0 = first ? x : x0;
+      v0 = first ? v : v0;
+      x1 = second ? x : x1;
+      v1 = second ? v : v1;
+    }
+    c += keep ? 1u : 0u;
+    a += ta ? 1u : 0u;
+    b += tb ? 1u : 0u;
+  }
+  return (self_only && !any) ? 0u : c;  // self-only entry dropped as a whole (:98-100)
+}
+
+// Marks bit 31 of every staged actor id of side S whose dot is above the
+// other side's top clock T (absent or out-of-range actor: 0).
+__device__ __forceinline__ void lean_flags(uint8_t* S, const uint8_t* T, uint32_t act, uint32_t ctr, uint32_t nd,
+                                           uint32_t A, uint32_t lane) {
+  for (uint32_t d = lane; d < nd; d += kWave) {
+    const uint32_t x = ld32(S, act + 4u * d);
+    const uint64_t v = ld64(S, ctr + 8u * d);
+    const uint64_t t = ld64(T, kHdrBytes + 8u * (x < A ? x : 0u));
+    const bool up = v > (x < A ? t : 0ull);
+    *(uint32_t*)(S + act + 4u * d) = x | (up ? kFlag : 0u);
+  }
+}
+
+// LABL (timing-only ablations, invalid output): 1 = stop after the merge
+// path + compaction, 2 = + dot flags, 3 = + counting join; 0 = real.
+template <uint32_t OUTCAP, int LABL = 0>
+__device__ __forceinline__ uint32_t lean_object(uint8_t* Ls, uint8_t* Rs, u32x4* Os, uint32_t A, uint32_t nL,
+                                                uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane, bool& big) {
+  big = false;
+  const uint32_t key = kHdrBytes + 8u * A;  // key section, both sides
+  const uint32_t ctrL = key + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
+  const uint32_t ctrR = key + 8u * nR, actR = ctrR + 8u * dR, endR = actR + 4u * dR;
+  const uint32_t P = nL + nR;
+  const uint32_t mn = nL < nR ? nL : nR;
+  const uint32_t top = mn ? 1u << (31u - __builtin_clz(mn)) : 0u;
+
+  // ---- 1. merge path on diagonal p = 2*lane (self first on ties)
+  const uint32_t p = 2u * lane < P ? 2u * lane : P;
+  const uint32_t lo = p > nR ? p - nR : 0u, hi = p < nL ? p : nL;
+  uint32_t i = lo;
+  for (uint32_t step = top; step != 0u; step >>= 1) {
+    const uint32_t cand = i + step;
+    const uint64_t kl = ld64(Ls, key + 8u * cand - 8u), kr = ld64(Rs, key + 8u * (p - cand));
+    i = (cand <= hi && kl <= kr) ? cand : i;
+  }
+  const uint32_t j = p - i;
+  const uint64_t kLm = ld64(Ls, key + 8u * i - 8u), kL0 = ld64(Ls, key + 8u * i), kL1 = ld64(Ls, key + 8u * i + 8u);
+  const uint64_t kR0 = ld64(Rs, key + 8u * j), kR1 = ld64(Rs, key + 8u * j + 8u);
+  // position p
+  const bool hl0 = i < nL, hr0 = j < nR;
+  const bool tl0 = hl0 && (!hr0 || kL0 <= kR0);
+  const uint32_t ty0 = tl0 ? ((hr0 && kL0 == kR0) ? kBoth : kSelf) : ((i > 0u && kLm == kR0) ? kNone : kOther);
+  // position p + 1
+  const uint32_t i1 = tl0 ? i + 1u : i, j1 = tl0 ? j : j + 1u;
+  const uint64_t kLa = tl0 ? kL1 : kL0, kLb = tl0 ? kL0 : kLm, kRa = tl0 ? kR0 : kR1;
+  const bool hl1 = i1 < nL, hr1 = j1 < nR;
+  const bool tl1 = hl1 && (!hr1 || kLa <= kRa);
+  const uint32_t ty1 = tl1 ? ((hr1 && kLa == kRa) ? kBoth : kSelf) : ((i1 > 0u && kLb == kRa) ? kNone : kOther);
+  const bool u0 = p < P && ty0 != kNone, u1 = p + 1u < P && ty1 != kNone;
+
+  // ---- 2. compact union members: lane u <- union member u
+  const uint32_t nu = (u0 ? 1u : 0u) + (u1 ? 1u : 0u);
+  const uint32_t incl = scan_incl(nu);
+  const uint32_t U = lane_of(incl, kWave - 1);
+  if (U > (uint32_t)kWave) return kLeanFallback;
+  uint32_t* desc = (uint32_t*)Os;
+  wave_sync();  // the copy-out that last read this stage is done with it
+  if (u0) desc[incl - nu] = (ty0 << 30) | (i << 15) | j;
+  if (u1) desc[incl - 1u] = (ty1 << 30) | (i1 << 15) | j1;
+  if (LABL == 1) return 0u;
+  // ---- 3. dots above the other side's top clock -> bit 31 of the actor id
+  lean_flags(Ls, Rs, actL, ctrL, dL, A, lane);
+  lean_flags(Rs, Ls, actR, ctrR, dR, A, lane);
+  wave_sync();
+  const uint32_t dsc = lane < U ? desc[lane] : 0u;
+  if (LABL == 2) {
+    if (__ballot(dsc == 0x12345u) != 0ull) *(uint32_t*)Os = dsc;
+    return 0u;
+  }
+
+  // ---- 4. join of union member `lane`
+  const uint32_t ty = dsc >> 30, mi = (dsc >> 15) & 0x7FFFu, mj = dsc & 0x7FFFu;
+  const uint32_t ab = ld32(Ls, endL + 4u * mi - 4u), ae_ = ld32(Ls, endL + 4u * mi);
+  const uint32_t bb = ld32(Rs, endR + 4u * mj - 4u), be_ = ld32(Rs, endR + 4u * mj);
+  const bool hs = (ty & kSelf) != 0u, ho = (ty & kOther) != 0u;
+  // run bounds, clamped to the dot counts (a malformed record cannot spin the loop)
+  const uint32_t ae = hs ? (ae_ < dL ? ae_ : dL) : 0u, be = ho ? (be_ < dR ? be_ : dR) : 0u;
+  const uint32_t a0 = hs && mi ? (ab < ae ? ab : ae) : 0u, b0 = ho && mj ? (bb < be ? bb : be) : 0u;
+  const bool self_only = ty == kSelf;
+  uint32_t x0 = 0, x1 = 0;
+  uint64_t v0 = 0, v1 = 0;
+  const uint32_t c = lean_join<false>(Ls, Rs, actL, ctrL, actR, ctrR, a0, ae, b0, be, self_only, x0, v0, x1, v1,
+                                      nullptr, nullptr, 0u);
+
+  if (LABL == 3) {
+    if (__ballot((c + x0 + x1 + (uint32_t)(v0 ^ v1)) == 0x12345u) != 0ull) *(uint32_t*)Os = c;
+    return 0u;
+  }
+  // ---- 5. output layout (no deferred block)
+  const uint64_t keepm = __ballot(c != 0u);
+  const uint32_t tot_mem = (uint32_t)__popcll(keepm);
+  const uint32_t cincl = scan_incl(c);
+  const uint32_t tot_dot = lane_of(cincl, kWave - 1);
+  const uint32_t o_key = kHdrBytes + 8u * A;
+  const uint32_t o_dctr = o_key + 8u * tot_mem, o_dact = o_dctr + 8u * tot_dot, o_mdend = o_dact + 4u * tot_dot;
+  const uint32_t o_mpad = o_mdend + 4u * tot_mem;
+  const uint32_t size = (((o_mpad + 7u) & ~7u) + 15u) & ~15u;
+  if (size > OUTCAP) {
+    big = true;
+    return 0u;
+  }
+  uint8_t* O = (uint8_t*)Os;
+  wave_sync();  // every lane has read its descriptor
+  // top clock: pointwise max (src/orswot.rs:153 -> src/vclock.rs:131-137)
+  for (uint32_t x = lane; x < A; x += kWave) {
+    const uint64_t l = ld64(Ls, kHdrBytes + 8u * x), r = ld64(Rs, kHdrBytes + 8u * x);
+    *(uint64_t*)(O + kHdrBytes + 8u * x) = l > r ? l : r;
+  }
+  if (c != 0u) {
+    const uint32_t midx = (uint32_t)__popcll(keepm & ((1ull << lane) - 1ull));
+    const uint32_t d0 = cincl - c;
+    const uint8_t* kb = hs ? Ls + key + 8u * mi : Rs + key + 8u * mj;
+    *(uint64_t*)(O + o_key + 8u * midx) = *(const uint64_t*)kb;
+    uint32_t* oact = (uint32_t*)(O + o_dact);
+    uint64_t* octr = (uint64_t*)(O + o_dctr);
+    if (c <= 2u) {
+      oact[d0] = x0;
+      octr[d0] = v0;
+      if (c == 2u) {
+        oact[d0 + 1u] = x1;
+        octr[d0 + 1u] = v1;
+      }
+    } else {
+      lean_join<true>(Ls, Rs, actL, ctrL, actR, ctrR, a0, ae, b0, be, self_only, x0, v0, x1, v1, oact, octr, d0);
+    }
+    *(uint32_t*)(O + o_mdend + 4u * midx) = d0 + c;
+  }
+  if (lane == 0u) {
+    for (uint32_t q = o_mpad; q < size; q += 4u) *(uint32_t*)(O + q) = 0u;
+    u32x4* h = (u32x4*)O;
+    h[0] = u32x4{size, A, tot_mem, tot_dot};
+    h[1] = u32x4{0u, 0u, 0u, 0u};
+  }
+  return size / 16u;
+}
+
 // Copy an output record from its LDS stage to HBM: 16-B coalesced,
 // non-temporal stores (the output is not re-read by this kernel).
 __device__ __forceinline__ void copy_out(const u32x4* src, uint8_t* dst, uint32_t n16, uint32_t lane) {
@@ -825,7 +1028,7 @@ __device__ __forceinline__ void stage(u32x4* dst, const u32x4 (&r)[kPer], uint32
   }
 }
 
-template <int MINW, int ABL>
+template <int MINW, int ABL, bool LEAN = false, int LABL = 0>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
@@ -910,12 +1113,28 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
       }
       mark<ABL>(st, 1);  // issue the next prefetch
       const FOut fo{out_s[wave][par], Ob + oo, cbase + t, Ooff, ctl, list, list_cap};
-      if ((defs >> t) & 1ull)
+      if ((defs >> t) & 1ull) {
         out_n16 = fast_object<true, ABL>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, m & 0xFFFFu, d & 0xFFFFu,
                                          m >> 16, d >> 16, lane, st);
-      else
-        out_n16 = fast_object<false, ABL>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, m & 0xFFFFu, d & 0xFFFFu,
-                                          m >> 16, d >> 16, lane, st);
+      } else {
+        out_n16 = kLeanFallback;
+        if (LEAN) {
+          bool big;
+          out_n16 = lean_object<kOutStage, LABL>((uint8_t*)sL, (uint8_t*)sR, out_s[wave][par], A, m & 0xFFFFu,
+                                           d & 0xFFFFu, m >> 16, d >> 16, lane, big);
+          if (big) {  // rare: output larger than the stage -> general kernel
+            if (lane == 0u) {
+              Ooff[cbase + t] |= kPending;
+              const uint32_t e = atomicAdd(&ctl[0], 1u);
+              if (e < list_cap) list[e] = cbase + t;
+            }
+            out_n16 = 0u;
+          }
+        }
+        if (out_n16 == kLeanFallback)
+          out_n16 = fast_object<false, ABL>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, m & 0xFFFFu,
+                                            d & 0xFFFFu, m >> 16, d >> 16, lane, st);
+      }
       out_dst = Ob + oo;
       par ^= 1u;
     }
@@ -935,25 +1154,43 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
 // kernel appends them to a list; a small fixed grid of single-wave blocks
 // joins each one, staged through LDS when both records fit kGenStage, else
 // straight from HBM, and clears its flag. If the list overflowed, the blocks
-// scan every output offset for flags instead. The last block to finish
-// (atomic ticket) resets the list for the next launch on this context.
+// scan every output offset for flags instead. The list counter is cleared by
+// an async memset queued before the fast kernel (no finishing-block ticket:
+// 512 same-address atomics serialised at the memory side cost ~50 us).
 // ======================================================================
 constexpr uint32_t kGenStage = 8192;
 constexpr uint32_t kGenBlocks = 512;
 
 __device__ __forceinline__ void general_one(const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb,
                                             const uint64_t* Roff, uint8_t* Ob, uint64_t* Ooff, uint64_t o, uint32_t A,
-                                            u32x4* sl, u32x4* sr, uint32_t lane) {
+                                            u32x4* sl, u32x4* sr, u32x4* so, uint32_t lane) {
   const uint64_t oo = Ooff[o] & ~kPending;
   const uint8_t* lr = Lb + Loff[o];
   const uint8_t* rr = Rb + Roff[o];
-  const uint32_t szl = uni(*(const uint32_t*)lr), szr = uni(*(const uint32_t*)rr);
+  const u32x4 hl0 = ((const u32x4*)lr)[0], hl1 = ((const u32x4*)lr)[1];
+  const u32x4 hr0 = ((const u32x4*)rr)[0], hr1 = ((const u32x4*)rr)[1];
+  const uint32_t szl = uni(hl0.x), szr = uni(hr0.x);
   if (szl <= kGenStage && szr <= kGenStage) {
     wave_sync();
     for (uint32_t k = lane; k < szl / 16; k += kWave) sl[k] = ((const u32x4*)lr)[k];
     for (uint32_t k = lane; k < szr / 16; k += kWave) sr[k] = ((const u32x4*)rr)[k];
     wave_sync();
-    merge_object((const uint8_t*)sl, (const uint8_t*)sr, Ob + oo, A, lane);
+    // the fast path's join when its limits hold (union positions, deferred
+    // clocks per side), with the general kernel's larger stages
+    uint32_t n16 = ~0u;
+    const uint32_t nL = uni(hl0.z), nR = uni(hr0.z), dL = uni(hl0.w), dR = uni(hr0.w);
+    if (nL + nR <= 2u * kWave && uni(hl1.x) <= 32u && uni(hr1.x) <= 32u) {
+      const FOut fo{so, Ob + oo, o, Ooff, nullptr, nullptr, 0u};
+      Stamps st{};
+      if ((uni(hl1.x) | uni(hr1.x)) != 0u)
+        n16 = fast_object<true, 0, kGenStage, true>((const uint8_t*)sl, (const uint8_t*)sr, fo, A, nL, dL, nR, dR,
+                                                    lane, st);
+      else
+        n16 = fast_object<false, 0, kGenStage, true>((const uint8_t*)sl, (const uint8_t*)sr, fo, A, nL, dL, nR, dR,
+                                                     lane, st);
+    }
+    if (n16 != ~0u) copy_out(so, Ob + oo, n16, lane);
+    else merge_object((const uint8_t*)sl, (const uint8_t*)sr, Ob + oo, A, lane);
   } else {
     merge_object(lr, rr, Ob + oo, A, lane);
   }
@@ -964,12 +1201,12 @@ __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, const uint8_t* __restrict__ Rb,
     const uint64_t* __restrict__ Roff, uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t n_obj,
     uint32_t A, uint32_t* __restrict__ ctl, const uint64_t* __restrict__ list, uint32_t list_cap) {
-  __shared__ u32x4 gen_s[2][kGenStage / 16];
+  __shared__ u32x4 gen_s[3][kGenStage / 16];
   const uint32_t lane = threadIdx.x;
   const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (n <= list_cap) {
     for (uint32_t e = blockIdx.x; e < n; e += gridDim.x)
-      general_one(Lb, Loff, Rb, Roff, Ob, Ooff, list[e], A, gen_s[0], gen_s[1], lane);
+      general_one(Lb, Loff, Rb, Roff, Ob, Ooff, list[e], A, gen_s[0], gen_s[1], gen_s[2], lane);
   } else {
     const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
     for (uint64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
@@ -977,15 +1214,7 @@ __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
       const uint64_t oo = obj < n_obj ? Ooff[obj] : 0ull;
       for (uint64_t pend = __ballot((oo & kPending) != 0ull); pend; pend &= pend - 1)
         general_one(Lb, Loff, Rb, Roff, Ob, Ooff, chunk * kWave + (uint32_t)__builtin_ctzll(pend), A, gen_s[0],
-                    gen_s[1], lane);
-    }
-  }
-  if (lane == 0) {
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    const uint32_t ticket = atomicAdd(&ctl[1], 1u);
-    if (ticket == gridDim.x - 1) {  // every block has read ctl[0]
-      __hip_atomic_store(&ctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    gen_s[1], gen_s[2], lane);
     }
   }
 }
@@ -1004,17 +1233,25 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // 101..103 are timing-only ablation builds (invalid output).
   const void* fn;
   switch (variant) {
-    case 1: fn = (const void*)orswot_merge_kernel<1, 0>; break;
+    case 6: fn = (const void*)orswot_merge_kernel<1, 0, true>; break;
+    case 111: fn = (const void*)orswot_merge_kernel<1, 0, true, 1>; break;
+    case 112: fn = (const void*)orswot_merge_kernel<1, 0, true, 2>; break;
+    case 113: fn = (const void*)orswot_merge_kernel<1, 0, true, 3>; break;
+    case 2: fn = (const void*)orswot_merge_kernel<2, 0>; break;
+    case 3: fn = (const void*)orswot_merge_kernel<3, 0>; break;
+    case 4: fn = (const void*)orswot_merge_kernel<4, 0>; break;
+    case 5: fn = (const void*)orswot_merge_kernel<5, 0>; break;
     case 101: fn = (const void*)orswot_merge_kernel<5, 1>; break;
     case 102: fn = (const void*)orswot_merge_kernel<5, 2>; break;
     case 103: fn = (const void*)orswot_merge_kernel<5, 3>; break;
     case 109: fn = (const void*)orswot_merge_kernel<5, 9>; break;
-    default: fn = (const void*)orswot_merge_kernel<5, 0>; break;  // measured best (tools/ab_bench.py)
+    default: fn = (const void*)orswot_merge_kernel<1, 0>; break;  // measured best (tools/ab_bench.py)
   }
   // Resident grid: the kernel's occupancy in 4-wave blocks per CU
   // (blocks_per_cu overrides), no more blocks than 64-object chunks need.
-  static std::atomic<int> occ_cache[8];  // per variant slot, 0 = not yet queried
-  const int slot = variant == 1 ? 1 : variant >= 101 && variant <= 103 ? variant - 98 : variant == 109 ? 6 : 0;
+  static std::atomic<int> occ_cache[16];  // per variant slot, 0 = not yet queried
+  const int slot = variant >= 1 && variant <= 6 ? variant : variant >= 101 && variant <= 103 ? variant - 95
+                   : variant == 109 ? 9 : variant >= 111 && variant <= 113 ? variant - 99 : 0;
   int occ = occ_cache[slot].load(std::memory_order_relaxed);
   if (occ == 0) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)
@@ -1027,6 +1264,7 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
   void* args[] = {&Lb, &Loff, &Lbytes, &Rb, &Roff, &Rbytes, &Ob, &Ooff, &Obytes, &n_obj, &n_actors, &status,
                   &ctl, &list, &list_cap};
+  if (hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
   if (hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) != hipSuccess)
     return CRDT_EHIP;
   hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
