@@ -114,6 +114,14 @@ int crdt_pncounter_merge(crdt_ctx* ctx, uint64_t* d_self, const uint64_t* d_othe
  *   u32 def_dend[n_def]      cumulative end of deferred clock d's dots
  *   u32 def_mend[n_def]      cumulative end of deferred clock d's member keys
  *   (pad to 16)
+ * SPARSE (CSR) top clock — header flags bit 0 (CRDT_ORSWOT_SPARSE_CLOCK), for
+ * large actor universes (BASELINE.json configs[4]): the
+ * top-clock section is instead
+ *   u64 clk_ctr [n_clk]      counters of the clock's n_clk = nnz actors
+ *   u32 clk_act [n_clk]      their actor ids, strictly increasing, < n_actors
+ *   (pad to 8)
+ * and everything after it is unchanged. A batch is either all dense (flags 0,
+ * n_clk == n_actors) or all sparse (flags 1, counters > 0).
  * Canonical: every counter stored in a run is > 0, every member clock, every
  * deferred clock and every deferred member set is non-empty, and deferred
  * clocks are strictly increasing in CLOCK ORDER = lexicographic order of their
@@ -127,8 +135,10 @@ typedef struct crdt_orswot_hdr {
   uint32_t n_def;
   uint32_t n_def_dot;
   uint32_t n_def_mem;
-  uint32_t flags;     /* must be 0 in ABI v1                              */
+  uint32_t flags;     /* 0 (dense top clock) or CRDT_ORSWOT_SPARSE_CLOCK  */
 } crdt_orswot_hdr;
+
+#define CRDT_ORSWOT_SPARSE_CLOCK 1u
 
 #define CRDT_ORSWOT_HDR_BYTES 32u
 #define CRDT_RECORD_ALIGN 16u
@@ -136,6 +146,10 @@ typedef struct crdt_orswot_hdr {
 /* Bytes of a record with these counts (header and padding included). */
 size_t crdt_orswot_record_bytes(uint32_t n_clk, uint32_t n_mem, uint32_t n_dot,
                                 uint32_t n_def, uint32_t n_def_dot, uint32_t n_def_mem);
+/* Same for either clock form (flags: 0 or CRDT_ORSWOT_SPARSE_CLOCK). */
+size_t crdt_orswot_record_bytes_ex(uint32_t n_clk, uint32_t n_mem, uint32_t n_dot,
+                                   uint32_t n_def, uint32_t n_def_dot, uint32_t n_def_mem,
+                                   uint32_t flags);
 
 /* A batch of records: record i starts at d_base + d_off[i] (16-B aligned). */
 typedef struct crdt_orswot_batch {
@@ -162,6 +176,15 @@ int crdt_orswot_merge(crdt_ctx* ctx, const crdt_orswot_batch* self,
                       uint64_t* d_out_off, size_t out_bytes, uint32_t n_actors,
                       void* stream);
 
+/* crdt_orswot_merge for either clock form: flags = 0 (dense top clocks,
+ * n_actors slots) or CRDT_ORSWOT_SPARSE_CLOCK (CSR top clocks over an actor
+ * universe of n_actors ids; the output records are sparse too). Same output
+ * placement and bounds. */
+int crdt_orswot_merge_ex(crdt_ctx* ctx, const crdt_orswot_batch* self,
+                         const crdt_orswot_batch* other, uint8_t* d_out_base,
+                         uint64_t* d_out_off, size_t out_bytes, uint32_t n_actors,
+                         uint32_t flags, void* stream);
+
 /* Same with host buffers: H2D, merge, D2H, synchronous (PCIe-inclusive path
  * used by a host `merge_batch(&mut [T], &[T])`). h_out_off receives offsets
  * into h_out_base (compacted, so h_out_bytes >= sum of merged record sizes
@@ -177,6 +200,8 @@ int crdt_orswot_merge_host(crdt_ctx* ctx, const uint8_t* h_self_base,
  * counters, non-empty runs, section sizes). Result via crdt_ctx_status. */
 int crdt_orswot_validate(crdt_ctx* ctx, const crdt_orswot_batch* batch,
                          uint32_t n_actors, void* stream);
+int crdt_orswot_validate_ex(crdt_ctx* ctx, const crdt_orswot_batch* batch,
+                            uint32_t n_actors, uint32_t flags, void* stream);
 
 /* Remove gaps: copies records into d_dst contiguously; d_dst_off receives the
  * new offsets. d_scratch needs crdt_orswot_compact_scratch_bytes(n_obj). */
@@ -218,10 +243,34 @@ typedef struct crdt_orswot_gen crdt_orswot_gen;
 int crdt_orswot_generate(uint64_t seed, size_t first_obj, size_t n_obj,
                          const crdt_orswot_gen_params* params, int n_threads,
                          crdt_orswot_gen** out);
-/* side 0 = self (L), 1 = other (R): host base, u64 offsets (n_obj), bytes. */
+/* side 0 = self (L), 1 = other (R) (or replica r): host base, u64 offsets (n_obj), bytes. */
 int crdt_orswot_gen_side(const crdt_orswot_gen* g, int side, const uint8_t** h_base,
                          const uint64_t** h_off, size_t* bytes);
 void crdt_orswot_gen_free(crdt_orswot_gen* g);
+
+/* Replica sets for anti-entropy (config 5): per object, a shared ancestor of
+ * `ancestor_adds` adds by actors of a per-object pool of `pool_actors` ids
+ * drawn from [0, universe); each of the n_replicas replicas then applies
+ * min..max divergent ops with its own `own_actors` ids (adds pct_add %,
+ * read-context removes, and in pct_deferred_obj % of objects pct_future_rm %
+ * removes whose context is advanced on another replica's actor, which
+ * defer). Side r of the result (crdt_orswot_gen_side) is replica r. flags:
+ * CRDT_ORSWOT_SPARSE_CLOCK encodes CSR top clocks (else dense, universe wide). */
+typedef struct crdt_orswot_rep_params {
+  uint32_t universe;         /* actor id universe (config 5: 1024)            */
+  uint32_t pool_actors;      /* ancestor actors per object (48)               */
+  uint32_t own_actors;       /* actors per replica per object (2)             */
+  uint32_t member_universe;  /* (64)                                          */
+  uint32_t ancestor_adds;    /* (48)                                          */
+  uint32_t min_div_ops;      /* (4)                                           */
+  uint32_t max_div_ops;      /* (16)                                          */
+  uint32_t pct_add;          /* (60)                                          */
+  uint32_t pct_future_rm;    /* (10)                                          */
+  uint32_t pct_deferred_obj; /* (8)                                           */
+} crdt_orswot_rep_params;
+int crdt_orswot_generate_replicas(uint64_t seed, size_t first_obj, size_t n_obj,
+                                  const crdt_orswot_rep_params* params, uint32_t n_replicas,
+                                  uint32_t flags, int n_threads, crdt_orswot_gen** out);
 
 /* Dense synthetic counters: u64[n_obj][n_actors] rows for objects
  * [first_obj, first_obj+n_obj), counter U[0, 2^bits) with `pct_zero` % zeros. */
@@ -244,6 +293,9 @@ int crdt_host_orswot_apply_rm(crdt_host_orswot* o, uint64_t member, const uint32
 /* Encode into h_rec (capacity cap); returns bytes written or a negative code. */
 long crdt_host_orswot_encode(const crdt_host_orswot* o, uint32_t n_actors, uint8_t* h_rec,
                              size_t cap);
+/* flags: 0 (dense, n_actors slots) or CRDT_ORSWOT_SPARSE_CLOCK (CSR top clock). */
+long crdt_host_orswot_encode_ex(const crdt_host_orswot* o, uint32_t n_actors, uint32_t flags,
+                                uint8_t* h_rec, size_t cap);
 crdt_host_orswot* crdt_host_orswot_decode(const uint8_t* h_rec, size_t bytes);
 
 #ifdef __cplusplus

@@ -217,9 +217,10 @@ struct PNCounter {
 // ------------------------------------------------- canonical record codec
 static inline size_t pad16(size_t x) { return (x + 15) & ~size_t(15); }
 
+// sparse: CSR top clock (header flags bit 0): u64 ctr[n_clk], u32 act[n_clk], pad 8.
 size_t record_bytes(uint32_t n_clk, uint32_t n_mem, uint32_t n_dot, uint32_t n_def,
-                    uint32_t n_def_dot, uint32_t n_def_mem) {
-  size_t b = CRDT_ORSWOT_HDR_BYTES + 8ull * n_clk;
+                    uint32_t n_def_dot, uint32_t n_def_mem, bool sparse = false) {
+  size_t b = CRDT_ORSWOT_HDR_BYTES + (sparse ? ((12ull * n_clk + 7) & ~size_t(7)) : 8ull * n_clk);
   b += 12ull * ((size_t)n_mem + n_dot);                 // member block
   b = (b + 7) & ~size_t(7);
   b += 12ull * n_def_dot + 8ull * n_def_mem + 8ull * n_def;  // deferred block
@@ -229,12 +230,15 @@ size_t record_bytes(uint32_t n_clk, uint32_t n_mem, uint32_t n_dot, uint32_t n_d
 // Section pointers of a record (layout: include/crdts_hip.h).
 struct Sections {
   uint64_t *clk, *key, *dctr, *fctr, *fkey;
-  uint32_t *dact, *mdend, *fact, *fdend, *fmend;
+  uint32_t *cact, *dact, *mdend, *fact, *fdend, *fmend;
 };
 static Sections sections(uint8_t* rec, const crdt_orswot_hdr& h) {
   Sections s;
+  const bool sparse = (h.flags & CRDT_ORSWOT_SPARSE_CLOCK) != 0;
   s.clk = (uint64_t*)(rec + CRDT_ORSWOT_HDR_BYTES);
-  s.key = s.clk + h.n_clk;
+  s.cact = (uint32_t*)(s.clk + h.n_clk);
+  s.key = sparse ? (uint64_t*)(rec + CRDT_ORSWOT_HDR_BYTES + ((12ull * h.n_clk + 7) & ~size_t(7)))
+                 : s.clk + h.n_clk;
   s.dctr = s.key + h.n_mem;
   s.dact = (uint32_t*)(s.dctr + h.n_dot);
   s.mdend = s.dact + h.n_dot;
@@ -258,8 +262,9 @@ static bool clock_less(const VClock& a, const VClock& b) {
   return ia == a.dots.end() && ib != b.dots.end();
 }
 
-// Encode; returns bytes or negative code. Dense clock of n_actors slots.
-long encode(const Orswot& o, uint32_t n_actors, uint8_t* out, size_t cap) {
+// Encode; returns bytes or negative code. Dense clock of n_actors slots, or
+// (sparse) the clock's nnz actors as CSR.
+long encode(const Orswot& o, uint32_t n_actors, uint8_t* out, size_t cap, bool sparse = false) {
   std::vector<std::pair<Member, const VClock*>> ents;
   for (const auto& kv : o.entries) ents.emplace_back(kv.first, &kv.second);
   std::sort(ents.begin(), ents.end(),
@@ -289,15 +294,22 @@ long encode(const Orswot& o, uint32_t n_actors, uint8_t* out, size_t cap) {
   for (auto& d : defs)
     for (auto& kv : d.first->dots)
       if (kv.first >= n_actors) return CRDT_EINVAL;
-  size_t bytes = record_bytes(n_actors, n_mem, n_dot, n_def, n_def_dot, n_def_mem);
+  const uint32_t n_clk = sparse ? (uint32_t)o.clock.dots.size() : n_actors;
+  size_t bytes = record_bytes(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem, sparse);
   if (bytes > cap) return CRDT_ECAPACITY;
   std::memset(out, 0, bytes);
-  crdt_orswot_hdr h = {(uint32_t)bytes, n_actors, n_mem, n_dot, n_def, n_def_dot, n_def_mem, 0};
+  crdt_orswot_hdr h = {(uint32_t)bytes, n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem,
+                       sparse ? CRDT_ORSWOT_SPARSE_CLOCK : 0u};
   std::memcpy(out, &h, sizeof h);
   Sections S = sections(out, h);
   uint64_t *clk = S.clk, *key = S.key, *dctr = S.dctr, *fctr = S.fctr, *fkey = S.fkey;
   uint32_t *dact = S.dact, *mdend = S.mdend, *fact = S.fact, *fdend = S.fdend, *fmend = S.fmend;
-  for (auto& kv : o.clock.dots) clk[kv.first] = kv.second;
+  if (sparse) {
+    uint32_t k = 0;
+    for (auto& kv : o.clock.dots) { clk[k] = kv.second; S.cact[k] = kv.first; ++k; }  // BTreeMap order
+  } else {
+    for (auto& kv : o.clock.dots) clk[kv.first] = kv.second;
+  }
   uint32_t d = 0;
   for (uint32_t m = 0; m < n_mem; ++m) {
     key[m] = ents[m].first;
@@ -318,15 +330,21 @@ bool decode(const uint8_t* rec, size_t avail, Orswot& o) {
   if (avail < CRDT_ORSWOT_HDR_BYTES) return false;
   crdt_orswot_hdr h;
   std::memcpy(&h, rec, sizeof h);
-  size_t bytes = record_bytes(h.n_clk, h.n_mem, h.n_dot, h.n_def, h.n_def_dot, h.n_def_mem);
-  if (bytes != h.size || bytes > avail || h.flags != 0) return false;
+  const bool sparse = h.flags == CRDT_ORSWOT_SPARSE_CLOCK;
+  if (h.flags != 0 && !sparse) return false;
+  size_t bytes = record_bytes(h.n_clk, h.n_mem, h.n_dot, h.n_def, h.n_def_dot, h.n_def_mem, sparse);
+  if (bytes != h.size || bytes > avail) return false;
   Sections S = sections(const_cast<uint8_t*>(rec), h);
   const uint64_t *clk = S.clk, *key = S.key, *dctr = S.dctr, *fctr = S.fctr, *fkey = S.fkey;
   const uint32_t *dact = S.dact, *mdend = S.mdend, *fact = S.fact, *fdend = S.fdend,
                  *fmend = S.fmend;
   o = Orswot();
-  for (uint32_t a = 0; a < h.n_clk; ++a)
-    if (clk[a]) o.clock.dots.emplace(a, clk[a]);
+  if (sparse) {
+    for (uint32_t k = 0; k < h.n_clk; ++k) o.clock.dots[S.cact[k]] = clk[k];
+  } else {
+    for (uint32_t a = 0; a < h.n_clk; ++a)
+      if (clk[a]) o.clock.dots.emplace(a, clk[a]);
+  }
   uint32_t d0 = 0;
   for (uint32_t m = 0; m < h.n_mem; ++m) {
     if (mdend[m] < d0 || mdend[m] > h.n_dot) return false;
@@ -389,10 +407,11 @@ size_t orc_record_bytes(uint32_t n_clk, uint32_t n_mem, uint32_t n_dot, uint32_t
 
 // Merge a batch of record pairs; output compacted (out_off computed here).
 // Returns 0, or a negative code (first failing object index in *bad).
-int orc_orswot_merge_batch(const uint8_t* lb, const uint64_t* loff, size_t lbytes,
-                           const uint8_t* rb, const uint64_t* roff, size_t rbytes, size_t n,
-                           uint32_t n_actors, uint8_t* ob, uint64_t* ooff, size_t ocap,
-                           int threads, int64_t* bad) {
+int orc_orswot_merge_batch_ex(const uint8_t* lb, const uint64_t* loff, size_t lbytes,
+                              const uint8_t* rb, const uint64_t* roff, size_t rbytes, size_t n,
+                              uint32_t n_actors, uint32_t flags, uint8_t* ob, uint64_t* ooff, size_t ocap,
+                              int threads, int64_t* bad) {
+  const bool sparse = (flags & CRDT_ORSWOT_SPARSE_CLOCK) != 0;
   std::vector<std::vector<uint8_t>> outs(n);
   std::vector<int> err(n, 0);
   parallel_for(n, threads, [&](size_t b, size_t e) {
@@ -405,7 +424,7 @@ int orc_orswot_merge_batch(const uint8_t* lb, const uint64_t* loff, size_t lbyte
       L.merge(R);
       std::vector<uint8_t> buf(record_bytes(n_actors, L.entries.size(), 0, 0, 0, 0) + 65536);
       long got;
-      while ((got = encode(L, n_actors, buf.data(), buf.size())) == CRDT_ECAPACITY)
+      while ((got = encode(L, n_actors, buf.data(), buf.size(), sparse)) == CRDT_ECAPACITY)
         buf.resize(buf.size() * 2);
       if (got < 0) { err[i] = (int)got; continue; }
       buf.resize(got);
@@ -421,6 +440,14 @@ int orc_orswot_merge_batch(const uint8_t* lb, const uint64_t* loff, size_t lbyte
     pos += outs[i].size();
   }
   return 0;
+}
+
+int orc_orswot_merge_batch(const uint8_t* lb, const uint64_t* loff, size_t lbytes,
+                           const uint8_t* rb, const uint64_t* roff, size_t rbytes, size_t n,
+                           uint32_t n_actors, uint8_t* ob, uint64_t* ooff, size_t ocap,
+                           int threads, int64_t* bad) {
+  return orc_orswot_merge_batch_ex(lb, loff, lbytes, rb, roff, rbytes, n, n_actors, 0u, ob, ooff, ocap,
+                                   threads, bad);
 }
 
 // CPU baseline: decode untimed, time only L[i].merge(&R[i]) for i in [0, n)
@@ -514,6 +541,9 @@ void orc_obj_apply_rm(void* h, uint64_t member, const uint32_t* act, const uint6
 void orc_obj_merge(void* dst, const void* src) { ((Orswot*)dst)->merge(*(const Orswot*)src); }
 long orc_obj_encode(const void* h, uint32_t n_actors, uint8_t* out, size_t cap) {
   return encode(*(const Orswot*)h, n_actors, out, cap);
+}
+long orc_obj_encode_ex(const void* h, uint32_t n_actors, uint32_t flags, uint8_t* out, size_t cap) {
+  return encode(*(const Orswot*)h, n_actors, out, cap, (flags & CRDT_ORSWOT_SPARSE_CLOCK) != 0);
 }
 void* orc_obj_decode(const uint8_t* rec, size_t bytes) {
   Orswot* o = new Orswot();

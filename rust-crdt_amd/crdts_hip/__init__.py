@@ -16,20 +16,24 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import (CRDT_ECAPACITY, CRDT_ENONCANON, CRDT_OK, EXPORTS, LIB_PATH, Batch, CrdtError, GenParams,
-                   check, lib)
+from ._lib import (CRDT_ECAPACITY, CRDT_ENONCANON, CRDT_OK, EXPORTS, LIB_PATH, SPARSE_CLOCK, Batch, CrdtError,
+                   GenParams, RepParams, check, lib)
 from .record import decode_record, encode_record, record_bytes
 
 __all__ = [
     "Engine", "OrswotBatch", "GenParams", "CrdtError", "generate_orswot", "generate_dense", "HostOrswot",
     "Orswot", "VClock", "GCounter", "PNCounter", "merge_batch", "decode_record", "encode_record",
-    "record_bytes", "CONFIG3", "EXPORTS", "LIB_PATH",
+    "record_bytes", "CONFIG3", "EXPORTS", "LIB_PATH", "CONFIG5", "SPARSE_CLOCK", "generate_replicas",
 ]
 
 # SURVEY.md §8(d) config 3 / BASELINE.json configs[2].
 CONFIG3 = dict(n_actors=16, member_universe=64, ancestor_adds=32, min_div_ops=4, max_div_ops=16, pct_add=60,
                pct_future_rm=10, pct_deferred_obj=8, pct_shared_actor=5)
 CONFIG3_SEED = 0xC0FFEE03
+# SURVEY.md §8(d) config 5 / BASELINE.json configs[4]: 1024-actor universe, CSR top clocks, 8 replicas.
+CONFIG5 = dict(universe=1024, pool_actors=48, own_actors=2, member_universe=64, ancestor_adds=48, min_div_ops=4,
+               max_div_ops=16, pct_add=60, pct_future_rm=10, pct_deferred_obj=8)
+CONFIG5_SEED = 0xC0FFEE05
 
 
 def _torch():
@@ -42,11 +46,14 @@ class OrswotBatch:
     """A batch of canonical Orswot records resident on one GPU.
 
     base: torch.uint8 device tensor; off: torch.int64 device tensor (u64 offsets).
+    flags: 0 (dense top clocks, n_actors slots) or SPARSE_CLOCK (CSR top clocks
+    over an actor universe of n_actors ids).
     """
 
-    def __init__(self, base, off, n_actors, nbytes=None):
+    def __init__(self, base, off, n_actors, nbytes=None, flags=0):
         self.base = base
         self.off = off
+        self.flags = int(flags)
         self.n_actors = int(n_actors)
         self.n_obj = int(off.numel())
         self.bytes = int(nbytes if nbytes is not None else base.numel())
@@ -55,7 +62,7 @@ class OrswotBatch:
         return Batch(self.base.data_ptr(), self.off.data_ptr(), self.n_obj, self.bytes)
 
     @classmethod
-    def from_host(cls, base, off, n_actors, device=0):
+    def from_host(cls, base, off, n_actors, device=0, flags=0):
         torch = _torch()
         base = np.ascontiguousarray(base, dtype=np.uint8)
         nb = max(16, (base.nbytes + 15) // 16 * 16)
@@ -63,10 +70,10 @@ class OrswotBatch:
         if base.nbytes:
             b[: base.nbytes].copy_(torch.from_numpy(base))
         o = torch.from_numpy(np.ascontiguousarray(off, dtype=np.uint64).view(np.int64)).to(f"cuda:{device}")
-        return cls(b, o, n_actors, nb)
+        return cls(b, o, n_actors, nb, flags)
 
     @classmethod
-    def from_records(cls, records, n_actors, device=0):
+    def from_records(cls, records, n_actors, device=0, flags=0):
         offs, pos = [], 0
         for r in records:
             offs.append(pos)
@@ -74,7 +81,7 @@ class OrswotBatch:
         base = np.zeros(max(pos, 16), dtype=np.uint8)
         for o, r in zip(offs, records):
             base[o:o + len(r)] = np.frombuffer(r, dtype=np.uint8)
-        return cls.from_host(base, np.array(offs, dtype=np.uint64), n_actors, device)
+        return cls.from_host(base, np.array(offs, dtype=np.uint64), n_actors, device, flags)
 
     def to_host(self):
         base = self.base.cpu().numpy()
@@ -134,18 +141,20 @@ class Engine:
         nb = L.bytes + R.bytes
         base = torch.empty(nb, dtype=torch.uint8, device=f"cuda:{self.device}")
         off = torch.empty(L.n_obj, dtype=torch.int64, device=f"cuda:{self.device}")
-        return OrswotBatch(base, off, L.n_actors, nb)
+        return OrswotBatch(base, off, L.n_actors, nb, L.flags)
 
     def orswot_merge(self, L: OrswotBatch, R: OrswotBatch, out: OrswotBatch | None = None, stream=None,
                      check_status=True):
         """out[i] = L[i].merge(&R[i])  (src/orswot.rs:87-157). Async unless check_status."""
-        if L.n_actors != R.n_actors or L.n_obj != R.n_obj:
+        if L.n_actors != R.n_actors or L.n_obj != R.n_obj or L.flags != R.flags:
             raise CrdtError(-1, "batch shapes differ")
         if out is None:
             out = self.orswot_alloc_out(L, R)
         lb, rb = L.cbatch(), R.cbatch()
-        rc = lib.crdt_orswot_merge(self.ctx, C.byref(lb), C.byref(rb), C.c_void_p(out.base.data_ptr()),
-                                   C.c_void_p(out.off.data_ptr()), out.bytes, L.n_actors, self._stream(stream))
+        out.flags = L.flags
+        rc = lib.crdt_orswot_merge_ex(self.ctx, C.byref(lb), C.byref(rb), C.c_void_p(out.base.data_ptr()),
+                                      C.c_void_p(out.off.data_ptr()), out.bytes, L.n_actors, L.flags,
+                                      self._stream(stream))
         check(rc, "crdt_orswot_merge")
         if check_status:
             self.status(stream)
@@ -153,7 +162,8 @@ class Engine:
 
     def orswot_validate(self, B: OrswotBatch, stream=None):
         b = B.cbatch()
-        check(lib.crdt_orswot_validate(self.ctx, C.byref(b), B.n_actors, self._stream(stream)), "validate")
+        check(lib.crdt_orswot_validate_ex(self.ctx, C.byref(b), B.n_actors, B.flags, self._stream(stream)),
+              "validate")
         self.status(stream)
 
     def orswot_compact(self, B: OrswotBatch, stream=None):
@@ -171,7 +181,7 @@ class Engine:
         if B.n_obj:
             last = int(doff[-1].item())
             used = last + int(dst[last:last + 4].cpu().numpy().view(np.uint32)[0])
-        return OrswotBatch(dst, doff, B.n_actors, max(16, (used + 15) // 16 * 16))
+        return OrswotBatch(dst, doff, B.n_actors, max(16, (used + 15) // 16 * 16), B.flags)
 
     # ---------------------------------------------------------------- dense
     def dense_merge(self, self_rows, other_rows, n_actors, kind="gcounter", stream=None):
@@ -207,16 +217,36 @@ def generate_orswot(n_obj, first_obj=0, seed=CONFIG3_SEED, params=None, threads=
     g = C.c_void_p()
     check(lib.crdt_orswot_generate(seed, first_obj, n_obj, C.byref(P), threads, C.byref(g)), "generate")
     try:
-        sides = []
-        for s in range(2):
-            bp, op, nb = C.c_void_p(), C.c_void_p(), C.c_size_t()
-            check(lib.crdt_orswot_gen_side(g, s, C.byref(bp), C.byref(op), C.byref(nb)), "gen_side")
-            base = np.ctypeslib.as_array((C.c_uint8 * max(1, nb.value)).from_address(bp.value)).copy() \
-                if nb.value else np.zeros(16, np.uint8)
-            off = np.ctypeslib.as_array((C.c_uint64 * max(1, n_obj)).from_address(op.value)).copy()[:n_obj] \
-                if n_obj else np.zeros(0, np.uint64)
-            sides.append((base, off))
+        sides = _copy_sides(g, 2, n_obj)
         return sides[0], sides[1]
+    finally:
+        lib.crdt_orswot_gen_free(g)
+
+
+def _copy_sides(g, n_sides, n_obj):
+    sides = []
+    for s in range(n_sides):
+        bp, op, nb = C.c_void_p(), C.c_void_p(), C.c_size_t()
+        check(lib.crdt_orswot_gen_side(g, s, C.byref(bp), C.byref(op), C.byref(nb)), "gen_side")
+        base = np.ctypeslib.as_array((C.c_uint8 * max(1, nb.value)).from_address(bp.value)).copy() \
+            if nb.value else np.zeros(16, np.uint8)
+        off = np.ctypeslib.as_array((C.c_uint64 * max(1, n_obj)).from_address(op.value)).copy()[:n_obj] \
+            if n_obj else np.zeros(0, np.uint64)
+        sides.append((base, off))
+    return sides
+
+
+def generate_replicas(n_obj, n_replicas=8, first_obj=0, seed=CONFIG5_SEED, params=None, sparse=True, threads=8):
+    """Replica sets for anti-entropy (config 5, include/crdts_hip.h): a list of
+    n_replicas (base, off) batches; replica r of object i is record i of batch r."""
+    d = dict(CONFIG5)
+    d.update(params or {})
+    P = RepParams(**{k: int(v) for k, v in d.items()})
+    g = C.c_void_p()
+    check(lib.crdt_orswot_generate_replicas(seed, first_obj, n_obj, C.byref(P), n_replicas,
+                                            SPARSE_CLOCK if sparse else 0, threads, C.byref(g)), "generate_replicas")
+    try:
+        return _copy_sides(g, n_replicas, n_obj)
     finally:
         lib.crdt_orswot_gen_free(g)
 
@@ -252,11 +282,11 @@ class HostOrswot:
         c = (C.c_uint64 * max(1, n))(*[int(y) for _, y in clock_pairs])
         check(lib.crdt_host_orswot_apply_rm(self.h, member, a, c, n), "apply_rm")
 
-    def encode(self, n_actors):
+    def encode(self, n_actors, flags=0):
         cap = 1 << 14
         while True:
             buf = (C.c_uint8 * cap)()
-            n = lib.crdt_host_orswot_encode(self.h, n_actors, buf, cap)
+            n = lib.crdt_host_orswot_encode_ex(self.h, n_actors, flags, buf, cap)
             if n == CRDT_ECAPACITY:
                 cap *= 4
                 continue
@@ -286,15 +316,21 @@ class Orswot:
     """Reference-shaped Orswot (src/orswot.rs:26-30) whose `merge` runs on the GPU.
 
     `n_actors` is the dense top-clock width used when the state crosses the
-    C ABI (actors must be interned to ids < n_actors).
+    C ABI (actors must be interned to ids < n_actors); with sparse=True the
+    top clock crosses as CSR and n_actors is only the actor-id universe.
     """
 
-    def __init__(self, n_actors=16, host=None):
+    def __init__(self, n_actors=16, host=None, sparse=False):
         self.n_actors = n_actors
+        self.sparse = bool(sparse)
         self.host = host or HostOrswot()
 
+    @property
+    def flags(self):
+        return SPARSE_CLOCK if self.sparse else 0
+
     def clone(self):
-        return Orswot(self.n_actors, self.host.clone())
+        return Orswot(self.n_actors, self.host.clone(), self.sparse)
 
     def apply_add(self, actor, counter, member):  # CmRDT::apply Op::Add
         self.host.apply_add(actor, counter, member)
@@ -306,7 +342,7 @@ class Orswot:
         merge_batch([self], [other], engine)
 
     def state(self):
-        return decode_record(self.host.encode(self.n_actors))
+        return decode_record(self.host.encode(self.n_actors, self.flags))
 
     def clock(self):
         return sorted(self.state()["clock"].items())
@@ -322,7 +358,7 @@ class Orswot:
         return len(self.state()["deferred"])
 
     def record(self):
-        return self.host.encode(self.n_actors)
+        return self.host.encode(self.n_actors, self.flags)
 
 
 def merge_batch(selfs, others, engine=None):
@@ -335,8 +371,9 @@ def merge_batch(selfs, others, engine=None):
     kinds = {type(x) for x in selfs} | {type(x) for x in others}
     if kinds == {Orswot}:
         n_actors = max(x.n_actors for x in list(selfs) + list(others))
-        L = OrswotBatch.from_records([x.host.encode(n_actors) for x in selfs], n_actors, eng.device)
-        R = OrswotBatch.from_records([x.host.encode(n_actors) for x in others], n_actors, eng.device)
+        fl = SPARSE_CLOCK if any(x.sparse for x in list(selfs) + list(others)) else 0
+        L = OrswotBatch.from_records([x.host.encode(n_actors, fl) for x in selfs], n_actors, eng.device, fl)
+        R = OrswotBatch.from_records([x.host.encode(n_actors, fl) for x in others], n_actors, eng.device, fl)
         out = eng.orswot_merge(L, R)
         for x, rec in zip(selfs, out.records()):
             x.host = HostOrswot.decode(rec)

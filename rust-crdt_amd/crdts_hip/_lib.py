@@ -39,6 +39,14 @@ class GenParams(C.Structure):
                                           "pct_shared_actor")]
 
 
+class RepParams(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("universe", "pool_actors", "own_actors", "member_universe",
+                                          "ancestor_adds", "min_div_ops", "max_div_ops", "pct_add",
+                                          "pct_future_rm", "pct_deferred_obj")]
+
+
+SPARSE_CLOCK = 1  # CRDT_ORSWOT_SPARSE_CLOCK
+
 # Every symbol include/crdts_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "crdt_ctx_create", "crdt_ctx_destroy", "crdt_ctx_status", "crdt_strerror", "crdt_abi_version",
@@ -48,7 +56,8 @@ EXPORTS = [
     "crdt_orswot_generate", "crdt_orswot_gen_side", "crdt_orswot_gen_free", "crdt_dense_generate",
     "crdt_host_orswot_new", "crdt_host_orswot_clone", "crdt_host_orswot_free",
     "crdt_host_orswot_apply_add", "crdt_host_orswot_apply_rm", "crdt_host_orswot_encode",
-    "crdt_host_orswot_decode",
+    "crdt_host_orswot_decode", "crdt_orswot_record_bytes_ex", "crdt_orswot_merge_ex",
+    "crdt_orswot_validate_ex", "crdt_orswot_generate_replicas", "crdt_host_orswot_encode_ex",
 ]
 
 
@@ -98,6 +107,11 @@ def _load():
         "crdt_host_orswot_apply_rm": (I, [P, U64, P, P, U32]),
         "crdt_host_orswot_encode": (C.c_long, [P, U32, P, SZ]),
         "crdt_host_orswot_decode": (P, [P, SZ]),
+        "crdt_orswot_record_bytes_ex": (SZ, [U32] * 7),
+        "crdt_orswot_merge_ex": (I, [P, BP, BP, P, P, SZ, U32, U32, P]),
+        "crdt_orswot_validate_ex": (I, [P, BP, U32, U32, P]),
+        "crdt_orswot_generate_replicas": (I, [U64, SZ, SZ, C.POINTER(RepParams), U32, U32, I, C.POINTER(P)]),
+        "crdt_host_orswot_encode_ex": (C.c_long, [P, U32, U32, P, SZ]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -8,14 +8,19 @@ from __future__ import annotations
 import struct
 
 HDR = 32
+SPARSE_CLOCK = 1  # header flags bit 0: CSR top clock (CRDT_ORSWOT_SPARSE_CLOCK)
 
 
 def _pad(x, a):
     return (x + a - 1) // a * a
 
 
-def record_bytes(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem):
-    b = _pad(HDR + 8 * n_clk + 12 * (n_mem + n_dot), 8)
+def _clock_bytes(n_clk, sparse):
+    return _pad(12 * n_clk, 8) if sparse else 8 * n_clk
+
+
+def record_bytes(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem, sparse=False):
+    b = _pad(HDR + _clock_bytes(n_clk, sparse) + 12 * (n_mem + n_dot), 8)
     return _pad(b + 12 * n_def_dot + 8 * n_def_mem + 8 * n_def, 16)
 
 
@@ -24,7 +29,10 @@ def decode_record(rec):
     rec = bytes(rec)
     size, n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem, flags = struct.unpack_from("<8I", rec, 0)
     o = HDR
-    clk = struct.unpack_from(f"<{n_clk}Q", rec, o); o += 8 * n_clk
+    sparse = bool(flags & SPARSE_CLOCK)
+    clk = struct.unpack_from(f"<{n_clk}Q", rec, o)
+    cact = struct.unpack_from(f"<{n_clk}I", rec, o + 8 * n_clk) if sparse else range(n_clk)
+    o += _clock_bytes(n_clk, sparse)
     keys = struct.unpack_from(f"<{n_mem}Q", rec, o); o += 8 * n_mem
     dctr = struct.unpack_from(f"<{n_dot}Q", rec, o); o += 8 * n_dot
     dact = struct.unpack_from(f"<{n_dot}I", rec, o); o += 4 * n_dot
@@ -42,25 +50,34 @@ def decode_record(rec):
     for de, me in zip(fdend, fmend):
         deferred.append((list(zip(fact[s:de], fctr[s:de])), list(fkey[t:me])))
         s, t = de, me
-    return dict(size=size, clock={a: c for a, c in enumerate(clk) if c}, entries=entries, deferred=deferred)
+    return dict(size=size, clock={a: c for a, c in zip(cact, clk) if c}, entries=entries, deferred=deferred)
 
 
-def encode_record(clock, entries, deferred, n_actors):
-    """clock {a: c}; entries {m: {a: c}}; deferred {tuple(sorted (a, c)): iterable(m)}."""
+def encode_record(clock, entries, deferred, n_actors, sparse=False):
+    """clock {a: c}; entries {m: {a: c}}; deferred {tuple(sorted (a, c)): iterable(m)}.
+    sparse: CSR top clock of the clock's nonzero actors (else n_actors dense slots)."""
     mems = sorted(entries)
     runs = [sorted(entries[m].items()) for m in mems]
     defs = sorted((tuple(k), sorted(v)) for k, v in deferred.items())
     n_mem, n_dot, n_def = len(mems), sum(map(len, runs)), len(defs)
     n_def_dot = sum(len(d[0]) for d in defs)
     n_def_mem = sum(len(d[1]) for d in defs)
-    size = record_bytes(n_actors, n_mem, n_dot, n_def, n_def_dot, n_def_mem)
+    cl = sorted((a, c) for a, c in clock.items() if c)
+    n_clk = len(cl) if sparse else n_actors
+    size = record_bytes(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem, sparse)
     out = bytearray(size)
-    struct.pack_into("<8I", out, 0, size, n_actors, n_mem, n_dot, n_def, n_def_dot, n_def_mem, 0)
+    struct.pack_into("<8I", out, 0, size, n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem,
+                     SPARSE_CLOCK if sparse else 0)
     o = HDR
-    clk = [0] * n_actors
-    for a, c in clock.items():
-        clk[a] = c
-    struct.pack_into(f"<{n_actors}Q", out, o, *clk); o += 8 * n_actors
+    if sparse:
+        struct.pack_into(f"<{n_clk}Q", out, o, *[c for _, c in cl])
+        struct.pack_into(f"<{n_clk}I", out, o + 8 * n_clk, *[a for a, _ in cl])
+    else:
+        clk = [0] * n_actors
+        for a, c in cl:
+            clk[a] = c
+        struct.pack_into(f"<{n_actors}Q", out, o, *clk)
+    o += _clock_bytes(n_clk, sparse)
     struct.pack_into(f"<{n_mem}Q", out, o, *mems); o += 8 * n_mem
     struct.pack_into(f"<{n_dot}Q", out, o, *[c for r in runs for _, c in r]); o += 8 * n_dot
     struct.pack_into(f"<{n_dot}I", out, o, *[a for r in runs for a, _ in r]); o += 4 * n_dot

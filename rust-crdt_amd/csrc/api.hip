@@ -161,7 +161,14 @@ int crdt_pncounter_merge(crdt_ctx* ctx, uint64_t* d_self, const uint64_t* d_othe
 int crdt_orswot_merge(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_orswot_batch* other,
                       uint8_t* d_out_base, uint64_t* d_out_off, size_t out_bytes, uint32_t n_actors,
                       void* stream) {
+  return crdt_orswot_merge_ex(ctx, self, other, d_out_base, d_out_off, out_bytes, n_actors, 0u, stream);
+}
+
+int crdt_orswot_merge_ex(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_orswot_batch* other,
+                         uint8_t* d_out_base, uint64_t* d_out_off, size_t out_bytes, uint32_t n_actors,
+                         uint32_t flags, void* stream) {
   if (!ctx || !self || !other || n_actors == 0 || self->n_obj != other->n_obj) return CRDT_EINVAL;
+  if (flags & ~CRDT_ORSWOT_SPARSE_CLOCK) return CRDT_EINVAL;
   if (self->n_obj == 0) return CRDT_OK;
   if (!self->base || !self->off || !other->base || !other->off || !d_out_base || !d_out_off)
     return CRDT_EINVAL;
@@ -169,6 +176,10 @@ int crdt_orswot_merge(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_o
   if (out_bytes < self->bytes + other->bytes) return CRDT_ECAPACITY;
   int rc = set_device(ctx);
   if (rc) return rc;
+  if (flags & CRDT_ORSWOT_SPARSE_CLOCK)
+    return launch_orswot_merge_sparse(self->base, self->off, self->bytes, other->base, other->off, other->bytes,
+                                      d_out_base, d_out_off, out_bytes, self->n_obj, n_actors, ctx->d_status,
+                                      S(stream));
   return launch_orswot_merge(self->base, self->off, self->bytes, other->base, other->off,
                              other->bytes, d_out_base, d_out_off, out_bytes, self->n_obj, n_actors,
                              ctx->d_status, ctx->d_ctl, ctx->d_list, ctx->list_cap, S(stream),
@@ -177,11 +188,16 @@ int crdt_orswot_merge(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_o
 
 int crdt_orswot_validate(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32_t n_actors,
                          void* stream) {
-  if (!ctx || !batch || n_actors == 0) return CRDT_EINVAL;
+  return crdt_orswot_validate_ex(ctx, batch, n_actors, 0u, stream);
+}
+
+int crdt_orswot_validate_ex(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32_t n_actors, uint32_t flags,
+                            void* stream) {
+  if (!ctx || !batch || n_actors == 0 || (flags & ~CRDT_ORSWOT_SPARSE_CLOCK)) return CRDT_EINVAL;
   if (batch->n_obj && (!batch->base || !batch->off)) return CRDT_EINVAL;
   int rc = set_device(ctx);
   if (rc) return rc;
-  return launch_orswot_validate(batch->base, batch->off, batch->bytes, batch->n_obj, n_actors,
+  return launch_orswot_validate(batch->base, batch->off, batch->bytes, batch->n_obj, n_actors, flags,
                                 ctx->d_status, S(stream));
 }
 

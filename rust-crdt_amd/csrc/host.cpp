@@ -84,7 +84,8 @@ struct HOrswot {
   }
 };
 
-long encode(const HOrswot& o, uint32_t n_actors, uint8_t* out, size_t cap) {
+// sparse: CSR top clock (flags bit 0): n_clk = nnz, ctr[] then act[] (crdts_hip.h).
+long encode(const HOrswot& o, uint32_t n_actors, uint8_t* out, size_t cap, bool sparse = false) {
   uint32_t n_mem = (uint32_t)o.entries.size(), n_dot = 0, n_def = (uint32_t)o.deferred.size();
   uint32_t n_def_dot = 0, n_def_mem = 0;
   for (auto& kv : o.entries) {
@@ -100,11 +101,12 @@ long encode(const HOrswot& o, uint32_t n_actors, uint8_t* out, size_t cap) {
   }
   for (auto& x : o.clock.d)
     if (x.first >= n_actors) return CRDT_EINVAL;
+  const uint32_t n_clk = sparse ? (uint32_t)o.clock.d.size() : n_actors;
   RecLayout L;
-  rec_layout(L, n_actors, n_mem, n_dot, n_def, n_def_dot, n_def_mem);
+  rec_layout(L, n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem, sparse);
   if (L.size > cap) return CRDT_ECAPACITY;
   std::memset(out, 0, L.size);
-  crdt_orswot_hdr h = {L.size, n_actors, n_mem, n_dot, n_def, n_def_dot, n_def_mem, 0};
+  crdt_orswot_hdr h = {L.size, n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem, sparse ? kSparseClock : 0u};
   std::memcpy(out, &h, sizeof h);
   uint64_t* clk = (uint64_t*)(out + L.o_clk);
   uint64_t* key = (uint64_t*)(out + L.o_key);
@@ -116,7 +118,13 @@ long encode(const HOrswot& o, uint32_t n_actors, uint8_t* out, size_t cap) {
   uint32_t* fact = (uint32_t*)(out + L.o_fact);
   uint32_t* fdend = (uint32_t*)(out + L.o_fdend);
   uint32_t* fmend = (uint32_t*)(out + L.o_fmend);
-  for (auto& x : o.clock.d) clk[x.first] = x.second;
+  if (sparse) {
+    uint32_t* cact = (uint32_t*)(out + L.o_cact);
+    uint32_t k = 0;
+    for (auto& x : o.clock.d) { clk[k] = x.second; cact[k] = x.first; ++k; }
+  } else {
+    for (auto& x : o.clock.d) clk[x.first] = x.second;
+  }
   uint32_t m = 0, d = 0;
   for (auto& kv : o.entries) {
     key[m] = kv.first;
@@ -138,9 +146,10 @@ bool decode(const uint8_t* rec, size_t avail, HOrswot& o) {
   if (avail < kHdrBytes) return false;
   crdt_orswot_hdr h;
   std::memcpy(&h, rec, sizeof h);
-  if (h.flags != 0) return false;
+  if (h.flags & ~kSparseClock) return false;
+  const bool sparse = (h.flags & kSparseClock) != 0;
   RecLayout L;
-  rec_layout(L, h.n_clk, h.n_mem, h.n_dot, h.n_def, h.n_def_dot, h.n_def_mem);
+  rec_layout(L, h.n_clk, h.n_mem, h.n_dot, h.n_def, h.n_def_dot, h.n_def_mem, sparse);
   if (L.size != h.size || L.size > avail) return false;
   const uint64_t* clk = (const uint64_t*)(rec + L.o_clk);
   const uint64_t* key = (const uint64_t*)(rec + L.o_key);
@@ -153,8 +162,16 @@ bool decode(const uint8_t* rec, size_t avail, HOrswot& o) {
   const uint32_t* fdend = (const uint32_t*)(rec + L.o_fdend);
   const uint32_t* fmend = (const uint32_t*)(rec + L.o_fmend);
   o = HOrswot();
-  for (uint32_t a = 0; a < h.n_clk; ++a)
-    if (clk[a]) o.clock.d.push_back({a, clk[a]});
+  if (sparse) {
+    const uint32_t* cact = (const uint32_t*)(rec + L.o_cact);
+    for (uint32_t k = 0; k < h.n_clk; ++k) {
+      if (k && cact[k] <= cact[k - 1]) return false;
+      o.clock.d.push_back({cact[k], clk[k]});
+    }
+  } else {
+    for (uint32_t a = 0; a < h.n_clk; ++a)
+      if (clk[a]) o.clock.d.push_back({a, clk[a]});
+  }
   uint32_t s = 0;
   for (uint32_t m = 0; m < h.n_mem; ++m) {
     if (mdend[m] < s || mdend[m] > h.n_dot) return false;
@@ -254,6 +271,77 @@ void gen_pair(uint64_t seed, uint64_t obj, const crdt_orswot_gen_params& P, HOrs
   }
 }
 
+// One object's replicas for replica anti-entropy (config 5, crdts_hip.h):
+// a shared ancestor over a per-object pool of actors drawn from a large
+// universe, then each replica diverges with its own actors.
+void gen_replicas(uint64_t seed, uint64_t obj, const crdt_orswot_rep_params& P, uint32_t n_rep,
+                  std::vector<HOrswot>& reps) {
+  SplitMix64 rng(seed ^ obj);
+  const uint32_t U = P.member_universe;
+  std::vector<uint64_t> keys(U);
+  for (uint32_t j = 0; j < U; ++j) {
+    uint64_t k;
+    do {
+      k = rng.next();
+    } while (std::find(keys.begin(), keys.begin() + j, k) != keys.begin() + j);
+    keys[j] = k;
+  }
+  auto draw_actors = [&](uint32_t n, std::vector<uint32_t>& out) {
+    out.clear();
+    while (out.size() < std::min(n, P.universe)) {
+      uint32_t a = rng.below(P.universe);
+      if (std::find(out.begin(), out.end(), a) == out.end()) out.push_back(a);
+    }
+  };
+  std::vector<uint32_t> pool;
+  draw_actors(P.pool_actors, pool);
+  std::vector<std::vector<uint32_t>> own(n_rep);
+  for (uint32_t r = 0; r < n_rep; ++r) draw_actors(P.own_actors, own[r]);
+  std::map<uint32_t, uint64_t> base;  // per-actor 40-bit history base
+  auto next_ctr = [&](const HOrswot& o, uint32_t a) {
+    auto it = base.find(a);
+    if (it == base.end()) it = base.emplace(a, rng.next() & ((1ull << 40) - 1)).first;
+    return std::max(o.clock.get(a), it->second) + 1;  // derive_add_ctx, src/ctx.rs:599-607
+  };
+  std::vector<uint32_t> perm(U);
+  for (uint32_t j = 0; j < U; ++j) perm[j] = j;
+  for (uint32_t j = U; j > 1; --j) std::swap(perm[j - 1], perm[rng.below(j)]);
+  HOrswot anc;
+  for (uint32_t k = 0; k < P.ancestor_adds && !pool.empty(); ++k) {
+    uint32_t a = pool[rng.below((uint32_t)pool.size())];
+    uint32_t m = k < U ? perm[k] : rng.below(U);
+    anc.apply_add(a, next_ctr(anc, a), keys[m]);
+  }
+  const bool defobj = rng.below(100) < P.pct_deferred_obj;
+  reps.assign(n_rep, anc);
+  for (uint32_t r = 0; r < n_rep; ++r) {
+    HOrswot& o = reps[r];
+    uint32_t span = P.max_div_ops >= P.min_div_ops ? P.max_div_ops - P.min_div_ops + 1 : 1;
+    uint32_t nops = P.min_div_ops + rng.below(span);
+    for (uint32_t k = 0; k < nops; ++k) {
+      uint32_t q = rng.below(100);
+      if (q < P.pct_add && !own[r].empty()) {
+        uint32_t a = own[r][rng.below((uint32_t)own[r].size())];
+        o.apply_add(a, next_ctr(o, a), keys[rng.below(U)]);
+      } else if (defobj && q >= 100 - P.pct_future_rm && n_rep > 1) {
+        // remove with a future context: advanced on another replica's actor
+        uint32_t r2 = (r + 1 + rng.below(n_rep - 1)) % n_rep;
+        if (own[r2].empty()) continue;
+        Clk c = o.clock;
+        uint32_t x = own[r2][rng.below((uint32_t)own[r2].size())];
+        c.witness(x, next_ctr(o, x) + rng.below(3));
+        o.apply_remove(keys[rng.below(U)], c);
+      } else {
+        if (o.entries.empty()) continue;
+        auto it = o.entries.begin();
+        std::advance(it, rng.below((uint32_t)o.entries.size()));
+        Clk c = it->second;
+        o.apply_remove(it->first, c);
+      }
+    }
+  }
+}
+
 template <class F>
 void parallel_for(size_t n, int threads, F f) {
   threads = std::max(1, threads);
@@ -274,41 +362,31 @@ void parallel_for(size_t n, int threads, F f) {
 }  // namespace
 
 struct crdt_orswot_gen {
-  std::vector<uint8_t> base[2];
-  std::vector<uint64_t> off[2];
+  std::vector<std::vector<uint8_t>> base;  // one batch per side / replica
+  std::vector<std::vector<uint64_t>> off;
 };
 
-struct crdt_host_orswot {
-  HOrswot o;
-};
-
-extern "C" {
-
-size_t crdt_orswot_record_bytes(uint32_t n_clk, uint32_t n_mem, uint32_t n_dot, uint32_t n_def,
-                                uint32_t n_def_dot, uint32_t n_def_mem) {
-  return (size_t)record_size64(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem);
-}
-
-int crdt_orswot_generate(uint64_t seed, size_t first_obj, size_t n_obj,
-                         const crdt_orswot_gen_params* params, int n_threads,
-                         crdt_orswot_gen** out) {
-  if (!params || !out || params->n_actors == 0 || params->member_universe == 0)
-    return CRDT_EINVAL;
-  const crdt_orswot_gen_params P = *params;
-  int T = std::max(1, n_threads);
-  std::vector<std::vector<uint8_t>> buf[2];
-  std::vector<std::vector<uint64_t>> loc[2];
-  for (int s = 0; s < 2; ++s) { buf[s].resize(T); loc[s].resize(T); }
-  std::vector<size_t> first(T + 1, n_obj);
+namespace {
+// Runs gen(i, states) for objects [0, n) on T threads and packs side s of
+// every object into batch s (16-B aligned records, object order).
+template <class G>
+int pack_sides(size_t n_obj, uint32_t n_sides, int T, uint32_t n_actors, bool sparse, G gen,
+               crdt_orswot_gen** out) {
+  T = std::max(1, T);
+  std::vector<std::vector<std::vector<uint8_t>>> buf(n_sides, std::vector<std::vector<uint8_t>>(T));
+  std::vector<std::vector<std::vector<uint64_t>>> loc(n_sides, std::vector<std::vector<uint64_t>>(T));
   std::vector<int> err(T, 0);
   parallel_for(n_obj, T, [&](size_t b, size_t e, int t) {
-    first[t] = b;
-    HOrswot L, R;
+    std::vector<HOrswot> st;
     std::vector<uint8_t> tmp(1 << 16);
     for (size_t i = b; i < e; ++i) {
-      gen_pair(seed, first_obj + i, P, L, R);
-      for (int s = 0; s < 2; ++s) {
-        long n = encode(s == 0 ? L : R, P.n_actors, tmp.data(), tmp.size());
+      gen(i, st);
+      for (uint32_t s = 0; s < n_sides; ++s) {
+        long n = encode(st[s], n_actors, tmp.data(), tmp.size(), sparse);
+        while (n == CRDT_ECAPACITY) {
+          tmp.resize(tmp.size() * 2);
+          n = encode(st[s], n_actors, tmp.data(), tmp.size(), sparse);
+        }
         if (n < 0) { err[t] = (int)n; return; }
         loc[s][t].push_back(buf[s][t].size());
         buf[s][t].insert(buf[s][t].end(), tmp.begin(), tmp.begin() + n);
@@ -318,7 +396,9 @@ int crdt_orswot_generate(uint64_t seed, size_t first_obj, size_t n_obj,
   for (int t = 0; t < T; ++t)
     if (err[t]) return err[t];
   auto* g = new crdt_orswot_gen();
-  for (int s = 0; s < 2; ++s) {
+  g->base.resize(n_sides);
+  g->off.resize(n_sides);
+  for (uint32_t s = 0; s < n_sides; ++s) {
     size_t total = 0;
     for (int t = 0; t < T; ++t) total += buf[s][t].size();
     g->base[s].resize(std::max<size_t>(total, 16));
@@ -335,10 +415,53 @@ int crdt_orswot_generate(uint64_t seed, size_t first_obj, size_t n_obj,
   *out = g;
   return CRDT_OK;
 }
+}  // namespace
+
+struct crdt_host_orswot {
+  HOrswot o;
+};
+
+extern "C" {
+
+size_t crdt_orswot_record_bytes(uint32_t n_clk, uint32_t n_mem, uint32_t n_dot, uint32_t n_def,
+                                uint32_t n_def_dot, uint32_t n_def_mem) {
+  return (size_t)record_size64(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem);
+}
+size_t crdt_orswot_record_bytes_ex(uint32_t n_clk, uint32_t n_mem, uint32_t n_dot, uint32_t n_def,
+                                   uint32_t n_def_dot, uint32_t n_def_mem, uint32_t flags) {
+  return (size_t)record_size64(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem,
+                               (flags & CRDT_ORSWOT_SPARSE_CLOCK) != 0);
+}
+
+int crdt_orswot_generate(uint64_t seed, size_t first_obj, size_t n_obj,
+                         const crdt_orswot_gen_params* params, int n_threads,
+                         crdt_orswot_gen** out) {
+  if (!params || !out || params->n_actors == 0 || params->member_universe == 0)
+    return CRDT_EINVAL;
+  const crdt_orswot_gen_params P = *params;
+  return pack_sides(n_obj, 2, n_threads, P.n_actors, false,
+                    [&](size_t i, std::vector<HOrswot>& st) {
+                      st.resize(2);
+                      gen_pair(seed, first_obj + i, P, st[0], st[1]);
+                    },
+                    out);
+}
+
+int crdt_orswot_generate_replicas(uint64_t seed, size_t first_obj, size_t n_obj,
+                                  const crdt_orswot_rep_params* params, uint32_t n_replicas,
+                                  uint32_t flags, int n_threads, crdt_orswot_gen** out) {
+  if (!params || !out || params->universe == 0 || params->member_universe == 0 || n_replicas == 0 ||
+      (flags & ~CRDT_ORSWOT_SPARSE_CLOCK))
+    return CRDT_EINVAL;
+  const crdt_orswot_rep_params P = *params;
+  return pack_sides(n_obj, n_replicas, n_threads, P.universe, (flags & CRDT_ORSWOT_SPARSE_CLOCK) != 0,
+                    [&](size_t i, std::vector<HOrswot>& st) { gen_replicas(seed, first_obj + i, P, n_replicas, st); },
+                    out);
+}
 
 int crdt_orswot_gen_side(const crdt_orswot_gen* g, int side, const uint8_t** h_base,
                          const uint64_t** h_off, size_t* bytes) {
-  if (!g || side < 0 || side > 1) return CRDT_EINVAL;
+  if (!g || side < 0 || (size_t)side >= g->base.size()) return CRDT_EINVAL;
   if (h_base) *h_base = g->base[side].data();
   if (h_off) *h_off = g->off[side].data();
   if (bytes) *bytes = g->base[side].size();
@@ -387,6 +510,11 @@ long crdt_host_orswot_encode(const crdt_host_orswot* o, uint32_t n_actors, uint8
                              size_t cap) {
   if (!o || !h_rec) return CRDT_EINVAL;
   return encode(o->o, n_actors, h_rec, cap);
+}
+long crdt_host_orswot_encode_ex(const crdt_host_orswot* o, uint32_t n_actors, uint32_t flags,
+                                uint8_t* h_rec, size_t cap) {
+  if (!o || !h_rec || (flags & ~CRDT_ORSWOT_SPARSE_CLOCK)) return CRDT_EINVAL;
+  return encode(o->o, n_actors, h_rec, cap, (flags & CRDT_ORSWOT_SPARSE_CLOCK) != 0);
 }
 crdt_host_orswot* crdt_host_orswot_decode(const uint8_t* h_rec, size_t bytes) {
   if (!h_rec) return nullptr;

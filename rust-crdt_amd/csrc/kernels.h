@@ -11,10 +11,14 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
                         uint64_t* list, uint32_t list_cap, hipStream_t stream, int blocks_per_cu,
                         int variant);
 
+int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
+                               const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
+                               uint64_t n_obj, uint32_t n_actors, int* status, hipStream_t stream);
+
 int launch_dense_max(uint64_t* self, const uint64_t* other, uint64_t n_words, hipStream_t stream);
 
 int launch_orswot_validate(const uint8_t* base, const uint64_t* off, uint64_t bytes, uint64_t n_obj,
-                           uint32_t n_actors, int* status, hipStream_t stream);
+                           uint32_t n_actors, uint32_t flags, int* status, hipStream_t stream);
 
 int launch_record_sizes(const uint8_t* base, const uint64_t* off, uint64_t n_obj, uint64_t* sizes,
                         hipStream_t stream);

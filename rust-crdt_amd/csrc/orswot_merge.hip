@@ -97,13 +97,13 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
 
 // Byte offsets of one record's sections (wave-uniform), relative to its base.
 struct RV {
-  uint32_t clk, key, dctr, dact, mdend, fctr, fkey, fact, fdend, fmend;
-  uint32_t n_mem, n_def;
+  uint32_t clk, cact, key, dctr, dact, mdend, fctr, fkey, fact, fdend, fmend;
+  uint32_t n_mem, n_def, n_clk;
 };
 
 __device__ __forceinline__ RV make_rv(const RecLayout& L) {
   RV v;
-  v.clk = L.o_clk; v.key = L.o_key; v.dctr = L.o_dctr; v.dact = L.o_dact; v.mdend = L.o_mdend;
+  v.clk = L.o_clk; v.cact = L.o_cact; v.n_clk = L.n_clk; v.key = L.o_key; v.dctr = L.o_dctr; v.dact = L.o_dact; v.mdend = L.o_mdend;
   v.fctr = L.o_fctr; v.fkey = L.o_fkey; v.fact = L.o_fact; v.fdend = L.o_fdend; v.fmend = L.o_fmend;
   v.n_mem = L.n_mem; v.n_def = L.n_def;
   return v;
@@ -119,6 +119,22 @@ __device__ __forceinline__ uint32_t g32(const uint8_t* b, uint32_t off, uint32_t
 // VClock::get on a dense top clock, absent = 0 (src/vclock.rs:206-210)
 __device__ __forceinline__ uint64_t top(const uint8_t* b, const RV& v, uint32_t a, uint32_t A) {
   return a < A ? g64(b, v.clk, a) : 0ull;
+}
+// First index k in [0, n) of the sparse clock's actor list with act[k] >= a.
+__device__ __forceinline__ uint32_t clk_lower_bound(const uint8_t* b, const RV& v, uint32_t a) {
+  uint32_t lo = 0, n = v.n_clk;
+  while (n) {
+    const uint32_t h = n >> 1;
+    if (g32(b, v.cact, lo + h) < a) { lo += h + 1; n -= h + 1; } else { n = h; }
+  }
+  return lo;
+}
+// VClock::get for either clock form: a CSR clock is searched (sorted actors).
+template <bool SP>
+__device__ __forceinline__ uint64_t topv(const uint8_t* b, const RV& v, uint32_t a, uint32_t A) {
+  if (!SP) return top(b, v, a, A);
+  const uint32_t k = clk_lower_bound(b, v, a);
+  return (k < v.n_clk && g32(b, v.cact, k) == a) ? g64(b, v.clk, k) : 0ull;
 }
 __device__ __forceinline__ uint32_t run_begin(const uint8_t* b, uint32_t off, uint32_t k) {
   return k ? g32(b, off, k - 1) : 0u;
@@ -189,7 +205,7 @@ __device__ __forceinline__ uint32_t merge_path(const Side& L, const Side& R, uin
 // captures the first output dot in (x0, v0); MODE 1 also stores the run at
 // oact/octr[d0..]. Lc/Rc are the PRE-merge top clocks. One loop step per
 // actor of the union of both runs, branch-free inside.
-template <int MODE>
+template <int MODE, bool SP = false>
 __device__ __forceinline__ uint32_t join(const Side& L, const Side& R, uint32_t type, uint32_t i,
                                          uint32_t j, uint32_t A, bool has_def, uint32_t& x0, uint64_t& v0,
                                          uint32_t* oact, uint64_t* octr, uint32_t d0) {
@@ -200,7 +216,7 @@ __device__ __forceinline__ uint32_t join(const Side& L, const Side& R, uint32_t 
     // a self-only entry is kept UNCHANGED iff !(clock <= other.clock) (:98-103)
     bool any = false;
     for (uint32_t d = a; d < ae && !any; ++d)
-      any = g64(L.b, L.v.dctr, d) > top(R.b, R.v, g32(L.b, L.v.dact, d), A);
+      any = g64(L.b, L.v.dctr, d) > topv<SP>(R.b, R.v, g32(L.b, L.v.dact, d), A);
     if (!any) ae = a;
   }
   uint64_t m = 0;
@@ -214,7 +230,7 @@ __device__ __forceinline__ uint32_t join(const Side& L, const Side& R, uint32_t 
     const uint32_t x = ta ? xa : xb;
     const uint64_t va = ta ? g64(L.b, L.v.dctr, a) : 0ull;
     const uint64_t vb = tb ? g64(R.b, R.v.dctr, b) : 0ull;
-    const uint64_t rc = top(R.b, R.v, x, A), lc = top(L.b, L.v, x, A);
+    const uint64_t rc = topv<SP>(R.b, R.v, x, A), lc = topv<SP>(L.b, L.v, x, A);
     // self-only: the whole run (kept); otherwise L[x] survives iff > Rc[x]
     // (:112, :133 analogue), R[x] iff > Lc[x] (:113, :133); a dot equal on
     // both sides is common (:109) and survives as is; result = max (:115-116)
@@ -253,12 +269,13 @@ __device__ __forceinline__ int clock_cmp(const Side& X, uint32_t k, const Side& 
 }
 
 // !(D <= merged clock): some dot of D exceeds max(Lc, Rc)  (src/orswot.rs:197)
+template <bool SP = false>
 __device__ __forceinline__ bool def_survives(const Side& X, uint32_t k, const Side& L, const Side& R,
                                              uint32_t A) {
   uint32_t e = g32(X.b, X.v.fdend, k);
   for (uint32_t d = run_begin(X.b, X.v.fdend, k); d < e; ++d) {
     uint32_t x = g32(X.b, X.v.fact, d);
-    uint64_t lc = top(L.b, L.v, x, A), rc = top(R.b, R.v, x, A);
+    uint64_t lc = topv<SP>(L.b, L.v, x, A), rc = topv<SP>(R.b, R.v, x, A);
     if (g64(X.b, X.v.fctr, d) > (lc > rc ? lc : rc)) return true;
   }
   return false;
@@ -274,6 +291,7 @@ struct DefOut {
 
 // Deferred union + filter (src/orswot.rs:141-148, then :155 -> :197-203),
 // single lane. With w == nullptr only counts.
+template <bool SP = false>
 __device__ void deferred_pass(const Side& L, const Side& R, uint32_t A, uint32_t& nd, uint32_t& ndd,
                               uint32_t& ndm, const DefOut* w) {
   uint32_t k = 0, l = 0;
@@ -282,7 +300,7 @@ __device__ void deferred_pass(const Side& L, const Side& R, uint32_t A, uint32_t
     const int c = k >= L.v.n_def ? 1 : (l >= R.v.n_def ? -1 : clock_cmp(L, k, R, l));
     const Side& X = c <= 0 ? L : R;
     const uint32_t kx = c <= 0 ? k : l;
-    if (def_survives(X, kx, L, R, A)) {
+    if (def_survives<SP>(X, kx, L, R, A)) {
       uint32_t e = g32(X.b, X.v.fdend, kx);
       for (uint32_t d = run_begin(X.b, X.v.fdend, kx); d < e; ++d) {
         if (w) { w->fact[ndd] = g32(X.b, X.v.fact, d); w->fctr[ndd] = g64(X.b, X.v.fctr, d); }
@@ -398,18 +416,66 @@ __device__ void deferred_pass_wave(const Side& L, const Side& R, uint32_t A, uin
 __device__ __forceinline__ RecLayout layout_at(const uint8_t* rec) {
   const uint32_t* h = (const uint32_t*)rec;
   RecLayout L;
-  rec_layout(L, uni(h[1]), uni(h[2]), uni(h[3]), uni(h[4]), uni(h[5]), uni(h[6]));
+  rec_layout(L, uni(h[1]), uni(h[2]), uni(h[3]), uni(h[4]), uni(h[5]), uni(h[6]), (uni(h[7]) & kSparseClock) != 0u);
   return L;
 }
 
+// Sparse (CSR) top-clock join, src/orswot.rs:153 -> VClock::merge
+// (src/vclock.rs:131-137): the sorted union of both actor lists, max on
+// common actors. Counts the union (every lane gets it); with O != nullptr
+// also writes ctr/act at O's clock section for a union of n_out entries.
+__device__ __forceinline__ uint32_t sparse_clock_join(const Side& L, const Side& R, uint8_t* O, uint32_t n_out,
+                                                      uint32_t lane) {
+  // union index of actor x = #L acts < x + #R acts < x - #common acts < x;
+  // the common count below an entry is a running wave prefix over its side.
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint32_t common = 0;
+  for (uint32_t base = 0; base < L.v.n_clk; base += kWave) {
+    const uint32_t k = base + lane;
+    const bool valid = k < L.v.n_clk;
+    const uint32_t x = valid ? g32(L.b, L.v.cact, k) : 0u;
+    const uint32_t r = valid ? clk_lower_bound(R.b, R.v, x) : 0u;
+    const bool eq = valid && r < R.v.n_clk && g32(R.b, R.v.cact, r) == x;
+    const uint64_t em = __ballot(eq);
+    if (O && valid) {
+      const uint32_t idx = k + r - (common + (uint32_t)__popcll(em & lt));
+      const uint64_t a = g64(L.b, L.v.clk, k), c = eq ? g64(R.b, R.v.clk, r) : 0ull;
+      ((uint64_t*)(O + kHdrBytes))[idx] = a > c ? a : c;
+      ((uint32_t*)(O + kHdrBytes + 8u * n_out))[idx] = x;
+    }
+    common += (uint32_t)__popcll(em);
+  }
+  if (O) {
+    uint32_t rc = 0;
+    for (uint32_t base = 0; base < R.v.n_clk; base += kWave) {
+      const uint32_t k = base + lane;
+      const bool valid = k < R.v.n_clk;
+      const uint32_t x = valid ? g32(R.b, R.v.cact, k) : 0u;
+      const uint32_t l = valid ? clk_lower_bound(L.b, L.v, x) : 0u;
+      const bool eq = valid && l < L.v.n_clk && g32(L.b, L.v.cact, l) == x;
+      const uint64_t em = __ballot(eq);
+      if (valid && !eq) {  // common actors were written by the self side
+        const uint32_t idx = k + l - (rc + (uint32_t)__popcll(em & lt));
+        ((uint64_t*)(O + kHdrBytes))[idx] = g64(R.b, R.v.clk, k);
+        ((uint32_t*)(O + kHdrBytes + 8u * n_out))[idx] = x;
+      }
+      rc += (uint32_t)__popcll(em);
+    }
+  }
+  return L.v.n_clk + R.v.n_clk - common;
+}
+
 // Join one object pair whose records sit at Ls / Rs (LDS stage or HBM) into
-// the output record at O (HBM).
+// the output record at O (HBM). SP: both records carry CSR top clocks (and
+// so does the output).
+template <bool SP = false>
 __device__ __forceinline__ void merge_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* O, uint32_t A,
                                              uint32_t lane) {
   const RecLayout LL = layout_at(Ls), RL = layout_at(Rs);
   const Side L{Ls, make_rv(LL)}, R{Rs, make_rv(RL)};
   const bool has_def = (L.v.n_def | R.v.n_def) != 0;
   const uint32_t P = L.v.n_mem + R.v.n_mem;
+  const uint32_t n_clk = SP ? uni(sparse_clock_join(L, R, nullptr, 0u, lane)) : A;
 
   // ---- pass 1: per-position join -> member / dot totals. For the first
   // two 64-wide chunks each lane keeps its candidate, count and first output
@@ -423,7 +489,7 @@ __device__ __forceinline__ void merge_object(const uint8_t* Ls, const uint8_t* R
     uint64_t v = 0;
     if (p < P) {
       type = merge_path(L, R, p, i, j);
-      if (type != kNone) cnt = join<0>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0);
+      if (type != kNone) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0);
     }
     const uint32_t q = (type << 30) | (i << 15) | j;
     if (base == 0) { q0 = q; c0 = cnt; x0 = x; v0 = v; }
@@ -435,7 +501,7 @@ __device__ __forceinline__ void merge_object(const uint8_t* Ls, const uint8_t* R
   tot_dot = uni(tot_dot);
 
   // ---- output member block (its offsets depend on the member totals only)
-  const uint32_t o_key = kHdrBytes + 8u * A;
+  const uint32_t o_key = kHdrBytes + clock_bytes(n_clk, SP);
   const uint32_t o_dctr = o_key + 8u * tot_mem;
   const uint32_t o_dact = o_dctr + 8u * tot_dot;
   const uint32_t o_mdend = o_dact + 4u * tot_dot;
@@ -447,9 +513,14 @@ __device__ __forceinline__ void merge_object(const uint8_t* Ls, const uint8_t* R
   uint32_t* omdend = (uint32_t*)(O + o_mdend);
 
   // top clock: pointwise max (src/orswot.rs:153 -> src/vclock.rs:131-137)
-  for (uint32_t a = lane; a < A; a += kWave) {
-    const uint64_t x = g64(Ls, L.v.clk, a), y = g64(Rs, R.v.clk, a);
-    ((uint64_t*)(O + kHdrBytes))[a] = x > y ? x : y;
+  if (SP) {
+    sparse_clock_join(L, R, O, n_clk, lane);
+    if (lane == 0u && (n_clk & 1u)) *(uint32_t*)(O + kHdrBytes + 12u * n_clk) = 0u;  // pad to 8
+  } else {
+    for (uint32_t a = lane; a < A; a += kWave) {
+      const uint64_t x = g64(Ls, L.v.clk, a), y = g64(Rs, R.v.clk, a);
+      ((uint64_t*)(O + kHdrBytes))[a] = x > y ? x : y;
+    }
   }
 
   // ---- pass 2: write kept members and their joined dot runs
@@ -466,7 +537,7 @@ __device__ __forceinline__ void merge_object(const uint8_t* Ls, const uint8_t* R
       cnt = 0; x = 0; v = 0;
       if (p < P) {
         type = merge_path(L, R, p, i, j);
-        if (type != kNone) cnt = join<0>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0);
+        if (type != kNone) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0);
       }
       q = (type << 30) | (i << 15) | j;
     }
@@ -481,7 +552,7 @@ __device__ __forceinline__ void merge_object(const uint8_t* Ls, const uint8_t* R
         odact[d0] = x;
         odctr[d0] = v;
       } else {
-        join<1>(L, R, type, i, j, A, has_def, x, v, odact, odctr, d0);
+        join<1, SP>(L, R, type, i, j, A, has_def, x, v, odact, odctr, d0);
       }
       omdend[midx] = d0 + cnt;
     }
@@ -494,19 +565,19 @@ __device__ __forceinline__ void merge_object(const uint8_t* Ls, const uint8_t* R
     uint32_t nd = 0, ndd = 0, ndm = 0;
     if (o_def != o_mpad) *(uint32_t*)(O + o_mpad) = 0u;
     if (has_def) {
-      deferred_pass(L, R, A, nd, ndd, ndm, nullptr);
+      deferred_pass<SP>(L, R, A, nd, ndd, ndm, nullptr);
       RecLayout OL;
-      rec_layout(OL, A, tot_mem, tot_dot, nd, ndd, ndm);
+      rec_layout(OL, n_clk, tot_mem, tot_dot, nd, ndd, ndm, SP);
       DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
                (uint32_t*)(O + OL.o_fdend), (uint32_t*)(O + OL.o_fmend)};
-      deferred_pass(L, R, A, nd, ndd, ndm, &w);
+      deferred_pass<SP>(L, R, A, nd, ndd, ndm, &w);
     }
     RecLayout OL;
-    rec_layout(OL, A, tot_mem, tot_dot, nd, ndd, ndm);
+    rec_layout(OL, n_clk, tot_mem, tot_dot, nd, ndd, ndm, SP);
     for (uint32_t b = OL.o_end; b < OL.size; b += 4) *(uint32_t*)(O + b) = 0u;
     u32x4* h = (u32x4*)O;
-    h[0] = u32x4{OL.size, A, tot_mem, tot_dot};
-    h[1] = u32x4{nd, ndd, ndm, 0u};
+    h[0] = u32x4{OL.size, n_clk, tot_mem, tot_dot};
+    h[1] = u32x4{nd, ndd, ndm, SP ? kSparseClock : 0u};
   }
 }
 
@@ -1219,6 +1290,57 @@ __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
   }
 }
 
+// ======================================================================
+// Sparse (CSR) top-clock batches (config 5: 1024-actor universe): one wave
+// per object pair, grid-stride over objects, both records staged through
+// LDS when they fit (else read from HBM), joined by merge_object<true>.
+// ======================================================================
+constexpr uint32_t kSpStage = 4096;
+
+__device__ __forceinline__ bool sparse_header_ok(u32x4 h0, u32x4 h1, uint64_t off, uint64_t bytes, uint32_t A) {
+  const uint64_t sz = record_size64(h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, true);
+  return (off & 15u) == 0 && off + kHdrBytes <= bytes && sz == h0.x && h0.y <= A && h1.w == kSparseClock &&
+         off + sz <= bytes;
+}
+
+__global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_sparse_kernel(
+    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
+    const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
+    uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
+    int* __restrict__ status) {
+  __shared__ u32x4 sp_s[kWavesPerBlock][2][kSpStage / 16];
+  const uint32_t lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t o = (uint64_t)blockIdx.x * kWavesPerBlock + wave; o < n_obj; o += n_waves) {
+    const uint64_t lo = Loff[o], ro = Roff[o];
+    u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
+    const bool inb = (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes && ro + kHdrBytes <= Rbytes;
+    if (inb) {
+      hl0 = ((const u32x4*)(Lb + lo))[0]; hl1 = ((const u32x4*)(Lb + lo))[1];
+      hr0 = ((const u32x4*)(Rb + ro))[0]; hr1 = ((const u32x4*)(Rb + ro))[1];
+    }
+    const bool ok = inb && sparse_header_ok(hl0, hl1, lo, Lbytes, A) && sparse_header_ok(hr0, hr1, ro, Rbytes, A) &&
+                    lo + ro + (uint64_t)hl0.x + hr0.x <= Obytes;
+    if (lane == 0u) Ooff[o] = lo + ro;
+    if (!ok) {
+      if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
+      continue;
+    }
+    const uint32_t szl = uni(hl0.x), szr = uni(hr0.x);
+    if (szl <= kSpStage && szr <= kSpStage) {
+      u32x4* sl = sp_s[wave][0];
+      u32x4* sr = sp_s[wave][1];
+      wave_sync();
+      for (uint32_t k = lane; k < szl / 16u; k += kWave) sl[k] = __builtin_nontemporal_load((const u32x4*)(Lb + lo) + k);
+      for (uint32_t k = lane; k < szr / 16u; k += kWave) sr[k] = __builtin_nontemporal_load((const u32x4*)(Rb + ro) + k);
+      wave_sync();
+      merge_object<true>((const uint8_t*)sl, (const uint8_t*)sr, Ob + lo + ro, A, lane);
+    } else {
+      merge_object<true>(Lb + lo, Rb + ro, Ob + lo + ro, A, lane);
+    }
+  }
+}
+
 }  // namespace
 
 int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
@@ -1269,6 +1391,24 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
     return CRDT_EHIP;
   hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
                      Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
+  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+}
+
+int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
+                               const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
+                               uint64_t n_obj, uint32_t n_actors, int* status, hipStream_t stream) {
+  if (n_obj == 0) return CRDT_OK;
+  int dev = 0, cus = 256, occ = 0;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)orswot_merge_sparse_kernel,
+                                                   kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)
+    occ = 4;
+  const uint64_t want = (n_obj + kWavesPerBlock - 1) / kWavesPerBlock;
+  const uint64_t cap = (uint64_t)cus * occ;
+  const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
+  hipLaunchKernelGGL(orswot_merge_sparse_kernel, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, stream, Lb, Loff,
+                     Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors, status);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 

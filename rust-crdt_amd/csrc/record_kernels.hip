@@ -13,16 +13,24 @@ __device__ __forceinline__ void fail(int* status) { atomicCAS(status, 0, CRDT_EN
 
 // One lane per record. Checks every invariant listed in include/crdts_hip.h.
 __global__ void validate_kernel(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-                                uint64_t bytes, uint64_t n_obj, uint32_t A, int* status) {
+                                uint64_t bytes, uint64_t n_obj, uint32_t A, uint32_t flags, int* status) {
   uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (i >= n_obj) return;
   uint64_t o = off[i];
   if ((o & 15u) || o + kHdrBytes > bytes) return fail(status);
   const uint8_t* r = base + o;
   const uint32_t* h = (const uint32_t*)r;
+  const bool sparse = (flags & kSparseClock) != 0;
+  if (h[7] != flags) return fail(status);
   RecLayout L;
-  rec_layout(L, h[1], h[2], h[3], h[4], h[5], h[6]);
-  if (h[0] != L.size || h[1] != A || h[7] != 0 || o + L.size > bytes) return fail(status);
+  rec_layout(L, h[1], h[2], h[3], h[4], h[5], h[6], sparse);
+  if (h[0] != L.size || (sparse ? h[1] > A : h[1] != A) || o + L.size > bytes) return fail(status);
+  if (sparse) {  // CSR top clock: actors strictly increasing and < A, counters > 0
+    const uint64_t* cc = (const uint64_t*)(r + L.o_clk);
+    const uint32_t* ca = (const uint32_t*)(r + L.o_cact);
+    for (uint32_t k = 0; k < L.n_clk; ++k)
+      if (ca[k] >= A || cc[k] == 0 || (k && !(ca[k - 1] < ca[k]))) return fail(status);
+  }
   const uint64_t* key = (const uint64_t*)(r + L.o_key);
   const uint64_t* dctr = (const uint64_t*)(r + L.o_dctr);
   const uint32_t* dact = (const uint32_t*)(r + L.o_dact);
@@ -95,11 +103,11 @@ __global__ __launch_bounds__(256) void copy_kernel(const uint8_t* __restrict__ s
 }  // namespace
 
 int launch_orswot_validate(const uint8_t* base, const uint64_t* off, uint64_t bytes, uint64_t n_obj,
-                           uint32_t n_actors, int* status, hipStream_t stream) {
+                           uint32_t n_actors, uint32_t flags, int* status, hipStream_t stream) {
   if (n_obj == 0) return CRDT_OK;
   uint32_t blocks = (uint32_t)((n_obj + 255) / 256);
   hipLaunchKernelGGL(validate_kernel, dim3(blocks), dim3(256), 0, stream, base, off, bytes, n_obj,
-                     n_actors, status);
+                     n_actors, flags, status);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 

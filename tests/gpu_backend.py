@@ -4,16 +4,17 @@ from __future__ import annotations
 
 
 class GpuBackend:
-    def __init__(self, engine, n_actors=16):
+    def __init__(self, engine, n_actors=16, sparse=False):
         import crdts_hip
 
         self.m = crdts_hip
         self.eng = engine
         self.n_actors = n_actors
+        self.sparse = sparse
         self.merges = 0
 
     def new(self):
-        return self.m.Orswot(self.n_actors)
+        return self.m.Orswot(self.n_actors, sparse=self.sparse)
 
     def clone(self, o):
         return o.clone()

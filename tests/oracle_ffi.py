@@ -35,6 +35,11 @@ def lib():
     L.orc_orswot_merge_batch.restype = C.c_int
     L.orc_orswot_merge_batch.argtypes = [P, P, C.c_size_t, P, P, C.c_size_t, C.c_size_t, C.c_uint32,
                                          P, P, C.c_size_t, C.c_int, C.POINTER(C.c_int64)]
+    L.orc_orswot_merge_batch_ex.restype = C.c_int
+    L.orc_orswot_merge_batch_ex.argtypes = [P, P, C.c_size_t, P, P, C.c_size_t, C.c_size_t, C.c_uint32,
+                                            C.c_uint32, P, P, C.c_size_t, C.c_int, C.POINTER(C.c_int64)]
+    L.orc_obj_encode_ex.restype = C.c_long
+    L.orc_obj_encode_ex.argtypes = [P, C.c_uint32, C.c_uint32, P, C.c_size_t]
     L.orc_orswot_bench.restype = C.c_double
     L.orc_orswot_bench.argtypes = [P, P, C.c_size_t, P, P, C.c_size_t, C.c_size_t, C.c_int]
     L.orc_dense_merge.restype = C.c_int
@@ -146,11 +151,11 @@ class OracleOrswot:
     def deferred_len(self):
         return int(lib().orc_obj_deferred_len(self.h))
 
-    def encode(self, n_actors):
+    def encode(self, n_actors, flags=0):
         cap = 1 << 16
         while True:
             buf = np.zeros(cap, dtype=np.uint8)
-            n = lib().orc_obj_encode(self.h, n_actors, _ptr(buf), cap)
+            n = lib().orc_obj_encode_ex(self.h, n_actors, flags, _ptr(buf), cap)
             if n == -4:
                 cap *= 4
                 continue
@@ -168,16 +173,17 @@ class OracleOrswot:
 
 
 # ------------------------------------------------------------- batches
-def orswot_merge_batch(lbase, loff, rbase, roff, n_actors, threads=8):
-    """Merge record batches (numpy u8 bases, u64 offsets). Returns (base, off)."""
+def orswot_merge_batch(lbase, loff, rbase, roff, n_actors, threads=8, flags=0):
+    """Merge record batches (numpy u8 bases, u64 offsets). Returns (base, off).
+    flags=1: CSR top clocks (inputs and output)."""
     n = len(loff)
     cap = int(lbase.nbytes + rbase.nbytes) + 64
     obase = np.zeros(cap, dtype=np.uint8)
     ooff = np.zeros(n, dtype=np.uint64)
     bad = C.c_int64(-1)
-    rc = lib().orc_orswot_merge_batch(_ptr(lbase), _ptr(loff), lbase.nbytes, _ptr(rbase), _ptr(roff),
-                                      rbase.nbytes, n, n_actors, _ptr(obase), _ptr(ooff), cap, threads,
-                                      C.byref(bad))
+    rc = lib().orc_orswot_merge_batch_ex(_ptr(lbase), _ptr(loff), lbase.nbytes, _ptr(rbase), _ptr(roff),
+                                         rbase.nbytes, n, n_actors, flags, _ptr(obase), _ptr(ooff), cap, threads,
+                                         C.byref(bad))
     if rc != 0:
         raise ValueError(f"oracle merge failed rc={rc} at object {bad.value}")
     return obase, ooff

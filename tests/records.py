@@ -17,8 +17,9 @@ def _pad(x, a):
     return (x + a - 1) // a * a
 
 
-def record_bytes(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem):
-    b = HDR + 8 * n_clk + 12 * (n_mem + n_dot)
+def record_bytes(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem, sparse=False):
+    # sparse (CSR) top clock: u64 ctr[n_clk] + u32 act[n_clk], padded to 8
+    b = HDR + (_pad(12 * n_clk, 8) if sparse else 8 * n_clk) + 12 * (n_mem + n_dot)
     b = _pad(b, 8)
     b += 12 * n_def_dot + 8 * n_def_mem + 8 * n_def
     return _pad(b, 16)
@@ -28,8 +29,9 @@ def _clock_key(pairs):
     return tuple(pairs)  # lexicographic over (actor, counter), prefix first == tuple order
 
 
-def encode(clock, entries, deferred, n_actors):
-    """clock: {a: c}; entries: {m: {a: c}}; deferred: {tuple(sorted pairs): set(m)}."""
+def encode(clock, entries, deferred, n_actors, sparse=False):
+    """clock: {a: c}; entries: {m: {a: c}}; deferred: {tuple(sorted pairs): set(m)}.
+    sparse: the top clock as CSR (header flags bit 0), n_clk = its nnz."""
     mems = sorted(entries)
     runs = [sorted(entries[m].items()) for m in mems]
     defs = sorted(((tuple(sorted(k)) if not isinstance(k, tuple) else k), sorted(v)) for k, v in deferred.items())
@@ -37,15 +39,22 @@ def encode(clock, entries, deferred, n_actors):
     n_def = len(defs)
     n_def_dot = sum(len(d[0]) for d in defs)
     n_def_mem = sum(len(d[1]) for d in defs)
-    size = record_bytes(n_actors, n_mem, n_dot, n_def, n_def_dot, n_def_mem)
+    pairs = sorted((a, c) for a, c in clock.items() if c)
+    n_clk = len(pairs) if sparse else n_actors
+    size = record_bytes(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem, sparse)
     out = bytearray(size)
-    struct.pack_into("<8I", out, 0, size, n_actors, n_mem, n_dot, n_def, n_def_dot, n_def_mem, 0)
+    struct.pack_into("<8I", out, 0, size, n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem, 1 if sparse else 0)
     o = HDR
-    clk = [0] * n_actors
-    for a, c in clock.items():
-        clk[a] = c
-    struct.pack_into(f"<{n_actors}Q", out, o, *clk)
-    o += 8 * n_actors
+    if sparse:
+        struct.pack_into(f"<{n_clk}Q", out, o, *[c for _, c in pairs])
+        struct.pack_into(f"<{n_clk}I", out, o + 8 * n_clk, *[a for a, _ in pairs])
+        o += _pad(12 * n_clk, 8)
+    else:
+        clk = [0] * n_actors
+        for a, c in pairs:
+            clk[a] = c
+        struct.pack_into(f"<{n_actors}Q", out, o, *clk)
+        o += 8 * n_actors
     struct.pack_into(f"<{n_mem}Q", out, o, *mems)
     o += 8 * n_mem
     struct.pack_into(f"<{n_dot}Q", out, o, *[c for r in runs for _, c in r])
@@ -82,7 +91,12 @@ def decode(rec):
     size, n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem, flags = struct.unpack_from("<8I", rec, 0)
     o = HDR
     clk = struct.unpack_from(f"<{n_clk}Q", rec, o)
-    o += 8 * n_clk
+    if flags & 1:
+        cact = struct.unpack_from(f"<{n_clk}I", rec, o + 8 * n_clk)
+        o += _pad(12 * n_clk, 8)
+    else:
+        cact = range(n_clk)
+        o += 8 * n_clk
     keys = struct.unpack_from(f"<{n_mem}Q", rec, o)
     o += 8 * n_mem
     dctr = struct.unpack_from(f"<{n_dot}Q", rec, o)
@@ -108,14 +122,14 @@ def decode(rec):
     for de, me in zip(fdend, fmend):
         deferred.append((list(zip(fact[s:de], fctr[s:de])), list(fkey[t:me])))
         s, t = de, me
-    return dict(size=size, flags=flags, clock={a: c for a, c in enumerate(clk) if c},
+    return dict(size=size, flags=flags, clock={a: c for a, c in zip(cact, clk) if c},
                 entries=entries, deferred=deferred)
 
 
-def from_py(orswot, n_actors):
+def from_py(orswot, n_actors, sparse=False):
     """Encode a crdts_ref.Orswot."""
     return encode(dict(orswot.clock.dots), {m: dict(c.dots) for m, c in orswot.entries.items()},
-                  {tuple(sorted(c.dots.items())): set(s) for c, s in orswot.deferred.items()}, n_actors)
+                  {tuple(sorted(c.dots.items())): set(s) for c, s in orswot.deferred.items()}, n_actors, sparse)
 
 
 def pack_batch(records, align=16):
