@@ -34,7 +34,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", default="orswot", choices=["orswot", "gcounter", "pncounter"])
+    p.add_argument("--workload", default="orswot",
+                   choices=["orswot", "gcounter", "pncounter", "orswot_csr", "gcounter_ae"])
+    p.add_argument("--replicas", type=int, default=8, help="orswot_csr at N=1: replicas folded locally")
     p.add_argument("--n-obj", type=int, default=None, help="objects per GPU")
     p.add_argument("--threads", type=int, default=16, help="host threads (generation, CPU baseline)")
     p.add_argument("--cpu-sample", type=int, default=500_000, help="objects in the CPU-baseline sample")
@@ -270,6 +272,170 @@ def run_dense(args, rank, world, local, kind):
     return res
 
 
+def _timed_steps(args, world, stream, fn):
+    """W warmup + K timed calls of fn(); returns (wall_s over ranks (max), mean event ms on `stream`)."""
+    import numpy as np
+    import torch
+
+    for _ in range(args.warmup):
+        fn()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    barrier(world)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        starts[k].record(stream)
+        fn()
+        ends[k].record(stream)
+    stream.synchronize()
+    barrier(world)
+    wall = max_over_ranks(time.perf_counter() - t0, world)
+    return wall, float(np.mean([a.elapsed_time(b) for a, b in zip(starts, ends)]))
+
+
+def run_orswot_csr(args, rank, world, local):
+    """Config 5 (BASELINE.json configs[4]): 1M Orswots with CSR top clocks over
+    a 1024-actor universe; replica anti-entropy. At N > 1 rank r holds replica
+    r and a step is all-gather (RCCL) + rank-order fold of the N replicas; at
+    N = 1 a step folds `--replicas` replicas held locally."""
+    import torch
+
+    import crdts_hip
+    from crdts_hip import replica
+
+    n = args.n_obj or 1_000_000
+    R = world if world > 1 else args.replicas
+    t0 = time.time()
+    reps = crdts_hip.generate_replicas(n, R, threads=args.threads)
+    gen_s = time.time() - t0
+    eng = crdts_hip.Engine(local)
+    SP, U = crdts_hip.SPARSE_CLOCK, crdts_hip.CONFIG5["universe"]
+    stream = torch.cuda.Stream(device=local)
+    if world > 1:
+        mine = crdts_hip.OrswotBatch.from_host(*reps[rank], U, device=local, flags=SP)
+        del reps
+
+        def step():
+            with torch.cuda.stream(stream):
+                return replica.orswot_anti_entropy(eng, mine)
+    else:
+        batches = [crdts_hip.OrswotBatch.from_host(b, o, U, device=local, flags=SP) for b, o in reps]
+        in_bytes = sum(int(b.nbytes) for b, _ in reps)
+        del reps
+        # preallocated fold outputs (a merged record is never larger than its inputs)
+        outs, acc = [], batches[0]
+        for B in batches[1:]:
+            outs.append(eng.orswot_alloc_out(acc, B))
+            acc = outs[-1]
+
+        def step():
+            acc = batches[0]
+            for B, o in zip(batches[1:], outs):
+                acc = eng.orswot_merge(acc, B, out=o, stream=stream, check_status=False)
+            return acc
+
+    final = step()
+    eng.status(stream)
+    wall, ev_ms = _timed_steps(args, world, stream, step)
+    eng.status(stream)
+    merges = n * (R - 1)
+    total = sum_over_ranks(float(merges * args.steps), world)
+    res = {
+        "metric": "replica anti-entropy: Orswot object merges/sec (node), CSR clocks, 1024-actor universe",
+        "value": total / wall, "unit": "object-merges/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic: op-simulated replicas (SplitMix64 seed 0xC0FFEE05 ^ object id)",
+        "config": {"workload": f"orswot_csr config5 (BASELINE.json configs[4]): {n} objects x {R} replicas, "
+                               "CSR top clocks, fold ((r0 ⊔ r1) ⊔ r2) ...",
+                   "replicas": R, "n_obj": n, "gen_s": round(gen_s, 2),
+                   "parallelism": "all-gather (RCCL) + local rank-order fold" if world > 1 else "local fold"},
+    }
+    if world == 1:
+        sizes = final.base.view(torch.int32)[(final.off // 4)].cpu().numpy().astype("int64")
+        # algorithmic bytes of the fold: every merge reads both inputs and writes its output;
+        # intermediate sizes are bounded by the final one, so this is a lower bound
+        alg = in_bytes + (R - 1) * int(sizes.sum()) + 3 * 8 * n * (R - 1)
+        ach = alg / (ev_ms * 1e-3) / 1e9
+        res["roofline"] = {"bound": "hbm", "kernel": "orswot_merge_sparse_kernel", "achieved": ach,
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                           "kernel_ms": ev_ms, "alg_bytes_per_launch": alg / (R - 1), "traffic": None}
+        if not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(REPO, "tests"))
+            import oracle_ffi
+
+            m = min(args.cpu_sample // 10, n)
+            sub = crdts_hip.generate_replicas(m, 2, threads=args.threads)
+            th = max(1, min(args.threads, os.cpu_count() or 1))
+            # oracle fold step r0 ⊔ r1 (decode untimed), same record form
+            secs = oracle_ffi.orswot_bench(sub[0][0], sub[0][1], sub[1][0], sub[1][1], th)
+            res["cpu_baseline"] = {"value": m / secs, "unit": "object-merges/s", "cores": th, "kind": "port",
+                                   "sample": f"{m} objects, replica 0 ⊔ replica 1, oracle merge loop, {th} threads"}
+    return res
+
+
+def run_gcounter_ae(args, rank, world, local):
+    """Config 4 (BASELINE.json configs[3]): 1B GCounters x 8 dense actor slots
+    (64 GB of u64 per GPU); replica r increments slot r. At N > 1 a step is the
+    in-place RCCL all-reduce(max) over xGMI (u64-exact); at N = 1 it is the
+    local join of two such replicas (dense_max_kernel)."""
+    import torch
+
+    import crdts_hip
+    from crdts_hip import replica
+
+    n = args.n_obj or 1_000_000_000
+    A = 8
+    dev = f"cuda:{local}"
+    g = torch.Generator(device=dev)
+    g.manual_seed(0xC0FFEE04)
+    base = torch.randint(0, 1 << 40, (n, A), dtype=torch.int64, device=dev, generator=g)
+    g.manual_seed(0xC0FFEE04 + 1 + rank)
+    mine_slot = rank % A
+    base[:, mine_slot] += torch.randint(1, 1 << 20, (n,), dtype=torch.int64, device=dev, generator=g)
+    eng = crdts_hip.Engine(local)
+    stream = torch.cuda.Stream(device=local)
+    if world > 1:
+        native = replica.native_u64_max(dev)
+
+        def step():
+            with torch.cuda.stream(stream):
+                replica.dense_allreduce_max(base, native=native)
+    else:
+        other = base.clone()
+        other[:, (mine_slot + 1) % A] += 1
+        native = None
+
+        def step():
+            eng.dense_merge(base, other, A, "gcounter", stream=stream)
+
+    wall, ev_ms = _timed_steps(args, world, stream, step)
+    bytes_per_gpu = 8 * n * A
+    res = {
+        "metric": "replica anti-entropy: GCounters joined/sec (node), 8 dense actors",
+        "value": sum_over_ranks(float(n * args.steps), world) / wall, "unit": "objects/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic: U[0,2^40) base + per-replica increments of its own slot",
+        "config": {"workload": f"gcounter_ae config4 (BASELINE.json configs[3]): {n} GCounters x {A} slots per GPU",
+                   "bytes_per_gpu": bytes_per_gpu,
+                   "parallelism": (f"RCCL all-reduce(max) over {world} GPUs, "
+                                   f"{'native u64' if native else 'sign-flipped i64'}") if world > 1
+                   else "local replica join (dense_max_kernel)"},
+    }
+    if world > 1:
+        # ring all-reduce bus bandwidth convention: 2 (N-1)/N x bytes / time
+        res["comm"] = {"algbw_GBps": bytes_per_gpu / (ev_ms * 1e-3) / 1e9,
+                       "busbw_GBps": 2 * (world - 1) / world * bytes_per_gpu / (ev_ms * 1e-3) / 1e9,
+                       "xgmi_peak_GBps": 7 * 153}
+    else:
+        ach = 3 * bytes_per_gpu / (ev_ms * 1e-3) / 1e9
+        res["roofline"] = {"bound": "hbm", "kernel": "dense_max_kernel", "achieved": ach, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "kernel_ms": ev_ms,
+                           "alg_bytes_per_launch": 3 * bytes_per_gpu, "traffic": None}
+    return res
+
+
 def main():
     args = parse()
     rank, world, local = dist_setup()
@@ -277,6 +443,10 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     if args.workload == "orswot":
         res = run_orswot(args, rank, world, local)
+    elif args.workload == "orswot_csr":
+        res = run_orswot_csr(args, rank, world, local)
+    elif args.workload == "gcounter_ae":
+        res = run_gcounter_ae(args, rank, world, local)
     else:
         res = run_dense(args, rank, world, local, args.workload)
     if rank == 0:

@@ -31,17 +31,50 @@ def _torch():
     return torch
 
 
-def dense_allreduce_max(rows, group=None, chunk_elems=1 << 28):
+_NATIVE_U64 = {}
+
+
+def native_u64_max(device, group=None):
+    """Whether this backend reduces torch.uint64 with MAX natively (RCCL's
+    ncclUint64 + ncclMax); probed once per device with a 2-element collective
+    whose answer needs unsigned order."""
+    torch = _torch()
+    import torch.distributed as dist
+
+    key = (str(device), id(group))
+    if key not in _NATIVE_U64:
+        ok = False
+        try:
+            rank = dist.get_rank(group)
+            t = torch.tensor([(1 << 63) + 5 if rank == 0 else 7, 3], dtype=torch.uint64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            ok = int(t[0].item()) == (1 << 63) + 5
+        except (RuntimeError, TypeError, ValueError):
+            ok = False
+        _NATIVE_U64[key] = ok
+    return _NATIVE_U64[key]
+
+
+def dense_allreduce_max(rows, group=None, chunk_elems=1 << 28, native=None):
     """In place: rows = max over ranks (u64 semantics) of rows.
 
     `rows` is an int64 tensor holding u64 counters (any shape), on the
-    process's GPU for nccl or on the CPU for gloo. Chunked so the temporary
-    sign flip stays in place and collectives stay <= 2 GiB.
+    process's GPU for nccl or on the CPU for gloo. Where the backend reduces
+    uint64 natively (RCCL ncclUint64/ncclMax; `native`, probed when None) the
+    rows are reduced as uint64 directly; otherwise through the sign flip
+    below. Chunked so collectives stay <= 2 GiB.
     """
     torch = _torch()
     import torch.distributed as dist
 
     flat = rows.view(-1)
+    if native is None:
+        native = native_u64_max(flat.device, group)
+    if native:
+        u = flat.view(torch.uint64)
+        for s in range(0, u.numel(), chunk_elems):
+            dist.all_reduce(u[s:s + chunk_elems], op=dist.ReduceOp.MAX, group=group)
+        return rows
     sign = torch.tensor(SIGN, dtype=torch.int64, device=flat.device)
     for s in range(0, flat.numel(), chunk_elems):
         part = flat[s:s + chunk_elems]
@@ -90,9 +123,10 @@ def orswot_anti_entropy(engine, batch, group=None, merge_fn=None):
 
     parts = orswot_gather(batch.base, batch.off, group)
     merge = merge_fn or (lambda L, R: engine.orswot_merge(L, R))
-    acc = OrswotBatch(parts[0][0], parts[0][1], batch.n_actors, parts[0][0].numel())
+    fl = getattr(batch, "flags", 0)  # dense or CSR top clocks, the same on every rank
+    acc = OrswotBatch(parts[0][0], parts[0][1], batch.n_actors, parts[0][0].numel(), fl)
     for base, off in parts[1:]:
-        acc = merge(acc, OrswotBatch(base, off, batch.n_actors, base.numel()))
+        acc = merge(acc, OrswotBatch(base, off, batch.n_actors, base.numel(), fl))
     return acc
 
 

@@ -82,6 +82,39 @@ def _orswot_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _orswot_sparse_worker(rank, world, port, q):
+    """Config-5 shape: every rank holds replica `rank` of the same objects
+    (CSR top clocks, 1024-actor universe)."""
+    _init(rank, world, port)
+    import crdts_hip
+    import oracle_ffi
+    from crdts_hip import replica
+
+    U, SP = 1024, crdts_hip.SPARSE_CLOCK
+    reps = crdts_hip.generate_replicas(250, world, threads=2)
+    mine = reps[rank]
+    B = crdts_hip.OrswotBatch(torch.from_numpy(mine[0].copy()), torch.from_numpy(mine[1].view(np.int64).copy()), U,
+                              mine[0].nbytes, SP)
+
+    def oracle_merge(L, R):
+        assert L.flags == R.flags == SP
+        ob, oo = oracle_ffi.orswot_merge_batch(L.base.numpy(), L.off.numpy().view(np.uint64), R.base.numpy(),
+                                               R.off.numpy().view(np.uint64), U, threads=2, flags=SP)
+        return crdts_hip.OrswotBatch(torch.from_numpy(ob), torch.from_numpy(oo.view(np.int64)), U, ob.nbytes, SP)
+
+    out = replica.orswot_anti_entropy(None, B, merge_fn=oracle_merge)
+    acc = reps[0]
+    for b, o in reps[1:]:
+        acc = oracle_ffi.orswot_merge_batch(acc[0], acc[1], b, o, U, threads=2, flags=SP)
+    ref = crdts_hip.OrswotBatch(torch.from_numpy(acc[0]), torch.from_numpy(acc[1].view(np.int64)), U, acc[0].nbytes)
+    dg = replica.digest(out)
+    d = torch.tensor([dg - (1 << 64) if dg >= (1 << 63) else dg], dtype=torch.int64)
+    ds = [torch.zeros_like(d) for _ in range(world)]
+    dist.all_gather(ds, d)
+    q.put((rank, [int(x.item()) % (1 << 64) for x in ds], replica.digest(ref), out.records() == ref.records()))
+    dist.destroy_process_group()
+
+
 def _guarded(fn, rank, world, port, q):
     try:
         fn(rank, world, port, q)
@@ -126,4 +159,11 @@ def test_orswot_anti_entropy_gloo(world):
     res = _run(_orswot_worker, world)
     for rank, digests, ref_digest, same in res:
         assert same, f"rank {rank} fold differs from the oracle's rank-order fold"
+        assert len(set(digests)) == 1 and digests[0] == ref_digest
+
+
+def test_orswot_sparse_anti_entropy_gloo():
+    res = _run(_orswot_sparse_worker, 3)
+    for rank, digests, ref_digest, same in res:
+        assert same, f"rank {rank} sparse fold differs from the oracle's rank-order fold"
         assert len(set(digests)) == 1 and digests[0] == ref_digest
