@@ -1076,6 +1076,228 @@ __device__ __forceinline__ uint32_t lean_object(uint8_t* Ls, uint8_t* Rs, u32x4*
   return size / 16u;
 }
 
+
+// ======================================================================
+// Mask path (v6): objects without deferred removes, A <= 32 actors, at most
+// 64 members and 64 dots per side and 64 union members (all of config 3 but
+// the ~7 % with deferred removes). Loop-free rework of the join for the
+// VALU issue rate, with the same rules as merge_object:
+//  1. dot-parallel pass per side: the member of each dot (run-head flags +
+//     mbcnt), its actor / counter kept in registers, and LDS atomic ORs
+//     building per member a 32-bit actor mask and a "survives" mask (the
+//     dot's counter is above the OTHER side's pre-merge top clock);
+//  2. member alignment by rank: every self member binary-searches its key
+//     among the other side's keys and vice versa; the union position is
+//     rank arithmetic (no merge-path twins, no scan);
+//  3. one dot-parallel pass over the other side's dots records, for actors
+//     present on both sides of a shared member, "equal" and "self >= other";
+//  4. per union member the join is pure mask logic (src/orswot.rs:94-138):
+//       lp = ML & (self_only ? ~0 : FL)   rp = MR & FR
+//       useA = (ML & MR & EQ) | (lp & (~rp | GE))   keep = useA | rp
+//     (self-only entries dropped as a whole iff ML & FL == 0, :98-103);
+//  5. every kept dot writes itself at its member's output base + the rank
+//     of its actor in the keep mask — no per-member loop anywhere.
+// Scratch: 3 KB of LDS per wave (kMaskScratch). Returns output 16-B pieces,
+// or kLeanFallback (union > 64 members, or an actor id >= 32).
+// ======================================================================
+constexpr uint32_t kMaskScratch = 3072;
+// scratch byte offsets
+constexpr uint32_t kMsL = 0;       // u32x2 [64]: L member i -> {actor mask, survives mask}
+constexpr uint32_t kMsR = 512;     // u32x2 [64]: R member j
+constexpr uint32_t kEqGe = 1024;   // u32x2 [64]: union member u -> {equal mask, self>=other mask}
+constexpr uint32_t kDesc = 1536;   // u32  [64]: union member u -> type << 16 | i << 8 | j
+constexpr uint32_t kOut = 1792;    // u32x4[64]: union member u -> {keep, useA, out dot base, -}  (1024 B)
+constexpr uint32_t kHeadL = 2816;  // u8   [64]: 1 at the first dot of each L member
+constexpr uint32_t kHeadR = 2880;  // u8   [64]
+constexpr uint32_t kUofI = 2944;   // u8   [64]: L member i -> union member
+constexpr uint32_t kUofJ = 3008;   // u8   [64]: R member j -> union member
+
+// LDS hand-off between lanes of one wave with every LDS op drained (lgkmcnt(0)).
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint32_t below(uint32_t mask, uint32_t x) { return __popc(mask & ((1u << x) - 1u)); }
+
+// #keys of the sorted list at `off` (n of them, n <= 64) strictly below k.
+__device__ __forceinline__ uint32_t rank_below(const uint8_t* b, uint32_t off, uint32_t n, uint64_t k) {
+  uint32_t base = 0;
+  for (uint32_t step = n ? 1u << (31u - __builtin_clz(n)) : 0u; step != 0u; step >>= 1) {  // binary lifting
+    const uint32_t cand = base + step;
+    const uint64_t kc = ld64(b, off + 8u * (cand - 1u));  // garbage beyond n, masked by cand <= n
+    base = (cand <= n && kc < k) ? cand : base;
+  }
+  return base;
+}
+
+template <uint32_t OUTCAP>
+__device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* X, u32x4* Os,
+                                                uint32_t A, uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR,
+                                                uint32_t lane, bool& big) {
+  big = false;
+  const uint32_t key = kHdrBytes + 8u * A;
+  const uint32_t ctrL = key + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
+  const uint32_t ctrR = key + 8u * nR, actR = ctrR + 8u * dR, endR = actR + 4u * dR;
+  const uint64_t lt = (1ull << lane) - 1ull;
+
+  // ---- dots of both sides in registers: actor, counter
+  const bool hdl = lane < dL, hdr = lane < dR;
+  const uint32_t xl = ld32(Ls, actL + 4u * lane), xr = ld32(Rs, actR + 4u * lane);
+  const uint64_t vl = ld64(Ls, ctrL + 8u * lane), vr = ld64(Rs, ctrR + 8u * lane);
+  if (__ballot((hdl && xl >= 32u) || (hdr && xr >= 32u)) != 0ull) return kLeanFallback;
+
+  // ---- 2. member alignment by rank (self first on equal keys)
+  const bool hml = lane < nL, hmr = lane < nR;
+  const uint64_t kl = ld64(Ls, key + 8u * lane), kr = ld64(Rs, key + 8u * lane);
+  const uint32_t rl = rank_below(Rs, key, nR, kl);  // # other keys < my self key
+  const uint32_t rr = rank_below(Ls, key, nL, kr);  // # self keys < my other key
+  const bool eql = hml && rl < nR && ld64(Rs, key + 8u * rl) == kl;
+  const bool eqr = hmr && rr < nL && ld64(Ls, key + 8u * rr) == kr;
+  const uint64_t EL = __ballot(eql), ER = __ballot(eqr);
+  const uint32_t U = nL + nR - (uint32_t)__popcll(EL);
+  if (U > (uint32_t)kWave) return kLeanFallback;
+  const uint32_t ul = lane + rl - mbcnt64(EL);  // # union keys below my self key
+  const uint32_t ur = lane + rr - mbcnt64(ER);
+
+  // ---- 1. per-member masks (LDS atomic OR) and run heads
+  uint32_t* msL = (uint32_t*)(X + kMsL);
+  uint32_t* msR = (uint32_t*)(X + kMsR);
+  uint32_t* eqge = (uint32_t*)(X + kEqGe);
+  wave_sync();
+  *(uint64_t*)(X + kMsL + 8u * lane) = 0ull;
+  *(uint64_t*)(X + kMsR + 8u * lane) = 0ull;
+  *(uint64_t*)(X + kEqGe + 8u * lane) = 0ull;
+  X[kHeadL + lane] = 0u;
+  X[kHeadR + lane] = 0u;
+  const uint32_t el0 = ld32(Ls, endL + 4u * lane - 4u), er0 = ld32(Rs, endR + 4u * lane - 4u);
+  const uint32_t sl = lane ? el0 : 0u, sr = lane ? er0 : 0u;  // run starts
+  if (hml && sl < 64u) X[kHeadL + sl] = 1u;
+  if (hmr && sr < 64u) X[kHeadR + sr] = 1u;
+  if (hml) {
+    *(uint32_t*)(X + kDesc + 4u * ul) = ((eql ? kBoth : kSelf) << 16) | (lane << 8) | (eql ? rl : 0u);
+    X[kUofI + lane] = (uint8_t)ul;
+  }
+  if (hmr) {
+    if (!eqr) *(uint32_t*)(X + kDesc + 4u * ur) = (kOther << 16) | (rr << 8) | lane;
+    X[kUofJ + lane] = (uint8_t)ur;
+  }
+  wave_sync();
+  const uint64_t HL = __ballot(hdl && X[kHeadL + lane] != 0u), HR = __ballot(hdr && X[kHeadR + lane] != 0u);
+  const uint32_t ml = mbcnt64(HL) + ((HL >> lane) & 1ull ? 1u : 0u) - 1u;  // member of my self dot
+  const uint32_t mr = mbcnt64(HR) + ((HR >> lane) & 1ull ? 1u : 0u) - 1u;
+  if (hdl) {
+    const uint64_t t = ld64(Rs, kHdrBytes + 8u * (xl < A ? xl : 0u));
+    const bool up = vl > (xl < A ? t : 0ull);
+    atomicOr(&msL[2u * (ml & 63u)], 1u << xl);
+    if (up) atomicOr(&msL[2u * (ml & 63u) + 1u], 1u << xl);
+  }
+  if (hdr) {
+    const uint64_t t = ld64(Ls, kHdrBytes + 8u * (xr < A ? xr : 0u));
+    const bool up = vr > (xr < A ? t : 0ull);
+    atomicOr(&msR[2u * (mr & 63u)], 1u << xr);
+    if (up) atomicOr(&msR[2u * (mr & 63u) + 1u], 1u << xr);
+  }
+  wave_sync();
+  // ---- 3. actors on both sides of a shared member: equal / self >= other
+  if (hdr) {
+    const uint32_t j = mr & 63u;
+    const uint32_t u = X[kUofJ + j];
+    const uint32_t d = *(const uint32_t*)(X + kDesc + 4u * u);
+    if ((d >> 16) == kBoth) {
+      const uint32_t i = (d >> 8) & 0xFFu;
+      const uint32_t ML = msL[2u * i];
+      if ((ML >> xr) & 1u) {
+        const uint32_t a0 = i ? ld32(Ls, endL + 4u * i - 4u) : 0u;
+        const uint64_t va = ld64(Ls, ctrL + 8u * ((a0 + below(ML, xr)) & 63u));
+        if (va == vr) atomicOr(&eqge[2u * u], 1u << xr);
+        if (va >= vr) atomicOr(&eqge[2u * u + 1u], 1u << xr);
+      }
+    }
+  }
+  wave_sync();
+  // ---- 4. per union member: mask join
+  const bool hu = lane < U;
+  const uint32_t d = hu ? *(const uint32_t*)(X + kDesc + 4u * lane) : 0u;
+  const uint32_t ty = d >> 16, mi = (d >> 8) & 0xFFu, mj = d & 0xFFu;
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  const uint64_t pl = *(const uint64_t*)(X + kMsL + 8u * mi), pr = *(const uint64_t*)(X + kMsR + 8u * mj);
+  const uint64_t pe = *(const uint64_t*)(X + kEqGe + 8u * lane);
+  const uint32_t ML = (ty & kSelf) ? (uint32_t)pl : 0u, FL = (ty & kSelf) ? (uint32_t)(pl >> 32) : 0u;
+  const uint32_t MR = (ty & kOther) ? (uint32_t)pr : 0u, FR = (ty & kOther) ? (uint32_t)(pr >> 32) : 0u;
+  const uint32_t EQ = ty == kBoth ? (uint32_t)pe : 0u, GE = ty == kBoth ? (uint32_t)(pe >> 32) : 0u;
+  const bool self_only = ty == kSelf;
+  const uint32_t lp = self_only ? ML : (ML & FL), rp = MR & FR;
+  const uint32_t useA = (ML & MR & EQ) | (lp & (~rp | GE));
+  uint32_t keep = useA | rp;
+  keep = (self_only && (ML & FL) == 0u) ? 0u : keep;
+  keep = hu ? keep : 0u;
+  const uint32_t c = __popc(keep);
+
+  // ---- 5. output layout (no deferred block)
+  const uint64_t keepm = __ballot(c != 0u);
+  const uint32_t tot_mem = (uint32_t)__popcll(keepm);
+  const uint32_t cincl = scan_incl(c);
+  const uint32_t tot_dot = lane_of(cincl, kWave - 1);
+  const uint32_t o_key = kHdrBytes + 8u * A;
+  const uint32_t o_dctr = o_key + 8u * tot_mem, o_dact = o_dctr + 8u * tot_dot, o_mdend = o_dact + 4u * tot_dot;
+  const uint32_t o_mpad = o_mdend + 4u * tot_mem;
+  const uint32_t size = (((o_mpad + 7u) & ~7u) + 15u) & ~15u;
+  if (size > OUTCAP) {
+    big = true;
+    return 0u;
+  }
+  const uint32_t d0 = cincl - c;
+  // useA restricted to kept actors: a dropped self-only entry writes nothing
+  *(u32x4*)(X + kOut + 16u * lane) = hu ? u32x4{keep, useA & keep, d0, 0u} : zero;
+  uint8_t* O = (uint8_t*)Os;
+  // the copy-out of the previous object read this stage long ago (in-order LDS)
+  if (c != 0u) {
+    const uint32_t midx = mbcnt64(keepm);
+    const uint64_t kk = (ty & kSelf) ? ld64(Ls, key + 8u * mi) : ld64(Rs, key + 8u * mj);
+    *(uint64_t*)(O + o_key + 8u * midx) = kk;
+    *(uint32_t*)(O + o_mdend + 4u * midx) = d0 + c;
+  }
+  for (uint32_t x = lane; x < A; x += kWave) {  // top clock: pointwise max (src/orswot.rs:153)
+    const uint64_t l = ld64(Ls, kHdrBytes + 8u * x), r = ld64(Rs, kHdrBytes + 8u * x);
+    *(uint64_t*)(O + kHdrBytes + 8u * x) = l > r ? l : r;
+  }
+  wave_sync();
+  uint32_t* oact = (uint32_t*)(O + o_dact);
+  uint64_t* octr = (uint64_t*)(O + o_dctr);
+  if (hdl) {  // self dots that survive, at their member's base + actor rank
+    const u32x4 o = *(const u32x4*)(X + kOut + 16u * X[kUofI + (ml & 63u)]);
+    if ((o.y >> xl) & 1u) {
+      const uint32_t idx = o.z + below(o.x, xl);
+      oact[idx] = xl;
+      octr[idx] = vl;
+    }
+  }
+  if (hdr) {  // other dots kept and not covered by a self dot
+    const u32x4 o = *(const u32x4*)(X + kOut + 16u * X[kUofJ + (mr & 63u)]);
+    if (((o.x & ~o.y) >> xr) & 1u) {
+      const uint32_t idx = o.z + below(o.x, xr);
+      oact[idx] = xr;
+      octr[idx] = vr;
+    }
+  }
+  if (lane < 4u) {  // zero the padding (o_mpad .. size, at most 15 bytes) and the header
+    const uint32_t q = o_mpad + 4u * lane;
+    if (q < size) *(uint32_t*)(O + q) = 0u;
+  }
+  if (lane == 0u) {
+    u32x4* h = (u32x4*)O;
+    h[0] = u32x4{size, A, tot_mem, tot_dot};
+    h[1] = zero;
+  }
+  return size / 16u;
+}
+
 // Copy an output record from its LDS stage to HBM: 16-B coalesced,
 // non-temporal stores (the output is not re-read by this kernel).
 __device__ __forceinline__ void copy_out(const u32x4* src, uint8_t* dst, uint32_t n16, uint32_t lane) {
@@ -1099,7 +1321,7 @@ __device__ __forceinline__ void stage(u32x4* dst, const u32x4 (&r)[kPer], uint32
   }
 }
 
-template <int MINW, int ABL, bool LEAN = false, int LABL = 0>
+template <int MINW, int ABL, bool LEAN = false, int LABL = 0, bool MASK = false>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
@@ -1172,7 +1394,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
       stage(sR, pr, nn >> 16, lane);
       wave_sync();
       mark<ABL>(st, 0);  // wait for the prefetched records + stage them
-      copy_out(out_s[wave][par ^ 1u], out_dst, out_n16, lane);
+      copy_out(out_s[wave][MASK ? 0u : par ^ 1u], out_dst, out_n16, lane);
       mark<ABL>(st, 6);
       const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
       const uint32_t m = lane_of(nm, t), d = lane_of(nd, t);
@@ -1184,7 +1406,23 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
       }
       mark<ABL>(st, 1);  // issue the next prefetch
       const FOut fo{out_s[wave][par], Ob + oo, cbase + t, Ooff, ctl, list, list_cap};
-      if ((defs >> t) & 1ull) {
+      const uint32_t nLt = m & 0xFFFFu, nRt = m >> 16, dLt = d & 0xFFFFu, dRt = d >> 16;
+      if (MASK && !((defs >> t) & 1ull) && A <= 32u && nLt <= 64u && nRt <= 64u && dLt <= 64u && dRt <= 64u) {
+        bool big;
+        out_n16 = mask_object<kOutStage>((const uint8_t*)sL, (const uint8_t*)sR, (uint8_t*)out_s[wave][1],
+                                         out_s[wave][0], A, nLt, dLt, nRt, dRt, lane, big);
+        if (big) {  // rare: output larger than the stage -> general kernel
+          if (lane == 0u) {
+            Ooff[cbase + t] |= kPending;
+            const uint32_t e = atomicAdd(&ctl[0], 1u);
+            if (e < list_cap) list[e] = cbase + t;
+          }
+          out_n16 = 0u;
+        }
+        if (out_n16 == kLeanFallback)
+          out_n16 = fast_object<false, ABL>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, nLt, dLt, nRt, dRt,
+                                            lane, st);
+      } else if ((defs >> t) & 1ull) {
         out_n16 = fast_object<true, ABL>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, m & 0xFFFFu, d & 0xFFFFu,
                                          m >> 16, d >> 16, lane, st);
       } else {
@@ -1207,9 +1445,9 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
                                             d & 0xFFFFu, m >> 16, d >> 16, lane, st);
       }
       out_dst = Ob + oo;
-      par ^= 1u;
+      if (!MASK) par ^= 1u;  // the mask path keeps one output stage (its twin is scratch)
     }
-    copy_out(out_s[wave][par ^ 1u], out_dst, out_n16, lane);  // drain the chunk's last object
+    copy_out(out_s[wave][MASK ? 0u : par ^ 1u], out_dst, out_n16, lane);  // drain the chunk's last object
   }
   if (ABL == 9 && lane < 8u) {  // per-wave phase sums -> the context's list buffer
     uint64_t v = 0;
@@ -1356,6 +1594,7 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   const void* fn;
   switch (variant) {
     case 6: fn = (const void*)orswot_merge_kernel<1, 0, true>; break;
+    case 7: fn = (const void*)orswot_merge_kernel<1, 0, false, 0, true>; break;
     case 111: fn = (const void*)orswot_merge_kernel<1, 0, true, 1>; break;
     case 112: fn = (const void*)orswot_merge_kernel<1, 0, true, 2>; break;
     case 113: fn = (const void*)orswot_merge_kernel<1, 0, true, 3>; break;
@@ -1367,12 +1606,13 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
     case 102: fn = (const void*)orswot_merge_kernel<5, 2>; break;
     case 103: fn = (const void*)orswot_merge_kernel<5, 3>; break;
     case 109: fn = (const void*)orswot_merge_kernel<5, 9>; break;
-    default: fn = (const void*)orswot_merge_kernel<1, 0>; break;  // measured best (tools/ab_bench.py)
+    case 1: fn = (const void*)orswot_merge_kernel<1, 0>; break;
+    default: fn = (const void*)orswot_merge_kernel<1, 0, false, 0, true>; break;  // measured best (tools/ab_bench.py)
   }
   // Resident grid: the kernel's occupancy in 4-wave blocks per CU
   // (blocks_per_cu overrides), no more blocks than 64-object chunks need.
   static std::atomic<int> occ_cache[16];  // per variant slot, 0 = not yet queried
-  const int slot = variant >= 1 && variant <= 6 ? variant : variant >= 101 && variant <= 103 ? variant - 95
+  const int slot = variant >= 1 && variant <= 7 ? variant : variant >= 101 && variant <= 103 ? variant - 95
                    : variant == 109 ? 9 : variant >= 111 && variant <= 113 ? variant - 99 : 0;
   int occ = occ_cache[slot].load(std::memory_order_relaxed);
   if (occ == 0) {
