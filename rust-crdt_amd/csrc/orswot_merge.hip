@@ -1136,10 +1136,14 @@ __device__ __forceinline__ uint32_t rank_below(const uint8_t* b, uint32_t off, u
   return base;
 }
 
-template <uint32_t OUTCAP>
+// HD: the object has deferred removes (<= 32 deferred clocks per side):
+// kept dots are checked against the deferred clocks listing their member
+// (apply_deferred -> apply_remove, src/orswot.rs:235-243, 195-211) and the
+// deferred block is the wave-cooperative union + filter (:141-148, :197).
+template <uint32_t OUTCAP, bool HD = false, int ABL = 0>
 __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* X, u32x4* Os,
                                                 uint32_t A, uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR,
-                                                uint32_t lane, bool& big) {
+                                                uint32_t lane, bool& big, Stamps* stp = nullptr) {
   big = false;
   const uint32_t key = kHdrBytes + 8u * A;
   const uint32_t ctrL = key + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
@@ -1164,6 +1168,7 @@ __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t
   if (U > (uint32_t)kWave) return kLeanFallback;
   const uint32_t ul = lane + rl - mbcnt64(EL);  // # union keys below my self key
   const uint32_t ur = lane + rr - mbcnt64(ER);
+  if (ABL == 9) mark<ABL>(*stp, 4);  // dot loads + rank search
 
   // ---- 1. per-member masks (LDS atomic OR) and run heads
   uint32_t* msL = (uint32_t*)(X + kMsL);
@@ -1204,6 +1209,7 @@ __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t
     if (up) atomicOr(&msR[2u * (mr & 63u) + 1u], 1u << xr);
   }
   wave_sync();
+  if (ABL == 9) mark<ABL>(*stp, 5);  // heads + mask atomics
   // ---- 3. actors on both sides of a shared member: equal / self >= other
   if (hdr) {
     const uint32_t j = mr & 63u;
@@ -1221,6 +1227,7 @@ __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t
     }
   }
   wave_sync();
+  if (ABL == 9) mark<ABL>(*stp, 6);  // equal / >= pass
   // ---- 4. per union member: mask join
   const bool hu = lane < U;
   const uint32_t d = hu ? *(const uint32_t*)(X + kDesc + 4u * lane) : 0u;
@@ -1237,39 +1244,66 @@ __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t
   uint32_t keep = useA | rp;
   keep = (self_only && (ML & FL) == 0u) ? 0u : keep;
   keep = hu ? keep : 0u;
+  uint32_t useK = useA & keep;  // a dropped self-only entry writes nothing
+  Side DL{Ls, RV{}}, DR{Rs, RV{}};
+  if (HD) {
+    // deferred removes: a kept dot (x, v) of member k dies if a deferred clock
+    // listing k has D[x] >= v; the dot lanes clear their bit in the keep mask
+    DL = side_of(Ls);
+    DR = side_of(Rs);
+    *(u32x4*)(X + kOut + 16u * lane) = u32x4{keep, useK, 0u, 0u};
+    wave_sync();
+    if (hdl) {
+      uint32_t* ok = (uint32_t*)(X + kOut + 16u * X[kUofI + (ml & 63u)]);
+      if ((ok[1] >> xl) & 1u) {
+        const uint64_t mk = dmask_of(DL, DR, ld64(Ls, key + 8u * (ml & 63u)));
+        if (mk && dkilled(DL, DR, mk, xl, vl)) atomicAnd(ok, ~(1u << xl));
+      }
+    }
+    if (hdr) {
+      uint32_t* ok = (uint32_t*)(X + kOut + 16u * X[kUofJ + (mr & 63u)]);
+      if (((ok[0] & ~ok[1]) >> xr) & 1u) {
+        const uint64_t mk = dmask_of(DL, DR, ld64(Rs, key + 8u * (mr & 63u)));
+        if (mk && dkilled(DL, DR, mk, xr, vr)) atomicAnd(ok, ~(1u << xr));
+      }
+    }
+    wave_sync();
+    keep = *(const uint32_t*)(X + kOut + 16u * lane);
+    useK &= keep;
+  }
   const uint32_t c = __popc(keep);
 
-  // ---- 5. output layout (no deferred block)
+  // ---- 5. output layout
   const uint64_t keepm = __ballot(c != 0u);
   const uint32_t tot_mem = (uint32_t)__popcll(keepm);
   const uint32_t cincl = scan_incl(c);
   const uint32_t tot_dot = lane_of(cincl, kWave - 1);
-  const uint32_t o_key = kHdrBytes + 8u * A;
-  const uint32_t o_dctr = o_key + 8u * tot_mem, o_dact = o_dctr + 8u * tot_dot, o_mdend = o_dact + 4u * tot_dot;
-  const uint32_t o_mpad = o_mdend + 4u * tot_mem;
-  const uint32_t size = (((o_mpad + 7u) & ~7u) + 15u) & ~15u;
+  uint32_t nd = 0, ndd = 0, ndm = 0;
+  if (HD) deferred_pass_wave(DL, DR, A, lane, nd, ndd, ndm, nullptr);
+  RecLayout OL;
+  rec_layout(OL, A, tot_mem, tot_dot, nd, ndd, ndm);
+  const uint32_t size = OL.size;
   if (size > OUTCAP) {
     big = true;
     return 0u;
   }
   const uint32_t d0 = cincl - c;
-  // useA restricted to kept actors: a dropped self-only entry writes nothing
-  *(u32x4*)(X + kOut + 16u * lane) = hu ? u32x4{keep, useA & keep, d0, 0u} : zero;
+  wave_sync();
+  *(u32x4*)(X + kOut + 16u * lane) = hu ? u32x4{keep, useK, d0, 0u} : zero;
   uint8_t* O = (uint8_t*)Os;
-  // the copy-out of the previous object read this stage long ago (in-order LDS)
   if (c != 0u) {
     const uint32_t midx = mbcnt64(keepm);
     const uint64_t kk = (ty & kSelf) ? ld64(Ls, key + 8u * mi) : ld64(Rs, key + 8u * mj);
-    *(uint64_t*)(O + o_key + 8u * midx) = kk;
-    *(uint32_t*)(O + o_mdend + 4u * midx) = d0 + c;
+    *(uint64_t*)(O + OL.o_key + 8u * midx) = kk;
+    *(uint32_t*)(O + OL.o_mdend + 4u * midx) = d0 + c;
   }
   for (uint32_t x = lane; x < A; x += kWave) {  // top clock: pointwise max (src/orswot.rs:153)
     const uint64_t l = ld64(Ls, kHdrBytes + 8u * x), r = ld64(Rs, kHdrBytes + 8u * x);
     *(uint64_t*)(O + kHdrBytes + 8u * x) = l > r ? l : r;
   }
   wave_sync();
-  uint32_t* oact = (uint32_t*)(O + o_dact);
-  uint64_t* octr = (uint64_t*)(O + o_dctr);
+  uint32_t* oact = (uint32_t*)(O + OL.o_dact);
+  uint64_t* octr = (uint64_t*)(O + OL.o_dctr);
   if (hdl) {  // self dots that survive, at their member's base + actor rank
     const u32x4 o = *(const u32x4*)(X + kOut + 16u * X[kUofI + (ml & 63u)]);
     if ((o.y >> xl) & 1u) {
@@ -1286,14 +1320,18 @@ __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t
       octr[idx] = vr;
     }
   }
-  if (lane < 4u) {  // zero the padding (o_mpad .. size, at most 15 bytes) and the header
-    const uint32_t q = o_mpad + 4u * lane;
-    if (q < size) *(uint32_t*)(O + q) = 0u;
+  if (HD) {  // deferred union keyed by clock (:141-148), kept iff !(D <= clock) (:197)
+    DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
+             (uint32_t*)(O + OL.o_fdend), (uint32_t*)(O + OL.o_fmend)};
+    deferred_pass_wave(DL, DR, A, lane, nd, ndd, ndm, &w);
   }
+  // zero padding: member block to 8 (<= 4 B) and record to 16 (<= 12 B)
+  if (lane == 0u && OL.o_def != OL.o_mpad) *(uint32_t*)(O + OL.o_mpad) = 0u;
+  if (lane >= 1u && lane < 4u && OL.o_end + 4u * (lane - 1u) < size) *(uint32_t*)(O + OL.o_end + 4u * (lane - 1u)) = 0u;
   if (lane == 0u) {
     u32x4* h = (u32x4*)O;
     h[0] = u32x4{size, A, tot_mem, tot_dot};
-    h[1] = zero;
+    h[1] = u32x4{nd, ndd, ndm, 0u};
   }
   return size / 16u;
 }
@@ -1321,14 +1359,17 @@ __device__ __forceinline__ void stage(u32x4* dst, const u32x4 (&r)[kPer], uint32
   }
 }
 
-template <int MINW, int ABL, bool LEAN = false, int LABL = 0, bool MASK = false>
+// MASK: non-deferred objects take mask_object. DIRECT (with MASK): outputs
+// are written straight to HBM (no LDS output stage), which frees LDS for a
+// 5th wave per SIMD.
+template <int MINW, int ABL, bool LEAN = false, int LABL = 0, bool MASK = false, bool DIRECT = false>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
     uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
     int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
   __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
-  __shared__ u32x4 out_s[kWavesPerBlock][2][kOutStage / 16];
+  __shared__ u32x4 out_s[kWavesPerBlock][DIRECT ? 1 : 2][(DIRECT ? kMaskScratch : kOutStage) / 16];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wave = threadIdx.x / kWave;
   u32x4* const sL = stage_s[wave][0];
@@ -1394,7 +1435,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
       stage(sR, pr, nn >> 16, lane);
       wave_sync();
       mark<ABL>(st, 0);  // wait for the prefetched records + stage them
-      copy_out(out_s[wave][MASK ? 0u : par ^ 1u], out_dst, out_n16, lane);
+      if (!DIRECT) copy_out(out_s[wave][MASK ? 0u : par ^ 1u], out_dst, out_n16, lane);
       mark<ABL>(st, 6);
       const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
       const uint32_t m = lane_of(nm, t), d = lane_of(nd, t);
@@ -1405,11 +1446,26 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
         prefetch(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
       }
       mark<ABL>(st, 1);  // issue the next prefetch
-      const FOut fo{out_s[wave][par], Ob + oo, cbase + t, Ooff, ctl, list, list_cap};
+      const FOut fo{DIRECT ? (u32x4*)(Ob + oo) : out_s[wave][par], Ob + oo, cbase + t, Ooff, ctl, list, list_cap};
       const uint32_t nLt = m & 0xFFFFu, nRt = m >> 16, dLt = d & 0xFFFFu, dRt = d >> 16;
-      if (MASK && !((defs >> t) & 1ull) && A <= 32u && nLt <= 64u && nRt <= 64u && dLt <= 64u && dRt <= 64u) {
+      if (DIRECT) {
+        uint32_t r = kLeanFallback;
+        bool big = false;
+        if (!((defs >> t) & 1ull) && A <= 32u && nLt <= 64u && nRt <= 64u && dLt <= 64u && dRt <= 64u)
+          r = mask_object<0xFFFFFFFFu>((const uint8_t*)sL, (const uint8_t*)sR, (uint8_t*)out_s[wave][0],
+                                       (u32x4*)(Ob + oo), A, nLt, dLt, nRt, dRt, lane, big);
+        if (r == kLeanFallback) {
+          if ((defs >> t) & 1ull)
+            fast_object<true, ABL, 0xFFFFFFFFu>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, nLt, dLt, nRt, dRt,
+                                                lane, st);
+          else
+            fast_object<false, ABL, 0xFFFFFFFFu>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, nLt, dLt, nRt,
+                                                 dRt, lane, st);
+        }
+        out_n16 = 0u;
+      } else if (MASK && !((defs >> t) & 1ull) && A <= 32u && nLt <= 64u && nRt <= 64u && dLt <= 64u && dRt <= 64u) {
         bool big;
-        out_n16 = mask_object<kOutStage>((const uint8_t*)sL, (const uint8_t*)sR, (uint8_t*)out_s[wave][1],
+        out_n16 = mask_object<kOutStage>((const uint8_t*)sL, (const uint8_t*)sR, (uint8_t*)out_s[wave][DIRECT ? 0 : 1],
                                          out_s[wave][0], A, nLt, dLt, nRt, dRt, lane, big);
         if (big) {  // rare: output larger than the stage -> general kernel
           if (lane == 0u) {
@@ -1447,7 +1503,112 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
       out_dst = Ob + oo;
       if (!MASK) par ^= 1u;  // the mask path keeps one output stage (its twin is scratch)
     }
-    copy_out(out_s[wave][MASK ? 0u : par ^ 1u], out_dst, out_n16, lane);  // drain the chunk's last object
+    if (!DIRECT) copy_out(out_s[wave][MASK ? 0u : par ^ 1u], out_dst, out_n16, lane);  // drain the chunk's last object
+  }
+  if (ABL == 9 && lane < 8u) {  // per-wave phase sums -> the context's list buffer
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v = lane == (uint32_t)k ? st.acc[k] : v;
+    list[wave_id * 8u + lane] = v;
+  }
+}
+
+// ======================================================================
+// Mask kernel (v6): every object that fits the mask path (records <= 2 KB,
+// A <= 32, <= 64 members / dots per side, <= 32 deferred clocks per side)
+// is joined by mask_object and written straight to HBM; everything else is
+// flagged for the general kernel. Only the mask path lives here, which keeps
+// the register budget low enough for 5 waves per SIMD.
+// ======================================================================
+template <int MINW, int ABL = 0>  // ABL 9: diagnostic phase stamps (tools/stamps.py)
+__global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kernel(
+    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
+    const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
+    uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
+    int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
+  __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
+  __shared__ u32x4 scr_s[kWavesPerBlock][kMaskScratch / 16];
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t wave = threadIdx.x / kWave;
+  u32x4* const sL = stage_s[wave][0];
+  u32x4* const sR = stage_s[wave][1];
+  uint8_t* const X = (uint8_t*)scr_s[wave];
+  const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint64_t rounds = (n_obj + n_waves * kWave - 1) / (n_waves * kWave);
+  const uint64_t cs = (n_obj + n_waves * rounds - 1) / (n_waves * rounds);
+  Stamps st{};
+  if (ABL == 9) st.last = stamp();
+  for (uint64_t cbase = wave_id * cs; cbase < n_obj; cbase += n_waves * cs) {
+    // ---- chunk state: lane k <-> object cbase + k
+    const uint64_t obj = cbase + lane;
+    const bool valid = lane < cs && obj < n_obj;
+    uint64_t lo = 0, ro = 0;
+    if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
+    u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
+    bool ok = valid && (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes && ro + kHdrBytes <= Rbytes;
+    if (ok) {
+      hl0 = ((const u32x4*)(Lb + lo))[0]; hl1 = ((const u32x4*)(Lb + lo))[1];
+      hr0 = ((const u32x4*)(Rb + ro))[0]; hr1 = ((const u32x4*)(Rb + ro))[1];
+    }
+    ok = ok && header_ok(hl0, hl1, lo, Lbytes, A) && header_ok(hr0, hr1, ro, Rbytes, A) &&
+         lo + ro + (uint64_t)hl0.x + hr0.x <= Obytes;
+    const bool fast = ok && hl0.x <= kFastStage && hr0.x <= kFastStage && A <= 32u && hl0.z <= 64u &&
+                      hr0.z <= 64u && hl0.w <= 64u && hr0.w <= 64u && hl1.x <= 32u && hr1.x <= 32u;
+    if (valid) Ooff[obj] = (lo + ro) | ((ok && !fast) ? kPending : 0ull);
+    if (ok && !fast) {  // hand the object to the general kernel
+      const uint32_t e = atomicAdd(&ctl[0], 1u);
+      if (e < list_cap) list[e] = obj;
+    }
+    if (__ballot(valid && !ok) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
+    const uint64_t runs = __ballot(fast);
+    if (runs == 0ull) continue;
+    const uint32_t n16 = fast ? (hl0.x / 16u) | ((hr0.x / 16u) << 16) : 0u;
+    const uint32_t nm = hl0.z | (hr0.z << 16), nd = hl0.w | (hr0.w << 16);
+    const uint64_t defs = __ballot(fast && (hl1.x | hr1.x) != 0u);
+
+    // ---- software pipeline: the next object's records are in flight while
+    // the current one is joined from LDS
+    uint64_t pend = runs;
+    uint32_t t = (uint32_t)__builtin_ctzll(pend);
+    u32x4 pl[kPer], pr[kPer];
+    uint32_t nn = lane_of(n16, t);
+    prefetch(pl, Lb + lane_of64(lo, t), nn & 0xFFFFu, lane);
+    prefetch(pr, Rb + lane_of64(ro, t), nn >> 16, lane);
+    mark<ABL>(st, 7);  // chunk state
+    while (pend) {
+      t = (uint32_t)__builtin_ctzll(pend);
+      pend &= pend - 1;
+      nn = lane_of(n16, t);
+      wave_sync();  // previous object's LDS reads are done
+      stage(sL, pl, nn & 0xFFFFu, lane);
+      stage(sR, pr, nn >> 16, lane);
+      wave_sync();
+      mark<ABL>(st, 0);  // wait for the prefetched records + stage them
+      const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
+      const uint32_t m = lane_of(nm, t), d = lane_of(nd, t);
+      if (pend) {
+        const uint32_t u = (uint32_t)__builtin_ctzll(pend);
+        const uint32_t nu = lane_of(n16, u);
+        prefetch(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
+        prefetch(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
+      }
+      mark<ABL>(st, 1);  // issue the next prefetch
+      bool big = false;
+      uint32_t r;
+      if ((defs >> t) & 1ull)
+        r = mask_object<0xFFFFFFFFu, true, ABL>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
+                                                 m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, &st);
+      else
+        r = mask_object<0xFFFFFFFFu, false, ABL>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
+                                                  m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, &st);
+      if (r == kLeanFallback && lane == 0u) {  // union > 64 members or actor >= 32: general kernel
+        Ooff[cbase + t] |= kPending;
+        const uint32_t e = atomicAdd(&ctl[0], 1u);
+        if (e < list_cap) list[e] = cbase + t;
+      }
+      mark<ABL>(st, (defs >> t) & 1ull ? 3 : 2);  // join (2: plain, 3: with deferred removes)
+    }
   }
   if (ABL == 9 && lane < 8u) {  // per-wave phase sums -> the context's list buffer
     uint64_t v = 0;
@@ -1595,6 +1756,12 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   switch (variant) {
     case 6: fn = (const void*)orswot_merge_kernel<1, 0, true>; break;
     case 7: fn = (const void*)orswot_merge_kernel<1, 0, false, 0, true>; break;
+    case 8: fn = (const void*)orswot_merge_kernel<1, 0, false, 0, true, true>; break;
+    case 9: fn = (const void*)orswot_merge_kernel<5, 0, false, 0, true, true>; break;
+    case 10: fn = (const void*)orswot_mask_kernel<5>; break;
+    case 11: fn = (const void*)orswot_mask_kernel<6>; break;
+    case 12: fn = (const void*)orswot_mask_kernel<4>; break;
+    case 14: fn = (const void*)orswot_mask_kernel<5, 9>; break;
     case 111: fn = (const void*)orswot_merge_kernel<1, 0, true, 1>; break;
     case 112: fn = (const void*)orswot_merge_kernel<1, 0, true, 2>; break;
     case 113: fn = (const void*)orswot_merge_kernel<1, 0, true, 3>; break;
@@ -1607,13 +1774,14 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
     case 103: fn = (const void*)orswot_merge_kernel<5, 3>; break;
     case 109: fn = (const void*)orswot_merge_kernel<5, 9>; break;
     case 1: fn = (const void*)orswot_merge_kernel<1, 0>; break;
-    default: fn = (const void*)orswot_merge_kernel<1, 0, false, 0, true>; break;  // measured best (tools/ab_bench.py)
+    case 13: fn = (const void*)orswot_merge_kernel<1, 0, false, 0, true>; break;
+    default: fn = (const void*)orswot_mask_kernel<5>; break;  // measured best (tools/ab_bench.py)
   }
   // Resident grid: the kernel's occupancy in 4-wave blocks per CU
   // (blocks_per_cu overrides), no more blocks than 64-object chunks need.
-  static std::atomic<int> occ_cache[16];  // per variant slot, 0 = not yet queried
-  const int slot = variant >= 1 && variant <= 7 ? variant : variant >= 101 && variant <= 103 ? variant - 95
-                   : variant == 109 ? 9 : variant >= 111 && variant <= 113 ? variant - 99 : 0;
+  static std::atomic<int> occ_cache[20];  // per variant slot, 0 = not yet queried
+  const int slot = variant >= 1 && variant <= 14 ? variant : variant >= 101 && variant <= 103 ? variant - 95
+                   : variant == 109 ? 13 : variant >= 111 && variant <= 113 ? variant - 99 + 3 : 0;
   int occ = occ_cache[slot].load(std::memory_order_relaxed);
   if (occ == 0) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)
@@ -1629,6 +1797,9 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   if (hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
   if (hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) != hipSuccess)
     return CRDT_EHIP;
+  // diagnostic stamp variants reuse the object list for their phase sums:
+  // no general pass after them (their output is not a valid batch anyway)
+  if (variant == 109 || variant == 14) return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
   hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
                      Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;

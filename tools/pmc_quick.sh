@@ -19,7 +19,7 @@ for sub in os.listdir(d):
     f = os.path.join(d, sub, "run_counter_collection.csv")
     if os.path.exists(f):
         for r in csv.DictReader(open(f)):
-            if "orswot_merge_kernel<" in r["Kernel_Name"]:
+            if ("orswot_merge_kernel<" in r["Kernel_Name"] or "orswot_mask_kernel<" in r["Kernel_Name"]):
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 res = {k: sum(v) / len(v) for k, v in agg.items()}
 json.dump(res, open(os.path.join(d, "summary.json"), "w"), indent=1)

@@ -9,8 +9,11 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "rust-crdt_amd"))
 
-PHASES = ["wait+stage", "prefetch issue", "merge path", "count join", "scan+layout(+def count)",
-          "member/def writes to LDS", "copy-out", "chunk state"]
+PHASES = (["wait+stage", "prefetch issue", "merge path", "count join", "scan+layout(+def count)",
+           "member/def writes to LDS", "copy-out", "chunk state"]
+          if os.environ.get("STAMP_VARIANT", "109") == "109" else
+          ["wait+stage", "prefetch issue", "mask: member join + writes", "mask: same (deferred objs)",
+           "mask: dot loads + rank search", "mask: heads + mask atomics", "mask: equal/>= pass", "chunk state"])
 
 
 def main():
@@ -25,9 +28,9 @@ def main():
     L = crdts_hip.OrswotBatch.from_host(lb, lo, 16)
     R = crdts_hip.OrswotBatch.from_host(rb, ro, 16)
     out = eng.orswot_alloc_out(L, R)
-    eng.set_variant(109)
+    eng.set_variant(int(os.environ.get("STAMP_VARIANT", "109")))
     for _ in range(3):
-        eng.orswot_merge(L, R, out=out)
+        eng.orswot_merge(L, R, out=out, check_status=False)
     n = 65536
     buf = np.zeros(n, dtype=np.uint64)
     s = torch.cuda.current_stream()

@@ -19,7 +19,7 @@ import os
 import shutil
 import sys
 
-KERNELS = {"orswot_merge_kernel": "orswot_merge_kernel<", "orswot_merge_general_kernel": "orswot_merge_general_kernel",
+KERNELS = {"orswot_merge_kernel": "orswot_mask_kernel<", "orswot_merge_kernel_v4": "orswot_merge_kernel<", "orswot_merge_general_kernel": "orswot_merge_general_kernel",
            "dense_max_kernel": "dense_max_kernel"}
 
 
