@@ -1100,17 +1100,19 @@ __device__ __forceinline__ uint32_t lean_object(uint8_t* Ls, uint8_t* Rs, u32x4*
 // Scratch: 3 KB of LDS per wave (kMaskScratch). Returns output 16-B pieces,
 // or kLeanFallback (union > 64 members, or an actor id >= 32).
 // ======================================================================
-constexpr uint32_t kMaskScratch = 3072;
-// scratch byte offsets
+constexpr uint32_t kMaskScratch = 3072;  // bytes reserved per wave (mask2_object uses 2 816)
+// mask_object scratch byte offsets (2 048 B used)
 constexpr uint32_t kMsL = 0;       // u32x2 [64]: L member i -> {actor mask, survives mask}
 constexpr uint32_t kMsR = 512;     // u32x2 [64]: R member j
+constexpr uint32_t kOut = 0;       // u32x4[64]: union member u -> {keep, useA, out dot base, -}; overlays
+                                   // msL/msR, which are dead once every union lane has read its masks
 constexpr uint32_t kEqGe = 1024;   // u32x2 [64]: union member u -> {equal mask, self>=other mask}
 constexpr uint32_t kDesc = 1536;   // u32  [64]: union member u -> type << 16 | i << 8 | j
-constexpr uint32_t kOut = 1792;    // u32x4[64]: union member u -> {keep, useA, out dot base, -}  (1024 B)
-constexpr uint32_t kHeadL = 2816;  // u8   [64]: 1 at the first dot of each L member
-constexpr uint32_t kHeadR = 2880;  // u8   [64]
-constexpr uint32_t kUofI = 2944;   // u8   [64]: L member i -> union member
-constexpr uint32_t kUofJ = 3008;   // u8   [64]: R member j -> union member
+constexpr uint32_t kHeadL = 1792;  // u8   [64]: 1 at the first dot of each L member
+constexpr uint32_t kHeadR = 1856;  // u8   [64]
+constexpr uint32_t kUofI = 1920;   // u8   [64]: L member i -> union member
+constexpr uint32_t kUofJ = 1984;   // u8   [64]: R member j -> union member
+constexpr uint32_t kMask1Scratch = 2048;
 
 // LDS hand-off between lanes of one wave with every LDS op drained (lgkmcnt(0)).
 __device__ __forceinline__ void lds_sync() {
@@ -1336,6 +1338,219 @@ __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t
   return size / 16u;
 }
 
+
+// ======================================================================
+// Mask path v2 (v7): the same mask join as mask_object with fewer dependent
+// LDS round trips — no run-head flags, no LDS atomics, no separate pass:
+//  - every member lane reads its own run (the first two dots straight-line,
+//    longer runs — 0.3 % in config 3 — in a loop) and forms its actor mask and
+//    "above the other side's top clock" mask itself, while the rank search
+//    of the member alignment is in flight;
+//  - an other-side member with a shared key reads its partner's run and
+//    forms the "equal" / "self >= other" masks itself;
+//  - the union-member lane writes its own output dots in actor order (bit
+//    order of the keep mask), values from registers for the first two dots
+//    of each run.
+// Scratch (per wave, 2 816 B): msL[64], msR[64] u32x4 {mask, survives, run
+// start, run length}; eqge[64] u32x2 (by other-side member); desc[64].
+// ======================================================================
+constexpr uint32_t k2MsL = 0, k2MsR = 1024, k2Eq = 2048, k2Desc = 2560;
+
+struct Run2 {
+  uint32_t a0, n, x0, x1;
+  uint64_t v0, v1;
+};
+
+// Run of member m (has = the lane owns a member) of a staged record.
+__device__ __forceinline__ Run2 read_run(const uint8_t* S, uint32_t end, uint32_t act, uint32_t ctr, uint32_t m,
+                                         uint32_t nd, bool has) {
+  const uint32_t e0 = ld32(S, end + 4u * m - 4u), e1 = ld32(S, end + 4u * m);
+  const uint32_t hi = e1 < nd ? e1 : nd;  // clamped: a malformed record cannot spin a loop
+  Run2 r;
+  r.a0 = has && m ? (e0 < hi ? e0 : hi) : 0u;
+  r.n = has ? hi - r.a0 : 0u;
+  r.x0 = ld32(S, act + 4u * r.a0);
+  r.x1 = ld32(S, act + 4u * r.a0 + 4u);
+  r.v0 = ld64(S, ctr + 8u * r.a0);
+  r.v1 = ld64(S, ctr + 8u * r.a0 + 8u);
+  return r;
+}
+
+__device__ __forceinline__ uint64_t top_of(const uint8_t* T, uint32_t x, uint32_t A) {
+  const uint64_t t = ld64(T, kHdrBytes + 8u * (x < A ? x : 0u));
+  return x < A ? t : 0ull;
+}
+
+// Actor mask M and "dot above T's top clock" mask F of run r; bad |= an
+// actor id >= 32.
+__device__ __forceinline__ void run_masks(const uint8_t* S, const uint8_t* T, uint32_t act, uint32_t ctr,
+                                          const Run2& r, uint32_t A, uint32_t& M, uint32_t& F, bool& bad) {
+  const uint64_t t0 = top_of(T, r.x0, A), t1 = top_of(T, r.x1, A);
+  const bool h0 = r.n >= 1u, h1 = r.n >= 2u;
+  M = (h0 ? 1u << (r.x0 & 31u) : 0u) | (h1 ? 1u << (r.x1 & 31u) : 0u);
+  F = (h0 && r.v0 > t0 ? 1u << (r.x0 & 31u) : 0u) | (h1 && r.v1 > t1 ? 1u << (r.x1 & 31u) : 0u);
+  bool b = (h0 && r.x0 >= 32u) || (h1 && r.x1 >= 32u);
+  for (uint32_t d = r.a0 + 2u; d < r.a0 + r.n; ++d) {  // runs of 3+ dots
+    const uint32_t x = ld32(S, act + 4u * d);
+    const uint64_t v = ld64(S, ctr + 8u * d);
+    M |= 1u << (x & 31u);
+    F |= v > top_of(T, x, A) ? 1u << (x & 31u) : 0u;
+    b = b || x >= 32u;
+  }
+  bad = bad || b;
+}
+
+// Counter of actor x in run r (x known present; p = its rank in the run).
+__device__ __forceinline__ uint64_t run_value(const uint8_t* S, uint32_t ctr, const Run2& r, uint32_t p) {
+  return p == 0u ? r.v0 : (p == 1u ? r.v1 : ld64(S, ctr + 8u * (r.a0 + p)));
+}
+
+template <uint32_t OUTCAP, bool HD = false, int ABL = 0>
+__device__ __forceinline__ uint32_t mask2_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* X, u32x4* Os,
+                                                 uint32_t A, uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR,
+                                                 uint32_t lane, bool& big, Stamps* stp = nullptr) {
+  big = false;
+  const uint32_t key = kHdrBytes + 8u * A;
+  const uint32_t ctrL = key + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
+  const uint32_t ctrR = key + 8u * nR, actR = ctrR + 8u * dR, endR = actR + 4u * dR;
+  const bool hml = lane < nL, hmr = lane < nR;
+
+  // ---- own runs and masks (member lane i of self, j of other)
+  const Run2 rl_ = read_run(Ls, endL, actL, ctrL, lane, dL, hml);
+  const Run2 rr_ = read_run(Rs, endR, actR, ctrR, lane, dR, hmr);
+  // ---- member alignment by rank (self first on equal keys)
+  const uint64_t kl = ld64(Ls, key + 8u * lane), kr = ld64(Rs, key + 8u * lane);
+  const uint32_t rl = rank_below(Rs, key, nR, kl);  // # other keys < my self key
+  const uint32_t rr = rank_below(Ls, key, nL, kr);  // # self keys < my other key
+  uint32_t ML, FL, MR, FR;
+  bool bad = false;
+  run_masks(Ls, Rs, actL, ctrL, rl_, A, ML, FL, bad);
+  run_masks(Rs, Ls, actR, ctrR, rr_, A, MR, FR, bad);
+  const bool eql = hml && rl < nR && ld64(Rs, key + 8u * rl) == kl;
+  const bool eqr = hmr && rr < nL && ld64(Ls, key + 8u * rr) == kr;
+  const uint64_t EL = __ballot(eql), ER = __ballot(eqr);
+  const uint32_t U = nL + nR - (uint32_t)__popcll(EL);
+  if (U > (uint32_t)kWave || __ballot(bad) != 0ull) return kLeanFallback;
+  const uint32_t ul = lane + rl - mbcnt64(EL);  // # union keys below my self key
+  const uint32_t ur = lane + rr - mbcnt64(ER);
+  if (ABL == 9) mark<ABL>(*stp, 4);  // runs + rank search
+  // ---- shared member (other side): equal / self >= other over common actors
+  uint32_t EQ = 0u, GE = 0u;
+  if (eqr) {
+    const Run2 p = read_run(Ls, endL, actL, ctrL, rr, dL, true);
+    uint32_t MP = (p.n >= 1u ? 1u << (p.x0 & 31u) : 0u) | (p.n >= 2u ? 1u << (p.x1 & 31u) : 0u);
+    for (uint32_t d = p.a0 + 2u; d < p.a0 + p.n; ++d) MP |= 1u << (ld32(Ls, actL + 4u * d) & 31u);
+    for (uint32_t q = 0; q < rr_.n; ++q) {  // my dots (1-2 almost always)
+      const uint32_t y = q == 0u ? rr_.x0 : (q == 1u ? rr_.x1 : ld32(Rs, actR + 4u * (rr_.a0 + q)));
+      const uint64_t w = q == 0u ? rr_.v0 : (q == 1u ? rr_.v1 : ld64(Rs, ctrR + 8u * (rr_.a0 + q)));
+      if ((MP >> (y & 31u)) & 1u) {
+        const uint64_t pv = run_value(Ls, ctrL, p, below(MP, y & 31u));
+        EQ |= pv == w ? 1u << (y & 31u) : 0u;
+        GE |= pv >= w ? 1u << (y & 31u) : 0u;
+      }
+    }
+  }
+  // ---- publish per-member summaries and the union descriptors
+  wave_sync();  // the previous object's readers of this scratch are done
+  if (hml) {
+    *(u32x4*)(X + k2MsL + 16u * lane) = u32x4{ML, FL, rl_.a0, rl_.n};
+    *(uint32_t*)(X + k2Desc + 4u * ul) = ((eql ? kBoth : kSelf) << 16) | (lane << 8) | (eql ? rl : 0u);
+  }
+  if (hmr) {
+    *(u32x4*)(X + k2MsR + 16u * lane) = u32x4{MR, FR, rr_.a0, rr_.n};
+    *(uint64_t*)(X + k2Eq + 8u * lane) = ((uint64_t)GE << 32) | EQ;
+    if (!eqr) *(uint32_t*)(X + k2Desc + 4u * ur) = (kOther << 16) | (rr << 8) | lane;
+  }
+  wave_sync();
+  if (ABL == 9) mark<ABL>(*stp, 5);  // equal / >= + publish
+  // ---- per union member: mask join
+  const bool hu = lane < U;
+  const uint32_t dsc = hu ? *(const uint32_t*)(X + k2Desc + 4u * lane) : 0u;
+  const uint32_t ty = dsc >> 16, mi = (dsc >> 8) & 0xFFu, mj = dsc & 0xFFu;
+  const u32x4 sl = *(const u32x4*)(X + k2MsL + 16u * (mi & 63u)), sr = *(const u32x4*)(X + k2MsR + 16u * (mj & 63u));
+  const uint64_t pe = *(const uint64_t*)(X + k2Eq + 8u * (mj & 63u));
+  const bool hs = (ty & kSelf) != 0u, ho = (ty & kOther) != 0u;
+  const uint32_t uML = hs ? sl.x : 0u, uFL = hs ? sl.y : 0u, uMR = ho ? sr.x : 0u, uFR = ho ? sr.y : 0u;
+  const uint32_t uEQ = ty == kBoth ? (uint32_t)pe : 0u, uGE = ty == kBoth ? (uint32_t)(pe >> 32) : 0u;
+  const bool self_only = ty == kSelf;
+  const uint32_t lp = self_only ? uML : (uML & uFL), rp = uMR & uFR;
+  const uint32_t useA = (uML & uMR & uEQ) | (lp & (~rp | uGE));
+  uint32_t keep = useA | rp;
+  keep = (self_only && (uML & uFL) == 0u) ? 0u : keep;
+  keep = hu ? keep : 0u;
+  // the union lane's runs: first two counters in registers
+  Run2 ra, rb;
+  ra.a0 = hs ? sl.z : 0u; ra.n = hs ? sl.w : 0u;
+  rb.a0 = ho ? sr.z : 0u; rb.n = ho ? sr.w : 0u;
+  ra.v0 = ld64(Ls, ctrL + 8u * ra.a0); ra.v1 = ld64(Ls, ctrL + 8u * ra.a0 + 8u);
+  rb.v0 = ld64(Rs, ctrR + 8u * rb.a0); rb.v1 = ld64(Rs, ctrR + 8u * rb.a0 + 8u);
+  const uint64_t mkey = hs ? ld64(Ls, key + 8u * mi) : ld64(Rs, key + 8u * mj);
+  Side DL{Ls, RV{}}, DR{Rs, RV{}};
+  if (HD) {  // deferred removes: kept dots dying to a deferred clock listing the member
+    DL = side_of(Ls);
+    DR = side_of(Rs);
+    const uint64_t mk = keep ? dmask_of(DL, DR, mkey) : 0ull;
+    if (mk) {
+      for (uint32_t rem = keep; rem; rem &= rem - 1u) {
+        const uint32_t x = (uint32_t)__builtin_ctz(rem);
+        const bool fa = (useA >> x) & 1u;
+        const uint64_t v = fa ? run_value(Ls, ctrL, ra, below(uML, x)) : run_value(Rs, ctrR, rb, below(uMR, x));
+        if (dkilled(DL, DR, mk, x, v)) keep &= ~(1u << x);
+      }
+    }
+  }
+  const uint32_t c = __popc(keep);
+
+  // ---- output layout
+  const uint64_t keepm = __ballot(c != 0u);
+  const uint32_t tot_mem = (uint32_t)__popcll(keepm);
+  const uint32_t cincl = scan_incl(c);
+  const uint32_t tot_dot = lane_of(cincl, kWave - 1);
+  uint32_t nd = 0, ndd = 0, ndm = 0;
+  if (HD) deferred_pass_wave(DL, DR, A, lane, nd, ndd, ndm, nullptr);
+  RecLayout OL;
+  rec_layout(OL, A, tot_mem, tot_dot, nd, ndd, ndm);
+  const uint32_t size = OL.size;
+  if (size > OUTCAP) {
+    big = true;
+    return 0u;
+  }
+  uint8_t* O = (uint8_t*)Os;
+  uint32_t* oact = (uint32_t*)(O + OL.o_dact);
+  uint64_t* octr = (uint64_t*)(O + OL.o_dctr);
+  if (c != 0u) {
+    const uint32_t midx = mbcnt64(keepm);
+    const uint32_t d0 = cincl - c;
+    *(uint64_t*)(O + OL.o_key + 8u * midx) = mkey;
+    *(uint32_t*)(O + OL.o_mdend + 4u * midx) = cincl;
+    uint32_t k = d0;
+    for (uint32_t rem = keep; rem; rem &= rem - 1u, ++k) {  // actor order = bit order
+      const uint32_t x = (uint32_t)__builtin_ctz(rem);
+      const bool fa = (useA >> x) & 1u;
+      const uint64_t v = fa ? run_value(Ls, ctrL, ra, below(uML, x)) : run_value(Rs, ctrR, rb, below(uMR, x));
+      oact[k] = x;
+      octr[k] = v;
+    }
+  }
+  for (uint32_t x = lane; x < A; x += kWave) {  // top clock: pointwise max (src/orswot.rs:153)
+    const uint64_t l = ld64(Ls, kHdrBytes + 8u * x), r = ld64(Rs, kHdrBytes + 8u * x);
+    *(uint64_t*)(O + kHdrBytes + 8u * x) = l > r ? l : r;
+  }
+  if (HD) {  // deferred union keyed by clock (:141-148), kept iff !(D <= clock) (:197)
+    DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
+             (uint32_t*)(O + OL.o_fdend), (uint32_t*)(O + OL.o_fmend)};
+    deferred_pass_wave(DL, DR, A, lane, nd, ndd, ndm, &w);
+  }
+  if (lane == 0u && OL.o_def != OL.o_mpad) *(uint32_t*)(O + OL.o_mpad) = 0u;
+  if (lane >= 1u && lane < 4u && OL.o_end + 4u * (lane - 1u) < size) *(uint32_t*)(O + OL.o_end + 4u * (lane - 1u)) = 0u;
+  if (lane == 0u) {
+    u32x4* h = (u32x4*)O;
+    h[0] = u32x4{size, A, tot_mem, tot_dot};
+    h[1] = u32x4{nd, ndd, ndm, 0u};
+  }
+  return size / 16u;
+}
+
 // Copy an output record from its LDS stage to HBM: 16-B coalesced,
 // non-temporal stores (the output is not re-read by this kernel).
 __device__ __forceinline__ void copy_out(const u32x4* src, uint8_t* dst, uint32_t n16, uint32_t lane) {
@@ -1520,14 +1735,14 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
 // flagged for the general kernel. Only the mask path lives here, which keeps
 // the register budget low enough for 5 waves per SIMD.
 // ======================================================================
-template <int MINW, int ABL = 0>  // ABL 9: diagnostic phase stamps (tools/stamps.py)
+template <int MINW, int ABL = 0, bool M2 = false>  // ABL 9: phase stamps; M2: mask2_object
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
     uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
     int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
   __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
-  __shared__ u32x4 scr_s[kWavesPerBlock][kMaskScratch / 16];
+  __shared__ u32x4 scr_s[kWavesPerBlock][(M2 ? kMaskScratch : kMask1Scratch) / 16];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wave = threadIdx.x / kWave;
   u32x4* const sL = stage_s[wave][0];
@@ -1596,12 +1811,20 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kern
       mark<ABL>(st, 1);  // issue the next prefetch
       bool big = false;
       uint32_t r;
-      if ((defs >> t) & 1ull)
+      if (M2) {
+        if ((defs >> t) & 1ull)
+          r = mask2_object<0xFFFFFFFFu, true, ABL>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
+                                                    m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, &st);
+        else
+          r = mask2_object<0xFFFFFFFFu, false, ABL>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
+                                                     m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, &st);
+      } else if ((defs >> t) & 1ull) {
         r = mask_object<0xFFFFFFFFu, true, ABL>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
                                                  m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, &st);
-      else
+      } else {
         r = mask_object<0xFFFFFFFFu, false, ABL>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
                                                   m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, &st);
+      }
       if (r == kLeanFallback && lane == 0u) {  // union > 64 members or actor >= 32: general kernel
         Ooff[cbase + t] |= kPending;
         const uint32_t e = atomicAdd(&ctl[0], 1u);
@@ -1762,6 +1985,9 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
     case 11: fn = (const void*)orswot_mask_kernel<6>; break;
     case 12: fn = (const void*)orswot_mask_kernel<4>; break;
     case 14: fn = (const void*)orswot_mask_kernel<5, 9>; break;
+    case 15: fn = (const void*)orswot_mask_kernel<5, 0, true>; break;
+    case 16: fn = (const void*)orswot_mask_kernel<5, 9, true>; break;
+    case 17: fn = (const void*)orswot_mask_kernel<4, 0, true>; break;
     case 111: fn = (const void*)orswot_merge_kernel<1, 0, true, 1>; break;
     case 112: fn = (const void*)orswot_merge_kernel<1, 0, true, 2>; break;
     case 113: fn = (const void*)orswot_merge_kernel<1, 0, true, 3>; break;
@@ -1775,13 +2001,13 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
     case 109: fn = (const void*)orswot_merge_kernel<5, 9>; break;
     case 1: fn = (const void*)orswot_merge_kernel<1, 0>; break;
     case 13: fn = (const void*)orswot_merge_kernel<1, 0, false, 0, true>; break;
-    default: fn = (const void*)orswot_mask_kernel<5>; break;  // measured best (tools/ab_bench.py)
+    default: fn = (const void*)orswot_mask_kernel<6>; break;  // measured best (tools/ab_bench.py)
   }
   // Resident grid: the kernel's occupancy in 4-wave blocks per CU
   // (blocks_per_cu overrides), no more blocks than 64-object chunks need.
-  static std::atomic<int> occ_cache[20];  // per variant slot, 0 = not yet queried
-  const int slot = variant >= 1 && variant <= 14 ? variant : variant >= 101 && variant <= 103 ? variant - 95
-                   : variant == 109 ? 13 : variant >= 111 && variant <= 113 ? variant - 99 + 3 : 0;
+  static std::atomic<int> occ_cache[24];  // per variant slot, 0 = not yet queried
+  const int slot = variant >= 1 && variant <= 17 ? variant : variant >= 101 && variant <= 103 ? variant - 95
+                   : variant == 109 ? 18 : variant >= 111 && variant <= 113 ? variant - 92 : 0;
   int occ = occ_cache[slot].load(std::memory_order_relaxed);
   if (occ == 0) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)
@@ -1799,7 +2025,7 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
     return CRDT_EHIP;
   // diagnostic stamp variants reuse the object list for their phase sums:
   // no general pass after them (their output is not a valid batch anyway)
-  if (variant == 109 || variant == 14) return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+  if (variant == 109 || variant == 14 || variant == 16) return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
   hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
                      Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
