@@ -1112,7 +1112,8 @@ constexpr uint32_t kHeadL = 1792;  // u8   [64]: 1 at the first dot of each L me
 constexpr uint32_t kHeadR = 1856;  // u8   [64]
 constexpr uint32_t kUofI = 1920;   // u8   [64]: L member i -> union member
 constexpr uint32_t kUofJ = 1984;   // u8   [64]: R member j -> union member
-constexpr uint32_t kMask1Scratch = 2048;
+constexpr uint32_t kTrash = 2048;  // u64  [64]: per-lane sink for predicated stores / atomics
+constexpr uint32_t kMask1Scratch = 2560;
 
 // LDS hand-off between lanes of one wave with every LDS op drained (lgkmcnt(0)).
 __device__ __forceinline__ void lds_sync() {
@@ -1172,10 +1173,14 @@ __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t
   const uint32_t ur = lane + rr - mbcnt64(ER);
   if (ABL == 9) mark<ABL>(*stp, 4);  // dot loads + rank search
 
-  // ---- 1. per-member masks (LDS atomic OR) and run heads
+  // ---- 1. per-member masks (LDS atomic OR) and run heads. Lane-conditional
+  // LDS stores are predicated by address (a lane with nothing to store writes
+  // its slot of the trash area) and atomics by value (OR 0): no exec-mask
+  // branches on this path.
   uint32_t* msL = (uint32_t*)(X + kMsL);
   uint32_t* msR = (uint32_t*)(X + kMsR);
   uint32_t* eqge = (uint32_t*)(X + kEqGe);
+  const uint32_t tr = kTrash + 8u * lane;  // distinct per lane: no same-address serialisation
   wave_sync();
   *(uint64_t*)(X + kMsL + 8u * lane) = 0ull;
   *(uint64_t*)(X + kMsR + 8u * lane) = 0ull;
@@ -1184,49 +1189,40 @@ __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t
   X[kHeadR + lane] = 0u;
   const uint32_t el0 = ld32(Ls, endL + 4u * lane - 4u), er0 = ld32(Rs, endR + 4u * lane - 4u);
   const uint32_t sl = lane ? el0 : 0u, sr = lane ? er0 : 0u;  // run starts
-  if (hml && sl < 64u) X[kHeadL + sl] = 1u;
-  if (hmr && sr < 64u) X[kHeadR + sr] = 1u;
-  if (hml) {
-    *(uint32_t*)(X + kDesc + 4u * ul) = ((eql ? kBoth : kSelf) << 16) | (lane << 8) | (eql ? rl : 0u);
-    X[kUofI + lane] = (uint8_t)ul;
-  }
-  if (hmr) {
-    if (!eqr) *(uint32_t*)(X + kDesc + 4u * ur) = (kOther << 16) | (rr << 8) | lane;
-    X[kUofJ + lane] = (uint8_t)ur;
-  }
+  X[(hml && sl < 64u) ? kHeadL + sl : tr] = 1u;
+  X[(hmr && sr < 64u) ? kHeadR + sr : tr] = 1u;
+  *(uint32_t*)(X + (hml ? kDesc + 4u * (ul & 63u) : tr)) =
+      ((eql ? kBoth : kSelf) << 16) | (lane << 8) | (eql ? rl : 0u);
+  *(uint32_t*)(X + ((hmr && !eqr) ? kDesc + 4u * (ur & 63u) : tr)) = (kOther << 16) | (rr << 8) | lane;
+  X[kUofI + lane] = (uint8_t)ul;  // slots of lanes without a member are never read
+  X[kUofJ + lane] = (uint8_t)ur;
   wave_sync();
   const uint64_t HL = __ballot(hdl && X[kHeadL + lane] != 0u), HR = __ballot(hdr && X[kHeadR + lane] != 0u);
   const uint32_t ml = mbcnt64(HL) + ((HL >> lane) & 1ull ? 1u : 0u) - 1u;  // member of my self dot
   const uint32_t mr = mbcnt64(HR) + ((HR >> lane) & 1ull ? 1u : 0u) - 1u;
-  if (hdl) {
-    const uint64_t t = ld64(Rs, kHdrBytes + 8u * (xl < A ? xl : 0u));
-    const bool up = vl > (xl < A ? t : 0ull);
-    atomicOr(&msL[2u * (ml & 63u)], 1u << xl);
-    if (up) atomicOr(&msL[2u * (ml & 63u) + 1u], 1u << xl);
-  }
-  if (hdr) {
-    const uint64_t t = ld64(Ls, kHdrBytes + 8u * (xr < A ? xr : 0u));
-    const bool up = vr > (xr < A ? t : 0ull);
-    atomicOr(&msR[2u * (mr & 63u)], 1u << xr);
-    if (up) atomicOr(&msR[2u * (mr & 63u) + 1u], 1u << xr);
+  {
+    const uint64_t tl = ld64(Rs, kHdrBytes + 8u * (xl < A ? xl : 0u)), trr = ld64(Ls, kHdrBytes + 8u * (xr < A ? xr : 0u));
+    const uint64_t bl = hdl ? 1ull << (xl & 31u) : 0ull, br = hdr ? 1ull << (xr & 31u) : 0ull;
+    const bool upl = vl > (xl < A ? tl : 0ull), upr = vr > (xr < A ? trr : 0ull);
+    // {actor mask, survives mask} of the dot's member in one 64-bit OR
+    atomicOr((unsigned long long*)(X + (hdl ? kMsL + 8u * (ml & 63u) : tr)), (unsigned long long)(bl | (upl ? bl << 32 : 0ull)));
+    atomicOr((unsigned long long*)(X + (hdr ? kMsR + 8u * (mr & 63u) : tr)), (unsigned long long)(br | (upr ? br << 32 : 0ull)));
   }
   wave_sync();
   if (ABL == 9) mark<ABL>(*stp, 5);  // heads + mask atomics
   // ---- 3. actors on both sides of a shared member: equal / self >= other
-  if (hdr) {
+  {
     const uint32_t j = mr & 63u;
-    const uint32_t u = X[kUofJ + j];
+    const uint32_t u = X[kUofJ + j] & 63u;
     const uint32_t d = *(const uint32_t*)(X + kDesc + 4u * u);
-    if ((d >> 16) == kBoth) {
-      const uint32_t i = (d >> 8) & 0xFFu;
-      const uint32_t ML = msL[2u * i];
-      if ((ML >> xr) & 1u) {
-        const uint32_t a0 = i ? ld32(Ls, endL + 4u * i - 4u) : 0u;
-        const uint64_t va = ld64(Ls, ctrL + 8u * ((a0 + below(ML, xr)) & 63u));
-        if (va == vr) atomicOr(&eqge[2u * u], 1u << xr);
-        if (va >= vr) atomicOr(&eqge[2u * u + 1u], 1u << xr);
-      }
-    }
+    const uint32_t i = (d >> 8) & 63u;
+    const uint32_t ML = msL[2u * i];
+    const uint32_t x = xr & 31u;
+    const bool sh = hdr && (d >> 16) == kBoth && ((ML >> x) & 1u);
+    const uint32_t a0 = i ? ld32(Ls, endL + 4u * i - 4u) : 0u;
+    const uint64_t va = ld64(Ls, ctrL + 8u * ((a0 + below(ML, x)) & 63u));
+    const uint64_t b = sh ? ((va == vr ? 1ull : 0ull) | (va >= vr ? 1ull << 32 : 0ull)) << x : 0ull;
+    atomicOr((unsigned long long*)(X + (sh ? kEqGe + 8u * u : tr)), (unsigned long long)b);
   }
   wave_sync();
   if (ABL == 9) mark<ABL>(*stp, 6);  // equal / >= pass
