@@ -1128,6 +1128,22 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
 }
 __device__ __forceinline__ uint32_t below(uint32_t mask, uint32_t x) { return __popc(mask & ((1u << x) - 1u)); }
 
+// Both member-alignment ranks in one loop (the two searches' LDS round trips
+// overlap): rl = # other keys < kl, rr = # self keys < kr.
+__device__ __forceinline__ void rank_both(const uint8_t* Ls, const uint8_t* Rs, uint32_t key, uint32_t nL,
+                                          uint32_t nR, uint64_t kl, uint64_t kr, uint32_t& rl, uint32_t& rr) {
+  const uint32_t n = nL > nR ? nL : nR;
+  uint32_t bl = 0, br = 0;
+  for (uint32_t step = n ? 1u << (31u - __builtin_clz(n)) : 0u; step != 0u; step >>= 1) {
+    const uint32_t cl = bl + step, cr = br + step;
+    const uint64_t kcl = ld64(Rs, key + 8u * (cl - 1u)), kcr = ld64(Ls, key + 8u * (cr - 1u));
+    bl = (cl <= nR && kcl < kl) ? cl : bl;
+    br = (cr <= nL && kcr < kr) ? cr : br;
+  }
+  rl = bl;
+  rr = br;
+}
+
 // #keys of the sorted list at `off` (n of them, n <= 64) strictly below k.
 __device__ __forceinline__ uint32_t rank_below(const uint8_t* b, uint32_t off, uint32_t n, uint64_t k) {
   uint32_t base = 0;
@@ -1162,8 +1178,8 @@ __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t
   // ---- 2. member alignment by rank (self first on equal keys)
   const bool hml = lane < nL, hmr = lane < nR;
   const uint64_t kl = ld64(Ls, key + 8u * lane), kr = ld64(Rs, key + 8u * lane);
-  const uint32_t rl = rank_below(Rs, key, nR, kl);  // # other keys < my self key
-  const uint32_t rr = rank_below(Ls, key, nL, kr);  // # self keys < my other key
+  uint32_t rl, rr;  // # other keys < my self key, # self keys < my other key
+  rank_both(Ls, Rs, key, nL, nR, kl, kr, rl, rr);
   const bool eql = hml && rl < nR && ld64(Rs, key + 8u * rl) == kl;
   const bool eqr = hmr && rr < nL && ld64(Ls, key + 8u * rr) == kr;
   const uint64_t EL = __ballot(eql), ER = __ballot(eqr);
@@ -2001,9 +2017,9 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   }
   // Resident grid: the kernel's occupancy in 4-wave blocks per CU
   // (blocks_per_cu overrides), no more blocks than 64-object chunks need.
-  static std::atomic<int> occ_cache[24];  // per variant slot, 0 = not yet queried
-  const int slot = variant >= 1 && variant <= 17 ? variant : variant >= 101 && variant <= 103 ? variant - 95
-                   : variant == 109 ? 18 : variant >= 111 && variant <= 113 ? variant - 92 : 0;
+  static std::atomic<int> occ_cache[26];  // per variant slot, 0 = not yet queried
+  const int slot = variant >= 1 && variant <= 19 ? variant : variant >= 101 && variant <= 103 ? variant - 95
+                   : variant == 109 ? 20 : variant >= 111 && variant <= 113 ? variant - 90 : 0;
   int occ = occ_cache[slot].load(std::memory_order_relaxed);
   if (occ == 0) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)
