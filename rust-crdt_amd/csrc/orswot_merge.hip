@@ -1167,7 +1167,6 @@ __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t
   const uint32_t key = kHdrBytes + 8u * A;
   const uint32_t ctrL = key + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
   const uint32_t ctrR = key + 8u * nR, actR = ctrR + 8u * dR, endR = actR + 4u * dR;
-  const uint64_t lt = (1ull << lane) - 1ull;
 
   // ---- dots of both sides in registers: actor, counter
   const bool hdl = lane < dL, hdr = lane < dR;
@@ -1194,8 +1193,6 @@ __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t
   // its slot of the trash area) and atomics by value (OR 0): no exec-mask
   // branches on this path.
   uint32_t* msL = (uint32_t*)(X + kMsL);
-  uint32_t* msR = (uint32_t*)(X + kMsR);
-  uint32_t* eqge = (uint32_t*)(X + kEqGe);
   const uint32_t tr = kTrash + 8u * lane;  // distinct per lane: no same-address serialisation
   wave_sync();
   *(uint64_t*)(X + kMsL + 8u * lane) = 0ull;
@@ -1586,6 +1583,22 @@ __device__ __forceinline__ void stage(u32x4* dst, const u32x4 (&r)[kPer], uint32
   }
 }
 
+// Branch-free forms for the mask kernel: every lane loads (indices past the
+// record re-read its last piece, in bounds, merged by the address coalescer)
+// and stores its pieces into the 2 KB stage (bytes past the record are never
+// read as record data).
+__device__ __forceinline__ void prefetch_all(u32x4 (&r)[kPer], const uint8_t* src, uint32_t n16, uint32_t lane) {
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t idx = lane + k * kWave;
+    r[k] = __builtin_nontemporal_load((const u32x4*)src + (idx < n16 ? idx : n16 - 1u));
+  }
+}
+__device__ __forceinline__ void stage_all(u32x4* dst, const u32x4 (&r)[kPer], uint32_t lane) {
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) dst[lane + k * kWave] = r[k];
+}
+
 // MASK: non-deferred objects take mask_object. DIRECT (with MASK): outputs
 // are written straight to HBM (no LDS output stage), which frees LDS for a
 // 5th wave per SIMD.
@@ -1800,16 +1813,16 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kern
     uint32_t t = (uint32_t)__builtin_ctzll(pend);
     u32x4 pl[kPer], pr[kPer];
     uint32_t nn = lane_of(n16, t);
-    prefetch(pl, Lb + lane_of64(lo, t), nn & 0xFFFFu, lane);
-    prefetch(pr, Rb + lane_of64(ro, t), nn >> 16, lane);
+    prefetch_all(pl, Lb + lane_of64(lo, t), nn & 0xFFFFu, lane);
+    prefetch_all(pr, Rb + lane_of64(ro, t), nn >> 16, lane);
     mark<ABL>(st, 7);  // chunk state
     while (pend) {
       t = (uint32_t)__builtin_ctzll(pend);
       pend &= pend - 1;
       nn = lane_of(n16, t);
       wave_sync();  // previous object's LDS reads are done
-      stage(sL, pl, nn & 0xFFFFu, lane);
-      stage(sR, pr, nn >> 16, lane);
+      stage_all(sL, pl, lane);
+      stage_all(sR, pr, lane);
       wave_sync();
       mark<ABL>(st, 0);  // wait for the prefetched records + stage them
       const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
@@ -1817,8 +1830,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kern
       if (pend) {
         const uint32_t u = (uint32_t)__builtin_ctzll(pend);
         const uint32_t nu = lane_of(n16, u);
-        prefetch(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
-        prefetch(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
+        prefetch_all(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
+        prefetch_all(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
       }
       mark<ABL>(st, 1);  // issue the next prefetch
       bool big = false;
@@ -2006,11 +2019,10 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
     case 2: fn = (const void*)orswot_merge_kernel<2, 0>; break;
     case 3: fn = (const void*)orswot_merge_kernel<3, 0>; break;
     case 4: fn = (const void*)orswot_merge_kernel<4, 0>; break;
-    case 5: fn = (const void*)orswot_merge_kernel<5, 0>; break;
-    case 101: fn = (const void*)orswot_merge_kernel<5, 1>; break;
-    case 102: fn = (const void*)orswot_merge_kernel<5, 2>; break;
-    case 103: fn = (const void*)orswot_merge_kernel<5, 3>; break;
-    case 109: fn = (const void*)orswot_merge_kernel<5, 9>; break;
+    case 101: fn = (const void*)orswot_merge_kernel<4, 1>; break;
+    case 102: fn = (const void*)orswot_merge_kernel<4, 2>; break;
+    case 103: fn = (const void*)orswot_merge_kernel<4, 3>; break;
+    case 109: fn = (const void*)orswot_merge_kernel<4, 9>; break;
     case 1: fn = (const void*)orswot_merge_kernel<1, 0>; break;
     case 13: fn = (const void*)orswot_merge_kernel<1, 0, false, 0, true>; break;
     default: fn = (const void*)orswot_mask_kernel<6>; break;  // measured best (tools/ab_bench.py)
