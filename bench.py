@@ -309,6 +309,8 @@ def run_orswot_csr(args, rank, world, local):
     reps = crdts_hip.generate_replicas(n, R, threads=args.threads)
     gen_s = time.time() - t0
     eng = crdts_hip.Engine(local)
+    if args.variant is not None:
+        eng.set_variant(args.variant)
     SP, U = crdts_hip.SPARSE_CLOCK, crdts_hip.CONFIG5["universe"]
     stream = torch.cuda.Stream(device=local)
     if world > 1:

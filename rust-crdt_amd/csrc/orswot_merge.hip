@@ -351,18 +351,20 @@ __device__ __forceinline__ int clock_cmp_wave(const Side& X, uint32_t k, const S
   return na == nb ? 0 : (na < nb ? -1 : 1);
 }
 
+template <bool SP = false>
 __device__ __forceinline__ bool def_survives_wave(const Side& X, uint32_t k, const Side& L, const Side& R, uint32_t A,
                                                   uint32_t lane) {
   const uint32_t s = uni(run_begin(X.b, X.v.fdend, k)), e = uni(g32(X.b, X.v.fdend, k));
   bool any = false;
   for (uint32_t d = s + lane; d < e; d += kWave) {
     const uint32_t x = g32(X.b, X.v.fact, d);
-    const uint64_t lc = top(L.b, L.v, x, A), rc = top(R.b, R.v, x, A);
+    const uint64_t lc = topv<SP>(L.b, L.v, x, A), rc = topv<SP>(R.b, R.v, x, A);
     any = any || g64(X.b, X.v.fctr, d) > (lc > rc ? lc : rc);
   }
   return __ballot(any) != 0ull;
 }
 
+template <bool SP = false>
 __device__ void deferred_pass_wave(const Side& L, const Side& R, uint32_t A, uint32_t lane, uint32_t& nd,
                                    uint32_t& ndd, uint32_t& ndm, const DefOut* w) {
   uint32_t k = 0, l = 0;
@@ -372,7 +374,7 @@ __device__ void deferred_pass_wave(const Side& L, const Side& R, uint32_t A, uin
     const int c = k >= nfL ? 1 : (l >= nfR ? -1 : clock_cmp_wave(L, k, R, l, lane));
     const Side& X = c <= 0 ? L : R;
     const uint32_t kx = c <= 0 ? k : l;
-    if (def_survives_wave(X, kx, L, R, A, lane)) {
+    if (def_survives_wave<SP>(X, kx, L, R, A, lane)) {
       const uint32_t s = uni(run_begin(X.b, X.v.fdend, kx)), e = uni(g32(X.b, X.v.fdend, kx));
       if (w)
         for (uint32_t d = s + lane; d < e; d += kWave) {
@@ -1560,6 +1562,252 @@ __device__ __forceinline__ uint32_t mask2_object(const uint8_t* Ls, const uint8_
   return size / 16u;
 }
 
+
+// ======================================================================
+// Sparse mask path: the mask join (mask_object) for CSR top clocks over an
+// actor universe of up to 1 024 ids (config 5). Actors are renumbered per
+// object by their rank in the union of the two top clocks (<= 64 entries,
+// sorted by actor id, so bit order is actor order); a per-wave u8 table maps
+// an actor id to that rank, each lookup verified against the union list (a
+// dot actor outside both top clocks falls back to the generic join). Masks
+// are 64-bit; everything else is mask_object's rules and layout, with the
+// output's top clock the union list itself (pointwise max, sparse form).
+// ======================================================================
+constexpr uint32_t kSpTableN = 1024;
+constexpr uint32_t kSpMsL = 0, kSpMsR = 1024, kSpOut = 0, kSpEq = 2048, kSpDesc = 3072, kSpHeadL = 3328,
+                   kSpHeadR = 3392, kSpUofI = 3456, kSpUofJ = 3520, kSpUcAct = 3584, kSpUcL = 3840, kSpUcR = 4352,
+                   kSpTrash = 4864, kSpTable = 5888;
+constexpr uint32_t kSpScratch = kSpTable + kSpTableN;  // 6 912 B per wave
+
+__device__ __forceinline__ uint32_t below64(uint64_t mask, uint32_t b) {
+  return (uint32_t)__popcll(mask & ((1ull << b) - 1ull));
+}
+
+// # of the n sorted u32 actor ids at `off` strictly below x (n <= 64).
+__device__ __forceinline__ uint32_t rank32(const uint8_t* b, uint32_t off, uint32_t n, uint32_t x) {
+  uint32_t base = 0;
+  for (uint32_t step = n ? 1u << (31u - __builtin_clz(n)) : 0u; step != 0u; step >>= 1) {
+    const uint32_t cand = base + step;
+    base = (cand <= n && ld32(b, off + 4u * (cand - 1u)) < x) ? cand : base;
+  }
+  return base;
+}
+
+template <bool HD>
+__device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* X, uint8_t* O,
+                                                       uint32_t A, uint32_t ncL, uint32_t nL, uint32_t dL,
+                                                       uint32_t ncR, uint32_t nR, uint32_t dR, uint32_t lane) {
+  const uint32_t keyL = kHdrBytes + clock_bytes(ncL, true), keyR = kHdrBytes + clock_bytes(ncR, true);
+  const uint32_t caL = kHdrBytes + 8u * ncL, caR = kHdrBytes + 8u * ncR;  // clock actor lists
+  const uint32_t ctrL = keyL + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
+  const uint32_t ctrR = keyR + 8u * nR, actR = ctrR + 8u * dR, endR = actR + 4u * dR;
+  const uint32_t tr = kSpTrash + 16u * lane;
+
+  // ---- union of the two top clocks (rank arithmetic, as for the members)
+  const bool hcl = lane < ncL, hcr = lane < ncR;
+  const uint32_t cxl = ld32(Ls, caL + 4u * lane), cxr = ld32(Rs, caR + 4u * lane);
+  const uint64_t cvl = ld64(Ls, kHdrBytes + 8u * lane), cvr = ld64(Rs, kHdrBytes + 8u * lane);
+  const uint32_t rcl = rank32(Rs, caR, ncR, cxl), rcr = rank32(Ls, caL, ncL, cxr);
+  const bool eqcl = hcl && rcl < ncR && ld32(Rs, caR + 4u * rcl) == cxl;
+  const bool eqcr = hcr && rcr < ncL && ld32(Ls, caL + 4u * rcr) == cxr;
+  const uint64_t ECL = __ballot(eqcl), ECR = __ballot(eqcr);
+  const uint32_t Uc = ncL + ncR - (uint32_t)__popcll(ECL);
+  if (Uc > (uint32_t)kWave || __ballot((hcl && cxl >= kSpTableN) || (hcr && cxr >= kSpTableN)) != 0ull)
+    return kLeanFallback;
+  const uint32_t ucl = lane + rcl - mbcnt64(ECL), ucr = lane + rcr - mbcnt64(ECR);
+  const uint64_t cvlr = ld64(Rs, kHdrBytes + 8u * rcl);  // other side's counter of a common actor
+
+  // ---- dots and members (as mask_object)
+  const bool hdl = lane < dL, hdr = lane < dR, hml = lane < nL, hmr = lane < nR;
+  const uint32_t xl = ld32(Ls, actL + 4u * lane), xr = ld32(Rs, actR + 4u * lane);
+  const uint64_t vl = ld64(Ls, ctrL + 8u * lane), vr = ld64(Rs, ctrR + 8u * lane);
+  if (__ballot((hdl && xl >= kSpTableN) || (hdr && xr >= kSpTableN)) != 0ull) return kLeanFallback;
+  const uint64_t kl = ld64(Ls, keyL + 8u * lane), kr = ld64(Rs, keyR + 8u * lane);
+  uint32_t rl = 0, rr = 0;
+  {
+    const uint32_t n = nL > nR ? nL : nR;
+    for (uint32_t step = n ? 1u << (31u - __builtin_clz(n)) : 0u; step != 0u; step >>= 1) {
+      const uint32_t cl = rl + step, cr = rr + step;
+      const uint64_t kcl = ld64(Rs, keyR + 8u * (cl - 1u)), kcr = ld64(Ls, keyL + 8u * (cr - 1u));
+      rl = (cl <= nR && kcl < kl) ? cl : rl;
+      rr = (cr <= nL && kcr < kr) ? cr : rr;
+    }
+  }
+  const bool eql = hml && rl < nR && ld64(Rs, keyR + 8u * rl) == kl;
+  const bool eqr = hmr && rr < nL && ld64(Ls, keyL + 8u * rr) == kr;
+  const uint64_t EL = __ballot(eql), ER = __ballot(eqr);
+  const uint32_t U = nL + nR - (uint32_t)__popcll(EL);
+  if (U > (uint32_t)kWave) return kLeanFallback;
+  const uint32_t ul = lane + rl - mbcnt64(EL), ur = lane + rr - mbcnt64(ER);
+
+  wave_sync();  // the previous object's readers of this scratch are done
+  // union clock entries + actor table
+  *(uint32_t*)(X + (hcl ? kSpUcAct + 4u * (ucl & 63u) : tr)) = cxl;
+  *(uint64_t*)(X + (hcl ? kSpUcL + 8u * (ucl & 63u) : tr)) = cvl;
+  *(uint64_t*)(X + (hcl ? kSpUcR + 8u * (ucl & 63u) : tr)) = eqcl ? cvlr : 0ull;
+  X[hcl ? kSpTable + cxl : tr] = (uint8_t)ucl;
+  const bool wr = hcr && !eqcr;
+  *(uint32_t*)(X + (wr ? kSpUcAct + 4u * (ucr & 63u) : tr)) = cxr;
+  *(uint64_t*)(X + (wr ? kSpUcL + 8u * (ucr & 63u) : tr)) = 0ull;
+  *(uint64_t*)(X + (wr ? kSpUcR + 8u * (ucr & 63u) : tr)) = cvr;
+  X[wr ? kSpTable + cxr : tr] = (uint8_t)ucr;
+  // member masks (zeroed), run heads, descriptors
+  *(u32x4*)(X + kSpMsL + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
+  *(u32x4*)(X + kSpMsR + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
+  *(u32x4*)(X + kSpEq + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
+  X[kSpHeadL + lane] = 0u;
+  X[kSpHeadR + lane] = 0u;
+  const uint32_t el0 = ld32(Ls, endL + 4u * lane - 4u), er0 = ld32(Rs, endR + 4u * lane - 4u);
+  const uint32_t sl = lane ? el0 : 0u, sr = lane ? er0 : 0u;
+  X[(hml && sl < 64u) ? kSpHeadL + sl : tr] = 1u;
+  X[(hmr && sr < 64u) ? kSpHeadR + sr : tr] = 1u;
+  *(uint32_t*)(X + (hml ? kSpDesc + 4u * (ul & 63u) : tr)) = ((eql ? kBoth : kSelf) << 16) | (lane << 8) | (eql ? rl : 0u);
+  *(uint32_t*)(X + ((hmr && !eqr) ? kSpDesc + 4u * (ur & 63u) : tr)) = (kOther << 16) | (rr << 8) | lane;
+  X[kSpUofI + lane] = (uint8_t)ul;
+  X[kSpUofJ + lane] = (uint8_t)ur;
+  wave_sync();
+  // dot -> union clock bit (verified), member of the dot
+  const uint32_t bl = X[kSpTable + (xl & (kSpTableN - 1u))] & 63u, br = X[kSpTable + (xr & (kSpTableN - 1u))] & 63u;
+  const bool okl = !hdl || (bl < Uc && *(const uint32_t*)(X + kSpUcAct + 4u * bl) == xl);
+  const bool okr = !hdr || (br < Uc && *(const uint32_t*)(X + kSpUcAct + 4u * br) == xr);
+  if (__ballot(!okl || !okr) != 0ull) return kLeanFallback;  // a dot actor outside both top clocks
+  const uint64_t HL = __ballot(hdl && X[kSpHeadL + lane] != 0u), HR = __ballot(hdr && X[kSpHeadR + lane] != 0u);
+  const uint32_t ml = mbcnt64(HL) + ((HL >> lane) & 1ull ? 1u : 0u) - 1u;
+  const uint32_t mr = mbcnt64(HR) + ((HR >> lane) & 1ull ? 1u : 0u) - 1u;
+  {
+    const uint64_t rc = *(const uint64_t*)(X + kSpUcR + 8u * bl), lc = *(const uint64_t*)(X + kSpUcL + 8u * br);
+    const uint64_t mbl = hdl ? 1ull << bl : 0ull, mbr = hdr ? 1ull << br : 0ull;
+    unsigned long long* pl = (unsigned long long*)(X + (hdl ? kSpMsL + 16u * (ml & 63u) : tr));
+    unsigned long long* pr = (unsigned long long*)(X + (hdr ? kSpMsR + 16u * (mr & 63u) : tr));
+    atomicOr(pl, (unsigned long long)mbl);
+    atomicOr(pl + 1, (unsigned long long)(vl > rc ? mbl : 0ull));
+    atomicOr(pr, (unsigned long long)mbr);
+    atomicOr(pr + 1, (unsigned long long)(vr > lc ? mbr : 0ull));
+  }
+  wave_sync();
+  // actors on both sides of a shared member: equal / self >= other
+  {
+    const uint32_t u = X[kSpUofJ + (mr & 63u)] & 63u;
+    const uint32_t d = *(const uint32_t*)(X + kSpDesc + 4u * u);
+    const uint32_t i = (d >> 8) & 63u;
+    const uint64_t ML = *(const uint64_t*)(X + kSpMsL + 16u * i);
+    const bool sh = hdr && (d >> 16) == kBoth && ((ML >> br) & 1ull);
+    const uint32_t a0 = i ? ld32(Ls, endL + 4u * i - 4u) : 0u;
+    const uint64_t va = ld64(Ls, ctrL + 8u * ((a0 + below64(ML, br)) & 63u));
+    unsigned long long* pe = (unsigned long long*)(X + (sh ? kSpEq + 16u * u : tr));
+    atomicOr(pe, (unsigned long long)(sh && va == vr ? 1ull << br : 0ull));
+    atomicOr(pe + 1, (unsigned long long)(sh && va >= vr ? 1ull << br : 0ull));
+  }
+  wave_sync();
+  // ---- per union member: mask join (src/orswot.rs:94-138)
+  const bool hu = lane < U;
+  const uint32_t dsc = hu ? *(const uint32_t*)(X + kSpDesc + 4u * lane) : 0u;
+  const uint32_t ty = dsc >> 16, mi = (dsc >> 8) & 63u, mj = dsc & 63u;
+  const u32x4 pl4 = *(const u32x4*)(X + kSpMsL + 16u * mi), pr4 = *(const u32x4*)(X + kSpMsR + 16u * mj);
+  const u32x4 pe4 = *(const u32x4*)(X + kSpEq + 16u * lane);
+  const uint64_t zl = ((uint64_t)pl4.y << 32) | pl4.x, zfl = ((uint64_t)pl4.w << 32) | pl4.z;
+  const uint64_t zr = ((uint64_t)pr4.y << 32) | pr4.x, zfr = ((uint64_t)pr4.w << 32) | pr4.z;
+  const uint64_t ML = (ty & kSelf) ? zl : 0ull, FL = (ty & kSelf) ? zfl : 0ull;
+  const uint64_t MR = (ty & kOther) ? zr : 0ull, FR = (ty & kOther) ? zfr : 0ull;
+  const uint64_t EQ = ty == kBoth ? (((uint64_t)pe4.y << 32) | pe4.x) : 0ull;
+  const uint64_t GE = ty == kBoth ? (((uint64_t)pe4.w << 32) | pe4.z) : 0ull;
+  const bool self_only = ty == kSelf;
+  const uint64_t lp = self_only ? ML : (ML & FL), rp = MR & FR;
+  const uint64_t useA = (ML & MR & EQ) | (lp & (~rp | GE));
+  uint64_t keep = useA | rp;
+  keep = (self_only && (ML & FL) == 0ull) ? 0ull : keep;
+  keep = hu ? keep : 0ull;
+  uint64_t useK = useA & keep;
+  Side DL{Ls, RV{}}, DR{Rs, RV{}};
+  if (HD) {  // deferred removes (apply_deferred -> apply_remove, src/orswot.rs:235-243, 195-211)
+    DL = side_of(Ls);
+    DR = side_of(Rs);
+    wave_sync();
+    *(uint64_t*)(X + kSpOut + 32u * lane) = keep;
+    *(uint64_t*)(X + kSpOut + 32u * lane + 8u) = useK;
+    wave_sync();
+    if (hdl) {
+      unsigned long long* ok = (unsigned long long*)(X + kSpOut + 32u * X[kSpUofI + (ml & 63u)]);
+      if ((ok[1] >> bl) & 1ull) {
+        const uint64_t mk = dmask_of(DL, DR, ld64(Ls, keyL + 8u * (ml & 63u)));
+        if (mk && dkilled(DL, DR, mk, xl, vl)) atomicAnd(ok, ~(1ull << bl));
+      }
+    }
+    if (hdr) {
+      unsigned long long* ok = (unsigned long long*)(X + kSpOut + 32u * X[kSpUofJ + (mr & 63u)]);
+      if (((ok[0] & ~ok[1]) >> br) & 1ull) {
+        const uint64_t mk = dmask_of(DL, DR, ld64(Rs, keyR + 8u * (mr & 63u)));
+        if (mk && dkilled(DL, DR, mk, xr, vr)) atomicAnd(ok, ~(1ull << br));
+      }
+    }
+    wave_sync();
+    keep = *(const uint64_t*)(X + kSpOut + 32u * lane);
+    useK &= keep;
+  }
+  const uint32_t c = (uint32_t)__popcll(keep);
+  // ---- output layout (sparse top clock of Uc entries)
+  const uint64_t keepm = __ballot(c != 0u);
+  const uint32_t tot_mem = (uint32_t)__popcll(keepm);
+  const uint32_t cincl = scan_incl(c);
+  const uint32_t tot_dot = lane_of(cincl, kWave - 1);
+  uint32_t nd = 0, ndd = 0, ndm = 0;
+  if (HD) deferred_pass_wave<true>(DL, DR, A, lane, nd, ndd, ndm, nullptr);
+  RecLayout OL;
+  rec_layout(OL, Uc, tot_mem, tot_dot, nd, ndd, ndm, true);
+  const uint32_t size = OL.size;
+  const uint32_t d0 = cincl - c;
+  wave_sync();
+  *(uint64_t*)(X + kSpOut + 32u * lane) = hu ? keep : 0ull;
+  *(uint64_t*)(X + kSpOut + 32u * lane + 8u) = hu ? useK : 0ull;
+  *(uint32_t*)(X + kSpOut + 32u * lane + 16u) = d0;
+  if (c != 0u) {
+    const uint32_t midx = mbcnt64(keepm);
+    const uint64_t kk = (ty & kSelf) ? ld64(Ls, keyL + 8u * mi) : ld64(Rs, keyR + 8u * mj);
+    *(uint64_t*)(O + OL.o_key + 8u * midx) = kk;
+    *(uint32_t*)(O + OL.o_mdend + 4u * midx) = d0 + c;
+  }
+  if (lane < Uc) {  // top clock: the union list, pointwise max (src/orswot.rs:153)
+    const uint64_t a = *(const uint64_t*)(X + kSpUcL + 8u * lane), b = *(const uint64_t*)(X + kSpUcR + 8u * lane);
+    *(uint64_t*)(O + kHdrBytes + 8u * lane) = a > b ? a : b;
+    *(uint32_t*)(O + kHdrBytes + 8u * Uc + 4u * lane) = *(const uint32_t*)(X + kSpUcAct + 4u * lane);
+  }
+  if (lane == 0u && (Uc & 1u)) *(uint32_t*)(O + kHdrBytes + 12u * Uc) = 0u;  // clock section pad to 8
+  wave_sync();
+  uint32_t* oact = (uint32_t*)(O + OL.o_dact);
+  uint64_t* octr = (uint64_t*)(O + OL.o_dctr);
+  if (hdl) {
+    const uint8_t* ob = X + kSpOut + 32u * X[kSpUofI + (ml & 63u)];
+    const uint64_t k = *(const uint64_t*)ob, ua = *(const uint64_t*)(ob + 8);
+    if ((ua >> bl) & 1ull) {
+      const uint32_t idx = *(const uint32_t*)(ob + 16) + below64(k, bl);
+      oact[idx] = xl;
+      octr[idx] = vl;
+    }
+  }
+  if (hdr) {
+    const uint8_t* ob = X + kSpOut + 32u * X[kSpUofJ + (mr & 63u)];
+    const uint64_t k = *(const uint64_t*)ob, ua = *(const uint64_t*)(ob + 8);
+    if (((k & ~ua) >> br) & 1ull) {
+      const uint32_t idx = *(const uint32_t*)(ob + 16) + below64(k, br);
+      oact[idx] = xr;
+      octr[idx] = vr;
+    }
+  }
+  if (HD) {
+    DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
+             (uint32_t*)(O + OL.o_fdend), (uint32_t*)(O + OL.o_fmend)};
+    deferred_pass_wave<true>(DL, DR, A, lane, nd, ndd, ndm, &w);
+  }
+  if (lane == 0u && OL.o_def != OL.o_mpad) *(uint32_t*)(O + OL.o_mpad) = 0u;
+  if (lane >= 1u && lane < 4u && OL.o_end + 4u * (lane - 1u) < size) *(uint32_t*)(O + OL.o_end + 4u * (lane - 1u)) = 0u;
+  if (lane == 0u) {
+    u32x4* h = (u32x4*)O;
+    h[0] = u32x4{size, Uc, tot_mem, tot_dot};
+    h[1] = u32x4{nd, ndd, ndm, kSparseClock};
+  }
+  return size / 16u;
+}
+
 // Copy an output record from its LDS stage to HBM: 16-B coalesced,
 // non-temporal stores (the output is not re-read by this kernel).
 __device__ __forceinline__ void copy_out(const u32x4* src, uint8_t* dst, uint32_t n16, uint32_t lane) {
@@ -1950,12 +2198,14 @@ __device__ __forceinline__ bool sparse_header_ok(u32x4 h0, u32x4 h1, uint64_t of
          off + sz <= bytes;
 }
 
+template <bool MASK>
 __global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_sparse_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
     uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
     int* __restrict__ status) {
   __shared__ u32x4 sp_s[kWavesPerBlock][2][kSpStage / 16];
+  __shared__ u32x4 sx_s[kWavesPerBlock][MASK ? kSpScratch / 16 : 1];
   const uint32_t lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
   for (uint64_t o = (uint64_t)blockIdx.x * kWavesPerBlock + wave; o < n_obj; o += n_waves) {
@@ -1981,7 +2231,18 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_sparse_ke
       for (uint32_t k = lane; k < szl / 16u; k += kWave) sl[k] = __builtin_nontemporal_load((const u32x4*)(Lb + lo) + k);
       for (uint32_t k = lane; k < szr / 16u; k += kWave) sr[k] = __builtin_nontemporal_load((const u32x4*)(Rb + ro) + k);
       wave_sync();
-      merge_object<true>((const uint8_t*)sl, (const uint8_t*)sr, Ob + lo + ro, A, lane);
+      uint32_t r = kLeanFallback;
+      if (MASK && A <= kSpTableN && uni(hl0.y) <= 64u && uni(hr0.y) <= 64u && uni(hl0.z) <= 64u &&
+          uni(hr0.z) <= 64u && uni(hl0.w) <= 64u && uni(hr0.w) <= 64u && uni(hl1.x) <= 32u && uni(hr1.x) <= 32u) {
+        uint8_t* X = (uint8_t*)sx_s[wave];
+        if ((uni(hl1.x) | uni(hr1.x)) != 0u)
+          r = sparse_mask_object<true>((const uint8_t*)sl, (const uint8_t*)sr, X, Ob + lo + ro, A, uni(hl0.y),
+                                       uni(hl0.z), uni(hl0.w), uni(hr0.y), uni(hr0.z), uni(hr0.w), lane);
+        else
+          r = sparse_mask_object<false>((const uint8_t*)sl, (const uint8_t*)sr, X, Ob + lo + ro, A, uni(hl0.y),
+                                        uni(hl0.z), uni(hl0.w), uni(hr0.y), uni(hr0.z), uni(hr0.w), lane);
+      }
+      if (r == kLeanFallback) merge_object<true>((const uint8_t*)sl, (const uint8_t*)sr, Ob + lo + ro, A, lane);
     } else {
       merge_object<true>(Lb + lo, Rb + ro, Ob + lo + ro, A, lane);
     }
@@ -2057,20 +2318,21 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
 
 int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                                const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
-                               uint64_t n_obj, uint32_t n_actors, int* status, hipStream_t stream) {
+                               uint64_t n_obj, uint32_t n_actors, int* status, hipStream_t stream, int sparse_variant) {
   if (n_obj == 0) return CRDT_OK;
   int dev = 0, cus = 256, occ = 0;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)orswot_merge_sparse_kernel,
-                                                   kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)
+  const void* fn = sparse_variant == 1 ? (const void*)orswot_merge_sparse_kernel<false>
+                                        : (const void*)orswot_merge_sparse_kernel<true>;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)
     occ = 4;
   const uint64_t want = (n_obj + kWavesPerBlock - 1) / kWavesPerBlock;
   const uint64_t cap = (uint64_t)cus * occ;
   const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
-  hipLaunchKernelGGL(orswot_merge_sparse_kernel, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, stream, Lb, Loff,
-                     Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors, status);
-  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+  void* args[] = {&Lb, &Loff, &Lbytes, &Rb, &Roff, &Rbytes, &Ob, &Ooff, &Obytes, &n_obj, &n_actors, &status};
+  return hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) == hipSuccess ? CRDT_OK
+                                                                                                       : CRDT_EHIP;
 }
 
 }  // namespace crdts_hip
