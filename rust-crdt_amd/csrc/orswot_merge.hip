@@ -1574,10 +1574,11 @@ __device__ __forceinline__ uint32_t mask2_object(const uint8_t* Ls, const uint8_
 // output's top clock the union list itself (pointwise max, sparse form).
 // ======================================================================
 constexpr uint32_t kSpTableN = 1024;
+// scratch byte offsets; run heads cover 128 dots per side (two 64-dot rounds)
 constexpr uint32_t kSpMsL = 0, kSpMsR = 1024, kSpOut = 0, kSpEq = 2048, kSpDesc = 3072, kSpHeadL = 3328,
-                   kSpHeadR = 3392, kSpUofI = 3456, kSpUofJ = 3520, kSpUcAct = 3584, kSpUcL = 3840, kSpUcR = 4352,
-                   kSpTrash = 4864, kSpTable = 5888;
-constexpr uint32_t kSpScratch = kSpTable + kSpTableN;  // 6 912 B per wave
+                   kSpHeadR = 3456, kSpUofI = 3584, kSpUofJ = 3648, kSpUcAct = 3712, kSpUcL = 3968, kSpUcR = 4480,
+                   kSpTrash = 4992, kSpTable = 6016;
+constexpr uint32_t kSpScratch = kSpTable + kSpTableN;  // 7 040 B per wave
 
 __device__ __forceinline__ uint32_t below64(uint64_t mask, uint32_t b) {
   return (uint32_t)__popcll(mask & ((1ull << b) - 1ull));
@@ -1617,11 +1618,9 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   const uint32_t ucl = lane + rcl - mbcnt64(ECL), ucr = lane + rcr - mbcnt64(ECR);
   const uint64_t cvlr = ld64(Rs, kHdrBytes + 8u * rcl);  // other side's counter of a common actor
 
-  // ---- dots and members (as mask_object)
-  const bool hdl = lane < dL, hdr = lane < dR, hml = lane < nL, hmr = lane < nR;
-  const uint32_t xl = ld32(Ls, actL + 4u * lane), xr = ld32(Rs, actR + 4u * lane);
-  const uint64_t vl = ld64(Ls, ctrL + 8u * lane), vr = ld64(Rs, ctrR + 8u * lane);
-  if (__ballot((hdl && xl >= kSpTableN) || (hdr && xr >= kSpTableN)) != 0ull) return kLeanFallback;
+  // ---- members (as mask_object); dots are handled in rounds of 64 (<= 128 per side)
+  const bool hml = lane < nL, hmr = lane < nR;
+  const uint32_t nrnd = (dL > dR ? dL : dR) > 64u ? 2u : 1u;
   const uint64_t kl = ld64(Ls, keyL + 8u * lane), kr = ld64(Rs, keyR + 8u * lane);
   uint32_t rl = 0, rr = 0;
   {
@@ -1656,25 +1655,36 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   *(u32x4*)(X + kSpMsR + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
   *(u32x4*)(X + kSpEq + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
   X[kSpHeadL + lane] = 0u;
+  X[kSpHeadL + 64u + lane] = 0u;
   X[kSpHeadR + lane] = 0u;
+  X[kSpHeadR + 64u + lane] = 0u;
   const uint32_t el0 = ld32(Ls, endL + 4u * lane - 4u), er0 = ld32(Rs, endR + 4u * lane - 4u);
   const uint32_t sl = lane ? el0 : 0u, sr = lane ? er0 : 0u;
-  X[(hml && sl < 64u) ? kSpHeadL + sl : tr] = 1u;
-  X[(hmr && sr < 64u) ? kSpHeadR + sr : tr] = 1u;
+  X[(hml && sl < 128u) ? kSpHeadL + sl : tr] = 1u;
+  X[(hmr && sr < 128u) ? kSpHeadR + sr : tr] = 1u;
   *(uint32_t*)(X + (hml ? kSpDesc + 4u * (ul & 63u) : tr)) = ((eql ? kBoth : kSelf) << 16) | (lane << 8) | (eql ? rl : 0u);
   *(uint32_t*)(X + ((hmr && !eqr) ? kSpDesc + 4u * (ur & 63u) : tr)) = (kOther << 16) | (rr << 8) | lane;
   X[kSpUofI + lane] = (uint8_t)ul;
   X[kSpUofJ + lane] = (uint8_t)ur;
   wave_sync();
-  // dot -> union clock bit (verified), member of the dot
-  const uint32_t bl = X[kSpTable + (xl & (kSpTableN - 1u))] & 63u, br = X[kSpTable + (xr & (kSpTableN - 1u))] & 63u;
-  const bool okl = !hdl || (bl < Uc && *(const uint32_t*)(X + kSpUcAct + 4u * bl) == xl);
-  const bool okr = !hdr || (br < Uc && *(const uint32_t*)(X + kSpUcAct + 4u * br) == xr);
-  if (__ballot(!okl || !okr) != 0ull) return kLeanFallback;  // a dot actor outside both top clocks
-  const uint64_t HL = __ballot(hdl && X[kSpHeadL + lane] != 0u), HR = __ballot(hdr && X[kSpHeadR + lane] != 0u);
-  const uint32_t ml = mbcnt64(HL) + ((HL >> lane) & 1ull ? 1u : 0u) - 1u;
-  const uint32_t mr = mbcnt64(HR) + ((HR >> lane) & 1ull ? 1u : 0u) - 1u;
-  {
+  // run-head masks of both rounds; the member of dot 64r + lane is
+  // (#heads at or below it) - 1
+  const uint64_t HL0 = __ballot(lane < dL && X[kSpHeadL + lane] != 0u);
+  const uint64_t HL1 = __ballot(64u + lane < dL && X[kSpHeadL + 64u + lane] != 0u);
+  const uint64_t HR0 = __ballot(lane < dR && X[kSpHeadR + lane] != 0u);
+  const uint64_t HR1 = __ballot(64u + lane < dR && X[kSpHeadR + 64u + lane] != 0u);
+  bool foreign = false;
+  for (uint32_t rd = 0; rd < nrnd; ++rd) {  // dot -> union clock bit (verified) -> member masks
+    const uint32_t d = 64u * rd + lane;
+    const bool hdl = d < dL, hdr = d < dR;
+    const uint32_t xl = ld32(Ls, actL + 4u * d), xr = ld32(Rs, actR + 4u * d);
+    const uint64_t vl = ld64(Ls, ctrL + 8u * d), vr = ld64(Rs, ctrR + 8u * d);
+    const uint64_t HL = rd ? HL1 : HL0, HR = rd ? HR1 : HR0;
+    const uint32_t ml = (rd ? (uint32_t)__popcll(HL0) : 0u) + mbcnt64(HL) + ((HL >> lane) & 1ull ? 1u : 0u) - 1u;
+    const uint32_t mr = (rd ? (uint32_t)__popcll(HR0) : 0u) + mbcnt64(HR) + ((HR >> lane) & 1ull ? 1u : 0u) - 1u;
+    const uint32_t bl = X[kSpTable + (xl & (kSpTableN - 1u))] & 63u, br = X[kSpTable + (xr & (kSpTableN - 1u))] & 63u;
+    foreign = foreign || (hdl && (xl >= kSpTableN || bl >= Uc || *(const uint32_t*)(X + kSpUcAct + 4u * bl) != xl)) ||
+              (hdr && (xr >= kSpTableN || br >= Uc || *(const uint32_t*)(X + kSpUcAct + 4u * br) != xr));
     const uint64_t rc = *(const uint64_t*)(X + kSpUcR + 8u * bl), lc = *(const uint64_t*)(X + kSpUcL + 8u * br);
     const uint64_t mbl = hdl ? 1ull << bl : 0ull, mbr = hdr ? 1ull << br : 0ull;
     unsigned long long* pl = (unsigned long long*)(X + (hdl ? kSpMsL + 16u * (ml & 63u) : tr));
@@ -1684,16 +1694,23 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     atomicOr(pr, (unsigned long long)mbr);
     atomicOr(pr + 1, (unsigned long long)(vr > lc ? mbr : 0ull));
   }
+  if (__ballot(foreign) != 0ull) return kLeanFallback;  // a dot actor outside both top clocks
   wave_sync();
-  // actors on both sides of a shared member: equal / self >= other
-  {
+  for (uint32_t rd = 0; rd < nrnd; ++rd) {  // actors on both sides of a shared member: equal / self >= other
+    const uint32_t dd = 64u * rd + lane;
+    const bool hdr = dd < dR;
+    const uint32_t xr = ld32(Rs, actR + 4u * dd);
+    const uint64_t vr = ld64(Rs, ctrR + 8u * dd);
+    const uint32_t br = X[kSpTable + (xr & (kSpTableN - 1u))] & 63u;
+    const uint64_t HR = rd ? HR1 : HR0;
+    const uint32_t mr = (rd ? (uint32_t)__popcll(HR0) : 0u) + mbcnt64(HR) + ((HR >> lane) & 1ull ? 1u : 0u) - 1u;
     const uint32_t u = X[kSpUofJ + (mr & 63u)] & 63u;
     const uint32_t d = *(const uint32_t*)(X + kSpDesc + 4u * u);
     const uint32_t i = (d >> 8) & 63u;
     const uint64_t ML = *(const uint64_t*)(X + kSpMsL + 16u * i);
     const bool sh = hdr && (d >> 16) == kBoth && ((ML >> br) & 1ull);
     const uint32_t a0 = i ? ld32(Ls, endL + 4u * i - 4u) : 0u;
-    const uint64_t va = ld64(Ls, ctrL + 8u * ((a0 + below64(ML, br)) & 63u));
+    const uint64_t va = ld64(Ls, ctrL + 8u * ((a0 + below64(ML, br)) & 127u));
     unsigned long long* pe = (unsigned long long*)(X + (sh ? kSpEq + 16u * u : tr));
     atomicOr(pe, (unsigned long long)(sh && va == vr ? 1ull << br : 0ull));
     atomicOr(pe + 1, (unsigned long long)(sh && va >= vr ? 1ull << br : 0ull));
@@ -1726,18 +1743,28 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     *(uint64_t*)(X + kSpOut + 32u * lane) = keep;
     *(uint64_t*)(X + kSpOut + 32u * lane + 8u) = useK;
     wave_sync();
-    if (hdl) {
-      unsigned long long* ok = (unsigned long long*)(X + kSpOut + 32u * X[kSpUofI + (ml & 63u)]);
-      if ((ok[1] >> bl) & 1ull) {
-        const uint64_t mk = dmask_of(DL, DR, ld64(Ls, keyL + 8u * (ml & 63u)));
-        if (mk && dkilled(DL, DR, mk, xl, vl)) atomicAnd(ok, ~(1ull << bl));
+    for (uint32_t rd = 0; rd < nrnd; ++rd) {
+      const uint32_t d = 64u * rd + lane;
+      const bool hdl = d < dL, hdr = d < dR;
+      const uint32_t xl = ld32(Ls, actL + 4u * d), xr = ld32(Rs, actR + 4u * d);
+      const uint64_t vl = ld64(Ls, ctrL + 8u * d), vr = ld64(Rs, ctrR + 8u * d);
+      const uint32_t bl = X[kSpTable + (xl & (kSpTableN - 1u))] & 63u, br = X[kSpTable + (xr & (kSpTableN - 1u))] & 63u;
+      const uint64_t HL = rd ? HL1 : HL0, HR = rd ? HR1 : HR0;
+      const uint32_t ml = (rd ? (uint32_t)__popcll(HL0) : 0u) + mbcnt64(HL) + ((HL >> lane) & 1ull ? 1u : 0u) - 1u;
+      const uint32_t mr = (rd ? (uint32_t)__popcll(HR0) : 0u) + mbcnt64(HR) + ((HR >> lane) & 1ull ? 1u : 0u) - 1u;
+      if (hdl) {
+        unsigned long long* ok = (unsigned long long*)(X + kSpOut + 32u * X[kSpUofI + (ml & 63u)]);
+        if ((ok[1] >> bl) & 1ull) {
+          const uint64_t mk = dmask_of(DL, DR, ld64(Ls, keyL + 8u * (ml & 63u)));
+          if (mk && dkilled(DL, DR, mk, xl, vl)) atomicAnd(ok, ~(1ull << bl));
+        }
       }
-    }
-    if (hdr) {
-      unsigned long long* ok = (unsigned long long*)(X + kSpOut + 32u * X[kSpUofJ + (mr & 63u)]);
-      if (((ok[0] & ~ok[1]) >> br) & 1ull) {
-        const uint64_t mk = dmask_of(DL, DR, ld64(Rs, keyR + 8u * (mr & 63u)));
-        if (mk && dkilled(DL, DR, mk, xr, vr)) atomicAnd(ok, ~(1ull << br));
+      if (hdr) {
+        unsigned long long* ok = (unsigned long long*)(X + kSpOut + 32u * X[kSpUofJ + (mr & 63u)]);
+        if (((ok[0] & ~ok[1]) >> br) & 1ull) {
+          const uint64_t mk = dmask_of(DL, DR, ld64(Rs, keyR + 8u * (mr & 63u)));
+          if (mk && dkilled(DL, DR, mk, xr, vr)) atomicAnd(ok, ~(1ull << br));
+        }
       }
     }
     wave_sync();
@@ -1775,22 +1802,32 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   wave_sync();
   uint32_t* oact = (uint32_t*)(O + OL.o_dact);
   uint64_t* octr = (uint64_t*)(O + OL.o_dctr);
-  if (hdl) {
-    const uint8_t* ob = X + kSpOut + 32u * X[kSpUofI + (ml & 63u)];
-    const uint64_t k = *(const uint64_t*)ob, ua = *(const uint64_t*)(ob + 8);
-    if ((ua >> bl) & 1ull) {
-      const uint32_t idx = *(const uint32_t*)(ob + 16) + below64(k, bl);
-      oact[idx] = xl;
-      octr[idx] = vl;
+  for (uint32_t rd = 0; rd < nrnd; ++rd) {  // every kept dot at its member's base + actor rank
+    const uint32_t d = 64u * rd + lane;
+    const bool hdl = d < dL, hdr = d < dR;
+    const uint32_t xl = ld32(Ls, actL + 4u * d), xr = ld32(Rs, actR + 4u * d);
+    const uint64_t vl = ld64(Ls, ctrL + 8u * d), vr = ld64(Rs, ctrR + 8u * d);
+    const uint32_t bl = X[kSpTable + (xl & (kSpTableN - 1u))] & 63u, br = X[kSpTable + (xr & (kSpTableN - 1u))] & 63u;
+    const uint64_t HL = rd ? HL1 : HL0, HR = rd ? HR1 : HR0;
+    const uint32_t ml = (rd ? (uint32_t)__popcll(HL0) : 0u) + mbcnt64(HL) + ((HL >> lane) & 1ull ? 1u : 0u) - 1u;
+    const uint32_t mr = (rd ? (uint32_t)__popcll(HR0) : 0u) + mbcnt64(HR) + ((HR >> lane) & 1ull ? 1u : 0u) - 1u;
+    if (hdl) {
+      const uint8_t* ob = X + kSpOut + 32u * X[kSpUofI + (ml & 63u)];
+      const uint64_t k = *(const uint64_t*)ob, ua = *(const uint64_t*)(ob + 8);
+      if ((ua >> bl) & 1ull) {
+        const uint32_t idx = *(const uint32_t*)(ob + 16) + below64(k, bl);
+        oact[idx] = xl;
+        octr[idx] = vl;
+      }
     }
-  }
-  if (hdr) {
-    const uint8_t* ob = X + kSpOut + 32u * X[kSpUofJ + (mr & 63u)];
-    const uint64_t k = *(const uint64_t*)ob, ua = *(const uint64_t*)(ob + 8);
-    if (((k & ~ua) >> br) & 1ull) {
-      const uint32_t idx = *(const uint32_t*)(ob + 16) + below64(k, br);
-      oact[idx] = xr;
-      octr[idx] = vr;
+    if (hdr) {
+      const uint8_t* ob = X + kSpOut + 32u * X[kSpUofJ + (mr & 63u)];
+      const uint64_t k = *(const uint64_t*)ob, ua = *(const uint64_t*)(ob + 8);
+      if (((k & ~ua) >> br) & 1ull) {
+        const uint32_t idx = *(const uint32_t*)(ob + 16) + below64(k, br);
+        oact[idx] = xr;
+        octr[idx] = vr;
+      }
     }
   }
   if (HD) {
@@ -2190,7 +2227,8 @@ __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
 // per object pair, grid-stride over objects, both records staged through
 // LDS when they fit (else read from HBM), joined by merge_object<true>.
 // ======================================================================
-constexpr uint32_t kSpStage = 4096;
+constexpr uint32_t kSpStage = 6144;
+constexpr int kSpWaves = 2;  // waves per block of the sparse kernel (LDS: 2 x (12 KB stage + 7 KB scratch))
 
 __device__ __forceinline__ bool sparse_header_ok(u32x4 h0, u32x4 h1, uint64_t off, uint64_t bytes, uint32_t A) {
   const uint64_t sz = record_size64(h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, true);
@@ -2199,16 +2237,16 @@ __device__ __forceinline__ bool sparse_header_ok(u32x4 h0, u32x4 h1, uint64_t of
 }
 
 template <bool MASK>
-__global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_sparse_kernel(
+__global__ __launch_bounds__(kWave * kSpWaves) void orswot_merge_sparse_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
     uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
     int* __restrict__ status) {
-  __shared__ u32x4 sp_s[kWavesPerBlock][2][kSpStage / 16];
-  __shared__ u32x4 sx_s[kWavesPerBlock][MASK ? kSpScratch / 16 : 1];
+  __shared__ u32x4 sp_s[kSpWaves][2][kSpStage / 16];
+  __shared__ u32x4 sx_s[kSpWaves][MASK ? kSpScratch / 16 : 1];
   const uint32_t lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
-  for (uint64_t o = (uint64_t)blockIdx.x * kWavesPerBlock + wave; o < n_obj; o += n_waves) {
+  const uint64_t n_waves = (uint64_t)gridDim.x * kSpWaves;
+  for (uint64_t o = (uint64_t)blockIdx.x * kSpWaves + wave; o < n_obj; o += n_waves) {
     const uint64_t lo = Loff[o], ro = Roff[o];
     u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
     const bool inb = (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes && ro + kHdrBytes <= Rbytes;
@@ -2233,7 +2271,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void orswot_merge_sparse_ke
       wave_sync();
       uint32_t r = kLeanFallback;
       if (MASK && A <= kSpTableN && uni(hl0.y) <= 64u && uni(hr0.y) <= 64u && uni(hl0.z) <= 64u &&
-          uni(hr0.z) <= 64u && uni(hl0.w) <= 64u && uni(hr0.w) <= 64u && uni(hl1.x) <= 32u && uni(hr1.x) <= 32u) {
+          uni(hr0.z) <= 64u && uni(hl0.w) <= 128u && uni(hr0.w) <= 128u && uni(hl1.x) <= 32u && uni(hr1.x) <= 32u) {
         uint8_t* X = (uint8_t*)sx_s[wave];
         if ((uni(hl1.x) | uni(hr1.x)) != 0u)
           r = sparse_mask_object<true>((const uint8_t*)sl, (const uint8_t*)sr, X, Ob + lo + ro, A, uni(hl0.y),
@@ -2325,13 +2363,13 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const void* fn = sparse_variant == 1 ? (const void*)orswot_merge_sparse_kernel<false>
                                         : (const void*)orswot_merge_sparse_kernel<true>;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kSpWaves, 0) != hipSuccess || occ < 1)
     occ = 4;
-  const uint64_t want = (n_obj + kWavesPerBlock - 1) / kWavesPerBlock;
+  const uint64_t want = (n_obj + kSpWaves - 1) / kSpWaves;
   const uint64_t cap = (uint64_t)cus * occ;
   const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
   void* args[] = {&Lb, &Loff, &Lbytes, &Rb, &Roff, &Rbytes, &Ob, &Ooff, &Obytes, &n_obj, &n_actors, &status};
-  return hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) == hipSuccess ? CRDT_OK
+  return hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kSpWaves), args, 0, stream) == hipSuccess ? CRDT_OK
                                                                                                        : CRDT_EHIP;
 }
 
