@@ -13,8 +13,8 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
 
 int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                                const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
-                               uint64_t n_obj, uint32_t n_actors, int* status, hipStream_t stream,
-                               int sparse_variant);
+                               uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
+                               uint32_t list_cap, hipStream_t stream, int sparse_variant);
 
 int launch_dense_max(uint64_t* self, const uint64_t* other, uint64_t n_words, hipStream_t stream);
 

@@ -76,8 +76,10 @@ __device__ __forceinline__ void mark(Stamps& st, int k) {
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint32_t lane_of(uint32_t v, uint32_t t) { return __builtin_amdgcn_readlane(v, t); }
 __device__ __forceinline__ uint64_t lane_of64(uint64_t v, uint32_t t) {
-  return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), t) << 32) |
-         __builtin_amdgcn_readlane((uint32_t)v, t);
+  // readlane yields int: widen through uint32_t, or a low half with bit 31
+  // set sign-extends over the high half (offsets >= 2 GiB)
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), t) << 32) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, t);
 }
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
@@ -2287,6 +2289,153 @@ __global__ __launch_bounds__(kWave * kSpWaves) void orswot_merge_sparse_kernel(
   }
 }
 
+// Sparse mask kernel: the dense mask kernel's structure for CSR batches.
+// Lane k of a chunk owns object cbase + k's header; objects that fit the
+// sparse mask join (both records together <= kSpPair, <= 64 clock entries /
+// members, <= 128 dots, <= 32 deferred clocks per side, A <= kSpTableN) are
+// joined one per wave from a single LDS pair stage (L at 0, R right after it)
+// while the next object's pair is in flight in registers; everything else is
+// flagged and listed for orswot_sparse_general_kernel.
+constexpr uint32_t kSpPair = 6144;
+constexpr uint32_t kSpPer = kSpPair / 16 / kWave;
+
+__device__ __forceinline__ void prefetch_pair(u32x4 (&r)[kSpPer], const uint8_t* L, const uint8_t* R, uint32_t nl,
+                                              uint32_t nr, uint32_t lane) {
+#pragma unroll
+  for (uint32_t k = 0; k < kSpPer; ++k) {
+    const uint32_t idx = lane + k * kWave;
+    const uint32_t j = idx - nl < nr ? idx - nl : nr - 1u;
+    r[k] = __builtin_nontemporal_load(idx < nl ? (const u32x4*)L + idx : (const u32x4*)R + j);
+  }
+}
+
+__device__ __forceinline__ void stage_pair(u32x4* dst, const u32x4 (&r)[kSpPer], uint32_t lane) {
+#pragma unroll
+  for (uint32_t k = 0; k < kSpPer; ++k) dst[lane + k * kWave] = r[k];
+}
+
+template <int MINW>
+__global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_mask_kernel(
+    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
+    const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
+    uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
+    int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
+  __shared__ u32x4 pair_s[kWavesPerBlock][kSpPair / 16];
+  __shared__ u32x4 scr_s[kWavesPerBlock][kSpScratch / 16];
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t wave = threadIdx.x / kWave;
+  u32x4* const S = pair_s[wave];
+  uint8_t* const X = (uint8_t*)scr_s[wave];
+  const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint64_t rounds = (n_obj + n_waves * kWave - 1) / (n_waves * kWave);
+  const uint64_t cs = (n_obj + n_waves * rounds - 1) / (n_waves * rounds);
+  for (uint64_t cbase = wave_id * cs; cbase < n_obj; cbase += n_waves * cs) {
+    const uint64_t obj = cbase + lane;
+    const bool valid = lane < cs && obj < n_obj;
+    uint64_t lo = 0, ro = 0;
+    if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
+    u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
+    bool ok = valid && (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes && ro + kHdrBytes <= Rbytes;
+    if (ok) {
+      hl0 = ((const u32x4*)(Lb + lo))[0]; hl1 = ((const u32x4*)(Lb + lo))[1];
+      hr0 = ((const u32x4*)(Rb + ro))[0]; hr1 = ((const u32x4*)(Rb + ro))[1];
+    }
+    ok = ok && sparse_header_ok(hl0, hl1, lo, Lbytes, A) && sparse_header_ok(hr0, hr1, ro, Rbytes, A) &&
+         lo + ro + (uint64_t)hl0.x + hr0.x <= Obytes;
+    const bool fast = ok && hl0.x + hr0.x <= kSpPair && A <= kSpTableN && hl0.y <= 64u && hr0.y <= 64u &&
+                      hl0.z <= 64u && hr0.z <= 64u && hl0.w <= 128u && hr0.w <= 128u && hl1.x <= 32u &&
+                      hr1.x <= 32u;
+    if (valid) Ooff[obj] = (lo + ro) | ((ok && !fast) ? kPending : 0ull);
+    if (ok && !fast) {
+      const uint32_t e = atomicAdd(&ctl[0], 1u);
+      if (e < list_cap) list[e] = obj;
+    }
+    if (__ballot(valid && !ok) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
+    uint64_t pend = __ballot(fast);
+    if (pend == 0ull) continue;
+    const uint32_t n16 = fast ? (hl0.x / 16u) | ((hr0.x / 16u) << 16) : 0u;
+    const uint32_t ncl = hl0.y | (hr0.y << 16), nm = hl0.z | (hr0.z << 16), nd = hl0.w | (hr0.w << 16);
+    const uint64_t defs = __ballot(fast && (hl1.x | hr1.x) != 0u);
+    uint32_t t = (uint32_t)__builtin_ctzll(pend);
+    u32x4 pf[kSpPer];
+    uint32_t nn = lane_of(n16, t);
+    prefetch_pair(pf, Lb + lane_of64(lo, t), Rb + lane_of64(ro, t), nn & 0xFFFFu, nn >> 16, lane);
+    while (pend) {
+      t = (uint32_t)__builtin_ctzll(pend);
+      pend &= pend - 1;
+      nn = lane_of(n16, t);
+      wave_sync();  // previous object's LDS reads are done
+      stage_pair(S, pf, lane);
+      wave_sync();
+      const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
+      const uint32_t c = lane_of(ncl, t), m = lane_of(nm, t), d = lane_of(nd, t);
+      if (pend) {
+        const uint32_t u = (uint32_t)__builtin_ctzll(pend);
+        const uint32_t nu = lane_of(n16, u);
+        prefetch_pair(pf, Lb + lane_of64(lo, u), Rb + lane_of64(ro, u), nu & 0xFFFFu, nu >> 16, lane);
+      }
+      const uint8_t* Ls = (const uint8_t*)S;
+      const uint8_t* Rs = Ls + 16u * (nn & 0xFFFFu);
+      uint32_t r;
+      if ((defs >> t) & 1ull)
+        r = sparse_mask_object<true>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu, d & 0xFFFFu, c >> 16,
+                                     m >> 16, d >> 16, lane);
+      else
+        r = sparse_mask_object<false>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu, d & 0xFFFFu, c >> 16,
+                                      m >> 16, d >> 16, lane);
+      if (r == kLeanFallback && lane == 0u) {  // union clock / members > 64 or a foreign dot actor
+        Ooff[cbase + t] |= kPending;
+        const uint32_t e = atomicAdd(&ctl[0], 1u);
+        if (e < list_cap) list[e] = cbase + t;
+      }
+    }
+  }
+}
+
+// The sparse kernel's general path: one wave per listed object, staged through
+// LDS when both records fit kGenStage, joined by merge_object<true>.
+__device__ __forceinline__ void sparse_general_one(const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb,
+                                                   const uint64_t* Roff, uint8_t* Ob, uint64_t* Ooff, uint64_t o,
+                                                   uint32_t A, u32x4* sl, u32x4* sr, uint32_t lane) {
+  const uint64_t oo = Ooff[o] & ~kPending;
+  const uint8_t* lr = Lb + Loff[o];
+  const uint8_t* rr = Rb + Roff[o];
+  const uint32_t szl = uni(((const uint32_t*)lr)[0]), szr = uni(((const uint32_t*)rr)[0]);
+  if (szl <= kGenStage && szr <= kGenStage) {
+    wave_sync();
+    for (uint32_t k = lane; k < szl / 16; k += kWave) sl[k] = ((const u32x4*)lr)[k];
+    for (uint32_t k = lane; k < szr / 16; k += kWave) sr[k] = ((const u32x4*)rr)[k];
+    wave_sync();
+    merge_object<true>((const uint8_t*)sl, (const uint8_t*)sr, Ob + oo, A, lane);
+  } else {
+    merge_object<true>(lr, rr, Ob + oo, A, lane);
+  }
+  if (lane == 0) Ooff[o] = oo;
+}
+
+__global__ __launch_bounds__(kWave) void orswot_sparse_general_kernel(
+    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, const uint8_t* __restrict__ Rb,
+    const uint64_t* __restrict__ Roff, uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t n_obj,
+    uint32_t A, uint32_t* __restrict__ ctl, const uint64_t* __restrict__ list, uint32_t list_cap) {
+  __shared__ u32x4 gen_s[2][kGenStage / 16];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (n <= list_cap) {
+    for (uint32_t e = blockIdx.x; e < n; e += gridDim.x)
+      sparse_general_one(Lb, Loff, Rb, Roff, Ob, Ooff, list[e], A, gen_s[0], gen_s[1], lane);
+  } else {  // list overflow: scan the flags
+    const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
+    for (uint64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
+      const uint64_t obj = chunk * kWave + lane;
+      const uint64_t oo = obj < n_obj ? Ooff[obj] : 0ull;
+      for (uint64_t pend = __ballot((oo & kPending) != 0ull); pend; pend &= pend - 1)
+        sparse_general_one(Lb, Loff, Rb, Roff, Ob, Ooff, chunk * kWave + (uint32_t)__builtin_ctzll(pend), A,
+                           gen_s[0], gen_s[1], lane);
+    }
+  }
+}
+
 }  // namespace
 
 int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
@@ -2356,21 +2505,45 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
 
 int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                                const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
-                               uint64_t n_obj, uint32_t n_actors, int* status, hipStream_t stream, int sparse_variant) {
+                               uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
+                               uint32_t list_cap, hipStream_t stream, int sparse_variant) {
   if (n_obj == 0) return CRDT_OK;
   int dev = 0, cus = 256, occ = 0;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const void* fn = sparse_variant == 1 ? (const void*)orswot_merge_sparse_kernel<false>
-                                        : (const void*)orswot_merge_sparse_kernel<true>;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kSpWaves, 0) != hipSuccess || occ < 1)
-    occ = 4;
-  const uint64_t want = (n_obj + kSpWaves - 1) / kSpWaves;
+  if (sparse_variant == 1 || sparse_variant == 2) {  // one wave per object (1: no mask join)
+    const void* fn = sparse_variant == 1 ? (const void*)orswot_merge_sparse_kernel<false>
+                                          : (const void*)orswot_merge_sparse_kernel<true>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kSpWaves, 0) != hipSuccess || occ < 1)
+      occ = 4;
+    const uint64_t want = (n_obj + kSpWaves - 1) / kSpWaves;
+    const uint64_t cap = (uint64_t)cus * occ;
+    const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
+    void* args[] = {&Lb, &Loff, &Lbytes, &Rb, &Roff, &Rbytes, &Ob, &Ooff, &Obytes, &n_obj, &n_actors, &status};
+    return hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kSpWaves), args, 0, stream) == hipSuccess ? CRDT_OK
+                                                                                                         : CRDT_EHIP;
+  }
+  const void* fn = (const void*)orswot_sparse_mask_kernel<3>;
+  static std::atomic<int> occ_cache{0};
+  occ = occ_cache.load(std::memory_order_relaxed);
+  if (occ == 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)
+      occ = 2;
+    occ_cache.store(occ, std::memory_order_relaxed);
+  }
+  const uint64_t chunks = (n_obj + kWave - 1) / kWave;
+  const uint64_t want = (chunks + kWavesPerBlock - 1) / kWavesPerBlock;
   const uint64_t cap = (uint64_t)cus * occ;
   const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
-  void* args[] = {&Lb, &Loff, &Lbytes, &Rb, &Roff, &Rbytes, &Ob, &Ooff, &Obytes, &n_obj, &n_actors, &status};
-  return hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kSpWaves), args, 0, stream) == hipSuccess ? CRDT_OK
-                                                                                                       : CRDT_EHIP;
+  void* args[] = {&Lb, &Loff, &Lbytes, &Rb, &Roff, &Rbytes, &Ob, &Ooff, &Obytes, &n_obj, &n_actors, &status,
+                  &ctl, &list, &list_cap};
+  if (hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
+  if (hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) != hipSuccess)
+    return CRDT_EHIP;
+  if (sparse_variant == 3) return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;  // diagnostics: no general pass
+  hipLaunchKernelGGL(orswot_sparse_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
+                     Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
+  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 
 }  // namespace crdts_hip
