@@ -2393,21 +2393,37 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
   }
 }
 
-// The sparse kernel's general path: one wave per listed object, staged through
-// LDS when both records fit kGenStage, joined by merge_object<true>.
+// The sparse kernel's general path: one wave per listed object (pairs larger
+// than the pair stage, or a union past 64 clock entries / members), staged
+// through LDS when both records fit kGenStage: joined by sparse_mask_object
+// when its limits hold, else by merge_object<true>.
 __device__ __forceinline__ void sparse_general_one(const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb,
                                                    const uint64_t* Roff, uint8_t* Ob, uint64_t* Ooff, uint64_t o,
-                                                   uint32_t A, u32x4* sl, u32x4* sr, uint32_t lane) {
+                                                   uint32_t A, u32x4* sl, u32x4* sr, uint8_t* X, uint32_t lane) {
   const uint64_t oo = Ooff[o] & ~kPending;
   const uint8_t* lr = Lb + Loff[o];
   const uint8_t* rr = Rb + Roff[o];
-  const uint32_t szl = uni(((const uint32_t*)lr)[0]), szr = uni(((const uint32_t*)rr)[0]);
+  const u32x4 hl0 = ((const u32x4*)lr)[0], hl1 = ((const u32x4*)lr)[1];
+  const u32x4 hr0 = ((const u32x4*)rr)[0], hr1 = ((const u32x4*)rr)[1];
+  const uint32_t szl = uni(hl0.x), szr = uni(hr0.x);
   if (szl <= kGenStage && szr <= kGenStage) {
     wave_sync();
     for (uint32_t k = lane; k < szl / 16; k += kWave) sl[k] = ((const u32x4*)lr)[k];
     for (uint32_t k = lane; k < szr / 16; k += kWave) sr[k] = ((const u32x4*)rr)[k];
     wave_sync();
-    merge_object<true>((const uint8_t*)sl, (const uint8_t*)sr, Ob + oo, A, lane);
+    uint32_t r = kLeanFallback;
+    const uint32_t cL = uni(hl0.y), nL = uni(hl0.z), dL = uni(hl0.w), cR = uni(hr0.y), nR = uni(hr0.z),
+                   dR = uni(hr0.w);
+    if (A <= kSpTableN && cL <= 64u && cR <= 64u && nL <= 64u && nR <= 64u && dL <= 128u && dR <= 128u &&
+        uni(hl1.x) <= 32u && uni(hr1.x) <= 32u) {
+      if ((uni(hl1.x) | uni(hr1.x)) != 0u)
+        r = sparse_mask_object<true>((const uint8_t*)sl, (const uint8_t*)sr, X, Ob + oo, A, cL, nL, dL, cR, nR, dR,
+                                     lane);
+      else
+        r = sparse_mask_object<false>((const uint8_t*)sl, (const uint8_t*)sr, X, Ob + oo, A, cL, nL, dL, cR, nR,
+                                      dR, lane);
+    }
+    if (r == kLeanFallback) merge_object<true>((const uint8_t*)sl, (const uint8_t*)sr, Ob + oo, A, lane);
   } else {
     merge_object<true>(lr, rr, Ob + oo, A, lane);
   }
@@ -2419,11 +2435,12 @@ __global__ __launch_bounds__(kWave) void orswot_sparse_general_kernel(
     const uint64_t* __restrict__ Roff, uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t n_obj,
     uint32_t A, uint32_t* __restrict__ ctl, const uint64_t* __restrict__ list, uint32_t list_cap) {
   __shared__ u32x4 gen_s[2][kGenStage / 16];
+  __shared__ u32x4 gx_s[kSpScratch / 16];
   const uint32_t lane = threadIdx.x;
   const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (n <= list_cap) {
     for (uint32_t e = blockIdx.x; e < n; e += gridDim.x)
-      sparse_general_one(Lb, Loff, Rb, Roff, Ob, Ooff, list[e], A, gen_s[0], gen_s[1], lane);
+      sparse_general_one(Lb, Loff, Rb, Roff, Ob, Ooff, list[e], A, gen_s[0], gen_s[1], (uint8_t*)gx_s, lane);
   } else {  // list overflow: scan the flags
     const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
     for (uint64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
@@ -2431,7 +2448,7 @@ __global__ __launch_bounds__(kWave) void orswot_sparse_general_kernel(
       const uint64_t oo = obj < n_obj ? Ooff[obj] : 0ull;
       for (uint64_t pend = __ballot((oo & kPending) != 0ull); pend; pend &= pend - 1)
         sparse_general_one(Lb, Loff, Rb, Roff, Ob, Ooff, chunk * kWave + (uint32_t)__builtin_ctzll(pend), A,
-                           gen_s[0], gen_s[1], lane);
+                           gen_s[0], gen_s[1], (uint8_t*)gx_s, lane);
     }
   }
 }
@@ -2541,7 +2558,7 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
   if (hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) != hipSuccess)
     return CRDT_EHIP;
   if (sparse_variant == 3) return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;  // diagnostics: no general pass
-  hipLaunchKernelGGL(orswot_sparse_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
+  hipLaunchKernelGGL(orswot_sparse_general_kernel, dim3(2 * kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
                      Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
