@@ -1580,6 +1580,9 @@ constexpr uint32_t kSpTableN = 1024;
 constexpr uint32_t kSpMsL = 0, kSpMsR = 1024, kSpOut = 0, kSpEq = 2048, kSpDesc = 3072, kSpHeadL = 3328,
                    kSpHeadR = 3456, kSpUofI = 3584, kSpUofJ = 3648, kSpUcAct = 3712, kSpUcL = 3968, kSpUcR = 4480,
                    kSpTrash = 4992, kSpTable = 6016;
+// the clock-union bitmap and its prefix table overlay the equal/>= masks
+// (zeroed only after the union positions are read)
+constexpr uint32_t kSpUbm = kSpEq, kSpUpre = kSpEq + 256u;
 constexpr uint32_t kSpScratch = kSpTable + kSpTableN;  // 7 040 B per wave
 
 __device__ __forceinline__ uint32_t below64(uint64_t mask, uint32_t b) {
@@ -1596,29 +1599,41 @@ __device__ __forceinline__ uint32_t rank32(const uint8_t* b, uint32_t off, uint3
   return base;
 }
 
-template <bool HD>
+template <bool HD, int ABL = 0>
 __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* X, uint8_t* O,
                                                        uint32_t A, uint32_t ncL, uint32_t nL, uint32_t dL,
-                                                       uint32_t ncR, uint32_t nR, uint32_t dR, uint32_t lane) {
+                                                       uint32_t ncR, uint32_t nR, uint32_t dR, uint32_t lane,
+                                                       Stamps* st = nullptr) {
   const uint32_t keyL = kHdrBytes + clock_bytes(ncL, true), keyR = kHdrBytes + clock_bytes(ncR, true);
   const uint32_t caL = kHdrBytes + 8u * ncL, caR = kHdrBytes + 8u * ncR;  // clock actor lists
   const uint32_t ctrL = keyL + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
   const uint32_t ctrR = keyR + 8u * nR, actR = ctrR + 8u * dR, endR = actR + 4u * dR;
   const uint32_t tr = kSpTrash + 16u * lane;
 
-  // ---- union of the two top clocks (rank arithmetic, as for the members)
+  // ---- union of the two top clocks: an actor's union position is the
+  // number of union-bitmap bits below it (both sides agree on a common actor)
   const bool hcl = lane < ncL, hcr = lane < ncR;
   const uint32_t cxl = ld32(Ls, caL + 4u * lane), cxr = ld32(Rs, caR + 4u * lane);
   const uint64_t cvl = ld64(Ls, kHdrBytes + 8u * lane), cvr = ld64(Rs, kHdrBytes + 8u * lane);
-  const uint32_t rcl = rank32(Rs, caR, ncR, cxl), rcr = rank32(Ls, caL, ncL, cxr);
-  const bool eqcl = hcl && rcl < ncR && ld32(Rs, caR + 4u * rcl) == cxl;
-  const bool eqcr = hcr && rcr < ncL && ld32(Ls, caL + 4u * rcr) == cxr;
-  const uint64_t ECL = __ballot(eqcl), ECR = __ballot(eqcr);
-  const uint32_t Uc = ncL + ncR - (uint32_t)__popcll(ECL);
-  if (Uc > (uint32_t)kWave || __ballot((hcl && cxl >= kSpTableN) || (hcr && cxr >= kSpTableN)) != 0ull)
-    return kLeanFallback;
-  const uint32_t ucl = lane + rcl - mbcnt64(ECL), ucr = lane + rcr - mbcnt64(ECR);
-  const uint64_t cvlr = ld64(Rs, kHdrBytes + 8u * rcl);  // other side's counter of a common actor
+  if (__ballot((hcl && cxl >= kSpTableN) || (hcr && cxr >= kSpTableN)) != 0ull) return kLeanFallback;
+  wave_sync();  // the previous object's readers of this scratch are done
+  if (lane < kSpTableN / 64u) *(uint64_t*)(X + kSpUbm + 8u * lane) = 0ull;
+  atomicOr((unsigned long long*)(X + (hcl ? kSpUbm + 8u * (cxl >> 6) : tr)), 1ull << (cxl & 63u));
+  atomicOr((unsigned long long*)(X + (hcr ? kSpUbm + 8u * (cxr >> 6) : tr)), 1ull << (cxr & 63u));
+  wave_sync();
+  const uint64_t bw = lane < kSpTableN / 64u ? *(const uint64_t*)(X + kSpUbm + 8u * lane) : 0ull;
+  const uint32_t bpc = (uint32_t)__popcll(bw), bin = scan_incl(bpc);
+  const uint32_t Uc = lane_of(bin, kSpTableN / 64u - 1u);
+  if (Uc > (uint32_t)kWave) return kLeanFallback;
+  if (lane < kSpTableN / 64u)
+    *(u32x4*)(X + kSpUpre + 16u * lane) = u32x4{(uint32_t)bw, (uint32_t)(bw >> 32), bin - bpc, 0u};
+  *(uint64_t*)(X + kSpUcL + 8u * lane) = 0ull;
+  *(uint64_t*)(X + kSpUcR + 8u * lane) = 0ull;
+  wave_sync();
+  const u32x4 pwl = *(const u32x4*)(X + kSpUpre + 16u * (cxl >> 6 & 15u));
+  const u32x4 pwr = *(const u32x4*)(X + kSpUpre + 16u * (cxr >> 6 & 15u));
+  const uint32_t ucl = pwl.z + below64(((uint64_t)pwl.y << 32) | pwl.x, cxl & 63u);
+  const uint32_t ucr = pwr.z + below64(((uint64_t)pwr.y << 32) | pwr.x, cxr & 63u);
 
   // ---- members (as mask_object); dots are handled in rounds of 64 (<= 128 per side)
   const bool hml = lane < nL, hmr = lane < nR;
@@ -1642,16 +1657,13 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   const uint32_t ul = lane + rl - mbcnt64(EL), ur = lane + rr - mbcnt64(ER);
 
   wave_sync();  // the previous object's readers of this scratch are done
-  // union clock entries + actor table
+  // union clock entries (each side its own counter) + actor table
   *(uint32_t*)(X + (hcl ? kSpUcAct + 4u * (ucl & 63u) : tr)) = cxl;
   *(uint64_t*)(X + (hcl ? kSpUcL + 8u * (ucl & 63u) : tr)) = cvl;
-  *(uint64_t*)(X + (hcl ? kSpUcR + 8u * (ucl & 63u) : tr)) = eqcl ? cvlr : 0ull;
   X[hcl ? kSpTable + cxl : tr] = (uint8_t)ucl;
-  const bool wr = hcr && !eqcr;
-  *(uint32_t*)(X + (wr ? kSpUcAct + 4u * (ucr & 63u) : tr)) = cxr;
-  *(uint64_t*)(X + (wr ? kSpUcL + 8u * (ucr & 63u) : tr)) = 0ull;
-  *(uint64_t*)(X + (wr ? kSpUcR + 8u * (ucr & 63u) : tr)) = cvr;
-  X[wr ? kSpTable + cxr : tr] = (uint8_t)ucr;
+  *(uint32_t*)(X + (hcr ? kSpUcAct + 4u * (ucr & 63u) : tr)) = cxr;
+  *(uint64_t*)(X + (hcr ? kSpUcR + 8u * (ucr & 63u) : tr)) = cvr;
+  X[hcr ? kSpTable + cxr : tr] = (uint8_t)ucr;
   // member masks (zeroed), run heads, descriptors
   *(u32x4*)(X + kSpMsL + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
   *(u32x4*)(X + kSpMsR + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
@@ -1669,6 +1681,7 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   X[kSpUofI + lane] = (uint8_t)ul;
   X[kSpUofJ + lane] = (uint8_t)ur;
   wave_sync();
+  if (ABL == 9) mark<ABL>(*st, 3);
   // run-head masks of both rounds; the member of dot 64r + lane is
   // (#heads at or below it) - 1
   const uint64_t HL0 = __ballot(lane < dL && X[kSpHeadL + lane] != 0u);
@@ -1698,6 +1711,7 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   }
   if (__ballot(foreign) != 0ull) return kLeanFallback;  // a dot actor outside both top clocks
   wave_sync();
+  if (ABL == 9) mark<ABL>(*st, 4);
   for (uint32_t rd = 0; rd < nrnd; ++rd) {  // actors on both sides of a shared member: equal / self >= other
     const uint32_t dd = 64u * rd + lane;
     const bool hdr = dd < dR;
@@ -1718,6 +1732,7 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     atomicOr(pe + 1, (unsigned long long)(sh && va >= vr ? 1ull << br : 0ull));
   }
   wave_sync();
+  if (ABL == 9) mark<ABL>(*st, 5);
   // ---- per union member: mask join (src/orswot.rs:94-138)
   const bool hu = lane < U;
   const uint32_t dsc = hu ? *(const uint32_t*)(X + kSpDesc + 4u * lane) : 0u;
@@ -1785,6 +1800,7 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   rec_layout(OL, Uc, tot_mem, tot_dot, nd, ndd, ndm, true);
   const uint32_t size = OL.size;
   const uint32_t d0 = cincl - c;
+  if (ABL == 9) mark<ABL>(*st, 6);
   wave_sync();
   *(uint64_t*)(X + kSpOut + 32u * lane) = hu ? keep : 0ull;
   *(uint64_t*)(X + kSpOut + 32u * lane + 8u) = hu ? useK : 0ull;
@@ -1844,6 +1860,7 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     h[0] = u32x4{size, Uc, tot_mem, tot_dot};
     h[1] = u32x4{nd, ndd, ndm, kSparseClock};
   }
+  if (ABL == 9) mark<ABL>(*st, 7);
   return size / 16u;
 }
 
@@ -2314,7 +2331,7 @@ __device__ __forceinline__ void stage_pair(u32x4* dst, const u32x4 (&r)[kSpPer],
   for (uint32_t k = 0; k < kSpPer; ++k) dst[lane + k * kWave] = r[k];
 }
 
-template <int MINW>
+template <int MINW, int ABL = 0>  // ABL 9: phase stamps into the list buffer (no general path)
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_mask_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
@@ -2330,6 +2347,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
   const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
   const uint64_t rounds = (n_obj + n_waves * kWave - 1) / (n_waves * kWave);
   const uint64_t cs = (n_obj + n_waves * rounds - 1) / (n_waves * rounds);
+  Stamps st{};
+  if (ABL == 9) st.last = stamp();
   for (uint64_t cbase = wave_id * cs; cbase < n_obj; cbase += n_waves * cs) {
     const uint64_t obj = cbase + lane;
     const bool valid = lane < cs && obj < n_obj;
@@ -2347,7 +2366,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
                       hl0.z <= 64u && hr0.z <= 64u && hl0.w <= 128u && hr0.w <= 128u && hl1.x <= 32u &&
                       hr1.x <= 32u;
     if (valid) Ooff[obj] = (lo + ro) | ((ok && !fast) ? kPending : 0ull);
-    if (ok && !fast) {
+    if (ABL != 9 && ok && !fast) {
       const uint32_t e = atomicAdd(&ctl[0], 1u);
       if (e < list_cap) list[e] = obj;
     }
@@ -2368,6 +2387,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
       wave_sync();  // previous object's LDS reads are done
       stage_pair(S, pf, lane);
       wave_sync();
+      mark<ABL>(st, 0);
       const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
       const uint32_t c = lane_of(ncl, t), m = lane_of(nm, t), d = lane_of(nd, t);
       if (pend) {
@@ -2375,21 +2395,28 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
         const uint32_t nu = lane_of(n16, u);
         prefetch_pair(pf, Lb + lane_of64(lo, u), Rb + lane_of64(ro, u), nu & 0xFFFFu, nu >> 16, lane);
       }
+      mark<ABL>(st, 1);
       const uint8_t* Ls = (const uint8_t*)S;
       const uint8_t* Rs = Ls + 16u * (nn & 0xFFFFu);
       uint32_t r;
       if ((defs >> t) & 1ull)
-        r = sparse_mask_object<true>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu, d & 0xFFFFu, c >> 16,
-                                     m >> 16, d >> 16, lane);
+        r = sparse_mask_object<true, ABL>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu, d & 0xFFFFu, c >> 16,
+                                          m >> 16, d >> 16, lane, &st);
       else
-        r = sparse_mask_object<false>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu, d & 0xFFFFu, c >> 16,
-                                      m >> 16, d >> 16, lane);
-      if (r == kLeanFallback && lane == 0u) {  // union clock / members > 64 or a foreign dot actor
+        r = sparse_mask_object<false, ABL>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu, d & 0xFFFFu, c >> 16,
+                                           m >> 16, d >> 16, lane, &st);
+      if (ABL != 9 && r == kLeanFallback && lane == 0u) {  // union clock / members > 64 or a foreign dot actor
         Ooff[cbase + t] |= kPending;
         const uint32_t e = atomicAdd(&ctl[0], 1u);
         if (e < list_cap) list[e] = cbase + t;
       }
     }
+  }
+  if (ABL == 9 && lane < 8u) {  // per-wave phase sums -> the context's list buffer
+    uint64_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v = lane == (uint32_t)q ? st.acc[q] : v;
+    list[wave_id * 8u + lane] = v;
   }
 }
 
@@ -2540,7 +2567,8 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
     return hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kSpWaves), args, 0, stream) == hipSuccess ? CRDT_OK
                                                                                                          : CRDT_EHIP;
   }
-  const void* fn = (const void*)orswot_sparse_mask_kernel<3>;
+  const void* fn = sparse_variant == 4 ? (const void*)orswot_sparse_mask_kernel<3, 9>
+                                        : (const void*)orswot_sparse_mask_kernel<3>;
   static std::atomic<int> occ_cache{0};
   occ = occ_cache.load(std::memory_order_relaxed);
   if (occ == 0) {
@@ -2557,7 +2585,7 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
   if (hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
   if (hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) != hipSuccess)
     return CRDT_EHIP;
-  if (sparse_variant == 3) return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;  // diagnostics: no general pass
+  if (sparse_variant == 3 || sparse_variant == 4) return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;  // diagnostics: no general pass
   hipLaunchKernelGGL(orswot_sparse_general_kernel, dim3(2 * kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
                      Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
