@@ -359,7 +359,7 @@ def run_orswot_csr(args, rank, world, local):
         # intermediate sizes are bounded by the final one, so this is a lower bound
         alg = in_bytes + (R - 1) * int(sizes.sum()) + 3 * 8 * n * (R - 1)
         ach = alg / (ev_ms * 1e-3) / 1e9
-        res["roofline"] = {"bound": "hbm", "kernel": "orswot_merge_sparse_kernel", "achieved": ach,
+        res["roofline"] = {"bound": "hbm", "kernel": "fold of 7 launches: orswot_sparse_mask_kernel + orswot_sparse_general_kernel", "achieved": ach,
                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                            "kernel_ms": ev_ms, "alg_bytes_per_launch": alg / (R - 1), "traffic": None}
         if not args.no_cpu_baseline:
