@@ -272,6 +272,47 @@ int crdt_orswot_generate_replicas(uint64_t seed, size_t first_obj, size_t n_obj,
                                   const crdt_orswot_rep_params* params, uint32_t n_replicas,
                                   uint32_t flags, int n_threads, crdt_orswot_gen** out);
 
+/* ------------------------------------------------------------------------ *
+ * Ingest / egest: the reference's binary form <-> canonical records
+ * (SURVEY.md §8(f) rank 1). The reference form of an Orswot<M, A> is
+ * `to_binary(&s)` = bincode 0.9 of its serde derives (src/lib.rs:62-83;
+ * fields src/orswot.rs:26-30, src/vclock.rs:54-57): u64 little-endian
+ * lengths before every map / set, fixed-width little-endian integers, HashMap
+ * and HashSet elements in any order, BTreeMap keys ascending. Actors (A) and
+ * members (M) are unsigned integers of actor_bytes / member_bytes in
+ * {1, 2, 4, 8}; they are the record's actor ids / member keys as they stand.
+ * Blob i is bytes [blob_off[i], blob_off[i] + blob_len[i]) of d_blobs
+ * (blob_bytes long, any alignment).
+ *
+ * Ingest = from_binary + canonicalisation; a blob a record cannot hold
+ * (zero counter, empty member clock / deferred clock / deferred set, actor
+ * >= n_actors, duplicates, BTreeMap keys out of order, truncated or trailing
+ * bytes) latches CRDT_ENONCANON; one with more than 256 members or 64
+ * deferred clocks latches CRDT_ECAPACITY (limits of this round).
+ *   1) crdt_orswot_bincode_record_sizes: d_sizes[i] = record bytes (0 if bad)
+ *   2) the caller places records (16-B aligned offsets, e.g. exclusive scan)
+ *   3) crdt_orswot_from_bincode writes record i at d_out + d_out_off[i].
+ * Egest = to_binary with HashMap / HashSet elements in ascending key (clock)
+ * order — one of the orders the reference may produce, decoded to an equal
+ * state by from_binary:
+ *   1) crdt_orswot_bincode_sizes: d_sizes[i] = blob bytes
+ *   2) the caller places blobs at 16-B aligned offsets (each zero-padded to 16)
+ *   3) crdt_orswot_to_bincode writes them.                                    */
+int crdt_orswot_bincode_record_sizes(crdt_ctx* ctx, const uint8_t* d_blobs, size_t blob_bytes,
+                                     const uint64_t* d_blob_off, const uint64_t* d_blob_len, size_t n_obj,
+                                     uint32_t actor_bytes, uint32_t member_bytes, uint32_t n_actors,
+                                     uint32_t flags, uint64_t* d_sizes, void* stream);
+int crdt_orswot_from_bincode(crdt_ctx* ctx, const uint8_t* d_blobs, size_t blob_bytes,
+                             const uint64_t* d_blob_off, const uint64_t* d_blob_len, size_t n_obj,
+                             uint32_t actor_bytes, uint32_t member_bytes, uint32_t n_actors, uint32_t flags,
+                             uint8_t* d_out, const uint64_t* d_out_off, size_t out_bytes, void* stream);
+int crdt_orswot_bincode_sizes(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32_t n_actors,
+                              uint32_t flags, uint32_t actor_bytes, uint32_t member_bytes, uint64_t* d_sizes,
+                              void* stream);
+int crdt_orswot_to_bincode(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32_t n_actors, uint32_t flags,
+                           uint32_t actor_bytes, uint32_t member_bytes, uint8_t* d_out,
+                           const uint64_t* d_out_off, size_t out_bytes, void* stream);
+
 /* Dense synthetic counters: u64[n_obj][n_actors] rows for objects
  * [first_obj, first_obj+n_obj), counter U[0, 2^bits) with `pct_zero` % zeros. */
 int crdt_dense_generate(uint64_t seed, size_t first_obj, size_t n_obj, uint32_t n_actors,

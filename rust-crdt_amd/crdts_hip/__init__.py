@@ -36,6 +36,14 @@ CONFIG5 = dict(universe=1024, pool_actors=48, own_actors=2, member_universe=64, 
 CONFIG5_SEED = 0xC0FFEE05
 
 
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 def _torch():
     import torch
 
@@ -184,6 +192,59 @@ class Engine:
         return OrswotBatch(dst, doff, B.n_actors, max(16, (used + 15) // 16 * 16), B.flags)
 
     # ---------------------------------------------------------------- dense
+    # ------------------------------------------------ bincode ingest / egest
+    def orswot_from_bincode(self, blobs, blob_off, blob_len, n_actors, actor_bytes, member_bytes, flags=0,
+                            stream=None, check_status=True):
+        """Records from the reference's binary form (`from_binary`, src/lib.rs:78-83).
+
+        blobs: torch.uint8 device tensor; blob_off / blob_len: torch.int64 device
+        tensors (u64). Returns an OrswotBatch of canonical records."""
+        torch = _torch()
+        n = int(blob_off.numel())
+        dev = f"cuda:{self.device}"
+        st = self._stream(stream)
+        sizes = torch.empty(n, dtype=torch.int64, device=dev)
+        check(lib.crdt_orswot_bincode_record_sizes(self.ctx, C.c_void_p(blobs.data_ptr()), int(blobs.numel()),
+                                                   C.c_void_p(blob_off.data_ptr()), C.c_void_p(blob_len.data_ptr()),
+                                                   n, actor_bytes, member_bytes, n_actors, flags,
+                                                   C.c_void_p(sizes.data_ptr()), st), "bincode_record_sizes")
+        with torch.cuda.stream(stream) if stream is not None else _nullctx():
+            ends = torch.cumsum(sizes, 0)
+            total = int(ends[-1].item()) if n else 0
+            off = ends - sizes
+        base = torch.empty(max(16, total), dtype=torch.uint8, device=dev)
+        check(lib.crdt_orswot_from_bincode(self.ctx, C.c_void_p(blobs.data_ptr()), int(blobs.numel()),
+                                           C.c_void_p(blob_off.data_ptr()), C.c_void_p(blob_len.data_ptr()), n,
+                                           actor_bytes, member_bytes, n_actors, flags, C.c_void_p(base.data_ptr()),
+                                           C.c_void_p(off.data_ptr()), int(base.numel()), st), "from_bincode")
+        if check_status:
+            self.status(stream)
+        return OrswotBatch(base, off, n_actors, int(base.numel()), flags)
+
+    def orswot_to_bincode(self, B: "OrswotBatch", actor_bytes, member_bytes, stream=None, check_status=True):
+        """The reference's binary form (`to_binary`, src/lib.rs:62-64) of every
+        record: (blobs uint8, blob_off int64, blob_len int64) device tensors;
+        blob i starts 16-B aligned and is zero-padded to 16."""
+        torch = _torch()
+        dev = f"cuda:{self.device}"
+        st = self._stream(stream)
+        b = B.cbatch()
+        lens = torch.empty(B.n_obj, dtype=torch.int64, device=dev)
+        check(lib.crdt_orswot_bincode_sizes(self.ctx, C.byref(b), B.n_actors, B.flags, actor_bytes, member_bytes,
+                                            C.c_void_p(lens.data_ptr()), st), "bincode_sizes")
+        with torch.cuda.stream(stream) if stream is not None else _nullctx():
+            padded = (lens + 15) // 16 * 16
+            ends = torch.cumsum(padded, 0)
+            total = int(ends[-1].item()) if B.n_obj else 0
+            off = ends - padded
+        out = torch.empty(max(16, total), dtype=torch.uint8, device=dev)
+        check(lib.crdt_orswot_to_bincode(self.ctx, C.byref(b), B.n_actors, B.flags, actor_bytes, member_bytes,
+                                         C.c_void_p(out.data_ptr()), C.c_void_p(off.data_ptr()), int(out.numel()),
+                                         st), "to_bincode")
+        if check_status:
+            self.status(stream)
+        return out, off, lens
+
     def dense_merge(self, self_rows, other_rows, n_actors, kind="gcounter", stream=None):
         """In place: self_rows = max(self_rows, other_rows) (src/vclock.rs:131-137).
 

@@ -58,6 +58,8 @@ EXPORTS = [
     "crdt_host_orswot_apply_add", "crdt_host_orswot_apply_rm", "crdt_host_orswot_encode",
     "crdt_host_orswot_decode", "crdt_orswot_record_bytes_ex", "crdt_orswot_merge_ex",
     "crdt_orswot_validate_ex", "crdt_orswot_generate_replicas", "crdt_host_orswot_encode_ex",
+    "crdt_orswot_bincode_record_sizes", "crdt_orswot_from_bincode", "crdt_orswot_bincode_sizes",
+    "crdt_orswot_to_bincode",
 ]
 
 
@@ -112,6 +114,10 @@ def _load():
         "crdt_orswot_validate_ex": (I, [P, BP, U32, U32, P]),
         "crdt_orswot_generate_replicas": (I, [U64, SZ, SZ, C.POINTER(RepParams), U32, U32, I, C.POINTER(P)]),
         "crdt_host_orswot_encode_ex": (C.c_long, [P, U32, U32, P, SZ]),
+        "crdt_orswot_bincode_record_sizes": (I, [P, P, SZ, P, P, SZ, U32, U32, U32, U32, P, P]),
+        "crdt_orswot_from_bincode": (I, [P, P, SZ, P, P, SZ, U32, U32, U32, U32, P, P, SZ, P]),
+        "crdt_orswot_bincode_sizes": (I, [P, BP, U32, U32, U32, U32, P, P]),
+        "crdt_orswot_to_bincode": (I, [P, BP, U32, U32, U32, U32, P, P, SZ, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -297,4 +297,61 @@ int crdt_orswot_merge_host(crdt_ctx* ctx, const uint8_t* h_self_base, const uint
   return CRDT_OK;
 }
 
+// ---------------------------------------------------------------- bincode codec
+namespace {
+bool bc_width_ok(uint32_t w) { return w == 1u || w == 2u || w == 4u || w == 8u; }
+}  // namespace
+
+int crdt_orswot_bincode_record_sizes(crdt_ctx* ctx, const uint8_t* d_blobs, size_t blob_bytes,
+                                     const uint64_t* d_blob_off, const uint64_t* d_blob_len, size_t n_obj,
+                                     uint32_t actor_bytes, uint32_t member_bytes, uint32_t n_actors,
+                                     uint32_t flags, uint64_t* d_sizes, void* stream) {
+  if (!ctx || (n_obj && (!d_blobs || !d_blob_off || !d_blob_len || !d_sizes)) || n_actors == 0 ||
+      !bc_width_ok(actor_bytes) || !bc_width_ok(member_bytes) || (flags & ~CRDT_ORSWOT_SPARSE_CLOCK))
+    return CRDT_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return launch_bincode_ingest(d_blobs, blob_bytes, d_blob_off, d_blob_len, n_obj, actor_bytes, member_bytes,
+                               n_actors, flags, d_sizes, nullptr, nullptr, 0, ctx->d_status, S(stream));
+}
+
+int crdt_orswot_from_bincode(crdt_ctx* ctx, const uint8_t* d_blobs, size_t blob_bytes,
+                             const uint64_t* d_blob_off, const uint64_t* d_blob_len, size_t n_obj,
+                             uint32_t actor_bytes, uint32_t member_bytes, uint32_t n_actors, uint32_t flags,
+                             uint8_t* d_out, const uint64_t* d_out_off, size_t out_bytes, void* stream) {
+  if (!ctx || (n_obj && (!d_blobs || !d_blob_off || !d_blob_len || !d_out || !d_out_off)) || n_actors == 0 ||
+      !bc_width_ok(actor_bytes) || !bc_width_ok(member_bytes) || (flags & ~CRDT_ORSWOT_SPARSE_CLOCK) ||
+      !aligned16(d_out))
+    return CRDT_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return launch_bincode_ingest(d_blobs, blob_bytes, d_blob_off, d_blob_len, n_obj, actor_bytes, member_bytes,
+                               n_actors, flags, nullptr, d_out, d_out_off, out_bytes, ctx->d_status, S(stream));
+}
+
+int crdt_orswot_bincode_sizes(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32_t n_actors, uint32_t flags,
+                              uint32_t actor_bytes, uint32_t member_bytes, uint64_t* d_sizes, void* stream) {
+  if (!ctx || !batch || (batch->n_obj && (!batch->base || !batch->off || !d_sizes)) || n_actors == 0 ||
+      !bc_width_ok(actor_bytes) || !bc_width_ok(member_bytes) || (flags & ~CRDT_ORSWOT_SPARSE_CLOCK) ||
+      (batch->n_obj && !aligned16(batch->base)))
+    return CRDT_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return launch_bincode_egest(batch->base, batch->bytes, batch->off, batch->n_obj, n_actors, flags, actor_bytes,
+                              member_bytes, d_sizes, nullptr, nullptr, 0, ctx->d_status, S(stream));
+}
+
+int crdt_orswot_to_bincode(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32_t n_actors, uint32_t flags,
+                           uint32_t actor_bytes, uint32_t member_bytes, uint8_t* d_out,
+                           const uint64_t* d_out_off, size_t out_bytes, void* stream) {
+  if (!ctx || !batch || (batch->n_obj && (!batch->base || !batch->off || !d_out || !d_out_off)) ||
+      n_actors == 0 || !bc_width_ok(actor_bytes) || !bc_width_ok(member_bytes) ||
+      (flags & ~CRDT_ORSWOT_SPARSE_CLOCK) || (batch->n_obj && (!aligned16(batch->base) || !aligned16(d_out))))
+    return CRDT_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return launch_bincode_egest(batch->base, batch->bytes, batch->off, batch->n_obj, n_actors, flags, actor_bytes,
+                              member_bytes, nullptr, d_out, d_out_off, out_bytes, ctx->d_status, S(stream));
+}
+
 }  // extern "C"

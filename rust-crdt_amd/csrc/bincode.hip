@@ -1,0 +1,541 @@
+// Ingest / egest codec between the reference's binary form of an Orswot and
+// the canonical record (include/crdts_hip.h). SURVEY.md §8(f) rank 1.
+//
+// The reference form is `to_binary(&orswot)` = bincode 0.9 of the serde
+// derives (src/lib.rs:62-83; struct Orswot src/orswot.rs:26-30, VClock
+// src/vclock.rs:54-57): fields in order, maps and sets as a u64 length +
+// elements, fixed-width little-endian integers; HashMap / HashSet iteration
+// order is arbitrary, BTreeMap order ascending. Actors and members are
+// unsigned integers of 1, 2, 4 or 8 bytes, used as the record's actor ids /
+// member keys directly (an order-preserving intern).
+//
+// Ingest canonicalises: members sorted by key, deferred clocks sorted in
+// CLOCK ORDER, deferred member sets sorted; it rejects what a record cannot
+// hold (zero counters, empty clocks or sets, actors >= n_actors, duplicates,
+// out-of-order BTreeMap keys, truncated or trailing bytes).
+//
+// One wave per object, grid-stride. A blob that fits the wave's LDS window is
+// staged there (16-B loads of the aligned span); the walk over its variable-
+// length entries is wave-uniform (every lane reads the same bytes), the
+// per-member / per-deferred-clock work is lane-parallel.
+#include <hip/hip_runtime.h>
+
+#include "../../include/crdts_hip.h"
+#include "kernels.h"
+#include "record_layout.h"
+
+namespace crdts_hip {
+namespace {
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+constexpr uint32_t kBcWave = 64;
+constexpr uint32_t kBcWaves = 4;        // waves per block
+constexpr uint32_t kBcStage = 4096;     // LDS window per wave (blob for ingest, blob for egest)
+constexpr uint32_t kBcMaxMem = 256;     // members per object on the ingest path
+constexpr uint32_t kBcMaxDef = 64;      // deferred clocks per object on the ingest path
+
+// per-wave ingest scratch (bytes)
+constexpr uint32_t kXPm = 0;                          // u32 member entry position [kBcMaxMem]
+constexpr uint32_t kXLm = kXPm + 4 * kBcMaxMem;       // u32 member dot count
+constexpr uint32_t kXKm = kXLm + 4 * kBcMaxMem;       // u64 member key
+constexpr uint32_t kXRm = kXKm + 8 * kBcMaxMem;       // u32 member rank
+constexpr uint32_t kXSm = kXRm + 4 * kBcMaxMem;       // u32 dot counts / offsets in sorted order
+constexpr uint32_t kXPd = kXSm + 4 * kBcMaxMem;       // u32 deferred clock position (its length word)
+constexpr uint32_t kXLd = kXPd + 4 * kBcMaxDef;       // u32 deferred clock entries
+constexpr uint32_t kXPs = kXLd + 4 * kBcMaxDef;       // u32 deferred set position (its length word)
+constexpr uint32_t kXLs = kXPs + 4 * kBcMaxDef;       // u32 deferred set size
+constexpr uint32_t kXSd = kXLs + 4 * kBcMaxDef;       // u32 sorted deferred clock entries -> offsets
+constexpr uint32_t kXSs = kXSd + 4 * kBcMaxDef;       // u32 sorted deferred set sizes -> offsets
+constexpr uint32_t kXRd = kXSs + 4 * kBcMaxDef;       // u32 deferred rank
+constexpr uint32_t kXBytes = kXRd + 4 * kBcMaxDef;    // 7 680 B
+
+__device__ __forceinline__ void bc_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t bc_uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t bc_uni64(uint64_t v) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+
+__device__ __forceinline__ uint32_t bc_scan_incl(uint32_t v, uint32_t lane) {
+#pragma unroll
+  for (uint32_t d = 1; d < kBcWave; d <<= 1) {
+    const uint32_t t = __shfl_up(v, d, kBcWave);
+    v += lane >= d ? t : 0u;
+  }
+  return v;
+}
+
+// little-endian unsigned integer of w bytes at p[pos]
+__device__ __forceinline__ uint64_t rdw(const uint8_t* p, uint64_t pos, uint32_t w) {
+  uint64_t v = 0;
+  for (uint32_t i = 0; i < w; ++i) v |= (uint64_t)p[pos + i] << (8u * i);
+  return v;
+}
+__device__ __forceinline__ void wrw(uint8_t* p, uint64_t pos, uint64_t v, uint32_t w) {
+  for (uint32_t i = 0; i < w; ++i) p[pos + i] = (uint8_t)(v >> (8u * i));
+}
+
+// lexicographic (actor, counter) order of two bincode clocks, a proper prefix
+// first (the record's CLOCK ORDER): -1, 0, 1
+__device__ int bc_clock_cmp(const uint8_t* B, uint64_t pa, uint32_t na, uint64_t pb, uint32_t nb, uint32_t wa) {
+  const uint32_t n = na < nb ? na : nb, st = wa + 8u;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t xa = rdw(B, pa + (uint64_t)st * i, wa), xb = rdw(B, pb + (uint64_t)st * i, wa);
+    if (xa != xb) return xa < xb ? -1 : 1;
+    const uint64_t ca = rdw(B, pa + (uint64_t)st * i + wa, 8), cb = rdw(B, pb + (uint64_t)st * i + wa, 8);
+    if (ca != cb) return ca < cb ? -1 : 1;
+  }
+  return na == nb ? 0 : (na < nb ? -1 : 1);
+}
+
+struct BcWalk {
+  uint32_t n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem;
+  int err;
+};
+
+// Wave-uniform walk over one blob: bounds, counts, entry positions (into X).
+__device__ BcWalk bc_walk(const uint8_t* B, uint64_t len, uint32_t wa, uint32_t wm, uint32_t A, uint8_t* X,
+                          uint32_t lane) {
+  BcWalk w{0, 0, 0, 0, 0, 0, 0};
+  const uint64_t sa = wa + 8u;
+  if (len < 24u) { w.err = CRDT_ENONCANON; return w; }
+  const uint64_t nclk = bc_uni64(rdw(B, 0, 8));
+  if (nclk > A || nclk > (len - 24u) / sa) { w.err = CRDT_ENONCANON; return w; }
+  w.n_clk = (uint32_t)nclk;
+  uint64_t p = 8u + nclk * sa;
+  const uint64_t nent = bc_uni64(rdw(B, p, 8));
+  p += 8u;
+  if (nent > kBcMaxMem) { w.err = CRDT_ECAPACITY; return w; }
+  w.n_mem = (uint32_t)nent;
+  for (uint32_t e = 0; e < (uint32_t)nent; ++e) {
+    if (p + wm + 8u > len) { w.err = CRDT_ENONCANON; return w; }
+    const uint64_t l = bc_uni64(rdw(B, p + wm, 8));
+    if (l == 0u || l > A || l > (len - (p + wm + 8u)) / sa) { w.err = CRDT_ENONCANON; return w; }
+    if (lane == (e & (kBcWave - 1u))) {
+      ((uint32_t*)(X + kXPm))[e] = (uint32_t)p;
+      ((uint32_t*)(X + kXLm))[e] = (uint32_t)l;
+    }
+    w.n_dot += (uint32_t)l;
+    p += wm + 8u + l * sa;
+  }
+  if (p + 8u > len) { w.err = CRDT_ENONCANON; return w; }
+  const uint64_t ndef = bc_uni64(rdw(B, p, 8));
+  p += 8u;
+  if (ndef > kBcMaxDef) { w.err = CRDT_ECAPACITY; return w; }
+  w.n_def = (uint32_t)ndef;
+  for (uint32_t d = 0; d < (uint32_t)ndef; ++d) {
+    if (p + 8u > len) { w.err = CRDT_ENONCANON; return w; }
+    const uint64_t lc = bc_uni64(rdw(B, p, 8));
+    if (lc == 0u || lc > A || lc > (len - (p + 8u)) / sa) { w.err = CRDT_ENONCANON; return w; }
+    const uint64_t q = p + 8u + lc * sa;
+    if (q + 8u > len) { w.err = CRDT_ENONCANON; return w; }
+    const uint64_t ls = bc_uni64(rdw(B, q, 8));
+    if (ls == 0u || ls > (len - (q + 8u)) / wm) { w.err = CRDT_ENONCANON; return w; }
+    if (lane == (d & (kBcWave - 1u))) {
+      ((uint32_t*)(X + kXPd))[d] = (uint32_t)p;
+      ((uint32_t*)(X + kXLd))[d] = (uint32_t)lc;
+      ((uint32_t*)(X + kXPs))[d] = (uint32_t)q;
+      ((uint32_t*)(X + kXLs))[d] = (uint32_t)ls;
+    }
+    w.n_def_dot += (uint32_t)lc;
+    w.n_def_mem += (uint32_t)ls;
+    p = q + 8u + ls * wm;
+  }
+  if (p != len) w.err = CRDT_ENONCANON;  // trailing bytes
+  return w;
+}
+
+// Exclusive prefix sum, in place, of n (<= 4 * 64) u32 at S.
+__device__ void bc_scan_excl(uint32_t* S, uint32_t n, uint32_t lane) {
+  uint32_t v[4], s = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4u; ++k) {
+    const uint32_t i = 4u * lane + k;
+    v[k] = i < n ? S[i] : 0u;
+    s += v[k];
+  }
+  const uint32_t incl = bc_scan_incl(s, lane);
+  uint32_t run = incl - s;
+  bc_sync();
+#pragma unroll
+  for (uint32_t k = 0; k < 4u; ++k) {
+    const uint32_t i = 4u * lane + k;
+    if (i < n) S[i] = run;
+    run += v[k];
+  }
+  bc_sync();
+}
+
+// Decode one blob (already walked) into its canonical record at O. Returns 0
+// or a CRDT_E* code (the record is then not valid).
+__device__ int bc_write_record(const uint8_t* B, const BcWalk& w, uint32_t wa, uint32_t wm, uint32_t A, bool sparse,
+                               uint8_t* X, uint8_t* O, uint32_t lane) {
+  RecLayout L;
+  rec_layout(L, sparse ? w.n_clk : A, w.n_mem, w.n_dot, w.n_def, w.n_def_dot, w.n_def_mem, sparse);
+  const uint64_t sa = wa + 8u;
+  bool bad = false;
+  // ---- top clock: BTreeMap order = strictly increasing actors
+  if (!sparse)
+    for (uint32_t a = lane; a < A; a += kBcWave) ((uint64_t*)(O + L.o_clk))[a] = 0ull;
+  __threadfence_block();
+  for (uint32_t k = lane; k < w.n_clk; k += kBcWave) {
+    const uint64_t e = 8u + k * sa;
+    const uint64_t x = rdw(B, e, wa), c = rdw(B, e + wa, 8);
+    bad = bad || x >= A || c == 0u || (k && rdw(B, e - sa, wa) >= x);
+    if (x < A) {
+      if (sparse) {
+        ((uint64_t*)(O + L.o_clk))[k] = c;
+        ((uint32_t*)(O + L.o_cact))[k] = (uint32_t)x;
+      } else {
+        ((uint64_t*)(O + L.o_clk))[x] = c;
+      }
+    }
+  }
+  if (sparse && lane == 0u && (w.n_clk & 1u)) *(uint32_t*)(O + L.o_cact + 4u * w.n_clk) = 0u;
+  // ---- members: rank by key (HashMap order is arbitrary), dot offsets in key order
+  uint32_t* Pm = (uint32_t*)(X + kXPm);
+  uint32_t* Lm = (uint32_t*)(X + kXLm);
+  uint64_t* Km = (uint64_t*)(X + kXKm);
+  uint32_t* Rm = (uint32_t*)(X + kXRm);
+  uint32_t* Sm = (uint32_t*)(X + kXSm);
+  bc_sync();
+  for (uint32_t e = lane; e < w.n_mem; e += kBcWave) Km[e] = rdw(B, Pm[e], wm);
+  bc_sync();
+  for (uint32_t e = lane; e < w.n_mem; e += kBcWave) {
+    const uint64_t k = Km[e];
+    uint32_t r = 0, eq = 0;
+    for (uint32_t f = 0; f < w.n_mem; ++f) {
+      const uint64_t kf = Km[f];
+      r += kf < k ? 1u : 0u;
+      eq += kf == k ? 1u : 0u;
+    }
+    bad = bad || eq != 1u;
+    Rm[e] = r;
+    Sm[r < kBcMaxMem ? r : 0u] = Lm[e];
+  }
+  bc_sync();
+  bc_scan_excl(Sm, w.n_mem, lane);
+  for (uint32_t e = lane; e < w.n_mem; e += kBcWave) {
+    const uint32_t r = Rm[e], d0 = Sm[r], l = Lm[e];
+    ((uint64_t*)(O + L.o_key))[r] = Km[e];
+    ((uint32_t*)(O + L.o_mdend))[r] = d0 + l;
+    const uint64_t p = Pm[e] + wm + 8u;
+    uint64_t prev = 0;
+    for (uint32_t i = 0; i < l; ++i) {
+      const uint64_t x = rdw(B, p + i * sa, wa), c = rdw(B, p + i * sa + wa, 8);
+      bad = bad || x >= A || c == 0u || (i && prev >= x);
+      prev = x;
+      ((uint32_t*)(O + L.o_dact))[d0 + i] = (uint32_t)x;
+      ((uint64_t*)(O + L.o_dctr))[d0 + i] = c;
+    }
+  }
+  // ---- deferred: clocks sorted in CLOCK ORDER, member sets sorted
+  uint32_t* Pd = (uint32_t*)(X + kXPd);
+  uint32_t* Ld = (uint32_t*)(X + kXLd);
+  uint32_t* Ps = (uint32_t*)(X + kXPs);
+  uint32_t* Ls = (uint32_t*)(X + kXLs);
+  uint32_t* Sd = (uint32_t*)(X + kXSd);
+  uint32_t* Ss = (uint32_t*)(X + kXSs);
+  uint32_t* Rd = (uint32_t*)(X + kXRd);
+  if (w.n_def) {
+    for (uint32_t d = lane; d < w.n_def; d += kBcWave) {
+      uint32_t r = 0;
+      for (uint32_t f = 0; f < w.n_def; ++f) {
+        if (f == d) continue;
+        const int c = bc_clock_cmp(B, Pd[f] + 8u, Ld[f], Pd[d] + 8u, Ld[d], wa);
+        r += c < 0 ? 1u : 0u;
+        bad = bad || c == 0;  // structurally equal HashMap keys
+      }
+      Rd[d] = r;
+      Sd[r < kBcMaxDef ? r : 0u] = Ld[d];
+      Ss[r < kBcMaxDef ? r : 0u] = Ls[d];
+    }
+    bc_sync();
+    bc_scan_excl(Sd, w.n_def, lane);
+    bc_scan_excl(Ss, w.n_def, lane);
+    for (uint32_t d = lane; d < w.n_def; d += kBcWave) {
+      const uint32_t r = Rd[d], a0 = Sd[r], m0 = Ss[r], lc = Ld[d], ls = Ls[d];
+      ((uint32_t*)(O + L.o_fdend))[r] = a0 + lc;
+      ((uint32_t*)(O + L.o_fmend))[r] = m0 + ls;
+      const uint64_t p = Pd[d] + 8u;
+      uint64_t prev = 0;
+      for (uint32_t i = 0; i < lc; ++i) {
+        const uint64_t x = rdw(B, p + i * sa, wa), c = rdw(B, p + i * sa + wa, 8);
+        bad = bad || x >= A || c == 0u || (i && prev >= x);
+        prev = x;
+        ((uint32_t*)(O + L.o_fact))[a0 + i] = (uint32_t)x;
+        ((uint64_t*)(O + L.o_fctr))[a0 + i] = c;
+      }
+      const uint64_t q = Ps[d] + 8u;
+      for (uint32_t i = 0; i < ls; ++i) {  // the set's elements by rank (HashSet order is arbitrary)
+        const uint64_t m = rdw(B, q + (uint64_t)i * wm, wm);
+        uint32_t rk = 0, eq = 0;
+        for (uint32_t j = 0; j < ls; ++j) {
+          const uint64_t mj = rdw(B, q + (uint64_t)j * wm, wm);
+          rk += mj < m ? 1u : 0u;
+          eq += mj == m ? 1u : 0u;
+        }
+        bad = bad || eq != 1u;
+        ((uint64_t*)(O + L.o_fkey))[m0 + (rk < ls ? rk : 0u)] = m;
+      }
+    }
+  }
+  // ---- padding and header
+  if (lane == 0u && L.o_def != L.o_mpad) *(uint32_t*)(O + L.o_mpad) = 0u;
+  if (lane >= 1u && lane < 4u && L.o_end + 4u * (lane - 1u) < L.size) *(uint32_t*)(O + L.o_end + 4u * (lane - 1u)) = 0u;
+  if (lane == 0u) {
+    uint32_t* h = (uint32_t*)O;
+    h[0] = L.size; h[1] = L.n_clk; h[2] = L.n_mem; h[3] = L.n_dot;
+    h[4] = L.n_def; h[5] = L.n_def_dot; h[6] = L.n_def_mem; h[7] = sparse ? kSparseClock : 0u;
+  }
+  return __ballot(bad) ? CRDT_ENONCANON : 0;
+}
+
+// Stage blob bytes [off, off + len) of a buffer of `bytes` bytes into the
+// wave's window; returns the pointer to the blob's first byte in LDS.
+__device__ const uint8_t* bc_stage(const uint8_t* base, uint64_t bytes, uint64_t off, uint64_t len, v4u* S,
+                                   uint32_t lane) {
+  const uint64_t a0 = off & ~15ull, a1 = (off + len + 15u) & ~15ull;
+  const uint32_t n16 = (uint32_t)((a1 - a0) / 16u);
+  bc_sync();
+  for (uint32_t k = lane; k < n16; k += kBcWave) {
+    const uint64_t g = a0 + 16ull * k;
+    if (g + 16u <= bytes) {
+      S[k] = __builtin_nontemporal_load((const v4u*)(base + g));
+    } else {  // the buffer's last partial line
+      uint8_t* s = (uint8_t*)(S + k);
+      for (uint32_t i = 0; i < 16u; ++i) s[i] = g + i < bytes ? base[g + i] : (uint8_t)0;
+    }
+  }
+  bc_sync();
+  return (const uint8_t*)S + (off - a0);
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(kBcWave * kBcWaves) void bincode_ingest_kernel(
+    const uint8_t* __restrict__ blobs, uint64_t blob_bytes, const uint64_t* __restrict__ boff,
+    const uint64_t* __restrict__ blen, uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags,
+    uint64_t* __restrict__ sizes, uint8_t* __restrict__ out, const uint64_t* __restrict__ ooff, uint64_t out_bytes,
+    int* __restrict__ status) {
+  __shared__ v4u st_s[kBcWaves][kBcStage / 16];
+  __shared__ v4u sx_s[kBcWaves][kXBytes / 16];
+  const uint32_t lane = threadIdx.x & (kBcWave - 1u), wave = threadIdx.x / kBcWave;
+  uint8_t* X = (uint8_t*)sx_s[wave];
+  const bool sparse = (flags & kSparseClock) != 0u;
+  for (uint64_t o = (uint64_t)blockIdx.x * kBcWaves + wave; o < n_obj; o += (uint64_t)gridDim.x * kBcWaves) {
+    const uint64_t off = boff[o], len = blen[o];
+    if (off > blob_bytes || len > blob_bytes - off) {
+      if (lane == 0u) {
+        atomicCAS(status, 0, CRDT_ENONCANON);
+        if (!WRITE) sizes[o] = 0u;
+      }
+      continue;
+    }
+    const uint8_t* B = len + 32u <= kBcStage ? bc_stage(blobs, blob_bytes, off, len, st_s[wave], lane) : blobs + off;
+    bc_sync();
+    const BcWalk w = bc_walk(B, len, wa, wm, A, X, lane);
+    if (w.err) {
+      if (lane == 0u) {
+        atomicCAS(status, 0, w.err);
+        if (!WRITE) sizes[o] = 0u;
+      }
+      continue;
+    }
+    const uint64_t size = record_size64(sparse ? w.n_clk : A, w.n_mem, w.n_dot, w.n_def, w.n_def_dot, w.n_def_mem,
+                                        sparse);
+    if (!WRITE) {
+      if (lane == 0u) sizes[o] = size;
+      continue;
+    }
+    const uint64_t oo = ooff[o];
+    if ((oo & 15u) || oo > out_bytes || size > out_bytes - oo) {
+      if (lane == 0u) atomicCAS(status, 0, CRDT_ECAPACITY);
+      continue;
+    }
+    bc_sync();
+    const int rc = bc_write_record(B, w, wa, wm, A, sparse, X, out + oo, lane);
+    if (rc && lane == 0u) atomicCAS(status, 0, rc);
+  }
+}
+
+// ---------------------------------------------------------------- egest
+__device__ __forceinline__ uint64_t bc_blob_len(const uint32_t* h, const uint8_t* r, uint32_t wa, uint32_t wm,
+                                                uint32_t nnz) {
+  (void)r;
+  const uint64_t sa = wa + 8u;
+  return 8u + nnz * sa + 8u + (uint64_t)h[2] * (wm + 8u) + (uint64_t)h[3] * sa + 8u + 16ull * h[4] +
+         (uint64_t)h[5] * sa + (uint64_t)h[6] * wm;
+}
+
+// nonzero top-clock entries of a record (dense: count of nonzero slots)
+__device__ uint32_t bc_nnz(const uint8_t* r, const uint32_t* h, uint32_t lane) {
+  if (h[7] & kSparseClock) return h[1];
+  uint32_t n = 0;
+  for (uint32_t a = lane; a < h[1]; a += kBcWave) n += ((const uint64_t*)(r + kHdrBytes))[a] != 0u ? 1u : 0u;
+  for (uint32_t d = 32; d >= 1; d >>= 1) n += __shfl_xor(n, d, kBcWave);
+  return n;
+}
+
+__device__ bool bc_record_ok(const uint8_t* base, uint64_t bytes, uint64_t off, uint32_t A, uint32_t flags) {
+  if ((off & 15u) || off + kHdrBytes > bytes) return false;
+  const uint32_t* h = (const uint32_t*)(base + off);
+  const bool sparse = (flags & kSparseClock) != 0u;
+  if (h[7] != flags || (sparse ? h[1] > A : h[1] != A)) return false;
+  const uint64_t sz = record_size64(h[1], h[2], h[3], h[4], h[5], h[6], sparse);
+  return sz == h[0] && off + sz <= bytes;
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(kBcWave * kBcWaves) void bincode_egest_kernel(
+    const uint8_t* __restrict__ rb, uint64_t rbytes, const uint64_t* __restrict__ roff, uint64_t n_obj, uint32_t A,
+    uint32_t flags, uint32_t wa, uint32_t wm, uint64_t* __restrict__ sizes, uint8_t* __restrict__ out,
+    const uint64_t* __restrict__ ooff, uint64_t out_bytes, int* __restrict__ status) {
+  __shared__ v4u st_s[kBcWaves][kBcStage / 16];
+  const uint32_t lane = threadIdx.x & (kBcWave - 1u), wave = threadIdx.x / kBcWave;
+  const uint64_t amax = wa >= 8u ? ~0ull : (1ull << (8u * wa)) - 1u, mmax = wm >= 8u ? ~0ull : (1ull << (8u * wm)) - 1u;
+  for (uint64_t o = (uint64_t)blockIdx.x * kBcWaves + wave; o < n_obj; o += (uint64_t)gridDim.x * kBcWaves) {
+    const uint64_t ro = roff[o];
+    if (!bc_record_ok(rb, rbytes, ro, A, flags)) {
+      if (lane == 0u) {
+        atomicCAS(status, 0, CRDT_ENONCANON);
+        if (!WRITE) sizes[o] = 0u;
+      }
+      continue;
+    }
+    const uint8_t* r = rb + ro;
+    const uint32_t* h = (const uint32_t*)r;
+    const bool sparse = (flags & kSparseClock) != 0u;
+    RecLayout L;
+    rec_layout(L, h[1], h[2], h[3], h[4], h[5], h[6], sparse);
+    const uint32_t nnz = bc_uni(bc_nnz(r, h, lane));
+    const uint64_t len = bc_blob_len(h, r, wa, wm, nnz);
+    if (!WRITE) {
+      if (lane == 0u) sizes[o] = len;
+      continue;
+    }
+    const uint64_t oo = ooff[o];
+    const uint64_t padded = (len + 15u) & ~15ull;
+    if ((oo & 15u) || oo > out_bytes || padded > out_bytes - oo) {
+      if (lane == 0u) atomicCAS(status, 0, CRDT_ECAPACITY);
+      continue;
+    }
+    const bool staged = padded <= kBcStage;
+    uint8_t* T = staged ? (uint8_t*)st_s[wave] : out + oo;
+    const uint64_t sa = wa + 8u;
+    bool bad = (uint64_t)(A - 1u) > amax;
+    bc_sync();
+    if (staged) {
+      for (uint32_t k = lane; k < (uint32_t)(padded / 16u); k += kBcWave) st_s[wave][k] = v4u{0u, 0u, 0u, 0u};
+    } else {
+      for (uint64_t k = len + lane; k < padded; k += kBcWave) T[k] = 0u;
+    }
+    bc_sync();
+    // top clock: BTreeMap<A, u64> = length, then (actor, counter) ascending
+    if (lane == 0u) wrw(T, 0, nnz, 8);
+    if (sparse) {
+      for (uint32_t k = lane; k < h[1]; k += kBcWave) {
+        wrw(T, 8u + k * sa, ((const uint32_t*)(r + L.o_cact))[k], wa);
+        wrw(T, 8u + k * sa + wa, ((const uint64_t*)(r + L.o_clk))[k], 8);
+      }
+    } else {
+      uint32_t run = 0;
+      for (uint32_t a0 = 0; a0 < h[1]; a0 += kBcWave) {
+        const uint32_t a = a0 + lane;
+        const uint64_t c = a < h[1] ? ((const uint64_t*)(r + L.o_clk))[a] : 0ull;
+        const uint64_t nz = __ballot(c != 0u);
+        const uint32_t k = run + __builtin_amdgcn_mbcnt_hi((uint32_t)(nz >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nz, 0u));
+        if (c != 0u) {
+          wrw(T, 8u + k * sa, a, wa);
+          wrw(T, 8u + k * sa + wa, c, 8);
+        }
+        run += (uint32_t)__popcll(nz);
+      }
+    }
+    // entries: HashMap<M, VClock<A>> = length, then (member, clock) — key order
+    const uint64_t E = 8u + nnz * sa;
+    if (lane == 0u) wrw(T, E, h[2], 8);
+    for (uint32_t m = lane; m < h[2]; m += kBcWave) {
+      const uint32_t s = m ? ((const uint32_t*)(r + L.o_mdend))[m - 1] : 0u, e = ((const uint32_t*)(r + L.o_mdend))[m];
+      const uint64_t p = E + 8u + (uint64_t)m * (wm + 8u) + (uint64_t)s * sa;
+      const uint64_t key = ((const uint64_t*)(r + L.o_key))[m];
+      bad = bad || key > mmax;
+      wrw(T, p, key, wm);
+      wrw(T, p + wm, e - s, 8);
+      for (uint32_t i = s; i < e; ++i) {
+        wrw(T, p + wm + 8u + (i - s) * sa, ((const uint32_t*)(r + L.o_dact))[i], wa);
+        wrw(T, p + wm + 8u + (i - s) * sa + wa, ((const uint64_t*)(r + L.o_dctr))[i], 8);
+      }
+    }
+    // deferred: HashMap<VClock<A>, HashSet<M>> = length, then (clock, set) — clock order
+    const uint64_t F = E + 8u + (uint64_t)h[2] * (wm + 8u) + (uint64_t)h[3] * sa;
+    if (lane == 0u) wrw(T, F, h[4], 8);
+    for (uint32_t d = lane; d < h[4]; d += kBcWave) {
+      const uint32_t s = d ? ((const uint32_t*)(r + L.o_fdend))[d - 1] : 0u, e = ((const uint32_t*)(r + L.o_fdend))[d];
+      const uint32_t ms = d ? ((const uint32_t*)(r + L.o_fmend))[d - 1] : 0u, me = ((const uint32_t*)(r + L.o_fmend))[d];
+      const uint64_t p = F + 8u + 16ull * d + (uint64_t)s * sa + (uint64_t)ms * wm;
+      wrw(T, p, e - s, 8);
+      for (uint32_t i = s; i < e; ++i) {
+        wrw(T, p + 8u + (i - s) * sa, ((const uint32_t*)(r + L.o_fact))[i], wa);
+        wrw(T, p + 8u + (i - s) * sa + wa, ((const uint64_t*)(r + L.o_fctr))[i], 8);
+      }
+      const uint64_t q = p + 8u + (uint64_t)(e - s) * sa;
+      wrw(T, q, me - ms, 8);
+      for (uint32_t j = ms; j < me; ++j) {
+        const uint64_t key = ((const uint64_t*)(r + L.o_fkey))[j];
+        bad = bad || key > mmax;
+        wrw(T, q + 8u + (uint64_t)(j - ms) * wm, key, wm);
+      }
+    }
+    if (staged) {
+      bc_sync();
+      for (uint32_t k = lane; k < (uint32_t)(padded / 16u); k += kBcWave)
+        __builtin_nontemporal_store(st_s[wave][k], (v4u*)(out + oo) + k);
+    }
+    if (__ballot(bad) && lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);  // a value wider than its field
+  }
+}
+
+uint32_t bc_blocks(uint64_t n_obj) {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const uint64_t want = (n_obj + kBcWaves - 1) / kBcWaves, cap = (uint64_t)cus * 8u;
+  return (uint32_t)(want < cap ? want : cap);
+}
+
+}  // namespace
+
+int launch_bincode_ingest(const uint8_t* blobs, uint64_t blob_bytes, const uint64_t* boff, const uint64_t* blen,
+                          uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags, uint64_t* sizes,
+                          uint8_t* out, const uint64_t* ooff, uint64_t out_bytes, int* status, hipStream_t stream) {
+  if (n_obj == 0) return CRDT_OK;
+  const uint32_t blocks = bc_blocks(n_obj);
+  if (sizes)
+    hipLaunchKernelGGL(bincode_ingest_kernel<false>, dim3(blocks), dim3(kBcWave * kBcWaves), 0, stream, blobs,
+                       blob_bytes, boff, blen, n_obj, wa, wm, A, flags, sizes, out, ooff, out_bytes, status);
+  else
+    hipLaunchKernelGGL(bincode_ingest_kernel<true>, dim3(blocks), dim3(kBcWave * kBcWaves), 0, stream, blobs,
+                       blob_bytes, boff, blen, n_obj, wa, wm, A, flags, sizes, out, ooff, out_bytes, status);
+  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+}
+
+int launch_bincode_egest(const uint8_t* rb, uint64_t rbytes, const uint64_t* roff, uint64_t n_obj, uint32_t A,
+                         uint32_t flags, uint32_t wa, uint32_t wm, uint64_t* sizes, uint8_t* out,
+                         const uint64_t* ooff, uint64_t out_bytes, int* status, hipStream_t stream) {
+  if (n_obj == 0) return CRDT_OK;
+  const uint32_t blocks = bc_blocks(n_obj);
+  if (sizes)
+    hipLaunchKernelGGL(bincode_egest_kernel<false>, dim3(blocks), dim3(kBcWave * kBcWaves), 0, stream, rb, rbytes,
+                       roff, n_obj, A, flags, wa, wm, sizes, out, ooff, out_bytes, status);
+  else
+    hipLaunchKernelGGL(bincode_egest_kernel<true>, dim3(blocks), dim3(kBcWave * kBcWaves), 0, stream, rb, rbytes,
+                       roff, n_obj, A, flags, wa, wm, sizes, out, ooff, out_bytes, status);
+  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+}
+
+}  // namespace crdts_hip

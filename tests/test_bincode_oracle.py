@@ -1,0 +1,108 @@
+"""CPU tests of the bincode restatement (oracle/bincode_ref.py) that pins the
+GPU ingest / egest codec (crdt_orswot_{from,to}_bincode), and of the
+product's host-side helpers for it. SURVEY.md §8(f) rank 1."""
+import os
+import random
+import struct
+import sys
+
+import pytest
+
+import records
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "oracle"))
+import bincode_ref as BC  # noqa: E402
+
+WIDTHS = [(1, 8), (2, 8), (4, 4), (8, 8)]
+
+
+def _states(n=200, seed=1, sparse=False):
+    import crdts_hip
+
+    if sparse:
+        (b, o), _ = crdts_hip.generate_replicas(n, 2, threads=4)
+    else:
+        (b, o), _ = crdts_hip.generate_orswot(n, first_obj=seed, threads=4)
+    return [records.decode(r) for r in records.unpack_batch(b, o)]
+
+
+def small_members(st):
+    """The same state with member keys replaced by their rank (order kept)."""
+    keys = sorted(set(st["entries"]) | {m for _, ms in st["deferred"] for m in ms})
+    r = {k: i + 1 for i, k in enumerate(keys)}
+    return dict(clock=st["clock"], entries={r[m]: d for m, d in st["entries"].items()},
+                deferred=[(c, [r[m] for m in ms]) for c, ms in st["deferred"]])
+
+
+def _fits(st, wa, wm):
+    amax, mmax = (1 << (8 * wa)) - 1, (1 << (8 * wm)) - 1
+    acts = list(st["clock"]) + [a for d in st["entries"].values() for a, _ in d] + \
+        [a for c, _ in st["deferred"] for a, _ in c]
+    mems = list(st["entries"]) + [m for _, ms in st["deferred"] for m in ms]
+    return all(a <= amax for a in acts) and all(m <= mmax for m in mems)
+
+
+def test_doc_example_bytes():
+    """src/lib.rs:53-60: Orswot<u8, u8> after one add of member 1 by actor 1.
+    Bytes derived from the format restatement (not from reference output)."""
+    st = dict(clock={1: 1}, entries={1: [(1, 1)]}, deferred=[])
+    b = BC.encode(st, 1, 1)
+    exp = (struct.pack("<Q", 1) + b"\x01" + struct.pack("<Q", 1) +      # clock {1: 1}
+           struct.pack("<Q", 1) + b"\x01" + struct.pack("<Q", 1) + b"\x01" + struct.pack("<Q", 1) +  # entries
+           struct.pack("<Q", 0))                                        # deferred {}
+    assert b == exp and len(b) == 51
+    assert BC.decode(b, 1, 1) == st
+
+
+@pytest.mark.parametrize("wa,wm", WIDTHS)
+def test_round_trip_generator_states(wa, wm):
+    rng = random.Random(wa * 10 + wm)
+    n = 0
+    for st in _states(300, seed=wa):
+        st = st if wm == 8 else small_members(st)
+        if not _fits(st, wa, wm):
+            continue
+        n += 1
+        want = dict(clock=st["clock"], entries=st["entries"], deferred=st["deferred"])
+        assert BC.decode(BC.encode(want, wa, wm), wa, wm) == want
+        assert BC.decode(BC.encode(want, wa, wm, rng=rng), wa, wm) == want  # any HashMap order
+    assert n > 100
+
+
+def test_round_trip_sparse_states():
+    for st in _states(100, sparse=True):
+        want = dict(clock=st["clock"], entries=st["entries"], deferred=st["deferred"])
+        assert BC.decode(BC.encode(want, 2, 8, rng=random.Random(3)), 2, 8) == want
+
+
+def test_deferred_states_present():
+    sts = _states(2000)
+    assert sum(1 for s in sts if s["deferred"]) > 20
+
+
+@pytest.mark.parametrize("damage", ["truncate", "trailing", "dup_member", "clock_order", "dup_set"])
+def test_malformed(damage):
+    st = dict(clock={1: 3, 2: 4}, entries={7: [(1, 3)], 9: [(2, 4)]}, deferred=[([(3, 1)], [5, 6])])
+    b = bytearray(BC.encode(st, 1, 1))
+    if damage == "truncate":
+        b = b[:-1]
+    elif damage == "trailing":
+        b += b"\x00"
+    elif damage == "dup_member":
+        b[8 + 2 * 9 + 8 + 18] = 7          # second member key := 7
+    elif damage == "clock_order":
+        b[8], b[17] = 2, 1                  # BTreeMap keys 2, 1
+    elif damage == "dup_set":
+        b[-1] = 5                            # set {5, 5}
+    with pytest.raises(BC.FormatError):
+        BC.decode(bytes(b), 1, 1)
+
+
+def test_record_form_agrees():
+    """decode(encode(record state)) re-encodes to the same canonical record."""
+    for st in _states(200, seed=9):
+        back = BC.decode(BC.encode(st, 1, 8, rng=random.Random(1)), 1, 8)
+        rec = records.encode(back["clock"], {m: dict(d) for m, d in back["entries"].items()},
+                             {tuple(c): set(ms) for c, ms in back["deferred"]}, 16)
+        assert records.decode(rec)["entries"] == st["entries"]
+        assert records.decode(rec)["deferred"] == st["deferred"]
