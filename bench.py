@@ -35,7 +35,7 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="orswot",
-                   choices=["orswot", "gcounter", "pncounter", "orswot_csr", "gcounter_ae"])
+                   choices=["orswot", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode"])
     p.add_argument("--replicas", type=int, default=8, help="orswot_csr at N=1: replicas folded locally")
     p.add_argument("--n-obj", type=int, default=None, help="objects per GPU")
     p.add_argument("--threads", type=int, default=16, help="host threads (generation, CPU baseline)")
@@ -438,6 +438,104 @@ def run_gcounter_ae(args, rank, world, local):
     return res
 
 
+def run_bincode(args, rank, world, local):
+    """ingest of the reference's binary form
+    (`from_binary`, src/lib.rs:78-83) into canonical records, and egest
+    (`to_binary`, :62-64), for the config-3 objects (1M per GPU, actors u8,
+    members u64). A step = one ingest of the whole shard: the sizes pass,
+    the offset scan and the decode pass, inputs resident in HBM; egest is
+    timed the same way and reported beside it."""
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    import crdts_hip
+    from crdts_hip._lib import check, lib
+
+    n = args.n_obj or 1_000_000
+    WA, WM, A = 1, 8, 16
+    (lb, lo), _ = crdts_hip.generate_orswot(n, first_obj=rank * n, threads=args.threads)
+    eng = crdts_hip.Engine(local)
+    dev = f"cuda:{local}"
+    B = crdts_hip.OrswotBatch.from_host(lb, lo, A, device=local)
+    blobs, boff, blen = eng.orswot_to_bincode(B, WA, WM)  # checked once; the timed steps reuse the buffers
+    back = eng.orswot_from_bincode(blobs, boff, blen, A, WA, WM)
+    assert torch.equal(back.base[: int(lb.nbytes)], B.base[: int(lb.nbytes)])
+    stream = torch.cuda.Stream(device=local)
+    st = C.c_void_p(stream.cuda_stream)
+    sizes = torch.empty(n, dtype=torch.int64, device=dev)
+    rec = torch.empty_like(back.base)
+    roff = torch.empty(n, dtype=torch.int64, device=dev)
+    p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+
+    def ingest():
+        check(lib.crdt_orswot_bincode_record_sizes(eng.ctx, p(blobs), int(blobs.numel()), p(boff), p(blen), n, WA,
+                                                   WM, A, 0, p(sizes), st))
+        with torch.cuda.stream(stream):
+            torch.cumsum(sizes, 0, out=roff)
+            roff.sub_(sizes)
+        check(lib.crdt_orswot_from_bincode(eng.ctx, p(blobs), int(blobs.numel()), p(boff), p(blen), n, WA, WM, A,
+                                           0, p(rec), p(roff), int(rec.numel()), st))
+
+    eb = B.cbatch()
+    lens = torch.empty(n, dtype=torch.int64, device=dev)
+    eoff = torch.empty(n, dtype=torch.int64, device=dev)
+    eout = torch.empty_like(blobs)
+
+    def egest():
+        check(lib.crdt_orswot_bincode_sizes(eng.ctx, C.byref(eb), A, 0, WA, WM, p(lens), st))
+        with torch.cuda.stream(stream):
+            pad = (lens + 15) // 16 * 16
+            torch.cumsum(pad, 0, out=eoff)
+            eoff.sub_(pad)
+        check(lib.crdt_orswot_to_bincode(eng.ctx, C.byref(eb), A, 0, WA, WM, p(eout), p(eoff), int(eout.numel()),
+                                         st))
+
+    wall, ev_ms = _timed_steps(args, world, stream, ingest)
+    eng.status(stream)
+    assert torch.equal(rec[: int(lb.nbytes)], B.base[: int(lb.nbytes)])
+    ewall, eev_ms = _timed_steps(args, world, stream, egest)
+    eng.status(stream)
+    assert torch.equal(eout, blobs)
+    blob_bytes = int(blen.sum().item())
+    rec_bytes = int(lb.nbytes)
+    # algorithmic bytes: ingest reads every blob twice (sizes pass, decode pass) + offsets/lengths,
+    # writes every record once + sizes/offsets; egest reads records twice, writes blobs once
+    alg_in = 2 * blob_bytes + rec_bytes + 8 * 6 * n
+    alg_eg = 2 * rec_bytes + blob_bytes + 8 * 5 * n
+    total = sum_over_ranks(float(n * args.steps), world)
+    res = {
+        "metric": "bincode ingest (from_binary -> canonical records) objects/sec (node)",
+        "value": total / wall, "unit": "objects/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8", "data": "synthetic: config-3 op-simulated Orswots, their to_binary form (actor u8, member u64)",
+        "config": {"workload": f"bincode config3: {n} objects per GPU, {blob_bytes / n:.0f} B blob, "
+                               f"{rec_bytes / n:.0f} B record", "parallelism": f"dp{world} (objects sharded)"},
+        "egest": {"value": sum_over_ranks(float(n * args.steps), world) / ewall, "unit": "objects/s",
+                  "ms_per_step": ewall / args.steps * 1e3, "achieved_GBps": alg_eg / (eev_ms * 1e-3) / 1e9},
+    }
+    if world == 1:
+        ach = alg_in / (ev_ms * 1e-3) / 1e9
+        res["roofline"] = {"bound": "hbm", "kernel": "bincode_ingest_kernel (sizes + decode) + scan",
+                           "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                           "kernel_ms": ev_ms, "alg_bytes_per_launch": alg_in, "traffic": None}
+        if not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(REPO, "tests"))
+            import oracle_ffi
+
+            m = min(args.cpu_sample // 5, n)
+            hb = blobs.cpu().numpy()
+            ho = boff[:m].cpu().numpy().astype(np.uint64)
+            hl = blen[:m].cpu().numpy().astype(np.uint64)
+            th = max(1, min(args.threads, os.cpu_count() or 1))
+            secs = oracle_ffi.bincode_ingest_bench(hb, ho, hl, WA, WM, A, 0, th)
+            res["cpu_baseline"] = {"value": m / secs, "unit": "objects/s", "cores": th, "kind": "port",
+                                   "sample": f"{m} blobs, from_binary into map/unordered_map + record encode, "
+                                             f"{th} threads"}
+    return res
+
+
 def main():
     args = parse()
     rank, world, local = dist_setup()
@@ -449,6 +547,8 @@ def main():
         res = run_orswot_csr(args, rank, world, local)
     elif args.workload == "gcounter_ae":
         res = run_gcounter_ae(args, rank, world, local)
+    elif args.workload == "bincode":
+        res = run_bincode(args, rank, world, local)
     else:
         res = run_dense(args, rank, world, local, args.workload)
     if rank == 0:

@@ -23,6 +23,7 @@
 // Canonical record encoding follows include/crdts_hip.h (the boundary spec);
 // this file has its own encoder/decoder, independent of the product's.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <cstring>
@@ -398,6 +399,91 @@ static void vclock_to_row(const VClock& v, uint64_t* row, uint32_t n) {
 
 using namespace oracle;
 
+// ---------------------------------------------------------------- binary form
+// to_binary / from_binary (src/lib.rs:62-83) = bincode 0.9 of the serde
+// derives on Orswot (src/orswot.rs:26-30) / VClock (src/vclock.rs:54-57),
+// restated (bincode is not vendored): u64 LE lengths before maps and sets,
+// fixed-width LE integers, fields in declaration order. Decoding fills the
+// reference-shaped containers (std::map / unordered_map / unordered_set),
+// i.e. it pays what `from_binary` pays; encoding walks them in their own
+// (hash) order as `to_binary` does.
+namespace oracle {
+struct BinReader {
+  const uint8_t* p;
+  size_t n, pos = 0;
+  bool ok = true;
+  uint64_t get(int w) {
+    if (pos + (size_t)w > n) { ok = false; return 0; }
+    uint64_t v = 0;
+    for (int i = 0; i < w; ++i) v |= (uint64_t)p[pos + i] << (8 * i);
+    pos += w;
+    return v;
+  }
+};
+
+static bool bin_vclock(BinReader& r, int wa, VClock& v) {
+  const uint64_t n = r.get(8);
+  if (!r.ok || n > r.n) return false;
+  bool first = true;
+  Actor last = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t a = r.get(wa), c = r.get(8);
+    if (!r.ok || a > 0xFFFFFFFFull || (!first && a <= last)) return false;  // BTreeMap: ascending keys
+    v.dots.emplace_hint(v.dots.end(), (Actor)a, c);
+    last = (Actor)a;
+    first = false;
+  }
+  return true;
+}
+
+bool from_binary(const uint8_t* p, size_t n, int wa, int wm, Orswot& o) {
+  BinReader r{p, n};
+  if (!bin_vclock(r, wa, o.clock)) return false;
+  const uint64_t ne = r.get(8);
+  if (!r.ok || ne > n) return false;
+  for (uint64_t i = 0; i < ne; ++i) {
+    const Member m = r.get(wm);
+    VClock v;
+    if (!r.ok || !bin_vclock(r, wa, v)) return false;
+    if (!o.entries.emplace(m, std::move(v)).second) return false;  // duplicate HashMap key
+  }
+  const uint64_t nd = r.get(8);
+  if (!r.ok || nd > n) return false;
+  for (uint64_t i = 0; i < nd; ++i) {
+    VClock v;
+    if (!bin_vclock(r, wa, v)) return false;
+    const uint64_t ns = r.get(8);
+    if (!r.ok || ns > n) return false;
+    std::unordered_set<Member> s;
+    for (uint64_t j = 0; j < ns; ++j) {
+      const Member m = r.get(wm);
+      if (!r.ok || !s.insert(m).second) return false;
+    }
+    if (!o.deferred.emplace(std::move(v), std::move(s)).second) return false;
+  }
+  return r.ok && r.pos == n;
+}
+
+static void put(std::vector<uint8_t>& out, uint64_t v, int w) {
+  for (int i = 0; i < w; ++i) out.push_back((uint8_t)(v >> (8 * i)));
+}
+static void bin_put_vclock(std::vector<uint8_t>& out, const VClock& v, int wa) {
+  put(out, v.dots.size(), 8);
+  for (const auto& kv : v.dots) { put(out, kv.first, wa); put(out, kv.second, 8); }
+}
+void to_binary(const Orswot& o, int wa, int wm, std::vector<uint8_t>& out) {
+  bin_put_vclock(out, o.clock, wa);
+  put(out, o.entries.size(), 8);
+  for (const auto& kv : o.entries) { put(out, kv.first, wm); bin_put_vclock(out, kv.second, wa); }
+  put(out, o.deferred.size(), 8);
+  for (const auto& kv : o.deferred) {
+    bin_put_vclock(out, kv.first, wa);
+    put(out, kv.second.size(), 8);
+    for (Member m : kv.second) put(out, m, wm);
+  }
+}
+}  // namespace oracle
+
 extern "C" {
 
 size_t orc_record_bytes(uint32_t n_clk, uint32_t n_mem, uint32_t n_dot, uint32_t n_def,
@@ -473,6 +559,60 @@ double orc_orswot_bench(const uint8_t* lb, const uint64_t* loff, size_t lbytes,
   for (size_t i = 0; i < n; i += 997) sink += L[i].entries.size();
   (void)sink;
   std::vector<Orswot>().swap(L);
+  return std::chrono::duration<double>(t1 - t0).count();
+}
+
+
+// Blob -> canonical record (0 ok / -2 not decodable or not canonical / -4 cap).
+long orc_bincode_to_record(const uint8_t* blob, size_t n, int wa, int wm, uint32_t n_actors, uint32_t flags,
+                           uint8_t* out, size_t cap) {
+  Orswot o;
+  if (!from_binary(blob, n, wa, wm, o)) return -2;
+  for (const auto& kv : o.clock.dots) if (kv.first >= n_actors || kv.second == 0) return -2;
+  return encode(o, n_actors, out, cap, (flags & CRDT_ORSWOT_SPARSE_CLOCK) != 0);
+}
+
+// CPU baseline of ingest: from_binary + canonical encode of n blobs over
+// `threads` std::threads; returns seconds (records written to thread-local
+// scratch, not kept).
+double orc_bincode_ingest_bench(const uint8_t* blobs, const uint64_t* off, const uint64_t* len, size_t n, int wa,
+                                int wm, uint32_t n_actors, uint32_t flags, int threads, int64_t* bad) {
+  std::atomic<int64_t> nbad{0};
+  auto t0 = std::chrono::steady_clock::now();
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    std::vector<uint8_t> rec(1 << 16);
+    for (size_t i = b; i < e; ++i) {
+      Orswot o;
+      if (!from_binary(blobs + off[i], len[i], wa, wm, o) ||
+          encode(o, n_actors, rec.data(), rec.size(), (flags & CRDT_ORSWOT_SPARSE_CLOCK) != 0) < 0)
+        nbad++;
+    }
+  });
+  auto t1 = std::chrono::steady_clock::now();
+  if (bad) *bad = nbad.load();
+  return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// CPU baseline of egest: decode records untimed, time to_binary of each.
+double orc_bincode_egest_bench(const uint8_t* rb, const uint64_t* roff, size_t rbytes, size_t n, int wa, int wm,
+                               int threads) {
+  std::vector<Orswot> objs(n);
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) decode(rb + roff[i], rbytes - roff[i], objs[i]);
+  });
+  std::atomic<size_t> total{0};
+  auto t0 = std::chrono::steady_clock::now();
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    std::vector<uint8_t> out;
+    size_t t = 0;
+    for (size_t i = b; i < e; ++i) {
+      out.clear();
+      to_binary(objs[i], wa, wm, out);
+      t += out.size();
+    }
+    total += t;
+  });
+  auto t1 = std::chrono::steady_clock::now();
   return std::chrono::duration<double>(t1 - t0).count();
 }
 

@@ -35,20 +35,43 @@ constexpr uint32_t kBcStage = 4096;     // LDS window per wave (blob for ingest,
 constexpr uint32_t kBcMaxMem = 256;     // members per object on the ingest path
 constexpr uint32_t kBcMaxDef = 64;      // deferred clocks per object on the ingest path
 
-// per-wave ingest scratch (bytes)
+// per-wave ingest scratch (bytes); the walk writes only the first kXWalk bytes
 constexpr uint32_t kXPm = 0;                          // u32 member entry position [kBcMaxMem]
 constexpr uint32_t kXLm = kXPm + 4 * kBcMaxMem;       // u32 member dot count
-constexpr uint32_t kXKm = kXLm + 4 * kBcMaxMem;       // u64 member key
-constexpr uint32_t kXRm = kXKm + 8 * kBcMaxMem;       // u32 member rank
-constexpr uint32_t kXSm = kXRm + 4 * kBcMaxMem;       // u32 dot counts / offsets in sorted order
-constexpr uint32_t kXPd = kXSm + 4 * kBcMaxMem;       // u32 deferred clock position (its length word)
+constexpr uint32_t kXPd = kXLm + 4 * kBcMaxMem;       // u32 deferred clock position (its length word)
 constexpr uint32_t kXLd = kXPd + 4 * kBcMaxDef;       // u32 deferred clock entries
 constexpr uint32_t kXPs = kXLd + 4 * kBcMaxDef;       // u32 deferred set position (its length word)
 constexpr uint32_t kXLs = kXPs + 4 * kBcMaxDef;       // u32 deferred set size
-constexpr uint32_t kXSd = kXLs + 4 * kBcMaxDef;       // u32 sorted deferred clock entries -> offsets
+constexpr uint32_t kXWalk = kXLs + 4 * kBcMaxDef;     // 3 072 B
+constexpr uint32_t kXRm = kXWalk;                     // u32 member rank
+constexpr uint32_t kXKc = kXRm;                       // u64 dense top clock scatter (before the ranking)
+constexpr uint32_t kXSm = kXRm + 4 * kBcMaxMem;       // u32 dot counts / offsets in sorted order
+constexpr uint32_t kXSd = kXSm + 4 * kBcMaxMem;       // u32 sorted deferred clock entries -> offsets
 constexpr uint32_t kXSs = kXSd + 4 * kBcMaxDef;       // u32 sorted deferred set sizes -> offsets
 constexpr uint32_t kXRd = kXSs + 4 * kBcMaxDef;       // u32 deferred rank
-constexpr uint32_t kXBytes = kXRd + 4 * kBcMaxDef;    // 7 680 B
+constexpr uint32_t kXBytes = kXRd + 4 * kBcMaxDef;    // 5 888 B
+static_assert(8 * kBcMaxMem <= kXSd - kXKc, "dense clock scatter fits the rank + offset arrays");
+
+// Diagnostic phase stamps (ST builds only, variant 301): s_memtime deltas.
+struct BcStamps {
+  uint64_t acc[8];
+  uint64_t last;
+};
+__device__ __forceinline__ uint64_t bc_now() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+template <bool ST>
+__device__ __forceinline__ void bc_mark(BcStamps* st, int k) {
+  if (ST) {
+    const uint64_t t = bc_now();
+    st->acc[k] += t - st->last;
+    st->last = t;
+  }
+}
 
 __device__ __forceinline__ void bc_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -62,6 +85,11 @@ __device__ __forceinline__ uint64_t bc_uni64(uint64_t v) {
          (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
 }
 
+__device__ __forceinline__ uint64_t bc_lane64(uint64_t v, uint32_t t) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), t) << 32) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, t);
+}
+
 __device__ __forceinline__ uint32_t bc_scan_incl(uint32_t v, uint32_t lane) {
 #pragma unroll
   for (uint32_t d = 1; d < kBcWave; d <<= 1) {
@@ -71,24 +99,56 @@ __device__ __forceinline__ uint32_t bc_scan_incl(uint32_t v, uint32_t lane) {
   return v;
 }
 
-// little-endian unsigned integer of w bytes at p[pos]
-__device__ __forceinline__ uint64_t rdw(const uint8_t* p, uint64_t pos, uint32_t w) {
-  uint64_t v = 0;
-  for (uint32_t i = 0; i < w; ++i) v |= (uint64_t)p[pos + i] << (8u * i);
-  return v;
-}
+// Blob bytes, read as little-endian unsigned integers of w bytes at a blob
+// position. LDS window (S = true): b is the window's 16-B aligned base and
+// the blob starts at b + d; a field is two aligned u64 reads and a funnel
+// shift (the window has >= 16 spare bytes past the blob). Global (S =
+// false, blobs too large for the window): byte loads.
+template <bool S>
+struct Src;
+template <>
+struct Src<true> {
+  static constexpr bool kWindow = true;
+  const uint8_t* b;
+  uint32_t d;
+  __device__ __forceinline__ uint64_t get(uint64_t pos, uint32_t w) const {
+    const uint32_t a = d + (uint32_t)pos;
+    const uint64_t* q = (const uint64_t*)(b + (a & ~7u));
+    const uint32_t sh = 8u * (a & 7u);
+    const uint64_t lo = q[0], hi = q[1];
+    const uint64_t v = sh ? (lo >> sh) | (hi << (64u - sh)) : lo;
+    return w >= 8u ? v : v & ((1ull << (8u * w)) - 1u);
+  }
+  // the low 32 bits of the field at pos: two aligned u32 reads + v_alignbit
+  __device__ __forceinline__ uint32_t lo32(uint32_t pos) const {
+    const uint32_t a = d + pos;
+    const uint32_t* q = (const uint32_t*)(b + (a & ~3u));
+    return __builtin_amdgcn_alignbit(q[1], q[0], (a & 3u) * 8u);
+  }
+};
+template <>
+struct Src<false> {
+  static constexpr bool kWindow = false;
+  const uint8_t* b;
+  __device__ __forceinline__ uint64_t get(uint64_t pos, uint32_t w) const {
+    uint64_t v = 0;
+    for (uint32_t i = 0; i < w; ++i) v |= (uint64_t)b[pos + i] << (8u * i);
+    return v;
+  }
+};
 __device__ __forceinline__ void wrw(uint8_t* p, uint64_t pos, uint64_t v, uint32_t w) {
   for (uint32_t i = 0; i < w; ++i) p[pos + i] = (uint8_t)(v >> (8u * i));
 }
 
 // lexicographic (actor, counter) order of two bincode clocks, a proper prefix
 // first (the record's CLOCK ORDER): -1, 0, 1
-__device__ int bc_clock_cmp(const uint8_t* B, uint64_t pa, uint32_t na, uint64_t pb, uint32_t nb, uint32_t wa) {
+template <class SRC>
+__device__ __forceinline__ int bc_clock_cmp(const SRC& B, uint64_t pa, uint32_t na, uint64_t pb, uint32_t nb, uint32_t wa) {
   const uint32_t n = na < nb ? na : nb, st = wa + 8u;
   for (uint32_t i = 0; i < n; ++i) {
-    const uint64_t xa = rdw(B, pa + (uint64_t)st * i, wa), xb = rdw(B, pb + (uint64_t)st * i, wa);
+    const uint64_t xa = B.get(pa + (uint64_t)st * i, wa), xb = B.get(pb + (uint64_t)st * i, wa);
     if (xa != xb) return xa < xb ? -1 : 1;
-    const uint64_t ca = rdw(B, pa + (uint64_t)st * i + wa, 8), cb = rdw(B, pb + (uint64_t)st * i + wa, 8);
+    const uint64_t ca = B.get(pa + (uint64_t)st * i + wa, 8), cb = B.get(pb + (uint64_t)st * i + wa, 8);
     if (ca != cb) return ca < cb ? -1 : 1;
   }
   return na == nb ? 0 : (na < nb ? -1 : 1);
@@ -100,43 +160,81 @@ struct BcWalk {
 };
 
 // Wave-uniform walk over one blob: bounds, counts, entry positions (into X).
-__device__ BcWalk bc_walk(const uint8_t* B, uint64_t len, uint32_t wa, uint32_t wm, uint32_t A, uint8_t* X,
+template <class SRC>
+__device__ __forceinline__ BcWalk bc_walk(const SRC& B, uint64_t len, uint32_t wa, uint32_t wm, uint32_t A, uint8_t* X,
                           uint32_t lane) {
   BcWalk w{0, 0, 0, 0, 0, 0, 0};
   const uint64_t sa = wa + 8u;
-  if (len < 24u) { w.err = CRDT_ENONCANON; return w; }
-  const uint64_t nclk = bc_uni64(rdw(B, 0, 8));
-  if (nclk > A || nclk > (len - 24u) / sa) { w.err = CRDT_ENONCANON; return w; }
+  if (len < 24u || len >= (1ull << 31)) { w.err = CRDT_ENONCANON; return w; }
+  const uint64_t nclk = bc_uni64(B.get(0, 8));
+  if (nclk > A || nclk * sa > len - 24u) { w.err = CRDT_ENONCANON; return w; }
   w.n_clk = (uint32_t)nclk;
   uint64_t p = 8u + nclk * sa;
-  const uint64_t nent = bc_uni64(rdw(B, p, 8));
+  const uint64_t nent = bc_uni64(B.get(p, 8));
   p += 8u;
   if (nent > kBcMaxMem) { w.err = CRDT_ECAPACITY; return w; }
   w.n_mem = (uint32_t)nent;
-  for (uint32_t e = 0; e < (uint32_t)nent; ++e) {
-    if (p + wm + 8u > len) { w.err = CRDT_ENONCANON; return w; }
-    const uint64_t l = bc_uni64(rdw(B, p + wm, 8));
-    if (l == 0u || l > A || l > (len - (p + wm + 8u)) / sa) { w.err = CRDT_ENONCANON; return w; }
-    if (lane == (e & (kBcWave - 1u))) {
-      ((uint32_t*)(X + kXPm))[e] = (uint32_t)p;
-      ((uint32_t*)(X + kXLm))[e] = (uint32_t)l;
+  if constexpr (SRC::kWindow) {
+    // the chain of entry positions is the only serial part: one LDS read and
+    // a multiply-add per entry (reads clamped into the window); every length
+    // is then validated lane-parallel
+    uint32_t q = (uint32_t)p;
+    const uint32_t L32 = (uint32_t)len, step = wm + 8u;
+    for (uint32_t e0 = 0; e0 < (uint32_t)nent; e0 += kBcWave) {
+      // lane j keeps entry e0 + j's position (a select per step, no stores in the chain)
+      uint32_t mine = 0;
+      const uint32_t ne = (uint32_t)nent - e0 < kBcWave ? (uint32_t)nent - e0 : kBcWave;
+      for (uint32_t j = 0; j < ne; ++j) {
+        mine = lane == j ? q : mine;
+        const uint32_t l = B.lo32(q + wm < L32 ? q + wm : L32);
+        q += step + (l < 0xFFFFu ? l : 0xFFFFu) * (uint32_t)sa;
+      }
+      if (lane < ne) ((uint32_t*)(X + kXPm))[e0 + lane] = mine;
     }
-    w.n_dot += (uint32_t)l;
-    p += wm + 8u + l * sa;
+    bc_sync();
+    for (uint32_t e = lane; e < (uint32_t)nent; e += kBcWave) {  // the full 64-bit lengths, in parallel
+      const uint32_t pe = ((const uint32_t*)(X + kXPm))[e];
+      const uint64_t l = B.get(pe + wm < L32 ? pe + wm : L32, 8);
+      ((uint32_t*)(X + kXLm))[e] = (l >> 32) ? 0xFFFFFFFFu : (uint32_t)l;
+    }
+    bc_sync();
+    bool bad = false;
+    uint32_t nd = 0;
+    for (uint32_t e = lane; e < (uint32_t)nent; e += kBcWave) {
+      const uint32_t pe = ((const uint32_t*)(X + kXPm))[e], l = ((const uint32_t*)(X + kXLm))[e];
+      bad = bad || l == 0u || l > A || (uint64_t)pe + wm + 8u + (uint64_t)l * sa > len;
+      nd += l;
+    }
+    if (__ballot(bad)) { w.err = CRDT_ENONCANON; return w; }
+    for (uint32_t dd = 32; dd >= 1; dd >>= 1) nd += __shfl_xor(nd, dd, kBcWave);
+    w.n_dot = bc_uni(nd);
+    p = q;
+  } else {
+    for (uint32_t e = 0; e < (uint32_t)nent; ++e) {
+      if (p + wm + 8u > len) { w.err = CRDT_ENONCANON; return w; }
+      const uint64_t l = bc_uni64(B.get(p + wm, 8));
+      if (l == 0u || l > A || l * sa > len - (p + wm + 8u)) { w.err = CRDT_ENONCANON; return w; }
+      if (lane == (e & (kBcWave - 1u))) {
+        ((uint32_t*)(X + kXPm))[e] = (uint32_t)p;
+        ((uint32_t*)(X + kXLm))[e] = (uint32_t)l;
+      }
+      w.n_dot += (uint32_t)l;
+      p += wm + 8u + l * sa;
+    }
   }
   if (p + 8u > len) { w.err = CRDT_ENONCANON; return w; }
-  const uint64_t ndef = bc_uni64(rdw(B, p, 8));
+  const uint64_t ndef = bc_uni64(B.get(p, 8));
   p += 8u;
   if (ndef > kBcMaxDef) { w.err = CRDT_ECAPACITY; return w; }
   w.n_def = (uint32_t)ndef;
   for (uint32_t d = 0; d < (uint32_t)ndef; ++d) {
     if (p + 8u > len) { w.err = CRDT_ENONCANON; return w; }
-    const uint64_t lc = bc_uni64(rdw(B, p, 8));
-    if (lc == 0u || lc > A || lc > (len - (p + 8u)) / sa) { w.err = CRDT_ENONCANON; return w; }
+    const uint64_t lc = bc_uni64(B.get(p, 8));
+    if (lc == 0u || lc > A || lc * sa > len - (p + 8u)) { w.err = CRDT_ENONCANON; return w; }
     const uint64_t q = p + 8u + lc * sa;
     if (q + 8u > len) { w.err = CRDT_ENONCANON; return w; }
-    const uint64_t ls = bc_uni64(rdw(B, q, 8));
-    if (ls == 0u || ls > (len - (q + 8u)) / wm) { w.err = CRDT_ENONCANON; return w; }
+    const uint64_t ls = bc_uni64(B.get(q, 8));
+    if (ls == 0u || ls > len || ls * wm > len - (q + 8u)) { w.err = CRDT_ENONCANON; return w; }
     if (lane == (d & (kBcWave - 1u))) {
       ((uint32_t*)(X + kXPd))[d] = (uint32_t)p;
       ((uint32_t*)(X + kXLd))[d] = (uint32_t)lc;
@@ -174,67 +272,98 @@ __device__ void bc_scan_excl(uint32_t* S, uint32_t n, uint32_t lane) {
 
 // Decode one blob (already walked) into its canonical record at O. Returns 0
 // or a CRDT_E* code (the record is then not valid).
-__device__ int bc_write_record(const uint8_t* B, const BcWalk& w, uint32_t wa, uint32_t wm, uint32_t A, bool sparse,
-                               uint8_t* X, uint8_t* O, uint32_t lane) {
+template <bool ST = false, class SRC>
+__device__ __forceinline__ int bc_write_record(const SRC& B, const BcWalk& w, uint32_t wa, uint32_t wm, uint32_t A, bool sparse,
+                               uint8_t* X, uint8_t* O, uint32_t lane, BcStamps* st = nullptr) {
   RecLayout L;
   rec_layout(L, sparse ? w.n_clk : A, w.n_mem, w.n_dot, w.n_def, w.n_def_dot, w.n_def_mem, sparse);
   const uint64_t sa = wa + 8u;
   bool bad = false;
-  // ---- top clock: BTreeMap order = strictly increasing actors
-  if (!sparse)
+  // ---- top clock: BTreeMap order = strictly increasing actors. Dense: the
+  // counters are scattered into LDS (the member-key area, free until the
+  // ranking) and the A slots written once, coalesced
+  const bool lds_clk = !sparse && A <= kBcMaxMem;
+  uint64_t* Kc = (uint64_t*)(X + kXKc);
+  if (lds_clk) {
+    for (uint32_t a = lane; a < A; a += kBcWave) Kc[a] = 0ull;
+    bc_sync();
+  } else if (!sparse) {
     for (uint32_t a = lane; a < A; a += kBcWave) ((uint64_t*)(O + L.o_clk))[a] = 0ull;
-  __threadfence_block();
+    __threadfence_block();
+  }
   for (uint32_t k = lane; k < w.n_clk; k += kBcWave) {
     const uint64_t e = 8u + k * sa;
-    const uint64_t x = rdw(B, e, wa), c = rdw(B, e + wa, 8);
-    bad = bad || x >= A || c == 0u || (k && rdw(B, e - sa, wa) >= x);
+    const uint64_t x = B.get(e, wa), c = B.get(e + wa, 8);
+    bad = bad || x >= A || c == 0u || (k && B.get(e - sa, wa) >= x);
     if (x < A) {
       if (sparse) {
         ((uint64_t*)(O + L.o_clk))[k] = c;
         ((uint32_t*)(O + L.o_cact))[k] = (uint32_t)x;
+      } else if (lds_clk) {
+        Kc[x] = c;
       } else {
         ((uint64_t*)(O + L.o_clk))[x] = c;
       }
     }
   }
+  if (lds_clk) {
+    bc_sync();
+    for (uint32_t a = lane; a < A; a += kBcWave) ((uint64_t*)(O + L.o_clk))[a] = Kc[a];
+    bc_sync();
+  }
   if (sparse && lane == 0u && (w.n_clk & 1u)) *(uint32_t*)(O + L.o_cact + 4u * w.n_clk) = 0u;
+  bc_mark<ST>(st, 2);
   // ---- members: rank by key (HashMap order is arbitrary), dot offsets in key order
   uint32_t* Pm = (uint32_t*)(X + kXPm);
   uint32_t* Lm = (uint32_t*)(X + kXLm);
-  uint64_t* Km = (uint64_t*)(X + kXKm);
   uint32_t* Rm = (uint32_t*)(X + kXRm);
   uint32_t* Sm = (uint32_t*)(X + kXSm);
   bc_sync();
-  for (uint32_t e = lane; e < w.n_mem; e += kBcWave) Km[e] = rdw(B, Pm[e], wm);
-  bc_sync();
-  for (uint32_t e = lane; e < w.n_mem; e += kBcWave) {
-    const uint64_t k = Km[e];
+  if (w.n_mem <= kBcWave) {  // every key in one register: broadcast by readlane
+    const uint64_t k = lane < w.n_mem ? B.get(Pm[lane], wm) : 0ull;
     uint32_t r = 0, eq = 0;
     for (uint32_t f = 0; f < w.n_mem; ++f) {
-      const uint64_t kf = Km[f];
+      const uint64_t kf = bc_lane64(k, f);
       r += kf < k ? 1u : 0u;
       eq += kf == k ? 1u : 0u;
     }
-    bad = bad || eq != 1u;
-    Rm[e] = r;
-    Sm[r < kBcMaxMem ? r : 0u] = Lm[e];
+    if (lane < w.n_mem) {
+      bad = bad || eq != 1u;
+      Rm[lane] = r;
+      Sm[r < kBcMaxMem ? r : 0u] = Lm[lane];
+    }
+  } else {
+    for (uint32_t e = lane; e < w.n_mem; e += kBcWave) {
+      const uint64_t k = B.get(Pm[e], wm);
+      uint32_t r = 0, eq = 0;
+      for (uint32_t f = 0; f < w.n_mem; ++f) {
+        const uint64_t kf = B.get(Pm[f], wm);
+        r += kf < k ? 1u : 0u;
+        eq += kf == k ? 1u : 0u;
+      }
+      bad = bad || eq != 1u;
+      Rm[e] = r;
+      Sm[r < kBcMaxMem ? r : 0u] = Lm[e];
+    }
   }
   bc_sync();
   bc_scan_excl(Sm, w.n_mem, lane);
+  bc_mark<ST>(st, 3);
   for (uint32_t e = lane; e < w.n_mem; e += kBcWave) {
     const uint32_t r = Rm[e], d0 = Sm[r], l = Lm[e];
-    ((uint64_t*)(O + L.o_key))[r] = Km[e];
+    ((uint64_t*)(O + L.o_key))[r] = B.get(Pm[e], wm);
     ((uint32_t*)(O + L.o_mdend))[r] = d0 + l;
     const uint64_t p = Pm[e] + wm + 8u;
     uint64_t prev = 0;
     for (uint32_t i = 0; i < l; ++i) {
-      const uint64_t x = rdw(B, p + i * sa, wa), c = rdw(B, p + i * sa + wa, 8);
+      const uint64_t x = B.get(p + i * sa, wa), c = B.get(p + i * sa + wa, 8);
       bad = bad || x >= A || c == 0u || (i && prev >= x);
       prev = x;
       ((uint32_t*)(O + L.o_dact))[d0 + i] = (uint32_t)x;
       ((uint64_t*)(O + L.o_dctr))[d0 + i] = c;
     }
   }
+  bc_mark<ST>(st, 4);
   // ---- deferred: clocks sorted in CLOCK ORDER, member sets sorted
   uint32_t* Pd = (uint32_t*)(X + kXPd);
   uint32_t* Ld = (uint32_t*)(X + kXLd);
@@ -266,7 +395,7 @@ __device__ int bc_write_record(const uint8_t* B, const BcWalk& w, uint32_t wa, u
       const uint64_t p = Pd[d] + 8u;
       uint64_t prev = 0;
       for (uint32_t i = 0; i < lc; ++i) {
-        const uint64_t x = rdw(B, p + i * sa, wa), c = rdw(B, p + i * sa + wa, 8);
+        const uint64_t x = B.get(p + i * sa, wa), c = B.get(p + i * sa + wa, 8);
         bad = bad || x >= A || c == 0u || (i && prev >= x);
         prev = x;
         ((uint32_t*)(O + L.o_fact))[a0 + i] = (uint32_t)x;
@@ -274,10 +403,10 @@ __device__ int bc_write_record(const uint8_t* B, const BcWalk& w, uint32_t wa, u
       }
       const uint64_t q = Ps[d] + 8u;
       for (uint32_t i = 0; i < ls; ++i) {  // the set's elements by rank (HashSet order is arbitrary)
-        const uint64_t m = rdw(B, q + (uint64_t)i * wm, wm);
+        const uint64_t m = B.get(q + (uint64_t)i * wm, wm);
         uint32_t rk = 0, eq = 0;
         for (uint32_t j = 0; j < ls; ++j) {
-          const uint64_t mj = rdw(B, q + (uint64_t)j * wm, wm);
+          const uint64_t mj = B.get(q + (uint64_t)j * wm, wm);
           rk += mj < m ? 1u : 0u;
           eq += mj == m ? 1u : 0u;
         }
@@ -294,73 +423,127 @@ __device__ int bc_write_record(const uint8_t* B, const BcWalk& w, uint32_t wa, u
     h[0] = L.size; h[1] = L.n_clk; h[2] = L.n_mem; h[3] = L.n_dot;
     h[4] = L.n_def; h[5] = L.n_def_dot; h[6] = L.n_def_mem; h[7] = sparse ? kSparseClock : 0u;
   }
-  return __ballot(bad) ? CRDT_ENONCANON : 0;
+  const int rc = __ballot(bad) ? CRDT_ENONCANON : 0;
+  bc_mark<ST>(st, 5);
+  return rc;
 }
 
-// Stage blob bytes [off, off + len) of a buffer of `bytes` bytes into the
-// wave's window; returns the pointer to the blob's first byte in LDS.
-__device__ const uint8_t* bc_stage(const uint8_t* base, uint64_t bytes, uint64_t off, uint64_t len, v4u* S,
-                                   uint32_t lane) {
-  const uint64_t a0 = off & ~15ull, a1 = (off + len + 15u) & ~15ull;
-  const uint32_t n16 = (uint32_t)((a1 - a0) / 16u);
+template <bool WRITE, bool ST = false, class SRC>
+__device__ __forceinline__ int bc_object(const SRC& B, uint64_t o, uint64_t len, uint32_t wa, uint32_t wm, uint32_t A,
+                                         bool sparse, uint8_t* X, uint64_t* sizes, uint8_t* out, const uint64_t* ooff,
+                                         uint64_t out_bytes, uint32_t lane, BcStamps* st = nullptr) {
+  const BcWalk w = bc_walk(B, len, wa, wm, A, X, lane);
+  bc_mark<ST>(st, 1);
+  if (w.err) return w.err;
+  const uint64_t size = record_size64(sparse ? w.n_clk : A, w.n_mem, w.n_dot, w.n_def, w.n_def_dot, w.n_def_mem,
+                                      sparse);
+  if (!WRITE) {
+    if (lane == 0u) sizes[o] = size;
+    return 0;
+  }
+  const uint64_t oo = ooff[o];
+  if ((oo & 15u) || oo > out_bytes || size > out_bytes - oo) return CRDT_ECAPACITY;
   bc_sync();
-  for (uint32_t k = lane; k < n16; k += kBcWave) {
-    const uint64_t g = a0 + 16ull * k;
-    if (g + 16u <= bytes) {
-      S[k] = __builtin_nontemporal_load((const v4u*)(base + g));
-    } else {  // the buffer's last partial line
-      uint8_t* s = (uint8_t*)(S + k);
-      for (uint32_t i = 0; i < 16u; ++i) s[i] = g + i < bytes ? base[g + i] : (uint8_t)0;
+  return bc_write_record<ST>(B, w, wa, wm, A, sparse, X, out + oo, lane, st);
+}
+
+constexpr uint32_t kBcPer = kBcStage / 16u / kBcWave;  // window lines per lane
+
+// The aligned 16-B lines covering one blob, into registers (lines past the
+// buffer's end, and the buffer's last partial line, byte by byte).
+__device__ __forceinline__ void bc_prefetch(v4u (&r)[kBcPer], const uint8_t* base, uint64_t bytes, uint64_t a0,
+                                            uint32_t n16, uint32_t lane) {
+#pragma unroll
+  for (uint32_t k = 0; k < kBcPer; ++k) {
+    const uint32_t idx = lane + k * kBcWave;
+    const uint64_t g = a0 + 16ull * idx;
+    if (idx < n16) {
+      if (g + 16u <= bytes) {
+        r[k] = __builtin_nontemporal_load((const v4u*)(base + g));
+      } else {
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        for (uint32_t i = 0; i < 16u; ++i)
+          if (g + i < bytes) w[i / 4u] |= (uint32_t)base[g + i] << (8u * (i & 3u));
+        r[k] = v4u{w[0], w[1], w[2], w[3]};
+      }
     }
   }
-  bc_sync();
-  return (const uint8_t*)S + (off - a0);
 }
 
-template <bool WRITE>
-__global__ __launch_bounds__(kBcWave * kBcWaves) void bincode_ingest_kernel(
+// One wave per 64-object chunk: lane k holds object cbase + k's blob extent;
+// the objects are then walked (and, WRITE, decoded) one by one from the LDS
+// window while the next windowed blob is in flight in registers.
+template <bool WRITE, bool ST = false>
+__global__ __launch_bounds__(kBcWave * kBcWaves, WRITE ? 4 : 5) void bincode_ingest_kernel(
     const uint8_t* __restrict__ blobs, uint64_t blob_bytes, const uint64_t* __restrict__ boff,
     const uint64_t* __restrict__ blen, uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags,
     uint64_t* __restrict__ sizes, uint8_t* __restrict__ out, const uint64_t* __restrict__ ooff, uint64_t out_bytes,
     int* __restrict__ status) {
   __shared__ v4u st_s[kBcWaves][kBcStage / 16];
-  __shared__ v4u sx_s[kBcWaves][kXBytes / 16];
+  __shared__ v4u sx_s[kBcWaves][(WRITE ? kXBytes : kXWalk) / 16];
   const uint32_t lane = threadIdx.x & (kBcWave - 1u), wave = threadIdx.x / kBcWave;
   uint8_t* X = (uint8_t*)sx_s[wave];
   const bool sparse = (flags & kSparseClock) != 0u;
-  for (uint64_t o = (uint64_t)blockIdx.x * kBcWaves + wave; o < n_obj; o += (uint64_t)gridDim.x * kBcWaves) {
-    const uint64_t off = boff[o], len = blen[o];
-    if (off > blob_bytes || len > blob_bytes - off) {
-      if (lane == 0u) {
-        atomicCAS(status, 0, CRDT_ENONCANON);
+  const uint64_t n_waves = (uint64_t)gridDim.x * kBcWaves;
+  const uint64_t wave_id = (uint64_t)blockIdx.x * kBcWaves + wave;
+  BcStamps stv{};
+  BcStamps* st = ST ? &stv : nullptr;
+  if (ST) stv.last = bc_now();
+  for (uint64_t cbase = wave_id * kBcWave; cbase < n_obj; cbase += n_waves * kBcWave) {
+    const uint64_t obj = cbase + lane;
+    const bool valid = obj < n_obj;
+    uint64_t off = 0, len = 0;
+    if (valid) { off = boff[obj]; len = blen[obj]; }
+    const bool inb = valid && off <= blob_bytes && len <= blob_bytes - off;
+    if (valid && !inb) {
+      atomicCAS(status, 0, CRDT_ENONCANON);
+      if (!WRITE) sizes[obj] = 0u;
+    }
+    const bool win = inb && len + 32u <= kBcStage;
+    const uint64_t a0 = off & ~15ull;
+    const uint32_t n16 = win ? (uint32_t)((((off + len + 15u) & ~15ull) - a0) / 16u) : 0u;
+    const uint64_t wins = __ballot(win);
+    uint64_t pend = __ballot(inb);
+    v4u pf[kBcPer];
+    uint64_t nxt = wins;
+    if (nxt) {
+      const uint32_t t = (uint32_t)__builtin_ctzll(nxt);
+      bc_prefetch(pf, blobs, blob_bytes, bc_lane64(a0, t), __builtin_amdgcn_readlane(n16, t), lane);
+    }
+    while (pend) {
+      const uint32_t t = (uint32_t)__builtin_ctzll(pend);
+      pend &= pend - 1;
+      const uint64_t o = cbase + t, ot = bc_lane64(off, t), lt = bc_lane64(len, t);
+      int rc;
+      if ((wins >> t) & 1ull) {
+        bc_sync();  // the previous object's window readers are done
+#pragma unroll
+        for (uint32_t k = 0; k < kBcPer; ++k) st_s[wave][lane + k * kBcWave] = pf[k];
+        bc_sync();
+        nxt &= nxt - 1;  // t was the lowest pending windowed object
+        if (nxt) {
+          const uint32_t u = (uint32_t)__builtin_ctzll(nxt);
+          bc_prefetch(pf, blobs, blob_bytes, bc_lane64(a0, u), __builtin_amdgcn_readlane(n16, u), lane);
+        }
+        const Src<true> B{(const uint8_t*)st_s[wave], (uint32_t)(ot & 15u)};
+        bc_mark<ST>(st, 0);
+        rc = bc_object<WRITE, ST>(B, o, lt, wa, wm, A, sparse, X, sizes, out, ooff, out_bytes, lane, st);
+      } else {
+        const Src<false> B{blobs + ot};
+        rc = bc_object<WRITE>(B, o, lt, wa, wm, A, sparse, X, sizes, out, ooff, out_bytes, lane);
+      }
+      if (rc && lane == 0u) {
+        atomicCAS(status, 0, rc);
         if (!WRITE) sizes[o] = 0u;
       }
-      continue;
+      bc_mark<ST>(st, 6);
     }
-    const uint8_t* B = len + 32u <= kBcStage ? bc_stage(blobs, blob_bytes, off, len, st_s[wave], lane) : blobs + off;
-    bc_sync();
-    const BcWalk w = bc_walk(B, len, wa, wm, A, X, lane);
-    if (w.err) {
-      if (lane == 0u) {
-        atomicCAS(status, 0, w.err);
-        if (!WRITE) sizes[o] = 0u;
-      }
-      continue;
-    }
-    const uint64_t size = record_size64(sparse ? w.n_clk : A, w.n_mem, w.n_dot, w.n_def, w.n_def_dot, w.n_def_mem,
-                                        sparse);
-    if (!WRITE) {
-      if (lane == 0u) sizes[o] = size;
-      continue;
-    }
-    const uint64_t oo = ooff[o];
-    if ((oo & 15u) || oo > out_bytes || size > out_bytes - oo) {
-      if (lane == 0u) atomicCAS(status, 0, CRDT_ECAPACITY);
-      continue;
-    }
-    bc_sync();
-    const int rc = bc_write_record(B, w, wa, wm, A, sparse, X, out + oo, lane);
-    if (rc && lane == 0u) atomicCAS(status, 0, rc);
+  }
+  if (ST && lane < 8u) {  // per-wave phase sums -> the debug buffer (sizes slot of the stamp build)
+    uint64_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v = lane == (uint32_t)q ? stv.acc[q] : v;
+    sizes[wave_id * 8u + lane] = v;
   }
 }
 
@@ -512,9 +695,15 @@ uint32_t bc_blocks(uint64_t n_obj) {
 
 int launch_bincode_ingest(const uint8_t* blobs, uint64_t blob_bytes, const uint64_t* boff, const uint64_t* blen,
                           uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags, uint64_t* sizes,
-                          uint8_t* out, const uint64_t* ooff, uint64_t out_bytes, int* status, hipStream_t stream) {
+                          uint8_t* out, const uint64_t* ooff, uint64_t out_bytes, int* status, hipStream_t stream,
+                          uint64_t* dbg) {
   if (n_obj == 0) return CRDT_OK;
   const uint32_t blocks = bc_blocks(n_obj);
+  if (dbg && !sizes) {  // diagnostic: decode pass with phase stamps into dbg (8 u64 per wave)
+    hipLaunchKernelGGL((bincode_ingest_kernel<true, true>), dim3(blocks), dim3(kBcWave * kBcWaves), 0, stream, blobs,
+                       blob_bytes, boff, blen, n_obj, wa, wm, A, flags, dbg, out, ooff, out_bytes, status);
+    return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+  }
   if (sizes)
     hipLaunchKernelGGL(bincode_ingest_kernel<false>, dim3(blocks), dim3(kBcWave * kBcWaves), 0, stream, blobs,
                        blob_bytes, boff, blen, n_obj, wa, wm, A, flags, sizes, out, ooff, out_bytes, status);

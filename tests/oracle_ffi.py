@@ -32,6 +32,13 @@ def lib():
     P, U8P, U64P, U32P = C.c_void_p, C.POINTER(C.c_uint8), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)
     L.orc_record_bytes.restype = C.c_size_t
     L.orc_record_bytes.argtypes = [C.c_uint32] * 6
+    L.orc_bincode_to_record.restype = C.c_long
+    L.orc_bincode_to_record.argtypes = [P, C.c_size_t, C.c_int, C.c_int, C.c_uint32, C.c_uint32, P, C.c_size_t]
+    L.orc_bincode_ingest_bench.restype = C.c_double
+    L.orc_bincode_ingest_bench.argtypes = [P, P, P, C.c_size_t, C.c_int, C.c_int, C.c_uint32, C.c_uint32, C.c_int,
+                                           C.POINTER(C.c_int64)]
+    L.orc_bincode_egest_bench.restype = C.c_double
+    L.orc_bincode_egest_bench.argtypes = [P, P, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int]
     L.orc_orswot_merge_batch.restype = C.c_int
     L.orc_orswot_merge_batch.argtypes = [P, P, C.c_size_t, P, P, C.c_size_t, C.c_size_t, C.c_uint32,
                                          P, P, C.c_size_t, C.c_int, C.POINTER(C.c_int64)]
@@ -187,6 +194,32 @@ def orswot_merge_batch(lbase, loff, rbase, roff, n_actors, threads=8, flags=0):
     if rc != 0:
         raise ValueError(f"oracle merge failed rc={rc} at object {bad.value}")
     return obase, ooff
+
+
+def bincode_to_record(blob, wa, wm, n_actors, flags=0):
+    """Blob -> canonical record through the C++ restatement (oracle/ref_cpu.cpp)."""
+    b = np.frombuffer(bytes(blob) or b"\0", dtype=np.uint8)
+    out = np.zeros(1 << 16, dtype=np.uint8)
+    n = lib().orc_bincode_to_record(_ptr(b), len(blob), wa, wm, n_actors, flags, _ptr(out), out.nbytes)
+    if n < 0:
+        raise ValueError(f"oracle bincode decode failed rc={n}")
+    return out[:n].tobytes()
+
+
+def bincode_ingest_bench(blobs, off, lens, wa, wm, n_actors, flags, threads):
+    bad = C.c_int64(0)
+    b = np.ascontiguousarray(blobs, dtype=np.uint8)
+    o = np.ascontiguousarray(off, dtype=np.uint64)
+    n_ = np.ascontiguousarray(lens, dtype=np.uint64)
+    secs = lib().orc_bincode_ingest_bench(_ptr(b), _ptr(o), _ptr(n_), len(o), wa, wm, n_actors, flags, threads,
+                                          C.byref(bad))
+    if bad.value:
+        raise ValueError(f"oracle bincode ingest: {bad.value} blobs failed")
+    return secs
+
+
+def bincode_egest_bench(rbase, roff, wa, wm, threads):
+    return lib().orc_bincode_egest_bench(_ptr(rbase), _ptr(roff), rbase.nbytes, len(roff), wa, wm, threads)
 
 
 def orswot_bench(lbase, loff, rbase, roff, threads):

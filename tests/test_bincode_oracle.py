@@ -106,3 +106,19 @@ def test_record_form_agrees():
                              {tuple(c): set(ms) for c, ms in back["deferred"]}, 16)
         assert records.decode(rec)["entries"] == st["entries"]
         assert records.decode(rec)["deferred"] == st["deferred"]
+
+
+def test_cpp_restatement_agrees(oracle):
+    """The C++ restatement (the CPU baseline's) and the Python one decode every
+    blob to the same canonical record, for dense and sparse states."""
+    rng = random.Random(11)
+    for st in _states(300, seed=21):
+        blob = BC.encode(dict(clock=st["clock"], entries=st["entries"], deferred=st["deferred"]), 1, 8, rng=rng)
+        assert oracle.bincode_to_record(blob, 1, 8, 16) == records.encode(
+            st["clock"], {m: dict(d) for m, d in st["entries"].items()},
+            {tuple(c): set(ms) for c, ms in st["deferred"]}, 16)
+    for st in _states(100, sparse=True):
+        blob = BC.encode(dict(clock=st["clock"], entries=st["entries"], deferred=st["deferred"]), 2, 8, rng=rng)
+        assert oracle.bincode_to_record(blob, 2, 8, 1024, 1) == records.encode(
+            st["clock"], {m: dict(d) for m, d in st["entries"].items()},
+            {tuple(c): set(ms) for c, ms in st["deferred"]}, 1024, True)
