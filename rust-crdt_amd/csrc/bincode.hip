@@ -548,21 +548,52 @@ __global__ __launch_bounds__(kBcWave * kBcWaves, WRITE ? 4 : 5) void bincode_ing
 }
 
 // ---------------------------------------------------------------- egest
-__device__ __forceinline__ uint64_t bc_blob_len(const uint32_t* h, const uint8_t* r, uint32_t wa, uint32_t wm,
-                                                uint32_t nnz) {
-  (void)r;
+// Blob writers. LDS window (zeroed first): a field is OR-ed in as the aligned
+// u32 pieces it covers (ds_or_b32; neighbouring fields of other lanes may
+// share a dword). Global (blobs too large for the window): byte stores.
+template <bool S>
+struct Dst;
+template <>
+struct Dst<true> {
+  uint8_t* t;
+  __device__ __forceinline__ void put(uint64_t pos, uint64_t v, uint32_t w) const {
+    const uint32_t a = (uint32_t)pos, sh = 8u * (a & 3u);
+    uint32_t* q = (uint32_t*)(t + (a & ~3u));
+    if (w == 8u) {
+      const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+      atomicOr(q, lo << sh);
+      atomicOr(q + 1, sh ? (hi << sh) | (lo >> (32u - sh)) : hi);
+      if (sh) atomicOr(q + 2, hi >> (32u - sh));
+    } else {
+      const uint32_t m = w == 4u ? (uint32_t)v : (uint32_t)v & ((1u << (8u * w)) - 1u);
+      atomicOr(q, m << sh);
+      if (sh + 8u * w > 32u) atomicOr(q + 1, m >> (32u - sh));
+    }
+  }
+};
+template <>
+struct Dst<false> {
+  uint8_t* t;
+  __device__ __forceinline__ void put(uint64_t pos, uint64_t v, uint32_t w) const {
+    for (uint32_t i = 0; i < w; ++i) t[pos + i] = (uint8_t)(v >> (8u * i));
+  }
+};
+
+__device__ __forceinline__ uint64_t bc_blob_len(const uint32_t* h, uint32_t wa, uint32_t wm, uint32_t nnz) {
   const uint64_t sa = wa + 8u;
   return 8u + nnz * sa + 8u + (uint64_t)h[2] * (wm + 8u) + (uint64_t)h[3] * sa + 8u + 16ull * h[4] +
          (uint64_t)h[5] * sa + (uint64_t)h[6] * wm;
 }
 
 // nonzero top-clock entries of a record (dense: count of nonzero slots)
-__device__ uint32_t bc_nnz(const uint8_t* r, const uint32_t* h, uint32_t lane) {
-  if (h[7] & kSparseClock) return h[1];
+__device__ __forceinline__ uint32_t bc_nnz(const uint8_t* r, uint32_t lane) {
+  const uint32_t* h = (const uint32_t*)r;
+  if (h[7] & kSparseClock) return bc_uni(h[1]);
+  const uint32_t n_clk = bc_uni(h[1]);
   uint32_t n = 0;
-  for (uint32_t a = lane; a < h[1]; a += kBcWave) n += ((const uint64_t*)(r + kHdrBytes))[a] != 0u ? 1u : 0u;
+  for (uint32_t a = lane; a < n_clk; a += kBcWave) n += ((const uint64_t*)(r + kHdrBytes))[a] != 0u ? 1u : 0u;
   for (uint32_t d = 32; d >= 1; d >>= 1) n += __shfl_xor(n, d, kBcWave);
-  return n;
+  return bc_uni(n);
 }
 
 __device__ bool bc_record_ok(const uint8_t* base, uint64_t bytes, uint64_t off, uint32_t A, uint32_t flags) {
@@ -574,113 +605,175 @@ __device__ bool bc_record_ok(const uint8_t* base, uint64_t bytes, uint64_t off, 
   return sz == h[0] && off + sz <= bytes;
 }
 
+// to_binary of one record r (header already validated) into T; returns
+// true when a value is wider than its field.
+template <class DST>
+__device__ __forceinline__ bool bc_emit(const uint8_t* r, const DST& T, uint32_t nnz, uint32_t wa, uint32_t wm,
+                                        uint64_t amax, uint64_t mmax, uint32_t lane) {
+  const uint32_t* h = (const uint32_t*)r;
+  const uint32_t n_clk = bc_uni(h[1]), n_mem = bc_uni(h[2]), n_dot = bc_uni(h[3]), n_def = bc_uni(h[4]);
+  const bool sparse = (bc_uni(h[7]) & kSparseClock) != 0u;
+  RecLayout L;
+  rec_layout(L, n_clk, n_mem, n_dot, n_def, bc_uni(h[5]), bc_uni(h[6]), sparse);
+  const uint64_t sa = wa + 8u;
+  bool bad = false;
+  // top clock: BTreeMap<A, u64> = length, then (actor, counter) ascending
+  if (lane == 0u) T.put(0, nnz, 8);
+  if (sparse) {
+    for (uint32_t k = lane; k < n_clk; k += kBcWave) {
+      const uint32_t x = ((const uint32_t*)(r + L.o_cact))[k];
+      bad = bad || x > amax;
+      T.put(8u + k * sa, x, wa);
+      T.put(8u + k * sa + wa, ((const uint64_t*)(r + L.o_clk))[k], 8);
+    }
+  } else {
+    uint32_t run = 0;
+    for (uint32_t a0 = 0; a0 < n_clk; a0 += kBcWave) {
+      const uint32_t a = a0 + lane;
+      const uint64_t c = a < n_clk ? ((const uint64_t*)(r + L.o_clk))[a] : 0ull;
+      const uint64_t nz = __ballot(c != 0u);
+      const uint32_t k = run + __builtin_amdgcn_mbcnt_hi((uint32_t)(nz >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nz, 0u));
+      if (c != 0u) {
+        bad = bad || a > amax;
+        T.put(8u + k * sa, a, wa);
+        T.put(8u + k * sa + wa, c, 8);
+      }
+      run += (uint32_t)__popcll(nz);
+    }
+  }
+  // entries: HashMap<M, VClock<A>> = length, then (member, clock) in key order
+  const uint64_t E = 8u + nnz * sa;
+  if (lane == 0u) T.put(E, n_mem, 8);
+  for (uint32_t m = lane; m < n_mem; m += kBcWave) {
+    const uint32_t b0 = m ? ((const uint32_t*)(r + L.o_mdend))[m - 1] : 0u, e = ((const uint32_t*)(r + L.o_mdend))[m];
+    const uint64_t p = E + 8u + (uint64_t)m * (wm + 8u) + (uint64_t)b0 * sa;
+    const uint64_t key = ((const uint64_t*)(r + L.o_key))[m];
+    bad = bad || key > mmax;
+    T.put(p, key, wm);
+    T.put(p + wm, e - b0, 8);
+    for (uint32_t i = b0; i < e; ++i) {
+      const uint32_t x = ((const uint32_t*)(r + L.o_dact))[i];
+      bad = bad || x > amax;
+      T.put(p + wm + 8u + (i - b0) * sa, x, wa);
+      T.put(p + wm + 8u + (i - b0) * sa + wa, ((const uint64_t*)(r + L.o_dctr))[i], 8);
+    }
+  }
+  // deferred: HashMap<VClock<A>, HashSet<M>> = length, then (clock, set) in clock order
+  const uint64_t F = E + 8u + (uint64_t)n_mem * (wm + 8u) + (uint64_t)n_dot * sa;
+  if (lane == 0u) T.put(F, n_def, 8);
+  for (uint32_t d = lane; d < n_def; d += kBcWave) {
+    const uint32_t b0 = d ? ((const uint32_t*)(r + L.o_fdend))[d - 1] : 0u, e = ((const uint32_t*)(r + L.o_fdend))[d];
+    const uint32_t ms = d ? ((const uint32_t*)(r + L.o_fmend))[d - 1] : 0u, me = ((const uint32_t*)(r + L.o_fmend))[d];
+    const uint64_t p = F + 8u + 16ull * d + (uint64_t)b0 * sa + (uint64_t)ms * wm;
+    T.put(p, e - b0, 8);
+    for (uint32_t i = b0; i < e; ++i) {
+      const uint32_t x = ((const uint32_t*)(r + L.o_fact))[i];
+      bad = bad || x > amax;
+      T.put(p + 8u + (i - b0) * sa, x, wa);
+      T.put(p + 8u + (i - b0) * sa + wa, ((const uint64_t*)(r + L.o_fctr))[i], 8);
+    }
+    const uint64_t q = p + 8u + (uint64_t)(e - b0) * sa;
+    T.put(q, me - ms, 8);
+    for (uint32_t j = ms; j < me; ++j) {
+      const uint64_t key = ((const uint64_t*)(r + L.o_fkey))[j];
+      bad = bad || key > mmax;
+      T.put(q + 8u + (uint64_t)(j - ms) * wm, key, wm);
+    }
+  }
+  return __ballot(bad) != 0ull;
+}
+
+// One wave per 64-record chunk. Sizes pass: blob length from the header and
+// the dense clock. Write pass: each record is prefetched into registers,
+// staged in an LDS window, its blob assembled in a second (zeroed) window
+// and copied out with 16-B stores; records or blobs larger than a window go
+// straight from / to HBM.
 template <bool WRITE>
-__global__ __launch_bounds__(kBcWave * kBcWaves) void bincode_egest_kernel(
+__global__ __launch_bounds__(kBcWave * kBcWaves, WRITE ? 4 : 8) void bincode_egest_kernel(
     const uint8_t* __restrict__ rb, uint64_t rbytes, const uint64_t* __restrict__ roff, uint64_t n_obj, uint32_t A,
     uint32_t flags, uint32_t wa, uint32_t wm, uint64_t* __restrict__ sizes, uint8_t* __restrict__ out,
     const uint64_t* __restrict__ ooff, uint64_t out_bytes, int* __restrict__ status) {
-  __shared__ v4u st_s[kBcWaves][kBcStage / 16];
+  __shared__ v4u rs_s[kBcWaves][WRITE ? kBcStage / 16 : 1];
+  __shared__ v4u ts_s[kBcWaves][WRITE ? kBcStage / 16 : 1];
   const uint32_t lane = threadIdx.x & (kBcWave - 1u), wave = threadIdx.x / kBcWave;
   const uint64_t amax = wa >= 8u ? ~0ull : (1ull << (8u * wa)) - 1u, mmax = wm >= 8u ? ~0ull : (1ull << (8u * wm)) - 1u;
-  for (uint64_t o = (uint64_t)blockIdx.x * kBcWaves + wave; o < n_obj; o += (uint64_t)gridDim.x * kBcWaves) {
-    const uint64_t ro = roff[o];
-    if (!bc_record_ok(rb, rbytes, ro, A, flags)) {
-      if (lane == 0u) {
-        atomicCAS(status, 0, CRDT_ENONCANON);
-        if (!WRITE) sizes[o] = 0u;
-      }
-      continue;
+  const uint64_t n_waves = (uint64_t)gridDim.x * kBcWaves;
+  const uint64_t wave_id = (uint64_t)blockIdx.x * kBcWaves + wave;
+  for (uint64_t cbase = wave_id * kBcWave; cbase < n_obj; cbase += n_waves * kBcWave) {
+    const uint64_t obj = cbase + lane;
+    const bool valid = obj < n_obj;
+    const uint64_t ro = valid ? roff[obj] : 0ull;
+    const bool ok = valid && bc_record_ok(rb, rbytes, ro, A, flags);
+    if (valid && !ok) {
+      atomicCAS(status, 0, CRDT_ENONCANON);
+      if (!WRITE) sizes[obj] = 0u;
     }
-    const uint8_t* r = rb + ro;
-    const uint32_t* h = (const uint32_t*)r;
-    const bool sparse = (flags & kSparseClock) != 0u;
-    RecLayout L;
-    rec_layout(L, h[1], h[2], h[3], h[4], h[5], h[6], sparse);
-    const uint32_t nnz = bc_uni(bc_nnz(r, h, lane));
-    const uint64_t len = bc_blob_len(h, r, wa, wm, nnz);
+    const uint32_t rsz = ok ? ((const uint32_t*)(rb + ro))[0] : 0u;
+    uint64_t pend = __ballot(ok);
     if (!WRITE) {
-      if (lane == 0u) sizes[o] = len;
+      while (pend) {
+        const uint32_t t = (uint32_t)__builtin_ctzll(pend);
+        pend &= pend - 1;
+        const uint8_t* r = rb + bc_lane64(ro, t);
+        const uint32_t nnz = bc_nnz(r, lane);
+        if (lane == 0u) sizes[cbase + t] = bc_blob_len((const uint32_t*)r, wa, wm, nnz);
+      }
       continue;
     }
-    const uint64_t oo = ooff[o];
-    const uint64_t padded = (len + 15u) & ~15ull;
-    if ((oo & 15u) || oo > out_bytes || padded > out_bytes - oo) {
-      if (lane == 0u) atomicCAS(status, 0, CRDT_ECAPACITY);
-      continue;
+    const bool win = ok && rsz <= kBcStage;
+    const uint64_t wins = __ballot(win);
+    v4u pf[kBcPer];
+    uint64_t nxt = wins;
+    if (nxt) {
+      const uint32_t t = (uint32_t)__builtin_ctzll(nxt);
+      bc_prefetch(pf, rb, rbytes, bc_lane64(ro, t), __builtin_amdgcn_readlane(rsz, t) / 16u, lane);
     }
-    const bool staged = padded <= kBcStage;
-    uint8_t* T = staged ? (uint8_t*)st_s[wave] : out + oo;
-    const uint64_t sa = wa + 8u;
     bool bad = (uint64_t)(A - 1u) > amax;
-    bc_sync();
-    if (staged) {
-      for (uint32_t k = lane; k < (uint32_t)(padded / 16u); k += kBcWave) st_s[wave][k] = v4u{0u, 0u, 0u, 0u};
-    } else {
-      for (uint64_t k = len + lane; k < padded; k += kBcWave) T[k] = 0u;
-    }
-    bc_sync();
-    // top clock: BTreeMap<A, u64> = length, then (actor, counter) ascending
-    if (lane == 0u) wrw(T, 0, nnz, 8);
-    if (sparse) {
-      for (uint32_t k = lane; k < h[1]; k += kBcWave) {
-        wrw(T, 8u + k * sa, ((const uint32_t*)(r + L.o_cact))[k], wa);
-        wrw(T, 8u + k * sa + wa, ((const uint64_t*)(r + L.o_clk))[k], 8);
-      }
-    } else {
-      uint32_t run = 0;
-      for (uint32_t a0 = 0; a0 < h[1]; a0 += kBcWave) {
-        const uint32_t a = a0 + lane;
-        const uint64_t c = a < h[1] ? ((const uint64_t*)(r + L.o_clk))[a] : 0ull;
-        const uint64_t nz = __ballot(c != 0u);
-        const uint32_t k = run + __builtin_amdgcn_mbcnt_hi((uint32_t)(nz >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nz, 0u));
-        if (c != 0u) {
-          wrw(T, 8u + k * sa, a, wa);
-          wrw(T, 8u + k * sa + wa, c, 8);
+    while (pend) {
+      const uint32_t t = (uint32_t)__builtin_ctzll(pend);
+      pend &= pend - 1;
+      const uint64_t o = cbase + t, oo = ooff[o];
+      if ((wins >> t) & 1ull) {
+        bc_sync();  // the previous object's window readers are done
+#pragma unroll
+        for (uint32_t k = 0; k < kBcPer; ++k) rs_s[wave][lane + k * kBcWave] = pf[k];
+        bc_sync();
+        nxt &= nxt - 1;
+        if (nxt) {
+          const uint32_t u = (uint32_t)__builtin_ctzll(nxt);
+          bc_prefetch(pf, rb, rbytes, bc_lane64(ro, u), __builtin_amdgcn_readlane(rsz, u) / 16u, lane);
         }
-        run += (uint32_t)__popcll(nz);
+        const uint8_t* r = (const uint8_t*)rs_s[wave];
+        const uint32_t nnz = bc_nnz(r, lane);
+        const uint64_t len = bc_blob_len((const uint32_t*)r, wa, wm, nnz), padded = (len + 15u) & ~15ull;
+        if ((oo & 15u) || oo > out_bytes || padded > out_bytes - oo) {
+          if (lane == 0u) atomicCAS(status, 0, CRDT_ECAPACITY);
+          continue;
+        }
+        if (padded <= kBcStage) {
+          for (uint32_t k = lane; k < (uint32_t)(padded / 16u); k += kBcWave) ts_s[wave][k] = v4u{0u, 0u, 0u, 0u};
+          bc_sync();
+          bad = bc_emit(r, Dst<true>{(uint8_t*)ts_s[wave]}, nnz, wa, wm, amax, mmax, lane) || bad;
+          bc_sync();
+          for (uint32_t k = lane; k < (uint32_t)(padded / 16u); k += kBcWave)
+            __builtin_nontemporal_store(ts_s[wave][k], (v4u*)(out + oo) + k);
+        } else {
+          for (uint64_t k = len + lane; k < padded; k += kBcWave) out[oo + k] = 0u;
+          bad = bc_emit(r, Dst<false>{out + oo}, nnz, wa, wm, amax, mmax, lane) || bad;
+        }
+      } else {
+        const uint8_t* r = rb + bc_lane64(ro, t);
+        const uint32_t nnz = bc_nnz(r, lane);
+        const uint64_t len = bc_blob_len((const uint32_t*)r, wa, wm, nnz), padded = (len + 15u) & ~15ull;
+        if ((oo & 15u) || oo > out_bytes || padded > out_bytes - oo) {
+          if (lane == 0u) atomicCAS(status, 0, CRDT_ECAPACITY);
+          continue;
+        }
+        for (uint64_t k = len + lane; k < padded; k += kBcWave) out[oo + k] = 0u;
+        bad = bc_emit(r, Dst<false>{out + oo}, nnz, wa, wm, amax, mmax, lane) || bad;
       }
     }
-    // entries: HashMap<M, VClock<A>> = length, then (member, clock) — key order
-    const uint64_t E = 8u + nnz * sa;
-    if (lane == 0u) wrw(T, E, h[2], 8);
-    for (uint32_t m = lane; m < h[2]; m += kBcWave) {
-      const uint32_t s = m ? ((const uint32_t*)(r + L.o_mdend))[m - 1] : 0u, e = ((const uint32_t*)(r + L.o_mdend))[m];
-      const uint64_t p = E + 8u + (uint64_t)m * (wm + 8u) + (uint64_t)s * sa;
-      const uint64_t key = ((const uint64_t*)(r + L.o_key))[m];
-      bad = bad || key > mmax;
-      wrw(T, p, key, wm);
-      wrw(T, p + wm, e - s, 8);
-      for (uint32_t i = s; i < e; ++i) {
-        wrw(T, p + wm + 8u + (i - s) * sa, ((const uint32_t*)(r + L.o_dact))[i], wa);
-        wrw(T, p + wm + 8u + (i - s) * sa + wa, ((const uint64_t*)(r + L.o_dctr))[i], 8);
-      }
-    }
-    // deferred: HashMap<VClock<A>, HashSet<M>> = length, then (clock, set) — clock order
-    const uint64_t F = E + 8u + (uint64_t)h[2] * (wm + 8u) + (uint64_t)h[3] * sa;
-    if (lane == 0u) wrw(T, F, h[4], 8);
-    for (uint32_t d = lane; d < h[4]; d += kBcWave) {
-      const uint32_t s = d ? ((const uint32_t*)(r + L.o_fdend))[d - 1] : 0u, e = ((const uint32_t*)(r + L.o_fdend))[d];
-      const uint32_t ms = d ? ((const uint32_t*)(r + L.o_fmend))[d - 1] : 0u, me = ((const uint32_t*)(r + L.o_fmend))[d];
-      const uint64_t p = F + 8u + 16ull * d + (uint64_t)s * sa + (uint64_t)ms * wm;
-      wrw(T, p, e - s, 8);
-      for (uint32_t i = s; i < e; ++i) {
-        wrw(T, p + 8u + (i - s) * sa, ((const uint32_t*)(r + L.o_fact))[i], wa);
-        wrw(T, p + 8u + (i - s) * sa + wa, ((const uint64_t*)(r + L.o_fctr))[i], 8);
-      }
-      const uint64_t q = p + 8u + (uint64_t)(e - s) * sa;
-      wrw(T, q, me - ms, 8);
-      for (uint32_t j = ms; j < me; ++j) {
-        const uint64_t key = ((const uint64_t*)(r + L.o_fkey))[j];
-        bad = bad || key > mmax;
-        wrw(T, q + 8u + (uint64_t)(j - ms) * wm, key, wm);
-      }
-    }
-    if (staged) {
-      bc_sync();
-      for (uint32_t k = lane; k < (uint32_t)(padded / 16u); k += kBcWave)
-        __builtin_nontemporal_store(st_s[wave][k], (v4u*)(out + oo) + k);
-    }
-    if (__ballot(bad) && lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);  // a value wider than its field
+    if (bad && lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);  // a value wider than its field
   }
 }
 
