@@ -35,7 +35,7 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="orswot",
-                   choices=["orswot", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode"])
+                   choices=["orswot", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply"])
     p.add_argument("--replicas", type=int, default=8, help="orswot_csr at N=1: replicas folded locally")
     p.add_argument("--n-obj", type=int, default=None, help="objects per GPU")
     p.add_argument("--threads", type=int, default=16, help="host threads (generation, CPU baseline)")
@@ -536,6 +536,148 @@ def run_bincode(args, rank, world, local):
     return res
 
 
+def _apply_ops(lb, lo, n):
+    """8 ops per config-3 object (numpy, deterministic): fresh adds to new and
+    existing members, a future-context remove that a later add releases
+    (apply_deferred), read-context removes that drop an entry / a dot."""
+    import numpy as np
+
+    C = np.uint64(1 << 33)
+    i = np.arange(n, dtype=np.uint64)
+    a = (i % np.uint64(16)).astype(np.uint32)
+    b = ((i + np.uint64(5)) % np.uint64(16)).astype(np.uint32)
+    hdr = lb[(lo[:, None].astype(np.int64) + np.arange(32)[None, :])].view(np.uint32).reshape(n, 8)
+    nm = hdr[:, 2].astype(np.int64)
+    key0 = lo.astype(np.int64) + 160
+    k0 = np.where(nm > 0, lb[key0[:, None] + np.arange(8)[None, :]].view(np.uint64).ravel(), np.uint64(11))
+    kmid = lo.astype(np.int64) + 160 + 8 * (nm // 2)
+    k1 = np.where(nm > 0, lb[kmid[:, None] + np.arange(8)[None, :]].view(np.uint64).ravel(), np.uint64(13))
+    new1 = (i * np.uint64(0x9E3779B97F4A7C15)) | np.uint64(1 << 63)
+    new2 = new1 ^ np.uint64(0x5555)
+    z = np.zeros(n, np.uint64)
+    # op table: (kind, member, actor, counter, rm-clock actor, rm-clock counter)
+    table = [(0, new1, a, C + np.uint64(1)), (0, k0, b, C + np.uint64(2)), (1, k1, a, C + np.uint64(5)),
+             (0, k1, a, C + np.uint64(3)), (0, new2, a, C + np.uint64(5)), (1, new1, a, C + np.uint64(1)),
+             (0, k0, b, C + np.uint64(6)), (1, k0, b, C + np.uint64(6))]
+    K = len(table)
+    kind = np.empty((n, K), np.uint32)
+    mem = np.empty((n, K), np.uint64)
+    act = np.zeros((n, K), np.uint32)
+    ctr = np.zeros((n, K), np.uint64)
+    npair = np.zeros((n, K), np.uint64)
+    cact, cctr = [], []
+    for j, (k, m, x, c) in enumerate(table):
+        kind[:, j] = k
+        mem[:, j] = m
+        if k == 0:
+            act[:, j] = x
+            ctr[:, j] = c
+        else:
+            npair[:, j] = 1
+            cact.append(x)
+            cctr.append(c)
+    rm_cols = [j for j, t in enumerate(table) if t[0] == 1]
+    ca = np.zeros((n, K), np.uint32)
+    cc = np.zeros((n, K), np.uint64)
+    for col, x, c in zip(rm_cols, cact, cctr):
+        ca[:, col] = x
+        cc[:, col] = c
+    sel = npair.ravel() > 0
+    clk_act = ca.ravel()[sel]
+    clk_ctr = cc.ravel()[sel]
+    clk_end = np.cumsum(npair.ravel()).astype(np.uint64)
+    obj_end = (np.arange(1, n + 1, dtype=np.uint64) * np.uint64(K))
+    del z
+    return obj_end, kind.ravel(), mem.ravel(), act.ravel(), ctr.ravel(), clk_end, clk_act, clk_ctr
+
+
+def run_apply(args, rank, world, local):
+    """SURVEY.md §8(f) rank 2: the batched op path (CmRDT::apply for Orswot,
+    src/orswot.rs:61-85) over the config-3 shard, 8 ops per object (adds,
+    deferred and read-context removes, deferred releases). A step = one
+    crdt_orswot_apply launch over all objects, inputs resident in HBM."""
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    import crdts_hip
+    from crdts_hip._lib import Ops, check, lib
+
+    n = args.n_obj or 1_000_000
+    A = 16
+    (lb, lo), _ = crdts_hip.generate_orswot(n, first_obj=rank * n, threads=args.threads)
+    ops_np = _apply_ops(lb, lo, n)
+    eng = crdts_hip.Engine(local)
+    dev = f"cuda:{local}"
+    B = crdts_hip.OrswotBatch.from_host(lb, lo, A, device=local)
+
+    def t64(x):
+        return torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).to(dev)
+
+    def t32(x):
+        return torch.from_numpy(np.ascontiguousarray(x).view(np.int32)).to(dev)
+
+    o_end, kind, mem, act, ctr, cend, cact, cctr = ops_np
+    ops = crdts_hip.OrswotOps(t64(o_end), t32(kind), t64(mem), t32(act), t64(ctr), t64(cend), t32(cact), t64(cctr))
+    first = eng.orswot_apply(B, ops)  # checked launch; reused buffers below
+    out, ooff = first.base, first.off
+    n_ops, n_clk = ops.n_ops, ops.n_clk
+    # spot parity against the oracle's op path on a sample
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_ffi
+
+    import records as R
+
+    got = first.records()[:300]
+    for i in range(300):
+        o = oracle_ffi.OracleOrswot.decode(bytes(lb[lo[i]:lo[i] + int(np.frombuffer(lb[lo[i]:lo[i] + 4], np.uint32)[0])]))
+        for q in range(int(o_end[i - 1]) if i else 0, int(o_end[i])):
+            if kind[q] == 0:
+                o.apply_add(int(act[q]), int(ctr[q]), int(mem[q]))
+            else:
+                b0 = int(cend[q - 1]) if q else 0
+                o.apply_rm(int(mem[q]), [(int(cact[k]), int(cctr[k])) for k in range(b0, int(cend[q]))])
+        assert o.encode(A) == got[i], f"apply parity, object {i}: {R.decode(got[i])}"
+    stream = torch.cuda.Stream(device=local)
+    st = C.c_void_p(stream.cuda_stream)
+    bt = B.cbatch()
+    co = ops.cops()
+
+    def step():
+        check(lib.crdt_orswot_apply(eng.ctx, C.byref(bt), C.byref(co), A, 0, C.c_void_p(out.data_ptr()),
+                                    C.c_void_p(ooff.data_ptr()), int(out.numel()), st))
+
+    wall, ev_ms = _timed_steps(args, world, stream, step)
+    eng.status(stream)
+    out_sizes = out.view(torch.int32)[(ooff // 4)].cpu().numpy().astype(np.int64)
+    alg = int(lb.nbytes) + int(out_sizes.sum()) + n_ops * (4 + 8 + 4 + 8 + 8) + n_clk * 12 + 8 * 3 * n
+    total = sum_over_ranks(float(n_ops * args.steps), world)
+    res = {
+        "metric": "batched Orswot op apply (CmRDT::apply) ops/sec (node)", "value": total / wall, "unit": "ops/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic: config-3 op-simulated Orswots + 8 generated ops each (adds, deferred / read-ctx removes)",
+        "config": {"workload": f"apply config3: {n} objects x {n_ops // n} ops per GPU",
+                   "parallelism": f"dp{world} (objects sharded)"},
+    }
+    if world == 1:
+        ach = alg / (ev_ms * 1e-3) / 1e9
+        res["roofline"] = {"bound": "hbm", "kernel": "orswot_apply_kernel", "achieved": ach, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "kernel_ms": ev_ms,
+                           "alg_bytes_per_launch": alg, "traffic": None}
+        if not args.no_cpu_baseline:
+            m = min(args.cpu_sample // 5, n)
+            th = max(1, min(args.threads, os.cpu_count() or 1))
+            sub = (o_end[:m], kind[:8 * m], mem[:8 * m], act[:8 * m], ctr[:8 * m], cend[:8 * m],
+                   cact[:int(cend[8 * m - 1])], cctr[:int(cend[8 * m - 1])])
+            secs = oracle_ffi.orswot_apply_bench(lb, lo[:m].astype(np.uint64), sub, th)
+            res["cpu_baseline"] = {"value": 8 * m / secs, "unit": "ops/s", "cores": th, "kind": "port",
+                                   "sample": f"{m} objects x 8 ops, oracle op path (std::map/unordered_map), "
+                                             f"{th} threads"}
+    return res
+
+
 def main():
     args = parse()
     rank, world, local = dist_setup()
@@ -549,6 +691,8 @@ def main():
         res = run_gcounter_ae(args, rank, world, local)
     elif args.workload == "bincode":
         res = run_bincode(args, rank, world, local)
+    elif args.workload == "apply":
+        res = run_apply(args, rank, world, local)
     else:
         res = run_dense(args, rank, world, local, args.workload)
     if rank == 0:

@@ -273,6 +273,38 @@ int crdt_orswot_generate_replicas(uint64_t seed, size_t first_obj, size_t n_obj,
                                   uint32_t flags, int n_threads, crdt_orswot_gen** out);
 
 /* ------------------------------------------------------------------------ *
+ * Batched op path: CmRDT::apply for Orswot (src/orswot.rs:61-85; Op enum
+ * :38-53): out[i] = self[i] after applying object i's ops in order.
+ *   Op::Add { dot: (actor, counter), member }   kind CRDT_OP_ADD
+ *   Op::Rm  { clock, member }                   kind CRDT_OP_RM; clock i is
+ *     pairs [clk_end[i-1], clk_end[i]) of clk_act / clk_ctr (canonical:
+ *     actors strictly increasing, counters > 0; Add ops own no pairs)
+ * Object i's ops are [obj_end[i-1], obj_end[i]). Record i of the output is
+ * written at d_out_off[i] = self.off[i] + 32*(ops before i) + 16*(clock pairs
+ * before i) + 32*i (set by the call), so out_bytes >= self.bytes + 32*n_ops +
+ * 16*n_clk + 32*n_obj suffices when self's records do not overlap and are in
+ * increasing offset order. Limits of this round (CRDT_ECAPACITY): <= 128
+ * top-clock entries, members, dots per member clock and Rm clock pairs; <= 512
+ * dots; <= 32 deferred clocks with <= 256 entries and <= 256 members.      */
+#define CRDT_OP_ADD 0u
+#define CRDT_OP_RM 1u
+typedef struct crdt_orswot_ops {
+  const uint64_t* obj_end;   /* device, n_obj  */
+  const uint32_t* kind;      /* device, n_ops  */
+  const uint64_t* member;    /* device, n_ops  */
+  const uint32_t* actor;     /* device, n_ops (Add) */
+  const uint64_t* counter;   /* device, n_ops (Add) */
+  const uint64_t* clk_end;   /* device, n_ops  */
+  const uint32_t* clk_act;   /* device, n_clk  */
+  const uint64_t* clk_ctr;   /* device, n_clk  */
+  size_t n_ops;
+  size_t n_clk;
+} crdt_orswot_ops;
+int crdt_orswot_apply(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_orswot_ops* ops,
+                      uint32_t n_actors, uint32_t flags, uint8_t* d_out, uint64_t* d_out_off,
+                      size_t out_bytes, void* stream);
+
+/* ------------------------------------------------------------------------ *
  * Ingest / egest: the reference's binary form <-> canonical records
  * (SURVEY.md §8(f) rank 1). The reference form of an Orswot<M, A> is
  * `to_binary(&s)` = bincode 0.9 of its serde derives (src/lib.rs:62-83;

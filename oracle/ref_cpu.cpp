@@ -616,6 +616,38 @@ double orc_bincode_egest_bench(const uint8_t* rb, const uint64_t* roff, size_t r
   return std::chrono::duration<double>(t1 - t0).count();
 }
 
+// CPU baseline of the batched op path: decode untimed, then time applying
+// every object's ops in order (CmRDT::apply, src/orswot.rs:61-85) over
+// `threads` std::threads. Returns seconds.
+double orc_orswot_apply_bench(const uint8_t* rb, const uint64_t* roff, size_t rbytes, size_t n,
+                              const uint64_t* obj_end, const uint32_t* kind, const uint64_t* member,
+                              const uint32_t* actor, const uint64_t* counter, const uint64_t* clk_end,
+                              const uint32_t* clk_act, const uint64_t* clk_ctr, int threads) {
+  std::vector<Orswot> objs(n);
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) decode(rb + roff[i], rbytes - roff[i], objs[i]);
+  });
+  auto t0 = std::chrono::steady_clock::now();
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) {
+      for (uint64_t q = i ? obj_end[i - 1] : 0; q < obj_end[i]; ++q) {
+        if (kind[q] == 0) {
+          objs[i].apply_add(actor[q], counter[q], member[q]);
+        } else {
+          VClock c;
+          for (uint64_t k = q ? clk_end[q - 1] : 0; k < clk_end[q]; ++k) c.dots.emplace(clk_act[k], clk_ctr[k]);
+          objs[i].apply_rm(member[q], c);
+        }
+      }
+    }
+  });
+  auto t1 = std::chrono::steady_clock::now();
+  volatile size_t sink = 0;
+  for (size_t i = 0; i < n; i += 997) sink += objs[i].entries.size();
+  (void)sink;
+  return std::chrono::duration<double>(t1 - t0).count();
+}
+
 // Dense VClock/GCounter rows, through the BTreeMap-style VClock::merge.
 int orc_dense_merge(uint64_t* self, const uint64_t* other, size_t n, uint32_t n_actors,
                     int threads) {

@@ -105,6 +105,49 @@ class OrswotBatch:
         return out
 
 
+class OrswotOps:
+    """A batch of Orswot ops (Op::Add / Op::Rm, src/orswot.rs:38-53) on the
+    device, grouped per object in order (crdt_orswot_ops)."""
+
+    ADD, RM = 0, 1
+
+    def __init__(self, obj_end, kind, member, actor, counter, clk_end, clk_act, clk_ctr):
+        self.t = (obj_end, kind, member, actor, counter, clk_end, clk_act, clk_ctr)
+        self.n_ops = int(kind.numel())
+        self.n_clk = int(clk_act.numel())
+
+    def cops(self):
+        from ._lib import Ops
+
+        p = [C.c_void_p(t.data_ptr()) if t.numel() else None for t in self.t]
+        return Ops(*p, self.n_ops, self.n_clk)
+
+    @classmethod
+    def from_lists(cls, per_obj, device=0):
+        """per_obj[i] = [("add", actor, counter, member) | ("rm", member, [(actor, counter), ...]), ...]"""
+        torch = _torch()
+        ends, kind, mem, act, ctr, cend, cact, cctr = [], [], [], [], [], [], [], []
+        for ops in per_obj:
+            for op in ops:
+                if op[0] == "add":
+                    kind.append(cls.ADD); act.append(op[1]); ctr.append(op[2]); mem.append(op[3])
+                else:
+                    kind.append(cls.RM); act.append(0); ctr.append(0); mem.append(op[1])
+                    for a, c in op[2]:
+                        cact.append(a); cctr.append(c)
+                cend.append(len(cact))
+            ends.append(len(kind))
+        dev = f"cuda:{device}"
+
+        def u64(x):
+            return torch.from_numpy(np.asarray(x, dtype=np.uint64).view(np.int64)).to(dev)
+
+        def u32(x):
+            return torch.from_numpy(np.asarray(x, dtype=np.uint32).view(np.int32)).to(dev)
+
+        return cls(u64(ends), u32(kind), u64(mem), u32(act), u64(ctr), u64(cend), u32(cact), u64(cctr))
+
+
 class Engine:
     """One crdt_ctx bound to a device. All merges run on the GPU."""
 
@@ -192,6 +235,24 @@ class Engine:
         return OrswotBatch(dst, doff, B.n_actors, max(16, (used + 15) // 16 * 16), B.flags)
 
     # ---------------------------------------------------------------- dense
+    # ------------------------------------------------ batched op path
+    def orswot_apply(self, B: "OrswotBatch", ops: "OrswotOps", stream=None, check_status=True):
+        """out[i] = B[i] after CmRDT::apply of object i's ops in order
+        (src/orswot.rs:61-85). Returns an OrswotBatch."""
+        torch = _torch()
+        dev = f"cuda:{self.device}"
+        cap = B.bytes + 32 * ops.n_ops + 16 * ops.n_clk + 32 * B.n_obj
+        base = torch.empty(max(16, cap), dtype=torch.uint8, device=dev)
+        off = torch.empty(B.n_obj, dtype=torch.int64, device=dev)
+        b = B.cbatch()
+        o = ops.cops()
+        check(lib.crdt_orswot_apply(self.ctx, C.byref(b), C.byref(o), B.n_actors, B.flags,
+                                    C.c_void_p(base.data_ptr()), C.c_void_p(off.data_ptr()), int(base.numel()),
+                                    self._stream(stream)), "orswot_apply")
+        if check_status:
+            self.status(stream)
+        return OrswotBatch(base, off, B.n_actors, int(base.numel()), B.flags)
+
     # ------------------------------------------------ bincode ingest / egest
     def orswot_from_bincode(self, blobs, blob_off, blob_len, n_actors, actor_bytes, member_bytes, flags=0,
                             stream=None, check_status=True):

@@ -59,8 +59,15 @@ EXPORTS = [
     "crdt_host_orswot_decode", "crdt_orswot_record_bytes_ex", "crdt_orswot_merge_ex",
     "crdt_orswot_validate_ex", "crdt_orswot_generate_replicas", "crdt_host_orswot_encode_ex",
     "crdt_orswot_bincode_record_sizes", "crdt_orswot_from_bincode", "crdt_orswot_bincode_sizes",
-    "crdt_orswot_to_bincode",
+    "crdt_orswot_to_bincode", "crdt_orswot_apply",
 ]
+
+
+class Ops(C.Structure):
+    """crdt_orswot_ops (include/crdts_hip.h)."""
+    _fields_ = [("obj_end", C.c_void_p), ("kind", C.c_void_p), ("member", C.c_void_p), ("actor", C.c_void_p),
+                ("counter", C.c_void_p), ("clk_end", C.c_void_p), ("clk_act", C.c_void_p),
+                ("clk_ctr", C.c_void_p), ("n_ops", C.c_size_t), ("n_clk", C.c_size_t)]
 
 
 def _load():
@@ -118,6 +125,7 @@ def _load():
         "crdt_orswot_from_bincode": (I, [P, P, SZ, P, P, SZ, U32, U32, U32, U32, P, P, SZ, P]),
         "crdt_orswot_bincode_sizes": (I, [P, BP, U32, U32, U32, U32, P, P]),
         "crdt_orswot_to_bincode": (I, [P, BP, U32, U32, U32, U32, P, P, SZ, P]),
+        "crdt_orswot_apply": (I, [P, BP, C.POINTER(Ops), U32, U32, P, P, SZ, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -355,4 +355,19 @@ int crdt_orswot_to_bincode(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32
                               member_bytes, nullptr, d_out, d_out_off, out_bytes, ctx->d_status, S(stream));
 }
 
+int crdt_orswot_apply(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_orswot_ops* ops, uint32_t n_actors,
+                      uint32_t flags, uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes, void* stream) {
+  if (!ctx || !self || !ops || n_actors == 0 || (flags & ~CRDT_ORSWOT_SPARSE_CLOCK)) return CRDT_EINVAL;
+  if (self->n_obj && (!self->base || !self->off || !ops->obj_end || !d_out || !d_out_off || !aligned16(d_out)))
+    return CRDT_EINVAL;
+  if (ops->n_ops && (!ops->kind || !ops->member || !ops->actor || !ops->counter || !ops->clk_end))
+    return CRDT_EINVAL;
+  if (ops->n_clk && (!ops->clk_act || !ops->clk_ctr)) return CRDT_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return launch_orswot_apply(self->base, self->bytes, self->off, self->n_obj, ops->obj_end, ops->kind, ops->member,
+                             ops->actor, ops->counter, ops->clk_end, ops->clk_act, ops->clk_ctr, n_actors, flags,
+                             d_out, d_out_off, out_bytes, ctx->d_status, S(stream));
+}
+
 }  // extern "C"

@@ -34,4 +34,10 @@ int launch_bincode_egest(const uint8_t* rb, uint64_t rbytes, const uint64_t* rof
                          uint32_t flags, uint32_t wa, uint32_t wm, uint64_t* sizes, uint8_t* out,
                          const uint64_t* ooff, uint64_t out_bytes, int* status, hipStream_t stream);
 
+int launch_orswot_apply(const uint8_t* sb, uint64_t sbytes, const uint64_t* soff, uint64_t n_obj,
+                        const uint64_t* obj_end, const uint32_t* kind, const uint64_t* member, const uint32_t* actor,
+                        const uint64_t* counter, const uint64_t* clk_end, const uint32_t* clk_act,
+                        const uint64_t* clk_ctr, uint32_t A, uint32_t flags, uint8_t* out, uint64_t* ooff,
+                        uint64_t out_bytes, int* status, hipStream_t stream);
+
 }  // namespace crdts_hip

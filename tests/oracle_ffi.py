@@ -37,6 +37,8 @@ def lib():
     L.orc_bincode_ingest_bench.restype = C.c_double
     L.orc_bincode_ingest_bench.argtypes = [P, P, P, C.c_size_t, C.c_int, C.c_int, C.c_uint32, C.c_uint32, C.c_int,
                                            C.POINTER(C.c_int64)]
+    L.orc_orswot_apply_bench.restype = C.c_double
+    L.orc_orswot_apply_bench.argtypes = [P, P, C.c_size_t, C.c_size_t] + [P] * 8 + [C.c_int]
     L.orc_bincode_egest_bench.restype = C.c_double
     L.orc_bincode_egest_bench.argtypes = [P, P, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int]
     L.orc_orswot_merge_batch.restype = C.c_int
@@ -220,6 +222,13 @@ def bincode_ingest_bench(blobs, off, lens, wa, wm, n_actors, flags, threads):
 
 def bincode_egest_bench(rbase, roff, wa, wm, threads):
     return lib().orc_bincode_egest_bench(_ptr(rbase), _ptr(roff), rbase.nbytes, len(roff), wa, wm, threads)
+
+
+def orswot_apply_bench(rbase, roff, ops_np, threads):
+    """ops_np: (obj_end, kind, member, actor, counter, clk_end, clk_act, clk_ctr) numpy arrays."""
+    arrs = [np.ascontiguousarray(a) for a in ops_np]
+    return lib().orc_orswot_apply_bench(_ptr(rbase), _ptr(roff), rbase.nbytes, len(roff), *[_ptr(a) for a in arrs],
+                                        threads)
 
 
 def orswot_bench(lbase, loff, rbase, roff, threads):
