@@ -35,7 +35,7 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="orswot",
-                   choices=["orswot", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply"])
+                   choices=["orswot", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply", "mvreg"])
     p.add_argument("--replicas", type=int, default=8, help="orswot_csr at N=1: replicas folded locally")
     p.add_argument("--n-obj", type=int, default=None, help="objects per GPU")
     p.add_argument("--threads", type=int, default=16, help="host threads (generation, CPU baseline)")
@@ -678,6 +678,90 @@ def run_apply(args, rank, world, local):
     return res
 
 
+def run_mvreg(args, rank, world, local):
+    """SURVEY.md §8(f) rank 4: batched MVReg<u64, A>::merge (src/mvreg.rs:121-153)
+    over 4M registers per GPU (A = 16 dense actors, 4 (clock, value) slots per
+    side, 8 out), and VClock partial_cmp (src/vclock.rs:59-71) over 100M row
+    pairs reported beside it. Inputs resident in HBM."""
+    import time as _t
+
+    import numpy as np
+    import torch
+
+    import crdts_hip
+
+    n = args.n_obj or 4_000_000
+    A, cap = 16, 4
+    dev = f"cuda:{local}"
+    g = torch.Generator(device=dev)
+    g.manual_seed(0xC0FFEE06 + rank)
+
+    def slab():
+        cnt = torch.randint(0, cap + 1, (n,), dtype=torch.int32, device=dev, generator=g)
+        clk = torch.randint(0, 3, (n, cap, A), dtype=torch.int64, device=dev, generator=g)
+        clk *= (torch.arange(cap, device=dev)[None, :, None] < cnt[:, None, None])
+        val = torch.randint(0, 1 << 62, (n, cap), dtype=torch.int64, device=dev, generator=g)
+        return cnt, clk, val
+
+    S, O = slab(), slab()
+    eng = crdts_hip.Engine(local)
+    stream = torch.cuda.Stream(device=local)
+    out = eng.mvreg_merge(S, O, A, stream=stream)
+    torch.cuda.synchronize()
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_ffi
+
+    m = 2000  # spot parity
+    hs = [t[:m].cpu().numpy() for t in S]
+    ho = [t[:m].cpu().numpy() for t in O]
+    en, ec, ev = oracle_ffi.mvreg_merge(hs[0].view(np.uint32), hs[1].view(np.uint64), hs[2].view(np.uint64),
+                                        ho[0].view(np.uint32), ho[1].view(np.uint64), ho[2].view(np.uint64), A, 2 * cap)
+    assert (out[0][:m].cpu().numpy().view(np.uint32) == en).all()
+    assert (out[1][:m].cpu().numpy().view(np.uint64) == ec).all()
+
+    def step():
+        eng.mvreg_merge(S, O, A, stream=stream, check_status=False)
+
+    wall, ev_ms = _timed_steps(args, world, stream, step)
+    eng.status(stream)
+    alg = 2 * n * (4 + cap * A * 8 + cap * 8) + n * (4 + 2 * cap * A * 8 + 2 * cap * 8)
+    # partial_cmp beside it: 100M dense row pairs
+    npc = 100_000_000 if world == 1 else 50_000_000
+    ra = torch.randint(0, 3, (npc, A), dtype=torch.int64, device=dev, generator=g)
+    rb = ra.clone()
+    rb[: npc // 2] += torch.randint(0, 2, (npc // 2, A), dtype=torch.int64, device=dev, generator=g)
+    pc = lambda: eng.vclock_partial_cmp(ra, rb, A, stream=stream)  # noqa: E731
+    pwall, pev = _timed_steps(args, world, stream, pc)
+    total = sum_over_ranks(float(n * args.steps), world)
+    res = {
+        "metric": "MVReg merges/sec (node)", "value": total / wall, "unit": "merges/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic: random MVRegs, 0-4 slots per side, 16 dense actors, counters U[0,3)",
+        "config": {"workload": f"mvreg: {n} MVReg<u64> merges per GPU, A=16, 4+4 -> 8 slots",
+                   "parallelism": f"dp{world} (objects sharded)"},
+        "partial_cmp": {"value": sum_over_ranks(float(npc * args.steps), world) / pwall, "unit": "pairs/s",
+                        "achieved_GBps": (2 * npc * A * 8 + npc) / (pev * 1e-3) / 1e9, "kernel_ms": pev},
+    }
+    if world == 1:
+        ach = alg / (ev_ms * 1e-3) / 1e9
+        res["roofline"] = {"bound": "hbm", "kernel": "mvreg_merge_kernel", "achieved": ach, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "kernel_ms": ev_ms, "alg_bytes_per_launch": alg,
+                           "traffic": None}
+        if not args.no_cpu_baseline:
+            mm = 200_000
+            hs = [t[:mm].cpu().numpy() for t in S]
+            ho = [t[:mm].cpu().numpy() for t in O]
+            t0 = _t.perf_counter()
+            oracle_ffi.mvreg_merge(hs[0].view(np.uint32), hs[1].view(np.uint64), hs[2].view(np.uint64),
+                                   ho[0].view(np.uint32), ho[1].view(np.uint64), ho[2].view(np.uint64), A, 2 * cap)
+            secs = _t.perf_counter() - t0
+            res["cpu_baseline"] = {"value": mm / secs, "unit": "merges/s", "cores": 1, "kind": "port",
+                                   "sample": f"{mm} MVReg merges, oracle (std::map clocks), 1 thread, "
+                                             "incl. slab<->map conversion"}
+    return res
+
+
 def main():
     args = parse()
     rank, world, local = dist_setup()
@@ -693,6 +777,8 @@ def main():
         res = run_bincode(args, rank, world, local)
     elif args.workload == "apply":
         res = run_apply(args, rank, world, local)
+    elif args.workload == "mvreg":
+        res = run_mvreg(args, rank, world, local)
     else:
         res = run_dense(args, rank, world, local, args.workload)
     if rank == 0:

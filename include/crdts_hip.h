@@ -273,6 +273,24 @@ int crdt_orswot_generate_replicas(uint64_t seed, size_t first_obj, size_t n_obj,
                                   uint32_t flags, int n_threads, crdt_orswot_gen** out);
 
 /* ------------------------------------------------------------------------ *
+ * VClock partial order and MVReg merge, batched.
+ * crdt_vclock_partial_cmp: d_out[i] = partial_cmp(a[i], b[i])
+ * (src/vclock.rs:59-71) over dense rows u64[n][n_actors], 0 = absent:
+ * 0 Equal, 1 Greater (b <= a), -1 Less (a <= b), 2 None (concurrent).
+ * crdt_mvreg_merge: MVReg<u64, A>::merge (src/mvreg.rs:121-153) over slabs
+ * of `cap` (clock row, value) slots per object, d_*_n[i] slots in use; the
+ * output keeps the reference's order (self's survivors, then other's) and
+ * zero-fills unused slots. cap <= 64 per side; more survivors than out_cap
+ * latch CRDT_ECAPACITY.                                                     */
+int crdt_vclock_partial_cmp(crdt_ctx* ctx, const uint64_t* d_a, const uint64_t* d_b, size_t n,
+                            uint32_t n_actors, int8_t* d_out, void* stream);
+int crdt_mvreg_merge(crdt_ctx* ctx, const uint32_t* d_self_n, const uint64_t* d_self_clk,
+                     const uint64_t* d_self_val, uint32_t self_cap, const uint32_t* d_other_n,
+                     const uint64_t* d_other_clk, const uint64_t* d_other_val, uint32_t other_cap,
+                     uint32_t* d_out_n, uint64_t* d_out_clk, uint64_t* d_out_val, uint32_t out_cap,
+                     size_t n_obj, uint32_t n_actors, void* stream);
+
+/* ------------------------------------------------------------------------ *
  * Batched op path: CmRDT::apply for Orswot (src/orswot.rs:61-85; Op enum
  * :38-53): out[i] = self[i] after applying object i's ops in order.
  *   Op::Add { dot: (actor, counter), member }   kind CRDT_OP_ADD

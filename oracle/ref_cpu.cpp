@@ -785,4 +785,58 @@ int orc_vclock_partial_cmp(const uint32_t* aa, const uint64_t* ac, uint32_t an,
   return mk(aa, ac, an).partial_cmp(mk(ba, bc, bn));
 }
 
+// ---------------------------------------------------------------- MVReg
+// MVReg<V, A> { vals: Vec<(VClock<A>, V)> } (src/mvreg.rs:14-18), V = u64.
+// merge (src/mvreg.rs:121-153): keep self's values no other value strictly
+// dominates (`clock < c`, :126), then other's values no self value strictly
+// dominates whose clock is not already kept (:136-150); order kept.
+// Batch form: dense rows (0 = absent), `cap` slots per object.
+int orc_mvreg_merge_batch(const uint32_t* sn, const uint64_t* sclk, const uint64_t* sval, uint32_t scap,
+                          const uint32_t* on, const uint64_t* oclk, const uint64_t* oval, uint32_t ocap,
+                          uint32_t* outn, uint64_t* oclk_out, uint64_t* oval_out, uint32_t outcap, size_t n,
+                          uint32_t n_actors) {
+  auto row = [&](const uint64_t* base, size_t obj, uint32_t cap, uint32_t k) {
+    return row_to_vclock(base + ((size_t)obj * cap + k) * n_actors, n_actors);
+  };
+  for (size_t i = 0; i < n; ++i) {
+    std::vector<std::pair<VClock, uint64_t>> self, other, vals;
+    for (uint32_t k = 0; k < sn[i]; ++k) self.emplace_back(row(sclk, i, scap, k), sval[i * scap + k]);
+    for (uint32_t k = 0; k < on[i]; ++k) other.emplace_back(row(oclk, i, ocap, k), oval[i * ocap + k]);
+    for (const auto& sv : self) {
+      size_t dom = 0;
+      for (const auto& ov : other) dom += sv.first.partial_cmp(ov.first) == -1 ? 1 : 0;  // clock < c
+      if (dom == 0) vals.push_back(sv);
+    }
+    for (const auto& ov : other) {
+      size_t dom = 0;
+      for (const auto& sv : self) dom += ov.first.partial_cmp(sv.first) == -1 ? 1 : 0;
+      if (dom == 0) {
+        bool is_new = true;
+        for (const auto& e : vals)
+          if (e.first == ov.first) { is_new = false; break; }
+        if (is_new) vals.push_back(ov);
+      }
+    }
+    if (vals.size() > outcap) return -4;
+    outn[i] = (uint32_t)vals.size();
+    for (uint32_t k = 0; k < outcap; ++k) {
+      uint64_t* r = oclk_out + ((size_t)i * outcap + k) * n_actors;
+      if (k < vals.size()) {
+        vclock_to_row(vals[k].first, r, n_actors);
+        oval_out[(size_t)i * outcap + k] = vals[k].second;
+      } else {
+        std::fill(r, r + n_actors, 0ull);
+        oval_out[(size_t)i * outcap + k] = 0;
+      }
+    }
+  }
+  return 0;
+}
+
+// Dense-row VClock partial_cmp batch (src/vclock.rs:59-71): 0 Equal, 1 Greater, -1 Less, 2 None.
+void orc_vclock_partial_cmp_rows(const uint64_t* a, const uint64_t* b, size_t n, uint32_t n_actors, int8_t* out) {
+  for (size_t i = 0; i < n; ++i)
+    out[i] = (int8_t)row_to_vclock(a + i * n_actors, n_actors).partial_cmp(row_to_vclock(b + i * n_actors, n_actors));
+}
+
 }  // extern "C"

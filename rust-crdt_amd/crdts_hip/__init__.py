@@ -235,6 +235,37 @@ class Engine:
         return OrswotBatch(dst, doff, B.n_actors, max(16, (used + 15) // 16 * 16), B.flags)
 
     # ---------------------------------------------------------------- dense
+    # ------------------------------------------------ VClock order / MVReg
+    def vclock_partial_cmp(self, a_rows, b_rows, n_actors, stream=None):
+        """partial_cmp of dense rows (src/vclock.rs:59-71): int8 tensor of
+        0 Equal, 1 Greater, -1 Less, 2 None."""
+        torch = _torch()
+        n = int(a_rows.numel()) // n_actors
+        out = torch.empty(n, dtype=torch.int8, device=a_rows.device)
+        check(lib.crdt_vclock_partial_cmp(self.ctx, C.c_void_p(a_rows.data_ptr()), C.c_void_p(b_rows.data_ptr()), n,
+                                          n_actors, C.c_void_p(out.data_ptr()), self._stream(stream)),
+              "vclock_partial_cmp")
+        return out
+
+    def mvreg_merge(self, self_slab, other_slab, n_actors, out_cap=None, stream=None, check_status=True):
+        """MVReg<u64, A>::merge (src/mvreg.rs:121-153) over slabs (n, clocks[n][cap][A], vals[n][cap])
+        of int32 / int64 device tensors; returns the output slab."""
+        torch = _torch()
+        sn, sc, sv = self_slab
+        on, oc, ov = other_slab
+        n_obj, scap, ocap = int(sn.numel()), int(sv.shape[1]), int(ov.shape[1])
+        cap = out_cap or scap + ocap
+        dev = sn.device
+        outn = torch.empty(n_obj, dtype=torch.int32, device=dev)
+        outc = torch.empty((n_obj, cap, n_actors), dtype=torch.int64, device=dev)
+        outv = torch.empty((n_obj, cap), dtype=torch.int64, device=dev)
+        p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+        check(lib.crdt_mvreg_merge(self.ctx, p(sn), p(sc), p(sv), scap, p(on), p(oc), p(ov), ocap, p(outn), p(outc),
+                                   p(outv), cap, n_obj, n_actors, self._stream(stream)), "mvreg_merge")
+        if check_status:
+            self.status(stream)
+        return outn, outc, outv
+
     # ------------------------------------------------ batched op path
     def orswot_apply(self, B: "OrswotBatch", ops: "OrswotOps", stream=None, check_status=True):
         """out[i] = B[i] after CmRDT::apply of object i's ops in order

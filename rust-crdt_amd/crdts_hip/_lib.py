@@ -59,7 +59,7 @@ EXPORTS = [
     "crdt_host_orswot_decode", "crdt_orswot_record_bytes_ex", "crdt_orswot_merge_ex",
     "crdt_orswot_validate_ex", "crdt_orswot_generate_replicas", "crdt_host_orswot_encode_ex",
     "crdt_orswot_bincode_record_sizes", "crdt_orswot_from_bincode", "crdt_orswot_bincode_sizes",
-    "crdt_orswot_to_bincode", "crdt_orswot_apply",
+    "crdt_orswot_to_bincode", "crdt_orswot_apply", "crdt_vclock_partial_cmp", "crdt_mvreg_merge",
 ]
 
 
@@ -126,6 +126,8 @@ def _load():
         "crdt_orswot_bincode_sizes": (I, [P, BP, U32, U32, U32, U32, P, P]),
         "crdt_orswot_to_bincode": (I, [P, BP, U32, U32, U32, U32, P, P, SZ, P]),
         "crdt_orswot_apply": (I, [P, BP, C.POINTER(Ops), U32, U32, P, P, SZ, P]),
+        "crdt_vclock_partial_cmp": (I, [P, P, P, SZ, U32, P, P]),
+        "crdt_mvreg_merge": (I, [P, P, P, P, U32, P, P, P, U32, P, P, P, U32, SZ, U32, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

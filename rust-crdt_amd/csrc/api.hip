@@ -370,4 +370,28 @@ int crdt_orswot_apply(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_o
                              d_out, d_out_off, out_bytes, ctx->d_status, S(stream));
 }
 
+int crdt_vclock_partial_cmp(crdt_ctx* ctx, const uint64_t* d_a, const uint64_t* d_b, size_t n, uint32_t n_actors,
+                            int8_t* d_out, void* stream) {
+  if (!ctx || n_actors == 0 || (n && (!d_a || !d_b || !d_out))) return CRDT_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return launch_vclock_cmp(d_a, d_b, n, n_actors, d_out, S(stream));
+}
+
+int crdt_mvreg_merge(crdt_ctx* ctx, const uint32_t* d_self_n, const uint64_t* d_self_clk, const uint64_t* d_self_val,
+                     uint32_t self_cap, const uint32_t* d_other_n, const uint64_t* d_other_clk,
+                     const uint64_t* d_other_val, uint32_t other_cap, uint32_t* d_out_n, uint64_t* d_out_clk,
+                     uint64_t* d_out_val, uint32_t out_cap, size_t n_obj, uint32_t n_actors, void* stream) {
+  if (!ctx || n_actors == 0 || self_cap == 0 || other_cap == 0 || self_cap > 64 || other_cap > 64 || out_cap == 0)
+    return CRDT_EINVAL;
+  if (n_obj && (!d_self_n || !d_self_clk || !d_self_val || !d_other_n || !d_other_clk || !d_other_val || !d_out_n ||
+                !d_out_clk || !d_out_val))
+    return CRDT_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return launch_mvreg_merge(d_self_n, d_self_clk, d_self_val, self_cap, d_other_n, d_other_clk, d_other_val,
+                            other_cap, d_out_n, d_out_clk, d_out_val, out_cap, n_obj, n_actors, ctx->d_status,
+                            S(stream));
+}
+
 }  // extern "C"

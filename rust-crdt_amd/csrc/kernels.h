@@ -40,4 +40,10 @@ int launch_orswot_apply(const uint8_t* sb, uint64_t sbytes, const uint64_t* soff
                         const uint64_t* clk_ctr, uint32_t A, uint32_t flags, uint8_t* out, uint64_t* ooff,
                         uint64_t out_bytes, int* status, hipStream_t stream);
 
+int launch_vclock_cmp(const uint64_t* a, const uint64_t* b, uint64_t n, uint32_t A, int8_t* out, hipStream_t stream);
+int launch_mvreg_merge(const uint32_t* sn, const uint64_t* sclk, const uint64_t* sval, uint32_t scap,
+                       const uint32_t* on, const uint64_t* oclk, const uint64_t* oval, uint32_t ocap, uint32_t* outn,
+                       uint64_t* outclk, uint64_t* outval, uint32_t outcap, uint64_t n_obj, uint32_t A, int* status,
+                       hipStream_t stream);
+
 }  // namespace crdts_hip

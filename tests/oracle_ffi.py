@@ -37,6 +37,11 @@ def lib():
     L.orc_bincode_ingest_bench.restype = C.c_double
     L.orc_bincode_ingest_bench.argtypes = [P, P, P, C.c_size_t, C.c_int, C.c_int, C.c_uint32, C.c_uint32, C.c_int,
                                            C.POINTER(C.c_int64)]
+    L.orc_mvreg_merge_batch.restype = C.c_int
+    L.orc_mvreg_merge_batch.argtypes = [P, P, P, C.c_uint32, P, P, P, C.c_uint32, P, P, P, C.c_uint32, C.c_size_t,
+                                        C.c_uint32]
+    L.orc_vclock_partial_cmp_rows.restype = None
+    L.orc_vclock_partial_cmp_rows.argtypes = [P, P, C.c_size_t, C.c_uint32, P]
     L.orc_orswot_apply_bench.restype = C.c_double
     L.orc_orswot_apply_bench.argtypes = [P, P, C.c_size_t, C.c_size_t] + [P] * 8 + [C.c_int]
     L.orc_bincode_egest_bench.restype = C.c_double
@@ -222,6 +227,29 @@ def bincode_ingest_bench(blobs, off, lens, wa, wm, n_actors, flags, threads):
 
 def bincode_egest_bench(rbase, roff, wa, wm, threads):
     return lib().orc_bincode_egest_bench(_ptr(rbase), _ptr(roff), rbase.nbytes, len(roff), wa, wm, threads)
+
+
+def mvreg_merge(sn, sclk, sval, on, oclk, oval, n_actors, out_cap):
+    """Batch MVReg::merge through the oracle: slabs as numpy (n,), (n, cap, A), (n, cap)."""
+    sn, on = (np.ascontiguousarray(x, dtype=np.uint32) for x in (sn, on))
+    sclk, sval, oclk, oval = (np.ascontiguousarray(x, dtype=np.uint64) for x in (sclk, sval, oclk, oval))
+    n = len(sn)
+    outn = np.zeros(n, np.uint32)
+    outc = np.zeros((n, out_cap, n_actors), np.uint64)
+    outv = np.zeros((n, out_cap), np.uint64)
+    rc = lib().orc_mvreg_merge_batch(_ptr(sn), _ptr(sclk), _ptr(sval), sval.shape[1], _ptr(on), _ptr(oclk),
+                                     _ptr(oval), oval.shape[1], _ptr(outn), _ptr(outc), _ptr(outv), out_cap, n,
+                                     n_actors)
+    if rc:
+        raise ValueError(f"oracle mvreg merge rc={rc}")
+    return outn, outc, outv
+
+
+def partial_cmp_rows(a, b, n_actors):
+    a, b = (np.ascontiguousarray(x, dtype=np.uint64) for x in (a, b))
+    out = np.zeros(a.size // n_actors, np.int8)
+    lib().orc_vclock_partial_cmp_rows(_ptr(a), _ptr(b), len(out), n_actors, _ptr(out))
+    return out
 
 
 def orswot_apply_bench(rbase, roff, ops_np, threads):
