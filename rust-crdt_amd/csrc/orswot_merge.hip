@@ -61,7 +61,7 @@ __device__ __forceinline__ uint64_t stamp() {
   return t;
 }
 struct Stamps {
-  uint64_t acc[8];
+  uint64_t acc[16];
   uint64_t last;
 };
 template <int ABL>
@@ -366,9 +366,65 @@ __device__ __forceinline__ bool def_survives_wave(const Side& X, uint32_t k, con
   return __ballot(any) != 0ull;
 }
 
+// One surviving deferred entry: clock kx of side X (c: -1 L only, 1 R only,
+// 0 on both sides — member sets united), written at the running counts.
+__device__ __forceinline__ void deferred_emit(const Side& L, const Side& R, int c, uint32_t k, uint32_t l,
+                                              uint32_t lane, uint32_t& nd, uint32_t& ndd, uint32_t& ndm,
+                                              const DefOut* w) {
+  const Side& X = c <= 0 ? L : R;
+  const uint32_t kx = c <= 0 ? k : l;
+  const uint32_t s = uni(run_begin(X.b, X.v.fdend, kx)), e = uni(g32(X.b, X.v.fdend, kx));
+  if (w)
+    for (uint32_t d = s + lane; d < e; d += kWave) {
+      w->fact[ndd + d - s] = g32(X.b, X.v.fact, d);
+      w->fctr[ndd + d - s] = g64(X.b, X.v.fctr, d);
+    }
+  ndd += e - s;
+  // member set: self's, other's (copied by the lanes), or — for a clock
+  // present on both sides — the sorted union of both (lane 0, rare)
+  if (c != 0) {
+    const uint32_t ms = uni(run_begin(X.b, X.v.fmend, kx)), me = uni(g32(X.b, X.v.fmend, kx));
+    if (w)
+      for (uint32_t j = ms + lane; j < me; j += kWave) w->fkey[ndm + j - ms] = g64(X.b, X.v.fkey, j);
+    ndm += me - ms;
+  } else {
+    uint32_t cnt = 0;
+    if (lane == 0u) {
+      uint32_t a = run_begin(L.b, L.v.fmend, k), ae = g32(L.b, L.v.fmend, k);
+      uint32_t b = run_begin(R.b, R.v.fmend, l), be = g32(R.b, R.v.fmend, l);
+      while (a < ae || b < be) {
+        const uint64_t ka = a < ae ? g64(L.b, L.v.fkey, a) : ~0ull;
+        const uint64_t kb = b < be ? g64(R.b, R.v.fkey, b) : ~0ull;
+        uint64_t km;
+        if (a < ae && (b >= be || ka < kb)) { km = ka; ++a; }
+        else if (b < be && (a >= ae || kb < ka)) { km = kb; ++b; }
+        else { km = ka; ++a; ++b; }
+        if (w) w->fkey[ndm + cnt] = km;
+        ++cnt;
+      }
+    }
+    ndm += lane_of(cnt, 0);
+  }
+  if (w && lane == 0u) { w->fdend[nd] = ndd; w->fmend[nd] = ndm; }
+  ++nd;
+}
+
+// The union walk. With `cache` (LDS, one u32 per survivor): a counting walk
+// (w == nullptr) records each survivor as k | l << 8 | (c + 1) << 16, and a
+// writing walk given the recorded count replays them without the clock
+// compares and survival tests.
 template <bool SP = false>
 __device__ void deferred_pass_wave(const Side& L, const Side& R, uint32_t A, uint32_t lane, uint32_t& nd,
-                                   uint32_t& ndd, uint32_t& ndm, const DefOut* w) {
+                                   uint32_t& ndd, uint32_t& ndm, const DefOut* w, uint32_t* cache = nullptr,
+                                   uint32_t n_cached = 0) {
+  if (w && cache) {
+    nd = ndd = ndm = 0;
+    for (uint32_t i = 0; i < n_cached; ++i) {
+      const uint32_t e = cache[i];
+      deferred_emit(L, R, (int)(e >> 16) - 1, e & 0xFFu, (e >> 8) & 0xFFu, lane, nd, ndd, ndm, w);
+    }
+    return;
+  }
   uint32_t k = 0, l = 0;
   nd = ndd = ndm = 0;
   const uint32_t nfL = uni(L.v.n_def), nfR = uni(R.v.n_def);
@@ -377,40 +433,8 @@ __device__ void deferred_pass_wave(const Side& L, const Side& R, uint32_t A, uin
     const Side& X = c <= 0 ? L : R;
     const uint32_t kx = c <= 0 ? k : l;
     if (def_survives_wave<SP>(X, kx, L, R, A, lane)) {
-      const uint32_t s = uni(run_begin(X.b, X.v.fdend, kx)), e = uni(g32(X.b, X.v.fdend, kx));
-      if (w)
-        for (uint32_t d = s + lane; d < e; d += kWave) {
-          w->fact[ndd + d - s] = g32(X.b, X.v.fact, d);
-          w->fctr[ndd + d - s] = g64(X.b, X.v.fctr, d);
-        }
-      ndd += e - s;
-      // member set: self's, other's (copied by the lanes), or — for a clock
-      // present on both sides — the sorted union of both (lane 0, rare)
-      if (c != 0) {
-        const uint32_t ms = uni(run_begin(X.b, X.v.fmend, kx)), me = uni(g32(X.b, X.v.fmend, kx));
-        if (w)
-          for (uint32_t j = ms + lane; j < me; j += kWave) w->fkey[ndm + j - ms] = g64(X.b, X.v.fkey, j);
-        ndm += me - ms;
-      } else {
-        uint32_t cnt = 0;
-        if (lane == 0u) {
-          uint32_t a = run_begin(L.b, L.v.fmend, k), ae = g32(L.b, L.v.fmend, k);
-          uint32_t b = run_begin(R.b, R.v.fmend, l), be = g32(R.b, R.v.fmend, l);
-          while (a < ae || b < be) {
-            const uint64_t ka = a < ae ? g64(L.b, L.v.fkey, a) : ~0ull;
-            const uint64_t kb = b < be ? g64(R.b, R.v.fkey, b) : ~0ull;
-            uint64_t km;
-            if (a < ae && (b >= be || ka < kb)) { km = ka; ++a; }
-            else if (b < be && (a >= ae || kb < ka)) { km = kb; ++b; }
-            else { km = ka; ++a; ++b; }
-            if (w) w->fkey[ndm + cnt] = km;
-            ++cnt;
-          }
-        }
-        ndm += lane_of(cnt, 0);
-      }
-      if (w && lane == 0u) { w->fdend[nd] = ndd; w->fmend[nd] = ndm; }
-      ++nd;
+      if (cache && lane == 0u) cache[nd] = k | (l << 8) | ((uint32_t)(c + 1) << 16);
+      deferred_emit(L, R, c, k, l, lane, nd, ndd, ndm, w);
     }
     if (c <= 0) ++k;
     if (c >= 0) ++l;
@@ -1634,6 +1658,7 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   const u32x4 pwr = *(const u32x4*)(X + kSpUpre + 16u * (cxr >> 6 & 15u));
   const uint32_t ucl = pwl.z + below64(((uint64_t)pwl.y << 32) | pwl.x, cxl & 63u);
   const uint32_t ucr = pwr.z + below64(((uint64_t)pwr.y << 32) | pwr.x, cxr & 63u);
+  if (ABL == 9) mark<ABL>(*st, 2);
 
   // ---- members (as mask_object); dots are handled in rounds of 64 (<= 128 per side)
   const bool hml = lane < nL, hmr = lane < nR;
@@ -1689,7 +1714,14 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   const uint64_t HR0 = __ballot(lane < dR && X[kSpHeadR + lane] != 0u);
   const uint64_t HR1 = __ballot(64u + lane < dR && X[kSpHeadR + 64u + lane] != 0u);
   bool foreign = false;
-  for (uint32_t rd = 0; rd < nrnd; ++rd) {  // dot -> union clock bit (verified) -> member masks
+  // each dot's actor, counter, union-clock bit and member, per round, kept in
+  // registers for the later passes (two rounds at most)
+  uint32_t rXL[2] = {0u, 0u}, rXR[2] = {0u, 0u}, rBL[2] = {0u, 0u}, rBR[2] = {0u, 0u};
+  uint32_t rML[2] = {0u, 0u}, rMR[2] = {0u, 0u};
+  uint64_t rVL[2] = {0ull, 0ull}, rVR[2] = {0ull, 0ull};
+#pragma unroll
+  for (uint32_t rd = 0; rd < 2u; ++rd) {  // dot -> union clock bit (verified) -> member masks
+    if (rd >= nrnd) break;
     const uint32_t d = 64u * rd + lane;
     const bool hdl = d < dL, hdr = d < dR;
     const uint32_t xl = ld32(Ls, actL + 4u * d), xr = ld32(Rs, actR + 4u * d);
@@ -1698,6 +1730,7 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     const uint32_t ml = (rd ? (uint32_t)__popcll(HL0) : 0u) + mbcnt64(HL) + ((HL >> lane) & 1ull ? 1u : 0u) - 1u;
     const uint32_t mr = (rd ? (uint32_t)__popcll(HR0) : 0u) + mbcnt64(HR) + ((HR >> lane) & 1ull ? 1u : 0u) - 1u;
     const uint32_t bl = X[kSpTable + (xl & (kSpTableN - 1u))] & 63u, br = X[kSpTable + (xr & (kSpTableN - 1u))] & 63u;
+    rXL[rd] = xl; rXR[rd] = xr; rVL[rd] = vl; rVR[rd] = vr; rBL[rd] = bl; rBR[rd] = br; rML[rd] = ml; rMR[rd] = mr;
     foreign = foreign || (hdl && (xl >= kSpTableN || bl >= Uc || *(const uint32_t*)(X + kSpUcAct + 4u * bl) != xl)) ||
               (hdr && (xr >= kSpTableN || br >= Uc || *(const uint32_t*)(X + kSpUcAct + 4u * br) != xr));
     const uint64_t rc = *(const uint64_t*)(X + kSpUcR + 8u * bl), lc = *(const uint64_t*)(X + kSpUcL + 8u * br);
@@ -1712,14 +1745,13 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   if (__ballot(foreign) != 0ull) return kLeanFallback;  // a dot actor outside both top clocks
   wave_sync();
   if (ABL == 9) mark<ABL>(*st, 4);
-  for (uint32_t rd = 0; rd < nrnd; ++rd) {  // actors on both sides of a shared member: equal / self >= other
+#pragma unroll
+  for (uint32_t rd = 0; rd < 2u; ++rd) {  // actors on both sides of a shared member: equal / self >= other
+    if (rd >= nrnd) break;
     const uint32_t dd = 64u * rd + lane;
     const bool hdr = dd < dR;
-    const uint32_t xr = ld32(Rs, actR + 4u * dd);
-    const uint64_t vr = ld64(Rs, ctrR + 8u * dd);
-    const uint32_t br = X[kSpTable + (xr & (kSpTableN - 1u))] & 63u;
-    const uint64_t HR = rd ? HR1 : HR0;
-    const uint32_t mr = (rd ? (uint32_t)__popcll(HR0) : 0u) + mbcnt64(HR) + ((HR >> lane) & 1ull ? 1u : 0u) - 1u;
+    const uint64_t vr = rVR[rd];
+    const uint32_t br = rBR[rd], mr = rMR[rd];
     const uint32_t u = X[kSpUofJ + (mr & 63u)] & 63u;
     const uint32_t d = *(const uint32_t*)(X + kSpDesc + 4u * u);
     const uint32_t i = (d >> 8) & 63u;
@@ -1760,15 +1792,13 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     *(uint64_t*)(X + kSpOut + 32u * lane) = keep;
     *(uint64_t*)(X + kSpOut + 32u * lane + 8u) = useK;
     wave_sync();
-    for (uint32_t rd = 0; rd < nrnd; ++rd) {
+#pragma unroll
+    for (uint32_t rd = 0; rd < 2u; ++rd) {
+      if (rd >= nrnd) break;
       const uint32_t d = 64u * rd + lane;
       const bool hdl = d < dL, hdr = d < dR;
-      const uint32_t xl = ld32(Ls, actL + 4u * d), xr = ld32(Rs, actR + 4u * d);
-      const uint64_t vl = ld64(Ls, ctrL + 8u * d), vr = ld64(Rs, ctrR + 8u * d);
-      const uint32_t bl = X[kSpTable + (xl & (kSpTableN - 1u))] & 63u, br = X[kSpTable + (xr & (kSpTableN - 1u))] & 63u;
-      const uint64_t HL = rd ? HL1 : HL0, HR = rd ? HR1 : HR0;
-      const uint32_t ml = (rd ? (uint32_t)__popcll(HL0) : 0u) + mbcnt64(HL) + ((HL >> lane) & 1ull ? 1u : 0u) - 1u;
-      const uint32_t mr = (rd ? (uint32_t)__popcll(HR0) : 0u) + mbcnt64(HR) + ((HR >> lane) & 1ull ? 1u : 0u) - 1u;
+      const uint32_t xl = rXL[rd], xr = rXR[rd], bl = rBL[rd], br = rBR[rd], ml = rML[rd], mr = rMR[rd];
+      const uint64_t vl = rVL[rd], vr = rVR[rd];
       if (hdl) {
         unsigned long long* ok = (unsigned long long*)(X + kSpOut + 32u * X[kSpUofI + (ml & 63u)]);
         if ((ok[1] >> bl) & 1ull) {
@@ -1787,6 +1817,7 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     wave_sync();
     keep = *(const uint64_t*)(X + kSpOut + 32u * lane);
     useK &= keep;
+    if (ABL == 9) mark<ABL>(*st, 10);
   }
   const uint32_t c = (uint32_t)__popcll(keep);
   // ---- output layout (sparse top clock of Uc entries)
@@ -1795,7 +1826,11 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   const uint32_t cincl = scan_incl(c);
   const uint32_t tot_dot = lane_of(cincl, kWave - 1);
   uint32_t nd = 0, ndd = 0, ndm = 0;
-  if (HD) deferred_pass_wave<true>(DL, DR, A, lane, nd, ndd, ndm, nullptr);
+  if (ABL == 9) mark<ABL>(*st, 6);
+  // survivors cached in the run-head area (free once the head ballots are taken; 64 entries)
+  uint32_t* dcache = (uint32_t*)(X + kSpHeadL);
+  if (HD) deferred_pass_wave<true>(DL, DR, A, lane, nd, ndd, ndm, nullptr, dcache);
+  if (ABL == 9) mark<ABL>(*st, 8);
   RecLayout OL;
   rec_layout(OL, Uc, tot_mem, tot_dot, nd, ndd, ndm, true);
   const uint32_t size = OL.size;
@@ -1820,15 +1855,13 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   wave_sync();
   uint32_t* oact = (uint32_t*)(O + OL.o_dact);
   uint64_t* octr = (uint64_t*)(O + OL.o_dctr);
-  for (uint32_t rd = 0; rd < nrnd; ++rd) {  // every kept dot at its member's base + actor rank
+#pragma unroll
+  for (uint32_t rd = 0; rd < 2u; ++rd) {  // every kept dot at its member's base + actor rank
+    if (rd >= nrnd) break;
     const uint32_t d = 64u * rd + lane;
     const bool hdl = d < dL, hdr = d < dR;
-    const uint32_t xl = ld32(Ls, actL + 4u * d), xr = ld32(Rs, actR + 4u * d);
-    const uint64_t vl = ld64(Ls, ctrL + 8u * d), vr = ld64(Rs, ctrR + 8u * d);
-    const uint32_t bl = X[kSpTable + (xl & (kSpTableN - 1u))] & 63u, br = X[kSpTable + (xr & (kSpTableN - 1u))] & 63u;
-    const uint64_t HL = rd ? HL1 : HL0, HR = rd ? HR1 : HR0;
-    const uint32_t ml = (rd ? (uint32_t)__popcll(HL0) : 0u) + mbcnt64(HL) + ((HL >> lane) & 1ull ? 1u : 0u) - 1u;
-    const uint32_t mr = (rd ? (uint32_t)__popcll(HR0) : 0u) + mbcnt64(HR) + ((HR >> lane) & 1ull ? 1u : 0u) - 1u;
+    const uint32_t xl = rXL[rd], xr = rXR[rd], bl = rBL[rd], br = rBR[rd], ml = rML[rd], mr = rMR[rd];
+    const uint64_t vl = rVL[rd], vr = rVR[rd];
     if (hdl) {
       const uint8_t* ob = X + kSpOut + 32u * X[kSpUofI + (ml & 63u)];
       const uint64_t k = *(const uint64_t*)ob, ua = *(const uint64_t*)(ob + 8);
@@ -1848,11 +1881,14 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
       }
     }
   }
+  if (ABL == 9) mark<ABL>(*st, 7);
   if (HD) {
     DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
              (uint32_t*)(O + OL.o_fdend), (uint32_t*)(O + OL.o_fmend)};
-    deferred_pass_wave<true>(DL, DR, A, lane, nd, ndd, ndm, &w);
+    wave_sync();
+    deferred_pass_wave<true>(DL, DR, A, lane, nd, ndd, ndm, &w, dcache, nd);
   }
+  if (ABL == 9) mark<ABL>(*st, 9);
   if (lane == 0u && OL.o_def != OL.o_mpad) *(uint32_t*)(O + OL.o_mpad) = 0u;
   if (lane >= 1u && lane < 4u && OL.o_end + 4u * (lane - 1u) < size) *(uint32_t*)(O + OL.o_end + 4u * (lane - 1u)) = 0u;
   if (lane == 0u) {
@@ -2412,11 +2448,11 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
       }
     }
   }
-  if (ABL == 9 && lane < 8u) {  // per-wave phase sums -> the context's list buffer
+  if (ABL == 9 && lane < 16u) {  // per-wave phase sums -> the context's list buffer
     uint64_t v = 0;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v = lane == (uint32_t)q ? st.acc[q] : v;
-    list[wave_id * 8u + lane] = v;
+    for (int q = 0; q < 16; ++q) v = lane == (uint32_t)q ? st.acc[q] : v;
+    list[wave_id * 16u + lane] = v;
   }
 }
 

@@ -11,7 +11,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "rust-crdt_amd"))
 
 PHASES = ["wait+stage", "prefetch issue", "clock union", "member ranks + scratch init", "dot masks",
-          "equal/>= pass", "join + deferred kill + layout", "writes (+deferred)"]
+          "equal/>= pass", "member join + layout", "dot/key/clock writes", "deferred pass (count)",
+          "deferred pass (write)", "deferred kill (HD)", "-", "-", "-", "-", "-"]
 
 
 def main():
@@ -39,7 +40,7 @@ def main():
     buf = np.zeros(m, dtype=np.uint64)
     s = torch.cuda.current_stream()
     assert lib.crdt_ctx_debug_read(eng.ctx, buf.ctypes.data, m, C.c_void_p(s.cuda_stream)) == 0
-    per = buf.reshape(-1, 8)
+    per = buf.reshape(-1, 16)
     per = per[per.sum(axis=1) > 0]
     tot = per.sum(axis=0).astype(np.float64)
     print(json.dumps({"step": K, "waves": int(per.shape[0]),
