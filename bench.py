@@ -35,7 +35,7 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="orswot",
-                   choices=["orswot", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply", "mvreg"])
+                   choices=["orswot", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply", "mvreg", "map"])
     p.add_argument("--replicas", type=int, default=8, help="orswot_csr at N=1: replicas folded locally")
     p.add_argument("--n-obj", type=int, default=None, help="objects per GPU")
     p.add_argument("--threads", type=int, default=16, help="host threads (generation, CPU baseline)")
@@ -762,6 +762,69 @@ def run_mvreg(args, rank, world, local):
     return res
 
 
+def run_map(args, rank, world, local):
+    """SURVEY.md §8(f) rank 3: batched Map<u64, MVReg<u64, A>, A>::merge
+    (src/map.rs:191-268) over 250k replica pairs per GPU built by op
+    simulation (A = 16; per side <= 8 keys, 4 values per key, 8 deferred
+    removes of <= 8 keys). A step = one crdt_map_mvreg_merge launch."""
+    import time as _t
+
+    import numpy as np
+    import torch
+
+    import crdts_hip
+
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_ffi
+
+    n = args.n_obj or 250_000
+    A, caps = 16, (8, 4, 8, 8)
+    L, R = oracle_ffi.map_generate(0xC0FFEE07 + rank, n, A, 8, 12, caps)
+    eng = crdts_hip.Engine(local)
+    dev = f"cuda:{local}"
+    dL, dR = L.to(dev), R.to(dev)
+    out = eng.map_mvreg_merge(dL, dR, A)
+    m = 2000
+    sub = lambda S: crdts_hip.MapSlab({f: v[:m] for f, v in S.a.items()}, S.kcap, S.mcap, S.dcap, S.scap)  # noqa: E731
+    exp = oracle_ffi.map_merge(sub(L), sub(R), A)
+    got = out.host()
+    for f in exp.a:
+        assert (got.a[f][:m] == exp.a[f]).all(), f"map merge parity: {f}"
+    stream = torch.cuda.Stream(device=local)
+
+    def step():
+        eng.map_mvreg_merge(dL, dR, A, stream=stream, check_status=False)
+
+    wall, ev_ms = _timed_steps(args, world, stream, step)
+    eng.status(stream)
+    nbytes = lambda S: sum(int(v.numel()) * v.element_size() for v in S.a.values())  # noqa: E731
+    alg = nbytes(dL) + nbytes(dR) + nbytes(out)
+    total = sum_over_ranks(float(n * args.steps), world)
+    res = {
+        "metric": "Map<u64, MVReg> merges/sec (node)", "value": total / wall, "unit": "merges/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic: op-simulated Map<u64, MVReg<u64>> replica pairs (updates, removes, deferred removes)",
+        "config": {"workload": f"map: {n} map merges per GPU, A=16, caps {caps}",
+                   "parallelism": f"dp{world} (objects sharded)"},
+    }
+    if world == 1:
+        ach = alg / (ev_ms * 1e-3) / 1e9
+        res["roofline"] = {"bound": "hbm", "kernel": "map_mvreg_merge_kernel", "achieved": ach, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "kernel_ms": ev_ms, "alg_bytes_per_launch": alg,
+                           "traffic": None}
+        if not args.no_cpu_baseline:
+            mm = 20_000
+            t0 = _t.perf_counter()
+            oracle_ffi.map_merge(sub(L) if mm == m else crdts_hip.MapSlab({f: v[:mm] for f, v in L.a.items()}, *caps),
+                                 crdts_hip.MapSlab({f: v[:mm] for f, v in R.a.items()}, *caps), A)
+            secs = _t.perf_counter() - t0
+            res["cpu_baseline"] = {"value": mm / secs, "unit": "merges/s", "cores": 1, "kind": "port",
+                                   "sample": f"{mm} map merges, oracle (std::map / BTreeMap-shaped), 1 thread, "
+                                             "incl. slab<->map conversion"}
+    return res
+
+
 def main():
     args = parse()
     rank, world, local = dist_setup()
@@ -779,6 +842,8 @@ def main():
         res = run_apply(args, rank, world, local)
     elif args.workload == "mvreg":
         res = run_mvreg(args, rank, world, local)
+    elif args.workload == "map":
+        res = run_map(args, rank, world, local)
     else:
         res = run_dense(args, rank, world, local, args.workload)
     if rank == 0:

@@ -273,6 +273,37 @@ int crdt_orswot_generate_replicas(uint64_t seed, size_t first_obj, size_t n_obj,
                                   uint32_t flags, int n_threads, crdt_orswot_gen** out);
 
 /* ------------------------------------------------------------------------ *
+ * Map<K, MVReg<u64, A>, A>::merge, batched (Map
+ * src/map.rs:82-98, merge :191-268, apply_rm :336-349, apply_deferred
+ * :323-333; MVReg truncate src/mvreg.rs:71-83 as the nested Causal value).
+ * Keys are u64. Dense, fixed-capacity slabs, object i owning:
+ *   clock[A]                            the map clock (0 = absent)
+ *   n_keys, keys[kcap] ascending         entries (BTreeMap order)
+ *   eclock[kcap][A]                      entry clocks
+ *   mv_n[kcap], mv_clock[kcap][mcap][A], mv_val[kcap][mcap]   nested MVRegs (Vec order)
+ *   n_def, dclock[dcap][A]               deferred removes in CLOCK ORDER
+ *   dset_n[dcap], dset[dcap][scap]       their key sets, ascending
+ * Unused slots are zero on output. Output capacities must be >= the sum of
+ * both inputs' (kcap, mcap, dcap, scap); per side kcap <= 32, mcap <= 16,
+ * dcap <= 32, scap <= 32, n_actors <= 64.                                    */
+typedef struct crdt_map_mvreg_slab {
+  uint64_t* clock;
+  uint32_t* n_keys;
+  uint64_t* keys;
+  uint64_t* eclock;
+  uint32_t* mv_n;
+  uint64_t* mv_clock;
+  uint64_t* mv_val;
+  uint32_t* n_def;
+  uint64_t* dclock;
+  uint32_t* dset_n;
+  uint64_t* dset;
+  uint32_t kcap, mcap, dcap, scap;
+} crdt_map_mvreg_slab;
+int crdt_map_mvreg_merge(crdt_ctx* ctx, const crdt_map_mvreg_slab* self, const crdt_map_mvreg_slab* other,
+                         const crdt_map_mvreg_slab* out, size_t n_obj, uint32_t n_actors, void* stream);
+
+/* ------------------------------------------------------------------------ *
  * VClock partial order and MVReg merge, batched.
  * crdt_vclock_partial_cmp: d_out[i] = partial_cmp(a[i], b[i])
  * (src/vclock.rs:59-71) over dense rows u64[n][n_actors], 0 = absent:

@@ -29,6 +29,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <set>
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
@@ -484,6 +485,152 @@ void to_binary(const Orswot& o, int wa, int wm, std::vector<uint8_t>& out) {
 }
 }  // namespace oracle
 
+namespace oracle {
+// ---------------------------------------------------------------- MVReg / Map
+// MVReg<u64, A> (src/mvreg.rs:14-18): merge :121-153, truncate :71-83,
+// apply(Put) :158-185.
+struct MVRegO {
+  std::vector<std::pair<VClock, uint64_t>> vals;
+  void merge(const MVRegO& other) {
+    std::vector<std::pair<VClock, uint64_t>> out;
+    for (const auto& sv : vals) {
+      bool dom = false;
+      for (const auto& ov : other.vals) dom = dom || sv.first.partial_cmp(ov.first) == -1;
+      if (!dom) out.push_back(sv);
+    }
+    for (const auto& ov : other.vals) {
+      bool dom = false;
+      for (const auto& sv : vals) dom = dom || ov.first.partial_cmp(sv.first) == -1;
+      if (dom) continue;
+      bool is_new = true;
+      for (const auto& e : out)
+        if (e.first == ov.first) { is_new = false; break; }
+      if (is_new) out.push_back(ov);
+    }
+    vals.swap(out);
+  }
+  void truncate(const VClock& c) {
+    std::vector<std::pair<VClock, uint64_t>> out;
+    for (auto v : vals) {
+      v.first.subtract(c);
+      if (!v.first.is_empty()) out.push_back(v);
+    }
+    vals.swap(out);
+  }
+  void apply_put(const VClock& clock, uint64_t val) {
+    if (clock.is_empty()) return;
+    std::vector<std::pair<VClock, uint64_t>> out;
+    for (const auto& v : vals)
+      if (!v.first.le(clock)) out.push_back(v);
+    vals.swap(out);
+    bool add = true;
+    for (const auto& v : vals)
+      if (v.first.partial_cmp(clock) == 1) add = false;  // existing_clock > clock
+    if (add) vals.emplace_back(clock, val);
+  }
+};
+
+// Map<u64, MVReg<u64, A>, A> (src/map.rs:82-98): merge :191-268, apply :162-188,
+// apply_rm :336-349, apply_deferred :323-333. std::map<VClock, ...> orders
+// deferred clocks lexicographically over (actor, counter): CLOCK ORDER.
+struct MapEntry {
+  VClock clock;
+  MVRegO val;
+};
+struct MapO {
+  VClock clock;
+  std::map<uint64_t, MapEntry> entries;
+  std::map<std::map<Actor, Counter>, std::set<uint64_t>> deferred;
+
+  void apply_rm(uint64_t key, const VClock& c) {
+    if (!c.le(clock)) deferred[c.dots].insert(key);
+    auto it = entries.find(key);
+    if (it != entries.end()) {
+      MapEntry e = it->second;
+      entries.erase(it);
+      e.clock.subtract(c);
+      if (!e.clock.is_empty()) {
+        e.val.truncate(c);
+        entries[key] = e;
+      }
+    }
+  }
+  void apply_deferred() {
+    auto d = deferred;
+    deferred.clear();
+    for (const auto& kv : d) {
+      VClock c;
+      c.dots = kv.first;
+      for (uint64_t k : kv.second) apply_rm(k, c);
+    }
+  }
+  void apply_up(Actor a, Counter ctr, uint64_t key, const VClock& put_clock, uint64_t val) {
+    if (clock.get(a) >= ctr) return;
+    MapEntry e;
+    auto it = entries.find(key);
+    if (it != entries.end()) { e = it->second; entries.erase(it); }
+    e.clock.witness(a, ctr);
+    e.val.apply_put(put_clock, val);
+    entries[key] = e;
+    clock.witness(a, ctr);
+    apply_deferred();
+  }
+  void merge(const MapO& other) {
+    std::map<uint64_t, MapEntry> keep;
+    for (const auto& kv : entries) {
+      MapEntry entry = kv.second;
+      auto oit = other.entries.find(kv.first);
+      if (oit == other.entries.end()) {
+        entry.clock.subtract(other.clock);
+        if (!entry.clock.is_empty()) {
+          VClock del = other.clock;
+          del.subtract(entry.clock);
+          entry.val.truncate(del);
+          keep[kv.first] = entry;
+        }
+      } else {
+        MapEntry oe = oit->second;
+        VClock common = entry.clock.intersection(oe.clock);
+        entry.clock.subtract(common);
+        oe.clock.subtract(common);
+        entry.clock.subtract(other.clock);
+        oe.clock.subtract(clock);
+        common.merge(entry.clock);
+        common.merge(oe.clock);
+        if (!common.is_empty()) {
+          entry.val.merge(oe.val);
+          VClock del = entry.clock;
+          del.merge(oe.clock);
+          del.subtract(common);
+          entry.val.truncate(del);
+          entry.clock = common;
+          keep[kv.first] = entry;
+        }
+      }
+    }
+    for (const auto& kv : other.entries) {
+      if (entries.count(kv.first)) continue;
+      MapEntry entry = kv.second;
+      entry.clock.subtract(clock);
+      if (!entry.clock.is_empty()) {
+        VClock del = clock;
+        del.subtract(entry.clock);
+        entry.val.truncate(del);
+        keep[kv.first] = entry;
+      }
+    }
+    for (const auto& kv : other.deferred) {  // apply_rm on the old entries: only the deferral survives
+      VClock c;
+      c.dots = kv.first;
+      for (uint64_t k : kv.second) apply_rm(k, c);
+    }
+    entries = keep;
+    clock.merge(other.clock);
+    apply_deferred();
+  }
+};
+}  // namespace oracle
+
 extern "C" {
 
 size_t orc_record_bytes(uint32_t n_clk, uint32_t n_mem, uint32_t n_dot, uint32_t n_def,
@@ -783,6 +930,151 @@ long orc_vclock_binop(int op, const uint32_t* aa, const uint64_t* ac, uint32_t a
 int orc_vclock_partial_cmp(const uint32_t* aa, const uint64_t* ac, uint32_t an,
                            const uint32_t* ba, const uint64_t* bc, uint32_t bn) {
   return mk(aa, ac, an).partial_cmp(mk(ba, bc, bn));
+}
+
+// ---------------------------------------------------------------- Map<u64, MVReg>
+static MapO map_from_slab(const crdt_map_mvreg_slab& S, size_t i, uint32_t A) {
+  MapO m;
+  m.clock = row_to_vclock(S.clock + i * A, A);
+  for (uint32_t k = 0; k < S.n_keys[i]; ++k) {
+    const size_t ki = i * S.kcap + k;
+    MapEntry e;
+    e.clock = row_to_vclock(S.eclock + ki * A, A);
+    for (uint32_t v = 0; v < S.mv_n[ki]; ++v)
+      e.val.vals.emplace_back(row_to_vclock(S.mv_clock + (ki * S.mcap + v) * A, A), S.mv_val[ki * S.mcap + v]);
+    m.entries[S.keys[ki]] = e;
+  }
+  for (uint32_t d = 0; d < S.n_def[i]; ++d) {
+    const size_t di = i * S.dcap + d;
+    auto& set = m.deferred[row_to_vclock(S.dclock + di * A, A).dots];
+    for (uint32_t j = 0; j < S.dset_n[di]; ++j) set.insert(S.dset[di * S.scap + j]);
+  }
+  return m;
+}
+
+static bool map_to_slab(const MapO& m, const crdt_map_mvreg_slab& S, size_t i, uint32_t A) {
+  if (m.entries.size() > S.kcap || m.deferred.size() > S.dcap) return false;
+  vclock_to_row(m.clock, S.clock + i * A, A);
+  S.n_keys[i] = (uint32_t)m.entries.size();
+  uint32_t k = 0;
+  for (uint32_t z = 0; z < S.kcap; ++z) {
+    const size_t ki = i * S.kcap + z;
+    S.keys[ki] = 0;
+    S.mv_n[ki] = 0;
+    std::fill(S.eclock + ki * A, S.eclock + (ki + 1) * A, 0ull);
+    std::fill(S.mv_clock + ki * S.mcap * A, S.mv_clock + (ki + 1) * S.mcap * A, 0ull);
+    std::fill(S.mv_val + ki * S.mcap, S.mv_val + (ki + 1) * S.mcap, 0ull);
+  }
+  for (const auto& kv : m.entries) {
+    const size_t ki = i * S.kcap + k++;
+    if (kv.second.val.vals.size() > S.mcap) return false;
+    S.keys[ki] = kv.first;
+    vclock_to_row(kv.second.clock, S.eclock + ki * A, A);
+    S.mv_n[ki] = (uint32_t)kv.second.val.vals.size();
+    for (uint32_t v = 0; v < S.mv_n[ki]; ++v) {
+      vclock_to_row(kv.second.val.vals[v].first, S.mv_clock + (ki * S.mcap + v) * A, A);
+      S.mv_val[ki * S.mcap + v] = kv.second.val.vals[v].second;
+    }
+  }
+  S.n_def[i] = (uint32_t)m.deferred.size();
+  for (uint32_t z = 0; z < S.dcap; ++z) {
+    const size_t di = i * S.dcap + z;
+    S.dset_n[di] = 0;
+    std::fill(S.dclock + di * A, S.dclock + (di + 1) * A, 0ull);
+    std::fill(S.dset + di * S.scap, S.dset + (di + 1) * S.scap, 0ull);
+  }
+  uint32_t d = 0;
+  for (const auto& kv : m.deferred) {
+    const size_t di = i * S.dcap + d++;
+    if (kv.second.size() > S.scap) return false;
+    VClock c;
+    c.dots = kv.first;
+    vclock_to_row(c, S.dclock + di * A, A);
+    S.dset_n[di] = (uint32_t)kv.second.size();
+    uint32_t j = 0;
+    for (uint64_t key : kv.second) S.dset[di * S.scap + j++] = key;
+  }
+  return true;
+}
+
+// out[i] = self[i].merge(&other[i]); 0, or -4 when an output capacity is exceeded.
+int orc_map_mvreg_merge_batch(const crdt_map_mvreg_slab* s, const crdt_map_mvreg_slab* o,
+                              const crdt_map_mvreg_slab* out, size_t n, uint32_t A) {
+  for (size_t i = 0; i < n; ++i) {
+    MapO m = map_from_slab(*s, i, A);
+    m.merge(map_from_slab(*o, i, A));
+    if (!map_to_slab(m, *out, i, A)) return -4;
+  }
+  return 0;
+}
+
+// Replica pairs by op simulation (the reference's quickcheck shape,
+// test/map.rs:520-740): per object a common history of updates
+// (update(key, get(key).derive_add_ctx(actor), |reg, ctx| reg.set(v, ctx)),
+// src/map.rs:300-313 + src/ctx.rs) and removes (rm(key, get(key)
+// .derive_rm_ctx())), then two replicas diverge with their own actors and
+// receive part of each other's ops, some out of order (deferred removes).
+int orc_map_mvreg_generate(uint64_t seed, size_t n, uint32_t A, uint32_t keys, int ops,
+                           const crdt_map_mvreg_slab* left, const crdt_map_mvreg_slab* right) {
+  struct Op { int kind; Actor a; Counter c; uint64_t key; VClock clock; uint64_t val; };
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t st = seed ^ (0x9E3779B97F4A7C15ull * (i + 1));
+    auto rnd = [&]() {
+      uint64_t z = (st += 0x9E3779B97F4A7C15ull);
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      return z ^ (z >> 31);
+    };
+    MapO rep[2];
+    std::vector<Op> log[2];
+    auto make = [&](MapO& m, int r, bool shared) {
+      Op op;
+      const uint64_t key = rnd() % keys;
+      if (rnd() % 100 < 70) {
+        const Actor a = shared ? (Actor)(rnd() % A) : (Actor)((2 + r) % A);
+        VClock cl = m.clock;  // get(key).derive_add_ctx(a): add_clock = the map clock
+        const Counter c = cl.inc(a);
+        cl.witness(a, c);
+        op = Op{0, a, c, key, cl, rnd() >> 8};
+      } else {
+        auto it = m.entries.find(key);  // get(key).derive_rm_ctx(): the entry clock
+        op = Op{1, 0, 0, key, it == m.entries.end() ? VClock() : it->second.clock, 0};
+      }
+      return op;
+    };
+    auto apply = [&](MapO& m, const Op& op) {
+      if (op.kind == 0) m.apply_up(op.a, op.c, op.key, op.clock, op.val);
+      else m.apply_rm(op.key, op.clock);
+    };
+    const int common = (int)(rnd() % (uint64_t)ops);
+    for (int k = 0; k < common; ++k) {
+      Op op = make(rep[0], 0, true);
+      apply(rep[0], op);
+      apply(rep[1], op);
+    }
+    for (int r = 0; r < 2; ++r) {
+      const int div = 1 + (int)(rnd() % (uint64_t)ops);
+      for (int k = 0; k < div; ++k) {
+        Op op = make(rep[r], r, false);
+        apply(rep[r], op);
+        log[r].push_back(op);
+      }
+    }
+    for (int r = 0; r < 2; ++r) {  // part of the other's ops, in a shuffled order (out-of-order removes defer)
+      std::vector<Op> sub;
+      for (const auto& op : log[1 - r])
+        if (rnd() % 100 < 40) sub.push_back(op);
+      if (rnd() % 100 < 15) {  // a remove from a third replica whose adds neither side has seen
+        VClock c = rep[r].clock;
+        c.witness((Actor)(A - 1), 1000 + rnd() % 8);
+        sub.push_back(Op{1, 0, 0, rnd() % keys, c, 0});
+      }
+      for (size_t k = sub.size(); k > 1; --k) std::swap(sub[k - 1], sub[rnd() % k]);
+      for (const auto& op : sub) apply(rep[r], op);
+    }
+    if (!map_to_slab(rep[0], *left, i, A) || !map_to_slab(rep[1], *right, i, A)) return -4;
+  }
+  return 0;
 }
 
 // ---------------------------------------------------------------- MVReg

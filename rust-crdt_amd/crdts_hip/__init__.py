@@ -148,6 +148,53 @@ class OrswotOps:
         return cls(u64(ends), u32(kind), u64(mem), u32(act), u64(ctr), u64(cend), u32(cact), u64(cctr))
 
 
+class MapSlab:
+    """Dense fixed-capacity slab of Map<u64, MVReg<u64, A>, A> states
+    (crdt_map_mvreg_slab, include/crdts_hip.h). Arrays are numpy (host) or
+    torch (device) with the shapes below; dtypes u32 / u64 (torch: int32 / int64)."""
+
+    FIELDS = ("clock", "n_keys", "keys", "eclock", "mv_n", "mv_clock", "mv_val", "n_def", "dclock", "dset_n", "dset")
+
+    def __init__(self, arrays, kcap, mcap, dcap, scap):
+        self.a = dict(arrays)
+        self.kcap, self.mcap, self.dcap, self.scap = kcap, mcap, dcap, scap
+
+    @staticmethod
+    def shapes(n, A, kcap, mcap, dcap, scap):
+        return {"clock": (n, A), "n_keys": (n,), "keys": (n, kcap), "eclock": (n, kcap, A), "mv_n": (n, kcap),
+                "mv_clock": (n, kcap, mcap, A), "mv_val": (n, kcap, mcap), "n_def": (n,), "dclock": (n, dcap, A),
+                "dset_n": (n, dcap), "dset": (n, dcap, scap)}
+
+    @classmethod
+    def alloc(cls, n, A, kcap, mcap, dcap, scap, device=None):
+        out = {}
+        for f, shp in cls.shapes(n, A, kcap, mcap, dcap, scap).items():
+            u32 = f in ("n_keys", "mv_n", "n_def", "dset_n")
+            if device is None:
+                out[f] = np.zeros(shp, np.uint32 if u32 else np.uint64)
+            else:
+                torch = _torch()
+                out[f] = torch.zeros(shp, dtype=torch.int32 if u32 else torch.int64, device=device)
+        return cls(out, kcap, mcap, dcap, scap)
+
+    def to(self, device):
+        torch = _torch()
+        return MapSlab({f: torch.from_numpy(np.ascontiguousarray(v).view(np.int32 if v.dtype == np.uint32 else np.int64))
+                        .to(device) for f, v in self.a.items()}, self.kcap, self.mcap, self.dcap, self.scap)
+
+    def host(self):
+        return MapSlab({f: (v.cpu().numpy().view(np.uint32 if v.dtype.itemsize == 4 else np.uint64)
+                            if hasattr(v, "cpu") else v) for f, v in self.a.items()},
+                       self.kcap, self.mcap, self.dcap, self.scap)
+
+    def cstruct(self):
+        from ._lib import MapSlabC
+
+        ptr = [C.c_void_p(v.data_ptr() if hasattr(v, "data_ptr") else v.ctypes.data) for v in
+               (self.a[f] for f in self.FIELDS)]
+        return MapSlabC(*ptr, self.kcap, self.mcap, self.dcap, self.scap)
+
+
 class Engine:
     """One crdt_ctx bound to a device. All merges run on the GPU."""
 
@@ -265,6 +312,20 @@ class Engine:
         if check_status:
             self.status(stream)
         return outn, outc, outv
+
+    # ------------------------------------------------ Map<u64, MVReg<u64>>
+    def map_mvreg_merge(self, S: "MapSlab", O: "MapSlab", n_actors, stream=None, check_status=True):
+        """Map::merge (src/map.rs:191-268) of device slabs; returns the output slab
+        (capacities = the sums of the inputs')."""
+        n = int(S.a["n_keys"].shape[0])
+        R = MapSlab.alloc(n, n_actors, S.kcap + O.kcap, S.mcap + O.mcap, S.dcap + O.dcap, S.scap + O.scap,
+                          device=S.a["clock"].device)
+        s, o, r = S.cstruct(), O.cstruct(), R.cstruct()
+        check(lib.crdt_map_mvreg_merge(self.ctx, C.byref(s), C.byref(o), C.byref(r), n, n_actors,
+                                       self._stream(stream)), "map_mvreg_merge")
+        if check_status:
+            self.status(stream)
+        return R
 
     # ------------------------------------------------ batched op path
     def orswot_apply(self, B: "OrswotBatch", ops: "OrswotOps", stream=None, check_status=True):

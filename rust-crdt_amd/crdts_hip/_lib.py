@@ -60,6 +60,7 @@ EXPORTS = [
     "crdt_orswot_validate_ex", "crdt_orswot_generate_replicas", "crdt_host_orswot_encode_ex",
     "crdt_orswot_bincode_record_sizes", "crdt_orswot_from_bincode", "crdt_orswot_bincode_sizes",
     "crdt_orswot_to_bincode", "crdt_orswot_apply", "crdt_vclock_partial_cmp", "crdt_mvreg_merge",
+    "crdt_map_mvreg_merge",
 ]
 
 
@@ -68,6 +69,13 @@ class Ops(C.Structure):
     _fields_ = [("obj_end", C.c_void_p), ("kind", C.c_void_p), ("member", C.c_void_p), ("actor", C.c_void_p),
                 ("counter", C.c_void_p), ("clk_end", C.c_void_p), ("clk_act", C.c_void_p),
                 ("clk_ctr", C.c_void_p), ("n_ops", C.c_size_t), ("n_clk", C.c_size_t)]
+
+
+class MapSlabC(C.Structure):
+    """crdt_map_mvreg_slab (include/crdts_hip.h)."""
+    _fields_ = [(f, C.c_void_p) for f in ("clock", "n_keys", "keys", "eclock", "mv_n", "mv_clock", "mv_val", "n_def",
+                                          "dclock", "dset_n", "dset")] + \
+               [(f, C.c_uint32) for f in ("kcap", "mcap", "dcap", "scap")]
 
 
 def _load():
@@ -128,6 +136,7 @@ def _load():
         "crdt_orswot_apply": (I, [P, BP, C.POINTER(Ops), U32, U32, P, P, SZ, P]),
         "crdt_vclock_partial_cmp": (I, [P, P, P, SZ, U32, P, P]),
         "crdt_mvreg_merge": (I, [P, P, P, P, U32, P, P, P, U32, P, P, P, U32, SZ, U32, P]),
+        "crdt_map_mvreg_merge": (I, [P, C.POINTER(MapSlabC), C.POINTER(MapSlabC), C.POINTER(MapSlabC), SZ, U32, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -394,4 +394,24 @@ int crdt_mvreg_merge(crdt_ctx* ctx, const uint32_t* d_self_n, const uint64_t* d_
                             S(stream));
 }
 
+int crdt_map_mvreg_merge(crdt_ctx* ctx, const crdt_map_mvreg_slab* self, const crdt_map_mvreg_slab* other,
+                         const crdt_map_mvreg_slab* out, size_t n_obj, uint32_t n_actors, void* stream) {
+  if (!ctx || !self || !other || !out || n_actors == 0 || n_actors > 64) return CRDT_EINVAL;
+  for (const crdt_map_mvreg_slab* x : {self, other})
+    if (x->kcap == 0 || x->kcap > 32 || x->mcap == 0 || x->mcap > 16 || x->dcap == 0 || x->dcap > 32 ||
+        x->scap == 0 || x->scap > 32)
+      return CRDT_EINVAL;
+  if (out->kcap < self->kcap + other->kcap || out->mcap < self->mcap + other->mcap ||
+      out->dcap < self->dcap + other->dcap || out->scap < self->scap + other->scap)
+    return CRDT_EINVAL;
+  if (n_obj)
+    for (const crdt_map_mvreg_slab* x : {self, other, out})
+      if (!x->clock || !x->n_keys || !x->keys || !x->eclock || !x->mv_n || !x->mv_clock || !x->mv_val || !x->n_def ||
+          !x->dclock || !x->dset_n || !x->dset)
+        return CRDT_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return launch_map_mvreg_merge(*self, *other, *out, n_obj, n_actors, ctx->d_status, S(stream));
+}
+
 }  // extern "C"

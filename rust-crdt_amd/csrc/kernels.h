@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/crdts_hip.h"
+
 namespace crdts_hip {
 
 int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
@@ -45,5 +47,8 @@ int launch_mvreg_merge(const uint32_t* sn, const uint64_t* sclk, const uint64_t*
                        const uint32_t* on, const uint64_t* oclk, const uint64_t* oval, uint32_t ocap, uint32_t* outn,
                        uint64_t* outclk, uint64_t* outval, uint32_t outcap, uint64_t n_obj, uint32_t A, int* status,
                        hipStream_t stream);
+
+int launch_map_mvreg_merge(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_slab& O, const crdt_map_mvreg_slab& R,
+                           uint64_t n_obj, uint32_t A, int* status, hipStream_t stream);
 
 }  // namespace crdts_hip

@@ -1,0 +1,276 @@
+// Map<u64, MVReg<u64, A>, A>::merge, batched.
+//
+// Reference: Map::merge (src/map.rs:191-268) — per key, the entry clocks are
+// reconciled against both map clocks (self-only :198-211, both :212-237,
+// other-only :241-250), nested values merged (MVReg::merge,
+// src/mvreg.rs:121-153) and truncated by the clock of the actors that removed
+// the entry (MVReg::truncate, src/mvreg.rs:71-83); other's deferred removes
+// are re-deferred against self's pre-merge clock (apply_rm :336-349 — its
+// entry edits land on the entries the merge then replaces, so only the
+// deferral survives), the clocks merge, and apply_deferred (:323-333)
+// subtracts every deferred clock from its keys' entries, dropping emptied
+// entries and truncating the rest, re-deferring the clocks not yet covered.
+// Subtracts commute, so each kept key takes all its deferred clocks at once.
+//
+// One wave per map pair; lane = actor slot (n_actors <= 64), so every VClock
+// operation on dense rows is one lane-parallel op plus a ballot; keys, values
+// and deferred entries are walked by wave-uniform loops.
+#include <hip/hip_runtime.h>
+
+#include "../../include/crdts_hip.h"
+#include "kernels.h"
+
+namespace crdts_hip {
+namespace {
+
+constexpr uint32_t kMpW = 64;
+constexpr uint32_t kMpComb = 64;  // combined deferred entries (<= dcap_self + dcap_other)
+constexpr uint32_t kMpVals = 32;  // kept values of one key (<= mcap_self + mcap_other)
+
+__device__ __forceinline__ void mp_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ uint64_t lane64(uint64_t v, uint32_t t) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), t) << 32) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, t);
+}
+// VClock::subtract (src/vclock.rs:236-242) on one slot
+__device__ __forceinline__ uint64_t vsub(uint64_t e, uint64_t c) { return c >= e ? 0ull : e; }
+__device__ __forceinline__ bool vany(uint64_t v) { return __ballot(v != 0ull) != 0ull; }
+__device__ __forceinline__ bool vle(uint64_t d, uint64_t c) { return __ballot(d > c) == 0ull; }
+__device__ __forceinline__ bool vstrict_less(uint64_t a, uint64_t b) {  // partial_cmp(a, b) == Less
+  return __ballot(a > b) == 0ull && __ballot(a < b) != 0ull;
+}
+// CLOCK ORDER of two dense rows (lexicographic over their (actor, counter) pairs, a proper prefix first)
+__device__ int vorder(uint64_t p, uint64_t q, uint32_t lane) {
+  const uint64_t diff = __ballot(p != q);
+  if (!diff) return 0;
+  const uint32_t x = (uint32_t)__builtin_ctzll(diff);
+  const uint64_t px = lane64(p, x), qx = lane64(q, x);
+  if (px && qx) return px < qx ? -1 : 1;
+  if (!px) return __ballot(p != 0ull && lane > x) ? 1 : -1;  // q has actor x; p continues past x, or ends
+  return __ballot(q != 0ull && lane > x) ? -1 : 1;
+}
+
+__device__ __forceinline__ uint64_t rowv(const uint64_t* base, uint64_t row, uint32_t A, uint32_t lane) {
+  return lane < A ? base[row * A + lane] : 0ull;
+}
+__device__ __forceinline__ bool set_has(const uint64_t* set, uint32_t n, uint64_t key, uint32_t lane) {
+  bool f = false;
+  for (uint32_t j = lane; j < n; j += kMpW) f = f || set[j] == key;
+  return __ballot(f) != 0ull;
+}
+
+__global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_slab S, crdt_map_mvreg_slab O,
+                                                               crdt_map_mvreg_slab R, uint64_t n_obj, uint32_t A,
+                                                               int* __restrict__ status) {
+  __shared__ uint32_t comb[kMpComb];     // (self deferred idx + 1) | (other deferred idx + 1) << 8
+  __shared__ uint32_t vals[kMpVals];     // kept value slots of the key: side << 8 | slot
+  const uint32_t lane = threadIdx.x;
+  for (uint64_t i = blockIdx.x; i < n_obj; i += gridDim.x) {
+    const uint64_t cS = rowv(S.clock, i, A, lane), cO = rowv(O.clock, i, A, lane);
+    const uint64_t cM = cS > cO ? cS : cO;  // VClock::merge
+    const uint32_t nS = __builtin_amdgcn_readfirstlane(S.n_keys[i]), nO = __builtin_amdgcn_readfirstlane(O.n_keys[i]);
+    const uint32_t dS = __builtin_amdgcn_readfirstlane(S.n_def[i]), dO = __builtin_amdgcn_readfirstlane(O.n_def[i]);
+    if (nS > S.kcap || nO > O.kcap || dS > S.dcap || dO > O.dcap) {
+      if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
+      continue;
+    }
+    // ---- combined deferred list: self's, plus other's that self's clock does not cover
+    //      (apply_rm's deferral, against the pre-merge clock), united in CLOCK ORDER
+    uint32_t nc = 0;
+    {
+      uint32_t a = 0, b = 0;
+      while (a < dS || b < dO) {
+        if (b < dO && vle(rowv(O.dclock, i * O.dcap + b, A, lane), cS)) { ++b; continue; }
+        int c;
+        if (a >= dS) c = 1;
+        else if (b >= dO) c = -1;
+        else c = vorder(rowv(S.dclock, i * S.dcap + a, A, lane), rowv(O.dclock, i * O.dcap + b, A, lane), lane);
+        const uint32_t e = (c <= 0 ? a + 1u : 0u) | ((c >= 0 ? b + 1u : 0u) << 8);
+        if (lane == 0u) comb[nc] = e;
+        ++nc;
+        if (c <= 0) ++a;
+        if (c >= 0) ++b;
+      }
+    }
+    mp_sync();
+    // ---- entries, key by key in ascending order
+    uint32_t nk = 0, a = 0, b = 0;
+    bool over = false;
+    while (a < nS || b < nO) {
+      const uint64_t ka = a < nS ? S.keys[i * S.kcap + a] : ~0ull, kb = b < nO ? O.keys[i * O.kcap + b] : ~0ull;
+      const bool hs = a < nS && (b >= nO || ka <= kb), ho = b < nO && (a >= nS || kb <= ka);
+      const uint64_t key = hs ? ka : kb;
+      const uint64_t ia = i * S.kcap + a, ib = i * O.kcap + b;
+      const uint64_t eS = hs ? rowv(S.eclock, ia, A, lane) : 0ull, eO = ho ? rowv(O.eclock, ib, A, lane) : 0ull;
+      uint64_t ec = 0, del = 0;
+      bool keep;
+      uint32_t nv = 0;
+      if (hs && !ho) {  // other has not seen it, or saw it and dropped it
+        ec = vsub(eS, cO);
+        keep = vany(ec);
+        del = vsub(cO, ec);
+        for (uint32_t v = 0; v < S.mv_n[ia] && v < S.mcap; ++v) { if (lane == 0u) vals[nv] = v; ++nv; }
+        mp_sync();
+      } else if (ho && !hs) {
+        ec = vsub(eO, cS);
+        keep = vany(ec);
+        del = vsub(cS, ec);
+        for (uint32_t v = 0; v < O.mv_n[ib] && v < O.mcap; ++v) { if (lane == 0u) vals[nv] = 256u | v; ++nv; }
+      } else {  // in both
+        const uint64_t common = (eS == eO && eS != 0ull) ? eS : 0ull;  // VClock::intersection
+        const uint64_t e1 = vsub(vsub(eS, common), cO), e2 = vsub(vsub(eO, common), cS);
+        uint64_t cm = common > e1 ? common : e1;
+        cm = cm > e2 ? cm : e2;
+        keep = vany(cm);
+        ec = cm;
+        del = vsub(e1 > e2 ? e1 : e2, cm);
+        // MVReg::merge (src/mvreg.rs:121-153): self's undominated, then other's undominated and new
+        const uint32_t ms = S.mv_n[ia] < S.mcap ? S.mv_n[ia] : S.mcap, mo = O.mv_n[ib] < O.mcap ? O.mv_n[ib] : O.mcap;
+        for (uint32_t v = 0; v < ms; ++v) {
+          const uint64_t sv = rowv(S.mv_clock, ia * S.mcap + v, A, lane);
+          bool dom = false;
+          for (uint32_t w = 0; w < mo && !dom; ++w) dom = vstrict_less(sv, rowv(O.mv_clock, ib * O.mcap + w, A, lane));
+          if (!dom) { if (lane == 0u) vals[nv] = v; ++nv; }
+        }
+        mp_sync();
+        const uint32_t nkeep_s = nv;
+        for (uint32_t w = 0; w < mo; ++w) {
+          const uint64_t ov = rowv(O.mv_clock, ib * O.mcap + w, A, lane);
+          bool dom = false;
+          for (uint32_t v = 0; v < ms && !dom; ++v) dom = vstrict_less(ov, rowv(S.mv_clock, ia * S.mcap + v, A, lane));
+          if (dom) continue;
+          bool dup = false;
+          for (uint32_t q = 0; q < nv && !dup; ++q) {
+            const uint32_t sl = vals[q];
+            const uint64_t kv = q < nkeep_s ? rowv(S.mv_clock, ia * S.mcap + (sl & 255u), A, lane)
+                                            : rowv(O.mv_clock, ib * O.mcap + (sl & 255u), A, lane);
+            dup = __ballot(kv != ov) == 0ull;
+          }
+          if (!dup) { if (lane == 0u) vals[nv] = 256u | w; ++nv; }
+          mp_sync();
+        }
+      }
+      mp_sync();
+      // ---- apply_deferred on this key: every combined deferred clock naming it
+      if (keep) {
+        for (uint32_t c = 0; c < nc; ++c) {
+          const uint32_t e = comb[c];
+          const uint32_t sa = e & 255u, sb = e >> 8;
+          bool named = false;
+          if (sa) {
+            const uint64_t di = i * S.dcap + sa - 1u;
+            named = set_has(S.dset + di * S.scap, S.dset_n[di], key, lane);
+          }
+          if (!named && sb) {
+            const uint64_t di = i * O.dcap + sb - 1u;
+            named = set_has(O.dset + di * O.scap, O.dset_n[di], key, lane);
+          }
+          if (!named) continue;
+          const uint64_t D = sa ? rowv(S.dclock, i * S.dcap + sa - 1u, A, lane) : rowv(O.dclock, i * O.dcap + sb - 1u, A, lane);
+          ec = vsub(ec, D);
+          del = del > D ? del : D;  // truncating by several clocks = by their max, slot by slot
+        }
+        keep = vany(ec);
+      }
+      if (keep) {
+        if (nk >= R.kcap) {
+          over = true;
+        } else {
+          const uint64_t ir = i * R.kcap + nk;
+          if (lane == 0u) R.keys[ir] = key;
+          if (lane < A) R.eclock[ir * A + lane] = ec;
+          uint32_t nout = 0;
+          for (uint32_t q = 0; q < nv; ++q) {  // MVReg::truncate(del), order kept
+            const uint32_t sl = vals[q];
+            const bool fromO = sl >= 256u;
+            const uint64_t src = fromO ? ib * O.mcap + (sl & 255u) : ia * S.mcap + (sl & 255u);
+            const uint64_t r = vsub(rowv(fromO ? O.mv_clock : S.mv_clock, src, A, lane), del);
+            if (!vany(r)) continue;
+            if (nout >= R.mcap) { over = true; break; }
+            if (lane < A) R.mv_clock[(ir * R.mcap + nout) * A + lane] = r;
+            if (lane == 0u) R.mv_val[ir * R.mcap + nout] = fromO ? O.mv_val[src] : S.mv_val[src];
+            ++nout;
+          }
+          if (lane == 0u) R.mv_n[ir] = nout;
+          for (uint32_t z = nout; z < R.mcap; ++z) {
+            if (lane < A) R.mv_clock[(ir * R.mcap + z) * A + lane] = 0ull;
+            if (lane == 0u) R.mv_val[ir * R.mcap + z] = 0ull;
+          }
+          ++nk;
+        }
+      }
+      mp_sync();
+      if (hs) ++a;
+      if (ho) ++b;
+    }
+    for (uint32_t z = nk; z < R.kcap; ++z) {  // unused key slots: zero
+      const uint64_t ir = i * R.kcap + z;
+      if (lane == 0u) { R.keys[ir] = 0ull; R.mv_n[ir] = 0u; }
+      if (lane < A) R.eclock[ir * A + lane] = 0ull;
+      for (uint32_t q = 0; q < R.mcap; ++q) {
+        if (lane < A) R.mv_clock[(ir * R.mcap + q) * A + lane] = 0ull;
+        if (lane == 0u) R.mv_val[ir * R.mcap + q] = 0ull;
+      }
+    }
+    if (lane == 0u) R.n_keys[i] = nk;
+    if (lane < A) R.clock[i * A + lane] = cM;
+    // ---- deferred kept: the combined clocks the merged clock does not cover, sets united
+    uint32_t nd = 0;
+    for (uint32_t c = 0; c < nc; ++c) {
+      const uint32_t e = comb[c];
+      const uint32_t sa = e & 255u, sb = e >> 8;
+      const uint64_t D = sa ? rowv(S.dclock, i * S.dcap + sa - 1u, A, lane) : rowv(O.dclock, i * O.dcap + sb - 1u, A, lane);
+      if (vle(D, cM)) continue;
+      if (nd >= R.dcap) { over = true; break; }
+      const uint64_t dr = i * R.dcap + nd;
+      if (lane < A) R.dclock[dr * A + lane] = D;
+      uint32_t cnt = 0;
+      if (lane == 0u) {  // sorted union of the two key sets
+        const uint64_t* xs = sa ? S.dset + (i * S.dcap + sa - 1u) * S.scap : nullptr;
+        const uint64_t* ys = sb ? O.dset + (i * O.dcap + sb - 1u) * O.scap : nullptr;
+        const uint32_t nx = sa ? S.dset_n[i * S.dcap + sa - 1u] : 0u, ny = sb ? O.dset_n[i * O.dcap + sb - 1u] : 0u;
+        uint32_t p = 0, q = 0;
+        while (p < nx || q < ny) {
+          const uint64_t kx = p < nx ? xs[p] : ~0ull, ky = q < ny ? ys[q] : ~0ull;
+          const uint64_t k = kx < ky ? kx : ky;
+          if (kx == k) ++p;
+          if (ky == k) ++q;
+          if (cnt < R.scap) R.dset[dr * R.scap + cnt] = k;
+          ++cnt;
+        }
+        for (uint32_t z = cnt; z < R.scap; ++z) R.dset[dr * R.scap + z] = 0ull;
+        R.dset_n[dr] = cnt < R.scap ? cnt : R.scap;
+      }
+      over = over || __builtin_amdgcn_readfirstlane(cnt) > R.scap;
+      ++nd;
+    }
+    for (uint32_t z = nd; z < R.dcap; ++z) {
+      const uint64_t dr = i * R.dcap + z;
+      if (lane < A) R.dclock[dr * A + lane] = 0ull;
+      if (lane == 0u) R.dset_n[dr] = 0u;
+      for (uint32_t q = lane; q < R.scap; q += kMpW) R.dset[dr * R.scap + q] = 0ull;
+    }
+    if (lane == 0u) R.n_def[i] = nd;
+    if (over && lane == 0u) atomicCAS(status, 0, CRDT_ECAPACITY);
+    mp_sync();
+  }
+}
+
+}  // namespace
+
+int launch_map_mvreg_merge(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_slab& O, const crdt_map_mvreg_slab& R,
+                           uint64_t n_obj, uint32_t A, int* status, hipStream_t stream) {
+  if (n_obj == 0) return CRDT_OK;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const uint64_t cap = (uint64_t)cus * 16u;
+  const uint32_t blocks = (uint32_t)(n_obj < cap ? n_obj : cap);
+  hipLaunchKernelGGL(map_mvreg_merge_kernel, dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A, status);
+  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+}
+
+}  // namespace crdts_hip

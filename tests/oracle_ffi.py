@@ -42,6 +42,10 @@ def lib():
                                         C.c_uint32]
     L.orc_vclock_partial_cmp_rows.restype = None
     L.orc_vclock_partial_cmp_rows.argtypes = [P, P, C.c_size_t, C.c_uint32, P]
+    L.orc_map_mvreg_merge_batch.restype = C.c_int
+    L.orc_map_mvreg_merge_batch.argtypes = [P, P, P, C.c_size_t, C.c_uint32]
+    L.orc_map_mvreg_generate.restype = C.c_int
+    L.orc_map_mvreg_generate.argtypes = [C.c_uint64, C.c_size_t, C.c_uint32, C.c_uint32, C.c_int, P, P]
     L.orc_orswot_apply_bench.restype = C.c_double
     L.orc_orswot_apply_bench.argtypes = [P, P, C.c_size_t, C.c_size_t] + [P] * 8 + [C.c_int]
     L.orc_bincode_egest_bench.restype = C.c_double
@@ -250,6 +254,32 @@ def partial_cmp_rows(a, b, n_actors):
     out = np.zeros(a.size // n_actors, np.int8)
     lib().orc_vclock_partial_cmp_rows(_ptr(a), _ptr(b), len(out), n_actors, _ptr(out))
     return out
+
+
+def map_generate(seed, n, A, keys, ops, caps):
+    """Replica pairs of Map<u64, MVReg<u64>> by op simulation -> (left, right) host MapSlabs."""
+    import crdts_hip
+
+    L = crdts_hip.MapSlab.alloc(n, A, *caps)
+    R = crdts_hip.MapSlab.alloc(n, A, *caps)
+    l, r = L.cstruct(), R.cstruct()
+    rc = lib().orc_map_mvreg_generate(seed, n, A, keys, ops, C.byref(l), C.byref(r))
+    if rc:
+        raise ValueError(f"map generate rc={rc} (capacity)")
+    return L, R
+
+
+def map_merge(S, O, A):
+    """Oracle Map::merge of host MapSlabs -> output MapSlab (capacities summed)."""
+    import crdts_hip
+
+    n = S.a["n_keys"].shape[0]
+    R = crdts_hip.MapSlab.alloc(n, A, S.kcap + O.kcap, S.mcap + O.mcap, S.dcap + O.dcap, S.scap + O.scap)
+    s, o, r = S.cstruct(), O.cstruct(), R.cstruct()
+    rc = lib().orc_map_mvreg_merge_batch(C.byref(s), C.byref(o), C.byref(r), n, A)
+    if rc:
+        raise ValueError(f"oracle map merge rc={rc}")
+    return R
 
 
 def orswot_apply_bench(rbase, roff, ops_np, threads):
