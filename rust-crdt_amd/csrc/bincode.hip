@@ -547,6 +547,87 @@ __global__ __launch_bounds__(kBcWave * kBcWaves, WRITE ? 4 : 5) void bincode_ing
   }
 }
 
+// ---------------------------------------------------------------- ingest sizes
+// The sizes pass needs only the walk's counts, so each LANE walks its own blob
+// (64 independent chains per wave instead of one): u64 fields are two aligned
+// 8-B loads and a funnel shift (byte loads within 16 B of the buffer's end).
+// Same checks, in the same order, as bc_walk.
+__device__ __forceinline__ uint64_t lane_get(const uint8_t* base, uint64_t bytes, uint64_t at, uint32_t w) {
+  uint64_t v;
+  if (at + 16u <= bytes) {
+    const uint64_t* q = (const uint64_t*)(base + (at & ~7ull));
+    const uint32_t sh = 8u * (uint32_t)(at & 7u);
+    const uint64_t lo = q[0], hi = q[1];
+    v = sh ? (lo >> sh) | (hi << (64u - sh)) : lo;
+  } else {
+    v = 0;
+    for (uint32_t i = 0; i < 8u && at + i < bytes; ++i) v |= (uint64_t)base[at + i] << (8u * i);
+  }
+  return w >= 8u ? v : v & ((1ull << (8u * w)) - 1u);
+}
+
+__global__ __launch_bounds__(256) void bincode_sizes_lane_kernel(
+    const uint8_t* __restrict__ blobs, uint64_t blob_bytes, const uint64_t* __restrict__ boff,
+    const uint64_t* __restrict__ blen, uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags,
+    uint64_t* __restrict__ sizes, int* __restrict__ status) {
+  const bool sparse = (flags & kSparseClock) != 0u;
+  const uint64_t sa = wa + 8u;
+  for (uint64_t o = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n_obj; o += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t off = boff[o], len = blen[o];
+    int err = 0;
+    uint32_t n_clk = 0, n_mem = 0, n_dot = 0, n_def = 0, n_fdot = 0, n_fmem = 0;
+    if (off > blob_bytes || len > blob_bytes - off || len < 24u || len >= (1ull << 31)) {
+      err = CRDT_ENONCANON;
+    } else {
+      const uint64_t nclk = lane_get(blobs, blob_bytes, off, 8);
+      if (nclk > A || nclk * sa > len - 24u) {
+        err = CRDT_ENONCANON;
+      } else {
+        n_clk = (uint32_t)nclk;
+        uint64_t p = 8u + nclk * sa;
+        const uint64_t nent = lane_get(blobs, blob_bytes, off + p, 8);
+        p += 8u;
+        if (nent > kBcMaxMem) err = CRDT_ECAPACITY;
+        for (uint64_t e = 0; !err && e < nent; ++e) {
+          if (p + wm + 8u > len) { err = CRDT_ENONCANON; break; }
+          const uint64_t l = lane_get(blobs, blob_bytes, off + p + wm, 8);
+          if (l == 0u || l > A || l * sa > len - (p + wm + 8u)) { err = CRDT_ENONCANON; break; }
+          n_dot += (uint32_t)l;
+          p += wm + 8u + l * sa;
+        }
+        n_mem = (uint32_t)nent;
+        if (!err && p + 8u > len) err = CRDT_ENONCANON;
+        uint64_t ndef = 0;
+        if (!err) {
+          ndef = lane_get(blobs, blob_bytes, off + p, 8);
+          p += 8u;
+          if (ndef > kBcMaxDef) err = CRDT_ECAPACITY;
+        }
+        for (uint64_t d = 0; !err && d < ndef; ++d) {
+          if (p + 8u > len) { err = CRDT_ENONCANON; break; }
+          const uint64_t lc = lane_get(blobs, blob_bytes, off + p, 8);
+          if (lc == 0u || lc > A || lc * sa > len - (p + 8u)) { err = CRDT_ENONCANON; break; }
+          const uint64_t q = p + 8u + lc * sa;
+          if (q + 8u > len) { err = CRDT_ENONCANON; break; }
+          const uint64_t ls = lane_get(blobs, blob_bytes, off + q, 8);
+          if (ls == 0u || ls > len || ls * wm > len - (q + 8u)) { err = CRDT_ENONCANON; break; }
+          n_fdot += (uint32_t)lc;
+          n_fmem += (uint32_t)ls;
+          p = q + 8u + ls * wm;
+        }
+        n_def = (uint32_t)ndef;
+        if (!err && p != len) err = CRDT_ENONCANON;
+      }
+    }
+    if (err) {
+      sizes[o] = 0u;
+      atomicCAS(status, 0, err);
+    } else {
+      sizes[o] = record_size64(sparse ? n_clk : A, n_mem, n_dot, n_def, n_fdot, n_fmem, sparse);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- egest
 // Blob writers. LDS window (zeroed first): a field is OR-ed in as the aligned
 // u32 pieces it covers (ds_or_b32; neighbouring fields of other lanes may
@@ -797,10 +878,14 @@ int launch_bincode_ingest(const uint8_t* blobs, uint64_t blob_bytes, const uint6
                        blob_bytes, boff, blen, n_obj, wa, wm, A, flags, dbg, out, ooff, out_bytes, status);
     return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
   }
-  if (sizes)
-    hipLaunchKernelGGL(bincode_ingest_kernel<false>, dim3(blocks), dim3(kBcWave * kBcWaves), 0, stream, blobs,
-                       blob_bytes, boff, blen, n_obj, wa, wm, A, flags, sizes, out, ooff, out_bytes, status);
-  else
+  if (sizes) {  // one lane per blob
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint64_t want = (n_obj + 255u) / 256u, cap = (uint64_t)cus * 8u;
+    hipLaunchKernelGGL(bincode_sizes_lane_kernel, dim3((uint32_t)(want < cap ? want : cap)), dim3(256), 0, stream,
+                       blobs, blob_bytes, boff, blen, n_obj, wa, wm, A, flags, sizes, status);
+  } else
     hipLaunchKernelGGL(bincode_ingest_kernel<true>, dim3(blocks), dim3(kBcWave * kBcWaves), 0, stream, blobs,
                        blob_bytes, boff, blen, n_obj, wa, wm, A, flags, sizes, out, ooff, out_bytes, status);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
