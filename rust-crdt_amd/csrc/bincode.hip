@@ -249,6 +249,28 @@ __device__ __forceinline__ BcWalk bc_walk(const SRC& B, uint64_t len, uint32_t w
   return w;
 }
 
+// The deferred part of the walk alone (positions into X), from the deferred
+// map's length word at p; counts and bounds were checked by the lane walk.
+template <class SRC>
+__device__ __forceinline__ void bc_walk_deferred(const SRC& B, uint64_t p, uint32_t wa, uint32_t wm, uint8_t* X,
+                                                 uint32_t lane) {
+  const uint64_t sa = wa + 8u;
+  const uint32_t ndef = (uint32_t)bc_uni64(B.get(p, 8));
+  p += 8u;
+  for (uint32_t d = 0; d < ndef; ++d) {
+    const uint64_t lc = bc_uni64(B.get(p, 8));
+    const uint64_t q = p + 8u + lc * sa;
+    const uint64_t ls = bc_uni64(B.get(q, 8));
+    if (lane == (d & (kBcWave - 1u))) {
+      ((uint32_t*)(X + kXPd))[d] = (uint32_t)p;
+      ((uint32_t*)(X + kXLd))[d] = (uint32_t)lc;
+      ((uint32_t*)(X + kXPs))[d] = (uint32_t)q;
+      ((uint32_t*)(X + kXLs))[d] = (uint32_t)ls;
+    }
+    p = q + 8u + ls * wm;
+  }
+}
+
 // Exclusive prefix sum, in place, of n (<= 4 * 64) u32 at S.
 __device__ void bc_scan_excl(uint32_t* S, uint32_t n, uint32_t lane) {
   uint32_t v[4], s = 0;
@@ -566,64 +588,177 @@ __device__ __forceinline__ uint64_t lane_get(const uint8_t* base, uint64_t bytes
   return w >= 8u ? v : v & ((1ull << (8u * w)) - 1u);
 }
 
+struct LaneWalk {
+  uint32_t n_clk, n_mem, n_dot, n_def, n_fdot, n_fmem;
+  uint64_t p_def;  // position of the deferred map's length word
+  int err;
+};
+
+// One lane's walk over its own blob. EMIT: every member entry's (position,
+// dot count) is also stored as a u64 at emit[e] (bounded by emit_end).
+template <bool EMIT>
+__device__ __forceinline__ LaneWalk lane_walk(const uint8_t* blobs, uint64_t blob_bytes, uint64_t off, uint64_t len,
+                                              uint32_t wa, uint32_t wm, uint32_t A, uint64_t* emit,
+                                              const uint8_t* emit_end) {
+  LaneWalk w{0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t sa = wa + 8u;
+  if (off > blob_bytes || len > blob_bytes - off || len < 24u || len >= (1ull << 31)) {
+    w.err = CRDT_ENONCANON;
+    return w;
+  }
+  const uint64_t nclk = lane_get(blobs, blob_bytes, off, 8);
+  if (nclk > A || nclk * sa > len - 24u) { w.err = CRDT_ENONCANON; return w; }
+  w.n_clk = (uint32_t)nclk;
+  uint64_t p = 8u + nclk * sa;
+  const uint64_t nent = lane_get(blobs, blob_bytes, off + p, 8);
+  p += 8u;
+  if (nent > kBcMaxMem) { w.err = CRDT_ECAPACITY; return w; }
+  for (uint64_t e = 0; e < nent; ++e) {
+    if (p + wm + 8u > len) { w.err = CRDT_ENONCANON; return w; }
+    const uint64_t l = lane_get(blobs, blob_bytes, off + p + wm, 8);
+    if (l == 0u || l > A || l * sa > len - (p + wm + 8u)) { w.err = CRDT_ENONCANON; return w; }
+    if (EMIT) {
+      if ((const uint8_t*)(emit + e + 1) > emit_end) { w.err = CRDT_ECAPACITY; return w; }
+      emit[e] = p | (l << 32);
+    }
+    w.n_dot += (uint32_t)l;
+    p += wm + 8u + l * sa;
+  }
+  w.n_mem = (uint32_t)nent;
+  if (p + 8u > len) { w.err = CRDT_ENONCANON; return w; }
+  w.p_def = p;
+  const uint64_t ndef = lane_get(blobs, blob_bytes, off + p, 8);
+  p += 8u;
+  if (ndef > kBcMaxDef) { w.err = CRDT_ECAPACITY; return w; }
+  for (uint64_t d = 0; d < ndef; ++d) {
+    if (p + 8u > len) { w.err = CRDT_ENONCANON; return w; }
+    const uint64_t lc = lane_get(blobs, blob_bytes, off + p, 8);
+    if (lc == 0u || lc > A || lc * sa > len - (p + 8u)) { w.err = CRDT_ENONCANON; return w; }
+    const uint64_t q = p + 8u + lc * sa;
+    if (q + 8u > len) { w.err = CRDT_ENONCANON; return w; }
+    const uint64_t ls = lane_get(blobs, blob_bytes, off + q, 8);
+    if (ls == 0u || ls > len || ls * wm > len - (q + 8u)) { w.err = CRDT_ENONCANON; return w; }
+    w.n_fdot += (uint32_t)lc;
+    w.n_fmem += (uint32_t)ls;
+    p = q + 8u + ls * wm;
+  }
+  w.n_def = (uint32_t)ndef;
+  if (p != len) w.err = CRDT_ENONCANON;
+  return w;
+}
+
 __global__ __launch_bounds__(256) void bincode_sizes_lane_kernel(
     const uint8_t* __restrict__ blobs, uint64_t blob_bytes, const uint64_t* __restrict__ boff,
     const uint64_t* __restrict__ blen, uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags,
     uint64_t* __restrict__ sizes, int* __restrict__ status) {
   const bool sparse = (flags & kSparseClock) != 0u;
-  const uint64_t sa = wa + 8u;
   for (uint64_t o = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n_obj; o += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t off = boff[o], len = blen[o];
-    int err = 0;
-    uint32_t n_clk = 0, n_mem = 0, n_dot = 0, n_def = 0, n_fdot = 0, n_fmem = 0;
-    if (off > blob_bytes || len > blob_bytes - off || len < 24u || len >= (1ull << 31)) {
-      err = CRDT_ENONCANON;
-    } else {
-      const uint64_t nclk = lane_get(blobs, blob_bytes, off, 8);
-      if (nclk > A || nclk * sa > len - 24u) {
-        err = CRDT_ENONCANON;
-      } else {
-        n_clk = (uint32_t)nclk;
-        uint64_t p = 8u + nclk * sa;
-        const uint64_t nent = lane_get(blobs, blob_bytes, off + p, 8);
-        p += 8u;
-        if (nent > kBcMaxMem) err = CRDT_ECAPACITY;
-        for (uint64_t e = 0; !err && e < nent; ++e) {
-          if (p + wm + 8u > len) { err = CRDT_ENONCANON; break; }
-          const uint64_t l = lane_get(blobs, blob_bytes, off + p + wm, 8);
-          if (l == 0u || l > A || l * sa > len - (p + wm + 8u)) { err = CRDT_ENONCANON; break; }
-          n_dot += (uint32_t)l;
-          p += wm + 8u + l * sa;
-        }
-        n_mem = (uint32_t)nent;
-        if (!err && p + 8u > len) err = CRDT_ENONCANON;
-        uint64_t ndef = 0;
-        if (!err) {
-          ndef = lane_get(blobs, blob_bytes, off + p, 8);
-          p += 8u;
-          if (ndef > kBcMaxDef) err = CRDT_ECAPACITY;
-        }
-        for (uint64_t d = 0; !err && d < ndef; ++d) {
-          if (p + 8u > len) { err = CRDT_ENONCANON; break; }
-          const uint64_t lc = lane_get(blobs, blob_bytes, off + p, 8);
-          if (lc == 0u || lc > A || lc * sa > len - (p + 8u)) { err = CRDT_ENONCANON; break; }
-          const uint64_t q = p + 8u + lc * sa;
-          if (q + 8u > len) { err = CRDT_ENONCANON; break; }
-          const uint64_t ls = lane_get(blobs, blob_bytes, off + q, 8);
-          if (ls == 0u || ls > len || ls * wm > len - (q + 8u)) { err = CRDT_ENONCANON; break; }
-          n_fdot += (uint32_t)lc;
-          n_fmem += (uint32_t)ls;
-          p = q + 8u + ls * wm;
-        }
-        n_def = (uint32_t)ndef;
-        if (!err && p != len) err = CRDT_ENONCANON;
-      }
-    }
-    if (err) {
+    const LaneWalk w = lane_walk<false>(blobs, blob_bytes, boff[o], blen[o], wa, wm, A, nullptr, nullptr);
+    if (w.err) {
       sizes[o] = 0u;
-      atomicCAS(status, 0, err);
+      atomicCAS(status, 0, w.err);
     } else {
-      sizes[o] = record_size64(sparse ? n_clk : A, n_mem, n_dot, n_def, n_fdot, n_fmem, sparse);
+      sizes[o] = record_size64(sparse ? w.n_clk : A, w.n_mem, w.n_dot, w.n_def, w.n_fdot, w.n_fmem, sparse);
+    }
+  }
+}
+
+// Decode pass. Each lane first walks its own blob of the chunk (as in the
+// sizes pass) and parks every member entry's (position, dot count) in its
+// output record's key section (overwritten later by the keys themselves);
+// the wave then decodes the chunk's objects one by one from the LDS window,
+// reading those pairs instead of walking the entry chain again.
+__global__ __launch_bounds__(kBcWave * kBcWaves, 4) void bincode_decode_kernel(
+    const uint8_t* __restrict__ blobs, uint64_t blob_bytes, const uint64_t* __restrict__ boff,
+    const uint64_t* __restrict__ blen, uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags,
+    uint8_t* __restrict__ out, const uint64_t* __restrict__ ooff, uint64_t out_bytes, int* __restrict__ status) {
+  __shared__ v4u st_s[kBcWaves][kBcStage / 16];
+  __shared__ v4u sx_s[kBcWaves][kXBytes / 16];
+  const uint32_t lane = threadIdx.x & (kBcWave - 1u), wave = threadIdx.x / kBcWave;
+  uint8_t* X = (uint8_t*)sx_s[wave];
+  const bool sparse = (flags & kSparseClock) != 0u;
+  const uint64_t n_waves = (uint64_t)gridDim.x * kBcWaves;
+  const uint64_t wave_id = (uint64_t)blockIdx.x * kBcWaves + wave;
+  for (uint64_t cbase = wave_id * kBcWave; cbase < n_obj; cbase += n_waves * kBcWave) {
+    const uint64_t obj = cbase + lane;
+    const bool valid = obj < n_obj;
+    uint64_t off = 0, len = 0, oo = 0;
+    if (valid) { off = boff[obj]; len = blen[obj]; oo = ooff[obj]; }
+    LaneWalk lw{0, 0, 0, 0, 0, 0, 0, 0};
+    if (valid) {
+      if ((oo & 15u) || oo > out_bytes) {
+        lw.err = CRDT_ECAPACITY;
+      } else {
+        // the key section follows the top clock; a sparse clock's size is the
+        // blob's first field (peeked here, re-checked by the walk)
+        const uint64_t nclk = (off <= blob_bytes && len >= 8u && len <= blob_bytes - off)
+                                  ? lane_get(blobs, blob_bytes, off, 8) : 0u;
+        const uint32_t kc = sparse ? (uint32_t)(nclk < A ? nclk : A) : A;
+        uint64_t* emit = (uint64_t*)(out + oo + kHdrBytes + clock_bytes(kc, sparse));
+        lw = lane_walk<true>(blobs, blob_bytes, off, len, wa, wm, A, emit, out + out_bytes);
+      }
+      if (!lw.err) {
+        const uint64_t sz = record_size64(sparse ? lw.n_clk : A, lw.n_mem, lw.n_dot, lw.n_def, lw.n_fdot, lw.n_fmem,
+                                          sparse);
+        if (sz > out_bytes - oo) lw.err = CRDT_ECAPACITY;
+      }
+      if (lw.err) atomicCAS(status, 0, lw.err);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // the parked pairs are visible to the whole wave
+    const bool ok = valid && !lw.err;
+    const bool win = ok && len + 32u <= kBcStage;
+    const uint64_t a0 = off & ~15ull;
+    const uint32_t n16 = win ? (uint32_t)((((off + len + 15u) & ~15ull) - a0) / 16u) : 0u;
+    const uint64_t wins = __ballot(win);
+    uint64_t pend = __ballot(ok);
+    v4u pf[kBcPer];
+    uint64_t nxt = wins;
+    if (nxt) {
+      const uint32_t t = (uint32_t)__builtin_ctzll(nxt);
+      bc_prefetch(pf, blobs, blob_bytes, bc_lane64(a0, t), __builtin_amdgcn_readlane(n16, t), lane);
+    }
+    while (pend) {
+      const uint32_t t = (uint32_t)__builtin_ctzll(pend);
+      pend &= pend - 1;
+      const uint64_t ot = bc_lane64(off, t), oot = bc_lane64(oo, t);
+      BcWalk w;
+      w.n_clk = __builtin_amdgcn_readlane(lw.n_clk, t);
+      w.n_mem = __builtin_amdgcn_readlane(lw.n_mem, t);
+      w.n_dot = __builtin_amdgcn_readlane(lw.n_dot, t);
+      w.n_def = __builtin_amdgcn_readlane(lw.n_def, t);
+      w.n_def_dot = __builtin_amdgcn_readlane(lw.n_fdot, t);
+      w.n_def_mem = __builtin_amdgcn_readlane(lw.n_fmem, t);
+      w.err = 0;
+      const uint64_t pdef = bc_lane64(lw.p_def, t);
+      // the parked (position, dot count) pairs -> the walk's LDS arrays
+      const uint64_t* keyarea = (const uint64_t*)(out + oot + kHdrBytes + clock_bytes(sparse ? w.n_clk : A, sparse));
+      bc_sync();
+      for (uint32_t e = lane; e < w.n_mem; e += kBcWave) {
+        const uint64_t pr = keyarea[e];
+        ((uint32_t*)(X + kXPm))[e] = (uint32_t)pr;
+        ((uint32_t*)(X + kXLm))[e] = (uint32_t)(pr >> 32);
+      }
+      int rc;
+      if ((wins >> t) & 1ull) {
+#pragma unroll
+        for (uint32_t k = 0; k < kBcPer; ++k) st_s[wave][lane + k * kBcWave] = pf[k];
+        bc_sync();
+        nxt &= nxt - 1;  // t was the lowest pending windowed object
+        if (nxt) {
+          const uint32_t u = (uint32_t)__builtin_ctzll(nxt);
+          bc_prefetch(pf, blobs, blob_bytes, bc_lane64(a0, u), __builtin_amdgcn_readlane(n16, u), lane);
+        }
+        const Src<true> B{(const uint8_t*)st_s[wave], (uint32_t)(ot & 15u)};
+        if (w.n_def) bc_walk_deferred(B, pdef, wa, wm, X, lane);
+        bc_sync();
+        rc = bc_write_record(B, w, wa, wm, A, sparse, X, out + oot, lane);
+      } else {
+        const Src<false> B{blobs + ot};
+        if (w.n_def) bc_walk_deferred(B, pdef, wa, wm, X, lane);
+        bc_sync();
+        rc = bc_write_record(B, w, wa, wm, A, sparse, X, out + oot, lane);
+      }
+      if (rc && lane == 0u) atomicCAS(status, 0, rc);
     }
   }
 }
@@ -886,8 +1021,8 @@ int launch_bincode_ingest(const uint8_t* blobs, uint64_t blob_bytes, const uint6
     hipLaunchKernelGGL(bincode_sizes_lane_kernel, dim3((uint32_t)(want < cap ? want : cap)), dim3(256), 0, stream,
                        blobs, blob_bytes, boff, blen, n_obj, wa, wm, A, flags, sizes, status);
   } else
-    hipLaunchKernelGGL(bincode_ingest_kernel<true>, dim3(blocks), dim3(kBcWave * kBcWaves), 0, stream, blobs,
-                       blob_bytes, boff, blen, n_obj, wa, wm, A, flags, sizes, out, ooff, out_bytes, status);
+    hipLaunchKernelGGL(bincode_decode_kernel, dim3(blocks), dim3(kBcWave * kBcWaves), 0, stream, blobs, blob_bytes,
+                       boff, blen, n_obj, wa, wm, A, flags, out, ooff, out_bytes, status);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 
