@@ -41,7 +41,7 @@ def parse():
     p.add_argument("--threads", type=int, default=16, help="host threads (generation, CPU baseline)")
     p.add_argument("--cpu-sample", type=int, default=500_000, help="objects in the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r01c.json"),
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r01d.json"),
                    help="measured per-launch HBM bytes (rocprofv3 PMC) to report as roofline.traffic")
     p.add_argument("--blocks-per-cu", type=int, default=None)
     p.add_argument("--variant", type=int, default=None, help="Orswot kernel variant (tuning/diagnostics)")
