@@ -366,8 +366,10 @@ int crdt_orswot_apply(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_o
   int rc = set_device(ctx);
   if (rc) return rc;
   return launch_orswot_apply(self->base, self->bytes, self->off, self->n_obj, ops->obj_end, ops->kind, ops->member,
-                             ops->actor, ops->counter, ops->clk_end, ops->clk_act, ops->clk_ctr, n_actors, flags,
-                             d_out, d_out_off, out_bytes, ctx->d_status, S(stream));
+                             ops->actor, ops->counter, ops->clk_end, ops->clk_act, ops->clk_ctr, ops->n_ops, ops->n_clk,
+                             n_actors, flags,
+                             d_out, d_out_off, out_bytes, ctx->d_status, ctx->d_ctl, ctx->d_list, ctx->list_cap,
+                             S(stream));
 }
 
 int crdt_vclock_partial_cmp(crdt_ctx* ctx, const uint64_t* d_a, const uint64_t* d_b, size_t n, uint32_t n_actors,

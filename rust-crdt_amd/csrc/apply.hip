@@ -20,6 +20,8 @@
 // + 16, padding <= 32).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "../../include/crdts_hip.h"
 #include "kernels.h"
 #include "record_layout.h"
@@ -28,29 +30,39 @@ namespace crdts_hip {
 namespace {
 
 constexpr uint32_t kAW = 64;
-constexpr uint32_t kApCk = 128;      // top clock: dense slots (n_actors <= 128) or sparse entries
-constexpr uint32_t kApMem = 128;     // members
-constexpr uint32_t kApDot = 512;     // member dots
-constexpr uint32_t kApDef = 32;      // deferred clocks
-constexpr uint32_t kApFDot = 256;    // deferred clock entries
-constexpr uint32_t kApFMem = 256;    // deferred members
-constexpr uint32_t kApTmp = 128;     // the clock an Rm / a deferred re-apply subtracts
+// Workspace capacities. Every object is first run in the small workspace
+// (8 KB of LDS: ~20 resident waves per CU); an object that outgrows it is
+// listed and redone from its input in the large one (16 KB).
+template <uint32_t CK, uint32_t MEM, uint32_t DOT, uint32_t DEF, uint32_t FDOT, uint32_t FMEM, uint32_t TMP>
+struct Caps {
+  static constexpr uint32_t kCk = CK;      // top clock: dense slots (n_actors <= kCk) or sparse entries
+  static constexpr uint32_t kMem = MEM;    // members
+  static constexpr uint32_t kDot = DOT;    // member dots
+  static constexpr uint32_t kDef = DEF;    // deferred clocks
+  static constexpr uint32_t kFDot = FDOT;  // deferred clock entries
+  static constexpr uint32_t kFMem = FMEM;  // deferred members
+  static constexpr uint32_t kTmp = TMP;    // the clock an Rm / a deferred re-apply subtracts
+};
+using SmallCaps = Caps<64, 64, 256, 16, 128, 128, 64>;
+using BigCaps = Caps<128, 128, 512, 32, 256, 256, 128>;
+constexpr uint64_t kApPending = 1ull << 63;  // out_off flag: object left for the large workspace
 
+template <class C>
 struct Ws {
-  uint64_t cctr[kApCk];
-  uint64_t key[kApMem];
-  uint64_t dctr[kApDot];
-  uint64_t fctr[kApFDot];
-  uint64_t fkey[kApFMem];
-  uint64_t tctr[kApTmp];
-  uint32_t cact[kApCk];
-  uint32_t dend[kApMem];
-  uint32_t dact[kApDot];
-  uint32_t fact[kApFDot];
-  uint32_t fdend[kApDef];
-  uint32_t fmend[kApDef];
-  uint32_t tact[kApTmp];
-  uint32_t dead[kApDef];
+  uint64_t cctr[C::kCk];
+  uint64_t key[C::kMem];
+  uint64_t dctr[C::kDot];
+  uint64_t fctr[C::kFDot];
+  uint64_t fkey[C::kFMem];
+  uint64_t tctr[C::kTmp];
+  uint32_t cact[C::kCk];
+  uint32_t dend[C::kMem];
+  uint32_t dact[C::kDot];
+  uint32_t fact[C::kFDot];
+  uint32_t fdend[C::kDef];
+  uint32_t fmend[C::kDef];
+  uint32_t tact[C::kTmp];
+  uint32_t dead[C::kDef];
 };
 
 struct Cnt {
@@ -120,23 +132,26 @@ __device__ __forceinline__ uint64_t list_get(const uint32_t* act, const uint64_t
   }
   return lo < n && act[lo] == x ? ctr[lo] : 0ull;
 }
-__device__ __forceinline__ uint64_t clock_get(const Ws& w, const Cnt& c, bool sparse, uint32_t x) {
+template <class C>
+__device__ __forceinline__ uint64_t clock_get(const Ws<C>& w, const Cnt& c, bool sparse, uint32_t x) {
   return sparse ? list_get(w.cact, w.cctr, c.clk, x) : (x < c.clk ? w.cctr[x] : 0ull);
 }
 
 // tmp <= top clock (for canonical clocks: every tmp entry <= the clock's)
-__device__ bool tmp_le_clock(const Ws& w, const Cnt& c, bool sparse, uint32_t lane) {
+template <class C>
+__device__ bool tmp_le_clock(const Ws<C>& w, const Cnt& c, bool sparse, uint32_t lane) {
   bool bad = false;
   for (uint32_t i = lane; i < c.tmp; i += kAW) bad = bad || w.tctr[i] > clock_get(w, c, sparse, w.tact[i]);
   return __ballot(bad) == 0ull;
 }
 
 // entries[m].subtract(tmp) (src/vclock.rs:236-242); drop the entry if empty
-__device__ void entry_subtract(Ws& w, Cnt& c, uint64_t m, uint32_t lane) {
+template <class C>
+__device__ void entry_subtract(Ws<C>& w, Cnt& c, uint64_t m, uint32_t lane) {
   const uint32_t pos = count_less(w.key, 0u, c.mem, m, lane);
   if (pos >= c.mem || w.key[pos] != m) return;
   const uint32_t b = pos ? w.dend[pos - 1] : 0u, e = w.dend[pos], n = e - b;
-  // the run has <= kApCk dots (one per actor): two per lane at most
+  // the run has <= C::kCk dots (one per actor): two per lane at most
   uint32_t x0 = 0, x1 = 0;
   uint64_t v0 = 0, v1 = 0;
   const bool h0 = lane < n, h1 = lane + kAW < n;
@@ -168,7 +183,8 @@ __device__ void entry_subtract(Ws& w, Cnt& c, uint64_t m, uint32_t lane) {
 
 // lexicographic (actor, counter) compare of deferred clock k with tmp, a
 // proper prefix first: -1, 0, 1 (per lane: k = the lane's clock)
-__device__ int def_cmp_tmp(const Ws& w, const Cnt& c, uint32_t k) {
+template <class C>
+__device__ int def_cmp_tmp(const Ws<C>& w, const Cnt& c, uint32_t k) {
   const uint32_t b = k ? w.fdend[k - 1] : 0u, n = w.fdend[k] - b;
   const uint32_t m = n < c.tmp ? n : c.tmp;
   for (uint32_t i = 0; i < m; ++i) {
@@ -181,7 +197,8 @@ __device__ int def_cmp_tmp(const Ws& w, const Cnt& c, uint32_t k) {
 }
 
 // deferred[tmp] += {m}; returns an error code on capacity overflow
-__device__ int deferred_add(Ws& w, Cnt& c, uint64_t m, uint32_t lane) {
+template <class C>
+__device__ int deferred_add(Ws<C>& w, Cnt& c, uint64_t m, uint32_t lane) {
   int cm = 1;
   if (lane < c.def) cm = def_cmp_tmp(w, c, lane);
   const uint64_t eq = __ballot(lane < c.def && cm == 0);
@@ -190,7 +207,7 @@ __device__ int deferred_add(Ws& w, Cnt& c, uint64_t m, uint32_t lane) {
     const uint32_t ms = k ? w.fmend[k - 1] : 0u, me = w.fmend[k];
     const uint32_t r = count_less(w.fkey, ms, me, m, lane);
     if (ms + r < me && w.fkey[ms + r] == m) return 0;  // already in the set
-    if (c.fmem + 1u > kApFMem) return CRDT_ECAPACITY;
+    if (c.fmem + 1u > C::kFMem) return CRDT_ECAPACITY;
     ins_gap(w.fkey, c.fmem, ms + r, 1u, lane);
     if (lane == 0u) w.fkey[ms + r] = m;
     ap_sync();
@@ -198,7 +215,7 @@ __device__ int deferred_add(Ws& w, Cnt& c, uint64_t m, uint32_t lane) {
     c.fmem += 1u;
     return 0;
   }
-  if (c.def + 1u > kApDef || c.fdot + c.tmp > kApFDot || c.fmem + 1u > kApFMem) return CRDT_ECAPACITY;
+  if (c.def + 1u > C::kDef || c.fdot + c.tmp > C::kFDot || c.fmem + 1u > C::kFMem) return CRDT_ECAPACITY;
   const uint32_t kk = ap_count(lane < c.def && cm < 0);  // clocks ordered before tmp
   const uint32_t o = kk ? w.fdend[kk - 1] : 0u, om = kk ? w.fmend[kk - 1] : 0u;
   ins_gap(w.fact, c.fdot, o, c.tmp, lane);
@@ -219,7 +236,8 @@ __device__ int deferred_add(Ws& w, Cnt& c, uint64_t m, uint32_t lane) {
 }
 
 // apply_deferred (src/orswot.rs:235-243)
-__device__ void apply_deferred(Ws& w, Cnt& c, bool sparse, uint32_t lane) {
+template <class C>
+__device__ void apply_deferred(Ws<C>& w, Cnt& c, bool sparse, uint32_t lane) {
   if (c.def == 0u) return;
   for (uint32_t k = 0; k < c.def; ++k) {
     const uint32_t b = k ? w.fdend[k - 1] : 0u, e = w.fdend[k];
@@ -250,7 +268,8 @@ __device__ void apply_deferred(Ws& w, Cnt& c, bool sparse, uint32_t lane) {
 }
 
 // Op::Add (src/orswot.rs:66-79)
-__device__ int op_add(Ws& w, Cnt& c, bool sparse, uint32_t A, uint32_t a, uint64_t ctr, uint64_t m, uint32_t lane) {
+template <class C>
+__device__ int op_add(Ws<C>& w, Cnt& c, bool sparse, uint32_t A, uint32_t a, uint64_t ctr, uint64_t m, uint32_t lane) {
   if (a >= A) return CRDT_ENONCANON;
   uint64_t cur = 0;
   uint32_t cpos = 0;
@@ -265,7 +284,7 @@ __device__ int op_add(Ws& w, Cnt& c, bool sparse, uint32_t A, uint32_t a, uint64
   // entries[m] (inserted empty when absent) .witness(dot)
   uint32_t pos = count_less(w.key, 0u, c.mem, m, lane);
   if (pos >= c.mem || w.key[pos] != m) {
-    if (c.mem + 1u > kApMem) return CRDT_ECAPACITY;
+    if (c.mem + 1u > C::kMem) return CRDT_ECAPACITY;
     const uint32_t at = pos ? w.dend[pos - 1] : 0u;
     ins_gap(w.key, c.mem, pos, 1u, lane);
     ins_gap(w.dend, c.mem, pos, 1u, lane);
@@ -280,7 +299,7 @@ __device__ int op_add(Ws& w, Cnt& c, bool sparse, uint32_t A, uint32_t a, uint64
     if (lane == 0u && w.dctr[b + r] < ctr) w.dctr[b + r] = ctr;
     ap_sync();
   } else {
-    if (c.dot + 1u > kApDot) return CRDT_ECAPACITY;
+    if (c.dot + 1u > C::kDot) return CRDT_ECAPACITY;
     ins_gap(w.dact, c.dot, b + r, 1u, lane);
     ins_gap(w.dctr, c.dot, b + r, 1u, lane);
     if (lane == 0u) { w.dact[b + r] = a; w.dctr[b + r] = ctr; }
@@ -293,7 +312,7 @@ __device__ int op_add(Ws& w, Cnt& c, bool sparse, uint32_t A, uint32_t a, uint64
     if (cpos < c.clk && w.cact[cpos] == a) {
       if (lane == 0u) w.cctr[cpos] = ctr;
     } else {
-      if (c.clk + 1u > kApCk) return CRDT_ECAPACITY;
+      if (c.clk + 1u > C::kCk) return CRDT_ECAPACITY;
       ins_gap(w.cact, c.clk, cpos, 1u, lane);
       ins_gap(w.cctr, c.clk, cpos, 1u, lane);
       if (lane == 0u) { w.cact[cpos] = a; w.cctr[cpos] = ctr; }
@@ -308,7 +327,8 @@ __device__ int op_add(Ws& w, Cnt& c, bool sparse, uint32_t A, uint32_t a, uint64
 }
 
 // Op::Rm -> apply_remove (src/orswot.rs:195-211); the op clock is in tmp
-__device__ int op_rm(Ws& w, Cnt& c, bool sparse, uint64_t m, uint32_t lane) {
+template <class C>
+__device__ int op_rm(Ws<C>& w, Cnt& c, bool sparse, uint64_t m, uint32_t lane) {
   if (!tmp_le_clock(w, c, sparse, lane)) {
     const int rc = deferred_add(w, c, m, lane);
     if (rc) return rc;
@@ -326,126 +346,253 @@ __device__ bool rec_ok(const uint8_t* base, uint64_t bytes, uint64_t off, uint32
   return sz == h[0] && off + sz <= bytes;
 }
 
-__global__ __launch_bounds__(kAW) void orswot_apply_kernel(
-    const uint8_t* __restrict__ sb, uint64_t sbytes, const uint64_t* __restrict__ soff, uint64_t n_obj,
-    const uint64_t* __restrict__ obj_end, const uint32_t* __restrict__ kind, const uint64_t* __restrict__ member,
-    const uint32_t* __restrict__ actor, const uint64_t* __restrict__ counter, const uint64_t* __restrict__ clk_end,
-    const uint32_t* __restrict__ clk_act, const uint64_t* __restrict__ clk_ctr, uint32_t A, uint32_t flags,
-    uint8_t* __restrict__ out, uint64_t* __restrict__ ooff, uint64_t out_bytes, int* __restrict__ status) {
-  __shared__ Ws w;
-  const uint32_t lane = threadIdx.x;
+struct ApArgs {
+  const uint8_t* sb;
+  uint64_t sbytes;
+  const uint64_t* soff;
+  uint64_t n_obj;
+  const uint64_t* obj_end;
+  const uint32_t* kind;
+  const uint64_t* member;
+  const uint32_t* actor;
+  const uint64_t* counter;
+  const uint64_t* clk_end;
+  const uint32_t* clk_act;
+  const uint64_t* clk_ctr;
+  uint64_t n_ops, n_clk;  // sizes of the op arrays / of the clock-pair arrays
+  uint32_t A, flags;
+  uint8_t* out;
+  uint64_t* ooff;
+  uint64_t out_bytes;
+  int* status;
+  uint32_t* ctl;      // [0]: # objects left for the large workspace
+  uint64_t* list;     // their indices (list_cap of them; beyond that, out_off flags)
+  uint32_t list_cap;
+};
+
+__device__ __forceinline__ uint32_t ap_lane(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint64_t ap_lane64(uint64_t v, uint32_t l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);
+}
+// ops q0 .. min(q0 + 64, oe) - 1: lane i holds op q0 + i
+__device__ __forceinline__ void op_fetch(const ApArgs& g, uint64_t q0, uint64_t oe, uint32_t lane, uint32_t& rk,
+                                         uint64_t& rm, uint32_t& ra, uint64_t& rn, uint64_t& re) {
+  const uint64_t q = q0 + lane;
+  if (q < oe && q < g.n_ops) {
+    rk = g.kind[q];
+    rm = g.member[q];
+    ra = g.actor[q];
+    rn = g.counter[q];
+    re = g.clk_end[q];
+  }
+}
+
+// clock pairs c0 .. c0 + 127 (the first Rm clocks of an object): lane i holds
+// pairs c0 + i and c0 + 64 + i
+__device__ __forceinline__ void clk_fetch(const ApArgs& g, uint64_t c0, uint32_t lane, uint32_t& xa0, uint64_t& xc0,
+                                          uint32_t& xa1, uint64_t& xc1) {
+  if (c0 + lane < g.n_clk) { xa0 = g.clk_act[c0 + lane]; xc0 = g.clk_ctr[c0 + lane]; }
+  if (c0 + kAW + lane < g.n_clk) { xa1 = g.clk_act[c0 + kAW + lane]; xc1 = g.clk_ctr[c0 + kAW + lane]; }
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t j) {
+  return ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)j, kAW) << 32) |
+         (uint64_t)(uint32_t)__shfl((int)(uint32_t)v, (int)j, kAW);
+}
+
+// One object: unpack, run its ops in order, write the canonical record.
+template <class C>
+__device__ int apply_one(Ws<C>& w, const ApArgs& g, uint64_t o, uint32_t lane) {
+  const uint8_t* __restrict__ sb = g.sb;
+  const uint64_t sbytes = g.sbytes, out_bytes = g.out_bytes;
+  const uint64_t* __restrict__ soff = g.soff;
+  const uint64_t* __restrict__ obj_end = g.obj_end;
+  const uint64_t* __restrict__ clk_end = g.clk_end;
+  const uint32_t A = g.A, flags = g.flags;
+  uint8_t* __restrict__ out = g.out;
+  uint64_t* __restrict__ ooff = g.ooff;
   const bool sparse = (flags & kSparseClock) != 0u;
-  for (uint64_t o = blockIdx.x; o < n_obj; o += gridDim.x) {
-    const uint64_t so = soff[o];
-    const uint64_t ob = o ? obj_end[o - 1] : 0u, oe = obj_end[o];
-    const uint64_t cb = ob ? clk_end[ob - 1] : 0u;
-    const uint64_t oo = so + 32u * ob + 16u * cb + 32u * o;
-    if (lane == 0u) ooff[o] = oo;
-    int rc = 0;
-    if (!rec_ok(sb, sbytes, so, A, flags) || oe < ob) rc = CRDT_ENONCANON;
-    const uint8_t* r = sb + so;
-    const uint32_t* h = (const uint32_t*)r;
-    Cnt c{};
-    if (!rc) {
-      c = Cnt{ap_uni(h[1]), ap_uni(h[2]), ap_uni(h[3]), ap_uni(h[4]), ap_uni(h[5]), ap_uni(h[6]), 0u};
-      if (c.clk > kApCk || c.mem > kApMem || c.dot > kApDot || c.def > kApDef || c.fdot > kApFDot ||
-          c.fmem > kApFMem)
-        rc = CRDT_ECAPACITY;
+  const uint64_t so = soff[o];
+  const uint64_t ob = o ? obj_end[o - 1] : 0u, oe = obj_end[o];
+  const uint64_t cb = ob ? clk_end[ob - 1] : 0u;
+  const uint64_t oo = so + 32u * ob + 16u * cb + 32u * o;
+  if (lane == 0u) ooff[o] = oo;  // also clears a pending flag
+  // the object's first 64 ops -> registers (lane i: op ob + i), loaded
+  // together with the record so the op loop waits on no global load
+  uint32_t rk = 0, ra = 0;
+  uint64_t rm = 0, rn = 0, re = 0, pe = cb;
+  op_fetch(g, ob, oe, lane, rk, rm, ra, rn, re);
+  uint32_t xa0 = 0, xa1 = 0;
+  uint64_t xc0 = 0, xc1 = 0;
+  clk_fetch(g, cb, lane, xa0, xc0, xa1, xc1);
+  int rc = 0;
+  if (!rec_ok(sb, sbytes, so, A, flags) || oe < ob || oe > g.n_ops) rc = CRDT_ENONCANON;
+  const uint8_t* r = sb + so;
+  const uint32_t* h = (const uint32_t*)r;
+  Cnt c{};
+  if (!rc) {
+    c = Cnt{ap_uni(h[1]), ap_uni(h[2]), ap_uni(h[3]), ap_uni(h[4]), ap_uni(h[5]), ap_uni(h[6]), 0u};
+    if (c.clk > C::kCk || c.mem > C::kMem || c.dot > C::kDot || c.def > C::kDef || c.fdot > C::kFDot ||
+        c.fmem > C::kFMem)
+      rc = CRDT_ECAPACITY;
+  }
+  if (!rc) {  // unpack the record into the workspace
+    RecLayout L;
+    rec_layout(L, c.clk, c.mem, c.dot, c.def, c.fdot, c.fmem, sparse);
+    for (uint32_t i = lane; i < c.clk; i += kAW) {
+      w.cctr[i] = ((const uint64_t*)(r + L.o_clk))[i];
+      if (sparse) w.cact[i] = ((const uint32_t*)(r + L.o_cact))[i];
     }
-    if (!rc) {  // unpack the record into the workspace
-      RecLayout L;
-      rec_layout(L, c.clk, c.mem, c.dot, c.def, c.fdot, c.fmem, sparse);
-      for (uint32_t i = lane; i < c.clk; i += kAW) {
-        w.cctr[i] = ((const uint64_t*)(r + L.o_clk))[i];
-        if (sparse) w.cact[i] = ((const uint32_t*)(r + L.o_cact))[i];
-      }
-      for (uint32_t i = lane; i < c.mem; i += kAW) {
-        w.key[i] = ((const uint64_t*)(r + L.o_key))[i];
-        w.dend[i] = ((const uint32_t*)(r + L.o_mdend))[i];
-      }
-      for (uint32_t i = lane; i < c.dot; i += kAW) {
-        w.dctr[i] = ((const uint64_t*)(r + L.o_dctr))[i];
-        w.dact[i] = ((const uint32_t*)(r + L.o_dact))[i];
-      }
-      for (uint32_t i = lane; i < c.fdot; i += kAW) {
-        w.fctr[i] = ((const uint64_t*)(r + L.o_fctr))[i];
-        w.fact[i] = ((const uint32_t*)(r + L.o_fact))[i];
-      }
-      for (uint32_t i = lane; i < c.fmem; i += kAW) w.fkey[i] = ((const uint64_t*)(r + L.o_fkey))[i];
-      for (uint32_t i = lane; i < c.def; i += kAW) {
-        w.fdend[i] = ((const uint32_t*)(r + L.o_fdend))[i];
-        w.fmend[i] = ((const uint32_t*)(r + L.o_fmend))[i];
-      }
-      ap_sync();
-      bool big = false;
-      for (uint32_t i = lane; i < c.mem; i += kAW) big = big || w.dend[i] - (i ? w.dend[i - 1] : 0u) > 2u * kAW;
-      if (__ballot(big)) rc = CRDT_ECAPACITY;
+    for (uint32_t i = lane; i < c.mem; i += kAW) {
+      w.key[i] = ((const uint64_t*)(r + L.o_key))[i];
+      w.dend[i] = ((const uint32_t*)(r + L.o_mdend))[i];
     }
-    for (uint64_t q = ob; q < oe && !rc; ++q) {  // the object's ops, in order
-      const uint32_t k = ap_uni(kind[q]);
-      const uint64_t m = ap_uni64(member[q]);
-      if (k == CRDT_OP_ADD) {
-        rc = op_add(w, c, sparse, A, ap_uni(actor[q]), ap_uni64(counter[q]), m, lane);
-      } else if (k == CRDT_OP_RM) {
-        const uint64_t b = q ? clk_end[q - 1] : 0u, e = clk_end[q];
-        if (e < b || e - b > kApTmp) { rc = e < b ? CRDT_ENONCANON : CRDT_ECAPACITY; break; }
-        bool bad = false;
+    for (uint32_t i = lane; i < c.dot; i += kAW) {
+      w.dctr[i] = ((const uint64_t*)(r + L.o_dctr))[i];
+      w.dact[i] = ((const uint32_t*)(r + L.o_dact))[i];
+    }
+    for (uint32_t i = lane; i < c.fdot; i += kAW) {
+      w.fctr[i] = ((const uint64_t*)(r + L.o_fctr))[i];
+      w.fact[i] = ((const uint32_t*)(r + L.o_fact))[i];
+    }
+    for (uint32_t i = lane; i < c.fmem; i += kAW) w.fkey[i] = ((const uint64_t*)(r + L.o_fkey))[i];
+    for (uint32_t i = lane; i < c.def; i += kAW) {
+      w.fdend[i] = ((const uint32_t*)(r + L.o_fdend))[i];
+      w.fmend[i] = ((const uint32_t*)(r + L.o_fmend))[i];
+    }
+    ap_sync();
+    bool big = false;
+    for (uint32_t i = lane; i < c.mem; i += kAW) big = big || w.dend[i] - (i ? w.dend[i - 1] : 0u) > 2u * kAW;
+    if (__ballot(big)) rc = CRDT_ECAPACITY;
+  }
+  for (uint64_t q = ob; q < oe && !rc; ++q) {  // the object's ops, in order
+    const uint32_t qi = (uint32_t)(q - ob) & (kAW - 1u);
+    if (qi == 0u && q != ob) {
+      op_fetch(g, q, oe, lane, rk, rm, ra, rn, re);
+      pe = ap_uni64(clk_end[q - 1]);
+    }
+    const uint32_t k = ap_lane(rk, qi);
+    const uint64_t m = ap_lane64(rm, qi);
+    if (k == CRDT_OP_ADD) {
+      rc = op_add(w, c, sparse, A, ap_lane(ra, qi), ap_lane64(rn, qi), m, lane);
+      if (qi == kAW - 1u) pe = ap_lane64(re, qi);
+    } else if (k == CRDT_OP_RM) {
+      const uint64_t b = qi ? ap_lane64(re, qi - 1u) : pe, e = ap_lane64(re, qi);
+      if (qi == kAW - 1u) pe = e;
+      if (e < b || e - b > C::kTmp) { rc = e < b ? CRDT_ENONCANON : CRDT_ECAPACITY; break; }
+      if (e > g.n_clk) { rc = CRDT_ENONCANON; break; }
+      bool bad = false;
+      if (e - cb <= 2u * kAW) {  // the pairs are in registers (clk_fetch)
+        uint32_t xlast = 0;  // the previous pass's last actor
+        for (uint32_t base = 0; base < (uint32_t)(e - b); base += kAW) {
+          const uint32_t i = base + lane;
+          const uint32_t j = (uint32_t)(b - cb) + i;  // pair j of the object's first 128
+          const uint32_t jl = j & (kAW - 1u);
+          const uint32_t a0 = (uint32_t)__shfl((int)xa0, (int)jl, kAW), a1 = (uint32_t)__shfl((int)xa1, (int)jl, kAW);
+          const uint64_t c0 = shfl64(xc0, jl), c1 = shfl64(xc1, jl);
+          const uint32_t x = j < kAW ? a0 : a1;
+          const uint64_t v = j < kAW ? c0 : c1;
+          uint32_t xp = (uint32_t)__shfl((int)x, (int)((lane - 1u) & (kAW - 1u)), kAW);
+          if (lane == 0u) xp = xlast;
+          if (i < (uint32_t)(e - b)) {
+            bad = bad || x >= A || v == 0u || (i && xp >= x);  // canonical VClock
+            w.tact[i] = x;
+            w.tctr[i] = v;
+          }
+          xlast = (uint32_t)__shfl((int)x, (int)(kAW - 1u), kAW);
+        }
+      } else {
         for (uint32_t i = lane; i < (uint32_t)(e - b); i += kAW) {
-          const uint32_t x = clk_act[b + i];
-          const uint64_t v = clk_ctr[b + i];
-          bad = bad || x >= A || v == 0u || (i && clk_act[b + i - 1] >= x);  // canonical VClock
+          const uint32_t x = g.clk_act[b + i];
+          const uint64_t v = g.clk_ctr[b + i];
+          bad = bad || x >= A || v == 0u || (i && g.clk_act[b + i - 1] >= x);  // canonical VClock
           w.tact[i] = x;
           w.tctr[i] = v;
         }
-        c.tmp = (uint32_t)(e - b);
-        ap_sync();
-        if (__ballot(bad)) { rc = CRDT_ENONCANON; break; }
-        rc = op_rm(w, c, sparse, m, lane);
-      } else {
-        rc = CRDT_ENONCANON;
+      }
+      c.tmp = (uint32_t)(e - b);
+      ap_sync();
+      if (__ballot(bad)) { rc = CRDT_ENONCANON; break; }
+      rc = op_rm(w, c, sparse, m, lane);
+    } else {
+      rc = CRDT_ENONCANON;
+    }
+  }
+  if (!rc) {  // write the canonical record
+    uint32_t n_clk = c.clk;
+    RecLayout L;
+    rec_layout(L, n_clk, c.mem, c.dot, c.def, c.fdot, c.fmem, sparse);
+    if (oo + L.size > out_bytes || (oo & 15u)) {
+      rc = CRDT_ECAPACITY;
+    } else {
+      uint8_t* O = out + oo;
+      for (uint32_t i = lane; i < n_clk; i += kAW) {
+        ((uint64_t*)(O + L.o_clk))[i] = w.cctr[i];
+        if (sparse) ((uint32_t*)(O + L.o_cact))[i] = w.cact[i];
+      }
+      if (sparse && lane == 0u && (n_clk & 1u)) *(uint32_t*)(O + L.o_cact + 4u * n_clk) = 0u;
+      for (uint32_t i = lane; i < c.mem; i += kAW) {
+        ((uint64_t*)(O + L.o_key))[i] = w.key[i];
+        ((uint32_t*)(O + L.o_mdend))[i] = w.dend[i];
+      }
+      for (uint32_t i = lane; i < c.dot; i += kAW) {
+        ((uint64_t*)(O + L.o_dctr))[i] = w.dctr[i];
+        ((uint32_t*)(O + L.o_dact))[i] = w.dact[i];
+      }
+      for (uint32_t i = lane; i < c.fdot; i += kAW) {
+        ((uint64_t*)(O + L.o_fctr))[i] = w.fctr[i];
+        ((uint32_t*)(O + L.o_fact))[i] = w.fact[i];
+      }
+      for (uint32_t i = lane; i < c.fmem; i += kAW) ((uint64_t*)(O + L.o_fkey))[i] = w.fkey[i];
+      for (uint32_t i = lane; i < c.def; i += kAW) {
+        ((uint32_t*)(O + L.o_fdend))[i] = w.fdend[i];
+        ((uint32_t*)(O + L.o_fmend))[i] = w.fmend[i];
+      }
+      if (lane == 0u && L.o_def != L.o_mpad) *(uint32_t*)(O + L.o_mpad) = 0u;
+      if (lane >= 1u && lane < 4u && L.o_end + 4u * (lane - 1u) < L.size)
+        *(uint32_t*)(O + L.o_end + 4u * (lane - 1u)) = 0u;
+      if (lane == 0u) {
+        uint32_t* oh = (uint32_t*)O;
+        oh[0] = L.size; oh[1] = n_clk; oh[2] = c.mem; oh[3] = c.dot;
+        oh[4] = c.def; oh[5] = c.fdot; oh[6] = c.fmem; oh[7] = sparse ? kSparseClock : 0u;
       }
     }
-    if (!rc) {  // write the canonical record
-      uint32_t n_clk = c.clk;
-      RecLayout L;
-      rec_layout(L, n_clk, c.mem, c.dot, c.def, c.fdot, c.fmem, sparse);
-      if (oo + L.size > out_bytes || (oo & 15u)) {
-        rc = CRDT_ECAPACITY;
-      } else {
-        uint8_t* O = out + oo;
-        for (uint32_t i = lane; i < n_clk; i += kAW) {
-          ((uint64_t*)(O + L.o_clk))[i] = w.cctr[i];
-          if (sparse) ((uint32_t*)(O + L.o_cact))[i] = w.cact[i];
-        }
-        if (sparse && lane == 0u && (n_clk & 1u)) *(uint32_t*)(O + L.o_cact + 4u * n_clk) = 0u;
-        for (uint32_t i = lane; i < c.mem; i += kAW) {
-          ((uint64_t*)(O + L.o_key))[i] = w.key[i];
-          ((uint32_t*)(O + L.o_mdend))[i] = w.dend[i];
-        }
-        for (uint32_t i = lane; i < c.dot; i += kAW) {
-          ((uint64_t*)(O + L.o_dctr))[i] = w.dctr[i];
-          ((uint32_t*)(O + L.o_dact))[i] = w.dact[i];
-        }
-        for (uint32_t i = lane; i < c.fdot; i += kAW) {
-          ((uint64_t*)(O + L.o_fctr))[i] = w.fctr[i];
-          ((uint32_t*)(O + L.o_fact))[i] = w.fact[i];
-        }
-        for (uint32_t i = lane; i < c.fmem; i += kAW) ((uint64_t*)(O + L.o_fkey))[i] = w.fkey[i];
-        for (uint32_t i = lane; i < c.def; i += kAW) {
-          ((uint32_t*)(O + L.o_fdend))[i] = w.fdend[i];
-          ((uint32_t*)(O + L.o_fmend))[i] = w.fmend[i];
-        }
-        if (lane == 0u && L.o_def != L.o_mpad) *(uint32_t*)(O + L.o_mpad) = 0u;
-        if (lane >= 1u && lane < 4u && L.o_end + 4u * (lane - 1u) < L.size)
-          *(uint32_t*)(O + L.o_end + 4u * (lane - 1u)) = 0u;
-        if (lane == 0u) {
-          uint32_t* oh = (uint32_t*)O;
-          oh[0] = L.size; oh[1] = n_clk; oh[2] = c.mem; oh[3] = c.dot;
-          oh[4] = c.def; oh[5] = c.fdot; oh[6] = c.fmem; oh[7] = sparse ? kSparseClock : 0u;
+  }
+  return rc;
+}
+
+// SMALL: every object in the small workspace; one that outgrows it is listed
+// (and flagged in out_off) instead of failing. Otherwise the large workspace
+// over the listed objects, or over the flagged ones when the list overflowed.
+template <class C, bool SMALL>
+__global__ __launch_bounds__(kAW) void orswot_apply_kernel(ApArgs g) {
+  __shared__ Ws<C> w;
+  const uint32_t lane = threadIdx.x;
+  if (SMALL) {
+    for (uint64_t o = blockIdx.x; o < g.n_obj; o += gridDim.x) {
+      const int rc = apply_one<C>(w, g, o, lane);
+      if (rc && lane == 0u) {
+        if (rc == CRDT_ECAPACITY) {
+          g.ooff[o] |= kApPending;
+          const uint32_t e = atomicAdd(&g.ctl[0], 1u);
+          if (e < g.list_cap) g.list[e] = o;
+        } else {
+          atomicCAS(g.status, 0, rc);
         }
       }
+      ap_sync();
     }
-    if (rc && lane == 0u) atomicCAS(status, 0, rc);
+    return;
+  }
+  const uint32_t n = ap_uni(__hip_atomic_load(&g.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (n == 0u) return;
+  const bool listed = n <= g.list_cap;
+  const uint64_t m = listed ? n : g.n_obj;
+  for (uint64_t e = blockIdx.x; e < m; e += gridDim.x) {
+    const uint64_t o = listed ? ap_uni64(g.list[e]) : e;
+    if (!listed && !(ap_uni64(g.ooff[o]) & kApPending)) continue;
+    const int rc = apply_one<C>(w, g, o, lane);
+    if (rc && lane == 0u) atomicCAS(g.status, 0, rc);
     ap_sync();
   }
 }
@@ -455,15 +602,40 @@ __global__ __launch_bounds__(kAW) void orswot_apply_kernel(
 int launch_orswot_apply(const uint8_t* sb, uint64_t sbytes, const uint64_t* soff, uint64_t n_obj,
                         const uint64_t* obj_end, const uint32_t* kind, const uint64_t* member, const uint32_t* actor,
                         const uint64_t* counter, const uint64_t* clk_end, const uint32_t* clk_act,
-                        const uint64_t* clk_ctr, uint32_t A, uint32_t flags, uint8_t* out, uint64_t* ooff,
-                        uint64_t out_bytes, int* status, hipStream_t stream) {
+                        const uint64_t* clk_ctr, uint64_t n_ops, uint64_t n_clk, uint32_t A, uint32_t flags,
+                        uint8_t* out, uint64_t* ooff,
+                        uint64_t out_bytes, int* status, uint32_t* ctl, uint64_t* list, uint32_t list_cap,
+                        hipStream_t stream) {
   if (n_obj == 0) return CRDT_OK;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const uint64_t cap = (uint64_t)cus * 9u;
-  const uint32_t blocks = (uint32_t)(n_obj < cap ? n_obj : cap);
-  hipLaunchKernelGGL(orswot_apply_kernel, dim3(blocks), dim3(kAW), 0, stream, sb, sbytes, soff, n_obj, obj_end, kind,
-                     member, actor, counter, clk_end, clk_act, clk_ctr, A, flags, out, ooff, out_bytes, status);
+  static std::atomic<int> occ_small{0}, occ_big{0};
+  auto occ_of = [](std::atomic<int>& slot, const void* fn) {
+    int occ = slot.load(std::memory_order_relaxed);
+    if (occ == 0) {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kAW, 0) != hipSuccess || occ < 1) occ = 8;
+      slot.store(occ, std::memory_order_relaxed);
+    }
+    return (uint64_t)occ;
+  };
+  const void* fs = (const void*)orswot_apply_kernel<SmallCaps, true>;
+  const void* fb = (const void*)orswot_apply_kernel<BigCaps, false>;
+  ApArgs g{sb, sbytes, soff, n_obj, obj_end, kind, member, actor, counter, clk_end, clk_act, clk_ctr, n_ops, n_clk,
+           A, flags, out, ooff, out_bytes, status, ctl, list, list_cap};
+  void* args[] = {&g};
+  if (hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
+  const bool dense_big = !(flags & kSparseClock) && A > SmallCaps::kCk;  // nothing fits the small workspace
+  if (dense_big) {  // every object in the large workspace: the "list overflowed" path with all objects flagged
+    if (hipMemsetD32Async((hipDeviceptr_t)ctl, 0xFFFFFFFF, 1, stream) != hipSuccess) return CRDT_EHIP;
+    if (hipMemsetAsync(ooff, 0xFF, 8 * n_obj, stream) != hipSuccess) return CRDT_EHIP;
+  } else {
+    const uint64_t cap = (uint64_t)cus * occ_of(occ_small, fs);
+    const uint32_t blocks = (uint32_t)(n_obj < cap ? n_obj : cap);
+    if (hipLaunchKernel(fs, dim3(blocks), dim3(kAW), args, 0, stream) != hipSuccess) return CRDT_EHIP;
+  }
+  const uint64_t capb = (uint64_t)cus * occ_of(occ_big, fb);
+  const uint32_t bb = (uint32_t)(n_obj < capb ? n_obj : capb);
+  if (hipLaunchKernel(fb, dim3(bb), dim3(kAW), args, 0, stream) != hipSuccess) return CRDT_EHIP;
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 

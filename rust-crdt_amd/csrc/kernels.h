@@ -39,8 +39,10 @@ int launch_bincode_egest(const uint8_t* rb, uint64_t rbytes, const uint64_t* rof
 int launch_orswot_apply(const uint8_t* sb, uint64_t sbytes, const uint64_t* soff, uint64_t n_obj,
                         const uint64_t* obj_end, const uint32_t* kind, const uint64_t* member, const uint32_t* actor,
                         const uint64_t* counter, const uint64_t* clk_end, const uint32_t* clk_act,
-                        const uint64_t* clk_ctr, uint32_t A, uint32_t flags, uint8_t* out, uint64_t* ooff,
-                        uint64_t out_bytes, int* status, hipStream_t stream);
+                        const uint64_t* clk_ctr, uint64_t n_ops, uint64_t n_clk, uint32_t A, uint32_t flags,
+                        uint8_t* out, uint64_t* ooff,
+                        uint64_t out_bytes, int* status, uint32_t* ctl, uint64_t* list, uint32_t list_cap,
+                        hipStream_t stream);
 
 int launch_vclock_cmp(const uint64_t* a, const uint64_t* b, uint64_t n, uint32_t A, int8_t* out, hipStream_t stream);
 int launch_mvreg_merge(const uint32_t* sn, const uint64_t* sclk, const uint64_t* sval, uint32_t scap,

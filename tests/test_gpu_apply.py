@@ -129,3 +129,66 @@ def test_apply_malformed_ops(gpu):
                 [("rm", 5, [(1, 0)])]):                   # zero counter in a clock
         with pytest.raises(CrdtError):
             gpu.orswot_apply(B, crdts_hip.OrswotOps.from_lists([bad]))
+
+
+def _record(rng, A, n_mem, n_def=0, sparse=False):
+    """A canonical record with n_mem members (1-3 dots each, under the clock)
+    and n_def deferred removes with future clocks."""
+    acts = rng.sample(range(A), min(A, 24))
+    clock = {a: rng.randrange(3, 40) for a in acts}
+    entries = {}
+    for _ in range(n_mem):
+        dots = {a: rng.randrange(1, clock[a] + 1) for a in rng.sample(acts, rng.randrange(1, 4))}
+        entries[rng.getrandbits(64)] = dots
+    deferred = {}
+    for _ in range(n_def):
+        a = rng.choice(acts)
+        deferred[((a, clock[a] + 1 + rng.randrange(3)),)] = {rng.getrandbits(64) for _ in range(rng.randrange(1, 4))}
+    return records.encode(clock, entries, deferred, A, sparse=sparse)
+
+
+def test_apply_workspace_tiers(gpu, oracle):
+    """Objects that fit the small workspace, objects that start beyond it
+    (65..128 members, > 256 dots, > 16 deferred clocks) and objects that outgrow
+    it part way through their ops, mixed in one batch: the ones that do not fit
+    are redone from their input in the large workspace."""
+    rng = random.Random(11)
+    recs = []
+    for i in range(600):
+        k = i % 4
+        n_mem = [rng.randrange(0, 40), rng.randrange(65, 120), rng.randrange(58, 64), rng.randrange(20, 40)][k]
+        n_def = [rng.randrange(0, 3), rng.randrange(0, 3), 0, rng.randrange(17, 24)][k]
+        recs.append(_record(rng, 16, n_mem, n_def))
+    _run(gpu, oracle, recs, 16, 0, seed=12, max_ops=16)
+
+
+def test_apply_workspace_tiers_sparse(gpu, oracle):
+    rng = random.Random(13)
+    recs = [_record(rng, 1024, rng.choice([10, 62, 90]), rng.randrange(0, 3), sparse=True) for _ in range(400)]
+    _run(gpu, oracle, recs, 1024, crdts_hip_sparse(), seed=14, max_ops=12)
+
+
+def crdts_hip_sparse():
+    import crdts_hip
+
+    return crdts_hip.SPARSE_CLOCK
+
+
+def test_apply_list_overflow(gpu, oracle):
+    """More large-workspace objects than the context's object list holds:
+    the large pass finds them by their out_off flag instead."""
+    rng = random.Random(15)
+    recs = [_record(rng, 16, rng.choice([20, 80]), 1) for _ in range(300)]
+    gpu.set_list_cap(8)
+    try:
+        _run(gpu, oracle, recs, 16, 0, seed=16, max_ops=6)
+    finally:
+        gpu.set_list_cap(65536)
+
+
+def test_apply_dense_wide_clock(gpu, oracle):
+    """n_actors beyond the small workspace's dense clock: every object goes
+    straight to the large one."""
+    rng = random.Random(17)
+    recs = [_record(rng, 100, rng.randrange(0, 50), rng.randrange(0, 3)) for _ in range(300)]
+    _run(gpu, oracle, recs, 100, 0, seed=18, max_ops=8)
