@@ -41,7 +41,7 @@ def parse():
     p.add_argument("--threads", type=int, default=16, help="host threads (generation, CPU baseline)")
     p.add_argument("--cpu-sample", type=int, default=500_000, help="objects in the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r01d.json"),
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r01e.json"),
                    help="measured per-launch HBM bytes (rocprofv3 PMC) to report as roofline.traffic")
     p.add_argument("--blocks-per-cu", type=int, default=None)
     p.add_argument("--variant", type=int, default=None, help="Orswot kernel variant (tuning/diagnostics)")
@@ -99,6 +99,17 @@ def load_traffic(path, key):
             return json.load(f).get(key)
     except (OSError, ValueError):
         return None
+
+
+def wl_traffic(args, workload, *kernels):
+    """Per-launch HBM bytes of the workload's measured kernels from its
+    rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/profile_workload.sh +
+    tools/traffic.py -> profiles/traffic_r01e_<workload>.json), summed over the
+    kernels one measured launch runs; None off the profiled (default) size."""
+    if args.n_obj is not None:
+        return None
+    vals = [load_traffic(os.path.join(REPO, "profiles", f"traffic_r01e_{workload}.json"), k) for k in kernels]
+    return None if any(v is None for v in vals) else float(sum(vals))
 
 
 def run_orswot(args, rank, world, local):
@@ -256,7 +267,8 @@ def run_dense(args, rank, world, local, kind):
                    "n_actors": A, "parallelism": f"objects sharded over {world} GPU(s), no collective"},
         "roofline": {"bound": "hbm", "kernel": "dense_max_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "kernel_ms": kernel_ms,
-                     "alg_bytes_per_launch": alg, "traffic": load_traffic(args.traffic_json, "dense_max_kernel")},
+                     "alg_bytes_per_launch": alg,
+                     "traffic": wl_traffic(args, "gcounter", "dense_max_kernel") if kind == "gcounter" else None},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -361,7 +373,8 @@ def run_orswot_csr(args, rank, world, local):
         ach = alg / (ev_ms * 1e-3) / 1e9
         res["roofline"] = {"bound": "hbm", "kernel": "fold of 7 launches: orswot_sparse_mask_kernel + orswot_sparse_general_kernel", "achieved": ach,
                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                           "kernel_ms": ev_ms, "alg_bytes_per_launch": alg / (R - 1), "traffic": None}
+                           "kernel_ms": ev_ms, "alg_bytes_per_launch": alg / (R - 1),
+                           "traffic": wl_traffic(args, "orswot_csr", "orswot_sparse_mask_kernel", "orswot_sparse_general_kernel")}
         if not args.no_cpu_baseline:
             sys.path.insert(0, os.path.join(REPO, "tests"))
             import oracle_ffi
@@ -519,7 +532,8 @@ def run_bincode(args, rank, world, local):
         ach = alg_in / (ev_ms * 1e-3) / 1e9
         res["roofline"] = {"bound": "hbm", "kernel": "bincode_ingest_kernel (sizes + decode) + scan",
                            "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                           "kernel_ms": ev_ms, "alg_bytes_per_launch": alg_in, "traffic": None}
+                           "kernel_ms": ev_ms, "alg_bytes_per_launch": alg_in,
+                           "traffic": wl_traffic(args, "bincode", "bincode_sizes_lane_kernel", "bincode_decode_kernel")}
         if not args.no_cpu_baseline:
             sys.path.insert(0, os.path.join(REPO, "tests"))
             import oracle_ffi
@@ -664,8 +678,8 @@ def run_apply(args, rank, world, local):
     if world == 1:
         ach = alg / (ev_ms * 1e-3) / 1e9
         res["roofline"] = {"bound": "hbm", "kernel": "orswot_apply_kernel", "achieved": ach, "peak": HBM_PEAK_GBS,
-                           "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "kernel_ms": ev_ms,
-                           "alg_bytes_per_launch": alg, "traffic": None}
+                           "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "kernel_ms": ev_ms, "alg_bytes_per_launch": alg,
+                           "traffic": wl_traffic(args, "apply", "orswot_apply_kernel_true", "orswot_apply_kernel_false")}
         if not args.no_cpu_baseline:
             m = min(args.cpu_sample // 5, n)
             th = max(1, min(args.threads, os.cpu_count() or 1))
@@ -747,7 +761,7 @@ def run_mvreg(args, rank, world, local):
         ach = alg / (ev_ms * 1e-3) / 1e9
         res["roofline"] = {"bound": "hbm", "kernel": "mvreg_merge_kernel", "achieved": ach, "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "kernel_ms": ev_ms, "alg_bytes_per_launch": alg,
-                           "traffic": None}
+                           "traffic": wl_traffic(args, "mvreg", "mvreg_merge_kernel")}
         if not args.no_cpu_baseline:
             mm = 200_000
             hs = [t[:mm].cpu().numpy() for t in S]
@@ -812,7 +826,7 @@ def run_map(args, rank, world, local):
         ach = alg / (ev_ms * 1e-3) / 1e9
         res["roofline"] = {"bound": "hbm", "kernel": "map_mvreg_merge_kernel", "achieved": ach, "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "kernel_ms": ev_ms, "alg_bytes_per_launch": alg,
-                           "traffic": None}
+                           "traffic": wl_traffic(args, "map", "map_mvreg_merge_kernel")}
         if not args.no_cpu_baseline:
             mm = 20_000
             t0 = _t.perf_counter()

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round-end evidence: the headline profile (tools/profile.sh) plus per-workload
+# trace + traffic passes. Usage (repo root, on the box): bash tools/profile_all.sh <tag>
+set -euo pipefail
+TAG=${1:-r01e}
+bash tools/profile.sh $TAG
+for wl in apply orswot_csr bincode mvreg map gcounter; do
+  echo "profiling $wl"
+  bash tools/profile_workload.sh $TAG $wl
+done

@@ -8,9 +8,12 @@ section): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports
 half the bytes of a wide (16 B/lane) coalesced streaming read, so it is
 doubled; WRITE_SIZE reads exactly for 16-B-per-lane streaming stores.
 
-    python tools/traffic.py gpurun_out/prof_r01 profiles/r01
+    python tools/traffic.py gpurun_out/prof_r01 profiles/r01 [traffic tag]
 writes profiles/r01_kernel_stats.csv, profiles/r01_pmc.json and
-profiles/traffic_r01.json (the file bench.py reads for roofline.traffic).
+profiles/traffic_<tag>.json (default tag r01: the file bench.py reads for
+roofline.traffic). The 16-B streaming-read calibration is exact for the
+record-streaming kernels; for kernels with other access widths (the slab
+kernels' 8-B rows) the absolute is uncalibrated (guide) and the note says so.
 """
 import collections
 import csv
@@ -21,18 +24,29 @@ import sys
 
 KERNELS = {"orswot_merge_kernel": "orswot_mask_kernel<", "orswot_merge_kernel_v4": "orswot_merge_kernel<", "orswot_merge_general_kernel": "orswot_merge_general_kernel",
            "dense_max_kernel": "dense_max_kernel"}
+# every other kernel of the library is summarised under its own name
+OTHER = ("orswot_apply_kernel", "orswot_sparse_mask_kernel", "orswot_sparse_general_kernel", "bincode_ingest_kernel",
+         "bincode_egest_kernel", "bincode_decode_kernel", "bincode_sizes_lane_kernel", "mvreg_merge_kernel",
+         "vclock_cmp_kernel", "map_mvreg_merge_kernel", "validate_kernel", "sizes_kernel", "copy_kernel")
 
 
 def short(name):
     for k, pat in KERNELS.items():
         if pat in name:
             return k
+    import re
+    for k in OTHER:  # whole identifier: mvreg_merge_kernel must not match map_mvreg_merge_kernel
+        if re.search(r"(?<![A-Za-z0-9_])" + k + r"(?![A-Za-z0-9_])", name):
+            # instantiations told apart by a trailing bool template argument
+            # (apply: small / large workspace; egest: two passes)
+            t = re.search(k + r"<.*(true|false)>\(", name)
+            return k + ("_" + t.group(1) if t else "")
     return None
 
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
-    tag = os.path.basename(dst)
+    tag = sys.argv[3] if len(sys.argv) > 3 else os.path.basename(dst)
     os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
     shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), dst + "_kernel_stats.csv")
     per = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -50,8 +64,10 @@ def main():
         if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
             rd = 2.0 * cs["FETCH_SIZE"] * 1024.0
             wr = cs["WRITE_SIZE"] * 1024.0
-            traffic[k] = {"read_bytes": rd, "write_bytes": wr, "total_bytes": rd + wr,
-                          "note": "per launch; FETCH_SIZE x2 (gfx950 16-B streaming-read correction), KiB->B"}
+            note = "per launch; FETCH_SIZE x2 (gfx950 16-B streaming-read correction), KiB->B"
+            if k.startswith(("mvreg_merge_kernel", "map_mvreg_merge_kernel", "vclock_cmp_kernel", "orswot_apply_kernel")):
+                note += "; 8-B/4-B accesses: absolute uncalibrated (MI355X_MICROARCH.md HBM section)"
+            traffic[k] = {"read_bytes": rd, "write_bytes": wr, "total_bytes": rd + wr, "note": note}
     json.dump({"pmc_avg_per_launch": pmc, "source": src}, open(dst + "_pmc.json", "w"), indent=1)
     tdir = os.path.dirname(dst) or "."
     json.dump({k: v["total_bytes"] for k, v in traffic.items()} | {"detail": traffic},
