@@ -196,10 +196,9 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
             ++nout;
           }
           if (lane == 0u) R.mv_n[ir] = nout;
-          for (uint32_t z = nout; z < R.mcap; ++z) {
-            if (lane < A) R.mv_clock[(ir * R.mcap + z) * A + lane] = 0ull;
-            if (lane == 0u) R.mv_val[ir * R.mcap + z] = 0ull;
-          }
+          // unused value slots: zero, all lanes over the flat tail
+          for (uint64_t e = (ir * R.mcap + nout) * A + lane; e < (ir + 1u) * R.mcap * A; e += kMpW) R.mv_clock[e] = 0ull;
+          for (uint64_t e = ir * R.mcap + nout + lane; e < (ir + 1u) * R.mcap; e += kMpW) R.mv_val[e] = 0ull;
           ++nk;
         }
       }
@@ -207,14 +206,12 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
       if (hs) ++a;
       if (ho) ++b;
     }
-    for (uint32_t z = nk; z < R.kcap; ++z) {  // unused key slots: zero
-      const uint64_t ir = i * R.kcap + z;
-      if (lane == 0u) { R.keys[ir] = 0ull; R.mv_n[ir] = 0u; }
-      if (lane < A) R.eclock[ir * A + lane] = 0ull;
-      for (uint32_t q = 0; q < R.mcap; ++q) {
-        if (lane < A) R.mv_clock[(ir * R.mcap + q) * A + lane] = 0ull;
-        if (lane == 0u) R.mv_val[ir * R.mcap + q] = 0ull;
-      }
+    {  // unused key slots: zero, all lanes over each array's flat tail
+      const uint64_t k0 = i * R.kcap + nk, k1 = (i + 1u) * R.kcap;
+      for (uint64_t e = k0 + lane; e < k1; e += kMpW) { R.keys[e] = 0ull; R.mv_n[e] = 0u; }
+      for (uint64_t e = k0 * A + lane; e < k1 * A; e += kMpW) R.eclock[e] = 0ull;
+      for (uint64_t e = k0 * R.mcap * A + lane; e < k1 * R.mcap * A; e += kMpW) R.mv_clock[e] = 0ull;
+      for (uint64_t e = k0 * R.mcap + lane; e < k1 * R.mcap; e += kMpW) R.mv_val[e] = 0ull;
     }
     if (lane == 0u) R.n_keys[i] = nk;
     if (lane < A) R.clock[i * A + lane] = cM;
@@ -248,11 +245,11 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
       over = over || __builtin_amdgcn_readfirstlane(cnt) > R.scap;
       ++nd;
     }
-    for (uint32_t z = nd; z < R.dcap; ++z) {
-      const uint64_t dr = i * R.dcap + z;
-      if (lane < A) R.dclock[dr * A + lane] = 0ull;
-      if (lane == 0u) R.dset_n[dr] = 0u;
-      for (uint32_t q = lane; q < R.scap; q += kMpW) R.dset[dr * R.scap + q] = 0ull;
+    {  // unused deferred slots: zero, flat tails
+      const uint64_t d0 = i * R.dcap + nd, d1 = (i + 1u) * R.dcap;
+      for (uint64_t e = d0 + lane; e < d1; e += kMpW) R.dset_n[e] = 0u;
+      for (uint64_t e = d0 * A + lane; e < d1 * A; e += kMpW) R.dclock[e] = 0ull;
+      for (uint64_t e = d0 * R.scap + lane; e < d1 * R.scap; e += kMpW) R.dset[e] = 0ull;
     }
     if (lane == 0u) R.n_def[i] = nd;
     if (over && lane == 0u) atomicCAS(status, 0, CRDT_ECAPACITY);
@@ -267,7 +264,7 @@ int launch_map_mvreg_merge(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_sl
   if (n_obj == 0) return CRDT_OK;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const uint64_t cap = (uint64_t)cus * 16u;
+  const uint64_t cap = (uint64_t)cus * 28u;  // 7 single-wave blocks per SIMD (61 VGPRs)
   const uint32_t blocks = (uint32_t)(n_obj < cap ? n_obj : cap);
   hipLaunchKernelGGL(map_mvreg_merge_kernel, dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A, status);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;

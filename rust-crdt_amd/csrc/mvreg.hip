@@ -66,20 +66,26 @@ __device__ __forceinline__ uint32_t row_flags(const uint64_t* p, const uint64_t*
   return f;
 }
 
-// One wave per object; self / other clocks staged in LDS (dynamic shared
-// memory: (scap + ocap) * A u64 + the S x O and O x O flag matrices).
-__global__ __launch_bounds__(kMW) void mvreg_merge_kernel(
+// One wave per object, W waves per block, each with its own LDS region
+// (dynamic shared memory, `per_wave` bytes: the self / other clock rows, the
+// S x O and O x O flag matrices, the output slot table). Output rows are
+// written slot-major in one coalesced pass: lane l of the wave writes u64
+// l, l + 64, ... of the object's [outcap][A] block, its source row read from
+// the slot table (kept self rows first, then kept other rows, order kept).
+__global__ __launch_bounds__(256) void mvreg_merge_kernel(
     const uint32_t* __restrict__ sn, const uint64_t* __restrict__ sclk, const uint64_t* __restrict__ sval, uint32_t scap,
     const uint32_t* __restrict__ on, const uint64_t* __restrict__ oclk, const uint64_t* __restrict__ oval, uint32_t ocap,
     uint32_t* __restrict__ outn, uint64_t* __restrict__ outclk, uint64_t* __restrict__ outval, uint32_t outcap,
-    uint64_t n_obj, uint32_t A, int* __restrict__ status) {
+    uint64_t n_obj, uint32_t A, uint32_t per_wave, int* __restrict__ status) {
   extern __shared__ uint64_t mv_s[];
-  uint64_t* S = mv_s;
-  uint64_t* O = mv_s + (size_t)scap * A;
+  const uint32_t lane = threadIdx.x & (kMW - 1u), wave = threadIdx.x / kMW, W = blockDim.x / kMW;
+  uint64_t* S = mv_s + (size_t)wave * (per_wave / 8u);
+  uint64_t* O = S + (size_t)scap * A;
   uint8_t* fso = (uint8_t*)(O + (size_t)ocap * A);  // [scap][ocap]
   uint8_t* foo = fso + scap * ocap;                   // [ocap][ocap]
-  const uint32_t lane = threadIdx.x;
-  for (uint64_t o = blockIdx.x; o < n_obj; o += gridDim.x) {
+  uint8_t* tab = foo + ocap * ocap;                   // [outcap]: output slot -> source row (64 + j: other j)
+  const uint32_t AO = outcap * A;
+  for (uint64_t o = (uint64_t)blockIdx.x * W + wave; o < n_obj; o += (uint64_t)gridDim.x * W) {
     const uint32_t ns = __builtin_amdgcn_readfirstlane(sn[o]), no = __builtin_amdgcn_readfirstlane(on[o]);
     if (ns > scap || no > ocap) {
       if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
@@ -119,26 +125,26 @@ __global__ __launch_bounds__(kMW) void mvreg_merge_kernel(
     }
     const uint32_t rs = __builtin_amdgcn_mbcnt_hi((uint32_t)(KS >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)KS, 0u));
     const uint32_t ro = nks + __builtin_amdgcn_mbcnt_hi((uint32_t)(KO >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)KO, 0u));
-    // every output slot: its source row (or zeros for an unused slot)
+    if (ks) tab[rs] = (uint8_t)lane;
+    if (ko) tab[ro] = (uint8_t)(64u + lane);
     if (lane == 0u) outn[o] = nk;
-    uint64_t* oc = outclk + o * (uint64_t)outcap * A;
     if (ks) outval[o * outcap + rs] = sval[o * scap + lane];
     if (ko) outval[o * outcap + ro] = oval[o * ocap + lane];
     for (uint32_t k = nk + lane; k < outcap; k += kMW) outval[o * outcap + k] = 0u;
-    for (uint32_t k = 0; k < outcap; ++k) {
-      int src = -1;  // wave-uniform: which kept row lands in slot k
-      uint32_t m = k;
-      if (k < nks) {
-        uint64_t t = KS;
-        for (uint32_t q = 0; q < m; ++q) t &= t - 1ull;
-        src = (int)__builtin_ctzll(t);
-      } else if (k < nk) {
-        uint64_t t = KO;
-        for (uint32_t q = 0; q < m - nks; ++q) t &= t - 1ull;
-        src = 64 + (int)__builtin_ctzll(t);
+    mv_sync();
+    uint64_t* oc = outclk + o * (uint64_t)AO;
+    uint32_t k = lane / A, x = lane % A;  // slot and actor of this lane's first element
+    const uint32_t dk = kMW / A, dx = kMW % A;  // per step of 64 elements
+    for (uint32_t e = lane; e < AO; e += kMW) {
+      uint64_t v = 0ull;
+      if (k < nk) {
+        const uint32_t src = tab[k];
+        v = src < 64u ? S[src * A + x] : O[(src - 64u) * A + x];
       }
-      const uint64_t* row = src < 0 ? nullptr : src < 64 ? S + (uint32_t)src * A : O + (uint32_t)(src - 64) * A;
-      for (uint32_t x = lane; x < A; x += kMW) oc[(uint64_t)k * A + x] = row ? row[x] : 0ull;
+      oc[e] = v;
+      k += dk;
+      x += dx;
+      if (x >= A) { x -= A; ++k; }
     }
   }
 }
@@ -162,14 +168,17 @@ int launch_mvreg_merge(const uint32_t* sn, const uint64_t* sclk, const uint64_t*
                        uint64_t* outclk, uint64_t* outval, uint32_t outcap, uint64_t n_obj, uint32_t A, int* status,
                        hipStream_t stream) {
   if (n_obj == 0) return CRDT_OK;
-  const size_t lds = 8ull * (scap + ocap) * A + (size_t)scap * ocap + (size_t)ocap * ocap + 16u;
-  if (lds > 60u * 1024u || scap > 64u || ocap > 64u) return CRDT_EINVAL;
+  // per-wave LDS: clock rows, flag matrices, slot table; 16-B multiple
+  const size_t per_wave = (8ull * (scap + ocap) * A + (size_t)scap * ocap + (size_t)ocap * ocap + outcap + 15u) & ~15ull;
+  if (per_wave > 60u * 1024u || scap > 64u || ocap > 64u) return CRDT_EINVAL;
+  uint32_t W = 4;  // waves per block, as many as 60 KB of LDS allow
+  while (W > 1u && W * per_wave > 60u * 1024u) --W;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const uint64_t cap = (uint64_t)cus * 16u;
-  const uint32_t blocks = (uint32_t)(n_obj < cap ? n_obj : cap);
-  hipLaunchKernelGGL(mvreg_merge_kernel, dim3(blocks), dim3(kMW), lds, stream, sn, sclk, sval, scap, on, oclk, oval,
-                     ocap, outn, outclk, outval, outcap, n_obj, A, status);
+  const uint64_t want = (n_obj + W - 1) / W, cap = (uint64_t)cus * (32u / W);  // ~8 waves per SIMD
+  const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
+  hipLaunchKernelGGL(mvreg_merge_kernel, dim3(blocks), dim3(kMW * W), W * per_wave, stream, sn, sclk, sval, scap, on,
+                     oclk, oval, ocap, outn, outclk, outval, outcap, n_obj, A, (uint32_t)per_wave, status);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 
