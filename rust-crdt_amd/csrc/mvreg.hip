@@ -56,16 +56,6 @@ __global__ __launch_bounds__(256) void vclock_cmp_kernel(const uint64_t* __restr
   }
 }
 
-// per-lane: compare two dense rows in LDS: bit0 = some x with p > q, bit1 = some x with p < q
-__device__ __forceinline__ uint32_t row_flags(const uint64_t* p, const uint64_t* q, uint32_t A) {
-  uint32_t f = 0;
-  for (uint32_t x = 0; x < A; ++x) {
-    const uint64_t u = p[x], v = q[x];
-    f |= (u > v ? 1u : 0u) | (u < v ? 2u : 0u);
-  }
-  return f;
-}
-
 // One wave per object, W waves per block, each with its own LDS region
 // (dynamic shared memory, `per_wave` bytes: the self / other clock rows, the
 // S x O and O x O flag matrices, the output slot table). Output rows are
@@ -85,20 +75,79 @@ __global__ __launch_bounds__(256) void mvreg_merge_kernel(
   uint8_t* foo = fso + scap * ocap;                   // [ocap][ocap]
   uint8_t* tab = foo + ocap * ocap;                   // [outcap]: output slot -> source row (64 + j: other j)
   const uint32_t AO = outcap * A;
-  for (uint64_t o = (uint64_t)blockIdx.x * W + wave; o < n_obj; o += (uint64_t)gridDim.x * W) {
-    const uint32_t ns = __builtin_amdgcn_readfirstlane(sn[o]), no = __builtin_amdgcn_readfirstlane(on[o]);
+  // Software pipeline: the next register pair's slot counts and the first 64
+  // u64 of each side's clock slab (every capacity slot, used or not: the
+  // count is not known yet) are loaded while this pair is merged.
+  const uint64_t stride = (uint64_t)gridDim.x * W;
+  const uint32_t pfS = scap * A < kMW ? scap * A : kMW, pfO = ocap * A < kMW ? ocap * A : kMW;
+  uint32_t nsn = 0, non = 0;
+  uint64_t nS = 0, nO = 0, nVs = 0, nVo = 0;  // clock elements; values (lane < cap)
+  uint64_t o = (uint64_t)blockIdx.x * W + wave;
+  if (o < n_obj) {
+    nsn = sn[o];
+    non = on[o];
+    if (lane < scap) nVs = sval[o * scap + lane];
+    if (lane < ocap) nVo = oval[o * ocap + lane];
+    if (lane < pfS) nS = sclk[o * scap * A + lane];
+    if (lane < pfO) nO = oclk[o * ocap * A + lane];
+  }
+  for (; o < n_obj; o += stride) {
+    const uint32_t ns = __builtin_amdgcn_readfirstlane(nsn), no = __builtin_amdgcn_readfirstlane(non);
+    const uint64_t cS = nS, cO = nO, cVs = nVs, cVo = nVo;
+    if (o + stride < n_obj) {
+      const uint64_t u = o + stride;
+      nsn = sn[u];
+      non = on[u];
+      if (lane < scap) nVs = sval[u * scap + lane];
+      if (lane < ocap) nVo = oval[u * ocap + lane];
+      if (lane < pfS) nS = sclk[u * scap * A + lane];
+      if (lane < pfO) nO = oclk[u * ocap * A + lane];
+    }
     if (ns > scap || no > ocap) {
       if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
       continue;
     }
     mv_sync();
-    for (uint32_t k = lane; k < ns * A; k += kMW) S[k] = sclk[o * scap * A + k];
-    for (uint32_t k = lane; k < no * A; k += kMW) O[k] = oclk[o * ocap * A + k];
+    if (lane < ns * A) S[lane] = cS;
+    if (lane < no * A) O[lane] = cO;
+    for (uint32_t k = kMW + lane; k < ns * A; k += kMW) S[k] = sclk[o * scap * A + k];
+    for (uint32_t k = kMW + lane; k < no * A; k += kMW) O[k] = oclk[o * ocap * A + k];
     mv_sync();
-    for (uint32_t p = lane; p < ns * no; p += kMW) fso[p] = (uint8_t)row_flags(S + (p / no) * A, O + (p % no) * A, A);
-    for (uint32_t p = lane; p < no * no; p += kMW) {
-      const uint32_t j = p / no, jj = p % no;
-      foo[p] = jj < j ? (uint8_t)row_flags(O + jj * A, O + j * A, A) : (uint8_t)3u;
+    {  // flag matrices: G lanes per clock pair (G | 64, wave-uniform), strided over the actors, OR-reduced
+      const uint32_t P1 = ns * no, P = P1 + no * no;
+      uint32_t G = 1;
+      while (G < kMW && 2u * G * P <= kMW && 2u * G <= A) G *= 2u;
+      const uint32_t lg = 31u - __builtin_clz(G);
+      for (uint32_t base = 0; base < P * G; base += kMW) {
+        const uint32_t id = base + lane, p = id >> lg, gl = id & (G - 1u);
+        uint32_t f = 3u;  // O x O entries on or above the diagonal are never read as "equal"
+        if (p < P) {
+          const uint64_t* pa = nullptr;
+          const uint64_t* pb = nullptr;
+          if (p < P1) {
+            pa = S + (p / no) * A;
+            pb = O + (p % no) * A;
+          } else {
+            const uint32_t q = p - P1, j = q / no, jj = q % no;
+            if (jj < j) {
+              pa = O + jj * A;
+              pb = O + j * A;
+            }
+          }
+          if (pa) {
+            f = 0u;
+            for (uint32_t x = gl; x < A; x += G) {
+              const uint64_t u = pa[x], v = pb[x];
+              f |= (u > v ? 1u : 0u) | (u < v ? 2u : 0u);
+            }
+          }
+        }
+        for (uint32_t off = 1; off < G; off <<= 1) f |= (uint32_t)__shfl_xor((int)f, (int)off, kMW);
+        if (p < P && gl == 0u) {
+          if (p < P1) fso[p] = (uint8_t)f;
+          else foo[p - P1] = (uint8_t)f;
+        }
+      }
     }
     mv_sync();
     // self i: kept unless some other clock strictly dominates it (flags == "only <")
@@ -128,8 +177,8 @@ __global__ __launch_bounds__(256) void mvreg_merge_kernel(
     if (ks) tab[rs] = (uint8_t)lane;
     if (ko) tab[ro] = (uint8_t)(64u + lane);
     if (lane == 0u) outn[o] = nk;
-    if (ks) outval[o * outcap + rs] = sval[o * scap + lane];
-    if (ko) outval[o * outcap + ro] = oval[o * ocap + lane];
+    if (ks) outval[o * outcap + rs] = cVs;
+    if (ko) outval[o * outcap + ro] = cVo;
     for (uint32_t k = nk + lane; k < outcap; k += kMW) outval[o * outcap + k] = 0u;
     mv_sync();
     uint64_t* oc = outclk + o * (uint64_t)AO;
