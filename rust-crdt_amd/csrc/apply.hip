@@ -337,6 +337,23 @@ __device__ int op_rm(Ws<C>& w, Cnt& c, bool sparse, uint64_t m, uint32_t lane) {
   return 0;
 }
 
+// Wave-uniform read of an input that no kernel of the launch writes, through
+// the constant address space: the compiler emits a scalar (SMEM) load, whose
+// wait (lgkmcnt) does not also wait for this wave's earlier vector stores, as
+// a vector load's vmcnt wait would (the counter drains in order).
+template <class T>
+__device__ __forceinline__ T ldc(const T* p) {
+  return *(const __attribute__((address_space(4))) T*)p;
+}
+
+// the record header (8 u32, already read) is consistent with the record's bounds
+__device__ bool rec_ok_h(const uint32_t (&h)[8], uint64_t bytes, uint64_t off, uint32_t A, uint32_t flags) {
+  const bool sparse = (flags & kSparseClock) != 0u;
+  if (h[7] != flags || (sparse ? h[1] > A : h[1] != A)) return false;
+  const uint64_t sz = record_size64(h[1], h[2], h[3], h[4], h[5], h[6], sparse);
+  return sz == h[0] && off + sz <= bytes;
+}
+
 __device__ bool rec_ok(const uint8_t* base, uint64_t bytes, uint64_t off, uint32_t A, uint32_t flags) {
   if ((off & 15u) || off + kHdrBytes > bytes) return false;
   const uint32_t* h = (const uint32_t*)(base + off);
@@ -412,9 +429,16 @@ __device__ int apply_one(Ws<C>& w, const ApArgs& g, uint64_t o, uint32_t lane) {
   uint8_t* __restrict__ out = g.out;
   uint64_t* __restrict__ ooff = g.ooff;
   const bool sparse = (flags & kSparseClock) != 0u;
-  const uint64_t so = soff[o];
-  const uint64_t ob = o ? obj_end[o - 1] : 0u, oe = obj_end[o];
-  const uint64_t cb = ob ? clk_end[ob - 1] : 0u;
+  const uint64_t so = ldc(soff + o);
+  const uint64_t ob = o ? ldc(obj_end + o - 1) : 0u, oe = ldc(obj_end + o);
+  const uint64_t cb = ob ? ldc(clk_end + ob - 1) : 0u;
+  uint32_t h[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};  // the record header, by scalar loads
+  const bool hdr_in = (so & 15u) == 0u && so + kHdrBytes <= sbytes;
+  if (hdr_in) {
+    const uint32_t* hp = (const uint32_t*)(sb + so);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = ldc(hp + k);
+  }
   const uint64_t oo = so + 32u * ob + 16u * cb + 32u * o;
   if (lane == 0u) ooff[o] = oo;  // also clears a pending flag
   // the object's first 64 ops -> registers (lane i: op ob + i), loaded
@@ -426,9 +450,8 @@ __device__ int apply_one(Ws<C>& w, const ApArgs& g, uint64_t o, uint32_t lane) {
   uint64_t xc0 = 0, xc1 = 0;
   clk_fetch(g, cb, lane, xa0, xc0, xa1, xc1);
   int rc = 0;
-  if (!rec_ok(sb, sbytes, so, A, flags) || oe < ob || oe > g.n_ops) rc = CRDT_ENONCANON;
+  if (!hdr_in || !rec_ok_h(h, sbytes, so, A, flags) || oe < ob || oe > g.n_ops) rc = CRDT_ENONCANON;
   const uint8_t* r = sb + so;
-  const uint32_t* h = (const uint32_t*)r;
   Cnt c{};
   if (!rc) {
     c = Cnt{ap_uni(h[1]), ap_uni(h[2]), ap_uni(h[3]), ap_uni(h[4]), ap_uni(h[5]), ap_uni(h[6]), 0u};
