@@ -462,24 +462,46 @@ __device__ int apply_one(Ws<C>& w, const ApArgs& g, uint64_t o, uint32_t lane) {
   if (!rc) {  // unpack the record into the workspace
     RecLayout L;
     rec_layout(L, c.clk, c.mem, c.dot, c.def, c.fdot, c.fmem, sparse);
-    for (uint32_t i = lane; i < c.clk; i += kAW) {
+    // element `lane` of every section first: all loads in flight together, one
+    // wait, then the workspace stores (the rest, past 64, after)
+    {
+      const uint32_t i = lane;
+      uint64_t v0 = 0, v1 = 0, v2 = 0, v3 = 0, v4 = 0;
+      uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0, u4 = 0, u5 = 0;
+      if (i < c.clk) {
+        v0 = ((const uint64_t*)(r + L.o_clk))[i];
+        if (sparse) u0 = ((const uint32_t*)(r + L.o_cact))[i];
+      }
+      if (i < c.mem) { v1 = ((const uint64_t*)(r + L.o_key))[i]; u1 = ((const uint32_t*)(r + L.o_mdend))[i]; }
+      if (i < c.dot) { v2 = ((const uint64_t*)(r + L.o_dctr))[i]; u2 = ((const uint32_t*)(r + L.o_dact))[i]; }
+      if (i < c.fdot) { v3 = ((const uint64_t*)(r + L.o_fctr))[i]; u3 = ((const uint32_t*)(r + L.o_fact))[i]; }
+      if (i < c.fmem) v4 = ((const uint64_t*)(r + L.o_fkey))[i];
+      if (i < c.def) { u4 = ((const uint32_t*)(r + L.o_fdend))[i]; u5 = ((const uint32_t*)(r + L.o_fmend))[i]; }
+      if (i < c.clk) { w.cctr[i] = v0; if (sparse) w.cact[i] = u0; }
+      if (i < c.mem) { w.key[i] = v1; w.dend[i] = u1; }
+      if (i < c.dot) { w.dctr[i] = v2; w.dact[i] = u2; }
+      if (i < c.fdot) { w.fctr[i] = v3; w.fact[i] = u3; }
+      if (i < c.fmem) w.fkey[i] = v4;
+      if (i < c.def) { w.fdend[i] = u4; w.fmend[i] = u5; }
+    }
+    for (uint32_t i = kAW + lane; i < c.clk; i += kAW) {
       w.cctr[i] = ((const uint64_t*)(r + L.o_clk))[i];
       if (sparse) w.cact[i] = ((const uint32_t*)(r + L.o_cact))[i];
     }
-    for (uint32_t i = lane; i < c.mem; i += kAW) {
+    for (uint32_t i = kAW + lane; i < c.mem; i += kAW) {
       w.key[i] = ((const uint64_t*)(r + L.o_key))[i];
       w.dend[i] = ((const uint32_t*)(r + L.o_mdend))[i];
     }
-    for (uint32_t i = lane; i < c.dot; i += kAW) {
+    for (uint32_t i = kAW + lane; i < c.dot; i += kAW) {
       w.dctr[i] = ((const uint64_t*)(r + L.o_dctr))[i];
       w.dact[i] = ((const uint32_t*)(r + L.o_dact))[i];
     }
-    for (uint32_t i = lane; i < c.fdot; i += kAW) {
+    for (uint32_t i = kAW + lane; i < c.fdot; i += kAW) {
       w.fctr[i] = ((const uint64_t*)(r + L.o_fctr))[i];
       w.fact[i] = ((const uint32_t*)(r + L.o_fact))[i];
     }
-    for (uint32_t i = lane; i < c.fmem; i += kAW) w.fkey[i] = ((const uint64_t*)(r + L.o_fkey))[i];
-    for (uint32_t i = lane; i < c.def; i += kAW) {
+    for (uint32_t i = kAW + lane; i < c.fmem; i += kAW) w.fkey[i] = ((const uint64_t*)(r + L.o_fkey))[i];
+    for (uint32_t i = kAW + lane; i < c.def; i += kAW) {
       w.fdend[i] = ((const uint32_t*)(r + L.o_fdend))[i];
       w.fmend[i] = ((const uint32_t*)(r + L.o_fmend))[i];
     }
