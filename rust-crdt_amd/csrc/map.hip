@@ -63,11 +63,19 @@ __device__ __forceinline__ bool set_has(const uint64_t* set, uint32_t n, uint64_
   return __ballot(f) != 0ull;
 }
 
+// VS: each key's value clock rows (both sides) are staged in LDS with one
+// load per lane per side before the MVReg merge / truncate reads them (the
+// launcher picks VS when mcap * A <= kVsRows on both sides); otherwise every
+// row read in the dominance loops is its own dependent global load.
+constexpr uint32_t kVsRows = 128;  // u64 per side
+
+template <bool VS>
 __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_slab S, crdt_map_mvreg_slab O,
                                                                crdt_map_mvreg_slab R, uint64_t n_obj, uint32_t A,
                                                                int* __restrict__ status) {
   __shared__ uint32_t comb[kMpComb];     // (self deferred idx + 1) | (other deferred idx + 1) << 8
   __shared__ uint32_t vals[kMpVals];     // kept value slots of the key: side << 8 | slot
+  __shared__ uint64_t vr[2][VS ? kVsRows : 1];  // the key's value clock rows: self, other
   const uint32_t lane = threadIdx.x;
   for (uint64_t i = blockIdx.x; i < n_obj; i += gridDim.x) {
     const uint64_t cS = rowv(S.clock, i, A, lane), cO = rowv(O.clock, i, A, lane);
@@ -106,6 +114,29 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
       const uint64_t key = hs ? ka : kb;
       const uint64_t ia = i * S.kcap + a, ib = i * O.kcap + b;
       const uint64_t eS = hs ? rowv(S.eclock, ia, A, lane) : 0ull, eO = ho ? rowv(O.eclock, ib, A, lane) : 0ull;
+      if (VS) {  // stage the key's value rows: every load in flight, then the LDS stores
+        const uint32_t n0 = hs ? S.mcap * A : 0u, n1 = ho ? O.mcap * A : 0u;
+        uint64_t x0 = 0, x1 = 0, y0 = 0, y1 = 0;
+        if (lane < n0) x0 = S.mv_clock[ia * S.mcap * A + lane];
+        if (lane + kMpW < n0) x1 = S.mv_clock[ia * S.mcap * A + lane + kMpW];
+        if (lane < n1) y0 = O.mv_clock[ib * O.mcap * A + lane];
+        if (lane + kMpW < n1) y1 = O.mv_clock[ib * O.mcap * A + lane + kMpW];
+        mp_sync();  // the previous key's reads of the stage are done
+        if (lane < n0) vr[0][lane] = x0;
+        if (lane + kMpW < n0) vr[0][lane + kMpW] = x1;
+        if (lane < n1) vr[1][lane] = y0;
+        if (lane + kMpW < n1) vr[1][lane + kMpW] = y1;
+        mp_sync();
+      }
+      // value clock row v of this key on a side (lane = actor)
+      auto srow = [&](uint32_t v) -> uint64_t {
+        if (VS) return lane < A ? vr[0][v * A + lane] : 0ull;
+        return rowv(S.mv_clock, ia * S.mcap + v, A, lane);
+      };
+      auto orow = [&](uint32_t v) -> uint64_t {
+        if (VS) return lane < A ? vr[1][v * A + lane] : 0ull;
+        return rowv(O.mv_clock, ib * O.mcap + v, A, lane);
+      };
       uint64_t ec = 0, del = 0;
       bool keep;
       uint32_t nv = 0;
@@ -131,23 +162,22 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
         // MVReg::merge (src/mvreg.rs:121-153): self's undominated, then other's undominated and new
         const uint32_t ms = S.mv_n[ia] < S.mcap ? S.mv_n[ia] : S.mcap, mo = O.mv_n[ib] < O.mcap ? O.mv_n[ib] : O.mcap;
         for (uint32_t v = 0; v < ms; ++v) {
-          const uint64_t sv = rowv(S.mv_clock, ia * S.mcap + v, A, lane);
+          const uint64_t sv = srow(v);
           bool dom = false;
-          for (uint32_t w = 0; w < mo && !dom; ++w) dom = vstrict_less(sv, rowv(O.mv_clock, ib * O.mcap + w, A, lane));
+          for (uint32_t w = 0; w < mo && !dom; ++w) dom = vstrict_less(sv, orow(w));
           if (!dom) { if (lane == 0u) vals[nv] = v; ++nv; }
         }
         mp_sync();
         const uint32_t nkeep_s = nv;
         for (uint32_t w = 0; w < mo; ++w) {
-          const uint64_t ov = rowv(O.mv_clock, ib * O.mcap + w, A, lane);
+          const uint64_t ov = orow(w);
           bool dom = false;
-          for (uint32_t v = 0; v < ms && !dom; ++v) dom = vstrict_less(ov, rowv(S.mv_clock, ia * S.mcap + v, A, lane));
+          for (uint32_t v = 0; v < ms && !dom; ++v) dom = vstrict_less(ov, srow(v));
           if (dom) continue;
           bool dup = false;
           for (uint32_t q = 0; q < nv && !dup; ++q) {
             const uint32_t sl = vals[q];
-            const uint64_t kv = q < nkeep_s ? rowv(S.mv_clock, ia * S.mcap + (sl & 255u), A, lane)
-                                            : rowv(O.mv_clock, ib * O.mcap + (sl & 255u), A, lane);
+            const uint64_t kv = q < nkeep_s ? srow(sl & 255u) : orow(sl & 255u);
             dup = __ballot(kv != ov) == 0ull;
           }
           if (!dup) { if (lane == 0u) vals[nv] = 256u | w; ++nv; }
@@ -188,7 +218,7 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
             const uint32_t sl = vals[q];
             const bool fromO = sl >= 256u;
             const uint64_t src = fromO ? ib * O.mcap + (sl & 255u) : ia * S.mcap + (sl & 255u);
-            const uint64_t r = vsub(rowv(fromO ? O.mv_clock : S.mv_clock, src, A, lane), del);
+            const uint64_t r = vsub(fromO ? orow(sl & 255u) : srow(sl & 255u), del);
             if (!vany(r)) continue;
             if (nout >= R.mcap) { over = true; break; }
             if (lane < A) R.mv_clock[(ir * R.mcap + nout) * A + lane] = r;
@@ -264,9 +294,12 @@ int launch_map_mvreg_merge(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_sl
   if (n_obj == 0) return CRDT_OK;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const uint64_t cap = (uint64_t)cus * 28u;  // 7 single-wave blocks per SIMD (61 VGPRs)
+  const uint64_t cap = (uint64_t)cus * 28u;  // 7 single-wave blocks per SIMD
   const uint32_t blocks = (uint32_t)(n_obj < cap ? n_obj : cap);
-  hipLaunchKernelGGL(map_mvreg_merge_kernel, dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A, status);
+  if (S.mcap * A <= kVsRows && O.mcap * A <= kVsRows)
+    hipLaunchKernelGGL(map_mvreg_merge_kernel<true>, dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A, status);
+  else
+    hipLaunchKernelGGL(map_mvreg_merge_kernel<false>, dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A, status);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 
