@@ -108,7 +108,13 @@ def wl_traffic(args, workload, *kernels):
     kernels one measured launch runs; None off the profiled (default) size."""
     if args.n_obj is not None:
         return None
-    vals = [load_traffic(os.path.join(REPO, "profiles", f"traffic_r01e_{workload}.json"), k) for k in kernels]
+    path = os.path.join(REPO, "profiles", f"traffic_r01e_{workload}.json")
+    vals = []
+    for k in kernels:  # a templated kernel is keyed by its bool instantiation (tools/traffic.py)
+        v = load_traffic(path, k)
+        for suffix in ("_true", "_false"):
+            v = load_traffic(path, k + suffix) if v is None else v
+        vals.append(v)
     return None if any(v is None for v in vals) else float(sum(vals))
 
 
