@@ -35,16 +35,17 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="orswot",
-                   choices=["orswot", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply", "mvreg", "map"])
+                   choices=["orswot", "vclock", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply",
+                            "mvreg", "map"])
     p.add_argument("--replicas", type=int, default=8, help="orswot_csr at N=1: replicas folded locally")
     p.add_argument("--n-obj", type=int, default=None, help="objects per GPU")
-    p.add_argument("--threads", type=int, default=16, help="host threads (generation, CPU baseline)")
+    p.add_argument("--threads", type=int, default=16, help="host threads for input generation")
+    p.add_argument("--cpu-threads", type=int, default=None,
+                   help="CPU-baseline threads (default: every host core, os.cpu_count() = nproc)")
     p.add_argument("--cpu-sample", type=int, default=500_000, help="objects in the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r01e.json"),
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r02.json"),
                    help="measured per-launch HBM bytes (rocprofv3 PMC) to report as roofline.traffic")
-    p.add_argument("--blocks-per-cu", type=int, default=None)
-    p.add_argument("--variant", type=int, default=None, help="Orswot kernel variant (tuning/diagnostics)")
     return p.parse_args()
 
 
@@ -118,6 +119,38 @@ def wl_traffic(args, workload, *kernels):
     return None if any(v is None for v in vals) else float(sum(vals))
 
 
+def cpu_quota():
+    """CPUs this process may actually use: the affinity set, capped by the
+    cgroup CPU quota (cpu.max / cfs_quota_us) where one is set — on the GPU box
+    nproc shows the whole machine while the job's quota is a share of it."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    for path, two in (("/sys/fs/cgroup/cpu.max", True), ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", False)):
+        try:
+            txt = open(path).read().split()
+            if two:
+                q, per = txt[0], txt[1]
+            else:
+                q, per = txt[0], open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read().split()[0]
+            if q not in ("max", "-1"):
+                n = min(n, max(1, -(-int(q) // int(per))))
+            break
+        except (OSError, IndexError, ValueError):
+            continue
+    return n
+
+
+def cpu_threads(args):
+    """CPU-baseline threads: one per host core this job can use (BASELINE.md's
+    "one std::thread per host core", standing in for rayon over objects).
+    That is nproc unless a cgroup quota caps the job below it; both are reported."""
+    return max(1, args.cpu_threads or cpu_quota())
+
+
+def cpu_cores_note():
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_quota": cpu_quota()}
+
+
 def run_orswot(args, rank, world, local):
     import numpy as np
     import torch
@@ -130,10 +163,6 @@ def run_orswot(args, rank, world, local):
     (lb, lo), (rb, ro) = crdts_hip.generate_orswot(n, first_obj=first, threads=args.threads)
     gen_s = time.time() - t0
     eng = crdts_hip.Engine(local)
-    if args.blocks_per_cu:
-        eng.set_blocks_per_cu(args.blocks_per_cu)
-    if args.variant is not None:
-        eng.set_variant(args.variant)
     L = crdts_hip.OrswotBatch.from_host(lb, lo, 16, device=local)
     R = crdts_hip.OrswotBatch.from_host(rb, ro, 16, device=local)
     out = eng.orswot_alloc_out(L, R)
@@ -164,7 +193,10 @@ def run_orswot(args, rank, world, local):
     total_objs = sum_over_ranks(float(n * args.steps), world)
     value = total_objs / wall
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic = load_traffic(args.traffic_json, "orswot_merge_kernel")
+    # measured HBM bytes of one launch (both kernels of the timed window), from
+    # the FETCH_SIZE / WRITE_SIZE passes of tools/profile.sh -> tools/traffic.py
+    tk = [load_traffic(args.traffic_json, k) for k in ("orswot_mask_kernel", "orswot_merge_general_kernel")]
+    traffic = None if args.n_obj is not None or tk[0] is None else tk[0] + (tk[1] or 0.0)
     res = {
         "metric": METRIC,
         "value": value,
@@ -189,7 +221,7 @@ def run_orswot(args, rank, world, local):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "orswot_merge_kernel",
+            "kernel": "orswot_mask_kernel (+ orswot_merge_general_kernel in the same window)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -213,7 +245,7 @@ def cpu_baseline_orswot(lb, lo, rb, ro, args):
     m = min(args.cpu_sample, len(lo))
     end = int(lo[m]) if m < len(lo) else lb.nbytes
     endr = int(ro[m]) if m < len(ro) else rb.nbytes
-    threads = max(1, min(args.threads, os.cpu_count() or 1))
+    threads = cpu_threads(args)
     secs = oracle_ffi.orswot_bench(lb[:end], lo[:m], rb[:endr], ro[:m], threads)
     m1 = max(1, m // 10)
     secs1 = oracle_ffi.orswot_bench(lb, lo[:m1], rb, ro[:m1], 1)
@@ -221,11 +253,71 @@ def cpu_baseline_orswot(lb, lo, rb, ro, args):
         "value": m / secs,
         "unit": "objects/s",
         "cores": threads,
-        "kind": "port",
+        "kind": "port", **cpu_cores_note(),
         "sample": f"first {m} objects of the same config-3 batch, merge loop only (decode untimed), "
                   f"{threads} std::threads static partition",
         "value_1core": m1 / secs1,
     }
+
+
+def run_vclock(args, rank, world, local):
+    """Config 1 (BASELINE.json configs[0]): 1M VClock pairwise merges, 16
+    actors, each present with p = 0.75, counters U[1, 2^32) (a drawn 0 is an
+    absent actor, the same state), SplitMix64 seed 0xC0FFEE01. BASELINE.md
+    names it CPU plumbing: the line reports the reference-shaped CPU merge
+    (VClock::merge over std::map, src/vclock.rs:131-137) at 1 core and at every
+    host core, with the GPU's dense_max_kernel merge of the same rows beside it
+    (a step = one launch over the 1M pairs, rows resident in HBM)."""
+    import numpy as np
+    import torch
+
+    import crdts_hip
+
+    n, A = args.n_obj or 1_000_000, 16
+    first = rank * n
+    a = crdts_hip.generate_dense(n, A, seed=0xC0FFEE01, first_obj=first, bits=32, pct_zero=25, threads=args.threads)
+    b = crdts_hip.generate_dense(n, A, seed=0xC0FFEE01 ^ 0x5EED, first_obj=first, bits=32, pct_zero=25,
+                                 threads=args.threads)
+    dev = f"cuda:{local}"
+    da = torch.from_numpy(a.view(np.int64)).to(dev)
+    db = torch.from_numpy(b.view(np.int64)).to(dev)
+    eng = crdts_hip.Engine(local)
+    stream = torch.cuda.Stream(device=local)
+    eng.dense_merge(da, db, A, "vclock", stream=stream)
+    eng.status(stream)
+    assert (da.cpu().numpy().view(np.uint64) == np.maximum(a, b)).all()  # spot parity (pointwise max)
+
+    def step():  # after the first merge self == max: same bytes read and written, same work
+        eng.dense_merge(da, db, A, "vclock", stream=stream)
+
+    wall, ev_ms = _timed_steps(args, world, stream, step)
+    alg = 24.0 * n * A
+    ach = alg / (ev_ms * 1e-3) / 1e9
+    total = sum_over_ranks(float(n * args.steps), world)
+    res = {
+        "metric": "VClock pairwise merges/sec (node), 16 actors",
+        "value": total / wall, "unit": "merges/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u64", "data": "synthetic: SplitMix64 0xC0FFEE01, p(present)=0.75, counters U[1,2^32)",
+        "config": {"workload": f"vclock config1 (BASELINE.json configs[0]): {n} VClock pairs x {A} actors",
+                   "parallelism": f"dp{world} (pairs sharded)"},
+        "roofline": {"bound": "hbm", "kernel": "dense_max_kernel", "achieved": ach, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "kernel_ms": ev_ms, "alg_bytes_per_launch": alg,
+                     "traffic": None, "note": "128 MB per side: launch-latency-scale, not a roofline case"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_ffi
+
+        th = cpu_threads(args)
+        secs = oracle_ffi.dense_bench(a.ravel(), b.ravel(), A, th)
+        m1 = n // 4
+        secs1 = oracle_ffi.dense_bench(a[:m1].ravel(), b[:m1].ravel(), A, 1)
+        res["cpu_baseline"] = {"value": n / secs, "unit": "merges/s", "cores": th, "kind": "port", **cpu_cores_note(),
+                               "sample": f"all {n} pairs on {th} std::threads (+ {m1} pairs on 1 core), "
+                                         "VClock::merge over std::map, conversion untimed",
+                               "value_1core": m1 / secs1}
+    return res
 
 
 def run_dense(args, rank, world, local, kind):
@@ -283,9 +375,9 @@ def run_dense(args, rank, world, local, kind):
         m = min(args.cpu_sample * 4, n)
         ha = a[: m * slots].cpu().numpy().view(np.uint64).copy()
         hb = b[: m * slots].cpu().numpy().view(np.uint64).copy()
-        threads = max(1, min(args.threads, os.cpu_count() or 1))
+        threads = cpu_threads(args)
         secs = oracle_ffi.dense_bench(ha, hb, slots, threads)
-        res["cpu_baseline"] = {"value": m / secs, "unit": "objects/s", "cores": threads, "kind": "port",
+        res["cpu_baseline"] = {"value": m / secs, "unit": "objects/s", "cores": threads, "kind": "port", **cpu_cores_note(),
                                "sample": f"first {m} rows, VClock::merge over std::map, {threads} threads"}
     return res
 
@@ -327,17 +419,15 @@ def run_orswot_csr(args, rank, world, local):
     reps = crdts_hip.generate_replicas(n, R, threads=args.threads)
     gen_s = time.time() - t0
     eng = crdts_hip.Engine(local)
-    if args.variant is not None:
-        eng.set_variant(args.variant)
     SP, U = crdts_hip.SPARSE_CLOCK, crdts_hip.CONFIG5["universe"]
     stream = torch.cuda.Stream(device=local)
     if world > 1:
         mine = crdts_hip.OrswotBatch.from_host(*reps[rank], U, device=local, flags=SP)
         del reps
+        replica.init_comm(eng)  # the context's own RCCL communicator (crdt_comm_init)
 
-        def step():
-            with torch.cuda.stream(stream):
-                return replica.orswot_anti_entropy(eng, mine)
+        def step():  # owner-sharded: crdt_orswot_replica_join over RCCL
+            return replica.orswot_anti_entropy(eng, mine)
     else:
         batches = [crdts_hip.OrswotBatch.from_host(b, o, U, device=local, flags=SP) for b, o in reps]
         in_bytes = sum(int(b.nbytes) for b, _ in reps)
@@ -369,7 +459,9 @@ def run_orswot_csr(args, rank, world, local):
         "config": {"workload": f"orswot_csr config5 (BASELINE.json configs[4]): {n} objects x {R} replicas, "
                                "CSR top clocks, fold ((r0 ⊔ r1) ⊔ r2) ...",
                    "replicas": R, "n_obj": n, "gen_s": round(gen_s, 2),
-                   "parallelism": "all-gather (RCCL) + local rank-order fold" if world > 1 else "local fold"},
+                   "parallelism": ("owner-sharded RCCL join: slices of range j -> rank j (send/recv), rank-order "
+                                   "fold of n/N objects, folded ranges all-gathered (crdt_orswot_replica_join)")
+                   if world > 1 else "local fold"},
     }
     if world == 1:
         sizes = final.base.view(torch.int32)[(final.off // 4)].cpu().numpy().astype("int64")
@@ -387,10 +479,10 @@ def run_orswot_csr(args, rank, world, local):
 
             m = min(args.cpu_sample // 10, n)
             sub = crdts_hip.generate_replicas(m, 2, threads=args.threads)
-            th = max(1, min(args.threads, os.cpu_count() or 1))
+            th = cpu_threads(args)
             # oracle fold step r0 ⊔ r1 (decode untimed), same record form
             secs = oracle_ffi.orswot_bench(sub[0][0], sub[0][1], sub[1][0], sub[1][1], th)
-            res["cpu_baseline"] = {"value": m / secs, "unit": "object-merges/s", "cores": th, "kind": "port",
+            res["cpu_baseline"] = {"value": m / secs, "unit": "object-merges/s", "cores": th, "kind": "port", **cpu_cores_note(),
                                    "sample": f"{m} objects, replica 0 ⊔ replica 1, oracle merge loop, {th} threads"}
     return res
 
@@ -417,11 +509,11 @@ def run_gcounter_ae(args, rank, world, local):
     eng = crdts_hip.Engine(local)
     stream = torch.cuda.Stream(device=local)
     if world > 1:
-        native = replica.native_u64_max(dev)
+        replica.init_comm(eng)  # the context's own RCCL communicator (crdt_comm_init)
+        native = True  # crdt_replica_allreduce_max: ncclUint64 + ncclMax, no sign-flip passes
 
         def step():
-            with torch.cuda.stream(stream):
-                replica.dense_allreduce_max(base, native=native)
+            replica.dense_allreduce_max(base, engine=eng, stream=stream)
     else:
         other = base.clone()
         other[:, (mine_slot + 1) % A] += 1
@@ -440,8 +532,8 @@ def run_gcounter_ae(args, rank, world, local):
         "data": "synthetic: U[0,2^40) base + per-replica increments of its own slot",
         "config": {"workload": f"gcounter_ae config4 (BASELINE.json configs[3]): {n} GCounters x {A} slots per GPU",
                    "bytes_per_gpu": bytes_per_gpu,
-                   "parallelism": (f"RCCL all-reduce(max) over {world} GPUs, "
-                                   f"{'native u64' if native else 'sign-flipped i64'}") if world > 1
+                   "parallelism": (f"RCCL all-reduce(max) over {world} GPUs, native u64 "
+                                   "(crdt_replica_allreduce_max)") if world > 1
                    else "local replica join (dense_max_kernel)"},
     }
     if world > 1:
@@ -548,9 +640,9 @@ def run_bincode(args, rank, world, local):
             hb = blobs.cpu().numpy()
             ho = boff[:m].cpu().numpy().astype(np.uint64)
             hl = blen[:m].cpu().numpy().astype(np.uint64)
-            th = max(1, min(args.threads, os.cpu_count() or 1))
+            th = cpu_threads(args)
             secs = oracle_ffi.bincode_ingest_bench(hb, ho, hl, WA, WM, A, 0, th)
-            res["cpu_baseline"] = {"value": m / secs, "unit": "objects/s", "cores": th, "kind": "port",
+            res["cpu_baseline"] = {"value": m / secs, "unit": "objects/s", "cores": th, "kind": "port", **cpu_cores_note(),
                                    "sample": f"{m} blobs, from_binary into map/unordered_map + record encode, "
                                              f"{th} threads"}
     return res
@@ -688,11 +780,11 @@ def run_apply(args, rank, world, local):
                            "traffic": wl_traffic(args, "apply", "orswot_apply_kernel_true", "orswot_apply_kernel_false")}
         if not args.no_cpu_baseline:
             m = min(args.cpu_sample // 5, n)
-            th = max(1, min(args.threads, os.cpu_count() or 1))
+            th = cpu_threads(args)
             sub = (o_end[:m], kind[:8 * m], mem[:8 * m], act[:8 * m], ctr[:8 * m], cend[:8 * m],
                    cact[:int(cend[8 * m - 1])], cctr[:int(cend[8 * m - 1])])
             secs = oracle_ffi.orswot_apply_bench(lb, lo[:m].astype(np.uint64), sub, th)
-            res["cpu_baseline"] = {"value": 8 * m / secs, "unit": "ops/s", "cores": th, "kind": "port",
+            res["cpu_baseline"] = {"value": 8 * m / secs, "unit": "ops/s", "cores": th, "kind": "port", **cpu_cores_note(),
                                    "sample": f"{m} objects x 8 ops, oracle op path (std::map/unordered_map), "
                                              f"{th} threads"}
     return res
@@ -776,7 +868,7 @@ def run_mvreg(args, rank, world, local):
             oracle_ffi.mvreg_merge(hs[0].view(np.uint32), hs[1].view(np.uint64), hs[2].view(np.uint64),
                                    ho[0].view(np.uint32), ho[1].view(np.uint64), ho[2].view(np.uint64), A, 2 * cap)
             secs = _t.perf_counter() - t0
-            res["cpu_baseline"] = {"value": mm / secs, "unit": "merges/s", "cores": 1, "kind": "port",
+            res["cpu_baseline"] = {"value": mm / secs, "unit": "merges/s", "cores": 1, "kind": "port", **cpu_cores_note(),
                                    "sample": f"{mm} MVReg merges, oracle (std::map clocks), 1 thread, "
                                              "incl. slab<->map conversion"}
     return res
@@ -839,7 +931,7 @@ def run_map(args, rank, world, local):
             oracle_ffi.map_merge(sub(L) if mm == m else crdts_hip.MapSlab({f: v[:mm] for f, v in L.a.items()}, *caps),
                                  crdts_hip.MapSlab({f: v[:mm] for f, v in R.a.items()}, *caps), A)
             secs = _t.perf_counter() - t0
-            res["cpu_baseline"] = {"value": mm / secs, "unit": "merges/s", "cores": 1, "kind": "port",
+            res["cpu_baseline"] = {"value": mm / secs, "unit": "merges/s", "cores": 1, "kind": "port", **cpu_cores_note(),
                                    "sample": f"{mm} map merges, oracle (std::map / BTreeMap-shaped), 1 thread, "
                                              "incl. slab<->map conversion"}
     return res
@@ -852,6 +944,8 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     if args.workload == "orswot":
         res = run_orswot(args, rank, world, local)
+    elif args.workload == "vclock":
+        res = run_vclock(args, rank, world, local)
     elif args.workload == "orswot_csr":
         res = run_orswot_csr(args, rank, world, local)
     elif args.workload == "gcounter_ae":

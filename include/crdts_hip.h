@@ -59,9 +59,13 @@ int crdt_ctx_destroy(crdt_ctx* ctx);
 /* Synchronizes `stream`, returns the first record-level error latched by any
  * kernel launched through ctx since the last call (and clears it). */
 int crdt_ctx_status(crdt_ctx* ctx, void* stream);
-/* Number of objects rejected by the last kernels (cleared by ctx_status). */
 const char* crdt_strerror(int code);
 int crdt_abi_version(void);
+/* Capacity (<= 65536, the default) of the context's list of objects handed
+ * from the fast Orswot / apply kernels to their general kernels. Past it the
+ * general kernels scan every output offset instead; results are identical.
+ * Lowering it exercises that overflow path (tests). */
+int crdt_ctx_set_list_cap(crdt_ctx* ctx, uint32_t cap);
 
 /* ------------------------------------------------------------------------ *
  * Dense clocks and counters.
@@ -169,6 +173,11 @@ typedef struct crdt_orswot_batch {
  * needs at most self.bytes + other.bytes bytes and no prefix scan: the output
  * batch (d_out_base, d_out_off) is itself a valid input batch (it may have
  * gaps between records; crdt_orswot_compact removes them).
+ * PRECONDITION (checked on the device; a violation latches CRDT_EINVAL and
+ * the offending objects are not written): on each side the records are in
+ * increasing offset order and do not overlap, off[i] + size[i] <= off[i+1],
+ * so that the output records cannot overlap either. Packed batches, merge
+ * outputs (with gaps) and compacted batches all satisfy it.
  * `n_actors` is the dense top-clock width shared by every record.
  */
 int crdt_orswot_merge(crdt_ctx* ctx, const crdt_orswot_batch* self,
@@ -209,6 +218,59 @@ size_t crdt_orswot_compact_scratch_bytes(size_t n_obj);
 int crdt_orswot_compact(crdt_ctx* ctx, const crdt_orswot_batch* src, uint8_t* d_dst,
                         uint64_t* d_dst_off, size_t dst_bytes, void* d_scratch,
                         void* stream);
+
+/* ------------------------------------------------------------------------ *
+ * Replica anti-entropy across GPUs over RCCL (xGMI) — SURVEY.md §8(b),(e);
+ * BASELINE.json configs[3] (dense) and configs[4] (Orswot). One process (or
+ * thread) per GPU, each holding a full replica of the same n objects. The
+ * context owns one RCCL communicator:
+ *   rank 0:     crdt_comm_unique_id(id), then the caller distributes the
+ *               CRDT_COMM_ID_BYTES bytes to every rank (its own channel);
+ *   every rank: crdt_comm_init(ctx, id, n_ranks, rank)     (collective).
+ * Every collective entry point below must be called by every rank, in the
+ * same order, on the stream each rank passes. A failure found on one rank
+ * (bad batch, capacity, a non-canonical record) is returned by all ranks.
+ * ------------------------------------------------------------------------ */
+#define CRDT_COMM_ID_BYTES 128
+int crdt_comm_unique_id(uint8_t* h_id);
+int crdt_comm_init(crdt_ctx* ctx, const uint8_t* h_id, int n_ranks, int rank);
+/* Also done by crdt_ctx_destroy. */
+int crdt_comm_destroy(crdt_ctx* ctx);
+
+/* Dense rows (VClock / GCounter / PNCounter rows, any width): d_rows[k] :=
+ * max over ranks of d_rows[k], k < n_words, in place and in u64 order
+ * (ncclAllReduce, ncclUint64, ncclMax; chunks of <= 1 GiB). It is
+ * VClock::merge (src/vclock.rs:131-137) across replicas: a pointwise max,
+ * commutative and associative, so the reduction order cannot change a bit. */
+int crdt_replica_allreduce_max(crdt_ctx* ctx, uint64_t* d_rows, size_t n_words, void* stream);
+
+/* Orswot replicas: out[i] = ((r0[i] ⊔ r1[i]) ⊔ r2[i]) ⊔ ... ⊔ r_{N-1}[i], the
+ * same bytes on every rank (the join is structurally non-commutative,
+ * src/orswot.rs:98-103 vs :132-138, so the fold order is fixed: rank order).
+ * Owner-sharded: the objects are split into N contiguous ranges; rank j
+ * receives every replica's slice of range j point-to-point, folds it in rank
+ * order with the batched merge kernel (crdt_orswot_merge_ex), compacts it,
+ * and the folded ranges are exchanged back. Per rank: 1/N of the fold work
+ * and about 2(N-1)/N of one replica's bytes sent and received.
+ * `mine`: this rank's replica (the same n_obj on every rank; records in
+ * increasing, non-overlapping offset order). The output is a packed batch,
+ * record i at d_out + d_out_off[i], *h_out_used = its extent in bytes;
+ * out_bytes >= crdt_orswot_replica_join_bound() suffices (the sum of every
+ * rank's replica bytes, a collective). Synchronous: returns when the output
+ * is complete on `stream`. */
+int crdt_orswot_replica_join_bound(crdt_ctx* ctx, const crdt_orswot_batch* mine, size_t* h_bound, void* stream);
+int crdt_orswot_replica_join(crdt_ctx* ctx, const crdt_orswot_batch* mine, uint32_t n_actors, uint32_t flags,
+                             uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes, size_t* h_out_used,
+                             void* stream);
+/* The same owner-sharded join over n_replicas (<= 64) replicas resident on
+ * this context's device: each replica is a virtual rank (a host thread with
+ * its own context and stream) and device copies are the transport; the code
+ * below the transport is crdt_orswot_replica_join's. For single-GPU
+ * rehearsal and tests of the exchange. out_bytes >= the sum of the replicas'
+ * (16-B aligned) bytes suffices. No communicator needed. */
+int crdt_orswot_replica_join_local(crdt_ctx* ctx, const crdt_orswot_batch* replicas, uint32_t n_replicas,
+                                   uint32_t n_actors, uint32_t flags, uint8_t* d_out, uint64_t* d_out_off,
+                                   size_t out_bytes, size_t* h_out_used, void* stream);
 
 /* ------------------------------------------------------------------------ *
  * Host-side helpers (no device work).
@@ -329,10 +391,14 @@ int crdt_mvreg_merge(crdt_ctx* ctx, const uint32_t* d_self_n, const uint64_t* d_
  *     pairs [clk_end[i-1], clk_end[i]) of clk_act / clk_ctr (canonical:
  *     actors strictly increasing, counters > 0; Add ops own no pairs)
  * Object i's ops are [obj_end[i-1], obj_end[i]). Record i of the output is
- * written at d_out_off[i] = self.off[i] + 32*(ops before i) + 16*(clock pairs
- * before i) + 32*i (set by the call), so out_bytes >= self.bytes + 32*n_ops +
- * 16*n_clk + 32*n_obj suffices when self's records do not overlap and are in
- * increasing offset order. Limits of this round (CRDT_ECAPACITY): <= 128
+ * written at d_out_off[i] = self.off[i] + P*(ops before i) + 16*(clock pairs
+ * before i) + 32*i (set by the call), P = 32 for dense top clocks and 48 for
+ * CSR ones (an Add may bring a new actor, member and dot: 36 B), so
+ * out_bytes >= self.bytes + P*n_ops + 16*n_clk + 32*n_obj suffices.
+ * PRECONDITION: self's records do not overlap and are in increasing offset
+ * order (as any packed or merged batch); a record that would outgrow its own
+ * span self.size + P*ops + 16*pairs + 32 latches CRDT_ECAPACITY and is not
+ * written. Limits of this round (CRDT_ECAPACITY): <= 128
  * top-clock entries, members, dots per member clock and Rm clock pairs; <= 512
  * dots; <= 32 deferred clocks with <= 256 entries and <= 256 members.      */
 #define CRDT_OP_ADD 0u

@@ -16,7 +16,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import (CRDT_ECAPACITY, CRDT_ENONCANON, CRDT_OK, EXPORTS, LIB_PATH, SPARSE_CLOCK, Batch, CrdtError,
+from ._lib import (CRDT_COMM_ID_BYTES, CRDT_ECAPACITY, CRDT_ENONCANON, CRDT_OK, EXPORTS, LIB_PATH, SPARSE_CLOCK, Batch, CrdtError,
                    GenParams, RepParams, check, lib)
 from .record import decode_record, encode_record, record_bytes
 
@@ -71,13 +71,15 @@ class OrswotBatch:
 
     @classmethod
     def from_host(cls, base, off, n_actors, device=0, flags=0):
+        """device: a GPU index, or None / "cpu" for host tensors (the CPU tests' gloo path)."""
         torch = _torch()
+        dev = "cpu" if device is None or device == "cpu" else (device if isinstance(device, str) else f"cuda:{device}")
         base = np.ascontiguousarray(base, dtype=np.uint8)
         nb = max(16, (base.nbytes + 15) // 16 * 16)
-        b = torch.zeros(nb, dtype=torch.uint8, device=f"cuda:{device}")
+        b = torch.zeros(nb, dtype=torch.uint8, device=dev)
         if base.nbytes:
             b[: base.nbytes].copy_(torch.from_numpy(base))
-        o = torch.from_numpy(np.ascontiguousarray(off, dtype=np.uint64).view(np.int64)).to(f"cuda:{device}")
+        o = torch.from_numpy(np.ascontiguousarray(off, dtype=np.uint64).view(np.int64)).to(dev)
         return cls(b, o, n_actors, nb, flags)
 
     @classmethod
@@ -218,12 +220,19 @@ class Engine:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         return C.c_void_p(s.cuda_stream)
 
+    @staticmethod
+    def _diag(name):
+        if not hasattr(lib, name):
+            raise RuntimeError(f"{name}: diagnostic build only (make -C rust-crdt_amd diag; CRDTS_HIP_DIAG=1)")
+        return getattr(lib, name)
+
     def set_blocks_per_cu(self, k):
-        check(lib.crdt_ctx_set_blocks_per_cu(self.ctx, int(k)), "set_blocks_per_cu")
+        """Diagnostic build only: workgroups per CU of the Orswot kernel."""
+        check(self._diag("crdt_ctx_set_blocks_per_cu")(self.ctx, int(k)), "set_blocks_per_cu")
 
     def set_variant(self, v):
-        """Tuning knob: Orswot fast-kernel variant (0 = default)."""
-        check(lib.crdt_ctx_set_variant(self.ctx, int(v)), "set_variant")
+        """Diagnostic build only: Orswot kernel variant (0 = the product kernel)."""
+        check(self._diag("crdt_ctx_set_variant")(self.ctx, int(v)), "set_variant")
 
     def set_list_cap(self, cap):
         """Test knob: capacity of the general-path object list (overflow -> full scan)."""
@@ -281,6 +290,70 @@ class Engine:
             used = last + int(dst[last:last + 4].cpu().numpy().view(np.uint32)[0])
         return OrswotBatch(dst, doff, B.n_actors, max(16, (used + 15) // 16 * 16), B.flags)
 
+    # ------------------------------------------------ replica anti-entropy (RCCL)
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """crdt_comm_unique_id: the RCCL id rank 0 hands to every rank."""
+        buf = (C.c_uint8 * CRDT_COMM_ID_BYTES)()
+        check(lib.crdt_comm_unique_id(buf), "comm_unique_id")
+        return bytes(buf)
+
+    def comm_init(self, uid: bytes, n_ranks: int, rank: int):
+        """crdt_comm_init (collective): this context owns an RCCL communicator."""
+        if len(uid) != CRDT_COMM_ID_BYTES:
+            raise CrdtError(-1, "comm id must be CRDT_COMM_ID_BYTES bytes")
+        buf = (C.c_uint8 * CRDT_COMM_ID_BYTES).from_buffer_copy(uid)
+        check(lib.crdt_comm_init(self.ctx, buf, int(n_ranks), int(rank)), "comm_init")
+        self.n_ranks, self.rank = int(n_ranks), int(rank)
+
+    @property
+    def has_comm(self):
+        return getattr(self, "n_ranks", 0) > 0
+
+    def comm_destroy(self):
+        check(lib.crdt_comm_destroy(self.ctx), "comm_destroy")
+        self.n_ranks = 0
+
+    def replica_allreduce_max(self, rows, stream=None):
+        """In place: rows := max over ranks (u64 order), ncclUint64 + ncclMax
+        (src/vclock.rs:131-137 across replicas). rows: int64 device tensor of u64."""
+        check(lib.crdt_replica_allreduce_max(self.ctx, C.c_void_p(rows.data_ptr()), rows.numel(),
+                                             self._stream(stream)), "replica_allreduce_max")
+        return rows
+
+    def orswot_replica_join(self, B: OrswotBatch, stream=None):
+        """((r0 ⊔ r1) ⊔ ...) of every rank's replica, owner-sharded over RCCL;
+        the same packed batch on every rank (crdt_orswot_replica_join)."""
+        torch = _torch()
+        b = B.cbatch()
+        bound = C.c_size_t(0)
+        check(lib.crdt_orswot_replica_join_bound(self.ctx, C.byref(b), C.byref(bound), self._stream(stream)),
+              "replica_join_bound")
+        dev = f"cuda:{self.device}"
+        base = torch.empty(max(16, bound.value), dtype=torch.uint8, device=dev)
+        off = torch.empty(B.n_obj, dtype=torch.int64, device=dev)
+        used = C.c_size_t(0)
+        check(lib.crdt_orswot_replica_join(self.ctx, C.byref(b), B.n_actors, B.flags, C.c_void_p(base.data_ptr()),
+                                           C.c_void_p(off.data_ptr()), base.numel(), C.byref(used),
+                                           self._stream(stream)), "orswot_replica_join")
+        return OrswotBatch(base, off, B.n_actors, max(16, used.value), B.flags)
+
+    def orswot_replica_join_local(self, batches, stream=None):
+        """The same owner-sharded join with every replica a virtual rank on this
+        device (crdt_orswot_replica_join_local)."""
+        torch = _torch()
+        arr = (Batch * len(batches))(*[x.cbatch() for x in batches])
+        cap = sum((x.bytes + 15) // 16 * 16 for x in batches)
+        dev = f"cuda:{self.device}"
+        base = torch.empty(max(16, cap), dtype=torch.uint8, device=dev)
+        off = torch.empty(batches[0].n_obj, dtype=torch.int64, device=dev)
+        used = C.c_size_t(0)
+        check(lib.crdt_orswot_replica_join_local(self.ctx, arr, len(batches), batches[0].n_actors, batches[0].flags,
+                                                 C.c_void_p(base.data_ptr()), C.c_void_p(off.data_ptr()),
+                                                 base.numel(), C.byref(used), self._stream(stream)),
+              "orswot_replica_join_local")
+        return OrswotBatch(base, off, batches[0].n_actors, max(16, used.value), batches[0].flags)
+
     # ---------------------------------------------------------------- dense
     # ------------------------------------------------ VClock order / MVReg
     def vclock_partial_cmp(self, a_rows, b_rows, n_actors, stream=None):
@@ -333,7 +406,8 @@ class Engine:
         (src/orswot.rs:61-85). Returns an OrswotBatch."""
         torch = _torch()
         dev = f"cuda:{self.device}"
-        cap = B.bytes + 32 * ops.n_ops + 16 * ops.n_clk + 32 * B.n_obj
+        per_op = 48 if B.flags & SPARSE_CLOCK else 32  # include/crdts_hip.h: output reservation per op
+        cap = B.bytes + per_op * ops.n_ops + 16 * ops.n_clk + 32 * B.n_obj
         base = torch.empty(max(16, cap), dtype=torch.uint8, device=dev)
         off = torch.empty(B.n_obj, dtype=torch.int64, device=dev)
         b = B.cbatch()

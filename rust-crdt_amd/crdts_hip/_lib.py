@@ -12,6 +12,11 @@ import os
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)  # rust-crdt_amd/
 LIB_PATH = os.path.join(ROOT, "lib", "libcrdts_hip.so")
+# tools/ may select the diagnostic build (make -C rust-crdt_amd diag: kernel
+# variants, phase stamps, tuning knobs) with CRDTS_HIP_DIAG=1; never the product.
+if os.environ.get("CRDTS_HIP_DIAG") == "1":
+    LIB_PATH = os.path.join(ROOT, "lib", "libcrdts_hip_diag.so")
+DIAG_SYMBOLS = {"crdt_ctx_set_blocks_per_cu", "crdt_ctx_set_variant", "crdt_ctx_debug_read"}
 
 CRDT_OK = 0
 CRDT_EINVAL = -1
@@ -60,8 +65,12 @@ EXPORTS = [
     "crdt_orswot_validate_ex", "crdt_orswot_generate_replicas", "crdt_host_orswot_encode_ex",
     "crdt_orswot_bincode_record_sizes", "crdt_orswot_from_bincode", "crdt_orswot_bincode_sizes",
     "crdt_orswot_to_bincode", "crdt_orswot_apply", "crdt_vclock_partial_cmp", "crdt_mvreg_merge",
-    "crdt_map_mvreg_merge",
+    "crdt_map_mvreg_merge", "crdt_ctx_set_list_cap",
+    "crdt_comm_unique_id", "crdt_comm_init", "crdt_comm_destroy", "crdt_replica_allreduce_max",
+    "crdt_orswot_replica_join_bound", "crdt_orswot_replica_join", "crdt_orswot_replica_join_local",
 ]
+
+CRDT_COMM_ID_BYTES = 128
 
 
 class Ops(C.Structure):
@@ -137,8 +146,17 @@ def _load():
         "crdt_vclock_partial_cmp": (I, [P, P, P, SZ, U32, P, P]),
         "crdt_mvreg_merge": (I, [P, P, P, P, U32, P, P, P, U32, P, P, P, U32, SZ, U32, P]),
         "crdt_map_mvreg_merge": (I, [P, C.POINTER(MapSlabC), C.POINTER(MapSlabC), C.POINTER(MapSlabC), SZ, U32, P]),
+        "crdt_comm_unique_id": (I, [P]),
+        "crdt_comm_init": (I, [P, P, I, I]),
+        "crdt_comm_destroy": (I, [P]),
+        "crdt_replica_allreduce_max": (I, [P, P, SZ, P]),
+        "crdt_orswot_replica_join_bound": (I, [P, BP, C.POINTER(SZ), P]),
+        "crdt_orswot_replica_join": (I, [P, BP, U32, U32, P, P, SZ, C.POINTER(SZ), P]),
+        "crdt_orswot_replica_join_local": (I, [P, BP, U32, U32, U32, P, P, SZ, C.POINTER(SZ), P]),
     }
     for name, (res, args) in sig.items():
+        if name in DIAG_SYMBOLS and not hasattr(L, name):
+            continue  # product build: diagnostic knobs are not exported
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

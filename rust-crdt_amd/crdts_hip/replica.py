@@ -1,22 +1,28 @@
-"""Replica anti-entropy across GPUs.
+"""Replica anti-entropy across GPUs: the
+Python front end.
 
-One process per GPU (torch.distributed; backend "nccl" is RCCL over xGMI).
-Every rank holds a full replica of the same objects; after anti-entropy every
-rank holds the join of all replicas, bit-identical on every rank.
+One process per GPU; every rank holds a full replica of the same objects and
+after anti-entropy every rank holds the join of all replicas, bit-identical.
 
-Dense counters (VClock / GCounter / PNCounter rows): the join is the
-pointwise u64 max (src/vclock.rs:131-137), associative and commutative, so a
-single all-reduce(max) is exact in any reduction order. RCCL/gloo reduce
-int64 with a signed max; flipping bit 63 maps unsigned order onto signed
-order (x -> x ^ 2^63 is monotone from u64 to i64), so
-    max_u64(xs) = max_i64(xs ^ 2^63) ^ 2^63
-bit-exactly, for every u64 value.
+On GPUs the work is done by the C ABI over RCCL (rust-crdt_amd/csrc/replica.hip):
+`init_comm` gives the Engine's context an RCCL communicator (the 128-byte id
+is broadcast over the torch.distributed group), then
+- `dense_allreduce_max` -> crdt_replica_allreduce_max: one in-place
+  ncclAllReduce(ncclUint64, ncclMax). The join is VClock::merge
+  (src/vclock.rs:131-137), a pointwise max: exact in any reduction order.
+- `orswot_anti_entropy` -> crdt_orswot_replica_join: OWNER-SHARDED. The join
+  is structurally NON-commutative (src/orswot.rs:98-103 vs :132-138), so the
+  result is the rank-order fold ((r0 ⊔ r1) ⊔ r2) ⊔ ...; the n objects are
+  split into N contiguous ranges, rank j receives every replica's slice of
+  range j (point-to-point), folds it in rank order, compacts it, and the folded
+  ranges are exchanged back. Per rank: n/N objects folded N-1 times and about
+  2(N-1)/N of one replica's bytes on the wire.
 
-Orswot: the join is NOT commutative structurally (src/orswot.rs:98-103 vs
-:132-138), so replicas are exchanged (all-gather of per-rank byte sizes, then
-of size-padded record blobs and offsets) and every rank folds them locally
-in rank order ((r0 ⊔ r1) ⊔ r2) ⊔ ... with the batched merge kernel, which
-gives identical bytes on every rank.
+Without a communicator (CPU tensors over gloo, tests) the same two functions
+run the same algorithm over torch.distributed (all_to_all_single /
+all_gather) with a caller-supplied merge (the oracle in the CPU tests): the
+dense max reduces int64 after flipping bit 63 (x -> x ^ 2^63 maps u64 order
+onto i64 order), since gloo's MAX is signed.
 """
 from __future__ import annotations
 
@@ -31,50 +37,36 @@ def _torch():
     return torch
 
 
-_NATIVE_U64 = {}
-
-
-def native_u64_max(device, group=None):
-    """Whether this backend reduces torch.uint64 with MAX natively (RCCL's
-    ncclUint64 + ncclMax); probed once per device with a 2-element collective
-    whose answer needs unsigned order."""
-    torch = _torch()
+def init_comm(engine, group=None):
+    """Collective: rank 0 draws an RCCL id, the group broadcasts it, and every
+    rank's engine context creates its communicator (crdt_comm_init)."""
     import torch.distributed as dist
 
-    key = (str(device), id(group))
-    if key not in _NATIVE_U64:
-        ok = False
-        try:
-            rank = dist.get_rank(group)
-            t = torch.tensor([(1 << 63) + 5 if rank == 0 else 7, 3], dtype=torch.uint64, device=device)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-            ok = int(t[0].item()) == (1 << 63) + 5
-        except (RuntimeError, TypeError, ValueError):
-            ok = False
-        _NATIVE_U64[key] = ok
-    return _NATIVE_U64[key]
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    box = [engine.comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0, group=group)
+    engine.comm_init(box[0], world, rank)
+    return engine
 
 
-def dense_allreduce_max(rows, group=None, chunk_elems=1 << 28, native=None):
+def _has_comm(engine):
+    return engine is not None and getattr(engine, "has_comm", False)
+
+
+def dense_allreduce_max(rows, group=None, chunk_elems=1 << 28, engine=None, stream=None):
     """In place: rows = max over ranks (u64 semantics) of rows.
 
-    `rows` is an int64 tensor holding u64 counters (any shape), on the
-    process's GPU for nccl or on the CPU for gloo. Where the backend reduces
-    uint64 natively (RCCL ncclUint64/ncclMax; `native`, probed when None) the
-    rows are reduced as uint64 directly; otherwise through the sign flip
-    below. Chunked so collectives stay <= 2 GiB.
+    `rows` is an int64 tensor holding u64 counters (any shape). With an engine
+    whose context owns a communicator: crdt_replica_allreduce_max (RCCL,
+    native ncclUint64 + ncclMax, no extra passes). Otherwise (gloo, CPU):
+    torch.distributed all-reduce through the sign flip, chunked.
     """
+    if _has_comm(engine):
+        return engine.replica_allreduce_max(rows, stream=stream)
     torch = _torch()
     import torch.distributed as dist
 
     flat = rows.view(-1)
-    if native is None:
-        native = native_u64_max(flat.device, group)
-    if native:
-        u = flat.view(torch.uint64)
-        for s in range(0, u.numel(), chunk_elems):
-            dist.all_reduce(u[s:s + chunk_elems], op=dist.ReduceOp.MAX, group=group)
-        return rows
     sign = torch.tensor(SIGN, dtype=torch.int64, device=flat.device)
     for s in range(0, flat.numel(), chunk_elems):
         part = flat[s:s + chunk_elems]
@@ -102,32 +94,83 @@ def _gather_bytes(buf_u8, group=None):
     return [o[:s] for o, s in zip(outs, sizes)]
 
 
-def orswot_gather(batch_base, batch_off, group=None):
-    """All-gather every rank's Orswot record batch (base: uint8 tensor,
-    off: int64 tensor of byte offsets; same n_obj on every rank).
-    Returns [(base_r, off_r)] in rank order, on the input's device."""
-    torch = _torch()
-    bases = _gather_bytes(batch_base, group)
-    offs = _gather_bytes(batch_off.view(torch.uint8), group)
-    return [(b, o.view(torch.int64)) for b, o in zip(bases, offs)]
+def ranges(n, world):
+    """Object range owned by each rank: [b_j, b_{j+1}), b_j = j*n // N (the C
+    ABI's split, crdt_orswot_replica_join)."""
+    return [n * j // world for j in range(world + 1)]
 
 
-def orswot_anti_entropy(engine, batch, group=None, merge_fn=None):
+def _record_sizes(base, off):
+    b = base.cpu().numpy()
+    o = off.cpu().numpy().view(np.uint64)
+    return np.array([int(b[x:x + 4].view(np.uint32)[0]) for x in o.tolist()], dtype=np.int64)
+
+
+def orswot_anti_entropy(engine, batch, group=None, merge_fn=None, stats=None):
     """Join the Orswot replicas of all ranks: returns an OrswotBatch equal to
     ((r0 ⊔ r1) ⊔ r2) ⊔ ... on every rank.
 
-    `merge_fn(L, R) -> OrswotBatch` defaults to engine.orswot_merge (the GPU
-    kernel); the gloo tests on CPU pass the oracle instead.
+    With an engine that owns a communicator and no merge_fn: the C ABI
+    (crdt_orswot_replica_join over RCCL, the batched GPU merge as the fold).
+    Otherwise the same owner-sharded algorithm over torch.distributed, folding
+    with merge_fn(L, R) -> OrswotBatch (default engine.orswot_merge). `stats`,
+    if a dict, receives this rank's exchange and fold counts.
     """
+    if merge_fn is None and _has_comm(engine):
+        return engine.orswot_replica_join(batch)
+    torch = _torch()
+    import torch.distributed as dist
+
     from . import OrswotBatch
 
-    parts = orswot_gather(batch.base, batch.off, group)
     merge = merge_fn or (lambda L, R: engine.orswot_merge(L, R))
-    fl = getattr(batch, "flags", 0)  # dense or CSR top clocks, the same on every rank
-    acc = OrswotBatch(parts[0][0], parts[0][1], batch.n_actors, parts[0][0].numel(), fl)
-    for base, off in parts[1:]:
-        acc = merge(acc, OrswotBatch(base, off, batch.n_actors, base.numel(), fl))
-    return acc
+    R_, me = dist.get_world_size(group), dist.get_rank(group)
+    n, fl, A = batch.n_obj, getattr(batch, "flags", 0), batch.n_actors
+    b = ranges(n, R_)
+    off = batch.off.cpu().numpy().view(np.uint64)
+    sizes = _record_sizes(batch.base, batch.off)
+    # 1. byte extent of my slice of every range, all-gathered
+    bounds = np.zeros(2 * R_, dtype=np.int64)
+    for j in range(R_):
+        if b[j + 1] > b[j]:
+            bounds[2 * j] = int(off[b[j]])
+            bounds[2 * j + 1] = int(off[b[j + 1] - 1]) + int(sizes[b[j + 1] - 1])
+    mine = torch.from_numpy(bounds).to(batch.base.device)
+    G = [torch.zeros_like(mine) for _ in range(R_)]
+    dist.all_gather(G, mine, group=group)
+    G = [g.cpu().numpy() for g in G]
+    # 2. every replica's slice of my range (records, then offsets)
+    send = torch.cat([batch.base[int(bounds[2 * j]):int(bounds[2 * j + 1])] for j in range(R_)])
+    in_splits = [int(bounds[2 * j + 1] - bounds[2 * j]) for j in range(R_)]
+    out_splits = [int(G[p][2 * me + 1] - G[p][2 * me]) for p in range(R_)]
+    recv = torch.empty(sum(out_splits), dtype=torch.uint8, device=batch.base.device)
+    dist.all_to_all_single(recv, send, out_splits, in_splits, group=group)
+    nr = b[me + 1] - b[me]
+    roff = torch.empty(nr * R_, dtype=torch.int64, device=batch.base.device)
+    dist.all_to_all_single(roff, batch.off.contiguous(), [nr] * R_, [b[j + 1] - b[j] for j in range(R_)], group=group)
+    pos = np.concatenate([[0], np.cumsum(out_splits)]).astype(np.int64)
+    pieces = []
+    for p in range(R_):
+        po = roff[p * nr:(p + 1) * nr] - int(G[p][2 * me])
+        pieces.append(OrswotBatch(recv[int(pos[p]):int(pos[p + 1])].contiguous(), po.contiguous(), A,
+                                  out_splits[p], fl))
+    # 3. rank-order fold of my range, compacted
+    acc = pieces[0]
+    for piece in pieces[1:]:
+        acc = merge(acc, piece) if nr else acc
+    shard = OrswotBatch.from_records(acc.records(), A, device=None, flags=fl) if nr else None
+    sb = shard.base[: shard.bytes] if shard is not None else torch.empty(0, dtype=torch.uint8)
+    so = shard.off if shard is not None else torch.empty(0, dtype=torch.int64)
+    # 4. the folded ranges, all-gathered and rebased
+    bases = _gather_bytes(sb.to(batch.base.device), group)
+    offs = _gather_bytes(so.to(batch.base.device).view(torch.uint8), group)
+    P = np.concatenate([[0], np.cumsum([x.numel() for x in bases])]).astype(np.int64)
+    out_off = torch.cat([o.view(torch.int64) + int(P[q]) for q, o in enumerate(offs)])
+    out_base = torch.cat(bases) if int(P[-1]) else torch.zeros(16, dtype=torch.uint8)
+    if isinstance(stats, dict):
+        stats.update(objects_folded=nr, merges=nr * (R_ - 1), bytes_sent=sum(in_splits) + int(sb.numel()) * (R_ - 1),
+                     bytes_received=sum(out_splits) + int(P[-1]) - int(sb.numel()))
+    return OrswotBatch(out_base, out_off, A, max(16, int(P[-1])), fl)
 
 
 def digest(batch) -> int:

@@ -8,24 +8,12 @@
 #include <vector>
 
 #include "../../include/crdts_hip.h"
+#include "ctx.h"
 #include "kernels.h"
 #include "record_layout.h"
 
 using namespace crdts_hip;
 
-// Device scratch of a context: status word, the general-path object list
-// and its control words. A context serves one stream at a time.
-constexpr uint32_t kDefaultListCap = 1u << 16;
-
-struct crdt_ctx {
-  int device;
-  int* d_status;        // d_scratch + 0
-  uint32_t* d_ctl;      // d_scratch + 16: [list count, finished-block ticket]
-  uint64_t* d_list;     // d_scratch + 64
-  uint32_t list_cap;
-  int blocks_per_cu;
-  int variant;  // fast-kernel register budget (min waves per SIMD); 0 = default
-};
 
 namespace {
 
@@ -98,6 +86,8 @@ int crdt_ctx_create(crdt_ctx** out, int device) {
 int crdt_ctx_destroy(crdt_ctx* ctx) {
   if (!ctx) return CRDT_EINVAL;
   (void)hipSetDevice(ctx->device);
+  (void)crdt_comm_destroy(ctx);
+  (void)hipFree(ctx->d_arena);
   (void)hipFree(ctx->d_status);
   delete ctx;
   return CRDT_OK;
@@ -113,15 +103,15 @@ int crdt_ctx_status(crdt_ctx* ctx, void* stream) {
   return st;
 }
 
-// Test knob (not in the public header): shrink the general-path list so the
-// overflow scan is exercised.
 int crdt_ctx_set_list_cap(crdt_ctx* ctx, uint32_t cap) {
   if (!ctx || cap > kDefaultListCap) return CRDT_EINVAL;
   ctx->list_cap = cap;
   return CRDT_OK;
 }
 
-// Diagnostics (not in the public header): copy the context's list buffer
+#ifdef CRDT_DIAG
+// Diagnostic build only (-DCRDT_DIAG, lib/libcrdts_hip_diag.so, used by
+// tools/): copy the context's list buffer
 // (holds per-wave phase stamps after a variant-109 launch).
 int crdt_ctx_debug_read(crdt_ctx* ctx, uint64_t* h_out, size_t n, void* stream) {
   if (!ctx || !h_out || n > 8ull * kDefaultListCap / 8) return CRDT_EINVAL;
@@ -131,19 +121,20 @@ int crdt_ctx_debug_read(crdt_ctx* ctx, uint64_t* h_out, size_t n, void* stream) 
   return CRDT_OK;
 }
 
-// Tuning knob (not in the public header): Orswot fast-kernel variant.
+// Orswot kernel variant (diagnostic build only).
 int crdt_ctx_set_variant(crdt_ctx* ctx, int v) {
   if (!ctx || v < 0) return CRDT_EINVAL;
   ctx->variant = v;
   return CRDT_OK;
 }
 
-// Tuning knob (not in the public header): workgroups per CU for the Orswot kernel.
+// Workgroups per CU for the Orswot kernel (diagnostic build only).
 int crdt_ctx_set_blocks_per_cu(crdt_ctx* ctx, int k) {
   if (!ctx || k < 0 || k > 64) return CRDT_EINVAL;  // 0 = the variant's occupancy
   ctx->blocks_per_cu = k;
   return CRDT_OK;
 }
+#endif  // CRDT_DIAG
 
 int crdt_vclock_dense_merge(crdt_ctx* ctx, uint64_t* d_self, const uint64_t* d_other, size_t n_obj,
                             uint32_t n_actors, void* stream) {

@@ -46,6 +46,8 @@ struct Caps {
 using SmallCaps = Caps<64, 64, 256, 16, 128, 128, 64>;
 using BigCaps = Caps<128, 128, 512, 32, 256, 256, 128>;
 constexpr uint64_t kApPending = 1ull << 63;  // out_off flag: object left for the large workspace
+constexpr uint64_t kApOpBytesDense = 32;   // output bytes reserved per op, dense top clocks
+constexpr uint64_t kApOpBytesSparse = 48;  // ... CSR top clocks (a new clock entry: +12 B)
 
 template <class C>
 struct Ws {
@@ -439,7 +441,13 @@ __device__ int apply_one(Ws<C>& w, const ApArgs& g, uint64_t o, uint32_t lane) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) h[k] = ldc(hp + k);
   }
-  const uint64_t oo = so + 32u * ob + 16u * cb + 32u * o;
+  // output placement: an op grows a record by at most 32 B in the dense form
+  // (new member key + run end + dot, or a deferred key + its two run ends)
+  // and 36 B in the sparse form (a new top-clock entry on top: 48 B keeps the
+  // 16-B alignment); each Rm clock pair by 16 B; padding by < 32 B per object
+  const uint64_t per_op = sparse ? kApOpBytesSparse : kApOpBytesDense;
+  const uint64_t oo = so + per_op * ob + 16u * cb + 32u * o;
+  const uint64_t ce = oe ? ldc(clk_end + oe - 1) : 0u;
   if (lane == 0u) ooff[o] = oo;  // also clears a pending flag
   // the object's first 64 ops -> registers (lane i: op ob + i), loaded
   // together with the record so the op loop waits on no global load
@@ -567,7 +575,10 @@ __device__ int apply_one(Ws<C>& w, const ApArgs& g, uint64_t o, uint32_t lane) {
     uint32_t n_clk = c.clk;
     RecLayout L;
     rec_layout(L, n_clk, c.mem, c.dot, c.def, c.fdot, c.fmem, sparse);
-    if (oo + L.size > out_bytes || (oo & 15u)) {
+    // never past this object's own reserved span (the next object's output
+    // starts right after it when the input records are packed in order)
+    const uint64_t span = (uint64_t)h[0] + per_op * (oe - ob) + 16u * (ce >= cb ? ce - cb : 0u) + 32u;
+    if (oo + L.size > out_bytes || (oo & 15u) || L.size > span) {
       rc = CRDT_ECAPACITY;
     } else {
       uint8_t* O = out + oo;

@@ -1,0 +1,31 @@
+// The context behind the opaque crdt_ctx of include/crdts_hip.h (internal).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "../../include/crdts_hip.h"
+
+namespace crdts_hip {
+// Device scratch of a context: status word, the general-path object list
+// and its control words. A context serves one stream at a time.
+constexpr uint32_t kDefaultListCap = 1u << 16;
+}  // namespace crdts_hip
+
+struct crdt_ctx {
+  int device;
+  int* d_status;        // d_scratch + 0
+  uint32_t* d_ctl;      // d_scratch + 16: [list count, finished-block ticket]
+  uint64_t* d_list;     // d_scratch + 64
+  uint32_t list_cap;
+  int blocks_per_cu;    // diagnostic builds only (crdt_ctx_set_blocks_per_cu)
+  int variant;          // diagnostic builds only (crdt_ctx_set_variant); 0 = the product kernels
+  // replica anti-entropy (replica.hip): the RCCL communicator this context
+  // owns (ncclComm_t; null until crdt_comm_init) and a growable device arena
+  void* comm = nullptr;
+  int n_ranks = 0, rank = 0;
+  uint64_t* d_comm_stage = nullptr;  // device staging of the small all-gathers
+  uint8_t* d_arena = nullptr;
+  size_t arena_bytes = 0;
+};

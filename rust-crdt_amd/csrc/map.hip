@@ -86,6 +86,17 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
       if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
       continue;
     }
+    // every value count within mcap and deferred set size within scap (the
+    // loops below read mv_n / dset_n slots of the slab row as counts)
+    bool bad = false;
+    for (uint32_t k = lane; k < nS; k += kMpW) bad = bad || S.mv_n[i * S.kcap + k] > S.mcap;
+    for (uint32_t k = lane; k < nO; k += kMpW) bad = bad || O.mv_n[i * O.kcap + k] > O.mcap;
+    for (uint32_t k = lane; k < dS; k += kMpW) bad = bad || S.dset_n[i * S.dcap + k] > S.scap;
+    for (uint32_t k = lane; k < dO; k += kMpW) bad = bad || O.dset_n[i * O.dcap + k] > O.scap;
+    if (__ballot(bad) != 0ull) {
+      if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
+      continue;
+    }
     // ---- combined deferred list: self's, plus other's that self's clock does not cover
     //      (apply_rm's deferral, against the pre-merge clock), united in CLOCK ORDER
     uint32_t nc = 0;

@@ -904,8 +904,13 @@ __device__ __forceinline__ uint32_t fast_object(const uint8_t* Ls, const uint8_t
   return OL.size / 16u;
 }
 
+// Returned by a fast join when the object is outside its limits.
+constexpr uint32_t kLeanFallback = 0xFFFFFFFFu;
 
+#ifdef CRDT_DIAG
 // ======================================================================
+// (Diagnostic build only, -DCRDT_DIAG: earlier designs kept for A/B timing
+// by tools/ab_bench.py; the product library does not contain them.)
 // Lean path (v5): objects without deferred removes whose union has at most
 // 64 members and nL + nR <= 128 — ~93 % of config 3. Same rules as
 // fast_object / merge_object, restructured for VALU economy:
@@ -924,7 +929,6 @@ __device__ __forceinline__ uint32_t fast_object(const uint8_t* Ls, const uint8_t
 // has more than 64 members (the caller then runs fast_object on the
 // untouched stage).
 // ======================================================================
-constexpr uint32_t kLeanFallback = 0xFFFFFFFFu;
 constexpr uint32_t kFlag = 0x80000000u;
 
 template <bool WRITE>
@@ -1103,6 +1107,7 @@ __device__ __forceinline__ uint32_t lean_object(uint8_t* Ls, uint8_t* Rs, u32x4*
   }
   return size / 16u;
 }
+#endif  // CRDT_DIAG
 
 
 // ======================================================================
@@ -1376,8 +1381,9 @@ __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t
 }
 
 
+#ifdef CRDT_DIAG
 // ======================================================================
-// Mask path v2 (v7): the same mask join as mask_object with fewer dependent
+// (Diagnostic build only.) Mask path v2 (v7): the same mask join as mask_object with fewer dependent
 // LDS round trips — no run-head flags, no LDS atomics, no separate pass:
 //  - every member lane reads its own run (the first two dots straight-line,
 //    longer runs — 0.3 % in config 3 — in a loop) and forms its actor mask and
@@ -1587,6 +1593,7 @@ __device__ __forceinline__ uint32_t mask2_object(const uint8_t* Ls, const uint8_
   }
   return size / 16u;
 }
+#endif  // CRDT_DIAG
 
 
 // ======================================================================
@@ -1907,6 +1914,7 @@ __device__ __forceinline__ void copy_out(const u32x4* src, uint8_t* dst, uint32_
   for (uint32_t k = lane; k < n16; k += kWave) __builtin_nontemporal_store(src[k], (u32x4*)dst + k);
 }
 
+#ifdef CRDT_DIAG
 __device__ __forceinline__ void prefetch(u32x4 (&r)[kPer], const uint8_t* src, uint32_t n16, uint32_t lane) {
 #pragma unroll
   for (uint32_t k = 0; k < kPer; ++k) {
@@ -1922,6 +1930,8 @@ __device__ __forceinline__ void stage(u32x4* dst, const u32x4 (&r)[kPer], uint32
     if (idx < n16) dst[idx] = r[k];
   }
 }
+
+#endif  // CRDT_DIAG
 
 // Branch-free forms for the mask kernel: every lane loads (indices past the
 // record re-read its last piece, in bounds, merged by the address coalescer)
@@ -1939,6 +1949,8 @@ __device__ __forceinline__ void stage_all(u32x4* dst, const u32x4 (&r)[kPer], ui
   for (uint32_t k = 0; k < kPer; ++k) dst[lane + k * kWave] = r[k];
 }
 
+#ifdef CRDT_DIAG
+// (Diagnostic build only: the v4 merge-path kernel and its variants.)
 // MASK: non-deferred objects take mask_object. DIRECT (with MASK): outputs
 // are written straight to HBM (no LDS output stage), which frees LDS for a
 // 5th wave per SIMD.
@@ -2092,6 +2104,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
     list[wave_id * 8u + lane] = v;
   }
 }
+#endif  // CRDT_DIAG
 
 // ======================================================================
 // Mask kernel (v6): every object that fits the mask path (records <= 2 KB,
@@ -2123,8 +2136,9 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kern
     // ---- chunk state: lane k <-> object cbase + k
     const uint64_t obj = cbase + lane;
     const bool valid = lane < cs && obj < n_obj;
-    uint64_t lo = 0, ro = 0;
+    uint64_t lo = 0, ro = 0, nlo = Lbytes, nro = Rbytes;
     if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
+    if (valid && obj + 1u < n_obj) { nlo = Loff[obj + 1u]; nro = Roff[obj + 1u]; }  // same lines: coalesced
     u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
     bool ok = valid && (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes && ro + kHdrBytes <= Rbytes;
     if (ok) {
@@ -2133,6 +2147,11 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kern
     }
     ok = ok && header_ok(hl0, hl1, lo, Lbytes, A) && header_ok(hr0, hr1, ro, Rbytes, A) &&
          lo + ro + (uint64_t)hl0.x + hr0.x <= Obytes;
+    // output placement precondition (out[i] at self.off[i] + other.off[i]):
+    // each side's records in increasing offset order, none overlapping the next
+    const bool placed = !ok || (nlo >= lo + hl0.x && nro >= ro + hr0.x);
+    if (__ballot(!placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_EINVAL);
+    ok = ok && placed;
     const bool fast = ok && hl0.x <= kFastStage && hr0.x <= kFastStage && A <= 32u && hl0.z <= 64u &&
                       hr0.z <= 64u && hl0.w <= 64u && hr0.w <= 64u && hl1.x <= 32u && hr1.x <= 32u;
     if (valid) Ooff[obj] = (lo + ro) | ((ok && !fast) ? kPending : 0ull);
@@ -2140,7 +2159,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kern
       const uint32_t e = atomicAdd(&ctl[0], 1u);
       if (e < list_cap) list[e] = obj;
     }
-    if (__ballot(valid && !ok) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
+    if (__ballot(valid && !ok && placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
     const uint64_t runs = __ballot(fast);
     if (runs == 0ull) continue;
     const uint32_t n16 = fast ? (hl0.x / 16u) | ((hr0.x / 16u) << 16) : 0u;
@@ -2176,6 +2195,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kern
       mark<ABL>(st, 1);  // issue the next prefetch
       bool big = false;
       uint32_t r;
+#ifdef CRDT_DIAG
       if (M2) {
         if ((defs >> t) & 1ull)
           r = mask2_object<0xFFFFFFFFu, true, ABL>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
@@ -2183,7 +2203,9 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kern
         else
           r = mask2_object<0xFFFFFFFFu, false, ABL>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
                                                      m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, &st);
-      } else if ((defs >> t) & 1ull) {
+      } else
+#endif
+      if ((defs >> t) & 1ull) {
         r = mask_object<0xFFFFFFFFu, true, ABL>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
                                                  m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, &st);
       } else {
@@ -2282,14 +2304,16 @@ __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
 // per object pair, grid-stride over objects, both records staged through
 // LDS when they fit (else read from HBM), joined by merge_object<true>.
 // ======================================================================
-constexpr uint32_t kSpStage = 6144;
-constexpr int kSpWaves = 2;  // waves per block of the sparse kernel (LDS: 2 x (12 KB stage + 7 KB scratch))
 
 __device__ __forceinline__ bool sparse_header_ok(u32x4 h0, u32x4 h1, uint64_t off, uint64_t bytes, uint32_t A) {
   const uint64_t sz = record_size64(h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, true);
   return (off & 15u) == 0 && off + kHdrBytes <= bytes && sz == h0.x && h0.y <= A && h1.w == kSparseClock &&
          off + sz <= bytes;
 }
+
+#ifdef CRDT_DIAG
+constexpr uint32_t kSpStage = 6144;
+constexpr int kSpWaves = 2;  // waves per block of the sparse kernel (LDS: 2 x (12 KB stage + 7 KB scratch))
 
 template <bool MASK>
 __global__ __launch_bounds__(kWave * kSpWaves) void orswot_merge_sparse_kernel(
@@ -2341,6 +2365,7 @@ __global__ __launch_bounds__(kWave * kSpWaves) void orswot_merge_sparse_kernel(
     }
   }
 }
+#endif  // CRDT_DIAG
 
 // Sparse mask kernel: the dense mask kernel's structure for CSR batches.
 // Lane k of a chunk owns object cbase + k's header; objects that fit the
@@ -2388,8 +2413,9 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
   for (uint64_t cbase = wave_id * cs; cbase < n_obj; cbase += n_waves * cs) {
     const uint64_t obj = cbase + lane;
     const bool valid = lane < cs && obj < n_obj;
-    uint64_t lo = 0, ro = 0;
+    uint64_t lo = 0, ro = 0, nlo = Lbytes, nro = Rbytes;
     if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
+    if (valid && obj + 1u < n_obj) { nlo = Loff[obj + 1u]; nro = Roff[obj + 1u]; }
     u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
     bool ok = valid && (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes && ro + kHdrBytes <= Rbytes;
     if (ok) {
@@ -2398,6 +2424,9 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
     }
     ok = ok && sparse_header_ok(hl0, hl1, lo, Lbytes, A) && sparse_header_ok(hr0, hr1, ro, Rbytes, A) &&
          lo + ro + (uint64_t)hl0.x + hr0.x <= Obytes;
+    const bool placed = !ok || (nlo >= lo + hl0.x && nro >= ro + hr0.x);  // as in orswot_mask_kernel
+    if (__ballot(!placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_EINVAL);
+    ok = ok && placed;
     const bool fast = ok && hl0.x + hr0.x <= kSpPair && A <= kSpTableN && hl0.y <= 64u && hr0.y <= 64u &&
                       hl0.z <= 64u && hr0.z <= 64u && hl0.w <= 128u && hr0.w <= 128u && hl1.x <= 32u &&
                       hr1.x <= 32u;
@@ -2406,7 +2435,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
       const uint32_t e = atomicAdd(&ctl[0], 1u);
       if (e < list_cap) list[e] = obj;
     }
-    if (__ballot(valid && !ok) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
+    if (__ballot(valid && !ok && placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
     uint64_t pend = __ballot(fast);
     if (pend == 0ull) continue;
     const uint32_t n16 = fast ? (hl0.x / 16u) | ((hr0.x / 16u) << 16) : 0u;
@@ -2526,9 +2555,11 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  // variant: the fast kernel's minimum waves per SIMD (register budget);
-  // 101..103 are timing-only ablation builds (invalid output).
-  const void* fn;
+  // The product kernel: orswot_mask_kernel at 6 waves per SIMD (measured
+  // best, tools/ab_bench.py). Other variants exist in -DCRDT_DIAG builds only
+  // (101..103 are timing-only ablations whose output is invalid).
+  const void* fn = (const void*)orswot_mask_kernel<6>;
+#ifdef CRDT_DIAG
   switch (variant) {
     case 6: fn = (const void*)orswot_merge_kernel<1, 0, true>; break;
     case 7: fn = (const void*)orswot_merge_kernel<1, 0, false, 0, true>; break;
@@ -2553,8 +2584,12 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
     case 109: fn = (const void*)orswot_merge_kernel<4, 9>; break;
     case 1: fn = (const void*)orswot_merge_kernel<1, 0>; break;
     case 13: fn = (const void*)orswot_merge_kernel<1, 0, false, 0, true>; break;
-    default: fn = (const void*)orswot_mask_kernel<6>; break;  // measured best (tools/ab_bench.py)
+    default: break;
   }
+#else
+  variant = 0;
+  blocks_per_cu = 0;
+#endif
   // Resident grid: the kernel's occupancy in 4-wave blocks per CU
   // (blocks_per_cu overrides), no more blocks than 64-object chunks need.
   static std::atomic<int> occ_cache[26];  // per variant slot, 0 = not yet queried
@@ -2591,6 +2626,7 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
   int dev = 0, cus = 256, occ = 0;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+#ifdef CRDT_DIAG
   if (sparse_variant == 1 || sparse_variant == 2) {  // one wave per object (1: no mask join)
     const void* fn = sparse_variant == 1 ? (const void*)orswot_merge_sparse_kernel<false>
                                           : (const void*)orswot_merge_sparse_kernel<true>;
@@ -2605,6 +2641,10 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
   }
   const void* fn = sparse_variant == 4 ? (const void*)orswot_sparse_mask_kernel<3, 9>
                                         : (const void*)orswot_sparse_mask_kernel<3>;
+#else
+  sparse_variant = 0;
+  const void* fn = (const void*)orswot_sparse_mask_kernel<3>;
+#endif
   static std::atomic<int> occ_cache{0};
   occ = occ_cache.load(std::memory_order_relaxed);
   if (occ == 0) {

@@ -1,0 +1,546 @@
+// Replica anti-entropy across GPUs (SURVEY.md §8(b),(e); BASELINE.json
+// configs[3] and configs[4]) behind the C ABI, on RCCL over xGMI.
+//
+// Dense clocks / counters: one in-place ncclAllReduce(ncclUint64, ncclMax).
+// The join is VClock::merge (src/vclock.rs:131-137), a pointwise max: any
+// reduction order gives the same bits, and RCCL reduces u64 natively.
+//
+// Orswot: the join is structurally NON-commutative (self-only entries kept
+// as they are, src/orswot.rs:98-103; other-only entries subtracted by the
+// self clock, :132-138), so the result is defined as the rank-order fold
+// ((r0 ⊔ r1) ⊔ r2) ⊔ ... and every rank must end with the same bytes. It is
+// computed owner-sharded: the n objects are split into N contiguous ranges,
+// rank j owns range j and
+//   1. learns every rank's byte extent of every range (all-gather of 2N u64);
+//   2. receives every replica's slice of range j — records and offsets —
+//      point-to-point from each peer (one grouped send/recv round: the 8-GPU
+//      node is fully connected, so each pair of GPUs uses its own xGMI link);
+//   3. folds the N slices in rank order with the batched merge kernel, then
+//      compacts the result (gaps removed);
+//   4. sends its folded range to every peer and receives theirs (grouped
+//      send/recv again), and rebases the gathered offsets.
+// Per rank that is 1/N of the fold work and ~2(N-1)/N replica sizes on the
+// wire, instead of N-1 replicas in and N-1 merges of everything.
+//
+// The per-rank code is written once against a Transport; RcclTransport is
+// the product, ThreadTransport runs the same code with one host thread per
+// virtual rank on ONE device (crdt_orswot_replica_join_local), which is how
+// the exchange logic is tested without a multi-GPU node.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/crdts_hip.h"
+#include "ctx.h"
+#include "kernels.h"
+
+using namespace crdts_hip;
+
+namespace {
+
+inline hipStream_t S(void* s) { return (hipStream_t)s; }
+inline uint64_t al16(uint64_t x) { return (x + 15u) & ~uint64_t(15); }
+inline uint64_t al256(uint64_t x) { return (x + 255u) & ~uint64_t(255); }
+
+constexpr size_t kAllReduceChunk = size_t(1) << 27;  // u64 words per collective (1 GiB)
+
+// ---------------------------------------------------------------- kernels
+// Byte extent of every object range of one replica: range j = objects
+// [b_j, b_{j+1}), b_j = j*n/N; bounds[2j] = off[b_j], bounds[2j+1] = end of
+// the range's last record (0, 0 for an empty range).
+__global__ void slice_bounds_kernel(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                                    uint64_t bytes, uint64_t n, uint32_t R, uint64_t* __restrict__ bounds) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= R) return;
+  const uint64_t b0 = n * j / R, b1 = n * (j + 1u) / R;
+  uint64_t s = 0, e = 0;
+  if (b1 > b0) {
+    s = off[b0];
+    const uint64_t last = off[b1 - 1u];
+    e = last + 32u <= bytes ? last + *(const uint32_t*)(base + last) : ~0ull;  // ~0: out of bounds
+  }
+  bounds[2u * j] = s;
+  bounds[2u * j + 1u] = e;
+}
+
+// off[i] := off[i] - sub[piece(i)] + add[piece(i)] for pieces of `per` objects
+// (piece p = objects [p*per, (p+1)*per)); or, with first != null, pieces
+// [first[p], first[p+1]).
+__global__ void rebase_kernel(uint64_t* __restrict__ off, uint64_t n, uint64_t per,
+                              const uint64_t* __restrict__ first, const uint64_t* __restrict__ sub,
+                              const uint64_t* __restrict__ add, uint32_t R) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t p;
+  if (first) {
+    p = 0;
+    while (p + 1u < R && first[p + 1u] <= i) ++p;
+  } else {
+    p = (uint32_t)(i / per);
+  }
+  off[i] = off[i] - sub[p] + add[p];
+}
+
+int launch_rebase(uint64_t* off, uint64_t n, uint64_t per, const uint64_t* first, const uint64_t* sub,
+                  const uint64_t* add, uint32_t R, hipStream_t st) {
+  if (n == 0) return CRDT_OK;
+  hipLaunchKernelGGL(rebase_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, off, n, per, first, sub,
+                     add, R);
+  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+}
+
+// ---------------------------------------------------------------- transports
+struct Xfer {
+  int peer;
+  const void* src;  // sends
+  void* dst;        // recvs
+  size_t bytes;
+};
+
+struct Transport {
+  int R = 1, me = 0;
+  virtual ~Transport() = default;
+  // blocking: every rank contributes n u64 (host), receives R*n in rank order
+  virtual int allgather(const uint64_t* h_in, size_t n, uint64_t* h_out, hipStream_t st) = 0;
+  // enqueued on st: every send matched by the peer's recv of the same size
+  virtual int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t st) = 0;
+};
+
+int nccl_rc(ncclResult_t r) { return r == ncclSuccess ? CRDT_OK : CRDT_ECOMM; }
+
+struct RcclTransport : Transport {
+  ncclComm_t comm;
+  uint64_t* d_buf;  // (R + 1) * (2R + 3) u64 of device staging for the all-gathers (ctx-owned)
+  RcclTransport(crdt_ctx* ctx, uint64_t* d) : comm((ncclComm_t)ctx->comm), d_buf(d) {
+    R = ctx->n_ranks;
+    me = ctx->rank;
+  }
+  int allgather(const uint64_t* h_in, size_t n, uint64_t* h_out, hipStream_t st) override {
+    if (hipMemcpyAsync(d_buf, h_in, 8 * n, hipMemcpyHostToDevice, st) != hipSuccess) return CRDT_EHIP;
+    int rc = nccl_rc(ncclAllGather(d_buf, d_buf + n, n, ncclUint64, comm, st));
+    if (rc) return rc;
+    if (hipMemcpyAsync(h_out, d_buf + n, 8 * n * R, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return CRDT_EHIP;
+    return CRDT_OK;
+  }
+  int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t st) override {
+    // the self part as device copies, the rest as one group of point-to-point
+    // transfers (xGMI is point-to-point: each peer pair has its own link)
+    for (const Xfer& x : sends)
+      if (x.peer == me && x.bytes)
+        for (const Xfer& y : recvs)
+          if (y.peer == me && y.src == x.src && y.bytes == x.bytes &&
+              hipMemcpyAsync(y.dst, x.src, x.bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+            return CRDT_EHIP;
+    int rc = nccl_rc(ncclGroupStart());
+    if (rc) return rc;
+    for (size_t k = 0; k < sends.size() && !rc; ++k)
+      if (sends[k].peer != me && sends[k].bytes)
+        rc = nccl_rc(ncclSend(sends[k].src, sends[k].bytes, ncclUint8, sends[k].peer, comm, st));
+    for (size_t k = 0; k < recvs.size() && !rc; ++k)
+      if (recvs[k].peer != me && recvs[k].bytes)
+        rc = nccl_rc(ncclRecv(recvs[k].dst, recvs[k].bytes, ncclUint8, recvs[k].peer, comm, st));
+    const int rc2 = nccl_rc(ncclGroupEnd());
+    return rc ? rc : rc2;
+  }
+};
+
+// R virtual ranks in one process, one host thread each, all on one device.
+struct ThreadGroup {
+  int R;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  std::vector<uint64_t> gather;                 // allgather staging
+  std::vector<std::vector<Xfer>> sends;         // per rank: its published sends
+  std::vector<hipEvent_t> ready, done;          // per rank: data ready / copies done
+  explicit ThreadGroup(int r) : R(r), sends(r), ready(r, nullptr), done(r, nullptr) {}
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    const uint64_t g = gen;
+    if (++arrived == R) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return gen != g; });
+    }
+  }
+};
+
+struct ThreadTransport : Transport {
+  ThreadGroup* g;
+  ThreadTransport(ThreadGroup* grp, int rank) : g(grp) {
+    R = grp->R;
+    me = rank;
+  }
+  int allgather(const uint64_t* h_in, size_t n, uint64_t* h_out, hipStream_t) override {
+    {
+      std::lock_guard<std::mutex> lk(g->mu);
+      if (g->gather.size() < n * R) g->gather.resize(n * R);
+    }
+    g->barrier();
+    std::memcpy(g->gather.data() + n * me, h_in, 8 * n);
+    g->barrier();
+    std::memcpy(h_out, g->gather.data(), 8 * n * R);
+    g->barrier();
+    return CRDT_OK;
+  }
+  int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t st) override {
+    g->sends[me] = sends;
+    int rc = hipEventRecord(g->ready[me], st) == hipSuccess ? CRDT_OK : CRDT_EHIP;
+    g->barrier();
+    for (const Xfer& y : recvs) {  // pull each peer's matching send (same order of sends to one peer)
+      if (!y.bytes || rc) continue;
+      size_t k = 0;
+      for (const Xfer& x : recvs) {
+        if (&x == &y) break;
+        if (x.peer == y.peer && x.bytes) ++k;
+      }
+      const Xfer* src = nullptr;
+      for (const Xfer& x : g->sends[y.peer])
+        if (x.peer == me && x.bytes && k-- == 0) { src = &x; break; }
+      if (!src || src->bytes != y.bytes) { rc = CRDT_ECOMM; continue; }
+      if (hipStreamWaitEvent(st, g->ready[y.peer], 0) != hipSuccess ||
+          hipMemcpyAsync(y.dst, src->src, y.bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        rc = CRDT_EHIP;
+    }
+    if (hipEventRecord(g->done[me], st) != hipSuccess) rc = CRDT_EHIP;
+    g->barrier();
+    for (int p = 0; p < R; ++p)  // our send buffers stay untouched until every reader copied them
+      if (hipStreamWaitEvent(st, g->done[p], 0) != hipSuccess) rc = CRDT_EHIP;
+    g->barrier();
+    return rc;
+  }
+};
+
+// ---------------------------------------------------------------- per-rank join
+int ensure_arena(crdt_ctx* ctx, size_t bytes) {
+  if (ctx->arena_bytes >= bytes) return CRDT_OK;
+  (void)hipFree(ctx->d_arena);
+  ctx->d_arena = nullptr;
+  ctx->arena_bytes = 0;
+  if (hipMalloc(&ctx->d_arena, bytes) != hipSuccess) return CRDT_EHIP;
+  ctx->arena_bytes = bytes;
+  return CRDT_OK;
+}
+
+int read_status(crdt_ctx* ctx, hipStream_t st) {
+  int v = 0;
+  if (hipMemcpyAsync(&v, ctx->d_status, sizeof v, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return CRDT_EHIP;
+  if (v && hipMemsetAsync(ctx->d_status, 0, sizeof(int), st) != hipSuccess) return CRDT_EHIP;
+  return v;
+}
+
+// The owner-sharded join, one rank's part. `out` may be null (the rank takes
+// part in the exchange but does not gather the result). A failure on one
+// rank is carried to every rank through the next all-gather, so all ranks
+// leave at the same step (none is left waiting in a collective).
+int orswot_join_rank(crdt_ctx* ctx, Transport& T, const crdt_orswot_batch* mine, uint32_t A, uint32_t flags,
+                     uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes, size_t* h_used, hipStream_t st) {
+  const int R = T.R, me = T.me;
+  const uint64_t n = mine->n_obj;
+  const bool want = d_out != nullptr;
+  auto b = [&](int j) { return n * (uint64_t)j / (uint64_t)R; };
+  const size_t head = al256(8ull * 5 * R);  // device tables: slice bounds (2R), rebase table (3R)
+
+  // 1. my byte extents of every range, all-gathered with the batch shape
+  int err = ensure_arena(ctx, head);
+  std::vector<uint64_t> mb(2 * R + 3, 0);
+  if (!err && n) {
+    if (!mine->base || !mine->off) {
+      err = CRDT_EINVAL;
+    } else {
+      hipLaunchKernelGGL(slice_bounds_kernel, dim3((R + 63) / 64), dim3(64), 0, st, mine->base, mine->off,
+                         (uint64_t)mine->bytes, n, (uint32_t)R, (uint64_t*)ctx->d_arena);
+      if (hipGetLastError() != hipSuccess ||
+          hipMemcpyAsync(mb.data(), ctx->d_arena, 16ull * R, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess)
+        err = CRDT_EHIP;
+      uint64_t prev_end = 0;
+      for (int j = 0; j < R && !err; ++j) {  // ranges in increasing, non-overlapping order, 16-B aligned
+        if (b(j + 1) == b(j)) continue;
+        const uint64_t s0 = mb[2 * j], e0 = mb[2 * j + 1];
+        if (e0 == ~0ull || e0 < s0 || e0 > mine->bytes || s0 < prev_end || ((s0 | e0) & 15u)) err = CRDT_EINVAL;
+        prev_end = e0;
+      }
+    }
+  }
+  mb[2 * R] = n;
+  mb[2 * R + 1] = (uint64_t)-err;
+  mb[2 * R + 2] = want ? 1u : 0u;
+  const size_t W = 2 * R + 3;
+  std::vector<uint64_t> G(W * R);
+  int rc = T.allgather(mb.data(), W, G.data(), st);
+  if (rc) return rc;
+  for (int p = 0; p < R; ++p) {
+    if (G[W * p + 2 * R] != n) return CRDT_EINVAL;  // the same object count on every rank
+    if (G[W * p + 2 * R + 1]) return -(int)G[W * p + 2 * R + 1];
+  }
+  auto gs = [&](int p, int j) { return G[W * p + 2 * j]; };  // rank p's start of range j
+  auto gsz = [&](int p, int j) { return G[W * p + 2 * j + 1] - G[W * p + 2 * j]; };
+  auto wants = [&](int p) { return G[W * p + 2 * R + 2] != 0; };
+
+  // 2. the arena: every replica's slice of my range + their offsets, two fold
+  //    buffers (ping-pong), compaction scratch
+  const uint64_t nr = b(me + 1) - b(me);
+  std::vector<uint64_t> pos(R + 1, 0);
+  for (int p = 0; p < R; ++p) pos[p + 1] = pos[p] + al16(gsz(p, me));
+  const uint64_t total = pos[R];
+  size_t cub_temp = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, cub_temp, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                         (int)(nr ? nr : 1));
+  size_t at = head;
+  auto take = [&](size_t bytes) { size_t o = at; at = al256(at + bytes); return o; };
+  const size_t o_recv = take(total), o_roff = take(8 * R * nr), o_fa = take(total), o_fb = take(total),
+               o_oa = take(8 * nr), o_ob = take(8 * nr), o_sz = take(8 * nr), o_cub = take(cub_temp);
+  err = ensure_arena(ctx, at);
+  {  // agree: a rank that cannot allocate stops every rank here
+    std::vector<uint64_t> e1 = {(uint64_t)-err}, E1(R);
+    if ((rc = T.allgather(e1.data(), 1, E1.data(), st))) return rc;
+    for (int p = 0; p < R; ++p)
+      if (E1[p]) return -(int)E1[p];
+  }
+  uint8_t* A8 = ctx->d_arena;
+  uint64_t* d_tab = (uint64_t*)A8 + 2 * R;
+  uint8_t* recv = A8 + o_recv;
+  uint64_t* roff = (uint64_t*)(A8 + o_roff);
+  std::vector<Xfer> sends, recvs;
+  for (int p = 0; p < R; ++p) {  // per peer: the records, then the offsets (same order on both ends)
+    const uint64_t np = b(p + 1) - b(p);
+    sends.push_back({p, n ? mine->base + gs(me, p) : nullptr, nullptr, gsz(me, p)});
+    sends.push_back({p, n ? mine->off + b(p) : nullptr, nullptr, 8 * np});
+    recvs.push_back({p, p == me && n ? mine->base + gs(me, me) : nullptr, recv + pos[p], gsz(p, me)});
+    recvs.push_back({p, p == me && n ? (const void*)(mine->off + b(me)) : nullptr, roff + nr * p, 8 * nr});
+  }
+  if ((rc = T.exchange(sends, recvs, st))) return rc;
+
+  // 3. offsets relative to each slice's own base, the rank-order fold, and
+  //    compaction into the fold buffer the result is not in
+  std::vector<uint64_t> tab(3 * R, 0);
+  for (int p = 0; p < R; ++p) tab[R + p] = gs(p, me);  // sub
+  if (hipMemcpyAsync(d_tab, tab.data(), 8ull * 3 * R, hipMemcpyHostToDevice, st) != hipSuccess) err = CRDT_EHIP;
+  if (!err) err = launch_rebase(roff, nr * R, nr ? nr : 1, nullptr, d_tab + R, d_tab + 2 * R, (uint32_t)R, st);
+  const uint8_t* acc = recv;
+  const uint64_t* acc_off = roff;
+  uint64_t acc_bytes = gsz(0, me);
+  for (int p = 1; p < R && nr && !err; ++p) {
+    uint8_t* o = A8 + (p % 2 ? o_fa : o_fb);
+    uint64_t* oo = (uint64_t*)(A8 + (p % 2 ? o_oa : o_ob));
+    const uint8_t* rb = recv + pos[p];
+    const uint64_t* ro = roff + nr * p;
+    const uint64_t cap = acc_bytes + gsz(p, me);
+    err = (flags & CRDT_ORSWOT_SPARSE_CLOCK)
+              ? launch_orswot_merge_sparse(acc, acc_off, acc_bytes, rb, ro, gsz(p, me), o, oo, cap, nr, A,
+                                           ctx->d_status, ctx->d_ctl, ctx->d_list, ctx->list_cap, st, 0)
+              : launch_orswot_merge(acc, acc_off, acc_bytes, rb, ro, gsz(p, me), o, oo, cap, nr, A, ctx->d_status,
+                                    ctx->d_ctl, ctx->d_list, ctx->list_cap, st, 0, 0);
+    acc = o;
+    acc_off = oo;
+    acc_bytes = cap;
+  }
+  const bool in_a = acc == A8 + o_fa;
+  uint8_t* shard = A8 + (in_a ? o_fb : o_fa);
+  uint64_t* shard_off = (uint64_t*)(A8 + (in_a ? o_ob : o_oa));
+  uint64_t* sizes = (uint64_t*)(A8 + o_sz);
+  uint64_t E = 0;
+  if (nr && !err) {
+    err = launch_record_sizes(acc, acc_off, nr, sizes, st);
+    if (!err && hipcub::DeviceScan::ExclusiveSum(A8 + o_cub, cub_temp, sizes, shard_off, (int)nr, st) != hipSuccess)
+      err = CRDT_EHIP;
+    uint64_t lo = 0, ls = 0;
+    if (!err && (hipMemcpyAsync(&lo, shard_off + nr - 1, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                 hipMemcpyAsync(&ls, sizes + nr - 1, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                 hipStreamSynchronize(st) != hipSuccess))
+      err = CRDT_EHIP;
+    E = lo + ls;
+    if (!err && E > total) err = CRDT_ENONCANON;  // a merged record never outgrows its inputs
+    if (!err) err = launch_record_copy(acc, acc_off, shard, shard_off, nr, st);
+  }
+  if (!err) err = read_status(ctx, st);  // record-level errors latched by the fold
+
+  // 4. every rank's folded range to every rank that gathers the result
+  std::vector<uint64_t> m2 = {E, (uint64_t)out_bytes, (uint64_t)-err};
+  std::vector<uint64_t> G2(3 * R);
+  if ((rc = T.allgather(m2.data(), 3, G2.data(), st))) return rc;
+  std::vector<uint64_t> P(R + 1, 0);
+  for (int q = 0; q < R; ++q) {
+    if (G2[3 * q + 2]) return -(int)G2[3 * q + 2];
+    P[q + 1] = P[q] + G2[3 * q];
+  }
+  for (int q = 0; q < R; ++q)
+    if (wants(q) && G2[3 * q + 1] < P[R]) return CRDT_ECAPACITY;  // every rank sees the same verdict
+  sends.clear();
+  recvs.clear();
+  for (int q = 0; q < R; ++q) {
+    if (wants(q)) {
+      sends.push_back({q, shard, nullptr, E});
+      sends.push_back({q, shard_off, nullptr, 8 * nr});
+    }
+    if (want) {
+      const uint64_t nq = b(q + 1) - b(q);
+      recvs.push_back({q, q == me ? shard : nullptr, d_out + P[q], G2[3 * q]});
+      recvs.push_back({q, q == me ? (const void*)shard_off : nullptr, d_out_off + b(q), 8 * nq});
+    }
+  }
+  rc = T.exchange(sends, recvs, st);
+  if (!rc && want) {
+    for (int q = 0; q < R; ++q) {
+      tab[q] = b(q);
+      tab[R + q] = 0;
+      tab[2 * R + q] = P[q];
+    }
+    if (hipMemcpyAsync(d_tab, tab.data(), 8ull * 3 * R, hipMemcpyHostToDevice, st) != hipSuccess) rc = CRDT_EHIP;
+    if (!rc) rc = launch_rebase(d_out_off, n, 1, d_tab, d_tab + R, d_tab + 2 * R, (uint32_t)R, st);
+    if (!rc && h_used) *h_used = P[R];
+  }
+  // the tables are read by kernels on st: finished before a later call reuses them
+  if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = CRDT_EHIP;
+  return rc;
+}
+
+int set_dev(crdt_ctx* ctx) { return hipSetDevice(ctx->device) == hipSuccess ? CRDT_OK : CRDT_EHIP; }
+
+}  // namespace
+
+extern "C" {
+
+int crdt_comm_unique_id(uint8_t* h_id) {
+  if (!h_id) return CRDT_EINVAL;
+  static_assert(sizeof(ncclUniqueId) == CRDT_COMM_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return CRDT_ECOMM;
+  std::memcpy(h_id, &id, sizeof id);
+  return CRDT_OK;
+}
+
+int crdt_comm_init(crdt_ctx* ctx, const uint8_t* h_id, int n_ranks, int rank) {
+  if (!ctx || !h_id || n_ranks < 1 || rank < 0 || rank >= n_ranks || ctx->comm) return CRDT_EINVAL;
+  int rc = set_dev(ctx);
+  if (rc) return rc;
+  ncclUniqueId id;
+  std::memcpy(&id, h_id, sizeof id);
+  uint64_t* stage = nullptr;
+  if (hipMalloc(&stage, 8ull * (n_ranks + 1) * (2 * n_ranks + 3)) != hipSuccess) return CRDT_EHIP;
+  ncclComm_t comm = nullptr;
+  if (ncclCommInitRank(&comm, n_ranks, id, rank) != ncclSuccess) {
+    (void)hipFree(stage);
+    return CRDT_ECOMM;
+  }
+  ctx->comm = comm;
+  ctx->d_comm_stage = stage;
+  ctx->n_ranks = n_ranks;
+  ctx->rank = rank;
+  return CRDT_OK;
+}
+
+int crdt_comm_destroy(crdt_ctx* ctx) {
+  if (!ctx) return CRDT_EINVAL;
+  if (!ctx->comm) return CRDT_OK;
+  (void)set_dev(ctx);
+  const ncclResult_t r = ncclCommDestroy((ncclComm_t)ctx->comm);
+  (void)hipFree(ctx->d_comm_stage);
+  ctx->d_comm_stage = nullptr;
+  ctx->comm = nullptr;
+  ctx->n_ranks = 0;
+  return r == ncclSuccess ? CRDT_OK : CRDT_ECOMM;
+}
+
+int crdt_replica_allreduce_max(crdt_ctx* ctx, uint64_t* d_rows, size_t n_words, void* stream) {
+  if (!ctx || !ctx->comm || (n_words && !d_rows)) return CRDT_EINVAL;
+  int rc = set_dev(ctx);
+  if (rc) return rc;
+  for (size_t s = 0; s < n_words && !rc; s += kAllReduceChunk) {
+    const size_t cnt = std::min(kAllReduceChunk, n_words - s);
+    rc = nccl_rc(ncclAllReduce(d_rows + s, d_rows + s, cnt, ncclUint64, ncclMax, (ncclComm_t)ctx->comm,
+                               S(stream)));
+  }
+  return rc;
+}
+
+int crdt_orswot_replica_join_bound(crdt_ctx* ctx, const crdt_orswot_batch* mine, size_t* h_bound, void* stream) {
+  if (!ctx || !ctx->comm || !mine || !h_bound) return CRDT_EINVAL;
+  int rc = set_dev(ctx);
+  if (rc || (rc = ensure_arena(ctx, 256))) return rc;
+  const uint64_t v = al16(mine->bytes);
+  uint64_t* d = (uint64_t*)ctx->d_arena;
+  uint64_t sum = 0;
+  if (hipMemcpyAsync(d, &v, 8, hipMemcpyHostToDevice, S(stream)) != hipSuccess) return CRDT_EHIP;
+  if ((rc = nccl_rc(ncclAllReduce(d, d + 1, 1, ncclUint64, ncclSum, (ncclComm_t)ctx->comm, S(stream))))) return rc;
+  if (hipMemcpyAsync(&sum, d + 1, 8, hipMemcpyDeviceToHost, S(stream)) != hipSuccess ||
+      hipStreamSynchronize(S(stream)) != hipSuccess)
+    return CRDT_EHIP;
+  *h_bound = sum;
+  return CRDT_OK;
+}
+
+int crdt_orswot_replica_join(crdt_ctx* ctx, const crdt_orswot_batch* mine, uint32_t n_actors, uint32_t flags,
+                             uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes, size_t* h_out_used,
+                             void* stream) {
+  if (!ctx || !ctx->comm || !mine || n_actors == 0 || (flags & ~CRDT_ORSWOT_SPARSE_CLOCK)) return CRDT_EINVAL;
+  if (mine->n_obj && (!d_out || !d_out_off || ((uintptr_t)d_out & 15u))) return CRDT_EINVAL;
+  int rc = set_dev(ctx);
+  if (rc) return rc;
+  RcclTransport T(ctx, ctx->d_comm_stage);
+  if (h_out_used) *h_out_used = 0;
+  return orswot_join_rank(ctx, T, mine, n_actors, flags, d_out, d_out_off, out_bytes, h_out_used, S(stream));
+}
+
+int crdt_orswot_replica_join_local(crdt_ctx* ctx, const crdt_orswot_batch* replicas, uint32_t n_replicas,
+                                   uint32_t n_actors, uint32_t flags, uint8_t* d_out, uint64_t* d_out_off,
+                                   size_t out_bytes, size_t* h_out_used, void* stream) {
+  if (!ctx || !replicas || n_replicas == 0 || n_replicas > 64 || n_actors == 0 ||
+      (flags & ~CRDT_ORSWOT_SPARSE_CLOCK))
+    return CRDT_EINVAL;
+  int rc = set_dev(ctx);
+  if (rc) return rc;
+  const int R = (int)n_replicas;
+  ThreadGroup g(R);
+  std::vector<crdt_ctx*> ctxs(R, nullptr);
+  std::vector<hipStream_t> streams(R, nullptr);
+  ctxs[0] = ctx;
+  streams[0] = S(stream);
+  for (int r = 0; r < R && !rc; ++r) {
+    if (r && (rc = crdt_ctx_create(&ctxs[r], ctx->device))) break;
+    if (r && hipStreamCreate(&streams[r]) != hipSuccess) rc = CRDT_EHIP;
+    if (hipEventCreateWithFlags(&g.ready[r], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&g.done[r], hipEventDisableTiming) != hipSuccess)
+      rc = CRDT_EHIP;
+  }
+  std::vector<int> rcs(R, CRDT_OK);
+  if (!rc) {
+    if (h_out_used) *h_out_used = 0;
+    auto run = [&](int r) {
+      (void)hipSetDevice(ctx->device);
+      ThreadTransport T(&g, r);
+      rcs[r] = orswot_join_rank(ctxs[r], T, &replicas[r], n_actors, flags, r == 0 ? d_out : nullptr,
+                                r == 0 ? d_out_off : nullptr, out_bytes, r == 0 ? h_out_used : nullptr, streams[r]);
+    };
+    std::vector<std::thread> th;
+    for (int r = 1; r < R; ++r) th.emplace_back(run, r);
+    run(0);
+    for (auto& t : th) t.join();
+    for (int r = 0; r < R && !rc; ++r) rc = rcs[r];
+  }
+  for (int r = 0; r < R; ++r) {
+    if (streams[r]) (void)hipStreamSynchronize(streams[r]);
+    if (r && streams[r]) (void)hipStreamDestroy(streams[r]);
+    if (r && ctxs[r]) (void)crdt_ctx_destroy(ctxs[r]);
+    if (g.ready[r]) (void)hipEventDestroy(g.ready[r]);
+    if (g.done[r]) (void)hipEventDestroy(g.done[r]);
+  }
+  return rc;
+}
+
+}  // extern "C"

@@ -38,6 +38,24 @@ def test_library_exports_every_declared_symbol():
     assert sorted(crdts_hip.EXPORTS) == declared_functions()
 
 
+def exported_functions(path):
+    """crdt_* functions in the library's dynamic symbol table (ELF .dynsym)."""
+    import subprocess
+
+    out = subprocess.run(["nm", "-D", "--defined-only", path], check=True, capture_output=True, text=True).stdout
+    return sorted({ln.split()[-1] for ln in out.splitlines()
+                   if len(ln.split()) == 3 and ln.split()[1] == "T" and ln.split()[-1].startswith("crdt_")})
+
+
+def test_exported_symbols_equal_declared_symbols():
+    """The product library exports exactly the header's functions: no
+    undeclared tuning / diagnostic entry points (those live in the
+    -DCRDT_DIAG build, lib/libcrdts_hip_diag.so, used by tools/ only)."""
+    import crdts_hip
+
+    assert exported_functions(crdts_hip.LIB_PATH) == declared_functions()
+
+
 def test_abi_version_and_strerror():
     import crdts_hip
     from crdts_hip._lib import lib

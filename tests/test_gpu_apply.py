@@ -192,3 +192,29 @@ def test_apply_dense_wide_clock(gpu, oracle):
     rng = random.Random(17)
     recs = [_record(rng, 100, rng.randrange(0, 50), rng.randrange(0, 3)) for _ in range(300)]
     _run(gpu, oracle, recs, 100, 0, seed=18, max_ops=8)
+
+
+def test_apply_sparse_growth_fresh_actors(gpu, oracle):
+    """Sparse records growing by the most an Add can add (a new top-clock
+    actor, a new member and its dot: 36 B): 9..16 such Adds on empty sparse
+    records, other objects after each in the batch. Every output must equal
+    the oracle's, so none overwrote its neighbour (the per-op reservation of
+    the CSR form, include/crdts_hip.h)."""
+    import crdts_hip
+
+    rng = random.Random(19)
+    empty = records.encode({}, {}, {}, 1024, sparse=True)
+    recs, per = [], []
+    for i in range(300):
+        if i % 2 == 0:
+            n = 9 + rng.randrange(8)
+            acts = rng.sample(range(1024), n)
+            per.append([("add", a, 1 + rng.randrange(5), rng.getrandbits(64)) for a in acts])
+            recs.append(empty)
+        else:
+            recs.append(_record(rng, 1024, rng.randrange(1, 20), rng.randrange(0, 2), sparse=True))
+            per.append([])
+    B = crdts_hip.OrswotBatch.from_records(recs, 1024, flags=crdts_hip.SPARSE_CLOCK)
+    out = gpu.orswot_apply(B, crdts_hip.OrswotOps.from_lists(per)).records()
+    exp = [_oracle_apply(oracle, r, o, 1024, crdts_hip.SPARSE_CLOCK) for r, o in zip(recs, per)]
+    assert out == exp

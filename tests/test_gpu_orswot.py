@@ -223,6 +223,28 @@ def test_validate_and_noncanonical_inputs(gpu):
     assert len(d["entries"]) > 1
 
 
+def test_misordered_offsets_rejected(gpu):
+    """The output placement out.off[i] = self.off[i] + other.off[i] needs each
+    side's records in increasing, non-overlapping offset order
+    (include/crdts_hip.h); a permuted batch must fail with CRDT_EINVAL
+    instead of two objects writing the same output bytes."""
+    import crdts_hip
+    from crdts_hip._lib import CRDT_EINVAL
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(100, threads=4)
+    perm = lo.copy()
+    perm[[10, 11]] = perm[[11, 10]]  # records 10 and 11 swapped on the self side only
+    with pytest.raises(crdts_hip.CrdtError) as e:
+        _gpu_merge(gpu, lb, perm, rb, ro, 16)
+    assert e.value.code == CRDT_EINVAL
+    shared = lo.copy()
+    shared[20] = shared[19]  # two objects sharing one record: overlapping
+    with pytest.raises(crdts_hip.CrdtError) as e:
+        _gpu_merge(gpu, lb, shared, rb, ro, 16)
+    assert e.value.code == CRDT_EINVAL
+    _gpu_merge(gpu, lb, lo, rb, ro, 16)  # the context is clean again
+
+
 def test_capacity_and_empty_batch(gpu):
     import torch
 

@@ -71,3 +71,21 @@ def test_gpu_map_merge(gpu, oracle, A, keys):
         for f in exp.a:
             bad = np.nonzero((got.a[f] != exp.a[f]).reshape(len(exp.a["n_keys"]), -1).any(axis=1))[0]
             assert len(bad) == 0, f"{f}: {len(bad)} maps differ, first {bad[0]}"
+
+
+@pytest.mark.gpu
+def test_gpu_map_malformed_counts_rejected(gpu, oracle):
+    """A value count above mcap or a deferred set size above scap is
+    rejected (CRDT_ENONCANON) instead of reading the next slot's data."""
+    import crdts_hip
+
+    L, R = oracle.map_generate(7, 64, 8, 6, 10, CAPS)
+    gpu.map_mvreg_merge(L.to("cuda:0"), R.to("cuda:0"), 8)  # well-formed: no error
+    for field, cap in (("mv_n", CAPS[1]), ("dset_n", CAPS[3])):
+        bad = crdts_hip.MapSlab({f: v.copy() for f, v in L.a.items()}, *CAPS)
+        rows = np.nonzero(bad.a["n_keys" if field == "mv_n" else "n_def"] > 0)[0]
+        assert len(rows)
+        bad.a[field][rows[0], 0] = cap + 1
+        with pytest.raises(crdts_hip.CrdtError) as e:
+            gpu.map_mvreg_merge(bad.to("cuda:0"), R.to("cuda:0"), 8)
+        assert e.value.code == crdts_hip.CRDT_ENONCANON

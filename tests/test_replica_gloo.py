@@ -2,10 +2,13 @@
 
 - dense: u64-exact all-reduce(max) via the sign flip, including counters
   >= 2^63 (where a plain signed max would be wrong);
-- Orswot: all-gather of size-padded record blobs + rank-order fold; with the
-  oracle as the fold (no GPU here) every rank ends with the oracle's
-  ((r0 ⊔ r1) ⊔ r2) bytes, identical on every rank.
-The same functions run on RCCL with the GPU kernel as the fold in bench.py.
+- Orswot: the OWNER-SHARDED join (rank j folds range j of every replica in
+  rank order, the folded ranges are all-gathered); with the oracle as the fold
+  (no GPU here) every rank ends with the oracle's ((r0 ⊔ r1) ⊔ r2) bytes,
+  identical on every rank, having folded only its 1/N of the objects.
+The same Python front end drives the C ABI over RCCL (crdt_orswot_replica_join,
+crdt_replica_allreduce_max) when the engine owns a communicator: bench.py at
+N > 1, and tests/test_gpu_replica.py.
 """
 import os
 import socket
@@ -68,7 +71,11 @@ def _orswot_worker(rank, world, port, q):
                                                R.off.numpy().view(np.uint64), 16, threads=2)
         return crdts_hip.OrswotBatch(torch.from_numpy(ob), torch.from_numpy(oo.view(np.int64)), 16, ob.nbytes)
 
-    out = replica.orswot_anti_entropy(None, B, merge_fn=oracle_merge)
+    stats = {}
+    out = replica.orswot_anti_entropy(None, B, merge_fn=oracle_merge, stats=stats)
+    b = replica.ranges(n, world)
+    assert stats["objects_folded"] == b[rank + 1] - b[rank]  # owner-sharded: 1/N of the objects
+    assert stats["merges"] == (b[rank + 1] - b[rank]) * (world - 1)
     dg = replica.digest(out)
     d = torch.tensor([dg - (1 << 64) if dg >= (1 << 63) else dg], dtype=torch.int64)
     ds = [torch.zeros_like(d) for _ in range(world)]
@@ -112,6 +119,31 @@ def _orswot_sparse_worker(rank, world, port, q):
     ds = [torch.zeros_like(d) for _ in range(world)]
     dist.all_gather(ds, d)
     q.put((rank, [int(x.item()) % (1 << 64) for x in ds], replica.digest(ref), out.records() == ref.records()))
+    dist.destroy_process_group()
+
+
+def _orswot_tiny_worker(rank, world, port, q):
+    """More ranks than objects: some ranges are empty."""
+    _init(rank, world, port)
+    import crdts_hip
+    import oracle_ffi
+    from crdts_hip import replica
+
+    gens = [crdts_hip.generate_orswot(2, threads=1, seed=90 + r)[0] for r in range(world)]
+    lb, lo = gens[rank]
+    B = crdts_hip.OrswotBatch(torch.from_numpy(lb.copy()), torch.from_numpy(lo.view(np.int64).copy()), 16, lb.nbytes)
+
+    def oracle_merge(L, R):
+        ob, oo = oracle_ffi.orswot_merge_batch(L.base.numpy(), L.off.numpy().view(np.uint64), R.base.numpy(),
+                                               R.off.numpy().view(np.uint64), 16, threads=1)
+        return crdts_hip.OrswotBatch(torch.from_numpy(ob), torch.from_numpy(oo.view(np.int64)), 16, ob.nbytes)
+
+    out = replica.orswot_anti_entropy(None, B, merge_fn=oracle_merge)
+    acc = gens[0]
+    for b, o in gens[1:]:
+        acc = oracle_ffi.orswot_merge_batch(acc[0], acc[1], b, o, 16, threads=1)
+    ref = crdts_hip.OrswotBatch(torch.from_numpy(acc[0]), torch.from_numpy(acc[1].view(np.int64)), 16, acc[0].nbytes)
+    q.put((rank, None, None, out.records() == ref.records()))
     dist.destroy_process_group()
 
 
@@ -167,3 +199,8 @@ def test_orswot_sparse_anti_entropy_gloo():
     for rank, digests, ref_digest, same in res:
         assert same, f"rank {rank} sparse fold differs from the oracle's rank-order fold"
         assert len(set(digests)) == 1 and digests[0] == ref_digest
+
+
+def test_orswot_anti_entropy_more_ranks_than_objects_gloo():
+    for rank, _, _, same in _run(_orswot_tiny_worker, 3):
+        assert same, f"rank {rank}: fold with empty ranges differs"

@@ -5,6 +5,8 @@ merge launch(es); prints median/min ms per variant as one JSON line."""
 import argparse
 import json
 import os
+
+os.environ.setdefault("CRDTS_HIP_DIAG", "1")  # variants / stamps: diagnostic build (make -C rust-crdt_amd diag)
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

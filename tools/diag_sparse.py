@@ -1,6 +1,9 @@
 """Diagnostics: one config-5 fold step at a given size, mask kernel alone
 (variant 203) then the full launch, synchronising after each; prints the
 general-path list it leaves behind."""
+import os
+
+os.environ.setdefault("CRDTS_HIP_DIAG", "1")  # variants / stamps: diagnostic build (make -C rust-crdt_amd diag)
 import ctypes as C
 import sys
 

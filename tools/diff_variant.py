@@ -3,6 +3,8 @@
 its records differ from the oracle's (first few objects)."""
 import argparse
 import os
+
+os.environ.setdefault("CRDTS_HIP_DIAG", "1")  # variants / stamps: diagnostic build (make -C rust-crdt_amd diag)
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -4,6 +4,8 @@ s_memtime stamps; read the SHARES, not the absolute run time)."""
 import ctypes as C
 import json
 import os
+
+os.environ.setdefault("CRDTS_HIP_DIAG", "1")  # variants / stamps: diagnostic build (make -C rust-crdt_amd diag)
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

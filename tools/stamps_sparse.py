@@ -5,6 +5,8 @@ config-5 replicas with the product kernel up to step K-1, then stamps step K."""
 import ctypes as C
 import json
 import os
+
+os.environ.setdefault("CRDTS_HIP_DIAG", "1")  # variants / stamps: diagnostic build (make -C rust-crdt_amd diag)
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
