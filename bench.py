@@ -195,7 +195,7 @@ def run_orswot(args, rank, world, local):
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     # measured HBM bytes of one launch (both kernels of the timed window), from
     # the FETCH_SIZE / WRITE_SIZE passes of tools/profile.sh -> tools/traffic.py
-    tk = [load_traffic(args.traffic_json, k) for k in ("orswot_mask_kernel", "orswot_merge_general_kernel")]
+    tk = [load_traffic(args.traffic_json, k) for k in ("orswot_join_kernel", "orswot_merge_general_kernel")]
     traffic = None if args.n_obj is not None or tk[0] is None else tk[0] + (tk[1] or 0.0)
     res = {
         "metric": METRIC,
@@ -221,7 +221,7 @@ def run_orswot(args, rank, world, local):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "orswot_mask_kernel (+ orswot_merge_general_kernel in the same window)",
+            "kernel": "orswot_join_kernel (+ orswot_merge_general_kernel in the same window)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

@@ -69,7 +69,7 @@ int crdt_ctx_create(crdt_ctx** out, int device) {
   c->blocks_per_cu = 0;
   c->list_cap = kDefaultListCap;
   c->variant = 0;
-  const size_t bytes = 64 + 8ull * kDefaultListCap;
+  const size_t bytes = 64 + 8ull * kDefaultListCap + kTrashBytes + 8ull * kDeferListCap;  // status, ctl, lists, sink
   uint8_t* scratch = nullptr;
   if (hipMalloc(&scratch, bytes) != hipSuccess || hipMemset(scratch, 0, bytes) != hipSuccess) {
     (void)hipFree(scratch);

@@ -11,6 +11,16 @@ namespace crdts_hip {
 // Device scratch of a context: status word, the general-path object list
 // and its control words. A context serves one stream at a time.
 constexpr uint32_t kDefaultListCap = 1u << 16;
+// Per-wave sink for the lane-predicated global stores of the join kernels
+// (a lane with nothing to store writes here instead of branching around the
+// store, so every object issues the same stores): kTrashWaves x 64 B, right
+// after the list in the context's scratch.
+constexpr uint32_t kTrashWaves = 8192;
+constexpr size_t kTrashBytes = 64ull * kTrashWaves;
+// Objects with deferred removes, listed by the join pass for the deferred
+// pass (after the sink); past kDeferListCap entries the deferred pass scans
+// the output offsets for their flag instead.
+constexpr uint32_t kDeferListCap = 1u << 20;
 }  // namespace crdts_hip
 
 struct crdt_ctx {

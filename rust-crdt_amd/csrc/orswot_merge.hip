@@ -32,6 +32,7 @@
 #include <atomic>
 
 #include "../../include/crdts_hip.h"
+#include "ctx.h"
 #include "kernels.h"
 #include "record_layout.h"
 
@@ -1381,6 +1382,311 @@ __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t
 }
 
 
+// ======================================================================
+// Mask path v8 (mask3_object): mask_object's join for objects without
+// deferred removes, rewritten for the instruction count. Same rules
+// (src/orswot.rs:94-138) and same output bytes; what changed:
+//  - every LDS access is a raw 32-bit LDS address kept in a VGPR (no
+//    generic-pointer arithmetic per access);
+//  - the rank searches clamp their probe address instead of testing the
+//    bound (a probe past the other list reads its last key: if that key is
+//    below, the rank is that list's length anyway), so a step is add / min
+//    / read / compare / select;
+//  - ballots come straight from the compares (one v_cmp into an SGPR pair)
+//    and every lane-conditional value is a select on such a mask: no
+//    divergent branches before the output stores;
+//  - the run-head flags of both sides are ds_permute scatters (lanes that
+//    own no member send to lane 0, which always starts a run), not LDS
+//    stores + loads;
+//  - values the next phase needs from another lane (the other side's top
+//    clock at a dot's actor, a run start, a member's partner / union slot)
+//    are ds_bpermute gathers from registers;
+//  - the union descriptor is one u16 per union slot (L index + 1 | R index
+//    + 1 << 8): both sides store their byte, shared keys land in one slot.
+// LDS scratch (per wave, k3Scratch bytes): msL / msR member masks (the
+// output table overlays them once read), equal/>= masks by union slot, the
+// union descriptors, a per-lane sink for the atomics of lanes with nothing
+// to add. Returns the output's 16-B pieces, or kLeanFallback (a dot actor
+// >= A, or a union of more than 64 members).
+// ======================================================================
+constexpr uint32_t k3MsL = 0, k3MsR = 512, k3Out = 0, k3EqGe = 1024, k3Desc = 1536, k3Trash = 1664;
+constexpr uint32_t k3Scratch = 2176;  // <= kMask1Scratch: the kernel's scratch also serves mask_object
+
+typedef const __attribute__((address_space(3))) uint64_t lds_cu64;
+typedef const __attribute__((address_space(3))) uint32_t lds_cu32;
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+__device__ __forceinline__ uint64_t lr64(uint32_t a) { return *(lds_cu64*)(size_t)a; }
+__device__ __forceinline__ uint32_t lr32(uint32_t a) { return *(lds_cu32*)(size_t)a; }
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) void*)p;
+}
+// ballots of compares: one v_cmp writing the wave mask (LLVM icmp predicates)
+constexpr int kEQ = 32, kNE = 33, kUGT = 34, kUGE = 35;
+template <int P>
+__device__ __forceinline__ uint64_t cmp64(uint64_t a, uint64_t b) {
+  return __builtin_amdgcn_uicmpl(a, b, P);
+}
+template <int P>
+__device__ __forceinline__ uint64_t cmp32(uint32_t a, uint32_t b) {
+  return __builtin_amdgcn_uicmp(a, b, P);
+}
+// this lane's bit of a wave mask, used straight as the select condition (no VALU)
+__device__ __forceinline__ bool bit_of(uint64_t m, uint32_t) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+__device__ __forceinline__ uint64_t lanes_below(uint32_t n) { return n >= 64u ? ~0ull : (1ull << n) - 1ull; }
+__device__ __forceinline__ uint32_t gather32(uint32_t v, uint32_t src_lane) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
+}
+__device__ __forceinline__ uint64_t gather64(uint64_t v, uint32_t src_lane) {
+  return ((uint64_t)gather32((uint32_t)(v >> 32), src_lane) << 32) | gather32((uint32_t)v, src_lane);
+}
+// lane k's value moved to lane k + 1 (lane 0 gets 0): DPP wave_shr:1 (gfx9)
+__device__ __forceinline__ uint32_t shift_up1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+
+// Copy an LDS-assembled record of n16 16-B pieces (1 <= n16 <= 128) to HBM:
+// two stores per lane, always; lanes past the record repeat its last piece
+// (the same bytes to the same address), so no lane needs a branch or a sink.
+// After a fallback the caller passes n16 = 1: piece 0 of the object's output
+// region gets garbage that the general kernel overwrites.
+__device__ __forceinline__ void copy_record_out(uint32_t src, uint8_t* O, uint32_t n16, uint32_t lane) {
+  const uint32_t i0 = lane < n16 ? lane : n16 - 1u, i1 = lane + kWave < n16 ? lane + kWave : n16 - 1u;
+  const u32x4 p0 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(src + 16u * i0);
+  const u32x4 p1 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(src + 16u * i1);
+  __builtin_nontemporal_store(p0, (u32x4*)(O + 16u * i0));
+  __builtin_nontemporal_store(p1, (u32x4*)(O + 16u * i1));
+}
+
+template <uint32_t OUTCAP, int OUT = 0>  // OUT: 0 direct stores, 1 sink-predicated, 2 LDS-assembled
+__device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint32_t uX, uint8_t* O, uint32_t A,
+                                                 uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane,
+                                                 bool& big, uint8_t* sink = nullptr) {
+  big = false;
+  const uint32_t key = kHdrBytes + 8u * A;
+  const uint32_t ctrL = key + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
+  const uint32_t ctrR = key + 8u * nR, actR = ctrR + 8u * dR, endR = actR + 4u * dR;
+  const uint32_t l4 = 4u * lane, l8 = 8u * lane;
+  const uint64_t mnL = lanes_below(nL), mnR = lanes_below(nR), mdL = lanes_below(dL), mdR = lanes_below(dR);
+
+  // ---- every lane-indexed element of both records: dots (actor, counter),
+  // member keys and run ends, top-clock entries (all loads independent)
+  const uint32_t xl = lr32(uL + actL + l4), xr = lr32(uR + actR + l4);
+  const uint64_t vl = lr64(uL + ctrL + l8), vr = lr64(uR + ctrR + l8);
+  const uint64_t kl = lr64(uL + key + l8), kr = lr64(uR + key + l8);
+  const uint32_t el = lr32(uL + endL + l4), er = lr32(uR + endR + l4);
+  const uint64_t tl = lr64(uL + kHdrBytes + l8), tr = lr64(uR + kHdrBytes + l8);  // lane a: actor a's counter
+  // fallback: a dot actor >= A (here) or a union past 64 members (below).
+  // With OUT != 0 the join runs on (every access stays in the wave's scratch /
+  // 64-lane ranges) and only its stores go to the sink, so that every object
+  // issues the same stores; otherwise it returns at once.
+  bool fb = ((cmp32<kUGE>(xl, A) & mdL) | (cmp32<kUGE>(xr, A) & mdR)) != 0ull;
+  if (OUT == 0 && fb) return kLeanFallback;
+
+  // ---- member alignment by rank (self first on equal keys): L lanes count
+  // R keys < kl, R lanes count L keys < kr; probe address = key[b - 1]
+  const uint32_t rk0 = uR + key - 8u, rkmax = uR + key + 8u * nR - 8u;
+  const uint32_t lk0 = uL + key - 8u, lkmax = uL + key + 8u * nL - 8u;
+  uint32_t pl = rk0, pr = lk0;
+  {
+    const uint32_t n = nL > nR ? nL : nR;
+    for (uint32_t step = n ? 8u << (31u - __builtin_clz(n)) : 0u; step >= 8u; step >>= 1) {
+      const uint32_t cl = pl + step, cr = pr + step;
+      const uint64_t kcl = lr64(cl < rkmax ? cl : rkmax), kcr = lr64(cr < lkmax ? cr : lkmax);
+      pl = kcl < kl ? cl : pl;
+      pr = kcr < kr ? cr : pr;
+    }
+  }
+  pl = pl < rkmax ? pl : rkmax;
+  pr = pr < lkmax ? pr : lkmax;
+  const uint32_t rl = (pl - rk0) >> 3, rr = (pr - lk0) >> 3;  // # R keys < kl, # L keys < kr
+  const uint64_t kel = lr64(pl + 8u < rkmax ? pl + 8u : rkmax), ker = lr64(pr + 8u < lkmax ? pr + 8u : lkmax);
+  // (an empty other side has no key to be equal to: the clamped probe read
+  // the word before its key section)
+  const uint64_t EL = nR ? cmp64<kEQ>(kel, kl) & mnL : 0ull, ER = nL ? cmp64<kEQ>(ker, kr) & mnR : 0ull;
+  const uint32_t U = nL + nR - (uint32_t)__popcll(EL);
+  fb = fb || U > (uint32_t)kWave;
+  if (OUT == 0 && fb) return kLeanFallback;
+  const uint32_t ul = lane + rl - mbcnt64(EL), ur = lane + rr - mbcnt64(ER);  // union slots
+
+  // ---- the member of every dot: run heads scattered by ds_permute (lanes
+  // without a member target lane 0, a head whenever there is a member)
+  const uint32_t sl = shift_up1(el), sr = shift_up1(er);  // run starts
+  const uint32_t hl = (uint32_t)__builtin_amdgcn_ds_permute((int)((bit_of(mnL, lane) ? sl : 0u) << 2), 1);
+  const uint32_t hr = (uint32_t)__builtin_amdgcn_ds_permute((int)((bit_of(mnR, lane) ? sr : 0u) << 2), 1);
+  const uint64_t HL = cmp32<kNE>(hl, 0u) & mdL, HR = cmp32<kNE>(hr, 0u) & mdR;
+  const uint32_t ml = __builtin_amdgcn_mbcnt_hi((uint32_t)(HL >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)HL, hl - 1u));
+  const uint32_t mr = __builtin_amdgcn_mbcnt_hi((uint32_t)(HR >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)HR, hr - 1u));
+
+  // ---- dots above the OTHER side's pre-merge top clock (survives masks)
+  const uint64_t SL = cmp64<kUGT>(vl, gather64(tr, xl & 31u)) & mdL;
+  const uint64_t SR = cmp64<kUGT>(vr, gather64(tl, xr & 31u)) & mdR;
+
+  // ---- scratch: zero the mask tables and union descriptors, then the
+  // per-member {actor mask, survives mask} by 64-bit atomic ORs
+  const uint32_t trash = uX + k3Trash + l8;
+  *(lds_u64*)(size_t)(uX + k3MsL + l8) = 0ull;
+  *(lds_u64*)(size_t)(uX + k3MsR + l8) = 0ull;
+  *(lds_u64*)(size_t)(uX + k3EqGe + l8) = 0ull;
+  *(lds_u16*)(size_t)(uX + k3Desc + 2u * lane) = (uint16_t)0;
+  wave_sync();
+  const uint32_t bl = 1u << (xl & 31u), br = 1u << (xr & 31u);
+  {
+    const uint64_t ol = ((uint64_t)(bit_of(SL, lane) ? bl : 0u) << 32) | (bit_of(mdL, lane) ? bl : 0u);
+    const uint64_t orr = ((uint64_t)(bit_of(SR, lane) ? br : 0u) << 32) | (bit_of(mdR, lane) ? br : 0u);
+    __hip_atomic_fetch_or((lds_u64*)(size_t)(bit_of(mdL, lane) ? uX + k3MsL + 8u * ml : trash), ol,
+                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or((lds_u64*)(size_t)(bit_of(mdR, lane) ? uX + k3MsR + 8u * mr : trash), orr,
+                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // union descriptors: L lanes store index + 1 in the low byte of their
+    // slot, R lanes in the high byte (a shared key: both, same slot)
+    *(lds_u8*)(size_t)(bit_of(mnL, lane) ? uX + k3Desc + 2u * ul : trash) = (uint8_t)(lane + 1u);
+    *(lds_u8*)(size_t)(bit_of(mnR, lane) ? uX + k3Desc + 2u * ur + 1u : trash) = (uint8_t)(lane + 1u);
+  }
+  wave_sync();
+
+  // ---- actors on both sides of a shared member: equal / self >= other,
+  // by the R dots (partner L member i and union slot u of the dot's member
+  // come from the R member lane; L's dot of the same actor by rank in ML)
+  const uint32_t pj = bit_of(ER, lane) ? (0x10000u | (ur << 8) | rr) : 0u;
+  const uint32_t q = gather32(pj, mr);
+  {
+    const uint32_t i = q & 63u, u = (q >> 8) & 63u;
+    const uint32_t MLi = lr32(uX + k3MsL + 8u * i);
+    const uint32_t a0 = gather32(sl, i);
+    const uint32_t idx = a0 + __popc(MLi & (br - 1u));
+    const uint64_t va = lr64(uL + ctrL + 8u * idx);
+    const uint64_t SH = cmp32<kNE>(q & 0x10000u, 0u) & cmp32<kNE>(MLi & br, 0u) & mdR;
+    const uint64_t EQ = cmp64<kEQ>(va, vr) & SH, GE = cmp64<kUGE>(va, vr) & SH;
+    const uint64_t o = ((uint64_t)(bit_of(GE, lane) ? br : 0u) << 32) | (bit_of(EQ, lane) ? br : 0u);
+    __hip_atomic_fetch_or((lds_u64*)(size_t)(bit_of(SH, lane) ? uX + k3EqGe + 8u * u : trash), o, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  wave_sync();
+
+  // ---- per union member: the mask join
+  const uint32_t dsc = *(const __attribute__((address_space(3))) uint16_t*)(size_t)(uX + k3Desc + 2u * lane);
+  const uint32_t mi = (dsc - 1u) & 63u, mj = ((dsc >> 8) - 1u) & 63u;
+  const uint64_t pL = lr64(uX + k3MsL + 8u * mi), pR = lr64(uX + k3MsR + 8u * mj), pE = lr64(uX + k3EqGe + l8);
+  const uint64_t mU = lanes_below(U);
+  const uint64_t hasL = cmp32<kNE>(dsc & 0xFFu, 0u) & mU, hasR = cmp32<kNE>(dsc >> 8, 0u) & mU;
+  const uint64_t selfonly = hasL & ~hasR;
+  const uint32_t ML = bit_of(hasL, lane) ? (uint32_t)pL : 0u, FL = (uint32_t)(pL >> 32) & ML;
+  const uint32_t MR = bit_of(hasR, lane) ? (uint32_t)pR : 0u, FR = (uint32_t)(pR >> 32) & MR;
+  const uint32_t EQm = (uint32_t)pE, GEm = (uint32_t)(pE >> 32);  // zero unless both sides
+  const uint32_t lp = bit_of(selfonly, lane) ? ML : FL, rp = FR;
+  const uint32_t useA = (ML & MR & EQm) | (lp & (~rp | GEm));
+  const uint64_t dropS = cmp32<kEQ>(FL, 0u) & selfonly;  // self-only entry not above R's clock: dropped whole
+  const uint32_t keep = (bit_of(dropS, lane) || !bit_of(mU, lane)) ? 0u : (useA | rp);
+  const uint32_t useK = useA & keep;
+  const uint32_t c = __popc(keep);
+
+  // ---- output layout
+  const uint64_t keepm = cmp32<kNE>(c, 0u);
+  const uint32_t tot_mem = (uint32_t)__popcll(keepm);
+  const uint32_t cincl = scan_incl(c);
+  const uint32_t tot_dot = lane_of(cincl, kWave - 1);
+  const uint32_t o_key = kHdrBytes + 8u * A, o_dctr = o_key + 8u * tot_mem, o_dact = o_dctr + 8u * tot_dot;
+  const uint32_t o_mdend = o_dact + 4u * tot_dot, o_mpad = o_mdend + 4u * tot_mem;
+  const uint32_t o_def = (o_mpad + 7u) & ~7u, size = (o_def + 15u) & ~15u;
+  if (OUT == 0 && size > OUTCAP) {
+    big = true;
+    return 0u;
+  }
+  const uint32_t d0 = cincl - c;
+  if (OUT < 2) *(__attribute__((address_space(3))) u32x4*)(size_t)(uX + k3Out + 16u * lane) = u32x4{keep, useK, d0, 0u};
+  const uint32_t midx = mbcnt64(keepm);
+  const uint64_t kk = lr64(bit_of(hasL, lane) ? uL + key + 8u * mi : uR + key + 8u * mj);
+  const uint32_t xl2 = xl, xr2 = xr;
+  const uint64_t vl2 = vl, vr2 = vr;
+  const uint64_t top = tl > tr ? tl : tr;  // top clock: pointwise max (:153)
+  wave_sync();
+  // every kept dot at its member's base + the rank of its actor in keep
+  const uint32_t gl = gather32(ul, ml), gr = gather32(ur, mr);
+  u32x4 ol, orr;
+  if (OUT >= 2) {  // {keep, useK, base} of the dot's member straight from the union lane's registers
+    ol = u32x4{gather32(keep, gl), gather32(useK, gl), gather32(d0, gl), 0u};
+    orr = u32x4{gather32(keep, gr), gather32(useK, gr), gather32(d0, gr), 0u};
+  } else {
+    ol = *(const __attribute__((address_space(3))) u32x4*)(size_t)(uX + k3Out + 16u * (gl & 63u));
+    orr = *(const __attribute__((address_space(3))) u32x4*)(size_t)(uX + k3Out + 16u * (gr & 63u));
+  }
+  const uint32_t il = ol.z + __popc(ol.x & (bl - 1u)), ir = orr.z + __popc(orr.x & (br - 1u));
+  const bool wl = bit_of(mdL, lane) && (ol.y & bl) != 0u;           // self dots that survive
+  const bool wr = bit_of(mdR, lane) && (orr.x & ~orr.y & br) != 0u;  // other dots kept, not under a self dot
+  if (OUT >= 2) {
+    // the record is assembled in LDS over the (now dead) input stage, then
+    // copied out with two 16-B stores per lane (sink-predicated): 2 vector
+    // store instructions per object instead of ~10 scattered ones, which
+    // occupied the texture-address unit (TA_BUSY 62-65 % of the kernel)
+    fb = fb || size > 2u * 16u * kWave;  // larger outputs: the general kernel
+    wave_sync();  // every read of the input stage (kk above) is done
+    const uint32_t tw = uX + k3Trash + l8;
+    *(lds_u64*)(size_t)(bit_of(keepm, lane) ? uL + o_key + 8u * midx : tw) = kk;
+    *(lds_u32*)(size_t)(bit_of(keepm, lane) ? uL + o_mdend + 4u * midx : tw) = d0 + c;
+    *(lds_u64*)(size_t)(lane < A ? uL + kHdrBytes + l8 : tw) = top;
+    *(lds_u32*)(size_t)(wl ? uL + o_dact + 4u * il : tw) = xl2;
+    *(lds_u64*)(size_t)(wl ? uL + o_dctr + 8u * il : tw) = vl2;
+    *(lds_u32*)(size_t)(wr ? uL + o_dact + 4u * ir : tw) = xr2;
+    *(lds_u64*)(size_t)(wr ? uL + o_dctr + 8u * ir : tw) = vr2;
+    const bool mp = lane == 0u && o_def != o_mpad;
+    const bool rp = lane >= 1u && lane < 4u && o_def + 4u * (lane - 1u) < size;
+    *(lds_u32*)(size_t)(mp ? uL + o_mpad : rp ? uL + o_def + 4u * (lane - 1u) : tw) = 0u;
+    const u32x4 hv = lane == 0u ? u32x4{size, A, tot_mem, tot_dot} : u32x4{0u, 0u, 0u, 0u};
+    *(__attribute__((address_space(3))) u32x4*)(size_t)(lane < 2u ? uL + 16u * lane : uX + k3Trash + 16u * (lane & 31u)) =
+        hv;  // (16-B sink slots: lanes l and l + 32 share one, inside the 512-B sink)
+    if (OUT == 2) {  // OUT 3: the caller copies the record out
+      wave_sync();
+      copy_record_out(uL, O, fb ? 1u : size / 16u, lane);
+    }
+  } else if (OUT == 1) {
+    // every store below is issued by every object: a lane with nothing to
+    // store writes the wave's sink instead (selects, no branches)
+    const bool kc = bit_of(keepm, lane) && !fb;
+    *(uint64_t*)(kc ? O + o_key + 8u * midx : sink) = kk;
+    *(uint32_t*)(kc ? O + o_mdend + 4u * midx : sink + 8) = d0 + c;
+    *(uint64_t*)(lane < A && !fb ? O + kHdrBytes + l8 : sink + 16) = top;
+    uint32_t* oact = (uint32_t*)(O + o_dact);
+    uint64_t* octr = (uint64_t*)(O + o_dctr);
+    *(uint32_t*)(wl && !fb ? (uint8_t*)(oact + il) : sink + 24) = xl2;
+    *(uint64_t*)(wl && !fb ? (uint8_t*)(octr + il) : sink + 32) = vl2;
+    *(uint32_t*)(wr && !fb ? (uint8_t*)(oact + ir) : sink + 24) = xr2;
+    *(uint64_t*)(wr && !fb ? (uint8_t*)(octr + ir) : sink + 32) = vr2;
+    // zero padding (member block to 8: <= 4 B, record to 16: <= 12 B) and the header
+    const bool mp = lane == 0u && o_def != o_mpad && !fb;
+    const bool rp = lane >= 1u && lane < 4u && o_def + 4u * (lane - 1u) < size && !fb;
+    *(uint32_t*)(mp ? O + o_mpad : rp ? O + o_def + 4u * (lane - 1u) : sink + 40) = 0u;
+    const u32x4 hv = lane == 0u ? u32x4{size, A, tot_mem, tot_dot} : u32x4{0u, 0u, 0u, 0u};
+    *(u32x4*)(lane < 2u && !fb ? O + 16u * lane : sink + 48) = hv;
+  } else {
+    if (c != 0u) {
+      *(uint64_t*)(O + o_key + 8u * midx) = kk;
+      *(uint32_t*)(O + o_mdend + 4u * midx) = d0 + c;
+    }
+    if (lane < A) *(uint64_t*)(O + kHdrBytes + l8) = top;
+    uint32_t* oact = (uint32_t*)(O + o_dact);
+    uint64_t* octr = (uint64_t*)(O + o_dctr);
+    if (wl) {
+      oact[il] = xl2;
+      octr[il] = vl2;
+    }
+    if (wr) {
+      oact[ir] = xr2;
+      octr[ir] = vr2;
+    }
+    if (lane == 0u && o_def != o_mpad) *(uint32_t*)(O + o_mpad) = 0u;
+    if (lane >= 1u && lane < 4u && o_def + 4u * (lane - 1u) < size) *(uint32_t*)(O + o_def + 4u * (lane - 1u)) = 0u;
+    if (lane == 0u) {
+      u32x4* h = (u32x4*)O;
+      h[0] = u32x4{size, A, tot_mem, tot_dot};
+      h[1] = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  return OUT != 0 && fb ? kLeanFallback : size / 16u;
+}
+
 #ifdef CRDT_DIAG
 // ======================================================================
 // (Diagnostic build only.) Mask path v2 (v7): the same mask join as mask_object with fewer dependent
@@ -1948,6 +2254,13 @@ __device__ __forceinline__ void stage_all(u32x4* dst, const u32x4 (&r)[kPer], ui
 #pragma unroll
   for (uint32_t k = 0; k < kPer; ++k) dst[lane + k * kWave] = r[k];
 }
+// Only the 64-piece rounds a record of n16 pieces reaches (n16 wave-uniform).
+__device__ __forceinline__ void stage_used(u32x4* dst, const u32x4 (&r)[kPer], uint32_t n16, uint32_t lane) {
+  dst[lane] = r[0];
+#pragma unroll
+  for (uint32_t k = 1; k < kPer; ++k)
+    if (n16 > k * kWave) dst[lane + k * kWave] = r[k];
+}
 
 #ifdef CRDT_DIAG
 // (Diagnostic build only: the v4 merge-path kernel and its variants.)
@@ -2113,7 +2426,9 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
 // flagged for the general kernel. Only the mask path lives here, which keeps
 // the register budget low enough for 5 waves per SIMD.
 // ======================================================================
-template <int MINW, int ABL = 0, bool M2 = false>  // ABL 9: phase stamps; M2: mask2_object
+// ABL 9: phase stamps; M2: mask2_object (diagnostic); M3: mask3_object for
+// the objects without deferred removes
+template <int MINW, int ABL = 0, bool M2 = false, bool M3 = false, bool SINK = false>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
@@ -2130,6 +2445,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kern
   const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
   const uint64_t rounds = (n_obj + n_waves * kWave - 1) / (n_waves * kWave);
   const uint64_t cs = (n_obj + n_waves * rounds - 1) / (n_waves * rounds);
+  // the wave's store sink: after the list in the context's scratch (ctx.h)
+  uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
   Stamps st{};
   if (ABL == 9) st.last = stamp();
   for (uint64_t cbase = wave_id * cs; cbase < n_obj; cbase += n_waves * cs) {
@@ -2205,7 +2522,10 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kern
                                                      m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, &st);
       } else
 #endif
-      if ((defs >> t) & 1ull) {
+      if (M3 && !((defs >> t) & 1ull)) {
+        r = mask3_object<0xFFFFFFFFu, SINK ? 1 : 0>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
+                                            d & 0xFFFFu, m >> 16, d >> 16, lane, big, sink);
+      } else if ((defs >> t) & 1ull) {
         r = mask_object<0xFFFFFFFFu, true, ABL>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
                                                  m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, &st);
       } else {
@@ -2225,6 +2545,229 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kern
 #pragma unroll
     for (int k = 0; k < 8; ++k) v = lane == (uint32_t)k ? st.acc[k] : v;
     list[wave_id * 8u + lane] = v;
+  }
+}
+
+// ======================================================================
+// Join kernel (v8): the product path. Two passes over the batch with one
+// kernel body:
+//  MODE 1 (join pass): objects without deferred removes that fit the mask
+//    join are joined by mask3_object; objects with deferred removes are
+//    flagged kPendingHD for the deferred pass; anything else (records past
+//    the stage, > 64 members / dots, A > 32, > 32 deferred clocks) is flagged
+//    kPending and listed for orswot_merge_general_kernel.
+//  MODE 2 (deferred pass): the kPendingHD objects, joined by
+//    mask_object<HD = true> (src/orswot.rs:141-157 with apply_deferred).
+// Splitting the deferred objects out keeps the join pass's object loop on
+// one path whose vector-memory operations are the same for every object —
+// the next object's record prefetch (re-prefetching the current one after
+// the last object of a chunk), then mask3_object's sink-predicated stores —
+// so the compiler's vmcnt accounting at the loop head waits for the
+// prefetch and not for the previous object's store acknowledgements (loads
+// and stores share vmcnt in issue order on gfx9). A fallback inside the
+// loop (a union past 64 members, a dot actor >= A) sets kPending by a
+// predicated store and raises ctl[1], which makes the general kernel scan
+// the offsets for flags instead of reading the list.
+// ======================================================================
+constexpr uint64_t kPendingHD = 1ull << 62;  // Ooff flag: object left for the deferred pass
+
+// The join of an object with deferred removes (mask_object<HD>, output
+// assembled in the wave's LDS output stage), kept out of line: its register
+// demand then stays out of the join kernel's loop (7 % of config-3 objects
+// pay for the call; the other 93 % keep the lean loop's occupancy).
+__attribute__((noinline)) __device__ uint32_t hd_join(const uint8_t* Ls, const uint8_t* Rs, uint8_t* X, u32x4* Os,
+                                                      uint32_t A, uint32_t m, uint32_t d, uint32_t lane,
+                                                      bool* big) {
+  bool b = false;
+  const uint32_t r = mask_object<kFastStage, true>(Ls, Rs, X, Os, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16,
+                                                   lane, b);
+  *big = b;
+  return r;
+}
+
+// HDD (MODE 3): the deferred objects' join writes straight to HBM
+// (mask_object<HD>) and is followed by the same tail stores as the other
+// path, redirected to the sink: every path issues at least as many stores
+// after the prefetch as the lean one, so its loop-head wait stays exact
+template <int MINW, int MODE, int OUT = 2, bool HDD = false>
+__global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kernel(
+    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
+    const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
+    uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
+    int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
+  __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
+  __shared__ u32x4 scr_s[kWavesPerBlock][(MODE == 1 ? k3Scratch : kMask1Scratch) / 16];
+  __shared__ u32x4 out_s[kWavesPerBlock][MODE == 3 && !HDD ? kFastStage / 16 : 1];  // assembled outputs (deferred objects)
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t wave = uni(threadIdx.x / kWave);  // wave-uniform: LDS bases in SGPRs
+  u32x4* const sL = stage_s[wave][0];
+  u32x4* const sR = stage_s[wave][1];
+  uint8_t* const X = (uint8_t*)scr_s[wave];
+  const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint64_t rounds = (n_obj + n_waves * kWave - 1) / (n_waves * kWave);
+  const uint64_t cs = (n_obj + n_waves * rounds - 1) / (n_waves * rounds);
+  uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
+  uint64_t* const dlist = (uint64_t*)((uint8_t*)(list + kDefaultListCap) + kTrashBytes);  // deferred objects
+  // MODE 2 reads the deferred list in chunks of 64 entries when it did not
+  // overflow, else scans every object's flag
+  const uint32_t n_def = MODE == 2 ? uni(__hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : 0u;
+  const bool listed = MODE == 2 && n_def <= kDeferListCap;
+  const uint64_t n_items = listed ? n_def : n_obj;
+  const uint64_t cs2 = listed ? kWave : cs;
+  for (uint64_t cbase = wave_id * cs2; cbase < n_items; cbase += n_waves * cs2) {
+    // ---- chunk state: lane k <-> object cbase + k (MODE 2 listed: entry cbase + k)
+    const uint64_t item = cbase + lane;
+    const bool valid = lane < cs2 && item < n_items;
+    const uint64_t obj = listed ? (valid ? dlist[item] : 0ull) : item;
+    uint64_t lo = 0, ro = 0;
+    u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
+    bool fast;
+    uint64_t defs = 0ull;  // MODE 3: the chunk's objects with deferred removes
+    if (MODE != 2) {
+      uint64_t nlo = Lbytes, nro = Rbytes;
+      if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
+      if (valid && obj + 1u < n_obj) { nlo = Loff[obj + 1u]; nro = Roff[obj + 1u]; }  // same lines: coalesced
+      bool ok = valid && (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes && ro + kHdrBytes <= Rbytes;
+      if (ok) {
+        hl0 = ((const u32x4*)(Lb + lo))[0]; hl1 = ((const u32x4*)(Lb + lo))[1];
+        hr0 = ((const u32x4*)(Rb + ro))[0]; hr1 = ((const u32x4*)(Rb + ro))[1];
+      }
+      ok = ok && header_ok(hl0, hl1, lo, Lbytes, A) && header_ok(hr0, hr1, ro, Rbytes, A) &&
+           lo + ro + (uint64_t)hl0.x + hr0.x <= Obytes;
+      // output placement precondition (out[i] at self.off[i] + other.off[i]):
+      // each side's records in increasing offset order, none overlapping the next
+      const bool placed = !ok || (nlo >= lo + hl0.x && nro >= ro + hr0.x);
+      if (__ballot(!placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_EINVAL);
+      ok = ok && placed;
+      const bool fits = ok && hl0.x <= kFastStage && hr0.x <= kFastStage && A <= 32u && hl0.z <= 64u &&
+                        hr0.z <= 64u && hl0.w <= 64u && hr0.w <= 64u;
+      const bool hd = fits && (hl1.x | hr1.x) != 0u && hl1.x <= 32u && hr1.x <= 32u;
+      fast = fits && (hl1.x | hr1.x) == 0u;
+      if (MODE == 3) {  // one pass: deferred objects joined here too
+        defs = __ballot(hd);
+        fast = fast || hd;
+      }
+      const bool gen = ok && !fast && !hd;
+      if (valid) Ooff[obj] = (lo + ro) | (gen ? kPending : 0ull) | (MODE == 1 && hd ? kPendingHD : 0ull);
+      if (MODE == 1) {  // list the deferred objects for the deferred pass
+        const uint64_t hm = __ballot(hd);
+        if (hm != 0ull) {
+          uint32_t base = 0;
+          if (lane == 0u) base = atomicAdd(&ctl[2], (uint32_t)__popcll(hm));
+          base = uni(base) + mbcnt64(hm);
+          if (hd && base < kDeferListCap) dlist[base] = obj;
+        }
+      }
+      if (gen) {  // hand the object to the general kernel
+        const uint32_t e = atomicAdd(&ctl[0], 1u);
+        if (e < list_cap) list[e] = obj;
+      }
+      if (__ballot(valid && !ok && placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
+    } else {  // the deferred pass: objects the join pass flagged kPendingHD (validated there)
+      const uint64_t fo = valid ? Ooff[obj] : 0ull;
+      fast = valid && (fo & kPendingHD) != 0ull;
+      if (fast) {
+        lo = Loff[obj];
+        ro = Roff[obj];
+        hl0 = ((const u32x4*)(Lb + lo))[0]; hl1 = ((const u32x4*)(Lb + lo))[1];
+        hr0 = ((const u32x4*)(Rb + ro))[0]; hr1 = ((const u32x4*)(Rb + ro))[1];
+      }
+    }
+    const uint64_t runs = __ballot(fast);
+    if (runs == 0ull) continue;
+    const uint32_t n16 = fast ? (hl0.x / 16u) | ((hr0.x / 16u) << 16) : 0u;
+    const uint32_t nm = hl0.z | (hr0.z << 16), nd = hl0.w | (hr0.w << 16);
+
+    // ---- software pipeline: the next object's records are in flight while
+    // the current one is joined from LDS. The loop is rotated so the wait for
+    // a prefetch (stage) has one predecessor, the previous object's stores:
+    // the compiler then lets those stores stay outstanding (vmcnt counts them
+    // as younger) instead of draining them at a merge with the prologue.
+    uint64_t pend = runs;
+    uint32_t t = (uint32_t)__builtin_ctzll(pend);
+    pend &= pend - 1;
+    u32x4 pl[kPer], pr[kPer];
+    {
+      const uint32_t nn = lane_of(n16, t);
+      prefetch_all(pl, Lb + lane_of64(lo, t), nn & 0xFFFFu, lane);
+      prefetch_all(pr, Rb + lane_of64(ro, t), nn >> 16, lane);
+    }
+    wave_sync();  // the previous chunk's last LDS reads are done
+    stage_all(sL, pl, lane);
+    stage_all(sR, pr, lane);
+    wave_sync();
+    for (;;) {
+      const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
+      const uint32_t m = lane_of(nm, t), d = lane_of(nd, t);
+      // the next object, or this one again after the chunk's last (a constant load count)
+      const uint32_t u = pend ? (uint32_t)__builtin_ctzll(pend) : t;
+      {
+        const uint32_t nu = lane_of(n16, u);
+        prefetch_all(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
+        prefetch_all(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
+      }
+      bool big = false;
+      uint32_t r;
+      if (MODE == 1) {
+        r = mask3_object<0xFFFFFFFFu, OUT>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
+                                            d & 0xFFFFu, m >> 16, d >> 16, lane, big, sink);
+        // fallback (union past 64 members / dot actor >= A): the general
+        // kernel, which finds it by its flag. Both stores are issued for every
+        // object (the store count stays fixed): the offset is rewritten with
+        // or without the flag, and the scan request goes to ctl[1] or to the
+        // wave's sink word (wave-uniform addresses and values)
+        const bool fbu = r == kLeanFallback;
+        *(Ooff + cbase + t) = oo | (fbu ? kPending : 0ull);
+        *(fbu ? ctl + 1 : (uint32_t*)sink) = 1u;  // the wave's own sink word: no shared line
+      } else if (MODE == 3) {
+        // both joins assemble the record in LDS (mask3_object over its input
+        // stage, mask_object<HD> in the wave's output stage); one copy-out
+        // and the fallback stores follow either: the same vector-memory
+        // operations for every object
+        uint32_t src;
+        bool direct = false;
+        if ((defs >> t) & 1ull) {
+          if (HDD) {
+            r = mask_object<0xFFFFFFFFu, true>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
+                                               m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big);
+            direct = true;
+          } else {
+            r = hd_join((const uint8_t*)sL, (const uint8_t*)sR, X, out_s[wave], A, m, d, lane, &big);
+          }
+          src = lds_addr(out_s[wave]);
+        } else {
+          r = mask3_object<0xFFFFFFFFu, 3>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
+                                           d & 0xFFFFu, m >> 16, d >> 16, lane, big, sink);
+          src = lds_addr(sL);
+        }
+        const bool fbu = big || r == kLeanFallback;  // wave-uniform
+        wave_sync();
+        if (HDD && direct) {  // the same two stores, to the sink
+          const u32x4 z = {0u, 0u, 0u, 0u};
+          __builtin_nontemporal_store(z, (u32x4*)sink);
+          __builtin_nontemporal_store(z, (u32x4*)sink + 1);
+        } else {
+          copy_record_out(src, Ob + oo, fbu ? 1u : r, lane);
+        }
+        *(Ooff + cbase + t) = oo | (fbu ? kPending : 0ull);
+        *(fbu ? ctl + 1 : (uint32_t*)sink) = 1u;  // the wave's own sink word: no shared line
+      } else {
+        r = mask_object<0xFFFFFFFFu, true>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
+                                           m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big);
+        if (lane == 0u) {
+          Ooff[lane_of64(obj, t)] = oo | (r == kLeanFallback ? kPending : 0ull);  // clears kPendingHD
+          if (r == kLeanFallback) ctl[1] = 1u;
+        }
+      }
+      if (pend == 0ull) break;
+      t = u;
+      pend &= pend - 1;
+      wave_sync();  // this object's LDS reads are done
+      stage_used(sL, pl, lane_of(n16, t) & 0xFFFFu, lane);
+      stage_used(sR, pr, lane_of(n16, t) >> 16, lane);
+      wave_sync();
+    }
   }
 }
 
@@ -2284,10 +2827,11 @@ __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
   __shared__ u32x4 gen_s[3][kGenStage / 16];
   const uint32_t lane = threadIdx.x;
   const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  if (n <= list_cap) {
+  const uint32_t scan = uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (n <= list_cap && scan == 0u) {
     for (uint32_t e = blockIdx.x; e < n; e += gridDim.x)
       general_one(Lb, Loff, Rb, Roff, Ob, Ooff, list[e], A, gen_s[0], gen_s[1], gen_s[2], lane);
-  } else {
+  } else {  // list overflow, or objects flagged without a list entry: scan the flags
     const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
     for (uint64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
       const uint64_t obj = chunk * kWave + lane;
@@ -2547,19 +3091,88 @@ __global__ __launch_bounds__(kWave) void orswot_sparse_general_kernel(
 
 }  // namespace
 
+namespace {
+// The join launch: MODE 3 (one pass) or the two passes MODE 1 + MODE 2,
+// then the general kernel.
+template <int MINW, bool ONE = true, bool HDD = false>
+int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
+                       const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
+                       uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
+                       uint32_t list_cap, hipStream_t stream, int blocks_per_cu) {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const void* f1;
+  const void* f2 = nullptr;
+  if constexpr (ONE) {
+    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD>;
+  } else {
+    f1 = (const void*)orswot_join_kernel<MINW, 1>;
+    f2 = (const void*)orswot_join_kernel<MINW, 2>;
+  }
+  static std::atomic<int> occ_cache[2][9];  // per (pass, MINW); HDD variants share: one of them per MINW
+  int occ[2];
+  const void* fs[2] = {f1, f2};
+  const int passes = ONE ? 1 : 2;
+  for (int k = 0; k < passes; ++k) {
+    occ[k] = occ_cache[ONE ? 1 - k : k][MINW].load(std::memory_order_relaxed);
+    if (occ[k] == 0) {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[k], fs[k], kWave * kWavesPerBlock, 0) != hipSuccess ||
+          occ[k] < 1)
+        occ[k] = 4;
+      occ_cache[ONE ? 1 - k : k][MINW].store(occ[k], std::memory_order_relaxed);
+    }
+  }
+  const uint64_t chunks = (n_obj + kWave - 1) / kWave;
+  const uint64_t want = (chunks + kWavesPerBlock - 1) / kWavesPerBlock;
+  void* args[] = {&Lb, &Loff, &Lbytes, &Rb, &Roff, &Rbytes, &Ob, &Ooff, &Obytes, &n_obj, &n_actors, &status,
+                  &ctl, &list, &list_cap};
+  if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
+  for (int k = 0; k < passes; ++k) {
+    const uint64_t cap = (uint64_t)cus * (blocks_per_cu > 0 ? blocks_per_cu : occ[k]);
+    const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
+    if (hipLaunchKernel(fs[k], dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) != hipSuccess)
+      return CRDT_EHIP;
+  }
+  hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
+                     Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
+  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+}
+}  // namespace
+
 int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                         const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff,
                         uint64_t Obytes, uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl,
                         uint64_t* list, uint32_t list_cap, hipStream_t stream, int blocks_per_cu, int variant) {
   if (n_obj == 0) return CRDT_OK;
+  auto go = [&](auto f) {
+    return f(Lb, Loff, Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors, status, ctl, list, list_cap,
+             stream, blocks_per_cu);
+  };
+#ifndef CRDT_DIAG
+  // The product path: orswot_join_kernel in one pass (mask3_object for the
+  // objects without deferred removes, mask_object<HD> for the rest) at 6
+  // waves per SIMD, then the general kernel (measured best, tools/ab_bench.py;
+  // DESIGN.md §4). Other variants exist in -DCRDT_DIAG builds only.
+  (void)variant;
+  return go(launch_join_passes<6, true, true>);
+#else
+  if (variant == 0 || (variant >= 25 && variant <= 31)) {
+    switch (variant) {
+      case 25: return go(launch_join_passes<4, false>);
+      case 26: return go(launch_join_passes<5, false>);
+      case 27: return go(launch_join_passes<6, false>);
+      case 28: return go(launch_join_passes<8, false>);
+      case 29: return go(launch_join_passes<4, true>);
+      case 30: return go(launch_join_passes<5, true, true>);
+      default: return go(launch_join_passes<6, true, true>);  // 0, 31: the product path
+    }
+  }
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  // The product kernel: orswot_mask_kernel at 6 waves per SIMD (measured
-  // best, tools/ab_bench.py). Other variants exist in -DCRDT_DIAG builds only
-  // (101..103 are timing-only ablations whose output is invalid).
+  // round-1 and experimental kernels (101..103: timing-only ablations whose
+  // output is invalid); 11 = the round-1 product (orswot_mask_kernel<6>)
   const void* fn = (const void*)orswot_mask_kernel<6>;
-#ifdef CRDT_DIAG
   switch (variant) {
     case 6: fn = (const void*)orswot_merge_kernel<1, 0, true>; break;
     case 7: fn = (const void*)orswot_merge_kernel<1, 0, false, 0, true>; break;
@@ -2572,6 +3185,13 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
     case 15: fn = (const void*)orswot_mask_kernel<5, 0, true>; break;
     case 16: fn = (const void*)orswot_mask_kernel<5, 9, true>; break;
     case 17: fn = (const void*)orswot_mask_kernel<4, 0, true>; break;
+    case 18: fn = (const void*)orswot_mask_kernel<6, 0, false, true>; break;
+    case 19: fn = (const void*)orswot_mask_kernel<7, 0, false, true>; break;
+    case 20: fn = (const void*)orswot_mask_kernel<5, 0, false, true>; break;
+    case 21: fn = (const void*)orswot_mask_kernel<4, 0, false, true>; break;
+    case 22: fn = (const void*)orswot_mask_kernel<7, 0, false, true, true>; break;
+    case 23: fn = (const void*)orswot_mask_kernel<5, 0, false, true, true>; break;
+    case 24: fn = (const void*)orswot_mask_kernel<6, 0, false, true, true>; break;
     case 111: fn = (const void*)orswot_merge_kernel<1, 0, true, 1>; break;
     case 112: fn = (const void*)orswot_merge_kernel<1, 0, true, 2>; break;
     case 113: fn = (const void*)orswot_merge_kernel<1, 0, true, 3>; break;
@@ -2586,15 +3206,10 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
     case 13: fn = (const void*)orswot_merge_kernel<1, 0, false, 0, true>; break;
     default: break;
   }
-#else
-  variant = 0;
-  blocks_per_cu = 0;
-#endif
   // Resident grid: the kernel's occupancy in 4-wave blocks per CU
   // (blocks_per_cu overrides), no more blocks than 64-object chunks need.
-  static std::atomic<int> occ_cache[26];  // per variant slot, 0 = not yet queried
-  const int slot = variant >= 1 && variant <= 19 ? variant : variant >= 101 && variant <= 103 ? variant - 95
-                   : variant == 109 ? 20 : variant >= 111 && variant <= 113 ? variant - 90 : 0;
+  static std::atomic<int> occ_cache[256];  // per variant, 0 = not yet queried
+  const int slot = variant & 255;
   int occ = occ_cache[slot].load(std::memory_order_relaxed);
   if (occ == 0) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)
@@ -2616,6 +3231,7 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
                      Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+#endif
 }
 
 int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,

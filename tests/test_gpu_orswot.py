@@ -326,3 +326,19 @@ def test_general_path_list_overflow_and_reset(gpu, oracle):
             _compare(_gpu_merge(gpu, cb, co, db, do, 16), ob2, oo2, f"fast after cap {cap}")
     finally:
         gpu.set_list_cap(65536)
+
+
+def test_empty_side_key_equal_to_clock_word(gpu, oracle):
+    """A side without members next to a member whose key equals the word in
+    front of the empty side's key section (its last top-clock counter): the
+    member is self-only / other-only, never matched (regression: the clamped
+    equal-key probe of the join read that word)."""
+    A = 4
+    full = records.encode({0: 1, 3: 2}, {3: {0: 1}, 7: {3: 2}}, {}, A)
+    empty = records.encode({3: 3}, {}, {}, A)  # top clock word [A-1] == 3 == a key of `full`
+    for L, R in ((full, empty), (empty, full)):
+        lb, lo = records.pack_batch([L] * 65 + [R])
+        rb, ro = records.pack_batch([R] * 65 + [L])
+        out = _gpu_merge(gpu, lb, lo, rb, ro, A)
+        ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, A, threads=4)
+        _compare(out, ob, oo, "empty side")

@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(REPO, "rust-crdt_amd"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--variants", default="0,1")
-    ap.add_argument("--bpc", default="8", help="blocks per CU values to sweep")
+    ap.add_argument("--bpc", default="0", help="blocks per CU values to sweep (0: the kernel's occupancy)")
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--n-obj", type=int, default=1_000_000)
     a = ap.parse_args()
@@ -47,11 +47,21 @@ def main():
             eng.status(s)
             if r > 0:
                 res[c].append(e0.elapsed_time(e1))
-            if r == 0 and c[0] < 100 and c not in seen:
+            if r == 0 and c[0] < 100 and c not in seen:  # byte-exact against the first variant
                 seen.add(c)
-                h = out.base.sum().item()
-                ref = h if ref is None else ref
-                assert h == ref, f"variant {c} output differs"
+                with torch.cuda.stream(s):  # same stream as the merge
+                    out.base.zero_()
+                eng.orswot_merge(L, R, out=out, stream=s, check_status=True)
+                s.synchronize()
+                if ref is None:
+                    with torch.cuda.stream(s):  # copied before the next launch on s rewrites out
+                        ref = (out.base.clone(), out.off.clone())
+                    s.synchronize()
+                elif not (torch.equal(out.base, ref[0]) and torch.equal(out.off, ref[1])):
+                    bad = (out.base != ref[0]).nonzero()
+                    bo = (out.off != ref[1]).nonzero().flatten()
+                    raise AssertionError(f"variant {c} output differs: {bad.numel()} bytes, first at {bad[:4].tolist()}; "
+                                         f"{bo.numel()} offsets, e.g. {[(int(i), int(out.off[i]), int(ref[1][i])) for i in bo[:4]]}")
     print(json.dumps({f"v{c[0]}_bpc{c[1]}": {"median_ms": float(np.median(v)), "min_ms": float(np.min(v))}
                       for c, v in res.items()}))
 
