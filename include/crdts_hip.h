@@ -366,6 +366,56 @@ int crdt_map_mvreg_merge(crdt_ctx* ctx, const crdt_map_mvreg_slab* self, const c
                          const crdt_map_mvreg_slab* out, size_t n_obj, uint32_t n_actors, void* stream);
 
 /* ------------------------------------------------------------------------ *
+ * Map<K, Orswot<u64, A>, A>::merge, batched (SURVEY.md §8(f) rank 3 as
+ * written: src/map.rs:192-269 with the nested value's Causal::truncate,
+ * src/orswot.rs:159-172, and Orswot::merge src/orswot.rs:87-157 for keys in
+ * both maps). Keys and members are u64. Dense, fixed-capacity slabs, object
+ * i owning:
+ *   clock[A]                                   the map clock (0 = absent)
+ *   n_keys, keys[kcap] ascending               entries (BTreeMap order)
+ *   eclock[kcap][A]                            entry clocks
+ *   nested Orswot per key:
+ *     vclock[kcap][A]                          its top clock
+ *     vn_mem[kcap], vmem[kcap][mcap]           members, ascending
+ *     vmclock[kcap][mcap][A]                   member clocks (an all-zero row is
+ *                                              an empty member clock, which
+ *                                              truncate may leave in the
+ *                                              reference; reachable states never
+ *                                              hold one)
+ *     vn_def[kcap], vdclock[kcap][vdcap][A]    deferred removes, CLOCK ORDER
+ *     vdset_n[kcap][vdcap], vdset[kcap][vdcap][vscap]   their member sets, ascending
+ *   n_def, dclock[dcap][A]                     the map's deferred removes, CLOCK ORDER
+ *   dset_n[dcap], dset[dcap][scap]             their key sets, ascending
+ * Unused slots are zero on output. Per side kcap, mcap, dcap, scap <= 32,
+ * vdcap, vscap <= 16, n_actors <= 64; output capacities must hold the result
+ * (else CRDT_ECAPACITY is latched for that object). The map's deferred
+ * removes are applied in CLOCK ORDER: the reference iterates a HashMap there
+ * (src/map.rs:325-333) and, with Orswot values, two deferred clocks naming
+ * the same key truncate its set in sequence, which can depend on that order
+ * (DESIGN.md §5e); CLOCK ORDER is one of the reference's possible orders. */
+typedef struct crdt_map_orswot_slab {
+  uint64_t* clock;
+  uint32_t* n_keys;
+  uint64_t* keys;
+  uint64_t* eclock;
+  uint64_t* vclock;
+  uint32_t* vn_mem;
+  uint64_t* vmem;
+  uint64_t* vmclock;
+  uint32_t* vn_def;
+  uint64_t* vdclock;
+  uint32_t* vdset_n;
+  uint64_t* vdset;
+  uint32_t* n_def;
+  uint64_t* dclock;
+  uint32_t* dset_n;
+  uint64_t* dset;
+  uint32_t kcap, mcap, vdcap, vscap, dcap, scap;
+} crdt_map_orswot_slab;
+int crdt_map_orswot_merge(crdt_ctx* ctx, const crdt_map_orswot_slab* self, const crdt_map_orswot_slab* other,
+                          const crdt_map_orswot_slab* out, size_t n_obj, uint32_t n_actors, void* stream);
+
+/* ------------------------------------------------------------------------ *
  * VClock partial order and MVReg merge, batched.
  * crdt_vclock_partial_cmp: d_out[i] = partial_cmp(a[i], b[i])
  * (src/vclock.rs:59-71) over dense rows u64[n][n_actors], 0 = absent:

@@ -254,3 +254,179 @@ class Orswot:
 
     def __eq__(self, other):
         return self.canonical() == other.canonical()
+
+
+class MVReg:
+    """src/mvreg.rs:14-18 — `vals: Vec<(VClock, V)>`; equality is set-like (:74-96)."""
+
+    def __init__(self):
+        self.vals = []
+
+    def clone(self):
+        r = MVReg()
+        r.vals = [(c.clone(), v) for c, v in self.vals]
+        return r
+
+    def truncate(self, clock):  # Causal :100-113
+        out = []
+        for c, v in self.vals:
+            c = c.clone()
+            c.subtract(clock)
+            if not c.is_empty():
+                out.append((c, v))
+        self.vals = out
+
+    def merge(self, other):  # CvRDT :121-153
+        vals = [(c.clone(), v) for c, v in self.vals if not any(c < oc for oc, _ in other.vals)]
+        for c, v in other.vals:
+            if any(c < sc for sc, _ in self.vals):
+                continue
+            if all(ec != c for ec, _ in vals):
+                vals.append((c.clone(), v))
+        self.vals = vals
+
+    def apply_put(self, clock, val):  # CmRDT Op::Put :158-186
+        if clock.is_empty():
+            return
+        self.vals = [(c, v) for c, v in self.vals if not (c <= clock)]
+        if not any(c > clock for c, _ in self.vals):
+            self.vals.append((clock.clone(), val))
+
+    def read(self):
+        return [v for _, v in self.vals]
+
+    def canonical(self):
+        return ("mvreg", tuple(sorted((c.canonical(), v) for c, v in self.vals)))
+
+
+def clock_order(clocks):
+    """CLOCK ORDER: lexicographic over the sorted (actor, counter) pairs."""
+    return sorted(clocks, key=lambda c: c.canonical())
+
+
+class Map:
+    """src/map.rs:82-98 — Map<K, V, A> with V = MVReg or Orswot (`factory`).
+
+    `order` is the iteration order apply_deferred (:325-333) takes over the
+    deferred clocks — a HashMap in the reference, so unspecified; default
+    CLOCK ORDER. With Orswot values the order can matter (see
+    tests/test_map_orswot.py)."""
+
+    def __init__(self, factory, order=clock_order):
+        self.factory = factory
+        self.order = order
+        self.clock = VClock()
+        self.entries = {}   # key -> [entry clock, val]   (BTreeMap)
+        self.deferred = {}  # VClock -> set(key)          (HashMap<VClock, BTreeSet<K>>)
+
+    def clone(self):
+        m = Map(self.factory, self.order)
+        m.clock = self.clock.clone()
+        m.entries = {k: [c.clone(), v.clone()] for k, (c, v) in self.entries.items()}
+        m.deferred = {c.clone(): set(s) for c, s in self.deferred.items()}
+        return m
+
+    def truncate(self, clock):  # Causal :131-158
+        for k in list(self.entries):
+            c, v = self.entries[k]
+            c.subtract(clock)
+            if c.is_empty():
+                del self.entries[k]
+            else:
+                v.truncate(clock)
+        d = {}
+        for c, s in self.deferred.items():
+            c = c.clone()
+            c.subtract(clock)
+            if not c.is_empty():
+                d[c] = set(s)
+        self.deferred = d
+        self.clock.subtract(clock)
+
+    # --- op path (src/map.rs:160-190, 304-323; ctx src/ctx.rs:45-60)
+    def get(self, key):
+        """ReadCtx: (add_clock, rm_clock, val or None), :291-302."""
+        e = self.entries.get(key)
+        return self.clock.clone(), (e[0].clone() if e else VClock()), (e[1] if e else None)
+
+    def apply_up(self, dot, key, inner):
+        """Op::Up {dot, key, op}: `inner(val)` applies the nested op (:169-187)."""
+        actor, counter = dot
+        if self.clock.get(actor) >= counter:
+            return
+        c, v = self.entries.pop(key, [VClock(), self.factory()])
+        c.witness(actor, counter)
+        inner(v)
+        self.entries[key] = [c, v]
+        self.clock.witness(actor, counter)
+        self.apply_deferred()
+
+    def apply_rm(self, key, clock):  # :336-350
+        if not (clock <= self.clock):
+            self.deferred.setdefault(clock.clone(), set()).add(key)
+        e = self.entries.pop(key, None)
+        if e is not None:
+            c, v = e
+            c.subtract(clock)
+            if not c.is_empty():
+                v.truncate(clock)
+                self.entries[key] = [c, v]
+
+    def apply_deferred(self):  # :325-333, in `order`
+        d = {c.clone(): set(s) for c, s in self.deferred.items()}
+        self.deferred = {}
+        for c in self.order(list(d)):
+            for k in sorted(d[c]):
+                self.apply_rm(k, c)
+
+    # --- CvRDT::merge :193-268
+    def merge(self, other):
+        other_remaining = {k: [c.clone(), v.clone()] for k, (c, v) in other.entries.items()}
+        keep = {}
+        for key, (c, v) in [(k, (c.clone(), v.clone())) for k, (c, v) in self.entries.items()]:
+            oe = other.entries.get(key)
+            if oe is None:
+                c.subtract(other.clock)
+                if not c.is_empty():
+                    deleted = other.clock.clone()
+                    deleted.subtract(c)
+                    v.truncate(deleted)
+                    keep[key] = [c, v]
+            else:
+                oc, ov = oe[0].clone(), oe[1].clone()
+                common = c.intersection(oc)
+                c.subtract(common)
+                oc.subtract(common)
+                c.subtract(other.clock)
+                oc.subtract(self.clock)
+                common.merge(c)
+                common.merge(oc)
+                if not common.is_empty():
+                    v.merge(ov)
+                    deleted = c.clone()
+                    deleted.merge(oc)
+                    deleted.subtract(common)
+                    v.truncate(deleted)
+                    keep[key] = [common, v]
+                del other_remaining[key]
+        for key, (c, v) in other_remaining.items():
+            c.subtract(self.clock)
+            if not c.is_empty():
+                deleted = self.clock.clone()
+                deleted.subtract(c)
+                v.truncate(deleted)
+                keep[key] = [c, v]
+        for clock, keys in other.deferred.items():  # apply_rm on the old entries: only the deferral lasts
+            for k in sorted(keys):
+                self.apply_rm(k, clock)
+        self.entries = keep
+        self.clock.merge(other.clock)
+        self.apply_deferred()
+
+    def canonical(self):
+        return (self.clock.canonical(),
+                tuple((k, c.canonical(), v.canonical()) for k, (c, v) in sorted(self.entries.items())),
+                tuple(sorted((c.canonical(), tuple(sorted(s))) for c, s in self.deferred.items())))
+
+    def __eq__(self, other):
+        return self.canonical() == other.canonical()

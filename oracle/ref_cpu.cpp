@@ -30,6 +30,7 @@
 #include <functional>
 #include <map>
 #include <set>
+#include <string>
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
@@ -196,6 +197,17 @@ struct Orswot {
     entries = std::move(keep);                            // :150
     clock.merge(other.clock);                             // :153
     apply_deferred();                                     // :155
+  }
+
+  // Causal::truncate — src/orswot.rs:159-172: merge with an empty set whose
+  // clock is `c`, then forget `c` from the top clock and every member clock
+  // (kept as is even if that empties one).
+  void truncate(const VClock& c) {
+    Orswot empty_set;
+    empty_set.clock = c;
+    merge(empty_set);
+    clock.subtract(c);
+    for (auto& kv : entries) kv.second.subtract(c);
   }
 };
 
@@ -1129,6 +1141,421 @@ int orc_mvreg_merge_batch(const uint32_t* sn, const uint64_t* sclk, const uint64
 void orc_vclock_partial_cmp_rows(const uint64_t* a, const uint64_t* b, size_t n, uint32_t n_actors, int8_t* out) {
   for (size_t i = 0; i < n; ++i)
     out[i] = (int8_t)row_to_vclock(a + i * n_actors, n_actors).partial_cmp(row_to_vclock(b + i * n_actors, n_actors));
+}
+
+
+}  // extern "C"
+
+namespace oracle {
+// ---------------------------------------------------------------- Map<u64, Orswot>
+// Map<u64, Orswot<u64, A>, A> (src/map.rs:82-98) — merge :192-269, apply
+// :163-189, apply_rm :336-350, apply_deferred :325-333 — with the nested
+// Orswot's merge / truncate above. The map's deferred removes are a HashMap
+// in the reference; here a std::map (CLOCK ORDER), and apply_deferred takes
+// an optional permutation of that order (`perm`, for enumerating the orders
+// the reference could take).
+struct MapOrEntry {
+  VClock clock;
+  Orswot val;
+};
+struct MapOrswotO {
+  VClock clock;
+  std::map<uint64_t, MapOrEntry> entries;
+  std::map<std::map<Actor, Counter>, std::set<uint64_t>> deferred;
+  const std::vector<int>* perm = nullptr;
+
+  void apply_rm(uint64_t key, const VClock& c) {  // :336-350
+    if (!c.le(clock)) deferred[c.dots].insert(key);
+    auto it = entries.find(key);
+    if (it != entries.end()) {
+      MapOrEntry e = it->second;
+      entries.erase(it);
+      e.clock.subtract(c);
+      if (!e.clock.is_empty()) {
+        e.val.truncate(c);
+        entries[key] = e;
+      }
+    }
+  }
+  void apply_deferred() {  // :325-333
+    auto d = deferred;
+    deferred.clear();
+    std::vector<std::pair<VClock, std::set<uint64_t>>> v;
+    for (const auto& kv : d) {
+      VClock c;
+      c.dots = kv.first;
+      v.emplace_back(c, kv.second);
+    }
+    if (perm && perm->size() == v.size()) {
+      auto w = v;
+      for (size_t k = 0; k < v.size(); ++k) v[k] = w[(*perm)[k]];
+    }
+    for (const auto& kv : v)
+      for (uint64_t k : kv.second) apply_rm(k, kv.first);
+  }
+  // Op::Up {dot, key, op} with op = the nested Orswot's Add or Rm (:169-187)
+  void apply_up(Actor a, Counter ctr, uint64_t key, int kind, Actor da, Counter dc, uint64_t member,
+                const VClock& rm_clock) {
+    if (clock.get(a) >= ctr) return;
+    MapOrEntry e;
+    auto it = entries.find(key);
+    if (it != entries.end()) { e = it->second; entries.erase(it); }
+    e.clock.witness(a, ctr);
+    if (kind == 0) e.val.apply_add(da, dc, member);
+    else e.val.apply_rm(member, rm_clock);
+    entries[key] = e;
+    clock.witness(a, ctr);
+    apply_deferred();
+  }
+  void merge(const MapOrswotO& other) {  // :193-268
+    std::map<uint64_t, MapOrEntry> keep;
+    for (const auto& kv : entries) {
+      MapOrEntry entry = kv.second;
+      auto oit = other.entries.find(kv.first);
+      if (oit == other.entries.end()) {
+        entry.clock.subtract(other.clock);
+        if (!entry.clock.is_empty()) {
+          VClock del = other.clock;
+          del.subtract(entry.clock);
+          entry.val.truncate(del);
+          keep[kv.first] = entry;
+        }
+      } else {
+        MapOrEntry oe = oit->second;
+        VClock common = entry.clock.intersection(oe.clock);
+        entry.clock.subtract(common);
+        oe.clock.subtract(common);
+        entry.clock.subtract(other.clock);
+        oe.clock.subtract(clock);
+        common.merge(entry.clock);
+        common.merge(oe.clock);
+        if (!common.is_empty()) {
+          entry.val.merge(oe.val);
+          VClock del = entry.clock;
+          del.merge(oe.clock);
+          del.subtract(common);
+          entry.val.truncate(del);
+          entry.clock = common;
+          keep[kv.first] = entry;
+        }
+      }
+    }
+    for (const auto& kv : other.entries) {
+      if (entries.count(kv.first)) continue;
+      MapOrEntry entry = kv.second;
+      entry.clock.subtract(clock);
+      if (!entry.clock.is_empty()) {
+        VClock del = clock;
+        del.subtract(entry.clock);
+        entry.val.truncate(del);
+        keep[kv.first] = entry;
+      }
+    }
+    for (const auto& kv : other.deferred) {  // apply_rm on the old entries: only the deferral survives
+      VClock c;
+      c.dots = kv.first;
+      for (uint64_t k : kv.second) apply_rm(k, c);
+    }
+    entries = keep;
+    clock.merge(other.clock);
+    apply_deferred();
+  }
+};
+
+static bool clock_dots_less(const std::map<Actor, Counter>& a, const std::map<Actor, Counter>& b) { return a < b; }
+
+static Orswot orswot_from_slab(const crdt_map_orswot_slab& S, size_t ki, uint32_t A) {
+  Orswot o;
+  o.clock = row_to_vclock(S.vclock + ki * A, A);
+  for (uint32_t m = 0; m < S.vn_mem[ki]; ++m)
+    o.entries[S.vmem[ki * S.mcap + m]] = row_to_vclock(S.vmclock + (ki * S.mcap + m) * A, A);
+  for (uint32_t d = 0; d < S.vn_def[ki]; ++d) {
+    const size_t di = ki * S.vdcap + d;
+    auto& set = o.deferred[row_to_vclock(S.vdclock + di * A, A)];
+    for (uint32_t j = 0; j < S.vdset_n[di]; ++j) set.insert(S.vdset[di * S.vscap + j]);
+  }
+  return o;
+}
+static MapOrswotO mapor_from_slab(const crdt_map_orswot_slab& S, size_t i, uint32_t A) {
+  MapOrswotO m;
+  m.clock = row_to_vclock(S.clock + i * A, A);
+  for (uint32_t k = 0; k < S.n_keys[i]; ++k) {
+    const size_t ki = i * S.kcap + k;
+    MapOrEntry e;
+    e.clock = row_to_vclock(S.eclock + ki * A, A);
+    e.val = orswot_from_slab(S, ki, A);
+    m.entries[S.keys[ki]] = e;
+  }
+  for (uint32_t d = 0; d < S.n_def[i]; ++d) {
+    const size_t di = i * S.dcap + d;
+    auto& set = m.deferred[row_to_vclock(S.dclock + di * A, A).dots];
+    for (uint32_t j = 0; j < S.dset_n[di]; ++j) set.insert(S.dset[di * S.scap + j]);
+  }
+  return m;
+}
+// One object's slab row, every slot written (unused ones zero); false when a capacity is exceeded.
+static bool mapor_to_slab(const MapOrswotO& m, const crdt_map_orswot_slab& S, size_t i, uint32_t A) {
+  if (m.entries.size() > S.kcap || m.deferred.size() > S.dcap) return false;
+  vclock_to_row(m.clock, S.clock + i * A, A);
+  S.n_keys[i] = (uint32_t)m.entries.size();
+  for (uint32_t z = 0; z < S.kcap; ++z) {
+    const size_t ki = i * S.kcap + z;
+    S.keys[ki] = 0;
+    S.vn_mem[ki] = 0;
+    S.vn_def[ki] = 0;
+    std::fill(S.eclock + ki * A, S.eclock + (ki + 1) * A, 0ull);
+    std::fill(S.vclock + ki * A, S.vclock + (ki + 1) * A, 0ull);
+    std::fill(S.vmem + ki * S.mcap, S.vmem + (ki + 1) * S.mcap, 0ull);
+    std::fill(S.vmclock + ki * S.mcap * A, S.vmclock + (ki + 1) * S.mcap * A, 0ull);
+    std::fill(S.vdclock + ki * S.vdcap * A, S.vdclock + (ki + 1) * S.vdcap * A, 0ull);
+    std::fill(S.vdset_n + ki * S.vdcap, S.vdset_n + (ki + 1) * S.vdcap, 0u);
+    std::fill(S.vdset + ki * S.vdcap * S.vscap, S.vdset + (ki + 1) * S.vdcap * S.vscap, 0ull);
+  }
+  uint32_t k = 0;
+  for (const auto& kv : m.entries) {
+    const size_t ki = i * S.kcap + k++;
+    const Orswot& o = kv.second.val;
+    if (o.entries.size() > S.mcap || o.deferred.size() > S.vdcap) return false;
+    S.keys[ki] = kv.first;
+    vclock_to_row(kv.second.clock, S.eclock + ki * A, A);
+    vclock_to_row(o.clock, S.vclock + ki * A, A);
+    std::vector<Member> mem;
+    for (const auto& e : o.entries) mem.push_back(e.first);
+    std::sort(mem.begin(), mem.end());
+    S.vn_mem[ki] = (uint32_t)mem.size();
+    for (uint32_t j = 0; j < mem.size(); ++j) {
+      S.vmem[ki * S.mcap + j] = mem[j];
+      vclock_to_row(o.entries.at(mem[j]), S.vmclock + (ki * S.mcap + j) * A, A);
+    }
+    std::vector<const VClock*> dk;
+    for (const auto& e : o.deferred) dk.push_back(&e.first);
+    std::sort(dk.begin(), dk.end(), [](const VClock* x, const VClock* y) { return clock_dots_less(x->dots, y->dots); });
+    S.vn_def[ki] = (uint32_t)dk.size();
+    for (uint32_t d = 0; d < dk.size(); ++d) {
+      const size_t di = ki * S.vdcap + d;
+      const auto& set = o.deferred.at(*dk[d]);
+      if (set.size() > S.vscap) return false;
+      vclock_to_row(*dk[d], S.vdclock + di * A, A);
+      std::vector<Member> ms(set.begin(), set.end());
+      std::sort(ms.begin(), ms.end());
+      S.vdset_n[di] = (uint32_t)ms.size();
+      for (uint32_t j = 0; j < ms.size(); ++j) S.vdset[di * S.vscap + j] = ms[j];
+    }
+  }
+  S.n_def[i] = (uint32_t)m.deferred.size();
+  for (uint32_t z = 0; z < S.dcap; ++z) {
+    const size_t di = i * S.dcap + z;
+    S.dset_n[di] = 0;
+    std::fill(S.dclock + di * A, S.dclock + (di + 1) * A, 0ull);
+    std::fill(S.dset + di * S.scap, S.dset + (di + 1) * S.scap, 0ull);
+  }
+  uint32_t d = 0;
+  for (const auto& kv : m.deferred) {
+    const size_t di = i * S.dcap + d++;
+    if (kv.second.size() > S.scap) return false;
+    VClock c;
+    c.dots = kv.first;
+    vclock_to_row(c, S.dclock + di * A, A);
+    S.dset_n[di] = (uint32_t)kv.second.size();
+    uint32_t j = 0;
+    for (uint64_t key : kv.second) S.dset[di * S.scap + j++] = key;
+  }
+  return true;
+}
+
+// Canonical text of a map (for comparing outcomes across deferred orders).
+static std::string mapor_key(const MapOrswotO& m) {
+  std::string s;
+  auto put = [&](uint64_t v) { s.append((const char*)&v, 8); };
+  auto putc = [&](const VClock& c) { put(c.dots.size()); for (auto& kv : c.dots) { put(kv.first); put(kv.second); } };
+  putc(m.clock);
+  for (const auto& kv : m.entries) {
+    put(kv.first);
+    putc(kv.second.clock);
+    const Orswot& o = kv.second.val;
+    putc(o.clock);
+    std::map<Member, const VClock*> es;
+    for (const auto& e : o.entries) es[e.first] = &e.second;
+    put(es.size());
+    for (auto& e : es) { put(e.first); putc(*e.second); }
+    std::map<std::map<Actor, Counter>, std::set<Member>> ds;
+    for (const auto& e : o.deferred) ds[e.first.dots].insert(e.second.begin(), e.second.end());
+    put(ds.size());
+    for (auto& e : ds) { VClock c; c.dots = e.first; putc(c); put(e.second.size()); for (Member x : e.second) put(x); }
+  }
+  put(m.deferred.size());
+  for (auto& e : m.deferred) { VClock c; c.dots = e.first; putc(c); put(e.second.size()); for (auto x : e.second) put(x); }
+  return s;
+}
+}  // namespace oracle
+
+extern "C" {
+
+// out[i] = self[i].merge(&other[i]) with apply_deferred in CLOCK ORDER; 0, or
+// -4 when an output capacity is exceeded.
+int orc_map_orswot_merge_batch(const crdt_map_orswot_slab* s, const crdt_map_orswot_slab* o,
+                               const crdt_map_orswot_slab* out, size_t n, uint32_t A) {
+  for (size_t i = 0; i < n; ++i) {
+    MapOrswotO m = mapor_from_slab(*s, i, A);
+    m.merge(mapor_from_slab(*o, i, A));
+    if (!mapor_to_slab(m, *out, i, A)) return -4;
+  }
+  return 0;
+}
+
+// Per object: the number of distinct merge results over every order the
+// final apply_deferred of Map::merge can take (all permutations of the
+// combined deferred clocks; -1 when there are more than `max_k` of them).
+int orc_map_orswot_order_outcomes(const crdt_map_orswot_slab* s, const crdt_map_orswot_slab* o, size_t n,
+                                  uint32_t A, int max_k, int32_t* outcomes) {
+  for (size_t i = 0; i < n; ++i) {
+    MapOrswotO a = mapor_from_slab(*s, i, A), b = mapor_from_slab(*o, i, A);
+    // the combined deferred count the final apply_deferred sees
+    MapOrswotO probe = a;
+    {
+      // replay merge up to apply_deferred: entries do not matter for the count
+      for (const auto& kv : b.deferred) {
+        VClock c;
+        c.dots = kv.first;
+        if (!c.le(probe.clock)) probe.deferred[kv.first];
+      }
+    }
+    const int k = (int)probe.deferred.size();
+    if (k > max_k) { outcomes[i] = -1; continue; }
+    std::vector<int> perm(k);
+    for (int j = 0; j < k; ++j) perm[j] = j;
+    std::set<std::string> seen;
+    do {
+      MapOrswotO m = a;
+      m.perm = &perm;
+      m.merge(b);
+      seen.insert(mapor_key(m));
+    } while (std::next_permutation(perm.begin(), perm.end()));
+    outcomes[i] = (int32_t)seen.size();
+  }
+  return 0;
+}
+
+// Replica pairs of Map<u64, Orswot<u64>> by op simulation (the shape of the
+// reference's own Map tests, test/orswot.rs:270-307 and src/map.rs:38-80):
+// a common history, then two replicas diverge with their own actors and get
+// part of each other's ops out of order; updates are
+//   update(key, get(key).derive_add_ctx(actor), |set, ctx| set.add(m, ctx))
+//   update(key, ..., |set, ctx| set.remove(m, set.contains(&m).derive_rm_ctx()))
+// and map removes rm(key, get(key).derive_rm_ctx()); with probability
+// pct_future a remove carries a clock from a third replica (deferred at the
+// map or at the nested set).
+int orc_map_orswot_generate(uint64_t seed, size_t n, uint32_t A, uint32_t keys, uint32_t members, int ops,
+                            int pct_future, const crdt_map_orswot_slab* left, const crdt_map_orswot_slab* right) {
+  struct Op { int kind; Actor a; Counter c; uint64_t key; int vkind; uint64_t member; VClock clock; };
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t st = seed ^ (0x9E3779B97F4A7C15ull * (i + 1));
+    auto rnd = [&]() {
+      uint64_t z = (st += 0x9E3779B97F4A7C15ull);
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      return z ^ (z >> 31);
+    };
+    MapOrswotO rep[2];
+    std::vector<Op> log[2];
+    auto future = [&](VClock c) {
+      c.witness((Actor)(A - 1), 1000 + rnd() % 4);
+      return c;
+    };
+    auto make = [&](MapOrswotO& m, int r, bool shared) {
+      Op op{};
+      op.key = rnd() % keys;
+      const uint64_t roll = rnd() % 100;
+      if (roll < 75) {  // an update: nested add (60 %) or nested remove (15 %)
+        op.kind = 0;
+        op.a = shared ? (Actor)(rnd() % (A - 1)) : (Actor)((2 + r) % (A - 1));
+        op.c = m.clock.inc(op.a);  // get(key).derive_add_ctx(a): the map clock's next dot
+        op.member = rnd() % members;
+        if (roll < 60) {
+          op.vkind = 0;
+        } else {
+          op.vkind = 1;
+          auto it = m.entries.find(op.key);
+          VClock rc;
+          if (it != m.entries.end()) {
+            auto jt = it->second.val.entries.find(op.member);
+            if (jt != it->second.val.entries.end()) rc = jt->second;
+          }
+          op.clock = (int)(rnd() % 100) < pct_future ? future(rc) : rc;
+        }
+      } else {  // a map remove with the entry's clock
+        op.kind = 1;
+        auto it = m.entries.find(op.key);
+        VClock rc = it == m.entries.end() ? VClock() : it->second.clock;
+        op.clock = (int)(rnd() % 100) < pct_future ? future(rc) : rc;
+      }
+      return op;
+    };
+    auto apply = [&](MapOrswotO& m, const Op& op) {
+      if (op.kind == 0) m.apply_up(op.a, op.c, op.key, op.vkind, op.a, op.c, op.member, op.clock);
+      else m.apply_rm(op.key, op.clock);
+    };
+    const int common = (int)(rnd() % (uint64_t)ops);
+    for (int k = 0; k < common; ++k) {
+      Op op = make(rep[0], 0, true);
+      apply(rep[0], op);
+      apply(rep[1], op);
+    }
+    for (int r = 0; r < 2; ++r) {
+      const int div = 1 + (int)(rnd() % (uint64_t)ops);
+      for (int k = 0; k < div; ++k) {
+        Op op = make(rep[r], r, false);
+        apply(rep[r], op);
+        log[r].push_back(op);
+      }
+    }
+    for (int r = 0; r < 2; ++r) {
+      std::vector<Op> sub;
+      for (const auto& op : log[1 - r])
+        if (rnd() % 100 < 40) sub.push_back(op);
+      for (size_t k = sub.size(); k > 1; --k) std::swap(sub[k - 1], sub[rnd() % k]);
+      for (const auto& op : sub) apply(rep[r], op);
+    }
+    if (!mapor_to_slab(rep[0], *left, i, A) || !mapor_to_slab(rep[1], *right, i, A)) return -4;
+  }
+  return 0;
+}
+
+// ---- handles (op-path KATs): Map<u64, Orswot> and Map<u64, MVReg>
+void* orc_mapor_new() { return new MapOrswotO(); }
+void* orc_mapor_clone(const void* h) { return new MapOrswotO(*(const MapOrswotO*)h); }
+void orc_mapor_free(void* h) { delete (MapOrswotO*)h; }
+// Op::Up{dot (a, c), key, Orswot Op::Add{dot (a, c), member}} (kind 0) or
+// Op::Up{dot, key, Orswot Op::Rm{clock, member}} (kind 1)
+void orc_mapor_apply_up(void* h, uint32_t a, uint64_t c, uint64_t key, int kind, uint64_t member,
+                        const uint32_t* ra, const uint64_t* rc, uint32_t rn) {
+  ((MapOrswotO*)h)->apply_up(a, c, key, kind, a, c, member, mk(ra, rc, rn));
+}
+void orc_mapor_apply_rm(void* h, uint64_t key, const uint32_t* ra, const uint64_t* rc, uint32_t rn) {
+  ((MapOrswotO*)h)->apply_rm(key, mk(ra, rc, rn));
+}
+void orc_mapor_merge(void* dst, const void* src) { ((MapOrswotO*)dst)->merge(*(const MapOrswotO*)src); }
+int orc_mapor_to_slab(const void* h, const crdt_map_orswot_slab* S, size_t i, uint32_t A) {
+  return mapor_to_slab(*(const MapOrswotO*)h, *S, i, A) ? 0 : -4;
+}
+void* orc_mapor_from_slab(const crdt_map_orswot_slab* S, size_t i, uint32_t A) {
+  return new MapOrswotO(mapor_from_slab(*S, i, A));
+}
+
+void* orc_mapmv_new() { return new MapO(); }
+void* orc_mapmv_clone(const void* h) { return new MapO(*(const MapO*)h); }
+void orc_mapmv_free(void* h) { delete (MapO*)h; }
+// Op::Up{dot (a, c), key, MVReg Op::Put{clock, val}}
+void orc_mapmv_apply_up(void* h, uint32_t a, uint64_t c, uint64_t key, const uint32_t* pa, const uint64_t* pc,
+                        uint32_t pn, uint64_t val) {
+  ((MapO*)h)->apply_up(a, c, key, mk(pa, pc, pn), val);
+}
+void orc_mapmv_apply_rm(void* h, uint64_t key, const uint32_t* ra, const uint64_t* rc, uint32_t rn) {
+  ((MapO*)h)->apply_rm(key, mk(ra, rc, rn));
+}
+void orc_mapmv_merge(void* dst, const void* src) { ((MapO*)dst)->merge(*(const MapO*)src); }
+int orc_mapmv_to_slab(const void* h, const crdt_map_mvreg_slab* S, size_t i, uint32_t A) {
+  return map_to_slab(*(const MapO*)h, *S, i, A) ? 0 : -4;
 }
 
 }  // extern "C"

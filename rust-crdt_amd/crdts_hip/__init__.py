@@ -197,6 +197,59 @@ class MapSlab:
         return MapSlabC(*ptr, self.kcap, self.mcap, self.dcap, self.scap)
 
 
+class MapOrswotSlab:
+    """Dense fixed-capacity slab of Map<u64, Orswot<u64, A>, A> states
+    (crdt_map_orswot_slab, include/crdts_hip.h): numpy (host) or torch
+    (device) arrays with the shapes below; dtypes u32 / u64 (torch: int32 /
+    int64). `caps` = dict(kcap, mcap, vdcap, vscap, dcap, scap)."""
+
+    U32 = ("n_keys", "vn_mem", "vn_def", "vdset_n", "n_def", "dset_n")
+
+    def __init__(self, arrays, caps):
+        self.a = dict(arrays)
+        self.caps = dict(caps)
+
+    @staticmethod
+    def shapes(n, A, kcap, mcap, vdcap, vscap, dcap, scap):
+        return {"clock": (n, A), "n_keys": (n,), "keys": (n, kcap), "eclock": (n, kcap, A), "vclock": (n, kcap, A),
+                "vn_mem": (n, kcap), "vmem": (n, kcap, mcap), "vmclock": (n, kcap, mcap, A), "vn_def": (n, kcap),
+                "vdclock": (n, kcap, vdcap, A), "vdset_n": (n, kcap, vdcap), "vdset": (n, kcap, vdcap, vscap),
+                "n_def": (n,), "dclock": (n, dcap, A), "dset_n": (n, dcap), "dset": (n, dcap, scap)}
+
+    @classmethod
+    def alloc(cls, n, A, device=None, **caps):
+        out = {}
+        for f, shp in cls.shapes(n, A, **caps).items():
+            u32 = f in cls.U32
+            if device is None:
+                out[f] = np.zeros(shp, np.uint32 if u32 else np.uint64)
+            else:
+                torch = _torch()
+                out[f] = torch.zeros(shp, dtype=torch.int32 if u32 else torch.int64, device=device)
+        return cls(out, caps)
+
+    @property
+    def n(self):
+        return int(self.a["n_keys"].shape[0])
+
+    def to(self, device):
+        torch = _torch()
+        return MapOrswotSlab({f: torch.from_numpy(np.ascontiguousarray(v).view(np.int32 if v.dtype == np.uint32
+                                                                                 else np.int64)).to(device)
+                              for f, v in self.a.items()}, self.caps)
+
+    def host(self):
+        return MapOrswotSlab({f: (v.cpu().numpy().view(np.uint32 if v.dtype.itemsize == 4 else np.uint64)
+                                  if hasattr(v, "cpu") else v) for f, v in self.a.items()}, self.caps)
+
+    def cstruct(self):
+        from ._lib import MAP_ORSWOT_CAPS, MAP_ORSWOT_FIELDS, MapOrswotSlabC
+
+        ptr = [C.c_void_p(self.a[f].data_ptr() if hasattr(self.a[f], "data_ptr") else self.a[f].ctypes.data)
+               for f in MAP_ORSWOT_FIELDS]
+        return MapOrswotSlabC(*ptr, *[self.caps[k] for k in MAP_ORSWOT_CAPS])
+
+
 class Engine:
     """One crdt_ctx bound to a device. All merges run on the GPU."""
 
@@ -396,6 +449,21 @@ class Engine:
         s, o, r = S.cstruct(), O.cstruct(), R.cstruct()
         check(lib.crdt_map_mvreg_merge(self.ctx, C.byref(s), C.byref(o), C.byref(r), n, n_actors,
                                        self._stream(stream)), "map_mvreg_merge")
+        if check_status:
+            self.status(stream)
+        return R
+
+    # ------------------------------------------------ Map<u64, Orswot<u64>>
+    def map_orswot_merge(self, S: "MapOrswotSlab", O: "MapOrswotSlab", n_actors, out_caps=None, stream=None,
+                         check_status=True):
+        """Map::merge with Orswot values (src/map.rs:192-269) of device slabs;
+        returns the output slab (default capacities: the sums of the inputs')."""
+        n = S.n
+        caps = out_caps or {k: S.caps[k] + O.caps[k] for k in S.caps}
+        R = MapOrswotSlab.alloc(n, n_actors, device=S.a["clock"].device, **caps)
+        s, o, r = S.cstruct(), O.cstruct(), R.cstruct()
+        check(lib.crdt_map_orswot_merge(self.ctx, C.byref(s), C.byref(o), C.byref(r), n, n_actors,
+                                        self._stream(stream)), "map_orswot_merge")
         if check_status:
             self.status(stream)
         return R

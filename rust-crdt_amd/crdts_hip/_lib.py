@@ -65,7 +65,7 @@ EXPORTS = [
     "crdt_orswot_validate_ex", "crdt_orswot_generate_replicas", "crdt_host_orswot_encode_ex",
     "crdt_orswot_bincode_record_sizes", "crdt_orswot_from_bincode", "crdt_orswot_bincode_sizes",
     "crdt_orswot_to_bincode", "crdt_orswot_apply", "crdt_vclock_partial_cmp", "crdt_mvreg_merge",
-    "crdt_map_mvreg_merge", "crdt_ctx_set_list_cap",
+    "crdt_map_mvreg_merge", "crdt_map_orswot_merge", "crdt_ctx_set_list_cap",
     "crdt_comm_unique_id", "crdt_comm_init", "crdt_comm_destroy", "crdt_replica_allreduce_max",
     "crdt_orswot_replica_join_bound", "crdt_orswot_replica_join", "crdt_orswot_replica_join_local",
 ]
@@ -85,6 +85,16 @@ class MapSlabC(C.Structure):
     _fields_ = [(f, C.c_void_p) for f in ("clock", "n_keys", "keys", "eclock", "mv_n", "mv_clock", "mv_val", "n_def",
                                           "dclock", "dset_n", "dset")] + \
                [(f, C.c_uint32) for f in ("kcap", "mcap", "dcap", "scap")]
+
+
+MAP_ORSWOT_FIELDS = ("clock", "n_keys", "keys", "eclock", "vclock", "vn_mem", "vmem", "vmclock", "vn_def", "vdclock",
+                     "vdset_n", "vdset", "n_def", "dclock", "dset_n", "dset")
+MAP_ORSWOT_CAPS = ("kcap", "mcap", "vdcap", "vscap", "dcap", "scap")
+
+
+class MapOrswotSlabC(C.Structure):
+    """crdt_map_orswot_slab (include/crdts_hip.h)."""
+    _fields_ = [(f, C.c_void_p) for f in MAP_ORSWOT_FIELDS] + [(f, C.c_uint32) for f in MAP_ORSWOT_CAPS]
 
 
 def _load():
@@ -146,6 +156,8 @@ def _load():
         "crdt_vclock_partial_cmp": (I, [P, P, P, SZ, U32, P, P]),
         "crdt_mvreg_merge": (I, [P, P, P, P, U32, P, P, P, U32, P, P, P, U32, SZ, U32, P]),
         "crdt_map_mvreg_merge": (I, [P, C.POINTER(MapSlabC), C.POINTER(MapSlabC), C.POINTER(MapSlabC), SZ, U32, P]),
+        "crdt_map_orswot_merge": (I, [P, C.POINTER(MapOrswotSlabC), C.POINTER(MapOrswotSlabC),
+                                      C.POINTER(MapOrswotSlabC), SZ, U32, P]),
         "crdt_comm_unique_id": (I, [P]),
         "crdt_comm_init": (I, [P, P, I, I]),
         "crdt_comm_destroy": (I, [P]),

@@ -407,4 +407,25 @@ int crdt_map_mvreg_merge(crdt_ctx* ctx, const crdt_map_mvreg_slab* self, const c
   return launch_map_mvreg_merge(*self, *other, *out, n_obj, n_actors, ctx->d_status, S(stream));
 }
 
+int crdt_map_orswot_merge(crdt_ctx* ctx, const crdt_map_orswot_slab* self, const crdt_map_orswot_slab* other,
+                          const crdt_map_orswot_slab* out, size_t n_obj, uint32_t n_actors, void* stream) {
+  if (!ctx || !self || !other || !out || n_actors == 0 || n_actors > 64) return CRDT_EINVAL;
+  for (const crdt_map_orswot_slab* x : {self, other})
+    if (x->kcap == 0 || x->kcap > 32 || x->mcap == 0 || x->mcap > 32 || x->vdcap == 0 || x->vdcap > 16 ||
+        x->vscap == 0 || x->vscap > 16 || x->dcap == 0 || x->dcap > 32 || x->scap == 0 || x->scap > 32)
+      return CRDT_EINVAL;
+  if (out->kcap == 0 || out->mcap == 0 || out->vdcap == 0 || out->vscap == 0 || out->dcap == 0 || out->scap == 0)
+    return CRDT_EINVAL;
+  if (map_orswot_lds_bytes(*self, *other, n_actors) > 65536) return CRDT_EINVAL;  // the kernel's workspace
+  if (n_obj)
+    for (const crdt_map_orswot_slab* x : {self, other, out})
+      if (!x->clock || !x->n_keys || !x->keys || !x->eclock || !x->vclock || !x->vn_mem || !x->vmem ||
+          !x->vmclock || !x->vn_def || !x->vdclock || !x->vdset_n || !x->vdset || !x->n_def || !x->dclock ||
+          !x->dset_n || !x->dset)
+        return CRDT_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return launch_map_orswot_merge(*self, *other, *out, n_obj, n_actors, ctx->d_status, S(stream));
+}
+
 }  // extern "C"

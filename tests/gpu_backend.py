@@ -16,6 +16,12 @@ class GpuBackend:
     def new(self):
         return self.m.Orswot(self.n_actors, sparse=self.sparse)
 
+    def load(self, state):
+        import kat_runner
+
+        rec = kat_runner._state_record(state, self.n_actors)
+        return self.m.Orswot(self.n_actors, host=self.m.HostOrswot.decode(rec), sparse=self.sparse)
+
     def clone(self, o):
         return o.clone()
 

@@ -22,6 +22,20 @@ def load_cases():
         return json.load(f)["cases"]
 
 
+def load_qc_scenarios():
+    """tests/golden/quickcheck_evolution.json (tools/make_golden_qc.py)."""
+    with open(os.path.join(GOLDEN, "quickcheck_evolution.json")) as f:
+        return json.load(f)["scenarios"]
+
+
+def _state_record(state, n_actors=16):
+    import records
+
+    return records.encode(dict((a, c) for a, c in state["clock"]),
+                          {m: dict((a, c) for a, c in clk) for m, clk in state["entries"]},
+                          {tuple((a, c) for a, c in d): set(ms) for d, ms in state["deferred"]}, n_actors)
+
+
 class PyBackend:
     """Backend over oracle/crdts_ref.py."""
 
@@ -35,6 +49,13 @@ class PyBackend:
 
     def new(self):
         return self.m.Orswot()
+
+    def load(self, state):
+        o = self.m.Orswot()
+        o.clock = self.m.VClock([tuple(x) for x in state["clock"]])
+        o.entries = {m: self.m.VClock([tuple(x) for x in c]) for m, c in state["entries"]}
+        o.deferred = {self.m.VClock([tuple(x) for x in d]): set(ms) for d, ms in state["deferred"]}
+        return o
 
     def clone(self, o):
         return o.clone()
@@ -72,6 +93,9 @@ class OracleBackend:
 
     def new(self):
         return self.f.OracleOrswot()
+
+    def load(self, state):
+        return self.f.OracleOrswot.decode(_state_record(state))
 
     def clone(self, o):
         return o.clone()
@@ -140,8 +164,8 @@ def run_case(case, backend, trace=None):
             backend.apply_rm(reps[st[1]], M(st[2]), [(A(a), int(c)) for a, c in st[3]])
         elif op == "merge":
             backend.merge(reps[st[1]], reps[st[2]])
-            if trace is not None:
-                trace.append((k, st[1], reps[st[1]]))
+            if trace is not None:  # a snapshot: the replica may change in later steps
+                trace.append((k, st[1], backend.clone(reps[st[1]])))
         elif op == "assert_value":
             got = backend.value(reps[st[1]])
             exp = sorted(M(x) for x in st[2])
@@ -167,3 +191,39 @@ def run_case(case, backend, trace=None):
         else:
             raise ValueError(f"unknown step {op}")
     return reps
+
+
+def qc_replay(scn, backend, i):
+    """One witness count of a quickcheck_evolution scenario: the op vector
+    replayed onto i witnesses (rule in the fixture's _doc), folded in index
+    order into a new set, then the empty 'defer plunger' (test/orswot.rs:44-62).
+    Returns (witnesses, merged)."""
+    ws = [backend.new() for _ in range(i)]
+    adds = {}
+    for op in scn["ops"]:
+        w = ws[op["actor"] % i]
+        if op["kind"] == "add":
+            adds[op["actor"]] = adds.get(op["actor"], 0) + 1
+            backend.apply_add(w, op["actor"], adds[op["actor"]], op["member"])
+        elif op["ctx"] is None:  # contains(member).derive_rm_ctx() on that witness
+            backend.apply_rm(w, op["member"], list(backend.entry(w, op["member"]) or []))
+        else:
+            backend.apply_rm(w, op["member"], [tuple(x) for x in op["ctx"]])
+    merged = backend.new()
+    for w in ws:
+        backend.merge(merged, w)
+    backend.merge(merged, backend.new())
+    return ws, merged
+
+
+def qc_fold(states, backend, trace=None):
+    """Fold a logged witness list in index order into a new set, then the plunger."""
+    merged = backend.new()
+    for k, st in enumerate(states):
+        backend.merge(merged, backend.load(st))
+        if trace is not None:
+            trace.append(backend.clone(merged))
+    backend.merge(merged, backend.new())
+    if trace is not None:
+        trace.append(backend.clone(merged))
+    return merged

@@ -90,6 +90,27 @@ def lib():
                                    C.c_size_t]
     L.orc_vclock_partial_cmp.restype = C.c_int
     L.orc_vclock_partial_cmp.argtypes = [U32P, U64P, C.c_uint32, U32P, U64P, C.c_uint32]
+    L.orc_map_orswot_merge_batch.restype = C.c_int
+    L.orc_map_orswot_merge_batch.argtypes = [P, P, P, C.c_size_t, C.c_uint32]
+    L.orc_map_orswot_order_outcomes.restype = C.c_int
+    L.orc_map_orswot_order_outcomes.argtypes = [P, P, C.c_size_t, C.c_uint32, C.c_int, P]
+    L.orc_map_orswot_generate.restype = C.c_int
+    L.orc_map_orswot_generate.argtypes = [C.c_uint64, C.c_size_t, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
+                                          C.c_int, P, P]
+    for pre in ("mapor", "mapmv"):
+        getattr(L, f"orc_{pre}_new").restype = P
+        getattr(L, f"orc_{pre}_clone").restype = P
+        getattr(L, f"orc_{pre}_clone").argtypes = [P]
+        getattr(L, f"orc_{pre}_free").argtypes = [P]
+        getattr(L, f"orc_{pre}_merge").argtypes = [P, P]
+        getattr(L, f"orc_{pre}_apply_rm").argtypes = [P, C.c_uint64, U32P, U64P, C.c_uint32]
+        getattr(L, f"orc_{pre}_to_slab").restype = C.c_int
+        getattr(L, f"orc_{pre}_to_slab").argtypes = [P, P, C.c_size_t, C.c_uint32]
+    L.orc_mapor_apply_up.argtypes = [P, C.c_uint32, C.c_uint64, C.c_uint64, C.c_int, C.c_uint64, U32P, U64P,
+                                     C.c_uint32]
+    L.orc_mapmv_apply_up.argtypes = [P, C.c_uint32, C.c_uint64, C.c_uint64, U32P, U64P, C.c_uint32, C.c_uint64]
+    L.orc_mapor_from_slab.restype = P
+    L.orc_mapor_from_slab.argtypes = [P, C.c_size_t, C.c_uint32]
     _lib = L
     return L
 
@@ -317,3 +338,88 @@ def dense_bench(self_rows, other_rows, n_actors, threads):
 
 def record_bytes(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem):
     return int(lib().orc_record_bytes(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem))
+
+
+# ------------------------------------------------------------- Map<u64, Orswot>
+MAP_ORSWOT_CAPS = dict(kcap=8, mcap=8, vdcap=4, vscap=4, dcap=8, scap=8)
+
+
+def map_orswot_generate(seed, n, A, keys, members, ops, pct_future, caps=None):
+    """Replica pairs of Map<u64, Orswot<u64>> by op simulation -> (left, right) host slabs."""
+    import crdts_hip
+
+    caps = caps or MAP_ORSWOT_CAPS
+    L = crdts_hip.MapOrswotSlab.alloc(n, A, **caps)
+    R = crdts_hip.MapOrswotSlab.alloc(n, A, **caps)
+    l, r = L.cstruct(), R.cstruct()
+    rc = lib().orc_map_orswot_generate(seed, n, A, keys, members, ops, pct_future, C.byref(l), C.byref(r))
+    if rc:
+        raise ValueError(f"map-orswot generate rc={rc} (capacity)")
+    return L, R
+
+
+def map_orswot_merge(S, O, A, out_caps=None):
+    """Oracle Map::merge (Orswot values, CLOCK ORDER apply_deferred) of host slabs."""
+    import crdts_hip
+
+    caps = out_caps or {k: S.caps[k] + O.caps[k] for k in S.caps}
+    R = crdts_hip.MapOrswotSlab.alloc(S.n, A, **caps)
+    s, o, r = S.cstruct(), O.cstruct(), R.cstruct()
+    rc = lib().orc_map_orswot_merge_batch(C.byref(s), C.byref(o), C.byref(r), S.n, A)
+    if rc:
+        raise ValueError(f"oracle map-orswot merge rc={rc}")
+    return R
+
+
+def map_orswot_order_outcomes(S, O, A, max_k=6):
+    """Per object: distinct Map::merge results over every order of the final
+    apply_deferred (-1: more than max_k deferred clocks, not enumerated)."""
+    out = np.zeros(S.n, dtype=np.int32)
+    s, o = S.cstruct(), O.cstruct()
+    lib().orc_map_orswot_order_outcomes(C.byref(s), C.byref(o), S.n, A, max_k, _ptr(out))
+    return out
+
+
+class OracleMap:
+    """Handle to an oracle Map<u64, Orswot<u64>> (kind "orswot") or Map<u64, MVReg<u64>> (kind "mvreg")."""
+
+    def __init__(self, kind, handle=None):
+        self.kind = kind
+        self.pre = "mapor" if kind == "orswot" else "mapmv"
+        self.h = handle if handle is not None else getattr(lib(), f"orc_{self.pre}_new")()
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            getattr(lib(), f"orc_{self.pre}_free")(self.h)
+            self.h = None
+
+    def clone(self):
+        return OracleMap(self.kind, getattr(lib(), f"orc_{self.pre}_clone")(self.h))
+
+    def apply_up_orswot(self, dot, key, kind, member, rm_pairs=()):
+        a, c, n = _clock_arrays(list(rm_pairs))
+        lib().orc_mapor_apply_up(self.h, dot[0], dot[1], key, kind, member, a, c, n)
+
+    def apply_up_mvreg(self, dot, key, put_pairs, val):
+        a, c, n = _clock_arrays(list(put_pairs))
+        lib().orc_mapmv_apply_up(self.h, dot[0], dot[1], key, a, c, n, val)
+
+    def apply_rm(self, key, pairs):
+        a, c, n = _clock_arrays(list(pairs))
+        getattr(lib(), f"orc_{self.pre}_apply_rm")(self.h, key, a, c, n)
+
+    def merge(self, other):
+        getattr(lib(), f"orc_{self.pre}_merge")(self.h, other.h)
+
+    def slab(self, A, caps):
+        import crdts_hip
+
+        if self.kind == "orswot":
+            S = crdts_hip.MapOrswotSlab.alloc(1, A, **caps)
+        else:
+            S = crdts_hip.MapSlab.alloc(1, A, caps["kcap"], caps["mcap"], caps["dcap"], caps["scap"])
+        st = S.cstruct()
+        rc = getattr(lib(), f"orc_{self.pre}_to_slab")(self.h, C.byref(st), 0, A)
+        if rc:
+            raise ValueError("oracle map to slab: capacity")
+        return S

@@ -1,0 +1,132 @@
+"""GPU parity: Map<u64, Orswot<u64, A>, A>::merge (crdt_map_orswot_merge,
+rust-crdt_amd/csrc/map_orswot.hip) against the oracle — slab-row exact — and
+the reference's Map KATs with every merge on the kernel.
+
+Map Val semantics: src/map.rs:192-269 (merge), :325-350 (apply_deferred,
+apply_rm), src/orswot.rs:87-172 (nested merge, truncate). The final
+apply_deferred runs in CLOCK ORDER (tests/test_map_orswot.py settles that the
+reference's HashMap order can matter; CLOCK ORDER is one of its orders)."""
+import numpy as np
+import pytest
+
+import map_kat_runner as mkr
+import map_slab
+import test_map_orswot as tmo
+from map_slab import crdts_ref
+
+pytestmark = pytest.mark.gpu
+A = 8
+CASES = mkr.load_cases()
+
+
+class GpuMapBackend(mkr.PyMapBackend):
+    """States built by the Python op path; every merge runs on the kernel: both
+    maps are interned to dense actor ids (order-preserving), written to slabs,
+    merged by crdt_map_orswot_merge (Orswot values) or crdt_map_mvreg_merge
+    (MVReg values), and read back."""
+
+    def __init__(self, eng):
+        self.eng = eng
+        self.merges = 0
+
+    def merge(self, dst, src):
+        import crdts_hip
+
+        acts = sorted(map_slab.actors_of(dst) | map_slab.actors_of(src)) or [0]
+        fwd = {a: i for i, a in enumerate(acts)}
+        back = {i: a for a, i in fwd.items()}
+        n = len(acts)
+        d, s = map_slab.relabel(dst, fwd), map_slab.relabel(src, fwd)
+        if dst.factory is crdts_ref.Orswot:
+            S = crdts_hip.MapOrswotSlab.alloc(1, n, **mkr.CAPS)
+            O = crdts_hip.MapOrswotSlab.alloc(1, n, **mkr.CAPS)
+            map_slab.orswot_map_to_row(d, S, 0, n)
+            map_slab.orswot_map_to_row(s, O, 0, n)
+            R = self.eng.map_orswot_merge(S.to("cuda"), O.to("cuda"), n).host()
+            out = map_slab.orswot_map_from_row(R, 0)
+        else:
+            S = crdts_hip.MapSlab.alloc(1, n, 4, 4, 4, 4)
+            O = crdts_hip.MapSlab.alloc(1, n, 4, 4, 4, 4)
+            map_slab.mvreg_map_to_row(d, S, 0, n)
+            map_slab.mvreg_map_to_row(s, O, 0, n)
+            R = self.eng.map_mvreg_merge(S.to("cuda"), O.to("cuda"), n).host()
+            out = map_slab.mvreg_map_from_row(R, 0)
+        out = map_slab.relabel(out, back)
+        dst.clock, dst.entries, dst.deferred = out.clock, out.entries, out.deferred
+        self.merges += 1
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_map_kat_on_gpu(case, gpu, oracle):
+    """Every KAT script with each merge on the kernel; the reference's asserts
+    hold and every merged state equals the oracle's."""
+    be = GpuMapBackend(gpu)
+    tg, to = [], []
+    a = mkr.run_case(case, be, tg)
+    b = mkr.run_case(case, mkr.OracleMapBackend(), to)
+    assert be.merges == sum(st[0] == "merge" for st in case["steps"])
+    assert all(x == y for (_, _, x), (_, _, y) in zip(tg, to))
+    assert all(a[k] == b[k] for k in a)
+
+
+def test_map_mvreg_kat_final_states_merge_on_gpu(gpu):
+    """The Map<u8, MVReg> op-path KATs end in equal maps; merging every pair of
+    their final states on the kernel gives the Python restatement's merge."""
+    be = GpuMapBackend(gpu)
+    for case in CASES:
+        fin = mkr.run_case(case, mkr.PyMapBackend())
+        names = sorted(fin)
+        for x in names:
+            for y in names:
+                g, p = fin[x].clone(), fin[x].clone()
+                be.merge(g, fin[y])
+                p.merge(fin[y])
+                assert g == p, (case["name"], x, y)
+
+
+@pytest.mark.parametrize("pct_future", [10, 35])
+def test_map_orswot_random_parity(gpu, oracle, pct_future):
+    """20k generated pairs, both orientations: kernel == oracle, slab-row exact."""
+    L, R = oracle.map_orswot_generate(0xB0B + pct_future, 20000, A, keys=4, members=6, ops=10,
+                                      pct_future=pct_future)
+    for S, O in ((L, R), (R, L)):
+        exp = oracle.map_orswot_merge(S, O, A)
+        got = gpu.map_orswot_merge(S.to("cuda"), O.to("cuda"), A).host()
+        for f in exp.a:
+            bad = np.nonzero((np.asarray(got.a[f]) != np.asarray(exp.a[f])).reshape(S.n, -1).any(axis=1))[0]
+            assert bad.size == 0, f"{f}: {bad.size} objects differ, first {bad[:5].tolist()}"
+
+
+def test_map_orswot_order_case_on_gpu(gpu, oracle):
+    """The reachable pair whose result depends on the deferred order: the
+    kernel gives the CLOCK ORDER outcome."""
+    import crdts_hip
+
+    a, b = tmo._order_case()
+    S = crdts_hip.MapOrswotSlab.alloc(1, A, **oracle.MAP_ORSWOT_CAPS)
+    O = crdts_hip.MapOrswotSlab.alloc(1, A, **oracle.MAP_ORSWOT_CAPS)
+    map_slab.orswot_map_to_row(a, S, 0, A)
+    map_slab.orswot_map_to_row(b, O, 0, A)
+    got = map_slab.orswot_map_from_row(gpu.map_orswot_merge(S.to("cuda"), O.to("cuda"), A).host(), 0)
+    exp = a.clone()
+    exp.merge(b)
+    assert got == exp and len(got.entries[7][1].deferred) == 1
+
+
+def test_map_orswot_errors(gpu, oracle):
+    import crdts_hip
+
+    L, R = oracle.map_orswot_generate(0xC4, 64, A, keys=4, members=6, ops=10, pct_future=20)
+    # output capacity: one key slot per map
+    caps = dict(oracle.MAP_ORSWOT_CAPS, kcap=1)
+    with pytest.raises(crdts_hip.CrdtError) as e:
+        gpu.map_orswot_merge(L.to("cuda"), R.to("cuda"), A, out_caps=caps)
+    assert e.value.code == crdts_hip.CRDT_ECAPACITY
+    # malformed counts: a nested member count above its capacity
+    bad = crdts_hip.MapOrswotSlab({f: v.copy() for f, v in L.a.items()}, L.caps)
+    k = int(np.nonzero(bad.a["n_keys"])[0][0])
+    bad.a["vn_mem"][k, 0] = bad.caps["mcap"] + 1
+    with pytest.raises(crdts_hip.CrdtError) as e:
+        gpu.map_orswot_merge(bad.to("cuda"), R.to("cuda"), A)
+    assert e.value.code == crdts_hip.CRDT_ENONCANON
+    gpu.status()  # the context is usable again after the latched error

@@ -14,6 +14,7 @@ from gpu_backend import GpuBackend
 
 pytestmark = pytest.mark.gpu
 CASES = kat_runner.load_cases()
+QC = kat_runner.load_qc_scenarios()
 
 
 def _dev_batch(crdts_hip, base, off, n_actors):
@@ -50,6 +51,31 @@ def test_orswot_kat_on_gpu(case, gpu, oracle):
     assert be.merges == sum(st[0] == "merge" for st in case["steps"])
     for (k1, n1, a), (k2, n2, b) in zip(tg, to):
         assert a.record() == b.encode(16), f"{case['name']} step {k1}"
+
+
+# ------------------------------------------------------------------ quickcheck_evolution.log
+@pytest.mark.parametrize("scn", QC, ids=[s["name"] for s in QC])
+def test_quickcheck_evolution_on_gpu(scn, gpu, oracle):
+    """quickcheck_evolution.log's 8 op vectors (inputs only, tests/golden/
+    quickcheck_evolution.json): every merge of the convergence property
+    (i = 2..10 witnesses + plunger) and of every logged witness-list fold runs
+    on the kernel; the merged record equals the oracle's at every witness
+    count and every fold step, and the witness counts converge."""
+    be, ob = GpuBackend(gpu, n_actors=16), kat_runner.OracleBackend()
+    results = set()
+    for i in range(2, 11):
+        _, mg = kat_runner.qc_replay(scn, be, i)
+        _, mo = kat_runner.qc_replay(scn, ob, i)
+        assert mg.record() == mo.encode(16), f"i={i}"
+        results.add(mg.record())
+    assert len(results) == 1
+    for ws in scn["witness_sets"]:
+        tg, to = [], []
+        kat_runner.qc_fold(ws["witnesses"], be, tg)
+        kat_runner.qc_fold(ws["witnesses"], ob, to)
+        for k, (a, b) in enumerate(zip(tg, to)):
+            assert a.record() == b.encode(16), f"log lines {ws['log_lines']} step {k}"
+    assert be.merges > 0
 
 
 # ------------------------------------------------------------------ prop_merge_converges

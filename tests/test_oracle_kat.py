@@ -22,6 +22,7 @@ import records
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASES = kat_runner.load_cases()
+QC = kat_runner.load_qc_scenarios()
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
@@ -188,3 +189,32 @@ def test_record_bytes_agree(oracle):
     for _ in range(200):
         args = [rng.randrange(0, 40) for _ in range(6)]
         assert oracle.record_bytes(*args) == records.record_bytes(*args)
+
+
+# ------------------------------------------------------------ quickcheck_evolution.log
+@pytest.mark.parametrize("scn", QC, ids=[s["name"] for s in QC])
+def test_quickcheck_evolution_converges(scn, oracle):
+    """The 8 op vectors of quickcheck_evolution.log (inputs only): replayed
+    onto i = 2..10 witnesses, the reference's convergence property
+    (test/orswot.rs:37-76) holds on the Python restatement and the C++ oracle,
+    and the two agree record-for-record at every witness count."""
+    py, ob = kat_runner.PyBackend(), kat_runner.OracleBackend()
+    results = set()
+    for i in range(2, 11):
+        _, mp = kat_runner.qc_replay(scn, py, i)
+        _, mo = kat_runner.qc_replay(scn, ob, i)
+        assert records.from_py(mp, 16) == mo.encode(16), f"i={i}"
+        results.add(mo.encode(16))
+    assert len(results) == 1, f"{scn['name']}: {len(results)} distinct merged states"
+
+
+@pytest.mark.parametrize("scn", QC, ids=[s["name"] for s in QC])
+def test_quickcheck_evolution_witness_sets(scn, oracle):
+    """Every witness list the log printed, folded in index order (+ plunger):
+    Python restatement == C++ oracle after every merge."""
+    for ws in scn["witness_sets"]:
+        tp, to = [], []
+        kat_runner.qc_fold(ws["witnesses"], kat_runner.PyBackend(), tp)
+        kat_runner.qc_fold(ws["witnesses"], kat_runner.OracleBackend(), to)
+        for k, (a, b) in enumerate(zip(tp, to)):
+            assert records.from_py(a, 16) == b.encode(16), f"log lines {ws['log_lines']} step {k}"
