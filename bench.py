@@ -36,7 +36,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="orswot",
                    choices=["orswot", "vclock", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply",
-                            "mvreg", "map"])
+                            "mvreg", "map", "map_orswot"])
     p.add_argument("--replicas", type=int, default=8, help="orswot_csr at N=1: replicas folded locally")
     p.add_argument("--n-obj", type=int, default=None, help="objects per GPU")
     p.add_argument("--threads", type=int, default=16, help="host threads for input generation")
@@ -105,11 +105,13 @@ def load_traffic(path, key):
 def wl_traffic(args, workload, *kernels):
     """Per-launch HBM bytes of the workload's measured kernels from its
     rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/profile_workload.sh +
-    tools/traffic.py -> profiles/traffic_r01e_<workload>.json), summed over the
+    tools/traffic.py -> profiles/traffic_r02_<workload>.json, else r01e), summed over the
     kernels one measured launch runs; None off the profiled (default) size."""
     if args.n_obj is not None:
         return None
-    path = os.path.join(REPO, "profiles", f"traffic_r01e_{workload}.json")
+    path = os.path.join(REPO, "profiles", f"traffic_r02_{workload}.json")  # newest profile first
+    if not os.path.exists(path):
+        path = os.path.join(REPO, "profiles", f"traffic_r01e_{workload}.json")
     vals = []
     for k in kernels:  # a templated kernel is keyed by its bool instantiation (tools/traffic.py)
         v = load_traffic(path, k)
@@ -430,7 +432,6 @@ def run_orswot_csr(args, rank, world, local):
             return replica.orswot_anti_entropy(eng, mine)
     else:
         batches = [crdts_hip.OrswotBatch.from_host(b, o, U, device=local, flags=SP) for b, o in reps]
-        in_bytes = sum(int(b.nbytes) for b, _ in reps)
         del reps
         # preallocated fold outputs (a merged record is never larger than its inputs)
         outs, acc = [], batches[0]
@@ -464,10 +465,14 @@ def run_orswot_csr(args, rank, world, local):
                    if world > 1 else "local fold"},
     }
     if world == 1:
-        sizes = final.base.view(torch.int32)[(final.off // 4)].cpu().numpy().astype("int64")
-        # algorithmic bytes of the fold: every merge reads both inputs and writes its output;
-        # intermediate sizes are bounded by the final one, so this is a lower bound
-        alg = in_bytes + (R - 1) * int(sizes.sum()) + 3 * 8 * n * (R - 1)
+        def rec_bytes(B):  # sum of the batch's record sizes (gaps excluded)
+            return int(B.base.view(torch.int32)[(B.off // 4)].sum(dtype=torch.int64).item())
+
+        # algorithmic bytes of the fold, from the real record sizes of every
+        # step: merge k reads acc_k (replica 0, then the previous output) and
+        # replica k+1, and writes its output; + 3 offsets per object-merge
+        outs_b = [rec_bytes(o) for o in outs]
+        alg = sum(rec_bytes(B) for B in batches) + sum(outs_b) + sum(outs_b[:-1]) + 3 * 8 * n * (R - 1)
         ach = alg / (ev_ms * 1e-3) / 1e9
         res["roofline"] = {"bound": "hbm", "kernel": "fold of 7 launches: orswot_sparse_mask_kernel + orswot_sparse_general_kernel", "achieved": ach,
                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
@@ -937,6 +942,72 @@ def run_map(args, rank, world, local):
     return res
 
 
+def run_map_orswot(args, rank, world, local):
+    """SURVEY.md §8(f) rank 3 as written: batched Map<u64, Orswot<u64, A>, A>::merge
+    (src/map.rs:192-269, nested Orswot::merge / truncate src/orswot.rs:87-172)
+    over 100k replica pairs per GPU built by op simulation (A = 16; per side
+    <= 8 keys of <= 8 members, 4 nested deferred removes, 8 map deferred
+    removes). A step = one crdt_map_orswot_merge launch."""
+    import time as _t
+
+    import torch
+
+    import crdts_hip
+
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_ffi
+
+    n = args.n_obj or 100_000
+    A = 16
+    caps = dict(kcap=8, mcap=8, vdcap=4, vscap=4, dcap=8, scap=8)
+    L, R = oracle_ffi.map_orswot_generate(0xC0FFEE08 + rank, n, A, 6, 8, 12, 20, caps)
+    eng = crdts_hip.Engine(local)
+    dev = f"cuda:{local}"
+    dL, dR = L.to(dev), R.to(dev)
+    out = eng.map_orswot_merge(dL, dR, A)
+    m = 2000
+    sub = lambda S, k: crdts_hip.MapOrswotSlab({f: v[:k] for f, v in S.a.items()}, S.caps)  # noqa: E731
+    exp = oracle_ffi.map_orswot_merge(sub(L, m), sub(R, m), A)
+    got = out.host()
+    for f in exp.a:
+        assert (got.a[f][:m] == exp.a[f]).all(), f"map-orswot merge parity: {f}"
+    stream = torch.cuda.Stream(device=local)
+
+    def step():
+        eng.map_orswot_merge(dL, dR, A, stream=stream, check_status=False)
+
+    wall, ev_ms = _timed_steps(args, world, stream, step)
+    eng.status(stream)
+    nbytes = lambda S: sum(int(v.numel()) * v.element_size() for v in S.a.values())  # noqa: E731
+    alg = nbytes(dL) + nbytes(dR) + nbytes(out)
+    total = sum_over_ranks(float(n * args.steps), world)
+    res = {
+        "metric": "Map<u64, Orswot> merges/sec (node)", "value": total / wall, "unit": "merges/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic: op-simulated Map<u64, Orswot<u64>> replica pairs (nested adds / removes, map removes, "
+                "deferred removes at both levels)",
+        "config": {"workload": f"map_orswot: {n} map merges per GPU, A=16, caps {caps}",
+                   "parallelism": f"dp{world} (objects sharded)"},
+    }
+    if world == 1:
+        ach = alg / (ev_ms * 1e-3) / 1e9
+        res["roofline"] = {"bound": "hbm", "kernel": "map_orswot_merge_kernel", "achieved": ach,
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "kernel_ms": ev_ms,
+                           "alg_bytes_per_launch": alg,
+                           "traffic": wl_traffic(args, "map_orswot", "map_orswot_merge_kernel")}
+        if not args.no_cpu_baseline:
+            mm = 10_000
+            t0 = _t.perf_counter()
+            oracle_ffi.map_orswot_merge(sub(L, mm), sub(R, mm), A)
+            secs = _t.perf_counter() - t0
+            res["cpu_baseline"] = {"value": mm / secs, "unit": "merges/s", "cores": 1, "kind": "port",
+                                   **cpu_cores_note(),
+                                   "sample": f"{mm} map merges, oracle (BTreeMap / HashMap-shaped containers), "
+                                             "1 thread, incl. slab<->map conversion"}
+    return res
+
+
 def main():
     args = parse()
     rank, world, local = dist_setup()
@@ -958,6 +1029,8 @@ def main():
         res = run_mvreg(args, rank, world, local)
     elif args.workload == "map":
         res = run_map(args, rank, world, local)
+    elif args.workload == "map_orswot":
+        res = run_map_orswot(args, rank, world, local)
     else:
         res = run_dense(args, rank, world, local, args.workload)
     if rank == 0:

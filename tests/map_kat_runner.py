@@ -56,11 +56,12 @@ class PyMapBackend:
 class OracleMapBackend:
     """C++ oracle handles; reads go through a slab row and the Python decoder."""
 
-    def __init__(self, n_actors=96):
+    def __init__(self, n_actors=100, caps=None):
         import oracle_ffi
 
         self.f = oracle_ffi
         self.A = n_actors
+        self.caps = caps or CAPS
 
     def new(self, kind):
         return self.f.OracleMap(kind)
@@ -69,7 +70,7 @@ class OracleMapBackend:
         return m.clone()
 
     def view(self, m):
-        S = m.slab(self.A, CAPS)
+        S = m.slab(self.A, self.caps)
         return map_slab.orswot_map_from_row(S, 0) if m.kind == "orswot" else map_slab.mvreg_map_from_row(S, 0)
 
     def apply_up_add(self, m, dot, key, member):
