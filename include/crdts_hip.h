@@ -487,6 +487,11 @@ int crdt_orswot_apply(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_o
  * bytes) latches CRDT_ENONCANON; one with more than 256 members or 64
  * deferred clocks latches CRDT_ECAPACITY (limits of this round).
  *   1) crdt_orswot_bincode_record_sizes: d_sizes[i] = record bytes (0 if bad)
+ *      — or, without reading the blobs, crdt_orswot_bincode_record_bounds:
+ *      d_bounds[i] >= the record bytes of any blob of length blob_len[i]
+ *      (16-B multiple; <= 48 + 8 n_actors + blob_len * max(12/(wa+8),
+ *      12/(wm+8), 8/wm)); records placed by bounds form a gapped batch, a
+ *      valid input everywhere (crdt_orswot_compact removes the gaps)
  *   2) the caller places records (16-B aligned offsets, e.g. exclusive scan)
  *   3) crdt_orswot_from_bincode writes record i at d_out + d_out_off[i].
  * Egest = to_binary with HashMap / HashSet elements in ascending key (clock)
@@ -499,6 +504,9 @@ int crdt_orswot_bincode_record_sizes(crdt_ctx* ctx, const uint8_t* d_blobs, size
                                      const uint64_t* d_blob_off, const uint64_t* d_blob_len, size_t n_obj,
                                      uint32_t actor_bytes, uint32_t member_bytes, uint32_t n_actors,
                                      uint32_t flags, uint64_t* d_sizes, void* stream);
+int crdt_orswot_bincode_record_bounds(crdt_ctx* ctx, const uint64_t* d_blob_len, size_t n_obj,
+                                      uint32_t actor_bytes, uint32_t member_bytes, uint32_t n_actors, uint32_t flags,
+                                      uint64_t* d_bounds, void* stream);
 int crdt_orswot_from_bincode(crdt_ctx* ctx, const uint8_t* d_blobs, size_t blob_bytes,
                              const uint64_t* d_blob_off, const uint64_t* d_blob_len, size_t n_obj,
                              uint32_t actor_bytes, uint32_t member_bytes, uint32_t n_actors, uint32_t flags,

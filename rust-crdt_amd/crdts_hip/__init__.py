@@ -489,20 +489,29 @@ class Engine:
 
     # ------------------------------------------------ bincode ingest / egest
     def orswot_from_bincode(self, blobs, blob_off, blob_len, n_actors, actor_bytes, member_bytes, flags=0,
-                            stream=None, check_status=True):
+                            stream=None, check_status=True, packed=True):
         """Records from the reference's binary form (`from_binary`, src/lib.rs:78-83).
 
         blobs: torch.uint8 device tensor; blob_off / blob_len: torch.int64 device
-        tensors (u64). Returns an OrswotBatch of canonical records."""
+        tensors (u64). Returns an OrswotBatch of canonical records: packed
+        (a sizes pass walks every blob first), or with packed=False placed by
+        crdt_orswot_bincode_record_bounds (blob lengths only: every blob is
+        read once; the batch has gaps)."""
         torch = _torch()
         n = int(blob_off.numel())
         dev = f"cuda:{self.device}"
         st = self._stream(stream)
         sizes = torch.empty(n, dtype=torch.int64, device=dev)
-        check(lib.crdt_orswot_bincode_record_sizes(self.ctx, C.c_void_p(blobs.data_ptr()), int(blobs.numel()),
-                                                   C.c_void_p(blob_off.data_ptr()), C.c_void_p(blob_len.data_ptr()),
-                                                   n, actor_bytes, member_bytes, n_actors, flags,
-                                                   C.c_void_p(sizes.data_ptr()), st), "bincode_record_sizes")
+        if packed:
+            check(lib.crdt_orswot_bincode_record_sizes(self.ctx, C.c_void_p(blobs.data_ptr()), int(blobs.numel()),
+                                                       C.c_void_p(blob_off.data_ptr()),
+                                                       C.c_void_p(blob_len.data_ptr()), n, actor_bytes, member_bytes,
+                                                       n_actors, flags, C.c_void_p(sizes.data_ptr()), st),
+                  "bincode_record_sizes")
+        else:
+            check(lib.crdt_orswot_bincode_record_bounds(self.ctx, C.c_void_p(blob_len.data_ptr()), n, actor_bytes,
+                                                        member_bytes, n_actors, flags, C.c_void_p(sizes.data_ptr()),
+                                                        st), "bincode_record_bounds")
         with torch.cuda.stream(stream) if stream is not None else _nullctx():
             ends = torch.cumsum(sizes, 0)
             total = int(ends[-1].item()) if n else 0

@@ -65,7 +65,7 @@ EXPORTS = [
     "crdt_orswot_validate_ex", "crdt_orswot_generate_replicas", "crdt_host_orswot_encode_ex",
     "crdt_orswot_bincode_record_sizes", "crdt_orswot_from_bincode", "crdt_orswot_bincode_sizes",
     "crdt_orswot_to_bincode", "crdt_orswot_apply", "crdt_vclock_partial_cmp", "crdt_mvreg_merge",
-    "crdt_map_mvreg_merge", "crdt_map_orswot_merge", "crdt_ctx_set_list_cap",
+    "crdt_map_mvreg_merge", "crdt_map_orswot_merge", "crdt_ctx_set_list_cap", "crdt_orswot_bincode_record_bounds",
     "crdt_comm_unique_id", "crdt_comm_init", "crdt_comm_destroy", "crdt_replica_allreduce_max",
     "crdt_orswot_replica_join_bound", "crdt_orswot_replica_join", "crdt_orswot_replica_join_local",
 ]
@@ -149,6 +149,7 @@ def _load():
         "crdt_orswot_generate_replicas": (I, [U64, SZ, SZ, C.POINTER(RepParams), U32, U32, I, C.POINTER(P)]),
         "crdt_host_orswot_encode_ex": (C.c_long, [P, U32, U32, P, SZ]),
         "crdt_orswot_bincode_record_sizes": (I, [P, P, SZ, P, P, SZ, U32, U32, U32, U32, P, P]),
+        "crdt_orswot_bincode_record_bounds": (I, [P, P, SZ, U32, U32, U32, U32, P, P]),
         "crdt_orswot_from_bincode": (I, [P, P, SZ, P, P, SZ, U32, U32, U32, U32, P, P, SZ, P]),
         "crdt_orswot_bincode_sizes": (I, [P, BP, U32, U32, U32, U32, P, P]),
         "crdt_orswot_to_bincode": (I, [P, BP, U32, U32, U32, U32, P, P, SZ, P]),

@@ -306,6 +306,17 @@ int crdt_orswot_bincode_record_sizes(crdt_ctx* ctx, const uint8_t* d_blobs, size
                                n_actors, flags, d_sizes, nullptr, nullptr, 0, ctx->d_status, S(stream));
 }
 
+int crdt_orswot_bincode_record_bounds(crdt_ctx* ctx, const uint64_t* d_blob_len, size_t n_obj,
+                                      uint32_t actor_bytes, uint32_t member_bytes, uint32_t n_actors, uint32_t flags,
+                                      uint64_t* d_bounds, void* stream) {
+  if (!ctx || (n_obj && (!d_blob_len || !d_bounds)) || !bc_width_ok(actor_bytes) || !bc_width_ok(member_bytes) ||
+      n_actors == 0 || (flags & ~CRDT_ORSWOT_SPARSE_CLOCK))
+    return CRDT_EINVAL;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return launch_bincode_bounds(d_blob_len, n_obj, actor_bytes, member_bytes, n_actors, flags, d_bounds, S(stream));
+}
+
 int crdt_orswot_from_bincode(crdt_ctx* ctx, const uint8_t* d_blobs, size_t blob_bytes,
                              const uint64_t* d_blob_off, const uint64_t* d_blob_len, size_t n_obj,
                              uint32_t actor_bytes, uint32_t member_bytes, uint32_t n_actors, uint32_t flags,

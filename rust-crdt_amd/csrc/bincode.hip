@@ -1000,7 +1000,41 @@ uint32_t bc_blocks(uint64_t n_obj) {
   return (uint32_t)(want < cap ? want : cap);
 }
 
+// Record placement without reading the blobs: a bound on the record size of
+// blob i from its length alone (crdt_orswot_bincode_record_bounds). Against
+// the blob's bytes (u64 lengths before the clock, entries and deferred maps;
+// wa / wm bytes per actor / member; 8 per counter), every record section is
+// at most c times the blob bytes it comes from, c = max(12 / (wa + 8),
+// 12 / (wm + 8), 8 / wm): a member (12 B: key + run end) vs wm + 8, a dot
+// (12 B) vs wa + 8, a deferred clock's two ends (8 B) vs its 16 B of
+// lengths, a deferred member (8 B) vs wm, a sparse top-clock entry (12 B) vs
+// wa + 8. The header, a dense clock and the paddings add 48 + 8 A at most.
+__device__ __forceinline__ uint64_t bc_record_bound(uint64_t L, uint32_t wa, uint32_t wm, uint32_t A, bool sparse) {
+  const uint64_t m1 = (12u * L + wa + 7u) / (wa + 8u), m2 = (12u * L + wm + 7u) / (wm + 8u),
+                 m3 = (8u * L + wm - 1u) / wm;
+  uint64_t c = m1 > m2 ? m1 : m2;
+  c = c > m3 ? c : m3;
+  return (48u + (sparse ? 0ull : 8ull * A) + c + 15u) & ~15ull;
+}
+
+__global__ __launch_bounds__(256) void bincode_bounds_kernel(const uint64_t* __restrict__ blen, uint64_t n_obj,
+                                                             uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags,
+                                                             uint64_t* __restrict__ bounds) {
+  const bool sparse = (flags & kSparseClock) != 0u;
+  for (uint64_t o = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n_obj; o += (uint64_t)gridDim.x * blockDim.x)
+    bounds[o] = bc_record_bound(blen[o], wa, wm, A, sparse);
+}
+
 }  // namespace
+
+int launch_bincode_bounds(const uint64_t* blen, uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A,
+                          uint32_t flags, uint64_t* bounds, hipStream_t stream) {
+  if (n_obj == 0) return CRDT_OK;
+  const uint64_t want = (n_obj + 255u) / 256u;
+  const uint32_t blocks = (uint32_t)(want < 4096u ? want : 4096u);
+  hipLaunchKernelGGL(bincode_bounds_kernel, dim3(blocks), dim3(256), 0, stream, blen, n_obj, wa, wm, A, flags, bounds);
+  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+}
 
 int launch_bincode_ingest(const uint8_t* blobs, uint64_t blob_bytes, const uint64_t* boff, const uint64_t* blen,
                           uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags, uint64_t* sizes,

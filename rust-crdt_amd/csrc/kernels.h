@@ -28,6 +28,8 @@ int launch_record_sizes(const uint8_t* base, const uint64_t* off, uint64_t n_obj
 int launch_record_copy(const uint8_t* src, const uint64_t* src_off, uint8_t* dst,
                        const uint64_t* dst_off, uint64_t n_obj, hipStream_t stream);
 
+int launch_bincode_bounds(const uint64_t* blen, uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A,
+                          uint32_t flags, uint64_t* bounds, hipStream_t stream);
 int launch_bincode_ingest(const uint8_t* blobs, uint64_t blob_bytes, const uint64_t* boff, const uint64_t* blen,
                           uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags, uint64_t* sizes,
                           uint8_t* out, const uint64_t* ooff, uint64_t out_bytes, int* status, hipStream_t stream,

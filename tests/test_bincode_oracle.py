@@ -122,3 +122,51 @@ def test_cpp_restatement_agrees(oracle):
         assert oracle.bincode_to_record(blob, 2, 8, 1024, 1) == records.encode(
             st["clock"], {m: dict(d) for m, d in st["entries"].items()},
             {tuple(c): set(ms) for c, ms in st["deferred"]}, 1024, True)
+
+
+def extreme_state(rng, A, wa, wm):
+    """A state stressing one bound term or another: many one-dot members,
+    big deferred sets of narrow members, several deferred clocks, or empty."""
+    alim = min(A, 1 << (8 * wa)) if wa < 8 else A
+    acts = rng.sample(range(alim), rng.choice([1, 2, min(5, alim), min(16, alim)]))
+    mlim = 1 << (8 * wm) if wm < 8 else 1 << 40
+    ents = {}
+    for _ in range(rng.choice([0, 1, 40])):
+        ents[rng.randrange(mlim)] = sorted((a, rng.randrange(1, 9))
+                                           for a in rng.sample(acts, rng.randrange(1, len(acts) + 1)))
+    clock = {}
+    for d in ents.values():
+        for a, c in d:
+            clock[a] = max(clock.get(a, 0), c)
+    deferred, seen = [], set()
+    for _ in range(rng.choice([0, 1, 8])):
+        dc = tuple(sorted((a, rng.randrange(10, 20)) for a in rng.sample(acts, rng.randrange(1, len(acts) + 1))))
+        if dc not in seen:
+            seen.add(dc)
+            deferred.append((list(dc), sorted({rng.randrange(mlim) for _ in range(rng.choice([1, 30]))})))
+    return dict(clock=clock, entries=ents, deferred=deferred)
+
+
+def bincode_record_bound(L, wa, wm, A, sparse):
+    """Mirror of bc_record_bound (rust-crdt_amd/csrc/bincode.hip): the record
+    bytes of any blob of L bytes are at most 48 + 8 A (dense) + ceil(c L),
+    c = max(12 / (wa + 8), 12 / (wm + 8), 8 / wm), rounded up to 16."""
+    c = max(-(-12 * L // (wa + 8)), -(-12 * L // (wm + 8)), -(-8 * L // wm))
+    return (48 + (0 if sparse else 8 * A) + c + 15) // 16 * 16
+
+
+@pytest.mark.parametrize("wa,wm", [(1, 1), (1, 8), (2, 2), (8, 1), (8, 8), (4, 2)])
+@pytest.mark.parametrize("sparse", [False, True])
+def test_record_bound_holds(wa, wm, sparse):
+    """The placement bound behind crdt_orswot_bincode_record_bounds, against
+    the real record size, on shapes that stress each of its terms."""
+    import random
+
+    rng = random.Random(wa * 10 + wm + sparse)
+    A = 256 if sparse else 16
+    for _ in range(2000):
+        st = extreme_state(rng, A, wa, wm)
+        L = len(BC.encode(st, wa, wm))
+        rec = records.encode(st["clock"], {m: dict(d) for m, d in st["entries"].items()},
+                             {tuple(c): set(ms) for c, ms in st["deferred"]}, A, sparse)
+        assert len(rec) <= bincode_record_bound(L, wa, wm, A, sparse), (len(rec), L, st)

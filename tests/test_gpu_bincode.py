@@ -16,7 +16,7 @@ import records
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "oracle"))
 import bincode_ref as BC  # noqa: E402
-from test_bincode_oracle import small_members  # noqa: E402
+from test_bincode_oracle import extreme_state, small_members  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -91,6 +91,7 @@ def test_widths_both_ways(gpu, wa, wm):
     rng = random.Random(wa + wm)
     t, bo, bl = _upload_blobs([BC.encode(s, wa, wm, rng=rng) for s in sts], rng)
     assert gpu.orswot_from_bincode(t, bo, bl, 16, wa, wm).records() == recs
+    assert gpu.orswot_from_bincode(t, bo, bl, 16, wa, wm, packed=False).records() == recs
     B = crdts_hip.OrswotBatch.from_records(recs, 16)
     assert _blobs_of(*gpu.orswot_to_bincode(B, wa, wm)) == [BC.encode(s, wa, wm) for s in sts]
 
@@ -106,6 +107,7 @@ def test_sparse_config5_both_ways(gpu):
     SP = crdts_hip.SPARSE_CLOCK
     out = gpu.orswot_from_bincode(t, bo, bl, 1024, 2, 8, flags=SP)
     assert out.records() == recs
+    assert gpu.orswot_from_bincode(t, bo, bl, 1024, 2, 8, flags=SP, packed=False).records() == recs
     B = crdts_hip.OrswotBatch.from_host(b, o, 1024, flags=SP)
     assert _blobs_of(*gpu.orswot_to_bincode(B, 2, 8)) == [BC.encode(s, 2, 8) for s in sts]
 
@@ -123,6 +125,33 @@ def test_round_trip_full_config3(gpu):
     assert torch.equal(back.off, B.off)
     n = int(b.nbytes)
     assert torch.equal(back.base[:n], B.base[:n])
+    # one-read ingest (records placed by their bounds): the same records with
+    # gaps; compacted, the same bytes
+    gapped = gpu.orswot_from_bincode(blobs, boff, blen, 16, 1, 8, packed=False)
+    sizes = gapped.base.view(torch.int32)[gapped.off // 4].to(torch.int64)
+    ref_sizes = B.base.view(torch.int32)[B.off // 4].to(torch.int64)
+    assert torch.equal(sizes, ref_sizes)
+    assert bool((gapped.off[1:] - gapped.off[:-1] >= sizes[:-1]).all())
+    packed = gpu.orswot_compact(gapped)
+    assert torch.equal(packed.off, B.off) and torch.equal(packed.base[:n], B.base[:n])
+
+
+@pytest.mark.parametrize("wa,wm", [(1, 1), (1, 8), (2, 2), (8, 1), (8, 8), (4, 2)])
+@pytest.mark.parametrize("sparse", [False, True])
+def test_bound_placement_extreme_shapes(gpu, wa, wm, sparse):
+    """Records placed by crdt_orswot_bincode_record_bounds for shapes that
+    stress each term of the bound (narrow members in big deferred sets, many
+    one-dot members, sparse clocks): every record is decoded whole into its
+    slot, byte-exact."""
+    import crdts_hip
+
+    rng = random.Random(wa * 10 + wm + sparse)
+    A = 256 if sparse else 16
+    sts = [extreme_state(rng, A, wa, wm) for _ in range(400)]
+    t, bo, bl = _upload_blobs([BC.encode(s, wa, wm) for s in sts])
+    SP = crdts_hip.SPARSE_CLOCK if sparse else 0
+    out = gpu.orswot_from_bincode(t, bo, bl, A, wa, wm, flags=SP, packed=False)
+    assert out.records() == [_rec(s, A, sparse) for s in sts]
 
 
 def test_malformed_blobs(gpu):
