@@ -112,19 +112,30 @@ __device__ __forceinline__ RV make_rv(const RecLayout& L) {
   return v;
 }
 
-// Record accessors (base = LDS stage or HBM record; offsets in bytes).
+// Record accessors (base = LDS stage or HBM record; offsets in bytes). The
+// base is a generic pointer, or an LDS-typed one (lds_cu8: ds_* loads, no
+// flat round trip) where the record is known to sit in the wave's stage.
+typedef const __attribute__((address_space(3))) uint8_t lds_cu8;
 __device__ __forceinline__ uint64_t g64(const uint8_t* b, uint32_t off, uint32_t i) {
   return *(const uint64_t*)(b + off + 8u * i);
 }
 __device__ __forceinline__ uint32_t g32(const uint8_t* b, uint32_t off, uint32_t i) {
   return *(const uint32_t*)(b + off + 4u * i);
 }
+__device__ __forceinline__ uint64_t g64(lds_cu8* b, uint32_t off, uint32_t i) {
+  return *(const __attribute__((address_space(3))) uint64_t*)(b + off + 8u * i);
+}
+__device__ __forceinline__ uint32_t g32(lds_cu8* b, uint32_t off, uint32_t i) {
+  return *(const __attribute__((address_space(3))) uint32_t*)(b + off + 4u * i);
+}
 // VClock::get on a dense top clock, absent = 0 (src/vclock.rs:206-210)
-__device__ __forceinline__ uint64_t top(const uint8_t* b, const RV& v, uint32_t a, uint32_t A) {
+template <class P>
+__device__ __forceinline__ uint64_t top(P b, const RV& v, uint32_t a, uint32_t A) {
   return a < A ? g64(b, v.clk, a) : 0ull;
 }
 // First index k in [0, n) of the sparse clock's actor list with act[k] >= a.
-__device__ __forceinline__ uint32_t clk_lower_bound(const uint8_t* b, const RV& v, uint32_t a) {
+template <class P>
+__device__ __forceinline__ uint32_t clk_lower_bound(P b, const RV& v, uint32_t a) {
   uint32_t lo = 0, n = v.n_clk;
   while (n) {
     const uint32_t h = n >> 1;
@@ -133,20 +144,24 @@ __device__ __forceinline__ uint32_t clk_lower_bound(const uint8_t* b, const RV& 
   return lo;
 }
 // VClock::get for either clock form: a CSR clock is searched (sorted actors).
-template <bool SP>
-__device__ __forceinline__ uint64_t topv(const uint8_t* b, const RV& v, uint32_t a, uint32_t A) {
+template <bool SP, class P>
+__device__ __forceinline__ uint64_t topv(P b, const RV& v, uint32_t a, uint32_t A) {
   if (!SP) return top(b, v, a, A);
   const uint32_t k = clk_lower_bound(b, v, a);
   return (k < v.n_clk && g32(b, v.cact, k) == a) ? g64(b, v.clk, k) : 0ull;
 }
-__device__ __forceinline__ uint32_t run_begin(const uint8_t* b, uint32_t off, uint32_t k) {
+template <class P>
+__device__ __forceinline__ uint32_t run_begin(P b, uint32_t off, uint32_t k) {
   return k ? g32(b, off, k - 1) : 0u;
 }
 
-struct Side {
-  const uint8_t* b;
+template <class P>
+struct SideT {
+  P b;
   RV v;
 };
+typedef SideT<const uint8_t*> Side;
+typedef SideT<lds_cu8*> SideL;  // a record in the wave's LDS stage
 
 // D[x] for deferred clock k (actor-sorted run), 0 if absent.
 __device__ __forceinline__ uint64_t def_get(const Side& s, uint32_t k, uint32_t x) {
@@ -336,7 +351,8 @@ __device__ void deferred_pass(const Side& L, const Side& R, uint32_t A, uint32_t
 // ORDER by a wave-uniform loop; per entry the dot-level work (clock compare,
 // survival test, copies) is spread over the lanes. With w == nullptr only
 // counts. Every lane returns the same counts.
-__device__ __forceinline__ int clock_cmp_wave(const Side& X, uint32_t k, const Side& Y, uint32_t l, uint32_t lane) {
+template <class S>
+__device__ __forceinline__ int clock_cmp_wave(const S& X, uint32_t k, const S& Y, uint32_t l, uint32_t lane) {
   const uint32_t a0 = uni(run_begin(X.b, X.v.fdend, k)), na = uni(g32(X.b, X.v.fdend, k)) - a0;
   const uint32_t b0 = uni(run_begin(Y.b, Y.v.fdend, l)), nb = uni(g32(Y.b, Y.v.fdend, l)) - b0;
   const uint32_t n = na < nb ? na : nb;
@@ -354,8 +370,8 @@ __device__ __forceinline__ int clock_cmp_wave(const Side& X, uint32_t k, const S
   return na == nb ? 0 : (na < nb ? -1 : 1);
 }
 
-template <bool SP = false>
-__device__ __forceinline__ bool def_survives_wave(const Side& X, uint32_t k, const Side& L, const Side& R, uint32_t A,
+template <bool SP = false, class S>
+__device__ __forceinline__ bool def_survives_wave(const S& X, uint32_t k, const S& L, const S& R, uint32_t A,
                                                   uint32_t lane) {
   const uint32_t s = uni(run_begin(X.b, X.v.fdend, k)), e = uni(g32(X.b, X.v.fdend, k));
   bool any = false;
@@ -369,10 +385,11 @@ __device__ __forceinline__ bool def_survives_wave(const Side& X, uint32_t k, con
 
 // One surviving deferred entry: clock kx of side X (c: -1 L only, 1 R only,
 // 0 on both sides — member sets united), written at the running counts.
-__device__ __forceinline__ void deferred_emit(const Side& L, const Side& R, int c, uint32_t k, uint32_t l,
+template <class S>
+__device__ __forceinline__ void deferred_emit(const S& L, const S& R, int c, uint32_t k, uint32_t l,
                                               uint32_t lane, uint32_t& nd, uint32_t& ndd, uint32_t& ndm,
                                               const DefOut* w) {
-  const Side& X = c <= 0 ? L : R;
+  const S& X = c <= 0 ? L : R;
   const uint32_t kx = c <= 0 ? k : l;
   const uint32_t s = uni(run_begin(X.b, X.v.fdend, kx)), e = uni(g32(X.b, X.v.fdend, kx));
   if (w)
@@ -414,8 +431,8 @@ __device__ __forceinline__ void deferred_emit(const Side& L, const Side& R, int 
 // (w == nullptr) records each survivor as k | l << 8 | (c + 1) << 16, and a
 // writing walk given the recorded count replays them without the clock
 // compares and survival tests.
-template <bool SP = false>
-__device__ void deferred_pass_wave(const Side& L, const Side& R, uint32_t A, uint32_t lane, uint32_t& nd,
+template <bool SP = false, class S = Side>
+__device__ void deferred_pass_wave(const S& L, const S& R, uint32_t A, uint32_t lane, uint32_t& nd,
                                    uint32_t& ndd, uint32_t& ndm, const DefOut* w, uint32_t* cache = nullptr,
                                    uint32_t n_cached = 0) {
   if (w && cache) {
@@ -431,7 +448,7 @@ __device__ void deferred_pass_wave(const Side& L, const Side& R, uint32_t A, uin
   const uint32_t nfL = uni(L.v.n_def), nfR = uni(R.v.n_def);
   while (k < nfL || l < nfR) {
     const int c = k >= nfL ? 1 : (l >= nfR ? -1 : clock_cmp_wave(L, k, R, l, lane));
-    const Side& X = c <= 0 ? L : R;
+    const S& X = c <= 0 ? L : R;
     const uint32_t kx = c <= 0 ? k : l;
     if (def_survives_wave<SP>(X, kx, L, R, A, lane)) {
       if (cache && lane == 0u) cache[nd] = k | (l << 8) | ((uint32_t)(c + 1) << 16);
@@ -1193,7 +1210,7 @@ __device__ __forceinline__ uint32_t rank_below(const uint8_t* b, uint32_t off, u
 // kept dots are checked against the deferred clocks listing their member
 // (apply_deferred -> apply_remove, src/orswot.rs:235-243, 195-211) and the
 // deferred block is the wave-cooperative union + filter (:141-148, :197).
-template <uint32_t OUTCAP, bool HD = false, int ABL = 0>
+template <uint32_t OUTCAP, bool HD = false, int ABL = 0, bool DC = false>
 __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* X, u32x4* Os,
                                                 uint32_t A, uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR,
                                                 uint32_t lane, bool& big, Stamps* stp = nullptr) {
@@ -1324,7 +1341,11 @@ __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t
   const uint32_t cincl = scan_incl(c);
   const uint32_t tot_dot = lane_of(cincl, kWave - 1);
   uint32_t nd = 0, ndd = 0, ndm = 0;
-  if (HD) deferred_pass_wave(DL, DR, A, lane, nd, ndd, ndm, nullptr);
+  // DC: the counting walk records its survivors (in the equal / >= area, read
+  // into registers above) and the writing walk replays them
+  uint32_t* const dcache = DC ? (uint32_t*)(X + kEqGe) : nullptr;
+  if (HD) deferred_pass_wave(DL, DR, A, lane, nd, ndd, ndm, nullptr, dcache);
+  const uint32_t nd_counted = nd;
   RecLayout OL;
   rec_layout(OL, A, tot_mem, tot_dot, nd, ndd, ndm);
   const uint32_t size = OL.size;
@@ -1368,7 +1389,7 @@ __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t
   if (HD) {  // deferred union keyed by clock (:141-148), kept iff !(D <= clock) (:197)
     DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
              (uint32_t*)(O + OL.o_fdend), (uint32_t*)(O + OL.o_fmend)};
-    deferred_pass_wave(DL, DR, A, lane, nd, ndd, ndm, &w);
+    deferred_pass_wave(DL, DR, A, lane, nd, ndd, ndm, &w, dcache, nd_counted);
   }
   // zero padding: member block to 8 (<= 4 B) and record to 16 (<= 12 B)
   if (lane == 0u && OL.o_def != OL.o_mpad) *(uint32_t*)(O + OL.o_mpad) = 0u;
@@ -1460,7 +1481,15 @@ __device__ __forceinline__ void copy_record_out(uint32_t src, uint8_t* O, uint32
   __builtin_nontemporal_store(p1, (u32x4*)(O + 16u * i1));
 }
 
-template <uint32_t OUTCAP, int OUT = 0>  // OUT: 0 direct stores, 1 sink-predicated, 2 LDS-assembled
+// HD (with OUT 0 only): objects with deferred removes — kept dots that a
+// deferred clock listing their member covers are cleared from the keep masks
+// (apply_deferred -> apply_remove, src/orswot.rs:235-243, :195-211) and the
+// deferred block (the union of both deferred maps in CLOCK ORDER, kept iff
+// !(D <= merged clock), :141-148, :197) is written after the member block.
+__device__ __forceinline__ const uint8_t* gptr(uint32_t a) {
+  return (const uint8_t*)(const __attribute__((address_space(3))) uint8_t*)(size_t)a;
+}
+template <uint32_t OUTCAP, int OUT = 0, bool HD = false, int HABL = 0>  // OUT: 0 direct stores, 1 sink-predicated, 2 LDS-assembled
 __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint32_t uX, uint8_t* O, uint32_t A,
                                                  uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane,
                                                  bool& big, uint8_t* sink = nullptr) {
@@ -1579,8 +1608,99 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
   const uint32_t lp = bit_of(selfonly, lane) ? ML : FL, rp = FR;
   const uint32_t useA = (ML & MR & EQm) | (lp & (~rp | GEm));
   const uint64_t dropS = cmp32<kEQ>(FL, 0u) & selfonly;  // self-only entry not above R's clock: dropped whole
-  const uint32_t keep = (bit_of(dropS, lane) || !bit_of(mU, lane)) ? 0u : (useA | rp);
-  const uint32_t useK = useA & keep;
+  uint32_t keep = (bit_of(dropS, lane) || !bit_of(mU, lane)) ? 0u : (useA | rp);
+  uint32_t useK = useA & keep;
+  Side DL{nullptr, RV{}}, DR{nullptr, RV{}};
+  if (HD && HABL != 1) {  // (HABL: timing-only ablations, diagnostic builds)
+    static_assert(!HD || OUT == 0, "deferred removes: direct stores only");
+    DL = side_of(gptr(uL));
+    DR = side_of(gptr(uR));
+    // {keep, useK} by union slot (over the member masks, read above), and by
+    // union slot the deferred clocks naming that member (bit k: self's clock
+    // k, 32 + k: other's) — built from the deferred member lists, one lane per
+    // (clock, member) item: the clock by a search over the run ends, the
+    // union slot by a search of the key among each side's members
+    const uint32_t dmt = uX + k3EqGe;
+    *(lds_u64*)(size_t)(uX + k3Out + l8) = (uint64_t)keep | ((uint64_t)useK << 32);
+    *(lds_u64*)(size_t)(dmt + l8) = 0ull;
+    wave_sync();
+    const uint32_t nfL = DL.v.n_def, nfR = DR.v.n_def;
+    const uint32_t nmL = nfL ? uni(lr32(uL + DL.v.fmend + 4u * (nfL - 1u))) : 0u;
+    const uint32_t nmR = nfR ? uni(lr32(uR + DR.v.fmend + 4u * (nfR - 1u))) : 0u;
+    for (uint32_t base = 0; base < nmL + nmR; base += kWave) {
+      const uint32_t it = base + lane;
+      const bool isL = it < nmL, act = it < nmL + nmR;
+      const uint32_t us = isL ? uL : uR, j = act ? (isL ? it : it - nmL) : 0u;
+      const uint32_t fk = isL ? DL.v.fkey : DR.v.fkey, fm = isL ? DL.v.fmend : DR.v.fmend;
+      const uint32_t nf = isL ? nfL : nfR;
+      const uint64_t m = lr64(us + fk + 8u * j);
+      uint32_t k = 0;  // # run ends <= j (n_def <= 32 per side)
+      for (uint32_t step = 32u; step; step >>= 1)
+        k = (k + step <= nf && lr32(us + fm + 4u * (k + step - 1u)) <= j) ? k + step : k;
+      // rank of m among each side's member keys (clamped probes), then equality
+      uint32_t ql = lk0, qr = rk0;
+      {
+        const uint32_t n = nL > nR ? nL : nR;
+        for (uint32_t step = n ? 8u << (31u - __builtin_clz(n)) : 0u; step >= 8u; step >>= 1) {
+          const uint32_t cl = ql + step, cr = qr + step;
+          ql = lr64(cl < lkmax ? cl : lkmax) < m ? cl : ql;
+          qr = lr64(cr < rkmax ? cr : rkmax) < m ? cr : qr;
+        }
+      }
+      ql = ql < lkmax ? ql : lkmax;
+      qr = qr < rkmax ? qr : rkmax;
+      const uint32_t il = (ql - lk0) >> 3, ir = (qr - rk0) >> 3;
+      const bool eqL = nL && il < nL && lr64(ql + 8u < lkmax ? ql + 8u : lkmax) == m;
+      const bool eqR = nR && ir < nR && lr64(qr + 8u < rkmax ? qr + 8u : rkmax) == m;
+      const uint32_t sul = gather32(ul, il & 63u), sur = gather32(ur, ir & 63u);  // every lane: bpermute sources
+      const uint32_t su = eqL ? sul : sur;
+      const bool hit = act && (eqL || eqR);
+      __hip_atomic_fetch_or((lds_u64*)(size_t)(hit ? dmt + 8u * (su & 63u) : uX + k3Trash + l8),
+                            hit ? 1ull << (isL ? k : 32u + k) : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    wave_sync();
+    // a surviving self dot / kept other dot of a named member: killed if D[x] >= v
+    const uint32_t gl = gather32(ul, ml) & 63u, gr = gather32(ur, mr) & 63u;
+    const uint64_t okl = lr64(uX + k3Out + 8u * gl), okr = lr64(uX + k3Out + 8u * gr);
+    uint64_t bitsl = (bit_of(mdL, lane) && ((uint32_t)(okl >> 32) & bl)) ? lr64(dmt + 8u * gl) : 0ull;
+    uint64_t bitsr = (bit_of(mdR, lane) && (((uint32_t)okr & ~(uint32_t)(okr >> 32)) & br)) ? lr64(dmt + 8u * gr) : 0ull;
+    // section addresses of both sides (scalars: no struct selected at run time)
+    const uint32_t fdL = uL + DL.v.fdend, faL = uL + DL.v.fact, fcL = uL + DL.v.fctr;
+    const uint32_t fdR = uR + DR.v.fdend, faR = uR + DR.v.fact, fcR = uR + DR.v.fctr;
+    // D[x] of clock bit kb: a fixed-trip binary search of its actor-sorted run
+    // (a deferred clock of an object on this path has <= A <= 32 entries)
+    auto dget = [&](uint32_t kb, uint32_t x) -> uint64_t {
+      const bool sL = kb < 32u;
+      const uint32_t kk = kb & 31u, fd = sL ? fdL : fdR, fa = sL ? faL : faR, fc = sL ? fcL : fcR;
+      uint32_t lo = kk ? lr32(fd + 4u * (kk - 1u)) : 0u;
+      const uint32_t e = lr32(fd + 4u * kk);
+      uint32_t len = e - lo;
+#pragma unroll
+      for (int st = 0; st < 6; ++st) {
+        const uint32_t half = len >> 1, mid = lo + half;
+        const bool go = len != 0u && lr32(fa + 4u * mid) < x;
+        lo = go ? mid + 1u : lo;
+        len = len == 0u ? 0u : (go ? len - half - 1u : half);
+      }
+      return (lo < e && lr32(fa + 4u * lo) == x) ? lr64(fc + 8u * lo) : 0ull;
+    };
+    bool kl2 = false, kr2 = false;
+    while (bitsl | bitsr) {  // both dots' clocks in the same trips
+      const uint64_t dl = bitsl ? dget((uint32_t)__builtin_ctzll(bitsl), xl & 31u) : 0ull;
+      const uint64_t dr = bitsr ? dget((uint32_t)__builtin_ctzll(bitsr), xr & 31u) : 0ull;
+      kl2 = kl2 || (bitsl && dl >= vl);
+      kr2 = kr2 || (bitsr && dr >= vr);
+      bitsl &= bitsl - 1u;
+      bitsr &= bitsr - 1u;
+    }
+    __hip_atomic_fetch_and((lds_u64*)(size_t)(kl2 ? uX + k3Out + 8u * gl : uX + k3Trash + l8), kl2 ? ~(uint64_t)bl : ~0ull,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_and((lds_u64*)(size_t)(kr2 ? uX + k3Out + 8u * gr : uX + k3Trash + l8), kr2 ? ~(uint64_t)br : ~0ull,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    wave_sync();
+    keep = bit_of(mU, lane) ? (uint32_t)lr64(uX + k3Out + l8) : 0u;
+    useK &= keep;
+  }
   const uint32_t c = __popc(keep);
 
   // ---- output layout
@@ -1588,9 +1708,17 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
   const uint32_t tot_mem = (uint32_t)__popcll(keepm);
   const uint32_t cincl = scan_incl(c);
   const uint32_t tot_dot = lane_of(cincl, kWave - 1);
+  // HD: the deferred union is counted first; its walk records the survivors
+  // (in the equal / >= area, read above) for the writing walk to replay
+  uint32_t nd = 0, ndd = 0, ndm = 0;
+  uint32_t* const dcache = HD ? (uint32_t*)gptr(uX + k3EqGe) : nullptr;
+  const SideL WL{(lds_cu8*)(size_t)uL, DL.v}, WR{(lds_cu8*)(size_t)uR, DR.v};  // the walks read LDS directly
+  if (HD && HABL != 2) deferred_pass_wave(WL, WR, A, lane, nd, ndd, ndm, nullptr, dcache);
   const uint32_t o_key = kHdrBytes + 8u * A, o_dctr = o_key + 8u * tot_mem, o_dact = o_dctr + 8u * tot_dot;
   const uint32_t o_mdend = o_dact + 4u * tot_dot, o_mpad = o_mdend + 4u * tot_mem;
-  const uint32_t o_def = (o_mpad + 7u) & ~7u, size = (o_def + 15u) & ~15u;
+  const uint32_t o_def = (o_mpad + 7u) & ~7u;
+  const uint32_t o_end = o_def + 12u * ndd + 8u * ndm + 8u * nd;  // == o_def without deferred removes
+  const uint32_t size = (o_end + 15u) & ~15u;
   if (OUT == 0 && size > OUTCAP) {
     big = true;
     return 0u;
@@ -1677,11 +1805,18 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
       octr[ir] = vr2;
     }
     if (lane == 0u && o_def != o_mpad) *(uint32_t*)(O + o_mpad) = 0u;
-    if (lane >= 1u && lane < 4u && o_def + 4u * (lane - 1u) < size) *(uint32_t*)(O + o_def + 4u * (lane - 1u)) = 0u;
+    if (lane >= 1u && lane < 4u && o_end + 4u * (lane - 1u) < size) *(uint32_t*)(O + o_end + 4u * (lane - 1u)) = 0u;
     if (lane == 0u) {
       u32x4* h = (u32x4*)O;
       h[0] = u32x4{size, A, tot_mem, tot_dot};
-      h[1] = u32x4{0u, 0u, 0u, 0u};
+      h[1] = u32x4{nd, ndd, ndm, 0u};
+    }
+    if (HD && HABL != 2) {  // the deferred block (rec_layout's order: ctr, key, act, dend, mend)
+      const uint32_t o_fkey = o_def + 8u * ndd, o_fact = o_fkey + 8u * ndm, o_fdend = o_fact + 4u * ndd;
+      DefOut w{(uint64_t*)(O + o_def), (uint64_t*)(O + o_fkey), (uint32_t*)(O + o_fact), (uint32_t*)(O + o_fdend),
+               (uint32_t*)(O + o_fdend + 4u * nd)};
+      uint32_t a1, a2, a3;
+      deferred_pass_wave(WL, WR, A, lane, a1, a2, a3, &w, dcache, nd);
     }
   }
   return OUT != 0 && fb ? kLeanFallback : size / 16u;
@@ -2589,7 +2724,7 @@ __attribute__((noinline)) __device__ uint32_t hd_join(const uint8_t* Ls, const u
 // (mask_object<HD>) and is followed by the same tail stores as the other
 // path, redirected to the sink: every path issues at least as many stores
 // after the prefetch as the lean one, so its loop-head wait stays exact
-template <int MINW, int MODE, int OUT = 2, bool HDD = false>
+template <int MINW, int MODE, int OUT = 2, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
@@ -2614,7 +2749,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
   const uint32_t n_def = MODE == 2 ? uni(__hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : 0u;
   const bool listed = MODE == 2 && n_def <= kDeferListCap;
   const uint64_t n_items = listed ? n_def : n_obj;
-  const uint64_t cs2 = listed ? kWave : cs;
+  const uint64_t cs2 = listed ? (M3HD ? 1u : kWave) : cs;  // M3HD: one listed object per wave (parallelism)
   for (uint64_t cbase = wave_id * cs2; cbase < n_items; cbase += n_waves * cs2) {
     // ---- chunk state: lane k <-> object cbase + k (MODE 2 listed: entry cbase + k)
     const uint64_t item = cbase + lane;
@@ -2729,8 +2864,12 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
         bool direct = false;
         if ((defs >> t) & 1ull) {
           if (HDD) {
-            r = mask_object<0xFFFFFFFFu, true>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
-                                               m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big);
+            if (M3HD)
+              r = mask3_object<0xFFFFFFFFu, 0, true, HABL>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
+                                                     d & 0xFFFFu, m >> 16, d >> 16, lane, big);
+            else
+              r = mask_object<0xFFFFFFFFu, true, 0, DC>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo),
+                                                        A, m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big);
             direct = true;
           } else {
             r = hd_join((const uint8_t*)sL, (const uint8_t*)sR, X, out_s[wave], A, m, d, lane, &big);
@@ -2753,8 +2892,12 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
         *(Ooff + cbase + t) = oo | (fbu ? kPending : 0ull);
         *(fbu ? ctl + 1 : (uint32_t*)sink) = 1u;  // the wave's own sink word: no shared line
       } else {
-        r = mask_object<0xFFFFFFFFu, true>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
-                                           m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big);
+        if (M3HD)
+          r = mask3_object<0xFFFFFFFFu, 0, true>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
+                                                 d & 0xFFFFu, m >> 16, d >> 16, lane, big);
+        else
+          r = mask_object<0xFFFFFFFFu, true>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
+                                             m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big);
         if (lane == 0u) {
           Ooff[lane_of64(obj, t)] = oo | (r == kLeanFallback ? kPending : 0ull);  // clears kPendingHD
           if (r == kLeanFallback) ctl[1] = 1u;
@@ -3094,7 +3237,7 @@ __global__ __launch_bounds__(kWave) void orswot_sparse_general_kernel(
 namespace {
 // The join launch: MODE 3 (one pass) or the two passes MODE 1 + MODE 2,
 // then the general kernel.
-template <int MINW, bool ONE = true, bool HDD = false>
+template <int MINW, bool ONE = true, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0>
 int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                        const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
                        uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
@@ -3104,10 +3247,10 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
   const void* f1;
   const void* f2 = nullptr;
   if constexpr (ONE) {
-    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD>;
+    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL>;
   } else {
     f1 = (const void*)orswot_join_kernel<MINW, 1>;
-    f2 = (const void*)orswot_join_kernel<MINW, 2>;
+    f2 = (const void*)orswot_join_kernel<MINW, 2, 2, false, false, M3HD>;
   }
   static std::atomic<int> occ_cache[2][9];  // per (pass, MINW); HDD variants share: one of them per MINW
   int occ[2];
@@ -3149,14 +3292,16 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
              stream, blocks_per_cu);
   };
 #ifndef CRDT_DIAG
-  // The product path: orswot_join_kernel in one pass (mask3_object for the
-  // objects without deferred removes, mask_object<HD> for the rest) at 6
+  // The product path: orswot_join_kernel in one pass (mask3_object for every
+  // object; those with deferred removes take its HD form, direct stores) at 6
   // waves per SIMD, then the general kernel (measured best, tools/ab_bench.py;
   // DESIGN.md §4). Other variants exist in -DCRDT_DIAG builds only.
   (void)variant;
-  return go(launch_join_passes<6, true, true>);
+  return go(launch_join_passes<6, true, true, true, true>);
 #else
-  if (variant == 0 || (variant >= 25 && variant <= 31)) {
+  if (variant == 134) return go(launch_join_passes<6, true, true, true, true, 1>);  // timing only: no kill
+  if (variant == 135) return go(launch_join_passes<6, true, true, true, true, 2>);  // timing only: no deferred block
+  if (variant == 0 || (variant >= 25 && variant <= 34)) {
     switch (variant) {
       case 25: return go(launch_join_passes<4, false>);
       case 26: return go(launch_join_passes<5, false>);
@@ -3164,7 +3309,11 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
       case 28: return go(launch_join_passes<8, false>);
       case 29: return go(launch_join_passes<4, true>);
       case 30: return go(launch_join_passes<5, true, true>);
-      default: return go(launch_join_passes<6, true, true>);  // 0, 31: the product path
+      case 32: return go(launch_join_passes<6, true, true, true>);
+      case 33: return go(launch_join_passes<6, true, true, true, true>);
+      case 34: return go(launch_join_passes<6, false, false, false, true>);
+      case 0: return go(launch_join_passes<6, true, true, true, true>);  // the product path
+      default: return go(launch_join_passes<6, true, true>);  // 31: round-2 v8
     }
   }
   int dev = 0, cus = 256;
