@@ -1039,6 +1039,9 @@ def main():
     else:
         res = run_dense(args, rank, world, local, args.workload)
     if rank == 0:
+        import crdts_hip
+
+        res["build"] = crdts_hip.build_record()  # the library this run loaded, vs __graft_entry__.build()'s record
         print(json.dumps(res), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -13,6 +13,7 @@ Device memory and streams come from torch (plumbing only).
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -665,6 +666,27 @@ class HostOrswot:
         if not h:
             raise CrdtError(CRDT_ENONCANON, "decode")
         return HostOrswot(h)
+
+
+def build_record():
+    """The loaded library's sha256 and, if present, the build record written
+    by __graft_entry__.build() (rust-crdt_amd/lib/build_info.json): whether
+    the library in use is the one that build produced."""
+    import hashlib
+    import json
+
+    with open(LIB_PATH, "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()
+    rec = {"loaded": os.path.relpath(LIB_PATH, os.path.dirname(os.path.dirname(LIB_PATH))), "sha256": sha}
+    info = os.path.join(os.path.dirname(LIB_PATH), "build_info.json")
+    try:
+        with open(info) as f:
+            b = json.load(f)
+        rec.update(built_sha256_matches=b.get("sha256") == sha, built_from=b.get("git_head"),
+                   built_dirty=b.get("git_dirty"), built_at=b.get("built_at"), built_on=b.get("host"))
+    except (OSError, ValueError):
+        rec["build_info"] = None
+    return rec
 
 
 _default_engine = None
