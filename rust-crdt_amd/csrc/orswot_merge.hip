@@ -164,7 +164,8 @@ typedef SideT<const uint8_t*> Side;
 typedef SideT<lds_cu8*> SideL;  // a record in the wave's LDS stage
 
 // D[x] for deferred clock k (actor-sorted run), 0 if absent.
-__device__ __forceinline__ uint64_t def_get(const Side& s, uint32_t k, uint32_t x) {
+template <class S>
+__device__ __forceinline__ uint64_t def_get(const S& s, uint32_t k, uint32_t x) {
   uint32_t e = g32(s.b, s.v.fdend, k);
   for (uint32_t d = run_begin(s.b, s.v.fdend, k); d < e; ++d) {
     uint32_t a = g32(s.b, s.v.fact, d);
@@ -173,7 +174,8 @@ __device__ __forceinline__ uint64_t def_get(const Side& s, uint32_t k, uint32_t 
   return 0ull;
 }
 
-__device__ __forceinline__ bool def_has_member(const Side& s, uint32_t k, uint64_t m) {
+template <class S>
+__device__ __forceinline__ bool def_has_member(const S& s, uint32_t k, uint64_t m) {
   uint32_t lo = run_begin(s.b, s.v.fmend, k), hi = g32(s.b, s.v.fmend, k);
   while (lo < hi) {
     uint32_t mid = (lo + hi) >> 1;
@@ -707,14 +709,16 @@ __device__ __forceinline__ uint32_t fpath(const FSide& L, const FSide& R, uint32
 // bit k (k < 32) / 32+k of the mask says deferred clock k of self / other
 // lists this member, so each output dot is checked only against those
 // clocks (apply_remove via apply_deferred, src/orswot.rs:195-211, 235-243).
-__device__ __forceinline__ uint64_t dmask_of(const Side& DL, const Side& DR, uint64_t m) {
+template <class S>
+__device__ __forceinline__ uint64_t dmask_of(const S& DL, const S& DR, uint64_t m) {
   uint64_t mask = 0;
   for (uint32_t k = 0; k < DL.v.n_def; ++k) mask |= def_has_member(DL, k, m) ? (1ull << k) : 0ull;
   for (uint32_t k = 0; k < DR.v.n_def; ++k) mask |= def_has_member(DR, k, m) ? (1ull << (32 + k)) : 0ull;
   return mask;
 }
 
-__device__ __forceinline__ bool dkilled(const Side& DL, const Side& DR, uint64_t mask, uint32_t x, uint64_t v) {
+template <class S>
+__device__ __forceinline__ bool dkilled(const S& DL, const S& DR, uint64_t mask, uint32_t x, uint64_t v) {
   for (; mask; mask &= mask - 1) {
     const uint32_t k = (uint32_t)__builtin_ctzll(mask);
     if ((k < 32 ? def_get(DL, k, x) : def_get(DR, k - 32, x)) >= v) return true;
@@ -2232,10 +2236,10 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   keep = (self_only && (ML & FL) == 0ull) ? 0ull : keep;
   keep = hu ? keep : 0ull;
   uint64_t useK = useA & keep;
-  Side DL{Ls, RV{}}, DR{Rs, RV{}};
+  SideL DL{(lds_cu8*)(size_t)lds_addr(Ls), RV{}}, DR{(lds_cu8*)(size_t)lds_addr(Rs), RV{}};  // LDS stages: ds_* reads
   if (HD) {  // deferred removes (apply_deferred -> apply_remove, src/orswot.rs:235-243, 195-211)
-    DL = side_of(Ls);
-    DR = side_of(Rs);
+    DL.v = make_rv(layout_at(Ls));
+    DR.v = make_rv(layout_at(Rs));
     wave_sync();
     *(uint64_t*)(X + kSpOut + 32u * lane) = keep;
     *(uint64_t*)(X + kSpOut + 32u * lane + 8u) = useK;
