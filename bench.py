@@ -546,6 +546,13 @@ def run_gcounter_ae(args, rank, world, local):
         res["comm"] = {"algbw_GBps": bytes_per_gpu / (ev_ms * 1e-3) / 1e9,
                        "busbw_GBps": 2 * (world - 1) / world * bytes_per_gpu / (ev_ms * 1e-3) / 1e9,
                        "xgmi_peak_GBps": 7 * 153}
+        # the owner-shard variant: reduce-scatter(max),
+        # each rank keeps its 1/N of the joined counters (crdt_replica_reduce_scatter_max)
+        flat = base.reshape(-1)[: (base.numel() // world) * world]
+        _, rs_ms = _timed_steps(args, world, stream,
+                                lambda: replica.dense_reduce_scatter_max(flat, engine=eng, stream=stream))
+        res["comm"]["reduce_scatter"] = {"ms": rs_ms, "algbw_GBps": bytes_per_gpu / (rs_ms * 1e-3) / 1e9,
+                                         "busbw_GBps": (world - 1) / world * bytes_per_gpu / (rs_ms * 1e-3) / 1e9}
     else:
         ach = 3 * bytes_per_gpu / (ev_ms * 1e-3) / 1e9
         res["roofline"] = {"bound": "hbm", "kernel": "dense_max_kernel", "achieved": ach, "peak": HBM_PEAK_GBS,

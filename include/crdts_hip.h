@@ -243,6 +243,12 @@ int crdt_comm_destroy(crdt_ctx* ctx);
  * VClock::merge (src/vclock.rs:131-137) across replicas: a pointwise max,
  * commutative and associative, so the reduction order cannot change a bit. */
 int crdt_replica_allreduce_max(crdt_ctx* ctx, uint64_t* d_rows, size_t n_words, void* stream);
+/* The owner-shard variant: rank r receives in
+ * d_shard the max over ranks of words [r n/N, (r+1) n/N) of d_rows (one
+ * ncclReduceScatter, ncclUint64 + ncclMax); n_words must be a multiple of
+ * the rank count. */
+int crdt_replica_reduce_scatter_max(crdt_ctx* ctx, const uint64_t* d_rows, size_t n_words, uint64_t* d_shard,
+                                    void* stream);
 
 /* Orswot replicas: out[i] = ((r0[i] ⊔ r1[i]) ⊔ r2[i]) ⊔ ... ⊔ r_{N-1}[i], the
  * same bytes on every rank (the join is structurally non-commutative,

@@ -375,6 +375,21 @@ class Engine:
                                              self._stream(stream)), "replica_allreduce_max")
         return rows
 
+    def replica_reduce_scatter_max(self, rows, stream=None):
+        """The owner shard of the u64 max over ranks: rank r gets words
+        [r n/N, (r+1) n/N) (crdt_replica_reduce_scatter_max). Returns a new
+        int64 device tensor of n/N words."""
+        torch = _torch()
+        flat = rows.reshape(-1)
+        n_ranks = self.n_ranks
+        if flat.numel() % n_ranks:
+            raise CrdtError(-1, "reduce_scatter: word count not a multiple of the rank count")
+        out = torch.empty(flat.numel() // n_ranks, dtype=torch.int64, device=flat.device)
+        check(lib.crdt_replica_reduce_scatter_max(self.ctx, C.c_void_p(flat.data_ptr()), flat.numel(),
+                                                  C.c_void_p(out.data_ptr()), self._stream(stream)),
+              "replica_reduce_scatter_max")
+        return out
+
     def orswot_replica_join(self, B: OrswotBatch, stream=None):
         """((r0 ⊔ r1) ⊔ ...) of every rank's replica, owner-sharded over RCCL;
         the same packed batch on every rank (crdt_orswot_replica_join)."""

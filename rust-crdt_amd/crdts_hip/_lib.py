@@ -67,6 +67,7 @@ EXPORTS = [
     "crdt_orswot_to_bincode", "crdt_orswot_apply", "crdt_vclock_partial_cmp", "crdt_mvreg_merge",
     "crdt_map_mvreg_merge", "crdt_map_orswot_merge", "crdt_ctx_set_list_cap", "crdt_orswot_bincode_record_bounds",
     "crdt_comm_unique_id", "crdt_comm_init", "crdt_comm_destroy", "crdt_replica_allreduce_max",
+    "crdt_replica_reduce_scatter_max",
     "crdt_orswot_replica_join_bound", "crdt_orswot_replica_join", "crdt_orswot_replica_join_local",
 ]
 
@@ -163,6 +164,7 @@ def _load():
         "crdt_comm_init": (I, [P, P, I, I]),
         "crdt_comm_destroy": (I, [P]),
         "crdt_replica_allreduce_max": (I, [P, P, SZ, P]),
+        "crdt_replica_reduce_scatter_max": (I, [P, P, SZ, P, P]),
         "crdt_orswot_replica_join_bound": (I, [P, BP, C.POINTER(SZ), P]),
         "crdt_orswot_replica_join": (I, [P, BP, U32, U32, P, P, SZ, C.POINTER(SZ), P]),
         "crdt_orswot_replica_join_local": (I, [P, BP, U32, U32, U32, P, P, SZ, C.POINTER(SZ), P]),

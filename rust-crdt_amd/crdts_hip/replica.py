@@ -10,6 +10,8 @@ is broadcast over the torch.distributed group), then
 - `dense_allreduce_max` -> crdt_replica_allreduce_max: one in-place
   ncclAllReduce(ncclUint64, ncclMax). The join is VClock::merge
   (src/vclock.rs:131-137), a pointwise max: exact in any reduction order.
+  `dense_reduce_scatter_max` -> crdt_replica_reduce_scatter_max: the
+  owner-shard variant (each rank keeps its 1/N of the joined words).
 - `orswot_anti_entropy` -> crdt_orswot_replica_join: OWNER-SHARDED. The join
   is structurally NON-commutative (src/orswot.rs:98-103 vs :132-138), so the
   result is the rank-order fold ((r0 ⊔ r1) ⊔ r2) ⊔ ...; the n objects are
@@ -74,6 +76,25 @@ def dense_allreduce_max(rows, group=None, chunk_elems=1 << 28, engine=None, stre
         dist.all_reduce(part, op=dist.ReduceOp.MAX, group=group)
         part.bitwise_xor_(sign)
     return rows
+
+
+def dense_reduce_scatter_max(rows, group=None, engine=None, stream=None):
+    """The owner-shard variant: this rank's
+    1/N of the rows' words, maxed over ranks (u64 order). With an engine that
+    owns a communicator: crdt_replica_reduce_scatter_max (one
+    ncclReduceScatter, ncclUint64 + ncclMax). Otherwise (gloo, CPU): the
+    all-reduce above, then this rank's slice."""
+    if _has_comm(engine):
+        return engine.replica_reduce_scatter_max(rows, stream=stream)
+    import torch.distributed as dist
+
+    world, me = dist.get_world_size(group), dist.get_rank(group)
+    flat = rows.reshape(-1).clone()
+    if flat.numel() % world:
+        raise ValueError("reduce_scatter: word count not a multiple of the rank count")
+    dense_allreduce_max(flat, group=group)
+    w = flat.numel() // world
+    return flat[me * w:(me + 1) * w].clone()
 
 
 def _gather_bytes(buf_u8, group=None):

@@ -2945,11 +2945,25 @@ __device__ __forceinline__ void general_one(const uint8_t* Lb, const uint64_t* L
     for (uint32_t k = lane; k < szl / 16; k += kWave) sl[k] = ((const u32x4*)lr)[k];
     for (uint32_t k = lane; k < szr / 16; k += kWave) sr[k] = ((const u32x4*)rr)[k];
     wave_sync();
-    // the fast path's join when its limits hold (union positions, deferred
-    // clocks per side), with the general kernel's larger stages
+    // the join kernel's mask3 join when its limits hold (<= 64 members and
+    // dots per side, <= 32 deferred clocks per side, A <= 32: in config 3 the
+    // objects sent here are records just past the join kernel's 2 KB stage),
+    // else the older fast join, with the general kernel's larger stages
     uint32_t n16 = ~0u;
     const uint32_t nL = uni(hl0.z), nR = uni(hr0.z), dL = uni(hl0.w), dR = uni(hr0.w);
-    if (nL + nR <= 2u * kWave && uni(hl1.x) <= 32u && uni(hr1.x) <= 32u) {
+    bool done = false;
+    if (A <= 32u && nL <= 64u && nR <= 64u && dL <= 64u && dR <= 64u && uni(hl1.x) <= 32u && uni(hr1.x) <= 32u) {
+      bool big = false;
+      const uint32_t r =
+          (uni(hl1.x) | uni(hr1.x)) != 0u
+              ? mask3_object<0xFFFFFFFFu, 0, true>(lds_addr(sl), lds_addr(sr), lds_addr(so), Ob + oo, A, nL, dL, nR, dR,
+                                                   lane, big)
+              : mask3_object<0xFFFFFFFFu, 0, false>(lds_addr(sl), lds_addr(sr), lds_addr(so), Ob + oo, A, nL, dL, nR,
+                                                    dR, lane, big);
+      done = r != kLeanFallback && !big;
+      wave_sync();  // the scratch (so) is reused below
+    }
+    if (!done && nL + nR <= 2u * kWave && uni(hl1.x) <= 32u && uni(hr1.x) <= 32u) {
       const FOut fo{so, Ob + oo, o, Ooff, nullptr, nullptr, 0u};
       Stamps st{};
       if ((uni(hl1.x) | uni(hr1.x)) != 0u)
@@ -2959,8 +2973,12 @@ __device__ __forceinline__ void general_one(const uint8_t* Lb, const uint64_t* L
         n16 = fast_object<false, 0, kGenStage, true>((const uint8_t*)sl, (const uint8_t*)sr, fo, A, nL, dL, nR, dR,
                                                      lane, st);
     }
-    if (n16 != ~0u) copy_out(so, Ob + oo, n16, lane);
-    else merge_object((const uint8_t*)sl, (const uint8_t*)sr, Ob + oo, A, lane);
+    if (done) {
+    } else if (n16 != ~0u) {
+      copy_out(so, Ob + oo, n16, lane);
+    } else {
+      merge_object((const uint8_t*)sl, (const uint8_t*)sr, Ob + oo, A, lane);
+    }
   } else {
     merge_object(lr, rr, Ob + oo, A, lane);
   }

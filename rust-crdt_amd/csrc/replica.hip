@@ -469,6 +469,17 @@ int crdt_replica_allreduce_max(crdt_ctx* ctx, uint64_t* d_rows, size_t n_words, 
   return rc;
 }
 
+int crdt_replica_reduce_scatter_max(crdt_ctx* ctx, const uint64_t* d_rows, size_t n_words, uint64_t* d_shard,
+                                    void* stream) {
+  if (!ctx || !ctx->comm || ctx->n_ranks <= 0 || n_words % (size_t)ctx->n_ranks || (n_words && (!d_rows || !d_shard)))
+    return CRDT_EINVAL;
+  int rc = set_dev(ctx);
+  if (rc) return rc;
+  if (n_words == 0) return CRDT_OK;
+  return nccl_rc(ncclReduceScatter(d_rows, d_shard, n_words / (size_t)ctx->n_ranks, ncclUint64, ncclMax,
+                                   (ncclComm_t)ctx->comm, S(stream)));
+}
+
 int crdt_orswot_replica_join_bound(crdt_ctx* ctx, const crdt_orswot_batch* mine, size_t* h_bound, void* stream) {
   if (!ctx || !ctx->comm || !mine || !h_bound) return CRDT_EINVAL;
   int rc = set_dev(ctx);

@@ -52,6 +52,20 @@ def test_rccl_world1_dense_allreduce_max(comm1):
     assert torch.equal(rows, before)
 
 
+def test_rccl_world1_reduce_scatter_max(comm1):
+    """crdt_replica_reduce_scatter_max at world size 1: the owner shard is
+    every word, unchanged (u64 values >= 2^63 included)."""
+    import torch
+
+    from crdts_hip import replica
+
+    rows = torch.randint(-(1 << 62), 1 << 62, (4096, 8), dtype=torch.int64, device="cuda:0")
+    rows[:5] = -3
+    shard = replica.dense_reduce_scatter_max(rows, engine=comm1)
+    torch.cuda.synchronize()
+    assert torch.equal(shard, rows.reshape(-1))
+
+
 def test_rccl_world1_orswot_replica_join(comm1, oracle):
     import crdts_hip
     from crdts_hip import replica

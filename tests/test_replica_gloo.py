@@ -45,11 +45,12 @@ def _dense_worker(rank, world, port, q):
     from crdts_hip import replica
 
     rng = np.random.default_rng(100 + rank)
-    rows = rng.integers(0, np.iinfo(np.uint64).max, size=(257, 16), dtype=np.uint64, endpoint=True)
+    rows = rng.integers(0, np.iinfo(np.uint64).max, size=(258, 16), dtype=np.uint64, endpoint=True)
     rows[rng.random(rows.shape) < 0.25] = 0
     t = torch.from_numpy(rows.view(np.int64).copy())
+    shard = replica.dense_reduce_scatter_max(t.clone())  # the owner-shard variant, before the in-place join
     replica.dense_allreduce_max(t, chunk_elems=1000)
-    q.put((rank, rows, t.numpy().view(np.uint64).copy()))
+    q.put((rank, rows, t.numpy().view(np.uint64).copy(), shard.numpy().view(np.uint64).copy()))
     dist.destroy_process_group()
 
 
@@ -182,8 +183,10 @@ def test_dense_allreduce_max_u64_exact_gloo():
     res = _run(_dense_worker, 2)
     exp = np.maximum(res[0][1], res[1][1])
     assert (exp >= np.uint64(1 << 63)).any()  # the sign-flip matters on this data
-    for _, _, got in res:
+    half = exp.size // 2
+    for r, _, got, shard in res:
         assert (got == exp).all()
+        assert (shard == exp.reshape(-1)[r * half:(r + 1) * half]).all()  # rank r owns words [r n/N, (r+1) n/N)
 
 
 @pytest.mark.parametrize("world", [2, 3])
