@@ -3449,8 +3449,11 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
   if (hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) != hipSuccess)
     return CRDT_EHIP;
   if (sparse_variant == 3 || sparse_variant == 4) return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;  // diagnostics: no general pass
-  hipLaunchKernelGGL(orswot_sparse_general_kernel, dim3(2 * kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
-                     Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
+  // one block per resident slot (6 single-wave blocks per CU fit its 23 KB of
+  // LDS): a fold step lists ~0.6 % of its objects here (pairs past the 6 KB
+  // stage), so the listed objects spread over every CU
+  hipLaunchKernelGGL(orswot_sparse_general_kernel, dim3((uint32_t)cus * 6u), dim3(kWave), 0, stream, Lb, Loff, Rb,
+                     Roff, Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 
