@@ -70,6 +70,22 @@ __device__ __forceinline__ bool set_has(const uint64_t* set, uint32_t n, uint64_
   return __ballot(f) != 0ull;
 }
 
+// dst[e] = at(e) for e < n, all lanes: 16-B non-temporal stores when dst is
+// 16-B aligned and n even (the zero-filled capacity dominates the bytes this
+// kernel writes), 8-B stores otherwise.
+typedef uint64_t mo_u64x2 __attribute__((ext_vector_type(2)));
+template <class F>
+__device__ __forceinline__ void fill64(uint64_t* dst, uint64_t n, uint32_t lane, F at) {
+  if ((((uintptr_t)dst) & 15u) == 0u && (n & 1u) == 0u) {
+    for (uint64_t p = lane; p < n / 2u; p += kMoW) {
+      const mo_u64x2 v = {at(2u * p), at(2u * p + 1u)};
+      __builtin_nontemporal_store(v, (mo_u64x2*)(dst + 2u * p));
+    }
+  } else {
+    for (uint64_t e = lane; e < n; e += kMoW) dst[e] = at(e);
+  }
+}
+
 // A nested Orswot under construction (LDS). The top clock is a register
 // (lane = actor) held by the caller.
 struct Ws {
@@ -264,17 +280,22 @@ __device__ bool ws_store(const Ws& W, uint64_t clk, const crdt_map_orswot_slab& 
   if (!fits) return false;
   if (lane < c.A) R.vclock[kr * c.A + lane] = clk;
   if (lane == 0u) { R.vn_mem[kr] = W.nm; R.vn_def[kr] = W.nd; }
-  for (uint32_t j = lane; j < R.mcap; j += kMoW) R.vmem[kr * R.mcap + j] = j < W.nm ? W.key[j] : 0ull;
-  for (uint32_t e = lane; e < R.mcap * c.A; e += kMoW)
-    R.vmclock[kr * R.mcap * c.A + e] = e < W.nm * c.A ? W.row[e] : 0ull;
-  for (uint32_t e = lane; e < R.vdcap * c.A; e += kMoW)
-    R.vdclock[kr * R.vdcap * c.A + e] = e < W.nd * c.A ? W.dclk[e] : 0ull;
-  for (uint32_t d = lane; d < R.vdcap; d += kMoW) R.vdset_n[kr * R.vdcap + d] = d < W.nd ? W.dn[d] : 0u;
-  for (uint32_t d = 0; d < R.vdcap; ++d) {
-    const uint32_t n = d < W.nd ? W.dn[d] : 0u;
-    for (uint32_t j = lane; j < R.vscap; j += kMoW)
-      R.vdset[(kr * R.vdcap + d) * R.vscap + j] = j < n ? W.dset[d * c.SW + j] : 0ull;
-  }
+  const uint32_t nm = W.nm, nmA = W.nm * c.A, ndA = W.nd * c.A, nd = W.nd, vs = R.vscap, SW = c.SW;
+  const uint64_t* key = W.key;
+  const uint64_t* row = W.row;
+  const uint64_t* dclk = W.dclk;
+  const uint64_t* dset = W.dset;
+  const uint32_t* dn = W.dn;
+  fill64(R.vmem + kr * R.mcap, R.mcap, lane, [&](uint64_t j) { return j < nm ? key[j] : 0ull; });
+  fill64(R.vmclock + kr * R.mcap * c.A, (uint64_t)R.mcap * c.A, lane,
+         [&](uint64_t e) { return e < nmA ? row[e] : 0ull; });
+  fill64(R.vdclock + kr * R.vdcap * c.A, (uint64_t)R.vdcap * c.A, lane,
+         [&](uint64_t e) { return e < ndA ? dclk[e] : 0ull; });
+  for (uint32_t d = lane; d < R.vdcap; d += kMoW) R.vdset_n[kr * R.vdcap + d] = d < nd ? dn[d] : 0u;
+  fill64(R.vdset + kr * R.vdcap * R.vscap, (uint64_t)R.vdcap * R.vscap, lane, [&](uint64_t e) {
+    const uint32_t d = (uint32_t)(e / vs), j = (uint32_t)(e % vs);
+    return (d < nd && j < dn[d]) ? dset[d * SW + j] : 0ull;
+  });
   return true;
 }
 
@@ -438,13 +459,16 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
     }
     {  // unused key slots: zero, all lanes over each array's flat tail
       const uint64_t k0 = i * R.kcap + nk, k1 = (i + 1u) * R.kcap;
-      for (uint64_t e = k0 + lane; e < k1; e += kMoW) { R.keys[e] = 0ull; R.vn_mem[e] = 0u; R.vn_def[e] = 0u; }
-      for (uint64_t e = k0 * A + lane; e < k1 * A; e += kMoW) { R.eclock[e] = 0ull; R.vclock[e] = 0ull; }
-      for (uint64_t e = k0 * R.mcap + lane; e < k1 * R.mcap; e += kMoW) R.vmem[e] = 0ull;
-      for (uint64_t e = k0 * R.mcap * A + lane; e < k1 * R.mcap * A; e += kMoW) R.vmclock[e] = 0ull;
-      for (uint64_t e = k0 * R.vdcap * A + lane; e < k1 * R.vdcap * A; e += kMoW) R.vdclock[e] = 0ull;
+      auto zero = [](uint64_t) { return 0ull; };
+      for (uint64_t e = k0 + lane; e < k1; e += kMoW) { R.vn_mem[e] = 0u; R.vn_def[e] = 0u; }
+      fill64(R.keys + k0, k1 - k0, lane, zero);
+      fill64(R.eclock + k0 * A, (k1 - k0) * A, lane, zero);
+      fill64(R.vclock + k0 * A, (k1 - k0) * A, lane, zero);
+      fill64(R.vmem + k0 * R.mcap, (k1 - k0) * R.mcap, lane, zero);
+      fill64(R.vmclock + k0 * R.mcap * A, (k1 - k0) * R.mcap * A, lane, zero);
+      fill64(R.vdclock + k0 * R.vdcap * A, (k1 - k0) * R.vdcap * A, lane, zero);
       for (uint64_t e = k0 * R.vdcap + lane; e < k1 * R.vdcap; e += kMoW) R.vdset_n[e] = 0u;
-      for (uint64_t e = k0 * R.vdcap * R.vscap + lane; e < k1 * R.vdcap * R.vscap; e += kMoW) R.vdset[e] = 0ull;
+      fill64(R.vdset + k0 * R.vdcap * R.vscap, (k1 - k0) * R.vdcap * R.vscap, lane, zero);
     }
     if (lane == 0u) R.n_keys[i] = nk;
     if (lane < A) R.clock[i * A + lane] = cM;
