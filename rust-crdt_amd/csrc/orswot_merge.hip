@@ -2826,25 +2826,33 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
     uint64_t pend = runs;
     uint32_t t = (uint32_t)__builtin_ctzll(pend);
     pend &= pend - 1;
+    // (HABL 3, timing only: every object of the chunk without deferred
+    // removes joins the records of the chunk's first such object)
+    const uint64_t nhd = runs & ~defs;
+    const uint32_t t0 = nhd ? (uint32_t)__builtin_ctzll(nhd) : t;
+    auto dsel = [&](uint32_t x) -> uint32_t { return HABL == 3 && !((defs >> x) & 1ull) ? t0 : x; };
     u32x4 pl[kPer], pr[kPer];
     {
-      const uint32_t nn = lane_of(n16, t);
-      prefetch_all(pl, Lb + lane_of64(lo, t), nn & 0xFFFFu, lane);
-      prefetch_all(pr, Rb + lane_of64(ro, t), nn >> 16, lane);
+      const uint32_t ts = dsel(t);
+      const uint32_t nn = lane_of(n16, ts);
+      prefetch_all(pl, Lb + lane_of64(lo, ts), nn & 0xFFFFu, lane);
+      prefetch_all(pr, Rb + lane_of64(ro, ts), nn >> 16, lane);
     }
     wave_sync();  // the previous chunk's last LDS reads are done
     stage_all(sL, pl, lane);
     stage_all(sR, pr, lane);
     wave_sync();
     for (;;) {
-      const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
-      const uint32_t m = lane_of(nm, t), d = lane_of(nd, t);
+      const uint64_t oo = HABL == 5 ? lane_of64(lo, t) : lane_of64(lo, t) + lane_of64(ro, t);
+      const uint32_t td = dsel(t);
+      const uint32_t m = lane_of(nm, td), d = lane_of(nd, td);
       // the next object, or this one again after the chunk's last (a constant load count)
       const uint32_t u = pend ? (uint32_t)__builtin_ctzll(pend) : t;
+      const uint32_t us = dsel(u);
       {
-        const uint32_t nu = lane_of(n16, u);
-        prefetch_all(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
-        prefetch_all(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
+        const uint32_t nu = lane_of(n16, us);
+        prefetch_all(pl, Lb + lane_of64(lo, us), nu & 0xFFFFu, lane);
+        prefetch_all(pr, Rb + lane_of64(ro, us), nu >> 16, lane);
       }
       bool big = false;
       uint32_t r;
@@ -2866,7 +2874,10 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
         // operations for every object
         uint32_t src;
         bool direct = false;
-        if ((defs >> t) & 1ull) {
+        if (HABL == 4 || HABL == 5) {  // timing only: no join, the self record copied out as the output (5: densely)
+          r = lane_of(n16, t) & 0xFFFFu;
+          src = lds_addr(sL);
+        } else if ((defs >> td) & 1ull) {
           if (HDD) {
             if (M3HD)
               r = mask3_object<0xFFFFFFFFu, 0, true, HABL>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
@@ -2894,7 +2905,13 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
           copy_record_out(src, Ob + oo, fbu ? 1u : r, lane);
         }
         *(Ooff + cbase + t) = oo | (fbu ? kPending : 0ull);
-        *(fbu ? ctl + 1 : (uint32_t*)sink) = 1u;  // the wave's own sink word: no shared line
+        if (fbu) {  // listed for the general kernel (a rare path: its extra memory operations
+                    // only add to the count the loop-head wait sees)
+          if (lane == 0u) {
+            const uint32_t e = atomicAdd(&ctl[0], 1u);
+            if (e < list_cap) list[e] = cbase + t;
+          }
+        }
       } else {
         if (M3HD)
           r = mask3_object<0xFFFFFFFFu, 0, true>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
@@ -2911,8 +2928,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
       t = u;
       pend &= pend - 1;
       wave_sync();  // this object's LDS reads are done
-      stage_used(sL, pl, lane_of(n16, t) & 0xFFFFu, lane);
-      stage_used(sR, pr, lane_of(n16, t) >> 16, lane);
+      stage_used(sL, pl, lane_of(n16, us) & 0xFFFFu, lane);
+      stage_used(sR, pr, lane_of(n16, us) >> 16, lane);
       wave_sync();
     }
   }
@@ -3323,6 +3340,9 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
 #else
   if (variant == 134) return go(launch_join_passes<6, true, true, true, true, 1>);  // timing only: no kill
   if (variant == 135) return go(launch_join_passes<6, true, true, true, true, 2>);  // timing only: no deferred block
+  if (variant == 136) return go(launch_join_passes<6, true, true, true, true, 3>);  // timing only: join without HBM
+  if (variant == 137) return go(launch_join_passes<6, true, true, true, true, 4>);  // timing only: HBM without join
+  if (variant == 138) return go(launch_join_passes<6, true, true, true, true, 5>);  // timing only: as 137, output dense
   if (variant == 0 || (variant >= 25 && variant <= 34)) {
     switch (variant) {
       case 25: return go(launch_join_passes<4, false>);
