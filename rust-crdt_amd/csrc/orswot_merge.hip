@@ -1493,7 +1493,8 @@ __device__ __forceinline__ void copy_record_out(uint32_t src, uint8_t* O, uint32
 __device__ __forceinline__ const uint8_t* gptr(uint32_t a) {
   return (const uint8_t*)(const __attribute__((address_space(3))) uint8_t*)(size_t)a;
 }
-template <uint32_t OUTCAP, int OUT = 0, bool HD = false, int HABL = 0>  // OUT: 0 direct stores, 1 sink-predicated, 2 LDS-assembled
+// RT: member ranks searched in padded key tables (else clamped probes of the stage)
+template <uint32_t OUTCAP, int OUT = 0, bool HD = false, int HABL = 0, bool RT = true>  // OUT: 0 direct stores, 1 sink-predicated, 2 LDS-assembled
 __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint32_t uX, uint8_t* O, uint32_t A,
                                                  uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane,
                                                  bool& big, uint8_t* sink = nullptr) {
@@ -1522,23 +1523,60 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
   // R keys < kl, R lanes count L keys < kr; probe address = key[b - 1]
   const uint32_t rk0 = uR + key - 8u, rkmax = uR + key + 8u * nR - 8u;
   const uint32_t lk0 = uL + key - 8u, lkmax = uL + key + 8u * nL - 8u;
-  uint32_t pl = rk0, pr = lk0;
-  {
+  uint32_t rl, rr;  // # R keys < kl, # L keys < kr
+  uint64_t EL, ER;
+  if (RT) {
+    // both key lists copied into 64-slot tables padded with ~0 (in the mask
+    // scratch, dead until the masks are zeroed below): the probes need no
+    // bound, and every probe address is the lane's position + an immediate
+    const uint32_t tL = uX + k3MsL, tR = uX + k3MsR;
+    *(lds_u64*)(size_t)(tL + l8) = bit_of(mnL, lane) ? kl : ~0ull;
+    *(lds_u64*)(size_t)(tR + l8) = bit_of(mnR, lane) ? kr : ~0ull;
+    wave_sync();
+    uint32_t ql = tR, qr = tL;  // address of the first key not known to be below the lane's key
     const uint32_t n = nL > nR ? nL : nR;
-    for (uint32_t step = n ? 8u << (31u - __builtin_clz(n)) : 0u; step >= 8u; step >>= 1) {
-      const uint32_t cl = pl + step, cr = pr + step;
-      const uint64_t kcl = lr64(cl < rkmax ? cl : rkmax), kcr = lr64(cr < lkmax ? cr : lkmax);
-      pl = kcl < kl ? cl : pl;
-      pr = kcr < kr ? cr : pr;
+    if (n >= 64u) {
+      ql = lr64(ql + 504u) < kl ? ql + 512u : ql;
+      qr = lr64(qr + 504u) < kr ? qr + 512u : qr;
     }
+    if (n >= 32u) {
+      ql = lr64(ql + 248u) < kl ? ql + 256u : ql;
+      qr = lr64(qr + 248u) < kr ? qr + 256u : qr;
+    }
+#pragma unroll
+    for (uint32_t step = 128u; step >= 8u; step >>= 1) {
+      const uint64_t a = lr64(ql + step - 8u), b = lr64(qr + step - 8u);
+      ql = a < kl ? ql + step : ql;
+      qr = b < kr ? qr + step : qr;
+    }
+    rl = (ql - tR) >> 3;
+    rr = (qr - tL) >> 3;
+    // the first key >= the lane's: equal only inside the other list (a real
+    // key may be ~0 too, so the padding is excluded by position)
+    const uint64_t kel = lr64(ql), ker = lr64(qr);
+    EL = cmp64<kEQ>(kel, kl) & cmp32<kUGT>(nR, rl) & mnL;
+    ER = cmp64<kEQ>(ker, kr) & cmp32<kUGT>(nL, rr) & mnR;
+  } else {
+    uint32_t pl = rk0, pr = lk0;
+    {
+      const uint32_t n = nL > nR ? nL : nR;
+      for (uint32_t step = n ? 8u << (31u - __builtin_clz(n)) : 0u; step >= 8u; step >>= 1) {
+        const uint32_t cl = pl + step, cr = pr + step;
+        const uint64_t kcl = lr64(cl < rkmax ? cl : rkmax), kcr = lr64(cr < lkmax ? cr : lkmax);
+        pl = kcl < kl ? cl : pl;
+        pr = kcr < kr ? cr : pr;
+      }
+    }
+    pl = pl < rkmax ? pl : rkmax;
+    pr = pr < lkmax ? pr : lkmax;
+    rl = (pl - rk0) >> 3;
+    rr = (pr - lk0) >> 3;
+    const uint64_t kel = lr64(pl + 8u < rkmax ? pl + 8u : rkmax), ker = lr64(pr + 8u < lkmax ? pr + 8u : lkmax);
+    // (an empty other side has no key to be equal to: the clamped probe read
+    // the word before its key section)
+    EL = nR ? cmp64<kEQ>(kel, kl) & mnL : 0ull;
+    ER = nL ? cmp64<kEQ>(ker, kr) & mnR : 0ull;
   }
-  pl = pl < rkmax ? pl : rkmax;
-  pr = pr < lkmax ? pr : lkmax;
-  const uint32_t rl = (pl - rk0) >> 3, rr = (pr - lk0) >> 3;  // # R keys < kl, # L keys < kr
-  const uint64_t kel = lr64(pl + 8u < rkmax ? pl + 8u : rkmax), ker = lr64(pr + 8u < lkmax ? pr + 8u : lkmax);
-  // (an empty other side has no key to be equal to: the clamped probe read
-  // the word before its key section)
-  const uint64_t EL = nR ? cmp64<kEQ>(kel, kl) & mnL : 0ull, ER = nL ? cmp64<kEQ>(ker, kr) & mnR : 0ull;
   const uint32_t U = nL + nR - (uint32_t)__popcll(EL);
   fb = fb || U > (uint32_t)kWave;
   if (OUT == 0 && fb) return kLeanFallback;
@@ -2728,7 +2766,8 @@ __attribute__((noinline)) __device__ uint32_t hd_join(const uint8_t* Ls, const u
 // (mask_object<HD>) and is followed by the same tail stores as the other
 // path, redirected to the sink: every path issues at least as many stores
 // after the prefetch as the lean one, so its loop-head wait stays exact
-template <int MINW, int MODE, int OUT = 2, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0>
+template <int MINW, int MODE, int OUT = 2, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
+          bool RT = true, uint32_t DYN = 0, uint32_t SF = 6>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
@@ -2743,6 +2782,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
   u32x4* const sR = stage_s[wave][1];
   uint8_t* const X = (uint8_t*)scr_s[wave];
   const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+  const uint64_t ts0 = HABL == 6 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
+  uint32_t n_joined = 0u, n_hd = 0u, n_chunk = 0u;                                  // (HABL 6: per-wave counts)
   const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
   const uint64_t rounds = (n_obj + n_waves * kWave - 1) / (n_waves * kWave);
   const uint64_t cs = (n_obj + n_waves * rounds - 1) / (n_waves * rounds);
@@ -2754,10 +2795,45 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
   const bool listed = MODE == 2 && n_def <= kDeferListCap;
   const uint64_t n_items = listed ? n_def : n_obj;
   const uint64_t cs2 = listed ? (M3HD ? 1u : kWave) : cs;  // M3HD: one listed object per wave (parallelism)
-  for (uint64_t cbase = wave_id * cs2; cbase < n_items; cbase += n_waves * cs2) {
+  // DYN (guided split): the first SF/8 of the objects in static rounds of
+  // chunks by wave index, the rest in chunks of DYN objects handed out by an
+  // atomic ticket (ctl[3], zeroed before the launch). The issue arbiter
+  // favours the oldest waves, so with a fully static split the youngest
+  // waves of a SIMD finish last and alone (tools/wave_tail.py: median wave
+  // done at 0.77 of the launch); the tickets go to whichever waves are ahead.
+  // A wave takes the ticket for its next chunk when the chunk before it
+  // starts, so the atomic's round trip is hidden behind that chunk.
+  const uint64_t s_total = DYN ? (SF >= 8 ? n_items : n_items * SF / 8u) : n_items;
+  const uint64_t rounds_s = DYN ? (s_total + n_waves * kWave - 1) / (n_waves * kWave) : 0;
+  const uint64_t cs_s = DYN && rounds_s ? (s_total + n_waves * rounds_s - 1) / (n_waves * rounds_s) : 1;
+  uint32_t ticket = 0u, it = 0u;
+  bool have_ticket = false;
+  uint64_t cbase = wave_id * cs2, cend = n_items;
+  auto static_chunk = [&](uint32_t k) { return k < rounds_s && (wave_id + k * n_waves) * cs_s < s_total; };
+  for (;;) {
+    if (DYN) {
+      if (static_chunk(it)) {
+        cbase = (wave_id + it * n_waves) * cs_s;
+        cend = cbase + cs_s < s_total ? cbase + cs_s : s_total;
+      } else {
+        if (!have_ticket && lane == 0u) ticket = atomicAdd(&ctl[3], 1u);
+        cbase = s_total + (uint64_t)uni(ticket) * DYN;
+        cend = cbase + DYN < n_items ? cbase + DYN : n_items;
+        have_ticket = false;
+        if (cbase >= n_items) break;
+      }
+      ++it;
+      if (!static_chunk(it)) {  // the next chunk is a ticket: take it now
+        if (lane == 0u) ticket = atomicAdd(&ctl[3], 1u);
+        have_ticket = true;
+      }
+    } else {
+      if (it++ > 0u) cbase += n_waves * cs2;
+      if (cbase >= n_items) break;
+    }
     // ---- chunk state: lane k <-> object cbase + k (MODE 2 listed: entry cbase + k)
     const uint64_t item = cbase + lane;
-    const bool valid = lane < cs2 && item < n_items;
+    const bool valid = DYN ? item < cend : lane < cs2 && item < n_items;
     const uint64_t obj = listed ? (valid ? dlist[item] : 0ull) : item;
     uint64_t lo = 0, ro = 0;
     u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
@@ -2814,6 +2890,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
       }
     }
     const uint64_t runs = __ballot(fast);
+    if (HABL == 6) ++n_chunk;
     if (runs == 0ull) continue;
     const uint32_t n16 = fast ? (hl0.x / 16u) | ((hr0.x / 16u) << 16) : 0u;
     const uint32_t nm = hl0.z | (hr0.z << 16), nd = hl0.w | (hr0.w << 16);
@@ -2880,7 +2957,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
         } else if ((defs >> td) & 1ull) {
           if (HDD) {
             if (M3HD)
-              r = mask3_object<0xFFFFFFFFu, 0, true, HABL>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
+              r = mask3_object<0xFFFFFFFFu, 0, true, HABL, RT>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
                                                      d & 0xFFFFu, m >> 16, d >> 16, lane, big);
             else
               r = mask_object<0xFFFFFFFFu, true, 0, DC>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo),
@@ -2891,11 +2968,12 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
           }
           src = lds_addr(out_s[wave]);
         } else {
-          r = mask3_object<0xFFFFFFFFu, 3>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
-                                           d & 0xFFFFu, m >> 16, d >> 16, lane, big, sink);
+          r = mask3_object<0xFFFFFFFFu, 3, false, 0, RT>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A,
+                                                         m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, sink);
           src = lds_addr(sL);
         }
         const bool fbu = big || r == kLeanFallback;  // wave-uniform
+        if (HABL == 6) { ++n_joined; n_hd += (defs >> td) & 1ull ? 1u : 0u; }
         wave_sync();
         if (HDD && direct) {  // the same two stores, to the sink
           const u32x4 z = {0u, 0u, 0u, 0u};
@@ -2933,7 +3011,407 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
       wave_sync();
     }
   }
+  if (HABL == 6 && lane == 0u && wave_id < 10922u) {  // timing only: the list's upper half holds the stamps
+    list[32768u + 3u * wave_id] = ts0;
+    list[32768u + 3u * wave_id + 1u] = __builtin_amdgcn_s_memrealtime();
+    list[32768u + 3u * wave_id + 2u] = ((uint64_t)n_joined << 32) | (n_hd << 16) | n_chunk;
+  }
 }
+
+#ifdef CRDT_DIAG
+// ======================================================================
+// (Diagnostic build only.) Join kernel v9: orswot_join_kernel's one-pass body (mask3
+// for every object; deferred-remove objects through mask3's HD form, direct
+// stores) over chunks of kDynG objects handed out at run time. With a static
+// split (v8) the per-wave work varied enough that the median wave finished
+// at 0.77 of the launch (tools/wave_tail.py); here the first chunk of a wave
+// is its index and every later one comes from an atomic ticket (ctl[3],
+// zeroed before the launch) taken when the previous chunk starts. Small
+// chunks make the chunk step frequent, so it is pipelined: while a chunk's
+// objects are joined, the next chunk's offsets (after the first object) and
+// record headers (after the second) are loaded into two registers laid out
+// by lane role, and the next chunk step reads them with ds_bpermute gathers
+// instead of waiting on two dependent HBM round trips.
+// ======================================================================
+constexpr uint32_t kDynG = 16;  // objects per chunk (the raw-load lane roles assume 16)
+
+__device__ __forceinline__ u32x4 gather128(u32x4 v, uint32_t src_lane) {
+  return u32x4{gather32(v.x, src_lane), gather32(v.y, src_lane), gather32(v.z, src_lane), gather32(v.w, src_lane)};
+}
+
+template <int MINW, int HABL = 0>
+__global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_dyn_kernel(
+    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
+    const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
+    uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
+    int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
+  __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
+  __shared__ u32x4 scr_s[kWavesPerBlock][kMask1Scratch / 16];
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t wave = uni(threadIdx.x / kWave);  // wave-uniform: LDS bases in SGPRs
+  u32x4* const sL = stage_s[wave][0];
+  u32x4* const sR = stage_s[wave][1];
+  uint8_t* const X = (uint8_t*)scr_s[wave];
+  const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint64_t ts0 = HABL == 6 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
+  uint32_t n_joined = 0u, n_hd = 0u, n_chunk = 0u;                                  // (HABL 6: per-wave counts)
+  uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
+  const uint64_t n_chunks = (n_obj + kDynG - 1) / kDynG;
+  const uint32_t sec = lane >> 4, k16 = lane & 15u;  // raw-load lane roles
+
+  // chunk c's offsets: lane l holds section l / 16 of object c * 16 + l % 16 —
+  // 0: Loff[o], 1: Roff[o], 2 / 3: the next object's (the batch size past the last)
+  auto load_offs = [&](uint64_t c) -> uint64_t {
+    const uint64_t o = c * kDynG + k16 + (sec >> 1);
+    const uint64_t past = (sec & 1u) ? Rbytes : Lbytes;
+    uint64_t v = past;
+    if (o < n_obj) v = ((sec & 1u) ? Roff : Loff)[o];
+    return v;
+  };
+  // chunk c's record headers: lane l holds 16-B half l / 32 of side (l / 16) & 1's
+  // header of object l % 16 (zero where the offset cannot hold a header)
+  auto load_hdrs = [&](uint64_t c, uint64_t offs) -> u32x4 {
+    const uint32_t side = sec & 1u, half = sec >> 1;
+    const uint64_t off = gather64(offs, side * 16u + k16);
+    const bool v = c * kDynG + k16 < n_obj && (off & 15u) == 0 && off + kHdrBytes <= (side ? Rbytes : Lbytes);
+    u32x4 h = {0u, 0u, 0u, 0u};
+    if (v) h = *((const u32x4*)((side ? Rb : Lb) + off) + half);
+    return h;
+  };
+
+  uint64_t c = wave_id;
+  uint64_t offs = 0ull;
+  u32x4 hdr = {0u, 0u, 0u, 0u};
+  if (c < n_chunks) {
+    offs = load_offs(c);
+    hdr = load_hdrs(c, offs);
+  }
+  uint32_t ticket = 0u;
+  while (c < n_chunks) {
+    if (lane == 0u) ticket = atomicAdd(&ctl[3], 1u);  // the chunk after this one
+    const uint64_t cbase = c * kDynG;
+    // ---- chunk step from the raw registers: lane k <-> object cbase + k
+    const uint64_t lo = gather64(offs, k16), ro = gather64(offs, 16u + k16);
+    const uint64_t nlo = gather64(offs, 32u + k16), nro = gather64(offs, 48u + k16);
+    const u32x4 hl0 = gather128(hdr, k16), hr0 = gather128(hdr, 16u + k16);
+    const u32x4 hl1 = gather128(hdr, 32u + k16), hr1 = gather128(hdr, 48u + k16);
+    const uint64_t obj = cbase + lane;
+    const bool valid = lane < kDynG && obj < n_obj;
+    bool ok = valid && (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes && ro + kHdrBytes <= Rbytes;
+    ok = ok && header_ok(hl0, hl1, lo, Lbytes, A) && header_ok(hr0, hr1, ro, Rbytes, A) &&
+         lo + ro + (uint64_t)hl0.x + hr0.x <= Obytes;
+    // output placement precondition (out[i] at self.off[i] + other.off[i]):
+    // each side's records in increasing offset order, none overlapping the next
+    const bool placed = !ok || (nlo >= lo + hl0.x && nro >= ro + hr0.x);
+    if (__ballot(!placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_EINVAL);
+    ok = ok && placed;
+    const bool fits = ok && hl0.x <= kFastStage && hr0.x <= kFastStage && A <= 32u && hl0.z <= 64u &&
+                      hr0.z <= 64u && hl0.w <= 64u && hr0.w <= 64u;
+    const bool hd = fits && (hl1.x | hr1.x) != 0u && hl1.x <= 32u && hr1.x <= 32u;
+    const bool fast = fits && ((hl1.x | hr1.x) == 0u || hd);
+    const uint64_t defs = __ballot(hd);
+    const bool gen = ok && !fast;
+    if (valid) Ooff[obj] = (lo + ro) | (gen ? kPending : 0ull);
+    if (gen) {  // hand the object to the general kernel
+      const uint32_t e = atomicAdd(&ctl[0], 1u);
+      if (e < list_cap) list[e] = obj;
+    }
+    if (__ballot(valid && !ok && placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
+    const uint64_t runs = __ballot(fast);
+    const uint32_t n16 = fast ? (hl0.x / 16u) | ((hr0.x / 16u) << 16) : 0u;
+    const uint32_t nm = hl0.z | (hr0.z << 16), nd = hl0.w | (hr0.w << 16);
+
+    // ---- the next chunk's raw loads, one step per joined object
+    uint64_t nc = n_chunks;
+    uint32_t step = 0u;
+    auto advance = [&]() {
+      if (step == 0u) {
+        nc = n_waves + uni(ticket);
+        if (nc < n_chunks) offs = load_offs(nc);
+      } else if (step == 1u && nc < n_chunks) {
+        hdr = load_hdrs(nc, offs);
+      }
+      ++step;
+    };
+
+    if (runs != 0ull) {
+      // ---- software pipeline (orswot_join_kernel's): the next object's
+      // records are in flight while the current one is joined from LDS
+      uint64_t pend = runs;
+      uint32_t t = (uint32_t)__builtin_ctzll(pend);
+      pend &= pend - 1;
+      u32x4 pl[kPer], pr[kPer];
+      {
+        const uint32_t nn = lane_of(n16, t);
+        prefetch_all(pl, Lb + lane_of64(lo, t), nn & 0xFFFFu, lane);
+        prefetch_all(pr, Rb + lane_of64(ro, t), nn >> 16, lane);
+      }
+      wave_sync();  // the previous chunk's last LDS reads are done
+      stage_all(sL, pl, lane);
+      stage_all(sR, pr, lane);
+      wave_sync();
+      for (;;) {
+        const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
+        const uint32_t m = lane_of(nm, t), d = lane_of(nd, t);
+        // the next object, or this one again after the chunk's last (a constant load count)
+        const uint32_t u = pend ? (uint32_t)__builtin_ctzll(pend) : t;
+        {
+          const uint32_t nu = lane_of(n16, u);
+          prefetch_all(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
+          prefetch_all(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
+        }
+        bool big = false;
+        uint32_t r;
+        const bool direct = (defs >> t) & 1ull;
+        if (direct) {
+          r = mask3_object<0xFFFFFFFFu, 0, true, HABL>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A,
+                                                       m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big);
+        } else {
+          r = mask3_object<0xFFFFFFFFu, 3>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
+                                           d & 0xFFFFu, m >> 16, d >> 16, lane, big, sink);
+        }
+        const bool fbu = big || r == kLeanFallback;  // wave-uniform
+        wave_sync();
+        if (direct) {  // the same two stores, to the sink
+          const u32x4 z = {0u, 0u, 0u, 0u};
+          __builtin_nontemporal_store(z, (u32x4*)sink);
+          __builtin_nontemporal_store(z, (u32x4*)sink + 1);
+        } else {
+          copy_record_out(lds_addr(sL), Ob + oo, fbu ? 1u : r, lane);
+        }
+        *(Ooff + cbase + t) = oo | (fbu ? kPending : 0ull);
+        if (fbu) {  // listed for the general kernel (a rare path)
+          if (lane == 0u) {
+            const uint32_t e = atomicAdd(&ctl[0], 1u);
+            if (e < list_cap) list[e] = cbase + t;
+          }
+        }
+        advance();
+        if (pend == 0ull) break;
+        t = u;
+        pend &= pend - 1;
+        wave_sync();  // this object's LDS reads are done
+        stage_used(sL, pl, lane_of(n16, u) & 0xFFFFu, lane);
+        stage_used(sR, pr, lane_of(n16, u) >> 16, lane);
+        wave_sync();
+      }
+    }
+    while (step < 2u) advance();  // a chunk with fewer than two joined objects
+    c = nc;
+  }
+  if (HABL == 6 && lane == 0u && wave_id < 10922u) {  // timing only: the list's upper half holds the stamps
+    list[32768u + 3u * wave_id] = ts0;
+    list[32768u + 3u * wave_id + 1u] = __builtin_amdgcn_s_memrealtime();
+    list[32768u + 3u * wave_id + 2u] = ((uint64_t)n_joined << 32) | (n_hd << 16) | n_chunk;
+  }
+}
+
+// ======================================================================
+// Join kernel v10: the v8 join (mask3_object; deferred-remove objects by its
+// HD form, direct stores) with a chunk step that waits on nothing.
+//  - A chunk's step loads only its offsets: L in lanes 0-31, R in lanes
+//    32-63, one lane past the last object holding the next object's offset
+//    (the placement check). Record headers are not loaded in the step: each
+//    record is prefetched blind — 2 KB from its offset, clamped to the
+//    batch — and its header is read from the stage (a record past 2 KB is
+//    detected there and goes to the general kernel).
+//  - The next chunk is resolved one object into the current one and its
+//    offsets loaded then, so the last object's prefetch is the next chunk's
+//    first object: chunk boundaries cost no round trip.
+//  - Guided split: the first SF/8 of the objects in static chunks by wave
+//    index, the rest in G-object chunks from an atomic ticket (ctl[3]). The
+//    issue arbiter favours the oldest waves; with a static split the
+//    youngest waves of a SIMD ran last and alone (tools/wave_tail.py).
+// ======================================================================
+constexpr uint32_t kV10Max = 31;  // objects per chunk (+1 boundary offset in 32 lanes)
+
+template <int MINW, uint32_t G, uint32_t SF, int HABL = 0>
+__global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_v10_kernel(
+    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
+    const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
+    uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
+    int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
+  static_assert(G >= 1 && G <= kV10Max, "chunk size");
+  __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
+  __shared__ u32x4 scr_s[kWavesPerBlock][kMask1Scratch / 16];
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t wave = uni(threadIdx.x / kWave);  // wave-uniform: LDS bases in SGPRs
+  u32x4* const sL = stage_s[wave][0];
+  u32x4* const sR = stage_s[wave][1];
+  uint8_t* const X = (uint8_t*)scr_s[wave];
+  const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint64_t ts0 = HABL == 6 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
+  uint32_t n_joined = 0u, n_hd = 0u, n_chunk = 0u;                                  // (HABL 6: per-wave counts)
+  uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
+
+  // ---- guided schedule
+  const uint64_t s_total = SF >= 8u ? n_obj : n_obj * SF / 8u;
+  const uint64_t rounds_s = (s_total + n_waves * kV10Max - 1) / (n_waves * kV10Max);
+  const uint64_t cs_s = rounds_s ? (s_total + n_waves * rounds_s - 1) / (n_waves * rounds_s) : 1u;
+  auto is_static = [&](uint32_t k) { return k < rounds_s && (wave_id + k * n_waves) * cs_s < s_total; };
+  // chunk k of this wave ([cb, ce)), tk = its ticket if it is not static
+  auto chunk_at = [&](uint32_t k, uint32_t tk, uint64_t& cb, uint64_t& ce) -> bool {
+    if (is_static(k)) {
+      cb = (wave_id + k * n_waves) * cs_s;
+      ce = cb + cs_s < s_total ? cb + cs_s : s_total;
+      return true;
+    }
+    cb = s_total + (uint64_t)tk * G;
+    ce = cb + G < n_obj ? cb + G : n_obj;
+    return cb < n_obj;
+  };
+  // a chunk's offsets: lane j < 32 Loff[cb + j], lane 32 + j Roff[cb + j], for
+  // j <= ce - cb (the batch size past the last object)
+  auto load_offs = [&](uint64_t cb, uint64_t ce) -> uint64_t {
+    const uint64_t o = cb + (lane & 31u);
+    const bool r = lane >= 32u;
+    uint64_t v = r ? Rbytes : Lbytes;
+    if (o <= ce && o < n_obj) v = (r ? Roff : Loff)[o];
+    return v;
+  };
+  // prefetch of an object's two records: up to the next object's offset (a
+  // record never extends past it, the placement rule), at most the 2 KB
+  // stage; an offset that cannot hold a record reads the wave's sink line
+  u32x4 pl[kPer], pr[kPer];
+  auto prefetch_obj = [&](uint64_t lo, uint64_t ro, uint64_t nlo, uint64_t nro) -> bool {
+    const bool okp = (lo & 15u) == 0 && lo + kHdrBytes <= Lbytes && (ro & 15u) == 0 && ro + kHdrBytes <= Rbytes &&
+                     nlo >= lo + kHdrBytes && nro >= ro + kHdrBytes;
+    const uint64_t el = nlo < Lbytes ? nlo : Lbytes, er = nro < Rbytes ? nro : Rbytes;
+    const uint64_t nl = (el - lo) / 16u, nr = (er - ro) / 16u;
+    prefetch_all(pl, okp ? Lb + lo : sink, okp ? (uint32_t)(nl < 2u * kWave ? nl : 2u * kWave) : 1u, lane);
+    prefetch_all(pr, okp ? Rb + ro : sink, okp ? (uint32_t)(nr < 2u * kWave ? nr : 2u * kWave) : 1u, lane);
+    return okp;
+  };
+  // staged pieces: the record's size (from lane 0's first piece), at most the stage
+  auto n16_of = [&](const u32x4 (&r)[kPer]) -> uint32_t {
+    const uint32_t sz = uni(r[0].x) / 16u;
+    return sz < 1u ? 1u : sz > 2u * kWave ? 2u * kWave : sz;
+  };
+
+  uint32_t ticket = 0u;
+  uint32_t k = 0;  // this wave's chunk index
+  if (!is_static(0) && lane == 0u) ticket = atomicAdd(&ctl[3], 1u);
+  uint64_t cb = 0, ce = 0;
+  if (chunk_at(0, uni(ticket), cb, ce)) {
+    uint64_t offs = load_offs(cb, ce);
+    if (!is_static(1) && lane == 0u) ticket = atomicAdd(&ctl[3], 1u);  // the ticket of chunk 1
+    uint32_t csz = (uint32_t)(ce - cb), t = 0;
+    uint64_t lo_t = lane_of64(offs, 0), ro_t = lane_of64(offs, 32);
+    bool okp_t = prefetch_obj(lo_t, ro_t, lane_of64(offs, 1), lane_of64(offs, 33));
+    wave_sync();
+    stage_used(sL, pl, n16_of(pl), lane);
+    stage_used(sR, pr, n16_of(pr), lane);
+    wave_sync();
+    uint64_t ncb = 0, nce = 0, noffs = 0;
+    bool next_known = false, have_next = false;
+    if (HABL == 6) ++n_chunk;
+    for (;;) {
+      // ---- resolve the next chunk (one object in, or at a 1-object chunk's only object)
+      if (!next_known && (t >= 1u || csz == 1u)) {
+        next_known = true;
+        have_next = chunk_at(k + 1u, uni(ticket), ncb, nce);
+        if (have_next) noffs = load_offs(ncb, nce);
+      }
+      const bool last = t + 1u == csz;
+      const uint64_t nlo_t = lane_of64(offs, t + 1u), nro_t = lane_of64(offs, 33u + t);  // placement bound
+      // after the wave's last object: this one again (a constant load count)
+      uint64_t lo_u = lo_t, ro_u = ro_t, nlo_u = nlo_t, nro_u = nro_t;
+      if (!last) {
+        lo_u = nlo_t;
+        ro_u = nro_t;
+        nlo_u = lane_of64(offs, t + 2u);
+        nro_u = lane_of64(offs, 34u + t);
+      } else if (have_next) {
+        lo_u = lane_of64(noffs, 0);
+        ro_u = lane_of64(noffs, 32);
+        nlo_u = lane_of64(noffs, 1);
+        nro_u = lane_of64(noffs, 33);
+      }
+      // ---- object t: its headers from the stage (wave-uniform checks)
+      const u32x4 hl0 = *(const __attribute__((address_space(3))) u32x4*)(size_t)lds_addr(sL);
+      const u32x4 hl1 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(lds_addr(sL) + 16u);
+      const u32x4 hr0 = *(const __attribute__((address_space(3))) u32x4*)(size_t)lds_addr(sR);
+      const u32x4 hr1 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(lds_addr(sR) + 16u);
+      // the next object's records are in flight while this one is joined
+      const bool okp_u = prefetch_obj(lo_u, ro_u, nlo_u, nro_u);
+      const u32x4 L0 = {uni(hl0.x), uni(hl0.y), uni(hl0.z), uni(hl0.w)};
+      const u32x4 L1 = {uni(hl1.x), uni(hl1.y), uni(hl1.z), uni(hl1.w)};
+      const u32x4 R0 = {uni(hr0.x), uni(hr0.y), uni(hr0.z), uni(hr0.w)};
+      const u32x4 R1 = {uni(hr1.x), uni(hr1.y), uni(hr1.z), uni(hr1.w)};
+      bool ok = okp_t && header_ok(L0, L1, lo_t, Lbytes, A) && header_ok(R0, R1, ro_t, Rbytes, A) &&
+                lo_t + ro_t + (uint64_t)L0.x + R0.x <= Obytes;
+      // output placement precondition (out[i] at self.off[i] + other.off[i]):
+      // each side's records in increasing offset order, none overlapping the next
+      const bool placed = !ok || (nlo_t >= lo_t + L0.x && nro_t >= ro_t + R0.x);
+      if (!placed && lane == 0u) atomicCAS(status, 0, CRDT_EINVAL);
+      ok = ok && placed;
+      if (!ok && placed && lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
+      const bool fits = ok && L0.x <= kFastStage && R0.x <= kFastStage && A <= 32u && L0.z <= 64u && R0.z <= 64u &&
+                        L0.w <= 64u && R0.w <= 64u;
+      const bool hd = fits && (L1.x | R1.x) != 0u && L1.x <= 32u && R1.x <= 32u;
+      const bool fast = fits && ((L1.x | R1.x) == 0u || hd);
+      const uint64_t oo = lo_t + ro_t;
+      bool big = false, direct = true;
+      uint32_t r = kLeanFallback;
+      if (hd) {
+        r = mask3_object<0xFFFFFFFFu, 0, true, HABL>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, L0.z, L0.w,
+                                                     R0.z, R0.w, lane, big);
+      } else if (fast) {
+        r = mask3_object<0xFFFFFFFFu, 3>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, L0.z, L0.w, R0.z,
+                                         R0.w, lane, big, sink);
+        direct = false;
+      }
+      const bool pend = ok && (big || r == kLeanFallback);  // wave-uniform: the general kernel's
+      if (HABL == 6 && fast) { ++n_joined; n_hd += hd ? 1u : 0u; }
+      wave_sync();
+      if (direct) {  // (deferred-remove, general or invalid objects) the same two stores, to the sink
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        __builtin_nontemporal_store(z, (u32x4*)sink);
+        __builtin_nontemporal_store(z, (u32x4*)sink + 1);
+      } else {
+        copy_record_out(lds_addr(sL), Ob + oo, pend ? 1u : r, lane);
+      }
+      *(Ooff + cb + t) = oo | (pend ? kPending : 0ull);
+      if (pend) {  // listed for the general kernel (a rare path)
+        if (lane == 0u) {
+          const uint32_t e = atomicAdd(&ctl[0], 1u);
+          if (e < list_cap) list[e] = cb + t;
+        }
+      }
+      // ---- advance
+      if (last) {
+        if (!have_next) break;
+        ++k;
+        cb = ncb;
+        ce = nce;
+        csz = (uint32_t)(ce - cb);
+        offs = noffs;
+        t = 0u;
+        next_known = false;
+        if (!is_static(k + 1u) && lane == 0u) ticket = atomicAdd(&ctl[3], 1u);  // the ticket of the chunk after
+        if (HABL == 6) ++n_chunk;
+      } else {
+        ++t;
+      }
+      lo_t = lo_u;
+      ro_t = ro_u;
+      okp_t = okp_u;
+      wave_sync();  // this object's LDS reads are done
+      stage_used(sL, pl, n16_of(pl), lane);
+      stage_used(sR, pr, n16_of(pr), lane);
+      wave_sync();
+    }
+  }
+  if (HABL == 6 && lane == 0u && wave_id < 10922u) {  // timing only: the list's upper half holds the stamps
+    list[32768u + 3u * wave_id] = ts0;
+    list[32768u + 3u * wave_id + 1u] = __builtin_amdgcn_s_memrealtime();
+    list[32768u + 3u * wave_id + 2u] = ((uint64_t)n_joined << 32) | (n_hd << 16) | n_chunk;
+  }
+}
+
+#endif  // CRDT_DIAG
 
 // ======================================================================
 // General path: objects the fast kernel flagged (records larger than its
@@ -3276,7 +3754,8 @@ __global__ __launch_bounds__(kWave) void orswot_sparse_general_kernel(
 namespace {
 // The join launch: MODE 3 (one pass) or the two passes MODE 1 + MODE 2,
 // then the general kernel.
-template <int MINW, bool ONE = true, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0>
+template <int MINW, bool ONE = true, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
+          bool RT = true, uint32_t DYN = 0, bool DK = false, uint32_t SF = 6, bool V10 = false>
 int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                        const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
                        uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
@@ -3285,23 +3764,31 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const void* f1;
   const void* f2 = nullptr;
+#ifdef CRDT_DIAG
+  if constexpr (V10) {
+    f1 = (const void*)orswot_join_v10_kernel<MINW, DYN, SF, HABL>;
+  } else if constexpr (DK) {
+    f1 = (const void*)orswot_join_dyn_kernel<MINW, HABL>;
+  } else
+#endif
   if constexpr (ONE) {
-    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL>;
+    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL, RT, DYN, SF>;
   } else {
     f1 = (const void*)orswot_join_kernel<MINW, 1>;
     f2 = (const void*)orswot_join_kernel<MINW, 2, 2, false, false, M3HD>;
   }
-  static std::atomic<int> occ_cache[2][9];  // per (pass, MINW); HDD variants share: one of them per MINW
+  static std::atomic<int> occ_cache[2][10];  // per (pass, MINW; slot 9: the v9 kernel); HDD variants share one per MINW
+  constexpr int slot = DK || V10 ? 9 : MINW;
   int occ[2];
   const void* fs[2] = {f1, f2};
   const int passes = ONE ? 1 : 2;
   for (int k = 0; k < passes; ++k) {
-    occ[k] = occ_cache[ONE ? 1 - k : k][MINW].load(std::memory_order_relaxed);
+    occ[k] = occ_cache[ONE ? 1 - k : k][slot].load(std::memory_order_relaxed);
     if (occ[k] == 0) {
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[k], fs[k], kWave * kWavesPerBlock, 0) != hipSuccess ||
           occ[k] < 1)
         occ[k] = 4;
-      occ_cache[ONE ? 1 - k : k][MINW].store(occ[k], std::memory_order_relaxed);
+      occ_cache[ONE ? 1 - k : k][slot].store(occ[k], std::memory_order_relaxed);
     }
   }
   const uint64_t chunks = (n_obj + kWave - 1) / kWave;
@@ -3333,17 +3820,47 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
 #ifndef CRDT_DIAG
   // The product path: orswot_join_kernel in one pass (mask3_object for every
   // object; those with deferred removes take its HD form, direct stores) at 6
-  // waves per SIMD, then the general kernel (measured best, tools/ab_bench.py;
-  // DESIGN.md §4). Other variants exist in -DCRDT_DIAG builds only.
+  // waves per SIMD with the guided split (5/8 of the objects in static chunks,
+  // the rest in 20-object ticket chunks), then the general kernel (measured
+  // best, tools/ab_bench.py). Other variants exist in
+  // -DCRDT_DIAG builds only.
   (void)variant;
-  return go(launch_join_passes<6, true, true, true, true>);
+  return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5>);
 #else
   if (variant == 134) return go(launch_join_passes<6, true, true, true, true, 1>);  // timing only: no kill
   if (variant == 135) return go(launch_join_passes<6, true, true, true, true, 2>);  // timing only: no deferred block
   if (variant == 136) return go(launch_join_passes<6, true, true, true, true, 3>);  // timing only: join without HBM
   if (variant == 137) return go(launch_join_passes<6, true, true, true, true, 4>);  // timing only: HBM without join
   if (variant == 138) return go(launch_join_passes<6, true, true, true, true, 5>);  // timing only: as 137, output dense
-  if (variant == 0 || (variant >= 25 && variant <= 34)) {
+  if (variant == 142) return go(launch_join_passes<6, true, true, true, true, 0, false>);  // r02e: clamped rank probes
+  if (variant == 143) return go(launch_join_passes<6, true, true, true, true, 6>);  // product + wave start / end stamps
+  // guided split: SF/8 static, the rest in DYN-object ticket chunks
+  if (variant == 150) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 6>);
+  if (variant == 151) return go(launch_join_passes<6, true, true, true, true, 0, true, 32, false, 6>);
+  if (variant == 152) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 4>);
+  if (variant == 153) return go(launch_join_passes<6, true, true, true, true, 0, true, 8, false, 6>);
+  if (variant == 154) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 7>);
+  if (variant == 155) return go(launch_join_passes<6, true, true, true, true, 6, true, 16, false, 6>);  // + stamps
+  if (variant == 180) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 2>);
+  if (variant == 181) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 3>);
+  if (variant == 182) return go(launch_join_passes<6, true, true, true, true, 0, true, 24, false, 4>);
+  if (variant == 183) return go(launch_join_passes<6, true, true, true, true, 0, true, 12, false, 4>);
+  if (variant == 184) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5>);
+  if (variant == 185) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 5>);
+  if (variant == 186) return go(launch_join_passes<6, true, true, true, true, 0, true, 24, false, 5>);
+  if (variant == 187) return go(launch_join_passes<6, true, true, true, true, 0, true, 24, false, 6>);
+  if (variant == 188) return go(launch_join_passes<6, true, true, true, true, 0, true, 28, false, 5>);
+  if (variant == 189) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 6>);
+  if (variant == 190) return go(launch_join_passes<6, true, true, true, true, 6, true, 20, false, 5>);  // + stamps
+  // v10: offsets-only chunk step, blind record prefetch, seamless chunk switch, guided split
+  if (variant == 170) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 6, true>);
+  if (variant == 171) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 4, true>);
+  if (variant == 172) return go(launch_join_passes<6, true, true, true, true, 0, true, 8, false, 6, true>);
+  if (variant == 173) return go(launch_join_passes<6, true, true, true, true, 0, true, 31, false, 8, true>);
+  if (variant == 174) return go(launch_join_passes<6, true, true, true, true, 6, true, 16, false, 6, true>);  // + stamps
+  if (variant == 160) return go(launch_join_passes<6, true, true, true, true, 0, true, 0, true>);  // v9 (dynamic, pipelined)
+  if (variant == 161) return go(launch_join_passes<6, true, true, true, true, 6, true, 0, true>);  // v9 + stamps
+  if (variant == 0 || (variant >= 25 && variant <= 35)) {
     switch (variant) {
       case 25: return go(launch_join_passes<4, false>);
       case 26: return go(launch_join_passes<5, false>);
@@ -3354,7 +3871,8 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
       case 32: return go(launch_join_passes<6, true, true, true>);
       case 33: return go(launch_join_passes<6, true, true, true, true>);
       case 34: return go(launch_join_passes<6, false, false, false, true>);
-      case 0: return go(launch_join_passes<6, true, true, true, true>);  // the product path
+      case 0: return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5>);  // the product path
+      case 35: return go(launch_join_passes<6, true, true, true, true>);  // r02e product: static split
       default: return go(launch_join_passes<6, true, true>);  // 31: round-2 v8
     }
   }

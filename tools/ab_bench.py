@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--bpc", default="0", help="blocks per CU values to sweep (0: the kernel's occupancy)")
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--n-obj", type=int, default=1_000_000)
+    ap.add_argument("--check", default="", help="variants >= 100 whose output is also compared byte for byte")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -47,7 +48,8 @@ def main():
             eng.status(s)
             if r > 0:
                 res[c].append(e0.elapsed_time(e1))
-            if r == 0 and c[0] < 100 and c not in seen:  # byte-exact against the first variant
+            checked = c[0] < 100 or str(c[0]) in a.check.split(",")
+            if r == 0 and checked and c not in seen:  # byte-exact against the first variant
                 seen.add(c)
                 with torch.cuda.stream(s):  # same stream as the merge
                     out.base.zero_()
