@@ -415,7 +415,7 @@ int crdt_map_mvreg_merge(crdt_ctx* ctx, const crdt_map_mvreg_slab* self, const c
         return CRDT_EINVAL;
   int rc = set_device(ctx);
   if (rc) return rc;
-  return launch_map_mvreg_merge(*self, *other, *out, n_obj, n_actors, ctx->d_status, S(stream));
+  return launch_map_mvreg_merge(*self, *other, *out, n_obj, n_actors, ctx->d_status, ctx->d_ctl, S(stream));
 }
 
 int crdt_map_orswot_merge(crdt_ctx* ctx, const crdt_map_orswot_slab* self, const crdt_map_orswot_slab* other,
@@ -436,7 +436,7 @@ int crdt_map_orswot_merge(crdt_ctx* ctx, const crdt_map_orswot_slab* self, const
         return CRDT_EINVAL;
   int rc = set_device(ctx);
   if (rc) return rc;
-  return launch_map_orswot_merge(*self, *other, *out, n_obj, n_actors, ctx->d_status, S(stream));
+  return launch_map_orswot_merge(*self, *other, *out, n_obj, n_actors, ctx->d_status, ctx->d_ctl, S(stream));
 }
 
 }  // extern "C"

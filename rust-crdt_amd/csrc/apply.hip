@@ -24,6 +24,7 @@
 
 #include "../../include/crdts_hip.h"
 #include "kernels.h"
+#include "sched.h"
 #include "record_layout.h"
 
 namespace crdts_hip {
@@ -625,7 +626,11 @@ __global__ __launch_bounds__(kAW) void orswot_apply_kernel(ApArgs g) {
   __shared__ Ws<C> w;
   const uint32_t lane = threadIdx.x;
   if (SMALL) {
-    for (uint64_t o = blockIdx.x; o < g.n_obj; o += gridDim.x) {
+    // BlockTickets (sched.h): half the objects by block index, the rest in
+    // 4-object atomic tickets (ctl[3]) — one call site, so apply_one is
+    // inlined once (two call sites doubled the kernel's VGPRs)
+    BlockTickets<4> sched(g.n_obj, g.ctl + 3, lane);
+    for (uint64_t o = sched.first(); o < g.n_obj; o = sched.next(o)) {
       const int rc = apply_one<C>(w, g, o, lane);
       if (rc && lane == 0u) {
         if (rc == CRDT_ECAPACITY) {
@@ -679,7 +684,7 @@ int launch_orswot_apply(const uint8_t* sb, uint64_t sbytes, const uint64_t* soff
   ApArgs g{sb, sbytes, soff, n_obj, obj_end, kind, member, actor, counter, clk_end, clk_act, clk_ctr, n_ops, n_clk,
            A, flags, out, ooff, out_bytes, status, ctl, list, list_cap};
   void* args[] = {&g};
-  if (hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
+  if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;  // ctl[3]: tickets
   const bool dense_big = !(flags & kSparseClock) && A > SmallCaps::kCk;  // nothing fits the small workspace
   if (dense_big) {  // every object in the large workspace: the "list overflowed" path with all objects flagged
     if (hipMemsetD32Async((hipDeviceptr_t)ctl, 0xFFFFFFFF, 1, stream) != hipSuccess) return CRDT_EHIP;

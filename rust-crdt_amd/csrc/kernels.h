@@ -53,9 +53,9 @@ int launch_mvreg_merge(const uint32_t* sn, const uint64_t* sclk, const uint64_t*
                        hipStream_t stream);
 
 int launch_map_mvreg_merge(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_slab& O, const crdt_map_mvreg_slab& R,
-                           uint64_t n_obj, uint32_t A, int* status, hipStream_t stream);
+                           uint64_t n_obj, uint32_t A, int* status, uint32_t* ctl, hipStream_t stream);
 int launch_map_orswot_merge(const crdt_map_orswot_slab& S, const crdt_map_orswot_slab& O,
-                            const crdt_map_orswot_slab& R, uint64_t n_obj, uint32_t A, int* status,
+                            const crdt_map_orswot_slab& R, uint64_t n_obj, uint32_t A, int* status, uint32_t* ctl,
                             hipStream_t stream);
 size_t map_orswot_lds_bytes(const crdt_map_orswot_slab& S, const crdt_map_orswot_slab& O, uint32_t A);
 

@@ -19,6 +19,7 @@
 
 #include "../../include/crdts_hip.h"
 #include "kernels.h"
+#include "sched.h"
 
 namespace crdts_hip {
 namespace {
@@ -72,12 +73,13 @@ constexpr uint32_t kVsRows = 128;  // u64 per side
 template <bool VS>
 __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_slab S, crdt_map_mvreg_slab O,
                                                                crdt_map_mvreg_slab R, uint64_t n_obj, uint32_t A,
-                                                               int* __restrict__ status) {
+                                                               int* __restrict__ status, uint32_t* __restrict__ ctl) {
   __shared__ uint32_t comb[kMpComb];     // (self deferred idx + 1) | (other deferred idx + 1) << 8
   __shared__ uint32_t vals[kMpVals];     // kept value slots of the key: side << 8 | slot
   __shared__ uint64_t vr[2][VS ? kVsRows : 1];  // the key's value clock rows: self, other
   const uint32_t lane = threadIdx.x;
-  for (uint64_t i = blockIdx.x; i < n_obj; i += gridDim.x) {
+  BlockTickets<4> sched(n_obj, ctl + 3, lane);  // (sched.h)
+  for (uint64_t i = sched.first(); i < n_obj; i = sched.next(i)) {
     const uint64_t cS = rowv(S.clock, i, A, lane), cO = rowv(O.clock, i, A, lane);
     const uint64_t cM = cS > cO ? cS : cO;  // VClock::merge
     const uint32_t nS = __builtin_amdgcn_readfirstlane(S.n_keys[i]), nO = __builtin_amdgcn_readfirstlane(O.n_keys[i]);
@@ -301,16 +303,17 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
 }  // namespace
 
 int launch_map_mvreg_merge(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_slab& O, const crdt_map_mvreg_slab& R,
-                           uint64_t n_obj, uint32_t A, int* status, hipStream_t stream) {
+                           uint64_t n_obj, uint32_t A, int* status, uint32_t* ctl, hipStream_t stream) {
   if (n_obj == 0) return CRDT_OK;
+  if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;  // ctl[3]: tickets
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const uint64_t cap = (uint64_t)cus * 28u;  // 7 single-wave blocks per SIMD
   const uint32_t blocks = (uint32_t)(n_obj < cap ? n_obj : cap);
   if (S.mcap * A <= kVsRows && O.mcap * A <= kVsRows)
-    hipLaunchKernelGGL(map_mvreg_merge_kernel<true>, dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A, status);
+    hipLaunchKernelGGL(map_mvreg_merge_kernel<true>, dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A, status, ctl);
   else
-    hipLaunchKernelGGL(map_mvreg_merge_kernel<false>, dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A, status);
+    hipLaunchKernelGGL(map_mvreg_merge_kernel<false>, dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A, status, ctl);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 

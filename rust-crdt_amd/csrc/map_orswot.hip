@@ -24,6 +24,7 @@
 
 #include "../../include/crdts_hip.h"
 #include "kernels.h"
+#include "sched.h"
 
 namespace crdts_hip {
 namespace {
@@ -301,7 +302,7 @@ __device__ bool ws_store(const Ws& W, uint64_t clk, const crdt_map_orswot_slab& 
 
 __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_slab S, crdt_map_orswot_slab O,
                                                                 crdt_map_orswot_slab R, uint64_t n_obj, uint32_t A,
-                                                                int* __restrict__ status) {
+                                                                int* __restrict__ status, uint32_t* __restrict__ ctl) {
   extern __shared__ uint64_t mo_lds[];
   __shared__ uint32_t comb[kMoComb];  // (self deferred idx + 1) | (other deferred idx + 1) << 8
   const uint32_t lane = threadIdx.x;
@@ -324,7 +325,8 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
   }
   uint32_t* const ddead = mdead + c.MW;
   mo_sync();
-  for (uint64_t i = blockIdx.x; i < n_obj; i += gridDim.x) {
+  BlockTickets<4> sched(n_obj, ctl + 3, lane);  // (sched.h)
+  for (uint64_t i = sched.first(); i < n_obj; i = sched.next(i)) {
     const uint64_t cS = rowv(S.clock, i, A, lane), cO = rowv(O.clock, i, A, lane);
     const uint64_t cM = vmax(cS, cO);  // VClock::merge
     const uint32_t nS = uni(S.n_keys[i]), nO = uni(O.n_keys[i]);
@@ -523,7 +525,7 @@ size_t map_orswot_lds_bytes(const crdt_map_orswot_slab& S, const crdt_map_orswot
 }
 
 int launch_map_orswot_merge(const crdt_map_orswot_slab& S, const crdt_map_orswot_slab& O,
-                            const crdt_map_orswot_slab& R, uint64_t n_obj, uint32_t A, int* status,
+                            const crdt_map_orswot_slab& R, uint64_t n_obj, uint32_t A, int* status, uint32_t* ctl,
                             hipStream_t stream) {
   if (n_obj == 0) return CRDT_OK;
   const size_t lds = map_orswot_lds_bytes(S, O, A);
@@ -532,7 +534,8 @@ int launch_map_orswot_merge(const crdt_map_orswot_slab& S, const crdt_map_orswot
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const uint64_t cap = (uint64_t)cus * 16u;
   const uint32_t blocks = (uint32_t)(n_obj < cap ? n_obj : cap);
-  hipLaunchKernelGGL(map_orswot_merge_kernel, dim3(blocks), dim3(kMoW), lds, stream, S, O, R, n_obj, A, status);
+  if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;  // ctl[3]: tickets
+  hipLaunchKernelGGL(map_orswot_merge_kernel, dim3(blocks), dim3(kMoW), lds, stream, S, O, R, n_obj, A, status, ctl);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 
