@@ -303,7 +303,7 @@ int crdt_orswot_bincode_record_sizes(crdt_ctx* ctx, const uint8_t* d_blobs, size
   int rc = set_device(ctx);
   if (rc) return rc;
   return launch_bincode_ingest(d_blobs, blob_bytes, d_blob_off, d_blob_len, n_obj, actor_bytes, member_bytes,
-                               n_actors, flags, d_sizes, nullptr, nullptr, 0, ctx->d_status, S(stream));
+                               n_actors, flags, d_sizes, nullptr, nullptr, 0, ctx->d_status, ctx->d_ctl, S(stream));
 }
 
 int crdt_orswot_bincode_record_bounds(crdt_ctx* ctx, const uint64_t* d_blob_len, size_t n_obj,
@@ -328,7 +328,7 @@ int crdt_orswot_from_bincode(crdt_ctx* ctx, const uint8_t* d_blobs, size_t blob_
   int rc = set_device(ctx);
   if (rc) return rc;
   return launch_bincode_ingest(d_blobs, blob_bytes, d_blob_off, d_blob_len, n_obj, actor_bytes, member_bytes,
-                               n_actors, flags, nullptr, d_out, d_out_off, out_bytes, ctx->d_status, S(stream),
+                               n_actors, flags, nullptr, d_out, d_out_off, out_bytes, ctx->d_status, ctx->d_ctl, S(stream),
                                ctx->variant == 301 ? ctx->d_list : nullptr);
 }
 
@@ -341,7 +341,7 @@ int crdt_orswot_bincode_sizes(crdt_ctx* ctx, const crdt_orswot_batch* batch, uin
   int rc = set_device(ctx);
   if (rc) return rc;
   return launch_bincode_egest(batch->base, batch->bytes, batch->off, batch->n_obj, n_actors, flags, actor_bytes,
-                              member_bytes, d_sizes, nullptr, nullptr, 0, ctx->d_status, S(stream));
+                              member_bytes, d_sizes, nullptr, nullptr, 0, ctx->d_status, ctx->d_ctl, S(stream));
 }
 
 int crdt_orswot_to_bincode(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32_t n_actors, uint32_t flags,
@@ -354,7 +354,7 @@ int crdt_orswot_to_bincode(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32
   int rc = set_device(ctx);
   if (rc) return rc;
   return launch_bincode_egest(batch->base, batch->bytes, batch->off, batch->n_obj, n_actors, flags, actor_bytes,
-                              member_bytes, nullptr, d_out, d_out_off, out_bytes, ctx->d_status, S(stream));
+                              member_bytes, nullptr, d_out, d_out_off, out_bytes, ctx->d_status, ctx->d_ctl, S(stream));
 }
 
 int crdt_orswot_apply(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_orswot_ops* ops, uint32_t n_actors,

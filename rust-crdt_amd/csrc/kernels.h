@@ -32,11 +32,11 @@ int launch_bincode_bounds(const uint64_t* blen, uint64_t n_obj, uint32_t wa, uin
                           uint32_t flags, uint64_t* bounds, hipStream_t stream);
 int launch_bincode_ingest(const uint8_t* blobs, uint64_t blob_bytes, const uint64_t* boff, const uint64_t* blen,
                           uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags, uint64_t* sizes,
-                          uint8_t* out, const uint64_t* ooff, uint64_t out_bytes, int* status, hipStream_t stream,
+                          uint8_t* out, const uint64_t* ooff, uint64_t out_bytes, int* status, uint32_t* ctl, hipStream_t stream,
                           uint64_t* dbg = nullptr);
 int launch_bincode_egest(const uint8_t* rb, uint64_t rbytes, const uint64_t* roff, uint64_t n_obj, uint32_t A,
                          uint32_t flags, uint32_t wa, uint32_t wm, uint64_t* sizes, uint8_t* out,
-                         const uint64_t* ooff, uint64_t out_bytes, int* status, hipStream_t stream);
+                         const uint64_t* ooff, uint64_t out_bytes, int* status, uint32_t* ctl, hipStream_t stream);
 
 int launch_orswot_apply(const uint8_t* sb, uint64_t sbytes, const uint64_t* soff, uint64_t n_obj,
                         const uint64_t* obj_end, const uint32_t* kind, const uint64_t* member, const uint32_t* actor,

@@ -47,4 +47,59 @@ struct BlockTickets {
   }
 };
 
+// Guided chunk schedule of the join kernels: the first SF/8 of n objects in
+// static rounds of (<= 64-object) chunks by wave index, the rest in chunks
+// of DYN objects handed out by an atomic ticket (ctl[3], zeroed before the
+// launch). The issue arbiter favours a SIMD's oldest waves, so with a static
+// split the youngest waves finish last and alone (tools/wave_tail.py: the
+// median wave was done at 0.77 of the launch); tickets go to the waves that
+// are ahead. A wave takes the ticket for its next chunk when the chunk before
+// it starts, so the atomic's round trip is hidden behind that chunk.
+// (GMIN > 0, diagnostic: ticket chunks shrink from DYN to GMIN as the pool
+// drains; the counter then counts objects.)
+template <uint32_t DYN, uint32_t SF, uint32_t GMIN = 0>
+struct GuidedSplit {
+  uint64_t n, wave_id, n_waves, s_total, rounds_s, cs_s;
+  uint32_t ticket = 0u, it = 0u, tsz = DYN, seen = 0u;
+  bool have_ticket = false;
+  __device__ GuidedSplit(uint64_t n_, uint64_t wave_id_, uint64_t n_waves_)
+      : n(n_), wave_id(wave_id_), n_waves(n_waves_) {
+    s_total = SF >= 8u ? n : n * SF / 8u;
+    rounds_s = (s_total + n_waves * 64u - 1) / (n_waves * 64u);  // chunks of <= 64 objects (one per lane)
+    cs_s = rounds_s ? (s_total + n_waves * rounds_s - 1) / (n_waves * rounds_s) : 1u;
+  }
+  __device__ bool is_static(uint32_t k) const { return k < rounds_s && (wave_id + k * n_waves) * cs_s < s_total; }
+  __device__ void take(uint32_t* ctr, uint32_t lane) {
+    if (GMIN) {
+      const uint64_t pool = n - s_total, left = pool > seen ? pool - seen : 0u;
+      const uint64_t want = left / (2u * n_waves);
+      tsz = want > DYN ? DYN : want < GMIN ? GMIN : (uint32_t)want;
+      if (lane == 0u) ticket = atomicAdd(ctr, tsz);
+    } else if (lane == 0u) {
+      ticket = atomicAdd(ctr, 1u);
+    }
+  }
+  // this wave's next chunk [cb, ce), or false when there is none
+  __device__ bool next(uint64_t& cb, uint64_t& ce, uint32_t* ctr, uint32_t lane) {
+    if (is_static(it)) {
+      cb = (wave_id + it * n_waves) * cs_s;
+      ce = cb + cs_s < s_total ? cb + cs_s : s_total;
+    } else {
+      if (!have_ticket) take(ctr, lane);
+      const uint32_t tk = __builtin_amdgcn_readfirstlane(ticket);
+      cb = s_total + (GMIN ? (uint64_t)tk : (uint64_t)tk * DYN);
+      ce = cb + tsz < n ? cb + tsz : n;
+      seen = tk + tsz;
+      have_ticket = false;
+      if (cb >= n) return false;
+    }
+    ++it;
+    if (!is_static(it)) {  // the next chunk is a ticket: take it now
+      take(ctr, lane);
+      have_ticket = true;
+    }
+    return true;
+  }
+};
+
 }  // namespace crdts_hip
