@@ -17,14 +17,17 @@ namespace crdts_hip {
 
 template <uint32_t K>
 struct BlockTickets {
-  uint64_t n, grid, s_rounds, s_total, end = 0, k = 0;
+  uint64_t n, unit, units, s_rounds, s_total, end = 0, k = 0;
   uint32_t* ctr;
   uint32_t tk = 0u, lane;
   bool dyn = false;
-  __device__ BlockTickets(uint64_t n_, uint32_t* ctr_, uint32_t lane_) : n(n_), ctr(ctr_), lane(lane_) {
-    grid = gridDim.x;
-    s_rounds = n / 2u / grid;
-    s_total = s_rounds * grid;
+  // unit / units: this wave's index among the waves sharing the objects
+  // (default: one wave per block)
+  __device__ BlockTickets(uint64_t n_, uint32_t* ctr_, uint32_t lane_, uint64_t unit_ = blockIdx.x,
+                          uint64_t units_ = gridDim.x)
+      : n(n_), unit(unit_), units(units_), ctr(ctr_), lane(lane_) {
+    s_rounds = n / 2u / units;
+    s_total = s_rounds * units;
   }
   __device__ uint64_t enter() {  // the next ticket's first object (n: none left)
     dyn = true;
@@ -36,11 +39,12 @@ struct BlockTickets {
   }
   __device__ uint64_t first() {
     if (lane == 0u) tk = atomicAdd(ctr, 1u);
-    return s_rounds ? (uint64_t)blockIdx.x : enter();
+    return s_rounds ? unit : enter();
   }
+  // the object after cur (n: none); may be called one object ahead
   __device__ uint64_t next(uint64_t cur) {
     if (!dyn) {
-      if (++k < s_rounds) return blockIdx.x + k * grid;
+      if (++k < s_rounds) return unit + k * units;
       return enter();
     }
     return cur + 1u < end ? cur + 1u : enter();
