@@ -368,3 +368,19 @@ def test_empty_side_key_equal_to_clock_word(gpu, oracle):
         out = _gpu_merge(gpu, lb, lo, rb, ro, A)
         ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, A, threads=4)
         _compare(out, ob, oo, "empty side")
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 63, 64, 65, 1000, 4097, 24_583])
+def test_guided_split_batch_sizes(n, gpu, oracle):
+    """The guided chunk schedule (static chunks for the first 5/8 of the
+    objects, ticket chunks of 20 for the rest; csrc/sched.h) covers every
+    object exactly once at sizes around its chunk boundaries: all-ticket
+    batches (n = 1), partial tickets, a partial last static round, and
+    repeated launches on one context (the ticket counter is re-zeroed)."""
+    import crdts_hip
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(n, threads=16, seed=1234 + n)
+    ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, 16, threads=16)
+    for _ in range(2):
+        out = _gpu_merge(gpu, lb, lo, rb, ro, 16)
+        _compare(out, ob, oo, f"n={n}")
