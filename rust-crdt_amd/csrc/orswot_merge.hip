@@ -3865,6 +3865,11 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   if (variant == 203) return go(launch_join_passes<6, true, true, true, true, 0, true, 32, false, 4, false, false, 8>);
   if (variant == 204) return go(launch_join_passes<6, true, true, true, true, 0, true, 40, false, 4, false, false, 10>);
   if (variant == 205) return go(launch_join_passes<6, true, true, true, true, 6, true, 32, false, 5, false, false, 8>);  // + stamps
+  // timing only, on the guided split: 244 no deferred kill, 245 no deferred block, 246 join without HBM, 247 HBM without join
+  if (variant == 244) return go(launch_join_passes<6, true, true, true, true, 1, true, 20, false, 5>);
+  if (variant == 245) return go(launch_join_passes<6, true, true, true, true, 2, true, 20, false, 5>);
+  if (variant == 246) return go(launch_join_passes<6, true, true, true, true, 3, true, 20, false, 5>);
+  if (variant == 247) return go(launch_join_passes<6, true, true, true, true, 4, true, 20, false, 5>);
   if (variant == 210) return go(launch_join_passes<6, true, true, true, true, 0, true, 32, false, 3>);
   if (variant == 211) return go(launch_join_passes<6, true, true, true, true, 0, true, 40, false, 2>);
   if (variant == 212) return go(launch_join_passes<6, true, true, true, true, 0, true, 32, false, 4>);
