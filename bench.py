@@ -11,8 +11,16 @@ HBM. Objects shard across ranks (weak scaling: 1M objects per GPU, object i
 generated from SplitMix64(seed ^ i) so the data is identical at any N); there
 is no collective on this path.
 
-    python bench.py [--gpus N --steps K --warmup W] [--workload orswot|gcounter|pncounter]
+    python bench.py [--gpus N --steps K --warmup W] [--workload orswot|gcounter|pncounter|...]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+At N > 1 without a launcher (no WORLD_SIZE in the environment) this process
+starts N worker processes of itself (RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_* set, one GPU each) before it makes any GPU call, relays rank 0's
+line and exits with the workers' status. At N > 1 the headline line also
+carries `anti_entropy`: configs 4 and 5 (BASELINE.json configs[3], [4]) over
+RCCL, each checked after its timed steps (identical digests on every rank,
+and a sample equal to a locally computed rank-order fold).
 """
 from __future__ import annotations
 
@@ -36,7 +44,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="orswot",
                    choices=["orswot", "vclock", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply",
-                            "mvreg", "map", "map_orswot"])
+                            "mvreg", "map", "map_orswot", "spawn_check"])
     p.add_argument("--replicas", type=int, default=8, help="orswot_csr at N=1: replicas folded locally")
     p.add_argument("--n-obj", type=int, default=None, help="objects per GPU")
     p.add_argument("--threads", type=int, default=16, help="host threads for input generation")
@@ -44,18 +52,73 @@ def parse():
                    help="CPU-baseline threads (default: every host core, os.cpu_count() = nproc)")
     p.add_argument("--cpu-sample", type=int, default=500_000, help="objects in the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-anti-entropy", action="store_true",
+                   help="N > 1: skip the config-4/5 anti-entropy sub-measurements of the headline line")
+    p.add_argument("--ae-steps", type=int, default=3, help="timed steps of each anti-entropy sub-measurement")
+    p.add_argument("--ae-n-obj", type=int, default=None,
+                   help="objects of the anti-entropy sub-measurements (default: the configs' own sizes)")
+    p.add_argument("--rehearse", action="store_true",
+                   help="rehearse the N > 1 logic on ONE GPU: every rank on cuda:0, gloo collectives, the Orswot "
+                        "join through crdt_orswot_replica_join_transport (tests; not a measurement)")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r02.json"),
                    help="measured per-launch HBM bytes (rocprofv3 PMC) to report as roofline.traffic")
     return p.parse_args()
 
 
-def dist_setup():
+def spawn_ranks(args):
+    """--gpus N > 1 without a launcher: start N fresh worker processes of this
+    script, one per GPU (RANK = LOCAL_RANK = r), rendezvous on 127.0.0.1. This
+    process never touches the GPU (no torch import before or after). Rank 0
+    prints the JSON line; the exit code is the first failing worker's (the
+    others are stopped then, so none waits in a collective forever)."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the others", file=sys.stderr)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc if rc >= 0 else 128 - rc
+
+
+def dist_setup(args):
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.workload == "spawn_check":  # CPU only: the launch path itself (tests/test_bench_spawn.py)
+        if world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        return rank, world, local
+    if args.rehearse:  # every rank on the one GPU, gloo: no RCCL (it cannot put two ranks on one GPU)
+        local = 0
+        torch.cuda.set_device(0)
+        if world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        return rank, world, local
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -235,6 +298,26 @@ def run_orswot(args, rank, world, local):
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_orswot(lb, lo, rb, ro, args)
+    if world > 1:
+        from crdts_hip import replica
+
+        del L, R, out, lb, lo, rb, ro
+        torch.cuda.empty_cache()
+        if not args.rehearse:
+            replica.init_comm(eng)  # the context's RCCL communicator: its rank count is reported
+            res["comm"] = {"rccl_ranks": eng.comm_count()}
+        if not args.no_anti_entropy:
+            # configs 4 and 5 over the same ranks (the driver's multi-GPU run
+            # measures and checks them with the headline), each with its own
+            # timed region, checked after it
+            sub = argparse.Namespace(**vars(args))
+            sub.steps, sub.warmup, sub.n_obj, sub.no_cpu_baseline = args.ae_steps, 1, args.ae_n_obj, True
+            res["anti_entropy"] = {}
+            for key, fn in (("config4_gcounter", run_gcounter_ae), ("config5_orswot_csr", run_orswot_csr)):
+                r = fn(sub, rank, world, local, eng=eng)
+                res["anti_entropy"][key] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "steps",
+                                                              "config", "comm", "check") if k in r}
+                torch.cuda.empty_cache()
     return res
 
 
@@ -405,11 +488,37 @@ def _timed_steps(args, world, stream, fn):
     return wall, float(np.mean([a.elapsed_time(b) for a, b in zip(starts, ends)]))
 
 
-def run_orswot_csr(args, rank, world, local):
+def _packed_digest(base_u8, used):
+    """crdts_hip.replica.digest of a PACKED batch (records contiguous in object
+    order from byte 0): sum over its u64 words w_k of w_k * (2k + 1) mod 2^64."""
+    import numpy as np
+
+    w = base_u8[:used].cpu().numpy().view(np.uint64)
+    k = np.arange(w.size, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        return int((w * (k * np.uint64(2) + np.uint64(1))).sum(dtype=np.uint64))
+
+
+def _gather_ints(vals, world):
+    """All-gather a few u64 values (as int64 on the GPU) -> list per rank."""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([v - (1 << 64) if v >= (1 << 63) else v for v in vals], dtype=torch.int64, device="cuda")
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [[int(x) % (1 << 64) for x in p.cpu().tolist()] for p in parts]
+
+
+def run_orswot_csr(args, rank, world, local, eng=None):
     """Config 5 (BASELINE.json configs[4]): 1M Orswots with CSR top clocks over
     a 1024-actor universe; replica anti-entropy. At N > 1 rank r holds replica
-    r and a step is all-gather (RCCL) + rank-order fold of the N replicas; at
-    N = 1 a step folds `--replicas` replicas held locally."""
+    r and a step is crdt_orswot_replica_join over RCCL (owner-sharded rank-order
+    fold of the N replicas, into a reused output buffer); after the timed
+    steps every rank's digest must be equal and a sample of objects from every
+    range must equal the oracle's rank-order fold. At N = 1 a step folds
+    `--replicas` replicas held locally."""
+    import numpy as np
     import torch
 
     import crdts_hip
@@ -418,18 +527,29 @@ def run_orswot_csr(args, rank, world, local):
     n = args.n_obj or 1_000_000
     R = world if world > 1 else args.replicas
     t0 = time.time()
-    reps = crdts_hip.generate_replicas(n, R, threads=args.threads)
+    reps = crdts_hip.generate_replicas(n, R, threads=args.threads, keep=(rank, 1) if world > 1 else None)
     gen_s = time.time() - t0
-    eng = crdts_hip.Engine(local)
+    eng = eng or crdts_hip.Engine(local)
     SP, U = crdts_hip.SPARSE_CLOCK, crdts_hip.CONFIG5["universe"]
     stream = torch.cuda.Stream(device=local)
+    check = None
     if world > 1:
-        mine = crdts_hip.OrswotBatch.from_host(*reps[rank], U, device=local, flags=SP)
+        mine = crdts_hip.OrswotBatch.from_host(*reps[0], U, device=local, flags=SP)
         del reps
-        replica.init_comm(eng)  # the context's own RCCL communicator (crdt_comm_init)
+        if args.rehearse:  # the same C++ join over the gloo transport
+            T = replica.GlooTransport()
+            bound = int(sum_over_ranks(float((mine.bytes + 15) // 16 * 16), world))
+            out = eng.orswot_replica_alloc_out(mine, bound)
 
-        def step():  # owner-sharded: crdt_orswot_replica_join over RCCL
-            return replica.orswot_anti_entropy(eng, mine)
+            def step():
+                return eng.orswot_replica_join_transport(mine, T, out=out, stream=stream)
+        else:
+            if not eng.has_comm:
+                replica.init_comm(eng)  # the context's own RCCL communicator (crdt_comm_init)
+            out = eng.orswot_replica_alloc_out(mine, eng.orswot_replica_join_bound(mine, stream))
+
+            def step():  # owner-sharded: crdt_orswot_replica_join over RCCL, reused output
+                return eng.orswot_replica_join(mine, out=out, stream=stream)
     else:
         batches = [crdts_hip.OrswotBatch.from_host(b, o, U, device=local, flags=SP) for b, o in reps]
         del reps
@@ -449,6 +569,39 @@ def run_orswot_csr(args, rank, world, local):
     eng.status(stream)
     wall, ev_ms = _timed_steps(args, world, stream, step)
     eng.status(stream)
+    if world > 1:
+        # self-check (outside the timed region): identical bytes on every rank,
+        # and a sample of every rank's range equal to the oracle's fold
+        final = step()
+        torch.cuda.synchronize()
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_ffi
+
+        dg = _packed_digest(final.base, final.bytes)
+        digests = [g[0] for g in _gather_ints([dg], world)]
+        b = replica.ranges(n, world)
+        host_b = final.base[: final.bytes].cpu().numpy()
+        host_o = final.off.cpu().numpy().view(np.uint64)
+        bad, sampled = 0, 0
+        for j in range(world):
+            m = min(32, b[j + 1] - b[j])
+            if m == 0:
+                continue
+            sub = crdts_hip.generate_replicas(m, R, first_obj=b[j], threads=4)
+            acc = sub[0]
+            for xb, xo in sub[1:]:
+                acc = oracle_ffi.orswot_merge_batch(acc[0], acc[1], xb, xo, U, threads=4, flags=SP)
+            for k in range(m):
+                o = int(host_o[b[j] + k])
+                size = int(host_b[o:o + 4].view(np.uint32)[0])
+                eo = int(acc[1][k])
+                esize = int(acc[0][eo:eo + 4].view(np.uint32)[0])
+                bad += int(host_b[o:o + size].tobytes() != acc[0][eo:eo + esize].tobytes())
+                sampled += 1
+        check = {"digests_equal": len(set(digests)) == 1, "digest": f"{dg:016x}", "sample_objects": sampled,
+                 "sample_mismatches": bad, "ok": len(set(digests)) == 1 and bad == 0}
+        if not check["ok"]:
+            print(f"bench.py rank {rank}: config-5 anti-entropy check FAILED: {check}", file=sys.stderr)
     merges = n * (R - 1)
     total = sum_over_ranks(float(merges * args.steps), world)
     res = {
@@ -464,6 +617,10 @@ def run_orswot_csr(args, rank, world, local):
                                    "fold of n/N objects, folded ranges all-gathered (crdt_orswot_replica_join)")
                    if world > 1 else "local fold"},
     }
+    if world > 1:
+        res["comm"] = {"rccl_ranks": None if args.rehearse else eng.comm_count(), "host_syncs_per_step": 4,
+                       "transport": "gloo (rehearsal)" if args.rehearse else "rccl"}
+        res["check"] = check
     if world == 1:
         def rec_bytes(B):  # sum of the batch's record sizes (gaps excluded)
             return int(B.base.view(torch.int32)[(B.off // 4)].sum(dtype=torch.int64).item())
@@ -492,12 +649,15 @@ def run_orswot_csr(args, rank, world, local):
     return res
 
 
-def run_gcounter_ae(args, rank, world, local):
+def run_gcounter_ae(args, rank, world, local, eng=None):
     """Config 4 (BASELINE.json configs[3]): 1B GCounters x 8 dense actor slots
     (64 GB of u64 per GPU); replica r increments slot r. At N > 1 a step is the
-    in-place RCCL all-reduce(max) over xGMI (u64-exact); at N = 1 it is the
-    local join of two such replicas (dense_max_kernel)."""
+    in-place RCCL all-reduce(max) over xGMI (u64-exact; repeated steps are
+    idempotent); after the timed steps every rank's digest of its 64 GB must be
+    equal, and sampled rows must equal the max over every rank's pre-join rows.
+    At N = 1 a step is the local join of two such replicas (dense_max_kernel)."""
     import torch
+    import torch.distributed as dist
 
     import crdts_hip
     from crdts_hip import replica
@@ -511,18 +671,28 @@ def run_gcounter_ae(args, rank, world, local):
     g.manual_seed(0xC0FFEE04 + 1 + rank)
     mine_slot = rank % A
     base[:, mine_slot] += torch.randint(1, 1 << 20, (n,), dtype=torch.int64, device=dev, generator=g)
-    eng = crdts_hip.Engine(local)
+    eng = eng or crdts_hip.Engine(local)
     stream = torch.cuda.Stream(device=local)
+    check = None
+    ae_eng = None if args.rehearse else eng  # rehearsal: the gloo path of replica.dense_allreduce_max
     if world > 1:
-        replica.init_comm(eng)  # the context's own RCCL communicator (crdt_comm_init)
-        native = True  # crdt_replica_allreduce_max: ncclUint64 + ncclMax, no sign-flip passes
+        if not args.rehearse and not eng.has_comm:
+            replica.init_comm(eng)  # the context's own RCCL communicator (crdt_comm_init)
+        # pre-join sample rows (head, middle, tail), every rank's, for the check
+        m = min(4096, n)
+        idx = torch.cat([torch.arange(0, m, device=dev), torch.arange(n // 2, n // 2 + m, device=dev) % n,
+                         torch.arange(n - m, n, device=dev)])
+        pre = base[idx].contiguous()
+        parts = [torch.empty_like(pre) for _ in range(world)]
+        dist.all_gather(parts, pre)
+        expect = torch.stack(parts).amax(0)  # counters < 2^41: signed max == u64 max here
+        del parts
 
         def step():
-            replica.dense_allreduce_max(base, engine=eng, stream=stream)
+            replica.dense_allreduce_max(base, engine=ae_eng, stream=stream)
     else:
         other = base.clone()
         other[:, (mine_slot + 1) % A] += 1
-        native = None
 
         def step():
             eng.dense_merge(base, other, A, "gcounter", stream=stream)
@@ -542,15 +712,26 @@ def run_gcounter_ae(args, rank, world, local):
                    else "local replica join (dense_max_kernel)"},
     }
     if world > 1:
+        torch.cuda.synchronize()
+        ok_sample = bool(torch.equal(base[idx], expect))
+        dg = int(base.sum(dtype=torch.int64).item()) % (1 << 64)  # wraps mod 2^64: order-independent
+        digests = [x[0] for x in _gather_ints([dg], world)]
+        check = {"digests_equal": len(set(digests)) == 1, "digest": f"{dg:016x}", "sample_rows": int(idx.numel()),
+                 "sample_ok": ok_sample, "ok": ok_sample and len(set(digests)) == 1}
+        if not check["ok"]:
+            print(f"bench.py rank {rank}: config-4 anti-entropy check FAILED: {check}", file=sys.stderr)
         # ring all-reduce bus bandwidth convention: 2 (N-1)/N x bytes / time
-        res["comm"] = {"algbw_GBps": bytes_per_gpu / (ev_ms * 1e-3) / 1e9,
+        res["comm"] = {"rccl_ranks": None if args.rehearse else eng.comm_count(),
+                       "transport": "gloo (rehearsal)" if args.rehearse else "rccl",
+                       "algbw_GBps": bytes_per_gpu / (ev_ms * 1e-3) / 1e9,
                        "busbw_GBps": 2 * (world - 1) / world * bytes_per_gpu / (ev_ms * 1e-3) / 1e9,
                        "xgmi_peak_GBps": 7 * 153}
+        res["check"] = check
         # the owner-shard variant: reduce-scatter(max),
         # each rank keeps its 1/N of the joined counters (crdt_replica_reduce_scatter_max)
         flat = base.reshape(-1)[: (base.numel() // world) * world]
         _, rs_ms = _timed_steps(args, world, stream,
-                                lambda: replica.dense_reduce_scatter_max(flat, engine=eng, stream=stream))
+                                lambda: replica.dense_reduce_scatter_max(flat, engine=ae_eng, stream=stream))
         res["comm"]["reduce_scatter"] = {"ms": rs_ms, "algbw_GBps": bytes_per_gpu / (rs_ms * 1e-3) / 1e9,
                                          "busbw_GBps": (world - 1) / world * bytes_per_gpu / (rs_ms * 1e-3) / 1e9}
     else:
@@ -559,6 +740,22 @@ def run_gcounter_ae(args, rank, world, local):
                            "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "kernel_ms": ev_ms,
                            "alg_bytes_per_launch": 3 * bytes_per_gpu, "traffic": None}
     return res
+
+
+def run_spawn_check(args, rank, world, local):
+    """CPU only (gloo): what the launch path gives each rank — its rank, the
+    world size, LOCAL_RANK (the GPU it would bind) and its pid — all-gathered."""
+    import torch
+    import torch.distributed as dist
+
+    me = torch.tensor([rank, world, local, os.getpid()], dtype=torch.int64)
+    parts = [torch.empty_like(me) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(parts, me)
+    else:
+        parts = [me]
+    return {"metric": "spawn_check", "value": float(world), "unit": "ranks", "n_gpus": world,
+            "ranks": [p.tolist() for p in parts]}
 
 
 def run_bincode(args, rank, world, local):
@@ -1022,10 +1219,14 @@ def run_map_orswot(args, rank, world, local):
 
 def main():
     args = parse()
-    rank, world, local = dist_setup()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))  # before any GPU call in this process
+    rank, world, local = dist_setup(args)
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    if args.workload == "orswot":
+    if args.workload == "spawn_check":
+        res = run_spawn_check(args, rank, world, local)
+    elif args.workload == "orswot":
         res = run_orswot(args, rank, world, local)
     elif args.workload == "vclock":
         res = run_vclock(args, rank, world, local)
@@ -1045,11 +1246,17 @@ def main():
         res = run_map_orswot(args, rank, world, local)
     else:
         res = run_dense(args, rank, world, local, args.workload)
+    failed = [k for k, v in res.get("anti_entropy", {}).items() if not (v.get("check") or {}).get("ok", True)]
+    if not (res.get("check") or {}).get("ok", True):
+        failed.append(args.workload)
     if rank == 0:
-        import crdts_hip
+        if args.workload != "spawn_check":
+            import crdts_hip
 
-        res["build"] = crdts_hip.build_record()  # the library this run loaded, vs __graft_entry__.build()'s record
+            res["build"] = crdts_hip.build_record()  # the library this run loaded, vs __graft_entry__.build()'s record
         print(json.dumps(res), flush=True)
+    if failed:
+        raise SystemExit(f"bench.py rank {rank}: cross-rank check failed: {failed}")
     if world > 1:
         import torch.distributed as dist
 

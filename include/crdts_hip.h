@@ -237,6 +237,9 @@ int crdt_comm_init(crdt_ctx* ctx, const uint8_t* h_id, int n_ranks, int rank);
 /* Also done by crdt_ctx_destroy. */
 int crdt_comm_destroy(crdt_ctx* ctx);
 
+/* *h_count := the number of ranks of the context's communicator (ncclCommCount). */
+int crdt_comm_count(crdt_ctx* ctx, int* h_count);
+
 /* Dense rows (VClock / GCounter / PNCounter rows, any width): d_rows[k] :=
  * max over ranks of d_rows[k], k < n_words, in place and in u64 order
  * (ncclAllReduce, ncclUint64, ncclMax; chunks of <= 1 GiB). It is
@@ -268,6 +271,36 @@ int crdt_orswot_replica_join_bound(crdt_ctx* ctx, const crdt_orswot_batch* mine,
 int crdt_orswot_replica_join(crdt_ctx* ctx, const crdt_orswot_batch* mine, uint32_t n_actors, uint32_t flags,
                              uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes, size_t* h_out_used,
                              void* stream);
+/* The same owner-sharded join over a transport of the caller's (one process
+ * per rank; e.g. gloo, MPI or a host network instead of RCCL) — no
+ * communicator needed on ctx. The code above the transport is
+ * crdt_orswot_replica_join's.
+ *   allgather: blocking; every rank contributes n u64 (h_in), h_out receives
+ *     n_ranks * n of them in rank order. Returns 0 or non-zero on failure.
+ *   exchange: device transfers; every send {peer, src, bytes} is matched, in
+ *     list order per peer, by that peer's recv {me, dst, bytes} of the same
+ *     size (sends and recvs with peer == rank are local copies, k-th to
+ *     k-th). src data is produced on `stream`; the transfers must be
+ *     complete, or ordered before later work on `stream`, when it returns.
+ *     Zero-byte entries move nothing. Returns 0 or non-zero on failure.
+ * A transport failure returns CRDT_ECOMM. */
+typedef struct crdt_xfer {
+  int peer;
+  const void* src;  /* device, sends */
+  void* dst;        /* device, recvs */
+  size_t bytes;
+} crdt_xfer;
+typedef struct crdt_transport {
+  int n_ranks, rank;
+  void* user;
+  int (*allgather)(void* user, const uint64_t* h_in, size_t n, uint64_t* h_out);
+  int (*exchange)(void* user, const crdt_xfer* sends, size_t n_sends, const crdt_xfer* recvs, size_t n_recvs,
+                  void* stream);
+} crdt_transport;
+int crdt_orswot_replica_join_transport(crdt_ctx* ctx, const crdt_transport* transport,
+                                       const crdt_orswot_batch* mine, uint32_t n_actors, uint32_t flags,
+                                       uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes, size_t* h_out_used,
+                                       void* stream);
 /* The same owner-sharded join over n_replicas (<= 64) replicas resident on
  * this context's device: each replica is a virtual rank (a host thread with
  * its own context and stream) and device copies are the transport; the code
@@ -339,6 +372,13 @@ typedef struct crdt_orswot_rep_params {
 int crdt_orswot_generate_replicas(uint64_t seed, size_t first_obj, size_t n_obj,
                                   const crdt_orswot_rep_params* params, uint32_t n_replicas,
                                   uint32_t flags, int n_threads, crdt_orswot_gen** out);
+/* The same replica sets, keeping only replicas [keep_first, keep_first +
+ * keep_count) (side s of the result = replica keep_first + s): a rank
+ * generates the replica it holds without encoding the others. */
+int crdt_orswot_generate_replicas_subset(uint64_t seed, size_t first_obj, size_t n_obj,
+                                         const crdt_orswot_rep_params* params, uint32_t n_replicas,
+                                         uint32_t keep_first, uint32_t keep_count, uint32_t flags, int n_threads,
+                                         crdt_orswot_gen** out);
 
 /* ------------------------------------------------------------------------ *
  * Map<K, MVReg<u64, A>, A>::merge, batched (Map

@@ -390,22 +390,61 @@ class Engine:
               "replica_reduce_scatter_max")
         return out
 
-    def orswot_replica_join(self, B: OrswotBatch, stream=None):
-        """((r0 ⊔ r1) ⊔ ...) of every rank's replica, owner-sharded over RCCL;
-        the same packed batch on every rank (crdt_orswot_replica_join)."""
-        torch = _torch()
+    def comm_count(self):
+        """Ranks of the context's RCCL communicator (ncclCommCount)."""
+        n = C.c_int(0)
+        check(lib.crdt_comm_count(self.ctx, C.byref(n)), "comm_count")
+        return n.value
+
+    def orswot_replica_join_bound(self, B: OrswotBatch, stream=None):
+        """Output bytes that suffice for crdt_orswot_replica_join (collective:
+        the sum of every rank's replica bytes)."""
         b = B.cbatch()
         bound = C.c_size_t(0)
         check(lib.crdt_orswot_replica_join_bound(self.ctx, C.byref(b), C.byref(bound), self._stream(stream)),
               "replica_join_bound")
+        return max(16, bound.value)
+
+    def orswot_replica_alloc_out(self, B: OrswotBatch, bound: int):
+        torch = _torch()
         dev = f"cuda:{self.device}"
-        base = torch.empty(max(16, bound.value), dtype=torch.uint8, device=dev)
-        off = torch.empty(B.n_obj, dtype=torch.int64, device=dev)
+        return OrswotBatch(torch.empty(max(16, bound), dtype=torch.uint8, device=dev),
+                           torch.empty(B.n_obj, dtype=torch.int64, device=dev), B.n_actors, max(16, bound), B.flags)
+
+    def orswot_replica_join(self, B: OrswotBatch, out: OrswotBatch | None = None, stream=None):
+        """((r0 ⊔ r1) ⊔ ...) of every rank's replica, owner-sharded over RCCL;
+        the same packed batch on every rank (crdt_orswot_replica_join). `out`
+        (from orswot_replica_alloc_out with a bound from
+        orswot_replica_join_bound) is reused when given, so a repeated join
+        runs no bound collective and allocates nothing."""
+        if out is None:
+            out = self.orswot_replica_alloc_out(B, self.orswot_replica_join_bound(B, stream))
+        b = B.cbatch()
         used = C.c_size_t(0)
-        check(lib.crdt_orswot_replica_join(self.ctx, C.byref(b), B.n_actors, B.flags, C.c_void_p(base.data_ptr()),
-                                           C.c_void_p(off.data_ptr()), base.numel(), C.byref(used),
-                                           self._stream(stream)), "orswot_replica_join")
-        return OrswotBatch(base, off, B.n_actors, max(16, used.value), B.flags)
+        check(lib.crdt_orswot_replica_join(self.ctx, C.byref(b), B.n_actors, B.flags,
+                                           C.c_void_p(out.base.data_ptr()), C.c_void_p(out.off.data_ptr()),
+                                           out.base.numel(), C.byref(used), self._stream(stream)),
+              "orswot_replica_join")
+        return OrswotBatch(out.base, out.off, B.n_actors, max(16, used.value), B.flags)
+
+    def orswot_replica_join_transport(self, B: OrswotBatch, transport, out: OrswotBatch | None = None,
+                                      out_bytes: int | None = None, stream=None):
+        """The same owner-sharded join over a caller transport
+        (crdt_orswot_replica_join_transport; `transport` has a `.c` TransportC,
+        e.g. replica.GlooTransport). out_bytes defaults to world x this
+        replica's bytes rounded up (enough when replicas are of similar size;
+        pass the all-reduced sum otherwise)."""
+        if out is None:
+            cap = out_bytes if out_bytes is not None else transport.world * ((B.bytes + 15) // 16 * 16 + 16)
+            out = self.orswot_replica_alloc_out(B, cap)
+        b = B.cbatch()
+        used = C.c_size_t(0)
+        check(lib.crdt_orswot_replica_join_transport(self.ctx, C.byref(transport.c), C.byref(b), B.n_actors,
+                                                     B.flags, C.c_void_p(out.base.data_ptr()),
+                                                     C.c_void_p(out.off.data_ptr()), out.base.numel(),
+                                                     C.byref(used), self._stream(stream)),
+              "orswot_replica_join_transport")
+        return OrswotBatch(out.base, out.off, B.n_actors, max(16, used.value), B.flags)
 
     def orswot_replica_join_local(self, batches, stream=None):
         """The same owner-sharded join with every replica a virtual rank on this
@@ -617,17 +656,27 @@ def _copy_sides(g, n_sides, n_obj):
     return sides
 
 
-def generate_replicas(n_obj, n_replicas=8, first_obj=0, seed=CONFIG5_SEED, params=None, sparse=True, threads=8):
+def generate_replicas(n_obj, n_replicas=8, first_obj=0, seed=CONFIG5_SEED, params=None, sparse=True, threads=8,
+                      keep=None):
     """Replica sets for anti-entropy (config 5, include/crdts_hip.h): a list of
-    n_replicas (base, off) batches; replica r of object i is record i of batch r."""
+    n_replicas (base, off) batches; replica r of object i is record i of batch r.
+    keep=(first, count): only replicas [first, first + count) are returned
+    (crdt_orswot_generate_replicas_subset; the same bytes)."""
     d = dict(CONFIG5)
     d.update(params or {})
     P = RepParams(**{k: int(v) for k, v in d.items()})
     g = C.c_void_p()
-    check(lib.crdt_orswot_generate_replicas(seed, first_obj, n_obj, C.byref(P), n_replicas,
-                                            SPARSE_CLOCK if sparse else 0, threads, C.byref(g)), "generate_replicas")
+    fl = SPARSE_CLOCK if sparse else 0
+    if keep is None:
+        check(lib.crdt_orswot_generate_replicas(seed, first_obj, n_obj, C.byref(P), n_replicas, fl, threads,
+                                                C.byref(g)), "generate_replicas")
+        count = n_replicas
+    else:
+        count = int(keep[1])
+        check(lib.crdt_orswot_generate_replicas_subset(seed, first_obj, n_obj, C.byref(P), n_replicas, int(keep[0]),
+                                                       count, fl, threads, C.byref(g)), "generate_replicas_subset")
     try:
-        return _copy_sides(g, n_replicas, n_obj)
+        return _copy_sides(g, count, n_obj)
     finally:
         lib.crdt_orswot_gen_free(g)
 

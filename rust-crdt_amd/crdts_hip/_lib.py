@@ -69,6 +69,7 @@ EXPORTS = [
     "crdt_comm_unique_id", "crdt_comm_init", "crdt_comm_destroy", "crdt_replica_allreduce_max",
     "crdt_replica_reduce_scatter_max",
     "crdt_orswot_replica_join_bound", "crdt_orswot_replica_join", "crdt_orswot_replica_join_local",
+    "crdt_comm_count", "crdt_orswot_replica_join_transport", "crdt_orswot_generate_replicas_subset",
 ]
 
 CRDT_COMM_ID_BYTES = 128
@@ -96,6 +97,22 @@ MAP_ORSWOT_CAPS = ("kcap", "mcap", "vdcap", "vscap", "dcap", "scap")
 class MapOrswotSlabC(C.Structure):
     """crdt_map_orswot_slab (include/crdts_hip.h)."""
     _fields_ = [(f, C.c_void_p) for f in MAP_ORSWOT_FIELDS] + [(f, C.c_uint32) for f in MAP_ORSWOT_CAPS]
+
+
+class Xfer(C.Structure):
+    """crdt_xfer (include/crdts_hip.h)."""
+    _fields_ = [("peer", C.c_int), ("src", C.c_void_p), ("dst", C.c_void_p), ("bytes", C.c_size_t)]
+
+
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_uint64))
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(Xfer), C.c_size_t, C.POINTER(Xfer), C.c_size_t,
+                          C.c_void_p)
+
+
+class TransportC(C.Structure):
+    """crdt_transport (include/crdts_hip.h): a caller-provided transport."""
+    _fields_ = [("n_ranks", C.c_int), ("rank", C.c_int), ("user", C.c_void_p), ("allgather", ALLGATHER_FN),
+                ("exchange", EXCHANGE_FN)]
 
 
 def _load():
@@ -168,6 +185,11 @@ def _load():
         "crdt_orswot_replica_join_bound": (I, [P, BP, C.POINTER(SZ), P]),
         "crdt_orswot_replica_join": (I, [P, BP, U32, U32, P, P, SZ, C.POINTER(SZ), P]),
         "crdt_orswot_replica_join_local": (I, [P, BP, U32, U32, U32, P, P, SZ, C.POINTER(SZ), P]),
+        "crdt_comm_count": (I, [P, C.POINTER(I)]),
+        "crdt_orswot_generate_replicas_subset": (I, [U64, SZ, SZ, C.POINTER(RepParams), U32, U32, U32, U32, I,
+                                                     C.POINTER(P)]),
+        "crdt_orswot_replica_join_transport": (I, [P, C.POINTER(TransportC), BP, U32, U32, P, P, SZ, C.POINTER(SZ),
+                                                   P]),
     }
     for name, (res, args) in sig.items():
         if name in DIAG_SYMBOLS and not hasattr(L, name):

@@ -194,6 +194,99 @@ def orswot_anti_entropy(engine, batch, group=None, merge_fn=None, stats=None):
     return OrswotBatch(out_base, out_off, A, max(16, int(P[-1])), fl)
 
 
+class GlooTransport:
+    """A crdt_transport over a torch.distributed group (e.g. gloo): the C
+    ABI's owner-sharded join (crdt_orswot_replica_join_transport) with every
+    rank a process, RCCL not involved. Device data is staged through host
+    memory (hipMemcpy), so this is a test / fallback transport — the product
+    multi-GPU path is RCCL (crdt_orswot_replica_join)."""
+
+    def __init__(self, group=None):
+        import ctypes as C
+
+        import torch.distributed as dist
+
+        from ._lib import ALLGATHER_FN, EXCHANGE_FN, TransportC
+
+        self.group = group
+        self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        self._hip = C.CDLL("libamdhip64.so.7")  # the HIP runtime already loaded (torch's)
+        self._hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        self._hip.hipStreamSynchronize.argtypes = [C.c_void_p]
+        self.calls = {"allgather": 0, "exchange": 0, "bytes_sent": 0, "bytes_received": 0}
+        self._ag = ALLGATHER_FN(self._allgather)
+        self._ex = EXCHANGE_FN(self._exchange)
+        self.c = TransportC(self.world, self.rank, None, self._ag, self._ex)
+
+    def _memcpy(self, dst, src, n):
+        if n and self._hip.hipMemcpy(dst, src, n, 4) != 0:  # hipMemcpyDefault
+            raise RuntimeError("hipMemcpy failed")
+
+    def _allgather(self, user, h_in, n, h_out):
+        try:
+            import torch
+            import torch.distributed as dist
+
+            mine = torch.from_numpy(np.ctypeslib.as_array(h_in, shape=(n,)).view(np.int64).copy())
+            parts = [torch.empty(n, dtype=torch.int64) for _ in range(self.world)]
+            dist.all_gather(parts, mine, group=self.group)
+            out = np.ctypeslib.as_array(h_out, shape=(n * self.world,)).view(np.int64)
+            out[:] = torch.cat(parts).numpy()
+            self.calls["allgather"] += 1
+            return 0
+        except Exception as e:  # noqa: BLE001 - reported to the C side as a transport failure
+            print(f"GlooTransport.allgather: {e!r}", flush=True)
+            return 1
+
+    def _exchange(self, user, sends, ns, recvs, nr, stream):
+        try:
+            import ctypes as C
+
+            import torch
+            import torch.distributed as dist
+
+            if self._hip.hipStreamSynchronize(stream) != 0:  # the sends' data is produced on `stream`
+                return 1
+            S = [sends[k] for k in range(ns)]
+            Rv = [recvs[k] for k in range(nr)]
+            me = self.rank
+            self_s = [x for x in S if x.peer == me]
+            self_r = [y for y in Rv if y.peer == me]
+            if len(self_s) != len(self_r):
+                return 1
+            for x, y in zip(self_s, self_r):  # k-th self send -> k-th self recv
+                if x.bytes != y.bytes:
+                    return 1
+                self._memcpy(y.dst, x.src, x.bytes)
+            reqs, landing = [], []
+            tag = {}
+            for x in S:  # tags: position among this pair's transfers (the same on both ends)
+                t = tag[("s", x.peer)] = tag.get(("s", x.peer), -1) + 1
+                if x.peer == me or not x.bytes:
+                    continue
+                h = np.empty(x.bytes, np.uint8)
+                self._memcpy(h.ctypes.data_as(C.c_void_p), x.src, x.bytes)
+                reqs.append(dist.isend(torch.from_numpy(h), x.peer, group=self.group, tag=t))
+                self.calls["bytes_sent"] += x.bytes
+            for y in Rv:
+                t = tag[("r", y.peer)] = tag.get(("r", y.peer), -1) + 1
+                if y.peer == me or not y.bytes:
+                    continue
+                h = torch.empty(y.bytes, dtype=torch.uint8)
+                reqs.append(dist.irecv(h, y.peer, group=self.group, tag=t))
+                landing.append((y, h))
+            for r in reqs:
+                r.wait()
+            for y, h in landing:
+                self._memcpy(y.dst, C.c_void_p(h.data_ptr()), y.bytes)
+                self.calls["bytes_received"] += y.bytes
+            self.calls["exchange"] += 1
+            return 0
+        except Exception as e:  # noqa: BLE001 - reported to the C side as a transport failure
+            print(f"GlooTransport.exchange: {e!r}", flush=True)
+            return 1
+
+
 def digest(batch) -> int:
     """Checksum of a batch's records in object order (offsets and gaps
     excluded, so gapped and compact batches of the same states agree):

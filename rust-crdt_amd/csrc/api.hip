@@ -212,7 +212,8 @@ int crdt_orswot_compact(crdt_ctx* ctx, const crdt_orswot_batch* src, uint8_t* d_
   uint8_t* temp = (uint8_t*)d_scratch + ((8 * src->n_obj + 255) & ~size_t(255));
   size_t temp_bytes = crdt_orswot_compact_scratch_bytes(src->n_obj) -
                       ((8 * src->n_obj + 255) & ~size_t(255)) - 256;
-  if ((rc = launch_record_sizes(src->base, src->off, src->n_obj, sizes, S(stream)))) return rc;
+  if ((rc = launch_record_sizes(src->base, src->off, src->bytes, src->n_obj, sizes, ctx->d_status, S(stream))))
+    return rc;
   if (hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, sizes, d_dst_off, (int)src->n_obj,
                                        S(stream)) != hipSuccess)
     return CRDT_EHIP;
@@ -225,7 +226,7 @@ int crdt_orswot_compact(crdt_ctx* ctx, const crdt_orswot_batch* src, uint8_t* d_
       hipStreamSynchronize(S(stream)) != hipSuccess)
     return CRDT_EHIP;
   if (last_off + last_size > dst_bytes) return CRDT_ECAPACITY;
-  return launch_record_copy(src->base, src->off, d_dst, d_dst_off, src->n_obj, S(stream));
+  return launch_record_copy(src->base, src->off, sizes, d_dst, d_dst_off, src->n_obj, S(stream));
 }
 
 int crdt_orswot_merge_host(crdt_ctx* ctx, const uint8_t* h_self_base, const uint64_t* h_self_off,

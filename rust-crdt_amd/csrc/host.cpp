@@ -367,11 +367,12 @@ struct crdt_orswot_gen {
 };
 
 namespace {
-// Runs gen(i, states) for objects [0, n) on T threads and packs side s of
-// every object into batch s (16-B aligned records, object order).
+// Runs gen(i, states) for objects [0, n) on T threads and packs side
+// keep_first + s of every object into batch s, s < n_sides (16-B aligned
+// records, object order).
 template <class G>
 int pack_sides(size_t n_obj, uint32_t n_sides, int T, uint32_t n_actors, bool sparse, G gen,
-               crdt_orswot_gen** out) {
+               crdt_orswot_gen** out, uint32_t keep_first = 0) {
   T = std::max(1, T);
   std::vector<std::vector<std::vector<uint8_t>>> buf(n_sides, std::vector<std::vector<uint8_t>>(T));
   std::vector<std::vector<std::vector<uint64_t>>> loc(n_sides, std::vector<std::vector<uint64_t>>(T));
@@ -382,10 +383,10 @@ int pack_sides(size_t n_obj, uint32_t n_sides, int T, uint32_t n_actors, bool sp
     for (size_t i = b; i < e; ++i) {
       gen(i, st);
       for (uint32_t s = 0; s < n_sides; ++s) {
-        long n = encode(st[s], n_actors, tmp.data(), tmp.size(), sparse);
+        long n = encode(st[keep_first + s], n_actors, tmp.data(), tmp.size(), sparse);
         while (n == CRDT_ECAPACITY) {
           tmp.resize(tmp.size() * 2);
-          n = encode(st[s], n_actors, tmp.data(), tmp.size(), sparse);
+          n = encode(st[keep_first + s], n_actors, tmp.data(), tmp.size(), sparse);
         }
         if (n < 0) { err[t] = (int)n; return; }
         loc[s][t].push_back(buf[s][t].size());
@@ -457,6 +458,20 @@ int crdt_orswot_generate_replicas(uint64_t seed, size_t first_obj, size_t n_obj,
   return pack_sides(n_obj, n_replicas, n_threads, P.universe, (flags & CRDT_ORSWOT_SPARSE_CLOCK) != 0,
                     [&](size_t i, std::vector<HOrswot>& st) { gen_replicas(seed, first_obj + i, P, n_replicas, st); },
                     out);
+}
+
+int crdt_orswot_generate_replicas_subset(uint64_t seed, size_t first_obj, size_t n_obj,
+                                         const crdt_orswot_rep_params* params, uint32_t n_replicas,
+                                         uint32_t keep_first, uint32_t keep_count, uint32_t flags, int n_threads,
+                                         crdt_orswot_gen** out) {
+  if (!params || !out || params->universe == 0 || params->member_universe == 0 || n_replicas == 0 ||
+      keep_count == 0 || keep_first >= n_replicas || keep_count > n_replicas - keep_first ||
+      (flags & ~CRDT_ORSWOT_SPARSE_CLOCK))
+    return CRDT_EINVAL;
+  const crdt_orswot_rep_params P = *params;
+  return pack_sides(n_obj, keep_count, n_threads, P.universe, (flags & CRDT_ORSWOT_SPARSE_CLOCK) != 0,
+                    [&](size_t i, std::vector<HOrswot>& st) { gen_replicas(seed, first_obj + i, P, n_replicas, st); },
+                    out, keep_first);
 }
 
 int crdt_orswot_gen_side(const crdt_orswot_gen* g, int side, const uint8_t** h_base,

@@ -23,9 +23,11 @@ int launch_dense_max(uint64_t* self, const uint64_t* other, uint64_t n_words, hi
 int launch_orswot_validate(const uint8_t* base, const uint64_t* off, uint64_t bytes, uint64_t n_obj,
                            uint32_t n_actors, uint32_t flags, int* status, hipStream_t stream);
 
-int launch_record_sizes(const uint8_t* base, const uint64_t* off, uint64_t n_obj, uint64_t* sizes,
-                        hipStream_t stream);
-int launch_record_copy(const uint8_t* src, const uint64_t* src_off, uint8_t* dst,
+// Bounds-checked record sizes (size 0 + CRDT_ENONCANON latched for a record
+// out of [0, bytes)), and the copy of sizes[i] bytes per record.
+int launch_record_sizes(const uint8_t* base, const uint64_t* off, uint64_t bytes, uint64_t n_obj, uint64_t* sizes,
+                        int* status, hipStream_t stream);
+int launch_record_copy(const uint8_t* src, const uint64_t* src_off, const uint64_t* sizes, uint8_t* dst,
                        const uint64_t* dst_off, uint64_t n_obj, hipStream_t stream);
 
 int launch_bincode_bounds(const uint64_t* blen, uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A,

@@ -78,15 +78,28 @@ __global__ void validate_kernel(const uint8_t* __restrict__ base, const uint64_t
   if (fs != L.n_def_dot || ms != L.n_def_mem) return fail(status);
 }
 
-__global__ void sizes_kernel(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-                             uint64_t n_obj, uint64_t* __restrict__ sizes) {
+// Record sizes, bounds-checked: a record whose header or extent is out of
+// [0, bytes), misaligned, or whose size is not a 16-B multiple >= the header
+// gets size 0 (nothing is copied for it) and latches CRDT_ENONCANON — e.g.
+// an object a merge rejected, whose output offset has no record behind it.
+__global__ void sizes_kernel(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off, uint64_t bytes,
+                             uint64_t n_obj, uint64_t* __restrict__ sizes, int* status) {
   uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (i < n_obj) sizes[i] = *(const uint32_t*)(base + off[i]);
+  if (i >= n_obj) return;
+  const uint64_t o = off[i];
+  uint64_t size = 0;
+  if (!(o & 15u) && o <= bytes && bytes - o >= kHdrBytes) {
+    const uint64_t s = *(const uint32_t*)(base + o);
+    if (s >= kHdrBytes && !(s & 15u) && s <= bytes - o) size = s;
+  }
+  if (!size) fail(status);
+  sizes[i] = size;
 }
 
-// One wave per record, 16-B copies.
+// One wave per record, 16-B copies of sizes[i] bytes (sizes_kernel's).
 __global__ __launch_bounds__(256) void copy_kernel(const uint8_t* __restrict__ src,
                                                    const uint64_t* __restrict__ src_off,
+                                                   const uint64_t* __restrict__ sizes,
                                                    uint8_t* __restrict__ dst,
                                                    const uint64_t* __restrict__ dst_off,
                                                    uint64_t n_obj) {
@@ -95,7 +108,7 @@ __global__ __launch_bounds__(256) void copy_kernel(const uint8_t* __restrict__ s
   for (uint64_t i = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64; i < n_obj; i += stride) {
     const uint4* s = (const uint4*)(src + src_off[i]);
     uint4* d = (uint4*)(dst + dst_off[i]);
-    uint32_t n16 = *(const uint32_t*)s / 16;
+    const uint32_t n16 = (uint32_t)(sizes[i] / 16);
     for (uint32_t k = lane; k < n16; k += 64) d[k] = s[k];
   }
 }
@@ -111,20 +124,20 @@ int launch_orswot_validate(const uint8_t* base, const uint64_t* off, uint64_t by
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 
-int launch_record_sizes(const uint8_t* base, const uint64_t* off, uint64_t n_obj, uint64_t* sizes,
-                        hipStream_t stream) {
+int launch_record_sizes(const uint8_t* base, const uint64_t* off, uint64_t bytes, uint64_t n_obj, uint64_t* sizes,
+                        int* status, hipStream_t stream) {
   if (n_obj == 0) return CRDT_OK;
   uint32_t blocks = (uint32_t)((n_obj + 255) / 256);
-  hipLaunchKernelGGL(sizes_kernel, dim3(blocks), dim3(256), 0, stream, base, off, n_obj, sizes);
+  hipLaunchKernelGGL(sizes_kernel, dim3(blocks), dim3(256), 0, stream, base, off, bytes, n_obj, sizes, status);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 
-int launch_record_copy(const uint8_t* src, const uint64_t* src_off, uint8_t* dst,
+int launch_record_copy(const uint8_t* src, const uint64_t* src_off, const uint64_t* sizes, uint8_t* dst,
                        const uint64_t* dst_off, uint64_t n_obj, hipStream_t stream) {
   if (n_obj == 0) return CRDT_OK;
   uint64_t want = (n_obj + 3) / 4;
   uint32_t blocks = (uint32_t)(want < 2048 ? want : 2048);
-  hipLaunchKernelGGL(copy_kernel, dim3(blocks), dim3(256), 0, stream, src, src_off, dst, dst_off,
+  hipLaunchKernelGGL(copy_kernel, dim3(blocks), dim3(256), 0, stream, src, src_off, sizes, dst, dst_off,
                      n_obj);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }

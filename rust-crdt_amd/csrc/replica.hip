@@ -52,12 +52,21 @@ inline uint64_t al256(uint64_t x) { return (x + 255u) & ~uint64_t(255); }
 constexpr size_t kAllReduceChunk = size_t(1) << 27;  // u64 words per collective (1 GiB)
 
 // ---------------------------------------------------------------- kernels
-// Byte extent of every object range of one replica: range j = objects
-// [b_j, b_{j+1}), b_j = j*n/N; bounds[2j] = off[b_j], bounds[2j+1] = end of
-// the range's last record (0, 0 for an empty range).
+// Step 1's all-gather row of this rank, written on the device so that the
+// slice bounds need no host round trip of their own: d[2j], d[2j+1] = byte
+// extent of object range j = [b_j, b_{j+1}), b_j = j*n/N, of this replica
+// (0, 0 for an empty range; ~0 as the end of a range whose last record
+// header lies out of bounds), then the host-known fields of the row.
 __global__ void slice_bounds_kernel(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-                                    uint64_t bytes, uint64_t n, uint32_t R, uint64_t* __restrict__ bounds) {
+                                    uint64_t bytes, uint64_t n, uint32_t R, uint64_t* __restrict__ d, uint64_t f0,
+                                    uint64_t f1, uint64_t f2, uint64_t f3) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j == 0) {
+    d[2u * R] = f0;
+    d[2u * R + 1u] = f1;
+    d[2u * R + 2u] = f2;
+    d[2u * R + 3u] = f3;
+  }
   if (j >= R) return;
   const uint64_t b0 = n * j / R, b1 = n * (j + 1u) / R;
   uint64_t s = 0, e = 0;
@@ -66,8 +75,8 @@ __global__ void slice_bounds_kernel(const uint8_t* __restrict__ base, const uint
     const uint64_t last = off[b1 - 1u];
     e = last + 32u <= bytes ? last + *(const uint32_t*)(base + last) : ~0ull;  // ~0: out of bounds
   }
-  bounds[2u * j] = s;
-  bounds[2u * j + 1u] = e;
+  d[2u * j] = s;
+  d[2u * j + 1u] = e;
 }
 
 // off[i] := off[i] - sub[piece(i)] + add[piece(i)] for pieces of `per` objects
@@ -97,59 +106,97 @@ int launch_rebase(uint64_t* off, uint64_t n, uint64_t per, const uint64_t* first
 }
 
 // ---------------------------------------------------------------- transports
-struct Xfer {
-  int peer;
-  const void* src;  // sends
-  void* dst;        // recvs
-  size_t bytes;
-};
+using Xfer = crdt_xfer;
 
 struct Transport {
   int R = 1, me = 0;
   virtual ~Transport() = default;
   // blocking: every rank contributes n u64 (host), receives R*n in rank order
   virtual int allgather(const uint64_t* h_in, size_t n, uint64_t* h_out, hipStream_t st) = 0;
+  // the same with the contribution in DEVICE memory, produced on st (one
+  // host synchronisation in all)
+  virtual int allgather_dev(const uint64_t* d_in, size_t n, uint64_t* h_out, hipStream_t st) {
+    std::vector<uint64_t> h(n);
+    if (n && (hipMemcpyAsync(h.data(), d_in, 8 * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+              hipStreamSynchronize(st) != hipSuccess))
+      return CRDT_EHIP;
+    return allgather(h.data(), n, h_out, st);
+  }
   // enqueued on st: every send matched by the peer's recv of the same size
   virtual int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t st) = 0;
 };
 
 int nccl_rc(ncclResult_t r) { return r == ncclSuccess ? CRDT_OK : CRDT_ECOMM; }
 
+// Device staging of the small all-gathers (ctx-owned, crdt_comm_init):
+// kStageRow u64 per rank and contribution.
+inline size_t stage_row(int R) { return 2ull * R + 8; }
+inline size_t stage_words(int R) { return (size_t)(R + 1) * stage_row(R); }
+
 struct RcclTransport : Transport {
   ncclComm_t comm;
-  uint64_t* d_buf;  // (R + 1) * (2R + 3) u64 of device staging for the all-gathers (ctx-owned)
+  uint64_t* d_buf;
   RcclTransport(crdt_ctx* ctx, uint64_t* d) : comm((ncclComm_t)ctx->comm), d_buf(d) {
     R = ctx->n_ranks;
     me = ctx->rank;
   }
-  int allgather(const uint64_t* h_in, size_t n, uint64_t* h_out, hipStream_t st) override {
-    if (hipMemcpyAsync(d_buf, h_in, 8 * n, hipMemcpyHostToDevice, st) != hipSuccess) return CRDT_EHIP;
-    int rc = nccl_rc(ncclAllGather(d_buf, d_buf + n, n, ncclUint64, comm, st));
+  int gather_out(const uint64_t* d_in, size_t n, uint64_t* h_out, hipStream_t st) {
+    if (n > stage_row(R)) return CRDT_EINVAL;
+    int rc = nccl_rc(ncclAllGather(d_in, d_buf + stage_row(R), n, ncclUint64, comm, st));
     if (rc) return rc;
-    if (hipMemcpyAsync(h_out, d_buf + n, 8 * n * R, hipMemcpyDeviceToHost, st) != hipSuccess ||
+    if (hipMemcpyAsync(h_out, d_buf + stage_row(R), 8 * n * R, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
       return CRDT_EHIP;
     return CRDT_OK;
   }
+  int allgather(const uint64_t* h_in, size_t n, uint64_t* h_out, hipStream_t st) override {
+    if (n > stage_row(R)) return CRDT_EINVAL;
+    if (hipMemcpyAsync(d_buf, h_in, 8 * n, hipMemcpyHostToDevice, st) != hipSuccess) return CRDT_EHIP;
+    return gather_out(d_buf, n, h_out, st);
+  }
+  int allgather_dev(const uint64_t* d_in, size_t n, uint64_t* h_out, hipStream_t st) override {
+    return gather_out(d_in, n, h_out, st);
+  }
   int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t st) override {
-    // the self part as device copies, the rest as one group of point-to-point
-    // transfers (xGMI is point-to-point: each peer pair has its own link)
-    for (const Xfer& x : sends)
-      if (x.peer == me && x.bytes)
-        for (const Xfer& y : recvs)
-          if (y.peer == me && y.src == x.src && y.bytes == x.bytes &&
-              hipMemcpyAsync(y.dst, x.src, x.bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
-            return CRDT_EHIP;
+    // the self part as device copies (k-th self send -> k-th self recv), the
+    // rest as one group of point-to-point transfers (xGMI is point-to-point:
+    // each peer pair has its own link)
+    size_t k = 0;
+    for (const Xfer& y : recvs) {
+      if (y.peer != me) continue;
+      while (k < sends.size() && sends[k].peer != me) ++k;
+      if (k == sends.size() || sends[k].bytes != y.bytes) return CRDT_ECOMM;
+      if (y.bytes && hipMemcpyAsync(y.dst, sends[k].src, y.bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return CRDT_EHIP;
+      ++k;
+    }
     int rc = nccl_rc(ncclGroupStart());
     if (rc) return rc;
-    for (size_t k = 0; k < sends.size() && !rc; ++k)
-      if (sends[k].peer != me && sends[k].bytes)
-        rc = nccl_rc(ncclSend(sends[k].src, sends[k].bytes, ncclUint8, sends[k].peer, comm, st));
-    for (size_t k = 0; k < recvs.size() && !rc; ++k)
-      if (recvs[k].peer != me && recvs[k].bytes)
-        rc = nccl_rc(ncclRecv(recvs[k].dst, recvs[k].bytes, ncclUint8, recvs[k].peer, comm, st));
+    for (size_t q = 0; q < sends.size() && !rc; ++q)
+      if (sends[q].peer != me && sends[q].bytes)
+        rc = nccl_rc(ncclSend(sends[q].src, sends[q].bytes, ncclUint8, sends[q].peer, comm, st));
+    for (size_t q = 0; q < recvs.size() && !rc; ++q)
+      if (recvs[q].peer != me && recvs[q].bytes)
+        rc = nccl_rc(ncclRecv(recvs[q].dst, recvs[q].bytes, ncclUint8, recvs[q].peer, comm, st));
     const int rc2 = nccl_rc(ncclGroupEnd());
     return rc ? rc : rc2;
+  }
+};
+
+// The caller's own transport (crdt_transport callbacks: e.g. gloo, MPI, a
+// host network), one process per rank; the data path is its business.
+struct CallbackTransport : Transport {
+  const crdt_transport* t;
+  explicit CallbackTransport(const crdt_transport* tt) : t(tt) {
+    R = tt->n_ranks;
+    me = tt->rank;
+  }
+  int allgather(const uint64_t* h_in, size_t n, uint64_t* h_out, hipStream_t) override {
+    return t->allgather(t->user, h_in, n, h_out) ? CRDT_ECOMM : CRDT_OK;
+  }
+  int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t st) override {
+    return t->exchange(t->user, sends.data(), sends.size(), recvs.data(), recvs.size(), (void*)st) ? CRDT_ECOMM
+                                                                                                  : CRDT_OK;
   }
 };
 
@@ -234,95 +281,122 @@ int ensure_arena(crdt_ctx* ctx, size_t bytes) {
   return CRDT_OK;
 }
 
-int read_status(crdt_ctx* ctx, hipStream_t st) {
-  int v = 0;
-  if (hipMemcpyAsync(&v, ctx->d_status, sizeof v, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)
-    return CRDT_EHIP;
-  if (v && hipMemsetAsync(ctx->d_status, 0, sizeof(int), st) != hipSuccess) return CRDT_EHIP;
-  return v;
+// Arena layout of rank j's part of a join (every rank can compute every
+// rank's, from the step-1 all-gather): head = step-1 row (2R + 4 u64) and the
+// rebase table (3R u64); then every replica's slice of range j, their
+// offsets, two fold buffers (ping-pong), sizes and scan scratch.
+struct Plan {
+  size_t head, o_recv, o_roff, o_fa, o_fb, o_oa, o_ob, o_sz, o_cub, cub_temp, end;
+};
+inline size_t plan_head(int R) { return al256(8ull * (2 * R + 4) + 8ull * 3 * R); }
+Plan make_plan(int R, uint64_t nr, uint64_t total) {
+  Plan P;
+  P.head = plan_head(R);
+  P.cub_temp = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, P.cub_temp, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                         (int)(nr ? nr : 1));
+  size_t at = P.head;
+  auto take = [&](size_t bytes) { size_t o = at; at = al256(at + bytes); return o; };
+  P.o_recv = take(total);
+  P.o_roff = take(8 * R * nr);
+  P.o_fa = take(total);
+  P.o_fb = take(total);
+  P.o_oa = take(8 * nr);
+  P.o_ob = take(8 * nr);
+  P.o_sz = take(8 * nr);
+  P.o_cub = take(P.cub_temp);
+  P.end = at;
+  return P;
 }
 
 // The owner-sharded join, one rank's part. `out` may be null (the rank takes
-// part in the exchange but does not gather the result). A failure on one
-// rank is carried to every rank through the next all-gather, so all ranks
-// leave at the same step (none is left waiting in a collective).
-int orswot_join_rank(crdt_ctx* ctx, Transport& T, const crdt_orswot_batch* mine, uint32_t A, uint32_t flags,
-                     uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes, size_t* h_used, hipStream_t st) {
+// part in the exchange but does not gather the result). Every verdict that
+// decides whether a rank goes on to the next collective is taken from
+// all-gathered data, so all ranks leave at the same step (none is left
+// waiting in a collective another has left). Host synchronisations per call
+// in the steady state (arena large enough on every rank): 4 — the step-1
+// all-gather, the compaction's sizes + status read, the step-4 all-gather,
+// and the final one (the call is synchronous).
+int orswot_join_rank_body(crdt_ctx* ctx, Transport& T, const crdt_orswot_batch* mine, uint32_t A, uint32_t flags,
+                          uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes, size_t* h_used, hipStream_t st) {
   const int R = T.R, me = T.me;
   const uint64_t n = mine->n_obj;
   const bool want = d_out != nullptr;
   auto b = [&](int j) { return n * (uint64_t)j / (uint64_t)R; };
-  const size_t head = al256(8ull * 5 * R);  // device tables: slice bounds (2R), rebase table (3R)
+  const size_t W = 2 * (size_t)R + 4;
 
-  // 1. my byte extents of every range, all-gathered with the batch shape
-  int err = ensure_arena(ctx, head);
-  std::vector<uint64_t> mb(2 * R + 3, 0);
-  if (!err && n) {
-    if (!mine->base || !mine->off) {
-      err = CRDT_EINVAL;
-    } else {
-      hipLaunchKernelGGL(slice_bounds_kernel, dim3((R + 63) / 64), dim3(64), 0, st, mine->base, mine->off,
-                         (uint64_t)mine->bytes, n, (uint32_t)R, (uint64_t*)ctx->d_arena);
-      if (hipGetLastError() != hipSuccess ||
-          hipMemcpyAsync(mb.data(), ctx->d_arena, 16ull * R, hipMemcpyDeviceToHost, st) != hipSuccess ||
-          hipStreamSynchronize(st) != hipSuccess)
-        err = CRDT_EHIP;
-      uint64_t prev_end = 0;
-      for (int j = 0; j < R && !err; ++j) {  // ranges in increasing, non-overlapping order, 16-B aligned
-        if (b(j + 1) == b(j)) continue;
-        const uint64_t s0 = mb[2 * j], e0 = mb[2 * j + 1];
-        if (e0 == ~0ull || e0 < s0 || e0 > mine->bytes || s0 < prev_end || ((s0 | e0) & 15u)) err = CRDT_EINVAL;
-        prev_end = e0;
-      }
-    }
+  // 1. my byte extents of every range + (n, error, want, arena capacity),
+  //    all-gathered straight from the device. A status latched by an earlier
+  //    launch on this context belongs to that launch: it is cleared here.
+  int err = ensure_arena(ctx, plan_head(R));
+  if (!err && n && (!mine->base || !mine->off)) err = CRDT_EINVAL;
+  if (err) {
+    std::vector<uint64_t> mb(W, 0), G(W * R);
+    mb[2 * R] = n;
+    mb[2 * R + 1] = (uint64_t)-err;
+    int rc = T.allgather(mb.data(), W, G.data(), st);
+    return rc ? rc : err;
   }
-  mb[2 * R] = n;
-  mb[2 * R + 1] = (uint64_t)-err;
-  mb[2 * R + 2] = want ? 1u : 0u;
-  const size_t W = 2 * R + 3;
+  uint64_t* d_row = (uint64_t*)ctx->d_arena;
+  uint64_t* d_tab = d_row + W;
+  if (hipMemsetAsync(ctx->d_status, 0, sizeof(int), st) != hipSuccess) return CRDT_EHIP;
+  hipLaunchKernelGGL(slice_bounds_kernel, dim3((R + 63) / 64), dim3(64), 0, st, n ? mine->base : nullptr,
+                     n ? mine->off : nullptr, (uint64_t)mine->bytes, n, (uint32_t)R, d_row, n, 0ull,
+                     want ? 1ull : 0ull, (uint64_t)ctx->arena_bytes);
+  if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
   std::vector<uint64_t> G(W * R);
-  int rc = T.allgather(mb.data(), W, G.data(), st);
+  int rc = T.allgather_dev(d_row, W, G.data(), st);
   if (rc) return rc;
-  for (int p = 0; p < R; ++p) {
-    if (G[W * p + 2 * R] != n) return CRDT_EINVAL;  // the same object count on every rank
-    if (G[W * p + 2 * R + 1]) return -(int)G[W * p + 2 * R + 1];
-  }
   auto gs = [&](int p, int j) { return G[W * p + 2 * j]; };  // rank p's start of range j
   auto gsz = [&](int p, int j) { return G[W * p + 2 * j + 1] - G[W * p + 2 * j]; };
   auto wants = [&](int p) { return G[W * p + 2 * R + 2] != 0; };
+  for (int p = 0; p < R; ++p) {  // the same verdict on every rank
+    if (G[W * p + 2 * R] != n) return CRDT_EINVAL;  // the same object count on every rank
+    if (G[W * p + 2 * R + 1]) return -(int)G[W * p + 2 * R + 1];
+    uint64_t prev_end = 0;
+    for (int j = 0; j < R; ++j) {  // ranges in increasing, non-overlapping order, 16-B aligned
+      if (b(j + 1) == b(j)) continue;
+      const uint64_t s0 = gs(p, j), e0 = G[W * p + 2 * j + 1];
+      if (e0 == ~0ull || e0 < s0 || s0 < prev_end || ((s0 | e0) & 15u)) return CRDT_EINVAL;
+      prev_end = e0;
+    }
+  }
+  auto plan_of = [&](int j) {
+    uint64_t total = 0;
+    for (int p = 0; p < R; ++p) total += al16(gsz(p, j));
+    return make_plan(R, b(j + 1) - b(j), total);
+  };
 
-  // 2. the arena: every replica's slice of my range + their offsets, two fold
-  //    buffers (ping-pong), compaction scratch
+  // 2. the arena (grown only where some rank must: then every rank agrees
+  //    on the outcome before any data moves), and every replica's slice of
+  //    my range, point-to-point
+  bool grow = false;
+  for (int p = 0; p < R; ++p) grow |= plan_of(p).end > G[W * p + 2 * R + 3];
+  Plan P = plan_of(me);
+  if (grow) {
+    err = ensure_arena(ctx, P.end);
+    uint64_t e1 = (uint64_t)-err;
+    std::vector<uint64_t> E1(R);
+    if ((rc = T.allgather(&e1, 1, E1.data(), st))) return rc;
+    for (int p = 0; p < R; ++p)
+      if (E1[p]) return -(int)E1[p];
+    d_row = (uint64_t*)ctx->d_arena;  // the arena may have moved
+    d_tab = d_row + W;
+  }
   const uint64_t nr = b(me + 1) - b(me);
   std::vector<uint64_t> pos(R + 1, 0);
   for (int p = 0; p < R; ++p) pos[p + 1] = pos[p] + al16(gsz(p, me));
   const uint64_t total = pos[R];
-  size_t cub_temp = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, cub_temp, (uint64_t*)nullptr, (uint64_t*)nullptr,
-                                         (int)(nr ? nr : 1));
-  size_t at = head;
-  auto take = [&](size_t bytes) { size_t o = at; at = al256(at + bytes); return o; };
-  const size_t o_recv = take(total), o_roff = take(8 * R * nr), o_fa = take(total), o_fb = take(total),
-               o_oa = take(8 * nr), o_ob = take(8 * nr), o_sz = take(8 * nr), o_cub = take(cub_temp);
-  err = ensure_arena(ctx, at);
-  {  // agree: a rank that cannot allocate stops every rank here
-    std::vector<uint64_t> e1 = {(uint64_t)-err}, E1(R);
-    if ((rc = T.allgather(e1.data(), 1, E1.data(), st))) return rc;
-    for (int p = 0; p < R; ++p)
-      if (E1[p]) return -(int)E1[p];
-  }
   uint8_t* A8 = ctx->d_arena;
-  uint64_t* d_tab = (uint64_t*)A8 + 2 * R;
-  uint8_t* recv = A8 + o_recv;
-  uint64_t* roff = (uint64_t*)(A8 + o_roff);
+  uint8_t* recv = A8 + P.o_recv;
+  uint64_t* roff = (uint64_t*)(A8 + P.o_roff);
   std::vector<Xfer> sends, recvs;
   for (int p = 0; p < R; ++p) {  // per peer: the records, then the offsets (same order on both ends)
     const uint64_t np = b(p + 1) - b(p);
     sends.push_back({p, n ? mine->base + gs(me, p) : nullptr, nullptr, gsz(me, p)});
     sends.push_back({p, n ? mine->off + b(p) : nullptr, nullptr, 8 * np});
-    recvs.push_back({p, p == me && n ? mine->base + gs(me, me) : nullptr, recv + pos[p], gsz(p, me)});
-    recvs.push_back({p, p == me && n ? (const void*)(mine->off + b(me)) : nullptr, roff + nr * p, 8 * nr});
+    recvs.push_back({p, nullptr, recv + pos[p], gsz(p, me)});
+    recvs.push_back({p, nullptr, roff + nr * p, 8 * nr});
   }
   if ((rc = T.exchange(sends, recvs, st))) return rc;
 
@@ -335,9 +409,11 @@ int orswot_join_rank(crdt_ctx* ctx, Transport& T, const crdt_orswot_batch* mine,
   const uint8_t* acc = recv;
   const uint64_t* acc_off = roff;
   uint64_t acc_bytes = gsz(0, me);
+  // one replica: nothing is merged, so the slice is checked in full here
+  if (!err && R == 1 && nr) err = launch_orswot_validate(acc, acc_off, acc_bytes, nr, A, flags, ctx->d_status, st);
   for (int p = 1; p < R && nr && !err; ++p) {
-    uint8_t* o = A8 + (p % 2 ? o_fa : o_fb);
-    uint64_t* oo = (uint64_t*)(A8 + (p % 2 ? o_oa : o_ob));
+    uint8_t* o = A8 + (p % 2 ? P.o_fa : P.o_fb);
+    uint64_t* oo = (uint64_t*)(A8 + (p % 2 ? P.o_oa : P.o_ob));
     const uint8_t* rb = recv + pos[p];
     const uint64_t* ro = roff + nr * p;
     const uint64_t cap = acc_bytes + gsz(p, me);
@@ -350,37 +426,43 @@ int orswot_join_rank(crdt_ctx* ctx, Transport& T, const crdt_orswot_batch* mine,
     acc_off = oo;
     acc_bytes = cap;
   }
-  const bool in_a = acc == A8 + o_fa;
-  uint8_t* shard = A8 + (in_a ? o_fb : o_fa);
-  uint64_t* shard_off = (uint64_t*)(A8 + (in_a ? o_ob : o_oa));
-  uint64_t* sizes = (uint64_t*)(A8 + o_sz);
+  const bool in_a = acc == A8 + P.o_fa;
+  uint8_t* shard = A8 + (in_a ? P.o_fb : P.o_fa);
+  uint64_t* shard_off = (uint64_t*)(A8 + (in_a ? P.o_ob : P.o_oa));
+  uint64_t* sizes = (uint64_t*)(A8 + P.o_sz);
   uint64_t E = 0;
   if (nr && !err) {
-    err = launch_record_sizes(acc, acc_off, nr, sizes, st);
-    if (!err && hipcub::DeviceScan::ExclusiveSum(A8 + o_cub, cub_temp, sizes, shard_off, (int)nr, st) != hipSuccess)
+    // record sizes, bounds-checked (an object the fold rejected leaves no
+    // record behind its offset: size 0 and CRDT_ENONCANON latched), the
+    // scan, and the fold's latched status, read in one synchronisation
+    err = launch_record_sizes(acc, acc_off, acc_bytes, nr, sizes, ctx->d_status, st);
+    if (!err && hipcub::DeviceScan::ExclusiveSum(A8 + P.o_cub, P.cub_temp, sizes, shard_off, (int)nr, st) !=
+                    hipSuccess)
       err = CRDT_EHIP;
     uint64_t lo = 0, ls = 0;
+    int stv = 0;
     if (!err && (hipMemcpyAsync(&lo, shard_off + nr - 1, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
                  hipMemcpyAsync(&ls, sizes + nr - 1, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                 hipMemcpyAsync(&stv, ctx->d_status, sizeof stv, hipMemcpyDeviceToHost, st) != hipSuccess ||
                  hipStreamSynchronize(st) != hipSuccess))
       err = CRDT_EHIP;
+    if (!err && stv) err = stv;  // record-level errors latched by the fold, validation or sizes
     E = lo + ls;
     if (!err && E > total) err = CRDT_ENONCANON;  // a merged record never outgrows its inputs
-    if (!err) err = launch_record_copy(acc, acc_off, shard, shard_off, nr, st);
+    if (!err) err = launch_record_copy(acc, acc_off, sizes, shard, shard_off, nr, st);
   }
-  if (!err) err = read_status(ctx, st);  // record-level errors latched by the fold
 
   // 4. every rank's folded range to every rank that gathers the result
-  std::vector<uint64_t> m2 = {E, (uint64_t)out_bytes, (uint64_t)-err};
+  uint64_t m2[3] = {E, (uint64_t)out_bytes, (uint64_t)-err};
   std::vector<uint64_t> G2(3 * R);
-  if ((rc = T.allgather(m2.data(), 3, G2.data(), st))) return rc;
-  std::vector<uint64_t> P(R + 1, 0);
+  if ((rc = T.allgather(m2, 3, G2.data(), st))) return rc;
+  std::vector<uint64_t> Pq(R + 1, 0);
   for (int q = 0; q < R; ++q) {
     if (G2[3 * q + 2]) return -(int)G2[3 * q + 2];
-    P[q + 1] = P[q] + G2[3 * q];
+    Pq[q + 1] = Pq[q] + G2[3 * q];
   }
   for (int q = 0; q < R; ++q)
-    if (wants(q) && G2[3 * q + 1] < P[R]) return CRDT_ECAPACITY;  // every rank sees the same verdict
+    if (wants(q) && G2[3 * q + 1] < Pq[R]) return CRDT_ECAPACITY;  // every rank sees the same verdict
   sends.clear();
   recvs.clear();
   for (int q = 0; q < R; ++q) {
@@ -390,8 +472,8 @@ int orswot_join_rank(crdt_ctx* ctx, Transport& T, const crdt_orswot_batch* mine,
     }
     if (want) {
       const uint64_t nq = b(q + 1) - b(q);
-      recvs.push_back({q, q == me ? shard : nullptr, d_out + P[q], G2[3 * q]});
-      recvs.push_back({q, q == me ? (const void*)shard_off : nullptr, d_out_off + b(q), 8 * nq});
+      recvs.push_back({q, nullptr, d_out + Pq[q], G2[3 * q]});
+      recvs.push_back({q, nullptr, d_out_off + b(q), 8 * nq});
     }
   }
   rc = T.exchange(sends, recvs, st);
@@ -399,14 +481,26 @@ int orswot_join_rank(crdt_ctx* ctx, Transport& T, const crdt_orswot_batch* mine,
     for (int q = 0; q < R; ++q) {
       tab[q] = b(q);
       tab[R + q] = 0;
-      tab[2 * R + q] = P[q];
+      tab[2 * R + q] = Pq[q];
     }
     if (hipMemcpyAsync(d_tab, tab.data(), 8ull * 3 * R, hipMemcpyHostToDevice, st) != hipSuccess) rc = CRDT_EHIP;
     if (!rc) rc = launch_rebase(d_out_off, n, 1, d_tab, d_tab + R, d_tab + 2 * R, (uint32_t)R, st);
-    if (!rc && h_used) *h_used = P[R];
+    if (!rc && h_used) *h_used = Pq[R];
   }
   // the tables are read by kernels on st: finished before a later call reuses them
   if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = CRDT_EHIP;
+  return rc;
+}
+
+// A failed join leaves no latched status behind (the next call starts clean).
+int orswot_join_rank(crdt_ctx* ctx, Transport& T, const crdt_orswot_batch* mine, uint32_t A, uint32_t flags,
+                     uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes, size_t* h_used, hipStream_t st) {
+  const int rc = orswot_join_rank_body(ctx, T, mine, A, flags, d_out, d_out_off, out_bytes, h_used, st);
+  if (rc) {
+    (void)hipStreamSynchronize(st);
+    (void)hipMemsetAsync(ctx->d_status, 0, sizeof(int), st);
+    (void)hipStreamSynchronize(st);
+  }
   return rc;
 }
 
@@ -432,7 +526,7 @@ int crdt_comm_init(crdt_ctx* ctx, const uint8_t* h_id, int n_ranks, int rank) {
   ncclUniqueId id;
   std::memcpy(&id, h_id, sizeof id);
   uint64_t* stage = nullptr;
-  if (hipMalloc(&stage, 8ull * (n_ranks + 1) * (2 * n_ranks + 3)) != hipSuccess) return CRDT_EHIP;
+  if (hipMalloc(&stage, 8ull * stage_words(n_ranks)) != hipSuccess) return CRDT_EHIP;
   ncclComm_t comm = nullptr;
   if (ncclCommInitRank(&comm, n_ranks, id, rank) != ncclSuccess) {
     (void)hipFree(stage);
@@ -455,6 +549,11 @@ int crdt_comm_destroy(crdt_ctx* ctx) {
   ctx->comm = nullptr;
   ctx->n_ranks = 0;
   return r == ncclSuccess ? CRDT_OK : CRDT_ECOMM;
+}
+
+int crdt_comm_count(crdt_ctx* ctx, int* h_count) {
+  if (!ctx || !ctx->comm || !h_count) return CRDT_EINVAL;
+  return nccl_rc(ncclCommCount((ncclComm_t)ctx->comm, h_count));
 }
 
 int crdt_replica_allreduce_max(crdt_ctx* ctx, uint64_t* d_rows, size_t n_words, void* stream) {
@@ -504,6 +603,22 @@ int crdt_orswot_replica_join(crdt_ctx* ctx, const crdt_orswot_batch* mine, uint3
   int rc = set_dev(ctx);
   if (rc) return rc;
   RcclTransport T(ctx, ctx->d_comm_stage);
+  if (h_out_used) *h_out_used = 0;
+  return orswot_join_rank(ctx, T, mine, n_actors, flags, d_out, d_out_off, out_bytes, h_out_used, S(stream));
+}
+
+int crdt_orswot_replica_join_transport(crdt_ctx* ctx, const crdt_transport* transport,
+                                       const crdt_orswot_batch* mine, uint32_t n_actors, uint32_t flags,
+                                       uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes, size_t* h_out_used,
+                                       void* stream) {
+  if (!ctx || !transport || !transport->allgather || !transport->exchange || transport->n_ranks < 1 ||
+      transport->rank < 0 || transport->rank >= transport->n_ranks || !mine || n_actors == 0 ||
+      (flags & ~CRDT_ORSWOT_SPARSE_CLOCK))
+    return CRDT_EINVAL;
+  if (mine->n_obj && (!d_out || !d_out_off || ((uintptr_t)d_out & 15u))) return CRDT_EINVAL;
+  int rc = set_dev(ctx);
+  if (rc) return rc;
+  CallbackTransport T(transport);
   if (h_out_used) *h_out_used = 0;
   return orswot_join_rank(ctx, T, mine, n_actors, flags, d_out, d_out_off, out_bytes, h_out_used, S(stream));
 }

@@ -1,0 +1,141 @@
+"""GPU, one process per rank: the PRODUCT's owner-sharded Orswot replica join
+(C++ `orswot_join_rank`, rust-crdt_amd/csrc/replica.hip) with ranks as real
+processes, world 1-3, all on the test box's one MI355X.
+
+RCCL cannot put two ranks on one GPU, so the ranks talk through
+crdt_orswot_replica_join_transport with a gloo transport (crdts_hip.replica.
+GlooTransport: host-staged all-gathers and point-to-point transfers). Every
+line of the join above the transport — slice bounds, the symmetric verdicts,
+the arena plan, the rank-order fold with the batched merge kernel, compaction,
+the result exchange and rebase — is the code crdt_orswot_replica_join runs
+over RCCL. Checked: every rank ends with the oracle's rank-order fold
+((r0 ⊔ r1) ⊔ r2) (src/orswot.rs:87-157, order fixed by :98-103 vs :132-138)
+byte for byte; a non-canonical record in the middle of a slice makes EVERY
+rank return the same error (none left in a collective), and the next join on
+the same contexts succeeds.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import records
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_fold(oracle_ffi, reps, A, flags=0):
+    acc = reps[0]
+    for b, o in reps[1:]:
+        acc = oracle_ffi.orswot_merge_batch(acc[0], acc[1], b, o, A, threads=4, flags=flags)
+    return records.unpack_batch(*acc)
+
+
+def _worker(rank, world, port, q):
+    import sys
+
+    for p in (os.path.join(REPO, "rust-crdt_amd"), os.path.join(REPO, "tests"), os.path.join(REPO, "oracle")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import crdts_hip
+    import oracle_ffi
+    from crdts_hip import replica
+
+    eng = crdts_hip.Engine(0)
+    T = replica.GlooTransport()
+    res = {"rank": rank}
+
+    # 1. dense records (config-3 shape), one distinct replica per rank
+    reps = [crdts_hip.generate_orswot(4_000, threads=4, seed=140 + r)[r % 2] for r in range(world)]
+    B = crdts_hip.OrswotBatch.from_host(*reps[rank], 16)
+    out = eng.orswot_replica_join_transport(B, T)
+    res["dense_ok"] = out.records() == _oracle_fold(oracle_ffi, reps, 16)
+    res["dense_digest"] = replica.digest(out)
+
+    # 2. CSR records, config-5 shape (replica r of the same objects on rank r)
+    U, SP = crdts_hip.CONFIG5["universe"], crdts_hip.SPARSE_CLOCK
+    sreps = crdts_hip.generate_replicas(3_000, world, threads=4)
+    SB = crdts_hip.OrswotBatch.from_host(*sreps[rank], U, flags=SP)
+    sout = eng.orswot_replica_join_transport(SB, T)
+    res["sparse_ok"] = sout.records() == _oracle_fold(oracle_ffi, sreps, U, SP)
+    res["sparse_digest"] = replica.digest(sout)
+
+    # 3. a non-canonical record (n_clk != n_actors) in the MIDDLE of the last
+    #    rank's slice of range 0: every rank must return the same error
+    bad_b, bad_o = reps[rank][0].copy(), reps[rank][1]
+    if rank == world - 1:
+        i = len(bad_o) // (2 * world)
+        o = int(bad_o[i])
+        bad_b[o + 4:o + 8] = np.frombuffer(np.uint32(17).tobytes(), np.uint8)
+    try:
+        eng.orswot_replica_join_transport(crdts_hip.OrswotBatch.from_host(bad_b, bad_o, 16), T)
+        res["bad_code"] = 0
+    except crdts_hip.CrdtError as e:
+        res["bad_code"] = e.code
+    # 4. the contexts are clean afterwards: the good join again
+    out2 = eng.orswot_replica_join_transport(B, T)
+    res["after_ok"] = replica.digest(out2) == res["dense_digest"]
+    eng.status()  # nothing left latched
+    res["calls"] = dict(T.calls)
+    q.put(res)
+    dist.destroy_process_group()
+
+
+def _guarded(rank, world, port, q):
+    try:
+        _worker(rank, world, port, q)
+    except BaseException:  # report instead of leaving the peers blocked in a collective
+        import traceback
+
+        q.put({"error": traceback.format_exc(), "rank": rank})
+        raise
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_product_join_across_processes(world):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_guarded, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = []
+    try:
+        for _ in range(world):
+            item = q.get(timeout=150)
+            if "error" in item:
+                raise AssertionError(f"rank {item['rank']} failed:\n{item['error']}")
+            res.append(item)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
+    res.sort(key=lambda r: r["rank"])
+    for r in res:
+        assert r["dense_ok"], f"rank {r['rank']}: dense join differs from the oracle's rank-order fold"
+        assert r["sparse_ok"], f"rank {r['rank']}: CSR join differs from the oracle's rank-order fold"
+        assert r["bad_code"] != 0, f"rank {r['rank']}: a non-canonical record was accepted"
+        assert r["after_ok"], f"rank {r['rank']}: the join after a failed one differs"
+    assert len({r["dense_digest"] for r in res}) == 1
+    assert len({r["sparse_digest"] for r in res}) == 1
+    assert len({r["bad_code"] for r in res}) == 1, [r["bad_code"] for r in res]
+    for r in res:  # 2 exchanges per completed join; the failed one stops after the first
+        assert r["calls"]["exchange"] == 2 + 2 + 1 + 2, r["calls"]
