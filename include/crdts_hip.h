@@ -88,6 +88,12 @@ int crdt_gcounter_merge(crdt_ctx* ctx, uint64_t* d_self, const uint64_t* d_other
 int crdt_pncounter_merge(crdt_ctx* ctx, uint64_t* d_self, const uint64_t* d_other,
                          size_t n_obj, uint32_t n_actors, void* stream);
 
+/* The same with HOST rows (H2D, merge, D2H, synchronous): the PCIe-inclusive
+ * path of a host `merge_batch(&mut [T], &[T])` for VClock / GCounter
+ * (n_slots = n_actors) and PNCounter (n_slots = 2 * n_actors, [P|N] rows). */
+int crdt_dense_merge_host(crdt_ctx* ctx, uint64_t* h_self, const uint64_t* h_other, size_t n_obj,
+                          uint32_t n_slots);
+
 /* ------------------------------------------------------------------------ *
  * Orswot canonical record (one object = one contiguous, self-describing
  * record; a batch = a byte buffer + a u64 byte offset per object).

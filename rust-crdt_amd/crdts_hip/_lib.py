@@ -70,6 +70,7 @@ EXPORTS = [
     "crdt_replica_reduce_scatter_max",
     "crdt_orswot_replica_join_bound", "crdt_orswot_replica_join", "crdt_orswot_replica_join_local",
     "crdt_comm_count", "crdt_orswot_replica_join_transport", "crdt_orswot_generate_replicas_subset",
+    "crdt_dense_merge_host",
 ]
 
 CRDT_COMM_ID_BYTES = 128
@@ -186,6 +187,7 @@ def _load():
         "crdt_orswot_replica_join": (I, [P, BP, U32, U32, P, P, SZ, C.POINTER(SZ), P]),
         "crdt_orswot_replica_join_local": (I, [P, BP, U32, U32, U32, P, P, SZ, C.POINTER(SZ), P]),
         "crdt_comm_count": (I, [P, C.POINTER(I)]),
+        "crdt_dense_merge_host": (I, [P, P, P, SZ, U32]),
         "crdt_orswot_generate_replicas_subset": (I, [U64, SZ, SZ, C.POINTER(RepParams), U32, U32, U32, U32, I,
                                                      C.POINTER(P)]),
         "crdt_orswot_replica_join_transport": (I, [P, C.POINTER(TransportC), BP, U32, U32, P, P, SZ, C.POINTER(SZ),

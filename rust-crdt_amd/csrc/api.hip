@@ -149,6 +149,27 @@ int crdt_pncounter_merge(crdt_ctx* ctx, uint64_t* d_self, const uint64_t* d_othe
   return dense(ctx, d_self, d_other, n_obj, 2ull * n_actors, stream);
 }
 
+int crdt_dense_merge_host(crdt_ctx* ctx, uint64_t* h_self, const uint64_t* h_other, size_t n_obj, uint32_t n_slots) {
+  if (!ctx || n_slots == 0 || (n_obj && (!h_self || !h_other))) return CRDT_EINVAL;
+  if (n_obj == 0) return CRDT_OK;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  const size_t bytes = 8ull * n_obj * n_slots;
+  uint64_t *dS = nullptr, *dO = nullptr;
+  hipStream_t st = nullptr;
+  bool ok = hipStreamCreate(&st) == hipSuccess && hipMalloc(&dS, bytes) == hipSuccess &&
+            hipMalloc(&dO, bytes) == hipSuccess &&
+            hipMemcpyAsync(dS, h_self, bytes, hipMemcpyHostToDevice, st) == hipSuccess &&
+            hipMemcpyAsync(dO, h_other, bytes, hipMemcpyHostToDevice, st) == hipSuccess;
+  if (ok) rc = launch_dense_max(dS, dO, (uint64_t)n_obj * n_slots, st);
+  ok = ok && rc == CRDT_OK && hipMemcpyAsync(h_self, dS, bytes, hipMemcpyDeviceToHost, st) == hipSuccess &&
+       hipStreamSynchronize(st) == hipSuccess;
+  (void)hipFree(dS);
+  (void)hipFree(dO);
+  if (st) (void)hipStreamDestroy(st);
+  return ok ? CRDT_OK : (rc ? rc : CRDT_EHIP);
+}
+
 int crdt_orswot_merge(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_orswot_batch* other,
                       uint8_t* d_out_base, uint64_t* d_out_off, size_t out_bytes, uint32_t n_actors,
                       void* stream) {

@@ -101,3 +101,23 @@ def test_gcounter_config2_chunk_properties(gpu):
     gpu.dense_merge(da, da.clone(), 64, "gcounter")  # idempotent
     gpu.status()
     assert (_host(db2) == r).all() and (_host(da) == r).all()
+
+
+@pytest.mark.parametrize("slots", [16, 128])
+def test_dense_merge_host_entry_point(gpu, oracle, slots):
+    """crdt_dense_merge_host (host rows: H2D, dense_max_kernel, D2H) — the
+    entry point INTEGRATION.md's MergeBatch for VClock / GCounter / PNCounter
+    calls — equals the oracle's VClock::merge per row (src/vclock.rs:131-137)."""
+    import ctypes as C
+
+    import crdts_hip
+    from crdts_hip._lib import check, lib
+
+    a = crdts_hip.generate_dense(3001, slots, seed=91)
+    b = crdts_hip.generate_dense(3001, slots, seed=92)
+    a[:5] = np.uint64((1 << 64) - 1)  # u64 values above 2^63 stay exact
+    exp = oracle.dense_merge(a, b, slots)
+    got = np.ascontiguousarray(a.copy())
+    check(lib.crdt_dense_merge_host(gpu.ctx, got.ctypes.data_as(C.c_void_p), b.ctypes.data_as(C.c_void_p),
+                                    got.shape[0], slots), "dense_merge_host")
+    assert (got == exp).all()
