@@ -44,7 +44,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="orswot",
                    choices=["orswot", "vclock", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply",
-                            "mvreg", "map", "map_orswot", "spawn_check"])
+                            "mvreg", "map", "map_orswot", "clock_csr", "spawn_check"])
     p.add_argument("--replicas", type=int, default=8, help="orswot_csr at N=1: replicas folded locally")
     p.add_argument("--n-obj", type=int, default=None, help="objects per GPU")
     p.add_argument("--threads", type=int, default=16, help="host threads for input generation")
@@ -742,6 +742,99 @@ def run_gcounter_ae(args, rank, world, local, eng=None):
     return res
 
 
+def run_clock_csr(args, rank, world, local):
+    """Sparse (CSR) VClock / GCounter merge (SURVEY.md §8(a) A2 / A6 over a
+    large actor universe; VClock::merge src/vclock.rs:131-137): 10M clock pairs
+    per GPU over a 1024-actor universe, ~48 actors per clock (one per band of
+    18 ids, present with p = 6/7), the other side sharing 75 % of the actors,
+    counters U[1, 2^40). A step = one crdt_vclock_csr_merge launch over the
+    batch (inputs resident in HBM); spot parity against the oracle first."""
+    import numpy as np
+    import torch
+
+    import crdts_hip
+
+    n = args.n_obj or 10_000_000
+    slots, universe = 56, 1024
+    band = universe // slots
+    dev = f"cuda:{local}"
+    g = torch.Generator(device=dev)
+    g.manual_seed(0xC0FFEE09 + rank)
+    js = torch.randint(0, band, (n, slots), dtype=torch.int32, device=dev, generator=g)
+    jo = torch.where(torch.rand((n, slots), device=dev, generator=g) < 0.75, js,
+                     torch.randint(0, band, (n, slots), dtype=torch.int32, device=dev, generator=g))
+    base = torch.arange(slots, dtype=torch.int32, device=dev)[None, :] * band
+    sides = []
+    for j in (js, jo):
+        present = torch.rand((n, slots), device=dev, generator=g) < 6 / 7
+        act = (base + j)[present].contiguous()
+        ln = present.sum(1, dtype=torch.int32)
+        off = torch.cumsum(ln, 0, dtype=torch.int64) - ln
+        ctr = torch.randint(1, 1 << 40, (act.numel(),), dtype=torch.int64, device=dev, generator=g)
+        sides.append(crdts_hip.ClockBatch(off, ln, act, ctr))
+        del present
+    del js, jo
+    S, O = sides
+    eng = crdts_hip.Engine(local)
+    stream = torch.cuda.Stream(device=local)
+    out = eng.clock_csr_merge(S, O, stream=stream)  # checked launch
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_ffi
+
+    m = 2000  # spot parity (the first m objects, re-based)
+    def head(B):
+        o = B.off[:m].cpu().numpy().view(np.uint64)
+        ln = B.len[:m].cpu().numpy().view(np.uint32)
+        e = int(o[-1]) + int(ln[-1])
+        return o, ln, B.act[:e].cpu().numpy().view(np.uint32), B.ctr[:e].cpu().numpy().view(np.uint64)
+    eo, el, ea, ec = oracle_ffi.vclock_csr_merge(head(S), head(O))
+    go, gl, ga, gc = out.off[:m].cpu().numpy().view(np.uint64), out.len[:m].cpu().numpy().view(np.uint32), None, None
+    assert (go == eo).all() and (gl == el).all(), "clock_csr spot parity: placement / lengths"
+    hact = out.act[: int(eo[-1]) + int(el[-1])].cpu().numpy().view(np.uint32)
+    hctr = out.ctr[: int(eo[-1]) + int(el[-1])].cpu().numpy().view(np.uint64)
+    for o_, l_ in zip(eo.tolist(), el.tolist()):
+        assert (hact[o_:o_ + l_] == ea[o_:o_ + l_]).all() and (hctr[o_:o_ + l_] == ec[o_:o_ + l_]).all()
+
+    def step():
+        eng.clock_csr_merge(S, O, out=out, stream=stream, check_status=False)
+
+    wall, ev_ms = _timed_steps(args, world, stream, step)
+    eng.status(stream)
+    nnz_s, nnz_o = S.n_entries, O.n_entries
+    nnz_u = int(out.len.sum(dtype=torch.int64).item())
+    alg = 12 * (nnz_s + nnz_o + nnz_u) + 3 * 12 * n  # entries read / written + (off, len) per object and side
+    ach = alg / (ev_ms * 1e-3) / 1e9
+    total = sum_over_ranks(float(n * args.steps), world)
+    res = {
+        "metric": "sparse (CSR) VClock merges/sec (node), 1024-actor universe",
+        "value": total / wall, "unit": "merges/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u64", "data": "synthetic: ~48 of 1024 actors per clock, 75 % shared across the pair, U[1,2^40)",
+        "config": {"workload": f"clock_csr: {n} CSR clock pairs per GPU, universe {universe}, "
+                               f"{nnz_s / n:.1f} + {nnz_o / n:.1f} -> {nnz_u / n:.1f} entries",
+                   "parallelism": f"dp{world} (objects sharded)"},
+    }
+    if world == 1:
+        res["roofline"] = {"bound": "hbm", "kernel": "clock_csr_merge_kernel", "achieved": ach, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "kernel_ms": ev_ms, "alg_bytes_per_launch": alg,
+                           "traffic": wl_traffic(args, "clock_csr", "clock_csr_merge_kernel")}
+        if not args.no_cpu_baseline:
+            mm = min(args.cpu_sample, n)
+            th = cpu_threads(args)
+
+            def headm(B):
+                o = B.off[:mm].cpu().numpy().view(np.uint64)
+                ln = B.len[:mm].cpu().numpy().view(np.uint32)
+                e = int(o[-1]) + int(ln[-1])
+                return o, ln, B.act[:e].cpu().numpy().view(np.uint32), B.ctr[:e].cpu().numpy().view(np.uint64)
+            secs = oracle_ffi.vclock_csr_bench(headm(S), headm(O), th)
+            res["cpu_baseline"] = {"value": mm / secs, "unit": "merges/s", "cores": th, "kind": "port",
+                                   **cpu_cores_note(),
+                                   "sample": f"first {mm} clock pairs, VClock::merge over std::map (decode untimed), "
+                                             f"{th} threads"}
+    return res
+
+
 def run_spawn_check(args, rank, world, local):
     """CPU only (gloo): what the launch path gives each rank — its rank, the
     world size, LOCAL_RANK (the GPU it would bind) and its pid — all-gathered."""
@@ -1244,6 +1337,8 @@ def main():
         res = run_map(args, rank, world, local)
     elif args.workload == "map_orswot":
         res = run_map_orswot(args, rank, world, local)
+    elif args.workload == "clock_csr":
+        res = run_clock_csr(args, rank, world, local)
     else:
         res = run_dense(args, rank, world, local, args.workload)
     failed = [k for k, v in res.get("anti_entropy", {}).items() if not (v.get("check") or {}).get("ok", True)]

@@ -95,6 +95,54 @@ int crdt_dense_merge_host(crdt_ctx* ctx, uint64_t* h_self, const uint64_t* h_oth
                           uint32_t n_slots);
 
 /* ------------------------------------------------------------------------ *
+ * Sparse (CSR) clocks and counters, for actor universes too large for dense
+ * rows (a 1024-actor universe with ~48 actors per
+ * clock is 8 KB dense and ~0.6 KB here). The reference clock is a
+ * BTreeMap<A, u64> (src/vclock.rs:54-57): here object i's clock is the run
+ * of entries [off[i], off[i] + len[i]) of act / ctr — actors strictly
+ * increasing (BTreeMap order of the interned ids), counters > 0 (`witness`
+ * never stores 0, :159-163). A batch may have gaps between runs.
+ *
+ * out[i] := self[i].merge(&other[i]): the sorted union of the two runs with
+ * the larger counter per actor — VClock::merge src/vclock.rs:131-137;
+ * GCounter::merge src/gcounter.rs:58-62; PNCounter::merge
+ * src/pncounter.rs:90-95 (its P and N clocks are two batches). The call
+ * writes out.off[i] := self.off[i] + other.off[i] and out.len[i] := the
+ * union's length (<= self.len[i] + other.len[i]), and the entries there, so
+ * out.n_entries >= self.n_entries + other.n_entries suffices and the output
+ * is itself a valid (gapped) input batch.
+ * PRECONDITION (checked on the device; a violation latches CRDT_EINVAL and
+ * the object's out.len is 0): on each side runs lie inside [0, n_entries)
+ * at increasing, non-overlapping offsets (off[i] + len[i] <= off[i+1]). A
+ * run that is not canonical (actors not strictly increasing, a zero counter)
+ * latches CRDT_ENONCANON (out.len 0). Runs of any length (<= 64 entries per
+ * side take the loop-free path).
+ * ------------------------------------------------------------------------ */
+typedef struct crdt_clock_csr {
+  const uint64_t* off;   /* device, n_obj: first entry of object i's run */
+  const uint32_t* len;   /* device, n_obj: entries of the run            */
+  const uint32_t* act;   /* device, n_entries: interned actor ids          */
+  const uint64_t* ctr;   /* device, n_entries: counters                    */
+  size_t n_obj;
+  size_t n_entries;      /* extent of act / ctr (bounds checks)            */
+} crdt_clock_csr;
+typedef struct crdt_clock_csr_out {
+  uint64_t* off;         /* device, n_obj (written)                        */
+  uint32_t* len;         /* device, n_obj (written)                        */
+  uint32_t* act;         /* device, n_entries                              */
+  uint64_t* ctr;         /* device, n_entries                              */
+  size_t n_entries;
+} crdt_clock_csr_out;
+int crdt_vclock_csr_merge(crdt_ctx* ctx, const crdt_clock_csr* self, const crdt_clock_csr* other,
+                          const crdt_clock_csr_out* out, void* stream);
+int crdt_gcounter_csr_merge(crdt_ctx* ctx, const crdt_clock_csr* self, const crdt_clock_csr* other,
+                            const crdt_clock_csr_out* out, void* stream);
+/* PNCounter: its P and N clocks as two batches of the same n_obj (one call). */
+int crdt_pncounter_csr_merge(crdt_ctx* ctx, const crdt_clock_csr* self_p, const crdt_clock_csr* self_n,
+                             const crdt_clock_csr* other_p, const crdt_clock_csr* other_n,
+                             const crdt_clock_csr_out* out_p, const crdt_clock_csr_out* out_n, void* stream);
+
+/* ------------------------------------------------------------------------ *
  * Orswot canonical record (one object = one contiguous, self-describing
  * record; a batch = a byte buffer + a u64 byte offset per object).
  *

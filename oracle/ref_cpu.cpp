@@ -839,6 +839,65 @@ int orc_pncounter_merge(uint64_t* self, const uint64_t* other, size_t n, uint32_
   });
   return 0;
 }
+// Sparse (CSR) clocks: object i's clock is the run [off[i], off[i] + len[i])
+// of (act, ctr) pairs (include/crdts_hip.h "Sparse (CSR) clocks"); merged by
+// VClock::merge over std::map (src/vclock.rs:131-137), the result written at
+// s_off[i] + o_off[i] (entries), out_len[i] = its length. A run that is not a
+// canonical BTreeMap image (actors not strictly increasing, a zero counter)
+// returns -2 with *bad = the object.
+static bool run_to_vclock(const uint32_t* a, const uint64_t* c, uint64_t n, VClock& v) {
+  for (uint64_t k = 0; k < n; ++k) {
+    if (c[k] == 0 || (k && a[k - 1] >= a[k])) return false;
+    v.dots.emplace_hint(v.dots.end(), a[k], c[k]);  // From<Vec<(A, u64)>>: witness each
+  }
+  return true;
+}
+int orc_vclock_csr_merge(const uint64_t* s_off, const uint32_t* s_len, const uint32_t* s_act,
+                         const uint64_t* s_ctr, const uint64_t* o_off, const uint32_t* o_len,
+                         const uint32_t* o_act, const uint64_t* o_ctr, size_t n, uint32_t* out_act,
+                         uint64_t* out_ctr, uint32_t* out_len, int threads, int64_t* bad) {
+  std::atomic<int64_t> first_bad{-1};
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) {
+      VClock a, o;
+      if (!run_to_vclock(s_act + s_off[i], s_ctr + s_off[i], s_len[i], a) ||
+          !run_to_vclock(o_act + o_off[i], o_ctr + o_off[i], o_len[i], o)) {
+        int64_t exp = -1;
+        first_bad.compare_exchange_strong(exp, (int64_t)i);
+        out_len[i] = 0;
+        continue;
+      }
+      a.merge(o);
+      uint64_t at = s_off[i] + o_off[i];
+      for (const auto& kv : a.dots) {
+        out_act[at] = kv.first;
+        out_ctr[at++] = kv.second;
+      }
+      out_len[i] = (uint32_t)a.dots.size();
+    }
+  });
+  if (bad) *bad = first_bad.load();
+  return first_bad.load() >= 0 ? -2 : 0;
+}
+// The CPU baseline of the CSR workload: the runs decoded into std::map
+// VClocks beforehand (untimed), VClock::merge timed.
+double orc_vclock_csr_bench(const uint64_t* s_off, const uint32_t* s_len, const uint32_t* s_act,
+                            const uint64_t* s_ctr, const uint64_t* o_off, const uint32_t* o_len,
+                            const uint32_t* o_act, const uint64_t* o_ctr, size_t n, int threads) {
+  std::vector<VClock> A(n), B(n);
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) {
+      run_to_vclock(s_act + s_off[i], s_ctr + s_off[i], s_len[i], A[i]);
+      run_to_vclock(o_act + o_off[i], o_ctr + o_off[i], o_len[i], B[i]);
+    }
+  });
+  auto t0 = std::chrono::steady_clock::now();
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) A[i].merge(B[i]);
+  });
+  auto t1 = std::chrono::steady_clock::now();
+  return std::chrono::duration<double>(t1 - t0).count();
+}
 double orc_dense_bench(const uint64_t* self, const uint64_t* other, size_t n, uint32_t n_actors,
                        int threads) {
   std::vector<GCounter> A(n), B(n);

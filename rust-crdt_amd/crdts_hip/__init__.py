@@ -24,7 +24,8 @@ from .record import decode_record, encode_record, record_bytes
 __all__ = [
     "Engine", "OrswotBatch", "GenParams", "CrdtError", "generate_orswot", "generate_dense", "HostOrswot",
     "Orswot", "VClock", "GCounter", "PNCounter", "merge_batch", "decode_record", "encode_record",
-    "record_bytes", "CONFIG3", "EXPORTS", "LIB_PATH", "CONFIG5", "SPARSE_CLOCK", "generate_replicas",
+    "record_bytes", "CONFIG3", "EXPORTS", "LIB_PATH", "CONFIG5", "SPARSE_CLOCK", "generate_replicas", "ClockBatch",
+    "generate_clocks_csr",
 ]
 
 # SURVEY.md §8(d) config 3 / BASELINE.json configs[2].
@@ -49,6 +50,56 @@ def _torch():
     import torch
 
     return torch
+
+
+class ClockBatch:
+    """A batch of sparse (CSR) clocks (include/crdts_hip.h crdt_clock_csr):
+    object i's clock is entries [off[i], off[i] + len[i]) of (act, ctr) —
+    actors strictly increasing, counters > 0. Tensors: off int64, len int32,
+    act int32, ctr int64 (u64 bits); host numpy or device torch."""
+
+    def __init__(self, off, len_, act, ctr, n_entries=None):
+        self.off, self.len, self.act, self.ctr = off, len_, act, ctr
+        self.n_obj = int(off.shape[0])
+        self.n_entries = int(act.shape[0]) if n_entries is None else int(n_entries)
+
+    @classmethod
+    def from_host(cls, off, len_, act, ctr, device=0):
+        torch = _torch()
+        dev = f"cuda:{device}"
+
+        def t(x, dt, ndt):
+            x = np.ascontiguousarray(x, dtype=ndt)
+            return torch.from_numpy(x.view(dt) if x.size else np.zeros(1, dt)).to(dev)
+
+        return cls(t(off, np.int64, np.uint64)[: len(off)], t(len_, np.int32, np.uint32)[: len(len_)],
+                   t(act, np.int32, np.uint32), t(ctr, np.int64, np.uint64), n_entries=len(act))
+
+    @classmethod
+    def from_lists(cls, clocks, device=0):
+        """clocks: list of {actor: counter} dicts (or sorted (actor, counter) lists)."""
+        runs = [sorted(dict(c).items()) for c in clocks]
+        lens = np.array([len(r) for r in runs], np.uint32)
+        off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64) if len(runs) else np.zeros(0, np.uint64)
+        act = np.array([a for r in runs for a, _ in r], np.uint32)
+        ctr = np.array([c for r in runs for _, c in r], np.uint64)
+        return cls.from_host(off, lens, act, ctr, device)
+
+    def cstruct(self):
+        from ._lib import ClockCsr
+
+        return ClockCsr(self.off.data_ptr(), self.len.data_ptr(), self.act.data_ptr(), self.ctr.data_ptr(),
+                        self.n_obj, self.n_entries)
+
+    def to_host(self):
+        return (self.off.cpu().numpy().view(np.uint64), self.len.cpu().numpy().view(np.uint32),
+                self.act[: self.n_entries].cpu().numpy().view(np.uint32),
+                self.ctr[: self.n_entries].cpu().numpy().view(np.uint64))
+
+    def clocks(self):
+        """Host list of sorted (actor, counter) lists, one per object."""
+        off, ln, act, ctr = self.to_host()
+        return [list(zip(act[o:o + n].tolist(), ctr[o:o + n].tolist())) for o, n in zip(off.tolist(), ln.tolist())]
 
 
 class OrswotBatch:
@@ -604,6 +655,47 @@ class Engine:
             self.status(stream)
         return out, off, lens
 
+    # ------------------------------------------------ sparse (CSR) clocks
+    def clock_csr_alloc_out(self, S: "ClockBatch", O: "ClockBatch"):
+        torch = _torch()
+        dev = f"cuda:{self.device}"
+        cap = max(1, S.n_entries + O.n_entries)
+        return ClockBatch(torch.empty(S.n_obj, dtype=torch.int64, device=dev),
+                          torch.empty(S.n_obj, dtype=torch.int32, device=dev),
+                          torch.empty(cap, dtype=torch.int32, device=dev),
+                          torch.empty(cap, dtype=torch.int64, device=dev), n_entries=cap)
+
+    def clock_csr_merge(self, S: "ClockBatch", O: "ClockBatch", out: "ClockBatch | None" = None, kind="vclock",
+                        stream=None, check_status=True):
+        """out[i] = S[i].merge(&O[i]) over sparse clocks (VClock::merge
+        src/vclock.rs:131-137; GCounter src/gcounter.rs:58-62): the sorted union,
+        counters max'ed, placed at S.off + O.off (crdt_vclock_csr_merge)."""
+        from ._lib import ClockCsrOut
+
+        out = out or self.clock_csr_alloc_out(S, O)
+        s, o = S.cstruct(), O.cstruct()
+        w = ClockCsrOut(out.off.data_ptr(), out.len.data_ptr(), out.act.data_ptr(), out.ctr.data_ptr(), out.n_entries)
+        fn = {"vclock": lib.crdt_vclock_csr_merge, "gcounter": lib.crdt_gcounter_csr_merge}[kind]
+        check(fn(self.ctx, C.byref(s), C.byref(o), C.byref(w), self._stream(stream)), f"{kind}_csr_merge")
+        if check_status:
+            self.status(stream)
+        return out
+
+    def pncounter_csr_merge(self, SP, SN, OP, ON, outs=None, stream=None, check_status=True):
+        """PNCounter::merge (src/pncounter.rs:90-95) over sparse P and N clocks
+        (crdt_pncounter_csr_merge); returns (out_p, out_n)."""
+        from ._lib import ClockCsrOut
+
+        op, on = outs or (self.clock_csr_alloc_out(SP, OP), self.clock_csr_alloc_out(SN, ON))
+        w = [ClockCsrOut(x.off.data_ptr(), x.len.data_ptr(), x.act.data_ptr(), x.ctr.data_ptr(), x.n_entries)
+             for x in (op, on)]
+        c = [x.cstruct() for x in (SP, SN, OP, ON)]
+        check(lib.crdt_pncounter_csr_merge(self.ctx, *[C.byref(x) for x in c], C.byref(w[0]), C.byref(w[1]),
+                                           self._stream(stream)), "pncounter_csr_merge")
+        if check_status:
+            self.status(stream)
+        return op, on
+
     def dense_merge(self, self_rows, other_rows, n_actors, kind="gcounter", stream=None):
         """In place: self_rows = max(self_rows, other_rows) (src/vclock.rs:131-137).
 
@@ -679,6 +771,31 @@ def generate_replicas(n_obj, n_replicas=8, first_obj=0, seed=CONFIG5_SEED, param
         return _copy_sides(g, count, n_obj)
     finally:
         lib.crdt_orswot_gen_free(g)
+
+
+def generate_clocks_csr(n_obj, seed, universe=1024, slots=56, p_present=6 / 7, overlap=0.75, bits=40):
+    """A pair of sparse clock batches (host numpy CSR: off u64, len u32, act
+    u32, ctr u64) over an actor universe of `universe` ids: each clock draws
+    from `slots` evenly spaced actor bands (one actor per band), each present
+    with p_present (~48 of 56 by default); the other side picks the same actor
+    in a band with probability `overlap` (replicas of one clock share most
+    actors), counters U[1, 2^bits)."""
+    rng = np.random.default_rng(seed)
+    band = universe // slots
+    js = rng.integers(0, band, (n_obj, slots), dtype=np.uint32)
+    jo = np.where(rng.random((n_obj, slots)) < overlap, js, rng.integers(0, band, (n_obj, slots), dtype=np.uint32))
+    base = (np.arange(slots, dtype=np.uint32) * band)[None, :]
+    out = []
+    for j in (js, jo):
+        present = rng.random((n_obj, slots)) < p_present
+        act = (base + j)[present].astype(np.uint32)
+        ctr = rng.integers(1, 1 << bits, act.size, dtype=np.uint64)
+        ln = present.sum(1).astype(np.uint32)
+        off = np.zeros(n_obj, np.uint64)
+        if n_obj:
+            off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+        out.append((off, ln, act, ctr))
+    return out[0], out[1]
 
 
 def generate_dense(n_obj, n_actors, seed, first_obj=0, bits=40, pct_zero=25, threads=8):

@@ -70,7 +70,7 @@ EXPORTS = [
     "crdt_replica_reduce_scatter_max",
     "crdt_orswot_replica_join_bound", "crdt_orswot_replica_join", "crdt_orswot_replica_join_local",
     "crdt_comm_count", "crdt_orswot_replica_join_transport", "crdt_orswot_generate_replicas_subset",
-    "crdt_dense_merge_host",
+    "crdt_dense_merge_host", "crdt_vclock_csr_merge", "crdt_gcounter_csr_merge", "crdt_pncounter_csr_merge",
 ]
 
 CRDT_COMM_ID_BYTES = 128
@@ -98,6 +98,18 @@ MAP_ORSWOT_CAPS = ("kcap", "mcap", "vdcap", "vscap", "dcap", "scap")
 class MapOrswotSlabC(C.Structure):
     """crdt_map_orswot_slab (include/crdts_hip.h)."""
     _fields_ = [(f, C.c_void_p) for f in MAP_ORSWOT_FIELDS] + [(f, C.c_uint32) for f in MAP_ORSWOT_CAPS]
+
+
+class ClockCsr(C.Structure):
+    """crdt_clock_csr (include/crdts_hip.h)."""
+    _fields_ = [("off", C.c_void_p), ("len", C.c_void_p), ("act", C.c_void_p), ("ctr", C.c_void_p),
+                ("n_obj", C.c_size_t), ("n_entries", C.c_size_t)]
+
+
+class ClockCsrOut(C.Structure):
+    """crdt_clock_csr_out (include/crdts_hip.h)."""
+    _fields_ = [("off", C.c_void_p), ("len", C.c_void_p), ("act", C.c_void_p), ("ctr", C.c_void_p),
+                ("n_entries", C.c_size_t)]
 
 
 class Xfer(C.Structure):
@@ -188,6 +200,9 @@ def _load():
         "crdt_orswot_replica_join_local": (I, [P, BP, U32, U32, U32, P, P, SZ, C.POINTER(SZ), P]),
         "crdt_comm_count": (I, [P, C.POINTER(I)]),
         "crdt_dense_merge_host": (I, [P, P, P, SZ, U32]),
+        "crdt_vclock_csr_merge": (I, [P, C.POINTER(ClockCsr), C.POINTER(ClockCsr), C.POINTER(ClockCsrOut), P]),
+        "crdt_gcounter_csr_merge": (I, [P, C.POINTER(ClockCsr), C.POINTER(ClockCsr), C.POINTER(ClockCsrOut), P]),
+        "crdt_pncounter_csr_merge": (I, [P] + [C.POINTER(ClockCsr)] * 4 + [C.POINTER(ClockCsrOut)] * 2 + [P]),
         "crdt_orswot_generate_replicas_subset": (I, [U64, SZ, SZ, C.POINTER(RepParams), U32, U32, U32, U32, I,
                                                      C.POINTER(P)]),
         "crdt_orswot_replica_join_transport": (I, [P, C.POINTER(TransportC), BP, U32, U32, P, P, SZ, C.POINTER(SZ),

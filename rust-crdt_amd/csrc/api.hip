@@ -149,6 +149,41 @@ int crdt_pncounter_merge(crdt_ctx* ctx, uint64_t* d_self, const uint64_t* d_othe
   return dense(ctx, d_self, d_other, n_obj, 2ull * n_actors, stream);
 }
 
+namespace {
+int csr_args_ok(const crdt_clock_csr* s, const crdt_clock_csr* o, const crdt_clock_csr_out* out) {
+  if (!s || !o || !out || s->n_obj != o->n_obj) return CRDT_EINVAL;
+  if (s->n_obj && (!s->off || !s->len || !o->off || !o->len || !out->off || !out->len)) return CRDT_EINVAL;
+  if (s->n_entries && (!s->act || !s->ctr)) return CRDT_EINVAL;
+  if (o->n_entries && (!o->act || !o->ctr)) return CRDT_EINVAL;
+  if (out->n_entries && (!out->act || !out->ctr)) return CRDT_EINVAL;
+  if (out->n_entries < s->n_entries + o->n_entries) return CRDT_ECAPACITY;
+  return CRDT_OK;
+}
+}  // namespace
+
+int crdt_vclock_csr_merge(crdt_ctx* ctx, const crdt_clock_csr* self, const crdt_clock_csr* other,
+                          const crdt_clock_csr_out* out, void* stream) {
+  if (!ctx) return CRDT_EINVAL;
+  int rc = csr_args_ok(self, other, out);
+  if (rc || (rc = set_device(ctx))) return rc;
+  return launch_clock_csr_merge(&self, &other, &out, 1, ctx->d_status, S(stream));
+}
+int crdt_gcounter_csr_merge(crdt_ctx* ctx, const crdt_clock_csr* self, const crdt_clock_csr* other,
+                            const crdt_clock_csr_out* out, void* stream) {
+  return crdt_vclock_csr_merge(ctx, self, other, out, stream);
+}
+int crdt_pncounter_csr_merge(crdt_ctx* ctx, const crdt_clock_csr* self_p, const crdt_clock_csr* self_n,
+                             const crdt_clock_csr* other_p, const crdt_clock_csr* other_n,
+                             const crdt_clock_csr_out* out_p, const crdt_clock_csr_out* out_n, void* stream) {
+  if (!ctx || !self_p || !self_n || self_p->n_obj != self_n->n_obj) return CRDT_EINVAL;
+  int rc = csr_args_ok(self_p, other_p, out_p);
+  if (rc || (rc = csr_args_ok(self_n, other_n, out_n)) || (rc = set_device(ctx))) return rc;
+  const crdt_clock_csr* s[2] = {self_p, self_n};
+  const crdt_clock_csr* o[2] = {other_p, other_n};
+  const crdt_clock_csr_out* w[2] = {out_p, out_n};
+  return launch_clock_csr_merge(s, o, w, 2, ctx->d_status, S(stream));
+}
+
 int crdt_dense_merge_host(crdt_ctx* ctx, uint64_t* h_self, const uint64_t* h_other, size_t n_obj, uint32_t n_slots) {
   if (!ctx || n_slots == 0 || (n_obj && (!h_self || !h_other))) return CRDT_EINVAL;
   if (n_obj == 0) return CRDT_OK;

@@ -18,6 +18,10 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
                                uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
                                uint32_t list_cap, hipStream_t stream, int sparse_variant);
 
+// Sparse clock joins: n_jobs (1 or 2: PNCounter's P and N) batches in one launch.
+int launch_clock_csr_merge(const crdt_clock_csr* const* self, const crdt_clock_csr* const* other,
+                           const crdt_clock_csr_out* const* out, int n_jobs, int* status, hipStream_t stream);
+
 int launch_dense_max(uint64_t* self, const uint64_t* other, uint64_t n_words, hipStream_t stream);
 
 int launch_orswot_validate(const uint8_t* base, const uint64_t* off, uint64_t bytes, uint64_t n_obj,

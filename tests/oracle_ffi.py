@@ -66,6 +66,10 @@ def lib():
     L.orc_pncounter_merge.argtypes = [P, P, C.c_size_t, C.c_uint32, C.c_int]
     L.orc_dense_bench.restype = C.c_double
     L.orc_dense_bench.argtypes = [P, P, C.c_size_t, C.c_uint32, C.c_int]
+    L.orc_vclock_csr_merge.restype = C.c_int
+    L.orc_vclock_csr_merge.argtypes = [P] * 8 + [C.c_size_t, P, P, P, C.c_int, C.POINTER(C.c_int64)]
+    L.orc_vclock_csr_bench.restype = C.c_double
+    L.orc_vclock_csr_bench.argtypes = [P] * 8 + [C.c_size_t, C.c_int]
     L.orc_obj_new.restype = P
     L.orc_obj_clone.restype = P
     L.orc_obj_clone.argtypes = [P]
@@ -321,6 +325,31 @@ def dense_merge(self_rows, other_rows, n_actors, threads=8):
     n = out.size // n_actors
     lib().orc_dense_merge(_ptr(out), _ptr(o), n, n_actors, threads)
     return out
+
+
+def vclock_csr_merge(s, o, threads=8):
+    """s, o: (off u64, len u32, act u32, ctr u64) numpy CSR batches of the same
+    n_obj. Returns (out_off, out_len, out_act, out_ctr), entries at s.off + o.off."""
+    so, sl, sa, sc = [np.ascontiguousarray(x) for x in s]
+    oo, ol, oa, oc = [np.ascontiguousarray(x) for x in o]
+    n = len(so)
+    cap = max(1, len(sa) + len(oa))
+    out_act = np.zeros(cap, np.uint32)
+    out_ctr = np.zeros(cap, np.uint64)
+    out_len = np.zeros(max(1, n), np.uint32)
+    bad = C.c_int64(-1)
+    rc = lib().orc_vclock_csr_merge(_ptr(so), _ptr(sl), _ptr(sa), _ptr(sc), _ptr(oo), _ptr(ol), _ptr(oa), _ptr(oc), n,
+                                    _ptr(out_act), _ptr(out_ctr), _ptr(out_len), threads, C.byref(bad))
+    if rc != 0:
+        raise ValueError(f"oracle csr merge: non-canonical run at object {bad.value}")
+    return (so + oo).astype(np.uint64), out_len[:n], out_act, out_ctr
+
+
+def vclock_csr_bench(s, o, threads):
+    so, sl, sa, sc = [np.ascontiguousarray(x) for x in s]
+    oo, ol, oa, oc = [np.ascontiguousarray(x) for x in o]
+    return lib().orc_vclock_csr_bench(_ptr(so), _ptr(sl), _ptr(sa), _ptr(sc), _ptr(oo), _ptr(ol), _ptr(oa), _ptr(oc),
+                                      len(so), threads)
 
 
 def pncounter_merge(self_rows, other_rows, n_actors, threads=8):
