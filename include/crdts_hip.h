@@ -197,6 +197,12 @@ typedef struct crdt_orswot_hdr {
 } crdt_orswot_hdr;
 
 #define CRDT_ORSWOT_SPARSE_CLOCK 1u
+/* Header flags bit 1: the record holds a member whose clock is EMPTY (an
+ * empty run). Only Causal::truncate produces one (crdt_orswot_truncate: the
+ * reference keeps such a member, src/orswot.rs:167-169); it is not a
+ * canonical input of the merge, apply and codec entry points, which reject
+ * it (CRDT_ENONCANON). */
+#define CRDT_ORSWOT_EMPTY_MEMBER_CLOCK 2u
 
 #define CRDT_ORSWOT_HDR_BYTES 32u
 #define CRDT_RECORD_ALIGN 16u
@@ -622,6 +628,23 @@ int crdt_orswot_to_bincode(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32
  * [first_obj, first_obj+n_obj), counter U[0, 2^bits) with `pct_zero` % zeros. */
 int crdt_dense_generate(uint64_t seed, size_t first_obj, size_t n_obj, uint32_t n_actors,
                         uint32_t bits, uint32_t pct_zero, int n_threads, uint64_t* h_rows);
+
+/* Causal::truncate, batched (src/orswot.rs:159-172; the Map of Orswots calls it
+ * on every value it keeps, src/map.rs): out[i] := self[i] after
+ * self[i].truncate(&clock[i]) — merge with an empty Orswot whose clock is
+ * clock[i] (incl. apply_deferred), then clock[i] subtracted from the top clock
+ * and from every member clock. clocks: a crdt_clock_csr batch of the same
+ * n_obj (any clock form of the records: actor ids as in the records).
+ * flags: 0 or CRDT_ORSWOT_SPARSE_CLOCK (the batch's record form). A truncated
+ * record is never larger than its input: record i is written at
+ * d_out_off[i] := self.off[i] (set by the call), so out_bytes >= self.bytes
+ * suffices. A member whose clock the subtract empties is kept with an empty
+ * clock, as in the reference, and its record carries
+ * CRDT_ORSWOT_EMPTY_MEMBER_CLOCK. A malformed record or clock run latches
+ * CRDT_ENONCANON (not written). */
+int crdt_orswot_truncate(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_clock_csr* clocks,
+                         uint32_t n_actors, uint32_t flags, uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes,
+                         void* stream);
 
 /* Host op-path builder used to construct states (tests, KAT scripts): an
  * opaque host Orswot with the reference's op semantics (src/orswot.rs:61-85,

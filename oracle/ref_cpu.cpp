@@ -312,8 +312,13 @@ long encode(const Orswot& o, uint32_t n_actors, uint8_t* out, size_t cap, bool s
   size_t bytes = record_bytes(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem, sparse);
   if (bytes > cap) return CRDT_ECAPACITY;
   std::memset(out, 0, bytes);
+  // an empty member clock (Causal::truncate can leave one, src/orswot.rs:167-169)
+  // is an empty run, flagged in the header
+  bool empty_clock = false;
+  for (auto& e : ents) empty_clock = empty_clock || e.second->dots.empty();
   crdt_orswot_hdr h = {(uint32_t)bytes, n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem,
-                       sparse ? CRDT_ORSWOT_SPARSE_CLOCK : 0u};
+                       (sparse ? CRDT_ORSWOT_SPARSE_CLOCK : 0u) |
+                           (empty_clock ? CRDT_ORSWOT_EMPTY_MEMBER_CLOCK : 0u)};
   std::memcpy(out, &h, sizeof h);
   Sections S = sections(out, h);
   uint64_t *clk = S.clk, *key = S.key, *dctr = S.dctr, *fctr = S.fctr, *fkey = S.fkey;
@@ -344,8 +349,8 @@ bool decode(const uint8_t* rec, size_t avail, Orswot& o) {
   if (avail < CRDT_ORSWOT_HDR_BYTES) return false;
   crdt_orswot_hdr h;
   std::memcpy(&h, rec, sizeof h);
-  const bool sparse = h.flags == CRDT_ORSWOT_SPARSE_CLOCK;
-  if (h.flags != 0 && !sparse) return false;
+  const bool sparse = (h.flags & CRDT_ORSWOT_SPARSE_CLOCK) != 0;
+  if (h.flags & ~(CRDT_ORSWOT_SPARSE_CLOCK | CRDT_ORSWOT_EMPTY_MEMBER_CLOCK)) return false;
   size_t bytes = record_bytes(h.n_clk, h.n_mem, h.n_dot, h.n_def, h.n_def_dot, h.n_def_mem, sparse);
   if (bytes != h.size || bytes > avail) return false;
   Sections S = sections(const_cast<uint8_t*>(rec), h);
@@ -667,6 +672,46 @@ int orc_orswot_merge_batch_ex(const uint8_t* lb, const uint64_t* loff, size_t lb
         continue;
       }
       L.merge(R);
+      std::vector<uint8_t> buf(record_bytes(n_actors, L.entries.size(), 0, 0, 0, 0) + 65536);
+      long got;
+      while ((got = encode(L, n_actors, buf.data(), buf.size(), sparse)) == CRDT_ECAPACITY)
+        buf.resize(buf.size() * 2);
+      if (got < 0) { err[i] = (int)got; continue; }
+      buf.resize(got);
+      outs[i] = std::move(buf);
+    }
+  });
+  size_t pos = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (err[i]) { if (bad) *bad = (int64_t)i; return err[i]; }
+    if (pos + outs[i].size() > ocap) { if (bad) *bad = (int64_t)i; return CRDT_ECAPACITY; }
+    std::memcpy(ob + pos, outs[i].data(), outs[i].size());
+    ooff[i] = pos;
+    pos += outs[i].size();
+  }
+  return 0;
+}
+
+// Causal::truncate (src/orswot.rs:159-172) of every record by its clock, the
+// clock i being the sorted run [coff[i], coff[i] + clen[i]) of (cact, cctr);
+// outputs packed into ob / ooff like orc_orswot_merge_batch_ex.
+int orc_orswot_truncate_batch(const uint8_t* lb, const uint64_t* loff, size_t lbytes, size_t n,
+                              const uint64_t* coff, const uint32_t* clen, const uint32_t* cact,
+                              const uint64_t* cctr, uint32_t n_actors, uint32_t flags, uint8_t* ob,
+                              uint64_t* ooff, size_t ocap, int threads, int64_t* bad) {
+  const bool sparse = (flags & CRDT_ORSWOT_SPARSE_CLOCK) != 0;
+  std::vector<std::vector<uint8_t>> outs(n);
+  std::vector<int> err(n, 0);
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) {
+      Orswot L;
+      if (!decode(lb + loff[i], lbytes - loff[i], L)) {
+        err[i] = CRDT_ENONCANON;
+        continue;
+      }
+      VClock c;
+      for (uint32_t k = 0; k < clen[i]; ++k) c.witness(cact[coff[i] + k], cctr[coff[i] + k]);
+      L.truncate(c);
       std::vector<uint8_t> buf(record_bytes(n_actors, L.entries.size(), 0, 0, 0, 0) + 65536);
       long got;
       while ((got = encode(L, n_actors, buf.data(), buf.size(), sparse)) == CRDT_ECAPACITY)

@@ -655,6 +655,21 @@ class Engine:
             self.status(stream)
         return out, off, lens
 
+    def orswot_truncate(self, B: OrswotBatch, clocks: "ClockBatch", stream=None, check_status=True):
+        """out[i] = B[i] after Causal::truncate(&clocks[i]) (src/orswot.rs:159-172),
+        written at B.off[i] (crdt_orswot_truncate). Returns an OrswotBatch."""
+        torch = _torch()
+        dev = f"cuda:{self.device}"
+        base = torch.empty(max(16, B.bytes), dtype=torch.uint8, device=dev)
+        off = torch.empty(B.n_obj, dtype=torch.int64, device=dev)
+        b, c = B.cbatch(), clocks.cstruct()
+        check(lib.crdt_orswot_truncate(self.ctx, C.byref(b), C.byref(c), B.n_actors, B.flags,
+                                       C.c_void_p(base.data_ptr()), C.c_void_p(off.data_ptr()), base.numel(),
+                                       self._stream(stream)), "orswot_truncate")
+        if check_status:
+            self.status(stream)
+        return OrswotBatch(base, off, B.n_actors, base.numel(), B.flags)
+
     # ------------------------------------------------ sparse (CSR) clocks
     def clock_csr_alloc_out(self, S: "ClockBatch", O: "ClockBatch"):
         torch = _torch()

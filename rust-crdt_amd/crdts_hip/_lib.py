@@ -71,6 +71,7 @@ EXPORTS = [
     "crdt_orswot_replica_join_bound", "crdt_orswot_replica_join", "crdt_orswot_replica_join_local",
     "crdt_comm_count", "crdt_orswot_replica_join_transport", "crdt_orswot_generate_replicas_subset",
     "crdt_dense_merge_host", "crdt_vclock_csr_merge", "crdt_gcounter_csr_merge", "crdt_pncounter_csr_merge",
+    "crdt_orswot_truncate",
 ]
 
 CRDT_COMM_ID_BYTES = 128
@@ -200,6 +201,7 @@ def _load():
         "crdt_orswot_replica_join_local": (I, [P, BP, U32, U32, U32, P, P, SZ, C.POINTER(SZ), P]),
         "crdt_comm_count": (I, [P, C.POINTER(I)]),
         "crdt_dense_merge_host": (I, [P, P, P, SZ, U32]),
+        "crdt_orswot_truncate": (I, [P, BP, C.POINTER(ClockCsr), U32, U32, P, P, SZ, P]),
         "crdt_vclock_csr_merge": (I, [P, C.POINTER(ClockCsr), C.POINTER(ClockCsr), C.POINTER(ClockCsrOut), P]),
         "crdt_gcounter_csr_merge": (I, [P, C.POINTER(ClockCsr), C.POINTER(ClockCsr), C.POINTER(ClockCsrOut), P]),
         "crdt_pncounter_csr_merge": (I, [P] + [C.POINTER(ClockCsr)] * 4 + [C.POINTER(ClockCsrOut)] * 2 + [P]),

@@ -184,6 +184,23 @@ int crdt_pncounter_csr_merge(crdt_ctx* ctx, const crdt_clock_csr* self_p, const 
   return launch_clock_csr_merge(s, o, w, 2, ctx->d_status, S(stream));
 }
 
+int crdt_orswot_truncate(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_clock_csr* clocks,
+                         uint32_t n_actors, uint32_t flags, uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes,
+                         void* stream) {
+  if (!ctx || !self || !clocks || n_actors == 0 || (flags & ~CRDT_ORSWOT_SPARSE_CLOCK) ||
+      clocks->n_obj != self->n_obj)
+    return CRDT_EINVAL;
+  if (self->n_obj == 0) return CRDT_OK;
+  if (!self->base || !self->off || !clocks->off || !clocks->len || !d_out || !d_out_off || !aligned16(d_out))
+    return CRDT_EINVAL;
+  if (clocks->n_entries && (!clocks->act || !clocks->ctr)) return CRDT_EINVAL;
+  if (out_bytes < self->bytes) return CRDT_ECAPACITY;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return launch_orswot_truncate(*self, *clocks, n_actors, flags, d_out, d_out_off, out_bytes, ctx->d_status,
+                                S(stream));
+}
+
 int crdt_dense_merge_host(crdt_ctx* ctx, uint64_t* h_self, const uint64_t* h_other, size_t n_obj, uint32_t n_slots) {
   if (!ctx || n_slots == 0 || (n_obj && (!h_self || !h_other))) return CRDT_EINVAL;
   if (n_obj == 0) return CRDT_OK;

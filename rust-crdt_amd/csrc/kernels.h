@@ -22,6 +22,9 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
 int launch_clock_csr_merge(const crdt_clock_csr* const* self, const crdt_clock_csr* const* other,
                            const crdt_clock_csr_out* const* out, int n_jobs, int* status, hipStream_t stream);
 
+int launch_orswot_truncate(const crdt_orswot_batch& self, const crdt_clock_csr& clocks, uint32_t A, uint32_t flags,
+                           uint8_t* out, uint64_t* out_off, uint64_t out_bytes, int* status, hipStream_t stream);
+
 int launch_dense_max(uint64_t* self, const uint64_t* other, uint64_t n_words, hipStream_t stream);
 
 int launch_orswot_validate(const uint8_t* base, const uint64_t* off, uint64_t bytes, uint64_t n_obj,

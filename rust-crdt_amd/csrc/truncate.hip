@@ -1,0 +1,377 @@
+// Batched Causal::truncate for Orswot records (src/orswot.rs:159-172):
+//
+//     let mut empty_set = Orswot::new(); empty_set.clock = clock.clone();
+//     self.merge(&empty_set);            // :87-157 with apply_deferred :235-243
+//     self.clock.subtract(&clock);       // vclock.rs:236-242
+//     for (_, member_clock) in self.entries.iter_mut() { member_clock.subtract(&clock); }
+//
+// Spelled out per record (c = the truncating clock, T = the top clock,
+// M = max(T, c) the merged clock; canonical clocks: `a <= b` iff every
+// a[x] <= b[x], vclock.rs:59-71):
+//  - a member (every entry is self-only against the empty set, :94-104) is
+//    kept by the merge iff some dot (x, v) of its clock has v > c[x];
+//  - apply_deferred: every deferred (D, S) is re-deferred iff !(D <= M)
+//    (the member set S unchanged), and every member of S loses the dots with
+//    D[x] >= v (apply_remove :195-211), dropped if that empties its clock;
+//  - the top clock keeps T[x] iff T[x] > c[x] (M[x] == c[x] otherwise);
+//  - a kept member keeps the dots with v > c[x] — possibly none: the
+//    reference keeps the member with an EMPTY clock then (it subtracts without
+//    dropping). Such a record is written with header flag
+//    CRDT_ORSWOT_EMPTY_MEMBER_CLOCK (an empty run), which the merge / apply /
+//    codec kernels do not accept (not canonical for them).
+// The output is never larger than the input (a subset of every section), so
+// record i is written at out_off[i] := self.off[i].
+//
+// One wave per record, lane = member (runs walked per lane) / deferred clock
+// in 64-wide chunks, two passes (count, write); lookups of c[x] and D[x]
+// binary-search the sorted runs. Not the hot path: latency-bound, any size.
+#include <hip/hip_runtime.h>
+
+#include "../../include/crdts_hip.h"
+#include "kernels.h"
+#include "record_layout.h"
+
+namespace crdts_hip {
+namespace {
+
+constexpr uint32_t kW = 64;
+constexpr uint32_t kEmptyClockFlag = 2u;  // CRDT_ORSWOT_EMPTY_MEMBER_CLOCK
+
+__device__ __forceinline__ void fail(int* status, int code) { atomicCAS(status, 0, code); }
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+  for (uint32_t s = 32u; s; s >>= 1) v += __shfl_xor(v, (int)s);
+  return v;
+}
+// exclusive prefix over lanes
+__device__ __forceinline__ uint32_t wave_excl(uint32_t v, uint32_t lane) {
+  uint32_t x = v;
+  for (uint32_t s = 1u; s < kW; s <<= 1) {
+    const uint32_t y = __shfl_up(x, (int)s);
+    x += lane >= s ? y : 0u;
+  }
+  return x - v;
+}
+
+// A sorted (actor, counter) run in memory; get(x) = its counter or 0.
+struct Run {
+  const uint32_t* a;
+  const uint64_t* c;
+  uint32_t n;
+  __device__ uint64_t get(uint32_t x) const {
+    uint32_t lo = 0, len = n;
+    while (len) {
+      const uint32_t h = len >> 1;
+      if (a[lo + h] < x) {
+        lo += h + 1u;
+        len -= h + 1u;
+      } else {
+        len = h;
+      }
+    }
+    return lo < n && a[lo] == x ? c[lo] : 0ull;
+  }
+};
+
+__device__ __forceinline__ bool has_key(const uint64_t* k, uint32_t n, uint64_t key) {
+  uint32_t lo = 0, len = n;
+  while (len) {
+    const uint32_t h = len >> 1;
+    if (k[lo + h] < key) {
+      lo += h + 1u;
+      len -= h + 1u;
+    } else {
+      len = h;
+    }
+  }
+  return lo < n && k[lo] == key;
+}
+
+struct Rec {
+  const uint8_t* r;
+  RecLayout L;
+  bool sparse;
+  __device__ const uint64_t* key() const { return (const uint64_t*)(r + L.o_key); }
+  __device__ const uint64_t* dctr() const { return (const uint64_t*)(r + L.o_dctr); }
+  __device__ const uint32_t* dact() const { return (const uint32_t*)(r + L.o_dact); }
+  __device__ const uint32_t* mdend() const { return (const uint32_t*)(r + L.o_mdend); }
+  __device__ const uint64_t* fctr() const { return (const uint64_t*)(r + L.o_fctr); }
+  __device__ const uint64_t* fkey() const { return (const uint64_t*)(r + L.o_fkey); }
+  __device__ const uint32_t* fact() const { return (const uint32_t*)(r + L.o_fact); }
+  __device__ const uint32_t* fdend() const { return (const uint32_t*)(r + L.o_fdend); }
+  __device__ const uint32_t* fmend() const { return (const uint32_t*)(r + L.o_fmend); }
+  // top clock T[x]
+  __device__ uint64_t top(uint32_t x) const {
+    if (!sparse) return x < L.n_clk ? ((const uint64_t*)(r + L.o_clk))[x] : 0ull;
+    return Run{(const uint32_t*)(r + L.o_cact), (const uint64_t*)(r + L.o_clk), L.n_clk}.get(x);
+  }
+  // run ends clamped to their section, begins to their end: a malformed
+  // record cannot send a lane outside its sections or a count negative
+  __device__ uint32_t m_end(uint32_t m) const { return min(mdend()[m], L.n_dot); }
+  __device__ uint32_t m_begin(uint32_t m) const { return m ? min(m_end(m - 1u), m_end(m)) : 0u; }
+  __device__ uint32_t fd_end(uint32_t k) const { return min(fdend()[k], L.n_def_dot); }
+  __device__ uint32_t fd_begin(uint32_t k) const { return k ? min(fd_end(k - 1u), fd_end(k)) : 0u; }
+  __device__ uint32_t fm_end(uint32_t k) const { return min(fmend()[k], L.n_def_mem); }
+  __device__ uint32_t fm_begin(uint32_t k) const { return k ? min(fm_end(k - 1u), fm_end(k)) : 0u; }
+};
+
+// Is the dot (x, v) of member `key` removed by a deferred clock naming the
+// member (apply_remove's subtract: D[x] >= v)?
+__device__ bool deferred_kills(const Rec& R, uint64_t key, uint32_t x, uint64_t v) {
+  for (uint32_t k = 0; k < R.L.n_def; ++k) {
+    const uint32_t m0 = R.fm_begin(k), m1 = R.fm_end(k);
+    if (!has_key(R.fkey() + m0, m1 - m0, key)) continue;
+    const uint32_t d0 = R.fd_begin(k), d1 = R.fd_end(k);
+    if (Run{R.fact() + d0, R.fctr() + d0, d1 - d0}.get(x) >= v) return true;
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(256) void orswot_truncate_kernel(const uint8_t* __restrict__ base,
+                                                              const uint64_t* __restrict__ off, uint64_t bytes,
+                                                              uint64_t n_obj, const uint64_t* __restrict__ coff,
+                                                              const uint32_t* __restrict__ clen,
+                                                              const uint32_t* __restrict__ cact,
+                                                              const uint64_t* __restrict__ cctr, uint64_t c_entries,
+                                                              uint32_t A, uint32_t flags, uint8_t* __restrict__ out,
+                                                              uint64_t* __restrict__ out_off, uint64_t out_bytes,
+                                                              int* status) {
+  const uint32_t lane = threadIdx.x & (kW - 1u);
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kW;
+  const uint64_t n_waves = (uint64_t)gridDim.x * blockDim.x / kW;
+  const bool sparse = (flags & kSparseClock) != 0u;
+  for (uint64_t i = wave; i < n_obj; i += n_waves) {
+    const uint64_t o = off[i];
+    if (lane == 0u) out_off[i] = o;
+    // ---- the record: header, layout, bounds (a bad record is not written)
+    bool ok = (o & 15u) == 0u && o <= bytes && bytes - o >= kHdrBytes;
+    uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (ok)
+      for (int k = 0; k < 8; ++k) h[k] = ((const uint32_t*)(base + o))[k];
+    Rec R{base + o, {}, sparse};
+    rec_layout(R.L, h[1], h[2], h[3], h[4], h[5], h[6], sparse);
+    ok = ok && h[0] == R.L.size && h[7] == flags && (sparse ? h[1] <= A : h[1] == A) && R.L.size <= bytes - o &&
+         o + R.L.size <= out_bytes;
+    const uint64_t c0 = coff[i];
+    const uint32_t cn = clen[i];
+    ok = ok && c0 <= c_entries && cn <= c_entries - c0;
+    if (!ok) {
+      if (lane == 0u) fail(status, CRDT_ENONCANON);
+      continue;
+    }
+    const Run c{cact + c0, cctr + c0, cn};
+    const RecLayout& L = R.L;
+    // run ends of member / deferred runs are clamped: a malformed record cannot
+    // send a lane past its sections
+
+    // ---- pass 1: counts
+    // top clock: T[x] kept iff T[x] > c[x]
+    uint32_t n_clk = 0;
+    for (uint32_t b = 0; b < L.n_clk; b += kW) {
+      const uint32_t k = b + lane;
+      uint64_t t = 0;
+      uint32_t x = k;
+      if (k < L.n_clk) {
+        if (sparse) x = ((const uint32_t*)(R.r + L.o_cact))[k];
+        t = ((const uint64_t*)(R.r + L.o_clk))[k];
+      }
+      n_clk += (uint32_t)__popcll(__ballot(k < L.n_clk && t > c.get(x)));
+    }
+    if (!sparse) n_clk = L.n_clk;  // dense: every slot is written (0 = absent)
+    // deferred: (D, S) re-deferred iff !(D <= M), M = max(T, c)
+    uint32_t n_def = 0, n_fdot = 0, n_fmem = 0;
+    for (uint32_t b = 0; b < L.n_def; b += kW) {
+      const uint32_t k = b + lane;
+      bool keepd = false;
+      uint32_t nd = 0, nm = 0;
+      if (k < L.n_def) {
+        const uint32_t d0 = R.fd_begin(k), d1 = R.fd_end(k);
+        for (uint32_t d = d0; d < d1; ++d) {
+          const uint32_t x = R.fact()[d];
+          const uint64_t t = R.top(x), cx = c.get(x);
+          keepd = keepd || R.fctr()[d] > (t > cx ? t : cx);
+        }
+        nd = d1 - d0;
+        nm = R.fm_end(k) - R.fm_begin(k);
+      }
+      n_def += (uint32_t)__popcll(__ballot(keepd));
+      n_fdot += wave_sum(keepd ? nd : 0u);
+      n_fmem += wave_sum(keepd ? nm : 0u);
+    }
+    // members: kept iff some dot v > c[x] and some dot survives the deferred
+    // subtracts; final dots: v > c[x] and not removed by a deferred clock
+    uint32_t n_mem = 0, n_dot = 0;
+    bool empty_clock = false;
+    for (uint32_t b = 0; b < L.n_mem; b += kW) {
+      const uint32_t m = b + lane;
+      uint32_t fin = 0;
+      bool above = false, alive = false;
+      if (m < L.n_mem) {
+        const uint64_t key = R.key()[m];
+        for (uint32_t d = R.m_begin(m); d < R.m_end(m); ++d) {
+          const uint32_t x = R.dact()[d];
+          const uint64_t v = R.dctr()[d];
+          const bool gt = v > c.get(x);
+          const bool dk = L.n_def && deferred_kills(R, key, x, v);
+          above = above || gt;
+          alive = alive || !dk;
+          fin += gt && !dk ? 1u : 0u;
+        }
+      }
+      const bool kept = above && alive;
+      n_mem += (uint32_t)__popcll(__ballot(kept));
+      n_dot += wave_sum(kept ? fin : 0u);
+      empty_clock = empty_clock || __ballot(kept && fin == 0u) != 0ull;
+    }
+    RecLayout O;
+    rec_layout(O, n_clk, n_mem, n_dot, n_def, n_fdot, n_fmem, sparse);
+    if (O.size > L.size) {  // cannot happen for a canonical record
+      if (lane == 0u) fail(status, CRDT_ENONCANON);
+      continue;
+    }
+    uint8_t* w = out + o;
+
+    // ---- pass 2: write
+    // top clock
+    {
+      uint32_t at = 0;
+      for (uint32_t b = 0; b < L.n_clk; b += kW) {
+        const uint32_t k = b + lane;
+        uint64_t t = 0;
+        uint32_t x = k;
+        if (k < L.n_clk) {
+          if (sparse) x = ((const uint32_t*)(R.r + L.o_cact))[k];
+          t = ((const uint64_t*)(R.r + L.o_clk))[k];
+        }
+        const bool keep = k < L.n_clk && t > c.get(x);
+        if (!sparse) {
+          if (k < L.n_clk) ((uint64_t*)(w + O.o_clk))[k] = keep ? t : 0ull;
+        } else {
+          const uint64_t K = __ballot(keep);
+          const uint32_t p = at + mbcnt(K);
+          if (keep) {
+            ((uint64_t*)(w + O.o_clk))[p] = t;
+            ((uint32_t*)(w + O.o_cact))[p] = x;
+          }
+          at += (uint32_t)__popcll(K);
+        }
+      }
+      if (sparse && lane == 0u && O.o_key != O.o_cact + 4u * n_clk)
+        *(uint32_t*)(w + O.o_cact + 4u * n_clk) = 0u;  // pad to 8
+    }
+    // members
+    {
+      uint32_t at_m = 0, at_d = 0;
+      for (uint32_t b = 0; b < L.n_mem; b += kW) {
+        const uint32_t m = b + lane;
+        uint32_t fin = 0;
+        bool above = false, alive = false;
+        uint64_t key = 0;
+        const uint32_t d0 = m < L.n_mem ? R.m_begin(m) : 0u;
+        const uint32_t d1 = m < L.n_mem ? R.m_end(m) : 0u;
+        if (m < L.n_mem) {
+          key = R.key()[m];
+          for (uint32_t d = d0; d < d1; ++d) {
+            const uint32_t x = R.dact()[d];
+            const uint64_t v = R.dctr()[d];
+            const bool gt = v > c.get(x);
+            const bool dk = L.n_def && deferred_kills(R, key, x, v);
+            above = above || gt;
+            alive = alive || !dk;
+            fin += gt && !dk ? 1u : 0u;
+          }
+        }
+        const bool kept = above && alive;
+        const uint64_t K = __ballot(kept);
+        const uint32_t pm = at_m + mbcnt(K);
+        const uint32_t cnt = kept ? fin : 0u;
+        const uint32_t pd = at_d + wave_excl(cnt, lane);
+        if (kept) {
+          ((uint64_t*)(w + O.o_key))[pm] = key;
+          ((uint32_t*)(w + O.o_mdend))[pm] = pd + cnt;
+          uint32_t q = pd;
+          for (uint32_t d = d0; d < d1; ++d) {
+            const uint32_t x = R.dact()[d];
+            const uint64_t v = R.dctr()[d];
+            if (v > c.get(x) && !(L.n_def && deferred_kills(R, key, x, v))) {
+              ((uint64_t*)(w + O.o_dctr))[q] = v;
+              ((uint32_t*)(w + O.o_dact))[q] = x;
+              ++q;
+            }
+          }
+        }
+        at_m += (uint32_t)__popcll(K);
+        at_d += wave_sum(cnt);
+      }
+    }
+    // deferred (kept ones, in their CLOCK ORDER, sets unchanged)
+    {
+      uint32_t at = 0, at_d = 0, at_m = 0;
+      for (uint32_t b = 0; b < L.n_def; b += kW) {
+        const uint32_t k = b + lane;
+        bool keepd = false;
+        uint32_t d0 = 0, d1 = 0, m0 = 0, m1 = 0;
+        if (k < L.n_def) {
+          d0 = R.fd_begin(k);
+          d1 = R.fd_end(k);
+          m0 = R.fm_begin(k);
+          m1 = R.fm_end(k);
+          for (uint32_t d = d0; d < d1; ++d) {
+            const uint32_t x = R.fact()[d];
+            const uint64_t t = R.top(x), cx = c.get(x);
+            keepd = keepd || R.fctr()[d] > (t > cx ? t : cx);
+          }
+        }
+        const uint64_t K = __ballot(keepd);
+        const uint32_t nd = keepd ? d1 - d0 : 0u, nm = keepd ? m1 - m0 : 0u;
+        const uint32_t p = at + mbcnt(K), pd = at_d + wave_excl(nd, lane), pmm = at_m + wave_excl(nm, lane);
+        if (keepd) {
+          for (uint32_t d = 0; d < nd; ++d) {
+            ((uint64_t*)(w + O.o_fctr))[pd + d] = R.fctr()[d0 + d];
+            ((uint32_t*)(w + O.o_fact))[pd + d] = R.fact()[d0 + d];
+          }
+          for (uint32_t j = 0; j < nm; ++j) ((uint64_t*)(w + O.o_fkey))[pmm + j] = R.fkey()[m0 + j];
+          ((uint32_t*)(w + O.o_fdend))[p] = pd + nd;
+          ((uint32_t*)(w + O.o_fmend))[p] = pmm + nm;
+        }
+        at += (uint32_t)__popcll(K);
+        at_d += wave_sum(nd);
+        at_m += wave_sum(nm);
+      }
+    }
+    // zero padding (member block to 8, record to 16) and the header
+    if (lane == 0u && O.o_def != O.o_mpad) *(uint32_t*)(w + O.o_mpad) = 0u;
+    if (lane >= 1u && lane < 4u && O.o_end + 4u * (lane - 1u) < O.size) *(uint32_t*)(w + O.o_end + 4u * (lane - 1u)) = 0u;
+    if (lane == 0u) {
+      uint32_t* hw = (uint32_t*)w;
+      hw[0] = O.size;
+      hw[1] = n_clk;
+      hw[2] = n_mem;
+      hw[3] = n_dot;
+      hw[4] = n_def;
+      hw[5] = n_fdot;
+      hw[6] = n_fmem;
+      hw[7] = flags | (empty_clock ? kEmptyClockFlag : 0u);
+    }
+  }
+}
+
+}  // namespace
+
+int launch_orswot_truncate(const crdt_orswot_batch& self, const crdt_clock_csr& clocks, uint32_t A, uint32_t flags,
+                           uint8_t* out, uint64_t* out_off, uint64_t out_bytes, int* status, hipStream_t stream) {
+  if (self.n_obj == 0) return CRDT_OK;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const uint64_t want = (self.n_obj + 3) / 4;
+  const uint64_t cap = (uint64_t)cus * 8;
+  const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
+  hipLaunchKernelGGL(orswot_truncate_kernel, dim3(blocks), dim3(256), 0, stream, self.base, self.off,
+                     (uint64_t)self.bytes, (uint64_t)self.n_obj, clocks.off, clocks.len, clocks.act, clocks.ctr,
+                     (uint64_t)clocks.n_entries, A, flags, out, out_off, out_bytes, status);
+  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+}
+
+}  // namespace crdts_hip

@@ -70,6 +70,9 @@ def lib():
     L.orc_vclock_csr_merge.argtypes = [P] * 8 + [C.c_size_t, P, P, P, C.c_int, C.POINTER(C.c_int64)]
     L.orc_vclock_csr_bench.restype = C.c_double
     L.orc_vclock_csr_bench.argtypes = [P] * 8 + [C.c_size_t, C.c_int]
+    L.orc_orswot_truncate_batch.restype = C.c_int
+    L.orc_orswot_truncate_batch.argtypes = [P, P, C.c_size_t, C.c_size_t, P, P, P, P, C.c_uint32, C.c_uint32, P, P,
+                                            C.c_size_t, C.c_int, C.POINTER(C.c_int64)]
     L.orc_obj_new.restype = P
     L.orc_obj_clone.restype = P
     L.orc_obj_clone.argtypes = [P]
@@ -343,6 +346,25 @@ def vclock_csr_merge(s, o, threads=8):
     if rc != 0:
         raise ValueError(f"oracle csr merge: non-canonical run at object {bad.value}")
     return (so + oo).astype(np.uint64), out_len[:n], out_act, out_ctr
+
+
+def orswot_truncate_batch(lbase, loff, clocks, n_actors, flags=0, threads=8):
+    """Causal::truncate of record i by clock i (clocks: numpy CSR (off, len,
+    act, ctr)); returns the packed (base, off) of the truncated records."""
+    lbase = np.ascontiguousarray(lbase, dtype=np.uint8)
+    loff = np.ascontiguousarray(loff, dtype=np.uint64)
+    co, cl, ca, cc = [np.ascontiguousarray(x) for x in clocks]
+    n = len(loff)
+    cap = lbase.nbytes + 16
+    obase = np.zeros(cap, np.uint8)
+    ooff = np.zeros(max(1, n), np.uint64)
+    bad = C.c_int64(-1)
+    rc = lib().orc_orswot_truncate_batch(_ptr(lbase), _ptr(loff), lbase.nbytes, n, _ptr(co), _ptr(cl), _ptr(ca),
+                                         _ptr(cc), n_actors, flags, _ptr(obase), _ptr(ooff), cap, threads,
+                                         C.byref(bad))
+    if rc != 0:
+        raise ValueError(f"oracle truncate failed rc={rc} at object {bad.value}")
+    return obase, ooff[:n]
 
 
 def vclock_csr_bench(s, o, threads):

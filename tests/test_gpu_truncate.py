@@ -1,0 +1,82 @@
+"""GPU parity: batched Causal::truncate for Orswot (crdt_orswot_truncate,
+src/orswot.rs:159-172) vs the oracle's Orswot::truncate, byte-exact: random
+canonical states incl. deferred clocks that cover member dots, where truncate
+leaves members with EMPTY clocks (CRDT_ORSWOT_EMPTY_MEMBER_CLOCK, kept as in
+the reference); config-3 states truncated by the other replica's top clock
+(the Map case: the remover's clock) and by partial clocks; CSR (config 5)
+records; and a record with an empty member clock rejected by the merge."""
+import random
+
+import numpy as np
+import pytest
+
+import records
+import truncate_cases as T
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(gpu, oracle, lb, lo, clocks_np, A, flags=0):
+    import crdts_hip
+
+    B = crdts_hip.OrswotBatch.from_host(lb, lo, A, flags=flags)
+    C = crdts_hip.ClockBatch.from_host(*clocks_np)
+    out = gpu.orswot_truncate(B, C)
+    got = out.records()
+    ob, oo = oracle.orswot_truncate_batch(lb, lo, clocks_np, A, flags, threads=16)
+    exp = records.unpack_batch(ob, oo)
+    bad = [i for i, (g, e) in enumerate(zip(got, exp)) if g != e]
+    assert not bad, f"{len(bad)}/{len(exp)} differ; first {bad[0]}: {records.decode(got[bad[0]])} vs " \
+                    f"{records.decode(exp[bad[0]])}"
+    assert (out.off.cpu().numpy().view(np.uint64) == lo.astype(np.uint64)).all()  # written in place of the input
+    return exp
+
+
+def test_random_states_incl_empty_member_clocks(gpu, oracle):
+    states, clocks, recs = T.cases(20_000, seed=9)
+    lb, lo = records.pack_batch(recs)
+    exp = _check(gpu, oracle, lb, lo, T.clocks_csr(clocks), 8)
+    flags = [int(np.frombuffer(r[28:32], np.uint32)[0]) for r in exp]
+    assert sum(1 for f in flags if f & 2) > 100  # empty member clocks occur and match
+
+
+def test_config3_truncated_by_the_other_replicas_clock(gpu, oracle):
+    import crdts_hip
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(50_000, threads=16, seed=12)
+    rng = random.Random(3)
+    clocks = []
+    for i, r in enumerate(records.unpack_batch(rb, ro)):
+        c = records.decode(r)["clock"]
+        if i % 3 == 1:  # a partial clock: some actors dropped, some counters lowered
+            c = {a: max(1, v - rng.randrange(3)) for a, v in c.items() if rng.random() < 0.7}
+        elif i % 3 == 2:
+            c = {}
+        clocks.append(c)
+    _check(gpu, oracle, lb, lo, T.clocks_csr(clocks), 16)
+
+
+def test_sparse_records(gpu, oracle):
+    import crdts_hip
+
+    U, SP = crdts_hip.CONFIG5["universe"], crdts_hip.SPARSE_CLOCK
+    reps = crdts_hip.generate_replicas(20_000, 2, threads=16)
+    clocks = [records.decode(r)["clock"] for r in records.unpack_batch(*reps[1])]
+    _check(gpu, oracle, reps[0][0], reps[0][1], T.clocks_csr(clocks), U, SP)
+
+
+def test_empty_member_clock_rejected_by_merge(gpu, oracle):
+    import crdts_hip
+    from crdts_hip._lib import CRDT_ENONCANON
+
+    # entry {a:5, b:1}, deferred {a:6} naming it (pending: a:6 > clock's a:5), c = {a:3, b:2}:
+    # the deferred subtract removes a:5, the final subtract b:1 -> an empty clock
+    rec = records.encode({0: 5, 1: 1}, {7: {0: 5, 1: 1}}, {((0, 6),): {7}}, 4)
+    lb, lo = records.pack_batch([rec])
+    exp = _check(gpu, oracle, lb, lo, T.clocks_csr([{0: 3, 1: 2}]), 4)
+    d = records.decode(exp[0])
+    assert d["entries"] == {7: []} and d["flags"] & 2
+    B = crdts_hip.OrswotBatch.from_host(*records.pack_batch(exp), 4)
+    with pytest.raises(crdts_hip.CrdtError) as e:
+        gpu.orswot_merge(B, B)
+    assert e.value.code == CRDT_ENONCANON
