@@ -14,4 +14,8 @@ timeout -k 10 300 python bench.py --gpus 2 --rehearse --n-obj 200000 --ae-n-obj 
 cut -c1-1500 $OUT/bench_rehearse2.json
 timeout -k 10 300 python bench.py > $OUT/bench_orswot.json 2> $OUT/bench_orswot.err || { echo BENCH_FAILED; tail -20 $OUT/bench_orswot.err; exit 1; }
 cut -c1-800 $OUT/bench_orswot.json
+for wl in ${EXTRA_WL:-}; do
+  timeout -k 10 300 python bench.py --workload $wl > $OUT/bench_$wl.json 2> $OUT/bench_$wl.err || { echo BENCH_FAILED $wl; tail -20 $OUT/bench_$wl.err; exit 1; }
+  echo "$wl $(cut -c1-700 $OUT/bench_$wl.json)"
+done
 echo ALL_OK
