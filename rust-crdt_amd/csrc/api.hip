@@ -69,7 +69,14 @@ int crdt_ctx_create(crdt_ctx** out, int device) {
   c->blocks_per_cu = 0;
   c->list_cap = kDefaultListCap;
   c->variant = 0;
-  const size_t bytes = 64 + 8ull * kDefaultListCap + kTrashBytes + 8ull * kDeferListCap;  // status, ctl, lists, sink
+  // status, ctl, the general-path list, the per-wave store sink; the deferred
+  // list after it is read and written only by the two-pass join variants of
+  // the diagnostic build
+#ifdef CRDT_DIAG
+  const size_t bytes = 64 + 8ull * kDefaultListCap + kTrashBytes + 8ull * kDeferListCap;
+#else
+  const size_t bytes = 64 + 8ull * kDefaultListCap + kTrashBytes;
+#endif
   uint8_t* scratch = nullptr;
   if (hipMalloc(&scratch, bytes) != hipSuccess || hipMemset(scratch, 0, bytes) != hipSuccess) {
     (void)hipFree(scratch);

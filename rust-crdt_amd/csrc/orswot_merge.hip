@@ -1499,6 +1499,9 @@ template <uint32_t OUTCAP, int OUT = 0, bool HD = false, int HABL = 0, bool RT =
 __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint32_t uX, uint8_t* O, uint32_t A,
                                                  uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane,
                                                  bool& big, uint8_t* sink = nullptr) {
+#ifndef CRDT_DIAG
+  static_assert(HABL == 0, "timing-only ablations (HABL != 0) exist in -DCRDT_DIAG builds only");
+#endif
   big = false;
   const uint32_t key = kHdrBytes + 8u * A;
   const uint32_t ctrL = key + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
@@ -2774,6 +2777,10 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
     uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
     int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
+#ifndef CRDT_DIAG
+  // the product kernel: one pass (MODE 3), no timing-only ablation
+  static_assert(HABL == 0 && MODE == 3, "ablations and the two-pass modes exist in -DCRDT_DIAG builds only");
+#endif
   __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
   __shared__ u32x4 scr_s[kWavesPerBlock][(MODE == 1 ? k3Scratch : kMask1Scratch) / 16];
   __shared__ u32x4 out_s[kWavesPerBlock][MODE == 3 && !HDD ? kFastStage / 16 : 1];  // assembled outputs (deferred objects)
@@ -2941,10 +2948,13 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
         // operations for every object
         uint32_t src;
         bool direct = false;
+#ifdef CRDT_DIAG
         if (HABL == 4 || HABL == 5) {  // timing only: no join, the self record copied out as the output (5: densely)
           r = lane_of(n16, t) & 0xFFFFu;
           src = lds_addr(sL);
-        } else if ((defs >> td) & 1ull) {
+        } else
+#endif
+        if ((defs >> td) & 1ull) {
           if (HDD) {
             if (M3HD)
               r = mask3_object<0xFFFFFFFFu, 0, true, HABL, RT>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
@@ -3001,11 +3011,18 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
       wave_sync();
     }
   }
+#ifdef CRDT_DIAG
   if (HABL == 6 && lane == 0u && wave_id < 10922u) {  // timing only: the list's upper half holds the stamps
     list[32768u + 3u * wave_id] = ts0;
     list[32768u + 3u * wave_id + 1u] = __builtin_amdgcn_s_memrealtime();
     list[32768u + 3u * wave_id + 2u] = ((uint64_t)n_joined << 32) | (n_hd << 16) | n_chunk;
   }
+#else
+  (void)ts0;
+  (void)n_joined;
+  (void)n_hd;
+  (void)n_chunk;
+#endif
 }
 
 #ifdef CRDT_DIAG
@@ -3760,6 +3777,9 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
                        const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
                        uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
                        uint32_t list_cap, hipStream_t stream, int blocks_per_cu) {
+#ifndef CRDT_DIAG
+  static_assert(HABL == 0 && ONE && !V10 && !DK, "the product launch: one pass, no timing-only ablation");
+#endif
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const void* f1;
@@ -3774,8 +3794,10 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
   if constexpr (ONE) {
     f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL, RT, DYN, SF, SPEC, GMIN>;
   } else {
+#ifdef CRDT_DIAG
     f1 = (const void*)orswot_join_kernel<MINW, 1>;
     f2 = (const void*)orswot_join_kernel<MINW, 2, 2, false, false, M3HD>;
+#endif
   }
   static std::atomic<int> occ_cache[2][10];  // per (pass, MINW; slot 9: the v9 kernel); HDD variants share one per MINW
   constexpr int slot = DK || V10 ? 9 : MINW;

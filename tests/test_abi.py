@@ -89,3 +89,18 @@ def test_device_entry_points_fail_cleanly_without_gpu():
 
     if not torch.cuda.is_available():
         assert rc == -6  # CRDT_ENODEV: never a silent CPU fallback
+
+
+def test_product_has_only_the_product_join_instantiation():
+    """The timing-only ablations (HABL != 0) and the two-pass join modes exist
+    in the -DCRDT_DIAG build only: the product library's code objects hold
+    exactly one orswot_join_kernel, MODE 3 with HABL 0 (static_asserts in
+    orswot_merge.hip keep it that way)."""
+    import crdts_hip
+
+    blob = open(crdts_hip.LIB_PATH, "rb").read()
+    names = set(re.findall(rb"orswot_join_kernelILi(\d+)ELi(\d+)ELi(\d+)ELb([01])ELb([01])ELb([01])ELi(\d+)E", blob))
+    assert names, "no orswot_join_kernel in the product library"
+    for minw, mode, out, hdd, dc, m3hd, habl in names:
+        assert mode == b"3" and habl == b"0", names
+    assert len(names) == 1, names
