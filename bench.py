@@ -424,6 +424,7 @@ def run_dense(args, rank, world, local, kind):
     b[torch.rand(n * slots, device=f"cuda:{local}", generator=g) < 0.25] = 0
     eng = crdts_hip.Engine(local)
     stream = torch.cuda.Stream(device=local)
+    torch.cuda.synchronize()  # generated on torch's stream; the merges run on `stream`
     for _ in range(args.warmup):
         eng.dense_merge(a, b, A, kind, stream=stream)
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -673,6 +674,7 @@ def run_gcounter_ae(args, rank, world, local, eng=None):
     base[:, mine_slot] += torch.randint(1, 1 << 20, (n,), dtype=torch.int64, device=dev, generator=g)
     eng = eng or crdts_hip.Engine(local)
     stream = torch.cuda.Stream(device=local)
+    torch.cuda.synchronize()  # generated on torch's stream; the joins run on `stream`
     check = None
     ae_eng = None if args.rehearse else eng  # rehearsal: the gloo path of replica.dense_allreduce_max
     if world > 1:
@@ -777,6 +779,7 @@ def run_clock_csr(args, rank, world, local):
     S, O = sides
     eng = crdts_hip.Engine(local)
     stream = torch.cuda.Stream(device=local)
+    torch.cuda.synchronize()  # the batches were generated on torch's stream; the merges run on `stream`
     out = eng.clock_csr_merge(S, O, stream=stream)  # checked launch
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_ffi
@@ -1125,6 +1128,7 @@ def run_mvreg(args, rank, world, local):
     S, O = slab(), slab()
     eng = crdts_hip.Engine(local)
     stream = torch.cuda.Stream(device=local)
+    torch.cuda.synchronize()  # generated on torch's stream; the merges run on `stream`
     out = eng.mvreg_merge(S, O, A, stream=stream)
     torch.cuda.synchronize()
     sys.path.insert(0, os.path.join(REPO, "tests"))

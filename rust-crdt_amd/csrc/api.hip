@@ -36,6 +36,18 @@ int dense(crdt_ctx* ctx, uint64_t* self, const uint64_t* other, size_t n_obj, ui
 
 }  // namespace
 
+int ctx_big_scratch(crdt_ctx* ctx, size_t bytes) {
+  if (ctx->big_bytes >= bytes) return CRDT_OK;
+  // the previous scratch may still be read by queued kernels of this context:
+  // hipFree synchronises the device first
+  (void)hipFree(ctx->d_big);
+  ctx->d_big = nullptr;
+  ctx->big_bytes = 0;
+  if (hipMalloc(&ctx->d_big, bytes) != hipSuccess) return CRDT_EHIP;
+  ctx->big_bytes = bytes;
+  return CRDT_OK;
+}
+
 extern "C" {
 
 int crdt_abi_version(void) { return CRDT_ABI_VERSION; }
@@ -94,6 +106,7 @@ int crdt_ctx_destroy(crdt_ctx* ctx) {
   if (!ctx) return CRDT_EINVAL;
   (void)hipSetDevice(ctx->device);
   (void)crdt_comm_destroy(ctx);
+  (void)hipFree(ctx->d_big);
   (void)hipFree(ctx->d_arena);
   (void)hipFree(ctx->d_status);
   delete ctx;
@@ -407,10 +420,12 @@ int crdt_orswot_from_bincode(crdt_ctx* ctx, const uint8_t* d_blobs, size_t blob_
       !aligned16(d_out))
     return CRDT_EINVAL;
   int rc = set_device(ctx);
-  if (rc) return rc;
+  const size_t big = launch_apply_huge_scratch_bytes() > launch_bincode_big_scratch_bytes()
+                         ? launch_apply_huge_scratch_bytes() : launch_bincode_big_scratch_bytes();
+  if (rc || (rc = ctx_big_scratch(ctx, big))) return rc;
   return launch_bincode_ingest(d_blobs, blob_bytes, d_blob_off, d_blob_len, n_obj, actor_bytes, member_bytes,
                                n_actors, flags, nullptr, d_out, d_out_off, out_bytes, ctx->d_status, ctx->d_ctl, S(stream),
-                               ctx->variant == 301 ? ctx->d_list : nullptr);
+                               ctx->variant == 301 ? ctx->d_list : nullptr, ctx->d_list, ctx->list_cap, ctx->d_big);
 }
 
 int crdt_orswot_bincode_sizes(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32_t n_actors, uint32_t flags,
@@ -448,11 +463,14 @@ int crdt_orswot_apply(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_o
   if (ops->n_clk && (!ops->clk_act || !ops->clk_ctr)) return CRDT_EINVAL;
   int rc = set_device(ctx);
   if (rc) return rc;
+  const size_t big = launch_apply_huge_scratch_bytes() > launch_bincode_big_scratch_bytes()
+                         ? launch_apply_huge_scratch_bytes() : launch_bincode_big_scratch_bytes();
+  if ((rc = ctx_big_scratch(ctx, big))) return rc;
   return launch_orswot_apply(self->base, self->bytes, self->off, self->n_obj, ops->obj_end, ops->kind, ops->member,
                              ops->actor, ops->counter, ops->clk_end, ops->clk_act, ops->clk_ctr, ops->n_ops, ops->n_clk,
                              n_actors, flags,
                              d_out, d_out_off, out_bytes, ctx->d_status, ctx->d_ctl, ctx->d_list, ctx->list_cap,
-                             S(stream));
+                             ctx->d_big, S(stream));
 }
 
 int crdt_vclock_partial_cmp(crdt_ctx* ctx, const uint64_t* d_a, const uint64_t* d_b, size_t n, uint32_t n_actors,

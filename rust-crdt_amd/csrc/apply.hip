@@ -34,8 +34,10 @@ constexpr uint32_t kAW = 64;
 // Workspace capacities. Every object is first run in the small workspace
 // (8 KB of LDS: ~20 resident waves per CU); an object that outgrows it is
 // listed and redone from its input in the large one (16 KB).
-template <uint32_t CK, uint32_t MEM, uint32_t DOT, uint32_t DEF, uint32_t FDOT, uint32_t FMEM, uint32_t TMP>
+template <uint32_t CK, uint32_t MEM, uint32_t DOT, uint32_t DEF, uint32_t FDOT, uint32_t FMEM, uint32_t TMP,
+          bool G = false>
 struct Caps {
+  static constexpr bool kG = G;            // the workspace lives in HBM (hand-offs wait for stores)
   static constexpr uint32_t kCk = CK;      // top clock: dense slots (n_actors <= kCk) or sparse entries
   static constexpr uint32_t kMem = MEM;    // members
   static constexpr uint32_t kDot = DOT;    // member dots
@@ -46,7 +48,12 @@ struct Caps {
 };
 using SmallCaps = Caps<64, 64, 256, 16, 128, 128, 64>;
 using BigCaps = Caps<128, 128, 512, 32, 256, 256, 128>;
+// the third tier: a workspace in HBM (one per wave of a 64-wave launch) for
+// objects past BigCaps — member clocks of any length up to kCk entries
+using HugeCaps = Caps<2048, 4096, 16384, 256, 4096, 4096, 2048, true>;
+constexpr uint32_t kApHugeWaves = 64;
 constexpr uint64_t kApPending = 1ull << 63;  // out_off flag: object left for the large workspace
+constexpr uint64_t kApPendingHuge = 1ull << 62;  // ... left for the HBM workspace
 constexpr uint64_t kApOpBytesDense = 32;   // output bytes reserved per op, dense top clocks
 constexpr uint64_t kApOpBytesSparse = 48;  // ... CSR top clocks (a new clock entry: +12 B)
 
@@ -72,10 +79,19 @@ struct Cnt {
   uint32_t clk, mem, dot, def, fdot, fmem, tmp;
 };
 
+// hand-off between the lanes of the wave through the workspace: LDS, or
+// (G) HBM, whose stores must have completed before another lane reads
+template <bool G = false>
 __device__ __forceinline__ void ap_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if constexpr (G) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
 }
 __device__ __forceinline__ uint32_t ap_uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t ap_uni64(uint64_t v) {
@@ -90,7 +106,7 @@ __device__ __forceinline__ uint32_t ap_sum(uint32_t v) {
 
 // a[pos..n) -> a[pos+cnt..n+cnt): chunks from the top, so no chunk's stores
 // land on a later chunk's loads
-template <class T>
+template <bool G = false, class T>
 __device__ void ins_gap(T* a, uint32_t n, uint32_t pos, uint32_t cnt, uint32_t lane) {
   for (int32_t base = (int32_t)n; base > (int32_t)pos; base -= (int32_t)kAW) {
     const int32_t i = base - 1 - (int32_t)lane;
@@ -99,10 +115,10 @@ __device__ void ins_gap(T* a, uint32_t n, uint32_t pos, uint32_t cnt, uint32_t l
       a[i + cnt] = v;
     }
   }
-  ap_sync();
+  ap_sync<G>();
 }
 // a[pos+cnt..n) -> a[pos..n-cnt)
-template <class T>
+template <bool G = false, class T>
 __device__ void del_gap(T* a, uint32_t n, uint32_t pos, uint32_t cnt, uint32_t lane) {
   for (uint32_t base = pos; base + cnt < n; base += kAW) {
     const uint32_t i = base + lane;
@@ -111,12 +127,12 @@ __device__ void del_gap(T* a, uint32_t n, uint32_t pos, uint32_t cnt, uint32_t l
       a[i] = v;
     }
   }
-  ap_sync();
+  ap_sync<G>();
 }
-template <class T>
+template <bool G = false, class T>
 __device__ void add_range(T* a, uint32_t b, uint32_t e, T d, uint32_t lane) {
   for (uint32_t i = b + lane; i < e; i += kAW) a[i] += d;
-  ap_sync();
+  ap_sync<G>();
 }
 // # of a[b..e) < x (a sorted or not: a plain count)
 template <class T>
@@ -154,32 +170,53 @@ __device__ void entry_subtract(Ws<C>& w, Cnt& c, uint64_t m, uint32_t lane) {
   const uint32_t pos = count_less(w.key, 0u, c.mem, m, lane);
   if (pos >= c.mem || w.key[pos] != m) return;
   const uint32_t b = pos ? w.dend[pos - 1] : 0u, e = w.dend[pos], n = e - b;
-  // the run has <= C::kCk dots (one per actor): two per lane at most
-  uint32_t x0 = 0, x1 = 0;
-  uint64_t v0 = 0, v1 = 0;
-  const bool h0 = lane < n, h1 = lane + kAW < n;
-  if (h0) { x0 = w.dact[b + lane]; v0 = w.dctr[b + lane]; }
-  if (h1) { x1 = w.dact[b + kAW + lane]; v1 = w.dctr[b + kAW + lane]; }
-  const bool k0 = h0 && !(list_get(w.tact, w.tctr, c.tmp, x0) >= v0);
-  const bool k1 = h1 && !(list_get(w.tact, w.tctr, c.tmp, x1) >= v1);
-  const uint64_t K0 = __ballot(k0), K1 = __ballot(k1);
-  const uint32_t kept = (uint32_t)__popcll(K0) + (uint32_t)__popcll(K1);
-  if (kept == n) return;
-  ap_sync();
-  const uint32_t r0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(K0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)K0, 0u));
-  const uint32_t r1 = (uint32_t)__popcll(K0) +
-                      __builtin_amdgcn_mbcnt_hi((uint32_t)(K1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)K1, 0u));
-  if (k0) { w.dact[b + r0] = x0; w.dctr[b + r0] = v0; }
-  if (k1) { w.dact[b + r1] = x1; w.dctr[b + r1] = v1; }
-  ap_sync();
+  uint32_t kept = 0;
+  if constexpr (C::kCk > 2u * kAW) {
+    // the HBM workspace: runs of any length, compacted in place 64 dots at a
+    // time (a chunk's writes land at or below its own reads, never on a later
+    // chunk's)
+    for (uint32_t base = 0; base < n; base += kAW) {
+      const bool h = base + lane < n;
+      uint32_t x = 0;
+      uint64_t v = 0;
+      if (h) { x = w.dact[b + base + lane]; v = w.dctr[b + base + lane]; }
+      const bool k = h && !(list_get(w.tact, w.tctr, c.tmp, x) >= v);
+      const uint64_t K = __ballot(k);
+      ap_sync<C::kG>();
+      const uint32_t r = kept + __builtin_amdgcn_mbcnt_hi((uint32_t)(K >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)K, 0u));
+      if (k && kept + (uint32_t)__popcll(K) < n + 1u) { w.dact[b + r] = x; w.dctr[b + r] = v; }
+      kept += (uint32_t)__popcll(K);
+      ap_sync<C::kG>();
+    }
+    if (kept == n) return;
+  } else {
+    // the run has <= C::kCk dots (one per actor): two per lane at most
+    uint32_t x0 = 0, x1 = 0;
+    uint64_t v0 = 0, v1 = 0;
+    const bool h0 = lane < n, h1 = lane + kAW < n;
+    if (h0) { x0 = w.dact[b + lane]; v0 = w.dctr[b + lane]; }
+    if (h1) { x1 = w.dact[b + kAW + lane]; v1 = w.dctr[b + kAW + lane]; }
+    const bool k0 = h0 && !(list_get(w.tact, w.tctr, c.tmp, x0) >= v0);
+    const bool k1 = h1 && !(list_get(w.tact, w.tctr, c.tmp, x1) >= v1);
+    const uint64_t K0 = __ballot(k0), K1 = __ballot(k1);
+    kept = (uint32_t)__popcll(K0) + (uint32_t)__popcll(K1);
+    if (kept == n) return;
+    ap_sync<C::kG>();
+    const uint32_t r0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(K0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)K0, 0u));
+    const uint32_t r1 = (uint32_t)__popcll(K0) +
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(K1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)K1, 0u));
+    if (k0) { w.dact[b + r0] = x0; w.dctr[b + r0] = v0; }
+    if (k1) { w.dact[b + r1] = x1; w.dctr[b + r1] = v1; }
+    ap_sync<C::kG>();
+  }
   const uint32_t drop = n - kept;
-  del_gap(w.dact, c.dot, b + kept, drop, lane);
-  del_gap(w.dctr, c.dot, b + kept, drop, lane);
+  del_gap<C::kG>(w.dact, c.dot, b + kept, drop, lane);
+  del_gap<C::kG>(w.dctr, c.dot, b + kept, drop, lane);
   c.dot -= drop;
-  add_range(w.dend, pos, c.mem, 0u - drop, lane);
+  add_range<C::kG>(w.dend, pos, c.mem, 0u - drop, lane);
   if (kept == 0u) {  // an empty member clock is removed (src/orswot.rs:206-208)
-    del_gap(w.key, c.mem, pos, 1u, lane);
-    del_gap(w.dend, c.mem, pos, 1u, lane);
+    del_gap<C::kG>(w.key, c.mem, pos, 1u, lane);
+    del_gap<C::kG>(w.dend, c.mem, pos, 1u, lane);
     c.mem -= 1u;
   }
 }
@@ -211,27 +248,27 @@ __device__ int deferred_add(Ws<C>& w, Cnt& c, uint64_t m, uint32_t lane) {
     const uint32_t r = count_less(w.fkey, ms, me, m, lane);
     if (ms + r < me && w.fkey[ms + r] == m) return 0;  // already in the set
     if (c.fmem + 1u > C::kFMem) return CRDT_ECAPACITY;
-    ins_gap(w.fkey, c.fmem, ms + r, 1u, lane);
+    ins_gap<C::kG>(w.fkey, c.fmem, ms + r, 1u, lane);
     if (lane == 0u) w.fkey[ms + r] = m;
-    ap_sync();
-    add_range(w.fmend, k, c.def, 1u, lane);
+    ap_sync<C::kG>();
+    add_range<C::kG>(w.fmend, k, c.def, 1u, lane);
     c.fmem += 1u;
     return 0;
   }
   if (c.def + 1u > C::kDef || c.fdot + c.tmp > C::kFDot || c.fmem + 1u > C::kFMem) return CRDT_ECAPACITY;
   const uint32_t kk = ap_count(lane < c.def && cm < 0);  // clocks ordered before tmp
   const uint32_t o = kk ? w.fdend[kk - 1] : 0u, om = kk ? w.fmend[kk - 1] : 0u;
-  ins_gap(w.fact, c.fdot, o, c.tmp, lane);
-  ins_gap(w.fctr, c.fdot, o, c.tmp, lane);
+  ins_gap<C::kG>(w.fact, c.fdot, o, c.tmp, lane);
+  ins_gap<C::kG>(w.fctr, c.fdot, o, c.tmp, lane);
   for (uint32_t i = lane; i < c.tmp; i += kAW) { w.fact[o + i] = w.tact[i]; w.fctr[o + i] = w.tctr[i]; }
-  ins_gap(w.fkey, c.fmem, om, 1u, lane);
+  ins_gap<C::kG>(w.fkey, c.fmem, om, 1u, lane);
   if (lane == 0u) w.fkey[om] = m;
-  ins_gap(w.fdend, c.def, kk, 1u, lane);
-  ins_gap(w.fmend, c.def, kk, 1u, lane);
+  ins_gap<C::kG>(w.fdend, c.def, kk, 1u, lane);
+  ins_gap<C::kG>(w.fmend, c.def, kk, 1u, lane);
   if (lane == 0u) { w.fdend[kk] = o + c.tmp; w.fmend[kk] = om + 1u; }
-  ap_sync();
-  add_range(w.fdend, kk + 1u, c.def + 1u, c.tmp, lane);
-  add_range(w.fmend, kk + 1u, c.def + 1u, 1u, lane);
+  ap_sync<C::kG>();
+  add_range<C::kG>(w.fdend, kk + 1u, c.def + 1u, c.tmp, lane);
+  add_range<C::kG>(w.fmend, kk + 1u, c.def + 1u, 1u, lane);
   c.def += 1u;
   c.fdot += c.tmp;
   c.fmem += 1u;
@@ -247,23 +284,23 @@ __device__ void apply_deferred(Ws<C>& w, Cnt& c, bool sparse, uint32_t lane) {
     const uint32_t ms = k ? w.fmend[k - 1] : 0u, me = w.fmend[k];
     for (uint32_t i = lane; i < e - b; i += kAW) { w.tact[i] = w.fact[b + i]; w.tctr[i] = w.fctr[b + i]; }
     c.tmp = e - b;
-    ap_sync();
+    ap_sync<C::kG>();
     for (uint32_t j = ms; j < me; ++j) entry_subtract(w, c, w.fkey[j], lane);
     const bool applied = tmp_le_clock(w, c, sparse, lane);
     if (lane == 0u) w.dead[k] = applied ? 1u : 0u;
-    ap_sync();
+    ap_sync<C::kG>();
   }
   for (int32_t k = (int32_t)c.def - 1; k >= 0; --k) {  // drop the applied ones (top down keeps indices valid)
     if (!w.dead[k]) continue;
     const uint32_t b = k ? w.fdend[k - 1] : 0u, e = w.fdend[k];
     const uint32_t ms = k ? w.fmend[k - 1] : 0u, me = w.fmend[k];
-    del_gap(w.fact, c.fdot, b, e - b, lane);
-    del_gap(w.fctr, c.fdot, b, e - b, lane);
-    del_gap(w.fkey, c.fmem, ms, me - ms, lane);
-    add_range(w.fdend, (uint32_t)k + 1u, c.def, 0u - (e - b), lane);
-    add_range(w.fmend, (uint32_t)k + 1u, c.def, 0u - (me - ms), lane);
-    del_gap(w.fdend, c.def, (uint32_t)k, 1u, lane);
-    del_gap(w.fmend, c.def, (uint32_t)k, 1u, lane);
+    del_gap<C::kG>(w.fact, c.fdot, b, e - b, lane);
+    del_gap<C::kG>(w.fctr, c.fdot, b, e - b, lane);
+    del_gap<C::kG>(w.fkey, c.fmem, ms, me - ms, lane);
+    add_range<C::kG>(w.fdend, (uint32_t)k + 1u, c.def, 0u - (e - b), lane);
+    add_range<C::kG>(w.fmend, (uint32_t)k + 1u, c.def, 0u - (me - ms), lane);
+    del_gap<C::kG>(w.fdend, c.def, (uint32_t)k, 1u, lane);
+    del_gap<C::kG>(w.fmend, c.def, (uint32_t)k, 1u, lane);
     c.fdot -= e - b;
     c.fmem -= me - ms;
     c.def -= 1u;
@@ -289,25 +326,25 @@ __device__ int op_add(Ws<C>& w, Cnt& c, bool sparse, uint32_t A, uint32_t a, uin
   if (pos >= c.mem || w.key[pos] != m) {
     if (c.mem + 1u > C::kMem) return CRDT_ECAPACITY;
     const uint32_t at = pos ? w.dend[pos - 1] : 0u;
-    ins_gap(w.key, c.mem, pos, 1u, lane);
-    ins_gap(w.dend, c.mem, pos, 1u, lane);
+    ins_gap<C::kG>(w.key, c.mem, pos, 1u, lane);
+    ins_gap<C::kG>(w.dend, c.mem, pos, 1u, lane);
     if (lane == 0u) { w.key[pos] = m; w.dend[pos] = at; }
-    ap_sync();
+    ap_sync<C::kG>();
     c.mem += 1u;
   }
   const uint32_t b = pos ? w.dend[pos - 1] : 0u, e = w.dend[pos];
   const uint32_t r = count_less(w.dact, b, e, a, lane);
-  if (e - b + 1u > 2u * kAW) return CRDT_ECAPACITY;  // entry_subtract holds a run in two registers per lane
+  if (C::kCk <= 2u * kAW && e - b + 1u > 2u * kAW) return CRDT_ECAPACITY;  // LDS tiers: a run in two registers per lane
   if (b + r < e && w.dact[b + r] == a) {
     if (lane == 0u && w.dctr[b + r] < ctr) w.dctr[b + r] = ctr;
-    ap_sync();
+    ap_sync<C::kG>();
   } else {
     if (c.dot + 1u > C::kDot) return CRDT_ECAPACITY;
-    ins_gap(w.dact, c.dot, b + r, 1u, lane);
-    ins_gap(w.dctr, c.dot, b + r, 1u, lane);
+    ins_gap<C::kG>(w.dact, c.dot, b + r, 1u, lane);
+    ins_gap<C::kG>(w.dctr, c.dot, b + r, 1u, lane);
     if (lane == 0u) { w.dact[b + r] = a; w.dctr[b + r] = ctr; }
-    ap_sync();
-    add_range(w.dend, pos, c.mem, 1u, lane);
+    ap_sync<C::kG>();
+    add_range<C::kG>(w.dend, pos, c.mem, 1u, lane);
     c.dot += 1u;
   }
   // clock.witness(dot)
@@ -316,15 +353,15 @@ __device__ int op_add(Ws<C>& w, Cnt& c, bool sparse, uint32_t A, uint32_t a, uin
       if (lane == 0u) w.cctr[cpos] = ctr;
     } else {
       if (c.clk + 1u > C::kCk) return CRDT_ECAPACITY;
-      ins_gap(w.cact, c.clk, cpos, 1u, lane);
-      ins_gap(w.cctr, c.clk, cpos, 1u, lane);
+      ins_gap<C::kG>(w.cact, c.clk, cpos, 1u, lane);
+      ins_gap<C::kG>(w.cctr, c.clk, cpos, 1u, lane);
       if (lane == 0u) { w.cact[cpos] = a; w.cctr[cpos] = ctr; }
       c.clk += 1u;
     }
   } else if (lane == 0u) {
     w.cctr[a] = ctr;
   }
-  ap_sync();
+  ap_sync<C::kG>();
   apply_deferred(w, c, sparse, lane);
   return 0;
 }
@@ -514,10 +551,12 @@ __device__ int apply_one(Ws<C>& w, const ApArgs& g, uint64_t o, uint32_t lane) {
       w.fdend[i] = ((const uint32_t*)(r + L.o_fdend))[i];
       w.fmend[i] = ((const uint32_t*)(r + L.o_fmend))[i];
     }
-    ap_sync();
-    bool big = false;
-    for (uint32_t i = lane; i < c.mem; i += kAW) big = big || w.dend[i] - (i ? w.dend[i - 1] : 0u) > 2u * kAW;
-    if (__ballot(big)) rc = CRDT_ECAPACITY;
+    ap_sync<C::kG>();
+    if constexpr (C::kCk <= 2u * kAW) {  // the LDS tiers hold a member's run in two registers per lane
+      bool big = false;
+      for (uint32_t i = lane; i < c.mem; i += kAW) big = big || w.dend[i] - (i ? w.dend[i - 1] : 0u) > 2u * kAW;
+      if (__ballot(big)) rc = CRDT_ECAPACITY;
+    }
   }
   for (uint64_t q = ob; q < oe && !rc; ++q) {  // the object's ops, in order
     const uint32_t qi = (uint32_t)(q - ob) & (kAW - 1u);
@@ -565,7 +604,7 @@ __device__ int apply_one(Ws<C>& w, const ApArgs& g, uint64_t o, uint32_t lane) {
         }
       }
       c.tmp = (uint32_t)(e - b);
-      ap_sync();
+      ap_sync<C::kG>();
       if (__ballot(bad)) { rc = CRDT_ENONCANON; break; }
       rc = op_rm(w, c, sparse, m, lane);
     } else {
@@ -618,14 +657,19 @@ __device__ int apply_one(Ws<C>& w, const ApArgs& g, uint64_t o, uint32_t lane) {
   return rc;
 }
 
-// SMALL: every object in the small workspace; one that outgrows it is listed
-// (and flagged in out_off) instead of failing. Otherwise the large workspace
-// over the listed objects, or over the flagged ones when the list overflowed.
-template <class C, bool SMALL>
-__global__ __launch_bounds__(kAW) void orswot_apply_kernel(ApArgs g) {
-  __shared__ Ws<C> w;
+// TIER 0: every object in the small workspace; one that outgrows it is listed
+// (and flagged in out_off) instead of failing. TIER 1: the large workspace
+// over the listed objects (or over the flagged ones when the list overflowed);
+// one that outgrows it is listed again for TIER 2: the HBM workspace (one per
+// block of a kApHugeWaves-block launch). The two lists are the halves of the
+// context's list: [0, cap/2) with count ctl[0], [cap/2, cap) with ctl[1].
+template <class C, int TIER>
+__global__ __launch_bounds__(kAW) void orswot_apply_kernel(ApArgs g, uint8_t* huge_ws) {
+  __shared__ Ws<C> w_lds[TIER == 2 ? 1 : 1];
+  Ws<C>& w = TIER == 2 ? *(Ws<C>*)(huge_ws + (uint64_t)blockIdx.x * sizeof(Ws<HugeCaps>)) : w_lds[0];
   const uint32_t lane = threadIdx.x;
-  if (SMALL) {
+  const uint32_t half = g.list_cap / 2u;
+  if (TIER == 0) {
     // BlockTickets (sched.h): half the objects by block index, the rest in
     // 4-object atomic tickets (ctl[3]) — one call site, so apply_one is
     // inlined once (two call sites doubled the kernel's VGPRs)
@@ -636,29 +680,41 @@ __global__ __launch_bounds__(kAW) void orswot_apply_kernel(ApArgs g) {
         if (rc == CRDT_ECAPACITY) {
           g.ooff[o] |= kApPending;
           const uint32_t e = atomicAdd(&g.ctl[0], 1u);
-          if (e < g.list_cap) g.list[e] = o;
+          if (e < half) g.list[e] = o;
         } else {
           atomicCAS(g.status, 0, rc);
         }
       }
-      ap_sync();
+      ap_sync<C::kG>();
     }
     return;
   }
-  const uint32_t n = ap_uni(__hip_atomic_load(&g.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const uint64_t flag = TIER == 1 ? kApPending : kApPendingHuge;
+  const uint32_t n = ap_uni(__hip_atomic_load(&g.ctl[TIER - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (n == 0u) return;
-  const bool listed = n <= g.list_cap;
+  const bool listed = n <= half;
+  const uint64_t* lst = g.list + (TIER == 1 ? 0u : half);
   const uint64_t m = listed ? n : g.n_obj;
   for (uint64_t e = blockIdx.x; e < m; e += gridDim.x) {
-    const uint64_t o = listed ? ap_uni64(g.list[e]) : e;
-    if (!listed && !(ap_uni64(g.ooff[o]) & kApPending)) continue;
+    const uint64_t o = listed ? ap_uni64(lst[e]) : e;
+    if (!listed && !(ap_uni64(g.ooff[o]) & flag)) continue;
     const int rc = apply_one<C>(w, g, o, lane);
-    if (rc && lane == 0u) atomicCAS(g.status, 0, rc);
-    ap_sync();
+    if (rc && lane == 0u) {
+      if (TIER == 1 && rc == CRDT_ECAPACITY) {
+        g.ooff[o] |= kApPendingHuge;
+        const uint32_t e2 = atomicAdd(&g.ctl[1], 1u);
+        if (e2 < half) g.list[half + e2] = o;
+      } else {
+        atomicCAS(g.status, 0, rc);
+      }
+    }
+    ap_sync<C::kG>();
   }
 }
 
 }  // namespace
+
+size_t launch_apply_huge_scratch_bytes() { return sizeof(Ws<HugeCaps>) * (size_t)kApHugeWaves; }
 
 int launch_orswot_apply(const uint8_t* sb, uint64_t sbytes, const uint64_t* soff, uint64_t n_obj,
                         const uint64_t* obj_end, const uint32_t* kind, const uint64_t* member, const uint32_t* actor,
@@ -666,8 +722,9 @@ int launch_orswot_apply(const uint8_t* sb, uint64_t sbytes, const uint64_t* soff
                         const uint64_t* clk_ctr, uint64_t n_ops, uint64_t n_clk, uint32_t A, uint32_t flags,
                         uint8_t* out, uint64_t* ooff,
                         uint64_t out_bytes, int* status, uint32_t* ctl, uint64_t* list, uint32_t list_cap,
-                        hipStream_t stream) {
+                        uint8_t* huge_ws, hipStream_t stream) {
   if (n_obj == 0) return CRDT_OK;
+  if (!huge_ws) return CRDT_EINVAL;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   static std::atomic<int> occ_small{0}, occ_big{0};
@@ -679,11 +736,12 @@ int launch_orswot_apply(const uint8_t* sb, uint64_t sbytes, const uint64_t* soff
     }
     return (uint64_t)occ;
   };
-  const void* fs = (const void*)orswot_apply_kernel<SmallCaps, true>;
-  const void* fb = (const void*)orswot_apply_kernel<BigCaps, false>;
+  const void* fs = (const void*)orswot_apply_kernel<SmallCaps, 0>;
+  const void* fb = (const void*)orswot_apply_kernel<BigCaps, 1>;
+  const void* fh = (const void*)orswot_apply_kernel<HugeCaps, 2>;
   ApArgs g{sb, sbytes, soff, n_obj, obj_end, kind, member, actor, counter, clk_end, clk_act, clk_ctr, n_ops, n_clk,
            A, flags, out, ooff, out_bytes, status, ctl, list, list_cap};
-  void* args[] = {&g};
+  void* args[] = {&g, &huge_ws};
   if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;  // ctl[3]: tickets
   const bool dense_big = !(flags & kSparseClock) && A > SmallCaps::kCk;  // nothing fits the small workspace
   if (dense_big) {  // every object in the large workspace: the "list overflowed" path with all objects flagged
@@ -697,6 +755,7 @@ int launch_orswot_apply(const uint8_t* sb, uint64_t sbytes, const uint64_t* soff
   const uint64_t capb = (uint64_t)cus * occ_of(occ_big, fb);
   const uint32_t bb = (uint32_t)(n_obj < capb ? n_obj : capb);
   if (hipLaunchKernel(fb, dim3(bb), dim3(kAW), args, 0, stream) != hipSuccess) return CRDT_EHIP;
+  if (hipLaunchKernel(fh, dim3(kApHugeWaves), dim3(kAW), args, 0, stream) != hipSuccess) return CRDT_EHIP;
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 

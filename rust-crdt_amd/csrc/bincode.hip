@@ -35,25 +35,36 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 constexpr uint32_t kBcWave = 64;
 constexpr uint32_t kBcWaves = 4;        // waves per block
 constexpr uint32_t kBcStage = 4096;     // LDS window per wave (blob for ingest, blob for egest)
-constexpr uint32_t kBcMaxMem = 256;     // members per object on the ingest path
-constexpr uint32_t kBcMaxDef = 64;      // deferred clocks per object on the ingest path
-
-// per-wave ingest scratch (bytes); the walk writes only the first kXWalk bytes
-constexpr uint32_t kXPm = 0;                          // u32 member entry position [kBcMaxMem]
-constexpr uint32_t kXLm = kXPm + 4 * kBcMaxMem;       // u32 member dot count
-constexpr uint32_t kXPd = kXLm + 4 * kBcMaxMem;       // u32 deferred clock position (its length word)
-constexpr uint32_t kXLd = kXPd + 4 * kBcMaxDef;       // u32 deferred clock entries
-constexpr uint32_t kXPs = kXLd + 4 * kBcMaxDef;       // u32 deferred set position (its length word)
-constexpr uint32_t kXLs = kXPs + 4 * kBcMaxDef;       // u32 deferred set size
-constexpr uint32_t kXWalk = kXLs + 4 * kBcMaxDef;     // 3 072 B
-constexpr uint32_t kXRm = kXWalk;                     // u32 member rank
-constexpr uint32_t kXKc = kXRm;                       // u64 dense top clock scatter (before the ranking)
-constexpr uint32_t kXSm = kXRm + 4 * kBcMaxMem;       // u32 dot counts / offsets in sorted order
-constexpr uint32_t kXSd = kXSm + 4 * kBcMaxMem;       // u32 sorted deferred clock entries -> offsets
-constexpr uint32_t kXSs = kXSd + 4 * kBcMaxDef;       // u32 sorted deferred set sizes -> offsets
-constexpr uint32_t kXRd = kXSs + 4 * kBcMaxDef;       // u32 deferred rank
-constexpr uint32_t kXBytes = kXRd + 4 * kBcMaxDef;    // 5 888 B
-static_assert(8 * kBcMaxMem <= kXSd - kXKc, "dense clock scatter fits the rank + offset arrays");
+// Ingest scratch of one wave (bytes), for objects of up to MEM members and DEF
+// deferred clocks: the walk writes only the first `Walk` bytes. The fast path
+// keeps it in LDS (XS: 256 members, 64 deferred clocks); objects past that are
+// listed and decoded by the large-object kernel from an HBM scratch (XB).
+template <uint32_t MEM, uint32_t DEF, bool GLOBAL>
+struct XLay {
+  static constexpr uint32_t kMem = MEM, kDef = DEF;
+  static constexpr bool kGlobal = GLOBAL;  // scratch in HBM (its hand-offs need vmcnt waits)
+  static constexpr uint32_t Pm = 0;                 // u32 member entry position [MEM]
+  static constexpr uint32_t Lm = Pm + 4 * MEM;      // u32 member dot count
+  static constexpr uint32_t Pd = Lm + 4 * MEM;      // u32 deferred clock position (its length word)
+  static constexpr uint32_t Ld = Pd + 4 * DEF;      // u32 deferred clock entries
+  static constexpr uint32_t Ps = Ld + 4 * DEF;      // u32 deferred set position (its length word)
+  static constexpr uint32_t Ls = Ps + 4 * DEF;      // u32 deferred set size
+  static constexpr uint32_t Walk = Ls + 4 * DEF;
+  static constexpr uint32_t Rm = Walk;              // u32 member rank
+  static constexpr uint32_t Kc = Rm;                // u64 dense top clock scatter (before the ranking)
+  static constexpr uint32_t Sm = Rm + 4 * MEM;      // u32 dot counts / offsets in sorted order
+  static constexpr uint32_t Sd = Sm + 4 * MEM;      // u32 sorted deferred clock entries -> offsets
+  static constexpr uint32_t Ss = Sd + 4 * DEF;      // u32 sorted deferred set sizes -> offsets
+  static constexpr uint32_t Rd = Ss + 4 * DEF;      // u32 deferred rank
+  static constexpr uint32_t Kk = Rd + 4 * DEF;      // u64 member keys (HBM scratch only: the ranking's operands)
+  static constexpr uint32_t Bytes = GLOBAL ? Kk + 8 * MEM : Kk;
+  static_assert(8 * MEM <= Sd - Kc, "dense clock scatter fits the rank + offset arrays");
+};
+using XS = XLay<256, 64, false>;      // 5 888 B of LDS per wave
+using XB = XLay<16384, 1024, true>;   // 409 600 B of HBM per large-object wave
+constexpr uint32_t kXWalk = XS::Walk;
+constexpr uint32_t kXBytes = XS::Bytes;
+constexpr uint32_t kBcBigWaves = 64;      // waves (one per block) of the large-object decode
 
 // Diagnostic phase stamps (ST builds only, variant 301): s_memtime deltas.
 struct BcStamps {
@@ -80,6 +91,19 @@ __device__ __forceinline__ void bc_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// hand-off between the lanes of one wave through the scratch: LDS (the fast
+// path) or HBM (the large-object path, whose stores must have landed)
+template <class XL>
+__device__ __forceinline__ void bc_xsync() {
+  if constexpr (XL::kGlobal) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  } else {
+    bc_sync();
+  }
 }
 
 __device__ __forceinline__ uint32_t bc_uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -163,7 +187,7 @@ struct BcWalk {
 };
 
 // Wave-uniform walk over one blob: bounds, counts, entry positions (into X).
-template <class SRC>
+template <class XL, class SRC>
 __device__ __forceinline__ BcWalk bc_walk(const SRC& B, uint64_t len, uint32_t wa, uint32_t wm, uint32_t A, uint8_t* X,
                           uint32_t lane) {
   BcWalk w{0, 0, 0, 0, 0, 0, 0};
@@ -175,7 +199,7 @@ __device__ __forceinline__ BcWalk bc_walk(const SRC& B, uint64_t len, uint32_t w
   uint64_t p = 8u + nclk * sa;
   const uint64_t nent = bc_uni64(B.get(p, 8));
   p += 8u;
-  if (nent > kBcMaxMem) { w.err = CRDT_ECAPACITY; return w; }
+  if (nent > XL::kMem) { w.err = CRDT_ECAPACITY; return w; }
   w.n_mem = (uint32_t)nent;
   if constexpr (SRC::kWindow) {
     // the chain of entry positions is the only serial part: one LDS read and
@@ -192,19 +216,19 @@ __device__ __forceinline__ BcWalk bc_walk(const SRC& B, uint64_t len, uint32_t w
         const uint32_t l = B.lo32(q + wm < L32 ? q + wm : L32);
         q += step + (l < 0xFFFFu ? l : 0xFFFFu) * (uint32_t)sa;
       }
-      if (lane < ne) ((uint32_t*)(X + kXPm))[e0 + lane] = mine;
+      if (lane < ne) ((uint32_t*)(X + XL::Pm))[e0 + lane] = mine;
     }
-    bc_sync();
+    bc_xsync<XL>();
     for (uint32_t e = lane; e < (uint32_t)nent; e += kBcWave) {  // the full 64-bit lengths, in parallel
-      const uint32_t pe = ((const uint32_t*)(X + kXPm))[e];
+      const uint32_t pe = ((const uint32_t*)(X + XL::Pm))[e];
       const uint64_t l = B.get(pe + wm < L32 ? pe + wm : L32, 8);
-      ((uint32_t*)(X + kXLm))[e] = (l >> 32) ? 0xFFFFFFFFu : (uint32_t)l;
+      ((uint32_t*)(X + XL::Lm))[e] = (l >> 32) ? 0xFFFFFFFFu : (uint32_t)l;
     }
-    bc_sync();
+    bc_xsync<XL>();
     bool bad = false;
     uint32_t nd = 0;
     for (uint32_t e = lane; e < (uint32_t)nent; e += kBcWave) {
-      const uint32_t pe = ((const uint32_t*)(X + kXPm))[e], l = ((const uint32_t*)(X + kXLm))[e];
+      const uint32_t pe = ((const uint32_t*)(X + XL::Pm))[e], l = ((const uint32_t*)(X + XL::Lm))[e];
       bad = bad || l == 0u || l > A || (uint64_t)pe + wm + 8u + (uint64_t)l * sa > len;
       nd += l;
     }
@@ -218,8 +242,8 @@ __device__ __forceinline__ BcWalk bc_walk(const SRC& B, uint64_t len, uint32_t w
       const uint64_t l = bc_uni64(B.get(p + wm, 8));
       if (l == 0u || l > A || l * sa > len - (p + wm + 8u)) { w.err = CRDT_ENONCANON; return w; }
       if (lane == (e & (kBcWave - 1u))) {
-        ((uint32_t*)(X + kXPm))[e] = (uint32_t)p;
-        ((uint32_t*)(X + kXLm))[e] = (uint32_t)l;
+        ((uint32_t*)(X + XL::Pm))[e] = (uint32_t)p;
+        ((uint32_t*)(X + XL::Lm))[e] = (uint32_t)l;
       }
       w.n_dot += (uint32_t)l;
       p += wm + 8u + l * sa;
@@ -228,7 +252,7 @@ __device__ __forceinline__ BcWalk bc_walk(const SRC& B, uint64_t len, uint32_t w
   if (p + 8u > len) { w.err = CRDT_ENONCANON; return w; }
   const uint64_t ndef = bc_uni64(B.get(p, 8));
   p += 8u;
-  if (ndef > kBcMaxDef) { w.err = CRDT_ECAPACITY; return w; }
+  if (ndef > XL::kDef) { w.err = CRDT_ECAPACITY; return w; }
   w.n_def = (uint32_t)ndef;
   for (uint32_t d = 0; d < (uint32_t)ndef; ++d) {
     if (p + 8u > len) { w.err = CRDT_ENONCANON; return w; }
@@ -239,10 +263,10 @@ __device__ __forceinline__ BcWalk bc_walk(const SRC& B, uint64_t len, uint32_t w
     const uint64_t ls = bc_uni64(B.get(q, 8));
     if (ls == 0u || ls > len || ls * wm > len - (q + 8u)) { w.err = CRDT_ENONCANON; return w; }
     if (lane == (d & (kBcWave - 1u))) {
-      ((uint32_t*)(X + kXPd))[d] = (uint32_t)p;
-      ((uint32_t*)(X + kXLd))[d] = (uint32_t)lc;
-      ((uint32_t*)(X + kXPs))[d] = (uint32_t)q;
-      ((uint32_t*)(X + kXLs))[d] = (uint32_t)ls;
+      ((uint32_t*)(X + XL::Pd))[d] = (uint32_t)p;
+      ((uint32_t*)(X + XL::Ld))[d] = (uint32_t)lc;
+      ((uint32_t*)(X + XL::Ps))[d] = (uint32_t)q;
+      ((uint32_t*)(X + XL::Ls))[d] = (uint32_t)ls;
     }
     w.n_def_dot += (uint32_t)lc;
     w.n_def_mem += (uint32_t)ls;
@@ -254,7 +278,7 @@ __device__ __forceinline__ BcWalk bc_walk(const SRC& B, uint64_t len, uint32_t w
 
 // The deferred part of the walk alone (positions into X), from the deferred
 // map's length word at p; counts and bounds were checked by the lane walk.
-template <class SRC>
+template <class XL = XS, class SRC>
 __device__ __forceinline__ void bc_walk_deferred(const SRC& B, uint64_t p, uint32_t wa, uint32_t wm, uint8_t* X,
                                                  uint32_t lane) {
   const uint64_t sa = wa + 8u;
@@ -265,39 +289,44 @@ __device__ __forceinline__ void bc_walk_deferred(const SRC& B, uint64_t p, uint3
     const uint64_t q = p + 8u + lc * sa;
     const uint64_t ls = bc_uni64(B.get(q, 8));
     if (lane == (d & (kBcWave - 1u))) {
-      ((uint32_t*)(X + kXPd))[d] = (uint32_t)p;
-      ((uint32_t*)(X + kXLd))[d] = (uint32_t)lc;
-      ((uint32_t*)(X + kXPs))[d] = (uint32_t)q;
-      ((uint32_t*)(X + kXLs))[d] = (uint32_t)ls;
+      ((uint32_t*)(X + XL::Pd))[d] = (uint32_t)p;
+      ((uint32_t*)(X + XL::Ld))[d] = (uint32_t)lc;
+      ((uint32_t*)(X + XL::Ps))[d] = (uint32_t)q;
+      ((uint32_t*)(X + XL::Ls))[d] = (uint32_t)ls;
     }
     p = q + 8u + ls * wm;
   }
 }
 
-// Exclusive prefix sum, in place, of n (<= 4 * 64) u32 at S.
+// Exclusive prefix sum, in place, of n u32 at S (256 per round, carried).
+template <class XL = XS>
 __device__ void bc_scan_excl(uint32_t* S, uint32_t n, uint32_t lane) {
-  uint32_t v[4], s = 0;
+  uint32_t carry = 0;
+  for (uint32_t b = 0; b < n; b += 4u * kBcWave) {
+    uint32_t v[4], s = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < 4u; ++k) {
-    const uint32_t i = 4u * lane + k;
-    v[k] = i < n ? S[i] : 0u;
-    s += v[k];
-  }
-  const uint32_t incl = bc_scan_incl(s, lane);
-  uint32_t run = incl - s;
-  bc_sync();
+    for (uint32_t k = 0; k < 4u; ++k) {
+      const uint32_t i = b + 4u * lane + k;
+      v[k] = i < n ? S[i] : 0u;
+      s += v[k];
+    }
+    const uint32_t incl = bc_scan_incl(s, lane);
+    uint32_t run = carry + incl - s;
+    carry += __shfl(incl, (int)(kBcWave - 1u), kBcWave);
+    bc_xsync<XL>();
 #pragma unroll
-  for (uint32_t k = 0; k < 4u; ++k) {
-    const uint32_t i = 4u * lane + k;
-    if (i < n) S[i] = run;
-    run += v[k];
+    for (uint32_t k = 0; k < 4u; ++k) {
+      const uint32_t i = b + 4u * lane + k;
+      if (i < n) S[i] = run;
+      run += v[k];
+    }
+    bc_xsync<XL>();
   }
-  bc_sync();
 }
 
 // Decode one blob (already walked) into its canonical record at O. Returns 0
 // or a CRDT_E* code (the record is then not valid).
-template <bool ST = false, class SRC>
+template <bool ST = false, class XL = XS, class SRC>
 __device__ __forceinline__ int bc_write_record(const SRC& B, const BcWalk& w, uint32_t wa, uint32_t wm, uint32_t A, bool sparse,
                                uint8_t* X, uint8_t* O, uint32_t lane, BcStamps* st = nullptr) {
   RecLayout L;
@@ -307,11 +336,11 @@ __device__ __forceinline__ int bc_write_record(const SRC& B, const BcWalk& w, ui
   // ---- top clock: BTreeMap order = strictly increasing actors. Dense: the
   // counters are scattered into LDS (the member-key area, free until the
   // ranking) and the A slots written once, coalesced
-  const bool lds_clk = !sparse && A <= kBcMaxMem;
-  uint64_t* Kc = (uint64_t*)(X + kXKc);
+  const bool lds_clk = !sparse && A <= XL::kMem;
+  uint64_t* Kc = (uint64_t*)(X + XL::Kc);
   if (lds_clk) {
     for (uint32_t a = lane; a < A; a += kBcWave) Kc[a] = 0ull;
-    bc_sync();
+    bc_xsync<XL>();
   } else if (!sparse) {
     for (uint32_t a = lane; a < A; a += kBcWave) ((uint64_t*)(O + L.o_clk))[a] = 0ull;
     __threadfence_block();
@@ -332,18 +361,18 @@ __device__ __forceinline__ int bc_write_record(const SRC& B, const BcWalk& w, ui
     }
   }
   if (lds_clk) {
-    bc_sync();
+    bc_xsync<XL>();
     for (uint32_t a = lane; a < A; a += kBcWave) ((uint64_t*)(O + L.o_clk))[a] = Kc[a];
-    bc_sync();
+    bc_xsync<XL>();
   }
   if (sparse && lane == 0u && (w.n_clk & 1u)) *(uint32_t*)(O + L.o_cact + 4u * w.n_clk) = 0u;
   bc_mark<ST>(st, 2);
   // ---- members: rank by key (HashMap order is arbitrary), dot offsets in key order
-  uint32_t* Pm = (uint32_t*)(X + kXPm);
-  uint32_t* Lm = (uint32_t*)(X + kXLm);
-  uint32_t* Rm = (uint32_t*)(X + kXRm);
-  uint32_t* Sm = (uint32_t*)(X + kXSm);
-  bc_sync();
+  uint32_t* Pm = (uint32_t*)(X + XL::Pm);
+  uint32_t* Lm = (uint32_t*)(X + XL::Lm);
+  uint32_t* Rm = (uint32_t*)(X + XL::Rm);
+  uint32_t* Sm = (uint32_t*)(X + XL::Sm);
+  bc_xsync<XL>();
   if (w.n_mem <= kBcWave) {  // every key in one register: broadcast by readlane
     const uint64_t k = lane < w.n_mem ? B.get(Pm[lane], wm) : 0ull;
     uint32_t r = 0, eq = 0;
@@ -355,24 +384,31 @@ __device__ __forceinline__ int bc_write_record(const SRC& B, const BcWalk& w, ui
     if (lane < w.n_mem) {
       bad = bad || eq != 1u;
       Rm[lane] = r;
-      Sm[r < kBcMaxMem ? r : 0u] = Lm[lane];
+      Sm[r < XL::kMem ? r : 0u] = Lm[lane];
     }
   } else {
+    // HBM scratch: the keys are read out of the blob once (u64 array), so the
+    // quadratic ranking reads 8-B words, not wm byte loads per comparison
+    uint64_t* Kk = (uint64_t*)(X + (XL::kGlobal ? XL::Kk : 0u));
+    if constexpr (XL::kGlobal) {
+      for (uint32_t e = lane; e < w.n_mem; e += kBcWave) Kk[e] = B.get(Pm[e], wm);
+      bc_xsync<XL>();
+    }
     for (uint32_t e = lane; e < w.n_mem; e += kBcWave) {
-      const uint64_t k = B.get(Pm[e], wm);
+      const uint64_t k = XL::kGlobal ? Kk[e] : B.get(Pm[e], wm);
       uint32_t r = 0, eq = 0;
       for (uint32_t f = 0; f < w.n_mem; ++f) {
-        const uint64_t kf = B.get(Pm[f], wm);
+        const uint64_t kf = XL::kGlobal ? Kk[f] : B.get(Pm[f], wm);
         r += kf < k ? 1u : 0u;
         eq += kf == k ? 1u : 0u;
       }
       bad = bad || eq != 1u;
       Rm[e] = r;
-      Sm[r < kBcMaxMem ? r : 0u] = Lm[e];
+      Sm[r < XL::kMem ? r : 0u] = Lm[e];
     }
   }
-  bc_sync();
-  bc_scan_excl(Sm, w.n_mem, lane);
+  bc_xsync<XL>();
+  bc_scan_excl<XL>(Sm, w.n_mem, lane);
   bc_mark<ST>(st, 3);
   for (uint32_t e = lane; e < w.n_mem; e += kBcWave) {
     const uint32_t r = Rm[e], d0 = Sm[r], l = Lm[e];
@@ -390,13 +426,13 @@ __device__ __forceinline__ int bc_write_record(const SRC& B, const BcWalk& w, ui
   }
   bc_mark<ST>(st, 4);
   // ---- deferred: clocks sorted in CLOCK ORDER, member sets sorted
-  uint32_t* Pd = (uint32_t*)(X + kXPd);
-  uint32_t* Ld = (uint32_t*)(X + kXLd);
-  uint32_t* Ps = (uint32_t*)(X + kXPs);
-  uint32_t* Ls = (uint32_t*)(X + kXLs);
-  uint32_t* Sd = (uint32_t*)(X + kXSd);
-  uint32_t* Ss = (uint32_t*)(X + kXSs);
-  uint32_t* Rd = (uint32_t*)(X + kXRd);
+  uint32_t* Pd = (uint32_t*)(X + XL::Pd);
+  uint32_t* Ld = (uint32_t*)(X + XL::Ld);
+  uint32_t* Ps = (uint32_t*)(X + XL::Ps);
+  uint32_t* Ls = (uint32_t*)(X + XL::Ls);
+  uint32_t* Sd = (uint32_t*)(X + XL::Sd);
+  uint32_t* Ss = (uint32_t*)(X + XL::Ss);
+  uint32_t* Rd = (uint32_t*)(X + XL::Rd);
   if (w.n_def) {
     for (uint32_t d = lane; d < w.n_def; d += kBcWave) {
       uint32_t r = 0;
@@ -407,12 +443,12 @@ __device__ __forceinline__ int bc_write_record(const SRC& B, const BcWalk& w, ui
         bad = bad || c == 0;  // structurally equal HashMap keys
       }
       Rd[d] = r;
-      Sd[r < kBcMaxDef ? r : 0u] = Ld[d];
-      Ss[r < kBcMaxDef ? r : 0u] = Ls[d];
+      Sd[r < XL::kDef ? r : 0u] = Ld[d];
+      Ss[r < XL::kDef ? r : 0u] = Ls[d];
     }
-    bc_sync();
-    bc_scan_excl(Sd, w.n_def, lane);
-    bc_scan_excl(Ss, w.n_def, lane);
+    bc_xsync<XL>();
+    bc_scan_excl<XL>(Sd, w.n_def, lane);
+    bc_scan_excl<XL>(Ss, w.n_def, lane);
     for (uint32_t d = lane; d < w.n_def; d += kBcWave) {
       const uint32_t r = Rd[d], a0 = Sd[r], m0 = Ss[r], lc = Ld[d], ls = Ls[d];
       ((uint32_t*)(O + L.o_fdend))[r] = a0 + lc;
@@ -453,11 +489,11 @@ __device__ __forceinline__ int bc_write_record(const SRC& B, const BcWalk& w, ui
   return rc;
 }
 
-template <bool WRITE, bool ST = false, class SRC>
+template <bool WRITE, bool ST = false, class XL = XS, class SRC>
 __device__ __forceinline__ int bc_object(const SRC& B, uint64_t o, uint64_t len, uint32_t wa, uint32_t wm, uint32_t A,
                                          bool sparse, uint8_t* X, uint64_t* sizes, uint8_t* out, const uint64_t* ooff,
                                          uint64_t out_bytes, uint32_t lane, BcStamps* st = nullptr) {
-  const BcWalk w = bc_walk(B, len, wa, wm, A, X, lane);
+  const BcWalk w = bc_walk<XL>(B, len, wa, wm, A, X, lane);
   bc_mark<ST>(st, 1);
   if (w.err) return w.err;
   const uint64_t size = record_size64(sparse ? w.n_clk : A, w.n_mem, w.n_dot, w.n_def, w.n_def_dot, w.n_def_mem,
@@ -468,8 +504,8 @@ __device__ __forceinline__ int bc_object(const SRC& B, uint64_t o, uint64_t len,
   }
   const uint64_t oo = ooff[o];
   if ((oo & 15u) || oo > out_bytes || size > out_bytes - oo) return CRDT_ECAPACITY;
-  bc_sync();
-  return bc_write_record<ST>(B, w, wa, wm, A, sparse, X, out + oo, lane, st);
+  bc_xsync<XL>();
+  return bc_write_record<ST, XL>(B, w, wa, wm, A, sparse, X, out + oo, lane, st);
 }
 
 constexpr uint32_t kBcPer = kBcStage / 16u / kBcWave;  // window lines per lane
@@ -615,7 +651,7 @@ __device__ __forceinline__ LaneWalk lane_walk(const uint8_t* blobs, uint64_t blo
   uint64_t p = 8u + nclk * sa;
   const uint64_t nent = lane_get(blobs, blob_bytes, off + p, 8);
   p += 8u;
-  if (nent > kBcMaxMem) { w.err = CRDT_ECAPACITY; return w; }
+  if (nent > XB::kMem) { w.err = CRDT_ECAPACITY; return w; }
   for (uint64_t e = 0; e < nent; ++e) {
     if (p + wm + 8u > len) { w.err = CRDT_ENONCANON; return w; }
     const uint64_t l = lane_get(blobs, blob_bytes, off + p + wm, 8);
@@ -632,7 +668,7 @@ __device__ __forceinline__ LaneWalk lane_walk(const uint8_t* blobs, uint64_t blo
   w.p_def = p;
   const uint64_t ndef = lane_get(blobs, blob_bytes, off + p, 8);
   p += 8u;
-  if (ndef > kBcMaxDef) { w.err = CRDT_ECAPACITY; return w; }
+  if (ndef > XB::kDef) { w.err = CRDT_ECAPACITY; return w; }
   for (uint64_t d = 0; d < ndef; ++d) {
     if (p + 8u > len) { w.err = CRDT_ENONCANON; return w; }
     const uint64_t lc = lane_get(blobs, blob_bytes, off + p, 8);
@@ -674,7 +710,8 @@ __global__ __launch_bounds__(256) void bincode_sizes_lane_kernel(
 __global__ __launch_bounds__(kBcWave * kBcWaves, 4) void bincode_decode_kernel(
     const uint8_t* __restrict__ blobs, uint64_t blob_bytes, const uint64_t* __restrict__ boff,
     const uint64_t* __restrict__ blen, uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags,
-    uint8_t* __restrict__ out, const uint64_t* __restrict__ ooff, uint64_t out_bytes, int* __restrict__ status, uint32_t* __restrict__ ctl) {
+    uint8_t* __restrict__ out, const uint64_t* __restrict__ ooff, uint64_t out_bytes, int* __restrict__ status,
+    uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
   __shared__ v4u st_s[kBcWaves][kBcStage / 16];
   __shared__ v4u sx_s[kBcWaves][kXBytes / 16];
   const uint32_t lane = threadIdx.x & (kBcWave - 1u), wave = threadIdx.x / kBcWave;
@@ -712,7 +749,15 @@ __global__ __launch_bounds__(kBcWave * kBcWaves, 4) void bincode_decode_kernel(
       if (lw.err) atomicCAS(status, 0, lw.err);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // the parked pairs are visible to the whole wave
-    const bool ok = valid && !lw.err;
+    // objects past the LDS scratch (> 256 members or > 64 deferred clocks) are
+    // listed for the large-object kernel (ctl[0]); past the list: CRDT_ECAPACITY
+    const bool big = valid && !lw.err && (lw.n_mem > XS::kMem || lw.n_def > XS::kDef);
+    if (big) {
+      const uint32_t e = atomicAdd(&ctl[0], 1u);
+      if (e < list_cap) list[e] = obj;
+      else atomicCAS(status, 0, CRDT_ECAPACITY);
+    }
+    const bool ok = valid && !lw.err && !big;
     const bool win = ok && len + 32u <= kBcStage;
     const uint64_t a0 = off & ~15ull;
     const uint32_t n16 = win ? (uint32_t)((((off + len + 15u) & ~15ull) - a0) / 16u) : 0u;
@@ -742,8 +787,8 @@ __global__ __launch_bounds__(kBcWave * kBcWaves, 4) void bincode_decode_kernel(
       bc_sync();
       for (uint32_t e = lane; e < w.n_mem; e += kBcWave) {
         const uint64_t pr = keyarea[e];
-        ((uint32_t*)(X + kXPm))[e] = (uint32_t)pr;
-        ((uint32_t*)(X + kXLm))[e] = (uint32_t)(pr >> 32);
+        ((uint32_t*)(X + XS::Pm))[e] = (uint32_t)pr;
+        ((uint32_t*)(X + XS::Lm))[e] = (uint32_t)(pr >> 32);
       }
       int rc;
       if ((wins >> t) & 1ull) {
@@ -769,6 +814,29 @@ __global__ __launch_bounds__(kBcWave * kBcWaves, 4) void bincode_decode_kernel(
     }
   }
 }
+
+// Large objects (listed by the decode pass): one wave per block, the walk and
+// the decode from HBM (Src<false>) with the wave's scratch in HBM (XB: up to
+// 16 384 members and 1 024 deferred clocks per object).
+__global__ __launch_bounds__(kBcWave) void bincode_decode_big_kernel(
+    const uint8_t* __restrict__ blobs, const uint64_t* __restrict__ boff, const uint64_t* __restrict__ blen,
+    uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags, uint8_t* __restrict__ out, const uint64_t* __restrict__ ooff,
+    uint64_t out_bytes, int* __restrict__ status, const uint32_t* __restrict__ ctl, const uint64_t* __restrict__ list,
+    uint32_t list_cap, uint8_t* __restrict__ scratch) {
+  const uint32_t lane = threadIdx.x;
+  uint8_t* X = scratch + (uint64_t)blockIdx.x * XB::Bytes;
+  const bool sparse = (flags & kSparseClock) != 0u;
+  const uint32_t n = bc_uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const uint32_t m = n < list_cap ? n : list_cap;
+  for (uint32_t e = blockIdx.x; e < m; e += gridDim.x) {
+    const uint64_t o = bc_uni64(list[e]);
+    const Src<false> B{blobs + boff[o]};
+    const int rc = bc_object<true, false, XB>(B, o, blen[o], wa, wm, A, sparse, X, nullptr, out, ooff, out_bytes, lane);
+    if (rc && lane == 0u) atomicCAS(status, 0, rc);
+  }
+}
+
+size_t bincode_big_scratch_bytes() { return (size_t)XB::Bytes * kBcBigWaves; }
 
 // ---------------------------------------------------------------- egest
 // Blob writers. LDS window (zeroed first): a field is OR-ed in as the aligned
@@ -1060,10 +1128,12 @@ int launch_bincode_bounds(const uint64_t* blen, uint64_t n_obj, uint32_t wa, uin
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 
+size_t launch_bincode_big_scratch_bytes() { return bincode_big_scratch_bytes(); }
+
 int launch_bincode_ingest(const uint8_t* blobs, uint64_t blob_bytes, const uint64_t* boff, const uint64_t* blen,
                           uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags, uint64_t* sizes,
                           uint8_t* out, const uint64_t* ooff, uint64_t out_bytes, int* status, uint32_t* ctl,
-                          hipStream_t stream, uint64_t* dbg) {
+                          hipStream_t stream, uint64_t* dbg, uint64_t* list, uint32_t list_cap, uint8_t* big_scratch) {
   if (n_obj == 0) return CRDT_OK;
   const uint32_t blocks = bc_blocks(n_obj);
   if (dbg && !sizes) {  // diagnostic: decode pass with phase stamps into dbg (8 u64 per wave)
@@ -1082,8 +1152,11 @@ int launch_bincode_ingest(const uint8_t* blobs, uint64_t blob_bytes, const uint6
     if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;  // ctl[3]: tickets
     static std::atomic<int> occ_d{0};
     const uint32_t rblocks = bc_resident_blocks(n_obj, (const void*)bincode_decode_kernel, occ_d);
+    if (!list || !big_scratch) return CRDT_EINVAL;
     hipLaunchKernelGGL(bincode_decode_kernel, dim3(rblocks), dim3(kBcWave * kBcWaves), 0, stream, blobs, blob_bytes,
-                       boff, blen, n_obj, wa, wm, A, flags, out, ooff, out_bytes, status, ctl);
+                       boff, blen, n_obj, wa, wm, A, flags, out, ooff, out_bytes, status, ctl, list, list_cap);
+    hipLaunchKernelGGL(bincode_decode_big_kernel, dim3(kBcBigWaves), dim3(kBcWave), 0, stream, blobs, boff, blen, wa,
+                       wm, A, flags, out, ooff, out_bytes, status, ctl, list, list_cap, big_scratch);
   }
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }

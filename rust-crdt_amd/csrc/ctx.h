@@ -38,4 +38,11 @@ struct crdt_ctx {
   uint64_t* d_comm_stage = nullptr;  // device staging of the small all-gathers
   uint8_t* d_arena = nullptr;
   size_t arena_bytes = 0;
+  // HBM scratch of the large-object paths (bincode ingest, apply), allocated
+  // on first use
+  uint8_t* d_big = nullptr;
+  size_t big_bytes = 0;
 };
+
+// Ensures ctx->d_big holds at least `bytes` (api.hip).
+int ctx_big_scratch(crdt_ctx* ctx, size_t bytes);

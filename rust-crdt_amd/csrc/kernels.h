@@ -39,10 +39,15 @@ int launch_record_copy(const uint8_t* src, const uint64_t* src_off, const uint64
 
 int launch_bincode_bounds(const uint64_t* blen, uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A,
                           uint32_t flags, uint64_t* bounds, hipStream_t stream);
+// decode (sizes == null): objects past the LDS scratch are listed (list,
+// list_cap) and decoded by a large-object kernel from big_scratch
+// (launch_bincode_big_scratch_bytes()).
 int launch_bincode_ingest(const uint8_t* blobs, uint64_t blob_bytes, const uint64_t* boff, const uint64_t* blen,
                           uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags, uint64_t* sizes,
                           uint8_t* out, const uint64_t* ooff, uint64_t out_bytes, int* status, uint32_t* ctl, hipStream_t stream,
-                          uint64_t* dbg = nullptr);
+                          uint64_t* dbg = nullptr, uint64_t* list = nullptr, uint32_t list_cap = 0,
+                          uint8_t* big_scratch = nullptr);
+size_t launch_bincode_big_scratch_bytes();
 int launch_bincode_egest(const uint8_t* rb, uint64_t rbytes, const uint64_t* roff, uint64_t n_obj, uint32_t A,
                          uint32_t flags, uint32_t wa, uint32_t wm, uint64_t* sizes, uint8_t* out,
                          const uint64_t* ooff, uint64_t out_bytes, int* status, uint32_t* ctl, hipStream_t stream);
@@ -53,7 +58,9 @@ int launch_orswot_apply(const uint8_t* sb, uint64_t sbytes, const uint64_t* soff
                         const uint64_t* clk_ctr, uint64_t n_ops, uint64_t n_clk, uint32_t A, uint32_t flags,
                         uint8_t* out, uint64_t* ooff,
                         uint64_t out_bytes, int* status, uint32_t* ctl, uint64_t* list, uint32_t list_cap,
-                        hipStream_t stream);
+                        uint8_t* huge_ws, hipStream_t stream);
+// HBM workspace of the apply's third tier (objects past the LDS workspaces)
+size_t launch_apply_huge_scratch_bytes();
 
 int launch_vclock_cmp(const uint64_t* a, const uint64_t* b, uint64_t n, uint32_t A, int8_t* out, hipStream_t stream);
 int launch_mvreg_merge(const uint32_t* sn, const uint64_t* sclk, const uint64_t* sval, uint32_t scap,

@@ -174,11 +174,17 @@ def test_malformed_blobs(gpu):
         with pytest.raises(CrdtError) as e:
             gpu.orswot_from_bincode(t, bo, bl, 16, 1, 1)
         assert e.value.code in (-2,), name
+    # past the LDS path's 256 members the large-object kernel decodes it ...
     big = dict(clock={1: 400}, entries={m: [(1, m + 1)] for m in range(300)}, deferred=[])
-    t, bo, bl = _upload_blobs([BC.encode(big, 1, 2)])
+    t, bo, bl = _upload_blobs([g, BC.encode(big, 1, 2, rng=random.Random(4)), g])
+    got = gpu.orswot_from_bincode(t, bo, bl, 16, 1, 2).records()
+    assert got[1] == _rec(big, 16, False)
+    # ... up to 16 384 members (the HBM scratch); past that, CRDT_ECAPACITY
+    huge = dict(clock={1: 20_000}, entries={m: [(1, m + 1)] for m in range(16_385)}, deferred=[])
+    t, bo, bl = _upload_blobs([BC.encode(huge, 1, 2)])
     with pytest.raises(CrdtError) as e:
         gpu.orswot_from_bincode(t, bo, bl, 16, 1, 2)
-    assert e.value.code == -4  # more members than this round's ingest limit
+    assert e.value.code == -4
     # egest: a member key wider than member_bytes
     B = crdts_hip.OrswotBatch.from_records([_rec(dict(clock={1: 1}, entries={300: [(1, 1)]}, deferred=[]), 16,
                                                  False)], 16)
