@@ -239,11 +239,20 @@ __device__ int def_cmp_tmp(const Ws<C>& w, const Cnt& c, uint32_t k) {
 // deferred[tmp] += {m}; returns an error code on capacity overflow
 template <class C>
 __device__ int deferred_add(Ws<C>& w, Cnt& c, uint64_t m, uint32_t lane) {
-  int cm = 1;
-  if (lane < c.def) cm = def_cmp_tmp(w, c, lane);
-  const uint64_t eq = __ballot(lane < c.def && cm == 0);
-  if (eq) {
-    const uint32_t k = (uint32_t)__builtin_ctzll(eq);
+  // the deferred clocks are in CLOCK ORDER: walk them 64 at a time, counting
+  // the ones ordered before tmp and stopping at the first chunk that holds an
+  // equal clock (kDef > 64 in the HBM tier)
+  uint32_t kk = 0u, keq = ~0u;
+  for (uint32_t k0 = 0; k0 < c.def; k0 += kAW) {
+    const bool h = k0 + lane < c.def;
+    const int cm = h ? def_cmp_tmp(w, c, k0 + lane) : 1;
+    const uint64_t eq = __ballot(h && cm == 0);
+    kk += ap_count(h && cm < 0);
+    if (eq) { keq = k0 + (uint32_t)__builtin_ctzll(eq); break; }
+    if (kk < k0 + kAW) break;  // a clock ordered after tmp: the rest are too
+  }
+  if (keq != ~0u) {
+    const uint32_t k = keq;
     const uint32_t ms = k ? w.fmend[k - 1] : 0u, me = w.fmend[k];
     const uint32_t r = count_less(w.fkey, ms, me, m, lane);
     if (ms + r < me && w.fkey[ms + r] == m) return 0;  // already in the set
@@ -256,8 +265,7 @@ __device__ int deferred_add(Ws<C>& w, Cnt& c, uint64_t m, uint32_t lane) {
     return 0;
   }
   if (c.def + 1u > C::kDef || c.fdot + c.tmp > C::kFDot || c.fmem + 1u > C::kFMem) return CRDT_ECAPACITY;
-  const uint32_t kk = ap_count(lane < c.def && cm < 0);  // clocks ordered before tmp
-  const uint32_t o = kk ? w.fdend[kk - 1] : 0u, om = kk ? w.fmend[kk - 1] : 0u;
+  const uint32_t o =kk ? w.fdend[kk - 1] : 0u, om = kk ? w.fmend[kk - 1] : 0u;
   ins_gap<C::kG>(w.fact, c.fdot, o, c.tmp, lane);
   ins_gap<C::kG>(w.fctr, c.fdot, o, c.tmp, lane);
   for (uint32_t i = lane; i < c.tmp; i += kAW) { w.fact[o + i] = w.tact[i]; w.fctr[o + i] = w.tctr[i]; }
@@ -664,9 +672,19 @@ __device__ int apply_one(Ws<C>& w, const ApArgs& g, uint64_t o, uint32_t lane) {
 // block of a kApHugeWaves-block launch). The two lists are the halves of the
 // context's list: [0, cap/2) with count ctl[0], [cap/2, cap) with ctl[1].
 template <class C, int TIER>
+__device__ __forceinline__ Ws<C>& ap_workspace(uint8_t* huge_ws) {
+  if constexpr (TIER == 2) {
+    return *(Ws<C>*)(huge_ws + (uint64_t)blockIdx.x * sizeof(Ws<C>));
+  } else {
+    __shared__ Ws<C> w_lds;
+    return w_lds;
+  }
+}
+
+template <class C, int TIER>
 __global__ __launch_bounds__(kAW) void orswot_apply_kernel(ApArgs g, uint8_t* huge_ws) {
-  __shared__ Ws<C> w_lds[TIER == 2 ? 1 : 1];
-  Ws<C>& w = TIER == 2 ? *(Ws<C>*)(huge_ws + (uint64_t)blockIdx.x * sizeof(Ws<HugeCaps>)) : w_lds[0];
+  static_assert(TIER != 2 || C::kG, "the HBM tier needs the HBM-fenced caps");
+  Ws<C>& w = ap_workspace<C, TIER>(huge_ws);
   const uint32_t lane = threadIdx.x;
   const uint32_t half = g.list_cap / 2u;
   if (TIER == 0) {

@@ -176,9 +176,10 @@ def test_malformed_blobs(gpu):
         assert e.value.code in (-2,), name
     # past the LDS path's 256 members the large-object kernel decodes it ...
     big = dict(clock={1: 400}, entries={m: [(1, m + 1)] for m in range(300)}, deferred=[])
-    t, bo, bl = _upload_blobs([g, BC.encode(big, 1, 2, rng=random.Random(4)), g])
+    g2 = BC.encode(good, 1, 2)  # the neighbours in the same member width
+    t, bo, bl = _upload_blobs([g2, BC.encode(big, 1, 2, rng=random.Random(4)), g2])
     got = gpu.orswot_from_bincode(t, bo, bl, 16, 1, 2).records()
-    assert got[1] == _rec(big, 16, False)
+    assert got == [_rec(good, 16, False), _rec(big, 16, False), _rec(good, 16, False)]
     # ... up to 16 384 members (the HBM scratch); past that, CRDT_ECAPACITY
     huge = dict(clock={1: 20_000}, entries={m: [(1, m + 1)] for m in range(16_385)}, deferred=[])
     t, bo, bl = _upload_blobs([BC.encode(huge, 1, 2)])
