@@ -34,6 +34,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "rust-crdt_amd"))
 
 HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md: 8.0 TB/s spec
+TRAFFIC_ROUNDS = ("r03", "r02", "r01e")  # profiles/traffic_<round>[_<workload>].json, newest first
 METRIC = "merged objects/sec (node) + achieved HBM GB/s % of peak, Orswot 1M×32 members"
 
 
@@ -44,7 +45,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="orswot",
                    choices=["orswot", "vclock", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply",
-                            "mvreg", "map", "map_orswot", "clock_csr", "spawn_check"])
+                            "mvreg", "map", "map_orswot", "clock_csr", "truncate", "spawn_check"])
     p.add_argument("--replicas", type=int, default=8, help="orswot_csr at N=1: replicas folded locally")
     p.add_argument("--n-obj", type=int, default=None, help="objects per GPU")
     p.add_argument("--threads", type=int, default=16, help="host threads for input generation")
@@ -60,7 +61,9 @@ def parse():
     p.add_argument("--rehearse", action="store_true",
                    help="rehearse the N > 1 logic on ONE GPU: every rank on cuda:0, gloo collectives, the Orswot "
                         "join through crdt_orswot_replica_join_transport (tests; not a measurement)")
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r02.json"),
+    p.add_argument("--traffic-json", default=next(
+        (f for f in (os.path.join(REPO, "profiles", f"traffic_{r}.json") for r in TRAFFIC_ROUNDS) if os.path.exists(f)),
+        None),
                    help="measured per-launch HBM bytes (rocprofv3 PMC) to report as roofline.traffic")
     return p.parse_args()
 
@@ -161,26 +164,33 @@ def load_traffic(path, key):
     try:
         with open(path) as f:
             return json.load(f).get(key)
-    except (OSError, ValueError):
+    except (OSError, ValueError, TypeError):
         return None
 
 
 def wl_traffic(args, workload, *kernels):
     """Per-launch HBM bytes of the workload's measured kernels from its
     rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/profile_workload.sh +
-    tools/traffic.py -> profiles/traffic_r02_<workload>.json, else r01e), summed over the
-    kernels one measured launch runs; None off the profiled (default) size."""
+    tools/traffic.py -> profiles/traffic_<round>_<workload>.json, newest round first),
+    summed over the kernels one measured launch runs (every instantiation of a
+    templated one: tools/traffic.py keys them <kernel>_<last template argument>);
+    None off the profiled (default) size."""
     if args.n_obj is not None:
         return None
-    path = os.path.join(REPO, "profiles", f"traffic_r02_{workload}.json")  # newest profile first
-    if not os.path.exists(path):
-        path = os.path.join(REPO, "profiles", f"traffic_r01e_{workload}.json")
+    path = None
+    for rnd in TRAFFIC_ROUNDS:
+        path = os.path.join(REPO, "profiles", f"traffic_{rnd}_{workload}.json")
+        if os.path.exists(path):
+            break
+    try:
+        with open(path) as f:
+            tab = json.load(f)
+    except (OSError, ValueError, TypeError):
+        return None
     vals = []
-    for k in kernels:  # a templated kernel is keyed by its bool instantiation (tools/traffic.py)
-        v = load_traffic(path, k)
-        for suffix in ("_true", "_false"):
-            v = load_traffic(path, k + suffix) if v is None else v
-        vals.append(v)
+    for k in kernels:
+        hits = [v for n, v in tab.items() if n != "detail" and (n == k or n.startswith(k + "_"))]
+        vals.append(sum(hits) if hits else None)
     return None if any(v is None for v in vals) else float(sum(vals))
 
 
@@ -838,6 +848,89 @@ def run_clock_csr(args, rank, world, local):
     return res
 
 
+def run_truncate(args, rank, world, local):
+    """Batched Causal::truncate for Orswot (src/orswot.rs:159-172) over the
+    config-3 shard: record i truncated by a clock derived from its own top
+    clock T — c[x] = T[x] - 2 for even actors, T[x] for actors 1 mod 4, absent
+    otherwise — so about a third of the member bytes and some top-clock entries
+    are dropped (config-3 dots sit within a few counts of T). A step = one crdt_orswot_truncate launch (inputs
+    resident in HBM); spot parity against the oracle first."""
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    import crdts_hip
+    from crdts_hip._lib import check, lib
+
+    n = args.n_obj or 1_000_000
+    A = 16
+    (lb, lo), _ = crdts_hip.generate_orswot(n, first_obj=rank * n, threads=args.threads)
+    top = lb[: lb.nbytes // 8 * 8].view(np.uint64)[(lo // 8 + 4)[:, None] + np.arange(A, dtype=np.uint64)[None, :]]
+    x = np.arange(A)
+    cut_at = np.where(x % 2 == 0, np.where(top > 2, top - 2, 0), np.where(x % 4 == 1, top, 0)).astype(np.uint64)
+    present = cut_at > 0
+    act = np.nonzero(present)[1].astype(np.uint32)
+    ctr = cut_at[present].astype(np.uint64)
+    ln = present.sum(1).astype(np.uint32)
+    coff = np.zeros(n, np.uint64)
+    coff[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+    del top, cut_at, present
+    eng = crdts_hip.Engine(local)
+    B = crdts_hip.OrswotBatch.from_host(lb, lo, A, device=local)
+    K = crdts_hip.ClockBatch.from_host(coff, ln, act, ctr, device=local)
+    stream = torch.cuda.Stream(device=local)
+    torch.cuda.synchronize()
+    out = eng.orswot_truncate(B, K, stream=stream)  # checked launch; its buffers are reused below
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_ffi
+
+    m = min(2000, n)  # spot parity: the first m records
+    e_end = int(coff[m - 1]) + int(ln[m - 1])
+    cut = int(lo[m]) if n > m else lb.nbytes
+    eb, eo = oracle_ffi.orswot_truncate_batch(lb[:cut], lo[:m], (coff[:m], ln[:m], act[:e_end], ctr[:e_end]), A)
+    got = crdts_hip.OrswotBatch(out.base, out.off[:m], A).records()
+    for i in range(m):
+        sz = int(np.frombuffer(eb[int(eo[i]):int(eo[i]) + 4].tobytes(), np.uint32)[0])
+        assert got[i] == eb[int(eo[i]):int(eo[i]) + sz].tobytes(), f"truncate spot parity, object {i}"
+    st = C.c_void_p(stream.cuda_stream)
+    bt, ct = B.cbatch(), K.cstruct()
+
+    def step():
+        check(lib.crdt_orswot_truncate(eng.ctx, C.byref(bt), C.byref(ct), A, 0, C.c_void_p(out.base.data_ptr()),
+                                       C.c_void_p(out.off.data_ptr()), int(out.base.numel()), st))
+
+    wall, ev_ms = _timed_steps(args, world, stream, step)
+    eng.status(stream)
+    out_sizes = out.base.view(torch.int32)[(out.off // 4)].cpu().numpy().astype(np.int64)
+    alg = int(lb.nbytes) + int(out_sizes.sum()) + 12 * int(ln.sum()) + n * (8 + 8 + 4 + 8)
+    total = sum_over_ranks(float(n * args.steps), world)
+    res = {
+        "metric": "batched Orswot::truncate objects/sec (node)", "value": total / wall, "unit": "objects/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic: config-3 op-simulated Orswots, each truncated by a clock derived from its top clock",
+        "config": {"workload": f"truncate config3: {n} objects per GPU, {ln.mean():.1f}-entry clocks, "
+                               f"{out_sizes.mean():.0f} B of {lb.nbytes / n:.0f} B kept per record",
+                   "parallelism": f"dp{world} (objects sharded)"},
+    }
+    if world == 1:
+        ach = alg / (ev_ms * 1e-3) / 1e9
+        res["roofline"] = {"bound": "hbm", "kernel": "orswot_truncate_kernel", "achieved": ach, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "kernel_ms": ev_ms, "alg_bytes_per_launch": alg,
+                           "traffic": wl_traffic(args, "truncate", "orswot_truncate_kernel")}
+        if not args.no_cpu_baseline:
+            mm = min(args.cpu_sample, n)
+            th = cpu_threads(args)
+            e2 = int(coff[mm - 1]) + int(ln[mm - 1])
+            secs = oracle_ffi.orswot_truncate_bench(lb, lo[:mm], (coff[:mm], ln[:mm], act[:e2], ctr[:e2]), th)
+            res["cpu_baseline"] = {"value": mm / secs, "unit": "objects/s", "cores": th, "kind": "port",
+                                   **cpu_cores_note(),
+                                   "sample": f"first {mm} objects, Orswot::truncate over the oracle's containers "
+                                             f"(decode untimed), {th} threads"}
+    return res
+
+
 def run_spawn_check(args, rank, world, local):
     """CPU only (gloo): what the launch path gives each rank — its rank, the
     world size, LOCAL_RANK (the GPU it would bind) and its pid — all-gathered."""
@@ -1087,7 +1180,7 @@ def run_apply(args, rank, world, local):
         ach = alg / (ev_ms * 1e-3) / 1e9
         res["roofline"] = {"bound": "hbm", "kernel": "orswot_apply_kernel", "achieved": ach, "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "kernel_ms": ev_ms, "alg_bytes_per_launch": alg,
-                           "traffic": wl_traffic(args, "apply", "orswot_apply_kernel_true", "orswot_apply_kernel_false")}
+                           "traffic": wl_traffic(args, "apply", "orswot_apply_kernel")}
         if not args.no_cpu_baseline:
             m = min(args.cpu_sample // 5, n)
             th = cpu_threads(args)
@@ -1343,6 +1436,8 @@ def main():
         res = run_map_orswot(args, rank, world, local)
     elif args.workload == "clock_csr":
         res = run_clock_csr(args, rank, world, local)
+    elif args.workload == "truncate":
+        res = run_truncate(args, rank, world, local)
     else:
         res = run_dense(args, rank, world, local, args.workload)
     failed = [k for k, v in res.get("anti_entropy", {}).items() if not (v.get("check") or {}).get("ok", True)]

@@ -852,6 +852,30 @@ double orc_orswot_apply_bench(const uint8_t* rb, const uint64_t* roff, size_t rb
   return std::chrono::duration<double>(t1 - t0).count();
 }
 
+// CPU baseline of the batched truncate: records and clocks decoded untimed,
+// then Orswot::truncate (src/orswot.rs:159-172) timed. Returns seconds.
+double orc_orswot_truncate_bench(const uint8_t* rb, const uint64_t* roff, size_t rbytes, size_t n,
+                                 const uint64_t* coff, const uint32_t* clen, const uint32_t* cact,
+                                 const uint64_t* cctr, int threads) {
+  std::vector<Orswot> objs(n);
+  std::vector<VClock> clocks(n);
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) {
+      decode(rb + roff[i], rbytes - roff[i], objs[i]);
+      for (uint32_t k = 0; k < clen[i]; ++k) clocks[i].witness(cact[coff[i] + k], cctr[coff[i] + k]);
+    }
+  });
+  auto t0 = std::chrono::steady_clock::now();
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) objs[i].truncate(clocks[i]);
+  });
+  auto t1 = std::chrono::steady_clock::now();
+  volatile size_t sink = 0;
+  for (size_t i = 0; i < n; i += 997) sink += objs[i].entries.size();
+  (void)sink;
+  return std::chrono::duration<double>(t1 - t0).count();
+}
+
 // Dense VClock/GCounter rows, through the BTreeMap-style VClock::merge.
 int orc_dense_merge(uint64_t* self, const uint64_t* other, size_t n, uint32_t n_actors,
                     int threads) {

@@ -655,13 +655,20 @@ class Engine:
             self.status(stream)
         return out, off, lens
 
-    def orswot_truncate(self, B: OrswotBatch, clocks: "ClockBatch", stream=None, check_status=True):
+    def orswot_truncate(self, B: OrswotBatch, clocks: "ClockBatch", out: "OrswotBatch | None" = None, stream=None,
+                        check_status=True):
         """out[i] = B[i] after Causal::truncate(&clocks[i]) (src/orswot.rs:159-172),
-        written at B.off[i] (crdt_orswot_truncate). Returns an OrswotBatch."""
+        written at B.off[i] (crdt_orswot_truncate). Returns an OrswotBatch
+        (`out`, reused, when given: at least B.bytes bytes and B.n_obj offsets)."""
         torch = _torch()
         dev = f"cuda:{self.device}"
-        base = torch.empty(max(16, B.bytes), dtype=torch.uint8, device=dev)
-        off = torch.empty(B.n_obj, dtype=torch.int64, device=dev)
+        if out is not None:
+            base, off = out.base, out.off
+            if base.numel() < B.bytes or off.numel() < B.n_obj:
+                raise ValueError("orswot_truncate: `out` is smaller than the input batch")
+        else:
+            base = torch.empty(max(16, B.bytes), dtype=torch.uint8, device=dev)
+            off = torch.empty(B.n_obj, dtype=torch.int64, device=dev)
         b, c = B.cbatch(), clocks.cstruct()
         check(lib.crdt_orswot_truncate(self.ctx, C.byref(b), C.byref(c), B.n_actors, B.flags,
                                        C.c_void_p(base.data_ptr()), C.c_void_p(off.data_ptr()), base.numel(),

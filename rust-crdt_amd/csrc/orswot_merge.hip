@@ -2435,6 +2435,29 @@ __device__ __forceinline__ void stage_all(u32x4* dst, const u32x4 (&r)[kPer], ui
 #pragma unroll
   for (uint32_t k = 0; k < kPer; ++k) dst[lane + k * kWave] = r[k];
 }
+// The same through a buffer resource over the record (base and size
+// wave-uniform, in SGPRs): pieces past the record are out of range, so they
+// return zeros without a memory access, and every lane's offset is a constant
+// (no per-object clamp or 64-bit address arithmetic in VGPRs).
+constexpr int kBufWord3 = 0x00020000;  // gfx9 buffer resource word 3: raw bytes
+constexpr int kBufNT = 2;              // cache policy: nontemporal (gfx94x/gfx950 NT bit)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bytes_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, kBufWord3);
+}
+__device__ __forceinline__ void prefetch_buf(u32x4 (&r)[kPer], const uint8_t* src, uint32_t n16, uint32_t lane) {
+  const __amdgpu_buffer_rsrc_t rs = bytes_rsrc(src, 16u * n16);
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) r[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * (lane + k * kWave)), 0, kBufNT);
+}
+// copy_record_out through a buffer resource of the record's n16 pieces: the
+// stores of lanes past the record are dropped (the instruction count is fixed)
+__device__ __forceinline__ void copy_record_buf(uint32_t src, uint8_t* O, uint32_t n16, uint32_t lane) {
+  const __amdgpu_buffer_rsrc_t rs = bytes_rsrc(O, 16u * n16);
+  const u32x4 p0 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(src + 16u * lane);
+  const u32x4 p1 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(src + 16u * (lane + kWave));
+  __builtin_amdgcn_raw_buffer_store_b128(p0, rs, (int)(16u * lane), 0, kBufNT);
+  __builtin_amdgcn_raw_buffer_store_b128(p1, rs, (int)(16u * (lane + kWave)), 0, kBufNT);
+}
 // Only the 64-piece rounds a record of n16 pieces reaches (n16 wave-uniform).
 __device__ __forceinline__ void stage_used(u32x4* dst, const u32x4 (&r)[kPer], uint32_t n16, uint32_t lane) {
   dst[lane] = r[0];
@@ -2770,8 +2793,11 @@ __attribute__((noinline)) __device__ uint32_t hd_join(const uint8_t* Ls, const u
 // (mask_object<HD>) and is followed by the same tail stores as the other
 // path, redirected to the sink: every path issues at least as many stores
 // after the prefetch as the lean one, so its loop-head wait stays exact
+// IO: 0 record prefetch and copy-out by global loads / stores with clamped
+// lane addresses; 1 prefetch through a buffer resource (prefetch_buf); 2 and
+// the copy-out too (copy_record_buf)
 template <int MINW, int MODE, int OUT = 2, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
-          bool RT = true, uint32_t DYN = 0, uint32_t SF = 6, bool SPEC = false, uint32_t GMIN = 0>
+          bool RT = true, uint32_t DYN = 0, uint32_t SF = 6, bool SPEC = false, uint32_t GMIN = 0, int IO = 0>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
@@ -2908,8 +2934,13 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
       const uint32_t ts = dsel(t);
       if (!SPEC || ts != 0u) {  // (SPEC: object 0's records are already in flight)
         const uint32_t nn = lane_of(n16, ts);
-        prefetch_all(pl, Lb + lane_of64(lo, ts), nn & 0xFFFFu, lane);
-        prefetch_all(pr, Rb + lane_of64(ro, ts), nn >> 16, lane);
+        if (IO >= 1) {
+          prefetch_buf(pl, Lb + lane_of64(lo, ts), nn & 0xFFFFu, lane);
+          prefetch_buf(pr, Rb + lane_of64(ro, ts), nn >> 16, lane);
+        } else {
+          prefetch_all(pl, Lb + lane_of64(lo, ts), nn & 0xFFFFu, lane);
+          prefetch_all(pr, Rb + lane_of64(ro, ts), nn >> 16, lane);
+        }
       }
     }
     wave_sync();  // the previous chunk's last LDS reads are done
@@ -2925,8 +2956,13 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
       const uint32_t us = dsel(u);
       {
         const uint32_t nu = lane_of(n16, us);
-        prefetch_all(pl, Lb + lane_of64(lo, us), nu & 0xFFFFu, lane);
-        prefetch_all(pr, Rb + lane_of64(ro, us), nu >> 16, lane);
+        if (IO >= 1) {
+          prefetch_buf(pl, Lb + lane_of64(lo, us), nu & 0xFFFFu, lane);
+          prefetch_buf(pr, Rb + lane_of64(ro, us), nu >> 16, lane);
+        } else {
+          prefetch_all(pl, Lb + lane_of64(lo, us), nu & 0xFFFFu, lane);
+          prefetch_all(pr, Rb + lane_of64(ro, us), nu >> 16, lane);
+        }
       }
       bool big = false;
       uint32_t r;
@@ -2979,6 +3015,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
           const u32x4 z = {0u, 0u, 0u, 0u};
           __builtin_nontemporal_store(z, (u32x4*)sink);
           __builtin_nontemporal_store(z, (u32x4*)sink + 1);
+        } else if (IO >= 2) {
+          copy_record_buf(src, Ob + oo, fbu ? 1u : r, lane);
         } else {
           copy_record_out(src, Ob + oo, fbu ? 1u : r, lane);
         }
@@ -3772,7 +3810,7 @@ namespace {
 // then the general kernel.
 template <int MINW, bool ONE = true, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
           bool RT = true, uint32_t DYN = 0, bool DK = false, uint32_t SF = 6, bool V10 = false, bool SPEC = false,
-          uint32_t GMIN = 0>
+          uint32_t GMIN = 0, int IO = 0>
 int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                        const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
                        uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
@@ -3792,7 +3830,7 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
   } else
 #endif
   if constexpr (ONE) {
-    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL, RT, DYN, SF, SPEC, GMIN>;
+    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL, RT, DYN, SF, SPEC, GMIN, IO>;
   } else {
 #ifdef CRDT_DIAG
     f1 = (const void*)orswot_join_kernel<MINW, 1>;
@@ -3888,6 +3926,9 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   if (variant == 204) return go(launch_join_passes<6, true, true, true, true, 0, true, 40, false, 4, false, false, 10>);
   if (variant == 205) return go(launch_join_passes<6, true, true, true, true, 6, true, 32, false, 5, false, false, 8>);  // + stamps
   // timing only, on the guided split: 244 no deferred kill, 245 no deferred block, 246 join without HBM, 247 HBM without join
+  // r03: record prefetch (250) and also the copy-out (251) through buffer resources
+  if (variant == 250) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 1>);
+  if (variant == 251) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 2>);
   if (variant == 244) return go(launch_join_passes<6, true, true, true, true, 1, true, 20, false, 5>);
   if (variant == 245) return go(launch_join_passes<6, true, true, true, true, 2, true, 20, false, 5>);
   if (variant == 246) return go(launch_join_passes<6, true, true, true, true, 3, true, 20, false, 5>);

@@ -70,6 +70,8 @@ def lib():
     L.orc_vclock_csr_merge.argtypes = [P] * 8 + [C.c_size_t, P, P, P, C.c_int, C.POINTER(C.c_int64)]
     L.orc_vclock_csr_bench.restype = C.c_double
     L.orc_vclock_csr_bench.argtypes = [P] * 8 + [C.c_size_t, C.c_int]
+    L.orc_orswot_truncate_bench.restype = C.c_double
+    L.orc_orswot_truncate_bench.argtypes = [P, P, C.c_size_t, C.c_size_t, P, P, P, P, C.c_int]
     L.orc_orswot_truncate_batch.restype = C.c_int
     L.orc_orswot_truncate_batch.argtypes = [P, P, C.c_size_t, C.c_size_t, P, P, P, P, C.c_uint32, C.c_uint32, P, P,
                                             C.c_size_t, C.c_int, C.POINTER(C.c_int64)]
@@ -365,6 +367,15 @@ def orswot_truncate_batch(lbase, loff, clocks, n_actors, flags=0, threads=8):
     if rc != 0:
         raise ValueError(f"oracle truncate failed rc={rc} at object {bad.value}")
     return obase, ooff[:n]
+
+
+def orswot_truncate_bench(lbase, loff, clocks, threads):
+    """Seconds of Orswot::truncate over the batch (decode untimed)."""
+    lbase = np.ascontiguousarray(lbase, dtype=np.uint8)
+    loff = np.ascontiguousarray(loff, dtype=np.uint64)
+    co, cl, ca, cc = [np.ascontiguousarray(x) for x in clocks]
+    return lib().orc_orswot_truncate_bench(_ptr(lbase), _ptr(loff), lbase.nbytes, len(loff), _ptr(co), _ptr(cl),
+                                           _ptr(ca), _ptr(cc), threads)
 
 
 def vclock_csr_bench(s, o, threads):

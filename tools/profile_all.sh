@@ -4,7 +4,7 @@
 set -euo pipefail
 TAG=${1:-r01e}
 bash tools/profile.sh $TAG
-for wl in apply orswot_csr bincode mvreg map gcounter; do
+for wl in ${WORKLOADS:-apply orswot_csr bincode clock_csr mvreg map map_orswot gcounter}; do
   echo "profiling $wl"
   bash tools/profile_workload.sh $TAG $wl
 done

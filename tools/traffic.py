@@ -27,6 +27,7 @@ KERNELS = {"orswot_join_kernel": "orswot_join_kernel<", "orswot_mask_kernel": "o
            "orswot_merge_general_kernel": "orswot_merge_general_kernel", "dense_max_kernel": "dense_max_kernel"}
 # every other kernel of the library is summarised under its own name
 OTHER = ("orswot_apply_kernel", "orswot_sparse_mask_kernel", "orswot_sparse_general_kernel", "bincode_ingest_kernel",
+         "clock_csr_merge_kernel", "orswot_truncate_kernel", "bincode_decode_big_kernel", "slice_bounds_kernel",
          "bincode_egest_kernel", "bincode_decode_kernel", "bincode_sizes_lane_kernel", "bincode_bounds_kernel", "mvreg_merge_kernel",
          "vclock_cmp_kernel", "map_mvreg_merge_kernel", "map_orswot_merge_kernel", "validate_kernel", "sizes_kernel", "copy_kernel")
 
@@ -38,9 +39,9 @@ def short(name):
     import re
     for k in OTHER:  # whole identifier: mvreg_merge_kernel must not match map_mvreg_merge_kernel
         if re.search(r"(?<![A-Za-z0-9_])" + k + r"(?![A-Za-z0-9_])", name):
-            # instantiations told apart by a trailing bool template argument
-            # (apply: small / large workspace; egest: two passes)
-            t = re.search(k + r"<.*(true|false)>\(", name)
+            # instantiations told apart by their last template argument
+            # (apply: workspace tier 0 / 1 / 2; egest: two passes)
+            t = re.search(k + r"<(?:.*[, ])?\(?(\w+)\)?>\(", name)
             return k + ("_" + t.group(1) if t else "")
     return None
 
