@@ -453,12 +453,16 @@ __device__ __forceinline__ void op_fetch(const ApArgs& g, uint64_t q0, uint64_t 
   }
 }
 
-// clock pairs c0 .. c0 + 127 (the first Rm clocks of an object): lane i holds
-// pairs c0 + i and c0 + 64 + i
-__device__ __forceinline__ void clk_fetch(const ApArgs& g, uint64_t c0, uint32_t lane, uint32_t& xa0, uint64_t& xc0,
-                                          uint32_t& xa1, uint64_t& xc1) {
-  if (c0 + lane < g.n_clk) { xa0 = g.clk_act[c0 + lane]; xc0 = g.clk_ctr[c0 + lane]; }
-  if (c0 + kAW + lane < g.n_clk) { xa1 = g.clk_act[c0 + kAW + lane]; xc1 = g.clk_ctr[c0 + kAW + lane]; }
+// clock pairs c0 .. min(c0 + 127, ce - 1) (the first Rm clocks of an object;
+// ce = its pairs' end): lane i holds pairs c0 + i and c0 + 64 + i. Bounded by
+// the object's own pairs: reading a fixed 128-pair window re-read the
+// neighbours' pairs (~1.5 KB per object, on another XCD's L2 for the next
+// object), ~1 GB of the launch's 2.3 GB of reads (profiles/r03_apply_*)
+__device__ __forceinline__ void clk_fetch(const ApArgs& g, uint64_t c0, uint64_t ce, uint32_t lane, uint32_t& xa0,
+                                          uint64_t& xc0, uint32_t& xa1, uint64_t& xc1) {
+  const uint64_t e = ce < g.n_clk ? ce : g.n_clk;
+  if (c0 + lane < e) { xa0 = g.clk_act[c0 + lane]; xc0 = g.clk_ctr[c0 + lane]; }
+  if (c0 + kAW + lane < e) { xa1 = g.clk_act[c0 + kAW + lane]; xc1 = g.clk_ctr[c0 + kAW + lane]; }
 }
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t j) {
   return ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)j, kAW) << 32) |
@@ -502,7 +506,7 @@ __device__ int apply_one(Ws<C>& w, const ApArgs& g, uint64_t o, uint32_t lane) {
   op_fetch(g, ob, oe, lane, rk, rm, ra, rn, re);
   uint32_t xa0 = 0, xa1 = 0;
   uint64_t xc0 = 0, xc1 = 0;
-  clk_fetch(g, cb, lane, xa0, xc0, xa1, xc1);
+  clk_fetch(g, cb, ce, lane, xa0, xc0, xa1, xc1);
   int rc = 0;
   if (!hdr_in || !rec_ok_h(h, sbytes, so, A, flags) || oe < ob || oe > g.n_ops) rc = CRDT_ENONCANON;
   const uint8_t* r = sb + so;
@@ -690,7 +694,9 @@ __global__ __launch_bounds__(kAW) void orswot_apply_kernel(ApArgs g, uint8_t* hu
   if (TIER == 0) {
     // BlockTickets (sched.h): half the objects by block index, the rest in
     // 4-object atomic tickets (ctl[3]) — one call site, so apply_one is
-    // inlined once (two call sites doubled the kernel's VGPRs)
+    // inlined once (two call sites doubled the kernel's VGPRs). (An
+    // XCD-aware split — contiguous object ranges per XCD — measured slower:
+    // 3.47 vs 2.67 ms)
     BlockTickets<4> sched(g.n_obj, g.ctl + 3, lane);
     for (uint64_t o = sched.first(); o < g.n_obj; o = sched.next(o)) {
       const int rc = apply_one<C>(w, g, o, lane);

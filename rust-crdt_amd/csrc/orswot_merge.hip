@@ -1437,6 +1437,8 @@ __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t
 // ======================================================================
 constexpr uint32_t k3MsL = 0, k3MsR = 512, k3Out = 0, k3EqGe = 1024, k3Desc = 1536, k3Trash = 1664;
 constexpr uint32_t k3Scratch = 2176;  // <= kMask1Scratch: the kernel's scratch also serves mask_object
+constexpr uint32_t k3DefMask = k3Scratch;  // u32 [64] (HK 1): actor mask per deferred clock
+static_assert(k3DefMask + 256u <= 2560u, "the deferred clock masks fit in the wave's scratch");
 
 typedef const __attribute__((address_space(3))) uint64_t lds_cu64;
 typedef const __attribute__((address_space(3))) uint32_t lds_cu32;
@@ -1495,7 +1497,9 @@ __device__ __forceinline__ const uint8_t* gptr(uint32_t a) {
   return (const uint8_t*)(const __attribute__((address_space(3))) uint8_t*)(size_t)a;
 }
 // RT: member ranks searched in padded key tables (else clamped probes of the stage)
-template <uint32_t OUTCAP, int OUT = 0, bool HD = false, int HABL = 0, bool RT = true>  // OUT: 0 direct stores, 1 sink-predicated, 2 LDS-assembled
+// HK (with HD): 1 = the kill pass finds a deferred member's union slot by one
+// search of a union key table and a clock's D[x] by its actor presence mask
+template <uint32_t OUTCAP, int OUT = 0, bool HD = false, int HABL = 0, bool RT = true, int HK = 0>  // OUT: 0 direct stores, 1 sink-predicated, 2 LDS-assembled
 __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint32_t uX, uint8_t* O, uint32_t A,
                                                  uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane,
                                                  bool& big, uint8_t* sink = nullptr) {
@@ -1673,6 +1677,55 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
     const uint32_t nfL = DL.v.n_def, nfR = DR.v.n_def;
     const uint32_t nmL = nfL ? uni(lr32(uL + DL.v.fmend + 4u * (nfL - 1u))) : 0u;
     const uint32_t nmR = nfR ? uni(lr32(uR + DR.v.fmend + 4u * (nfR - 1u))) : 0u;
+    if (HK == 1) {
+      // the union keys by slot (slots are in key order), over the R member
+      // masks read above, padded with ~0; and per deferred clock (lanes 0-31:
+      // self's, 32-63: other's) the mask of the actors it holds
+      const uint32_t ut = uX + k3MsR;
+      const uint64_t ukey = lr64(bit_of(hasL, lane) ? uL + key + 8u * mi : uR + key + 8u * mj);
+      *(lds_u64*)(size_t)(ut + l8) = bit_of(mU, lane) ? ukey : ~0ull;
+      // the masks: one lane per deferred clock entry of either side (its
+      // clock by a search of the run ends), OR-ed into its clock's slot
+      *(lds_u32*)(size_t)(uX + k3DefMask + 4u * lane) = 0u;
+      wave_sync();
+      const uint32_t ndL = nfL ? uni(lr32(uL + DL.v.fdend + 4u * (nfL - 1u))) : 0u;
+      const uint32_t ndR = nfR ? uni(lr32(uR + DR.v.fdend + 4u * (nfR - 1u))) : 0u;
+      bool wide = false;  // an actor >= 32 (not canonical here): the general kernel joins the object
+      for (uint32_t base = 0; base < ndL + ndR; base += kWave) {
+        const uint32_t it = base + lane;
+        const bool isL = it < ndL, act = it < ndL + ndR;
+        const uint32_t us = isL ? uL : uR, e = act ? (isL ? it : it - ndL) : 0u;
+        const uint32_t fd = us + (isL ? DL.v.fdend : DR.v.fdend), nf = isL ? nfL : nfR;
+        uint32_t k = 0;  // # run ends <= e
+        for (uint32_t step = 32u; step; step >>= 1)
+          k = (k + step <= nf && lr32(fd + 4u * (k + step - 1u)) <= e) ? k + step : k;
+        const uint32_t a = lr32(us + (isL ? DL.v.fact : DR.v.fact) + 4u * e);
+        wide = wide || (act && a >= 32u);
+        const bool put = act && a < 32u;
+        __hip_atomic_fetch_or((lds_u32*)(size_t)(put ? uX + k3DefMask + 4u * (isL ? k : 32u + k) : uX + k3Trash + l8),
+                              put ? 1u << a : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      if (__ballot(wide) != 0ull) return kLeanFallback;
+      wave_sync();
+      for (uint32_t base = 0; base < nmL + nmR; base += kWave) {
+        const uint32_t it = base + lane;
+        const bool isL = it < nmL, act = it < nmL + nmR;
+        const uint32_t us = isL ? uL : uR, j = act ? (isL ? it : it - nmL) : 0u;
+        const uint32_t fk = isL ? DL.v.fkey : DR.v.fkey, fm = isL ? DL.v.fmend : DR.v.fmend;
+        const uint32_t nf = isL ? nfL : nfR;
+        const uint64_t m = lr64(us + fk + 8u * j);
+        uint32_t k = 0;  // # run ends <= j (n_def <= 32 per side)
+        for (uint32_t step = 32u; step; step >>= 1)
+          k = (k + step <= nf && lr32(us + fm + 4u * (k + step - 1u)) <= j) ? k + step : k;
+        uint32_t q = ut;  // the first union key >= m (the table is 64 slots)
+#pragma unroll
+        for (uint32_t step = 256u; step >= 8u; step >>= 1) q = lr64(q + step - 8u) < m ? q + step : q;
+        const uint32_t su = (q - ut) >> 3;
+        const bool hit = act && su < U && lr64(q) == m;
+        __hip_atomic_fetch_or((lds_u64*)(size_t)(hit ? dmt + 8u * su : uX + k3Trash + l8),
+                              hit ? 1ull << (isL ? k : 32u + k) : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    } else
     for (uint32_t base = 0; base < nmL + nmR; base += kWave) {
       const uint32_t it = base + lane;
       const bool isL = it < nmL, act = it < nmL + nmR;
@@ -1716,6 +1769,13 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
     // D[x] of clock bit kb: a fixed-trip binary search of its actor-sorted run
     // (a deferred clock of an object on this path has <= A <= 32 entries)
     auto dget = [&](uint32_t kb, uint32_t x) -> uint64_t {
+      if (HK == 1) {  // D[x] by the clock's actor mask: its rank among the clock's actors
+        const bool sL = kb < 32u;
+        const uint32_t kk = kb & 31u, fd = sL ? fdL : fdR, fc = sL ? fcL : fcR;
+        const uint32_t msk = lr32(uX + k3DefMask + 4u * kb);
+        const uint32_t lo = kk ? lr32(fd + 4u * (kk - 1u)) : 0u;
+        return (msk >> x) & 1u ? lr64(fc + 8u * (lo + __popc(msk & ((1u << x) - 1u)))) : 0ull;
+      }
       const bool sL = kb < 32u;
       const uint32_t kk = kb & 31u, fd = sL ? fdL : fdR, fa = sL ? faL : faR, fc = sL ? fcL : fcR;
       uint32_t lo = kk ? lr32(fd + 4u * (kk - 1u)) : 0u;
@@ -2444,10 +2504,11 @@ constexpr int kBufNT = 2;              // cache policy: nontemporal (gfx94x/gfx9
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t bytes_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, kBufWord3);
 }
+template <int AUX = kBufNT>
 __device__ __forceinline__ void prefetch_buf(u32x4 (&r)[kPer], const uint8_t* src, uint32_t n16, uint32_t lane) {
   const __amdgpu_buffer_rsrc_t rs = bytes_rsrc(src, 16u * n16);
 #pragma unroll
-  for (uint32_t k = 0; k < kPer; ++k) r[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * (lane + k * kWave)), 0, kBufNT);
+  for (uint32_t k = 0; k < kPer; ++k) r[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * (lane + k * kWave)), 0, AUX);
 }
 // copy_record_out through a buffer resource of the record's n16 pieces: the
 // stores of lanes past the record are dropped (the instruction count is fixed)
@@ -2797,7 +2858,8 @@ __attribute__((noinline)) __device__ uint32_t hd_join(const uint8_t* Ls, const u
 // lane addresses; 1 prefetch through a buffer resource (prefetch_buf); 2 and
 // the copy-out too (copy_record_buf)
 template <int MINW, int MODE, int OUT = 2, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
-          bool RT = true, uint32_t DYN = 0, uint32_t SF = 6, bool SPEC = false, uint32_t GMIN = 0, int IO = 0>
+          bool RT = true, uint32_t DYN = 0, uint32_t SF = 6, bool SPEC = false, uint32_t GMIN = 0, int IO = 0,
+          int HK = 0>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
@@ -2935,8 +2997,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
       if (!SPEC || ts != 0u) {  // (SPEC: object 0's records are already in flight)
         const uint32_t nn = lane_of(n16, ts);
         if (IO >= 1) {
-          prefetch_buf(pl, Lb + lane_of64(lo, ts), nn & 0xFFFFu, lane);
-          prefetch_buf(pr, Rb + lane_of64(ro, ts), nn >> 16, lane);
+          prefetch_buf<IO == 3 ? 0 : kBufNT>(pl, Lb + lane_of64(lo, ts), nn & 0xFFFFu, lane);
+          prefetch_buf<IO == 3 ? 0 : kBufNT>(pr, Rb + lane_of64(ro, ts), nn >> 16, lane);
         } else {
           prefetch_all(pl, Lb + lane_of64(lo, ts), nn & 0xFFFFu, lane);
           prefetch_all(pr, Rb + lane_of64(ro, ts), nn >> 16, lane);
@@ -2957,8 +3019,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
       {
         const uint32_t nu = lane_of(n16, us);
         if (IO >= 1) {
-          prefetch_buf(pl, Lb + lane_of64(lo, us), nu & 0xFFFFu, lane);
-          prefetch_buf(pr, Rb + lane_of64(ro, us), nu >> 16, lane);
+          prefetch_buf<IO == 3 ? 0 : kBufNT>(pl, Lb + lane_of64(lo, us), nu & 0xFFFFu, lane);
+          prefetch_buf<IO == 3 ? 0 : kBufNT>(pr, Rb + lane_of64(ro, us), nu >> 16, lane);
         } else {
           prefetch_all(pl, Lb + lane_of64(lo, us), nu & 0xFFFFu, lane);
           prefetch_all(pr, Rb + lane_of64(ro, us), nu >> 16, lane);
@@ -2993,7 +3055,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
         if ((defs >> td) & 1ull) {
           if (HDD) {
             if (M3HD)
-              r = mask3_object<0xFFFFFFFFu, 0, true, HABL, RT>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
+              r = mask3_object<0xFFFFFFFFu, 0, true, HABL, RT, HK>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
                                                      d & 0xFFFFu, m >> 16, d >> 16, lane, big);
             else
               r = mask_object<0xFFFFFFFFu, true, 0, DC>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo),
@@ -3015,7 +3077,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
           const u32x4 z = {0u, 0u, 0u, 0u};
           __builtin_nontemporal_store(z, (u32x4*)sink);
           __builtin_nontemporal_store(z, (u32x4*)sink + 1);
-        } else if (IO >= 2) {
+        } else if (IO == 2) {
           copy_record_buf(src, Ob + oo, fbu ? 1u : r, lane);
         } else {
           copy_record_out(src, Ob + oo, fbu ? 1u : r, lane);
@@ -3810,7 +3872,7 @@ namespace {
 // then the general kernel.
 template <int MINW, bool ONE = true, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
           bool RT = true, uint32_t DYN = 0, bool DK = false, uint32_t SF = 6, bool V10 = false, bool SPEC = false,
-          uint32_t GMIN = 0, int IO = 0>
+          uint32_t GMIN = 0, int IO = 0, int HK = 0>
 int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                        const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
                        uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
@@ -3830,7 +3892,7 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
   } else
 #endif
   if constexpr (ONE) {
-    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL, RT, DYN, SF, SPEC, GMIN, IO>;
+    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL, RT, DYN, SF, SPEC, GMIN, IO, HK>;
   } else {
 #ifdef CRDT_DIAG
     f1 = (const void*)orswot_join_kernel<MINW, 1>;
@@ -3929,6 +3991,9 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // r03: record prefetch (250) and also the copy-out (251) through buffer resources
   if (variant == 250) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 1>);
   if (variant == 251) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 2>);
+  if (variant == 253) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 3>);
+  // r03: the kill pass by a union key table and per-clock actor masks (HK 1)
+  if (variant == 252) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 0, 1>);
   if (variant == 244) return go(launch_join_passes<6, true, true, true, true, 1, true, 20, false, 5>);
   if (variant == 245) return go(launch_join_passes<6, true, true, true, true, 2, true, 20, false, 5>);
   if (variant == 246) return go(launch_join_passes<6, true, true, true, true, 3, true, 20, false, 5>);

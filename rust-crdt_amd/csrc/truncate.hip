@@ -27,6 +27,8 @@
 // binary-search the sorted runs. Not the hot path: latency-bound, any size.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "../../include/crdts_hip.h"
 #include "kernels.h"
 #include "record_layout.h"
@@ -129,39 +131,53 @@ __device__ bool deferred_kills(const Rec& R, uint64_t key, uint32_t x, uint64_t 
   return false;
 }
 
-__global__ __launch_bounds__(256) void orswot_truncate_kernel(const uint8_t* __restrict__ base,
-                                                              const uint64_t* __restrict__ off, uint64_t bytes,
-                                                              uint64_t n_obj, const uint64_t* __restrict__ coff,
-                                                              const uint32_t* __restrict__ clen,
-                                                              const uint32_t* __restrict__ cact,
-                                                              const uint64_t* __restrict__ cctr, uint64_t c_entries,
-                                                              uint32_t A, uint32_t flags, uint8_t* __restrict__ out,
-                                                              uint64_t* __restrict__ out_off, uint64_t out_bytes,
-                                                              int* status) {
-  const uint32_t lane = threadIdx.x & (kW - 1u);
-  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kW;
-  const uint64_t n_waves = (uint64_t)gridDim.x * blockDim.x / kW;
-  const bool sparse = (flags & kSparseClock) != 0u;
-  for (uint64_t i = wave; i < n_obj; i += n_waves) {
-    const uint64_t o = off[i];
-    if (lane == 0u) out_off[i] = o;
-    // ---- the record: header, layout, bounds (a bad record is not written)
-    bool ok = (o & 15u) == 0u && o <= bytes && bytes - o >= kHdrBytes;
-    uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (ok)
-      for (int k = 0; k < 8; ++k) h[k] = ((const uint32_t*)(base + o))[k];
-    Rec R{base + o, {}, sparse};
-    rec_layout(R.L, h[1], h[2], h[3], h[4], h[5], h[6], sparse);
-    ok = ok && h[0] == R.L.size && h[7] == flags && (sparse ? h[1] <= A : h[1] == A) && R.L.size <= bytes - o &&
-         o + R.L.size <= out_bytes;
-    const uint64_t c0 = coff[i];
-    const uint32_t cn = clen[i];
-    ok = ok && c0 <= c_entries && cn <= c_entries - c0;
-    if (!ok) {
-      if (lane == 0u) fail(status, CRDT_ENONCANON);
-      continue;
-    }
-    const Run c{cact + c0, cctr + c0, cn};
+struct TruncArgs {
+  const uint8_t* base;
+  const uint64_t* off;
+  uint64_t bytes, n_obj;
+  const uint64_t* coff;
+  const uint32_t* clen;
+  const uint32_t* cact;
+  const uint64_t* cctr;
+  uint64_t c_entries;
+  uint32_t A, flags;
+  uint8_t* out;
+  uint64_t* out_off;
+  uint64_t out_bytes;
+  int* status;
+};
+
+// A record's header read and checked (a bad record latches CRDT_ENONCANON
+// and is not written); its layout in R, its clock in c.
+__device__ __forceinline__ bool truncate_open(const TruncArgs& g, uint64_t i, uint32_t lane, Rec& R, Run& c,
+                                              uint64_t& o) {
+  const bool sparse = (g.flags & kSparseClock) != 0u;
+  o = g.off[i];
+  if (lane == 0u) g.out_off[i] = o;
+  bool ok = (o & 15u) == 0u && o <= g.bytes && g.bytes - o >= kHdrBytes;
+  uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (ok)
+    for (int k = 0; k < 8; ++k) h[k] = ((const uint32_t*)(g.base + o))[k];
+  R = Rec{g.base + o, {}, sparse};
+  rec_layout(R.L, h[1], h[2], h[3], h[4], h[5], h[6], sparse);
+  ok = ok && h[0] == R.L.size && h[7] == g.flags && (sparse ? h[1] <= g.A : h[1] == g.A) &&
+       R.L.size <= g.bytes - o && o + R.L.size <= g.out_bytes;
+  const uint64_t c0 = g.coff[i];
+  const uint32_t cn = g.clen[i];
+  ok = ok && c0 <= g.c_entries && cn <= g.c_entries - c0;
+  if (!ok && lane == 0u) fail(g.status, CRDT_ENONCANON);
+  c = Run{g.cact + c0, g.cctr + c0, cn};
+  return ok;
+}
+
+// The general form: every read straight from HBM (any record size, dense or
+// CSR top clock, any number of deferred clocks).
+__device__ void truncate_global(const TruncArgs& g, const Rec& R, const Run& c, uint64_t o, uint32_t lane) {
+  const bool sparse = R.sparse;
+  const uint32_t flags = g.flags;
+  int* const status = g.status;
+  uint8_t* const out = g.out;
+  {
     const RecLayout& L = R.L;
     // run ends of member / deferred runs are clamped: a malformed record cannot
     // send a lane past its sections
@@ -229,7 +245,7 @@ __global__ __launch_bounds__(256) void orswot_truncate_kernel(const uint8_t* __r
     rec_layout(O, n_clk, n_mem, n_dot, n_def, n_fdot, n_fmem, sparse);
     if (O.size > L.size) {  // cannot happen for a canonical record
       if (lane == 0u) fail(status, CRDT_ENONCANON);
-      continue;
+      return;
     }
     uint8_t* w = out + o;
 
@@ -358,6 +374,258 @@ __global__ __launch_bounds__(256) void orswot_truncate_kernel(const uint8_t* __r
   }
 }
 
+// ---------------------------------------------------------------- LDS form
+// Records of dense top clocks over A <= 32 actors, <= kTStage bytes and <= 8
+// deferred clocks (config 3: every record) are staged in LDS with the
+// truncating clock as a dense row c[x] and every deferred clock as a dense row
+// D_k[x]; each member carries the mask of the deferred clocks naming it. The
+// same two passes then read only LDS: c[x] and D_k[x] are one read each
+// instead of binary searches through HBM. Everything else takes
+// truncate_global.
+constexpr uint32_t kTStage = 4096;
+constexpr uint32_t kTDef = 8;
+constexpr uint32_t kTA = 32;
+constexpr uint32_t kTWaves = 4;
+struct TWs {
+  uint32_t stage[kTStage / 4];
+  uint64_t ct[kTA];
+  uint64_t drow[kTDef][kTA];
+  uint32_t nm[kTStage / 24];  // per member: the deferred clocks naming it (a member takes >= 24 B of a record)
+};
+
+__device__ __forceinline__ void tsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ void truncate_lds(const TruncArgs& g, const Rec& R, const Run& c, uint64_t o, uint32_t lane, TWs& w) {
+  const RecLayout& L = R.L;
+  const uint32_t A = L.n_clk;
+  // ---- stage the record, the clock and the deferred rows
+  const uint32_t n16 = L.size / 16u;
+  for (uint32_t p = lane; p < n16; p += kW) ((uint4*)w.stage)[p] = ((const uint4*)R.r)[p];
+  if (lane < kTA) w.ct[lane] = 0ull;
+  for (uint32_t k = lane; k < kTDef * kTA; k += kW) w.drow[k / kTA][k % kTA] = 0ull;
+  for (uint32_t m = lane; m < L.n_mem; m += kW) w.nm[m] = 0u;
+  tsync();
+  for (uint32_t e = lane; e < c.n; e += kW) {
+    const uint32_t x = c.a[e];
+    if (x < kTA) w.ct[x] = c.c[e];  // actors >= A name nothing a dense record holds
+  }
+  const uint8_t* S = (const uint8_t*)w.stage;
+  const uint32_t* fdend = (const uint32_t*)(S + L.o_fdend);
+  const uint32_t* fmend = (const uint32_t*)(S + L.o_fmend);
+  const uint32_t* fact = (const uint32_t*)(S + L.o_fact);
+  const uint64_t* fctr = (const uint64_t*)(S + L.o_fctr);
+  const uint64_t* fkey = (const uint64_t*)(S + L.o_fkey);
+  const uint64_t* key = (const uint64_t*)(S + L.o_key);
+  const uint32_t* dact = (const uint32_t*)(S + L.o_dact);
+  const uint64_t* dctr = (const uint64_t*)(S + L.o_dctr);
+  const uint32_t* mdend = (const uint32_t*)(S + L.o_mdend);
+  const uint64_t* top = (const uint64_t*)(S + L.o_clk);
+  auto clock_of = [&](const uint32_t* ends, uint32_t j) {  // # run ends <= j: the clock of item j (<= kTDef runs)
+    uint32_t k = 0;
+    for (uint32_t t = 0; t < L.n_def; ++t) k += ends[t] <= j ? 1u : 0u;
+    return k;
+  };
+  for (uint32_t e = lane; e < L.n_def_dot; e += kW) {
+    const uint32_t k = clock_of(fdend, e), x = fact[e];
+    if (k < kTDef && x < kTA) w.drow[k][x] = fctr[e];
+  }
+  for (uint32_t j = lane; j < L.n_def_mem; j += kW) {
+    const uint32_t k = clock_of(fmend, j);
+    const uint64_t m = fkey[j];
+    uint32_t lo = 0, len = L.n_mem;  // the member's index (absent: no member to name)
+    while (len) {
+      const uint32_t h = len >> 1;
+      if (key[lo + h] < m) { lo += h + 1u; len -= h + 1u; } else { len = h; }
+    }
+    if (lo < L.n_mem && key[lo] == m && k < kTDef) atomicOr(&w.nm[lo], 1u << k);
+  }
+  tsync();
+  auto mend = [&](uint32_t m) { return min(mdend[m], L.n_dot); };
+  auto mbeg = [&](uint32_t m) { return m ? min(mend(m - 1u), mend(m)) : 0u; };
+  auto fdb = [&](uint32_t k) { return k ? min(min(fdend[k - 1u], L.n_def_dot), min(fdend[k], L.n_def_dot)) : 0u; };
+  auto fde = [&](uint32_t k) { return min(fdend[k], L.n_def_dot); };
+  auto fmb = [&](uint32_t k) { return k ? min(min(fmend[k - 1u], L.n_def_mem), min(fmend[k], L.n_def_mem)) : 0u; };
+  auto fme = [&](uint32_t k) { return min(fmend[k], L.n_def_mem); };
+  auto killed = [&](uint32_t names, uint32_t x, uint64_t v) {
+    bool dk = false;
+    for (uint32_t b = names; b; b &= b - 1u) dk = dk || w.drow[__builtin_ctz(b)][x] >= v;
+    return dk;
+  };
+
+  // ---- pass 1: counts (the dense top clock keeps all A slots)
+  uint32_t n_def = 0, n_fdot = 0, n_fmem = 0;
+  for (uint32_t b = 0; b < L.n_def; b += kW) {
+    const uint32_t k = b + lane;
+    bool keepd = false;
+    uint32_t nd = 0, nmm = 0;
+    if (k < L.n_def) {
+      for (uint32_t d = fdb(k); d < fde(k); ++d) {
+        const uint32_t x = fact[d];
+        const uint64_t t = x < A ? top[x] : 0ull, cx = x < kTA ? w.ct[x] : 0ull;
+        keepd = keepd || fctr[d] > (t > cx ? t : cx);
+      }
+      nd = fde(k) - fdb(k);
+      nmm = fme(k) - fmb(k);
+    }
+    n_def += (uint32_t)__popcll(__ballot(keepd));
+    n_fdot += wave_sum(keepd ? nd : 0u);
+    n_fmem += wave_sum(keepd ? nmm : 0u);
+  }
+  uint32_t n_mem = 0, n_dot = 0;
+  bool empty_clock = false;
+  for (uint32_t b = 0; b < L.n_mem; b += kW) {
+    const uint32_t m = b + lane;
+    uint32_t fin = 0;
+    bool above = false, alive = false;
+    if (m < L.n_mem) {
+      const uint32_t names = w.nm[m];
+      for (uint32_t d = mbeg(m); d < mend(m); ++d) {
+        const uint32_t x = dact[d];
+        const uint64_t v = dctr[d];
+        const bool gt = v > w.ct[x & (kTA - 1u)];
+        const bool dk = killed(names, x & (kTA - 1u), v);
+        above = above || gt;
+        alive = alive || !dk;
+        fin += gt && !dk ? 1u : 0u;
+      }
+    }
+    const bool kept = above && alive;
+    n_mem += (uint32_t)__popcll(__ballot(kept));
+    n_dot += wave_sum(kept ? fin : 0u);
+    empty_clock = empty_clock || __ballot(kept && fin == 0u) != 0ull;
+  }
+  RecLayout O;
+  rec_layout(O, A, n_mem, n_dot, n_def, n_fdot, n_fmem, false);
+  if (O.size > L.size) {  // cannot happen for a canonical record
+    if (lane == 0u) fail(g.status, CRDT_ENONCANON);
+    return;
+  }
+  uint8_t* wout = g.out + o;
+
+  // ---- pass 2: write (HBM)
+  if (lane < A) ((uint64_t*)(wout + O.o_clk))[lane] = top[lane] > w.ct[lane] ? top[lane] : 0ull;
+  {
+    uint32_t at_m = 0, at_d = 0;
+    for (uint32_t b = 0; b < L.n_mem; b += kW) {
+      const uint32_t m = b + lane;
+      uint32_t fin = 0, names = 0;
+      bool above = false, alive = false;
+      const uint32_t d0 = m < L.n_mem ? mbeg(m) : 0u, d1 = m < L.n_mem ? mend(m) : 0u;
+      if (m < L.n_mem) {
+        names = w.nm[m];
+        for (uint32_t d = d0; d < d1; ++d) {
+          const uint32_t x = dact[d] & (kTA - 1u);
+          const uint64_t v = dctr[d];
+          const bool gt = v > w.ct[x];
+          const bool dk = killed(names, x, v);
+          above = above || gt;
+          alive = alive || !dk;
+          fin += gt && !dk ? 1u : 0u;
+        }
+      }
+      const bool kept = above && alive;
+      const uint64_t K = __ballot(kept);
+      const uint32_t pm = at_m + mbcnt(K);
+      const uint32_t cnt = kept ? fin : 0u;
+      const uint32_t pd = at_d + wave_excl(cnt, lane);
+      if (kept) {
+        ((uint64_t*)(wout + O.o_key))[pm] = key[m];
+        ((uint32_t*)(wout + O.o_mdend))[pm] = pd + cnt;
+        uint32_t q = pd;
+        for (uint32_t d = d0; d < d1; ++d) {
+          const uint32_t x = dact[d] & (kTA - 1u);
+          const uint64_t v = dctr[d];
+          if (v > w.ct[x] && !killed(names, x, v)) {
+            ((uint64_t*)(wout + O.o_dctr))[q] = v;
+            ((uint32_t*)(wout + O.o_dact))[q] = dact[d];
+            ++q;
+          }
+        }
+      }
+      at_m += (uint32_t)__popcll(K);
+      at_d += wave_sum(cnt);
+    }
+  }
+  {
+    uint32_t at = 0, at_d = 0, at_m = 0;
+    for (uint32_t b = 0; b < L.n_def; b += kW) {
+      const uint32_t k = b + lane;
+      bool keepd = false;
+      uint32_t d0 = 0, d1 = 0, m0 = 0, m1 = 0;
+      if (k < L.n_def) {
+        d0 = fdb(k);
+        d1 = fde(k);
+        m0 = fmb(k);
+        m1 = fme(k);
+        for (uint32_t d = d0; d < d1; ++d) {
+          const uint32_t x = fact[d];
+          const uint64_t t = x < A ? top[x] : 0ull, cx = x < kTA ? w.ct[x] : 0ull;
+          keepd = keepd || fctr[d] > (t > cx ? t : cx);
+        }
+      }
+      const uint64_t K = __ballot(keepd);
+      const uint32_t nd = keepd ? d1 - d0 : 0u, nmm = keepd ? m1 - m0 : 0u;
+      const uint32_t p = at + mbcnt(K), pd = at_d + wave_excl(nd, lane), pmm = at_m + wave_excl(nmm, lane);
+      if (keepd) {
+        for (uint32_t d = 0; d < nd; ++d) {
+          ((uint64_t*)(wout + O.o_fctr))[pd + d] = fctr[d0 + d];
+          ((uint32_t*)(wout + O.o_fact))[pd + d] = fact[d0 + d];
+        }
+        for (uint32_t j = 0; j < nmm; ++j) ((uint64_t*)(wout + O.o_fkey))[pmm + j] = fkey[m0 + j];
+        ((uint32_t*)(wout + O.o_fdend))[p] = pd + nd;
+        ((uint32_t*)(wout + O.o_fmend))[p] = pmm + nmm;
+      }
+      at += (uint32_t)__popcll(K);
+      at_d += wave_sum(nd);
+      at_m += wave_sum(nmm);
+    }
+  }
+  if (lane == 0u && O.o_def != O.o_mpad) *(uint32_t*)(wout + O.o_mpad) = 0u;
+  if (lane >= 1u && lane < 4u && O.o_end + 4u * (lane - 1u) < O.size) *(uint32_t*)(wout + O.o_end + 4u * (lane - 1u)) = 0u;
+  if (lane == 0u) {
+    uint32_t* hw = (uint32_t*)wout;
+    hw[0] = O.size;
+    hw[1] = A;
+    hw[2] = n_mem;
+    hw[3] = n_dot;
+    hw[4] = n_def;
+    hw[5] = n_fdot;
+    hw[6] = n_fmem;
+    hw[7] = g.flags | (empty_clock ? kEmptyClockFlag : 0u);
+  }
+  tsync();  // the stage is reused by the wave's next record
+}
+
+__global__ __launch_bounds__(kW * kTWaves) void orswot_truncate_kernel(TruncArgs g) {
+  __shared__ TWs ws[kTWaves];
+  const uint32_t lane = threadIdx.x & (kW - 1u), wv = threadIdx.x / kW;
+  const uint64_t wave = (uint64_t)blockIdx.x * kTWaves + wv;
+  const uint64_t n_waves = (uint64_t)gridDim.x * kTWaves;
+  for (uint64_t i = wave; i < g.n_obj; i += n_waves) {
+    Rec R;
+    Run c;
+    uint64_t o;
+    if (!truncate_open(g, i, lane, R, c, o)) continue;
+    const RecLayout& L = R.L;
+    const bool lds = !R.sparse && L.n_clk <= kTA && L.size <= kTStage && L.n_def <= kTDef && L.n_mem <= kTStage / 24u;
+    if (lds) {
+      // every dot and deferred actor below A (else not canonical: the general form decides)
+      bool wide = false;
+      for (uint32_t d = lane; d < L.n_dot; d += kW) wide = wide || ((const uint32_t*)(R.r + L.o_dact))[d] >= L.n_clk;
+      for (uint32_t d = lane; d < L.n_def_dot; d += kW) wide = wide || ((const uint32_t*)(R.r + L.o_fact))[d] >= L.n_clk;
+      if (__ballot(wide) == 0ull) {
+        truncate_lds(g, R, c, o, lane, ws[wv]);
+        continue;
+      }
+    }
+    truncate_global(g, R, c, o, lane);
+  }
+}
+
 }  // namespace
 
 int launch_orswot_truncate(const crdt_orswot_batch& self, const crdt_clock_csr& clocks, uint32_t A, uint32_t flags,
@@ -365,12 +633,20 @@ int launch_orswot_truncate(const crdt_orswot_batch& self, const crdt_clock_csr& 
   if (self.n_obj == 0) return CRDT_OK;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const uint64_t want = (self.n_obj + 3) / 4;
-  const uint64_t cap = (uint64_t)cus * 8;
+  static std::atomic<int> occ{0};
+  int o = occ.load(std::memory_order_relaxed);
+  if (o == 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (const void*)orswot_truncate_kernel, kW * kTWaves, 0) !=
+            hipSuccess || o < 1)
+      o = 2;
+    occ.store(o, std::memory_order_relaxed);
+  }
+  const uint64_t want = (self.n_obj + kTWaves - 1) / kTWaves;
+  const uint64_t cap = (uint64_t)cus * (uint64_t)o;
   const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
-  hipLaunchKernelGGL(orswot_truncate_kernel, dim3(blocks), dim3(256), 0, stream, self.base, self.off,
-                     (uint64_t)self.bytes, (uint64_t)self.n_obj, clocks.off, clocks.len, clocks.act, clocks.ctr,
-                     (uint64_t)clocks.n_entries, A, flags, out, out_off, out_bytes, status);
+  const TruncArgs g{self.base, self.off, (uint64_t)self.bytes, (uint64_t)self.n_obj, clocks.off, clocks.len,
+                    clocks.act, clocks.ctr, (uint64_t)clocks.n_entries, A, flags, out, out_off, out_bytes, status};
+  hipLaunchKernelGGL(orswot_truncate_kernel, dim3(blocks), dim3(kW * kTWaves), 0, stream, g);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 

@@ -40,6 +40,19 @@ def test_random_states_incl_empty_member_clocks(gpu, oracle):
     assert sum(1 for f in flags if f & 2) > 100  # empty member clocks occur and match
 
 
+@pytest.mark.parametrize("A", [8, 40])
+def test_both_kernel_forms_in_one_batch(gpu, oracle, A):
+    """The kernel stages a record in LDS when it is dense, A <= 32, <= 4 KB and
+    has <= 8 deferred clocks, else reads it from HBM: at A = 8 one batch mixes
+    ordinary records with ones of 9-12 deferred clocks and > 4 KB ones (150-300
+    members); at A = 40 every record takes the HBM form."""
+    shapes = [{}, {"n_def": (9, 10, 12)}, {"members": 300}, {}]
+    states, clocks, recs = T.cases(4_000, A=A, seed=17, shapes=shapes)
+    assert max(len(r) for r in recs) > 4096 and max(len(s[2]) for s in states) > 8
+    lb, lo = records.pack_batch(recs)
+    _check(gpu, oracle, lb, lo, T.clocks_csr(clocks), A)
+
+
 def test_config3_truncated_by_the_other_replicas_clock(gpu, oracle):
     import crdts_hip
 

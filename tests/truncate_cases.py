@@ -11,7 +11,7 @@ import crdts_ref
 import records
 
 
-def random_state(rng, A, members=10):
+def random_state(rng, A, members=10, n_def=(0, 0, 1, 2, 3)):
     clock = {a: rng.randrange(1, 12) for a in range(A) if rng.random() < 0.8}
     entries = {}
     for m in rng.sample(range(1, 10_000), rng.randrange(0, members)):
@@ -19,7 +19,7 @@ def random_state(rng, A, members=10):
         if dots:
             entries[m] = dots
     deferred = {}
-    for _ in range(rng.choice([0, 0, 1, 2, 3])):
+    for _ in range(rng.choice(n_def)):
         d = {a: rng.randrange(1, 16) for a in range(A) if rng.random() < 0.3}
         if not d or all(clock.get(a, 0) >= c for a, c in d.items()):
             d[rng.randrange(A)] = 20 + rng.randrange(5)  # !(D <= clock): a pending remove
@@ -58,9 +58,10 @@ def clocks_csr(clocks):
     return off, ln, act, ctr
 
 
-def cases(n, A=8, seed=5):
+def cases(n, A=8, seed=5, shapes=None):
+    """shapes: optional list of random_state keyword sets, cycled over the n states."""
     rng = random.Random(seed)
-    states = [random_state(rng, A) for _ in range(n)]
+    states = [random_state(rng, A, **(shapes[i % len(shapes)] if shapes else {})) for i in range(n)]
     clocks = [truncating_clock(rng, A) for _ in range(n)]
     recs = [records.encode(c, e, d, A) for c, e, d in states]
     return states, clocks, recs

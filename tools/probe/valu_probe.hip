@@ -21,7 +21,7 @@ __global__ void valu_kernel(uint64_t* out, int iters) {
     if (OP == 3) asm volatile(R16("v_add_u32_e32 %0, %1, %2\n") : "=v"(e) : "v"(c), "v"(d));
     if (OP == 4) asm volatile(R16("v_mbcnt_lo_u32_b32 %0, %1, %2\n") : "=v"(e) : "s"((uint32_t)m), "v"(d));
     if (OP == 5) asm volatile(R16("v_cmp_eq_u64_e64 %0, %1, %2\n") : "=s"(m) : "v"(a), "v"(b));
-    if (OP == 6) asm volatile(R16("s_add_u32 %0, %1, 1\n") : "=s"(e) : "s"((uint32_t)m));
+    if (OP == 6) asm volatile(R16("v_bcnt_u32_b32 %0, %1, %2\n") : "=v"(e) : "v"(c), "v"(d));
     if (OP == 7) asm volatile(R16("v_lshl_add_u32 %0, %1, 3, %2\n") : "=v"(e) : "v"(c), "v"(d));
   }
   if (threadIdx.x == 0) out[blockIdx.x] = m + e;
@@ -48,7 +48,7 @@ int main() {
   uint64_t* d;
   if (hipMalloc(&d, 8 << 20) != hipSuccess) return 1;
   const char* names[] = {"v_cmp_lt_u32", "v_cmp_lt_u64", "v_cndmask_b32", "v_add_u32", "v_mbcnt_lo", "v_cmp_eq_u64",
-                         "s_add_u32", "v_lshl_add_u32"};
+                         "v_bcnt_u32_b32", "v_lshl_add_u32"};
   for (int w : {1, 2, 4, 8}) {
     printf("waves/SIMD %d:", w);
     const int it = 20000;
@@ -56,6 +56,7 @@ int main() {
                   run<4>(w, it, d), run<5>(w, it, d), run<6>(w, it, d), run<7>(w, it, d)};
     for (int k = 0; k < 8; ++k) printf(" %s %.3f ns", names[k], r[k]);
     printf("\n");
+    fflush(stdout);
   }
   return 0;
 }
