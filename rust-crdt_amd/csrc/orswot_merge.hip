@@ -2510,6 +2510,47 @@ __device__ __forceinline__ void prefetch_buf(u32x4 (&r)[kPer], const uint8_t* sr
 #pragma unroll
   for (uint32_t k = 0; k < kPer; ++k) r[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * (lane + k * kWave)), 0, AUX);
 }
+// prefetch_all with the record base and its last piece made wave-uniform
+// (SGPRs): each load is the SGPR base + a 32-bit lane offset (saddr form),
+// so the per-load VALU is the clamp and the shift, no 64-bit address add
+__device__ __forceinline__ void prefetch_sa(u32x4 (&r)[kPer], const uint8_t* src, uint32_t n16, uint32_t lane) {
+  const uint64_t b = (uint64_t)src;
+  typedef const __attribute__((address_space(1))) u32x4 gu32x4;
+  const __attribute__((address_space(1))) uint8_t* s = (const __attribute__((address_space(1))) uint8_t*)(
+      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+      (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b));  // (int -> u32 first: no sign extension)
+  const uint32_t last = __builtin_amdgcn_readfirstlane(n16 - 1u);
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t idx = lane + k * kWave;
+    r[k] = __builtin_nontemporal_load((gu32x4*)(s + 16u * (idx < last ? idx : last)));
+  }
+}
+// prefetch_sa with the clamp done on byte offsets (one v_min per load: the
+// lane's offset against the wave-uniform offset of the last piece)
+__device__ __forceinline__ void prefetch_sb(u32x4 (&r)[kPer], const uint8_t* src, uint32_t n16, uint32_t lane) {
+  const uint64_t b = (uint64_t)src;
+  typedef const __attribute__((address_space(1))) u32x4 gu32x4;
+  const __attribute__((address_space(1))) uint8_t* s = (const __attribute__((address_space(1))) uint8_t*)(
+      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+      (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b));  // (int -> u32 first: no sign extension)
+  const uint32_t lastb = 16u * __builtin_amdgcn_readfirstlane(n16 - 1u);
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t ob = 16u * (lane + k * kWave);
+    r[k] = __builtin_nontemporal_load((gu32x4*)(s + (ob < lastb ? ob : lastb)));
+  }
+}
+// copy_record_out with the clamp on byte offsets (wave-uniform last piece)
+__device__ __forceinline__ void copy_record_sb(uint32_t src, uint8_t* O, uint32_t n16, uint32_t lane) {
+  const uint32_t lastb = 16u * __builtin_amdgcn_readfirstlane(n16 - 1u);
+  const uint32_t b0 = 16u * lane, b1 = 16u * (lane + kWave);
+  const uint32_t o0 = b0 < lastb ? b0 : lastb, o1 = b1 < lastb ? b1 : lastb;
+  const u32x4 p0 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(src + o0);
+  const u32x4 p1 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(src + o1);
+  __builtin_nontemporal_store(p0, (u32x4*)(O + o0));
+  __builtin_nontemporal_store(p1, (u32x4*)(O + o1));
+}
 // copy_record_out through a buffer resource of the record's n16 pieces: the
 // stores of lanes past the record are dropped (the instruction count is fixed)
 __device__ __forceinline__ void copy_record_buf(uint32_t src, uint8_t* O, uint32_t n16, uint32_t lane) {
@@ -2518,6 +2559,32 @@ __device__ __forceinline__ void copy_record_buf(uint32_t src, uint8_t* O, uint32
   const u32x4 p1 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(src + 16u * (lane + kWave));
   __builtin_amdgcn_raw_buffer_store_b128(p0, rs, (int)(16u * lane), 0, kBufNT);
   __builtin_amdgcn_raw_buffer_store_b128(p1, rs, (int)(16u * (lane + kWave)), 0, kBufNT);
+}
+// The join kernel's record prefetch / copy-out by its IO variant (see
+// orswot_join_kernel): 0 clamped global loads / stores, 1-3 buffer
+// resources, 4 and 7 the saddr prefetch, 5-6 the byte-clamped prefetch;
+// copy-out byte-clamped for 5 and 7 (a carried-offset form, the current
+// object's offsets kept in SGPRs from the iteration that prefetched it,
+// spilled SGPRs: 0.789 vs 0.753 ms)
+template <int IO>
+__device__ __forceinline__ void prefetch_io(u32x4 (&r)[kPer], const uint8_t* src, uint32_t n16, uint32_t lane) {
+  if constexpr (IO >= 1 && IO <= 3)
+    prefetch_buf<IO == 3 ? 0 : kBufNT>(r, src, n16, lane);
+  else if constexpr (IO == 4 || IO == 7)
+    prefetch_sa(r, src, n16, lane);
+  else if constexpr (IO == 5 || IO == 6)
+    prefetch_sb(r, src, n16, lane);
+  else
+    prefetch_all(r, src, n16, lane);
+}
+template <int IO>
+__device__ __forceinline__ void copy_io(uint32_t src, uint8_t* O, uint32_t n16, uint32_t lane) {
+  if constexpr (IO == 2)
+    copy_record_buf(src, O, n16, lane);
+  else if constexpr (IO == 5 || IO == 7)
+    copy_record_sb(src, O, n16, lane);
+  else
+    copy_record_out(src, O, n16, lane);
 }
 // Only the 64-piece rounds a record of n16 pieces reaches (n16 wave-uniform).
 __device__ __forceinline__ void stage_used(u32x4* dst, const u32x4 (&r)[kPer], uint32_t n16, uint32_t lane) {
@@ -2996,13 +3063,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
       const uint32_t ts = dsel(t);
       if (!SPEC || ts != 0u) {  // (SPEC: object 0's records are already in flight)
         const uint32_t nn = lane_of(n16, ts);
-        if (IO >= 1) {
-          prefetch_buf<IO == 3 ? 0 : kBufNT>(pl, Lb + lane_of64(lo, ts), nn & 0xFFFFu, lane);
-          prefetch_buf<IO == 3 ? 0 : kBufNT>(pr, Rb + lane_of64(ro, ts), nn >> 16, lane);
-        } else {
-          prefetch_all(pl, Lb + lane_of64(lo, ts), nn & 0xFFFFu, lane);
-          prefetch_all(pr, Rb + lane_of64(ro, ts), nn >> 16, lane);
-        }
+        prefetch_io<IO>(pl, Lb + lane_of64(lo, ts), nn & 0xFFFFu, lane);
+        prefetch_io<IO>(pr, Rb + lane_of64(ro, ts), nn >> 16, lane);
       }
     }
     wave_sync();  // the previous chunk's last LDS reads are done
@@ -3016,16 +3078,9 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
       // the next object, or this one again after the chunk's last (a constant load count)
       const uint32_t u = pend ? (uint32_t)__builtin_ctzll(pend) : t;
       const uint32_t us = dsel(u);
-      {
-        const uint32_t nu = lane_of(n16, us);
-        if (IO >= 1) {
-          prefetch_buf<IO == 3 ? 0 : kBufNT>(pl, Lb + lane_of64(lo, us), nu & 0xFFFFu, lane);
-          prefetch_buf<IO == 3 ? 0 : kBufNT>(pr, Rb + lane_of64(ro, us), nu >> 16, lane);
-        } else {
-          prefetch_all(pl, Lb + lane_of64(lo, us), nu & 0xFFFFu, lane);
-          prefetch_all(pr, Rb + lane_of64(ro, us), nu >> 16, lane);
-        }
-      }
+      const uint32_t nu = lane_of(n16, us);
+      prefetch_io<IO>(pl, Lb + lane_of64(lo, us), nu & 0xFFFFu, lane);
+      prefetch_io<IO>(pr, Rb + lane_of64(ro, us), nu >> 16, lane);
       bool big = false;
       uint32_t r;
       if (MODE == 1) {
@@ -3077,10 +3132,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
           const u32x4 z = {0u, 0u, 0u, 0u};
           __builtin_nontemporal_store(z, (u32x4*)sink);
           __builtin_nontemporal_store(z, (u32x4*)sink + 1);
-        } else if (IO == 2) {
-          copy_record_buf(src, Ob + oo, fbu ? 1u : r, lane);
         } else {
-          copy_record_out(src, Ob + oo, fbu ? 1u : r, lane);
+          copy_io<IO>(src, Ob + oo, fbu ? 1u : r, lane);
         }
         *(Ooff + cbase + t) = oo | (fbu ? kPending : 0ull);
         if (fbu) {  // listed for the general kernel (a rare path: its extra memory operations
@@ -3106,8 +3159,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
       t = u;
       pend &= pend - 1;
       wave_sync();  // this object's LDS reads are done
-      stage_used(sL, pl, lane_of(n16, us) & 0xFFFFu, lane);
-      stage_used(sR, pr, lane_of(n16, us) >> 16, lane);
+      stage_used(sL, pl, nu & 0xFFFFu, lane);
+      stage_used(sR, pr, nu >> 16, lane);
       wave_sync();
     }
   }
@@ -3943,11 +3996,12 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // The product path: orswot_join_kernel in one pass (mask3_object for every
   // object; those with deferred removes take its HD form, direct stores) at 6
   // waves per SIMD with the guided split (5/8 of the objects in static chunks,
-  // the rest in 20-object ticket chunks), then the general kernel (measured
-  // best, tools/ab_bench.py). Other variants exist in
+  // the rest in 20-object ticket chunks), record prefetch in the saddr form
+  // and the copy-out clamped on byte offsets (IO 7), then the general kernel
+  // (measured best, tools/ab_bench.py). Other variants exist in
   // -DCRDT_DIAG builds only.
   (void)variant;
-  return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5>);
+  return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7>);
 #else
   if (variant == 134) return go(launch_join_passes<6, true, true, true, true, 1>);  // timing only: no kill
   if (variant == 135) return go(launch_join_passes<6, true, true, true, true, 2>);  // timing only: no deferred block
@@ -3991,6 +4045,10 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // r03: record prefetch (250) and also the copy-out (251) through buffer resources
   if (variant == 250) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 1>);
   if (variant == 251) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 2>);
+  if (variant == 256) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 6>);
+  if (variant == 257) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7>);
+  if (variant == 255) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 5>);
+  if (variant == 254) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 4>);
   if (variant == 253) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 3>);
   // r03: the kill pass by a union key table and per-clock actor masks (HK 1)
   if (variant == 252) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 0, 1>);

@@ -31,7 +31,7 @@ struct BlockTickets {
   }
   __device__ uint64_t enter() {  // the next ticket's first object (n: none left)
     dyn = true;
-    const uint64_t o0 = s_total + (uint64_t)__builtin_amdgcn_readfirstlane(tk) * K;
+    const uint64_t o0 = s_total + (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(tk) * K;
     if (o0 >= n) return n;
     end = o0 + K < n ? o0 + K : n;
     if (lane == 0u) tk = atomicAdd(ctr, 1u);  // the ticket after this one
