@@ -1499,7 +1499,10 @@ __device__ __forceinline__ const uint8_t* gptr(uint32_t a) {
 // RT: member ranks searched in padded key tables (else clamped probes of the stage)
 // HK (with HD): 1 = the kill pass finds a deferred member's union slot by one
 // search of a union key table and a clock's D[x] by its actor presence mask
-template <uint32_t OUTCAP, int OUT = 0, bool HD = false, int HABL = 0, bool RT = true, int HK = 0>  // OUT: 0 direct stores, 1 sink-predicated, 2 LDS-assembled
+// PK: objects with nL + nR <= 64 members search both sides' ranks in ONE
+// 64-lane pass (L members in lanes [0, nL), R members in [nL, nL + nR)), half
+// the search instructions of the two-sided form
+template <uint32_t OUTCAP, int OUT = 0, bool HD = false, int HABL = 0, bool RT = true, int HK = 0, bool PK = false>  // OUT: 0 direct stores, 1 sink-predicated, 2 LDS-assembled
 __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint32_t uX, uint8_t* O, uint32_t A,
                                                  uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane,
                                                  bool& big, uint8_t* sink = nullptr) {
@@ -1541,8 +1544,26 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
     *(lds_u64*)(size_t)(tL + l8) = bit_of(mnL, lane) ? kl : ~0ull;
     *(lds_u64*)(size_t)(tR + l8) = bit_of(mnR, lane) ? kr : ~0ull;
     wave_sync();
-    uint32_t ql = tR, qr = tL;  // address of the first key not known to be below the lane's key
     const uint32_t n = nL > nR ? nL : nR;
+    if (PK && nL + nR <= (uint32_t)kWave) {
+      // lane i < nL: L member i (searches tR); nL <= lane < nL + nR: R member
+      // lane - nL (searches tL); the rest search tR for ~0 (masked out)
+      const bool isR = lane >= nL;
+      const uint64_t k = isR ? lr64(tR + 8u * ((lane - nL) & 63u)) : kl;
+      const uint32_t t0 = isR ? tL : tR;
+      uint32_t q = t0;
+      if (n >= 64u) q = lr64(q + 504u) < k ? q + 512u : q;
+      if (n >= 32u) q = lr64(q + 248u) < k ? q + 256u : q;
+#pragma unroll
+      for (uint32_t step = 128u; step >= 8u; step >>= 1) q = lr64(q + step - 8u) < k ? q + step : q;
+      const uint32_t r = (q - t0) >> 3;
+      const uint64_t E = cmp64<kEQ>(lr64(q), k) & cmp32<kUGT>(isR ? nL : nR, r) & lanes_below(nL + nR);
+      rl = r;
+      rr = gather32(r, (nL + lane) & 63u);
+      EL = E & mnL;
+      ER = nL < 64u ? (E >> nL) & mnR : 0ull;
+    } else {
+    uint32_t ql = tR, qr = tL;  // address of the first key not known to be below the lane's key
     if (n >= 64u) {
       ql = lr64(ql + 504u) < kl ? ql + 512u : ql;
       qr = lr64(qr + 504u) < kr ? qr + 512u : qr;
@@ -1564,6 +1585,7 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
     const uint64_t kel = lr64(ql), ker = lr64(qr);
     EL = cmp64<kEQ>(kel, kl) & cmp32<kUGT>(nR, rl) & mnL;
     ER = cmp64<kEQ>(ker, kr) & cmp32<kUGT>(nL, rr) & mnR;
+    }
   } else {
     uint32_t pl = rk0, pr = lk0;
     {
@@ -2926,7 +2948,7 @@ __attribute__((noinline)) __device__ uint32_t hd_join(const uint8_t* Ls, const u
 // the copy-out too (copy_record_buf)
 template <int MINW, int MODE, int OUT = 2, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
           bool RT = true, uint32_t DYN = 0, uint32_t SF = 6, bool SPEC = false, uint32_t GMIN = 0, int IO = 0,
-          int HK = 0>
+          int HK = 0, bool PK = false>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
@@ -3110,7 +3132,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
         if ((defs >> td) & 1ull) {
           if (HDD) {
             if (M3HD)
-              r = mask3_object<0xFFFFFFFFu, 0, true, HABL, RT, HK>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
+              r = mask3_object<0xFFFFFFFFu, 0, true, HABL, RT, HK, PK>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
                                                      d & 0xFFFFu, m >> 16, d >> 16, lane, big);
             else
               r = mask_object<0xFFFFFFFFu, true, 0, DC>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo),
@@ -3121,7 +3143,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
           }
           src = lds_addr(out_s[wave]);
         } else {
-          r = mask3_object<0xFFFFFFFFu, 3, false, 0, RT>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A,
+          r = mask3_object<0xFFFFFFFFu, 3, false, 0, RT, 0, PK>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A,
                                                          m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, sink);
           src = lds_addr(sL);
         }
@@ -3925,7 +3947,7 @@ namespace {
 // then the general kernel.
 template <int MINW, bool ONE = true, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
           bool RT = true, uint32_t DYN = 0, bool DK = false, uint32_t SF = 6, bool V10 = false, bool SPEC = false,
-          uint32_t GMIN = 0, int IO = 0, int HK = 0>
+          uint32_t GMIN = 0, int IO = 0, int HK = 0, bool PK = false>
 int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                        const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
                        uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
@@ -3945,7 +3967,7 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
   } else
 #endif
   if constexpr (ONE) {
-    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL, RT, DYN, SF, SPEC, GMIN, IO, HK>;
+    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL, RT, DYN, SF, SPEC, GMIN, IO, HK, PK>;
   } else {
 #ifdef CRDT_DIAG
     f1 = (const void*)orswot_join_kernel<MINW, 1>;
@@ -3997,11 +4019,12 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // object; those with deferred removes take its HD form, direct stores) at 6
   // waves per SIMD with the guided split (5/8 of the objects in static chunks,
   // the rest in 20-object ticket chunks), record prefetch in the saddr form
-  // and the copy-out clamped on byte offsets (IO 7), then the general kernel
+  // and the copy-out clamped on byte offsets (IO 7), both sides' member ranks
+  // in one packed pass when nL + nR <= 64 (PK), then the general kernel
   // (measured best, tools/ab_bench.py). Other variants exist in
   // -DCRDT_DIAG builds only.
   (void)variant;
-  return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7>);
+  return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true>);
 #else
   if (variant == 134) return go(launch_join_passes<6, true, true, true, true, 1>);  // timing only: no kill
   if (variant == 135) return go(launch_join_passes<6, true, true, true, true, 2>);  // timing only: no deferred block
@@ -4045,6 +4068,8 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // r03: record prefetch (250) and also the copy-out (251) through buffer resources
   if (variant == 250) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 1>);
   if (variant == 251) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 2>);
+  // r03: both sides' member ranks in one packed pass when nL + nR <= 64 (PK)
+  if (variant == 259) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true>);
   if (variant == 256) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 6>);
   if (variant == 257) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7>);
   if (variant == 255) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 5>);

@@ -399,21 +399,60 @@ __device__ __forceinline__ void tsync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ void truncate_lds(const TruncArgs& g, const Rec& R, const Run& c, uint64_t o, uint32_t lane, TWs& w) {
-  const RecLayout& L = R.L;
-  const uint32_t A = L.n_clk;
-  // ---- stage the record, the clock and the deferred rows
+constexpr uint32_t kTPer = kTStage / 16u / kW;  // 16-B record pieces per lane
+typedef uint32_t tu32x4 __attribute__((ext_vector_type(4)));
+// An LDS-form object's record (every 16-B piece, clamped to its last) and the
+// first 64 entries of its clock, in registers one object ahead
+struct TPre {
+  tu32x4 r[kTPer];
+  uint32_t a;
+  uint64_t c;
+};
+__device__ __forceinline__ void tfetch(TPre& p, const uint8_t* rec, uint32_t n16, const Run& c, uint32_t lane) {
+#pragma unroll
+  for (uint32_t k = 0; k < kTPer; ++k) {
+    const uint32_t i = lane + k * kW;
+    p.r[k] = __builtin_nontemporal_load((const tu32x4*)rec + (i < n16 ? i : n16 - 1u));
+  }
+  p.a = 0xFFFFFFFFu;
+  p.c = 0ull;
+  if (lane < c.n) { p.a = c.a[lane]; p.c = c.c[lane]; }
+}
+
+// Stage an LDS-form record (p: its prefetched pieces and first 64 clock
+// entries; c: its clock run, for entries past those) and zero the tables.
+__device__ void tstage(TWs& w, const RecLayout& L, const TPre& p, const Run& c, uint32_t lane) {
   const uint32_t n16 = L.size / 16u;
-  for (uint32_t p = lane; p < n16; p += kW) ((uint4*)w.stage)[p] = ((const uint4*)R.r)[p];
+#pragma unroll
+  for (uint32_t k = 0; k < kTPer; ++k)
+    if (lane + k * kW < n16) ((tu32x4*)w.stage)[lane + k * kW] = p.r[k];
   if (lane < kTA) w.ct[lane] = 0ull;
   for (uint32_t k = lane; k < kTDef * kTA; k += kW) w.drow[k / kTA][k % kTA] = 0ull;
   for (uint32_t m = lane; m < L.n_mem; m += kW) w.nm[m] = 0u;
   tsync();
-  for (uint32_t e = lane; e < c.n; e += kW) {
+  if (p.a < kTA) w.ct[p.a] = p.c;  // actors >= A name nothing a dense record holds
+  for (uint32_t e = kW + lane; e < c.n; e += kW) {
     const uint32_t x = c.a[e];
-    if (x < kTA) w.ct[x] = c.c[e];  // actors >= A name nothing a dense record holds
+    if (x < kTA) w.ct[x] = c.c[e];
   }
+}
+
+// The LDS form of one staged record. wide: a dot or deferred actor >= A (not
+// canonical here): nothing written, the HBM form decides.
+__device__ void truncate_lds(const TruncArgs& g, const Rec& R, uint64_t o, uint32_t lane, TWs& w, bool& wide) {
+  const RecLayout& L = R.L;
+  const uint32_t A = L.n_clk;
   const uint8_t* S = (const uint8_t*)w.stage;
+  {
+    bool wd = false;
+    for (uint32_t d = lane; d < L.n_dot; d += kW) wd = wd || ((const uint32_t*)(S + L.o_dact))[d] >= A;
+    for (uint32_t d = lane; d < L.n_def_dot; d += kW) wd = wd || ((const uint32_t*)(S + L.o_fact))[d] >= A;
+    if (__ballot(wd) != 0ull) {
+      wide = true;
+      tsync();
+      return;
+    }
+  }
   const uint32_t* fdend = (const uint32_t*)(S + L.o_fdend);
   const uint32_t* fmend = (const uint32_t*)(S + L.o_fmend);
   const uint32_t* fact = (const uint32_t*)(S + L.o_fact);
@@ -600,29 +639,88 @@ __device__ void truncate_lds(const TruncArgs& g, const Rec& R, const Run& c, uin
   tsync();  // the stage is reused by the wave's next record
 }
 
+// One wave per 64-record chunk: lane k reads record cbase + k's offset, clock
+// run and header (one round trip for the chunk); then the chunk's LDS-form
+// records are truncated one by one with the next one's record and clock in
+// flight in registers, and the others (CSR top clocks, records past the LDS
+// limits or not canonical here) in the HBM form.
 __global__ __launch_bounds__(kW * kTWaves) void orswot_truncate_kernel(TruncArgs g) {
   __shared__ TWs ws[kTWaves];
   const uint32_t lane = threadIdx.x & (kW - 1u), wv = threadIdx.x / kW;
+  TWs& w = ws[wv];
   const uint64_t wave = (uint64_t)blockIdx.x * kTWaves + wv;
   const uint64_t n_waves = (uint64_t)gridDim.x * kTWaves;
-  for (uint64_t i = wave; i < g.n_obj; i += n_waves) {
+  const bool sparse = (g.flags & kSparseClock) != 0u;
+  for (uint64_t cb = wave * kW; cb < g.n_obj; cb += n_waves * kW) {
+    const uint64_t obj = cb + lane;
+    const bool valid = obj < g.n_obj;
+    uint64_t o = 0, c0 = 0;
+    uint32_t cn = 0;
+    if (valid) {
+      o = g.off[obj];
+      c0 = g.coff[obj];
+      cn = g.clen[obj];
+      g.out_off[obj] = o;
+    }
+    bool ok = valid && (o & 15u) == 0u && o <= g.bytes && g.bytes - o >= kHdrBytes;
+    tu32x4 h0 = {0u, 0u, 0u, 0u}, h1 = h0;
+    if (ok) {
+      h0 = ((const tu32x4*)(g.base + o))[0];
+      h1 = ((const tu32x4*)(g.base + o))[1];
+    }
+    RecLayout L;
+    rec_layout(L, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, sparse);
+    ok = ok && h0.x == L.size && h1.w == g.flags && (sparse ? h0.y <= g.A : h0.y == g.A) && L.size <= g.bytes - o &&
+         o + L.size <= g.out_bytes && c0 <= g.c_entries && cn <= g.c_entries - c0;
+    if (__ballot(valid && !ok) != 0ull && lane == 0u) fail(g.status, CRDT_ENONCANON);
+    const bool lds = ok && !sparse && h0.y <= kTA && L.size <= kTStage && h1.x <= kTDef && h0.z <= kTStage / 24u;
+    auto rec_of = [&](uint32_t t, Rec& R, Run& c, uint64_t& ot) {
+      ot = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)o, t) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(o >> 32), t) << 32);
+      const uint64_t ct0 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)c0, t) |
+                           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(c0 >> 32), t) << 32);
+      R = Rec{g.base + ot, {}, sparse};
+      rec_layout(R.L, __builtin_amdgcn_readlane(h0.y, t), __builtin_amdgcn_readlane(h0.z, t),
+                 __builtin_amdgcn_readlane(h0.w, t), __builtin_amdgcn_readlane(h1.x, t),
+                 __builtin_amdgcn_readlane(h1.y, t), __builtin_amdgcn_readlane(h1.z, t), sparse);
+      c = Run{g.cact + ct0, g.cctr + ct0, (uint32_t)__builtin_amdgcn_readlane(cn, t)};
+    };
+    // the HBM form (rare on dense batches)
+    for (uint64_t m = __ballot(ok && !lds); m; m &= m - 1u) {
+      Rec R;
+      Run c;
+      uint64_t ot;
+      rec_of((uint32_t)__builtin_ctzll(m), R, c, ot);
+      truncate_global(g, R, c, ot, lane);
+    }
+    // the LDS form, one record ahead
+    uint64_t pend = __ballot(lds);
+    if (pend == 0ull) continue;
+    uint32_t t = (uint32_t)__builtin_ctzll(pend);
+    pend &= pend - 1u;
     Rec R;
     Run c;
-    uint64_t o;
-    if (!truncate_open(g, i, lane, R, c, o)) continue;
-    const RecLayout& L = R.L;
-    const bool lds = !R.sparse && L.n_clk <= kTA && L.size <= kTStage && L.n_def <= kTDef && L.n_mem <= kTStage / 24u;
-    if (lds) {
-      // every dot and deferred actor below A (else not canonical: the general form decides)
-      bool wide = false;
-      for (uint32_t d = lane; d < L.n_dot; d += kW) wide = wide || ((const uint32_t*)(R.r + L.o_dact))[d] >= L.n_clk;
-      for (uint32_t d = lane; d < L.n_def_dot; d += kW) wide = wide || ((const uint32_t*)(R.r + L.o_fact))[d] >= L.n_clk;
-      if (__ballot(wide) == 0ull) {
-        truncate_lds(g, R, c, o, lane, ws[wv]);
-        continue;
+    uint64_t ot;
+    rec_of(t, R, c, ot);
+    TPre p;
+    tfetch(p, R.r, R.L.size / 16u, c, lane);
+    for (;;) {
+      const Rec Rc = R;
+      const uint64_t oc = ot;
+      const Run cc = c;
+      tstage(w, Rc.L, p, cc, lane);
+      const bool more = pend != 0ull;
+      if (more) {  // the next record's loads, in flight while this one is truncated
+        t = (uint32_t)__builtin_ctzll(pend);
+        pend &= pend - 1u;
+        rec_of(t, R, c, ot);
+        tfetch(p, R.r, R.L.size / 16u, c, lane);
       }
+      bool wide = false;
+      truncate_lds(g, Rc, oc, lane, w, wide);
+      if (wide) truncate_global(g, Rc, cc, oc, lane);
+      if (!more) break;
     }
-    truncate_global(g, R, c, o, lane);
   }
 }
 
