@@ -492,7 +492,9 @@ int crdt_map_mvreg_merge(crdt_ctx* ctx, const crdt_map_mvreg_slab* self, const c
  *     vdset_n[kcap][vdcap], vdset[kcap][vdcap][vscap]   their member sets, ascending
  *   n_def, dclock[dcap][A]                     the map's deferred removes, CLOCK ORDER
  *   dset_n[dcap], dset[dcap][scap]             their key sets, ascending
- * Unused slots are zero on output. Per side kcap, mcap, dcap, scap <= 32,
+ * Only the used slots of the output are written: slots past a count keep
+ * whatever the buffer held (a reader goes by the counts; zeroing them cost
+ * ~10x the state's own bytes in writes). Per side kcap, mcap, dcap, scap <= 32,
  * vdcap, vscap <= 16, n_actors <= 64; output capacities must hold the result
  * (else CRDT_ECAPACITY is latched for that object). The map's deferred
  * removes are applied in CLOCK ORDER: the reference iterates a HashMap there

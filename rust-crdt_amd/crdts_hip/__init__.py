@@ -294,6 +294,41 @@ class MapOrswotSlab:
         return MapOrswotSlab({f: (v.cpu().numpy().view(np.uint32 if v.dtype.itemsize == 4 else np.uint64)
                                   if hasattr(v, "cpu") else v) for f, v in self.a.items()}, self.caps)
 
+    def used_masks(self):
+        """Per field, a boolean array of its shape: the slots the state uses
+        (key slots below n_keys, members below vn_mem, deferred below vn_def /
+        n_def, set elements below their sizes; clocks and counts of used
+        slots). Host slabs."""
+        a = self.host().a
+        kcap, mcap, vdcap, vscap, dcap, scap = (self.caps[k] for k in ("kcap", "mcap", "vdcap", "vscap", "dcap",
+                                                                      "scap"))
+        key = np.arange(kcap)[None, :] < a["n_keys"][:, None]  # [n, kcap]
+        mem = key[:, :, None] & (np.arange(mcap)[None, None, :] < a["vn_mem"][:, :, None])  # [n, kcap, mcap]
+        vdef = key[:, :, None] & (np.arange(vdcap)[None, None, :] < a["vn_def"][:, :, None])  # [n, kcap, vdcap]
+        vset = vdef[..., None] & (np.arange(vscap)[None, None, None, :] < a["vdset_n"][..., None])
+        dfr = np.arange(dcap)[None, :] < a["n_def"][:, None]  # [n, dcap]
+        dset = dfr[..., None] & (np.arange(scap)[None, None, :] < a["dset_n"][..., None])
+        full = lambda f: np.ones(a[f].shape, bool)  # noqa: E731
+        per = {"clock": full("clock"), "n_keys": full("n_keys"), "n_def": full("n_def"), "keys": key,
+               "eclock": key[..., None], "vclock": key[..., None], "vn_mem": key, "vn_def": key, "vmem": mem,
+               "vmclock": mem[..., None], "vdclock": vdef[..., None], "vdset_n": vdef, "vdset": vset,
+               "dclock": dfr[..., None], "dset_n": dfr, "dset": dset}
+        return {f: np.broadcast_to(m, a[f].shape) for f, m in per.items()}
+
+    def canonical(self):
+        """Host copy with every slot past its count zeroed: the merge writes
+        only the used slots (include/crdts_hip.h), so two slabs hold the same
+        states iff their canonical forms are equal."""
+        a = {f: np.array(v, copy=True) for f, v in self.host().a.items()}
+        for f, m in self.used_masks().items():
+            a[f][~m] = 0
+        return MapOrswotSlab(a, self.caps)
+
+    def used_bytes(self):
+        """Bytes of the used slots (the state's own bytes, not its capacity)."""
+        h = self.host().a
+        return int(sum(int(m.sum()) * h[f].dtype.itemsize for f, m in self.used_masks().items()))
+
     def cstruct(self):
         from ._lib import MAP_ORSWOT_CAPS, MAP_ORSWOT_FIELDS, MapOrswotSlabC
 
@@ -561,12 +596,14 @@ class Engine:
 
     # ------------------------------------------------ Map<u64, Orswot<u64>>
     def map_orswot_merge(self, S: "MapOrswotSlab", O: "MapOrswotSlab", n_actors, out_caps=None, stream=None,
-                         check_status=True):
+                         check_status=True, out=None):
         """Map::merge with Orswot values (src/map.rs:192-269) of device slabs;
-        returns the output slab (default capacities: the sums of the inputs')."""
+        returns the output slab (default capacities: the sums of the inputs').
+        Only the used slots of the output are written (`out`, if given, is
+        reused as it is: compare `.canonical()` forms)."""
         n = S.n
         caps = out_caps or {k: S.caps[k] + O.caps[k] for k in S.caps}
-        R = MapOrswotSlab.alloc(n, n_actors, device=S.a["clock"].device, **caps)
+        R = out if out is not None else MapOrswotSlab.alloc(n, n_actors, device=S.a["clock"].device, **caps)
         s, o, r = S.cstruct(), O.cstruct(), R.cstruct()
         check(lib.crdt_map_orswot_merge(self.ctx, C.byref(s), C.byref(o), C.byref(r), n, n_actors,
                                         self._stream(stream)), "map_orswot_merge")

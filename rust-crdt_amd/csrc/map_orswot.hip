@@ -72,8 +72,7 @@ __device__ __forceinline__ bool set_has(const uint64_t* set, uint32_t n, uint64_
 }
 
 // dst[e] = at(e) for e < n, all lanes: 16-B non-temporal stores when dst is
-// 16-B aligned and n even (the zero-filled capacity dominates the bytes this
-// kernel writes), 8-B stores otherwise.
+// 16-B aligned and n even, 8-B stores otherwise.
 typedef uint64_t mo_u64x2 __attribute__((ext_vector_type(2)));
 template <class F>
 __device__ __forceinline__ void fill64(uint64_t* dst, uint64_t n, uint32_t lane, F at) {
@@ -287,16 +286,14 @@ __device__ bool ws_store(const Ws& W, uint64_t clk, const crdt_map_orswot_slab& 
   const uint64_t* dclk = W.dclk;
   const uint64_t* dset = W.dset;
   const uint32_t* dn = W.dn;
-  fill64(R.vmem + kr * R.mcap, R.mcap, lane, [&](uint64_t j) { return j < nm ? key[j] : 0ull; });
-  fill64(R.vmclock + kr * R.mcap * c.A, (uint64_t)R.mcap * c.A, lane,
-         [&](uint64_t e) { return e < nmA ? row[e] : 0ull; });
-  fill64(R.vdclock + kr * R.vdcap * c.A, (uint64_t)R.vdcap * c.A, lane,
-         [&](uint64_t e) { return e < ndA ? dclk[e] : 0ull; });
-  for (uint32_t d = lane; d < R.vdcap; d += kMoW) R.vdset_n[kr * R.vdcap + d] = d < nd ? dn[d] : 0u;
-  fill64(R.vdset + kr * R.vdcap * R.vscap, (uint64_t)R.vdcap * R.vscap, lane, [&](uint64_t e) {
-    const uint32_t d = (uint32_t)(e / vs), j = (uint32_t)(e % vs);
-    return (d < nd && j < dn[d]) ? dset[d * SW + j] : 0ull;
-  });
+  // only the used slots are written (the capacity past the counts is left
+  // as it was: include/crdts_hip.h)
+  fill64(R.vmem + kr * R.mcap, nm, lane, [&](uint64_t j) { return key[j]; });
+  fill64(R.vmclock + kr * R.mcap * c.A, nmA, lane, [&](uint64_t e) { return row[e]; });
+  fill64(R.vdclock + kr * R.vdcap * c.A, ndA, lane, [&](uint64_t e) { return dclk[e]; });
+  for (uint32_t d = lane; d < nd; d += kMoW) R.vdset_n[kr * R.vdcap + d] = dn[d];
+  for (uint32_t d = 0; d < nd; ++d)
+    fill64(R.vdset + (kr * R.vdcap + d) * vs, uni(dn[d]), lane, [&](uint64_t j) { return dset[d * SW + j]; });
   return true;
 }
 
@@ -459,19 +456,6 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
       if (hs) ++a;
       if (ho) ++b;
     }
-    {  // unused key slots: zero, all lanes over each array's flat tail
-      const uint64_t k0 = i * R.kcap + nk, k1 = (i + 1u) * R.kcap;
-      auto zero = [](uint64_t) { return 0ull; };
-      for (uint64_t e = k0 + lane; e < k1; e += kMoW) { R.vn_mem[e] = 0u; R.vn_def[e] = 0u; }
-      fill64(R.keys + k0, k1 - k0, lane, zero);
-      fill64(R.eclock + k0 * A, (k1 - k0) * A, lane, zero);
-      fill64(R.vclock + k0 * A, (k1 - k0) * A, lane, zero);
-      fill64(R.vmem + k0 * R.mcap, (k1 - k0) * R.mcap, lane, zero);
-      fill64(R.vmclock + k0 * R.mcap * A, (k1 - k0) * R.mcap * A, lane, zero);
-      fill64(R.vdclock + k0 * R.vdcap * A, (k1 - k0) * R.vdcap * A, lane, zero);
-      for (uint64_t e = k0 * R.vdcap + lane; e < k1 * R.vdcap; e += kMoW) R.vdset_n[e] = 0u;
-      fill64(R.vdset + k0 * R.vdcap * R.vscap, (k1 - k0) * R.vdcap * R.vscap, lane, zero);
-    }
     if (lane == 0u) R.n_keys[i] = nk;
     if (lane < A) R.clock[i * A + lane] = cM;
     // ---- map deferred kept: the combined clocks the merged clock does not cover, sets united
@@ -498,17 +482,10 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
           if (cnt < R.scap) R.dset[dr * R.scap + cnt] = kk;
           ++cnt;
         }
-        for (uint32_t z = cnt; z < R.scap; ++z) R.dset[dr * R.scap + z] = 0ull;
         R.dset_n[dr] = cnt < R.scap ? cnt : R.scap;
       }
       over = over || uni(cnt) > R.scap;
       ++nd;
-    }
-    {
-      const uint64_t d0 = i * R.dcap + nd, d1 = (i + 1u) * R.dcap;
-      for (uint64_t e = d0 + lane; e < d1; e += kMoW) R.dset_n[e] = 0u;
-      for (uint64_t e = d0 * A + lane; e < d1 * A; e += kMoW) R.dclock[e] = 0ull;
-      for (uint64_t e = d0 * R.scap + lane; e < d1 * R.scap; e += kMoW) R.dset[e] = 0ull;
     }
     if (lane == 0u) R.n_def[i] = nd;
     if (over && lane == 0u) atomicCAS(status, 0, CRDT_ECAPACITY);

@@ -2939,6 +2939,129 @@ __attribute__((noinline)) __device__ uint32_t hd_join(const uint8_t* Ls, const u
   return r;
 }
 
+// DRN (the product): the objects past the join's limits are joined inside
+// the same launch, not by a second kernel. They are listed as before (the
+// entry = object index | the launch's epoch tag); when a block's four waves
+// have left the object loop, its wave 0 claims listed entries and joins them
+// by mask3_object from 8 KB stages carved out of the block's whole LDS
+// (drain_one), marking each entry done; the last block to finish joins what
+// is left, resets the words the next launch uses and advances the epoch (no
+// memset before a launch). The short general kernel that follows (the kernel
+// boundary orders it after every store of the join) clears the flags of the
+// done entries and joins the rest itself; a list overflow makes it scan.
+// No fence and no acquire / release is used across blocks: on this part
+// those write back / invalidate a whole XCD's L2 (the first form of the drain
+// took the launch from 0.75 to 1.19 ms). What crosses blocks does so through
+// agent-scope atomics (the counters and the entries), and a drained object's
+// output offset is not read from Ooff (it is Loff + Roff by the placement rule).
+// Words (relative to the kernel's ctl), p = the launch's epoch parity:
+// [p] list count, [2] claimed, [3] chunk tickets, [4] epoch, [5] blocks done,
+// [6 + p] list overflow. The general kernel of epoch e reads [e & 1] and
+// [6 + (e & 1)]; the last block of epoch e + 1 zeroes them for epoch e + 2.
+constexpr uint32_t kTagShift = 40;  // list entry: object index | tag << 40 | done << 63
+constexpr uint64_t kObjMask = (1ull << kTagShift) - 1ull;
+constexpr uint64_t kEntryDone = 1ull << 63;
+__device__ __forceinline__ uint64_t list_tag(uint32_t epoch) {
+  return (uint64_t)(epoch % 0x7FFFFFu + 1u) << kTagShift;  // never 0: entries other kernels wrote never match
+}
+constexpr uint32_t kDrainStage = 8192;  // per side: half of the block's record stages
+
+// One listed object joined by mask3_object from the block's 8 KB stages (uL,
+// uR; uX the scratch: LDS addresses); false, with nothing written, when it is
+// past mask3's limits even so (the general kernel then joins it).
+__device__ __forceinline__ bool drain_one(const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb,
+                                          const uint64_t* Roff, uint8_t* Ob, uint64_t o, uint32_t A, uint32_t uL,
+                                          uint32_t uR, uint32_t uX, uint32_t lane) {
+  const uint64_t lo = Loff[o], ro = Roff[o];
+  const uint8_t* lr = Lb + lo;
+  const uint8_t* rr = Rb + ro;
+  const u32x4 hl0 = ((const u32x4*)lr)[0], hl1 = ((const u32x4*)lr)[1];
+  const u32x4 hr0 = ((const u32x4*)rr)[0], hr1 = ((const u32x4*)rr)[1];
+  const uint32_t szl = uni(hl0.x), szr = uni(hr0.x), nL = uni(hl0.z), nR = uni(hr0.z), dL = uni(hl0.w),
+                 dR = uni(hr0.w);
+  if (!(szl <= kDrainStage && szr <= kDrainStage && A <= 32u && nL <= 64u && nR <= 64u && dL <= 64u && dR <= 64u &&
+        uni(hl1.x) <= 32u && uni(hr1.x) <= 32u))
+    return false;
+  wave_sync();
+  for (uint32_t k = lane; k < szl / 16u; k += kWave)
+    *(__attribute__((address_space(3))) u32x4*)(size_t)(uL + 16u * k) = ((const u32x4*)lr)[k];
+  for (uint32_t k = lane; k < szr / 16u; k += kWave)
+    *(__attribute__((address_space(3))) u32x4*)(size_t)(uR + 16u * k) = ((const u32x4*)rr)[k];
+  wave_sync();
+  bool big = false;
+  const uint32_t r = mask3_object<0xFFFFFFFFu, 0, true>(uL, uR, uX, Ob + lo + ro, A, nL, dL, nR, dR, lane, big);
+  wave_sync();
+  return r != kLeanFallback;  // (a union past 64 members: found before any store)
+}
+
+// The drain of one block (its wave 0, after the block's four waves left the
+// object loop): claim listed entries while there are any; the last block
+// takes what is left and resets the words of the next launch.
+// (ST, diagnostic builds: per-block times and counts in the list's upper half)
+template <bool ST = false>
+__device__ __forceinline__ void join_drain(const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb,
+                                           const uint64_t* Roff, uint8_t* Ob, uint32_t A, uint32_t* ctl,
+                                           uint64_t* list, uint32_t list_cap, uint32_t uL, uint32_t uR, uint32_t uX,
+                                           uint32_t lane, uint32_t n_blocks) {
+  constexpr int R = __ATOMIC_RELAXED, SA = __HIP_MEMORY_SCOPE_AGENT;
+  const uint64_t t_in = ST ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  uint32_t n_mine = 0u;
+  const uint32_t ep = uni(__hip_atomic_load(&ctl[4], R, SA)), p = ep & 1u;
+  const uint64_t tag = list_tag(ep);
+  // entry e of this launch (its lister may still be between its count and its store)
+  auto entry = [&](uint32_t e) -> uint64_t {
+    uint64_t v;
+    do {
+      v = __hip_atomic_load(&list[e], R, SA);
+      v = ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+    } while ((v & ~kObjMask) != tag);
+    return v;
+  };
+  auto one = [&](uint32_t e) {
+    const uint64_t v = entry(e);
+    if (drain_one(Lb, Loff, Rb, Roff, Ob, v & kObjMask, A, uL, uR, uX, lane) && lane == 0u)
+      __hip_atomic_store(&list[e], v | kEntryDone, R, SA);
+  };
+  for (;;) {
+    const uint32_t n = uni(__hip_atomic_load(&ctl[p], R, SA)), c = uni(__hip_atomic_load(&ctl[2], R, SA));
+    if (c >= (n < list_cap ? n : list_cap)) break;
+    uint32_t won = 0u;
+    if (lane == 0u) {
+      uint32_t want = c;
+      won = __hip_atomic_compare_exchange_strong(&ctl[2], &want, c + 1u, R, R, SA) ? 1u : 0u;
+    }
+    if (uni(won)) {
+      one(c);
+      ++n_mine;
+    }
+  }
+  uint32_t d = 0u;
+  if (lane == 0u) d = __hip_atomic_fetch_add(&ctl[5], 1u, R, SA);
+  if (ST && lane == 0u && blockIdx.x < 8000u) {
+    list[32768u + 4u * blockIdx.x] = t_in;
+    list[32768u + 4u * blockIdx.x + 1u] = __builtin_amdgcn_s_memrealtime();
+    list[32768u + 4u * blockIdx.x + 2u] = ((uint64_t)n_mine << 32) | uni(d);
+  }
+  if (uni(d) != n_blocks - 1u) return;
+  // the last block: every other block has passed its barrier (its listing is
+  // stored) and left its drain
+  const uint32_t n = uni(__hip_atomic_load(&ctl[p], R, SA));
+  const uint32_t c0 = uni(__hip_atomic_load(&ctl[2], R, SA));
+  for (uint32_t c = c0; c < (n < list_cap ? n : list_cap); ++c) one(c);
+  if (ST && lane == 0u) {
+    list[32768u + 4u * blockIdx.x + 3u] = __builtin_amdgcn_s_memrealtime();
+    list[32760u] = ((uint64_t)n << 32) | c0;
+  }
+  if (lane == 0u) {  // the next launch's words; this launch's count and overflow flag stay for the general kernel
+    __hip_atomic_store(&ctl[p ^ 1u], 0u, R, SA);
+    __hip_atomic_store(&ctl[6u + (p ^ 1u)], 0u, R, SA);
+    __hip_atomic_store(&ctl[2], 0u, R, SA);
+    __hip_atomic_store(&ctl[3], 0u, R, SA);
+    __hip_atomic_store(&ctl[5], 0u, R, SA);
+    __hip_atomic_store(&ctl[4], ep + 1u, R, SA);
+  }
+}
+
 // HDD (MODE 3): the deferred objects' join writes straight to HBM
 // (mask_object<HD>) and is followed by the same tail stores as the other
 // path, redirected to the sink: every path issues at least as many stores
@@ -2948,7 +3071,7 @@ __attribute__((noinline)) __device__ uint32_t hd_join(const uint8_t* Ls, const u
 // the copy-out too (copy_record_buf)
 template <int MINW, int MODE, int OUT = 2, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
           bool RT = true, uint32_t DYN = 0, uint32_t SF = 6, bool SPEC = false, uint32_t GMIN = 0, int IO = 0,
-          int HK = 0, bool PK = false>
+          int HK = 0, bool PK = false, bool DRN = false>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
@@ -2967,7 +3090,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
   u32x4* const sR = stage_s[wave][1];
   uint8_t* const X = (uint8_t*)scr_s[wave];
   const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
-  const uint64_t ts0 = HABL == 6 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
+  const uint64_t ts0 = HABL == 6 || HABL == 7 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
   uint32_t n_joined = 0u, n_hd = 0u, n_chunk = 0u;                                  // (HABL 6: per-wave counts)
   const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
   const uint64_t rounds = (n_obj + n_waves * kWave - 1) / (n_waves * kWave);
@@ -3047,7 +3170,16 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
           if (hd && base < kDeferListCap) dlist[base] = obj;
         }
       }
-      if (gen) {  // hand the object to the general kernel
+      if (DRN) {  // listed for the drain (a rare path)
+        if (__ballot(gen) != 0ull) {
+          const uint32_t ep = uni(__hip_atomic_load(&ctl[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          const uint32_t e = gen ? atomicAdd(&ctl[ep & 1u], 1u) : 0u;
+          if (gen && e < list_cap)
+            __hip_atomic_store(&list[e], obj | list_tag(ep), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (__ballot(gen && e >= list_cap) != 0ull && lane == 0u)  // past the list: the general kernel scans
+            __hip_atomic_store(&ctl[6u + (ep & 1u)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else if (gen) {  // hand the object to the general kernel
         const uint32_t e = atomicAdd(&ctl[0], 1u);
         if (e < list_cap) list[e] = obj;
       }
@@ -3155,10 +3287,21 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
           __builtin_nontemporal_store(z, (u32x4*)sink);
           __builtin_nontemporal_store(z, (u32x4*)sink + 1);
         } else {
-          copy_io<IO>(src, Ob + oo, fbu ? 1u : r, lane);
+          // (DRN: a fallback's placeholder piece goes to the sink: the drain,
+          // possibly on another XCD, writes that record in this launch)
+          copy_io<IO>(src, DRN && fbu ? sink : Ob + oo, fbu ? 1u : r, lane);
         }
         *(Ooff + cbase + t) = oo | (fbu ? kPending : 0ull);
-        if (fbu) {  // listed for the general kernel (a rare path: its extra memory operations
+        if (DRN && fbu) {  // listed for the drain (past the list: the general kernel scans)
+          if (lane == 0u) {
+            const uint32_t ep = __hip_atomic_load(&ctl[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t e = atomicAdd(&ctl[ep & 1u], 1u);
+            if (e < list_cap)
+              __hip_atomic_store(&list[e], (cbase + t) | list_tag(ep), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+              __hip_atomic_store(&ctl[6u + (ep & 1u)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        } else if (fbu) {  // listed for the general kernel (a rare path: its extra memory operations
                     // only add to the count the loop-head wait sees)
           if (lane == 0u) {
             const uint32_t e = atomicAdd(&ctl[0], 1u);
@@ -3185,6 +3328,14 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
       stage_used(sR, pr, nu >> 16, lane);
       wave_sync();
     }
+  }
+  if (DRN && HABL != 8) {  // the block's LDS is free once its four waves are here: wave 0 drains the list
+    __syncthreads();
+    if (HABL == 9) return;  // (timing only: the barrier without the drain)
+    if (HABL == 7 && wave == 0u && lane == 0u && blockIdx.x == 0u) list[32761u] = ts0;
+    if (wave == 0u)
+      join_drain<HABL == 7>(Lb, Loff, Rb, Roff, Ob, A, ctl, list, list_cap, lds_addr(stage_s[0][0]),
+                            lds_addr(stage_s[2][0]), lds_addr(scr_s[0]), lane, gridDim.x);
   }
 #ifdef CRDT_DIAG
   if (HABL == 6 && lane == 0u && wave_id < 10922u) {  // timing only: the list's upper half holds the stamps
@@ -3236,7 +3387,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_dyn_
   uint8_t* const X = (uint8_t*)scr_s[wave];
   const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
   const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint64_t ts0 = HABL == 6 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
+  const uint64_t ts0 = HABL == 6 || HABL == 7 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
   uint32_t n_joined = 0u, n_hd = 0u, n_chunk = 0u;                                  // (HABL 6: per-wave counts)
   uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
   const uint64_t n_chunks = (n_obj + kDynG - 1) / kDynG;
@@ -3424,7 +3575,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_v10_
   uint8_t* const X = (uint8_t*)scr_s[wave];
   const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
   const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint64_t ts0 = HABL == 6 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
+  const uint64_t ts0 = HABL == 6 || HABL == 7 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
   uint32_t n_joined = 0u, n_hd = 0u, n_chunk = 0u;                                  // (HABL 6: per-wave counts)
   uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
 
@@ -3665,11 +3816,27 @@ __device__ __forceinline__ void general_one(const uint8_t* Lb, const uint64_t* L
 __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, const uint8_t* __restrict__ Rb,
     const uint64_t* __restrict__ Roff, uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t n_obj,
-    uint32_t A, uint32_t* __restrict__ ctl, const uint64_t* __restrict__ list, uint32_t list_cap) {
+    uint32_t A, uint32_t* __restrict__ ctl, const uint64_t* __restrict__ list, uint32_t list_cap,
+    const uint32_t* __restrict__ drn) {
   __shared__ u32x4 gen_s[3][kGenStage / 16];
   const uint32_t lane = threadIdx.x;
-  const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  const uint32_t scan = uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (drn) {  // after a draining join (DRN): the flags of its done entries, its leftovers
+    const uint32_t ep = uni(__hip_atomic_load(&drn[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - 1u;  // (advanced)
+    const uint32_t p = ep & 1u, n = uni(__hip_atomic_load(&drn[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (uni(__hip_atomic_load(&drn[6u + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+      for (uint32_t e = blockIdx.x; e < n; e += gridDim.x) {
+        const uint64_t v = __hip_atomic_load(&list[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), o = v & kObjMask;
+        if (v & kEntryDone) {
+          if (lane == 0u) Ooff[o] = Loff[o] + Roff[o];
+        } else {
+          general_one(Lb, Loff, Rb, Roff, Ob, Ooff, o, A, gen_s[0], gen_s[1], gen_s[2], lane);
+        }
+      }
+      return;
+    }
+  }  // (a list overflow: every flag is scanned, drained objects joined again)
+  const uint32_t n = drn ? ~0u : uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const uint32_t scan = drn ? 1u : uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (n <= list_cap && scan == 0u) {
     for (uint32_t e = blockIdx.x; e < n; e += gridDim.x)
       general_one(Lb, Loff, Rb, Roff, Ob, Ooff, list[e], A, gen_s[0], gen_s[1], gen_s[2], lane);
@@ -3947,7 +4114,7 @@ namespace {
 // then the general kernel.
 template <int MINW, bool ONE = true, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
           bool RT = true, uint32_t DYN = 0, bool DK = false, uint32_t SF = 6, bool V10 = false, bool SPEC = false,
-          uint32_t GMIN = 0, int IO = 0, int HK = 0, bool PK = false>
+          uint32_t GMIN = 0, int IO = 0, int HK = 0, bool PK = false, bool DRN = false>
 int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                        const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
                        uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
@@ -3967,7 +4134,7 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
   } else
 #endif
   if constexpr (ONE) {
-    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL, RT, DYN, SF, SPEC, GMIN, IO, HK, PK>;
+    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL, RT, DYN, SF, SPEC, GMIN, IO, HK, PK, DRN>;
   } else {
 #ifdef CRDT_DIAG
     f1 = (const void*)orswot_join_kernel<MINW, 1>;
@@ -3990,17 +4157,23 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
   }
   const uint64_t chunks = (n_obj + kWave - 1) / kWave;
   const uint64_t want = (chunks + kWavesPerBlock - 1) / kWavesPerBlock;
+  // DRN: the kernel's own control words (ctl[4..11]), reset by its last
+  // block; the general kernel then clears the drained objects' flags
+  uint32_t* kctl = DRN ? ctl + 4 : ctl;
   void* args[] = {&Lb, &Loff, &Lbytes, &Rb, &Roff, &Rbytes, &Ob, &Ooff, &Obytes, &n_obj, &n_actors, &status,
-                  &ctl, &list, &list_cap};
-  if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
+                  &kctl, &list, &list_cap};
+  if (!DRN && hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
+  // (HABL 8 / 9, timing only: no drain, so the host zeroes the kernel's words)
+  if (DRN && (HABL == 8 || HABL == 9) && hipMemsetAsync(kctl, 0, 8 * sizeof(uint32_t), stream) != hipSuccess)
+    return CRDT_EHIP;
   for (int k = 0; k < passes; ++k) {
     const uint64_t cap = (uint64_t)cus * (blocks_per_cu > 0 ? blocks_per_cu : occ[k]);
     const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
     if (hipLaunchKernel(fs[k], dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) != hipSuccess)
       return CRDT_EHIP;
   }
-  hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
-                     Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
+  hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff, Ob,
+                     Ooff, n_obj, n_actors, ctl, list, list_cap, DRN ? (const uint32_t*)kctl : nullptr);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 }  // namespace
@@ -4070,6 +4243,18 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   if (variant == 251) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 2>);
   // r03: both sides' member ranks in one packed pass when nL + nR <= 64 (PK)
   if (variant == 259) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true>);
+  if (variant == 262)  // timing only: DRN without the drain (and without its barrier: 263 keeps it)
+    return go(launch_join_passes<6, true, true, true, true, 8, true, 20, false, 5, false, false, 0, 7, 0, true, true>);
+  if (variant == 263)
+    return go(launch_join_passes<6, true, true, true, true, 9, true, 20, false, 5, false, false, 0, 7, 0, true, true>);
+  if (variant == 261)  // + drain stamps (HABL 7, timing only: list upper half)
+    return go(launch_join_passes<6, true, true, true, true, 7, true, 20, false, 5, false, false, 0, 7, 0, true, true>);
+  // r03: + the drain (DRN: no general kernel, no memset), the product for n_actors <= 32
+  if (variant == 260) {
+    if (n_actors > 32u)
+      return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true>);
+    return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, true>);
+  }
   if (variant == 256) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 6>);
   if (variant == 257) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7>);
   if (variant == 255) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 5>);
@@ -4172,7 +4357,7 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // no general pass after them (their output is not a valid batch anyway)
   if (variant == 109 || variant == 14 || variant == 16) return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
   hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
-                     Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
+                     Ob, Ooff, n_obj, n_actors, ctl, list, list_cap, nullptr);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 #endif
 }

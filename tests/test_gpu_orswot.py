@@ -384,3 +384,56 @@ def test_guided_split_batch_sizes(n, gpu, oracle):
     for _ in range(2):
         out = _gpu_merge(gpu, lb, lo, rb, ro, 16)
         _compare(out, ob, oo, f"n={n}")
+
+
+def _mixed_batch(n_small=20_000, seed=21):
+    """Config-3 pairs with two kinds of objects past the join's limits mixed
+    in at random positions, all over 16 actors: records past the 2 KB stage
+    (listed at the chunk step) and pairs of near-disjoint ~45-member sides
+    whose union passes 64 members (found inside the join)."""
+    import crdts_hip
+
+    (sb, so), (tb, to) = crdts_hip.generate_orswot(n_small, threads=16, seed=seed)
+    big = dict(member_universe=200, ancestor_adds=150, max_div_ops=40)
+    (bb, bo), (cb, co) = crdts_hip.generate_orswot(300, threads=16, seed=seed + 1, params=big)
+    wide = dict(member_universe=100_000, ancestor_adds=45, min_div_ops=0, max_div_ops=2)
+    (wb, wo), _ = crdts_hip.generate_orswot(300, threads=16, seed=seed + 2, params=wide)
+    (xb, xo), _ = crdts_hip.generate_orswot(300, threads=16, seed=seed + 3, params=wide)
+    L = records.unpack_batch(sb, so) + records.unpack_batch(bb, bo) + records.unpack_batch(wb, wo)
+    R = records.unpack_batch(tb, to) + records.unpack_batch(cb, co) + records.unpack_batch(xb, xo)
+    perm = np.random.default_rng(seed).permutation(len(L))
+    lb, lo = records.pack_batch([L[i] for i in perm])
+    rb, ro = records.pack_batch([R[i] for i in perm])
+    return lb, lo, rb, ro
+
+
+def test_drain_mixed_batch_list_caps(gpu, oracle):
+    """The product join drains its own list (no general kernel, no memset:
+    orswot_join_kernel DRN): objects past the 2 KB stage and unions past 64
+    members, listed at random positions of a config-3 batch, are joined inside
+    the launch; with a small or empty list the listers join them from HBM.
+    Launches repeat on one context (the kernel re-zeroes its control words and
+    advances the entry epoch) and alternate with the 64-actor path, which
+    zeroes its own words and writes untagged list entries."""
+    lb, lo, rb, ro = _mixed_batch()
+    ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, 16, threads=16)
+    # how many objects leave the fast path: some of each kind
+    hl = lb.view(np.uint32)[(lo // 4).astype(np.int64)]
+    hr = rb.view(np.uint32)[(ro // 4).astype(np.int64)]
+    assert ((hl > 2048) | (hr > 2048)).sum() > 100
+    gl = np.stack([lb[int(o) + 8:int(o) + 12].view(np.uint32)[0] for o in lo])
+    assert (gl >= 40).sum() > 100
+    import crdts_hip
+
+    params = dict(n_actors=64, member_universe=200, ancestor_adds=150, max_div_ops=40)
+    (pb, po), (qb, qo) = crdts_hip.generate_orswot(200, threads=16, seed=4, params=params)
+    pob, poo = oracle.orswot_merge_batch(pb, po, qb, qo, 64, threads=16)
+    try:
+        for cap in (65536, 8, 0, 65536, 65536):
+            gpu.set_list_cap(cap)
+            _compare(_gpu_merge(gpu, lb, lo, rb, ro, 16), ob, oo, f"mixed, cap {cap}")
+            _compare(_gpu_merge(gpu, pb, po, qb, qo, 64), pob, poo, f"64 actors after cap {cap}")
+        for k in range(3):  # back to back on one stream
+            _compare(_gpu_merge(gpu, lb, lo, rb, ro, 16), ob, oo, f"repeat {k}")
+    finally:
+        gpu.set_list_cap(65536)
