@@ -26,9 +26,7 @@ constexpr uint32_t kDeferListCap = 1u << 20;
 struct crdt_ctx {
   int device;
   int* d_status;        // d_scratch + 0
-  uint32_t* d_ctl;      // d_scratch + 16: [list count, scan flag, deferred count, chunk tickets] (zeroed by
-                        // each launcher), then the Orswot join's own [list count, claimed, blocks done, tickets,
-                        // epoch] at [4..8] (left zeroed by the kernel itself: orswot_join_kernel DRN)
+  uint32_t* d_ctl;      // d_scratch + 16: [list count, scan flag, deferred count, chunk tickets] (+ spare)
   uint64_t* d_list;     // d_scratch + 64
   uint32_t list_cap;
   int blocks_per_cu;    // diagnostic builds only (crdt_ctx_set_blocks_per_cu)

@@ -1502,13 +1502,22 @@ __device__ __forceinline__ const uint8_t* gptr(uint32_t a) {
 // PK: objects with nL + nR <= 64 members search both sides' ranks in ONE
 // 64-lane pass (L members in lanes [0, nL), R members in [nL, nL + nR)), half
 // the search instructions of the two-sided form
-template <uint32_t OUTCAP, int OUT = 0, bool HD = false, int HABL = 0, bool RT = true, int HK = 0, bool PK = false>  // OUT: 0 direct stores, 1 sink-predicated, 2 LDS-assembled
+template <uint32_t OUTCAP, int OUT = 0, bool HD = false, int HABL = 0, bool RT = true, int HK = 0, bool PK = false,
+          bool BK = false>  // OUT: 0 direct stores, 1 sink-predicated, 2 LDS-assembled
 __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint32_t uX, uint8_t* O, uint32_t A,
                                                  uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane,
                                                  bool& big, uint8_t* sink = nullptr) {
 #ifndef CRDT_DIAG
   static_assert(HABL == 0, "timing-only ablations (HABL != 0) exist in -DCRDT_DIAG builds only");
 #endif
+  // BK: LDS bank conflicts — union descriptors one dword per slot (L index in
+  // byte 0, R index in byte 1: no two lanes' byte stores share a dword), the
+  // sink moved past them, 4-byte sink stores at a 4-byte lane stride (an
+  // 8-byte stride put two lanes in every bank), the header written under exec
+  static_assert(!(BK && HK == 1), "BK moves the sink over HK 1's deferred clock masks");
+  constexpr uint32_t TR = BK ? 1792u : k3Trash;  // the wave's sink (512 B)
+  constexpr uint32_t DS = BK ? 4u : 2u;          // bytes per union descriptor
+  static_assert(!BK || TR >= k3Desc + 256u, "BK descriptors: 64 dwords before the sink");
   big = false;
   const uint32_t key = kHdrBytes + 8u * A;
   const uint32_t ctrL = key + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
@@ -1627,11 +1636,14 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
 
   // ---- scratch: zero the mask tables and union descriptors, then the
   // per-member {actor mask, survives mask} by 64-bit atomic ORs
-  const uint32_t trash = uX + k3Trash + l8;
+  const uint32_t trash = uX + TR + l8;
   *(lds_u64*)(size_t)(uX + k3MsL + l8) = 0ull;
   *(lds_u64*)(size_t)(uX + k3MsR + l8) = 0ull;
   *(lds_u64*)(size_t)(uX + k3EqGe + l8) = 0ull;
-  *(lds_u16*)(size_t)(uX + k3Desc + 2u * lane) = (uint16_t)0;
+  if (BK)
+    *(lds_u32*)(size_t)(uX + k3Desc + 4u * lane) = 0u;
+  else
+    *(lds_u16*)(size_t)(uX + k3Desc + 2u * lane) = (uint16_t)0;
   wave_sync();
   const uint32_t bl = 1u << (xl & 31u), br = 1u << (xr & 31u);
   {
@@ -1643,8 +1655,9 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     // union descriptors: L lanes store index + 1 in the low byte of their
     // slot, R lanes in the high byte (a shared key: both, same slot)
-    *(lds_u8*)(size_t)(bit_of(mnL, lane) ? uX + k3Desc + 2u * ul : trash) = (uint8_t)(lane + 1u);
-    *(lds_u8*)(size_t)(bit_of(mnR, lane) ? uX + k3Desc + 2u * ur + 1u : trash) = (uint8_t)(lane + 1u);
+    const uint32_t trash1 = BK ? uX + TR + 4u * lane : trash;
+    *(lds_u8*)(size_t)(bit_of(mnL, lane) ? uX + k3Desc + DS * ul : trash1) = (uint8_t)(lane + 1u);
+    *(lds_u8*)(size_t)(bit_of(mnR, lane) ? uX + k3Desc + DS * ur + 1u : trash1) = (uint8_t)(lane + 1u);
   }
   wave_sync();
 
@@ -1668,7 +1681,8 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
   wave_sync();
 
   // ---- per union member: the mask join
-  const uint32_t dsc = *(const __attribute__((address_space(3))) uint16_t*)(size_t)(uX + k3Desc + 2u * lane);
+  const uint32_t dsc = BK ? lr32(uX + k3Desc + 4u * lane)
+                          : *(const __attribute__((address_space(3))) uint16_t*)(size_t)(uX + k3Desc + 2u * lane);
   const uint32_t mi = (dsc - 1u) & 63u, mj = ((dsc >> 8) - 1u) & 63u;
   const uint64_t pL = lr64(uX + k3MsL + 8u * mi), pR = lr64(uX + k3MsR + 8u * mj), pE = lr64(uX + k3EqGe + l8);
   const uint64_t mU = lanes_below(U);
@@ -1724,7 +1738,7 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
         const uint32_t a = lr32(us + (isL ? DL.v.fact : DR.v.fact) + 4u * e);
         wide = wide || (act && a >= 32u);
         const bool put = act && a < 32u;
-        __hip_atomic_fetch_or((lds_u32*)(size_t)(put ? uX + k3DefMask + 4u * (isL ? k : 32u + k) : uX + k3Trash + l8),
+        __hip_atomic_fetch_or((lds_u32*)(size_t)(put ? uX + k3DefMask + 4u * (isL ? k : 32u + k) : uX + TR + l8),
                               put ? 1u << a : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       if (__ballot(wide) != 0ull) return kLeanFallback;
@@ -1744,7 +1758,7 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
         for (uint32_t step = 256u; step >= 8u; step >>= 1) q = lr64(q + step - 8u) < m ? q + step : q;
         const uint32_t su = (q - ut) >> 3;
         const bool hit = act && su < U && lr64(q) == m;
-        __hip_atomic_fetch_or((lds_u64*)(size_t)(hit ? dmt + 8u * su : uX + k3Trash + l8),
+        __hip_atomic_fetch_or((lds_u64*)(size_t)(hit ? dmt + 8u * su : uX + TR + l8),
                               hit ? 1ull << (isL ? k : 32u + k) : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     } else
@@ -1776,7 +1790,7 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
       const uint32_t sul = gather32(ul, il & 63u), sur = gather32(ur, ir & 63u);  // every lane: bpermute sources
       const uint32_t su = eqL ? sul : sur;
       const bool hit = act && (eqL || eqR);
-      __hip_atomic_fetch_or((lds_u64*)(size_t)(hit ? dmt + 8u * (su & 63u) : uX + k3Trash + l8),
+      __hip_atomic_fetch_or((lds_u64*)(size_t)(hit ? dmt + 8u * (su & 63u) : uX + TR + l8),
                             hit ? 1ull << (isL ? k : 32u + k) : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     wave_sync();
@@ -1821,9 +1835,9 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
       bitsl &= bitsl - 1u;
       bitsr &= bitsr - 1u;
     }
-    __hip_atomic_fetch_and((lds_u64*)(size_t)(kl2 ? uX + k3Out + 8u * gl : uX + k3Trash + l8), kl2 ? ~(uint64_t)bl : ~0ull,
+    __hip_atomic_fetch_and((lds_u64*)(size_t)(kl2 ? uX + k3Out + 8u * gl : uX + TR + l8), kl2 ? ~(uint64_t)bl : ~0ull,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_and((lds_u64*)(size_t)(kr2 ? uX + k3Out + 8u * gr : uX + k3Trash + l8), kr2 ? ~(uint64_t)br : ~0ull,
+    __hip_atomic_fetch_and((lds_u64*)(size_t)(kr2 ? uX + k3Out + 8u * gr : uX + TR + l8), kr2 ? ~(uint64_t)br : ~0ull,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     wave_sync();
     keep = bit_of(mU, lane) ? (uint32_t)lr64(uX + k3Out + l8) : 0u;
@@ -1879,20 +1893,24 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
     // occupied the texture-address unit (TA_BUSY 62-65 % of the kernel)
     fb = fb || size > 2u * 16u * kWave;  // larger outputs: the general kernel
     wave_sync();  // every read of the input stage (kk above) is done
-    const uint32_t tw = uX + k3Trash + l8;
+    const uint32_t tw = uX + TR + l8, tw4 = BK ? uX + TR + 4u * lane : tw;
     *(lds_u64*)(size_t)(bit_of(keepm, lane) ? uL + o_key + 8u * midx : tw) = kk;
-    *(lds_u32*)(size_t)(bit_of(keepm, lane) ? uL + o_mdend + 4u * midx : tw) = d0 + c;
+    *(lds_u32*)(size_t)(bit_of(keepm, lane) ? uL + o_mdend + 4u * midx : tw4) = d0 + c;
     *(lds_u64*)(size_t)(lane < A ? uL + kHdrBytes + l8 : tw) = top;
-    *(lds_u32*)(size_t)(wl ? uL + o_dact + 4u * il : tw) = xl2;
+    *(lds_u32*)(size_t)(wl ? uL + o_dact + 4u * il : tw4) = xl2;
     *(lds_u64*)(size_t)(wl ? uL + o_dctr + 8u * il : tw) = vl2;
-    *(lds_u32*)(size_t)(wr ? uL + o_dact + 4u * ir : tw) = xr2;
+    *(lds_u32*)(size_t)(wr ? uL + o_dact + 4u * ir : tw4) = xr2;
     *(lds_u64*)(size_t)(wr ? uL + o_dctr + 8u * ir : tw) = vr2;
     const bool mp = lane == 0u && o_def != o_mpad;
     const bool rp = lane >= 1u && lane < 4u && o_def + 4u * (lane - 1u) < size;
-    *(lds_u32*)(size_t)(mp ? uL + o_mpad : rp ? uL + o_def + 4u * (lane - 1u) : tw) = 0u;
+    *(lds_u32*)(size_t)(mp ? uL + o_mpad : rp ? uL + o_def + 4u * (lane - 1u) : tw4) = 0u;
     const u32x4 hv = lane == 0u ? u32x4{size, A, tot_mem, tot_dot} : u32x4{0u, 0u, 0u, 0u};
-    *(__attribute__((address_space(3))) u32x4*)(size_t)(lane < 2u ? uL + 16u * lane : uX + k3Trash + 16u * (lane & 31u)) =
-        hv;  // (16-B sink slots: lanes l and l + 32 share one, inside the 512-B sink)
+    if (BK) {
+      if (lane < 2u) *(__attribute__((address_space(3))) u32x4*)(size_t)(uL + 16u * lane) = hv;
+    } else {
+      *(__attribute__((address_space(3))) u32x4*)(size_t)(lane < 2u ? uL + 16u * lane : uX + TR + 16u * (lane & 31u)) =
+          hv;  // (16-B sink slots: lanes l and l + 32 share one, inside the 512-B sink)
+    }
     if (OUT == 2) {  // OUT 3: the caller copies the record out
       wave_sync();
       copy_record_out(uL, O, fb ? 1u : size / 16u, lane);
@@ -2939,129 +2957,6 @@ __attribute__((noinline)) __device__ uint32_t hd_join(const uint8_t* Ls, const u
   return r;
 }
 
-// DRN (the product): the objects past the join's limits are joined inside
-// the same launch, not by a second kernel. They are listed as before (the
-// entry = object index | the launch's epoch tag); when a block's four waves
-// have left the object loop, its wave 0 claims listed entries and joins them
-// by mask3_object from 8 KB stages carved out of the block's whole LDS
-// (drain_one), marking each entry done; the last block to finish joins what
-// is left, resets the words the next launch uses and advances the epoch (no
-// memset before a launch). The short general kernel that follows (the kernel
-// boundary orders it after every store of the join) clears the flags of the
-// done entries and joins the rest itself; a list overflow makes it scan.
-// No fence and no acquire / release is used across blocks: on this part
-// those write back / invalidate a whole XCD's L2 (the first form of the drain
-// took the launch from 0.75 to 1.19 ms). What crosses blocks does so through
-// agent-scope atomics (the counters and the entries), and a drained object's
-// output offset is not read from Ooff (it is Loff + Roff by the placement rule).
-// Words (relative to the kernel's ctl), p = the launch's epoch parity:
-// [p] list count, [2] claimed, [3] chunk tickets, [4] epoch, [5] blocks done,
-// [6 + p] list overflow. The general kernel of epoch e reads [e & 1] and
-// [6 + (e & 1)]; the last block of epoch e + 1 zeroes them for epoch e + 2.
-constexpr uint32_t kTagShift = 40;  // list entry: object index | tag << 40 | done << 63
-constexpr uint64_t kObjMask = (1ull << kTagShift) - 1ull;
-constexpr uint64_t kEntryDone = 1ull << 63;
-__device__ __forceinline__ uint64_t list_tag(uint32_t epoch) {
-  return (uint64_t)(epoch % 0x7FFFFFu + 1u) << kTagShift;  // never 0: entries other kernels wrote never match
-}
-constexpr uint32_t kDrainStage = 8192;  // per side: half of the block's record stages
-
-// One listed object joined by mask3_object from the block's 8 KB stages (uL,
-// uR; uX the scratch: LDS addresses); false, with nothing written, when it is
-// past mask3's limits even so (the general kernel then joins it).
-__device__ __forceinline__ bool drain_one(const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb,
-                                          const uint64_t* Roff, uint8_t* Ob, uint64_t o, uint32_t A, uint32_t uL,
-                                          uint32_t uR, uint32_t uX, uint32_t lane) {
-  const uint64_t lo = Loff[o], ro = Roff[o];
-  const uint8_t* lr = Lb + lo;
-  const uint8_t* rr = Rb + ro;
-  const u32x4 hl0 = ((const u32x4*)lr)[0], hl1 = ((const u32x4*)lr)[1];
-  const u32x4 hr0 = ((const u32x4*)rr)[0], hr1 = ((const u32x4*)rr)[1];
-  const uint32_t szl = uni(hl0.x), szr = uni(hr0.x), nL = uni(hl0.z), nR = uni(hr0.z), dL = uni(hl0.w),
-                 dR = uni(hr0.w);
-  if (!(szl <= kDrainStage && szr <= kDrainStage && A <= 32u && nL <= 64u && nR <= 64u && dL <= 64u && dR <= 64u &&
-        uni(hl1.x) <= 32u && uni(hr1.x) <= 32u))
-    return false;
-  wave_sync();
-  for (uint32_t k = lane; k < szl / 16u; k += kWave)
-    *(__attribute__((address_space(3))) u32x4*)(size_t)(uL + 16u * k) = ((const u32x4*)lr)[k];
-  for (uint32_t k = lane; k < szr / 16u; k += kWave)
-    *(__attribute__((address_space(3))) u32x4*)(size_t)(uR + 16u * k) = ((const u32x4*)rr)[k];
-  wave_sync();
-  bool big = false;
-  const uint32_t r = mask3_object<0xFFFFFFFFu, 0, true>(uL, uR, uX, Ob + lo + ro, A, nL, dL, nR, dR, lane, big);
-  wave_sync();
-  return r != kLeanFallback;  // (a union past 64 members: found before any store)
-}
-
-// The drain of one block (its wave 0, after the block's four waves left the
-// object loop): claim listed entries while there are any; the last block
-// takes what is left and resets the words of the next launch.
-// (ST, diagnostic builds: per-block times and counts in the list's upper half)
-template <bool ST = false>
-__device__ __forceinline__ void join_drain(const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb,
-                                           const uint64_t* Roff, uint8_t* Ob, uint32_t A, uint32_t* ctl,
-                                           uint64_t* list, uint32_t list_cap, uint32_t uL, uint32_t uR, uint32_t uX,
-                                           uint32_t lane, uint32_t n_blocks) {
-  constexpr int R = __ATOMIC_RELAXED, SA = __HIP_MEMORY_SCOPE_AGENT;
-  const uint64_t t_in = ST ? __builtin_amdgcn_s_memrealtime() : 0ull;
-  uint32_t n_mine = 0u;
-  const uint32_t ep = uni(__hip_atomic_load(&ctl[4], R, SA)), p = ep & 1u;
-  const uint64_t tag = list_tag(ep);
-  // entry e of this launch (its lister may still be between its count and its store)
-  auto entry = [&](uint32_t e) -> uint64_t {
-    uint64_t v;
-    do {
-      v = __hip_atomic_load(&list[e], R, SA);
-      v = ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
-    } while ((v & ~kObjMask) != tag);
-    return v;
-  };
-  auto one = [&](uint32_t e) {
-    const uint64_t v = entry(e);
-    if (drain_one(Lb, Loff, Rb, Roff, Ob, v & kObjMask, A, uL, uR, uX, lane) && lane == 0u)
-      __hip_atomic_store(&list[e], v | kEntryDone, R, SA);
-  };
-  for (;;) {
-    const uint32_t n = uni(__hip_atomic_load(&ctl[p], R, SA)), c = uni(__hip_atomic_load(&ctl[2], R, SA));
-    if (c >= (n < list_cap ? n : list_cap)) break;
-    uint32_t won = 0u;
-    if (lane == 0u) {
-      uint32_t want = c;
-      won = __hip_atomic_compare_exchange_strong(&ctl[2], &want, c + 1u, R, R, SA) ? 1u : 0u;
-    }
-    if (uni(won)) {
-      one(c);
-      ++n_mine;
-    }
-  }
-  uint32_t d = 0u;
-  if (lane == 0u) d = __hip_atomic_fetch_add(&ctl[5], 1u, R, SA);
-  if (ST && lane == 0u && blockIdx.x < 8000u) {
-    list[32768u + 4u * blockIdx.x] = t_in;
-    list[32768u + 4u * blockIdx.x + 1u] = __builtin_amdgcn_s_memrealtime();
-    list[32768u + 4u * blockIdx.x + 2u] = ((uint64_t)n_mine << 32) | uni(d);
-  }
-  if (uni(d) != n_blocks - 1u) return;
-  // the last block: every other block has passed its barrier (its listing is
-  // stored) and left its drain
-  const uint32_t n = uni(__hip_atomic_load(&ctl[p], R, SA));
-  const uint32_t c0 = uni(__hip_atomic_load(&ctl[2], R, SA));
-  for (uint32_t c = c0; c < (n < list_cap ? n : list_cap); ++c) one(c);
-  if (ST && lane == 0u) {
-    list[32768u + 4u * blockIdx.x + 3u] = __builtin_amdgcn_s_memrealtime();
-    list[32760u] = ((uint64_t)n << 32) | c0;
-  }
-  if (lane == 0u) {  // the next launch's words; this launch's count and overflow flag stay for the general kernel
-    __hip_atomic_store(&ctl[p ^ 1u], 0u, R, SA);
-    __hip_atomic_store(&ctl[6u + (p ^ 1u)], 0u, R, SA);
-    __hip_atomic_store(&ctl[2], 0u, R, SA);
-    __hip_atomic_store(&ctl[3], 0u, R, SA);
-    __hip_atomic_store(&ctl[5], 0u, R, SA);
-    __hip_atomic_store(&ctl[4], ep + 1u, R, SA);
-  }
-}
-
 // HDD (MODE 3): the deferred objects' join writes straight to HBM
 // (mask_object<HD>) and is followed by the same tail stores as the other
 // path, redirected to the sink: every path issues at least as many stores
@@ -3071,7 +2966,7 @@ __device__ __forceinline__ void join_drain(const uint8_t* Lb, const uint64_t* Lo
 // the copy-out too (copy_record_buf)
 template <int MINW, int MODE, int OUT = 2, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
           bool RT = true, uint32_t DYN = 0, uint32_t SF = 6, bool SPEC = false, uint32_t GMIN = 0, int IO = 0,
-          int HK = 0, bool PK = false, bool DRN = false>
+          int HK = 0, bool PK = false, bool BK = false>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
@@ -3090,7 +2985,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
   u32x4* const sR = stage_s[wave][1];
   uint8_t* const X = (uint8_t*)scr_s[wave];
   const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
-  const uint64_t ts0 = HABL == 6 || HABL == 7 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
+  const uint64_t ts0 = HABL == 6 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
   uint32_t n_joined = 0u, n_hd = 0u, n_chunk = 0u;                                  // (HABL 6: per-wave counts)
   const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
   const uint64_t rounds = (n_obj + n_waves * kWave - 1) / (n_waves * kWave);
@@ -3170,16 +3065,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
           if (hd && base < kDeferListCap) dlist[base] = obj;
         }
       }
-      if (DRN) {  // listed for the drain (a rare path)
-        if (__ballot(gen) != 0ull) {
-          const uint32_t ep = uni(__hip_atomic_load(&ctl[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          const uint32_t e = gen ? atomicAdd(&ctl[ep & 1u], 1u) : 0u;
-          if (gen && e < list_cap)
-            __hip_atomic_store(&list[e], obj | list_tag(ep), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (__ballot(gen && e >= list_cap) != 0ull && lane == 0u)  // past the list: the general kernel scans
-            __hip_atomic_store(&ctl[6u + (ep & 1u)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      } else if (gen) {  // hand the object to the general kernel
+      if (gen) {  // hand the object to the general kernel
         const uint32_t e = atomicAdd(&ctl[0], 1u);
         if (e < list_cap) list[e] = obj;
       }
@@ -3264,7 +3150,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
         if ((defs >> td) & 1ull) {
           if (HDD) {
             if (M3HD)
-              r = mask3_object<0xFFFFFFFFu, 0, true, HABL, RT, HK, PK>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
+              r = mask3_object<0xFFFFFFFFu, 0, true, HABL, RT, HK, PK, BK>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
                                                      d & 0xFFFFu, m >> 16, d >> 16, lane, big);
             else
               r = mask_object<0xFFFFFFFFu, true, 0, DC>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo),
@@ -3275,7 +3161,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
           }
           src = lds_addr(out_s[wave]);
         } else {
-          r = mask3_object<0xFFFFFFFFu, 3, false, 0, RT, 0, PK>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A,
+          r = mask3_object<0xFFFFFFFFu, 3, false, 0, RT, 0, PK, BK>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A,
                                                          m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, sink);
           src = lds_addr(sL);
         }
@@ -3287,21 +3173,10 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
           __builtin_nontemporal_store(z, (u32x4*)sink);
           __builtin_nontemporal_store(z, (u32x4*)sink + 1);
         } else {
-          // (DRN: a fallback's placeholder piece goes to the sink: the drain,
-          // possibly on another XCD, writes that record in this launch)
-          copy_io<IO>(src, DRN && fbu ? sink : Ob + oo, fbu ? 1u : r, lane);
+          copy_io<IO>(src, Ob + oo, fbu ? 1u : r, lane);
         }
         *(Ooff + cbase + t) = oo | (fbu ? kPending : 0ull);
-        if (DRN && fbu) {  // listed for the drain (past the list: the general kernel scans)
-          if (lane == 0u) {
-            const uint32_t ep = __hip_atomic_load(&ctl[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t e = atomicAdd(&ctl[ep & 1u], 1u);
-            if (e < list_cap)
-              __hip_atomic_store(&list[e], (cbase + t) | list_tag(ep), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else
-              __hip_atomic_store(&ctl[6u + (ep & 1u)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        } else if (fbu) {  // listed for the general kernel (a rare path: its extra memory operations
+        if (fbu) {  // listed for the general kernel (a rare path: its extra memory operations
                     // only add to the count the loop-head wait sees)
           if (lane == 0u) {
             const uint32_t e = atomicAdd(&ctl[0], 1u);
@@ -3328,14 +3203,6 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
       stage_used(sR, pr, nu >> 16, lane);
       wave_sync();
     }
-  }
-  if (DRN && HABL != 8) {  // the block's LDS is free once its four waves are here: wave 0 drains the list
-    __syncthreads();
-    if (HABL == 9) return;  // (timing only: the barrier without the drain)
-    if (HABL == 7 && wave == 0u && lane == 0u && blockIdx.x == 0u) list[32761u] = ts0;
-    if (wave == 0u)
-      join_drain<HABL == 7>(Lb, Loff, Rb, Roff, Ob, A, ctl, list, list_cap, lds_addr(stage_s[0][0]),
-                            lds_addr(stage_s[2][0]), lds_addr(scr_s[0]), lane, gridDim.x);
   }
 #ifdef CRDT_DIAG
   if (HABL == 6 && lane == 0u && wave_id < 10922u) {  // timing only: the list's upper half holds the stamps
@@ -3387,7 +3254,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_dyn_
   uint8_t* const X = (uint8_t*)scr_s[wave];
   const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
   const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint64_t ts0 = HABL == 6 || HABL == 7 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
+  const uint64_t ts0 = HABL == 6 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
   uint32_t n_joined = 0u, n_hd = 0u, n_chunk = 0u;                                  // (HABL 6: per-wave counts)
   uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
   const uint64_t n_chunks = (n_obj + kDynG - 1) / kDynG;
@@ -3575,7 +3442,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_v10_
   uint8_t* const X = (uint8_t*)scr_s[wave];
   const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
   const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint64_t ts0 = HABL == 6 || HABL == 7 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
+  const uint64_t ts0 = HABL == 6 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
   uint32_t n_joined = 0u, n_hd = 0u, n_chunk = 0u;                                  // (HABL 6: per-wave counts)
   uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
 
@@ -3816,27 +3683,11 @@ __device__ __forceinline__ void general_one(const uint8_t* Lb, const uint64_t* L
 __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, const uint8_t* __restrict__ Rb,
     const uint64_t* __restrict__ Roff, uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t n_obj,
-    uint32_t A, uint32_t* __restrict__ ctl, const uint64_t* __restrict__ list, uint32_t list_cap,
-    const uint32_t* __restrict__ drn) {
+    uint32_t A, uint32_t* __restrict__ ctl, const uint64_t* __restrict__ list, uint32_t list_cap) {
   __shared__ u32x4 gen_s[3][kGenStage / 16];
   const uint32_t lane = threadIdx.x;
-  if (drn) {  // after a draining join (DRN): the flags of its done entries, its leftovers
-    const uint32_t ep = uni(__hip_atomic_load(&drn[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - 1u;  // (advanced)
-    const uint32_t p = ep & 1u, n = uni(__hip_atomic_load(&drn[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    if (uni(__hip_atomic_load(&drn[6u + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
-      for (uint32_t e = blockIdx.x; e < n; e += gridDim.x) {
-        const uint64_t v = __hip_atomic_load(&list[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), o = v & kObjMask;
-        if (v & kEntryDone) {
-          if (lane == 0u) Ooff[o] = Loff[o] + Roff[o];
-        } else {
-          general_one(Lb, Loff, Rb, Roff, Ob, Ooff, o, A, gen_s[0], gen_s[1], gen_s[2], lane);
-        }
-      }
-      return;
-    }
-  }  // (a list overflow: every flag is scanned, drained objects joined again)
-  const uint32_t n = drn ? ~0u : uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  const uint32_t scan = drn ? 1u : uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const uint32_t scan = uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (n <= list_cap && scan == 0u) {
     for (uint32_t e = blockIdx.x; e < n; e += gridDim.x)
       general_one(Lb, Loff, Rb, Roff, Ob, Ooff, list[e], A, gen_s[0], gen_s[1], gen_s[2], lane);
@@ -4114,7 +3965,7 @@ namespace {
 // then the general kernel.
 template <int MINW, bool ONE = true, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
           bool RT = true, uint32_t DYN = 0, bool DK = false, uint32_t SF = 6, bool V10 = false, bool SPEC = false,
-          uint32_t GMIN = 0, int IO = 0, int HK = 0, bool PK = false, bool DRN = false>
+          uint32_t GMIN = 0, int IO = 0, int HK = 0, bool PK = false, bool BK = false>
 int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                        const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
                        uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
@@ -4134,7 +3985,7 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
   } else
 #endif
   if constexpr (ONE) {
-    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL, RT, DYN, SF, SPEC, GMIN, IO, HK, PK, DRN>;
+    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL, RT, DYN, SF, SPEC, GMIN, IO, HK, PK, BK>;
   } else {
 #ifdef CRDT_DIAG
     f1 = (const void*)orswot_join_kernel<MINW, 1>;
@@ -4157,23 +4008,17 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
   }
   const uint64_t chunks = (n_obj + kWave - 1) / kWave;
   const uint64_t want = (chunks + kWavesPerBlock - 1) / kWavesPerBlock;
-  // DRN: the kernel's own control words (ctl[4..11]), reset by its last
-  // block; the general kernel then clears the drained objects' flags
-  uint32_t* kctl = DRN ? ctl + 4 : ctl;
   void* args[] = {&Lb, &Loff, &Lbytes, &Rb, &Roff, &Rbytes, &Ob, &Ooff, &Obytes, &n_obj, &n_actors, &status,
-                  &kctl, &list, &list_cap};
-  if (!DRN && hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
-  // (HABL 8 / 9, timing only: no drain, so the host zeroes the kernel's words)
-  if (DRN && (HABL == 8 || HABL == 9) && hipMemsetAsync(kctl, 0, 8 * sizeof(uint32_t), stream) != hipSuccess)
-    return CRDT_EHIP;
+                  &ctl, &list, &list_cap};
+  if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
   for (int k = 0; k < passes; ++k) {
     const uint64_t cap = (uint64_t)cus * (blocks_per_cu > 0 ? blocks_per_cu : occ[k]);
     const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
     if (hipLaunchKernel(fs[k], dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) != hipSuccess)
       return CRDT_EHIP;
   }
-  hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff, Ob,
-                     Ooff, n_obj, n_actors, ctl, list, list_cap, DRN ? (const uint32_t*)kctl : nullptr);
+  hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
+                     Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 }  // namespace
@@ -4193,11 +4038,11 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // waves per SIMD with the guided split (5/8 of the objects in static chunks,
   // the rest in 20-object ticket chunks), record prefetch in the saddr form
   // and the copy-out clamped on byte offsets (IO 7), both sides' member ranks
-  // in one packed pass when nL + nR <= 64 (PK), then the general kernel
-  // (measured best, tools/ab_bench.py). Other variants exist in
-  // -DCRDT_DIAG builds only.
+  // in one packed pass when nL + nR <= 64 (PK) and mask3's bank-conflict
+  // layout (BK), then the general kernel (measured best, tools/ab_bench.py;
+  // DESIGN.md §4). Other variants exist in -DCRDT_DIAG builds only.
   (void)variant;
-  return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true>);
+  return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, true>);
 #else
   if (variant == 134) return go(launch_join_passes<6, true, true, true, true, 1>);  // timing only: no kill
   if (variant == 135) return go(launch_join_passes<6, true, true, true, true, 2>);  // timing only: no deferred block
@@ -4243,18 +4088,8 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   if (variant == 251) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 2>);
   // r03: both sides' member ranks in one packed pass when nL + nR <= 64 (PK)
   if (variant == 259) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true>);
-  if (variant == 262)  // timing only: DRN without the drain (and without its barrier: 263 keeps it)
-    return go(launch_join_passes<6, true, true, true, true, 8, true, 20, false, 5, false, false, 0, 7, 0, true, true>);
-  if (variant == 263)
-    return go(launch_join_passes<6, true, true, true, true, 9, true, 20, false, 5, false, false, 0, 7, 0, true, true>);
-  if (variant == 261)  // + drain stamps (HABL 7, timing only: list upper half)
-    return go(launch_join_passes<6, true, true, true, true, 7, true, 20, false, 5, false, false, 0, 7, 0, true, true>);
-  // r03: + the drain (DRN: no general kernel, no memset), the product for n_actors <= 32
-  if (variant == 260) {
-    if (n_actors > 32u)
-      return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true>);
-    return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, true>);
-  }
+  // r03: + BK (mask3's LDS bank-conflict layout: dword descriptors, 4-B sink stride, header under exec)
+  if (variant == 264) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, true>);
   if (variant == 256) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 6>);
   if (variant == 257) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7>);
   if (variant == 255) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 5>);
@@ -4357,7 +4192,7 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // no general pass after them (their output is not a valid batch anyway)
   if (variant == 109 || variant == 14 || variant == 16) return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
   hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
-                     Ob, Ooff, n_obj, n_actors, ctl, list, list_cap, nullptr);
+                     Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 #endif
 }

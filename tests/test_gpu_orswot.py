@@ -407,14 +407,13 @@ def _mixed_batch(n_small=20_000, seed=21):
     return lb, lo, rb, ro
 
 
-def test_drain_mixed_batch_list_caps(gpu, oracle):
-    """The product join drains its own list (no general kernel, no memset:
-    orswot_join_kernel DRN): objects past the 2 KB stage and unions past 64
-    members, listed at random positions of a config-3 batch, are joined inside
-    the launch; with a small or empty list the listers join them from HBM.
-    Launches repeat on one context (the kernel re-zeroes its control words and
-    advances the entry epoch) and alternate with the 64-actor path, which
-    zeroes its own words and writes untagged list entries."""
+def test_mixed_batch_general_path_list_caps(gpu, oracle):
+    """Objects past the join kernel's limits at random positions of a
+    config-3 batch — records past the 2 KB stage (listed at the chunk step)
+    and unions past 64 members (found inside the join) — go to the general
+    kernel; with a small or empty list it scans the flags instead. Launches
+    repeat on one context and alternate with the 64-actor path (every object
+    general)."""
     lb, lo, rb, ro = _mixed_batch()
     ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, 16, threads=16)
     # how many objects leave the fast path: some of each kind

@@ -4,7 +4,7 @@
 # Usage (on the box, from the repo root): bash tools/profile.sh <tag> [bench args...]
 set -euo pipefail
 TAG=${1:-r01}; shift || true
-ARGS=${@:---steps 10 --warmup 2 --no-cpu-baseline}
+ARGS=${@:---steps 10 --warmup 50 --no-cpu-baseline}
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG

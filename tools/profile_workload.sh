@@ -4,7 +4,7 @@
 # Usage (repo root, on the box): bash tools/profile_workload.sh <tag> <workload> [bench args...]
 set -euo pipefail
 TAG=$1; WL=$2; shift 2
-ARGS="--workload $WL --steps 5 --warmup 1 --no-cpu-baseline $*"
+ARGS="--workload $WL --steps 5 --warmup 20 --no-cpu-baseline $*"
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_${TAG}_$WL
