@@ -451,7 +451,8 @@ int crdt_orswot_generate_replicas_subset(uint64_t seed, size_t first_obj, size_t
  *   mv_n[kcap], mv_clock[kcap][mcap][A], mv_val[kcap][mcap]   nested MVRegs (Vec order)
  *   n_def, dclock[dcap][A]               deferred removes in CLOCK ORDER
  *   dset_n[dcap], dset[dcap][scap]       their key sets, ascending
- * Unused slots are zero on output. Output capacities must be >= the sum of
+ * Only the used slots of the output are written (slots past a count keep
+ * what the buffer held). Output capacities must be >= the sum of
  * both inputs' (kcap, mcap, dcap, scap); per side kcap <= 32, mcap <= 16,
  * dcap <= 32, scap <= 32, n_actors <= 64.                                    */
 typedef struct crdt_map_mvreg_slab {

@@ -241,6 +241,34 @@ class MapSlab:
                             if hasattr(v, "cpu") else v) for f, v in self.a.items()},
                        self.kcap, self.mcap, self.dcap, self.scap)
 
+    def used_masks(self):
+        """Per field, a boolean array of its shape: the slots the state uses
+        (keys below n_keys, values below mv_n, deferred below n_def, set
+        elements below dset_n). Host slabs."""
+        a = self.host().a
+        key = np.arange(self.kcap)[None, :] < a["n_keys"][:, None]  # [n, kcap]
+        val = key[:, :, None] & (np.arange(self.mcap)[None, None, :] < a["mv_n"][:, :, None])  # [n, kcap, mcap]
+        dfr = np.arange(self.dcap)[None, :] < a["n_def"][:, None]  # [n, dcap]
+        dset = dfr[..., None] & (np.arange(self.scap)[None, None, :] < a["dset_n"][..., None])
+        full = lambda f: np.ones(a[f].shape, bool)  # noqa: E731
+        per = {"clock": full("clock"), "n_keys": full("n_keys"), "n_def": full("n_def"), "keys": key,
+               "eclock": key[..., None], "mv_n": key, "mv_clock": val[..., None], "mv_val": val,
+               "dclock": dfr[..., None], "dset_n": dfr, "dset": dset}
+        return {f: np.broadcast_to(m, a[f].shape) for f, m in per.items()}
+
+    def canonical(self):
+        """Host copy with every slot past its count zeroed (the merge writes
+        only the used slots, include/crdts_hip.h)."""
+        a = {f: np.array(v, copy=True) for f, v in self.host().a.items()}
+        for f, m in self.used_masks().items():
+            a[f][~m] = 0
+        return MapSlab(a, self.kcap, self.mcap, self.dcap, self.scap)
+
+    def used_bytes(self):
+        """Bytes of the used slots (the state's own bytes, not its capacity)."""
+        h = self.host().a
+        return int(sum(int(m.sum()) * h[f].dtype.itemsize for f, m in self.used_masks().items()))
+
     def cstruct(self):
         from ._lib import MapSlabC
 
@@ -581,12 +609,13 @@ class Engine:
         return outn, outc, outv
 
     # ------------------------------------------------ Map<u64, MVReg<u64>>
-    def map_mvreg_merge(self, S: "MapSlab", O: "MapSlab", n_actors, stream=None, check_status=True):
+    def map_mvreg_merge(self, S: "MapSlab", O: "MapSlab", n_actors, stream=None, check_status=True, out=None):
         """Map::merge (src/map.rs:191-268) of device slabs; returns the output slab
-        (capacities = the sums of the inputs')."""
+        (capacities = the sums of the inputs'). Only the used slots of the
+        output are written (`out`, if given, is reused as it is)."""
         n = int(S.a["n_keys"].shape[0])
-        R = MapSlab.alloc(n, n_actors, S.kcap + O.kcap, S.mcap + O.mcap, S.dcap + O.dcap, S.scap + O.scap,
-                          device=S.a["clock"].device)
+        R = out if out is not None else MapSlab.alloc(n, n_actors, S.kcap + O.kcap, S.mcap + O.mcap,
+                                                      S.dcap + O.dcap, S.scap + O.scap, device=S.a["clock"].device)
         s, o, r = S.cstruct(), O.cstruct(), R.cstruct()
         check(lib.crdt_map_mvreg_merge(self.ctx, C.byref(s), C.byref(o), C.byref(r), n, n_actors,
                                        self._stream(stream)), "map_mvreg_merge")

@@ -268,7 +268,7 @@ int crdt_orswot_merge_ex(crdt_ctx* ctx, const crdt_orswot_batch* self, const crd
   return launch_orswot_merge(self->base, self->off, self->bytes, other->base, other->off,
                              other->bytes, d_out_base, d_out_off, out_bytes, self->n_obj, n_actors,
                              ctx->d_status, ctx->d_ctl, ctx->d_list, ctx->list_cap, S(stream),
-                             ctx->blocks_per_cu, ctx->variant);
+                             ctx->blocks_per_cu, ctx->variant, &ctx->join_seq);
 }
 
 int crdt_orswot_validate(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32_t n_actors,

@@ -6,6 +6,7 @@
 #include <cstdint>
 
 #include "../../include/crdts_hip.h"
+#include "kernels.h"
 
 namespace crdts_hip {
 // Device scratch of a context: status word, the general-path object list
@@ -31,6 +32,9 @@ struct crdt_ctx {
   uint32_t list_cap;
   int blocks_per_cu;    // diagnostic builds only (crdt_ctx_set_blocks_per_cu)
   int variant;          // diagnostic builds only (crdt_ctx_set_variant); 0 = the product kernels
+  // the Orswot join's launch sequence: alternate launches use the control
+  // words ctl[4..7] / ctl[8..11] (launch_orswot_merge, no memset)
+  crdts_hip::JoinSeq join_seq{0u, false};
   // replica anti-entropy (replica.hip): the RCCL communicator this context
   // owns (ncclComm_t; null until crdt_comm_init) and a growable device arena
   void* comm = nullptr;

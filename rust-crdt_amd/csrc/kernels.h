@@ -7,11 +7,17 @@
 
 namespace crdts_hip {
 
+// The join launches' sequence on one context (its control-word set
+// alternates per launch; dirty: zero both sets before the next launch).
+struct JoinSeq {
+  uint32_t seq;
+  bool dirty;
+};
 int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                         const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff,
                         uint64_t Obytes, uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl,
                         uint64_t* list, uint32_t list_cap, hipStream_t stream, int blocks_per_cu,
-                        int variant);
+                        int variant, JoinSeq* js);
 
 int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                                const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,

@@ -238,23 +238,13 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
             if (lane == 0u) R.mv_val[ir * R.mcap + nout] = fromO ? O.mv_val[src] : S.mv_val[src];
             ++nout;
           }
-          if (lane == 0u) R.mv_n[ir] = nout;
-          // unused value slots: zero, all lanes over the flat tail
-          for (uint64_t e = (ir * R.mcap + nout) * A + lane; e < (ir + 1u) * R.mcap * A; e += kMpW) R.mv_clock[e] = 0ull;
-          for (uint64_t e = ir * R.mcap + nout + lane; e < (ir + 1u) * R.mcap; e += kMpW) R.mv_val[e] = 0ull;
+          if (lane == 0u) R.mv_n[ir] = nout;  // (slots past the counts are not written: include/crdts_hip.h)
           ++nk;
         }
       }
       mp_sync();
       if (hs) ++a;
       if (ho) ++b;
-    }
-    {  // unused key slots: zero, all lanes over each array's flat tail
-      const uint64_t k0 = i * R.kcap + nk, k1 = (i + 1u) * R.kcap;
-      for (uint64_t e = k0 + lane; e < k1; e += kMpW) { R.keys[e] = 0ull; R.mv_n[e] = 0u; }
-      for (uint64_t e = k0 * A + lane; e < k1 * A; e += kMpW) R.eclock[e] = 0ull;
-      for (uint64_t e = k0 * R.mcap * A + lane; e < k1 * R.mcap * A; e += kMpW) R.mv_clock[e] = 0ull;
-      for (uint64_t e = k0 * R.mcap + lane; e < k1 * R.mcap; e += kMpW) R.mv_val[e] = 0ull;
     }
     if (lane == 0u) R.n_keys[i] = nk;
     if (lane < A) R.clock[i * A + lane] = cM;
@@ -282,17 +272,10 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
           if (cnt < R.scap) R.dset[dr * R.scap + cnt] = k;
           ++cnt;
         }
-        for (uint32_t z = cnt; z < R.scap; ++z) R.dset[dr * R.scap + z] = 0ull;
         R.dset_n[dr] = cnt < R.scap ? cnt : R.scap;
       }
       over = over || __builtin_amdgcn_readfirstlane(cnt) > R.scap;
       ++nd;
-    }
-    {  // unused deferred slots: zero, flat tails
-      const uint64_t d0 = i * R.dcap + nd, d1 = (i + 1u) * R.dcap;
-      for (uint64_t e = d0 + lane; e < d1; e += kMpW) R.dset_n[e] = 0u;
-      for (uint64_t e = d0 * A + lane; e < d1 * A; e += kMpW) R.dclock[e] = 0ull;
-      for (uint64_t e = d0 * R.scap + lane; e < d1 * R.scap; e += kMpW) R.dset[e] = 0ull;
     }
     if (lane == 0u) R.n_def[i] = nd;
     if (over && lane == 0u) atomicCAS(status, 0, CRDT_ECAPACITY);

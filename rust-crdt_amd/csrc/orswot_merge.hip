@@ -3683,9 +3683,14 @@ __device__ __forceinline__ void general_one(const uint8_t* Lb, const uint64_t* L
 __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, const uint8_t* __restrict__ Rb,
     const uint64_t* __restrict__ Roff, uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t n_obj,
-    uint32_t A, uint32_t* __restrict__ ctl, const uint64_t* __restrict__ list, uint32_t list_cap) {
+    uint32_t A, uint32_t* __restrict__ ctl, const uint64_t* __restrict__ list, uint32_t list_cap,
+    uint32_t* __restrict__ zero4) {
   __shared__ u32x4 gen_s[3][kGenStage / 16];
   const uint32_t lane = threadIdx.x;
+  // NM: the control words of the other parity (the launch before this one
+  // used them; the launch after it will) are zeroed here, so no memset
+  // precedes a join launch (launch_join_passes)
+  if (zero4 && blockIdx.x == 0u && lane < 4u) zero4[lane] = 0u;
   const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   const uint32_t scan = uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (n <= list_cap && scan == 0u) {
@@ -3965,11 +3970,11 @@ namespace {
 // then the general kernel.
 template <int MINW, bool ONE = true, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
           bool RT = true, uint32_t DYN = 0, bool DK = false, uint32_t SF = 6, bool V10 = false, bool SPEC = false,
-          uint32_t GMIN = 0, int IO = 0, int HK = 0, bool PK = false, bool BK = false>
+          uint32_t GMIN = 0, int IO = 0, int HK = 0, bool PK = false, bool BK = false, bool NM = false>
 int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                        const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
                        uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
-                       uint32_t list_cap, hipStream_t stream, int blocks_per_cu) {
+                       uint32_t list_cap, hipStream_t stream, int blocks_per_cu, JoinSeq* js) {
 #ifndef CRDT_DIAG
   static_assert(HABL == 0 && ONE && !V10 && !DK, "the product launch: one pass, no timing-only ablation");
 #endif
@@ -4008,9 +4013,21 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
   }
   const uint64_t chunks = (n_obj + kWave - 1) / kWave;
   const uint64_t want = (chunks + kWavesPerBlock - 1) / kWavesPerBlock;
+  // NM: two sets of the four control words after the shared ones (ctl[4..7],
+  // ctl[8..11]), used by alternate launches of this context; the general
+  // kernel of a launch zeroes the other set, which the next launch uses, so
+  // no memset (a runtime fill kernel plus a ~10 us dispatch gap, r03k trace)
+  // precedes the join. After a failed launch the context zeroes both first.
+  uint32_t* set = NM ? ctl + 4u + 4u * (js->seq & 1u) : ctl;
+  uint32_t* const other = NM ? ctl + 4u + 4u * (~js->seq & 1u) : nullptr;
   void* args[] = {&Lb, &Loff, &Lbytes, &Rb, &Roff, &Rbytes, &Ob, &Ooff, &Obytes, &n_obj, &n_actors, &status,
-                  &ctl, &list, &list_cap};
-  if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
+                  &set, &list, &list_cap};
+  if (NM) {
+    if (js->dirty && hipMemsetAsync(ctl + 4, 0, 8 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
+    js->dirty = true;  // until both kernels are launched
+  } else if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) {
+    return CRDT_EHIP;
+  }
   for (int k = 0; k < passes; ++k) {
     const uint64_t cap = (uint64_t)cus * (blocks_per_cu > 0 ? blocks_per_cu : occ[k]);
     const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
@@ -4018,19 +4035,27 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
       return CRDT_EHIP;
   }
   hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
-                     Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
-  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+                     Ob, Ooff, n_obj, n_actors, set, list, list_cap, other);
+  if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
+  if (NM) {
+    ++js->seq;
+    js->dirty = false;
+  }
+  return CRDT_OK;
 }
 }  // namespace
 
 int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                         const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff,
                         uint64_t Obytes, uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl,
-                        uint64_t* list, uint32_t list_cap, hipStream_t stream, int blocks_per_cu, int variant) {
+                        uint64_t* list, uint32_t list_cap, hipStream_t stream, int blocks_per_cu, int variant,
+                        JoinSeq* js) {
   if (n_obj == 0) return CRDT_OK;
+  JoinSeq local{0u, true};
+  if (!js) js = &local;  // (no context state: the words are zeroed first)
   auto go = [&](auto f) {
     return f(Lb, Loff, Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors, status, ctl, list, list_cap,
-             stream, blocks_per_cu);
+             stream, blocks_per_cu, js);
   };
 #ifndef CRDT_DIAG
   // The product path: orswot_join_kernel in one pass (mask3_object for every
@@ -4042,7 +4067,7 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // layout (BK), then the general kernel (measured best, tools/ab_bench.py;
   // DESIGN.md §4). Other variants exist in -DCRDT_DIAG builds only.
   (void)variant;
-  return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, true>);
+  return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, true, true>);
 #else
   if (variant == 134) return go(launch_join_passes<6, true, true, true, true, 1>);  // timing only: no kill
   if (variant == 135) return go(launch_join_passes<6, true, true, true, true, 2>);  // timing only: no deferred block
@@ -4090,6 +4115,8 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   if (variant == 259) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true>);
   // r03: + BK (mask3's LDS bank-conflict layout: dword descriptors, 4-B sink stride, header under exec)
   if (variant == 264) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, true>);
+  // r03: + NM (no memset before the join: alternating control-word sets, zeroed by the general kernel)
+  if (variant == 265) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, true, true>);
   if (variant == 256) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 6>);
   if (variant == 257) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7>);
   if (variant == 255) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 5>);
@@ -4192,7 +4219,7 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // no general pass after them (their output is not a valid batch anyway)
   if (variant == 109 || variant == 14 || variant == 16) return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
   hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
-                     Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
+                     Ob, Ooff, n_obj, n_actors, ctl, list, list_cap, nullptr);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 #endif
 }

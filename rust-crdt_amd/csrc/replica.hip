@@ -421,7 +421,7 @@ int orswot_join_rank_body(crdt_ctx* ctx, Transport& T, const crdt_orswot_batch* 
               ? launch_orswot_merge_sparse(acc, acc_off, acc_bytes, rb, ro, gsz(p, me), o, oo, cap, nr, A,
                                            ctx->d_status, ctx->d_ctl, ctx->d_list, ctx->list_cap, st, 0)
               : launch_orswot_merge(acc, acc_off, acc_bytes, rb, ro, gsz(p, me), o, oo, cap, nr, A, ctx->d_status,
-                                    ctx->d_ctl, ctx->d_list, ctx->list_cap, st, 0, 0);
+                                    ctx->d_ctl, ctx->d_list, ctx->list_cap, st, 0, 0, &ctx->join_seq);
     acc = o;
     acc_off = oo;
     acc_bytes = cap;

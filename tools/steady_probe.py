@@ -19,6 +19,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--launches", type=int, default=400)
     ap.add_argument("--n-obj", type=int, default=1_000_000)
+    ap.add_argument("--window", action="store_true",
+                    help="also time the same launches with two events around the whole run (no per-launch events)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -41,7 +43,17 @@ def main():
     eng.status(s)
     ms = [e0.elapsed_time(e1) for e0, e1 in ev]
     win = [round(float(np.median(ms[i:i + 10])), 4) for i in range(0, len(ms), 10)]
-    print(json.dumps({"launches": a.launches, "median_by_10": win, "ms": [round(x, 4) for x in ms]}))
+    res = {"launches": a.launches, "median_by_10": win, "ms": [round(x, 4) for x in ms],
+           "per_launch_events_span_ms": ev[0][0].elapsed_time(ev[-1][1]) / a.launches}
+    if a.window:  # the same launches again, events only around the whole run
+        w0, w1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        w0.record(s)
+        for _ in range(a.launches):
+            eng.orswot_merge(L, R, out=out, stream=s, check_status=False)
+        w1.record(s)
+        s.synchronize()
+        res["window_events_ms_per_launch"] = w0.elapsed_time(w1) / a.launches
+    print(json.dumps(res))
 
 
 if __name__ == "__main__":
