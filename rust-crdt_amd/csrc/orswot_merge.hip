@@ -3637,8 +3637,27 @@ __device__ __forceinline__ void general_one(const uint8_t* Lb, const uint64_t* L
   const uint32_t szl = uni(hl0.x), szr = uni(hr0.x);
   if (szl <= kGenStage && szr <= kGenStage) {
     wave_sync();
-    for (uint32_t k = lane; k < szl / 16; k += kWave) sl[k] = ((const u32x4*)lr)[k];
-    for (uint32_t k = lane; k < szr / 16; k += kWave) sr[k] = ((const u32x4*)rr)[k];
+    // both records staged 4 KB per side at a time: every load of a round is
+    // issued before its stores (one memory round trip per 4 KB, not per 1 KB)
+    {
+      constexpr uint32_t kB = 4;
+      const uint32_t nl = szl / 16, nr = szr / 16, nmax = nl > nr ? nl : nr;
+      for (uint32_t k0 = 0; k0 < nmax; k0 += kB * kWave) {
+        u32x4 tl[kB], tr[kB];
+#pragma unroll
+        for (uint32_t j = 0; j < kB; ++j) {
+          const uint32_t k = k0 + j * kWave + lane;
+          if (k < nl) tl[j] = ((const u32x4*)lr)[k];
+          if (k < nr) tr[j] = ((const u32x4*)rr)[k];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kB; ++j) {
+          const uint32_t k = k0 + j * kWave + lane;
+          if (k < nl) sl[k] = tl[j];
+          if (k < nr) sr[k] = tr[j];
+        }
+      }
+    }
     wave_sync();
     // the join kernel's mask3 join when its limits hold (<= 64 members and
     // dots per side, <= 32 deferred clocks per side, A <= 32: in config 3 the
@@ -3693,9 +3712,13 @@ __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
   if (zero4 && blockIdx.x == 0u && lane < 4u) zero4[lane] = 0u;
   const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   const uint32_t scan = uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  // (the block's first entry is read with the count, a round trip less; an
+  // entry past the count is stale and not used)
+  const uint64_t first = blockIdx.x < list_cap ? list[blockIdx.x] : 0ull;
   if (n <= list_cap && scan == 0u) {
     for (uint32_t e = blockIdx.x; e < n; e += gridDim.x)
-      general_one(Lb, Loff, Rb, Roff, Ob, Ooff, list[e], A, gen_s[0], gen_s[1], gen_s[2], lane);
+      general_one(Lb, Loff, Rb, Roff, Ob, Ooff, e == blockIdx.x ? first : list[e], A, gen_s[0], gen_s[1], gen_s[2],
+                  lane);
   } else {  // list overflow, or objects flagged without a list entry: scan the flags
     const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
     for (uint64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
@@ -3918,8 +3941,27 @@ __device__ __forceinline__ void sparse_general_one(const uint8_t* Lb, const uint
   const uint32_t szl = uni(hl0.x), szr = uni(hr0.x);
   if (szl <= kGenStage && szr <= kGenStage) {
     wave_sync();
-    for (uint32_t k = lane; k < szl / 16; k += kWave) sl[k] = ((const u32x4*)lr)[k];
-    for (uint32_t k = lane; k < szr / 16; k += kWave) sr[k] = ((const u32x4*)rr)[k];
+    // both records staged 4 KB per side at a time: every load of a round is
+    // issued before its stores (one memory round trip per 4 KB, not per 1 KB)
+    {
+      constexpr uint32_t kB = 4;
+      const uint32_t nl = szl / 16, nr = szr / 16, nmax = nl > nr ? nl : nr;
+      for (uint32_t k0 = 0; k0 < nmax; k0 += kB * kWave) {
+        u32x4 tl[kB], tr[kB];
+#pragma unroll
+        for (uint32_t j = 0; j < kB; ++j) {
+          const uint32_t k = k0 + j * kWave + lane;
+          if (k < nl) tl[j] = ((const u32x4*)lr)[k];
+          if (k < nr) tr[j] = ((const u32x4*)rr)[k];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kB; ++j) {
+          const uint32_t k = k0 + j * kWave + lane;
+          if (k < nl) sl[k] = tl[j];
+          if (k < nr) sr[k] = tr[j];
+        }
+      }
+    }
     wave_sync();
     uint32_t r = kLeanFallback;
     const uint32_t cL = uni(hl0.y), nL = uni(hl0.z), dL = uni(hl0.w), cR = uni(hr0.y), nR = uni(hr0.z),
