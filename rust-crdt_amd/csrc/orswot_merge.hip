@@ -635,7 +635,7 @@ __device__ __forceinline__ void merge_object(const uint8_t* Ls, const uint8_t* R
 __device__ __forceinline__ bool header_ok(u32x4 h0, u32x4 h1, uint64_t off, uint64_t bytes, uint32_t A) {
   const uint64_t sz = record_size64(h0.y, h0.z, h0.w, h1.x, h1.y, h1.z);
   return (off & 15u) == 0 && off + kHdrBytes <= bytes && sz == h0.x && h0.y == A && h1.w == 0u &&
-         off + sz <= bytes;
+         (h1.x != 0u || (h1.y | h1.z) == 0u) && off + sz <= bytes;
 }
 
 // ======================================================================
@@ -1503,7 +1503,7 @@ __device__ __forceinline__ const uint8_t* gptr(uint32_t a) {
 // 64-lane pass (L members in lanes [0, nL), R members in [nL, nL + nR)), half
 // the search instructions of the two-sided form
 template <uint32_t OUTCAP, int OUT = 0, bool HD = false, int HABL = 0, bool RT = true, int HK = 0, bool PK = false,
-          bool BK = false>  // OUT: 0 direct stores, 1 sink-predicated, 2 LDS-assembled
+          int BK = 0>  // OUT: 0 direct stores, 1 sink-predicated, 2 LDS-assembled
 __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint32_t uX, uint8_t* O, uint32_t A,
                                                  uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane,
                                                  bool& big, uint8_t* sink = nullptr) {
@@ -2966,7 +2966,7 @@ __attribute__((noinline)) __device__ uint32_t hd_join(const uint8_t* Ls, const u
 // the copy-out too (copy_record_buf)
 template <int MINW, int MODE, int OUT = 2, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
           bool RT = true, uint32_t DYN = 0, uint32_t SF = 6, bool SPEC = false, uint32_t GMIN = 0, int IO = 0,
-          int HK = 0, bool PK = false, bool BK = false>
+          int HK = 0, bool PK = false, int BK = 0>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
@@ -3150,7 +3150,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
         if ((defs >> td) & 1ull) {
           if (HDD) {
             if (M3HD)
-              r = mask3_object<0xFFFFFFFFu, 0, true, HABL, RT, HK, PK, BK>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
+              r = mask3_object<0xFFFFFFFFu, 0, true, HABL, RT, HK, PK, BK ? 1 : 0>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
                                                      d & 0xFFFFu, m >> 16, d >> 16, lane, big);
             else
               r = mask_object<0xFFFFFFFFu, true, 0, DC>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo),
@@ -4012,7 +4012,7 @@ namespace {
 // then the general kernel.
 template <int MINW, bool ONE = true, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
           bool RT = true, uint32_t DYN = 0, bool DK = false, uint32_t SF = 6, bool V10 = false, bool SPEC = false,
-          uint32_t GMIN = 0, int IO = 0, int HK = 0, bool PK = false, bool BK = false, bool NM = false>
+          uint32_t GMIN = 0, int IO = 0, int HK = 0, bool PK = false, int BK = 0, bool NM = false>
 int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                        const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
                        uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
@@ -4109,7 +4109,7 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // layout (BK), then the general kernel (measured best, tools/ab_bench.py;
   // DESIGN.md §4). Other variants exist in -DCRDT_DIAG builds only.
   (void)variant;
-  return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, true, true>);
+  return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true>);
 #else
   if (variant == 134) return go(launch_join_passes<6, true, true, true, true, 1>);  // timing only: no kill
   if (variant == 135) return go(launch_join_passes<6, true, true, true, true, 2>);  // timing only: no deferred block
@@ -4156,9 +4156,10 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // r03: both sides' member ranks in one packed pass when nL + nR <= 64 (PK)
   if (variant == 259) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true>);
   // r03: + BK (mask3's LDS bank-conflict layout: dword descriptors, 4-B sink stride, header under exec)
-  if (variant == 264) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, true>);
+  if (variant == 264) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1>);
   // r03: + NM (no memset before the join: alternating control-word sets, zeroed by the general kernel)
-  if (variant == 265) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, true, true>);
+  if (variant == 265) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true>);
+
   if (variant == 256) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 6>);
   if (variant == 257) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7>);
   if (variant == 255) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 5>);

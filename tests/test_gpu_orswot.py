@@ -436,3 +436,27 @@ def test_mixed_batch_general_path_list_caps(gpu, oracle):
             _compare(_gpu_merge(gpu, lb, lo, rb, ro, 16), ob, oo, f"repeat {k}")
     finally:
         gpu.set_list_cap(65536)
+
+
+def test_header_without_deferred_clocks_but_deferred_counts_rejected(gpu):
+    """A record whose header says n_def = 0 but counts deferred dots or
+    members (sized to match, so the size check alone passes) is not
+    canonical: the merge kernel rejects it (header_ok) rather than copy
+    those counts into an output header."""
+    import crdts_hip
+    from crdts_hip._lib import CRDT_ENONCANON
+
+    A = 16
+    good = records.encode({0: 2, 3: 1}, {5: {0: 2}, 9: {3: 1}}, {}, A)
+    for dot, mem in ((1, 0), (0, 1)):
+        n = records.record_bytes(A, 2, 2, 0, dot, mem)
+        bad = bytearray(good) + bytes(n - len(good))
+        h = np.frombuffer(bad, np.uint32)
+        h[0], h[5], h[6] = n, dot, mem
+        lb, lo = records.pack_batch([bytes(bad)] * 70)
+        rb, ro = records.pack_batch([good] * 70)
+        with pytest.raises(crdts_hip.CrdtError) as e:
+            _gpu_merge(gpu, lb, lo, rb, ro, A)
+        assert e.value.code == CRDT_ENONCANON
+    lb, lo = records.pack_batch([good] * 70)
+    _gpu_merge(gpu, lb, lo, lb, lo, A)  # the context is clean again
