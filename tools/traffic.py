@@ -51,6 +51,22 @@ def main():
     tag = sys.argv[3] if len(sys.argv) > 3 else os.path.basename(dst)
     os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
     shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), dst + "_kernel_stats.csv")
+    # the stats average every launch, the clock ramp of the first ~30 included;
+    # the timed steps are the trace's last launches: their mean per kernel
+    # (STEADY_LAUNCHES, default 10 = profile.sh's --steps) is what the bench's
+    # HIP-event time is compared with
+    n_last = int(os.environ.get("STEADY_LAUNCHES", "10"))
+    tr = os.path.join(src, "kt", "run_kernel_trace.csv")
+    if os.path.exists(tr):
+        rows = sorted(csv.DictReader(open(tr)), key=lambda r: int(r["Start_Timestamp"]))
+        durs = collections.defaultdict(list)
+        for r in rows:
+            k = short(r["Kernel_Name"])
+            if k:
+                durs[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+        json.dump({k: {"launches": len(v), "mean_ms_all": sum(v) / len(v), "last": min(n_last, len(v)),
+                       "mean_ms_last": sum(v[-n_last:]) / len(v[-n_last:])} for k, v in durs.items()},
+                  open(dst + "_kernel_steady.json", "w"), indent=1)
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     for d in sorted(os.listdir(src)):
         f = os.path.join(src, d, "run_counter_collection.csv")
