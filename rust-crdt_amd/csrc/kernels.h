@@ -22,7 +22,7 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
 int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                                const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
                                uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
-                               uint32_t list_cap, hipStream_t stream, int sparse_variant);
+                               uint32_t list_cap, hipStream_t stream, int sparse_variant, JoinSeq* js);
 
 // Sparse clock joins: n_jobs (1 or 2: PNCounter's P and N) batches in one launch.
 int launch_clock_csr_merge(const crdt_clock_csr* const* self, const crdt_clock_csr* const* other,

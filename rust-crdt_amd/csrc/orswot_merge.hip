@@ -3985,10 +3985,12 @@ __device__ __forceinline__ void sparse_general_one(const uint8_t* Lb, const uint
 __global__ __launch_bounds__(kWave) void orswot_sparse_general_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, const uint8_t* __restrict__ Rb,
     const uint64_t* __restrict__ Roff, uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t n_obj,
-    uint32_t A, uint32_t* __restrict__ ctl, const uint64_t* __restrict__ list, uint32_t list_cap) {
+    uint32_t A, uint32_t* __restrict__ ctl, const uint64_t* __restrict__ list, uint32_t list_cap,
+    uint32_t* __restrict__ zero4) {
   __shared__ u32x4 gen_s[2][kGenStage / 16];
   __shared__ u32x4 gx_s[kSpScratch / 16];
   const uint32_t lane = threadIdx.x;
+  if (zero4 && blockIdx.x == 0u && lane < 4u) zero4[lane] = 0u;  // (the next launch's words: as the dense path)
   const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (n <= list_cap) {
     for (uint32_t e = blockIdx.x; e < n; e += gridDim.x)
@@ -4270,8 +4272,10 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
 int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                                const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
                                uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
-                               uint32_t list_cap, hipStream_t stream, int sparse_variant) {
+                               uint32_t list_cap, hipStream_t stream, int sparse_variant, JoinSeq* js) {
   if (n_obj == 0) return CRDT_OK;
+  JoinSeq local{0u, true};
+  if (!js) js = &local;
   int dev = 0, cus = 256, occ = 0;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -4313,9 +4317,20 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
   const uint64_t want = (chunks + kWavesPerBlock - 1) / kWavesPerBlock;
   const uint64_t cap = (uint64_t)cus * occ;
   const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
+  // the product (sparse_variant 0) takes the dense join's alternating
+  // control-word sets (launch_join_passes NM: no memset before the launch);
+  // diagnostic variants keep ctl[0..3] and the memset
+  const bool nm = sparse_variant == 0;
+  uint32_t* set = nm ? ctl + 4u + 4u * (js->seq & 1u) : ctl;
+  uint32_t* const other = nm ? ctl + 4u + 4u * (~js->seq & 1u) : nullptr;
   void* args[] = {&Lb, &Loff, &Lbytes, &Rb, &Roff, &Rbytes, &Ob, &Ooff, &Obytes, &n_obj, &n_actors, &status,
-                  &ctl, &list, &list_cap};
-  if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;  // ctl[3]: tickets
+                  &set, &list, &list_cap};
+  if (nm) {
+    if (js->dirty && hipMemsetAsync(ctl + 4, 0, 8 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
+    js->dirty = true;  // until both kernels are launched
+  } else if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) {  // ctl[3]: tickets
+    return CRDT_EHIP;
+  }
   if (hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) != hipSuccess)
     return CRDT_EHIP;
   if (sparse_variant == 3 || sparse_variant == 4) return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;  // diagnostics: no general pass
@@ -4323,8 +4338,13 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
   // LDS): a fold step lists ~0.6 % of its objects here (pairs past the 6 KB
   // stage), so the listed objects spread over every CU
   hipLaunchKernelGGL(orswot_sparse_general_kernel, dim3((uint32_t)cus * 6u), dim3(kWave), 0, stream, Lb, Loff, Rb,
-                     Roff, Ob, Ooff, n_obj, n_actors, ctl, list, list_cap);
-  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+                     Roff, Ob, Ooff, n_obj, n_actors, set, list, list_cap, other);
+  if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
+  if (nm) {
+    ++js->seq;
+    js->dirty = false;
+  }
+  return CRDT_OK;
 }
 
 }  // namespace crdts_hip

@@ -419,7 +419,7 @@ int orswot_join_rank_body(crdt_ctx* ctx, Transport& T, const crdt_orswot_batch* 
     const uint64_t cap = acc_bytes + gsz(p, me);
     err = (flags & CRDT_ORSWOT_SPARSE_CLOCK)
               ? launch_orswot_merge_sparse(acc, acc_off, acc_bytes, rb, ro, gsz(p, me), o, oo, cap, nr, A,
-                                           ctx->d_status, ctx->d_ctl, ctx->d_list, ctx->list_cap, st, 0)
+                                           ctx->d_status, ctx->d_ctl, ctx->d_list, ctx->list_cap, st, 0, &ctx->join_seq)
               : launch_orswot_merge(acc, acc_off, acc_bytes, rb, ro, gsz(p, me), o, oo, cap, nr, A, ctx->d_status,
                                     ctx->d_ctl, ctx->d_list, ctx->list_cap, st, 0, 0, &ctx->join_seq);
     acc = o;
