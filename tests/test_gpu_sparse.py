@@ -147,3 +147,30 @@ def test_sparse_validate_and_form_mismatch(gpu):
     acts[0], acts[1] = acts[1], acts[0]
     with pytest.raises(crdts_hip.CrdtError):
         gpu.orswot_validate(crdts_hip.OrswotBatch.from_host(b, o, U, flags=SPARSE))
+
+
+def test_dense_and_sparse_launches_alternate_on_one_context(gpu, oracle):
+    """The dense and the sparse join share the context's alternating
+    control-word sets (no memset before a launch: each launch's general
+    kernel zeroes the set the next launch uses). Dense and sparse launches,
+    with objects past the 2 KB / 6 KB stages in both, interleaved on one
+    context in runs of 1, 2 and 3 — every output equals the oracle's."""
+    import crdts_hip
+
+    (db, do), (eb, eo) = crdts_hip.generate_orswot(6_000, threads=16, seed=71)
+    big = dict(member_universe=200, ancestor_adds=150, max_div_ops=40)
+    (fb, fo), (gb, go) = crdts_hip.generate_orswot(200, threads=16, seed=72, params=big)
+    dl, dr = records.unpack_batch(db, do) + records.unpack_batch(fb, fo), \
+        records.unpack_batch(eb, eo) + records.unpack_batch(gb, go)
+    lb, lo = records.pack_batch(dl)
+    rb, ro = records.pack_batch(dr)
+    dexp = oracle.orswot_merge_batch(lb, lo, rb, ro, 16, threads=16)
+    (sa, sao), (sb, sbo) = crdts_hip.generate_replicas(6_000, 2, threads=16, seed=73)
+    sexp = oracle.orswot_merge_batch(sa, sao, sb, sbo, U, threads=16, flags=SPARSE)
+    L = crdts_hip.OrswotBatch.from_host(lb, lo, 16)
+    R = crdts_hip.OrswotBatch.from_host(rb, ro, 16)
+    for k, kind in enumerate("dsddssdddsss"):
+        if kind == "d":
+            _compare(gpu.orswot_merge(L, R).records(), *dexp, f"dense launch {k}")
+        else:
+            _compare(_merge(gpu, sa, sao, sb, sbo).records(), *sexp, f"sparse launch {k}")
