@@ -495,6 +495,78 @@ __device__ void truncate_lds(const TruncArgs& g, const Rec& R, uint64_t o, uint3
     return dk;
   };
 
+  // ---- one pass for records without deferred removes, <= 64 members of <=
+  // 4 dots (config 3's common record): every lane reads its member's key and
+  // dots into registers, counts and layout follow from two wave reductions,
+  // then the output record is assembled over the stage (all reads are done,
+  // so writing in place is safe) and copied out with 16-B stores — the
+  // scattered 4- / 8-B HBM stores of the general write pass below kept the
+  // texture-address unit busy (as they did in the join). With
+  // no deferred clock nothing is killed, so a kept member keeps >= 1 dot.
+  constexpr uint32_t kTK = 4;  // dots per member held in registers
+  if (L.n_def == 0u && L.n_mem <= kW &&
+      __ballot(lane < L.n_mem && mend(lane) - mbeg(lane) > kTK) == 0ull) {
+    const bool hm = lane < L.n_mem;
+    const uint32_t d0 = hm ? mbeg(lane) : 0u, nd = hm ? mend(lane) - d0 : 0u;
+    const uint64_t kk = hm ? key[lane] : 0ull;
+    uint32_t xs[kTK];
+    uint64_t vs[kTK];
+    uint32_t keepb = 0u, fin = 0u;  // bit j: dot j is kept (above c, none of these records kills)
+    bool above = false;
+#pragma unroll
+    for (uint32_t j = 0; j < kTK; ++j) {
+      xs[j] = j < nd ? dact[d0 + j] : 0u;
+      vs[j] = j < nd ? dctr[d0 + j] : 0ull;
+      const bool gt = j < nd && vs[j] > w.ct[xs[j] & (kTA - 1u)];
+      above = above || gt;
+      keepb |= gt ? 1u << j : 0u;
+      fin += gt ? 1u : 0u;
+    }
+    const uint64_t tx = lane < A ? top[lane] : 0ull, cx = lane < A ? w.ct[lane] : 0ull;
+    const bool kept = hm && above;  // (alive: no deferred clock names a member here)
+    const uint64_t K = __ballot(kept);
+    const uint32_t pm = mbcnt(K), cnt = kept ? fin : 0u, pd = wave_excl(cnt, lane);
+    const uint32_t n_mem = (uint32_t)__popcll(K), n_dot = wave_sum(cnt);
+    RecLayout O;
+    rec_layout(O, A, n_mem, n_dot, 0u, 0u, 0u, false);
+    if (O.size > L.size) {  // cannot happen for a canonical record
+      if (lane == 0u) fail(g.status, CRDT_ENONCANON);
+      tsync();
+      return;
+    }
+    uint8_t* wout = g.out + o;
+    tsync();  // every read of the stage is done: the output is assembled over it
+    uint8_t* S8 = (uint8_t*)w.stage;
+    if (lane < A) ((uint64_t*)(S8 + O.o_clk))[lane] = tx > cx ? tx : 0ull;
+    if (kept) {
+      ((uint64_t*)(S8 + O.o_key))[pm] = kk;
+      ((uint32_t*)(S8 + O.o_mdend))[pm] = pd + cnt;
+      uint32_t q = pd;
+#pragma unroll
+      for (uint32_t j = 0; j < kTK; ++j) {
+        if ((keepb >> j) & 1u) {
+          ((uint64_t*)(S8 + O.o_dctr))[q] = vs[j];
+          ((uint32_t*)(S8 + O.o_dact))[q] = xs[j];
+          ++q;
+        }
+      }
+    }
+    if (lane == 0u && O.o_def != O.o_mpad) *(uint32_t*)(S8 + O.o_mpad) = 0u;
+    if (lane >= 1u && lane < 4u && O.o_end + 4u * (lane - 1u) < O.size) *(uint32_t*)(S8 + O.o_end + 4u * (lane - 1u)) = 0u;
+    if (lane < 8u) {
+      const uint32_t hv[8] = {O.size, A, n_mem, n_dot, 0u, 0u, 0u, g.flags};
+      uint32_t h = 0u;
+#pragma unroll
+      for (uint32_t t = 0; t < 8u; ++t) h = lane == t ? hv[t] : h;
+      ((uint32_t*)S8)[lane] = h;
+    }
+    tsync();
+    for (uint32_t k = lane; k < O.size / 16u; k += kW)
+      __builtin_nontemporal_store(((const tu32x4*)S8)[k], (tu32x4*)wout + k);
+    tsync();  // the stage is reused by the wave's next record
+    return;
+  }
+
   // ---- pass 1: counts (the dense top clock keeps all A slots)
   uint32_t n_def = 0, n_fdot = 0, n_fmem = 0;
   for (uint32_t b = 0; b < L.n_def; b += kW) {
@@ -644,7 +716,7 @@ __device__ void truncate_lds(const TruncArgs& g, const Rec& R, uint64_t o, uint3
 // records are truncated one by one with the next one's record and clock in
 // flight in registers, and the others (CSR top clocks, records past the LDS
 // limits or not canonical here) in the HBM form.
-__global__ __launch_bounds__(kW * kTWaves) void orswot_truncate_kernel(TruncArgs g) {
+__global__ __launch_bounds__(kW * kTWaves, 4) void orswot_truncate_kernel(TruncArgs g) {
   __shared__ TWs ws[kTWaves];
   const uint32_t lane = threadIdx.x & (kW - 1u), wv = threadIdx.x / kW;
   TWs& w = ws[wv];

@@ -93,3 +93,22 @@ def test_empty_member_clock_rejected_by_merge(gpu, oracle):
     with pytest.raises(crdts_hip.CrdtError) as e:
         gpu.orswot_merge(B, B)
     assert e.value.code == CRDT_ENONCANON
+
+
+@pytest.mark.parametrize("A,shape", [(4, {"members": 90, "n_def": (0,)}), (16, {"members": 12, "n_def": (0,)}),
+                                     (8, {"members": 10, "n_def": (0, 1)})])
+def test_single_pass_form_and_its_limits(gpu, oracle, A, shape):
+    """Records without deferred removes, <= 64 members of <= 4 dots take the
+    single-pass LDS form (output assembled over the stage, 16-B copy-out);
+    past 64 members (A = 4, up to 89 members in < 4 KB) or with a member of
+    more than 4 dots (A = 16) the two-pass form — mixed in one batch with
+    records that have deferred removes."""
+    states, clocks, recs = T.cases(6_000, A=A, seed=23 + A, shapes=[shape, {}])
+    n_mem = [len(s[1]) for s in states]
+    most = [max((len(c) for c in s[1].values()), default=0) for s in states]
+    if A == 4:
+        assert sum(1 for n, r in zip(n_mem, recs) if n > 64 and len(r) <= 4096) > 100
+    if A == 16:
+        assert sum(1 for m in most if m > 4) > 100
+    lb, lo = records.pack_batch(recs)
+    _check(gpu, oracle, lb, lo, T.clocks_csr(clocks), A)
