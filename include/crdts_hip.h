@@ -643,8 +643,11 @@ int crdt_dense_generate(uint64_t seed, size_t first_obj, size_t n_obj, uint32_t 
  * d_out_off[i] := self.off[i] (set by the call), so out_bytes >= self.bytes
  * suffices. A member whose clock the subtract empties is kept with an empty
  * clock, as in the reference, and its record carries
- * CRDT_ORSWOT_EMPTY_MEMBER_CLOCK. A malformed record or clock run latches
- * CRDT_ENONCANON (not written). */
+ * CRDT_ORSWOT_EMPTY_MEMBER_CLOCK; such a record is a valid input of this call
+ * (truncating it again drops those members: empty <= c, src/orswot.rs:98-103).
+ * A malformed record or clock run (actors not strictly increasing, a zero
+ * counter) latches CRDT_ENONCANON (that record is not written). d_out must
+ * not overlap the input records (CRDT_EINVAL): the call is not in place. */
 int crdt_orswot_truncate(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_clock_csr* clocks,
                          uint32_t n_actors, uint32_t flags, uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes,
                          void* stream);

@@ -725,7 +725,9 @@ class Engine:
                         check_status=True):
         """out[i] = B[i] after Causal::truncate(&clocks[i]) (src/orswot.rs:159-172),
         written at B.off[i] (crdt_orswot_truncate). Returns an OrswotBatch
-        (`out`, reused, when given: at least B.bytes bytes and B.n_obj offsets)."""
+        (`out`, reused, when given: at least B.bytes bytes and B.n_obj offsets;
+        it must not share memory with B's records — the call is not in place,
+        CRDT_EINVAL)."""
         torch = _torch()
         dev = f"cuda:{self.device}"
         if out is not None:

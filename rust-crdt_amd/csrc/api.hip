@@ -215,6 +215,10 @@ int crdt_orswot_truncate(crdt_ctx* ctx, const crdt_orswot_batch* self, const crd
     return CRDT_EINVAL;
   if (clocks->n_entries && (!clocks->act || !clocks->ctr)) return CRDT_EINVAL;
   if (out_bytes < self->bytes) return CRDT_ECAPACITY;
+  // out must not alias the input: the HBM form compacts sections toward lower
+  // offsets while other lanes still read them
+  const uintptr_t ib = (uintptr_t)self->base, ob = (uintptr_t)d_out;
+  if (ob < ib + self->bytes && ib < ob + out_bytes) return CRDT_EINVAL;
   int rc = set_device(ctx);
   if (rc) return rc;
   return launch_orswot_truncate(*self, *clocks, n_actors, flags, d_out, d_out_off, out_bytes, ctx->d_status,

@@ -91,6 +91,27 @@ __device__ __forceinline__ bool has_key(const uint64_t* k, uint32_t n, uint64_t 
   return lo < n && k[lo] == key;
 }
 
+// Is the truncating clock run canonical — actors strictly increasing,
+// counters > 0 (crdts_hip.h: a malformed run latches CRDT_ENONCANON)? Both
+// lookups (Run::get's binary search, the LDS form's dense row) assume it.
+// a0 / c0: this lane's entry of the first 64 (any value past the run).
+__device__ __forceinline__ bool run_canonical(const Run& c, uint32_t a0, uint64_t c0, uint32_t lane) {
+  bool bad = false;
+  for (uint32_t b = 0; b < c.n; b += kW) {
+    const uint32_t e = b + lane;
+    uint32_t a = a0;
+    uint64_t v = c0;
+    if (b) {
+      a = e < c.n ? c.a[e] : 0u;
+      v = e < c.n ? c.c[e] : 1ull;
+    }
+    uint32_t prev = __shfl_up(a, 1);
+    if (lane == 0u && b) prev = c.a[b - 1u];
+    bad = bad || (e < c.n && (v == 0ull || (e > 0u && a <= prev)));
+  }
+  return __ballot(bad) == 0ull;
+}
+
 struct Rec {
   const uint8_t* r;
   RecLayout L;
@@ -146,29 +167,6 @@ struct TruncArgs {
   uint64_t out_bytes;
   int* status;
 };
-
-// A record's header read and checked (a bad record latches CRDT_ENONCANON
-// and is not written); its layout in R, its clock in c.
-__device__ __forceinline__ bool truncate_open(const TruncArgs& g, uint64_t i, uint32_t lane, Rec& R, Run& c,
-                                              uint64_t& o) {
-  const bool sparse = (g.flags & kSparseClock) != 0u;
-  o = g.off[i];
-  if (lane == 0u) g.out_off[i] = o;
-  bool ok = (o & 15u) == 0u && o <= g.bytes && g.bytes - o >= kHdrBytes;
-  uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (ok)
-    for (int k = 0; k < 8; ++k) h[k] = ((const uint32_t*)(g.base + o))[k];
-  R = Rec{g.base + o, {}, sparse};
-  rec_layout(R.L, h[1], h[2], h[3], h[4], h[5], h[6], sparse);
-  ok = ok && h[0] == R.L.size && h[7] == g.flags && (sparse ? h[1] <= g.A : h[1] == g.A) &&
-       R.L.size <= g.bytes - o && o + R.L.size <= g.out_bytes;
-  const uint64_t c0 = g.coff[i];
-  const uint32_t cn = g.clen[i];
-  ok = ok && c0 <= g.c_entries && cn <= g.c_entries - c0;
-  if (!ok && lane == 0u) fail(g.status, CRDT_ENONCANON);
-  c = Run{g.cact + c0, g.cctr + c0, cn};
-  return ok;
-}
 
 // The general form: every read straight from HBM (any record size, dense or
 // CSR top clock, any number of deferred clocks).
@@ -742,7 +740,9 @@ __global__ __launch_bounds__(kW * kTWaves, 4) void orswot_truncate_kernel(TruncA
     }
     RecLayout L;
     rec_layout(L, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, sparse);
-    ok = ok && h0.x == L.size && h1.w == g.flags && (sparse ? h0.y <= g.A : h0.y == g.A) && L.size <= g.bytes - o &&
+    // a record truncate wrote may hold empty member clocks (flag bit 1): truncating
+    // it again drops them (empty <= c), as the reference's repeated truncates do
+    ok = ok && h0.x == L.size && (h1.w & ~kEmptyClockFlag) == g.flags && (sparse ? h0.y <= g.A : h0.y == g.A) && L.size <= g.bytes - o &&
          o + L.size <= g.out_bytes && c0 <= g.c_entries && cn <= g.c_entries - c0;
     if (__ballot(valid && !ok) != 0ull && lane == 0u) fail(g.status, CRDT_ENONCANON);
     const bool lds = ok && !sparse && h0.y <= kTA && L.size <= kTStage && h1.x <= kTDef && h0.z <= kTStage / 24u;
@@ -763,7 +763,9 @@ __global__ __launch_bounds__(kW * kTWaves, 4) void orswot_truncate_kernel(TruncA
       Run c;
       uint64_t ot;
       rec_of((uint32_t)__builtin_ctzll(m), R, c, ot);
-      truncate_global(g, R, c, ot, lane);
+      const bool cok = run_canonical(c, lane < c.n ? c.a[lane] : 0u, lane < c.n ? c.c[lane] : 1ull, lane);
+      if (cok) truncate_global(g, R, c, ot, lane);
+      else if (lane == 0u) fail(g.status, CRDT_ENONCANON);
     }
     // the LDS form, one record ahead
     uint64_t pend = __ballot(lds);
@@ -781,6 +783,7 @@ __global__ __launch_bounds__(kW * kTWaves, 4) void orswot_truncate_kernel(TruncA
       const uint64_t oc = ot;
       const Run cc = c;
       tstage(w, Rc.L, p, cc, lane);
+      const bool cok = run_canonical(cc, p.a, p.c, lane);
       const bool more = pend != 0ull;
       if (more) {  // the next record's loads, in flight while this one is truncated
         t = (uint32_t)__builtin_ctzll(pend);
@@ -789,8 +792,13 @@ __global__ __launch_bounds__(kW * kTWaves, 4) void orswot_truncate_kernel(TruncA
         tfetch(p, R.r, R.L.size / 16u, c, lane);
       }
       bool wide = false;
-      truncate_lds(g, Rc, oc, lane, w, wide);
-      if (wide) truncate_global(g, Rc, cc, oc, lane);
+      if (cok) {
+        truncate_lds(g, Rc, oc, lane, w, wide);
+        if (wide) truncate_global(g, Rc, cc, oc, lane);
+      } else {
+        if (lane == 0u) fail(g.status, CRDT_ENONCANON);
+        tsync();  // the stage is reused by the wave's next record
+      }
       if (!more) break;
     }
   }

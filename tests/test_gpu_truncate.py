@@ -112,3 +112,83 @@ def test_single_pass_form_and_its_limits(gpu, oracle, A, shape):
         assert sum(1 for m in most if m > 4) > 100
     lb, lo = records.pack_batch(recs)
     _check(gpu, oracle, lb, lo, T.clocks_csr(clocks), A)
+
+
+@pytest.mark.parametrize("A,shapes", [(8, None), (40, None), (8, [{}, {"members": 300}])])
+def test_truncate_twice(gpu, oracle, A, shapes):
+    """A record truncate wrote (possibly with empty member clocks, header flag
+    bit 1) is a valid input of truncate: the reference's Map calls
+    val.truncate again on a nested Orswot (src/map.rs apply_rm / truncate) and
+    drops the empty-clock members then (empty <= c). Both kernel forms (A = 8:
+    LDS and HBM; A = 40: HBM), byte-exact vs the oracle's second truncate."""
+    import crdts_hip
+
+    states, clocks, recs = T.cases(6_000, A=A, seed=31 + A, shapes=shapes)
+    lb, lo = records.pack_batch(recs)
+    first = _check(gpu, oracle, lb, lo, T.clocks_csr(clocks), A)
+    assert sum(1 for r in first if np.frombuffer(r[28:32], np.uint32)[0] & 2) > 50
+    rng = random.Random(A)
+    again = [{a: v + rng.randrange(3) for a, v in c.items() if rng.random() < 0.8} for c in clocks]
+    lb2, lo2 = records.pack_batch(first)
+    second = _check(gpu, oracle, lb2, lo2, T.clocks_csr(again), A)
+    # the handmade case of test_empty_member_clock_rejected_by_merge, truncated again
+    rec = records.encode({0: 5, 1: 1}, {7: {0: 5, 1: 1}}, {((0, 6),): {7}}, 4)
+    one = _check(gpu, oracle, *records.pack_batch([rec]), T.clocks_csr([{0: 3, 1: 2}]), 4)
+    two = _check(gpu, oracle, *records.pack_batch(one), T.clocks_csr([{1: 1}]), 4)
+    assert records.decode(two[0])["entries"] == {} and not records.decode(two[0])["flags"] & 2
+    B = crdts_hip.OrswotBatch.from_host(*records.pack_batch(two), 4)
+    assert gpu.orswot_merge(B, B).records() == two  # canonical again: the merge takes it
+
+
+@pytest.mark.parametrize("A", [8, 40])
+@pytest.mark.parametrize("bad", ["unsorted", "duplicate", "zero", "unsorted_past_64"])
+def test_noncanonical_clock_run_rejected(gpu, A, bad):
+    """A truncating clock run whose actors are not strictly increasing or that
+    holds a zero counter latches CRDT_ENONCANON (crdts_hip.h), in the LDS form
+    (A = 8) and the HBM form (A = 40); a run longer than 64 entries is checked
+    past its first 64 too."""
+    import crdts_hip
+    from crdts_hip._lib import CRDT_ENONCANON
+
+    states, clocks, recs = T.cases(200, A=A, seed=41)
+    off, ln, act, ctr = T.clocks_csr(clocks)
+    k = 117
+    if bad == "unsorted_past_64":
+        run = [(a, 3) for a in range(70)]
+        run[66], run[67] = run[67], run[66]
+    else:
+        run = [(0, 2), (2, 5), (5, 1)]
+        if bad == "unsorted":
+            run[1], run[2] = run[2], run[1]
+        elif bad == "duplicate":
+            run[2] = (2, 7)
+        else:
+            run[1] = (2, 0)
+    runs = [sorted(c.items()) for c in clocks]
+    runs[k] = run
+    ln = np.array([len(r) for r in runs], np.uint32)
+    off = np.zeros(len(runs), np.uint64)
+    off[1:] = np.cumsum(ln[:-1])
+    act = np.array([a for r in runs for a, _ in r], np.uint32)
+    ctr = np.array([c for r in runs for _, c in r], np.uint64)
+    lb, lo = records.pack_batch(recs)
+    B = crdts_hip.OrswotBatch.from_host(lb, lo, A)
+    C = crdts_hip.ClockBatch.from_host(off, ln, act, ctr)
+    with pytest.raises(crdts_hip.CrdtError) as e:
+        gpu.orswot_truncate(B, C)
+    assert e.value.code == CRDT_ENONCANON
+
+
+def test_out_aliasing_the_input_rejected(gpu):
+    """crdt_orswot_truncate is not in place: an output range overlapping the
+    input records is CRDT_EINVAL (checked before any launch)."""
+    import crdts_hip
+    from crdts_hip._lib import CRDT_EINVAL
+
+    states, clocks, recs = T.cases(300, A=40, seed=3)
+    B = crdts_hip.OrswotBatch.from_host(*records.pack_batch(recs), 40)
+    C = crdts_hip.ClockBatch.from_host(*T.clocks_csr(clocks))
+    with pytest.raises(crdts_hip.CrdtError) as e:
+        gpu.orswot_truncate(B, C, out=B)
+    assert e.value.code == CRDT_EINVAL
+    gpu.orswot_truncate(B, C)  # the context is still usable

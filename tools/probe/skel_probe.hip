@@ -1,0 +1,180 @@
+// Data-flow skeleton of orswot_join_kernel (diagnostic, not product): the
+// product's chunk step, register prefetch one object ahead, LDS staging of
+// both records and an LDS -> HBM copy-out of an output-sized record, with NO
+// join (a synthetic dependent VALU chain of `spin` steps stands in for it).
+// The two knobs are the two data-flow changes VERDICT r03 asks to measure:
+//   HDR 0 : the chunk step reads each object's two 32-B record headers (lane =
+//           object, 64 scattered 128-B lines per side per chunk: the product)
+//   HDR 1 : it reads an 8-B per-object shape word per side instead (size and
+//           counts, coalesced: 512 B per side per chunk)
+//   PACK 0: output record i at lo[i] + ro[i] (the product's placement)
+//   PACK 1: output records packed back to back per chunk from lo[c0] + ro[c0]
+// The output stands in with the self record (its size ~ the merged size).
+//   hipcc --offload-arch=gfx950 -O3 -shared -fPIC skel_probe.hip -o libskel.so
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+constexpr int kWave = 64;
+constexpr int kWpb = 4;
+constexpr int kPer = 2;  // 16-B pieces per lane per record (records <= 2 KB)
+constexpr uint32_t kPad = 26624 / kWpb / 16 - 2 * kPer * kWave;  // LDS per wave as the product's (6 blocks/CU)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4 gu32x4;
+
+__device__ __forceinline__ uint32_t lane_of(uint32_t v, uint32_t t) { return __builtin_amdgcn_readlane(v, t); }
+__device__ __forceinline__ uint64_t lane_of64(uint64_t v, uint32_t t) {
+  return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), t) << 32) | __builtin_amdgcn_readlane((uint32_t)v, t);
+}
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ const __attribute__((address_space(1))) uint8_t* sbase(const uint8_t* src) {
+  const uint64_t b = (uint64_t)src;
+  return (const __attribute__((address_space(1))) uint8_t*)(
+      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+      (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b));
+}
+// the product's prefetch_sa: wave-uniform base, clamped 32-bit lane offsets
+__device__ __forceinline__ void prefetch(u32x4 (&r)[kPer], const uint8_t* src, uint32_t n16, uint32_t lane) {
+  const auto* s = sbase(src);
+  const uint32_t last = __builtin_amdgcn_readfirstlane(n16 - 1u);
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t idx = lane + k * kWave;
+    r[k] = __builtin_nontemporal_load((gu32x4*)(s + 16u * (idx < last ? idx : last)));
+  }
+}
+__device__ __forceinline__ void stage(u32x4* dst, const u32x4 (&r)[kPer], uint32_t n16, uint32_t lane) {
+  dst[lane] = r[0];
+#pragma unroll
+  for (uint32_t k = 1; k < kPer; ++k)
+    if (n16 > k * kWave) dst[lane + k * kWave] = r[k];
+}
+// the product's copy_record_sb: two 16-B stores per lane, byte-clamped
+__device__ __forceinline__ void copy_out(const u32x4* src, uint8_t* O, uint32_t n16, uint32_t lane, bool nt) {
+  const uint32_t last = __builtin_amdgcn_readfirstlane(n16 - 1u);
+  const uint32_t i0 = lane < last ? lane : last, i1 = lane + kWave < last ? lane + kWave : last;
+  const u32x4 p0 = src[i0], p1 = src[i1];
+  if (nt) {
+    __builtin_nontemporal_store(p0, (u32x4*)O + i0);
+    __builtin_nontemporal_store(p1, (u32x4*)O + i1);
+  } else {
+    ((u32x4*)O)[i0] = p0;
+    ((u32x4*)O)[i1] = p1;
+  }
+}
+
+template <int HDR, int PACK, bool NT>
+__global__ __launch_bounds__(kWave* kWpb, 6) void skel_kernel(const uint8_t* __restrict__ Lb,
+                                                               const uint64_t* __restrict__ Loff,
+                                                               const uint64_t* __restrict__ Lsh,
+                                                               const uint8_t* __restrict__ Rb,
+                                                               const uint64_t* __restrict__ Roff,
+                                                               const uint64_t* __restrict__ Rsh,
+                                                               uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff,
+                                                               uint64_t n_obj, uint32_t* sinkp) {
+  __shared__ u32x4 st[kWpb][2 * kPer * kWave + kPad];
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+  u32x4* const sL = st[wave];
+  u32x4* const sR = st[wave] + kPer * kWave;
+  const uint64_t wave_id = (uint64_t)blockIdx.x * kWpb + wave, n_waves = (uint64_t)gridDim.x * kWpb;
+  uint32_t sink = 0;
+  const uint32_t spin = sinkp[1];
+  // the product's static split: equal chunks of cs <= 64 objects
+  const uint64_t rounds = (n_obj + n_waves * kWave - 1) / (n_waves * kWave);
+  const uint64_t cs = (n_obj + n_waves * rounds - 1) / (n_waves * rounds);
+  for (uint64_t cbase = wave_id * cs; cbase < n_obj; cbase += n_waves * cs) {
+    const uint64_t obj = cbase + lane;
+    const bool valid = lane < cs && obj < n_obj;
+    uint64_t lo = 0, ro = 0;
+    uint32_t szl = 0, szr = 0, meta = 0;
+    if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
+    if (HDR == 0) {
+      u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
+      if (valid) {
+        hl0 = ((const u32x4*)(Lb + lo))[0]; hl1 = ((const u32x4*)(Lb + lo))[1];
+        hr0 = ((const u32x4*)(Rb + ro))[0]; hr1 = ((const u32x4*)(Rb + ro))[1];
+      }
+      szl = hl0.x; szr = hr0.x;
+      meta = hl0.z + hr0.w + hl1.x + hr1.x;
+    } else {
+      uint64_t a = 0, b = 0;
+      if (valid) { a = Lsh[obj]; b = Rsh[obj]; }
+      szl = (uint32_t)a; szr = (uint32_t)b;
+      meta = (uint32_t)(a >> 32) + (uint32_t)(b >> 32);
+    }
+    const bool ok = valid && szl <= 2048u && szr <= 2048u && szl >= 16u && szr >= 16u;
+    sink += meta;
+    const uint32_t n16 = ok ? (szl / 16u) | ((szr / 16u) << 16) : 0u;
+    uint64_t pend = __ballot(ok);
+    if (!pend) continue;
+    uint64_t cur = lane_of64(lo, 0) + lane_of64(ro, 0);
+    u32x4 pl[kPer], pr[kPer];
+    uint32_t t = __builtin_ctzll(pend);
+    pend &= pend - 1;
+    uint32_t nt16 = lane_of(n16, t);
+    prefetch(pl, Lb + lane_of64(lo, t), nt16 & 0xFFFFu, lane);
+    prefetch(pr, Rb + lane_of64(ro, t), nt16 >> 16, lane);
+    wave_sync();
+    stage(sL, pl, nt16 & 0xFFFFu, lane);
+    stage(sR, pr, nt16 >> 16, lane);
+    wave_sync();
+    for (;;) {
+      const uint32_t u = pend ? (uint32_t)__builtin_ctzll(pend) : t;
+      const uint32_t nu = lane_of(n16, u);
+      prefetch(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
+      prefetch(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
+      {  // synthetic join: a dependent LDS read + VALU chain
+        uint32_t h = ((const uint32_t*)sR)[lane] ^ ((const uint32_t*)sL)[lane];
+        for (uint32_t q = 0; q < spin; ++q) h = h * 0x9e3779b1u + (h >> 7);
+        sink += h;
+      }
+      const uint32_t on16 = nt16 & 0xFFFFu;  // output stand-in: the self record
+      const uint64_t oo = PACK ? cur : lane_of64(lo, t) + lane_of64(ro, t);
+      cur += 16u * on16;
+      wave_sync();
+      copy_out(sL, Ob + oo, on16, lane, NT);
+      if (lane == 0) Ooff[cbase + t] = oo;
+      if (!pend) break;
+      t = u;
+      nt16 = nu;
+      pend &= pend - 1;
+      wave_sync();
+      stage(sL, pl, nu & 0xFFFFu, lane);
+      stage(sR, pr, nu >> 16, lane);
+      wave_sync();
+    }
+  }
+  if (sink == 0x9e3779b9u) sinkp[0] = sink;
+}
+}  // namespace
+
+extern "C" int skel_launch(int variant, int blocks_per_cu, const uint8_t* Lb, const uint64_t* Loff,
+                           const uint64_t* Lsh, const uint8_t* Rb, const uint64_t* Roff, const uint64_t* Rsh,
+                           uint8_t* Ob, uint64_t* Ooff, uint64_t n_obj, uint32_t* sink, void* stream) {
+  const void* fn = nullptr;
+  switch (variant) {  // HDR * 10 + PACK (+100: default-policy stores)
+    case 0: fn = (const void*)skel_kernel<0, 0, true>; break;
+    case 1: fn = (const void*)skel_kernel<0, 1, true>; break;
+    case 10: fn = (const void*)skel_kernel<1, 0, true>; break;
+    case 11: fn = (const void*)skel_kernel<1, 1, true>; break;
+    case 100: fn = (const void*)skel_kernel<0, 0, false>; break;
+    case 101: fn = (const void*)skel_kernel<0, 1, false>; break;
+    case 110: fn = (const void*)skel_kernel<1, 0, false>; break;
+    case 111: fn = (const void*)skel_kernel<1, 1, false>; break;
+    default: return -1;
+  }
+  int occ = 0;
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kWpb, 0);
+  if (blocks_per_cu > 0 && blocks_per_cu < occ) occ = blocks_per_cu;
+  const uint64_t chunks = (n_obj + 63) / 64;
+  uint64_t blocks = 256ull * occ;
+  if (blocks > (chunks + kWpb - 1) / kWpb) blocks = (chunks + kWpb - 1) / kWpb;
+  void* args[] = {&Lb, &Loff, &Lsh, &Rb, &Roff, &Rsh, &Ob, &Ooff, &n_obj, &sink};
+  return hipLaunchKernel(fn, dim3((uint32_t)blocks), dim3(kWave * kWpb), args, 0, (hipStream_t)stream) == hipSuccess
+             ? occ
+             : -2;
+}
