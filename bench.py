@@ -252,7 +252,10 @@ def run_orswot(args, rank, world, local):
     out_sizes = out.base.view(torch.int32)[(out.off // 4)].cpu().numpy().astype(np.int64)
     in_bytes = int(lb.nbytes + rb.nbytes)
     out_bytes = int(out_sizes.sum())
-    alg_bytes = in_bytes + out_bytes + 3 * 8 * n  # + L/R offsets read, out offsets written
+    rec_bytes = in_bytes + out_bytes + 3 * 8 * n  # record bytes: + L/R offsets read, out offsets written
+    # the roofline numerator: SURVEY.md §8(d)'s compact bytes of both inputs
+    # and the output (no headers, padding or offsets), from the records' headers
+    alg_bytes = L.compact_bytes() + R.compact_bytes() + out.compact_bytes()
 
     for _ in range(args.warmup):
         eng.orswot_merge(L, R, out=out, stream=stream, check_status=False)
@@ -272,6 +275,7 @@ def run_orswot(args, rank, world, local):
     total_objs = sum_over_ranks(float(n * args.steps), world)
     value = total_objs / wall
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    achieved_rec = rec_bytes / (kernel_ms * 1e-3) / 1e9
     # measured HBM bytes of one launch (both kernels of the timed window), from
     # the FETCH_SIZE / WRITE_SIZE passes of tools/profile.sh -> tools/traffic.py
     tk = [load_traffic(args.traffic_json, k) for k in ("orswot_join_kernel", "orswot_merge_general_kernel")]
@@ -295,6 +299,7 @@ def run_orswot(args, rank, world, local):
             "n_obj_per_gpu": n,
             "n_actors": 16,
             "alg_bytes_per_merge": alg_bytes / n,
+            "record_bytes_per_merge": rec_bytes / n,
             "parallelism": f"objects sharded over {world} GPU(s), no collective",
             "gen_s": round(gen_s, 2),
         },
@@ -307,7 +312,10 @@ def run_orswot(args, rank, world, local):
             "frac": achieved / HBM_PEAK_GBS,
             "kernel_ms": kernel_ms,
             "alg_bytes_per_launch": alg_bytes,
+            "alg_bytes_def": "SURVEY.md §8(d) compact bytes of self + other + out (no header / padding / offsets)",
             "traffic": traffic,
+            "record_bytes": {"per_launch": rec_bytes, "achieved": achieved_rec, "frac": achieved_rec / HBM_PEAK_GBS,
+                             "def": "the record layout's bytes: headers, padding, + 3 x 8 B offsets per object"},
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -687,12 +695,20 @@ def run_orswot_csr(args, rank, world, local, eng=None):
         # step: merge k reads acc_k (replica 0, then the previous output) and
         # replica k+1, and writes its output; + 3 offsets per object-merge
         outs_b = [rec_bytes(o) for o in outs]
-        alg = sum(rec_bytes(B) for B in batches) + sum(outs_b) + sum(outs_b[:-1]) + 3 * 8 * n * (R - 1)
+        alg_rec = sum(rec_bytes(B) for B in batches) + sum(outs_b) + sum(outs_b[:-1]) + 3 * 8 * n * (R - 1)
+        # the roofline numerator: SURVEY.md §8(d)'s compact bytes of every merge's two inputs and output
+        outs_c = [o.compact_bytes() for o in outs]
+        alg = sum(B.compact_bytes() for B in batches) + sum(outs_c) + sum(outs_c[:-1])
         ach = alg / (ev_ms * 1e-3) / 1e9
+        ach_rec = alg_rec / (ev_ms * 1e-3) / 1e9
         res["roofline"] = {"bound": "hbm", "kernel": "fold of 7 launches: orswot_sparse_mask_kernel + orswot_sparse_general_kernel", "achieved": ach,
                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                            "kernel_ms": ev_ms, "alg_bytes_per_launch": alg / (R - 1),
-                           "traffic": wl_traffic(args, "orswot_csr", "orswot_sparse_mask_kernel", "orswot_sparse_general_kernel")}
+                           "alg_bytes_def": "SURVEY.md §8(d) compact bytes (CSR top = 4 + 12 nnz) of both inputs + "
+                                            "output of every fold merge, no header / padding / offsets",
+                           "traffic": wl_traffic(args, "orswot_csr", "orswot_sparse_mask_kernel", "orswot_sparse_general_kernel"),
+                           "record_bytes": {"per_launch": alg_rec / (R - 1), "achieved": ach_rec,
+                                            "frac": ach_rec / HBM_PEAK_GBS}}
         if not args.no_cpu_baseline:
             sys.path.insert(0, os.path.join(REPO, "tests"))
             import oracle_ffi

@@ -557,9 +557,12 @@ int crdt_mvreg_merge(crdt_ctx* ctx, const uint32_t* d_self_n, const uint64_t* d_
  * PRECONDITION: self's records do not overlap and are in increasing offset
  * order (as any packed or merged batch); a record that would outgrow its own
  * span self.size + P*ops + 16*pairs + 32 latches CRDT_ECAPACITY and is not
- * written. Limits of this round (CRDT_ECAPACITY): <= 128
- * top-clock entries, members, dots per member clock and Rm clock pairs; <= 512
- * dots; <= 32 deferred clocks with <= 256 entries and <= 256 members.      */
+ * written. Limits per object, at every step of its op list (past one:
+ * CRDT_ECAPACITY, the object is not written): <= 2048 top-clock entries (dense:
+ * n_actors <= 2048), <= 4096 members, <= 16384 dots, <= 2048 pairs in an Rm
+ * clock, <= 256 deferred clocks with <= 4096 entries and <= 4096 members in
+ * all. (Objects are joined in an 8 KB LDS workspace, those that outgrow it in
+ * a 16 KB one, the rest in an HBM workspace: the limits are the last one's.) */
 #define CRDT_OP_ADD 0u
 #define CRDT_OP_RM 1u
 typedef struct crdt_orswot_ops {
@@ -593,8 +596,10 @@ int crdt_orswot_apply(crdt_ctx* ctx, const crdt_orswot_batch* self, const crdt_o
  * Ingest = from_binary + canonicalisation; a blob a record cannot hold
  * (zero counter, empty member clock / deferred clock / deferred set, actor
  * >= n_actors, duplicates, BTreeMap keys out of order, truncated or trailing
- * bytes) latches CRDT_ENONCANON; one with more than 256 members or 64
- * deferred clocks latches CRDT_ECAPACITY (limits of this round).
+ * bytes) latches CRDT_ENONCANON; one with more than 16384 members or more
+ * than 1024 deferred clocks latches CRDT_ECAPACITY, and so do the objects of
+ * one call past its first 65536 with more than 256 members or 64 deferred
+ * clocks (those are decoded by a second kernel from an HBM scratch).
  *   1) crdt_orswot_bincode_record_sizes: d_sizes[i] = record bytes (0 if bad)
  *      — or, without reading the blobs, crdt_orswot_bincode_record_bounds:
  *      d_bounds[i] >= the record bytes of any blob of length blob_len[i]

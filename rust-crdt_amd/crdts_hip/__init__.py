@@ -150,6 +150,16 @@ class OrswotBatch:
         off = self.off.cpu().numpy().view(np.uint64)
         return base, off
 
+    def compact_bytes(self):
+        """Σ over the records of SURVEY.md §8(d)'s compact algorithmic bytes
+        (record.compact_bytes), from the headers gathered on the device."""
+        torch = _torch()
+        w = self.base[: self.base.numel() // 4 * 4].view(torch.int32)
+        h = w[(self.off // 4)[:, None] + torch.arange(8, device=self.off.device)[None, :]].to(torch.int64)
+        sp = (h[:, 7] & SPARSE_CLOCK) != 0
+        top = torch.where(sp, 4 + 12 * h[:, 1], 8 * h[:, 1])
+        return int((top + 8 + 12 * h[:, 2] + 12 * h[:, 3] + 8 * h[:, 4] + 12 * h[:, 5] + 8 * h[:, 6]).sum().item())
+
     def records(self):
         base, off = self.to_host()
         out = []

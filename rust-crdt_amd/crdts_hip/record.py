@@ -96,3 +96,25 @@ def encode_record(clock, entries, deferred, n_actors, sparse=False):
     struct.pack_into(f"<{n_def}I", out, o, *de); o += 4 * n_def
     struct.pack_into(f"<{n_def}I", out, o, *me)
     return bytes(out)
+
+
+def compact_bytes(n_clk, n_mem, n_dot, n_def, n_def_dot, n_def_mem, sparse=False):
+    """SURVEY.md §8(d)'s algorithmic bytes of one Orswot side in the compact
+    layout (no header, no padding): top + 4 + 4 + Σ_members(8 key + 4 dot-off +
+    12·dots) + Σ_deferred(4 + 12·dots + 4 + 8·members), top = 8·A dense or
+    4 + 12·nnz sparse. Works elementwise on numpy arrays of header counts."""
+    top = 4 + 12 * n_clk if sparse else 8 * n_clk
+    return top + 8 + 12 * n_mem + 12 * n_dot + 8 * n_def + 12 * n_def_dot + 8 * n_def_mem
+
+
+def batch_compact_bytes(base, off):
+    """Σ compact_bytes over a batch's records, read from their headers
+    (base: uint8 numpy buffer, off: record offsets; flags bit 0 per record)."""
+    import numpy as np
+
+    w = np.asarray(base)[: len(base) // 4 * 4].view(np.uint32)
+    i = (np.asarray(off, dtype=np.uint64) // np.uint64(4)).astype(np.int64)
+    h = [w[i + k].astype(np.int64) for k in range(8)]
+    sp = (h[7] & SPARSE_CLOCK) != 0
+    top = np.where(sp, 4 + 12 * h[1], 8 * h[1])
+    return int((top + 8 + 12 * h[2] + 12 * h[3] + 8 * h[4] + 12 * h[5] + 8 * h[6]).sum())
