@@ -491,7 +491,7 @@ def run_dense(args, rank, world, local, kind):
 
 class TimingEvents:
     """n (start, end) pairs of timing-only HIP events on torch's HIP runtime
-    (the already-loaded libamdhip64.so.7): created with
+    (the already-loaded libamdhip64, crdts_hip._lib.hip_runtime): created with
     hipEventDisableSystemFence, so recording one does not write back and
     invalidate the caches between two steps — a per-step torch event does,
     and that gap (~11 us per step, tools/steady_probe.py) is not part of the
@@ -504,8 +504,10 @@ class TimingEvents:
 
         import torch  # noqa: F401  (its HIP runtime is the one bound below)
 
+        from crdts_hip._lib import hip_runtime
+
         self.C = C
-        self.hip = C.CDLL("libamdhip64.so.7")
+        self.hip = hip_runtime()
         self.hip.hipEventCreateWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_uint]
         self.hip.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
         self.hip.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
@@ -633,7 +635,9 @@ def run_orswot_csr(args, rank, world, local, eng=None):
 
     final = step()
     eng.status(stream)
+    syncs0 = eng.host_syncs()
     wall, ev_ms = _timed_steps(args, world, stream, step)
+    syncs_per_step = (eng.host_syncs() - syncs0) / float(args.warmup + args.steps)
     eng.status(stream)
     if world > 1:
         # self-check (outside the timed region): identical bytes on every rank,
@@ -684,7 +688,7 @@ def run_orswot_csr(args, rank, world, local, eng=None):
                    if world > 1 else "local fold"},
     }
     if world > 1:
-        res["comm"] = {"rccl_ranks": None if args.rehearse else eng.comm_count(), "host_syncs_per_step": 4,
+        res["comm"] = {"rccl_ranks": None if args.rehearse else eng.comm_count(), "host_syncs_per_step": syncs_per_step,
                        "transport": "gloo (rehearsal)" if args.rehearse else "rccl"}
         res["check"] = check
     if world == 1:

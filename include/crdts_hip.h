@@ -66,6 +66,10 @@ int crdt_abi_version(void);
  * general kernels scan every output offset instead; results are identical.
  * Lowering it exercises that overflow path (tests). */
 int crdt_ctx_set_list_cap(crdt_ctx* ctx, uint32_t cap);
+/* Host synchronisations with the device (stream waits) the context's replica
+ * joins have made so far (crdt_orswot_replica_join*: 3 per call in the steady
+ * state). A counter for callers that profile the join's per-step cost. */
+uint64_t crdt_ctx_host_syncs(const crdt_ctx* ctx);
 
 /* ------------------------------------------------------------------------ *
  * Dense clocks and counters.

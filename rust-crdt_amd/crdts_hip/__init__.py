@@ -514,6 +514,10 @@ class Engine:
               "replica_reduce_scatter_max")
         return out
 
+    def host_syncs(self):
+        """Host synchronisations the context's replica joins made so far (crdt_ctx_host_syncs)."""
+        return int(lib.crdt_ctx_host_syncs(self.ctx))
+
     def comm_count(self):
         """Ranks of the context's RCCL communicator (ncclCommCount)."""
         n = C.c_int(0)

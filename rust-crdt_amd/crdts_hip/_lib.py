@@ -71,10 +71,25 @@ EXPORTS = [
     "crdt_orswot_replica_join_bound", "crdt_orswot_replica_join", "crdt_orswot_replica_join_local",
     "crdt_comm_count", "crdt_orswot_replica_join_transport", "crdt_orswot_generate_replicas_subset",
     "crdt_dense_merge_host", "crdt_vclock_csr_merge", "crdt_gcounter_csr_merge", "crdt_pncounter_csr_merge",
-    "crdt_orswot_truncate",
+    "crdt_orswot_truncate", "crdt_ctx_host_syncs",
 ]
 
 CRDT_COMM_ID_BYTES = 128
+
+
+def hip_runtime():
+    """The HIP runtime library this process already has loaded (torch's), found
+    in /proc/self/maps — not a fixed soname, so a ROCm major version change does
+    not load a second runtime. Falls back to the unversioned soname."""
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                path = line.split()[-1] if line.strip() else ""
+                if os.path.basename(path).startswith("libamdhip64.so"):
+                    return C.CDLL(path)
+    except OSError:
+        pass
+    return C.CDLL("libamdhip64.so")
 
 
 class Ops(C.Structure):
@@ -151,6 +166,7 @@ def _load():
         "crdt_ctx_status": (I, [P, P]),
         "crdt_ctx_set_blocks_per_cu": (I, [P, I]),
         "crdt_ctx_set_list_cap": (I, [P, U32]),
+        "crdt_ctx_host_syncs": (U64, [P]),
         "crdt_ctx_set_variant": (I, [P, I]),
         "crdt_ctx_debug_read": (I, [P, P, SZ, P]),
         "crdt_strerror": (C.c_char_p, [I]),

@@ -206,11 +206,11 @@ class GlooTransport:
 
         import torch.distributed as dist
 
-        from ._lib import ALLGATHER_FN, EXCHANGE_FN, TransportC
+        from ._lib import ALLGATHER_FN, EXCHANGE_FN, TransportC, hip_runtime
 
         self.group = group
         self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
-        self._hip = C.CDLL("libamdhip64.so.7")  # the HIP runtime already loaded (torch's)
+        self._hip = hip_runtime()  # the HIP runtime already loaded (torch's)
         self._hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
         self._hip.hipStreamSynchronize.argtypes = [C.c_void_p]
         self.calls = {"allgather": 0, "exchange": 0, "bytes_sent": 0, "bytes_received": 0}
@@ -234,11 +234,31 @@ class GlooTransport:
             out[:] = torch.cat(parts).numpy()
             self.calls["allgather"] += 1
             return 0
-        except Exception as e:  # noqa: BLE001 - reported to the C side as a transport failure
-            print(f"GlooTransport.allgather: {e!r}", flush=True)
-            return 1
+        except Exception as e:  # noqa: BLE001 - peers may be inside the collective
+            self._abandon("allgather", e)
+
+    @staticmethod
+    def _abandon(what, e):
+        """A transport failure after the peers may have posted their side of the
+        collective: they would wait forever, so this process exits (non-zero)
+        and its peers' waits fail on the closed connection — no rank is left
+        waiting in a collective another has left."""
+        import os
+        import sys
+
+        print(f"GlooTransport.{what}: {e!r}; exiting so that no peer waits forever", file=sys.stderr, flush=True)
+        os._exit(70)
 
     def _exchange(self, user, sends, ns, recvs, nr, stream):
+        # the local checks first: a mismatch found before any request is
+        # posted is returned as a failure (the C side reports CRDT_ECOMM)
+        S = [sends[k] for k in range(ns)]
+        Rv = [recvs[k] for k in range(nr)]
+        me = self.rank
+        self_s = [x for x in S if x.peer == me]
+        self_r = [y for y in Rv if y.peer == me]
+        if len(self_s) != len(self_r) or any(x.bytes != y.bytes for x, y in zip(self_s, self_r)):
+            self._abandon("exchange", ValueError("self transfers do not pair up"))
         try:
             import ctypes as C
 
@@ -246,17 +266,8 @@ class GlooTransport:
             import torch.distributed as dist
 
             if self._hip.hipStreamSynchronize(stream) != 0:  # the sends' data is produced on `stream`
-                return 1
-            S = [sends[k] for k in range(ns)]
-            Rv = [recvs[k] for k in range(nr)]
-            me = self.rank
-            self_s = [x for x in S if x.peer == me]
-            self_r = [y for y in Rv if y.peer == me]
-            if len(self_s) != len(self_r):
-                return 1
+                raise RuntimeError("hipStreamSynchronize failed")
             for x, y in zip(self_s, self_r):  # k-th self send -> k-th self recv
-                if x.bytes != y.bytes:
-                    return 1
                 self._memcpy(y.dst, x.src, x.bytes)
             reqs, landing = [], []
             tag = {}
@@ -282,9 +293,8 @@ class GlooTransport:
                 self.calls["bytes_received"] += y.bytes
             self.calls["exchange"] += 1
             return 0
-        except Exception as e:  # noqa: BLE001 - reported to the C side as a transport failure
-            print(f"GlooTransport.exchange: {e!r}", flush=True)
-            return 1
+        except Exception as e:  # noqa: BLE001 - peers may be inside the collective
+            self._abandon("exchange", e)
 
 
 def digest(batch) -> int:

@@ -298,6 +298,8 @@ size_t crdt_orswot_compact_scratch_bytes(size_t n_obj) {
   return ((8 * n_obj + 255) & ~size_t(255)) + temp + 256;
 }
 
+uint64_t crdt_ctx_host_syncs(const crdt_ctx* ctx) { return ctx ? ctx->host_syncs : 0ull; }
+
 int crdt_orswot_compact(crdt_ctx* ctx, const crdt_orswot_batch* src, uint8_t* d_dst,
                         uint64_t* d_dst_off, size_t dst_bytes, void* d_scratch, void* stream) {
   if (!ctx || !src || (src->n_obj && (!src->base || !src->off || !d_dst || !d_dst_off || !d_scratch)))
@@ -324,7 +326,7 @@ int crdt_orswot_compact(crdt_ctx* ctx, const crdt_orswot_batch* src, uint8_t* d_
       hipStreamSynchronize(S(stream)) != hipSuccess)
     return CRDT_EHIP;
   if (last_off + last_size > dst_bytes) return CRDT_ECAPACITY;
-  return launch_record_copy(src->base, src->off, sizes, d_dst, d_dst_off, src->n_obj, S(stream));
+  return launch_record_copy(src->base, src->off, sizes, d_dst, d_dst_off, src->n_obj, dst_bytes, S(stream));
 }
 
 int crdt_orswot_merge_host(crdt_ctx* ctx, const uint8_t* h_self_base, const uint64_t* h_self_off,

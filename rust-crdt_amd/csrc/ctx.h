@@ -46,6 +46,8 @@ struct crdt_ctx {
   // on first use
   uint8_t* d_big = nullptr;
   size_t big_bytes = 0;
+  // host synchronisations made by the replica joins so far (crdt_ctx_host_syncs)
+  uint64_t host_syncs = 0;
 };
 
 // Ensures ctx->d_big holds at least `bytes` (api.hip).

@@ -40,8 +40,9 @@ int launch_orswot_validate(const uint8_t* base, const uint64_t* off, uint64_t by
 // out of [0, bytes)), and the copy of sizes[i] bytes per record.
 int launch_record_sizes(const uint8_t* base, const uint64_t* off, uint64_t bytes, uint64_t n_obj, uint64_t* sizes,
                         int* status, hipStream_t stream);
+// records whose [dst_off, dst_off + size) does not fit dst_bytes are not copied
 int launch_record_copy(const uint8_t* src, const uint64_t* src_off, const uint64_t* sizes, uint8_t* dst,
-                       const uint64_t* dst_off, uint64_t n_obj, hipStream_t stream);
+                       const uint64_t* dst_off, uint64_t n_obj, uint64_t dst_bytes, hipStream_t stream);
 
 int launch_bincode_bounds(const uint64_t* blen, uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A,
                           uint32_t flags, uint64_t* bounds, hipStream_t stream);

@@ -102,13 +102,15 @@ __global__ __launch_bounds__(256) void copy_kernel(const uint8_t* __restrict__ s
                                                    const uint64_t* __restrict__ sizes,
                                                    uint8_t* __restrict__ dst,
                                                    const uint64_t* __restrict__ dst_off,
-                                                   uint64_t n_obj) {
+                                                   uint64_t n_obj, uint64_t dst_bytes) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t stride = (uint64_t)gridDim.x * 4;
   for (uint64_t i = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64; i < n_obj; i += stride) {
     const uint4* s = (const uint4*)(src + src_off[i]);
-    uint4* d = (uint4*)(dst + dst_off[i]);
-    const uint32_t n16 = (uint32_t)(sizes[i] / 16);
+    const uint64_t o = dst_off[i], sz = sizes[i];
+    if (o > dst_bytes || sz > dst_bytes - o) continue;
+    uint4* d = (uint4*)(dst + o);
+    const uint32_t n16 = (uint32_t)(sz / 16);
     for (uint32_t k = lane; k < n16; k += 64) d[k] = s[k];
   }
 }
@@ -133,12 +135,12 @@ int launch_record_sizes(const uint8_t* base, const uint64_t* off, uint64_t bytes
 }
 
 int launch_record_copy(const uint8_t* src, const uint64_t* src_off, const uint64_t* sizes, uint8_t* dst,
-                       const uint64_t* dst_off, uint64_t n_obj, hipStream_t stream) {
+                       const uint64_t* dst_off, uint64_t n_obj, uint64_t dst_bytes, hipStream_t stream) {
   if (n_obj == 0) return CRDT_OK;
   uint64_t want = (n_obj + 3) / 4;
   uint32_t blocks = (uint32_t)(want < 2048 ? want : 2048);
   hipLaunchKernelGGL(copy_kernel, dim3(blocks), dim3(256), 0, stream, src, src_off, sizes, dst, dst_off,
-                     n_obj);
+                     n_obj, dst_bytes);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 

@@ -57,13 +57,18 @@ constexpr size_t kAllReduceChunk = size_t(1) << 27;  // u64 words per collective
 // extent of object range j = [b_j, b_{j+1}), b_j = j*n/N, of this replica
 // (0, 0 for an empty range; ~0 as the end of a range whose last record
 // header lies out of bounds), then the host-known fields of the row.
+// Row word 2R + 1 is the error word: a status an earlier launch on this
+// context latched and the caller has not read is reported through it (every
+// rank then fails the join with it) and cleared.
 __global__ void slice_bounds_kernel(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                     uint64_t bytes, uint64_t n, uint32_t R, uint64_t* __restrict__ d, uint64_t f0,
-                                    uint64_t f1, uint64_t f2, uint64_t f3) {
+                                    int* __restrict__ status, uint64_t f2, uint64_t f3) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j == 0) {
+    const int st = *status;
+    *status = 0;
     d[2u * R] = f0;
-    d[2u * R + 1u] = f1;
+    d[2u * R + 1u] = (uint64_t)(int64_t)-st;
     d[2u * R + 2u] = f2;
     d[2u * R + 3u] = f3;
   }
@@ -97,6 +102,21 @@ __global__ void rebase_kernel(uint64_t* __restrict__ off, uint64_t n, uint64_t p
   off[i] = off[i] - sub[p] + add[p];
 }
 
+// The step-4 row of the owner-sharded join, on the device: {E = bytes of the
+// compacted folded range, out_bytes, error word (the fold's latched status, or
+// CRDT_ENONCANON when E outgrows the inputs)} — all-gathered straight from
+// here, so the compaction's sizes and the status need no read of their own.
+__global__ void join_row_kernel(const uint64_t* __restrict__ shard_off, const uint64_t* __restrict__ sizes,
+                                uint64_t nr, uint64_t total, uint64_t out_bytes, int* __restrict__ status,
+                                uint64_t* __restrict__ row) {
+  if (threadIdx.x != 0) return;
+  const uint64_t E = nr ? shard_off[nr - 1u] + sizes[nr - 1u] : 0ull;
+  const int st = *status;
+  row[0] = E;
+  row[1] = out_bytes;
+  row[2] = st ? (uint64_t)(int64_t)-st : (E > total ? (uint64_t)(int64_t)-CRDT_ENONCANON : 0ull);
+}
+
 int launch_rebase(uint64_t* off, uint64_t n, uint64_t per, const uint64_t* first, const uint64_t* sub,
                   const uint64_t* add, uint32_t R, hipStream_t st) {
   if (n == 0) return CRDT_OK;
@@ -110,15 +130,19 @@ using Xfer = crdt_xfer;
 
 struct Transport {
   int R = 1, me = 0;
+  uint64_t syncs = 0;  // host synchronisations with the device made here
   virtual ~Transport() = default;
+  int sync(hipStream_t st) {
+    ++syncs;
+    return hipStreamSynchronize(st) == hipSuccess ? CRDT_OK : CRDT_EHIP;
+  }
   // blocking: every rank contributes n u64 (host), receives R*n in rank order
   virtual int allgather(const uint64_t* h_in, size_t n, uint64_t* h_out, hipStream_t st) = 0;
   // the same with the contribution in DEVICE memory, produced on st (one
   // host synchronisation in all)
   virtual int allgather_dev(const uint64_t* d_in, size_t n, uint64_t* h_out, hipStream_t st) {
     std::vector<uint64_t> h(n);
-    if (n && (hipMemcpyAsync(h.data(), d_in, 8 * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
-              hipStreamSynchronize(st) != hipSuccess))
+    if (n && (hipMemcpyAsync(h.data(), d_in, 8 * n, hipMemcpyDeviceToHost, st) != hipSuccess || sync(st)))
       return CRDT_EHIP;
     return allgather(h.data(), n, h_out, st);
   }
@@ -144,8 +168,7 @@ struct RcclTransport : Transport {
     if (n > stage_row(R)) return CRDT_EINVAL;
     int rc = nccl_rc(ncclAllGather(d_in, d_buf + stage_row(R), n, ncclUint64, comm, st));
     if (rc) return rc;
-    if (hipMemcpyAsync(h_out, d_buf + stage_row(R), 8 * n * R, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
+    if (hipMemcpyAsync(h_out, d_buf + stage_row(R), 8 * n * R, hipMemcpyDeviceToHost, st) != hipSuccess || sync(st))
       return CRDT_EHIP;
     return CRDT_OK;
   }
@@ -282,13 +305,13 @@ int ensure_arena(crdt_ctx* ctx, size_t bytes) {
 }
 
 // Arena layout of rank j's part of a join (every rank can compute every
-// rank's, from the step-1 all-gather): head = step-1 row (2R + 4 u64) and the
-// rebase table (3R u64); then every replica's slice of range j, their
+// rank's, from the step-1 all-gather): head = step-1 row (2R + 4 u64), the
+// rebase table (3R u64) and the step-4 row (3 u64); then every replica's slice of range j, their
 // offsets, two fold buffers (ping-pong), sizes and scan scratch.
 struct Plan {
   size_t head, o_recv, o_roff, o_fa, o_fb, o_oa, o_ob, o_sz, o_cub, cub_temp, end;
 };
-inline size_t plan_head(int R) { return al256(8ull * (2 * R + 4) + 8ull * 3 * R); }
+inline size_t plan_head(int R) { return al256(8ull * (2 * R + 4) + 8ull * 3 * R + 8ull * 3); }  // + the step-4 row
 Plan make_plan(int R, uint64_t nr, uint64_t total) {
   Plan P;
   P.head = plan_head(R);
@@ -314,9 +337,10 @@ Plan make_plan(int R, uint64_t nr, uint64_t total) {
 // decides whether a rank goes on to the next collective is taken from
 // all-gathered data, so all ranks leave at the same step (none is left
 // waiting in a collective another has left). Host synchronisations per call
-// in the steady state (arena large enough on every rank): 4 — the step-1
-// all-gather, the compaction's sizes + status read, the step-4 all-gather,
-// and the final one (the call is synchronous).
+// in the steady state (arena large enough on every rank): 3 — the step-1
+// all-gather, the step-4 all-gather (its row — the compacted range's size and
+// the fold's status — is produced on the device), and the final one (the call
+// is synchronous). They are counted in ctx->host_syncs.
 int orswot_join_rank_body(crdt_ctx* ctx, Transport& T, const crdt_orswot_batch* mine, uint32_t A, uint32_t flags,
                           uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes, size_t* h_used, hipStream_t st) {
   const int R = T.R, me = T.me;
@@ -339,9 +363,8 @@ int orswot_join_rank_body(crdt_ctx* ctx, Transport& T, const crdt_orswot_batch* 
   }
   uint64_t* d_row = (uint64_t*)ctx->d_arena;
   uint64_t* d_tab = d_row + W;
-  if (hipMemsetAsync(ctx->d_status, 0, sizeof(int), st) != hipSuccess) return CRDT_EHIP;
   hipLaunchKernelGGL(slice_bounds_kernel, dim3((R + 63) / 64), dim3(64), 0, st, n ? mine->base : nullptr,
-                     n ? mine->off : nullptr, (uint64_t)mine->bytes, n, (uint32_t)R, d_row, n, 0ull,
+                     n ? mine->off : nullptr, (uint64_t)mine->bytes, n, (uint32_t)R, d_row, n, ctx->d_status,
                      want ? 1ull : 0ull, (uint64_t)ctx->arena_bytes);
   if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
   std::vector<uint64_t> G(W * R);
@@ -430,32 +453,34 @@ int orswot_join_rank_body(crdt_ctx* ctx, Transport& T, const crdt_orswot_batch* 
   uint8_t* shard = A8 + (in_a ? P.o_fb : P.o_fa);
   uint64_t* shard_off = (uint64_t*)(A8 + (in_a ? P.o_ob : P.o_oa));
   uint64_t* sizes = (uint64_t*)(A8 + P.o_sz);
-  uint64_t E = 0;
   if (nr && !err) {
     // record sizes, bounds-checked (an object the fold rejected leaves no
-    // record behind its offset: size 0 and CRDT_ENONCANON latched), the
-    // scan, and the fold's latched status, read in one synchronisation
+    // record behind its offset: size 0 and CRDT_ENONCANON latched), the scan,
+    // and the copy (each record only where it fits the shard buffer); the
+    // compacted size and the fold's status go out with the step-4 row
     err = launch_record_sizes(acc, acc_off, acc_bytes, nr, sizes, ctx->d_status, st);
     if (!err && hipcub::DeviceScan::ExclusiveSum(A8 + P.o_cub, P.cub_temp, sizes, shard_off, (int)nr, st) !=
                     hipSuccess)
       err = CRDT_EHIP;
-    uint64_t lo = 0, ls = 0;
-    int stv = 0;
-    if (!err && (hipMemcpyAsync(&lo, shard_off + nr - 1, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                 hipMemcpyAsync(&ls, sizes + nr - 1, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                 hipMemcpyAsync(&stv, ctx->d_status, sizeof stv, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                 hipStreamSynchronize(st) != hipSuccess))
-      err = CRDT_EHIP;
-    if (!err && stv) err = stv;  // record-level errors latched by the fold, validation or sizes
-    E = lo + ls;
-    if (!err && E > total) err = CRDT_ENONCANON;  // a merged record never outgrows its inputs
-    if (!err) err = launch_record_copy(acc, acc_off, sizes, shard, shard_off, nr, st);
+    if (!err) err = launch_record_copy(acc, acc_off, sizes, shard, shard_off, nr, total, st);
   }
 
-  // 4. every rank's folded range to every rank that gathers the result
-  uint64_t m2[3] = {E, (uint64_t)out_bytes, (uint64_t)-err};
+  // 4. every rank's folded range to every rank that gathers the result: the
+  //    row {E, out_bytes, error} all-gathered from the device (from the host
+  //    when a launch failed here)
   std::vector<uint64_t> G2(3 * R);
-  if ((rc = T.allgather(m2, 3, G2.data(), st))) return rc;
+  if (!err) {
+    uint64_t* d_row2 = d_tab + 3 * R;
+    hipLaunchKernelGGL(join_row_kernel, dim3(1), dim3(64), 0, st, shard_off, sizes, nr, (uint64_t)total,
+                       (uint64_t)out_bytes, ctx->d_status, d_row2);
+    if (hipGetLastError() != hipSuccess) err = CRDT_EHIP;
+    if (!err && (rc = T.allgather_dev(d_row2, 3, G2.data(), st))) return rc;
+  }
+  if (err) {
+    uint64_t m2[3] = {0, (uint64_t)out_bytes, (uint64_t)-err};
+    if ((rc = T.allgather(m2, 3, G2.data(), st))) return rc;
+  }
+  const uint64_t E = G2[3 * me];
   std::vector<uint64_t> Pq(R + 1, 0);
   for (int q = 0; q < R; ++q) {
     if (G2[3 * q + 2]) return -(int)G2[3 * q + 2];
@@ -488,7 +513,7 @@ int orswot_join_rank_body(crdt_ctx* ctx, Transport& T, const crdt_orswot_batch* 
     if (!rc && h_used) *h_used = Pq[R];
   }
   // the tables are read by kernels on st: finished before a later call reuses them
-  if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = CRDT_EHIP;
+  if (T.sync(st) && !rc) rc = CRDT_EHIP;
   return rc;
 }
 
@@ -496,6 +521,7 @@ int orswot_join_rank_body(crdt_ctx* ctx, Transport& T, const crdt_orswot_batch* 
 int orswot_join_rank(crdt_ctx* ctx, Transport& T, const crdt_orswot_batch* mine, uint32_t A, uint32_t flags,
                      uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes, size_t* h_used, hipStream_t st) {
   const int rc = orswot_join_rank_body(ctx, T, mine, A, flags, d_out, d_out_off, out_bytes, h_used, st);
+  ctx->host_syncs += T.syncs;
   if (rc) {
     (void)hipStreamSynchronize(st);
     (void)hipMemsetAsync(ctx->d_status, 0, sizeof(int), st);
