@@ -52,6 +52,8 @@ def parse():
                    choices=["orswot", "vclock", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply",
                             "mvreg", "map", "map_orswot", "clock_csr", "truncate", "spawn_check"])
     p.add_argument("--replicas", type=int, default=8, help="orswot_csr at N=1: replicas folded locally")
+    p.add_argument("--n-actors", type=int, default=16,
+                   help="orswot: dense top-clock actors (config 3: 16; 33-64 take the 64-bit actor-mask join)")
     p.add_argument("--n-obj", type=int, default=None, help="objects per GPU")
     p.add_argument("--threads", type=int, default=16, help="host threads for input generation")
     p.add_argument("--cpu-threads", type=int, default=None,
@@ -240,11 +242,13 @@ def run_orswot(args, rank, world, local):
     n = args.n_obj or 1_000_000
     first = rank * n
     t0 = time.time()
-    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(n, first_obj=first, threads=args.threads)
+    A = args.n_actors
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(n, first_obj=first, threads=args.threads,
+                                                   params=None if A == 16 else {"n_actors": A})
     gen_s = time.time() - t0
     eng = crdts_hip.Engine(local)
-    L = crdts_hip.OrswotBatch.from_host(lb, lo, 16, device=local)
-    R = crdts_hip.OrswotBatch.from_host(rb, ro, 16, device=local)
+    L = crdts_hip.OrswotBatch.from_host(lb, lo, A, device=local)
+    R = crdts_hip.OrswotBatch.from_host(rb, ro, A, device=local)
     out = eng.orswot_alloc_out(L, R)
     stream = torch.cuda.Stream(device=local)
     # one checked launch, then algorithmic bytes from the real output sizes
@@ -279,7 +283,7 @@ def run_orswot(args, rank, world, local):
     # measured HBM bytes of one launch (both kernels of the timed window), from
     # the FETCH_SIZE / WRITE_SIZE passes of tools/profile.sh -> tools/traffic.py
     tk = [load_traffic(args.traffic_json, k) for k in ("orswot_join_kernel", "orswot_merge_general_kernel")]
-    traffic = None if args.n_obj is not None or tk[0] is None else tk[0] + (tk[1] or 0.0)
+    traffic = None if args.n_obj is not None or A != 16 or tk[0] is None else tk[0] + (tk[1] or 0.0)
     res = {
         "metric": METRIC,
         "value": value,
@@ -294,10 +298,12 @@ def run_orswot(args, rank, world, local):
         "dtype": "u64",
         "data": "synthetic: op-simulated Orswot pairs (SplitMix64 seed 0xC0FFEE03 ^ object id)",
         "config": {
-            "workload": "orswot_merge config3 (BASELINE.json configs[2]): 1M objects/GPU x ~31 members/side "
-                        "x 16 dense actors incl. deferred removes",
+            "workload": ("orswot_merge config3 (BASELINE.json configs[2]): 1M objects/GPU x ~31 members/side "
+                         "x 16 dense actors incl. deferred removes") if A == 16 else
+                        (f"orswot_merge config3 shape over {A} dense actors (64-bit actor-mask join): "
+                         f"{n} objects/GPU incl. deferred removes"),
             "n_obj_per_gpu": n,
-            "n_actors": 16,
+            "n_actors": A,
             "alg_bytes_per_merge": alg_bytes / n,
             "record_bytes_per_merge": rec_bytes / n,
             "parallelism": f"objects sharded over {world} GPU(s), no collective",

@@ -1435,7 +1435,7 @@ __device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t
 // to add. Returns the output's 16-B pieces, or kLeanFallback (a dot actor
 // >= A, or a union of more than 64 members).
 // ======================================================================
-constexpr uint32_t k3MsL = 0, k3MsR = 512, k3Out = 0, k3EqGe = 1024, k3Desc = 1536, k3Trash = 1664;
+constexpr uint32_t k3Desc = 1536, k3Trash = 1664;  // (the rest of mask3's layout: M3Lay)
 constexpr uint32_t k3Scratch = 2176;  // <= kMask1Scratch: the kernel's scratch also serves mask_object
 constexpr uint32_t k3DefMask = k3Scratch;  // u32 [64] (HK 1): actor mask per deferred clock
 static_assert(k3DefMask + 256u <= 2560u, "the deferred clock masks fit in the wave's scratch");
@@ -1488,6 +1488,22 @@ __device__ __forceinline__ void copy_record_out(uint32_t src, uint8_t* O, uint32
   __builtin_nontemporal_store(p1, (u32x4*)(O + 16u * i1));
 }
 
+// mask3_object's per-wave scratch by actor-mask width: {actor mask, survives
+// mask} per member of each side, {equal, >=} per union slot, the union
+// descriptors and the sink (BK layout). Out ({keep, useK} by union slot, the
+// deferred-remove objects) overlays the member masks once they are read.
+template <int AW> struct M3Lay;
+template <> struct M3Lay<32> {
+  using MT = uint32_t;
+  static constexpr uint32_t MsL = 0, MsR = 512, Out = 0, EqGe = 1024, Desc = 1536, TrBK = 1792;
+  static constexpr uint32_t Bytes = 2560;  // == kMask1Scratch
+};
+template <> struct M3Lay<64> {
+  using MT = uint64_t;
+  static constexpr uint32_t MsL = 0, MsR = 1024, Out = 0, EqGe = 2048, Desc = 3072, TrBK = 3328;
+  static constexpr uint32_t Bytes = 3840;
+};
+
 // HD (with OUT 0 only): objects with deferred removes — kept dots that a
 // deferred clock listing their member covers are cleared from the keep masks
 // (apply_deferred -> apply_remove, src/orswot.rs:235-243, :195-211) and the
@@ -1503,7 +1519,7 @@ __device__ __forceinline__ const uint8_t* gptr(uint32_t a) {
 // 64-lane pass (L members in lanes [0, nL), R members in [nL, nL + nR)), half
 // the search instructions of the two-sided form
 template <uint32_t OUTCAP, int OUT = 0, bool HD = false, int HABL = 0, bool RT = true, int HK = 0, bool PK = false,
-          int BK = 0>  // OUT: 0 direct stores, 1 sink-predicated, 2 LDS-assembled
+          int BK = 0, int AW = 32>  // OUT: 0 direct stores, 1 sink-predicated, 2 LDS-assembled; AW: actor mask bits
 __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint32_t uX, uint8_t* O, uint32_t A,
                                                  uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane,
                                                  bool& big, uint8_t* sink = nullptr) {
@@ -1518,6 +1534,13 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
   constexpr uint32_t TR = BK ? 1792u : k3Trash;  // the wave's sink (512 B)
   constexpr uint32_t DS = BK ? 4u : 2u;          // bytes per union descriptor
   static_assert(!BK || TR >= k3Desc + 256u, "BK descriptors: 64 dwords before the sink");
+  // AW 64 (dense top clocks of 33-64 actors): 64-bit actor masks, the mask
+  // tables twice as wide (M3Lay<64>), the BK layout only
+  static_assert(AW == 32 || (AW == 64 && BK && HK == 0), "AW 64: the product's BK form");
+  using MT = typename M3Lay<AW>::MT;
+  constexpr uint32_t MsL = M3Lay<AW>::MsL, MsR = M3Lay<AW>::MsR, EqGe = M3Lay<AW>::EqGe, Desc = M3Lay<AW>::Desc;
+  constexpr uint32_t Out = M3Lay<AW>::Out, MW = sizeof(MT), ME = 2u * MW;  // mask word, {mask, mask} entry
+  constexpr uint32_t TRW = AW == 64 ? M3Lay<AW>::TrBK : TR;  // the wave's sink
   big = false;
   const uint32_t key = kHdrBytes + 8u * A;
   const uint32_t ctrL = key + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
@@ -1549,7 +1572,7 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
     // both key lists copied into 64-slot tables padded with ~0 (in the mask
     // scratch, dead until the masks are zeroed below): the probes need no
     // bound, and every probe address is the lane's position + an immediate
-    const uint32_t tL = uX + k3MsL, tR = uX + k3MsR;
+    const uint32_t tL = uX + MsL, tR = uX + MsR;
     *(lds_u64*)(size_t)(tL + l8) = bit_of(mnL, lane) ? kl : ~0ull;
     *(lds_u64*)(size_t)(tR + l8) = bit_of(mnR, lane) ? kr : ~0ull;
     wave_sync();
@@ -1631,33 +1654,50 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
   const uint32_t mr = __builtin_amdgcn_mbcnt_hi((uint32_t)(HR >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)HR, hr - 1u));
 
   // ---- dots above the OTHER side's pre-merge top clock (survives masks)
-  const uint64_t SL = cmp64<kUGT>(vl, gather64(tr, xl & 31u)) & mdL;
-  const uint64_t SR = cmp64<kUGT>(vr, gather64(tl, xr & 31u)) & mdR;
+  const uint64_t SL = cmp64<kUGT>(vl, gather64(tr, xl & (AW - 1u))) & mdL;
+  const uint64_t SR = cmp64<kUGT>(vr, gather64(tl, xr & (AW - 1u))) & mdR;
 
   // ---- scratch: zero the mask tables and union descriptors, then the
   // per-member {actor mask, survives mask} by 64-bit atomic ORs
-  const uint32_t trash = uX + TR + l8;
-  *(lds_u64*)(size_t)(uX + k3MsL + l8) = 0ull;
-  *(lds_u64*)(size_t)(uX + k3MsR + l8) = 0ull;
-  *(lds_u64*)(size_t)(uX + k3EqGe + l8) = 0ull;
+  const uint32_t trash = uX + TRW + l8;
+  *(lds_u64*)(size_t)(uX + MsL + l8) = 0ull;
+  *(lds_u64*)(size_t)(uX + MsR + l8) = 0ull;
+  *(lds_u64*)(size_t)(uX + EqGe + l8) = 0ull;
+  if (AW == 64) {
+    *(lds_u64*)(size_t)(uX + MsL + 512u + l8) = 0ull;
+    *(lds_u64*)(size_t)(uX + MsR + 512u + l8) = 0ull;
+    *(lds_u64*)(size_t)(uX + EqGe + 512u + l8) = 0ull;
+  }
   if (BK)
-    *(lds_u32*)(size_t)(uX + k3Desc + 4u * lane) = 0u;
+    *(lds_u32*)(size_t)(uX + Desc + 4u * lane) = 0u;
   else
-    *(lds_u16*)(size_t)(uX + k3Desc + 2u * lane) = (uint16_t)0;
+    *(lds_u16*)(size_t)(uX + Desc + 2u * lane) = (uint16_t)0;
   wave_sync();
-  const uint32_t bl = 1u << (xl & 31u), br = 1u << (xr & 31u);
-  {
+  const MT bl = (MT)1 << (xl & (AW - 1u)), br = (MT)1 << (xr & (AW - 1u));
+  if (AW == 64) {  // {actor mask, survives mask} as two 64-bit words per member
+    const uint32_t al = bit_of(mdL, lane) ? uX + MsL + ME * ml : trash, ar = bit_of(mdR, lane) ? uX + MsR + ME * mr : trash;
+    __hip_atomic_fetch_or((lds_u64*)(size_t)al, bit_of(mdL, lane) ? (uint64_t)bl : 0ull, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or((lds_u64*)(size_t)(al + (bit_of(mdL, lane) ? 8u : 0u)), bit_of(SL, lane) ? (uint64_t)bl : 0ull,
+                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or((lds_u64*)(size_t)ar, bit_of(mdR, lane) ? (uint64_t)br : 0ull, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or((lds_u64*)(size_t)(ar + (bit_of(mdR, lane) ? 8u : 0u)), bit_of(SR, lane) ? (uint64_t)br : 0ull,
+                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  } else {
     const uint64_t ol = ((uint64_t)(bit_of(SL, lane) ? bl : 0u) << 32) | (bit_of(mdL, lane) ? bl : 0u);
     const uint64_t orr = ((uint64_t)(bit_of(SR, lane) ? br : 0u) << 32) | (bit_of(mdR, lane) ? br : 0u);
-    __hip_atomic_fetch_or((lds_u64*)(size_t)(bit_of(mdL, lane) ? uX + k3MsL + 8u * ml : trash), ol,
+    __hip_atomic_fetch_or((lds_u64*)(size_t)(bit_of(mdL, lane) ? uX + MsL + 8u * ml : trash), ol,
                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_or((lds_u64*)(size_t)(bit_of(mdR, lane) ? uX + k3MsR + 8u * mr : trash), orr,
+    __hip_atomic_fetch_or((lds_u64*)(size_t)(bit_of(mdR, lane) ? uX + MsR + 8u * mr : trash), orr,
                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  {
     // union descriptors: L lanes store index + 1 in the low byte of their
     // slot, R lanes in the high byte (a shared key: both, same slot)
-    const uint32_t trash1 = BK ? uX + TR + 4u * lane : trash;
-    *(lds_u8*)(size_t)(bit_of(mnL, lane) ? uX + k3Desc + DS * ul : trash1) = (uint8_t)(lane + 1u);
-    *(lds_u8*)(size_t)(bit_of(mnR, lane) ? uX + k3Desc + DS * ur + 1u : trash1) = (uint8_t)(lane + 1u);
+    const uint32_t trash1 = BK ? uX + TRW + 4u * lane : trash;
+    *(lds_u8*)(size_t)(bit_of(mnL, lane) ? uX + Desc + DS * ul : trash1) = (uint8_t)(lane + 1u);
+    *(lds_u8*)(size_t)(bit_of(mnR, lane) ? uX + Desc + DS * ur + 1u : trash1) = (uint8_t)(lane + 1u);
   }
   wave_sync();
 
@@ -1668,34 +1708,59 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
   const uint32_t q = gather32(pj, mr);
   {
     const uint32_t i = q & 63u, u = (q >> 8) & 63u;
-    const uint32_t MLi = lr32(uX + k3MsL + 8u * i);
+    const MT MLi = AW == 64 ? (MT)lr64(uX + MsL + ME * i) : (MT)lr32(uX + MsL + 8u * i);
     const uint32_t a0 = gather32(sl, i);
-    const uint32_t idx = a0 + __popc(MLi & (br - 1u));
+    const uint32_t idx = a0 + (uint32_t)__builtin_popcountg(MLi & (br - (MT)1));
     const uint64_t va = lr64(uL + ctrL + 8u * idx);
-    const uint64_t SH = cmp32<kNE>(q & 0x10000u, 0u) & cmp32<kNE>(MLi & br, 0u) & mdR;
+    const uint64_t SH = cmp32<kNE>(q & 0x10000u, 0u) &
+                        (AW == 64 ? cmp64<kNE>((uint64_t)(MLi & br), 0ull) : cmp32<kNE>((uint32_t)(MLi & br), 0u)) & mdR;
     const uint64_t EQ = cmp64<kEQ>(va, vr) & SH, GE = cmp64<kUGE>(va, vr) & SH;
-    const uint64_t o = ((uint64_t)(bit_of(GE, lane) ? br : 0u) << 32) | (bit_of(EQ, lane) ? br : 0u);
-    __hip_atomic_fetch_or((lds_u64*)(size_t)(bit_of(SH, lane) ? uX + k3EqGe + 8u * u : trash), o, __ATOMIC_RELAXED,
-                          __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (AW == 64) {  // {equal, >=} as two 64-bit words per union slot
+      const uint32_t ae = bit_of(SH, lane) ? uX + EqGe + ME * u : trash;
+      __hip_atomic_fetch_or((lds_u64*)(size_t)ae, bit_of(EQ, lane) ? (uint64_t)br : 0ull, __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_or((lds_u64*)(size_t)(ae + (bit_of(SH, lane) ? 8u : 0u)), bit_of(GE, lane) ? (uint64_t)br : 0ull,
+                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      const uint64_t o = ((uint64_t)(bit_of(GE, lane) ? br : 0u) << 32) | (bit_of(EQ, lane) ? br : 0u);
+      __hip_atomic_fetch_or((lds_u64*)(size_t)(bit_of(SH, lane) ? uX + EqGe + 8u * u : trash), o, __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
   }
   wave_sync();
 
   // ---- per union member: the mask join
-  const uint32_t dsc = BK ? lr32(uX + k3Desc + 4u * lane)
-                          : *(const __attribute__((address_space(3))) uint16_t*)(size_t)(uX + k3Desc + 2u * lane);
+  const uint32_t dsc = BK ? lr32(uX + Desc + 4u * lane)
+                          : *(const __attribute__((address_space(3))) uint16_t*)(size_t)(uX + Desc + 2u * lane);
   const uint32_t mi = (dsc - 1u) & 63u, mj = ((dsc >> 8) - 1u) & 63u;
-  const uint64_t pL = lr64(uX + k3MsL + 8u * mi), pR = lr64(uX + k3MsR + 8u * mj), pE = lr64(uX + k3EqGe + l8);
   const uint64_t mU = lanes_below(U);
   const uint64_t hasL = cmp32<kNE>(dsc & 0xFFu, 0u) & mU, hasR = cmp32<kNE>(dsc >> 8, 0u) & mU;
   const uint64_t selfonly = hasL & ~hasR;
-  const uint32_t ML = bit_of(hasL, lane) ? (uint32_t)pL : 0u, FL = (uint32_t)(pL >> 32) & ML;
-  const uint32_t MR = bit_of(hasR, lane) ? (uint32_t)pR : 0u, FR = (uint32_t)(pR >> 32) & MR;
-  const uint32_t EQm = (uint32_t)pE, GEm = (uint32_t)(pE >> 32);  // zero unless both sides
-  const uint32_t lp = bit_of(selfonly, lane) ? ML : FL, rp = FR;
-  const uint32_t useA = (ML & MR & EQm) | (lp & (~rp | GEm));
-  const uint64_t dropS = cmp32<kEQ>(FL, 0u) & selfonly;  // self-only entry not above R's clock: dropped whole
-  uint32_t keep = (bit_of(dropS, lane) || !bit_of(mU, lane)) ? 0u : (useA | rp);
-  uint32_t useK = useA & keep;
+  MT ML, FL, MR, FR, EQm, GEm;  // EQm / GEm: zero unless both sides
+  if (AW == 64) {
+    const uint64_t pL0 = lr64(uX + MsL + ME * mi), pL1 = lr64(uX + MsL + ME * mi + 8u);
+    const uint64_t pR0 = lr64(uX + MsR + ME * mj), pR1 = lr64(uX + MsR + ME * mj + 8u);
+    EQm = (MT)lr64(uX + EqGe + ME * lane);
+    GEm = (MT)lr64(uX + EqGe + ME * lane + 8u);
+    ML = bit_of(hasL, lane) ? (MT)pL0 : (MT)0;
+    FL = (MT)pL1 & ML;
+    MR = bit_of(hasR, lane) ? (MT)pR0 : (MT)0;
+    FR = (MT)pR1 & MR;
+  } else {
+    const uint64_t pL = lr64(uX + MsL + 8u * mi), pR = lr64(uX + MsR + 8u * mj), pE = lr64(uX + EqGe + l8);
+    ML = bit_of(hasL, lane) ? (MT)(uint32_t)pL : (MT)0;
+    FL = (MT)(uint32_t)(pL >> 32) & ML;
+    MR = bit_of(hasR, lane) ? (MT)(uint32_t)pR : (MT)0;
+    FR = (MT)(uint32_t)(pR >> 32) & MR;
+    EQm = (MT)(uint32_t)pE;
+    GEm = (MT)(uint32_t)(pE >> 32);
+  }
+  const MT lp = bit_of(selfonly, lane) ? ML : FL, rp = FR;
+  const MT useA = (ML & MR & EQm) | (lp & (~rp | GEm));
+  const uint64_t dropS = (AW == 64 ? cmp64<kEQ>((uint64_t)FL, 0ull) : cmp32<kEQ>((uint32_t)FL, 0u)) &
+                         selfonly;  // self-only entry not above R's clock: dropped whole
+  MT keep = (bit_of(dropS, lane) || !bit_of(mU, lane)) ? (MT)0 : (useA | rp);
+  MT useK = useA & keep;
   Side DL{nullptr, RV{}}, DR{nullptr, RV{}};
   if (HD && HABL != 1) {  // (HABL: timing-only ablations, diagnostic builds)
     static_assert(!HD || OUT == 0, "deferred removes: direct stores only");
@@ -1706,8 +1771,13 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
     // k, 32 + k: other's) — built from the deferred member lists, one lane per
     // (clock, member) item: the clock by a search over the run ends, the
     // union slot by a search of the key among each side's members
-    const uint32_t dmt = uX + k3EqGe;
-    *(lds_u64*)(size_t)(uX + k3Out + l8) = (uint64_t)keep | ((uint64_t)useK << 32);
+    const uint32_t dmt = uX + EqGe;
+    if (AW == 64) {
+      *(lds_u64*)(size_t)(uX + Out + ME * lane) = (uint64_t)keep;
+      *(lds_u64*)(size_t)(uX + Out + ME * lane + 8u) = (uint64_t)useK;
+    } else {
+      *(lds_u64*)(size_t)(uX + Out + l8) = (uint64_t)keep | ((uint64_t)useK << 32);
+    }
     *(lds_u64*)(size_t)(dmt + l8) = 0ull;
     wave_sync();
     const uint32_t nfL = DL.v.n_def, nfR = DR.v.n_def;
@@ -1717,7 +1787,7 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
       // the union keys by slot (slots are in key order), over the R member
       // masks read above, padded with ~0; and per deferred clock (lanes 0-31:
       // self's, 32-63: other's) the mask of the actors it holds
-      const uint32_t ut = uX + k3MsR;
+      const uint32_t ut = uX + MsR;
       const uint64_t ukey = lr64(bit_of(hasL, lane) ? uL + key + 8u * mi : uR + key + 8u * mj);
       *(lds_u64*)(size_t)(ut + l8) = bit_of(mU, lane) ? ukey : ~0ull;
       // the masks: one lane per deferred clock entry of either side (its
@@ -1738,7 +1808,7 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
         const uint32_t a = lr32(us + (isL ? DL.v.fact : DR.v.fact) + 4u * e);
         wide = wide || (act && a >= 32u);
         const bool put = act && a < 32u;
-        __hip_atomic_fetch_or((lds_u32*)(size_t)(put ? uX + k3DefMask + 4u * (isL ? k : 32u + k) : uX + TR + l8),
+        __hip_atomic_fetch_or((lds_u32*)(size_t)(put ? uX + k3DefMask + 4u * (isL ? k : 32u + k) : uX + TRW + l8),
                               put ? 1u << a : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       if (__ballot(wide) != 0ull) return kLeanFallback;
@@ -1758,7 +1828,7 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
         for (uint32_t step = 256u; step >= 8u; step >>= 1) q = lr64(q + step - 8u) < m ? q + step : q;
         const uint32_t su = (q - ut) >> 3;
         const bool hit = act && su < U && lr64(q) == m;
-        __hip_atomic_fetch_or((lds_u64*)(size_t)(hit ? dmt + 8u * su : uX + TR + l8),
+        __hip_atomic_fetch_or((lds_u64*)(size_t)(hit ? dmt + 8u * su : uX + TRW + l8),
                               hit ? 1ull << (isL ? k : 32u + k) : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     } else
@@ -1790,15 +1860,27 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
       const uint32_t sul = gather32(ul, il & 63u), sur = gather32(ur, ir & 63u);  // every lane: bpermute sources
       const uint32_t su = eqL ? sul : sur;
       const bool hit = act && (eqL || eqR);
-      __hip_atomic_fetch_or((lds_u64*)(size_t)(hit ? dmt + 8u * (su & 63u) : uX + TR + l8),
+      __hip_atomic_fetch_or((lds_u64*)(size_t)(hit ? dmt + 8u * (su & 63u) : uX + TRW + l8),
                             hit ? 1ull << (isL ? k : 32u + k) : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     wave_sync();
     // a surviving self dot / kept other dot of a named member: killed if D[x] >= v
     const uint32_t gl = gather32(ul, ml) & 63u, gr = gather32(ur, mr) & 63u;
-    const uint64_t okl = lr64(uX + k3Out + 8u * gl), okr = lr64(uX + k3Out + 8u * gr);
-    uint64_t bitsl = (bit_of(mdL, lane) && ((uint32_t)(okl >> 32) & bl)) ? lr64(dmt + 8u * gl) : 0ull;
-    uint64_t bitsr = (bit_of(mdR, lane) && (((uint32_t)okr & ~(uint32_t)(okr >> 32)) & br)) ? lr64(dmt + 8u * gr) : 0ull;
+    MT kpl, ukl, kpr, ukr;  // {keep, useK} of the dot's union slot
+    if (AW == 64) {
+      kpl = (MT)lr64(uX + Out + ME * gl);
+      ukl = (MT)lr64(uX + Out + ME * gl + 8u);
+      kpr = (MT)lr64(uX + Out + ME * gr);
+      ukr = (MT)lr64(uX + Out + ME * gr + 8u);
+    } else {
+      const uint64_t okl = lr64(uX + Out + 8u * gl), okr = lr64(uX + Out + 8u * gr);
+      kpl = (MT)(uint32_t)okl;
+      ukl = (MT)(uint32_t)(okl >> 32);
+      kpr = (MT)(uint32_t)okr;
+      ukr = (MT)(uint32_t)(okr >> 32);
+    }
+    uint64_t bitsl = (bit_of(mdL, lane) && (ukl & bl)) ? lr64(dmt + 8u * gl) : 0ull;
+    uint64_t bitsr = (bit_of(mdR, lane) && ((kpr & ~ukr) & br)) ? lr64(dmt + 8u * gr) : 0ull;
     // section addresses of both sides (scalars: no struct selected at run time)
     const uint32_t fdL = uL + DL.v.fdend, faL = uL + DL.v.fact, fcL = uL + DL.v.fctr;
     const uint32_t fdR = uR + DR.v.fdend, faR = uR + DR.v.fact, fcR = uR + DR.v.fctr;
@@ -1818,7 +1900,7 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
       const uint32_t e = lr32(fd + 4u * kk);
       uint32_t len = e - lo;
 #pragma unroll
-      for (int st = 0; st < 6; ++st) {
+      for (int st = 0; st < (AW == 64 ? 7 : 6); ++st) {  // a clock of <= AW entries
         const uint32_t half = len >> 1, mid = lo + half;
         const bool go = len != 0u && lr32(fa + 4u * mid) < x;
         lo = go ? mid + 1u : lo;
@@ -1828,22 +1910,22 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
     };
     bool kl2 = false, kr2 = false;
     while (bitsl | bitsr) {  // both dots' clocks in the same trips
-      const uint64_t dl = bitsl ? dget((uint32_t)__builtin_ctzll(bitsl), xl & 31u) : 0ull;
-      const uint64_t dr = bitsr ? dget((uint32_t)__builtin_ctzll(bitsr), xr & 31u) : 0ull;
+      const uint64_t dl = bitsl ? dget((uint32_t)__builtin_ctzll(bitsl), xl & (AW - 1u)) : 0ull;
+      const uint64_t dr = bitsr ? dget((uint32_t)__builtin_ctzll(bitsr), xr & (AW - 1u)) : 0ull;
       kl2 = kl2 || (bitsl && dl >= vl);
       kr2 = kr2 || (bitsr && dr >= vr);
       bitsl &= bitsl - 1u;
       bitsr &= bitsr - 1u;
     }
-    __hip_atomic_fetch_and((lds_u64*)(size_t)(kl2 ? uX + k3Out + 8u * gl : uX + TR + l8), kl2 ? ~(uint64_t)bl : ~0ull,
+    __hip_atomic_fetch_and((lds_u64*)(size_t)(kl2 ? uX + Out + ME * gl : uX + TRW + l8), kl2 ? ~(uint64_t)bl : ~0ull,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_and((lds_u64*)(size_t)(kr2 ? uX + k3Out + 8u * gr : uX + TR + l8), kr2 ? ~(uint64_t)br : ~0ull,
+    __hip_atomic_fetch_and((lds_u64*)(size_t)(kr2 ? uX + Out + ME * gr : uX + TRW + l8), kr2 ? ~(uint64_t)br : ~0ull,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     wave_sync();
-    keep = bit_of(mU, lane) ? (uint32_t)lr64(uX + k3Out + l8) : 0u;
+    keep = bit_of(mU, lane) ? (MT)lr64(uX + Out + ME * lane) : (MT)0;
     useK &= keep;
   }
-  const uint32_t c = __popc(keep);
+  const uint32_t c = (uint32_t)__builtin_popcountg(keep);
 
   // ---- output layout
   const uint64_t keepm = cmp32<kNE>(c, 0u);
@@ -1853,7 +1935,7 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
   // HD: the deferred union is counted first; its walk records the survivors
   // (in the equal / >= area, read above) for the writing walk to replay
   uint32_t nd = 0, ndd = 0, ndm = 0;
-  uint32_t* const dcache = HD ? (uint32_t*)gptr(uX + k3EqGe) : nullptr;
+  uint32_t* const dcache = HD ? (uint32_t*)gptr(uX + EqGe) : nullptr;
   const SideL WL{(lds_cu8*)(size_t)uL, DL.v}, WR{(lds_cu8*)(size_t)uR, DR.v};  // the walks read LDS directly
   if (HD && HABL != 2) deferred_pass_wave(WL, WR, A, lane, nd, ndd, ndm, nullptr, dcache);
   const uint32_t o_key = kHdrBytes + 8u * A, o_dctr = o_key + 8u * tot_mem, o_dact = o_dctr + 8u * tot_dot;
@@ -1866,7 +1948,8 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
     return 0u;
   }
   const uint32_t d0 = cincl - c;
-  if (OUT < 2) *(__attribute__((address_space(3))) u32x4*)(size_t)(uX + k3Out + 16u * lane) = u32x4{keep, useK, d0, 0u};
+  if (OUT < 2 && AW == 32)
+    *(__attribute__((address_space(3))) u32x4*)(size_t)(uX + Out + 16u * lane) = u32x4{(uint32_t)keep, (uint32_t)useK, d0, 0u};
   const uint32_t midx = mbcnt64(keepm);
   const uint64_t kk = lr64(bit_of(hasL, lane) ? uL + key + 8u * mi : uR + key + 8u * mj);
   const uint32_t xl2 = xl, xr2 = xr;
@@ -1875,17 +1958,36 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
   wave_sync();
   // every kept dot at its member's base + the rank of its actor in keep
   const uint32_t gl = gather32(ul, ml), gr = gather32(ur, mr);
-  u32x4 ol, orr;
-  if (OUT >= 2) {  // {keep, useK, base} of the dot's member straight from the union lane's registers
-    ol = u32x4{gather32(keep, gl), gather32(useK, gl), gather32(d0, gl), 0u};
-    orr = u32x4{gather32(keep, gr), gather32(useK, gr), gather32(d0, gr), 0u};
+  MT okl, oul, okr, our;  // {keep, useK} of the dot's member
+  uint32_t obl, obr;      // and its output dot base
+  if (OUT >= 2 || AW == 64) {  // straight from the union lane's registers
+    if (AW == 64) {
+      okl = (MT)gather64((uint64_t)keep, gl);
+      oul = (MT)gather64((uint64_t)useK, gl);
+      okr = (MT)gather64((uint64_t)keep, gr);
+      our = (MT)gather64((uint64_t)useK, gr);
+    } else {
+      okl = (MT)gather32((uint32_t)keep, gl);
+      oul = (MT)gather32((uint32_t)useK, gl);
+      okr = (MT)gather32((uint32_t)keep, gr);
+      our = (MT)gather32((uint32_t)useK, gr);
+    }
+    obl = gather32(d0, gl);
+    obr = gather32(d0, gr);
   } else {
-    ol = *(const __attribute__((address_space(3))) u32x4*)(size_t)(uX + k3Out + 16u * (gl & 63u));
-    orr = *(const __attribute__((address_space(3))) u32x4*)(size_t)(uX + k3Out + 16u * (gr & 63u));
+    const u32x4 ol = *(const __attribute__((address_space(3))) u32x4*)(size_t)(uX + Out + 16u * (gl & 63u));
+    const u32x4 orr = *(const __attribute__((address_space(3))) u32x4*)(size_t)(uX + Out + 16u * (gr & 63u));
+    okl = (MT)ol.x;
+    oul = (MT)ol.y;
+    obl = ol.z;
+    okr = (MT)orr.x;
+    our = (MT)orr.y;
+    obr = orr.z;
   }
-  const uint32_t il = ol.z + __popc(ol.x & (bl - 1u)), ir = orr.z + __popc(orr.x & (br - 1u));
-  const bool wl = bit_of(mdL, lane) && (ol.y & bl) != 0u;           // self dots that survive
-  const bool wr = bit_of(mdR, lane) && (orr.x & ~orr.y & br) != 0u;  // other dots kept, not under a self dot
+  const uint32_t il = obl + (uint32_t)__builtin_popcountg(okl & (bl - (MT)1));
+  const uint32_t ir = obr + (uint32_t)__builtin_popcountg(okr & (br - (MT)1));
+  const bool wl = bit_of(mdL, lane) && (oul & bl) != (MT)0;          // self dots that survive
+  const bool wr = bit_of(mdR, lane) && (okr & ~our & br) != (MT)0;  // other dots kept, not under a self dot
   if (OUT >= 2) {
     // the record is assembled in LDS over the (now dead) input stage, then
     // copied out with two 16-B stores per lane (sink-predicated): 2 vector
@@ -1893,7 +1995,7 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
     // occupied the texture-address unit (TA_BUSY 62-65 % of the kernel)
     fb = fb || size > 2u * 16u * kWave;  // larger outputs: the general kernel
     wave_sync();  // every read of the input stage (kk above) is done
-    const uint32_t tw = uX + TR + l8, tw4 = BK ? uX + TR + 4u * lane : tw;
+    const uint32_t tw = uX + TRW + l8, tw4 = BK ? uX + TRW + 4u * lane : tw;
     *(lds_u64*)(size_t)(bit_of(keepm, lane) ? uL + o_key + 8u * midx : tw) = kk;
     *(lds_u32*)(size_t)(bit_of(keepm, lane) ? uL + o_mdend + 4u * midx : tw4) = d0 + c;
     *(lds_u64*)(size_t)(lane < A ? uL + kHdrBytes + l8 : tw) = top;
@@ -1908,7 +2010,7 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
     if (BK) {
       if (lane < 2u) *(__attribute__((address_space(3))) u32x4*)(size_t)(uL + 16u * lane) = hv;
     } else {
-      *(__attribute__((address_space(3))) u32x4*)(size_t)(lane < 2u ? uL + 16u * lane : uX + TR + 16u * (lane & 31u)) =
+      *(__attribute__((address_space(3))) u32x4*)(size_t)(lane < 2u ? uL + 16u * lane : uX + TRW + 16u * (lane & 31u)) =
           hv;  // (16-B sink slots: lanes l and l + 32 share one, inside the 512-B sink)
     }
     if (OUT == 2) {  // OUT 3: the caller copies the record out
@@ -2819,6 +2921,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kern
   const uint64_t cs = (n_obj + n_waves * rounds - 1) / (n_waves * rounds);
   // the wave's store sink: after the list in the context's scratch (ctx.h)
   uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
+  [[maybe_unused]] uint32_t tacc = 0u;  // TCH: the touch loads' values (kept live, stored never in practice)
   Stamps st{};
   if (ABL == 9) st.last = stamp();
   for (uint64_t cbase = wave_id * cs; cbase < n_obj; cbase += n_waves * cs) {
@@ -2964,9 +3067,18 @@ __attribute__((noinline)) __device__ uint32_t hd_join(const uint8_t* Ls, const u
 // IO: 0 record prefetch and copy-out by global loads / stores with clamped
 // lane addresses; 1 prefetch through a buffer resource (prefetch_buf); 2 and
 // the copy-out too (copy_record_buf)
+// PO (MODE 3): packed output — a chunk's consecutive joined objects are
+// written back to back (each record right after the previous one's end, never
+// past its own self.off + other.off, so the capacity rule is unchanged): whole
+// 128-B lines instead of a partial line at both ends of every record, which
+// the memory side completes by read-modify-write (tools/probe/skel_probe.hip:
+// the record stream with a synthetic join, 1.08 -> 0.87 ms). An object after
+// one the pass did not join (listed for the general kernel at the chunk step,
+// or not valid) starts at its own self.off + other.off again; an object that
+// falls back inside the loop keeps its two inputs' bytes for the general kernel.
 template <int MINW, int MODE, int OUT = 2, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
           bool RT = true, uint32_t DYN = 0, uint32_t SF = 6, bool SPEC = false, uint32_t GMIN = 0, int IO = 0,
-          int HK = 0, bool PK = false, int BK = 0>
+          int HK = 0, bool PK = false, int BK = 0, bool PO = false, int TCH = 0, int AW = 32>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
@@ -2974,10 +3086,13 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
     int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
 #ifndef CRDT_DIAG
   // the product kernel: one pass (MODE 3), no timing-only ablation
-  static_assert(HABL == 0 && MODE == 3, "ablations and the two-pass modes exist in -DCRDT_DIAG builds only");
+  static_assert(HABL == 0 && MODE == 3 && PO, "ablations and the two-pass modes exist in -DCRDT_DIAG builds only");
 #endif
+  static_assert(!PO || MODE == 3, "packed output: the one-pass join");
   __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
-  __shared__ u32x4 scr_s[kWavesPerBlock][(MODE == 1 ? k3Scratch : kMask1Scratch) / 16];
+  static_assert(M3Lay<32>::Bytes == kMask1Scratch, "mask3's AW 32 scratch is the kernel's");
+  static_assert(AW == 32 || (MODE == 3 && HDD && M3HD), "AW 64: the one-pass product form");
+  __shared__ u32x4 scr_s[kWavesPerBlock][(MODE == 1 ? k3Scratch : M3Lay<AW>::Bytes) / 16];
   __shared__ u32x4 out_s[kWavesPerBlock][MODE == 3 && !HDD ? kFastStage / 16 : 1];  // assembled outputs (deferred objects)
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wave = uni(threadIdx.x / kWave);  // wave-uniform: LDS bases in SGPRs
@@ -2991,6 +3106,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
   const uint64_t rounds = (n_obj + n_waves * kWave - 1) / (n_waves * kWave);
   const uint64_t cs = (n_obj + n_waves * rounds - 1) / (n_waves * rounds);
   uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
+  [[maybe_unused]] uint32_t tacc = 0u;  // TCH: the touch loads' values (kept live, stored never in practice)
   uint64_t* const dlist = (uint64_t*)((uint8_t*)(list + kDefaultListCap) + kTrashBytes);  // deferred objects
   // MODE 2 reads the deferred list in chunks of 64 entries when it did not
   // overflow, else scans every object's flag
@@ -3046,7 +3162,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
       const bool placed = !ok || (nlo >= lo + hl0.x && nro >= ro + hr0.x);
       if (__ballot(!placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_EINVAL);
       ok = ok && placed;
-      const bool fits = ok && hl0.x <= kFastStage && hr0.x <= kFastStage && A <= 32u && hl0.z <= 64u &&
+      const bool fits = ok && hl0.x <= kFastStage && hr0.x <= kFastStage && A <= (uint32_t)AW && hl0.z <= 64u &&
                         hr0.z <= 64u && hl0.w <= 64u && hr0.w <= 64u;
       const bool hd = fits && (hl1.x | hr1.x) != 0u && hl1.x <= 32u && hr1.x <= 32u;
       fast = fits && (hl1.x | hr1.x) == 0u;
@@ -3111,8 +3227,12 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
     stage_all(sL, pl, lane);
     stage_all(sR, pr, lane);
     wave_sync();
+    uint64_t cur = 0;         // PO: where the next record goes if it follows the last one joined
+    uint32_t tnext = kWave;   // PO: the object that record would be (none yet in this chunk)
+    uint32_t tv = 0u;         // TCH: the last touch load's value (consumed one object later)
     for (;;) {
-      const uint64_t oo = HABL == 5 ? lane_of64(lo, t) : lane_of64(lo, t) + lane_of64(ro, t);
+      const uint64_t nat = HABL == 5 ? lane_of64(lo, t) : lane_of64(lo, t) + lane_of64(ro, t);
+      const uint64_t oo = PO && t == tnext ? (cur < nat ? cur : nat) : nat;
       const uint32_t td = dsel(t);
       const uint32_t m = lane_of(nm, td), d = lane_of(nd, td);
       // the next object, or this one again after the chunk's last (a constant load count)
@@ -3121,6 +3241,23 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
       const uint32_t nu = lane_of(n16, us);
       prefetch_io<IO>(pl, Lb + lane_of64(lo, us), nu & 0xFFFFu, lane);
       prefetch_io<IO>(pr, Rb + lane_of64(ro, us), nu >> 16, lane);
+      if (TCH) {
+        // TCH: one dword per 128-B line of the object after the next (lanes
+        // 0-15: its self record, 16-31: its other record; 32-63 repeat them),
+        // so that its record prefetch, one object later, finds the lines in
+        // the caches: the wave has two objects' bytes in flight for the price
+        // of one VGPR. The loaded value is consumed (folded into tacc) only
+        // when the next touch is issued, so no wait is placed on it sooner.
+        const uint64_t pend2 = pend ? pend & (pend - 1ull) : 0ull;
+        const uint32_t v = pend2 ? (uint32_t)__builtin_ctzll(pend2) : u;
+        const uint32_t nv = lane_of(n16, v);
+        const bool rs = (lane & 16u) != 0u;
+        const uint32_t last = 16u * (rs ? nv >> 16 : nv & 0xFFFFu) - 4u;
+        const uint32_t ob = 128u * (lane & 15u);
+        const uint8_t* const tb = rs ? Rb + lane_of64(ro, v) : Lb + lane_of64(lo, v);
+        tacc ^= tv;
+        tv = *(const uint32_t*)(tb + (ob < last ? ob : last));
+      }
       bool big = false;
       uint32_t r;
       if (MODE == 1) {
@@ -3150,7 +3287,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
         if ((defs >> td) & 1ull) {
           if (HDD) {
             if (M3HD)
-              r = mask3_object<0xFFFFFFFFu, 0, true, HABL, RT, HK, PK, BK ? 1 : 0>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
+              r = mask3_object<0xFFFFFFFFu, 0, true, HABL, RT, HK, PK, BK ? 1 : 0, AW>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
                                                      d & 0xFFFFu, m >> 16, d >> 16, lane, big);
             else
               r = mask_object<0xFFFFFFFFu, true, 0, DC>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo),
@@ -3161,7 +3298,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
           }
           src = lds_addr(out_s[wave]);
         } else {
-          r = mask3_object<0xFFFFFFFFu, 3, false, 0, RT, 0, PK, BK>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A,
+          r = mask3_object<0xFFFFFFFFu, 3, false, 0, RT, 0, PK, BK, AW>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A,
                                                          m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, sink);
           src = lds_addr(sL);
         }
@@ -3183,6 +3320,11 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
             if (e < list_cap) list[e] = cbase + t;
           }
         }
+        if (PO) {  // the next record's place: after this one (a fallback keeps both inputs' bytes)
+          const uint32_t nt = lane_of(n16, td);
+          cur = oo + 16ull * (fbu ? (nt & 0xFFFFu) + (nt >> 16) : uni(r));
+          tnext = t + 1u;
+        }
       } else {
         if (M3HD)
           r = mask3_object<0xFFFFFFFFu, 0, true>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
@@ -3203,7 +3345,9 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
       stage_used(sR, pr, nu >> 16, lane);
       wave_sync();
     }
+    if (TCH) tacc ^= tv;
   }
+  if (TCH && tacc == A + 0x9e3779b9u) *(uint32_t*)sink = tacc;  // (keeps the touches; a value no record word has here)
 #ifdef CRDT_DIAG
   if (HABL == 6 && lane == 0u && wave_id < 10922u) {  // timing only: the list's upper half holds the stamps
     list[32768u + 3u * wave_id] = ts0;
@@ -3257,6 +3401,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_dyn_
   const uint64_t ts0 = HABL == 6 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
   uint32_t n_joined = 0u, n_hd = 0u, n_chunk = 0u;                                  // (HABL 6: per-wave counts)
   uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
+  [[maybe_unused]] uint32_t tacc = 0u;  // TCH: the touch loads' values (kept live, stored never in practice)
   const uint64_t n_chunks = (n_obj + kDynG - 1) / kDynG;
   const uint32_t sec = lane >> 4, k16 = lane & 15u;  // raw-load lane roles
 
@@ -3445,6 +3590,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_v10_
   const uint64_t ts0 = HABL == 6 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
   uint32_t n_joined = 0u, n_hd = 0u, n_chunk = 0u;                                  // (HABL 6: per-wave counts)
   uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
+  [[maybe_unused]] uint32_t tacc = 0u;  // TCH: the touch loads' values (kept live, stored never in practice)
 
   // ---- guided schedule
   const uint64_t s_total = SF >= 8u ? n_obj : n_obj * SF / 8u;
@@ -4014,13 +4160,14 @@ namespace {
 // then the general kernel.
 template <int MINW, bool ONE = true, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
           bool RT = true, uint32_t DYN = 0, bool DK = false, uint32_t SF = 6, bool V10 = false, bool SPEC = false,
-          uint32_t GMIN = 0, int IO = 0, int HK = 0, bool PK = false, int BK = 0, bool NM = false>
+          uint32_t GMIN = 0, int IO = 0, int HK = 0, bool PK = false, int BK = 0, bool NM = false, bool PO = false,
+          int TCH = 0, int AW = 32>
 int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                        const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
                        uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
                        uint32_t list_cap, hipStream_t stream, int blocks_per_cu, JoinSeq* js) {
 #ifndef CRDT_DIAG
-  static_assert(HABL == 0 && ONE && !V10 && !DK, "the product launch: one pass, no timing-only ablation");
+  static_assert(HABL == 0 && ONE && !V10 && !DK && PO, "the product launch: one pass, no timing-only ablation");
 #endif
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -4034,7 +4181,8 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
   } else
 #endif
   if constexpr (ONE) {
-    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL, RT, DYN, SF, SPEC, GMIN, IO, HK, PK, BK>;
+    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL, RT, DYN, SF, SPEC, GMIN, IO, HK, PK, BK, PO,
+                                         TCH, AW>;
   } else {
 #ifdef CRDT_DIAG
     f1 = (const void*)orswot_join_kernel<MINW, 1>;
@@ -4042,7 +4190,7 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
 #endif
   }
   static std::atomic<int> occ_cache[2][10];  // per (pass, MINW; slot 9: the v9 kernel); HDD variants share one per MINW
-  constexpr int slot = DK || V10 ? 9 : MINW;
+  constexpr int slot = DK || V10 ? 9 : (AW == 64 ? 8 : MINW);
   int occ[2];
   const void* fs[2] = {f1, f2};
   const int passes = ONE ? 1 : 2;
@@ -4111,8 +4259,15 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // layout (BK), then the general kernel (measured best, tools/ab_bench.py;
   // DESIGN.md §4). Other variants exist in -DCRDT_DIAG builds only.
   (void)variant;
-  return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true>);
+  if (n_actors > 32u)  // dense top clocks of 33-64 actors: the same join with 64-bit actor masks, 5 waves/SIMD
+    return go(launch_join_passes<5, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true,
+                                 true, 0, 64>);
+  return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true,
+                               true>);
 #else
+  if (n_actors > 32u && (variant == 0 || variant == 270))
+    return go(launch_join_passes<5, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true,
+                                 true, 0, 64>);
   if (variant == 134) return go(launch_join_passes<6, true, true, true, true, 1>);  // timing only: no kill
   if (variant == 135) return go(launch_join_passes<6, true, true, true, true, 2>);  // timing only: no deferred block
   if (variant == 136) return go(launch_join_passes<6, true, true, true, true, 3>);  // timing only: join without HBM
@@ -4161,6 +4316,11 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   if (variant == 264) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1>);
   // r03: + NM (no memset before the join: alternating control-word sets, zeroed by the general kernel)
   if (variant == 265) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true>);
+  // r04: + PO (packed output: consecutive records back to back) — the product
+  if (variant == 270) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true, true>);
+  // r04: + TCH (a one-dword-per-line touch of the object after the next), with (271) and without (272) PO
+  if (variant == 271) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true, true, 1>);
+  if (variant == 272) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true, false, 1>);
 
   if (variant == 256) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 6>);
   if (variant == 257) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7>);

@@ -132,8 +132,12 @@ def test_config3_differential_200k(gpu, oracle):
     out = _gpu_merge(gpu, lb, lo, rb, ro, 16)
     ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, 16, threads=16)
     _compare(out, ob, oo, "config3 200k")
-    # output offsets are self.off + other.off
-    assert (out.off.cpu().numpy().view(np.uint64) == lo + ro).all()
+    # placement (include/crdts_hip.h): never past self.off + other.off, in
+    # object order without overlap, and packed back to back almost everywhere
+    o = out.off.cpu().numpy().view(np.uint64)
+    size = np.array([len(r) for r in out.records()], np.uint64)
+    assert (o <= lo + ro).all() and (o[1:] >= o[:-1] + size[:-1]).all()
+    assert (o[1:] == o[:-1] + size[:-1]).mean() > 0.9
 
 
 def test_config3_reverse_orientation(gpu, oracle):
@@ -460,3 +464,22 @@ def test_header_without_deferred_clocks_but_deferred_counts_rejected(gpu):
         assert e.value.code == CRDT_ENONCANON
     lb, lo = records.pack_batch([good] * 70)
     _gpu_merge(gpu, lb, lo, lb, lo, A)  # the context is clean again
+
+
+# ------------------------------------------------------------------ 33-64 dense actors
+@pytest.mark.parametrize("A,n", [(64, 100_000), (33, 30_000), (48, 30_000)])
+def test_dense_33_to_64_actors(gpu, oracle, A, n):
+    """Dense top clocks of 33-64 actors take the join kernel's 64-bit actor
+    mask form (mask3_object<AW 64>; the reference clock has no actor bound,
+    src/vclock.rs:54-57): config-3-shaped pairs over A actors, deferred-remove
+    objects included, byte-exact against the oracle (bench.py --n-actors 64
+    times the same form)."""
+    import crdts_hip
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(n, threads=16, seed=0xC0FFEE03 + A, params={"n_actors": A})
+    recs = records.unpack_batch(lb, lo)
+    assert sum(1 for r in recs[:2000] if records.decode(r)["deferred"]) > 20  # deferred removes present
+    assert max(a for r in recs[:2000] for a in records.decode(r)["clock"]) >= 32  # actors past the 32-bit masks
+    out = _gpu_merge(gpu, lb, lo, rb, ro, A)
+    ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, A, threads=16)
+    _compare(out, ob, oo, f"A={A}")
