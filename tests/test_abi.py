@@ -95,7 +95,8 @@ def test_product_has_only_the_product_join_instantiation():
     """The timing-only ablations (HABL != 0) and the two-pass join modes exist
     in the -DCRDT_DIAG build only: the product library's code objects hold
     exactly one orswot_join_kernel, MODE 3 with HABL 0 (static_asserts in
-    orswot_merge.hip keep it that way)."""
+    orswot_merge.hip keep it that way) — one per actor-mask width: the 32-bit
+    form at 6 waves/SIMD and the 64-bit form (dense clocks of 33-64 actors) at 5."""
     import crdts_hip
 
     blob = open(crdts_hip.LIB_PATH, "rb").read()
@@ -103,4 +104,6 @@ def test_product_has_only_the_product_join_instantiation():
     assert names, "no orswot_join_kernel in the product library"
     for minw, mode, out, hdd, dc, m3hd, habl in names:
         assert mode == b"3" and habl == b"0", names
-    assert len(names) == 1, names
+    assert sorted(n[0] for n in names) == [b"5", b"6"], names
+    widths = set(re.findall(rb"orswot_join_kernelI\S*?ELi0ELi(32|64)EEEv", blob))
+    assert widths == {b"32", b"64"}, widths
