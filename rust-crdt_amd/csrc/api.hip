@@ -268,7 +268,7 @@ int crdt_orswot_merge_ex(crdt_ctx* ctx, const crdt_orswot_batch* self, const crd
     return launch_orswot_merge_sparse(self->base, self->off, self->bytes, other->base, other->off, other->bytes,
                                       d_out_base, d_out_off, out_bytes, self->n_obj, n_actors, ctx->d_status,
                                       ctx->d_ctl, ctx->d_list, ctx->list_cap, S(stream),
-                                      ctx->variant >= 201 && ctx->variant <= 210 ? ctx->variant - 200 : 0,
+                                      ctx->variant >= 201 && ctx->variant <= 211 ? ctx->variant - 200 : 0,
                                       &ctx->join_seq);
   return launch_orswot_merge(self->base, self->off, self->bytes, other->base, other->off,
                              other->bytes, d_out_base, d_out_off, out_bytes, self->n_obj, n_actors,
@@ -526,10 +526,10 @@ int crdt_map_mvreg_merge(crdt_ctx* ctx, const crdt_map_mvreg_slab* self, const c
 
 int crdt_map_orswot_merge(crdt_ctx* ctx, const crdt_map_orswot_slab* self, const crdt_map_orswot_slab* other,
                           const crdt_map_orswot_slab* out, size_t n_obj, uint32_t n_actors, void* stream) {
-  if (!ctx || !self || !other || !out || n_actors == 0 || n_actors > 64) return CRDT_EINVAL;
+  if (!ctx || !self || !other || !out || n_actors == 0 || n_actors > 128) return CRDT_EINVAL;
   for (const crdt_map_orswot_slab* x : {self, other})
-    if (x->kcap == 0 || x->kcap > 32 || x->mcap == 0 || x->mcap > 32 || x->vdcap == 0 || x->vdcap > 16 ||
-        x->vscap == 0 || x->vscap > 16 || x->dcap == 0 || x->dcap > 32 || x->scap == 0 || x->scap > 32)
+    if (x->kcap == 0 || x->kcap > 4096 || x->mcap == 0 || x->mcap > 256 || x->vdcap == 0 || x->vdcap > 32 ||
+        x->vscap == 0 || x->vscap > 32 || x->dcap == 0 || x->dcap > 32 || x->scap == 0 || x->scap > 4096)
       return CRDT_EINVAL;
   if (out->kcap == 0 || out->mcap == 0 || out->vdcap == 0 || out->vscap == 0 || out->dcap == 0 || out->scap == 0)
     return CRDT_EINVAL;

@@ -15,8 +15,9 @@
 // deferred clocks is truncated by each in turn, in CLOCK ORDER (the reference
 // iterates a HashMap there; DESIGN.md §5e shows the order can matter).
 //
-// One wave per map pair; lane = actor slot (n_actors <= 64), so every VClock
-// operation on dense rows is one lane-parallel op plus a ballot. The nested
+// One wave per map pair; lane = actor slot, NS slots per lane (NS = 1 for
+// n_actors <= 64, 2 for <= 128: lane l holds actors l and l + 64), so every
+// VClock operation on dense rows is NS lane-parallel ops plus a ballot. The nested
 // set being built lives in an LDS workspace (member keys + member clock rows
 // + deferred clocks + their member sets), double-buffered for the set merge;
 // keys, members and deferred entries are walked by wave-uniform loops.
@@ -46,24 +47,83 @@ __device__ __forceinline__ uint64_t lane64(uint64_t v, uint32_t t) {
   return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), t) << 32) |
          (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, t);
 }
-// VClock::subtract (src/vclock.rs:236-242) on one slot
-__device__ __forceinline__ uint64_t vsub(uint64_t e, uint64_t c) { return c >= e ? 0ull : e; }
-__device__ __forceinline__ uint64_t vmax(uint64_t a, uint64_t b) { return a > b ? a : b; }
-__device__ __forceinline__ bool vany(uint64_t v) { return __ballot(v != 0ull) != 0ull; }
-// `d <= c` on PartialOrd (src/vclock.rs:59-71) for dense rows: every slot of d within c
-__device__ __forceinline__ bool vle(uint64_t d, uint64_t c) { return __ballot(d > c) == 0ull; }
-// CLOCK ORDER of two dense rows (lexicographic over their (actor, counter) pairs, a proper prefix first)
-__device__ int vorder(uint64_t p, uint64_t q, uint32_t lane) {
-  const uint64_t diff = __ballot(p != q);
-  if (!diff) return 0;
-  const uint32_t x = (uint32_t)__builtin_ctzll(diff);
-  const uint64_t px = lane64(p, x), qx = lane64(q, x);
-  if (px && qx) return px < qx ? -1 : 1;
-  if (!px) return __ballot(p != 0ull && lane > x) ? 1 : -1;
-  return __ballot(q != 0ull && lane > x) ? -1 : 1;
+// A dense clock row in registers: slot s of lane l is actor l + 64 s.
+template <int NS>
+struct Row {
+  uint64_t v[NS];
+};
+template <int NS>
+__device__ __forceinline__ Row<NS> zrow() {
+  Row<NS> r;
+  for (int k = 0; k < NS; ++k) r.v[k] = 0ull;
+  return r;
 }
-__device__ __forceinline__ uint64_t rowv(const uint64_t* base, uint64_t row, uint32_t A, uint32_t lane) {
-  return lane < A ? base[row * A + lane] : 0ull;
+// VClock::subtract (src/vclock.rs:236-242), slot by slot
+template <int NS>
+__device__ __forceinline__ Row<NS> vsub(Row<NS> e, Row<NS> c) {
+  for (int k = 0; k < NS; ++k) e.v[k] = c.v[k] >= e.v[k] ? 0ull : e.v[k];
+  return e;
+}
+template <int NS>
+__device__ __forceinline__ Row<NS> vmax(Row<NS> a, Row<NS> b) {
+  for (int k = 0; k < NS; ++k) a.v[k] = a.v[k] > b.v[k] ? a.v[k] : b.v[k];
+  return a;
+}
+template <int NS>
+__device__ __forceinline__ bool vany(Row<NS> v) {
+  bool a = false;
+  for (int k = 0; k < NS; ++k) a = a || v.v[k] != 0ull;
+  return __ballot(a) != 0ull;
+}
+// `d <= c` on PartialOrd (src/vclock.rs:59-71) for dense rows: every slot of d within c
+template <int NS>
+__device__ __forceinline__ bool vle(Row<NS> d, Row<NS> c) {
+  bool gt = false;
+  for (int k = 0; k < NS; ++k) gt = gt || d.v[k] > c.v[k];
+  return __ballot(gt) == 0ull;
+}
+// VClock::intersection (src/vclock.rs:219-228): the slots equal on both sides
+template <int NS>
+__device__ __forceinline__ Row<NS> vcommon(Row<NS> a, Row<NS> b) {
+  for (int k = 0; k < NS; ++k) a.v[k] = (a.v[k] == b.v[k] && a.v[k] != 0ull) ? a.v[k] : 0ull;
+  return a;
+}
+// CLOCK ORDER of two dense rows (lexicographic over their (actor, counter)
+// pairs, a proper prefix first): decided at the first actor where they differ
+template <int NS>
+__device__ int vorder(Row<NS> p, Row<NS> q, uint32_t lane) {
+  for (int k = 0; k < NS; ++k) {
+    const uint64_t diff = __ballot(p.v[k] != q.v[k]);
+    if (!diff) continue;
+    const uint32_t x = (uint32_t)__builtin_ctzll(diff);
+    const uint64_t px = lane64(p.v[k], x), qx = lane64(q.v[k], x);
+    if (px && qx) return px < qx ? -1 : 1;
+    // one side has no entry at actor 64k + x: the other's next entry decides
+    bool later = false;  // does the side WITHOUT x hold an actor above it?
+    for (int j = k; j < NS; ++j) {
+      const uint64_t w = !px ? p.v[j] : q.v[j];
+      later = later || (w != 0ull && (j > k || lane > x));
+    }
+    const bool any = __ballot(later) != 0ull;
+    return !px ? (any ? 1 : -1) : (any ? -1 : 1);
+  }
+  return 0;
+}
+// row `row` of a [.][A] array / a row at `base`
+template <int NS>
+__device__ __forceinline__ Row<NS> ldrow(const uint64_t* base, uint32_t A, uint32_t lane) {
+  Row<NS> r;
+  for (int k = 0; k < NS; ++k) r.v[k] = lane + 64u * k < A ? base[lane + 64u * k] : 0ull;
+  return r;
+}
+template <int NS>
+__device__ __forceinline__ Row<NS> rowv(const uint64_t* base, uint64_t row, uint32_t A, uint32_t lane) {
+  return ldrow<NS>(base + row * A, A, lane);
+}
+template <int NS>
+__device__ __forceinline__ void strow(uint64_t* base, Row<NS> r, uint32_t A, uint32_t lane) {
+  for (int k = 0; k < NS; ++k)
+    if (lane + 64u * k < A) base[lane + 64u * k] = r.v[k];
 }
 __device__ __forceinline__ bool set_has(const uint64_t* set, uint32_t n, uint64_t key, uint32_t lane) {
   bool f = false;
@@ -120,10 +180,11 @@ __device__ void ws_load(Ws& W, const crdt_map_orswot_slab& X, uint64_t ki, const
 // after the members flagged in mdead are dropped: every deferred clock is
 // subtracted from the members of its set (a member left empty is dropped),
 // and kept only if `clk` does not cover it. Then both lists are compacted.
-__device__ void ws_apply_deferred(Ws& W, uint64_t clk, uint32_t* mdead, uint32_t* ddead, const Caps& c,
+template <int NS>
+__device__ void ws_apply_deferred(Ws& W, Row<NS> clk, uint32_t* mdead, uint32_t* ddead, const Caps& c,
                                   uint32_t lane) {
   for (uint32_t d = 0; d < W.nd; ++d) {
-    const uint64_t D = lane < c.A ? W.dclk[d * c.A + lane] : 0ull;
+    const Row<NS> D = ldrow<NS>(W.dclk + d * c.A, c.A, lane);
     const uint32_t n = uni(W.dn[d]);
     for (uint32_t j = 0; j < n; ++j) {
       const uint64_t m = uni64(W.dset[d * c.SW + j]);
@@ -134,8 +195,8 @@ __device__ void ws_apply_deferred(Ws& W, uint64_t clk, uint32_t* mdead, uint32_t
         else hi = mid;
       }
       if (lo >= W.nm || uni64(W.key[lo]) != m || uni(mdead[lo])) continue;
-      const uint64_t r = lane < c.A ? vsub(W.row[lo * c.A + lane], D) : 0ull;
-      if (lane < c.A) W.row[lo * c.A + lane] = r;
+      const Row<NS> r = vsub(ldrow<NS>(W.row + lo * c.A, c.A, lane), D);
+      strow(W.row + lo * c.A, r, c.A, lane);
       const bool gone = !vany(r);
       mo_sync();
       if (gone && lane == 0u) mdead[lo] = 1u;
@@ -151,10 +212,10 @@ __device__ void ws_apply_deferred(Ws& W, uint64_t clk, uint32_t* mdead, uint32_t
     if (uni(mdead[j])) continue;
     if (k != j) {
       const uint64_t key = W.key[j];
-      const uint64_t r = lane < c.A ? W.row[j * c.A + lane] : 0ull;
+      const Row<NS> r = ldrow<NS>(W.row + j * c.A, c.A, lane);
       mo_sync();
       if (lane == 0u) W.key[k] = key;
-      if (lane < c.A) W.row[k * c.A + lane] = r;
+      strow(W.row + k * c.A, r, c.A, lane);
       mo_sync();
     }
     ++k;
@@ -164,11 +225,11 @@ __device__ void ws_apply_deferred(Ws& W, uint64_t clk, uint32_t* mdead, uint32_t
   for (uint32_t d = 0; d < W.nd; ++d) {
     if (uni(ddead[d])) continue;
     if (k != d) {
-      const uint64_t D = lane < c.A ? W.dclk[d * c.A + lane] : 0ull;
+      const Row<NS> D = ldrow<NS>(W.dclk + d * c.A, c.A, lane);
       const uint32_t n = uni(W.dn[d]);
       uint64_t s0 = lane < n ? W.dset[d * c.SW + lane] : 0ull;
       mo_sync();
-      if (lane < c.A) W.dclk[k * c.A + lane] = D;
+      strow(W.dclk + k * c.A, D, c.A, lane);
       if (lane == 0u) W.dn[k] = n;
       if (lane < n) W.dset[k * c.SW + lane] = s0;  // SW <= 64
       mo_sync();
@@ -183,18 +244,19 @@ __device__ void ws_apply_deferred(Ws& W, uint64_t clk, uint32_t* mdead, uint32_t
 
 // Orswot::merge (src/orswot.rs:87-157): Wn = Wc.merge(&other), other = key
 // slot ko of O. `sclk` (Wc's top clock) becomes the merged clock.
-__device__ void ws_merge(const Ws& Wc, Ws& Wn, uint64_t& sclk, const crdt_map_orswot_slab& O, uint64_t ko,
+template <int NS>
+__device__ void ws_merge(const Ws& Wc, Ws& Wn, Row<NS>& sclk, const crdt_map_orswot_slab& O, uint64_t ko,
                          uint32_t* mdead, uint32_t* ddead, const Caps& c, uint32_t lane) {
-  const uint64_t oclk = rowv(O.vclock, ko, c.A, lane);
+  const Row<NS> oclk = rowv<NS>(O.vclock, ko, c.A, lane);
   const uint32_t no = uni(O.vn_mem[ko]);
   uint32_t a = 0, b = 0, n = 0;
   while (a < Wc.nm || b < no) {
     const uint64_t ka = a < Wc.nm ? uni64(Wc.key[a]) : ~0ull;
     const uint64_t kb = b < no ? uni64(O.vmem[ko * O.mcap + b]) : ~0ull;
     const bool hs = a < Wc.nm && (b >= no || ka <= kb), ho = b < no && (a >= Wc.nm || kb <= ka);
-    const uint64_t r = hs && lane < c.A ? Wc.row[a * c.A + lane] : 0ull;
-    const uint64_t orow = ho ? rowv(O.vmclock, ko * O.mcap + b, c.A, lane) : 0ull;
-    uint64_t out;
+    const Row<NS> r = hs ? ldrow<NS>(Wc.row + a * c.A, c.A, lane) : zrow<NS>();
+    const Row<NS> orow = ho ? rowv<NS>(O.vmclock, ko * O.mcap + b, c.A, lane) : zrow<NS>();
+    Row<NS> out;
     bool keep;
     if (hs && !ho) {  // :94-104: dropped iff other has seen all of it
       out = r;
@@ -203,14 +265,14 @@ __device__ void ws_merge(const Ws& Wc, Ws& Wn, uint64_t& sclk, const crdt_map_or
       out = vsub(orow, sclk);
       keep = vany(out);
     } else {  // :105-128
-      const uint64_t common = (r == orow && r != 0ull) ? r : 0ull;  // VClock::intersection
-      const uint64_t e1 = vsub(vsub(r, common), oclk), e2 = vsub(vsub(orow, common), sclk);
+      const Row<NS> common = vcommon(r, orow);  // VClock::intersection
+      const Row<NS> e1 = vsub(vsub(r, common), oclk), e2 = vsub(vsub(orow, common), sclk);
       out = vmax(vmax(common, e1), e2);
       keep = vany(out);
     }
     if (keep) {
       if (lane == 0u) Wn.key[n] = hs ? ka : kb;
-      if (lane < c.A) Wn.row[n * c.A + lane] = out;
+      strow(Wn.row + n * c.A, out, c.A, lane);
       ++n;
     }
     if (hs) ++a;
@@ -221,13 +283,13 @@ __device__ void ws_merge(const Ws& Wc, Ws& Wn, uint64_t& sclk, const crdt_map_or
   const uint32_t od = uni(O.vn_def[ko]);
   uint32_t p = 0, q = 0, nd = 0;
   while (p < Wc.nd || q < od) {
-    const uint64_t dp = p < Wc.nd && lane < c.A ? Wc.dclk[p * c.A + lane] : 0ull;
-    const uint64_t dq = q < od ? rowv(O.vdclock, ko * O.vdcap + q, c.A, lane) : 0ull;
+    const Row<NS> dp = p < Wc.nd ? ldrow<NS>(Wc.dclk + p * c.A, c.A, lane) : zrow<NS>();
+    const Row<NS> dq = q < od ? rowv<NS>(O.vdclock, ko * O.vdcap + q, c.A, lane) : zrow<NS>();
     int ord;
     if (p >= Wc.nd) ord = 1;
     else if (q >= od) ord = -1;
     else ord = vorder(dp, dq, lane);
-    if (lane < c.A) Wn.dclk[nd * c.A + lane] = ord <= 0 ? dp : dq;
+    strow(Wn.dclk + nd * c.A, ord <= 0 ? dp : dq, c.A, lane);
     if (lane == 0u) {  // sorted union of the member sets
       const uint64_t* xs = ord <= 0 ? Wc.dset + p * c.SW : nullptr;
       const uint32_t nx = ord <= 0 ? Wc.dn[p] : 0u;
@@ -254,12 +316,13 @@ __device__ void ws_merge(const Ws& Wc, Ws& Wn, uint64_t& sclk, const crdt_map_or
 }
 
 // Orswot::truncate (src/orswot.rs:159-172) of W (top clock `clk`) by `t`.
-__device__ void ws_truncate(Ws& W, uint64_t& clk, uint64_t t, uint32_t* mdead, uint32_t* ddead, const Caps& c,
+template <int NS>
+__device__ void ws_truncate(Ws& W, Row<NS>& clk, Row<NS> t, uint32_t* mdead, uint32_t* ddead, const Caps& c,
                             uint32_t lane) {
   // merge with an empty set whose clock is t: members t covers are dropped
   // (:94-104); it has no entries or deferred removes; the clocks merge
   for (uint32_t j = 0; j < W.nm; ++j) {
-    const bool covered = vle(lane < c.A ? W.row[j * c.A + lane] : 0ull, t);
+    const bool covered = vle(ldrow<NS>(W.row + j * c.A, c.A, lane), t);
     if (covered && lane == 0u) mdead[j] = 1u;
   }
   clk = vmax(clk, t);
@@ -267,18 +330,18 @@ __device__ void ws_truncate(Ws& W, uint64_t& clk, uint64_t t, uint32_t* mdead, u
   ws_apply_deferred(W, clk, mdead, ddead, c, lane);
   // forget t from the top clock and every member clock (an emptied member stays)
   clk = vsub(clk, t);
-  if (lane < c.A)
-    for (uint32_t j = 0; j < W.nm; ++j) W.row[j * c.A + lane] = vsub(W.row[j * c.A + lane], t);
+  for (uint32_t j = 0; j < W.nm; ++j) strow(W.row + j * c.A, vsub(ldrow<NS>(W.row + j * c.A, c.A, lane), t), c.A, lane);
   mo_sync();
 }
 
 // Write W (top clock clk) into key slot kr of R; false if a capacity is exceeded.
-__device__ bool ws_store(const Ws& W, uint64_t clk, const crdt_map_orswot_slab& R, uint64_t kr, const Caps& c,
+template <int NS>
+__device__ bool ws_store(const Ws& W, Row<NS> clk, const crdt_map_orswot_slab& R, uint64_t kr, const Caps& c,
                          uint32_t lane) {
   bool fits = W.nm <= R.mcap && W.nd <= R.vdcap;
   for (uint32_t d = 0; d < W.nd; ++d) fits = fits && uni(W.dn[d]) <= R.vscap;
   if (!fits) return false;
-  if (lane < c.A) R.vclock[kr * c.A + lane] = clk;
+  strow(R.vclock + kr * c.A, clk, c.A, lane);
   if (lane == 0u) { R.vn_mem[kr] = W.nm; R.vn_def[kr] = W.nd; }
   const uint32_t nm = W.nm, nmA = W.nm * c.A, ndA = W.nd * c.A, nd = W.nd, vs = R.vscap, SW = c.SW;
   const uint64_t* key = W.key;
@@ -297,6 +360,7 @@ __device__ bool ws_store(const Ws& W, uint64_t clk, const crdt_map_orswot_slab& 
   return true;
 }
 
+template <int NS>
 __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_slab S, crdt_map_orswot_slab O,
                                                                 crdt_map_orswot_slab R, uint64_t n_obj, uint32_t A,
                                                                 int* __restrict__ status, uint32_t* __restrict__ ctl) {
@@ -324,8 +388,8 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
   mo_sync();
   BlockTickets<4> sched(n_obj, ctl + 3, lane);  // (sched.h)
   for (uint64_t i = sched.first(); i < n_obj; i = sched.next(i)) {
-    const uint64_t cS = rowv(S.clock, i, A, lane), cO = rowv(O.clock, i, A, lane);
-    const uint64_t cM = vmax(cS, cO);  // VClock::merge
+    const Row<NS> cS = rowv<NS>(S.clock, i, A, lane), cO = rowv<NS>(O.clock, i, A, lane);
+    const Row<NS> cM = vmax(cS, cO);  // VClock::merge
     const uint32_t nS = uni(S.n_keys[i]), nO = uni(O.n_keys[i]);
     const uint32_t dS = uni(S.n_def[i]), dO = uni(O.n_def[i]);
     if (nS > S.kcap || nO > O.kcap || dS > S.dcap || dO > O.dcap) {
@@ -356,11 +420,11 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
     {
       uint32_t a = 0, b = 0;
       while (a < dS || b < dO) {
-        if (b < dO && vle(rowv(O.dclock, i * O.dcap + b, A, lane), cS)) { ++b; continue; }
+        if (b < dO && vle(rowv<NS>(O.dclock, i * O.dcap + b, A, lane), cS)) { ++b; continue; }
         int o;
         if (a >= dS) o = 1;
         else if (b >= dO) o = -1;
-        else o = vorder(rowv(S.dclock, i * S.dcap + a, A, lane), rowv(O.dclock, i * O.dcap + b, A, lane), lane);
+        else o = vorder(rowv<NS>(S.dclock, i * S.dcap + a, A, lane), rowv<NS>(O.dclock, i * O.dcap + b, A, lane), lane);
         if (lane == 0u) comb[nc] = (o <= 0 ? a + 1u : 0u) | ((o >= 0 ? b + 1u : 0u) << 8);
         ++nc;
         if (o <= 0) ++a;
@@ -368,9 +432,9 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
       }
     }
     mo_sync();
-    auto comb_clock = [&](uint32_t e) -> uint64_t {
+    auto comb_clock = [&](uint32_t e) -> Row<NS> {
       const uint32_t sa = e & 255u, sb = e >> 8;
-      return sa ? rowv(S.dclock, i * S.dcap + sa - 1u, A, lane) : rowv(O.dclock, i * O.dcap + sb - 1u, A, lane);
+      return sa ? rowv<NS>(S.dclock, i * S.dcap + sa - 1u, A, lane) : rowv<NS>(O.dclock, i * O.dcap + sb - 1u, A, lane);
     };
     auto comb_names = [&](uint32_t e, uint64_t key) -> bool {
       const uint32_t sa = e & 255u, sb = e >> 8;
@@ -394,8 +458,9 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
       const bool hs = a < nS && (b >= nO || ka <= kb), ho = b < nO && (a >= nS || kb <= ka);
       const uint64_t key = hs ? ka : kb;
       const uint64_t ia = i * S.kcap + a, ib = i * O.kcap + b;
-      const uint64_t eS = hs ? rowv(S.eclock, ia, A, lane) : 0ull, eO = ho ? rowv(O.eclock, ib, A, lane) : 0ull;
-      uint64_t ec, del;
+      const Row<NS> eS = hs ? rowv<NS>(S.eclock, ia, A, lane) : zrow<NS>();
+      const Row<NS> eO = ho ? rowv<NS>(O.eclock, ib, A, lane) : zrow<NS>();
+      Row<NS> ec, del;
       if (hs && !ho) {  // other has not seen it, or saw it and dropped it
         ec = vsub(eS, cO);
         del = vsub(cO, ec);
@@ -403,8 +468,8 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
         ec = vsub(eO, cS);
         del = vsub(cS, ec);
       } else {
-        const uint64_t common = (eS == eO && eS != 0ull) ? eS : 0ull;  // VClock::intersection
-        const uint64_t e1 = vsub(vsub(eS, common), cO), e2 = vsub(vsub(eO, common), cS);
+        const Row<NS> common = vcommon(eS, eO);  // VClock::intersection
+        const Row<NS> e1 = vsub(vsub(eS, common), cO), e2 = vsub(vsub(eO, common), cS);
         ec = vmax(vmax(common, e1), e2);
         del = vsub(vmax(e1, e2), ec);
       }
@@ -422,11 +487,11 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
       }
       if (keep) {
         // the nested set: self's (merged with other's when both have the key) ...
-        uint64_t vclk;
+        Row<NS> vclk;
         Ws Wk;
         if (hs) {
           ws_load(W0, S, ia, c, lane);
-          vclk = rowv(S.vclock, ia, A, lane);
+          vclk = rowv<NS>(S.vclock, ia, A, lane);
           if (ho) {
             ws_merge(W0, W1, vclk, O, ib, mdead, ddead, c, lane);
             Wk = W1;
@@ -435,7 +500,7 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
           }
         } else {
           ws_load(W0, O, ib, c, lane);
-          vclk = rowv(O.vclock, ib, A, lane);
+          vclk = rowv<NS>(O.vclock, ib, A, lane);
           Wk = W0;
         }
         // ... truncated by the removers' clock (Map::merge), then by each deferred
@@ -446,7 +511,7 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
         const uint64_t ir = i * R.kcap + nk;
         if (ws_store(Wk, vclk, R, ir, c, lane)) {
           if (lane == 0u) R.keys[ir] = key;
-          if (lane < A) R.eclock[ir * A + lane] = ec;
+          strow(R.eclock + ir * A, ec, A, lane);
           ++nk;
         } else {
           over = true;
@@ -457,17 +522,17 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
       if (ho) ++b;
     }
     if (lane == 0u) R.n_keys[i] = nk;
-    if (lane < A) R.clock[i * A + lane] = cM;
+    strow(R.clock + i * A, cM, A, lane);
     // ---- map deferred kept: the combined clocks the merged clock does not cover, sets united
     uint32_t nd = 0;
     for (uint32_t k = 0; k < nc; ++k) {
       const uint32_t e = comb[k];
       const uint32_t sa = e & 255u, sb = e >> 8;
-      const uint64_t D = comb_clock(e);
+      const Row<NS> D = comb_clock(e);
       if (vle(D, cM)) continue;
       if (nd >= R.dcap) { over = true; break; }
       const uint64_t dr = i * R.dcap + nd;
-      if (lane < A) R.dclock[dr * A + lane] = D;
+      strow(R.dclock + dr * A, D, A, lane);
       uint32_t cnt = 0;
       if (lane == 0u) {  // sorted union of the two key sets
         const uint64_t* xs = sa ? S.dset + (i * S.dcap + sa - 1u) * S.scap : nullptr;
@@ -512,7 +577,12 @@ int launch_map_orswot_merge(const crdt_map_orswot_slab& S, const crdt_map_orswot
   const uint64_t cap = (uint64_t)cus * 16u;
   const uint32_t blocks = (uint32_t)(n_obj < cap ? n_obj : cap);
   if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;  // ctl[3]: tickets
-  hipLaunchKernelGGL(map_orswot_merge_kernel, dim3(blocks), dim3(kMoW), lds, stream, S, O, R, n_obj, A, status, ctl);
+  if (A > 64u)
+    hipLaunchKernelGGL(map_orswot_merge_kernel<2>, dim3(blocks), dim3(kMoW), lds, stream, S, O, R, n_obj, A, status,
+                       ctl);
+  else
+    hipLaunchKernelGGL(map_orswot_merge_kernel<1>, dim3(blocks), dim3(kMoW), lds, stream, S, O, R, n_obj, A, status,
+                       ctl);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 

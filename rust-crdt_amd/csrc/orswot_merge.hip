@@ -2319,7 +2319,12 @@ __device__ __forceinline__ uint32_t rank32(const uint8_t* b, uint32_t off, uint3
   return base;
 }
 
-template <bool HD, int ABL = 0>
+// ASM (objects without deferred removes, Ls the start of a pair stage that
+// can hold the output: the sparse mask kernel's): the output record is
+// assembled over the pair stage once every read of it is done and copied out
+// with 16-B stores, instead of scattered 4- / 8-B stores to HBM (as mask3's
+// OUT 2 does for the dense join)
+template <bool HD, int ABL = 0, bool ASM = false>
 __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* X, uint8_t* O,
                                                        uint32_t A, uint32_t ncL, uint32_t nL, uint32_t dL,
                                                        uint32_t ncR, uint32_t nR, uint32_t dR, uint32_t lane,
@@ -2532,15 +2537,33 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   const uint32_t size = OL.size;
   const uint32_t d0 = cincl - c;
   if (ABL == 9) mark<ABL>(*st, 6);
-  wave_sync();
-  *(uint64_t*)(X + kSpOut + 32u * lane) = hu ? keep : 0ull;
-  *(uint64_t*)(X + kSpOut + 32u * lane + 8u) = hu ? useK : 0ull;
-  *(uint32_t*)(X + kSpOut + 32u * lane + 16u) = d0;
-  if (c != 0u) {
-    const uint32_t midx = mbcnt64(keepm);
-    const uint64_t kk = (ty & kSelf) ? ld64(Ls, keyL + 8u * mi) : ld64(Rs, keyR + 8u * mj);
-    *(uint64_t*)(O + OL.o_key + 8u * midx) = kk;
-    *(uint32_t*)(O + OL.o_mdend + 4u * midx) = d0 + c;
+  static_assert(!(ASM && HD), "ASM: objects without deferred removes (the deferred walk reads the stages)");
+  uint8_t* const O_ = O;
+  if (ASM) {
+    // the last read of the pair stage (the kept members' keys; the dots are
+    // in registers), then the record is written over the stage
+    const uint64_t kk = c != 0u ? ((ty & kSelf) ? ld64(Ls, keyL + 8u * mi) : ld64(Rs, keyR + 8u * mj)) : 0ull;
+    wave_sync();
+    O = const_cast<uint8_t*>(Ls);
+    *(uint64_t*)(X + kSpOut + 32u * lane) = hu ? keep : 0ull;
+    *(uint64_t*)(X + kSpOut + 32u * lane + 8u) = hu ? useK : 0ull;
+    *(uint32_t*)(X + kSpOut + 32u * lane + 16u) = d0;
+    if (c != 0u) {
+      const uint32_t midx = mbcnt64(keepm);
+      *(uint64_t*)(O + OL.o_key + 8u * midx) = kk;
+      *(uint32_t*)(O + OL.o_mdend + 4u * midx) = d0 + c;
+    }
+  } else {
+    wave_sync();
+    *(uint64_t*)(X + kSpOut + 32u * lane) = hu ? keep : 0ull;
+    *(uint64_t*)(X + kSpOut + 32u * lane + 8u) = hu ? useK : 0ull;
+    *(uint32_t*)(X + kSpOut + 32u * lane + 16u) = d0;
+    if (c != 0u) {
+      const uint32_t midx = mbcnt64(keepm);
+      const uint64_t kk = (ty & kSelf) ? ld64(Ls, keyL + 8u * mi) : ld64(Rs, keyR + 8u * mj);
+      *(uint64_t*)(O + OL.o_key + 8u * midx) = kk;
+      *(uint32_t*)(O + OL.o_mdend + 4u * midx) = d0 + c;
+    }
   }
   if (lane < Uc) {  // top clock: the union list, pointwise max (src/orswot.rs:153)
     const uint64_t a = *(const uint64_t*)(X + kSpUcL + 8u * lane), b = *(const uint64_t*)(X + kSpUcR + 8u * lane);
@@ -2591,6 +2614,10 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     u32x4* h = (u32x4*)O;
     h[0] = u32x4{size, Uc, tot_mem, tot_dot};
     h[1] = u32x4{nd, ndd, ndm, kSparseClock};
+  }
+  if (ASM) {  // the assembled record out of the stage: 16-B coalesced non-temporal stores
+    wave_sync();
+    for (uint32_t k = lane; k < size / 16u; k += kWave) __builtin_nontemporal_store(((const u32x4*)O)[k], (u32x4*)O_ + k);
   }
   if (ABL == 9) mark<ABL>(*st, 7);
   return size / 16u;
@@ -3970,7 +3997,7 @@ __device__ __forceinline__ void stage_pair(u32x4* dst, const u32x4 (&r)[kSpPer],
   for (uint32_t k = 0; k < kSpPer; ++k) dst[lane + k * kWave] = r[k];
 }
 
-template <int MINW, int ABL = 0, uint32_t DYN = 0, uint32_t SF = 5>  // ABL 9: phase stamps into the list buffer (no general path)
+template <int MINW, int ABL = 0, uint32_t DYN = 0, uint32_t SF = 5, bool SASM = false>  // ABL 9: phase stamps into the list buffer (no general path)
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_mask_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
@@ -4055,7 +4082,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
         r = sparse_mask_object<true, ABL>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu, d & 0xFFFFu, c >> 16,
                                           m >> 16, d >> 16, lane, &st);
       else
-        r = sparse_mask_object<false, ABL>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu, d & 0xFFFFu, c >> 16,
+        r = sparse_mask_object<false, ABL, SASM>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu, d & 0xFFFFu, c >> 16,
                                            m >> 16, d >> 16, lane, &st);
       if (ABL != 9 && r == kLeanFallback && lane == 0u) {  // union clock / members > 64 or a foreign dot actor
         Ooff[cbase + t] |= kPending;
@@ -4459,6 +4486,7 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
                    : sparse_variant == 8 ? (const void*)orswot_sparse_mask_kernel<3, 0, 32, 5>
                    : sparse_variant == 9 ? (const void*)orswot_sparse_mask_kernel<3, 0, 12, 5>
                    : sparse_variant == 10 ? (const void*)orswot_sparse_mask_kernel<3>  // r02e: static split
+                   : sparse_variant == 11 ? (const void*)orswot_sparse_mask_kernel<3, 0, 16, 5, true>  // r04: + SASM
                                         : (const void*)orswot_sparse_mask_kernel<3, 0, 16, 5>;
 #else
   sparse_variant = 0;

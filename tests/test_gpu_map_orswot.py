@@ -138,3 +138,24 @@ def test_map_orswot_errors(gpu, oracle):
         gpu.map_orswot_merge(bad.to("cuda"), R.to("cuda"), A)
     assert e.value.code == crdts_hip.CRDT_ENONCANON
     gpu.status()  # the context is usable again after the latched error
+
+
+def test_map_orswot_200_keys_100_actors(gpu, oracle):
+    """Maps past the round-3 slab limits (32 keys, 64 actors): ~200 keys per
+    map over 100 actors (the kernel's two-slots-per-lane rows: lane l holds
+    actors l and l + 64), nested and map-level deferred removes whose clocks
+    name actor 99, both orientations, slab-row exact against the oracle
+    (src/map.rs:192-269)."""
+    import crdts_hip
+
+    A100 = 100
+    caps = dict(kcap=256, mcap=8, vdcap=8, vscap=8, dcap=32, scap=64)
+    L, R = oracle.map_orswot_generate(0x200A, 48, A100, keys=400, members=6, ops=450, pct_future=20, caps=caps)
+    assert (L.a["n_keys"] >= 200).sum() > 10 and L.a["clock"][:, 64:].any()
+    assert L.a["vn_def"].sum() > 20 and L.a["n_def"].sum() > 10
+    for S, O in ((L, R), (R, L)):
+        exp = oracle.map_orswot_merge(S, O, A100).canonical()
+        got = gpu.map_orswot_merge(S.to("cuda"), O.to("cuda"), A100).canonical()
+        for f in exp.a:
+            bad = np.nonzero((np.asarray(got.a[f]) != np.asarray(exp.a[f])).reshape(S.n, -1).any(axis=1))[0]
+            assert bad.size == 0, f"{f}: {bad.size} objects differ, first {bad[:5].tolist()}"
