@@ -930,207 +930,6 @@ __device__ __forceinline__ uint32_t fast_object(const uint8_t* Ls, const uint8_t
 // Returned by a fast join when the object is outside its limits.
 constexpr uint32_t kLeanFallback = 0xFFFFFFFFu;
 
-#ifdef CRDT_DIAG
-// ======================================================================
-// (Diagnostic build only, -DCRDT_DIAG: earlier designs kept for A/B timing
-// by tools/ab_bench.py; the product library does not contain them.)
-// Lean path (v5): objects without deferred removes whose union has at most
-// 64 members and nL + nR <= 128 — ~93 % of config 3. Same rules as
-// fast_object / merge_object, restructured for VALU economy:
-//  1. merge path over the diagonal 2*lane only; the lane then settles union
-//     positions 2*lane and 2*lane+1 with one extra compare (no second
-//     64-position round for nL + nR > 64);
-//  2. the (up to 2) union members per lane are compacted through LDS so that
-//     lane u owns union member u (twins of keys present on both sides vanish);
-//  3. one dot-parallel pass precomputes, for every dot, whether it is above
-//     the OTHER side's pre-merge top clock (L[x] > Rc[x], R[x] > Lc[x]) and
-//     keeps it in bit 31 of the staged actor id — the join loop then reads
-//     no top clock at all;
-//  4. the per-member join loop (src/orswot.rs:94-138) is branch-free per
-//     step and captures the first two output dots in registers.
-// Returns the output size in 16-B pieces, or kLeanFallback when the union
-// has more than 64 members (the caller then runs fast_object on the
-// untouched stage).
-// ======================================================================
-constexpr uint32_t kFlag = 0x80000000u;
-
-template <bool WRITE>
-__device__ __forceinline__ uint32_t lean_join(const uint8_t* Ls, const uint8_t* Rs, uint32_t actL, uint32_t ctrL,
-                                              uint32_t actR, uint32_t ctrR, uint32_t a, uint32_t ae, uint32_t b,
-                                              uint32_t be, bool self_only, uint32_t& x0, uint64_t& v0, uint32_t& x1,
-                                              uint64_t& v1, uint32_t* oact, uint64_t* octr, uint32_t d0) {
-  uint32_t c = 0;
-  bool any = false;
-  while (a < ae || b < be) {
-    const uint32_t xa2 = ld32(Ls, actL + 4u * a), xb2 = ld32(Rs, actR + 4u * b);
-    const uint64_t va = ld64(Ls, ctrL + 8u * a), vb = ld64(Rs, ctrR + 8u * b);
-    const uint32_t xa = a < ae ? (xa2 & ~kFlag) : 0xFFFFFFFFu;
-    const uint32_t xb = b < be ? (xb2 & ~kFlag) : 0xFFFFFFFFu;
-    const bool ta = xa <= xb, tb = xb <= xa;
-    const bool fa = (int32_t)xa2 < 0, fb = (int32_t)xb2 < 0;
-    // both present and equal: common dot (:109); else L[x] survives iff
-    // > Rc[x] (self-only: the whole run, :98-103), R[x] iff > Lc[x]; max.
-    const bool lp = ta && (self_only || fa), rp = tb && fb;
-    const bool useA = (ta && tb && va == vb) || (lp && (!rp || va >= vb));
-    const bool keep = useA || rp;
-    const uint64_t v = useA ? va : vb;
-    const uint32_t x = ta ? xa : xb;
-    any = any || (ta && fa);
-    if (WRITE) {
-      if (keep) {
-        oact[d0 + c] = x;
-        octr[d0 + c] = v;
-      }
-    } else {
-      const bool first = keep && c == 0u, second = keep && c == 1u;
-      x0 = first ? x : x0;
-      v0 = first ? v : v0;
-      x1 = second ? x : x1;
-      v1 = second ? v : v1;
-    }
-    c += keep ? 1u : 0u;
-    a += ta ? 1u : 0u;
-    b += tb ? 1u : 0u;
-  }
-  return (self_only && !any) ? 0u : c;  // self-only entry dropped as a whole (:98-100)
-}
-
-// Marks bit 31 of every staged actor id of side S whose dot is above the
-// other side's top clock T (absent or out-of-range actor: 0).
-__device__ __forceinline__ void lean_flags(uint8_t* S, const uint8_t* T, uint32_t act, uint32_t ctr, uint32_t nd,
-                                           uint32_t A, uint32_t lane) {
-  for (uint32_t d = lane; d < nd; d += kWave) {
-    const uint32_t x = ld32(S, act + 4u * d);
-    const uint64_t v = ld64(S, ctr + 8u * d);
-    const uint64_t t = ld64(T, kHdrBytes + 8u * (x < A ? x : 0u));
-    const bool up = v > (x < A ? t : 0ull);
-    *(uint32_t*)(S + act + 4u * d) = x | (up ? kFlag : 0u);
-  }
-}
-
-// LABL (timing-only ablations, invalid output): 1 = stop after the merge
-// path + compaction, 2 = + dot flags, 3 = + counting join; 0 = real.
-template <uint32_t OUTCAP, int LABL = 0>
-__device__ __forceinline__ uint32_t lean_object(uint8_t* Ls, uint8_t* Rs, u32x4* Os, uint32_t A, uint32_t nL,
-                                                uint32_t dL, uint32_t nR, uint32_t dR, uint32_t lane, bool& big) {
-  big = false;
-  const uint32_t key = kHdrBytes + 8u * A;  // key section, both sides
-  const uint32_t ctrL = key + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
-  const uint32_t ctrR = key + 8u * nR, actR = ctrR + 8u * dR, endR = actR + 4u * dR;
-  const uint32_t P = nL + nR;
-  const uint32_t mn = nL < nR ? nL : nR;
-  const uint32_t top = mn ? 1u << (31u - __builtin_clz(mn)) : 0u;
-
-  // ---- 1. merge path on diagonal p = 2*lane (self first on ties)
-  const uint32_t p = 2u * lane < P ? 2u * lane : P;
-  const uint32_t lo = p > nR ? p - nR : 0u, hi = p < nL ? p : nL;
-  uint32_t i = lo;
-  for (uint32_t step = top; step != 0u; step >>= 1) {
-    const uint32_t cand = i + step;
-    const uint64_t kl = ld64(Ls, key + 8u * cand - 8u), kr = ld64(Rs, key + 8u * (p - cand));
-    i = (cand <= hi && kl <= kr) ? cand : i;
-  }
-  const uint32_t j = p - i;
-  const uint64_t kLm = ld64(Ls, key + 8u * i - 8u), kL0 = ld64(Ls, key + 8u * i), kL1 = ld64(Ls, key + 8u * i + 8u);
-  const uint64_t kR0 = ld64(Rs, key + 8u * j), kR1 = ld64(Rs, key + 8u * j + 8u);
-  // position p
-  const bool hl0 = i < nL, hr0 = j < nR;
-  const bool tl0 = hl0 && (!hr0 || kL0 <= kR0);
-  const uint32_t ty0 = tl0 ? ((hr0 && kL0 == kR0) ? kBoth : kSelf) : ((i > 0u && kLm == kR0) ? kNone : kOther);
-  // position p + 1
-  const uint32_t i1 = tl0 ? i + 1u : i, j1 = tl0 ? j : j + 1u;
-  const uint64_t kLa = tl0 ? kL1 : kL0, kLb = tl0 ? kL0 : kLm, kRa = tl0 ? kR0 : kR1;
-  const bool hl1 = i1 < nL, hr1 = j1 < nR;
-  const bool tl1 = hl1 && (!hr1 || kLa <= kRa);
-  const uint32_t ty1 = tl1 ? ((hr1 && kLa == kRa) ? kBoth : kSelf) : ((i1 > 0u && kLb == kRa) ? kNone : kOther);
-  const bool u0 = p < P && ty0 != kNone, u1 = p + 1u < P && ty1 != kNone;
-
-  // ---- 2. compact union members: lane u <- union member u
-  const uint32_t nu = (u0 ? 1u : 0u) + (u1 ? 1u : 0u);
-  const uint32_t incl = scan_incl(nu);
-  const uint32_t U = lane_of(incl, kWave - 1);
-  if (U > (uint32_t)kWave) return kLeanFallback;
-  uint32_t* desc = (uint32_t*)Os;
-  wave_sync();  // the copy-out that last read this stage is done with it
-  if (u0) desc[incl - nu] = (ty0 << 30) | (i << 15) | j;
-  if (u1) desc[incl - 1u] = (ty1 << 30) | (i1 << 15) | j1;
-  if (LABL == 1) return 0u;
-  // ---- 3. dots above the other side's top clock -> bit 31 of the actor id
-  lean_flags(Ls, Rs, actL, ctrL, dL, A, lane);
-  lean_flags(Rs, Ls, actR, ctrR, dR, A, lane);
-  wave_sync();
-  const uint32_t dsc = lane < U ? desc[lane] : 0u;
-  if (LABL == 2) {
-    if (__ballot(dsc == 0x12345u) != 0ull) *(uint32_t*)Os = dsc;
-    return 0u;
-  }
-
-  // ---- 4. join of union member `lane`
-  const uint32_t ty = dsc >> 30, mi = (dsc >> 15) & 0x7FFFu, mj = dsc & 0x7FFFu;
-  const uint32_t ab = ld32(Ls, endL + 4u * mi - 4u), ae_ = ld32(Ls, endL + 4u * mi);
-  const uint32_t bb = ld32(Rs, endR + 4u * mj - 4u), be_ = ld32(Rs, endR + 4u * mj);
-  const bool hs = (ty & kSelf) != 0u, ho = (ty & kOther) != 0u;
-  // run bounds, clamped to the dot counts (a malformed record cannot spin the loop)
-  const uint32_t ae = hs ? (ae_ < dL ? ae_ : dL) : 0u, be = ho ? (be_ < dR ? be_ : dR) : 0u;
-  const uint32_t a0 = hs && mi ? (ab < ae ? ab : ae) : 0u, b0 = ho && mj ? (bb < be ? bb : be) : 0u;
-  const bool self_only = ty == kSelf;
-  uint32_t x0 = 0, x1 = 0;
-  uint64_t v0 = 0, v1 = 0;
-  const uint32_t c = lean_join<false>(Ls, Rs, actL, ctrL, actR, ctrR, a0, ae, b0, be, self_only, x0, v0, x1, v1,
-                                      nullptr, nullptr, 0u);
-
-  if (LABL == 3) {
-    if (__ballot((c + x0 + x1 + (uint32_t)(v0 ^ v1)) == 0x12345u) != 0ull) *(uint32_t*)Os = c;
-    return 0u;
-  }
-  // ---- 5. output layout (no deferred block)
-  const uint64_t keepm = __ballot(c != 0u);
-  const uint32_t tot_mem = (uint32_t)__popcll(keepm);
-  const uint32_t cincl = scan_incl(c);
-  const uint32_t tot_dot = lane_of(cincl, kWave - 1);
-  const uint32_t o_key = kHdrBytes + 8u * A;
-  const uint32_t o_dctr = o_key + 8u * tot_mem, o_dact = o_dctr + 8u * tot_dot, o_mdend = o_dact + 4u * tot_dot;
-  const uint32_t o_mpad = o_mdend + 4u * tot_mem;
-  const uint32_t size = (((o_mpad + 7u) & ~7u) + 15u) & ~15u;
-  if (size > OUTCAP) {
-    big = true;
-    return 0u;
-  }
-  uint8_t* O = (uint8_t*)Os;
-  wave_sync();  // every lane has read its descriptor
-  // top clock: pointwise max (src/orswot.rs:153 -> src/vclock.rs:131-137)
-  for (uint32_t x = lane; x < A; x += kWave) {
-    const uint64_t l = ld64(Ls, kHdrBytes + 8u * x), r = ld64(Rs, kHdrBytes + 8u * x);
-    *(uint64_t*)(O + kHdrBytes + 8u * x) = l > r ? l : r;
-  }
-  if (c != 0u) {
-    const uint32_t midx = (uint32_t)__popcll(keepm & ((1ull << lane) - 1ull));
-    const uint32_t d0 = cincl - c;
-    const uint8_t* kb = hs ? Ls + key + 8u * mi : Rs + key + 8u * mj;
-    *(uint64_t*)(O + o_key + 8u * midx) = *(const uint64_t*)kb;
-    uint32_t* oact = (uint32_t*)(O + o_dact);
-    uint64_t* octr = (uint64_t*)(O + o_dctr);
-    if (c <= 2u) {
-      oact[d0] = x0;
-      octr[d0] = v0;
-      if (c == 2u) {
-        oact[d0 + 1u] = x1;
-        octr[d0 + 1u] = v1;
-      }
-    } else {
-      lean_join<true>(Ls, Rs, actL, ctrL, actR, ctrR, a0, ae, b0, be, self_only, x0, v0, x1, v1, oact, octr, d0);
-    }
-    *(uint32_t*)(O + o_mdend + 4u * midx) = d0 + c;
-  }
-  if (lane == 0u) {
-    for (uint32_t q = o_mpad; q < size; q += 4u) *(uint32_t*)(O + q) = 0u;
-    u32x4* h = (u32x4*)O;
-    h[0] = u32x4{size, A, tot_mem, tot_dot};
-    h[1] = u32x4{0u, 0u, 0u, 0u};
-  }
-  return size / 16u;
-}
-#endif  // CRDT_DIAG
 
 
 // ======================================================================
@@ -1153,10 +952,9 @@ __device__ __forceinline__ uint32_t lean_object(uint8_t* Ls, uint8_t* Rs, u32x4*
 //     (self-only entries dropped as a whole iff ML & FL == 0, :98-103);
 //  5. every kept dot writes itself at its member's output base + the rank
 //     of its actor in the keep mask — no per-member loop anywhere.
-// Scratch: 3 KB of LDS per wave (kMaskScratch). Returns output 16-B pieces,
+// Scratch: kMask1Scratch bytes of LDS per wave. Returns output 16-B pieces,
 // or kLeanFallback (union > 64 members, or an actor id >= 32).
 // ======================================================================
-constexpr uint32_t kMaskScratch = 3072;  // bytes reserved per wave (mask2_object uses 2 816)
 // mask_object scratch byte offsets (2 048 B used)
 constexpr uint32_t kMsL = 0;       // u32x2 [64]: L member i -> {actor mask, survives mask}
 constexpr uint32_t kMsR = 512;     // u32x2 [64]: R member j
@@ -2070,219 +1868,6 @@ __device__ __forceinline__ uint32_t mask3_object(uint32_t uL, uint32_t uR, uint3
   return OUT != 0 && fb ? kLeanFallback : size / 16u;
 }
 
-#ifdef CRDT_DIAG
-// ======================================================================
-// (Diagnostic build only.) Mask path v2 (v7): the same mask join as mask_object with fewer dependent
-// LDS round trips — no run-head flags, no LDS atomics, no separate pass:
-//  - every member lane reads its own run (the first two dots straight-line,
-//    longer runs — 0.3 % in config 3 — in a loop) and forms its actor mask and
-//    "above the other side's top clock" mask itself, while the rank search
-//    of the member alignment is in flight;
-//  - an other-side member with a shared key reads its partner's run and
-//    forms the "equal" / "self >= other" masks itself;
-//  - the union-member lane writes its own output dots in actor order (bit
-//    order of the keep mask), values from registers for the first two dots
-//    of each run.
-// Scratch (per wave, 2 816 B): msL[64], msR[64] u32x4 {mask, survives, run
-// start, run length}; eqge[64] u32x2 (by other-side member); desc[64].
-// ======================================================================
-constexpr uint32_t k2MsL = 0, k2MsR = 1024, k2Eq = 2048, k2Desc = 2560;
-
-struct Run2 {
-  uint32_t a0, n, x0, x1;
-  uint64_t v0, v1;
-};
-
-// Run of member m (has = the lane owns a member) of a staged record.
-__device__ __forceinline__ Run2 read_run(const uint8_t* S, uint32_t end, uint32_t act, uint32_t ctr, uint32_t m,
-                                         uint32_t nd, bool has) {
-  const uint32_t e0 = ld32(S, end + 4u * m - 4u), e1 = ld32(S, end + 4u * m);
-  const uint32_t hi = e1 < nd ? e1 : nd;  // clamped: a malformed record cannot spin a loop
-  Run2 r;
-  r.a0 = has && m ? (e0 < hi ? e0 : hi) : 0u;
-  r.n = has ? hi - r.a0 : 0u;
-  r.x0 = ld32(S, act + 4u * r.a0);
-  r.x1 = ld32(S, act + 4u * r.a0 + 4u);
-  r.v0 = ld64(S, ctr + 8u * r.a0);
-  r.v1 = ld64(S, ctr + 8u * r.a0 + 8u);
-  return r;
-}
-
-__device__ __forceinline__ uint64_t top_of(const uint8_t* T, uint32_t x, uint32_t A) {
-  const uint64_t t = ld64(T, kHdrBytes + 8u * (x < A ? x : 0u));
-  return x < A ? t : 0ull;
-}
-
-// Actor mask M and "dot above T's top clock" mask F of run r; bad |= an
-// actor id >= 32.
-__device__ __forceinline__ void run_masks(const uint8_t* S, const uint8_t* T, uint32_t act, uint32_t ctr,
-                                          const Run2& r, uint32_t A, uint32_t& M, uint32_t& F, bool& bad) {
-  const uint64_t t0 = top_of(T, r.x0, A), t1 = top_of(T, r.x1, A);
-  const bool h0 = r.n >= 1u, h1 = r.n >= 2u;
-  M = (h0 ? 1u << (r.x0 & 31u) : 0u) | (h1 ? 1u << (r.x1 & 31u) : 0u);
-  F = (h0 && r.v0 > t0 ? 1u << (r.x0 & 31u) : 0u) | (h1 && r.v1 > t1 ? 1u << (r.x1 & 31u) : 0u);
-  bool b = (h0 && r.x0 >= 32u) || (h1 && r.x1 >= 32u);
-  for (uint32_t d = r.a0 + 2u; d < r.a0 + r.n; ++d) {  // runs of 3+ dots
-    const uint32_t x = ld32(S, act + 4u * d);
-    const uint64_t v = ld64(S, ctr + 8u * d);
-    M |= 1u << (x & 31u);
-    F |= v > top_of(T, x, A) ? 1u << (x & 31u) : 0u;
-    b = b || x >= 32u;
-  }
-  bad = bad || b;
-}
-
-// Counter of actor x in run r (x known present; p = its rank in the run).
-__device__ __forceinline__ uint64_t run_value(const uint8_t* S, uint32_t ctr, const Run2& r, uint32_t p) {
-  return p == 0u ? r.v0 : (p == 1u ? r.v1 : ld64(S, ctr + 8u * (r.a0 + p)));
-}
-
-template <uint32_t OUTCAP, bool HD = false, int ABL = 0>
-__device__ __forceinline__ uint32_t mask2_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* X, u32x4* Os,
-                                                 uint32_t A, uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR,
-                                                 uint32_t lane, bool& big, Stamps* stp = nullptr) {
-  big = false;
-  const uint32_t key = kHdrBytes + 8u * A;
-  const uint32_t ctrL = key + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
-  const uint32_t ctrR = key + 8u * nR, actR = ctrR + 8u * dR, endR = actR + 4u * dR;
-  const bool hml = lane < nL, hmr = lane < nR;
-
-  // ---- own runs and masks (member lane i of self, j of other)
-  const Run2 rl_ = read_run(Ls, endL, actL, ctrL, lane, dL, hml);
-  const Run2 rr_ = read_run(Rs, endR, actR, ctrR, lane, dR, hmr);
-  // ---- member alignment by rank (self first on equal keys)
-  const uint64_t kl = ld64(Ls, key + 8u * lane), kr = ld64(Rs, key + 8u * lane);
-  const uint32_t rl = rank_below(Rs, key, nR, kl);  // # other keys < my self key
-  const uint32_t rr = rank_below(Ls, key, nL, kr);  // # self keys < my other key
-  uint32_t ML, FL, MR, FR;
-  bool bad = false;
-  run_masks(Ls, Rs, actL, ctrL, rl_, A, ML, FL, bad);
-  run_masks(Rs, Ls, actR, ctrR, rr_, A, MR, FR, bad);
-  const bool eql = hml && rl < nR && ld64(Rs, key + 8u * rl) == kl;
-  const bool eqr = hmr && rr < nL && ld64(Ls, key + 8u * rr) == kr;
-  const uint64_t EL = __ballot(eql), ER = __ballot(eqr);
-  const uint32_t U = nL + nR - (uint32_t)__popcll(EL);
-  if (U > (uint32_t)kWave || __ballot(bad) != 0ull) return kLeanFallback;
-  const uint32_t ul = lane + rl - mbcnt64(EL);  // # union keys below my self key
-  const uint32_t ur = lane + rr - mbcnt64(ER);
-  if (ABL == 9) mark<ABL>(*stp, 4);  // runs + rank search
-  // ---- shared member (other side): equal / self >= other over common actors
-  uint32_t EQ = 0u, GE = 0u;
-  if (eqr) {
-    const Run2 p = read_run(Ls, endL, actL, ctrL, rr, dL, true);
-    uint32_t MP = (p.n >= 1u ? 1u << (p.x0 & 31u) : 0u) | (p.n >= 2u ? 1u << (p.x1 & 31u) : 0u);
-    for (uint32_t d = p.a0 + 2u; d < p.a0 + p.n; ++d) MP |= 1u << (ld32(Ls, actL + 4u * d) & 31u);
-    for (uint32_t q = 0; q < rr_.n; ++q) {  // my dots (1-2 almost always)
-      const uint32_t y = q == 0u ? rr_.x0 : (q == 1u ? rr_.x1 : ld32(Rs, actR + 4u * (rr_.a0 + q)));
-      const uint64_t w = q == 0u ? rr_.v0 : (q == 1u ? rr_.v1 : ld64(Rs, ctrR + 8u * (rr_.a0 + q)));
-      if ((MP >> (y & 31u)) & 1u) {
-        const uint64_t pv = run_value(Ls, ctrL, p, below(MP, y & 31u));
-        EQ |= pv == w ? 1u << (y & 31u) : 0u;
-        GE |= pv >= w ? 1u << (y & 31u) : 0u;
-      }
-    }
-  }
-  // ---- publish per-member summaries and the union descriptors
-  wave_sync();  // the previous object's readers of this scratch are done
-  if (hml) {
-    *(u32x4*)(X + k2MsL + 16u * lane) = u32x4{ML, FL, rl_.a0, rl_.n};
-    *(uint32_t*)(X + k2Desc + 4u * ul) = ((eql ? kBoth : kSelf) << 16) | (lane << 8) | (eql ? rl : 0u);
-  }
-  if (hmr) {
-    *(u32x4*)(X + k2MsR + 16u * lane) = u32x4{MR, FR, rr_.a0, rr_.n};
-    *(uint64_t*)(X + k2Eq + 8u * lane) = ((uint64_t)GE << 32) | EQ;
-    if (!eqr) *(uint32_t*)(X + k2Desc + 4u * ur) = (kOther << 16) | (rr << 8) | lane;
-  }
-  wave_sync();
-  if (ABL == 9) mark<ABL>(*stp, 5);  // equal / >= + publish
-  // ---- per union member: mask join
-  const bool hu = lane < U;
-  const uint32_t dsc = hu ? *(const uint32_t*)(X + k2Desc + 4u * lane) : 0u;
-  const uint32_t ty = dsc >> 16, mi = (dsc >> 8) & 0xFFu, mj = dsc & 0xFFu;
-  const u32x4 sl = *(const u32x4*)(X + k2MsL + 16u * (mi & 63u)), sr = *(const u32x4*)(X + k2MsR + 16u * (mj & 63u));
-  const uint64_t pe = *(const uint64_t*)(X + k2Eq + 8u * (mj & 63u));
-  const bool hs = (ty & kSelf) != 0u, ho = (ty & kOther) != 0u;
-  const uint32_t uML = hs ? sl.x : 0u, uFL = hs ? sl.y : 0u, uMR = ho ? sr.x : 0u, uFR = ho ? sr.y : 0u;
-  const uint32_t uEQ = ty == kBoth ? (uint32_t)pe : 0u, uGE = ty == kBoth ? (uint32_t)(pe >> 32) : 0u;
-  const bool self_only = ty == kSelf;
-  const uint32_t lp = self_only ? uML : (uML & uFL), rp = uMR & uFR;
-  const uint32_t useA = (uML & uMR & uEQ) | (lp & (~rp | uGE));
-  uint32_t keep = useA | rp;
-  keep = (self_only && (uML & uFL) == 0u) ? 0u : keep;
-  keep = hu ? keep : 0u;
-  // the union lane's runs: first two counters in registers
-  Run2 ra, rb;
-  ra.a0 = hs ? sl.z : 0u; ra.n = hs ? sl.w : 0u;
-  rb.a0 = ho ? sr.z : 0u; rb.n = ho ? sr.w : 0u;
-  ra.v0 = ld64(Ls, ctrL + 8u * ra.a0); ra.v1 = ld64(Ls, ctrL + 8u * ra.a0 + 8u);
-  rb.v0 = ld64(Rs, ctrR + 8u * rb.a0); rb.v1 = ld64(Rs, ctrR + 8u * rb.a0 + 8u);
-  const uint64_t mkey = hs ? ld64(Ls, key + 8u * mi) : ld64(Rs, key + 8u * mj);
-  Side DL{Ls, RV{}}, DR{Rs, RV{}};
-  if (HD) {  // deferred removes: kept dots dying to a deferred clock listing the member
-    DL = side_of(Ls);
-    DR = side_of(Rs);
-    const uint64_t mk = keep ? dmask_of(DL, DR, mkey) : 0ull;
-    if (mk) {
-      for (uint32_t rem = keep; rem; rem &= rem - 1u) {
-        const uint32_t x = (uint32_t)__builtin_ctz(rem);
-        const bool fa = (useA >> x) & 1u;
-        const uint64_t v = fa ? run_value(Ls, ctrL, ra, below(uML, x)) : run_value(Rs, ctrR, rb, below(uMR, x));
-        if (dkilled(DL, DR, mk, x, v)) keep &= ~(1u << x);
-      }
-    }
-  }
-  const uint32_t c = __popc(keep);
-
-  // ---- output layout
-  const uint64_t keepm = __ballot(c != 0u);
-  const uint32_t tot_mem = (uint32_t)__popcll(keepm);
-  const uint32_t cincl = scan_incl(c);
-  const uint32_t tot_dot = lane_of(cincl, kWave - 1);
-  uint32_t nd = 0, ndd = 0, ndm = 0;
-  if (HD) deferred_pass_wave(DL, DR, A, lane, nd, ndd, ndm, nullptr);
-  RecLayout OL;
-  rec_layout(OL, A, tot_mem, tot_dot, nd, ndd, ndm);
-  const uint32_t size = OL.size;
-  if (size > OUTCAP) {
-    big = true;
-    return 0u;
-  }
-  uint8_t* O = (uint8_t*)Os;
-  uint32_t* oact = (uint32_t*)(O + OL.o_dact);
-  uint64_t* octr = (uint64_t*)(O + OL.o_dctr);
-  if (c != 0u) {
-    const uint32_t midx = mbcnt64(keepm);
-    const uint32_t d0 = cincl - c;
-    *(uint64_t*)(O + OL.o_key + 8u * midx) = mkey;
-    *(uint32_t*)(O + OL.o_mdend + 4u * midx) = cincl;
-    uint32_t k = d0;
-    for (uint32_t rem = keep; rem; rem &= rem - 1u, ++k) {  // actor order = bit order
-      const uint32_t x = (uint32_t)__builtin_ctz(rem);
-      const bool fa = (useA >> x) & 1u;
-      const uint64_t v = fa ? run_value(Ls, ctrL, ra, below(uML, x)) : run_value(Rs, ctrR, rb, below(uMR, x));
-      oact[k] = x;
-      octr[k] = v;
-    }
-  }
-  for (uint32_t x = lane; x < A; x += kWave) {  // top clock: pointwise max (src/orswot.rs:153)
-    const uint64_t l = ld64(Ls, kHdrBytes + 8u * x), r = ld64(Rs, kHdrBytes + 8u * x);
-    *(uint64_t*)(O + kHdrBytes + 8u * x) = l > r ? l : r;
-  }
-  if (HD) {  // deferred union keyed by clock (:141-148), kept iff !(D <= clock) (:197)
-    DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
-             (uint32_t*)(O + OL.o_fdend), (uint32_t*)(O + OL.o_fmend)};
-    deferred_pass_wave(DL, DR, A, lane, nd, ndd, ndm, &w);
-  }
-  if (lane == 0u && OL.o_def != OL.o_mpad) *(uint32_t*)(O + OL.o_mpad) = 0u;
-  if (lane >= 1u && lane < 4u && OL.o_end + 4u * (lane - 1u) < size) *(uint32_t*)(O + OL.o_end + 4u * (lane - 1u)) = 0u;
-  if (lane == 0u) {
-    u32x4* h = (u32x4*)O;
-    h[0] = u32x4{size, A, tot_mem, tot_dot};
-    h[1] = u32x4{nd, ndd, ndm, 0u};
-  }
-  return size / 16u;
-}
-#endif  // CRDT_DIAG
 
 
 // ======================================================================
@@ -2630,24 +2215,6 @@ __device__ __forceinline__ void copy_out(const u32x4* src, uint8_t* dst, uint32_
   for (uint32_t k = lane; k < n16; k += kWave) __builtin_nontemporal_store(src[k], (u32x4*)dst + k);
 }
 
-#ifdef CRDT_DIAG
-__device__ __forceinline__ void prefetch(u32x4 (&r)[kPer], const uint8_t* src, uint32_t n16, uint32_t lane) {
-#pragma unroll
-  for (uint32_t k = 0; k < kPer; ++k) {
-    const uint32_t idx = lane + k * kWave;
-    if (idx < n16) r[k] = __builtin_nontemporal_load((const u32x4*)src + idx);
-  }
-}
-
-__device__ __forceinline__ void stage(u32x4* dst, const u32x4 (&r)[kPer], uint32_t n16, uint32_t lane) {
-#pragma unroll
-  for (uint32_t k = 0; k < kPer; ++k) {
-    const uint32_t idx = lane + k * kWave;
-    if (idx < n16) dst[idx] = r[k];
-  }
-}
-
-#endif  // CRDT_DIAG
 
 // Branch-free forms for the mask kernel: every lane loads (indices past the
 // record re-read its last piece, in bounds, merged by the address coalescer)
@@ -2763,162 +2330,6 @@ __device__ __forceinline__ void stage_used(u32x4* dst, const u32x4 (&r)[kPer], u
     if (n16 > k * kWave) dst[lane + k * kWave] = r[k];
 }
 
-#ifdef CRDT_DIAG
-// (Diagnostic build only: the v4 merge-path kernel and its variants.)
-// MASK: non-deferred objects take mask_object. DIRECT (with MASK): outputs
-// are written straight to HBM (no LDS output stage), which frees LDS for a
-// 5th wave per SIMD.
-template <int MINW, int ABL, bool LEAN = false, int LABL = 0, bool MASK = false, bool DIRECT = false>
-__global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_kernel(
-    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
-    const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
-    uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
-    int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
-  __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
-  __shared__ u32x4 out_s[kWavesPerBlock][DIRECT ? 1 : 2][(DIRECT ? kMaskScratch : kOutStage) / 16];
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint32_t wave = threadIdx.x / kWave;
-  u32x4* const sL = stage_s[wave][0];
-  u32x4* const sR = stage_s[wave][1];
-  // Rounds of chunks: in round r wave w takes chunk r * n_waves + w of `cs`
-  // consecutive objects, cs <= 64 chosen so every wave gets the same number
-  // of rounds (no tail) while concurrent waves read neighbouring memory.
-  const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
-  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint64_t rounds = (n_obj + n_waves * kWave - 1) / (n_waves * kWave);
-  const uint64_t cs = (n_obj + n_waves * rounds - 1) / (n_waves * rounds);
-
-  Stamps st{};
-  if (ABL == 9) st.last = stamp();
-  for (uint64_t cbase = wave_id * cs; cbase < n_obj; cbase += n_waves * cs) {
-    // ---- chunk state: lane k <-> object cbase + k
-    const uint64_t obj = cbase + lane;
-    const bool valid = lane < cs && obj < n_obj;
-    uint64_t lo = 0, ro = 0;
-    if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
-    u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
-    bool ok = valid && (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes &&
-              ro + kHdrBytes <= Rbytes;
-    if (ok) {
-      hl0 = ((const u32x4*)(Lb + lo))[0]; hl1 = ((const u32x4*)(Lb + lo))[1];
-      hr0 = ((const u32x4*)(Rb + ro))[0]; hr1 = ((const u32x4*)(Rb + ro))[1];
-    }
-    ok = ok && header_ok(hl0, hl1, lo, Lbytes, A) && header_ok(hr0, hr1, ro, Rbytes, A) &&
-         lo + ro + (uint64_t)hl0.x + hr0.x <= Obytes;
-    const bool fast = ok && hl0.x <= kFastStage && hr0.x <= kFastStage && hl1.x <= 32u && hr1.x <= 32u &&
-                      hl0.z + hr0.z <= 2u * kWave;
-    if (valid) Ooff[obj] = (lo + ro) | ((ok && !fast) ? kPending : 0ull);
-    if (ok && !fast) {  // hand the object to the general kernel
-      const uint32_t e = atomicAdd(&ctl[0], 1u);
-      if (e < list_cap) list[e] = obj;
-    }
-    if (__ballot(valid && !ok) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
-    const uint64_t runs = __ballot(fast);
-    if (runs == 0ull) continue;
-    const uint32_t n16 = fast ? (hl0.x / 16u) | ((hr0.x / 16u) << 16) : 0u;
-    const uint32_t nm = hl0.z | (hr0.z << 16), nd = hl0.w | (hr0.w << 16);
-    const uint64_t defs = __ballot(fast && (hl1.x | hr1.x) != 0u);  // objects with deferred removes
-
-    // ---- software pipeline: the next fast object's records are in flight
-    // while the current one is joined from LDS.
-    uint64_t pend = runs;
-    uint32_t t = (uint32_t)__builtin_ctzll(pend);
-    u32x4 pl[kPer], pr[kPer];
-    uint32_t nn = lane_of(n16, t);
-    prefetch(pl, Lb + lane_of64(lo, t), nn & 0xFFFFu, lane);
-    prefetch(pr, Rb + lane_of64(ro, t), nn >> 16, lane);
-    mark<ABL>(st, 7);  // chunk state
-    // output stages alternate; object t-1's copy-out is issued right after
-    // object t is staged, so its stores drain while object t is joined
-    uint32_t par = 0, out_n16 = 0;
-    uint8_t* out_dst = Ob;
-    while (pend) {
-      t = (uint32_t)__builtin_ctzll(pend);
-      pend &= pend - 1;
-      nn = lane_of(n16, t);
-      wave_sync();  // previous object's LDS reads are done
-      stage(sL, pl, nn & 0xFFFFu, lane);
-      stage(sR, pr, nn >> 16, lane);
-      wave_sync();
-      mark<ABL>(st, 0);  // wait for the prefetched records + stage them
-      if (!DIRECT) copy_out(out_s[wave][MASK ? 0u : par ^ 1u], out_dst, out_n16, lane);
-      mark<ABL>(st, 6);
-      const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
-      const uint32_t m = lane_of(nm, t), d = lane_of(nd, t);
-      if (pend) {
-        const uint32_t u = (uint32_t)__builtin_ctzll(pend);
-        const uint32_t nu = lane_of(n16, u);
-        prefetch(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
-        prefetch(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
-      }
-      mark<ABL>(st, 1);  // issue the next prefetch
-      const FOut fo{DIRECT ? (u32x4*)(Ob + oo) : out_s[wave][par], Ob + oo, cbase + t, Ooff, ctl, list, list_cap};
-      const uint32_t nLt = m & 0xFFFFu, nRt = m >> 16, dLt = d & 0xFFFFu, dRt = d >> 16;
-      if (DIRECT) {
-        uint32_t r = kLeanFallback;
-        bool big = false;
-        if (!((defs >> t) & 1ull) && A <= 32u && nLt <= 64u && nRt <= 64u && dLt <= 64u && dRt <= 64u)
-          r = mask_object<0xFFFFFFFFu>((const uint8_t*)sL, (const uint8_t*)sR, (uint8_t*)out_s[wave][0],
-                                       (u32x4*)(Ob + oo), A, nLt, dLt, nRt, dRt, lane, big);
-        if (r == kLeanFallback) {
-          if ((defs >> t) & 1ull)
-            fast_object<true, ABL, 0xFFFFFFFFu>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, nLt, dLt, nRt, dRt,
-                                                lane, st);
-          else
-            fast_object<false, ABL, 0xFFFFFFFFu>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, nLt, dLt, nRt,
-                                                 dRt, lane, st);
-        }
-        out_n16 = 0u;
-      } else if (MASK && !((defs >> t) & 1ull) && A <= 32u && nLt <= 64u && nRt <= 64u && dLt <= 64u && dRt <= 64u) {
-        bool big;
-        out_n16 = mask_object<kOutStage>((const uint8_t*)sL, (const uint8_t*)sR, (uint8_t*)out_s[wave][DIRECT ? 0 : 1],
-                                         out_s[wave][0], A, nLt, dLt, nRt, dRt, lane, big);
-        if (big) {  // rare: output larger than the stage -> general kernel
-          if (lane == 0u) {
-            Ooff[cbase + t] |= kPending;
-            const uint32_t e = atomicAdd(&ctl[0], 1u);
-            if (e < list_cap) list[e] = cbase + t;
-          }
-          out_n16 = 0u;
-        }
-        if (out_n16 == kLeanFallback)
-          out_n16 = fast_object<false, ABL>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, nLt, dLt, nRt, dRt,
-                                            lane, st);
-      } else if ((defs >> t) & 1ull) {
-        out_n16 = fast_object<true, ABL>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, m & 0xFFFFu, d & 0xFFFFu,
-                                         m >> 16, d >> 16, lane, st);
-      } else {
-        out_n16 = kLeanFallback;
-        if (LEAN) {
-          bool big;
-          out_n16 = lean_object<kOutStage, LABL>((uint8_t*)sL, (uint8_t*)sR, out_s[wave][par], A, m & 0xFFFFu,
-                                           d & 0xFFFFu, m >> 16, d >> 16, lane, big);
-          if (big) {  // rare: output larger than the stage -> general kernel
-            if (lane == 0u) {
-              Ooff[cbase + t] |= kPending;
-              const uint32_t e = atomicAdd(&ctl[0], 1u);
-              if (e < list_cap) list[e] = cbase + t;
-            }
-            out_n16 = 0u;
-          }
-        }
-        if (out_n16 == kLeanFallback)
-          out_n16 = fast_object<false, ABL>((const uint8_t*)sL, (const uint8_t*)sR, fo, A, m & 0xFFFFu,
-                                            d & 0xFFFFu, m >> 16, d >> 16, lane, st);
-      }
-      out_dst = Ob + oo;
-      if (!MASK) par ^= 1u;  // the mask path keeps one output stage (its twin is scratch)
-    }
-    if (!DIRECT) copy_out(out_s[wave][MASK ? 0u : par ^ 1u], out_dst, out_n16, lane);  // drain the chunk's last object
-  }
-  if (ABL == 9 && lane < 8u) {  // per-wave phase sums -> the context's list buffer
-    uint64_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v = lane == (uint32_t)k ? st.acc[k] : v;
-    list[wave_id * 8u + lane] = v;
-  }
-}
-#endif  // CRDT_DIAG
 
 // ======================================================================
 // Mask kernel (v6): every object that fits the mask path (records <= 2 KB,
@@ -2927,16 +2338,15 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_merge_ker
 // flagged for the general kernel. Only the mask path lives here, which keeps
 // the register budget low enough for 5 waves per SIMD.
 // ======================================================================
-// ABL 9: phase stamps; M2: mask2_object (diagnostic); M3: mask3_object for
-// the objects without deferred removes
-template <int MINW, int ABL = 0, bool M2 = false, bool M3 = false, bool SINK = false>
+// ABL 9: phase stamps; M3: mask3_object for the objects without deferred removes
+template <int MINW, int ABL = 0, bool M3 = false, bool SINK = false>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
     uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
     int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
   __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
-  __shared__ u32x4 scr_s[kWavesPerBlock][(M2 ? kMaskScratch : kMask1Scratch) / 16];
+  __shared__ u32x4 scr_s[kWavesPerBlock][kMask1Scratch / 16];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wave = threadIdx.x / kWave;
   u32x4* const sL = stage_s[wave][0];
@@ -2948,7 +2358,6 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kern
   const uint64_t cs = (n_obj + n_waves * rounds - 1) / (n_waves * rounds);
   // the wave's store sink: after the list in the context's scratch (ctx.h)
   uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
-  [[maybe_unused]] uint32_t tacc = 0u;  // TCH: the touch loads' values (kept live, stored never in practice)
   Stamps st{};
   if (ABL == 9) st.last = stamp();
   for (uint64_t cbase = wave_id * cs; cbase < n_obj; cbase += n_waves * cs) {
@@ -3014,16 +2423,6 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kern
       mark<ABL>(st, 1);  // issue the next prefetch
       bool big = false;
       uint32_t r;
-#ifdef CRDT_DIAG
-      if (M2) {
-        if ((defs >> t) & 1ull)
-          r = mask2_object<0xFFFFFFFFu, true, ABL>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
-                                                    m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, &st);
-        else
-          r = mask2_object<0xFFFFFFFFu, false, ABL>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
-                                                     m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, &st);
-      } else
-#endif
       if (M3 && !((defs >> t) & 1ull)) {
         r = mask3_object<0xFFFFFFFFu, SINK ? 1 : 0>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
                                             d & 0xFFFFu, m >> 16, d >> 16, lane, big, sink);
@@ -3389,402 +2788,6 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
 #endif
 }
 
-#ifdef CRDT_DIAG
-// ======================================================================
-// (Diagnostic build only.) Join kernel v9: orswot_join_kernel's one-pass body (mask3
-// for every object; deferred-remove objects through mask3's HD form, direct
-// stores) over chunks of kDynG objects handed out at run time. With a static
-// split (v8) the per-wave work varied enough that the median wave finished
-// at 0.77 of the launch (tools/wave_tail.py); here the first chunk of a wave
-// is its index and every later one comes from an atomic ticket (ctl[3],
-// zeroed before the launch) taken when the previous chunk starts. Small
-// chunks make the chunk step frequent, so it is pipelined: while a chunk's
-// objects are joined, the next chunk's offsets (after the first object) and
-// record headers (after the second) are loaded into two registers laid out
-// by lane role, and the next chunk step reads them with ds_bpermute gathers
-// instead of waiting on two dependent HBM round trips.
-// ======================================================================
-constexpr uint32_t kDynG = 16;  // objects per chunk (the raw-load lane roles assume 16)
-
-__device__ __forceinline__ u32x4 gather128(u32x4 v, uint32_t src_lane) {
-  return u32x4{gather32(v.x, src_lane), gather32(v.y, src_lane), gather32(v.z, src_lane), gather32(v.w, src_lane)};
-}
-
-template <int MINW, int HABL = 0>
-__global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_dyn_kernel(
-    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
-    const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
-    uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
-    int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
-  __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
-  __shared__ u32x4 scr_s[kWavesPerBlock][kMask1Scratch / 16];
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint32_t wave = uni(threadIdx.x / kWave);  // wave-uniform: LDS bases in SGPRs
-  u32x4* const sL = stage_s[wave][0];
-  u32x4* const sR = stage_s[wave][1];
-  uint8_t* const X = (uint8_t*)scr_s[wave];
-  const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
-  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint64_t ts0 = HABL == 6 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
-  uint32_t n_joined = 0u, n_hd = 0u, n_chunk = 0u;                                  // (HABL 6: per-wave counts)
-  uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
-  [[maybe_unused]] uint32_t tacc = 0u;  // TCH: the touch loads' values (kept live, stored never in practice)
-  const uint64_t n_chunks = (n_obj + kDynG - 1) / kDynG;
-  const uint32_t sec = lane >> 4, k16 = lane & 15u;  // raw-load lane roles
-
-  // chunk c's offsets: lane l holds section l / 16 of object c * 16 + l % 16 —
-  // 0: Loff[o], 1: Roff[o], 2 / 3: the next object's (the batch size past the last)
-  auto load_offs = [&](uint64_t c) -> uint64_t {
-    const uint64_t o = c * kDynG + k16 + (sec >> 1);
-    const uint64_t past = (sec & 1u) ? Rbytes : Lbytes;
-    uint64_t v = past;
-    if (o < n_obj) v = ((sec & 1u) ? Roff : Loff)[o];
-    return v;
-  };
-  // chunk c's record headers: lane l holds 16-B half l / 32 of side (l / 16) & 1's
-  // header of object l % 16 (zero where the offset cannot hold a header)
-  auto load_hdrs = [&](uint64_t c, uint64_t offs) -> u32x4 {
-    const uint32_t side = sec & 1u, half = sec >> 1;
-    const uint64_t off = gather64(offs, side * 16u + k16);
-    const bool v = c * kDynG + k16 < n_obj && (off & 15u) == 0 && off + kHdrBytes <= (side ? Rbytes : Lbytes);
-    u32x4 h = {0u, 0u, 0u, 0u};
-    if (v) h = *((const u32x4*)((side ? Rb : Lb) + off) + half);
-    return h;
-  };
-
-  uint64_t c = wave_id;
-  uint64_t offs = 0ull;
-  u32x4 hdr = {0u, 0u, 0u, 0u};
-  if (c < n_chunks) {
-    offs = load_offs(c);
-    hdr = load_hdrs(c, offs);
-  }
-  uint32_t ticket = 0u;
-  while (c < n_chunks) {
-    if (lane == 0u) ticket = atomicAdd(&ctl[3], 1u);  // the chunk after this one
-    const uint64_t cbase = c * kDynG;
-    // ---- chunk step from the raw registers: lane k <-> object cbase + k
-    const uint64_t lo = gather64(offs, k16), ro = gather64(offs, 16u + k16);
-    const uint64_t nlo = gather64(offs, 32u + k16), nro = gather64(offs, 48u + k16);
-    const u32x4 hl0 = gather128(hdr, k16), hr0 = gather128(hdr, 16u + k16);
-    const u32x4 hl1 = gather128(hdr, 32u + k16), hr1 = gather128(hdr, 48u + k16);
-    const uint64_t obj = cbase + lane;
-    const bool valid = lane < kDynG && obj < n_obj;
-    bool ok = valid && (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes && ro + kHdrBytes <= Rbytes;
-    ok = ok && header_ok(hl0, hl1, lo, Lbytes, A) && header_ok(hr0, hr1, ro, Rbytes, A) &&
-         lo + ro + (uint64_t)hl0.x + hr0.x <= Obytes;
-    // output placement precondition (out[i] at self.off[i] + other.off[i]):
-    // each side's records in increasing offset order, none overlapping the next
-    const bool placed = !ok || (nlo >= lo + hl0.x && nro >= ro + hr0.x);
-    if (__ballot(!placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_EINVAL);
-    ok = ok && placed;
-    const bool fits = ok && hl0.x <= kFastStage && hr0.x <= kFastStage && A <= 32u && hl0.z <= 64u &&
-                      hr0.z <= 64u && hl0.w <= 64u && hr0.w <= 64u;
-    const bool hd = fits && (hl1.x | hr1.x) != 0u && hl1.x <= 32u && hr1.x <= 32u;
-    const bool fast = fits && ((hl1.x | hr1.x) == 0u || hd);
-    const uint64_t defs = __ballot(hd);
-    const bool gen = ok && !fast;
-    if (valid) Ooff[obj] = (lo + ro) | (gen ? kPending : 0ull);
-    if (gen) {  // hand the object to the general kernel
-      const uint32_t e = atomicAdd(&ctl[0], 1u);
-      if (e < list_cap) list[e] = obj;
-    }
-    if (__ballot(valid && !ok && placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
-    const uint64_t runs = __ballot(fast);
-    const uint32_t n16 = fast ? (hl0.x / 16u) | ((hr0.x / 16u) << 16) : 0u;
-    const uint32_t nm = hl0.z | (hr0.z << 16), nd = hl0.w | (hr0.w << 16);
-
-    // ---- the next chunk's raw loads, one step per joined object
-    uint64_t nc = n_chunks;
-    uint32_t step = 0u;
-    auto advance = [&]() {
-      if (step == 0u) {
-        nc = n_waves + uni(ticket);
-        if (nc < n_chunks) offs = load_offs(nc);
-      } else if (step == 1u && nc < n_chunks) {
-        hdr = load_hdrs(nc, offs);
-      }
-      ++step;
-    };
-
-    if (runs != 0ull) {
-      // ---- software pipeline (orswot_join_kernel's): the next object's
-      // records are in flight while the current one is joined from LDS
-      uint64_t pend = runs;
-      uint32_t t = (uint32_t)__builtin_ctzll(pend);
-      pend &= pend - 1;
-      u32x4 pl[kPer], pr[kPer];
-      {
-        const uint32_t nn = lane_of(n16, t);
-        prefetch_all(pl, Lb + lane_of64(lo, t), nn & 0xFFFFu, lane);
-        prefetch_all(pr, Rb + lane_of64(ro, t), nn >> 16, lane);
-      }
-      wave_sync();  // the previous chunk's last LDS reads are done
-      stage_all(sL, pl, lane);
-      stage_all(sR, pr, lane);
-      wave_sync();
-      for (;;) {
-        const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
-        const uint32_t m = lane_of(nm, t), d = lane_of(nd, t);
-        // the next object, or this one again after the chunk's last (a constant load count)
-        const uint32_t u = pend ? (uint32_t)__builtin_ctzll(pend) : t;
-        {
-          const uint32_t nu = lane_of(n16, u);
-          prefetch_all(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
-          prefetch_all(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
-        }
-        bool big = false;
-        uint32_t r;
-        const bool direct = (defs >> t) & 1ull;
-        if (direct) {
-          r = mask3_object<0xFFFFFFFFu, 0, true, HABL>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A,
-                                                       m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big);
-        } else {
-          r = mask3_object<0xFFFFFFFFu, 3>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
-                                           d & 0xFFFFu, m >> 16, d >> 16, lane, big, sink);
-        }
-        const bool fbu = big || r == kLeanFallback;  // wave-uniform
-        wave_sync();
-        if (direct) {  // the same two stores, to the sink
-          const u32x4 z = {0u, 0u, 0u, 0u};
-          __builtin_nontemporal_store(z, (u32x4*)sink);
-          __builtin_nontemporal_store(z, (u32x4*)sink + 1);
-        } else {
-          copy_record_out(lds_addr(sL), Ob + oo, fbu ? 1u : r, lane);
-        }
-        *(Ooff + cbase + t) = oo | (fbu ? kPending : 0ull);
-        if (fbu) {  // listed for the general kernel (a rare path)
-          if (lane == 0u) {
-            const uint32_t e = atomicAdd(&ctl[0], 1u);
-            if (e < list_cap) list[e] = cbase + t;
-          }
-        }
-        advance();
-        if (pend == 0ull) break;
-        t = u;
-        pend &= pend - 1;
-        wave_sync();  // this object's LDS reads are done
-        stage_used(sL, pl, lane_of(n16, u) & 0xFFFFu, lane);
-        stage_used(sR, pr, lane_of(n16, u) >> 16, lane);
-        wave_sync();
-      }
-    }
-    while (step < 2u) advance();  // a chunk with fewer than two joined objects
-    c = nc;
-  }
-  if (HABL == 6 && lane == 0u && wave_id < 10922u) {  // timing only: the list's upper half holds the stamps
-    list[32768u + 3u * wave_id] = ts0;
-    list[32768u + 3u * wave_id + 1u] = __builtin_amdgcn_s_memrealtime();
-    list[32768u + 3u * wave_id + 2u] = ((uint64_t)n_joined << 32) | (n_hd << 16) | n_chunk;
-  }
-}
-
-// ======================================================================
-// Join kernel v10: the v8 join (mask3_object; deferred-remove objects by its
-// HD form, direct stores) with a chunk step that waits on nothing.
-//  - A chunk's step loads only its offsets: L in lanes 0-31, R in lanes
-//    32-63, one lane past the last object holding the next object's offset
-//    (the placement check). Record headers are not loaded in the step: each
-//    record is prefetched blind — 2 KB from its offset, clamped to the
-//    batch — and its header is read from the stage (a record past 2 KB is
-//    detected there and goes to the general kernel).
-//  - The next chunk is resolved one object into the current one and its
-//    offsets loaded then, so the last object's prefetch is the next chunk's
-//    first object: chunk boundaries cost no round trip.
-//  - Guided split: the first SF/8 of the objects in static chunks by wave
-//    index, the rest in G-object chunks from an atomic ticket (ctl[3]). The
-//    issue arbiter favours the oldest waves; with a static split the
-//    youngest waves of a SIMD ran last and alone (tools/wave_tail.py).
-// ======================================================================
-constexpr uint32_t kV10Max = 31;  // objects per chunk (+1 boundary offset in 32 lanes)
-
-template <int MINW, uint32_t G, uint32_t SF, int HABL = 0>
-__global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_v10_kernel(
-    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
-    const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
-    uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
-    int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
-  static_assert(G >= 1 && G <= kV10Max, "chunk size");
-  __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
-  __shared__ u32x4 scr_s[kWavesPerBlock][kMask1Scratch / 16];
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint32_t wave = uni(threadIdx.x / kWave);  // wave-uniform: LDS bases in SGPRs
-  u32x4* const sL = stage_s[wave][0];
-  u32x4* const sR = stage_s[wave][1];
-  uint8_t* const X = (uint8_t*)scr_s[wave];
-  const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
-  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint64_t ts0 = HABL == 6 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
-  uint32_t n_joined = 0u, n_hd = 0u, n_chunk = 0u;                                  // (HABL 6: per-wave counts)
-  uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
-  [[maybe_unused]] uint32_t tacc = 0u;  // TCH: the touch loads' values (kept live, stored never in practice)
-
-  // ---- guided schedule
-  const uint64_t s_total = SF >= 8u ? n_obj : n_obj * SF / 8u;
-  const uint64_t rounds_s = (s_total + n_waves * kV10Max - 1) / (n_waves * kV10Max);
-  const uint64_t cs_s = rounds_s ? (s_total + n_waves * rounds_s - 1) / (n_waves * rounds_s) : 1u;
-  auto is_static = [&](uint32_t k) { return k < rounds_s && (wave_id + k * n_waves) * cs_s < s_total; };
-  // chunk k of this wave ([cb, ce)), tk = its ticket if it is not static
-  auto chunk_at = [&](uint32_t k, uint32_t tk, uint64_t& cb, uint64_t& ce) -> bool {
-    if (is_static(k)) {
-      cb = (wave_id + k * n_waves) * cs_s;
-      ce = cb + cs_s < s_total ? cb + cs_s : s_total;
-      return true;
-    }
-    cb = s_total + (uint64_t)tk * G;
-    ce = cb + G < n_obj ? cb + G : n_obj;
-    return cb < n_obj;
-  };
-  // a chunk's offsets: lane j < 32 Loff[cb + j], lane 32 + j Roff[cb + j], for
-  // j <= ce - cb (the batch size past the last object)
-  auto load_offs = [&](uint64_t cb, uint64_t ce) -> uint64_t {
-    const uint64_t o = cb + (lane & 31u);
-    const bool r = lane >= 32u;
-    uint64_t v = r ? Rbytes : Lbytes;
-    if (o <= ce && o < n_obj) v = (r ? Roff : Loff)[o];
-    return v;
-  };
-  // prefetch of an object's two records: up to the next object's offset (a
-  // record never extends past it, the placement rule), at most the 2 KB
-  // stage; an offset that cannot hold a record reads the wave's sink line
-  u32x4 pl[kPer], pr[kPer];
-  auto prefetch_obj = [&](uint64_t lo, uint64_t ro, uint64_t nlo, uint64_t nro) -> bool {
-    const bool okp = (lo & 15u) == 0 && lo + kHdrBytes <= Lbytes && (ro & 15u) == 0 && ro + kHdrBytes <= Rbytes &&
-                     nlo >= lo + kHdrBytes && nro >= ro + kHdrBytes;
-    const uint64_t el = nlo < Lbytes ? nlo : Lbytes, er = nro < Rbytes ? nro : Rbytes;
-    const uint64_t nl = (el - lo) / 16u, nr = (er - ro) / 16u;
-    prefetch_all(pl, okp ? Lb + lo : sink, okp ? (uint32_t)(nl < 2u * kWave ? nl : 2u * kWave) : 1u, lane);
-    prefetch_all(pr, okp ? Rb + ro : sink, okp ? (uint32_t)(nr < 2u * kWave ? nr : 2u * kWave) : 1u, lane);
-    return okp;
-  };
-  // staged pieces: the record's size (from lane 0's first piece), at most the stage
-  auto n16_of = [&](const u32x4 (&r)[kPer]) -> uint32_t {
-    const uint32_t sz = uni(r[0].x) / 16u;
-    return sz < 1u ? 1u : sz > 2u * kWave ? 2u * kWave : sz;
-  };
-
-  uint32_t ticket = 0u;
-  uint32_t k = 0;  // this wave's chunk index
-  if (!is_static(0) && lane == 0u) ticket = atomicAdd(&ctl[3], 1u);
-  uint64_t cb = 0, ce = 0;
-  if (chunk_at(0, uni(ticket), cb, ce)) {
-    uint64_t offs = load_offs(cb, ce);
-    if (!is_static(1) && lane == 0u) ticket = atomicAdd(&ctl[3], 1u);  // the ticket of chunk 1
-    uint32_t csz = (uint32_t)(ce - cb), t = 0;
-    uint64_t lo_t = lane_of64(offs, 0), ro_t = lane_of64(offs, 32);
-    bool okp_t = prefetch_obj(lo_t, ro_t, lane_of64(offs, 1), lane_of64(offs, 33));
-    wave_sync();
-    stage_used(sL, pl, n16_of(pl), lane);
-    stage_used(sR, pr, n16_of(pr), lane);
-    wave_sync();
-    uint64_t ncb = 0, nce = 0, noffs = 0;
-    bool next_known = false, have_next = false;
-    if (HABL == 6) ++n_chunk;
-    for (;;) {
-      // ---- resolve the next chunk (one object in, or at a 1-object chunk's only object)
-      if (!next_known && (t >= 1u || csz == 1u)) {
-        next_known = true;
-        have_next = chunk_at(k + 1u, uni(ticket), ncb, nce);
-        if (have_next) noffs = load_offs(ncb, nce);
-      }
-      const bool last = t + 1u == csz;
-      const uint64_t nlo_t = lane_of64(offs, t + 1u), nro_t = lane_of64(offs, 33u + t);  // placement bound
-      // after the wave's last object: this one again (a constant load count)
-      uint64_t lo_u = lo_t, ro_u = ro_t, nlo_u = nlo_t, nro_u = nro_t;
-      if (!last) {
-        lo_u = nlo_t;
-        ro_u = nro_t;
-        nlo_u = lane_of64(offs, t + 2u);
-        nro_u = lane_of64(offs, 34u + t);
-      } else if (have_next) {
-        lo_u = lane_of64(noffs, 0);
-        ro_u = lane_of64(noffs, 32);
-        nlo_u = lane_of64(noffs, 1);
-        nro_u = lane_of64(noffs, 33);
-      }
-      // ---- object t: its headers from the stage (wave-uniform checks)
-      const u32x4 hl0 = *(const __attribute__((address_space(3))) u32x4*)(size_t)lds_addr(sL);
-      const u32x4 hl1 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(lds_addr(sL) + 16u);
-      const u32x4 hr0 = *(const __attribute__((address_space(3))) u32x4*)(size_t)lds_addr(sR);
-      const u32x4 hr1 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(lds_addr(sR) + 16u);
-      // the next object's records are in flight while this one is joined
-      const bool okp_u = prefetch_obj(lo_u, ro_u, nlo_u, nro_u);
-      const u32x4 L0 = {uni(hl0.x), uni(hl0.y), uni(hl0.z), uni(hl0.w)};
-      const u32x4 L1 = {uni(hl1.x), uni(hl1.y), uni(hl1.z), uni(hl1.w)};
-      const u32x4 R0 = {uni(hr0.x), uni(hr0.y), uni(hr0.z), uni(hr0.w)};
-      const u32x4 R1 = {uni(hr1.x), uni(hr1.y), uni(hr1.z), uni(hr1.w)};
-      bool ok = okp_t && header_ok(L0, L1, lo_t, Lbytes, A) && header_ok(R0, R1, ro_t, Rbytes, A) &&
-                lo_t + ro_t + (uint64_t)L0.x + R0.x <= Obytes;
-      // output placement precondition (out[i] at self.off[i] + other.off[i]):
-      // each side's records in increasing offset order, none overlapping the next
-      const bool placed = !ok || (nlo_t >= lo_t + L0.x && nro_t >= ro_t + R0.x);
-      if (!placed && lane == 0u) atomicCAS(status, 0, CRDT_EINVAL);
-      ok = ok && placed;
-      if (!ok && placed && lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
-      const bool fits = ok && L0.x <= kFastStage && R0.x <= kFastStage && A <= 32u && L0.z <= 64u && R0.z <= 64u &&
-                        L0.w <= 64u && R0.w <= 64u;
-      const bool hd = fits && (L1.x | R1.x) != 0u && L1.x <= 32u && R1.x <= 32u;
-      const bool fast = fits && ((L1.x | R1.x) == 0u || hd);
-      const uint64_t oo = lo_t + ro_t;
-      bool big = false, direct = true;
-      uint32_t r = kLeanFallback;
-      if (hd) {
-        r = mask3_object<0xFFFFFFFFu, 0, true, HABL>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, L0.z, L0.w,
-                                                     R0.z, R0.w, lane, big);
-      } else if (fast) {
-        r = mask3_object<0xFFFFFFFFu, 3>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, L0.z, L0.w, R0.z,
-                                         R0.w, lane, big, sink);
-        direct = false;
-      }
-      const bool pend = ok && (big || r == kLeanFallback);  // wave-uniform: the general kernel's
-      if (HABL == 6 && fast) { ++n_joined; n_hd += hd ? 1u : 0u; }
-      wave_sync();
-      if (direct) {  // (deferred-remove, general or invalid objects) the same two stores, to the sink
-        const u32x4 z = {0u, 0u, 0u, 0u};
-        __builtin_nontemporal_store(z, (u32x4*)sink);
-        __builtin_nontemporal_store(z, (u32x4*)sink + 1);
-      } else {
-        copy_record_out(lds_addr(sL), Ob + oo, pend ? 1u : r, lane);
-      }
-      *(Ooff + cb + t) = oo | (pend ? kPending : 0ull);
-      if (pend) {  // listed for the general kernel (a rare path)
-        if (lane == 0u) {
-          const uint32_t e = atomicAdd(&ctl[0], 1u);
-          if (e < list_cap) list[e] = cb + t;
-        }
-      }
-      // ---- advance
-      if (last) {
-        if (!have_next) break;
-        ++k;
-        cb = ncb;
-        ce = nce;
-        csz = (uint32_t)(ce - cb);
-        offs = noffs;
-        t = 0u;
-        next_known = false;
-        if (!is_static(k + 1u) && lane == 0u) ticket = atomicAdd(&ctl[3], 1u);  // the ticket of the chunk after
-        if (HABL == 6) ++n_chunk;
-      } else {
-        ++t;
-      }
-      lo_t = lo_u;
-      ro_t = ro_u;
-      okp_t = okp_u;
-      wave_sync();  // this object's LDS reads are done
-      stage_used(sL, pl, n16_of(pl), lane);
-      stage_used(sR, pr, n16_of(pr), lane);
-      wave_sync();
-    }
-  }
-  if (HABL == 6 && lane == 0u && wave_id < 10922u) {  // timing only: the list's upper half holds the stamps
-    list[32768u + 3u * wave_id] = ts0;
-    list[32768u + 3u * wave_id + 1u] = __builtin_amdgcn_s_memrealtime();
-    list[32768u + 3u * wave_id + 2u] = ((uint64_t)n_joined << 32) | (n_hd << 16) | n_chunk;
-  }
-}
-
-#endif  // CRDT_DIAG
 
 // ======================================================================
 // General path: objects the fast kernel flagged (records larger than its
@@ -3916,61 +2919,6 @@ __device__ __forceinline__ bool sparse_header_ok(u32x4 h0, u32x4 h1, uint64_t of
          off + sz <= bytes;
 }
 
-#ifdef CRDT_DIAG
-constexpr uint32_t kSpStage = 6144;
-constexpr int kSpWaves = 2;  // waves per block of the sparse kernel (LDS: 2 x (12 KB stage + 7 KB scratch))
-
-template <bool MASK>
-__global__ __launch_bounds__(kWave * kSpWaves) void orswot_merge_sparse_kernel(
-    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
-    const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
-    uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
-    int* __restrict__ status) {
-  __shared__ u32x4 sp_s[kSpWaves][2][kSpStage / 16];
-  __shared__ u32x4 sx_s[kSpWaves][MASK ? kSpScratch / 16 : 1];
-  const uint32_t lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  const uint64_t n_waves = (uint64_t)gridDim.x * kSpWaves;
-  for (uint64_t o = (uint64_t)blockIdx.x * kSpWaves + wave; o < n_obj; o += n_waves) {
-    const uint64_t lo = Loff[o], ro = Roff[o];
-    u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
-    const bool inb = (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes && ro + kHdrBytes <= Rbytes;
-    if (inb) {
-      hl0 = ((const u32x4*)(Lb + lo))[0]; hl1 = ((const u32x4*)(Lb + lo))[1];
-      hr0 = ((const u32x4*)(Rb + ro))[0]; hr1 = ((const u32x4*)(Rb + ro))[1];
-    }
-    const bool ok = inb && sparse_header_ok(hl0, hl1, lo, Lbytes, A) && sparse_header_ok(hr0, hr1, ro, Rbytes, A) &&
-                    lo + ro + (uint64_t)hl0.x + hr0.x <= Obytes;
-    if (lane == 0u) Ooff[o] = lo + ro;
-    if (!ok) {
-      if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
-      continue;
-    }
-    const uint32_t szl = uni(hl0.x), szr = uni(hr0.x);
-    if (szl <= kSpStage && szr <= kSpStage) {
-      u32x4* sl = sp_s[wave][0];
-      u32x4* sr = sp_s[wave][1];
-      wave_sync();
-      for (uint32_t k = lane; k < szl / 16u; k += kWave) sl[k] = __builtin_nontemporal_load((const u32x4*)(Lb + lo) + k);
-      for (uint32_t k = lane; k < szr / 16u; k += kWave) sr[k] = __builtin_nontemporal_load((const u32x4*)(Rb + ro) + k);
-      wave_sync();
-      uint32_t r = kLeanFallback;
-      if (MASK && A <= kSpTableN && uni(hl0.y) <= 64u && uni(hr0.y) <= 64u && uni(hl0.z) <= 64u &&
-          uni(hr0.z) <= 64u && uni(hl0.w) <= 128u && uni(hr0.w) <= 128u && uni(hl1.x) <= 32u && uni(hr1.x) <= 32u) {
-        uint8_t* X = (uint8_t*)sx_s[wave];
-        if ((uni(hl1.x) | uni(hr1.x)) != 0u)
-          r = sparse_mask_object<true>((const uint8_t*)sl, (const uint8_t*)sr, X, Ob + lo + ro, A, uni(hl0.y),
-                                       uni(hl0.z), uni(hl0.w), uni(hr0.y), uni(hr0.z), uni(hr0.w), lane);
-        else
-          r = sparse_mask_object<false>((const uint8_t*)sl, (const uint8_t*)sr, X, Ob + lo + ro, A, uni(hl0.y),
-                                        uni(hl0.z), uni(hl0.w), uni(hr0.y), uni(hr0.z), uni(hr0.w), lane);
-      }
-      if (r == kLeanFallback) merge_object<true>((const uint8_t*)sl, (const uint8_t*)sr, Ob + lo + ro, A, lane);
-    } else {
-      merge_object<true>(Lb + lo, Rb + ro, Ob + lo + ro, A, lane);
-    }
-  }
-}
-#endif  // CRDT_DIAG
 
 // Sparse mask kernel: the dense mask kernel's structure for CSR batches.
 // Lane k of a chunk owns object cbase + k's header; objects that fit the
@@ -4186,7 +3134,7 @@ namespace {
 // The join launch: MODE 3 (one pass) or the two passes MODE 1 + MODE 2,
 // then the general kernel.
 template <int MINW, bool ONE = true, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
-          bool RT = true, uint32_t DYN = 0, bool DK = false, uint32_t SF = 6, bool V10 = false, bool SPEC = false,
+          bool RT = true, uint32_t DYN = 0, bool DK_ = false, uint32_t SF = 6, bool V10_ = false, bool SPEC = false,
           uint32_t GMIN = 0, int IO = 0, int HK = 0, bool PK = false, int BK = 0, bool NM = false, bool PO = false,
           int TCH = 0, int AW = 32>
 int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
@@ -4194,19 +3142,12 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
                        uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
                        uint32_t list_cap, hipStream_t stream, int blocks_per_cu, JoinSeq* js) {
 #ifndef CRDT_DIAG
-  static_assert(HABL == 0 && ONE && !V10 && !DK && PO, "the product launch: one pass, no timing-only ablation");
+  static_assert(HABL == 0 && ONE && PO, "the product launch: one pass, no timing-only ablation");
 #endif
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const void* f1;
   const void* f2 = nullptr;
-#ifdef CRDT_DIAG
-  if constexpr (V10) {
-    f1 = (const void*)orswot_join_v10_kernel<MINW, DYN, SF, HABL>;
-  } else if constexpr (DK) {
-    f1 = (const void*)orswot_join_dyn_kernel<MINW, HABL>;
-  } else
-#endif
   if constexpr (ONE) {
     f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL, RT, DYN, SF, SPEC, GMIN, IO, HK, PK, BK, PO,
                                          TCH, AW>;
@@ -4217,7 +3158,7 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
 #endif
   }
   static std::atomic<int> occ_cache[2][10];  // per (pass, MINW; slot 9: the v9 kernel); HDD variants share one per MINW
-  constexpr int slot = DK || V10 ? 9 : (AW == 64 ? 8 : MINW);
+  constexpr int slot = AW == 64 ? 8 : MINW;
   int occ[2];
   const void* fs[2] = {f1, f2};
   const int passes = ONE ? 1 : 2;
@@ -4365,14 +3306,6 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   if (variant == 212) return go(launch_join_passes<6, true, true, true, true, 0, true, 32, false, 4>);
   if (variant == 213) return go(launch_join_passes<6, true, true, true, true, 0, true, 24, false, 3>);
   if (variant == 214) return go(launch_join_passes<6, true, true, true, true, 0, true, 48, false, 2>);
-  // v10: offsets-only chunk step, blind record prefetch, seamless chunk switch, guided split
-  if (variant == 170) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 6, true>);
-  if (variant == 171) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 4, true>);
-  if (variant == 172) return go(launch_join_passes<6, true, true, true, true, 0, true, 8, false, 6, true>);
-  if (variant == 173) return go(launch_join_passes<6, true, true, true, true, 0, true, 31, false, 8, true>);
-  if (variant == 174) return go(launch_join_passes<6, true, true, true, true, 6, true, 16, false, 6, true>);  // + stamps
-  if (variant == 160) return go(launch_join_passes<6, true, true, true, true, 0, true, 0, true>);  // v9 (dynamic, pipelined)
-  if (variant == 161) return go(launch_join_passes<6, true, true, true, true, 6, true, 0, true>);  // v9 + stamps
   if (variant == 0 || (variant >= 25 && variant <= 35)) {
     switch (variant) {
       case 25: return go(launch_join_passes<4, false>);
@@ -4396,36 +3329,17 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // output is invalid); 11 = the round-1 product (orswot_mask_kernel<6>)
   const void* fn = (const void*)orswot_mask_kernel<6>;
   switch (variant) {
-    case 6: fn = (const void*)orswot_merge_kernel<1, 0, true>; break;
-    case 7: fn = (const void*)orswot_merge_kernel<1, 0, false, 0, true>; break;
-    case 8: fn = (const void*)orswot_merge_kernel<1, 0, false, 0, true, true>; break;
-    case 9: fn = (const void*)orswot_merge_kernel<5, 0, false, 0, true, true>; break;
     case 10: fn = (const void*)orswot_mask_kernel<5>; break;
     case 11: fn = (const void*)orswot_mask_kernel<6>; break;
     case 12: fn = (const void*)orswot_mask_kernel<4>; break;
     case 14: fn = (const void*)orswot_mask_kernel<5, 9>; break;
-    case 15: fn = (const void*)orswot_mask_kernel<5, 0, true>; break;
-    case 16: fn = (const void*)orswot_mask_kernel<5, 9, true>; break;
-    case 17: fn = (const void*)orswot_mask_kernel<4, 0, true>; break;
-    case 18: fn = (const void*)orswot_mask_kernel<6, 0, false, true>; break;
-    case 19: fn = (const void*)orswot_mask_kernel<7, 0, false, true>; break;
-    case 20: fn = (const void*)orswot_mask_kernel<5, 0, false, true>; break;
-    case 21: fn = (const void*)orswot_mask_kernel<4, 0, false, true>; break;
-    case 22: fn = (const void*)orswot_mask_kernel<7, 0, false, true, true>; break;
-    case 23: fn = (const void*)orswot_mask_kernel<5, 0, false, true, true>; break;
-    case 24: fn = (const void*)orswot_mask_kernel<6, 0, false, true, true>; break;
-    case 111: fn = (const void*)orswot_merge_kernel<1, 0, true, 1>; break;
-    case 112: fn = (const void*)orswot_merge_kernel<1, 0, true, 2>; break;
-    case 113: fn = (const void*)orswot_merge_kernel<1, 0, true, 3>; break;
-    case 2: fn = (const void*)orswot_merge_kernel<2, 0>; break;
-    case 3: fn = (const void*)orswot_merge_kernel<3, 0>; break;
-    case 4: fn = (const void*)orswot_merge_kernel<4, 0>; break;
-    case 101: fn = (const void*)orswot_merge_kernel<4, 1>; break;
-    case 102: fn = (const void*)orswot_merge_kernel<4, 2>; break;
-    case 103: fn = (const void*)orswot_merge_kernel<4, 3>; break;
-    case 109: fn = (const void*)orswot_merge_kernel<4, 9>; break;
-    case 1: fn = (const void*)orswot_merge_kernel<1, 0>; break;
-    case 13: fn = (const void*)orswot_merge_kernel<1, 0, false, 0, true>; break;
+    case 18: fn = (const void*)orswot_mask_kernel<6, 0, true>; break;
+    case 19: fn = (const void*)orswot_mask_kernel<7, 0, true>; break;
+    case 20: fn = (const void*)orswot_mask_kernel<5, 0, true>; break;
+    case 21: fn = (const void*)orswot_mask_kernel<4, 0, true>; break;
+    case 22: fn = (const void*)orswot_mask_kernel<7, 0, true, true>; break;
+    case 23: fn = (const void*)orswot_mask_kernel<5, 0, true, true>; break;
+    case 24: fn = (const void*)orswot_mask_kernel<6, 0, true, true>; break;
     default: break;
   }
   // Resident grid: the kernel's occupancy in 4-wave blocks per CU
@@ -4467,18 +3381,6 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
 #ifdef CRDT_DIAG
-  if (sparse_variant == 1 || sparse_variant == 2) {  // one wave per object (1: no mask join)
-    const void* fn = sparse_variant == 1 ? (const void*)orswot_merge_sparse_kernel<false>
-                                          : (const void*)orswot_merge_sparse_kernel<true>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kSpWaves, 0) != hipSuccess || occ < 1)
-      occ = 4;
-    const uint64_t want = (n_obj + kSpWaves - 1) / kSpWaves;
-    const uint64_t cap = (uint64_t)cus * occ;
-    const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
-    void* args[] = {&Lb, &Loff, &Lbytes, &Rb, &Roff, &Rbytes, &Ob, &Ooff, &Obytes, &n_obj, &n_actors, &status};
-    return hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kSpWaves), args, 0, stream) == hipSuccess ? CRDT_OK
-                                                                                                         : CRDT_EHIP;
-  }
   const void* fn = sparse_variant == 4 ? (const void*)orswot_sparse_mask_kernel<3, 9>
                    : sparse_variant == 5 ? (const void*)orswot_sparse_mask_kernel<3, 0, 20, 5>
                    : sparse_variant == 6 ? (const void*)orswot_sparse_mask_kernel<3, 0, 24, 4>
