@@ -90,9 +90,10 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
     }
     // every value count within mcap and deferred set size within scap (the
     // loops below read mv_n / dset_n slots of the slab row as counts)
-    bool bad = false;
-    for (uint32_t k = lane; k < nS; k += kMpW) bad = bad || S.mv_n[i * S.kcap + k] > S.mcap;
-    for (uint32_t k = lane; k < nO; k += kMpW) bad = bad || O.mv_n[i * O.kcap + k] > O.mcap;
+    // (kcap <= 32: lane k holds key k's value count, which the value-row stage
+    // below reads by readlane — no dependent load on the per-key chain)
+    const uint32_t vnS = lane < nS ? S.mv_n[i * S.kcap + lane] : 0u, vnO = lane < nO ? O.mv_n[i * O.kcap + lane] : 0u;
+    bool bad = vnS > S.mcap || vnO > O.mcap;
     for (uint32_t k = lane; k < dS; k += kMpW) bad = bad || S.dset_n[i * S.dcap + k] > S.scap;
     for (uint32_t k = lane; k < dO; k += kMpW) bad = bad || O.dset_n[i * O.dcap + k] > O.scap;
     if (__ballot(bad) != 0ull) {
@@ -127,8 +128,9 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
       const uint64_t key = hs ? ka : kb;
       const uint64_t ia = i * S.kcap + a, ib = i * O.kcap + b;
       const uint64_t eS = hs ? rowv(S.eclock, ia, A, lane) : 0ull, eO = ho ? rowv(O.eclock, ib, A, lane) : 0ull;
-      if (VS) {  // stage the key's value rows: every load in flight, then the LDS stores
-        const uint32_t n0 = hs ? S.mcap * A : 0u, n1 = ho ? O.mcap * A : 0u;
+      if (VS) {  // stage the key's used value rows: every load in flight, then the LDS stores
+        const uint32_t n0 = hs ? (uint32_t)__builtin_amdgcn_readlane(vnS, a) * A : 0u;
+        const uint32_t n1 = ho ? (uint32_t)__builtin_amdgcn_readlane(vnO, b) * A : 0u;
         uint64_t x0 = 0, x1 = 0, y0 = 0, y1 = 0;
         if (lane < n0) x0 = S.mv_clock[ia * S.mcap * A + lane];
         if (lane + kMpW < n0) x1 = S.mv_clock[ia * S.mcap * A + lane + kMpW];
