@@ -445,6 +445,26 @@ class Engine:
             self.status(stream)
         return out
 
+    def orswot_fold(self, batches, out: OrswotBatch | None = None, stream=None, check_status=True):
+        """((b0 ⊔ b1) ⊔ b2) ⊔ ... of CSR-clock batches of the same objects
+        (crdt_orswot_fold: the fused replica fold, no intermediate batch in
+        HBM). Returns an OrswotBatch (`out`, reused, when given: at least the
+        batches' bytes together and n_obj offsets)."""
+        torch = _torch()
+        B0 = batches[0]
+        total = sum(B.bytes for B in batches)
+        if out is None:
+            out = OrswotBatch(torch.empty(max(16, total), dtype=torch.uint8, device=B0.base.device),
+                              torch.empty(B0.n_obj, dtype=torch.int64, device=B0.base.device), B0.n_actors,
+                              max(16, total), B0.flags)
+        arr = (Batch * len(batches))(*[B.cbatch() for B in batches])
+        check(lib.crdt_orswot_fold(self.ctx, arr, len(batches), B0.n_actors, B0.flags,
+                                   C.c_void_p(out.base.data_ptr()), C.c_void_p(out.off.data_ptr()), out.bytes,
+                                   self._stream(stream)), "orswot_fold")
+        if check_status:
+            self.status(stream)
+        return out
+
     def orswot_validate(self, B: OrswotBatch, stream=None):
         b = B.cbatch()
         check(lib.crdt_orswot_validate_ex(self.ctx, C.byref(b), B.n_actors, B.flags, self._stream(stream)),

@@ -276,6 +276,32 @@ int crdt_orswot_merge_ex(crdt_ctx* ctx, const crdt_orswot_batch* self, const crd
                              ctx->blocks_per_cu, ctx->variant, &ctx->join_seq);
 }
 
+int crdt_orswot_fold(crdt_ctx* ctx, const crdt_orswot_batch* reps, uint32_t n_reps, uint32_t n_actors,
+                     uint32_t flags, uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes, void* stream) {
+  if (!ctx || !reps || n_reps == 0 || n_reps > kFoldMaxReps || n_actors == 0) return CRDT_EINVAL;
+  if (flags != CRDT_ORSWOT_SPARSE_CLOCK) return CRDT_EINVAL;  // the fused fold is the CSR form's (header)
+  const size_t n = reps[0].n_obj;
+  size_t total = 0;
+  const uint8_t* bases[kFoldMaxReps];
+  const uint64_t* offs[kFoldMaxReps];
+  uint64_t bytes[kFoldMaxReps];
+  for (uint32_t r = 0; r < n_reps; ++r) {
+    if (reps[r].n_obj != n) return CRDT_EINVAL;
+    if (n && (!reps[r].base || !reps[r].off || !aligned16(reps[r].base))) return CRDT_EINVAL;
+    bases[r] = reps[r].base;
+    offs[r] = reps[r].off;
+    bytes[r] = reps[r].bytes;
+    total += reps[r].bytes;
+  }
+  if (n == 0) return CRDT_OK;
+  if (!d_out || !d_out_off || !aligned16(d_out)) return CRDT_EINVAL;
+  if (out_bytes < total) return CRDT_ECAPACITY;
+  int rc = set_device(ctx);
+  if (rc || (rc = ctx_big_scratch(ctx, fold_scratch_bytes()))) return rc;
+  return launch_orswot_fold_sparse(bases, offs, bytes, n_reps, n, d_out, d_out_off, n_actors, ctx->d_status,
+                                   ctx->d_ctl, ctx->d_list, ctx->list_cap, ctx->d_big, S(stream));
+}
+
 int crdt_orswot_validate(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32_t n_actors,
                          void* stream) {
   return crdt_orswot_validate_ex(ctx, batch, n_actors, 0u, stream);
