@@ -149,7 +149,7 @@ def test_map_orswot_200_keys_100_actors(gpu, oracle):
     import crdts_hip
 
     A100 = 100
-    caps = dict(kcap=256, mcap=8, vdcap=8, vscap=8, dcap=32, scap=64)
+    caps = dict(kcap=512, mcap=8, vdcap=8, vscap=8, dcap=32, scap=64)
     L, R = oracle.map_orswot_generate(0x200A, 48, A100, keys=400, members=6, ops=450, pct_future=20, caps=caps)
     assert (L.a["n_keys"] >= 200).sum() > 10 and L.a["clock"][:, 64:].any()
     assert L.a["vn_def"].sum() > 20 and L.a["n_def"].sum() > 10
