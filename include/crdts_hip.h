@@ -231,16 +231,12 @@ typedef struct crdt_orswot_batch {
  * out[i] := self[i].merge(&other[i])   — src/orswot.rs:87-157 incl.
  * apply_deferred (:235-243) / apply_remove (:195-211).
  *
- * The output record i is written at d_out_base + d_out_off[i] (written by the
- * kernel), where d_out_off[i] <= self.off[i] + other.off[i]: consecutive
- * records are packed back to back (d_out_off[i+1] = d_out_off[i] + size[i])
- * wherever the kernel joins both objects in one pass, and a record that
- * follows one it did not is placed at its own self.off + other.off. Because a
+ * The output record i is written at d_out_base + d_out_off[i] where
+ * d_out_off[i] := self.off[i] + other.off[i] (written by the kernel). Because a
  * merged record is never larger than the two inputs together, the output
  * needs at most self.bytes + other.bytes bytes and no prefix scan: the output
- * batch (d_out_base, d_out_off) is itself a valid input batch (records in
- * object order, not overlapping; it may have gaps between records, which
- * crdt_orswot_compact removes).
+ * batch (d_out_base, d_out_off) is itself a valid input batch (it may have
+ * gaps between records; crdt_orswot_compact removes them).
  * PRECONDITION (checked on the device; a violation latches CRDT_EINVAL and
  * the offending objects are not written): on each side the records are in
  * increasing offset order and do not overlap, off[i] + size[i] <= off[i+1],
