@@ -272,17 +272,15 @@ int crdt_orswot_merge_host(crdt_ctx* ctx, const uint8_t* h_self_base,
 /* The replica fold, batched: out[i] := ((reps[0][i] ⊔ reps[1][i]) ⊔ reps[2][i])
  * ⊔ ... ⊔ reps[n_reps-1][i] — Orswot::merge (src/orswot.rs:87-157) in rank
  * order, the fold of replica anti-entropy (BASELINE.json configs[4]) — over
- * n_reps <= 16 batches of the same n_obj objects, byte-equal to n_reps - 1
- * crdt_orswot_merge_ex calls. CSR-clock batches only (flags =
- * CRDT_ORSWOT_SPARSE_CLOCK; dense batches: CRDT_EINVAL). The fold runs fused:
- * one wave folds an object's records in sequence with the accumulator in
- * LDS, so no intermediate record is written to HBM (records past 4 KB, or
- * steps past the mask join's limits, take a general per-object path). Output
+ * n_reps batches of the same n_obj objects: n_reps - 1 batched merges
+ * (crdt_orswot_merge_ex) with the intermediate batches in a context-owned
+ * buffer. flags: 0 (dense top clocks) or CRDT_ORSWOT_SPARSE_CLOCK. Output
  * record i at d_out_off[i] := sum_r reps[r].off[i] (written by the call);
  * out_bytes >= sum_r reps[r].bytes. Each batch: records in increasing offset
- * order, not overlapping (as crdt_orswot_merge). The general path keeps an
- * object's intermediate records of up to 256 KB (a larger one latches
- * CRDT_ECAPACITY). */
+ * order, not overlapping (as crdt_orswot_merge). (A fused form — one wave
+ * folding an object's records with the accumulator in LDS, no intermediate
+ * batch in HBM — measured slower on config 5: the fold is bound by the joins,
+ * not by the intermediate bytes; DESIGN.md.) */
 int crdt_orswot_fold(crdt_ctx* ctx, const crdt_orswot_batch* reps, uint32_t n_reps, uint32_t n_actors,
                      uint32_t flags, uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes, void* stream);
 

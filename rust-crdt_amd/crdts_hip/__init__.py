@@ -446,9 +446,9 @@ class Engine:
         return out
 
     def orswot_fold(self, batches, out: OrswotBatch | None = None, stream=None, check_status=True):
-        """((b0 ⊔ b1) ⊔ b2) ⊔ ... of CSR-clock batches of the same objects
-        (crdt_orswot_fold: the fused replica fold, no intermediate batch in
-        HBM). Returns an OrswotBatch (`out`, reused, when given: at least the
+        """((b0 ⊔ b1) ⊔ b2) ⊔ ... of batches of the same objects (crdt_orswot_fold:
+        the rank-order fold of replica anti-entropy, R - 1 batched merges).
+        Returns an OrswotBatch (`out`, reused, when given: at least the
         batches' bytes together and n_obj offsets)."""
         torch = _torch()
         B0 = batches[0]

@@ -108,6 +108,7 @@ int crdt_ctx_destroy(crdt_ctx* ctx) {
   (void)crdt_comm_destroy(ctx);
   (void)hipFree(ctx->d_big);
   (void)hipFree(ctx->d_arena);
+  (void)hipFree(ctx->d_fold);
   (void)hipFree(ctx->d_status);
   delete ctx;
   return CRDT_OK;
@@ -278,28 +279,60 @@ int crdt_orswot_merge_ex(crdt_ctx* ctx, const crdt_orswot_batch* self, const crd
 
 int crdt_orswot_fold(crdt_ctx* ctx, const crdt_orswot_batch* reps, uint32_t n_reps, uint32_t n_actors,
                      uint32_t flags, uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes, void* stream) {
-  if (!ctx || !reps || n_reps == 0 || n_reps > kFoldMaxReps || n_actors == 0) return CRDT_EINVAL;
-  if (flags != CRDT_ORSWOT_SPARSE_CLOCK) return CRDT_EINVAL;  // the fused fold is the CSR form's (header)
+  if (!ctx || !reps || n_reps == 0 || n_actors == 0 || (flags & ~CRDT_ORSWOT_SPARSE_CLOCK)) return CRDT_EINVAL;
   const size_t n = reps[0].n_obj;
   size_t total = 0;
-  const uint8_t* bases[kFoldMaxReps];
-  const uint64_t* offs[kFoldMaxReps];
-  uint64_t bytes[kFoldMaxReps];
   for (uint32_t r = 0; r < n_reps; ++r) {
     if (reps[r].n_obj != n) return CRDT_EINVAL;
     if (n && (!reps[r].base || !reps[r].off || !aligned16(reps[r].base))) return CRDT_EINVAL;
-    bases[r] = reps[r].base;
-    offs[r] = reps[r].off;
-    bytes[r] = reps[r].bytes;
     total += reps[r].bytes;
   }
   if (n == 0) return CRDT_OK;
   if (!d_out || !d_out_off || !aligned16(d_out)) return CRDT_EINVAL;
   if (out_bytes < total) return CRDT_ECAPACITY;
   int rc = set_device(ctx);
-  if (rc || (rc = ctx_big_scratch(ctx, fold_scratch_bytes()))) return rc;
-  return launch_orswot_fold_sparse(bases, offs, bytes, n_reps, n, d_out, d_out_off, n_actors, ctx->d_status,
-                                   ctx->d_ctl, ctx->d_list, ctx->list_cap, ctx->d_big, S(stream));
+  if (rc) return rc;
+  hipStream_t st = S(stream);
+  if (n_reps == 1) {  // the batch itself, at its own offsets
+    if (hipMemcpyAsync(d_out, reps[0].base, reps[0].bytes, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_out_off, reps[0].off, 8 * n, hipMemcpyDeviceToDevice, st) != hipSuccess)
+      return CRDT_EHIP;
+    return launch_orswot_validate(d_out, d_out_off, out_bytes, n, n_actors, flags, ctx->d_status, st);
+  }
+  // intermediate batches: two of the first n_reps - 1 batches' bytes together
+  // (an accumulator never outgrows its inputs) plus their offsets
+  const size_t acc_cap = (total - reps[n_reps - 1].bytes + 255) & ~size_t(255);
+  const size_t need = 2 * acc_cap + 2 * ((8 * n + 255) & ~size_t(255));
+  if (n_reps > 2 && ctx->fold_bytes < need) {
+    (void)hipFree(ctx->d_fold);
+    ctx->d_fold = nullptr;
+    ctx->fold_bytes = 0;
+    if (hipMalloc(&ctx->d_fold, need) != hipSuccess) return CRDT_EHIP;
+    ctx->fold_bytes = need;
+  }
+  uint8_t* buf[2] = {ctx->d_fold, ctx->d_fold + acc_cap};
+  uint64_t* boff[2] = {(uint64_t*)(ctx->d_fold + 2 * acc_cap),
+                       (uint64_t*)(ctx->d_fold + 2 * acc_cap + ((8 * n + 255) & ~size_t(255)))};
+  const uint8_t* acc = reps[0].base;
+  const uint64_t* acc_off = reps[0].off;
+  uint64_t acc_bytes = reps[0].bytes;
+  for (uint32_t r = 1; r < n_reps && !rc; ++r) {  // ((r0 ⊔ r1) ⊔ r2) ⊔ ..., each step one batched merge
+    const bool last = r + 1 == n_reps;
+    uint8_t* o = last ? d_out : buf[r & 1u];
+    uint64_t* oo = last ? d_out_off : boff[r & 1u];
+    const uint64_t cap = last ? out_bytes : acc_bytes + reps[r].bytes;
+    rc = (flags & CRDT_ORSWOT_SPARSE_CLOCK)
+             ? launch_orswot_merge_sparse(acc, acc_off, acc_bytes, reps[r].base, reps[r].off, reps[r].bytes, o, oo,
+                                          cap, n, n_actors, ctx->d_status, ctx->d_ctl, ctx->d_list, ctx->list_cap,
+                                          st, 0, &ctx->join_seq)
+             : launch_orswot_merge(acc, acc_off, acc_bytes, reps[r].base, reps[r].off, reps[r].bytes, o, oo, cap, n,
+                                   n_actors, ctx->d_status, ctx->d_ctl, ctx->d_list, ctx->list_cap, st, 0, 0,
+                                   &ctx->join_seq);
+    acc = o;
+    acc_off = oo;
+    acc_bytes = cap;
+  }
+  return rc;
 }
 
 int crdt_orswot_validate(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32_t n_actors,

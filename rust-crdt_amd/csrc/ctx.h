@@ -48,6 +48,9 @@ struct crdt_ctx {
   size_t big_bytes = 0;
   // host synchronisations made by the replica joins so far (crdt_ctx_host_syncs)
   uint64_t host_syncs = 0;
+  // crdt_orswot_fold's intermediate batches (two, ping-pong), grown on demand
+  uint8_t* d_fold = nullptr;
+  size_t fold_bytes = 0;
 };
 
 // Ensures ctx->d_big holds at least `bytes` (api.hip).

@@ -19,14 +19,6 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
                         uint64_t* list, uint32_t list_cap, hipStream_t stream, int blocks_per_cu,
                         int variant, JoinSeq* js);
 
-// The fused replica fold of R <= kFoldMaxReps CSR-clock batches (orswot_merge.hip);
-// scratch: fold_scratch_bytes() of HBM (the general path's intermediate records).
-constexpr uint32_t kFoldMaxReps = 16;
-size_t fold_scratch_bytes();
-int launch_orswot_fold_sparse(const uint8_t* const* bases, const uint64_t* const* offs, const uint64_t* bytes,
-                              uint32_t R, uint64_t n_obj, uint8_t* Ob, uint64_t* Ooff,
-                              uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list, uint32_t list_cap,
-                              uint8_t* scratch, hipStream_t stream);
 int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                                const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
                                uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,

@@ -3137,268 +3137,6 @@ __global__ __launch_bounds__(kWave) void orswot_sparse_general_kernel(
 }
 
 
-// ======================================================================
-// Fused replica fold (config 5, BASELINE.json configs[4]): out[i] =
-// ((r0[i] ⊔ r1[i]) ⊔ r2[i]) ⊔ ... over R batches of CSR-clock records, each
-// step Orswot::merge (src/orswot.rs:87-157) — the rank-order fold of the
-// replica join. One wave folds an object's R records in sequence with the
-// accumulator held in the LDS pair stage: each step's output is assembled
-// over the stage (sparse_mask_object ASM) and the next replica's record is
-// staged right behind it, so the R - 2 intermediate records never go to HBM
-// (the fold's bytes drop from Σ_steps (acc + rep + out) to Σ reps + out).
-// The next record of the sequence — the object's next replica, or the next
-// object's first — is in flight in registers during each step; its extent is
-// taken from the next object's offset in that batch (the placement rule), so
-// no header read precedes it. A step with deferred removes on either side
-// writes its output to the object's output slot (the walk over the deferred
-// clocks reads the stages) and reads it back. An object a step cannot take
-// (a record past 4 KB, the pair past the stage, the mask join's limits) is
-// listed for orswot_sparse_fold_general_kernel, which folds it from the start
-// one wave per object with the general join. Output record i is written at
-// Σ_r r.off[i] (never larger than the inputs together).
-// ======================================================================
-struct FoldPtrs {  // a kernel argument (the kernarg segment; lanes index it by replica)
-  const uint8_t* b[kFoldMaxReps];
-  const uint64_t* off[kFoldMaxReps];
-  uint64_t bytes[kFoldMaxReps];
-};
-constexpr uint32_t kFoldPer = 4;  // 16-B pieces per lane of a record in flight (<= 4 KB)
-
-__device__ __forceinline__ void fold_fetch(u32x4 (&r)[kFoldPer], const uint8_t* src, uint32_t n16, uint32_t lane) {
-  if (n16 == 0u) return;  // (no record there: nothing is staged either)
-  const uint32_t last = n16 - 1u;
-#pragma unroll
-  for (uint32_t k = 0; k < kFoldPer; ++k) {
-    const uint32_t idx = lane + k * kWave;
-    r[k] = __builtin_nontemporal_load((const u32x4*)src + (idx < last ? idx : last));
-  }
-}
-__device__ __forceinline__ void fold_stage(u32x4* dst, const u32x4 (&r)[kFoldPer], uint32_t n16, uint32_t lane) {
-#pragma unroll
-  for (uint32_t k = 0; k < kFoldPer; ++k)
-    if (lane + k * kWave < n16) dst[lane + k * kWave] = r[k];
-}
-// sparse_header_ok of a record staged in LDS at byte offset `at`, extent `ext` bytes
-__device__ __forceinline__ bool fold_header(const uint8_t* S, uint32_t at, uint64_t ext, uint32_t A, u32x4& h0,
-                                            u32x4& h1) {
-  const u32x4* h = (const u32x4*)(S + at);
-  h0 = u32x4{uni(h[0].x), uni(h[0].y), uni(h[0].z), uni(h[0].w)};
-  h1 = u32x4{uni(h[1].x), uni(h[1].y), uni(h[1].z), uni(h[1].w)};
-  return sparse_header_ok(h0, h1, 0u, ext, A);
-}
-
-template <int MINW, uint32_t DYN = 16, uint32_t SF = 5>
-__global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_fold_kernel(
-    const FoldPtrs F, uint32_t R, uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff,
-    uint64_t n_obj, uint32_t A, int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list,
-    uint32_t list_cap) {
-  __shared__ u32x4 pair_s[kWavesPerBlock][kSpPair / 16];
-  __shared__ u32x4 scr_s[kWavesPerBlock][kSpScratch / 16];
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint32_t wave = uni(threadIdx.x / kWave);
-  u32x4* const S = pair_s[wave];
-  const uint8_t* const Su8 = (const uint8_t*)S;
-  uint8_t* const X = (uint8_t*)scr_s[wave];
-  const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
-  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
-  // lane r < R: replica r's offsets and base; lane 16 + r: replica r's offsets
-  // again, for the bound of a record (the next object's offset, or the batch end)
-  const uint32_t rr = lane & 15u;
-  const bool rl = rr < R && lane < 32u;
-  const uint64_t* const offp = rl ? F.off[rr] : nullptr;
-  const uint64_t basev = rl ? (uint64_t)F.b[rr] : 0ull;
-  const uint64_t endv = rl ? F.bytes[rr] : 0ull;
-  auto offs = [&](uint64_t i) -> uint64_t {  // lane r: r.off[i]; lane 16 + r: the end bound of that record
-    uint64_t v = 0ull;
-    if (rl) v = lane < 16u ? offp[i] : (i + 1u < n_obj ? offp[i + 1u] : endv);
-    return v;
-  };
-  // record r of the object whose offsets are in ov: its address and 16-B pieces (<= 4 KB staged)
-  auto rec_of = [&](uint64_t ov, uint32_t r, const uint8_t*& p, uint64_t& ext) {
-    const uint64_t o = lane_of64(ov, r), e0 = lane_of64(ov, 16u + r), end = lane_of64(endv, r);
-    const uint64_t e = e0 < end ? e0 : end;  // within the batch whatever the offsets hold
-    ext = e > o && (o & 15u) == 0u ? e - o : 0ull;
-    p = (const uint8_t*)lane_of64(basev, r) + o;
-  };
-  auto pieces = [](uint64_t ext) -> uint32_t { return ext >= 4096u ? 256u : (uint32_t)(ext / 16u); };
-  GuidedSplit<DYN, SF> gs(n_obj, wave_id, n_waves);
-  uint64_t cb = 0, ce = 0;
-  u32x4 pf[kFoldPer];
-  while (gs.next(cb, ce, &ctl[3], lane)) {
-    uint64_t i = cb, ov = offs(cb), ovn = cb + 1u < ce ? offs(cb + 1u) : 0ull;
-    const uint8_t* pin;
-    uint64_t ext;
-    rec_of(ov, 0u, pin, ext);
-    uint32_t nin = pieces(ext);
-    fold_fetch(pf, pin, nin, lane);
-    uint64_t nat = 0ull;
-    for (uint32_t r = 0; r < R; ++r) nat += lane_of64(ov, r);
-    uint32_t r = 0u, sa = 0u;
-    bool dead = false, bad = false;
-    uint64_t extc = ext;  // extent of the record in flight
-    u32x4 a0 = {0, 0, 0, 0}, a1 = a0;  // the accumulator's header
-    for (;;) {
-      // ---- stage the record in flight at the end of the accumulator
-      const uint32_t at = r == 0u ? 0u : sa;
-      const bool room = !dead && at + 16u * nin <= kSpPair && nin >= 2u;
-      wave_sync();
-      if (room) fold_stage(S + at / 16u, pf, nin, lane);
-      wave_sync();
-      // ---- the next record of the sequence into flight
-      uint32_t rn = r + 1u;
-      uint64_t inext = i;
-      if (rn == R) { rn = 0u; inext = i + 1u; }
-      const bool more = inext < ce;
-      uint64_t extn = 0ull;
-      if (more) {
-        const uint8_t* pn;
-        rec_of(rn == 0u ? ovn : ov, rn, pn, extn);
-        fold_fetch(pf, pn, pieces(extn), lane);
-      }
-      // ---- step r of object i
-      if (!dead) {
-        u32x4 h0, h1;
-        if (!room) {
-          // a record the stage cannot take: malformed (too short) or too large
-          dead = true;
-          bad = nin < 2u;
-        } else if (!fold_header(Su8, at, extc, A, h0, h1)) {
-          dead = bad = true;
-        } else if (h0.x > 16u * nin) {  // a record past the 4 KB in flight
-          dead = true;
-        } else if (r == 0u) {
-          a0 = h0;
-          a1 = h1;
-          sa = h0.x;
-          if (R == 1u) {  // a single replica: the record itself
-            for (uint32_t k = lane; k < sa / 16u; k += kWave) __builtin_nontemporal_store(S[k], (u32x4*)(Ob + nat) + k);
-          }
-        } else {
-          const bool fits = sa + h0.x <= kSpPair && A <= kSpTableN && a0.y <= 64u && h0.y <= 64u && a0.z <= 64u &&
-                            h0.z <= 64u && a0.w <= 128u && h0.w <= 128u && a1.x <= 32u && h1.x <= 32u;
-          if (!fits) {
-            dead = true;
-          } else {
-            const bool last = r + 1u == R;
-            uint32_t res;
-            if ((a1.x | h1.x) != 0u) {  // deferred removes: out to the output slot, then back into the stage
-              res = sparse_mask_object<true>(Su8, Su8 + at, X, Ob + nat, A, a0.y, a0.z, a0.w, h0.y, h0.z, h0.w, lane);
-              if (res != kLeanFallback && !last) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                wave_sync();
-                for (uint32_t k = lane; k < res; k += kWave) S[k] = ((const u32x4*)(Ob + nat))[k];
-              }
-            } else {
-              res = sparse_mask_object<false, 0, true>(Su8, Su8 + at, X, last ? Ob + nat : nullptr, A, a0.y, a0.z,
-                                                       a0.w, h0.y, h0.z, h0.w, lane);
-            }
-            if (res == kLeanFallback) {
-              dead = true;
-            } else {
-              sa = 16u * res;
-              wave_sync();
-              const u32x4* h = (const u32x4*)Su8;  // the new accumulator's header (in the stage)
-              a0 = u32x4{uni(h[0].x), uni(h[0].y), uni(h[0].z), uni(h[0].w)};
-              a1 = u32x4{uni(h[1].x), uni(h[1].y), uni(h[1].z), uni(h[1].w)};
-            }
-          }
-        }
-      }
-      if (r + 1u == R) {  // object i done: its slot, or listed for the general fold
-        if (lane == 0u) Ooff[i] = nat | (dead && !bad ? kPending : 0ull);
-        if (bad && lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
-        if (dead && !bad && lane == 0u) {
-          const uint32_t e = atomicAdd(&ctl[0], 1u);
-          if (e < list_cap) list[e] = i;
-          else ctl[1] = 1u;  // the general fold scans the flags
-        }
-        if (!more) break;
-        i = inext;
-        ov = ovn;
-        ovn = i + 1u < ce ? offs(i + 1u) : 0ull;
-        nat = 0ull;
-        for (uint32_t q = 0; q < R; ++q) nat += lane_of64(ov, q);
-        dead = bad = false;
-        sa = 0u;
-      }
-      r = rn;
-      nin = pieces(extn);
-      extc = extn;
-    }
-  }
-}
-
-// The fold's general path: one wave per listed object, folded from its first
-// replica with sparse_join_ptrs (8 KB LDS stages when both records fit, else
-// from HBM), the intermediate records in the wave's two HBM buffers of
-// kFoldScratch bytes (a larger accumulator latches CRDT_ECAPACITY), the last
-// step into the object's output slot.
-constexpr uint64_t kFoldScratch = 1ull << 18;
-constexpr uint32_t kFoldGenBlocks = 256;
-__global__ __launch_bounds__(kWave) void orswot_sparse_fold_general_kernel(
-    const FoldPtrs F, uint32_t R, uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff,
-    uint64_t n_obj, uint32_t A, int* __restrict__ status, const uint32_t* __restrict__ ctl,
-    const uint64_t* __restrict__ list, uint32_t list_cap, uint8_t* __restrict__ scratch) {
-  __shared__ u32x4 gen_s[2][kGenStage / 16];
-  __shared__ u32x4 gx_s[kSpScratch / 16];
-  const uint32_t lane = threadIdx.x;
-  uint8_t* const buf[2] = {scratch + 2ull * kFoldScratch * blockIdx.x, scratch + (2ull * blockIdx.x + 1u) * kFoldScratch};
-  const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  const uint32_t scan = uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  // record r of object i, its header checked against its batch and the next object's record
-  auto rec_ok = [&](uint32_t r, uint64_t i) -> const uint8_t* {
-    const uint64_t o = F.off[r][i], e = i + 1u < n_obj ? F.off[r][i + 1u] : F.bytes[r];
-    if ((o & 15u) || o + kHdrBytes > F.bytes[r]) return nullptr;
-    const u32x4* h = (const u32x4*)(F.b[r] + o);
-    const u32x4 h0 = h[0], h1 = h[1];
-    return sparse_header_ok(h0, h1, o, F.bytes[r], A) && o + h0.x <= e ? F.b[r] + o : nullptr;
-  };
-  auto fold_one = [&](uint64_t i) {
-    const uint64_t oo = Ooff[i] & ~kPending;
-    const uint8_t* acc = rec_ok(0u, i);
-    if (acc == nullptr) {
-      if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
-      return;
-    }
-    uint64_t acc_size = *(const uint32_t*)acc;
-    if (R == 1u) {  // a single replica: the record itself
-      for (uint32_t k = lane; k < acc_size / 16u; k += kWave) ((u32x4*)(Ob + oo))[k] = ((const u32x4*)acc)[k];
-    }
-    for (uint32_t r = 1; r < R; ++r) {
-      const uint8_t* rec = rec_ok(r, i);
-      if (rec == nullptr) {
-        if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
-        return;
-      }
-      const uint64_t rs = *(const uint32_t*)rec;
-      uint8_t* const o = r + 1u == R ? Ob + oo : buf[r & 1u];
-      if (r + 1u < R && acc_size + rs > kFoldScratch) {
-        if (lane == 0u) atomicCAS(status, 0, CRDT_ECAPACITY);
-        return;
-      }
-      sparse_join_ptrs(acc, rec, o, A, gen_s[0], gen_s[1], (uint8_t*)gx_s, lane);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the output is read back by this wave next
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      wave_sync();
-      acc = o;
-      acc_size = *(const uint32_t*)o;
-    }
-    if (lane == 0u) Ooff[i] = oo;
-  };
-  if (n <= list_cap && scan == 0u) {
-    for (uint32_t e = blockIdx.x; e < n; e += gridDim.x) fold_one(list[e]);
-  } else {
-    const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
-    for (uint64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
-      const uint64_t obj = chunk * kWave + lane;
-      const uint64_t oo = obj < n_obj ? Ooff[obj] : 0ull;
-      for (uint64_t pend = __ballot((oo & kPending) != 0ull); pend; pend &= pend - 1)
-        fold_one(chunk * kWave + (uint32_t)__builtin_ctzll(pend));
-    }
-  }
-}
-
 }  // namespace
 
 namespace {
@@ -3708,45 +3446,5 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
   return CRDT_OK;
 }
 
-
-size_t fold_scratch_bytes() { return 2ull * kFoldScratch * kFoldGenBlocks; }
-
-// The fused fold of R <= kFoldMaxReps CSR batches, then its general path for
-// the listed objects.
-int launch_orswot_fold_sparse(const uint8_t* const* bases, const uint64_t* const* offs, const uint64_t* bytes,
-                              uint32_t R, uint64_t n_obj, uint8_t* Ob, uint64_t* Ooff,
-                              uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list, uint32_t list_cap,
-                              uint8_t* scratch, hipStream_t stream) {
-  if (n_obj == 0) return CRDT_OK;
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess)
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const void* fn = (const void*)orswot_sparse_fold_kernel<3>;
-  static std::atomic<int> occ_cache{0};
-  int occ = occ_cache.load(std::memory_order_relaxed);
-  if (occ == 0) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)
-      occ = 2;
-    occ_cache.store(occ, std::memory_order_relaxed);
-  }
-  const uint64_t chunks = (n_obj + kWave - 1) / kWave;
-  const uint64_t want = (chunks + kWavesPerBlock - 1) / kWavesPerBlock;
-  const uint64_t cap = (uint64_t)cus * occ;
-  const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
-  if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
-  if (R == 0u || R > kFoldMaxReps) return CRDT_EINVAL;
-  FoldPtrs F{};
-  for (uint32_t r = 0; r < R; ++r) {
-    F.b[r] = bases[r];
-    F.off[r] = offs[r];
-    F.bytes[r] = bytes[r];
-  }
-  void* args[] = {&F, &R, &Ob, &Ooff, &n_obj, &n_actors, &status, &ctl, &list, &list_cap};
-  if (hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) != hipSuccess)
-    return CRDT_EHIP;
-  hipLaunchKernelGGL(orswot_sparse_fold_general_kernel, dim3(kFoldGenBlocks), dim3(kWave), 0, stream, F, R, Ob, Ooff,
-                     n_obj, n_actors, status, ctl, list, list_cap, scratch);
-  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
-}
 
 }  // namespace crdts_hip

@@ -1,10 +1,9 @@
-"""GPU parity of the fused replica fold (crdt_orswot_fold: ((r0 ⊔ r1) ⊔ r2)
-⊔ ... with Orswot::merge, src/orswot.rs:87-157, over CSR-clock batches —
-BASELINE.json configs[4]) against the oracle's sequential fold, byte-exact
-per record: config-5 replicas (8, and 1-3 replicas), objects whose records
-outgrow the fused path (4 KB in flight, the 6 KB pair stage) and take the
-per-object general path, deferred-remove objects (their steps go through the
-output slot), the placement rule, and malformed input."""
+"""GPU parity of the replica fold (crdt_orswot_fold: ((r0 ⊔ r1) ⊔ r2) ⊔ ...
+with Orswot::merge, src/orswot.rs:87-157 — BASELINE.json configs[4]) against
+the oracle's sequential fold, byte-exact per record: config-5 CSR replicas
+(8, and 1-3 replicas), dense config-3-shaped replicas, records past the join
+kernel's stage (its general kernel), deferred-remove objects, the placement
+rule, and malformed input."""
 import numpy as np
 import pytest
 
@@ -74,8 +73,18 @@ def test_fold_rejects_malformed_and_dense(gpu):
     with pytest.raises(crdts_hip.CrdtError) as e:
         gpu.orswot_fold(B)
     assert e.value.code == crdts_hip.CRDT_ENONCANON
-    D = [crdts_hip.OrswotBatch.from_host(*crdts_hip.generate_orswot(100, threads=2)[0], 16) for _ in range(2)]
-    with pytest.raises(crdts_hip.CrdtError) as e:
-        gpu.orswot_fold(D)
-    assert e.value.code == -1  # CRDT_EINVAL: the fused fold is the CSR form's
     gpu.orswot_fold([crdts_hip.OrswotBatch.from_host(x, y, U, flags=SP) for x, y in reps])  # usable again
+
+
+def test_fold_dense(gpu, oracle):
+    """Dense top clocks (config-3 shape over 16 actors): 5 replicas, the
+    second of each pair of generated sides standing in for further replicas."""
+    import crdts_hip
+
+    sides = []
+    for k in range(3):
+        (lb, lo), (rb, ro) = crdts_hip.generate_orswot(5_000, threads=8, seed=0xF01D + k)
+        sides += [(lb, lo), (rb, ro)]
+    reps = sides[:5]
+    got, _ = _fold(gpu, reps, 16, 0)
+    assert got == _oracle_fold(oracle, reps, 16, 0)
