@@ -61,6 +61,7 @@ struct XLay {
   static_assert(8 * MEM <= Sd - Kc, "dense clock scatter fits the rank + offset arrays");
 };
 using XS = XLay<256, 64, false>;      // 5 888 B of LDS per wave
+using XS5 = XLay<128, 32, false>;     // 2 944 B: five 4-wave blocks per CU
 using XB = XLay<16384, 1024, true>;   // 409 600 B of HBM per large-object wave
 constexpr uint32_t kXWalk = XS::Walk;
 constexpr uint32_t kXBytes = XS::Bytes;
@@ -202,22 +203,26 @@ __device__ __forceinline__ BcWalk bc_walk(const SRC& B, uint64_t len, uint32_t w
   if (nent > XL::kMem) { w.err = CRDT_ECAPACITY; return w; }
   w.n_mem = (uint32_t)nent;
   if constexpr (SRC::kWindow) {
-    // the chain of entry positions is the only serial part: one LDS read and
-    // a multiply-add per entry (reads clamped into the window); every length
-    // is then validated lane-parallel
-    uint32_t q = (uint32_t)p;
-    const uint32_t L32 = (uint32_t)len, step = wm + 8u;
+    // the chain of entry positions is the only serial part: one LDS round
+    // trip and three dependent ALU steps per entry, carried on the window
+    // byte offset of each entry's length field (clamped into the blob); every
+    // length is then validated lane-parallel
+    const uint32_t L32 = (uint32_t)len, step = wm + 8u, lim = B.d + L32, sa32 = (uint32_t)sa;
+    uint32_t a = bc_uni(B.d + (uint32_t)p + wm);
     for (uint32_t e0 = 0; e0 < (uint32_t)nent; e0 += kBcWave) {
-      // lane j keeps entry e0 + j's position (a select per step, no stores in the chain)
+      // lane j keeps entry e0 + j's length-field offset (a select per step, no stores in the chain)
       uint32_t mine = 0;
-      const uint32_t ne = (uint32_t)nent - e0 < kBcWave ? (uint32_t)nent - e0 : kBcWave;
+      const uint32_t ne = bc_uni((uint32_t)nent - e0 < kBcWave ? (uint32_t)nent - e0 : kBcWave);
       for (uint32_t j = 0; j < ne; ++j) {
-        mine = lane == j ? q : mine;
-        const uint32_t l = B.lo32(q + wm < L32 ? q + wm : L32);
-        q += step + (l < 0xFFFFu ? l : 0xFFFFu) * (uint32_t)sa;
+        mine = lane == j ? a : mine;
+        const uint32_t ac = a < lim ? a : lim;
+        const uint32_t* q = (const uint32_t*)(B.b + (ac & ~3u));
+        const uint32_t l = __builtin_amdgcn_alignbit(q[1], q[0], ac * 8u);
+        a = __builtin_amdgcn_readfirstlane(__umul24(l < 0xFFFFu ? l : 0xFFFFu, sa32) + a + step);
       }
-      if (lane < ne) ((uint32_t*)(X + XL::Pm))[e0 + lane] = mine;
+      if (lane < ne) ((uint32_t*)(X + XL::Pm))[e0 + lane] = mine - B.d - wm;
     }
+    const uint32_t q = a - B.d - wm;
     bc_xsync<XL>();
     for (uint32_t e = lane; e < (uint32_t)nent; e += kBcWave) {  // the full 64-bit lengths, in parallel
       const uint32_t pe = ((const uint32_t*)(X + XL::Pm))[e];
@@ -345,10 +350,23 @@ __device__ __forceinline__ int bc_write_record(const SRC& B, const BcWalk& w, ui
     for (uint32_t a = lane; a < A; a += kBcWave) ((uint64_t*)(O + L.o_clk))[a] = 0ull;
     __threadfence_block();
   }
-  for (uint32_t k = lane; k < w.n_clk; k += kBcWave) {
+  uint64_t carry = 0;  // the actor before this round's first entry
+  for (uint32_t k0 = 0; k0 < w.n_clk; k0 += kBcWave) {
+    const uint32_t k = k0 + lane;
+    const bool on = k < w.n_clk;
     const uint64_t e = 8u + k * sa;
-    const uint64_t x = B.get(e, wa), c = B.get(e + wa, 8);
-    bad = bad || x >= A || c == 0u || (k && B.get(e - sa, wa) >= x);
+    uint64_t x = 0, c = 0;
+    if (on) {
+      x = B.get(e, wa);
+      c = B.get(e + wa, 8);
+    }
+    // the previous entry's actor from the lane below (BTreeMap order: strictly increasing)
+    uint64_t px = ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(x >> 32), 1, kBcWave) << 32) |
+                  (uint32_t)__shfl_up((int)(uint32_t)x, 1, kBcWave);
+    if (lane == 0u) px = carry;
+    carry = bc_lane64(x, kBcWave - 1u);
+    if (!on) continue;
+    bad = bad || x >= A || c == 0u || (k && px >= x);
     if (x < A) {
       if (sparse) {
         ((uint64_t*)(O + L.o_clk))[k] = c;
@@ -375,14 +393,13 @@ __device__ __forceinline__ int bc_write_record(const SRC& B, const BcWalk& w, ui
   bc_xsync<XL>();
   if (w.n_mem <= kBcWave) {  // every key in one register: broadcast by readlane
     const uint64_t k = lane < w.n_mem ? B.get(Pm[lane], wm) : 0ull;
-    uint32_t r = 0, eq = 0;
-    for (uint32_t f = 0; f < w.n_mem; ++f) {
-      const uint64_t kf = bc_lane64(k, f);
-      r += kf < k ? 1u : 0u;
-      eq += kf == k ? 1u : 0u;
-    }
+    uint32_t r = 0;
+    for (uint32_t f = 0; f < w.n_mem; ++f) r += bc_lane64(k, f) < k ? 1u : 0u;
+    // the ranks (# keys below) sum to n (n - 1) / 2 exactly when no two keys are equal
+    uint32_t rs = lane < w.n_mem ? r : 0u;
+    for (uint32_t dd = 32; dd >= 1; dd >>= 1) rs += __shfl_xor(rs, dd, kBcWave);
+    bad = bad || bc_uni(rs) != w.n_mem * (w.n_mem - 1u) / 2u;
     if (lane < w.n_mem) {
-      bad = bad || eq != 1u;
       Rm[lane] = r;
       Sm[r < XL::kMem ? r : 0u] = Lm[lane];
     }
@@ -702,18 +719,46 @@ __global__ __launch_bounds__(256) void bincode_sizes_lane_kernel(
   }
 }
 
+// One object of the read-once decode pass: the wave-uniform walk (bc_walk)
+// and the record writer over the same source; an object past the LDS scratch
+// (XL: members or deferred clocks) is listed for the large-object kernel
+// (ctl[0]; past the list: CRDT_ECAPACITY).
+template <class XL, class SRC>
+__device__ __forceinline__ int bc_decode_listed(const SRC& B, uint64_t o, uint64_t len, uint32_t wa, uint32_t wm,
+                                                uint32_t A, bool sparse, uint8_t* X, uint8_t* out, uint64_t oo,
+                                                uint64_t out_bytes, uint32_t* ctl, uint64_t* list, uint32_t list_cap,
+                                                uint32_t lane) {
+  const BcWalk w = bc_walk<XL>(B, len, wa, wm, A, X, lane);
+  if (w.err == CRDT_ECAPACITY) {
+    uint32_t e = 0u;
+    if (lane == 0u) {
+      e = atomicAdd(&ctl[0], 1u);
+      if (e < list_cap) list[e] = o;
+    }
+    return bc_uni(e) < list_cap ? 0 : CRDT_ECAPACITY;
+  }
+  if (w.err) return w.err;
+  const uint64_t size = record_size64(sparse ? w.n_clk : A, w.n_mem, w.n_dot, w.n_def, w.n_def_dot, w.n_def_mem,
+                                      sparse);
+  if (size > out_bytes - oo) return CRDT_ECAPACITY;
+  bc_xsync<XL>();
+  return bc_write_record<false, XL>(B, w, wa, wm, A, sparse, X, out + oo, lane);
+}
+
 // Decode pass. Each lane first walks its own blob of the chunk (as in the
 // sizes pass) and parks every member entry's (position, dot count) in its
 // output record's key section (overwritten later by the keys themselves);
 // the wave then decodes the chunk's objects one by one from the LDS window,
 // reading those pairs instead of walking the entry chain again.
-__global__ __launch_bounds__(kBcWave * kBcWaves, 4) void bincode_decode_kernel(
+template <bool LW, class XL = XS, int OCC = 4>
+__global__ __launch_bounds__(kBcWave * kBcWaves, OCC) void bincode_decode_kernel(
     const uint8_t* __restrict__ blobs, uint64_t blob_bytes, const uint64_t* __restrict__ boff,
     const uint64_t* __restrict__ blen, uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags,
     uint8_t* __restrict__ out, const uint64_t* __restrict__ ooff, uint64_t out_bytes, int* __restrict__ status,
     uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
   __shared__ v4u st_s[kBcWaves][kBcStage / 16];
-  __shared__ v4u sx_s[kBcWaves][kXBytes / 16];
+  static_assert(!LW || XL::kMem == XS::kMem, "the lane walk's listing uses XS");
+  __shared__ v4u sx_s[kBcWaves][XL::Bytes / 16];
   const uint32_t lane = threadIdx.x & (kBcWave - 1u), wave = threadIdx.x / kBcWave;
   uint8_t* X = (uint8_t*)sx_s[wave];
   const bool sparse = (flags & kSparseClock) != 0u;
@@ -729,7 +774,13 @@ __global__ __launch_bounds__(kBcWave * kBcWaves, 4) void bincode_decode_kernel(
     uint64_t off = 0, len = 0, oo = 0;
     if (valid) { off = boff[obj]; len = blen[obj]; oo = ooff[obj]; }
     LaneWalk lw{0, 0, 0, 0, 0, 0, 0, 0};
-    if (valid) {
+    if (!LW) {  // bounds only: each object is walked from its window
+      if (valid) {
+        if ((oo & 15u) || oo > out_bytes) lw.err = CRDT_ECAPACITY;
+        else if (off > blob_bytes || len > blob_bytes - off) lw.err = CRDT_ENONCANON;
+        if (lw.err) atomicCAS(status, 0, lw.err);
+      }
+    } else if (valid) {
       if ((oo & 15u) || oo > out_bytes) {
         lw.err = CRDT_ECAPACITY;
       } else {
@@ -748,10 +799,10 @@ __global__ __launch_bounds__(kBcWave * kBcWaves, 4) void bincode_decode_kernel(
       }
       if (lw.err) atomicCAS(status, 0, lw.err);
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // the parked pairs are visible to the whole wave
+    if (LW) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // the parked pairs are visible to the whole wave
     // objects past the LDS scratch (> 256 members or > 64 deferred clocks) are
     // listed for the large-object kernel (ctl[0]); past the list: CRDT_ECAPACITY
-    const bool big = valid && !lw.err && (lw.n_mem > XS::kMem || lw.n_def > XS::kDef);
+    const bool big = LW && valid && !lw.err && (lw.n_mem > XS::kMem || lw.n_def > XS::kDef);
     if (big) {
       const uint32_t e = atomicAdd(&ctl[0], 1u);
       if (e < list_cap) list[e] = obj;
@@ -769,7 +820,30 @@ __global__ __launch_bounds__(kBcWave * kBcWaves, 4) void bincode_decode_kernel(
       const uint32_t t = (uint32_t)__builtin_ctzll(nxt);
       bc_prefetch(pf, blobs, blob_bytes, bc_lane64(a0, t), __builtin_amdgcn_readlane(n16, t), lane);
     }
-    while (pend) {
+    while (pend && !LW) {  // read once: walk + decode from the window
+      const uint32_t t = (uint32_t)__builtin_ctzll(pend);
+      pend &= pend - 1;
+      const uint64_t o = cbase + t, ot = bc_lane64(off, t), oot = bc_lane64(oo, t), lt = bc_lane64(len, t);
+      int rc;
+      if ((wins >> t) & 1ull) {
+        bc_sync();  // the previous object's window readers are done
+#pragma unroll
+        for (uint32_t k = 0; k < kBcPer; ++k) st_s[wave][lane + k * kBcWave] = pf[k];
+        bc_sync();
+        nxt &= nxt - 1;  // t was the lowest pending windowed object
+        if (nxt) {
+          const uint32_t u = (uint32_t)__builtin_ctzll(nxt);
+          bc_prefetch(pf, blobs, blob_bytes, bc_lane64(a0, u), __builtin_amdgcn_readlane(n16, u), lane);
+        }
+        const Src<true> B{(const uint8_t*)st_s[wave], (uint32_t)(ot & 15u)};
+        rc = bc_decode_listed<XL>(B, o, lt, wa, wm, A, sparse, X, out, oot, out_bytes, ctl, list, list_cap, lane);
+      } else {
+        const Src<false> B{blobs + ot};
+        rc = bc_decode_listed<XL>(B, o, lt, wa, wm, A, sparse, X, out, oot, out_bytes, ctl, list, list_cap, lane);
+      }
+      if (rc && lane == 0u) atomicCAS(status, 0, rc);
+    }
+    while (pend && LW) {
       const uint32_t t = (uint32_t)__builtin_ctzll(pend);
       pend &= pend - 1;
       const uint64_t ot = bc_lane64(off, t), oot = bc_lane64(oo, t);
@@ -1133,7 +1207,8 @@ size_t launch_bincode_big_scratch_bytes() { return bincode_big_scratch_bytes(); 
 int launch_bincode_ingest(const uint8_t* blobs, uint64_t blob_bytes, const uint64_t* boff, const uint64_t* blen,
                           uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags, uint64_t* sizes,
                           uint8_t* out, const uint64_t* ooff, uint64_t out_bytes, int* status, uint32_t* ctl,
-                          hipStream_t stream, uint64_t* dbg, uint64_t* list, uint32_t list_cap, uint8_t* big_scratch) {
+                          hipStream_t stream, uint64_t* dbg, uint64_t* list, uint32_t list_cap, uint8_t* big_scratch,
+                          int walk) {
   if (n_obj == 0) return CRDT_OK;
   const uint32_t blocks = bc_blocks(n_obj);
   if (dbg && !sizes) {  // diagnostic: decode pass with phase stamps into dbg (8 u64 per wave)
@@ -1150,11 +1225,24 @@ int launch_bincode_ingest(const uint8_t* blobs, uint64_t blob_bytes, const uint6
                        blobs, blob_bytes, boff, blen, n_obj, wa, wm, A, flags, sizes, status);
   } else {
     if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;  // ctl[3]: tickets
-    static std::atomic<int> occ_d{0};
-    const uint32_t rblocks = bc_resident_blocks(n_obj, (const void*)bincode_decode_kernel, occ_d);
+    static std::atomic<int> occ_d{0}, occ_r{0}, occ_5{0};
     if (!list || !big_scratch) return CRDT_EINVAL;
-    hipLaunchKernelGGL(bincode_decode_kernel, dim3(rblocks), dim3(kBcWave * kBcWaves), 0, stream, blobs, blob_bytes,
-                       boff, blen, n_obj, wa, wm, A, flags, out, ooff, out_bytes, status, ctl, list, list_cap);
+    if (walk == 1) {
+      const uint32_t rblocks = bc_resident_blocks(n_obj, (const void*)bincode_decode_kernel<true>, occ_d);
+      hipLaunchKernelGGL(bincode_decode_kernel<true>, dim3(rblocks), dim3(kBcWave * kBcWaves), 0, stream, blobs,
+                         blob_bytes, boff, blen, n_obj, wa, wm, A, flags, out, ooff, out_bytes, status, ctl, list,
+                         list_cap);
+    } else if (walk == 2) {
+      const uint32_t rblocks = bc_resident_blocks(n_obj, (const void*)bincode_decode_kernel<false, XS5, 5>, occ_5);
+      hipLaunchKernelGGL((bincode_decode_kernel<false, XS5, 5>), dim3(rblocks), dim3(kBcWave * kBcWaves), 0, stream,
+                         blobs, blob_bytes, boff, blen, n_obj, wa, wm, A, flags, out, ooff, out_bytes, status, ctl,
+                         list, list_cap);
+    } else {
+      const uint32_t rblocks = bc_resident_blocks(n_obj, (const void*)bincode_decode_kernel<false>, occ_r);
+      hipLaunchKernelGGL(bincode_decode_kernel<false>, dim3(rblocks), dim3(kBcWave * kBcWaves), 0, stream, blobs,
+                         blob_bytes, boff, blen, n_obj, wa, wm, A, flags, out, ooff, out_bytes, status, ctl, list,
+                         list_cap);
+    }
     hipLaunchKernelGGL(bincode_decode_big_kernel, dim3(kBcBigWaves), dim3(kBcWave), 0, stream, blobs, boff, blen, wa,
                        wm, A, flags, out, ooff, out_bytes, status, ctl, list, list_cap, big_scratch);
   }
