@@ -745,11 +745,18 @@ __device__ __forceinline__ int bc_decode_listed(const SRC& B, uint64_t o, uint64
   return bc_write_record<false, XL>(B, w, wa, wm, A, sparse, X, out + oo, lane);
 }
 
-// Decode pass. Each lane first walks its own blob of the chunk (as in the
-// sizes pass) and parks every member entry's (position, dot count) in its
-// output record's key section (overwritten later by the keys themselves);
-// the wave then decodes the chunk's objects one by one from the LDS window,
-// reading those pairs instead of walking the entry chain again.
+// Decode pass, one wave per chunk of objects (guided split). Product (LW =
+// false): every blob is read from HBM once — its aligned lines prefetched
+// into registers while the previous object is decoded, staged in the LDS
+// window, walked there by the wave (bc_walk: the entry chain, then every
+// length lane-parallel) and decoded from it; an object past the LDS scratch
+// is listed for the large-object kernel. Diagnostic (LW = true, variant 305,
+// the round-3 product): each lane first walks its own blob of the chunk over
+// HBM (as in the sizes pass) and parks every member entry's (position, dot
+// count) in its output record's key section; the wave then decodes from the
+// window reading those pairs — faster by 4 % on config 3 but every blob is
+// read twice and the pairs written and read back (2.3x the algorithmic bytes,
+// DESIGN.md §9).
 template <bool LW, class XL = XS, int OCC = 4>
 __global__ __launch_bounds__(kBcWave * kBcWaves, OCC) void bincode_decode_kernel(
     const uint8_t* __restrict__ blobs, uint64_t blob_bytes, const uint64_t* __restrict__ boff,
@@ -1228,15 +1235,25 @@ int launch_bincode_ingest(const uint8_t* blobs, uint64_t blob_bytes, const uint6
     static std::atomic<int> occ_d{0}, occ_r{0}, occ_5{0};
     if (!list || !big_scratch) return CRDT_EINVAL;
     if (walk == 1) {
+#ifdef CRDT_DIAG
       const uint32_t rblocks = bc_resident_blocks(n_obj, (const void*)bincode_decode_kernel<true>, occ_d);
       hipLaunchKernelGGL(bincode_decode_kernel<true>, dim3(rblocks), dim3(kBcWave * kBcWaves), 0, stream, blobs,
                          blob_bytes, boff, blen, n_obj, wa, wm, A, flags, out, ooff, out_bytes, status, ctl, list,
                          list_cap);
+#else
+      (void)occ_d;
+      return CRDT_EINVAL;
+#endif
     } else if (walk == 2) {
+#ifdef CRDT_DIAG
       const uint32_t rblocks = bc_resident_blocks(n_obj, (const void*)bincode_decode_kernel<false, XS5, 5>, occ_5);
       hipLaunchKernelGGL((bincode_decode_kernel<false, XS5, 5>), dim3(rblocks), dim3(kBcWave * kBcWaves), 0, stream,
                          blobs, blob_bytes, boff, blen, n_obj, wa, wm, A, flags, out, ooff, out_bytes, status, ctl,
                          list, list_cap);
+#else
+      (void)occ_5;
+      return CRDT_EINVAL;
+#endif
     } else {
       const uint32_t rblocks = bc_resident_blocks(n_obj, (const void*)bincode_decode_kernel<false>, occ_r);
       hipLaunchKernelGGL(bincode_decode_kernel<false>, dim3(rblocks), dim3(kBcWave * kBcWaves), 0, stream, blobs,

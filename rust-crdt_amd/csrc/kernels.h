@@ -53,7 +53,7 @@ int launch_bincode_ingest(const uint8_t* blobs, uint64_t blob_bytes, const uint6
                           uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags, uint64_t* sizes,
                           uint8_t* out, const uint64_t* ooff, uint64_t out_bytes, int* status, uint32_t* ctl, hipStream_t stream,
                           uint64_t* dbg = nullptr, uint64_t* list = nullptr, uint32_t list_cap = 0,
-                          uint8_t* big_scratch = nullptr, int walk = 1);
+                          uint8_t* big_scratch = nullptr, int walk = 0);
 size_t launch_bincode_big_scratch_bytes();
 int launch_bincode_egest(const uint8_t* rb, uint64_t rbytes, const uint64_t* roff, uint64_t n_obj, uint32_t A,
                          uint32_t flags, uint32_t wa, uint32_t wm, uint64_t* sizes, uint8_t* out,
