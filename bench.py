@@ -14,6 +14,12 @@ is no collective on this path.
     python bench.py [--gpus N --steps K --warmup W] [--workload orswot|gcounter|pncounter|...]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
+Before the W untimed warmup steps, the step itself runs untimed and back to
+back for --settle-ms (default 200 ms, the same count on every rank): the
+part's clock settles over ~25 ms of continuous launches after the inputs are
+generated, so with a small W the timed steps would otherwise measure the ramp
+(DESIGN.md §9). The line reports it under `settle`.
+
 At N > 1 without a launcher (no WORLD_SIZE in the environment) this process
 starts N worker processes of itself (RANK / LOCAL_RANK / WORLD_SIZE /
 MASTER_* set, one GPU each) before it makes any GPU call, relays rank 0's
@@ -48,6 +54,11 @@ def parse():
     # launches after the inputs are generated (tools/steady_probe.py: 0.88 ->
     # 0.75 ms per headline launch); the timed steps then see the steady state
     p.add_argument("--warmup", type=int, default=50)
+    # before the W warmup steps, untimed launches of the same step until the
+    # device has run it for this long: the clock ramp is a matter of time
+    # (~25 ms of back-to-back launches), not of step count, so a small W
+    # (the driver's 5 x 0.75 ms) would otherwise time the ramp
+    p.add_argument("--settle-ms", type=float, default=200.0)
     p.add_argument("--workload", default="orswot",
                    choices=["orswot", "vclock", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply",
                             "mvreg", "map", "map_orswot", "clock_csr", "truncate", "spawn_check"])
@@ -261,6 +272,7 @@ def run_orswot(args, rank, world, local):
     # and the output (no headers, padding or offsets), from the records' headers
     alg_bytes = L.compact_bytes() + R.compact_bytes() + out.compact_bytes()
 
+    settle(args, stream, lambda: eng.orswot_merge(L, R, out=out, stream=stream, check_status=False), world)
     for _ in range(args.warmup):
         eng.orswot_merge(L, R, out=out, stream=stream, check_status=False)
     ev = TimingEvents(args.steps)  # HIP events around every launch (timing only: no system fence)
@@ -453,6 +465,7 @@ def run_dense(args, rank, world, local, kind):
     eng = crdts_hip.Engine(local)
     stream = torch.cuda.Stream(device=local)
     torch.cuda.synchronize()  # generated on torch's stream; the merges run on `stream`
+    settle(args, stream, lambda: eng.dense_merge(a, b, A, kind, stream=stream), world)
     for _ in range(args.warmup):
         eng.dense_merge(a, b, A, kind, stream=stream)
     ev = TimingEvents(args.steps)
@@ -542,11 +555,37 @@ class TimingEvents:
             self.hip.hipEventDestroy(e)
 
 
+SETTLE = {}  # the settle phase of this run, reported in the JSON line
+
+
+def settle(args, stream, fn, world=1):
+    """Untimed calls of fn() (the timed step itself), back to back, for about
+    args.settle_ms of device time before the W warmup steps. The count comes
+    from the slowest rank's time per call, so every rank makes the same number
+    of calls (a step may hold collectives)."""
+    if args.settle_ms <= 0:
+        return
+    t0 = time.perf_counter()
+    for _ in range(8):
+        fn()
+    stream.synchronize()
+    per = max_over_ranks((time.perf_counter() - t0) / 8.0, world)
+    n = min(4096, max(0, int(args.settle_ms * 1e-3 / max(per, 1e-6)) - 8))
+    for k in range(n):
+        fn()
+        if k % 64 == 63:
+            stream.synchronize()  # bounded queue depth
+    stream.synchronize()
+    SETTLE.update({"ms": round((time.perf_counter() - t0) * 1e3, 1), "launches": 8 + n,
+                   "note": "untimed calls of the timed step before the W warmup steps (the clock ramp, DESIGN.md §9)"})
+
+
 def _timed_steps(args, world, stream, fn):
-    """W warmup + K timed calls of fn(); returns (wall_s over ranks (max), mean event ms on `stream`)."""
+    """settle + W warmup + K timed calls of fn(); returns (wall_s over ranks (max), mean event ms on `stream`)."""
     import numpy as np
     import torch
 
+    settle(args, stream, fn, world)
     for _ in range(args.warmup):
         fn()
     ev = TimingEvents(args.steps)
@@ -1545,6 +1584,8 @@ def main():
             import crdts_hip
 
             res["build"] = crdts_hip.build_record()  # the library this run loaded, vs __graft_entry__.build()'s record
+        if SETTLE:
+            res["settle"] = dict(SETTLE)
         print(json.dumps(res), flush=True)
     if failed:
         raise SystemExit(f"bench.py rank {rank}: cross-rank check failed: {failed}")

@@ -150,14 +150,114 @@ __global__ __launch_bounds__(kWave* kWpb, 6) void skel_kernel(const uint8_t* __r
   }
   if (sink == 0x9e3779b9u) sinkp[0] = sink;
 }
+
+// Prefetch two objects ahead (two register sets, the loop unrolled by two so
+// no registers are copied), chunk step and copy-out as skel_kernel<0, 0, NT>.
+template <int OCC>
+__global__ __launch_bounds__(kWave* kWpb, OCC) void skel2_kernel(const uint8_t* __restrict__ Lb,
+                                                                 const uint64_t* __restrict__ Loff,
+                                                                 const uint8_t* __restrict__ Rb,
+                                                                 const uint64_t* __restrict__ Roff,
+                                                                 uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff,
+                                                                 uint64_t n_obj, uint32_t* sinkp) {
+  __shared__ u32x4 st[kWpb][2 * kPer * kWave + kPad];
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+  u32x4* const sL = st[wave];
+  u32x4* const sR = st[wave] + kPer * kWave;
+  const uint64_t wave_id = (uint64_t)blockIdx.x * kWpb + wave, n_waves = (uint64_t)gridDim.x * kWpb;
+  uint32_t sink = 0;
+  const uint32_t spin = sinkp[1];
+  const uint64_t rounds = (n_obj + n_waves * kWave - 1) / (n_waves * kWave);
+  const uint64_t cs = (n_obj + n_waves * rounds - 1) / (n_waves * rounds);
+  for (uint64_t cbase = wave_id * cs; cbase < n_obj; cbase += n_waves * cs) {
+    const uint64_t obj = cbase + lane;
+    const bool valid = lane < cs && obj < n_obj;
+    uint64_t lo = 0, ro = 0;
+    if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
+    u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
+    if (valid) {
+      hl0 = ((const u32x4*)(Lb + lo))[0]; hl1 = ((const u32x4*)(Lb + lo))[1];
+      hr0 = ((const u32x4*)(Rb + ro))[0]; hr1 = ((const u32x4*)(Rb + ro))[1];
+    }
+    const uint32_t szl = hl0.x, szr = hr0.x;
+    sink += hl0.z + hr0.w + hl1.x + hr1.x;
+    const bool ok = valid && szl <= 2048u && szr <= 2048u && szl >= 16u && szr >= 16u;
+    const uint32_t n16 = ok ? (szl / 16u) | ((szr / 16u) << 16) : 0u;
+    uint64_t pend = __ballot(ok);
+    u32x4 aL[kPer], aR[kPer], bL[kPer], bR[kPer];
+    uint32_t ta = 64u, tb = 64u;  // the objects in flight in set a / b (64: none)
+    auto take = [&](uint32_t& t) {
+      t = pend ? (uint32_t)__builtin_ctzll(pend) : 64u;
+      pend &= pend - 1;
+    };
+    auto issue = [&](u32x4 (&pl)[kPer], u32x4 (&pr)[kPer], uint32_t t) {
+      if (t < 64u) {
+        const uint32_t nt16 = lane_of(n16, t);
+        prefetch(pl, Lb + lane_of64(lo, t), nt16 & 0xFFFFu, lane);
+        prefetch(pr, Rb + lane_of64(ro, t), nt16 >> 16, lane);
+      }
+    };
+    auto work = [&](u32x4 (&pl)[kPer], u32x4 (&pr)[kPer], uint32_t t) {
+      const uint32_t nt16 = lane_of(n16, t);
+      wave_sync();
+      stage(sL, pl, nt16 & 0xFFFFu, lane);
+      stage(sR, pr, nt16 >> 16, lane);
+      wave_sync();
+    };
+    auto finish = [&](uint32_t t) {
+      uint32_t h = ((const uint32_t*)sR)[lane] ^ ((const uint32_t*)sL)[lane];
+      for (uint32_t q = 0; q < spin; ++q) h = h * 0x9e3779b1u + (h >> 7);
+      sink += h;
+      const uint32_t on16 = lane_of(n16, t) & 0xFFFFu;
+      const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
+      wave_sync();
+      copy_out(sL, Ob + oo, on16, lane, true);
+      if (lane == 0) Ooff[cbase + t] = oo;
+    };
+    take(ta);
+    issue(aL, aR, ta);
+    take(tb);
+    issue(bL, bR, tb);
+    while (ta < 64u) {
+      work(aL, aR, ta);
+      uint32_t tn;
+      take(tn);
+      issue(aL, aR, tn);  // two objects ahead
+      finish(ta);
+      ta = tn;
+      if (tb >= 64u) break;
+      work(bL, bR, tb);
+      take(tn);
+      issue(bL, bR, tn);
+      finish(tb);
+      tb = tn;
+    }
+  }
+  if (sink == 0x9e3779b9u) sinkp[0] = sink;
+}
 }  // namespace
 
 extern "C" int skel_launch(int variant, int blocks_per_cu, const uint8_t* Lb, const uint64_t* Loff,
                            const uint64_t* Lsh, const uint8_t* Rb, const uint64_t* Roff, const uint64_t* Rsh,
                            uint8_t* Ob, uint64_t* Ooff, uint64_t n_obj, uint32_t* sink, void* stream) {
   const void* fn = nullptr;
+  if (variant >= 200) {  // skel2_kernel: prefetch depth 2 (200: 5 waves/SIMD, 201: 6, 202: 4)
+    const void* f2 = variant == 200 ? (const void*)skel2_kernel<5> : variant == 201 ? (const void*)skel2_kernel<6>
+                                                                                  : (const void*)skel2_kernel<4>;
+    if (blocks_per_cu <= 0) blocks_per_cu = variant == 200 ? 5 : variant == 201 ? 6 : 4;  // waves per SIMD
+    int occ2 = 0;
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, f2, kWave * kWpb, 0);
+    if (blocks_per_cu > 0 && blocks_per_cu < occ2) occ2 = blocks_per_cu;
+    const uint64_t chunks2 = (n_obj + 63) / 64;
+    uint64_t blocks2 = 256ull * occ2;
+    if (blocks2 > (chunks2 + kWpb - 1) / kWpb) blocks2 = (chunks2 + kWpb - 1) / kWpb;
+    void* args2[] = {&Lb, &Loff, &Rb, &Roff, &Ob, &Ooff, &n_obj, &sink};
+    return hipLaunchKernel(f2, dim3((uint32_t)blocks2), dim3(kWave * kWpb), args2, 0, (hipStream_t)stream) ==
+                   hipSuccess ? occ2 : -2;
+  }
   switch (variant) {  // HDR * 10 + PACK (+100: default-policy stores)
     case 0: fn = (const void*)skel_kernel<0, 0, true>; break;
+    case 3: fn = (const void*)skel_kernel<0, 0, true>; if (blocks_per_cu <= 0) blocks_per_cu = 5; break;  // D1 at 5 waves/SIMD
     case 1: fn = (const void*)skel_kernel<0, 1, true>; break;
     case 10: fn = (const void*)skel_kernel<1, 0, true>; break;
     case 11: fn = (const void*)skel_kernel<1, 1, true>; break;
