@@ -9,6 +9,10 @@ if [ -n "${SKEL:-}" ]; then
   timeout -k 10 300 python tools/probe/run_skel.py --variants 0,3,200,201,202 --spins 0,120 > $O/skel.json 2> $O/skel.err || { echo SKEL_FAILED; tail -20 $O/skel.err; exit 1; }
   cat $O/skel.json
 fi
+if [ -n "${AB:-}" ]; then
+  timeout -k 10 400 python tools/ab_bench.py --variants $AB --rounds 12 --check ${AB_CHECK:-} > $O/ab.json 2> $O/ab.err || { echo AB_FAILED; tail -20 $O/ab.err; exit 1; }
+  cat $O/ab.json
+fi
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_w5.json 2> $O/bench_w5.err || { echo BENCH_W5_FAILED; tail -20 $O/bench_w5.err; exit 1; }
 cut -c1-400 $O/bench_w5.json
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { echo BENCH_FAILED; tail -20 $O/bench.err; exit 1; }
