@@ -21,9 +21,43 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CAPS = dict(kcap=4, mcap=4, vdcap=4, vscap=4, dcap=4, scap=4)
 
 
-def load_cases():
+def load_cases(nested=False):
+    """The flat Map KATs (Orswot / MVReg values: every backend), or with
+    nested=True the TestMap ones (Map<u8, Map<u8, MVReg>>: the Python
+    restatement only)."""
     with open(os.path.join(GOLDEN, "kat_map.json")) as f:
-        return json.load(f)["cases"]
+        cases = json.load(f)["cases"]
+    return [c for c in cases if (c.get("kind") == "nested") == nested]
+
+
+def nested_map():
+    """TestMap (test/map.rs:8): Map<u8, Map<u8, MVReg<u8, u8>, u8>, u8>."""
+    return crdts_ref.Map(lambda: crdts_ref.Map(crdts_ref.MVReg))
+
+
+def apply_raw(m, op):
+    """A literal nested Op (the JSON form of kat_map.json's `raw` steps):
+    Op::Nop, Op::Rm {clock, key}, Op::Up {dot, key, op} with the inner
+    Map<u8, MVReg> op Nop | Rm | Up {dot, key, Put {clock, val}} (src/map.rs:160-190)."""
+    if op == "nop":
+        return
+    if "rm" in op:
+        m.apply_rm(op["rm"]["key"], crdts_ref.VClock([tuple(p) for p in op["rm"]["clock"]]))
+        return
+    up = op["up"]
+    m.apply_up(tuple(up["dot"]), up["key"], lambda v: apply_raw_inner(v, up["op"]))
+
+
+def apply_raw_inner(v, op):
+    if op == "nop":
+        return
+    if "rm" in op:
+        v.apply_rm(op["rm"]["key"], crdts_ref.VClock([tuple(p) for p in op["rm"]["clock"]]))
+        return
+    up = op["up"]
+    put = up["op"]["put"]
+    v.apply_up(tuple(up["dot"]), up["key"],
+               lambda r: r.apply_put(crdts_ref.VClock([tuple(p) for p in put["clock"]]), put["val"]))
 
 
 def _pairs(clock):
@@ -32,6 +66,8 @@ def _pairs(clock):
 
 class PyMapBackend:
     def new(self, kind):
+        if kind == "nested":
+            return nested_map()
         return crdts_ref.Map(crdts_ref.Orswot if kind == "orswot" else crdts_ref.MVReg)
 
     def clone(self, m):
@@ -48,6 +84,15 @@ class PyMapBackend:
 
     def apply_rm(self, m, key, pairs):
         m.apply_rm(key, crdts_ref.VClock(pairs))
+
+    def apply_nested_put(self, m, dot, key1, key2, clock, val):
+        # map.update(key1, ctx, |map, ctx| map.update(key2, ctx, |reg, ctx| reg.set(val, ctx))):
+        # Op::Up {ctx.dot, key1, Op::Up {ctx.dot, key2, Put {ctx.clock, val}}}
+        apply_raw(m, {"up": {"dot": list(dot), "key": key1,
+                             "op": {"up": {"dot": list(dot), "key": key2, "op": {"put": {"clock": clock, "val": val}}}}}})
+
+    def apply_raw(self, m, op):
+        apply_raw(m, op)
 
     def merge(self, dst, src):
         dst.merge(src)
@@ -102,12 +147,14 @@ def run_case(case, backend, trace=None):
             v = backend.view(maps[st[2]])
             add, rm, _ = v.get(st[3])
             ctxs[st[1]] = (_pairs(add), _pairs(rm))
-        elif op in ("up_add", "up_put"):  # derive_add_ctx(actor): dot = add_clock.inc(actor), clock = add_clock + dot
+        elif op in ("up_add", "up_put", "nup_put"):  # derive_add_ctx(actor): dot = add_clock.inc(actor), clock = add_clock + dot
             add, _ = ctxs[st[2]]
             actor = st[3]
             dot = (actor, dict(add).get(actor, 0) + 1)
             clock = sorted({**dict(add), actor: dot[1]}.items())
-            ops[st[1]] = (op, dot, st[4], st[5], clock)
+            ops[st[1]] = (op, dot, st[4], st[5:] if op == "nup_put" else st[5], clock)
+        elif op == "raw":
+            ops[st[1]] = ("raw", None, None, st[2], None)
         elif op == "rm":  # derive_rm_ctx: the entry clock
             ops[st[1]] = ("rm", None, st[3], None, ctxs[st[2]][1])
         elif op == "apply":
@@ -117,6 +164,10 @@ def run_case(case, backend, trace=None):
                 backend.apply_up_add(m, dot, key, arg)
             elif kind == "up_put":
                 backend.apply_up_put(m, dot, key, clock, arg)
+            elif kind == "nup_put":
+                backend.apply_nested_put(m, dot, key, arg[0], clock, arg[1])
+            elif kind == "raw":
+                backend.apply_raw(m, arg)
             else:
                 backend.apply_rm(m, key, clock)
         elif op == "merge":
@@ -131,6 +182,10 @@ def run_case(case, backend, trace=None):
         elif op == "assert_read":
             v = backend.view(maps[st[1]]).get(st[2])[2]
             assert v is not None and sorted(v.read()) == sorted(st[3]), f"{where}"
+        elif op == "assert_nested_read":  # get(k1).val.and_then(|m| m.get(k2).val).map(|r| r.read().val)
+            v = backend.view(maps[st[1]]).get(st[2])[2]
+            r = v.get(st[3])[2] if v is not None else None
+            assert r is not None and sorted(r.read()) == sorted(st[4]), f"{where}"
         elif op == "assert_eq":
             a, b = backend.view(maps[st[1]]), backend.view(maps[st[2]])
             assert a == b, f"{where}: {a.canonical()} != {b.canonical()}"
