@@ -472,8 +472,9 @@ int crdt_orswot_generate_replicas_subset(uint64_t seed, size_t first_obj, size_t
  *   dset_n[dcap], dset[dcap][scap]       their key sets, ascending
  * Only the used slots of the output are written (slots past a count keep
  * what the buffer held). Output capacities must be >= the sum of
- * both inputs' (kcap, mcap, dcap, scap); per side kcap <= 32, mcap <= 16,
- * dcap <= 32, scap <= 32, n_actors <= 64.                                    */
+ * both inputs' (kcap, mcap, dcap, scap); per side kcap <= 4096, mcap <= 128,
+ * dcap <= 64, scap <= 4096, n_actors <= 128 (else CRDT_EINVAL); a merged map
+ * past the output's capacities latches CRDT_ECAPACITY for that object.       */
 typedef struct crdt_map_mvreg_slab {
   uint64_t* clock;
   uint32_t* n_keys;
@@ -554,8 +555,10 @@ int crdt_map_orswot_merge(crdt_ctx* ctx, const crdt_map_orswot_slab* self, const
  * crdt_mvreg_merge: MVReg<u64, A>::merge (src/mvreg.rs:121-153) over slabs
  * of `cap` (clock row, value) slots per object, d_*_n[i] slots in use; the
  * output keeps the reference's order (self's survivors, then other's) and
- * zero-fills unused slots. cap <= 64 per side; more survivors than out_cap
- * latch CRDT_ECAPACITY.                                                     */
+ * zero-fills unused slots. cap <= 1024 per side (registers of <= 64 slots
+ * per side whose rows fit 60 KB of LDS per wave take the fast kernel, the
+ * rest a one-wave-per-pair kernel reading the rows from HBM); more survivors
+ * than out_cap latch CRDT_ECAPACITY.                                        */
 int crdt_vclock_partial_cmp(crdt_ctx* ctx, const uint64_t* d_a, const uint64_t* d_b, size_t n,
                             uint32_t n_actors, int8_t* d_out, void* stream);
 int crdt_mvreg_merge(crdt_ctx* ctx, const uint32_t* d_self_n, const uint64_t* d_self_clk,

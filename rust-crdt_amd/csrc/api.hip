@@ -552,7 +552,7 @@ int crdt_mvreg_merge(crdt_ctx* ctx, const uint32_t* d_self_n, const uint64_t* d_
                      uint32_t self_cap, const uint32_t* d_other_n, const uint64_t* d_other_clk,
                      const uint64_t* d_other_val, uint32_t other_cap, uint32_t* d_out_n, uint64_t* d_out_clk,
                      uint64_t* d_out_val, uint32_t out_cap, size_t n_obj, uint32_t n_actors, void* stream) {
-  if (!ctx || n_actors == 0 || self_cap == 0 || other_cap == 0 || self_cap > 64 || other_cap > 64 || out_cap == 0)
+  if (!ctx || n_actors == 0 || self_cap == 0 || other_cap == 0 || self_cap > 1024 || other_cap > 1024 || out_cap == 0)
     return CRDT_EINVAL;
   if (n_obj && (!d_self_n || !d_self_clk || !d_self_val || !d_other_n || !d_other_clk || !d_other_val || !d_out_n ||
                 !d_out_clk || !d_out_val))
@@ -566,10 +566,10 @@ int crdt_mvreg_merge(crdt_ctx* ctx, const uint32_t* d_self_n, const uint64_t* d_
 
 int crdt_map_mvreg_merge(crdt_ctx* ctx, const crdt_map_mvreg_slab* self, const crdt_map_mvreg_slab* other,
                          const crdt_map_mvreg_slab* out, size_t n_obj, uint32_t n_actors, void* stream) {
-  if (!ctx || !self || !other || !out || n_actors == 0 || n_actors > 64) return CRDT_EINVAL;
+  if (!ctx || !self || !other || !out || n_actors == 0 || n_actors > 128) return CRDT_EINVAL;
   for (const crdt_map_mvreg_slab* x : {self, other})
-    if (x->kcap == 0 || x->kcap > 32 || x->mcap == 0 || x->mcap > 16 || x->dcap == 0 || x->dcap > 32 ||
-        x->scap == 0 || x->scap > 32)
+    if (x->kcap == 0 || x->kcap > 4096 || x->mcap == 0 || x->mcap > 128 || x->dcap == 0 || x->dcap > 64 ||
+        x->scap == 0 || x->scap > 4096)
       return CRDT_EINVAL;
   if (out->kcap < self->kcap + other->kcap || out->mcap < self->mcap + other->mcap ||
       out->dcap < self->dcap + other->dcap || out->scap < self->scap + other->scap)

@@ -12,51 +12,30 @@
 // entries and truncating the rest, re-deferring the clocks not yet covered.
 // Subtracts commute, so each kept key takes all its deferred clocks at once.
 //
-// One wave per map pair; lane = actor slot (n_actors <= 64), so every VClock
-// operation on dense rows is one lane-parallel op plus a ballot; keys, values
-// and deferred entries are walked by wave-uniform loops.
+// One wave per map pair; lane = actor slot, NS slots per lane (NS = 1 for
+// n_actors <= 64, 2 for <= 128: map_rows.h), so every VClock operation on
+// dense rows is NS lane-parallel ops plus a ballot; keys, values and deferred
+// entries are walked by wave-uniform loops.
 #include <hip/hip_runtime.h>
 
 #include "../../include/crdts_hip.h"
 #include "kernels.h"
+#include "map_rows.h"
 #include "sched.h"
 
 namespace crdts_hip {
 namespace {
 
+using namespace maprow;  // Row<NS> and the VClock ops on it (map_rows.h)
+
 constexpr uint32_t kMpW = 64;
-constexpr uint32_t kMpComb = 64;  // combined deferred entries (<= dcap_self + dcap_other)
-constexpr uint32_t kMpVals = 32;  // kept values of one key (<= mcap_self + mcap_other)
+constexpr uint32_t kMpComb = 128;  // combined deferred entries (<= dcap_self + dcap_other, dcap <= 64)
+constexpr uint32_t kMpVals = 256;  // kept values of one key (<= mcap_self + mcap_other, mcap <= 128)
 
 __device__ __forceinline__ void mp_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-__device__ __forceinline__ uint64_t lane64(uint64_t v, uint32_t t) {
-  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), t) << 32) |
-         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, t);
-}
-// VClock::subtract (src/vclock.rs:236-242) on one slot
-__device__ __forceinline__ uint64_t vsub(uint64_t e, uint64_t c) { return c >= e ? 0ull : e; }
-__device__ __forceinline__ bool vany(uint64_t v) { return __ballot(v != 0ull) != 0ull; }
-__device__ __forceinline__ bool vle(uint64_t d, uint64_t c) { return __ballot(d > c) == 0ull; }
-__device__ __forceinline__ bool vstrict_less(uint64_t a, uint64_t b) {  // partial_cmp(a, b) == Less
-  return __ballot(a > b) == 0ull && __ballot(a < b) != 0ull;
-}
-// CLOCK ORDER of two dense rows (lexicographic over their (actor, counter) pairs, a proper prefix first)
-__device__ int vorder(uint64_t p, uint64_t q, uint32_t lane) {
-  const uint64_t diff = __ballot(p != q);
-  if (!diff) return 0;
-  const uint32_t x = (uint32_t)__builtin_ctzll(diff);
-  const uint64_t px = lane64(p, x), qx = lane64(q, x);
-  if (px && qx) return px < qx ? -1 : 1;
-  if (!px) return __ballot(p != 0ull && lane > x) ? 1 : -1;  // q has actor x; p continues past x, or ends
-  return __ballot(q != 0ull && lane > x) ? -1 : 1;
-}
-
-__device__ __forceinline__ uint64_t rowv(const uint64_t* base, uint64_t row, uint32_t A, uint32_t lane) {
-  return lane < A ? base[row * A + lane] : 0ull;
 }
 __device__ __forceinline__ bool set_has(const uint64_t* set, uint32_t n, uint64_t key, uint32_t lane) {
   bool f = false;
@@ -70,7 +49,7 @@ __device__ __forceinline__ bool set_has(const uint64_t* set, uint32_t n, uint64_
 // row read in the dominance loops is its own dependent global load.
 constexpr uint32_t kVsRows = 128;  // u64 per side
 
-template <bool VS>
+template <bool VS, int NS>
 __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_slab S, crdt_map_mvreg_slab O,
                                                                crdt_map_mvreg_slab R, uint64_t n_obj, uint32_t A,
                                                                int* __restrict__ status, uint32_t* __restrict__ ctl) {
@@ -80,8 +59,8 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
   const uint32_t lane = threadIdx.x;
   BlockTickets<4> sched(n_obj, ctl + 3, lane);  // (sched.h)
   for (uint64_t i = sched.first(); i < n_obj; i = sched.next(i)) {
-    const uint64_t cS = rowv(S.clock, i, A, lane), cO = rowv(O.clock, i, A, lane);
-    const uint64_t cM = cS > cO ? cS : cO;  // VClock::merge
+    const Row<NS> cS = rowv<NS>(S.clock, i, A, lane), cO = rowv<NS>(O.clock, i, A, lane);
+    const Row<NS> cM = vmax(cS, cO);  // VClock::merge
     const uint32_t nS = __builtin_amdgcn_readfirstlane(S.n_keys[i]), nO = __builtin_amdgcn_readfirstlane(O.n_keys[i]);
     const uint32_t dS = __builtin_amdgcn_readfirstlane(S.n_def[i]), dO = __builtin_amdgcn_readfirstlane(O.n_def[i]);
     if (nS > S.kcap || nO > O.kcap || dS > S.dcap || dO > O.dcap) {
@@ -89,11 +68,13 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
       continue;
     }
     // every value count within mcap and deferred set size within scap (the
-    // loops below read mv_n / dset_n slots of the slab row as counts)
-    // (kcap <= 32: lane k holds key k's value count, which the value-row stage
-    // below reads by readlane — no dependent load on the per-key chain)
+    // loops below read mv_n / dset_n slots of the slab row as counts); lane k
+    // keeps key k's value count (keys < 64), which the value-row stage below
+    // reads by readlane (no dependent load on the per-key chain)
     const uint32_t vnS = lane < nS ? S.mv_n[i * S.kcap + lane] : 0u, vnO = lane < nO ? O.mv_n[i * O.kcap + lane] : 0u;
     bool bad = vnS > S.mcap || vnO > O.mcap;
+    for (uint32_t k = lane + kMpW; k < nS; k += kMpW) bad = bad || S.mv_n[i * S.kcap + k] > S.mcap;
+    for (uint32_t k = lane + kMpW; k < nO; k += kMpW) bad = bad || O.mv_n[i * O.kcap + k] > O.mcap;
     for (uint32_t k = lane; k < dS; k += kMpW) bad = bad || S.dset_n[i * S.dcap + k] > S.scap;
     for (uint32_t k = lane; k < dO; k += kMpW) bad = bad || O.dset_n[i * O.dcap + k] > O.scap;
     if (__ballot(bad) != 0ull) {
@@ -106,11 +87,11 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
     {
       uint32_t a = 0, b = 0;
       while (a < dS || b < dO) {
-        if (b < dO && vle(rowv(O.dclock, i * O.dcap + b, A, lane), cS)) { ++b; continue; }
+        if (b < dO && vle(rowv<NS>(O.dclock, i * O.dcap + b, A, lane), cS)) { ++b; continue; }
         int c;
         if (a >= dS) c = 1;
         else if (b >= dO) c = -1;
-        else c = vorder(rowv(S.dclock, i * S.dcap + a, A, lane), rowv(O.dclock, i * O.dcap + b, A, lane), lane);
+        else c = vorder(rowv<NS>(S.dclock, i * S.dcap + a, A, lane), rowv<NS>(O.dclock, i * O.dcap + b, A, lane), lane);
         const uint32_t e = (c <= 0 ? a + 1u : 0u) | ((c >= 0 ? b + 1u : 0u) << 8);
         if (lane == 0u) comb[nc] = e;
         ++nc;
@@ -127,10 +108,15 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
       const bool hs = a < nS && (b >= nO || ka <= kb), ho = b < nO && (a >= nS || kb <= ka);
       const uint64_t key = hs ? ka : kb;
       const uint64_t ia = i * S.kcap + a, ib = i * O.kcap + b;
-      const uint64_t eS = hs ? rowv(S.eclock, ia, A, lane) : 0ull, eO = ho ? rowv(O.eclock, ib, A, lane) : 0ull;
+      const Row<NS> eS = hs ? rowv<NS>(S.eclock, ia, A, lane) : zrow<NS>();
+      const Row<NS> eO = ho ? rowv<NS>(O.eclock, ib, A, lane) : zrow<NS>();
+      // the key's value counts (within mcap: checked above)
+      const uint32_t ms = !hs ? 0u : a < kMpW ? (uint32_t)__builtin_amdgcn_readlane(vnS, a)
+                                             : (uint32_t)__builtin_amdgcn_readfirstlane(S.mv_n[ia]);
+      const uint32_t mo = !ho ? 0u : b < kMpW ? (uint32_t)__builtin_amdgcn_readlane(vnO, b)
+                                             : (uint32_t)__builtin_amdgcn_readfirstlane(O.mv_n[ib]);
       if (VS) {  // stage the key's used value rows: every load in flight, then the LDS stores
-        const uint32_t n0 = hs ? (uint32_t)__builtin_amdgcn_readlane(vnS, a) * A : 0u;
-        const uint32_t n1 = ho ? (uint32_t)__builtin_amdgcn_readlane(vnO, b) * A : 0u;
+        const uint32_t n0 = ms * A, n1 = mo * A;
         uint64_t x0 = 0, x1 = 0, y0 = 0, y1 = 0;
         if (lane < n0) x0 = S.mv_clock[ia * S.mcap * A + lane];
         if (lane + kMpW < n0) x1 = S.mv_clock[ia * S.mcap * A + lane + kMpW];
@@ -143,41 +129,39 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
         if (lane + kMpW < n1) vr[1][lane + kMpW] = y1;
         mp_sync();
       }
-      // value clock row v of this key on a side (lane = actor)
-      auto srow = [&](uint32_t v) -> uint64_t {
-        if (VS) return lane < A ? vr[0][v * A + lane] : 0ull;
-        return rowv(S.mv_clock, ia * S.mcap + v, A, lane);
+      // value clock row v of this key on a side
+      auto srow = [&](uint32_t v) -> Row<NS> {
+        if (VS) return ldrow<NS>(&vr[0][v * A], A, lane);
+        return rowv<NS>(S.mv_clock, ia * S.mcap + v, A, lane);
       };
-      auto orow = [&](uint32_t v) -> uint64_t {
-        if (VS) return lane < A ? vr[1][v * A + lane] : 0ull;
-        return rowv(O.mv_clock, ib * O.mcap + v, A, lane);
+      auto orow = [&](uint32_t v) -> Row<NS> {
+        if (VS) return ldrow<NS>(&vr[1][v * A], A, lane);
+        return rowv<NS>(O.mv_clock, ib * O.mcap + v, A, lane);
       };
-      uint64_t ec = 0, del = 0;
+      Row<NS> ec = zrow<NS>(), del = zrow<NS>();
       bool keep;
       uint32_t nv = 0;
       if (hs && !ho) {  // other has not seen it, or saw it and dropped it
         ec = vsub(eS, cO);
         keep = vany(ec);
         del = vsub(cO, ec);
-        for (uint32_t v = 0; v < S.mv_n[ia] && v < S.mcap; ++v) { if (lane == 0u) vals[nv] = v; ++nv; }
+        for (uint32_t v = 0; v < ms; ++v) { if (lane == 0u) vals[nv] = v; ++nv; }
         mp_sync();
       } else if (ho && !hs) {
         ec = vsub(eO, cS);
         keep = vany(ec);
         del = vsub(cS, ec);
-        for (uint32_t v = 0; v < O.mv_n[ib] && v < O.mcap; ++v) { if (lane == 0u) vals[nv] = 256u | v; ++nv; }
+        for (uint32_t v = 0; v < mo; ++v) { if (lane == 0u) vals[nv] = 256u | v; ++nv; }
       } else {  // in both
-        const uint64_t common = (eS == eO && eS != 0ull) ? eS : 0ull;  // VClock::intersection
-        const uint64_t e1 = vsub(vsub(eS, common), cO), e2 = vsub(vsub(eO, common), cS);
-        uint64_t cm = common > e1 ? common : e1;
-        cm = cm > e2 ? cm : e2;
+        const Row<NS> common = vcommon(eS, eO);  // VClock::intersection
+        const Row<NS> e1 = vsub(vsub(eS, common), cO), e2 = vsub(vsub(eO, common), cS);
+        const Row<NS> cm = vmax(vmax(common, e1), e2);
         keep = vany(cm);
         ec = cm;
-        del = vsub(e1 > e2 ? e1 : e2, cm);
+        del = vsub(vmax(e1, e2), cm);
         // MVReg::merge (src/mvreg.rs:121-153): self's undominated, then other's undominated and new
-        const uint32_t ms = S.mv_n[ia] < S.mcap ? S.mv_n[ia] : S.mcap, mo = O.mv_n[ib] < O.mcap ? O.mv_n[ib] : O.mcap;
         for (uint32_t v = 0; v < ms; ++v) {
-          const uint64_t sv = srow(v);
+          const Row<NS> sv = srow(v);
           bool dom = false;
           for (uint32_t w = 0; w < mo && !dom; ++w) dom = vstrict_less(sv, orow(w));
           if (!dom) { if (lane == 0u) vals[nv] = v; ++nv; }
@@ -185,15 +169,14 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
         mp_sync();
         const uint32_t nkeep_s = nv;
         for (uint32_t w = 0; w < mo; ++w) {
-          const uint64_t ov = orow(w);
+          const Row<NS> ov = orow(w);
           bool dom = false;
           for (uint32_t v = 0; v < ms && !dom; ++v) dom = vstrict_less(ov, srow(v));
           if (dom) continue;
           bool dup = false;
           for (uint32_t q = 0; q < nv && !dup; ++q) {
             const uint32_t sl = vals[q];
-            const uint64_t kv = q < nkeep_s ? srow(sl & 255u) : orow(sl & 255u);
-            dup = __ballot(kv != ov) == 0ull;
+            dup = veq(q < nkeep_s ? srow(sl & 255u) : orow(sl & 255u), ov);
           }
           if (!dup) { if (lane == 0u) vals[nv] = 256u | w; ++nv; }
           mp_sync();
@@ -215,9 +198,10 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
             named = set_has(O.dset + di * O.scap, O.dset_n[di], key, lane);
           }
           if (!named) continue;
-          const uint64_t D = sa ? rowv(S.dclock, i * S.dcap + sa - 1u, A, lane) : rowv(O.dclock, i * O.dcap + sb - 1u, A, lane);
+          const Row<NS> D = sa ? rowv<NS>(S.dclock, i * S.dcap + sa - 1u, A, lane)
+                               : rowv<NS>(O.dclock, i * O.dcap + sb - 1u, A, lane);
           ec = vsub(ec, D);
-          del = del > D ? del : D;  // truncating by several clocks = by their max, slot by slot
+          del = vmax(del, D);  // truncating by several clocks = by their max, slot by slot
         }
         keep = vany(ec);
       }
@@ -227,16 +211,16 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
         } else {
           const uint64_t ir = i * R.kcap + nk;
           if (lane == 0u) R.keys[ir] = key;
-          if (lane < A) R.eclock[ir * A + lane] = ec;
+          strow<NS>(R.eclock + ir * A, ec, A, lane);
           uint32_t nout = 0;
           for (uint32_t q = 0; q < nv; ++q) {  // MVReg::truncate(del), order kept
             const uint32_t sl = vals[q];
             const bool fromO = sl >= 256u;
             const uint64_t src = fromO ? ib * O.mcap + (sl & 255u) : ia * S.mcap + (sl & 255u);
-            const uint64_t r = vsub(fromO ? orow(sl & 255u) : srow(sl & 255u), del);
+            const Row<NS> r = vsub(fromO ? orow(sl & 255u) : srow(sl & 255u), del);
             if (!vany(r)) continue;
             if (nout >= R.mcap) { over = true; break; }
-            if (lane < A) R.mv_clock[(ir * R.mcap + nout) * A + lane] = r;
+            strow<NS>(R.mv_clock + (ir * R.mcap + nout) * A, r, A, lane);
             if (lane == 0u) R.mv_val[ir * R.mcap + nout] = fromO ? O.mv_val[src] : S.mv_val[src];
             ++nout;
           }
@@ -249,17 +233,18 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
       if (ho) ++b;
     }
     if (lane == 0u) R.n_keys[i] = nk;
-    if (lane < A) R.clock[i * A + lane] = cM;
+    strow<NS>(R.clock + i * A, cM, A, lane);
     // ---- deferred kept: the combined clocks the merged clock does not cover, sets united
     uint32_t nd = 0;
     for (uint32_t c = 0; c < nc; ++c) {
       const uint32_t e = comb[c];
       const uint32_t sa = e & 255u, sb = e >> 8;
-      const uint64_t D = sa ? rowv(S.dclock, i * S.dcap + sa - 1u, A, lane) : rowv(O.dclock, i * O.dcap + sb - 1u, A, lane);
+      const Row<NS> D = sa ? rowv<NS>(S.dclock, i * S.dcap + sa - 1u, A, lane)
+                           : rowv<NS>(O.dclock, i * O.dcap + sb - 1u, A, lane);
       if (vle(D, cM)) continue;
       if (nd >= R.dcap) { over = true; break; }
       const uint64_t dr = i * R.dcap + nd;
-      if (lane < A) R.dclock[dr * A + lane] = D;
+      strow<NS>(R.dclock + dr * A, D, A, lane);
       uint32_t cnt = 0;
       if (lane == 0u) {  // sorted union of the two key sets
         const uint64_t* xs = sa ? S.dset + (i * S.dcap + sa - 1u) * S.scap : nullptr;
@@ -295,10 +280,16 @@ int launch_map_mvreg_merge(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_sl
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const uint64_t cap = (uint64_t)cus * 28u;  // 7 single-wave blocks per SIMD
   const uint32_t blocks = (uint32_t)(n_obj < cap ? n_obj : cap);
-  if (S.mcap * A <= kVsRows && O.mcap * A <= kVsRows)
-    hipLaunchKernelGGL(map_mvreg_merge_kernel<true>, dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A, status, ctl);
+  const bool vs = (uint64_t)S.mcap * A <= kVsRows && (uint64_t)O.mcap * A <= kVsRows;
+  if (A > 64u)  // 65-128 actors: two slots per lane
+    hipLaunchKernelGGL((map_mvreg_merge_kernel<false, 2>), dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A,
+                       status, ctl);
+  else if (vs)
+    hipLaunchKernelGGL((map_mvreg_merge_kernel<true, 1>), dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A,
+                       status, ctl);
   else
-    hipLaunchKernelGGL(map_mvreg_merge_kernel<false>, dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A, status, ctl);
+    hipLaunchKernelGGL((map_mvreg_merge_kernel<false, 1>), dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A,
+                       status, ctl);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 

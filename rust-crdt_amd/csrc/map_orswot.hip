@@ -25,6 +25,7 @@
 
 #include "../../include/crdts_hip.h"
 #include "kernels.h"
+#include "map_rows.h"
 #include "sched.h"
 
 namespace crdts_hip {
@@ -43,88 +44,7 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_re
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | (uint64_t)uni((uint32_t)v);
 }
-__device__ __forceinline__ uint64_t lane64(uint64_t v, uint32_t t) {
-  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), t) << 32) |
-         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, t);
-}
-// A dense clock row in registers: slot s of lane l is actor l + 64 s.
-template <int NS>
-struct Row {
-  uint64_t v[NS];
-};
-template <int NS>
-__device__ __forceinline__ Row<NS> zrow() {
-  Row<NS> r;
-  for (int k = 0; k < NS; ++k) r.v[k] = 0ull;
-  return r;
-}
-// VClock::subtract (src/vclock.rs:236-242), slot by slot
-template <int NS>
-__device__ __forceinline__ Row<NS> vsub(Row<NS> e, Row<NS> c) {
-  for (int k = 0; k < NS; ++k) e.v[k] = c.v[k] >= e.v[k] ? 0ull : e.v[k];
-  return e;
-}
-template <int NS>
-__device__ __forceinline__ Row<NS> vmax(Row<NS> a, Row<NS> b) {
-  for (int k = 0; k < NS; ++k) a.v[k] = a.v[k] > b.v[k] ? a.v[k] : b.v[k];
-  return a;
-}
-template <int NS>
-__device__ __forceinline__ bool vany(Row<NS> v) {
-  bool a = false;
-  for (int k = 0; k < NS; ++k) a = a || v.v[k] != 0ull;
-  return __ballot(a) != 0ull;
-}
-// `d <= c` on PartialOrd (src/vclock.rs:59-71) for dense rows: every slot of d within c
-template <int NS>
-__device__ __forceinline__ bool vle(Row<NS> d, Row<NS> c) {
-  bool gt = false;
-  for (int k = 0; k < NS; ++k) gt = gt || d.v[k] > c.v[k];
-  return __ballot(gt) == 0ull;
-}
-// VClock::intersection (src/vclock.rs:219-228): the slots equal on both sides
-template <int NS>
-__device__ __forceinline__ Row<NS> vcommon(Row<NS> a, Row<NS> b) {
-  for (int k = 0; k < NS; ++k) a.v[k] = (a.v[k] == b.v[k] && a.v[k] != 0ull) ? a.v[k] : 0ull;
-  return a;
-}
-// CLOCK ORDER of two dense rows (lexicographic over their (actor, counter)
-// pairs, a proper prefix first): decided at the first actor where they differ
-template <int NS>
-__device__ int vorder(Row<NS> p, Row<NS> q, uint32_t lane) {
-  for (int k = 0; k < NS; ++k) {
-    const uint64_t diff = __ballot(p.v[k] != q.v[k]);
-    if (!diff) continue;
-    const uint32_t x = (uint32_t)__builtin_ctzll(diff);
-    const uint64_t px = lane64(p.v[k], x), qx = lane64(q.v[k], x);
-    if (px && qx) return px < qx ? -1 : 1;
-    // one side has no entry at actor 64k + x: the other's next entry decides
-    bool later = false;  // does the side WITHOUT x hold an actor above it?
-    for (int j = k; j < NS; ++j) {
-      const uint64_t w = !px ? p.v[j] : q.v[j];
-      later = later || (w != 0ull && (j > k || lane > x));
-    }
-    const bool any = __ballot(later) != 0ull;
-    return !px ? (any ? 1 : -1) : (any ? -1 : 1);
-  }
-  return 0;
-}
-// row `row` of a [.][A] array / a row at `base`
-template <int NS>
-__device__ __forceinline__ Row<NS> ldrow(const uint64_t* base, uint32_t A, uint32_t lane) {
-  Row<NS> r;
-  for (int k = 0; k < NS; ++k) r.v[k] = lane + 64u * k < A ? base[lane + 64u * k] : 0ull;
-  return r;
-}
-template <int NS>
-__device__ __forceinline__ Row<NS> rowv(const uint64_t* base, uint64_t row, uint32_t A, uint32_t lane) {
-  return ldrow<NS>(base + row * A, A, lane);
-}
-template <int NS>
-__device__ __forceinline__ void strow(uint64_t* base, Row<NS> r, uint32_t A, uint32_t lane) {
-  for (int k = 0; k < NS; ++k)
-    if (lane + 64u * k < A) base[lane + 64u * k] = r.v[k];
-}
+using namespace maprow;  // Row<NS> and the VClock ops on it (map_rows.h)
 __device__ __forceinline__ bool set_has(const uint64_t* set, uint32_t n, uint64_t key, uint32_t lane) {
   bool f = false;
   for (uint32_t j = lane; j < n; j += kMoW) f = f || set[j] == key;

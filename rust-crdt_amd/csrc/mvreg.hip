@@ -198,6 +198,85 @@ __global__ __launch_bounds__(256) void mvreg_merge_kernel(
   }
 }
 
+// Registers past the fast kernel's limits (> 64 slots per side, or rows that
+// do not fit its LDS): one wave per pair, the clock rows read from HBM, the
+// same keep rules and output form (self's survivors in order, then other's;
+// unused slots zeroed); the kept flags of the current pair in LDS.
+constexpr uint32_t kMvBigCap = 1024;  // slots per side
+
+__device__ __forceinline__ uint32_t mv_cmp_rows(const uint64_t* a, const uint64_t* b, uint32_t A) {
+  uint32_t f = 0u;  // 1: some a > b, 2: some a < b
+  for (uint32_t x = 0; x < A; ++x) f |= (a[x] > b[x] ? 1u : 0u) | (a[x] < b[x] ? 2u : 0u);
+  return f;
+}
+
+__global__ __launch_bounds__(kMW) void mvreg_merge_big_kernel(
+    const uint32_t* __restrict__ sn, const uint64_t* __restrict__ sclk, const uint64_t* __restrict__ sval, uint32_t scap,
+    const uint32_t* __restrict__ on, const uint64_t* __restrict__ oclk, const uint64_t* __restrict__ oval, uint32_t ocap,
+    uint32_t* __restrict__ outn, uint64_t* __restrict__ outclk, uint64_t* __restrict__ outval, uint32_t outcap,
+    uint64_t n_obj, uint32_t A, int* __restrict__ status) {
+  __shared__ uint8_t ks_s[2 * kMvBigCap];  // kept flags: self slots, then other slots
+  const uint32_t lane = threadIdx.x;
+  for (uint64_t o = blockIdx.x; o < n_obj; o += gridDim.x) {
+    const uint32_t ns = __builtin_amdgcn_readfirstlane(sn[o]), no = __builtin_amdgcn_readfirstlane(on[o]);
+    if (ns > scap || no > ocap) {
+      if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
+      continue;
+    }
+    const uint64_t* S = sclk + o * scap * A;
+    const uint64_t* O = oclk + o * ocap * A;
+    // self i: kept unless some other clock strictly dominates it
+    uint32_t nks = 0u;
+    mv_sync();  // the previous pair's readers of ks_s are done
+    for (uint32_t i = lane; i < ns; i += kMW) {
+      bool k = true;
+      for (uint32_t j = 0; j < no && k; ++j) k = mv_cmp_rows(S + (uint64_t)i * A, O + (uint64_t)j * A, A) != 2u;
+      ks_s[i] = k ? 1u : 0u;
+    }
+    mv_sync();
+    for (uint32_t i = lane; i < ns; i += kMW) nks += ks_s[i];
+    // other j: kept unless a self clock strictly dominates it, it equals a kept
+    // self clock, or it equals an earlier other clock
+    uint32_t nko = 0u;
+    for (uint32_t c0 = 0; c0 < no; c0 += kMW) {
+      const uint32_t j = c0 + lane;
+      bool k = j < no;
+      for (uint32_t i = 0; i < ns && k; ++i) {
+        const uint32_t f = mv_cmp_rows(S + (uint64_t)i * A, O + (uint64_t)j * A, A);
+        k = f != 1u && !(f == 0u && ks_s[i]);
+      }
+      for (uint32_t jj = 0; jj < j && k; ++jj) k = mv_cmp_rows(O + (uint64_t)jj * A, O + (uint64_t)j * A, A) != 0u;
+      nko += (uint32_t)__popcll(__ballot(k));
+      if (j < no) ks_s[ns + j] = k ? 1u : 0u;
+    }
+    for (uint32_t d = 32; d >= 1; d >>= 1) nks += (uint32_t)__shfl_xor((int)nks, (int)d, kMW);
+    const uint32_t nk = __builtin_amdgcn_readfirstlane(nks) + nko;
+    if (nk > outcap) {
+      if (lane == 0u) atomicCAS(status, 0, CRDT_ECAPACITY);
+      continue;
+    }
+    mv_sync();
+    // survivors in order, one row per lane-round; then the unused slots zeroed
+    uint64_t* oc = outclk + o * (uint64_t)outcap * A;
+    uint32_t pos = 0u;
+    for (uint32_t c0 = 0; c0 < ns + no; c0 += kMW) {
+      const uint32_t t = c0 + lane;
+      const bool k = t < ns + no && ks_s[t];
+      const uint64_t m = __ballot(k);
+      const uint32_t r = pos + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (k) {
+        const uint64_t* src = t < ns ? S + (uint64_t)t * A : O + (uint64_t)(t - ns) * A;
+        for (uint32_t x = 0; x < A; ++x) oc[(uint64_t)r * A + x] = src[x];
+        outval[o * outcap + r] = t < ns ? sval[o * scap + t] : oval[o * ocap + (t - ns)];
+      }
+      pos += (uint32_t)__popcll(m);
+    }
+    for (uint64_t e = (uint64_t)nk * A + lane; e < (uint64_t)outcap * A; e += kMW) oc[e] = 0ull;
+    for (uint32_t k = nk + lane; k < outcap; k += kMW) outval[o * outcap + k] = 0u;
+    if (lane == 0u) outn[o] = nk;
+  }
+}
+
 }  // namespace
 
 int launch_vclock_cmp(const uint64_t* a, const uint64_t* b, uint64_t n, uint32_t A, int8_t* out, hipStream_t stream) {
@@ -219,7 +298,15 @@ int launch_mvreg_merge(const uint32_t* sn, const uint64_t* sclk, const uint64_t*
   if (n_obj == 0) return CRDT_OK;
   // per-wave LDS: clock rows, flag matrices, slot table; 16-B multiple
   const size_t per_wave = (8ull * (scap + ocap) * A + (size_t)scap * ocap + (size_t)ocap * ocap + outcap + 15u) & ~15ull;
-  if (per_wave > 60u * 1024u || scap > 64u || ocap > 64u) return CRDT_EINVAL;
+  if (scap > kMvBigCap || ocap > kMvBigCap) return CRDT_EINVAL;
+  if (per_wave > 60u * 1024u || scap > 64u || ocap > 64u) {  // past the fast kernel's limits
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint64_t cap = (uint64_t)cus * 16u;
+    hipLaunchKernelGGL(mvreg_merge_big_kernel, dim3((uint32_t)(n_obj < cap ? n_obj : cap)), dim3(kMW), 0, stream, sn,
+                       sclk, sval, scap, on, oclk, oval, ocap, outn, outclk, outval, outcap, n_obj, A, status);
+    return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+  }
   uint32_t W = 4;  // waves per block, as many as 60 KB of LDS allow
   while (W > 1u && W * per_wave > 60u * 1024u) --W;
   int dev = 0, cus = 256;

@@ -121,3 +121,89 @@ def test_gpu_map_malformed_counts_rejected(gpu, oracle):
         with pytest.raises(crdts_hip.CrdtError) as e:
             gpu.map_mvreg_merge(bad.to("cuda:0"), R.to("cuda:0"), 8)
         assert e.value.code == crdts_hip.CRDT_ENONCANON
+
+
+def _exact(gpu, oracle, S, O, A):
+    import crdts_hip
+
+    exp = oracle.map_merge(S, O, A).canonical()
+    out = crdts_hip.MapSlab.alloc(S.a["n_keys"].shape[0], A, S.kcap + O.kcap, S.mcap + O.mcap, S.dcap + O.dcap,
+                                  S.scap + O.scap, device="cuda:0")
+    got = gpu.map_mvreg_merge(S.to("cuda:0"), O.to("cuda:0"), A, out=out).canonical()
+    for f in exp.a:
+        bad = np.nonzero((got.a[f] != exp.a[f]).reshape(len(exp.a["n_keys"]), -1).any(axis=1))[0]
+        assert len(bad) == 0, f"{f}: {len(bad)} maps differ, first {bad[:5].tolist()}"
+    return exp
+
+
+@pytest.mark.gpu
+def test_gpu_map_200_keys_100_actors(gpu, oracle):
+    """Maps past the round-3 slab limits (32 keys, 64 actors): ~170-260 keys
+    per map over 100 actors (two slots per lane: lane l holds actors l and
+    l + 64; keys past 64 read their value counts from the slab), both
+    orientations, slab-row exact against the oracle (src/map.rs:192-269)."""
+    A = 100
+    L, R = oracle.map_generate(0x200B, 48, A, 400, 450, (512, 8, 32, 64))
+    assert (L.a["n_keys"] >= 200).sum() > 5 and L.a["clock"][:, 64:].any()
+    for S, O in ((L, R), (R, L)):
+        exp = _exact(gpu, oracle, S, O, A)
+    assert exp.a["n_keys"].max() > 128
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("A", [60, 128])
+def test_gpu_map_many_concurrent_values(gpu, oracle, A):
+    """Registers of up to 30 (A = 60) / 62 (A = 128) concurrent values per
+    side (the round-3 limit was 16): on every key of map L, each of L's
+    actors puts a value with only its own dot in the clock (none dominates
+    another), R does the same with the other actors and a few values that
+    dominate some of L's; the merged register keeps up to 60 / 122 values
+    (MVReg::merge, src/mvreg.rs:121-153).
+    Built on the Python op path, merged on the GPU, slab-exact vs the oracle."""
+    import crdts_hip
+    import map_slab
+    from map_slab import crdts_ref
+
+    rng = np.random.default_rng(A)
+    n, keys = 16, 3
+    half = A // 2
+    caps = (4, 64, 4, 4)
+    L = crdts_hip.MapSlab.alloc(n, A, *caps)
+    R = crdts_hip.MapSlab.alloc(n, A, *caps)
+    for i in range(n):
+        for slab, actors in ((L, range(0, half)), (R, range(half, A))):
+            m = crdts_ref.Map(crdts_ref.MVReg)
+            acts = [a for a in actors if rng.random() < 0.9][:64]
+            for k in range(keys):
+                for a in acts:
+                    dot = (a, m.clock.get(a) + 1)
+                    clk = crdts_ref.VClock({a: dot[1]})
+                    if slab is R and rng.random() < 0.1:  # a put that saw one of L's values: dominates it
+                        clk.witness(int(rng.integers(0, half)), 1)
+                    m.apply_up(dot, k, lambda r, c=clk, v=int(rng.integers(1 << 40)): r.apply_put(c, v))
+            map_slab.mvreg_map_to_row(m, slab, i, A)
+    assert L.a["mv_n"].max() > 16  # past the round-3 limits: 16 per side, 32 merged
+    for S, O in ((L, R), (R, L)):
+        exp = _exact(gpu, oracle, S, O, A)
+    assert exp.a["mv_n"].max() > 32
+
+
+@pytest.mark.gpu
+def test_gpu_map_slab_limits(gpu, oracle):
+    """The documented per-side limits (include/crdts_hip.h): kcap 4096, mcap
+    128, dcap 64, scap 4096, n_actors 128 are accepted; one past each is
+    CRDT_EINVAL before any launch."""
+    import crdts_hip
+    from crdts_hip._lib import CRDT_EINVAL
+
+    def run(A, kcap=4, mcap=4, dcap=4, scap=4):
+        S = crdts_hip.MapSlab.alloc(2, A, kcap, mcap, dcap, scap, device="cuda:0")
+        return gpu.map_mvreg_merge(S, S, A)
+
+    run(128)
+    for kw in ({"kcap": 4096}, {"mcap": 128}, {"dcap": 64}, {"scap": 4096}):
+        run(8, **kw)
+    for A, kw in ((129, {}), (8, {"kcap": 4097}), (8, {"mcap": 129}), (8, {"dcap": 65}), (8, {"scap": 4097})):
+        with pytest.raises(crdts_hip.CrdtError) as e:
+            run(A, **kw)
+        assert e.value.code == CRDT_EINVAL, (A, kw)

@@ -88,6 +88,31 @@ def test_gpu_mvreg_merge(gpu, oracle, A, cap, hi):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("A,cap,hi,n", [(8, 100, 3, 3000), (16, 300, 2, 300), (512, 16, 2, 2000)])
+def test_gpu_mvreg_merge_big(gpu, oracle, A, cap, hi, n):
+    """Registers past the fast kernel's limits take the one-wave kernel:
+    more than 64 slots per side (100, 300), or rows too large for its LDS
+    (16 slots x 512 actors: 128 KB per wave). Exact vs the oracle."""
+    import torch
+
+    rng = np.random.default_rng(A * 1000 + cap)
+    S = _slab(_random_regs(rng, n, cap, A, hi), cap, A)
+    O = _slab(_random_regs(rng, n, cap, A, hi), cap, A)
+    exp = oracle.mvreg_merge(*S, *O, A, 2 * cap)
+
+    def dev(t):
+        t = np.ascontiguousarray(t)
+        return torch.from_numpy(t.view(np.int32 if t.dtype == np.uint32 else np.int64)).to("cuda:0")
+
+    got = gpu.mvreg_merge(tuple(dev(x) for x in S), tuple(dev(x) for x in O), A)
+    gn = got[0].cpu().numpy().view(np.uint32)
+    assert (gn == exp[0]).all()
+    assert (got[1].cpu().numpy().view(np.uint64) == exp[1]).all()
+    assert (got[2].cpu().numpy().view(np.uint64) == exp[2]).all()
+    assert exp[0].max() > (64 if cap > 64 else 8)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("A", [1, 8, 16, 64, 100, 300])
 def test_gpu_partial_cmp(gpu, oracle, A):
     import torch
