@@ -61,7 +61,7 @@ def parse():
     p.add_argument("--settle-ms", type=float, default=200.0)
     p.add_argument("--workload", default="orswot",
                    choices=["orswot", "vclock", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply",
-                            "mvreg", "map", "map_orswot", "clock_csr", "truncate", "spawn_check"])
+                            "mvreg", "map", "map_orswot", "map_map", "clock_csr", "truncate", "spawn_check"])
     p.add_argument("--replicas", type=int, default=8, help="orswot_csr at N=1: replicas folded locally")
     p.add_argument("--n-actors", type=int, default=16,
                    help="orswot: dense top-clock actors (config 3: 16; 33-64 take the 64-bit actor-mask join)")
@@ -1474,6 +1474,94 @@ def run_map(args, rank, world, local):
     return res
 
 
+def run_map_map(args, rank, world, local):
+    """Nested maps — the reference's TestMap, Map<u64, Map<u64, MVReg<u64>>>
+    (test/map.rs:4-8; Map::merge src/map.rs:191-268 with the inner map's merge
+    and truncate as the value's): batched crdt_map_map_merge over 200k
+    replica pairs per GPU, A = 16, <= 4 outer and 4 inner keys per map. The
+    pairs come from the op-path generator of the parity tests
+    (tests/nested_gen.py: nested puts, outer and inner removes through read
+    contexts, early third-replica removes left deferred, partial out-of-order
+    exchange): 10k distinct pairs, tiled. A step = one crdt_map_map_merge
+    (three launches: outer pass, inner merges, inner truncations)."""
+    import random
+    import time as _t
+
+    import numpy as np
+    import torch
+
+    import crdts_hip
+
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import map_slab
+    import nested_gen
+
+    n = args.n_obj or 200_000
+    A, caps, inner = 16, dict(kcap=4, dcap=8, scap=4), (4, 8, 8, 4)
+    n0 = min(n, 10_000)
+    rng = random.Random(0xC0FFEE09 + rank)
+    pairs = [nested_gen.pair(rng, list(range(A))) for _ in range(n0)]
+    L0 = crdts_hip.MapMapSlab.alloc(n0, A, inner_caps=inner, **caps)
+    R0 = crdts_hip.MapMapSlab.alloc(n0, A, inner_caps=inner, **caps)
+    for i, (x, y) in enumerate(pairs):
+        map_slab.nested_map_to_row(x, L0, i, A)
+        map_slab.nested_map_to_row(y, R0, i, A)
+    reps = -(-n // n0)
+
+    def tile(S):
+        t = lambda v: np.concatenate([v] * reps)[: n * (v.shape[0] // n0)]  # noqa: E731
+        return crdts_hip.MapMapSlab({f: t(v) for f, v in S.a.items()}, S.kcap, S.dcap, S.scap,
+                                    crdts_hip.MapSlab({f: t(v) for f, v in S.inner.a.items()}, *S.inner_caps))
+
+    L, R = tile(L0), tile(R0)
+    eng = crdts_hip.Engine(local)
+    dev = f"cuda:{local}"
+    dL, dR = L.to(dev), R.to(dev)
+    out = eng.map_map_merge(dL, dR, A)
+    h = out.host()
+    for i in range(0, n0, max(1, n0 // 500)):  # parity on a sample: the restatement's merge
+        exp = pairs[i][0].clone()
+        exp.merge(pairs[i][1])
+        assert map_slab.nested_map_from_row(h, i) == exp, f"nested map merge parity: pair {i}"
+    stream = torch.cuda.Stream(device=local)
+
+    def step():  # into the same output slabs every step (the merge writes only its used slots)
+        eng.map_map_merge(dL, dR, A, stream=stream, check_status=False, out=out)
+
+    wall, ev_ms = _timed_steps(args, world, stream, step)
+    eng.status(stream)
+    alg = L.used_bytes() + R.used_bytes() + out.used_bytes()
+    total = sum_over_ranks(float(n * args.steps), world)
+    res = {
+        "metric": "nested Map<u64, Map<u64, MVReg>> merges/sec (node)", "value": total / wall, "unit": "merges/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": f"synthetic: {n0} op-simulated TestMap replica pairs (tests/nested_gen.py), tiled to {n}",
+        "config": {"workload": f"map_map: {n} nested map merges per GPU, A={A}, outer caps {caps}, inner caps {inner}",
+                   "parallelism": f"dp{world} (objects sharded)"},
+    }
+    if world == 1:
+        ach = alg / (ev_ms * 1e-3) / 1e9
+        res["roofline"] = {"bound": "hbm", "kernel": "map_map_outer_kernel + map_mvreg_merge_kernel (tasks) + "
+                           "map_mvreg_truncate_kernel", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": ach / HBM_PEAK_GBS, "kernel_ms": ev_ms, "alg_bytes_per_launch": alg,
+                           "alg_bytes_def": "the used slots of both inputs and the output, outer and nested",
+                           "traffic": wl_traffic(args, "map_map", "map_map_outer_kernel", "map_mvreg_merge_kernel",
+                                                 "map_mvreg_truncate_kernel")}
+        if not args.no_cpu_baseline:
+            mm = 2000
+            t0 = _t.perf_counter()
+            for x, y in pairs[:mm]:
+                z = x.clone()
+                z.merge(y)
+            secs = _t.perf_counter() - t0
+            res["cpu_baseline"] = {"value": mm / secs, "unit": "merges/s", "cores": 1, "kind": "port",
+                                   **cpu_cores_note(),
+                                   "sample": f"{mm} nested map merges, the Python restatement (oracle/crdts_ref.py), "
+                                             "1 thread"}
+    return res
+
+
 def run_map_orswot(args, rank, world, local):
     """SURVEY.md §8(f) rank 3 as written: batched Map<u64, Orswot<u64, A>, A>::merge
     (src/map.rs:192-269, nested Orswot::merge / truncate src/orswot.rs:87-172)
@@ -1570,6 +1658,8 @@ def main():
         res = run_map(args, rank, world, local)
     elif args.workload == "map_orswot":
         res = run_map_orswot(args, rank, world, local)
+    elif args.workload == "map_map":
+        res = run_map_map(args, rank, world, local)
     elif args.workload == "clock_csr":
         res = run_clock_csr(args, rank, world, local)
     elif args.workload == "truncate":

@@ -493,6 +493,40 @@ int crdt_map_mvreg_merge(crdt_ctx* ctx, const crdt_map_mvreg_slab* self, const c
                          const crdt_map_mvreg_slab* out, size_t n_obj, uint32_t n_actors, void* stream);
 
 /* ------------------------------------------------------------------------ *
+ * Map<K, Map<K, MVReg<u64, A>, A>, A>::merge, batched: the reference's own
+ * Map test type (TestMap, test/map.rs:4-8; Map::merge src/map.rs:191-268 with
+ * the inner map's merge and Causal::truncate :131-158 as the value's). Keys
+ * are u64. Object i's outer map:
+ *   clock[A], n_keys, keys[kcap] ascending, eclock[kcap][A]
+ *   n_def, dclock[dcap][A] (CLOCK ORDER), dset_n[dcap], dset[dcap][scap]
+ * and, for key slot k, its nested map as object i * kcap + k of `inner` (a
+ * crdt_map_mvreg_slab of n_obj * kcap maps; its own limits as above).
+ * Outer limits per side: kcap <= 4096, dcap <= 64, scap <= 4096; n_actors <=
+ * 128; output capacities (outer and inner) >= the sums of the inputs' (else
+ * CRDT_EINVAL); a result past them latches CRDT_ECAPACITY. d_scratch needs
+ * crdt_map_map_merge_scratch_bytes(out, n_obj, n_actors) bytes (the per-slot
+ * merge tasks, truncating clocks and a scratch inner slab). Only used slots
+ * of the output are written. Where two deferred clocks of an inner map
+ * become equal under truncation the later one's key set is kept (the
+ * reference inserts into a HashMap there). */
+typedef struct crdt_map_map_slab {
+  uint64_t* clock;
+  uint32_t* n_keys;
+  uint64_t* keys;
+  uint64_t* eclock;
+  uint32_t* n_def;
+  uint64_t* dclock;
+  uint32_t* dset_n;
+  uint64_t* dset;
+  uint32_t kcap, dcap, scap;
+  crdt_map_mvreg_slab inner;
+} crdt_map_map_slab;
+size_t crdt_map_map_merge_scratch_bytes(const crdt_map_map_slab* out, size_t n_obj, uint32_t n_actors);
+int crdt_map_map_merge(crdt_ctx* ctx, const crdt_map_map_slab* self, const crdt_map_map_slab* other,
+                       const crdt_map_map_slab* out, size_t n_obj, uint32_t n_actors, void* d_scratch,
+                       size_t scratch_bytes, void* stream);
+
+/* ------------------------------------------------------------------------ *
  * Map<K, Orswot<u64, A>, A>::merge, batched (SURVEY.md §8(f) rank 3 as
  * written: src/map.rs:192-269 with the nested value's Causal::truncate,
  * src/orswot.rs:159-172, and Orswot::merge src/orswot.rs:87-157 for keys in

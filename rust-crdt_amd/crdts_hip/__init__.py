@@ -25,7 +25,7 @@ __all__ = [
     "Engine", "OrswotBatch", "GenParams", "CrdtError", "generate_orswot", "generate_dense", "HostOrswot",
     "Orswot", "VClock", "GCounter", "PNCounter", "merge_batch", "decode_record", "encode_record",
     "record_bytes", "CONFIG3", "EXPORTS", "LIB_PATH", "CONFIG5", "SPARSE_CLOCK", "generate_replicas", "ClockBatch",
-    "generate_clocks_csr",
+    "generate_clocks_csr", "MapMapSlab",
 ]
 
 # SURVEY.md §8(d) config 3 / BASELINE.json configs[2].
@@ -285,6 +285,97 @@ class MapSlab:
         ptr = [C.c_void_p(v.data_ptr() if hasattr(v, "data_ptr") else v.ctypes.data) for v in
                (self.a[f] for f in self.FIELDS)]
         return MapSlabC(*ptr, self.kcap, self.mcap, self.dcap, self.scap)
+
+
+class MapMapSlab:
+    """Dense slab of Map<u64, Map<u64, MVReg<u64, A>, A>, A> states — the
+    reference's TestMap (crdt_map_map_slab, include/crdts_hip.h): the outer
+    map's arrays (shapes below) and `inner`, a MapSlab of n * kcap nested
+    maps (key slot k of object i: inner object i * kcap + k)."""
+
+    FIELDS = ("clock", "n_keys", "keys", "eclock", "n_def", "dclock", "dset_n", "dset")
+
+    def __init__(self, arrays, kcap, dcap, scap, inner):
+        self.a = dict(arrays)
+        self.kcap, self.dcap, self.scap = kcap, dcap, scap
+        self.inner = inner
+
+    @property
+    def n(self):
+        return int(self.a["n_keys"].shape[0])
+
+    @staticmethod
+    def shapes(n, A, kcap, dcap, scap):
+        return {"clock": (n, A), "n_keys": (n,), "keys": (n, kcap), "eclock": (n, kcap, A), "n_def": (n,),
+                "dclock": (n, dcap, A), "dset_n": (n, dcap), "dset": (n, dcap, scap)}
+
+    @classmethod
+    def alloc(cls, n, A, kcap, dcap, scap, inner_caps, device=None):
+        """inner_caps: (kcap, mcap, dcap, scap) of the nested maps."""
+        out = {}
+        for f, shp in cls.shapes(n, A, kcap, dcap, scap).items():
+            u32 = f in ("n_keys", "n_def", "dset_n")
+            if device is None:
+                out[f] = np.zeros(shp, np.uint32 if u32 else np.uint64)
+            else:
+                torch = _torch()
+                out[f] = torch.zeros(shp, dtype=torch.int32 if u32 else torch.int64, device=device)
+        return cls(out, kcap, dcap, scap, MapSlab.alloc(n * kcap, A, *inner_caps, device=device))
+
+    @property
+    def inner_caps(self):
+        return (self.inner.kcap, self.inner.mcap, self.inner.dcap, self.inner.scap)
+
+    def to(self, device):
+        torch = _torch()
+        return MapMapSlab({f: torch.from_numpy(np.ascontiguousarray(v).view(np.int32 if v.dtype == np.uint32
+                                                                              else np.int64)).to(device)
+                           for f, v in self.a.items()}, self.kcap, self.dcap, self.scap, self.inner.to(device))
+
+    def host(self):
+        return MapMapSlab({f: (v.cpu().numpy().view(np.uint32 if v.dtype.itemsize == 4 else np.uint64)
+                               if hasattr(v, "cpu") else v) for f, v in self.a.items()},
+                          self.kcap, self.dcap, self.scap, self.inner.host())
+
+    def canonical(self):
+        """Host copy with every slot past its count zeroed, outer and inner
+        (nested maps of unused key slots zeroed whole)."""
+        h = self.host()
+        a = {f: np.array(v, copy=True) for f, v in h.a.items()}
+        key = np.arange(self.kcap)[None, :] < a["n_keys"][:, None]
+        dfr = np.arange(self.dcap)[None, :] < a["n_def"][:, None]
+        dset = dfr[..., None] & (np.arange(self.scap)[None, None, :] < a["dset_n"][..., None])
+        for f, m in (("keys", key), ("eclock", key[..., None]), ("dclock", dfr[..., None]), ("dset_n", dfr),
+                     ("dset", dset)):
+            a[f][~np.broadcast_to(m, a[f].shape)] = 0
+        inner = h.inner.canonical()
+        dead = ~key.reshape(-1)
+        for f, v in inner.a.items():
+            v[dead] = 0
+        return MapMapSlab(a, self.kcap, self.dcap, self.scap, inner)
+
+    def used_bytes(self):
+        """Bytes of the used slots: the outer map's, and the nested maps' of
+        its used key slots (the state's own bytes, not the capacity)."""
+        h = self.host()
+        a = h.a
+        key = np.arange(self.kcap)[None, :] < a["n_keys"][:, None]
+        dfr = np.arange(self.dcap)[None, :] < a["n_def"][:, None]
+        dset = dfr[..., None] & (np.arange(self.scap)[None, None, :] < a["dset_n"][..., None])
+        A = a["clock"].shape[1]
+        outer = 8 * A * self.n + 8 * self.n + int(key.sum()) * (8 + 8 * A) + int(dfr.sum()) * (8 * A + 4) + \
+            int(dset.sum()) * 8
+        used = key.reshape(-1)
+        inner = int(sum(int((m.reshape(m.shape[0], -1)[used]).sum()) * h.inner.a[f].dtype.itemsize
+                        for f, m in h.inner.used_masks().items()))
+        return outer + inner
+
+    def cstruct(self):
+        from ._lib import MAP_MAP_FIELDS, MapMapSlabC
+
+        ptr = [C.c_void_p(self.a[f].data_ptr() if hasattr(self.a[f], "data_ptr") else self.a[f].ctypes.data)
+               for f in MAP_MAP_FIELDS]
+        return MapMapSlabC(*ptr, self.kcap, self.dcap, self.scap, self.inner.cstruct())
 
 
 class MapOrswotSlab:
@@ -653,6 +744,30 @@ class Engine:
         s, o, r = S.cstruct(), O.cstruct(), R.cstruct()
         check(lib.crdt_map_mvreg_merge(self.ctx, C.byref(s), C.byref(o), C.byref(r), n, n_actors,
                                        self._stream(stream)), "map_mvreg_merge")
+        if check_status:
+            self.status(stream)
+        return R
+
+    # ------------------------------------------------ Map<u64, Map<u64, MVReg<u64>>>
+    def map_map_merge(self, S: "MapMapSlab", O: "MapMapSlab", n_actors, stream=None, check_status=True, out=None):
+        """Map::merge of nested maps (src/map.rs:191-268 with the inner map as
+        the value: its merge and Causal::truncate) of device slabs; returns
+        the output slab (capacities: the sums of the inputs', outer and inner)."""
+        torch = _torch()
+        n = S.n
+        R = out if out is not None else MapMapSlab.alloc(
+            n, n_actors, S.kcap + O.kcap, S.dcap + O.dcap, S.scap + O.scap,
+            tuple(x + y for x, y in zip(S.inner_caps, O.inner_caps)), device=S.a["clock"].device)
+        s, o, r = S.cstruct(), O.cstruct(), R.cstruct()
+        nb = int(lib.crdt_map_map_merge_scratch_bytes(C.byref(r), n, n_actors))
+        # the engine keeps the scratch (grown as needed): a launch in flight on
+        # another stream never sees it freed
+        sc = getattr(self, "_map_map_scratch", None)
+        if sc is None or sc.numel() < nb or sc.device != S.a["clock"].device:
+            sc = self._map_map_scratch = torch.empty(max(16, nb), dtype=torch.uint8, device=S.a["clock"].device)
+        check(lib.crdt_map_map_merge(self.ctx, C.byref(s), C.byref(o), C.byref(r), n, n_actors,
+                                     C.c_void_p(sc.data_ptr()), int(sc.numel()), self._stream(stream)),
+              "map_map_merge")
         if check_status:
             self.status(stream)
         return R

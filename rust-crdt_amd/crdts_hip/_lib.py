@@ -72,6 +72,7 @@ EXPORTS = [
     "crdt_comm_count", "crdt_orswot_replica_join_transport", "crdt_orswot_generate_replicas_subset",
     "crdt_dense_merge_host", "crdt_vclock_csr_merge", "crdt_gcounter_csr_merge", "crdt_pncounter_csr_merge",
     "crdt_orswot_truncate", "crdt_ctx_host_syncs", "crdt_orswot_fold",
+    "crdt_map_map_merge_scratch_bytes", "crdt_map_map_merge",
 ]
 
 CRDT_COMM_ID_BYTES = 128
@@ -104,6 +105,15 @@ class MapSlabC(C.Structure):
     _fields_ = [(f, C.c_void_p) for f in ("clock", "n_keys", "keys", "eclock", "mv_n", "mv_clock", "mv_val", "n_def",
                                           "dclock", "dset_n", "dset")] + \
                [(f, C.c_uint32) for f in ("kcap", "mcap", "dcap", "scap")]
+
+
+MAP_MAP_FIELDS = ("clock", "n_keys", "keys", "eclock", "n_def", "dclock", "dset_n", "dset")
+
+
+class MapMapSlabC(C.Structure):
+    """crdt_map_map_slab (include/crdts_hip.h): the outer map and its inner Map<u64, MVReg> slab."""
+    _fields_ = [(f, C.c_void_p) for f in MAP_MAP_FIELDS] + [(f, C.c_uint32) for f in ("kcap", "dcap", "scap")] + \
+               [("inner", MapSlabC)]
 
 
 MAP_ORSWOT_FIELDS = ("clock", "n_keys", "keys", "eclock", "vclock", "vn_mem", "vmem", "vmclock", "vn_def", "vdclock",
@@ -208,6 +218,9 @@ def _load():
         "crdt_map_mvreg_merge": (I, [P, C.POINTER(MapSlabC), C.POINTER(MapSlabC), C.POINTER(MapSlabC), SZ, U32, P]),
         "crdt_map_orswot_merge": (I, [P, C.POINTER(MapOrswotSlabC), C.POINTER(MapOrswotSlabC),
                                       C.POINTER(MapOrswotSlabC), SZ, U32, P]),
+        "crdt_map_map_merge_scratch_bytes": (SZ, [C.POINTER(MapMapSlabC), SZ, U32]),
+        "crdt_map_map_merge": (I, [P, C.POINTER(MapMapSlabC), C.POINTER(MapMapSlabC), C.POINTER(MapMapSlabC), SZ,
+                                   U32, P, SZ, P]),
         "crdt_comm_unique_id": (I, [P]),
         "crdt_comm_init": (I, [P, P, I, I]),
         "crdt_comm_destroy": (I, [P]),

@@ -584,6 +584,46 @@ int crdt_map_mvreg_merge(crdt_ctx* ctx, const crdt_map_mvreg_slab* self, const c
   return launch_map_mvreg_merge(*self, *other, *out, n_obj, n_actors, ctx->d_status, ctx->d_ctl, S(stream));
 }
 
+static bool map_mvreg_caps_ok(const crdt_map_mvreg_slab* x) {
+  return x->kcap && x->kcap <= 4096 && x->mcap && x->mcap <= 128 && x->dcap && x->dcap <= 64 && x->scap &&
+         x->scap <= 4096;
+}
+static bool map_mvreg_ptrs_ok(const crdt_map_mvreg_slab* x) {
+  return x->clock && x->n_keys && x->keys && x->eclock && x->mv_n && x->mv_clock && x->mv_val && x->n_def && x->dclock &&
+         x->dset_n && x->dset;
+}
+
+size_t crdt_map_map_merge_scratch_bytes(const crdt_map_map_slab* out, size_t n_obj, uint32_t n_actors) {
+  return out ? map_map_scratch_bytes(*out, n_obj, n_actors) : 0u;
+}
+
+int crdt_map_map_merge(crdt_ctx* ctx, const crdt_map_map_slab* self, const crdt_map_map_slab* other,
+                       const crdt_map_map_slab* out, size_t n_obj, uint32_t n_actors, void* d_scratch,
+                       size_t scratch_bytes, void* stream) {
+  if (!ctx || !self || !other || !out || n_actors == 0 || n_actors > 128) return CRDT_EINVAL;
+  for (const crdt_map_map_slab* x : {self, other})
+    if (x->kcap == 0 || x->kcap > 4096 || x->dcap == 0 || x->dcap > 64 || x->scap == 0 || x->scap > 4096 ||
+        !map_mvreg_caps_ok(&x->inner))
+      return CRDT_EINVAL;
+  const crdt_map_mvreg_slab &si = self->inner, &oi = other->inner, &ri = out->inner;
+  if (out->kcap < self->kcap + other->kcap || out->dcap < self->dcap + other->dcap ||
+      out->scap < self->scap + other->scap || ri.kcap < si.kcap + oi.kcap || ri.mcap < si.mcap + oi.mcap ||
+      ri.dcap < si.dcap + oi.dcap || ri.scap < si.scap + oi.scap)
+    return CRDT_EINVAL;
+  if (n_obj) {
+    for (const crdt_map_map_slab* x : {self, other, out})
+      if (!x->clock || !x->n_keys || !x->keys || !x->eclock || !x->n_def || !x->dclock || !x->dset_n || !x->dset ||
+          !map_mvreg_ptrs_ok(&x->inner))
+        return CRDT_EINVAL;
+    if (!d_scratch || scratch_bytes < map_map_scratch_bytes(*out, n_obj, n_actors) || ((uintptr_t)d_scratch & 15u))
+      return CRDT_EINVAL;
+  }
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  return launch_map_map_merge(*self, *other, *out, n_obj, n_actors, (uint8_t*)d_scratch, ctx->d_status, ctx->d_ctl,
+                              S(stream));
+}
+
 int crdt_map_orswot_merge(crdt_ctx* ctx, const crdt_map_orswot_slab* self, const crdt_map_orswot_slab* other,
                           const crdt_map_orswot_slab* out, size_t n_obj, uint32_t n_actors, void* stream) {
   if (!ctx || !self || !other || !out || n_actors == 0 || n_actors > 128) return CRDT_EINVAL;

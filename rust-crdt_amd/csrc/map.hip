@@ -49,20 +49,38 @@ __device__ __forceinline__ bool set_has(const uint64_t* set, uint32_t n, uint64_
 // row read in the dominance loops is its own dependent global load.
 constexpr uint32_t kVsRows = 128;  // u64 per side
 
-template <bool VS, int NS>
+// G (the nested map's inner pass): n_obj tasks, task t merges S row tsrc[2t]
+// with O row tsrc[2t + 1] into R row t; kMpNone marks an absent side (an
+// empty map: merge(m, empty) = m for a canonical m), both absent: no task.
+constexpr uint64_t kMpNone = ~0ull;
+
+template <bool VS, int NS, bool G = false>
 __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_slab S, crdt_map_mvreg_slab O,
-                                                               crdt_map_mvreg_slab R, uint64_t n_obj, uint32_t A,
-                                                               int* __restrict__ status, uint32_t* __restrict__ ctl) {
+                                                               crdt_map_mvreg_slab Rout, uint64_t n_obj, uint32_t A,
+                                                               int* __restrict__ status, uint32_t* __restrict__ ctl,
+                                                               const uint64_t* __restrict__ tsrc = nullptr,
+                                                               const uint64_t* __restrict__ Tb = nullptr,
+                                                               crdt_map_mvreg_slab Tmp = {}) {
   __shared__ uint32_t comb[kMpComb];     // (self deferred idx + 1) | (other deferred idx + 1) << 8
   __shared__ uint32_t vals[kMpVals];     // kept value slots of the key: side << 8 | slot
   __shared__ uint64_t vr[2][VS ? kVsRows : 1];  // the key's value clock rows: self, other
   const uint32_t lane = threadIdx.x;
   BlockTickets<4> sched(n_obj, ctl + 3, lane);  // (sched.h)
   for (uint64_t i = sched.first(); i < n_obj; i = sched.next(i)) {
-    const Row<NS> cS = rowv<NS>(S.clock, i, A, lane), cO = rowv<NS>(O.clock, i, A, lane);
+    const uint64_t si = G ? tsrc[2 * i] : i, oi = G ? tsrc[2 * i + 1] : i, ri = i;
+    const bool hasS = !G || si != kMpNone, hasO = !G || oi != kMpNone;
+    if (G && !hasS && !hasO) continue;
+    // G: a task whose merged map is truncated afterwards goes to Tmp (read by
+    // map_mvreg_truncate_kernel), the rest to the output
+    const bool to_tmp = G && Tb != nullptr && vany(rowv<NS>(Tb, i, A, lane));
+    const crdt_map_mvreg_slab& R = to_tmp ? Tmp : Rout;
+    const Row<NS> cS = hasS ? rowv<NS>(S.clock, si, A, lane) : zrow<NS>();
+    const Row<NS> cO = hasO ? rowv<NS>(O.clock, oi, A, lane) : zrow<NS>();
     const Row<NS> cM = vmax(cS, cO);  // VClock::merge
-    const uint32_t nS = __builtin_amdgcn_readfirstlane(S.n_keys[i]), nO = __builtin_amdgcn_readfirstlane(O.n_keys[i]);
-    const uint32_t dS = __builtin_amdgcn_readfirstlane(S.n_def[i]), dO = __builtin_amdgcn_readfirstlane(O.n_def[i]);
+    const uint32_t nS = hasS ? __builtin_amdgcn_readfirstlane(S.n_keys[si]) : 0u;
+    const uint32_t nO = hasO ? __builtin_amdgcn_readfirstlane(O.n_keys[oi]) : 0u;
+    const uint32_t dS = hasS ? __builtin_amdgcn_readfirstlane(S.n_def[si]) : 0u;
+    const uint32_t dO = hasO ? __builtin_amdgcn_readfirstlane(O.n_def[oi]) : 0u;
     if (nS > S.kcap || nO > O.kcap || dS > S.dcap || dO > O.dcap) {
       if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
       continue;
@@ -71,12 +89,12 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
     // loops below read mv_n / dset_n slots of the slab row as counts); lane k
     // keeps key k's value count (keys < 64), which the value-row stage below
     // reads by readlane (no dependent load on the per-key chain)
-    const uint32_t vnS = lane < nS ? S.mv_n[i * S.kcap + lane] : 0u, vnO = lane < nO ? O.mv_n[i * O.kcap + lane] : 0u;
+    const uint32_t vnS = lane < nS ? S.mv_n[si * S.kcap + lane] : 0u, vnO = lane < nO ? O.mv_n[oi * O.kcap + lane] : 0u;
     bool bad = vnS > S.mcap || vnO > O.mcap;
-    for (uint32_t k = lane + kMpW; k < nS; k += kMpW) bad = bad || S.mv_n[i * S.kcap + k] > S.mcap;
-    for (uint32_t k = lane + kMpW; k < nO; k += kMpW) bad = bad || O.mv_n[i * O.kcap + k] > O.mcap;
-    for (uint32_t k = lane; k < dS; k += kMpW) bad = bad || S.dset_n[i * S.dcap + k] > S.scap;
-    for (uint32_t k = lane; k < dO; k += kMpW) bad = bad || O.dset_n[i * O.dcap + k] > O.scap;
+    for (uint32_t k = lane + kMpW; k < nS; k += kMpW) bad = bad || S.mv_n[si * S.kcap + k] > S.mcap;
+    for (uint32_t k = lane + kMpW; k < nO; k += kMpW) bad = bad || O.mv_n[oi * O.kcap + k] > O.mcap;
+    for (uint32_t k = lane; k < dS; k += kMpW) bad = bad || S.dset_n[si * S.dcap + k] > S.scap;
+    for (uint32_t k = lane; k < dO; k += kMpW) bad = bad || O.dset_n[oi * O.dcap + k] > O.scap;
     if (__ballot(bad) != 0ull) {
       if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
       continue;
@@ -87,11 +105,11 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
     {
       uint32_t a = 0, b = 0;
       while (a < dS || b < dO) {
-        if (b < dO && vle(rowv<NS>(O.dclock, i * O.dcap + b, A, lane), cS)) { ++b; continue; }
+        if (b < dO && vle(rowv<NS>(O.dclock, oi * O.dcap + b, A, lane), cS)) { ++b; continue; }
         int c;
         if (a >= dS) c = 1;
         else if (b >= dO) c = -1;
-        else c = vorder(rowv<NS>(S.dclock, i * S.dcap + a, A, lane), rowv<NS>(O.dclock, i * O.dcap + b, A, lane), lane);
+        else c = vorder(rowv<NS>(S.dclock, si * S.dcap + a, A, lane), rowv<NS>(O.dclock, oi * O.dcap + b, A, lane), lane);
         const uint32_t e = (c <= 0 ? a + 1u : 0u) | ((c >= 0 ? b + 1u : 0u) << 8);
         if (lane == 0u) comb[nc] = e;
         ++nc;
@@ -104,10 +122,10 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
     uint32_t nk = 0, a = 0, b = 0;
     bool over = false;
     while (a < nS || b < nO) {
-      const uint64_t ka = a < nS ? S.keys[i * S.kcap + a] : ~0ull, kb = b < nO ? O.keys[i * O.kcap + b] : ~0ull;
+      const uint64_t ka = a < nS ? S.keys[si * S.kcap + a] : ~0ull, kb = b < nO ? O.keys[oi * O.kcap + b] : ~0ull;
       const bool hs = a < nS && (b >= nO || ka <= kb), ho = b < nO && (a >= nS || kb <= ka);
       const uint64_t key = hs ? ka : kb;
-      const uint64_t ia = i * S.kcap + a, ib = i * O.kcap + b;
+      const uint64_t ia = si * S.kcap + a, ib = oi * O.kcap + b;
       const Row<NS> eS = hs ? rowv<NS>(S.eclock, ia, A, lane) : zrow<NS>();
       const Row<NS> eO = ho ? rowv<NS>(O.eclock, ib, A, lane) : zrow<NS>();
       // the key's value counts (within mcap: checked above)
@@ -190,16 +208,16 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
           const uint32_t sa = e & 255u, sb = e >> 8;
           bool named = false;
           if (sa) {
-            const uint64_t di = i * S.dcap + sa - 1u;
+            const uint64_t di = si * S.dcap + sa - 1u;
             named = set_has(S.dset + di * S.scap, S.dset_n[di], key, lane);
           }
           if (!named && sb) {
-            const uint64_t di = i * O.dcap + sb - 1u;
+            const uint64_t di = oi * O.dcap + sb - 1u;
             named = set_has(O.dset + di * O.scap, O.dset_n[di], key, lane);
           }
           if (!named) continue;
-          const Row<NS> D = sa ? rowv<NS>(S.dclock, i * S.dcap + sa - 1u, A, lane)
-                               : rowv<NS>(O.dclock, i * O.dcap + sb - 1u, A, lane);
+          const Row<NS> D = sa ? rowv<NS>(S.dclock, si * S.dcap + sa - 1u, A, lane)
+                               : rowv<NS>(O.dclock, oi * O.dcap + sb - 1u, A, lane);
           ec = vsub(ec, D);
           del = vmax(del, D);  // truncating by several clocks = by their max, slot by slot
         }
@@ -209,7 +227,7 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
         if (nk >= R.kcap) {
           over = true;
         } else {
-          const uint64_t ir = i * R.kcap + nk;
+          const uint64_t ir = ri * R.kcap + nk;
           if (lane == 0u) R.keys[ir] = key;
           strow<NS>(R.eclock + ir * A, ec, A, lane);
           uint32_t nout = 0;
@@ -232,24 +250,24 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
       if (hs) ++a;
       if (ho) ++b;
     }
-    if (lane == 0u) R.n_keys[i] = nk;
-    strow<NS>(R.clock + i * A, cM, A, lane);
+    if (lane == 0u) R.n_keys[ri] = nk;
+    strow<NS>(R.clock + ri * A, cM, A, lane);
     // ---- deferred kept: the combined clocks the merged clock does not cover, sets united
     uint32_t nd = 0;
     for (uint32_t c = 0; c < nc; ++c) {
       const uint32_t e = comb[c];
       const uint32_t sa = e & 255u, sb = e >> 8;
-      const Row<NS> D = sa ? rowv<NS>(S.dclock, i * S.dcap + sa - 1u, A, lane)
-                           : rowv<NS>(O.dclock, i * O.dcap + sb - 1u, A, lane);
+      const Row<NS> D = sa ? rowv<NS>(S.dclock, si * S.dcap + sa - 1u, A, lane)
+                           : rowv<NS>(O.dclock, oi * O.dcap + sb - 1u, A, lane);
       if (vle(D, cM)) continue;
       if (nd >= R.dcap) { over = true; break; }
-      const uint64_t dr = i * R.dcap + nd;
+      const uint64_t dr = ri * R.dcap + nd;
       strow<NS>(R.dclock + dr * A, D, A, lane);
       uint32_t cnt = 0;
       if (lane == 0u) {  // sorted union of the two key sets
-        const uint64_t* xs = sa ? S.dset + (i * S.dcap + sa - 1u) * S.scap : nullptr;
-        const uint64_t* ys = sb ? O.dset + (i * O.dcap + sb - 1u) * O.scap : nullptr;
-        const uint32_t nx = sa ? S.dset_n[i * S.dcap + sa - 1u] : 0u, ny = sb ? O.dset_n[i * O.dcap + sb - 1u] : 0u;
+        const uint64_t* xs = sa ? S.dset + (si * S.dcap + sa - 1u) * S.scap : nullptr;
+        const uint64_t* ys = sb ? O.dset + (oi * O.dcap + sb - 1u) * O.scap : nullptr;
+        const uint32_t nx = sa ? S.dset_n[si * S.dcap + sa - 1u] : 0u, ny = sb ? O.dset_n[oi * O.dcap + sb - 1u] : 0u;
         uint32_t p = 0, q = 0;
         while (p < nx || q < ny) {
           const uint64_t kx = p < nx ? xs[p] : ~0ull, ky = q < ny ? ys[q] : ~0ull;
@@ -264,8 +282,91 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
       over = over || __builtin_amdgcn_readfirstlane(cnt) > R.scap;
       ++nd;
     }
-    if (lane == 0u) R.n_def[i] = nd;
+    if (lane == 0u) R.n_def[ri] = nd;
     if (over && lane == 0u) atomicCAS(status, 0, CRDT_ECAPACITY);
+    mp_sync();
+  }
+}
+
+// Map<u64, MVReg>::truncate (Causal, src/map.rs:131-158, with
+// MVReg::truncate src/mvreg.rs:100-113 on every kept entry's register) of the
+// maps the task form wrote to Tmp, by their row of Tb, into R (same row):
+// entry clocks lose the clock (emptied entries dropped, the rest keep their
+// surviving values in order), deferred clocks lose it (emptied ones dropped;
+// two that become equal keep the later one's key set, as the reference's
+// HashMap insert does over the merge's CLOCK ORDER; output re-sorted in CLOCK
+// ORDER), and the map clock loses it.
+template <int NS>
+__global__ __launch_bounds__(kMpW) void map_mvreg_truncate_kernel(crdt_map_mvreg_slab Tmp, crdt_map_mvreg_slab R,
+                                                                  const uint64_t* __restrict__ Tb,
+                                                                  const uint64_t* __restrict__ tsrc, uint64_t n,
+                                                                  uint32_t A, int* __restrict__ status,
+                                                                  uint32_t* __restrict__ ctl) {
+  __shared__ uint32_t keep_d[kMpComb];  // surviving deferred (source index), CLOCK ORDER of the truncated clocks
+  const uint32_t lane = threadIdx.x;
+  BlockTickets<4> sched(n, ctl + 3, lane);
+  for (uint64_t t = sched.first(); t < n; t = sched.next(t)) {
+    if (tsrc[2 * t] == kMpNone && tsrc[2 * t + 1] == kMpNone) continue;
+    const Row<NS> c = rowv<NS>(Tb, t, A, lane);
+    if (!vany(c)) continue;  // (written to R by the merge)
+    strow<NS>(R.clock + t * A, vsub(rowv<NS>(Tmp.clock, t, A, lane), c), A, lane);
+    const uint32_t nk = __builtin_amdgcn_readfirstlane(Tmp.n_keys[t]);
+    uint32_t out = 0;
+    for (uint32_t k = 0; k < nk; ++k) {
+      const uint64_t ik = t * Tmp.kcap + k;
+      const Row<NS> e = vsub(rowv<NS>(Tmp.eclock, ik, A, lane), c);
+      if (!vany(e)) continue;
+      const uint64_t ok = t * R.kcap + out;
+      if (lane == 0u) R.keys[ok] = Tmp.keys[ik];
+      strow<NS>(R.eclock + ok * A, e, A, lane);
+      const uint32_t nv = __builtin_amdgcn_readfirstlane(Tmp.mv_n[ik]);
+      uint32_t nout = 0;
+      for (uint32_t v = 0; v < nv; ++v) {
+        const Row<NS> r = vsub(rowv<NS>(Tmp.mv_clock, ik * Tmp.mcap + v, A, lane), c);
+        if (!vany(r)) continue;
+        strow<NS>(R.mv_clock + (ok * R.mcap + nout) * A, r, A, lane);
+        if (lane == 0u) R.mv_val[ok * R.mcap + nout] = Tmp.mv_val[ik * Tmp.mcap + v];
+        ++nout;
+      }
+      if (lane == 0u) R.mv_n[ok] = nout;
+      ++out;
+    }
+    if (lane == 0u) R.n_keys[t] = out;
+    // deferred: survivors, later equal clocks replacing earlier ones, then CLOCK ORDER
+    const uint32_t nd = __builtin_amdgcn_readfirstlane(Tmp.n_def[t]);
+    uint32_t ns = 0;
+    for (uint32_t d = 0; d < nd; ++d) {
+      const Row<NS> D = vsub(rowv<NS>(Tmp.dclock, t * Tmp.dcap + d, A, lane), c);
+      if (!vany(D)) continue;
+      uint32_t at = ns, pos = ns;
+      for (uint32_t q = 0; q < ns; ++q) {
+        const uint32_t sq = keep_d[q];
+        const Row<NS> Q = vsub(rowv<NS>(Tmp.dclock, t * Tmp.dcap + sq, A, lane), c);
+        const int o = vorder(D, Q, lane);
+        if (o == 0) { at = q; break; }   // equal: this (later) one replaces it
+        if (o < 0 && pos == ns) pos = q; // insertion point
+      }
+      mp_sync();
+      if (at < ns) {
+        if (lane == 0u) keep_d[at] = d;
+      } else {
+        if (lane == 0u) {
+          for (uint32_t q = ns; q > pos; --q) keep_d[q] = keep_d[q - 1];
+          keep_d[pos] = d;
+        }
+        ++ns;
+      }
+      mp_sync();
+    }
+    for (uint32_t q = 0; q < ns; ++q) {
+      const uint32_t sq = keep_d[q];
+      const uint64_t src = t * Tmp.dcap + sq, dst = t * R.dcap + q;
+      strow<NS>(R.dclock + dst * A, vsub(rowv<NS>(Tmp.dclock, src, A, lane), c), A, lane);
+      const uint32_t m = __builtin_amdgcn_readfirstlane(Tmp.dset_n[src]);
+      for (uint32_t j = lane; j < m; j += kMpW) R.dset[dst * R.scap + j] = Tmp.dset[src * Tmp.scap + j];
+      if (lane == 0u) R.dset_n[dst] = m;
+    }
+    if (lane == 0u) R.n_def[t] = ns;
     mp_sync();
   }
 }
@@ -290,6 +391,33 @@ int launch_map_mvreg_merge(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_sl
   else
     hipLaunchKernelGGL((map_mvreg_merge_kernel<false, 1>), dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A,
                        status, ctl);
+  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+}
+
+int launch_map_mvreg_merge_tasks(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_slab& O,
+                                 const crdt_map_mvreg_slab& R, const crdt_map_mvreg_slab& Tmp, const uint64_t* tsrc,
+                                 const uint64_t* Tb, uint64_t n_tasks, uint32_t A, int* status, uint32_t* ctl,
+                                 hipStream_t stream) {
+  if (n_tasks == 0) return CRDT_OK;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const uint64_t cap = (uint64_t)cus * 28u;
+  const uint32_t blocks = (uint32_t)(n_tasks < cap ? n_tasks : cap);
+  if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
+  if (A > 64u)
+    hipLaunchKernelGGL((map_mvreg_merge_kernel<false, 2, true>), dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_tasks,
+                       A, status, ctl, tsrc, Tb, Tmp);
+  else
+    hipLaunchKernelGGL((map_mvreg_merge_kernel<false, 1, true>), dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_tasks,
+                       A, status, ctl, tsrc, Tb, Tmp);
+  if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
+  if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
+  if (A > 64u)
+    hipLaunchKernelGGL((map_mvreg_truncate_kernel<2>), dim3(blocks), dim3(kMpW), 0, stream, Tmp, R, Tb, tsrc, n_tasks,
+                       A, status, ctl);
+  else
+    hipLaunchKernelGGL((map_mvreg_truncate_kernel<1>), dim3(blocks), dim3(kMpW), 0, stream, Tmp, R, Tb, tsrc, n_tasks,
+                       A, status, ctl);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 

@@ -125,6 +125,47 @@ def mvreg_map_from_row(S, i):
     return m
 
 
+def nested_map_to_row(m, S, i, A):
+    """Write a crdts_ref.Map of Map<u64, MVReg> values (the reference's
+    TestMap) as row i of a host MapMapSlab: the outer map's arrays, and key
+    slot k's nested map as inner object i * kcap + k."""
+    a = S.a
+    for f in a:
+        a[f][i] = 0
+    a["clock"][i] = _row(m.clock, A)
+    keys = sorted(m.entries)
+    assert len(keys) <= S.kcap and len(m.deferred) <= S.dcap
+    a["n_keys"][i] = len(keys)
+    for k in range(S.kcap):
+        for f in S.inner.a:
+            S.inner.a[f][i * S.kcap + k] = 0
+    for k, key in enumerate(keys):
+        ec, v = m.entries[key]
+        a["keys"][i, k] = key
+        a["eclock"][i, k] = _row(ec, A)
+        mvreg_map_to_row(v, S.inner, i * S.kcap + k, A)
+    defs = crdts_ref.clock_order(list(m.deferred))
+    a["n_def"][i] = len(defs)
+    for d, c in enumerate(defs):
+        ks = sorted(m.deferred[c])
+        assert len(ks) <= S.scap
+        a["dclock"][i, d] = _row(c, A)
+        a["dset_n"][i, d] = len(ks)
+        a["dset"][i, d, :len(ks)] = ks
+
+
+def nested_map_from_row(S, i):
+    a = S.a
+    m = crdts_ref.Map(lambda: crdts_ref.Map(crdts_ref.MVReg))
+    m.clock = _clock(a["clock"][i])
+    for k in range(int(a["n_keys"][i])):
+        m.entries[int(a["keys"][i, k])] = [_clock(a["eclock"][i, k]), mvreg_map_from_row(S.inner, i * S.kcap + k)]
+    for d in range(int(a["n_def"][i])):
+        n = int(a["dset_n"][i, d])
+        m.deferred[_clock(a["dclock"][i, d])] = set(int(x) for x in a["dset"][i, d, :n])
+    return m
+
+
 def rows_equal(S, i, T, j):
     return all(np.array_equal(S.a[f][i], T.a[f][j]) for f in S.a)
 
@@ -134,12 +175,15 @@ def _relabel_clock(c, f):
 
 
 def relabel(m, f):
-    """A copy of map `m` (either value kind) with every actor id a renamed to f[a]
-    (an order-preserving interning keeps CLOCK ORDER and every comparison)."""
+    """A copy of map `m` (any value kind: MVReg, Orswot, a nested map) with
+    every actor id a renamed to f[a] (an order-preserving interning keeps
+    CLOCK ORDER and every comparison)."""
     r = crdts_ref.Map(m.factory, m.order)
     r.clock = _relabel_clock(m.clock, f)
     for k, (c, v) in m.entries.items():
-        if isinstance(v, crdts_ref.Orswot):
+        if isinstance(v, crdts_ref.Map):
+            o = relabel(v, f)
+        elif isinstance(v, crdts_ref.Orswot):
             o = crdts_ref.Orswot()
             o.clock = _relabel_clock(v.clock, f)
             o.entries = {x: _relabel_clock(e, f) for x, e in v.entries.items()}
@@ -156,7 +200,9 @@ def actors_of(m):
     s = set(m.clock.dots)
     for c, v in m.entries.values():
         s |= set(c.dots)
-        if isinstance(v, crdts_ref.Orswot):
+        if isinstance(v, crdts_ref.Map):
+            s |= actors_of(v)
+        elif isinstance(v, crdts_ref.Orswot):
             s |= set(v.clock.dots)
             for e in v.entries.values():
                 s |= set(e.dots)
