@@ -18,6 +18,8 @@
 // entries are walked by wave-uniform loops.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "../../include/crdts_hip.h"
 #include "kernels.h"
 #include "map_rows.h"
@@ -65,7 +67,8 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
   __shared__ uint32_t vals[kMpVals];     // kept value slots of the key: side << 8 | slot
   __shared__ uint64_t vr[2][VS ? kVsRows : 1];  // the key's value clock rows: self, other
   const uint32_t lane = threadIdx.x;
-  BlockTickets<4> sched(n_obj, ctl + 3, lane);  // (sched.h)
+  // (sched.h; G: most tasks are empty slots, a plain stride balances them)
+  typename std::conditional<G, GridStride, BlockTickets<4>>::type sched(n_obj, ctl + 3, lane);
   for (uint64_t i = sched.first(); i < n_obj; i = sched.next(i)) {
     const uint64_t si = G ? tsrc[2 * i] : i, oi = G ? tsrc[2 * i + 1] : i, ri = i;
     const bool hasS = !G || si != kMpNone, hasO = !G || oi != kMpNone;
@@ -304,7 +307,7 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_truncate_kernel(crdt_map_mvreg
                                                                   uint32_t* __restrict__ ctl) {
   __shared__ uint32_t keep_d[kMpComb];  // surviving deferred (source index), CLOCK ORDER of the truncated clocks
   const uint32_t lane = threadIdx.x;
-  BlockTickets<4> sched(n, ctl + 3, lane);
+  GridStride sched(n, ctl + 3, lane);  // (most tasks are empty or not truncated)
   for (uint64_t t = sched.first(); t < n; t = sched.next(t)) {
     if (tsrc[2 * t] == kMpNone && tsrc[2 * t + 1] == kMpNone) continue;
     const Row<NS> c = rowv<NS>(Tb, t, A, lane);
@@ -396,13 +399,21 @@ int launch_map_mvreg_merge(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_sl
 
 int launch_map_mvreg_merge_tasks(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_slab& O,
                                  const crdt_map_mvreg_slab& R, const crdt_map_mvreg_slab& Tmp, const uint64_t* tsrc,
-                                 const uint64_t* Tb, uint64_t n_tasks, uint32_t A, int* status, uint32_t* ctl,
-                                 hipStream_t stream) {
+                                 const uint64_t* Tb, uint64_t n_tasks, uint32_t slots, uint32_t A, int* status,
+                                 uint32_t* ctl, hipStream_t stream) {
   if (n_tasks == 0) return CRDT_OK;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const uint64_t cap = (uint64_t)cus * 28u;
-  const uint32_t blocks = (uint32_t)(n_tasks < cap ? n_tasks : cap);
+  uint32_t blocks = (uint32_t)(n_tasks < cap ? n_tasks : cap);
+  // the kept keys are an object's first slots: a grid stride coprime with the
+  // slots per object spreads them over every block (one sharing a factor
+  // with it would leave the blocks of the last slots idle)
+  auto gcd = [](uint32_t a, uint32_t b) {
+    while (b) { const uint32_t t = a % b; a = b; b = t; }
+    return a;
+  };
+  while (blocks > 1u && slots > 1u && gcd(blocks, slots) != 1u) --blocks;
   if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
   if (A > 64u)
     hipLaunchKernelGGL((map_mvreg_merge_kernel<false, 2, true>), dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_tasks,

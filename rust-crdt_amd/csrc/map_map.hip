@@ -255,7 +255,7 @@ int launch_map_map_merge(const crdt_map_map_slab& S, const crdt_map_map_slab& O,
     hipLaunchKernelGGL((map_map_outer_kernel<1>), dim3(blocks), dim3(kMmW), 0, stream, S, O, R, n_obj, A, tsrc, Tb,
                        status, ctl);
   if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
-  return launch_map_mvreg_merge_tasks(S.inner, O.inner, R.inner, T, tsrc, Tb, nt, A, status, ctl, stream);
+  return launch_map_mvreg_merge_tasks(S.inner, O.inner, R.inner, T, tsrc, Tb, nt, R.kcap, A, status, ctl, stream);
 }
 
 }  // namespace crdts_hip

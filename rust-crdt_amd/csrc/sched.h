@@ -51,6 +51,16 @@ struct BlockTickets {
   }
 };
 
+// The plain grid-stride schedule with BlockTickets' interface: for the task
+// launches whose items are mostly empty (the nested map's per-slot tasks),
+// where a ticket atomic per few items would cost more than the imbalance.
+struct GridStride {
+  uint64_t n;
+  __device__ GridStride(uint64_t n_, uint32_t*, uint32_t) : n(n_) {}
+  __device__ uint64_t first() const { return blockIdx.x; }
+  __device__ uint64_t next(uint64_t cur) const { return cur + gridDim.x; }
+};
+
 // Guided chunk schedule of the join kernels: the first SF/8 of n objects in
 // static rounds of (<= 64-object) chunks by wave index, the rest in chunks
 // of DYN objects handed out by an atomic ticket (ctl[3], zeroed before the
