@@ -2451,25 +2451,36 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kern
 }
 
 // ======================================================================
-// Join kernel (v8): the product path. Two passes over the batch with one
-// kernel body:
-//  MODE 1 (join pass): objects without deferred removes that fit the mask
-//    join are joined by mask3_object; objects with deferred removes are
-//    flagged kPendingHD for the deferred pass; anything else (records past
-//    the stage, > 64 members / dots, A > 32, > 32 deferred clocks) is flagged
-//    kPending and listed for orswot_merge_general_kernel.
-//  MODE 2 (deferred pass): the kPendingHD objects, joined by
-//    mask_object<HD = true> (src/orswot.rs:141-157 with apply_deferred).
-// Splitting the deferred objects out keeps the join pass's object loop on
-// one path whose vector-memory operations are the same for every object —
-// the next object's record prefetch (re-prefetching the current one after
-// the last object of a chunk), then mask3_object's sink-predicated stores —
-// so the compiler's vmcnt accounting at the loop head waits for the
-// prefetch and not for the previous object's store acknowledgements (loads
-// and stores share vmcnt in issue order on gfx9). A fallback inside the
-// loop (a union past 64 members, a dot actor >= A) sets kPending by a
-// predicated store and raises ctl[1], which makes the general kernel scan
-// the offsets for flags instead of reading the list.
+// Join kernel: the product path (orswot_join_kernel, MODE 3). One pass over
+// the batch, one wave per chunk of objects (the guided split, sched.h): the
+// chunk step validates the 64 objects' headers lane-parallel and lists what
+// the mask join cannot take (records past the 2 KB stage, > 64 members or
+// dots, A > AW, > 32 deferred clocks) for orswot_merge_general_kernel; the
+// wave then joins its objects one by one from the LDS pair stage while the
+// next object's records are in flight in registers — mask3_object for every
+// object, its HD form (direct stores) for the 7 % with deferred removes
+// (src/orswot.rs:87-157 with apply_deferred) — and copies the assembled record
+// out. Every path issues the same vector-memory operations per object (the
+// deferred form's tail stores go to the wave's sink), so the compiler's
+// vmcnt accounting at the loop head waits for the prefetch and not for the
+// previous object's store acknowledgements (loads and stores share vmcnt in
+// issue order on gfx9). A fallback inside the loop (a union past 64 members,
+// a dot actor >= A) sets kPending and lists the object for the general kernel.
+//
+// Template knobs and the product's values (launch_product_join below; every
+// other value exists for the diagnostic A/B variants of -DCRDT_DIAG builds,
+// DESIGN.md §4 / §8 / §9 give the measurements):
+//   MINW 6 (5 for AW 64)  waves per SIMD (launch bound)
+//   MODE 3                one pass (1 / 2: the earlier two-pass split)
+//   OUT 2, HDD, DC, M3HD  deferred objects through mask3_object's HD form, direct stores
+//   HABL 0                timing-only ablations off
+//   RT                    member ranks by register search
+//   DYN 20, SF 5, GMIN 0  guided split: 5/8 of the objects in static chunks, then 20-object tickets
+//   SPEC false            no speculative first-object prefetch
+//   IO 7                  saddr record prefetch, copy-out clamped on byte offsets
+//   HK 0, PK, BK 1        packed two-sided rank search, bank-conflict scratch layout
+//   PO false, TCH 0       natural output placement, no touch prefetch
+//   AW 32 / 64            actor-mask width (dense top clocks of <= 32 / 33-64 actors)
 // ======================================================================
 constexpr uint64_t kPendingHD = 1ull << 62;  // Ooff flag: object left for the deferred pass
 
@@ -3214,6 +3225,21 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
 }
 }  // namespace
 
+namespace {
+// The product join launch (the knob list above), named once.
+template <int MINW, int AW>
+int launch_product_join(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
+                        const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
+                        uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
+                        uint32_t list_cap, hipStream_t stream, int blocks_per_cu, JoinSeq* js) {
+  return launch_join_passes<MINW, /*ONE*/ true, /*HDD*/ true, /*DC*/ true, /*M3HD*/ true, /*HABL*/ 0, /*RT*/ true,
+                            /*DYN*/ 20, /*DK_*/ false, /*SF*/ 5, /*V10_*/ false, /*SPEC*/ false, /*GMIN*/ 0,
+                            /*IO*/ 7, /*HK*/ 0, /*PK*/ true, /*BK*/ 1, /*NM*/ true, /*PO*/ false, /*TCH*/ 0, AW>(
+      Lb, Loff, Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors, status, ctl, list, list_cap, stream,
+      blocks_per_cu, js);
+}
+}  // namespace
+
 int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                         const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff,
                         uint64_t Obytes, uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl,
@@ -3238,13 +3264,10 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   (void)variant;
   // (packed output placement, PO, measured 1-1.5 % slower here: diag variant 270)
   if (n_actors > 32u)  // dense top clocks of 33-64 actors: the same join with 64-bit actor masks, 5 waves/SIMD
-    return go(launch_join_passes<5, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true,
-                                 false, 0, 64>);
-  return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true>);
+    return go(launch_product_join<5, 64>);
+  return go(launch_product_join<6, 32>);
 #else
-  if (n_actors > 32u && (variant == 0 || variant == 265))
-    return go(launch_join_passes<5, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true,
-                                 false, 0, 64>);
+  if (n_actors > 32u && (variant == 0 || variant == 265)) return go(launch_product_join<5, 64>);
   if (variant == 134) return go(launch_join_passes<6, true, true, true, true, 1>);  // timing only: no kill
   if (variant == 135) return go(launch_join_passes<6, true, true, true, true, 2>);  // timing only: no deferred block
   if (variant == 136) return go(launch_join_passes<6, true, true, true, true, 3>);  // timing only: join without HBM
@@ -3292,7 +3315,7 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // r03: + BK (mask3's LDS bank-conflict layout: dword descriptors, 4-B sink stride, header under exec)
   if (variant == 264) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1>);
   // r03: + NM (no memset before the join: alternating control-word sets, zeroed by the general kernel)
-  if (variant == 265) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true>);
+  if (variant == 265) return go(launch_product_join<6, 32>);
   // r04: + PO (packed output: consecutive records back to back): 0.750 vs 0.741 ms (265, the product)
   if (variant == 270) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true, true>);
   // r04: + TCH (a one-dword-per-line touch of the object after the next), with (271) and without (272) PO
