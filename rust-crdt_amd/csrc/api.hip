@@ -492,7 +492,7 @@ int crdt_orswot_from_bincode(crdt_ctx* ctx, const uint8_t* d_blobs, size_t blob_
   return launch_bincode_ingest(d_blobs, blob_bytes, d_blob_off, d_blob_len, n_obj, actor_bytes, member_bytes,
                                n_actors, flags, nullptr, d_out, d_out_off, out_bytes, ctx->d_status, ctx->d_ctl, S(stream),
                                ctx->variant == 301 ? ctx->d_list : nullptr, ctx->d_list, ctx->list_cap, ctx->d_big,
-                               ctx->variant == 305 ? 1 : ctx->variant == 304 ? 2 : 0);
+                               ctx->variant == 305 ? 1 : ctx->variant == 304 ? 2 : ctx->variant == 306 ? 3 : 0);
 }
 
 int crdt_orswot_bincode_sizes(crdt_ctx* ctx, const crdt_orswot_batch* batch, uint32_t n_actors, uint32_t flags,

@@ -333,7 +333,8 @@ __device__ void bc_scan_excl(uint32_t* S, uint32_t n, uint32_t lane) {
 // or a CRDT_E* code (the record is then not valid).
 template <bool ST = false, class XL = XS, class SRC>
 __device__ __forceinline__ int bc_write_record(const SRC& B, const BcWalk& w, uint32_t wa, uint32_t wm, uint32_t A, bool sparse,
-                               uint8_t* X, uint8_t* O, uint32_t lane, BcStamps* st = nullptr) {
+                               uint8_t* X, uint8_t* O, uint32_t lane, BcStamps* st = nullptr,
+                               uint32_t moff = 0) {
   RecLayout L;
   rec_layout(L, sparse ? w.n_clk : A, w.n_mem, w.n_dot, w.n_def, w.n_def_dot, w.n_def_mem, sparse);
   const uint64_t sa = wa + 8u;
@@ -386,8 +387,8 @@ __device__ __forceinline__ int bc_write_record(const SRC& B, const BcWalk& w, ui
   if (sparse && lane == 0u && (w.n_clk & 1u)) *(uint32_t*)(O + L.o_cact + 4u * w.n_clk) = 0u;
   bc_mark<ST>(st, 2);
   // ---- members: rank by key (HashMap order is arbitrary), dot offsets in key order
-  uint32_t* Pm = (uint32_t*)(X + XL::Pm);
-  uint32_t* Lm = (uint32_t*)(X + XL::Lm);
+  uint32_t* Pm = (uint32_t*)(X + XL::Pm) + moff;  // (moff: the group walk's slice of the entry arrays)
+  uint32_t* Lm = (uint32_t*)(X + XL::Lm) + moff;
   uint32_t* Rm = (uint32_t*)(X + XL::Rm);
   uint32_t* Sm = (uint32_t*)(X + XL::Sm);
   bc_xsync<XL>();
@@ -719,6 +720,58 @@ __global__ __launch_bounds__(256) void bincode_sizes_lane_kernel(
   }
 }
 
+// The group walk of the read-once decode pass: each lane walks its own blob
+// out of the LDS window that holds a group of blobs (bc_walk's checks, in
+// lane_walk's order), and with `write` parks every member entry's position
+// and dot count at Pm / Lm[base + e]: one entry chain per lane, the group's
+// chains in parallel instead of one after another.
+__device__ __forceinline__ LaneWalk bc_lane_walk_window(const Src<true>& B, uint64_t len, uint32_t wa, uint32_t wm,
+                                                        uint32_t A, uint32_t* Pm, uint32_t* Lm, uint32_t base,
+                                                        bool write) {
+  LaneWalk w{0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t sa = wa + 8u;
+  if (len < 24u || len >= (1ull << 31)) { w.err = CRDT_ENONCANON; return w; }
+  const uint64_t nclk = B.get(0, 8);
+  if (nclk > A || nclk * sa > len - 24u) { w.err = CRDT_ENONCANON; return w; }
+  w.n_clk = (uint32_t)nclk;
+  uint64_t p = 8u + nclk * sa;
+  const uint64_t nent = B.get(p, 8);
+  p += 8u;
+  if (nent > XS::kMem) { w.err = CRDT_ECAPACITY; return w; }
+  for (uint32_t e = 0; e < (uint32_t)nent; ++e) {
+    if (p + wm + 8u > len) { w.err = CRDT_ENONCANON; return w; }
+    const uint64_t l = B.get(p + wm, 8);
+    if (l == 0u || l > A || l * sa > len - (p + wm + 8u)) { w.err = CRDT_ENONCANON; return w; }
+    if (write) {
+      Pm[base + e] = (uint32_t)p;
+      Lm[base + e] = (uint32_t)l;
+    }
+    w.n_dot += (uint32_t)l;
+    p += wm + 8u + l * sa;
+  }
+  w.n_mem = (uint32_t)nent;
+  if (p + 8u > len) { w.err = CRDT_ENONCANON; return w; }
+  w.p_def = p;
+  const uint64_t ndef = B.get(p, 8);
+  p += 8u;
+  if (ndef > XS::kDef) { w.err = CRDT_ECAPACITY; return w; }
+  for (uint64_t d = 0; d < ndef; ++d) {
+    if (p + 8u > len) { w.err = CRDT_ENONCANON; return w; }
+    const uint64_t lc = B.get(p, 8);
+    if (lc == 0u || lc > A || lc * sa > len - (p + 8u)) { w.err = CRDT_ENONCANON; return w; }
+    const uint64_t q = p + 8u + lc * sa;
+    if (q + 8u > len) { w.err = CRDT_ENONCANON; return w; }
+    const uint64_t ls = B.get(q, 8);
+    if (ls == 0u || ls > len || ls * wm > len - (q + 8u)) { w.err = CRDT_ENONCANON; return w; }
+    w.n_fdot += (uint32_t)lc;
+    w.n_fmem += (uint32_t)ls;
+    p = q + 8u + ls * wm;
+  }
+  w.n_def = (uint32_t)ndef;
+  if (p != len) w.err = CRDT_ENONCANON;
+  return w;
+}
+
 // One object of the read-once decode pass: the wave-uniform walk (bc_walk)
 // and the record writer over the same source; an object past the LDS scratch
 // (XL: members or deferred clocks) is listed for the large-object kernel
@@ -757,7 +810,7 @@ __device__ __forceinline__ int bc_decode_listed(const SRC& B, uint64_t o, uint64
 // window reading those pairs — faster by 4 % on config 3 but every blob is
 // read twice and the pairs written and read back (2.3x the algorithmic bytes,
 // DESIGN.md §9).
-template <bool LW, class XL = XS, int OCC = 4>
+template <bool LW, class XL = XS, int OCC = 4, bool GW = false>
 __global__ __launch_bounds__(kBcWave * kBcWaves, OCC) void bincode_decode_kernel(
     const uint8_t* __restrict__ blobs, uint64_t blob_bytes, const uint64_t* __restrict__ boff,
     const uint64_t* __restrict__ blen, uint64_t n_obj, uint32_t wa, uint32_t wm, uint32_t A, uint32_t flags,
@@ -822,6 +875,117 @@ __global__ __launch_bounds__(kBcWave * kBcWaves, OCC) void bincode_decode_kernel
     const uint64_t wins = __ballot(win);
     uint64_t pend = __ballot(ok);
     v4u pf[kBcPer];
+    if constexpr (GW && !LW) {
+      // GW: groups of windowed objects whose blobs fit one window together;
+      // the group's entry chains are walked lane-parallel, then its objects
+      // decoded one by one from the window (read once, one chain step per
+      // group step instead of per object)
+      static_assert(XL::kMem == XS::kMem, "the group walk parks its entries in XS's arrays");
+      uint64_t rem = wins;
+      auto group_of = [&](uint64_t& g, uint64_t& ga, uint32_t& gn) {
+        const uint32_t t = (uint32_t)__builtin_ctzll(rem);
+        ga = bc_lane64(a0, t);
+        const bool fit = ((rem >> lane) & 1ull) && off >= ga && off + len + 16u <= ga + kBcStage;
+        g = __ballot(fit);
+        uint32_t e = fit ? (uint32_t)(off + len - ga) : 0u;  // the group's end, < kBcStage past ga
+        for (uint32_t dd = 32; dd >= 1; dd >>= 1) e = max(e, (uint32_t)__shfl_xor((int)e, (int)dd, kBcWave));
+        gn = (bc_uni(e) + 15u) / 16u;
+        rem &= ~g;
+      };
+      uint64_t gc = 0ull, ga = 0ull;
+      uint32_t gn = 0u;
+      if (rem) {
+        group_of(gc, ga, gn);
+        bc_prefetch(pf, blobs, blob_bytes, ga, gn, lane);
+      }
+      uint32_t* Pm = (uint32_t*)(X + XS::Pm);
+      uint32_t* Lm = (uint32_t*)(X + XS::Lm);
+      const uint8_t* wb = (const uint8_t*)st_s[wave];
+      uint64_t slow = pend & ~wins;  // decoded one by one from HBM after the groups
+      while (gc) {
+        bc_sync();  // the previous group's window and scratch readers are done
+#pragma unroll
+        for (uint32_t k = 0; k < kBcPer; ++k) st_s[wave][lane + k * kBcWave] = pf[k];
+        bc_sync();
+        const uint64_t gcur = gc, acur = ga;
+        gc = 0ull;
+        if (rem) {  // the next group's span in flight while this one is decoded
+          group_of(gc, ga, gn);
+          bc_prefetch(pf, blobs, blob_bytes, ga, gn, lane);
+        }
+        const bool mine = (gcur >> lane) & 1ull;
+        const Src<true> Bm{wb, (uint32_t)(off - acur)};
+        // the entry counts first (each lane's blob header), their offsets in
+        // the entry arrays by a scan, then every chain walked and parked
+        uint32_t cnt = 0u;
+        if (mine && len >= 24u && len < (1ull << 31)) {
+          const uint64_t nclk = Bm.get(0, 8);
+          if (nclk <= A && nclk * (wa + 8u) <= len - 24u) {
+            const uint64_t ne = Bm.get(8u + nclk * (wa + 8u), 8);
+            cnt = ne <= XS::kMem ? (uint32_t)ne : 0u;
+          }
+        }
+        const uint32_t incl = bc_scan_incl(cnt, lane), base = incl - cnt;
+        const bool fits = __builtin_amdgcn_readlane(incl, kBcWave - 1u) <= XS::kMem;
+        LaneWalk lw2{0, 0, 0, 0, 0, 0, 0, 0};
+        if (mine) lw2 = bc_lane_walk_window(Bm, len, wa, wm, A, Pm, Lm, base, fits);
+        bc_xsync<XS>();
+        if (!fits) {  // (entry arrays overflowed: a malformed or oversized group) one object at a time
+          slow |= gcur;
+          continue;
+        }
+        for (uint64_t pend2 = gcur; pend2; pend2 &= pend2 - 1) {
+          const uint32_t t = (uint32_t)__builtin_ctzll(pend2);
+          const uint64_t o = cbase + t, oot = bc_lane64(oo, t);
+          const Src<true> B{wb, (uint32_t)(bc_lane64(off, t) - acur)};
+          int rc;
+          {
+            const int err = __builtin_amdgcn_readlane(lw2.err, t);
+            if (err == CRDT_ECAPACITY) {  // past the LDS scratch: the large-object kernel
+              uint32_t e = 0u;
+              if (lane == 0u) {
+                e = atomicAdd(&ctl[0], 1u);
+                if (e < list_cap) list[e] = o;
+              }
+              rc = bc_uni(e) < list_cap ? 0 : CRDT_ECAPACITY;
+            } else if (err) {
+              rc = err;
+            } else {
+              BcWalk w;
+              w.n_clk = __builtin_amdgcn_readlane(lw2.n_clk, t);
+              w.n_mem = __builtin_amdgcn_readlane(lw2.n_mem, t);
+              w.n_dot = __builtin_amdgcn_readlane(lw2.n_dot, t);
+              w.n_def = __builtin_amdgcn_readlane(lw2.n_def, t);
+              w.n_def_dot = __builtin_amdgcn_readlane(lw2.n_fdot, t);
+              w.n_def_mem = __builtin_amdgcn_readlane(lw2.n_fmem, t);
+              w.err = 0;
+              const uint64_t size = record_size64(sparse ? w.n_clk : A, w.n_mem, w.n_dot, w.n_def, w.n_def_dot,
+                                                  w.n_def_mem, sparse);
+              if (size > out_bytes - oot) {
+                rc = CRDT_ECAPACITY;
+              } else {
+                bc_sync();  // the previous object's readers of the deferred arrays are done
+                if (w.n_def) bc_walk_deferred(B, bc_lane64(lw2.p_def, t), wa, wm, X, lane);
+                bc_sync();
+                rc = bc_write_record<false, XL>(B, w, wa, wm, A, sparse, X, out + oot, lane, nullptr,
+                                                __builtin_amdgcn_readlane(base, t));
+              }
+            }
+          }
+          if (rc && lane == 0u) atomicCAS(status, 0, rc);
+        }
+      }
+      // the blobs past the window (len + 32 > 4 KB): one by one from HBM
+      for (uint64_t pend2 = slow; pend2; pend2 &= pend2 - 1) {
+        const uint32_t t = (uint32_t)__builtin_ctzll(pend2);
+        const uint64_t o = cbase + t, ot = bc_lane64(off, t), oot = bc_lane64(oo, t), lt = bc_lane64(len, t);
+        const Src<false> B{blobs + ot};
+        const int rc = bc_decode_listed<XL>(B, o, lt, wa, wm, A, sparse, X, out, oot, out_bytes, ctl, list, list_cap,
+                                            lane);
+        if (rc && lane == 0u) atomicCAS(status, 0, rc);
+      }
+      continue;
+    }
     uint64_t nxt = wins;
     if (nxt) {
       const uint32_t t = (uint32_t)__builtin_ctzll(nxt);
@@ -1232,7 +1396,7 @@ int launch_bincode_ingest(const uint8_t* blobs, uint64_t blob_bytes, const uint6
                        blobs, blob_bytes, boff, blen, n_obj, wa, wm, A, flags, sizes, status);
   } else {
     if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;  // ctl[3]: tickets
-    static std::atomic<int> occ_d{0}, occ_r{0}, occ_5{0};
+    static std::atomic<int> occ_d{0}, occ_r{0}, occ_5{0}, occ_g{0};
     if (!list || !big_scratch) return CRDT_EINVAL;
     if (walk == 1) {
 #ifdef CRDT_DIAG
@@ -1242,6 +1406,17 @@ int launch_bincode_ingest(const uint8_t* blobs, uint64_t blob_bytes, const uint6
                          list_cap);
 #else
       (void)occ_d;
+      return CRDT_EINVAL;
+#endif
+    } else if (walk == 3) {
+#ifdef CRDT_DIAG
+      // the per-object read-once walk (the r04 product before the group walk)
+      const uint32_t rblocks = bc_resident_blocks(n_obj, (const void*)bincode_decode_kernel<false>, occ_r);
+      hipLaunchKernelGGL(bincode_decode_kernel<false>, dim3(rblocks), dim3(kBcWave * kBcWaves), 0, stream, blobs,
+                         blob_bytes, boff, blen, n_obj, wa, wm, A, flags, out, ooff, out_bytes, status, ctl, list,
+                         list_cap);
+#else
+      (void)occ_r;
       return CRDT_EINVAL;
 #endif
     } else if (walk == 2) {
@@ -1254,11 +1429,11 @@ int launch_bincode_ingest(const uint8_t* blobs, uint64_t blob_bytes, const uint6
       (void)occ_5;
       return CRDT_EINVAL;
 #endif
-    } else {
-      const uint32_t rblocks = bc_resident_blocks(n_obj, (const void*)bincode_decode_kernel<false>, occ_r);
-      hipLaunchKernelGGL(bincode_decode_kernel<false>, dim3(rblocks), dim3(kBcWave * kBcWaves), 0, stream, blobs,
-                         blob_bytes, boff, blen, n_obj, wa, wm, A, flags, out, ooff, out_bytes, status, ctl, list,
-                         list_cap);
+    } else {  // product: the read-once group walk
+      const uint32_t rblocks = bc_resident_blocks(n_obj, (const void*)bincode_decode_kernel<false, XS, 4, true>, occ_g);
+      hipLaunchKernelGGL((bincode_decode_kernel<false, XS, 4, true>), dim3(rblocks), dim3(kBcWave * kBcWaves), 0,
+                         stream, blobs, blob_bytes, boff, blen, n_obj, wa, wm, A, flags, out, ooff, out_bytes, status,
+                         ctl, list, list_cap);
     }
     hipLaunchKernelGGL(bincode_decode_big_kernel, dim3(kBcBigWaves), dim3(kBcWave), 0, stream, blobs, boff, blen, wa,
                        wm, A, flags, out, ooff, out_bytes, status, ctl, list, list_cap, big_scratch);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of the bincode decode pass (crdt_orswot_from_bincode
 on bound-placed records, config 3, 1M objects, actors u8 / members u64) over
-diagnostic variants (0: product, read once; 305: lane walk; 304: read once at 5 waves/SIMD); each variant's
+diagnostic variants (0: product, read-once group walk; 306: read once per object; 305: lane walk; 304: read once at 5 waves/SIMD); each variant's
 records are compared byte for byte with variant 0's. One JSON line."""
 import argparse
 import ctypes as C
