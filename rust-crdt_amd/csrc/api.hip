@@ -642,7 +642,8 @@ int crdt_map_orswot_merge(crdt_ctx* ctx, const crdt_map_orswot_slab* self, const
         return CRDT_EINVAL;
   int rc = set_device(ctx);
   if (rc) return rc;
-  return launch_map_orswot_merge(*self, *other, *out, n_obj, n_actors, ctx->d_status, ctx->d_ctl, S(stream));
+  return launch_map_orswot_merge(*self, *other, *out, n_obj, n_actors, ctx->d_status, ctx->d_ctl, S(stream),
+                                 ctx->variant);
 }
 
 }  // extern "C"

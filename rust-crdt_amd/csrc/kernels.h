@@ -90,7 +90,7 @@ int launch_map_map_merge(const crdt_map_map_slab& S, const crdt_map_map_slab& O,
                          hipStream_t stream);
 int launch_map_orswot_merge(const crdt_map_orswot_slab& S, const crdt_map_orswot_slab& O,
                             const crdt_map_orswot_slab& R, uint64_t n_obj, uint32_t A, int* status, uint32_t* ctl,
-                            hipStream_t stream);
+                            hipStream_t stream, int variant = 0);
 size_t map_orswot_lds_bytes(const crdt_map_orswot_slab& S, const crdt_map_orswot_slab& O, uint32_t A);
 
 }  // namespace crdts_hip

@@ -19,8 +19,11 @@
 // n_actors <= 64, 2 for <= 128: lane l holds actors l and l + 64), so every
 // VClock operation on dense rows is NS lane-parallel ops plus a ballot. The nested
 // set being built lives in an LDS workspace (member keys + member clock rows
-// + deferred clocks + their member sets), double-buffered for the set merge;
-// keys, members and deferred entries are walked by wave-uniform loops.
+// + deferred clocks + their member sets); a key's two nested sets are staged
+// into it by wide loads (one round trip per side), the merge writes a third;
+// the object's map deferred sets are staged once per object when they fit
+// kMoStageMax. Keys, members and deferred entries are then
+// walked by wave-uniform loops over LDS, not over HBM round trips.
 #include <hip/hip_runtime.h>
 
 #include "../../include/crdts_hip.h"
@@ -34,6 +37,7 @@ namespace {
 constexpr uint32_t kMoW = 64;
 constexpr uint32_t kMoComb = 64;       // combined map deferred entries (<= dcap_self + dcap_other)
 constexpr uint32_t kMoLdsMax = 65536;  // workspace limit per wave
+constexpr uint32_t kMoStageMax = 4096;  // map deferred staging area limit per wave
 
 __device__ __forceinline__ void mo_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -73,27 +77,35 @@ struct Ws {
   uint64_t* row;   // [MW][A] member clocks
   uint64_t* dclk;  // [DW][A] deferred clocks, CLOCK ORDER
   uint32_t* dn;    // [DW] set sizes
-  uint64_t* dset;  // [DW][SW] member sets, ascending
-  uint32_t nm, nd;
+  uint64_t* dset;  // [DW][sw] member sets, ascending
+  uint32_t nm, nd, sw;
 };
 struct Caps {
   uint32_t MW, DW, SW, A;
 };
 
 // Load key slot ki of a slab's nested set into W.
-__device__ void ws_load(Ws& W, const crdt_map_orswot_slab& X, uint64_t ki, const Caps& c, uint32_t lane) {
-  W.nm = uni(X.vn_mem[ki]);
-  W.nd = uni(X.vn_def[ki]);
+// Key slot ki of a slab's nested set into W: its two counts (ws_counts), then
+// every array (ws_copy: each load independent of the others' results — the
+// deferred sets copied capacity-strided, their sizes by one lane each), so a
+// caller staging both sides' slots pays one round trip for the counts and one
+// for the data, then one mo_sync.
+__device__ __forceinline__ void ws_counts(Ws& W, const crdt_map_orswot_slab& X, uint64_t ki, uint32_t k, uint32_t vm,
+                                          uint32_t vd) {
+  // key k's counts: lane k of the registers the key walk loaded (k < 64)
+  W.nm = k < kMoW ? (uint32_t)__builtin_amdgcn_readlane(vm, k) : uni(X.vn_mem[ki]);
+  W.nd = k < kMoW ? (uint32_t)__builtin_amdgcn_readlane(vd, k) : uni(X.vn_def[ki]);
+}
+__device__ void ws_copy(Ws& W, const crdt_map_orswot_slab& X, uint64_t ki, const Caps& c, uint32_t lane) {
   for (uint32_t j = lane; j < W.nm; j += kMoW) W.key[j] = X.vmem[ki * X.mcap + j];
   for (uint32_t e = lane; e < W.nm * c.A; e += kMoW) W.row[e] = X.vmclock[ki * X.mcap * c.A + e];
   for (uint32_t e = lane; e < W.nd * c.A; e += kMoW) W.dclk[e] = X.vdclock[ki * X.vdcap * c.A + e];
-  for (uint32_t d = 0; d < W.nd; ++d) {
-    const uint64_t di = ki * X.vdcap + d;
-    const uint32_t n = uni(X.vdset_n[di]);
-    if (lane == 0u) W.dn[d] = n;
-    for (uint32_t j = lane; j < n; j += kMoW) W.dset[d * c.SW + j] = X.vdset[di * X.vscap + j];
+  if (lane < W.nd) W.dn[lane] = X.vdset_n[ki * X.vdcap + lane];  // nd <= vdcap <= 32
+  const uint32_t vs = X.vscap;
+  for (uint32_t e = lane; e < W.nd * vs; e += kMoW) {
+    const uint32_t d = e / vs;
+    W.dset[d * W.sw + (e - d * vs)] = X.vdset[ki * X.vdcap * vs + e];
   }
-  mo_sync();
 }
 
 // Orswot::apply_deferred (src/orswot.rs:235-243) on W under top clock `clk`,
@@ -107,7 +119,7 @@ __device__ void ws_apply_deferred(Ws& W, Row<NS> clk, uint32_t* mdead, uint32_t*
     const Row<NS> D = ldrow<NS>(W.dclk + d * c.A, c.A, lane);
     const uint32_t n = uni(W.dn[d]);
     for (uint32_t j = 0; j < n; ++j) {
-      const uint64_t m = uni64(W.dset[d * c.SW + j]);
+      const uint64_t m = uni64(W.dset[d * W.sw + j]);
       uint32_t lo = 0, hi = W.nm;  // binary search over the (sorted) members
       while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -147,11 +159,11 @@ __device__ void ws_apply_deferred(Ws& W, Row<NS> clk, uint32_t* mdead, uint32_t*
     if (k != d) {
       const Row<NS> D = ldrow<NS>(W.dclk + d * c.A, c.A, lane);
       const uint32_t n = uni(W.dn[d]);
-      uint64_t s0 = lane < n ? W.dset[d * c.SW + lane] : 0ull;
+      uint64_t s0 = lane < n ? W.dset[d * W.sw + lane] : 0ull;
       mo_sync();
       strow(W.dclk + k * c.A, D, c.A, lane);
       if (lane == 0u) W.dn[k] = n;
-      if (lane < n) W.dset[k * c.SW + lane] = s0;  // SW <= 64
+      if (lane < n) W.dset[k * W.sw + lane] = s0;  // sw <= 64
       mo_sync();
     }
     ++k;
@@ -162,20 +174,19 @@ __device__ void ws_apply_deferred(Ws& W, Row<NS> clk, uint32_t* mdead, uint32_t*
   mo_sync();
 }
 
-// Orswot::merge (src/orswot.rs:87-157): Wn = Wc.merge(&other), other = key
-// slot ko of O. `sclk` (Wc's top clock) becomes the merged clock.
+// Orswot::merge (src/orswot.rs:87-157): Wn = Wc.merge(&Wo), Wo's top clock
+// oclk. `sclk` (Wc's top clock) becomes the merged clock.
 template <int NS>
-__device__ void ws_merge(const Ws& Wc, Ws& Wn, Row<NS>& sclk, const crdt_map_orswot_slab& O, uint64_t ko,
-                         uint32_t* mdead, uint32_t* ddead, const Caps& c, uint32_t lane) {
-  const Row<NS> oclk = rowv<NS>(O.vclock, ko, c.A, lane);
-  const uint32_t no = uni(O.vn_mem[ko]);
+__device__ void ws_merge(const Ws& Wc, const Ws& Wo, Ws& Wn, Row<NS>& sclk, Row<NS> oclk, uint32_t* mdead,
+                         uint32_t* ddead, const Caps& c, uint32_t lane) {
+  const uint32_t no = Wo.nm;
   uint32_t a = 0, b = 0, n = 0;
   while (a < Wc.nm || b < no) {
     const uint64_t ka = a < Wc.nm ? uni64(Wc.key[a]) : ~0ull;
-    const uint64_t kb = b < no ? uni64(O.vmem[ko * O.mcap + b]) : ~0ull;
+    const uint64_t kb = b < no ? uni64(Wo.key[b]) : ~0ull;
     const bool hs = a < Wc.nm && (b >= no || ka <= kb), ho = b < no && (a >= Wc.nm || kb <= ka);
     const Row<NS> r = hs ? ldrow<NS>(Wc.row + a * c.A, c.A, lane) : zrow<NS>();
-    const Row<NS> orow = ho ? rowv<NS>(O.vmclock, ko * O.mcap + b, c.A, lane) : zrow<NS>();
+    const Row<NS> orow = ho ? ldrow<NS>(Wo.row + b * c.A, c.A, lane) : zrow<NS>();
     Row<NS> out;
     bool keep;
     if (hs && !ho) {  // :94-104: dropped iff other has seen all of it
@@ -200,28 +211,28 @@ __device__ void ws_merge(const Ws& Wc, Ws& Wn, Row<NS>& sclk, const crdt_map_ors
   }
   Wn.nm = n;
   // deferred: union by clock (:141-148), sets united — CLOCK ORDER merge of both lists
-  const uint32_t od = uni(O.vn_def[ko]);
+  const uint32_t od = Wo.nd;
   uint32_t p = 0, q = 0, nd = 0;
   while (p < Wc.nd || q < od) {
     const Row<NS> dp = p < Wc.nd ? ldrow<NS>(Wc.dclk + p * c.A, c.A, lane) : zrow<NS>();
-    const Row<NS> dq = q < od ? rowv<NS>(O.vdclock, ko * O.vdcap + q, c.A, lane) : zrow<NS>();
+    const Row<NS> dq = q < od ? ldrow<NS>(Wo.dclk + q * c.A, c.A, lane) : zrow<NS>();
     int ord;
     if (p >= Wc.nd) ord = 1;
     else if (q >= od) ord = -1;
     else ord = vorder(dp, dq, lane);
     strow(Wn.dclk + nd * c.A, ord <= 0 ? dp : dq, c.A, lane);
     if (lane == 0u) {  // sorted union of the member sets
-      const uint64_t* xs = ord <= 0 ? Wc.dset + p * c.SW : nullptr;
+      const uint64_t* xs = ord <= 0 ? Wc.dset + p * Wc.sw : nullptr;
       const uint32_t nx = ord <= 0 ? Wc.dn[p] : 0u;
-      const uint64_t* ys = ord >= 0 ? O.vdset + (ko * O.vdcap + q) * O.vscap : nullptr;
-      const uint32_t ny = ord >= 0 ? O.vdset_n[ko * O.vdcap + q] : 0u;
+      const uint64_t* ys = ord >= 0 ? Wo.dset + q * Wo.sw : nullptr;
+      const uint32_t ny = ord >= 0 ? Wo.dn[q] : 0u;
       uint32_t i = 0, j = 0, k = 0;
       while (i < nx || j < ny) {
         const uint64_t kx = i < nx ? xs[i] : ~0ull, ky = j < ny ? ys[j] : ~0ull;
         const uint64_t m = kx < ky ? kx : ky;
         if (kx == m) ++i;
         if (ky == m) ++j;
-        Wn.dset[nd * c.SW + k++] = m;
+        Wn.dset[nd * Wn.sw + k++] = m;
       }
       Wn.dn[nd] = k;
     }
@@ -263,7 +274,7 @@ __device__ bool ws_store(const Ws& W, Row<NS> clk, const crdt_map_orswot_slab& R
   if (!fits) return false;
   strow(R.vclock + kr * c.A, clk, c.A, lane);
   if (lane == 0u) { R.vn_mem[kr] = W.nm; R.vn_def[kr] = W.nd; }
-  const uint32_t nm = W.nm, nmA = W.nm * c.A, ndA = W.nd * c.A, nd = W.nd, vs = R.vscap, SW = c.SW;
+  const uint32_t nm = W.nm, nmA = W.nm * c.A, ndA = W.nd * c.A, nd = W.nd, vs = R.vscap, SW = W.sw;
   const uint64_t* key = W.key;
   const uint64_t* row = W.row;
   const uint64_t* dclk = W.dclk;
@@ -281,28 +292,38 @@ __device__ bool ws_store(const Ws& W, Row<NS> clk, const crdt_map_orswot_slab& R
 }
 
 template <int NS>
-__global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_slab S, crdt_map_orswot_slab O,
+__global__ __launch_bounds__(kMoW, 4) void map_orswot_merge_kernel(crdt_map_orswot_slab S, crdt_map_orswot_slab O,
                                                                 crdt_map_orswot_slab R, uint64_t n_obj, uint32_t A,
-                                                                int* __restrict__ status, uint32_t* __restrict__ ctl) {
+                                                                uint32_t md_cap, int* __restrict__ status,
+                                                                uint32_t* __restrict__ ctl) {
   extern __shared__ uint64_t mo_lds[];
   __shared__ uint32_t comb[kMoComb];  // (self deferred idx + 1) | (other deferred idx + 1) << 8
+  __shared__ uint32_t dn_s[3][kMoComb];  // the three workspaces' deferred set sizes
+  __shared__ uint32_t mdn[2][32];        // the object's map deferred set sizes (dcap <= 32), self / other
   const uint32_t lane = threadIdx.x;
   const Caps c{S.mcap + O.mcap, S.vdcap + O.vdcap, S.vscap + O.vscap, A};
-  // workspace: two nested sets, then the member / deferred drop flags
-  Ws W0, W1;
+  // workspaces: self's key slot (W0), other's (W2), their merge (W1); then the
+  // member / deferred drop flags and the map deferred staging area
+  Ws W0, W1, W2;
   uint32_t* mdead;
+  uint64_t* md;
   {
     uint64_t* p = mo_lds;
-    for (Ws* w : {&W0, &W1}) {
-      w->key = p; p += c.MW;
-      w->row = p; p += c.MW * A;
-      w->dclk = p; p += c.DW * A;
-      w->dset = p; p += c.DW * c.SW;
-      w->dn = (uint32_t*)p; p += (c.DW + 1u) / 2u;
-      w->nm = w->nd = 0u;
+    const uint32_t caps[3][3] = {{S.mcap, S.vdcap, S.vscap}, {c.MW, c.DW, c.SW}, {O.mcap, O.vdcap, O.vscap}};
+    Ws* ws[3] = {&W0, &W1, &W2};
+    for (int w = 0; w < 3; ++w) {
+      const uint32_t m = caps[w][0], d = caps[w][1];
+      ws[w]->key = p; p += m;
+      ws[w]->row = p; p += m * A;
+      ws[w]->dclk = p; p += d * A;
+      ws[w]->dset = p; p += d * caps[w][2];
+      ws[w]->dn = dn_s[w];
+      ws[w]->sw = caps[w][2];
+      ws[w]->nm = ws[w]->nd = 0u;
     }
     mdead = (uint32_t*)p;
     for (uint32_t j = lane; j < c.MW + c.DW; j += kMoW) mdead[j] = 0u;
+    md = p + (c.MW + c.DW + 1u) / 2u;
   }
   uint32_t* const ddead = mdead + c.MW;
   mo_sync();
@@ -316,35 +337,68 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
       if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
       continue;
     }
-    // every count the loops below trust, within its capacity
-    bool bad = false;
-    for (uint32_t k = lane; k < nS; k += kMoW) {
+    // the first 64 keys of each side and their nested counts in registers
+    // (lane k: key k), one round trip
+    const bool ls = lane < nS, lo = lane < nO;
+    const uint64_t kregS = ls ? S.keys[i * S.kcap + lane] : 0ull, kregO = lo ? O.keys[i * O.kcap + lane] : 0ull;
+    const uint32_t vmS = ls ? S.vn_mem[i * S.kcap + lane] : 0u, vdS = ls ? S.vn_def[i * S.kcap + lane] : 0u;
+    const uint32_t vmO = lo ? O.vn_mem[i * O.kcap + lane] : 0u, vdO = lo ? O.vn_def[i * O.kcap + lane] : 0u;
+    // every count the loops below trust, within its capacity (the nested
+    // deferred set sizes read capacity-wide, so their loads issue together)
+    bool bad = vmS > S.mcap || vdS > S.vdcap || vmO > O.mcap || vdO > O.vdcap;
+    if (ls)
+      for (uint32_t d = 0; d < S.vdcap; ++d) {
+        const uint32_t x = S.vdset_n[(i * S.kcap + lane) * S.vdcap + d];
+        bad |= (d < vdS) & (x > S.vscap);
+      }
+    if (lo)
+      for (uint32_t d = 0; d < O.vdcap; ++d) {
+        const uint32_t x = O.vdset_n[(i * O.kcap + lane) * O.vdcap + d];
+        bad |= (d < vdO) & (x > O.vscap);
+      }
+    for (uint32_t k = kMoW + lane; k < nS; k += kMoW) {
       const uint64_t ki = i * S.kcap + k;
       bad = bad || S.vn_mem[ki] > S.mcap || S.vn_def[ki] > S.vdcap;
       for (uint32_t d = 0; !bad && d < S.vn_def[ki]; ++d) bad = S.vdset_n[ki * S.vdcap + d] > S.vscap;
     }
-    for (uint32_t k = lane; k < nO; k += kMoW) {
+    for (uint32_t k = kMoW + lane; k < nO; k += kMoW) {
       const uint64_t ki = i * O.kcap + k;
       bad = bad || O.vn_mem[ki] > O.mcap || O.vn_def[ki] > O.vdcap;
       for (uint32_t d = 0; !bad && d < O.vn_def[ki]; ++d) bad = O.vdset_n[ki * O.vdcap + d] > O.vscap;
     }
-    for (uint32_t k = lane; k < dS; k += kMoW) bad = bad || S.dset_n[i * S.dcap + k] > S.scap;
-    for (uint32_t k = lane; k < dO; k += kMoW) bad = bad || O.dset_n[i * O.dcap + k] > O.scap;
+    // (dS, dO <= dcap <= 32: one lane per deferred entry)
+    const uint32_t nsS = lane < dS ? S.dset_n[i * S.dcap + lane] : 0u, nsO = lane < dO ? O.dset_n[i * O.dcap + lane] : 0u;
+    bad = bad || nsS > S.scap || nsO > O.scap;
     if (__ballot(bad) != 0ull) {
       if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
       continue;
     }
+    if (lane < 32u) { mdn[0][lane] = nsS; mdn[1][lane] = nsO; }
+    // the map deferred sets staged in LDS when they fit (md_cap words): the
+    // key loop asks each of them about every key. (Staging their clocks too
+    // cost more occupancy than the round trips it saved: DESIGN.md §9.)
+    const uint32_t sS = S.scap, sO = O.scap;
+    const bool st = (uint64_t)dS * sS + (uint64_t)dO * sO <= md_cap;
+    uint64_t* const mdS = md;
+    uint64_t* const mdO = mdS + dS * sS;
+    if (st) {
+      for (uint32_t e = lane; e < dS * sS; e += kMoW) mdS[e] = S.dset[i * S.dcap * sS + e];
+      for (uint32_t e = lane; e < dO * sO; e += kMoW) mdO[e] = O.dset[i * O.dcap * sO + e];
+    }
+    mo_sync();
+    auto sdc = [&](uint32_t a) -> Row<NS> { return rowv<NS>(S.dclock, i * S.dcap + a, A, lane); };
+    auto odc = [&](uint32_t b) -> Row<NS> { return rowv<NS>(O.dclock, i * O.dcap + b, A, lane); };
     // ---- combined map deferred list: self's, plus other's that self's clock does not cover
     //      (apply_rm's deferral, against the pre-merge clock), united in CLOCK ORDER
     uint32_t nc = 0;
     {
       uint32_t a = 0, b = 0;
       while (a < dS || b < dO) {
-        if (b < dO && vle(rowv<NS>(O.dclock, i * O.dcap + b, A, lane), cS)) { ++b; continue; }
+        if (b < dO && vle(odc(b), cS)) { ++b; continue; }
         int o;
         if (a >= dS) o = 1;
         else if (b >= dO) o = -1;
-        else o = vorder(rowv<NS>(S.dclock, i * S.dcap + a, A, lane), rowv<NS>(O.dclock, i * O.dcap + b, A, lane), lane);
+        else o = vorder(sdc(a), odc(b), lane);
         if (lane == 0u) comb[nc] = (o <= 0 ? a + 1u : 0u) | ((o >= 0 ? b + 1u : 0u) << 8);
         ++nc;
         if (o <= 0) ++a;
@@ -354,18 +408,19 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
     mo_sync();
     auto comb_clock = [&](uint32_t e) -> Row<NS> {
       const uint32_t sa = e & 255u, sb = e >> 8;
-      return sa ? rowv<NS>(S.dclock, i * S.dcap + sa - 1u, A, lane) : rowv<NS>(O.dclock, i * O.dcap + sb - 1u, A, lane);
+      return sa ? sdc(sa - 1u) : odc(sb - 1u);
     };
-    auto comb_names = [&](uint32_t e, uint64_t key) -> bool {
-      const uint32_t sa = e & 255u, sb = e >> 8;
-      bool named = false;
-      if (sa) {
-        const uint64_t di = i * S.dcap + sa - 1u;
-        named = set_has(S.dset + di * S.scap, S.dset_n[di], key, lane);
-      }
-      if (!named && sb) {
-        const uint64_t di = i * O.dcap + sb - 1u;
-        named = set_has(O.dset + di * O.scap, O.dset_n[di], key, lane);
+    // the combined entries naming `key`, as a bit mask over the list
+    auto comb_named = [&](uint64_t key) -> uint64_t {
+      uint64_t named = 0ull;
+      for (uint32_t k = 0; k < nc; ++k) {
+        const uint32_t e = comb[k], sa = e & 255u, sb = e >> 8;
+        bool f = false;
+        if (sa)
+          f = set_has(st ? mdS + (sa - 1u) * sS : S.dset + (i * S.dcap + sa - 1u) * sS, mdn[0][sa - 1u], key, lane);
+        if (!f && sb)
+          f = set_has(st ? mdO + (sb - 1u) * sO : O.dset + (i * O.dcap + sb - 1u) * sO, mdn[1][sb - 1u], key, lane);
+        named |= f ? 1ull << k : 0ull;
       }
       return named;
     };
@@ -373,18 +428,24 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
     uint32_t nk = 0, a = 0, b = 0;
     bool over = false;
     while (a < nS || b < nO) {
-      const uint64_t ka = a < nS ? uni64(S.keys[i * S.kcap + a]) : ~0ull;
-      const uint64_t kb = b < nO ? uni64(O.keys[i * O.kcap + b]) : ~0ull;
-      const bool hs = a < nS && (b >= nO || ka <= kb), ho = b < nO && (a >= nS || kb <= ka);
-      const uint64_t key = hs ? ka : kb;
+      const uint64_t ka = a < nS ? (a < kMoW ? lane64(kregS, a) : uni64(S.keys[i * S.kcap + a])) : ~0ull;
+      const uint64_t kb = b < nO ? (b < kMoW ? lane64(kregO, b) : uni64(O.keys[i * O.kcap + b])) : ~0ull;
+      const bool chs = a < nS && (b >= nO || ka <= kb), cho = b < nO && (a >= nS || kb <= ka);
+      const uint64_t ckey = chs ? ka : kb;
       const uint64_t ia = i * S.kcap + a, ib = i * O.kcap + b;
-      const Row<NS> eS = hs ? rowv<NS>(S.eclock, ia, A, lane) : zrow<NS>();
-      const Row<NS> eO = ho ? rowv<NS>(O.eclock, ib, A, lane) : zrow<NS>();
+      const uint32_t ca = a, cb = b;
+      if (chs) ++a;
+      if (cho) ++b;
+      // both entry clocks and both nested top clocks in one round trip
+      const Row<NS> eS = chs ? rowv<NS>(S.eclock, ia, A, lane) : zrow<NS>();
+      const Row<NS> eO = cho ? rowv<NS>(O.eclock, ib, A, lane) : zrow<NS>();
+      const Row<NS> vS = chs ? rowv<NS>(S.vclock, ia, A, lane) : zrow<NS>();
+      const Row<NS> vO = cho ? rowv<NS>(O.vclock, ib, A, lane) : zrow<NS>();
       Row<NS> ec, del;
-      if (hs && !ho) {  // other has not seen it, or saw it and dropped it
+      if (chs && !cho) {  // other has not seen it, or saw it and dropped it
         ec = vsub(eS, cO);
         del = vsub(cO, ec);
-      } else if (ho && !hs) {
+      } else if (cho && !chs) {
         ec = vsub(eO, cS);
         del = vsub(cS, ec);
       } else {
@@ -396,9 +457,9 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
       bool keep = vany(ec);
       // apply_deferred: the entry clock loses every combined clock naming the key
       // (subtracts commute; an entry emptied at any step is gone for good)
+      const uint64_t named = keep && nc ? comb_named(ckey) : 0ull;
       if (keep) {
-        for (uint32_t k = 0; k < nc; ++k)
-          if (comb_names(comb[k], key)) ec = vsub(ec, comb_clock(comb[k]));
+        for (uint64_t m = named; m; m &= m - 1) ec = vsub(ec, comb_clock(comb[__builtin_ctzll(m)]));
         keep = vany(ec);
       }
       if (keep && nk >= R.kcap) {
@@ -407,30 +468,25 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
       }
       if (keep) {
         // the nested set: self's (merged with other's when both have the key) ...
-        Row<NS> vclk;
-        Ws Wk;
-        if (hs) {
-          ws_load(W0, S, ia, c, lane);
-          vclk = rowv<NS>(S.vclock, ia, A, lane);
-          if (ho) {
-            ws_merge(W0, W1, vclk, O, ib, mdead, ddead, c, lane);
-            Wk = W1;
-          } else {
-            Wk = W0;
-          }
-        } else {
-          ws_load(W0, O, ib, c, lane);
-          vclk = rowv<NS>(O.vclock, ib, A, lane);
-          Wk = W0;
+        if (chs) ws_counts(W0, S, ia, ca, vmS, vdS);
+        if (cho) ws_counts(W2, O, ib, cb, vmO, vdO);
+        if (chs) ws_copy(W0, S, ia, c, lane);
+        if (cho) ws_copy(W2, O, ib, c, lane);
+        mo_sync();
+        Row<NS> vclk = chs ? vS : vO;
+        Ws Wk = chs ? W0 : W2;
+        if (chs && cho) {
+          ws_merge(W0, W2, W1, vclk, vO, mdead, ddead, c, lane);
+          Wk = W1;
         }
         // ... truncated by the removers' clock (Map::merge), then by each deferred
         // clock naming the key, in CLOCK ORDER (apply_deferred -> apply_rm)
         ws_truncate(Wk, vclk, del, mdead, ddead, c, lane);
-        for (uint32_t k = 0; k < nc; ++k)
-          if (comb_names(comb[k], key)) ws_truncate(Wk, vclk, comb_clock(comb[k]), mdead, ddead, c, lane);
+        for (uint64_t m = named; m; m &= m - 1)
+          ws_truncate(Wk, vclk, comb_clock(comb[__builtin_ctzll(m)]), mdead, ddead, c, lane);
         const uint64_t ir = i * R.kcap + nk;
         if (ws_store(Wk, vclk, R, ir, c, lane)) {
-          if (lane == 0u) R.keys[ir] = key;
+          if (lane == 0u) R.keys[ir] = ckey;
           strow(R.eclock + ir * A, ec, A, lane);
           ++nk;
         } else {
@@ -438,8 +494,6 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
         }
         mo_sync();
       }
-      if (hs) ++a;
-      if (ho) ++b;
     }
     if (lane == 0u) R.n_keys[i] = nk;
     strow(R.clock + i * A, cM, A, lane);
@@ -455,9 +509,9 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
       strow(R.dclock + dr * A, D, A, lane);
       uint32_t cnt = 0;
       if (lane == 0u) {  // sorted union of the two key sets
-        const uint64_t* xs = sa ? S.dset + (i * S.dcap + sa - 1u) * S.scap : nullptr;
-        const uint64_t* ys = sb ? O.dset + (i * O.dcap + sb - 1u) * O.scap : nullptr;
-        const uint32_t nx = sa ? S.dset_n[i * S.dcap + sa - 1u] : 0u, ny = sb ? O.dset_n[i * O.dcap + sb - 1u] : 0u;
+        const uint64_t* xs = sa ? (st ? mdS + (sa - 1u) * sS : S.dset + (i * S.dcap + sa - 1u) * sS) : nullptr;
+        const uint64_t* ys = sb ? (st ? mdO + (sb - 1u) * sO : O.dset + (i * O.dcap + sb - 1u) * sO) : nullptr;
+        const uint32_t nx = sa ? mdn[0][sa - 1u] : 0u, ny = sb ? mdn[1][sb - 1u] : 0u;
         uint32_t p = 0, q = 0;
         while (p < nx || q < ny) {
           const uint64_t kx = p < nx ? xs[p] : ~0ull, ky = q < ny ? ys[q] : ~0ull;
@@ -480,29 +534,36 @@ __global__ __launch_bounds__(kMoW) void map_orswot_merge_kernel(crdt_map_orswot_
 
 }  // namespace
 
+// The kernel's dynamic workspace: self's and other's key slots and their
+// merge (W0, W2, W1), the drop flags (the deferred set sizes are static LDS).
+// This is the bound crdt_map_orswot_merge checks against 64 KB.
 size_t map_orswot_lds_bytes(const crdt_map_orswot_slab& S, const crdt_map_orswot_slab& O, uint32_t A) {
+  auto per = [&](size_t m, size_t d, size_t s) { return 8 * (m + m * A + d * A + d * s); };
   const size_t MW = S.mcap + O.mcap, DW = S.vdcap + O.vdcap, SW = S.vscap + O.vscap;
-  const size_t per = 8 * (MW + MW * A + DW * A + DW * SW + (DW + 1) / 2);
-  return 2 * per + 4 * (MW + DW) + 16;
+  return per(S.mcap, S.vdcap, S.vscap) + per(O.mcap, O.vdcap, O.vscap) + per(MW, DW, SW) + 8 * ((MW + DW + 1) / 2);
 }
 
 int launch_map_orswot_merge(const crdt_map_orswot_slab& S, const crdt_map_orswot_slab& O,
                             const crdt_map_orswot_slab& R, uint64_t n_obj, uint32_t A, int* status, uint32_t* ctl,
-                            hipStream_t stream) {
+                            hipStream_t stream, int variant) {
   if (n_obj == 0) return CRDT_OK;
   const size_t lds = map_orswot_lds_bytes(S, O, A);
   if (lds > kMoLdsMax) return CRDT_EINVAL;
-  int dev = 0, cus = 256;
+  // the map deferred staging area: the capacity's sets when they fit
+  // kMoStageMax (diag variant 401: none, the sets read from HBM)
+  const size_t md = 8 * ((size_t)S.dcap * S.scap + (size_t)O.dcap * O.scap);
+  const size_t md_bytes = (variant == 401 || md > kMoStageMax || lds + md > kMoLdsMax) ? 0 : md;
+  const uint32_t md_cap = (uint32_t)(md_bytes / 8);
+  const void* fn = A > 64u ? (const void*)map_orswot_merge_kernel<2> : (const void*)map_orswot_merge_kernel<1>;
+  int dev = 0, cus = 256, occ = 0;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const uint64_t cap = (uint64_t)cus * 16u;
+  // one single-wave block per resident slot (LDS-bound: the workspace sizes it)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kMoW, lds + md_bytes) != hipSuccess || occ < 1) occ = 16;
+  const uint64_t cap = (uint64_t)cus * (uint32_t)occ;
   const uint32_t blocks = (uint32_t)(n_obj < cap ? n_obj : cap);
   if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;  // ctl[3]: tickets
-  if (A > 64u)
-    hipLaunchKernelGGL(map_orswot_merge_kernel<2>, dim3(blocks), dim3(kMoW), lds, stream, S, O, R, n_obj, A, status,
-                       ctl);
-  else
-    hipLaunchKernelGGL(map_orswot_merge_kernel<1>, dim3(blocks), dim3(kMoW), lds, stream, S, O, R, n_obj, A, status,
-                       ctl);
+  void* args[] = {(void*)&S, (void*)&O, (void*)&R, &n_obj, &A, (void*)&md_cap, &status, &ctl};
+  if (hipLaunchKernel(fn, dim3(blocks), dim3(kMoW), args, lds + md_bytes, stream) != hipSuccess) return CRDT_EHIP;
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 
