@@ -85,11 +85,11 @@ struct Caps {
 };
 
 // Load key slot ki of a slab's nested set into W.
-// Key slot ki of a slab's nested set into W: its two counts (ws_counts), then
-// every array (ws_copy: each load independent of the others' results — the
-// deferred sets copied capacity-strided, their sizes by one lane each), so a
-// caller staging both sides' slots pays one round trip for the counts and one
-// for the data, then one mo_sync.
+// Key slot ki of a slab's nested set into W: its two counts (ws_counts, from
+// the key walk's registers), then every array (ws_copy: each load
+// independent of the others' results — the deferred sets copied
+// capacity-strided, their sizes by one lane each — so both sides' slots cost
+// one round trip), then the caller's mo_sync.
 __device__ __forceinline__ void ws_counts(Ws& W, const crdt_map_orswot_slab& X, uint64_t ki, uint32_t k, uint32_t vm,
                                           uint32_t vd) {
   // key k's counts: lane k of the registers the key walk loaded (k < 64)
@@ -102,7 +102,7 @@ __device__ void ws_copy(Ws& W, const crdt_map_orswot_slab& X, uint64_t ki, const
   for (uint32_t e = lane; e < W.nd * c.A; e += kMoW) W.dclk[e] = X.vdclock[ki * X.vdcap * c.A + e];
   if (lane < W.nd) W.dn[lane] = X.vdset_n[ki * X.vdcap + lane];  // nd <= vdcap <= 32
   const uint32_t vs = X.vscap;
-  for (uint32_t e = lane; e < W.nd * vs; e += kMoW) {
+  for (uint32_t e = lane; e < W.nd * vs; e += kMoW) {  // capacity-strided: no wait for the sizes
     const uint32_t d = e / vs;
     W.dset[d * W.sw + (e - d * vs)] = X.vdset[ki * X.vdcap * vs + e];
   }
@@ -374,6 +374,7 @@ __global__ __launch_bounds__(kMoW, 4) void map_orswot_merge_kernel(crdt_map_orsw
       continue;
     }
     if (lane < 32u) { mdn[0][lane] = nsS; mdn[1][lane] = nsO; }
+    mo_sync();
     // the map deferred sets staged in LDS when they fit (md_cap words): the
     // key loop asks each of them about every key. (Staging their clocks too
     // cost more occupancy than the round trips it saved: DESIGN.md §9.)
@@ -381,9 +382,15 @@ __global__ __launch_bounds__(kMoW, 4) void map_orswot_merge_kernel(crdt_map_orsw
     const bool st = (uint64_t)dS * sS + (uint64_t)dO * sO <= md_cap;
     uint64_t* const mdS = md;
     uint64_t* const mdO = mdS + dS * sS;
-    if (st) {
-      for (uint32_t e = lane; e < dS * sS; e += kMoW) mdS[e] = S.dset[i * S.dcap * sS + e];
-      for (uint32_t e = lane; e < dO * sO; e += kMoW) mdO[e] = O.dset[i * O.dcap * sO + e];
+    if (st) {  // the used entries of each set
+      for (uint32_t e = lane; e < dS * sS; e += kMoW) {
+        const uint32_t d = e / sS;
+        if (e - d * sS < mdn[0][d]) mdS[e] = S.dset[i * S.dcap * sS + e];
+      }
+      for (uint32_t e = lane; e < dO * sO; e += kMoW) {
+        const uint32_t d = e / sO;
+        if (e - d * sO < mdn[1][d]) mdO[e] = O.dset[i * O.dcap * sO + e];
+      }
     }
     mo_sync();
     auto sdc = [&](uint32_t a) -> Row<NS> { return rowv<NS>(S.dclock, i * S.dcap + a, A, lane); };
