@@ -192,3 +192,46 @@ def test_malformed_blobs(gpu):
     with pytest.raises(CrdtError):
         gpu.orswot_to_bincode(B, 1, 1)
     gpu.status()  # latched errors were cleared by the raising calls
+
+
+def test_group_walk_shapes(gpu):
+    """The decode pass walks the blobs that share one 4 KB window as a group
+    (lane-parallel entry chains): ~30 small blobs per group, a blob past the
+    scratch's deferred limit inside a group (sent to the large-object
+    kernel), blobs straddling the window edge — records byte-exact; a
+    malformed blob inside a group, and blobs whose claimed entry counts
+    overflow the group's entry arrays (the per-object fallback) — errors
+    latched. (Valid blobs cannot overflow them: an entry takes >= 18 B, so a
+    4 KB window holds < 256.)"""
+    from crdts_hip._lib import CrdtError
+
+    rng = random.Random(11)
+
+    def tiny(k, nm):
+        return dict(clock={1 + k % 15: 1 + k}, entries={(k * 7 + j) % 250: [(1 + k % 15, 1 + j % (1 + k))]
+                                                         for j in range(nm)}, deferred=[])
+
+    # 120 blobs of 5-6 members, ~30 to a window
+    sts = [tiny(k, 5 + k % 2) for k in range(120)]
+    # a small blob with 100 deferred clocks (past the scratch's deferred limit) among them
+    sts[40] = dict(clock={2: 1}, entries={3: [(2, 1)]}, deferred=[([(1, d + 1)], [d % 200]) for d in range(100)])
+    # blobs of ~1.3 KB so that groups end at the window edge
+    sts += [dict(clock={1: 90}, entries={m: [(1, m + 1)] for m in range(70 + k)}, deferred=[]) for k in range(12)]
+    t, bo, bl = _upload_blobs([BC.encode(s, 1, 1, rng=rng) for s in sts], rng)
+    exp = [_rec(s, 16, False) for s in sts]
+    assert gpu.orswot_from_bincode(t, bo, bl, 16, 1, 1).records() == exp
+    assert gpu.orswot_from_bincode(t, bo, bl, 16, 1, 1, packed=False).records() == exp
+    # one malformed blob (a trailing byte) in the middle of a group
+    blobs = [BC.encode(s, 1, 1) for s in sts[:20]]
+    blobs[9] = blobs[9] + b"\x00"
+    t, bo, bl = _upload_blobs(blobs)
+    with pytest.raises(CrdtError) as e:
+        gpu.orswot_from_bincode(t, bo, bl, 16, 1, 1)
+    assert e.value.code == -2
+    # two blobs claiming 200 entries each in one window
+    liar = (0).to_bytes(8, "little") + (200).to_bytes(8, "little") + bytes(40)
+    t, bo, bl = _upload_blobs([BC.encode(s, 1, 1) for s in sts[:3]] + [liar, liar] + [BC.encode(sts[3], 1, 1)])
+    with pytest.raises(CrdtError) as e:
+        gpu.orswot_from_bincode(t, bo, bl, 16, 1, 1)
+    assert e.value.code == -2
+    gpu.status()
