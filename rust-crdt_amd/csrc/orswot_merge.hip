@@ -3428,12 +3428,13 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
   // chunks): 15.3 -> 13.5 ms per 8-replica fold of 1M objects (tools/ab_sparse.py)
   const void* fn = (const void*)orswot_sparse_mask_kernel<3, 0, 16, 5>;
 #endif
-  static std::atomic<int> occ_cache{0};
-  occ = occ_cache.load(std::memory_order_relaxed);
+  static std::atomic<int> occ_cache[16];  // per variant (the product: 0)
+  const int oslot = sparse_variant >= 0 && sparse_variant < 16 ? sparse_variant : 0;
+  occ = occ_cache[oslot].load(std::memory_order_relaxed);
   if (occ == 0) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)
       occ = 2;
-    occ_cache.store(occ, std::memory_order_relaxed);
+    occ_cache[oslot].store(occ, std::memory_order_relaxed);
   }
   const uint64_t chunks = (n_obj + kWave - 1) / kWave;
   const uint64_t want = (chunks + kWavesPerBlock - 1) / kWavesPerBlock;
