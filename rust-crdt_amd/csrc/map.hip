@@ -50,6 +50,9 @@ __device__ __forceinline__ bool set_has(const uint64_t* set, uint32_t n, uint64_
 // launcher picks VS when mcap * A <= kVsRows on both sides); otherwise every
 // row read in the dominance loops is its own dependent global load.
 constexpr uint32_t kVsRows = 128;  // u64 per side
+// the object's map deferred sets are staged in LDS (asked about every key)
+// when both sides' fit kMdStage u64
+constexpr uint32_t kMdStage = 128;
 
 // G (the nested map's inner pass): n_obj tasks, task t merges S row tsrc[2t]
 // with O row tsrc[2t + 1] into R row t; kMpNone marks an absent side (an
@@ -57,7 +60,7 @@ constexpr uint32_t kVsRows = 128;  // u64 per side
 constexpr uint64_t kMpNone = ~0ull;
 
 template <bool VS, int NS, bool G = false>
-__global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_slab S, crdt_map_mvreg_slab O,
+__global__ __launch_bounds__(kMpW, 7) void map_mvreg_merge_kernel(crdt_map_mvreg_slab S, crdt_map_mvreg_slab O,
                                                                crdt_map_mvreg_slab Rout, uint64_t n_obj, uint32_t A,
                                                                int* __restrict__ status, uint32_t* __restrict__ ctl,
                                                                const uint64_t* __restrict__ tsrc = nullptr,
@@ -66,6 +69,8 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
   __shared__ uint32_t comb[kMpComb];     // (self deferred idx + 1) | (other deferred idx + 1) << 8
   __shared__ uint32_t vals[kMpVals];     // kept value slots of the key: side << 8 | slot
   __shared__ uint64_t vr[2][VS ? kVsRows : 1];  // the key's value clock rows: self, other
+  __shared__ uint64_t md[kMdStage];             // the object's map deferred sets (when they fit)
+  __shared__ uint32_t mdn[2][64];               // their sizes (dcap <= 64), self / other
   const uint32_t lane = threadIdx.x;
   // (sched.h; G: most tasks are empty slots, a plain stride balances them)
   typename std::conditional<G, GridStride, BlockTickets<4>>::type sched(n_obj, ctl + 3, lane);
@@ -92,16 +97,40 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
     // loops below read mv_n / dset_n slots of the slab row as counts); lane k
     // keeps key k's value count (keys < 64), which the value-row stage below
     // reads by readlane (no dependent load on the per-key chain)
+    // (and its key; lane d: map deferred entry d's set size, dcap <= 64)
     const uint32_t vnS = lane < nS ? S.mv_n[si * S.kcap + lane] : 0u, vnO = lane < nO ? O.mv_n[oi * O.kcap + lane] : 0u;
-    bool bad = vnS > S.mcap || vnO > O.mcap;
+    const uint64_t kregS = lane < nS ? S.keys[si * S.kcap + lane] : 0ull;
+    const uint64_t kregO = lane < nO ? O.keys[oi * O.kcap + lane] : 0ull;
+    const uint32_t dnS = lane < dS ? S.dset_n[si * S.dcap + lane] : 0u, dnO = lane < dO ? O.dset_n[oi * O.dcap + lane] : 0u;
+    bool bad = vnS > S.mcap || vnO > O.mcap || dnS > S.scap || dnO > O.scap;
     for (uint32_t k = lane + kMpW; k < nS; k += kMpW) bad = bad || S.mv_n[si * S.kcap + k] > S.mcap;
     for (uint32_t k = lane + kMpW; k < nO; k += kMpW) bad = bad || O.mv_n[oi * O.kcap + k] > O.mcap;
-    for (uint32_t k = lane; k < dS; k += kMpW) bad = bad || S.dset_n[si * S.dcap + k] > S.scap;
-    for (uint32_t k = lane; k < dO; k += kMpW) bad = bad || O.dset_n[oi * O.dcap + k] > O.scap;
     if (__ballot(bad) != 0ull) {
       if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
       continue;
     }
+    // the map deferred sets (used entries) staged in LDS when they fit
+    const uint32_t sS = S.scap, sO = O.scap;
+    const bool st = (uint64_t)dS * sS + (uint64_t)dO * sO <= kMdStage;
+    mp_sync();  // the previous object's readers of md / mdn are done
+    mdn[0][lane] = dnS;
+    mdn[1][lane] = dnO;
+    mp_sync();
+    if (st) {
+      for (uint32_t e = lane; e < dS * sS; e += kMpW) {
+        const uint32_t d = e / sS;
+        if (e - d * sS < mdn[0][d]) md[e] = S.dset[si * S.dcap * sS + e];
+      }
+      for (uint32_t e = lane; e < dO * sO; e += kMpW) {
+        const uint32_t d = e / sO;
+        if (e - d * sO < mdn[1][d]) md[dS * sS + e] = O.dset[oi * O.dcap * sO + e];
+      }
+    }
+    // map deferred entry d's set (x: 0 self, 1 other)
+    auto dset_of = [&](uint32_t x, uint32_t d) -> const uint64_t* {
+      if (x == 0u) return st ? md + d * sS : S.dset + (si * S.dcap + d) * sS;
+      return st ? md + dS * sS + d * sO : O.dset + (oi * O.dcap + d) * sO;
+    };
     // ---- combined deferred list: self's, plus other's that self's clock does not cover
     //      (apply_rm's deferral, against the pre-merge clock), united in CLOCK ORDER
     uint32_t nc = 0;
@@ -125,7 +154,8 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
     uint32_t nk = 0, a = 0, b = 0;
     bool over = false;
     while (a < nS || b < nO) {
-      const uint64_t ka = a < nS ? S.keys[si * S.kcap + a] : ~0ull, kb = b < nO ? O.keys[oi * O.kcap + b] : ~0ull;
+      const uint64_t ka = a < nS ? (a < kMpW ? lane64(kregS, a) : S.keys[si * S.kcap + a]) : ~0ull;
+      const uint64_t kb = b < nO ? (b < kMpW ? lane64(kregO, b) : O.keys[oi * O.kcap + b]) : ~0ull;
       const bool hs = a < nS && (b >= nO || ka <= kb), ho = b < nO && (a >= nS || kb <= ka);
       const uint64_t key = hs ? ka : kb;
       const uint64_t ia = si * S.kcap + a, ib = oi * O.kcap + b;
@@ -210,14 +240,8 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
           const uint32_t e = comb[c];
           const uint32_t sa = e & 255u, sb = e >> 8;
           bool named = false;
-          if (sa) {
-            const uint64_t di = si * S.dcap + sa - 1u;
-            named = set_has(S.dset + di * S.scap, S.dset_n[di], key, lane);
-          }
-          if (!named && sb) {
-            const uint64_t di = oi * O.dcap + sb - 1u;
-            named = set_has(O.dset + di * O.scap, O.dset_n[di], key, lane);
-          }
+          if (sa) named = set_has(dset_of(0u, sa - 1u), mdn[0][sa - 1u], key, lane);
+          if (!named && sb) named = set_has(dset_of(1u, sb - 1u), mdn[1][sb - 1u], key, lane);
           if (!named) continue;
           const Row<NS> D = sa ? rowv<NS>(S.dclock, si * S.dcap + sa - 1u, A, lane)
                                : rowv<NS>(O.dclock, oi * O.dcap + sb - 1u, A, lane);
@@ -268,9 +292,9 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_merge_kernel(crdt_map_mvreg_sl
       strow<NS>(R.dclock + dr * A, D, A, lane);
       uint32_t cnt = 0;
       if (lane == 0u) {  // sorted union of the two key sets
-        const uint64_t* xs = sa ? S.dset + (si * S.dcap + sa - 1u) * S.scap : nullptr;
-        const uint64_t* ys = sb ? O.dset + (oi * O.dcap + sb - 1u) * O.scap : nullptr;
-        const uint32_t nx = sa ? S.dset_n[si * S.dcap + sa - 1u] : 0u, ny = sb ? O.dset_n[oi * O.dcap + sb - 1u] : 0u;
+        const uint64_t* xs = sa ? dset_of(0u, sa - 1u) : nullptr;
+        const uint64_t* ys = sb ? dset_of(1u, sb - 1u) : nullptr;
+        const uint32_t nx = sa ? mdn[0][sa - 1u] : 0u, ny = sb ? mdn[1][sb - 1u] : 0u;
         uint32_t p = 0, q = 0;
         while (p < nx || q < ny) {
           const uint64_t kx = p < nx ? xs[p] : ~0ull, ky = q < ny ? ys[q] : ~0ull;
