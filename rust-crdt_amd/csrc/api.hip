@@ -581,7 +581,8 @@ int crdt_map_mvreg_merge(crdt_ctx* ctx, const crdt_map_mvreg_slab* self, const c
         return CRDT_EINVAL;
   int rc = set_device(ctx);
   if (rc) return rc;
-  return launch_map_mvreg_merge(*self, *other, *out, n_obj, n_actors, ctx->d_status, ctx->d_ctl, S(stream));
+  return launch_map_mvreg_merge(*self, *other, *out, n_obj, n_actors, ctx->d_status, ctx->d_ctl, S(stream),
+                                ctx->variant);
 }
 
 static bool map_mvreg_caps_ok(const crdt_map_mvreg_slab* x) {

@@ -76,7 +76,7 @@ int launch_mvreg_merge(const uint32_t* sn, const uint64_t* sclk, const uint64_t*
                        hipStream_t stream);
 
 int launch_map_mvreg_merge(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_slab& O, const crdt_map_mvreg_slab& R,
-                           uint64_t n_obj, uint32_t A, int* status, uint32_t* ctl, hipStream_t stream);
+                           uint64_t n_obj, uint32_t A, int* status, uint32_t* ctl, hipStream_t stream, int variant = 0);
 // The nested map's inner pass (map_map.hip): task t merges S row tsrc[2t]
 // with O row tsrc[2t + 1] (~0: an absent side) into R row t, or into Tmp row
 // t when Tb row t is non-empty, and then Tmp row t truncated by Tb row t into R.

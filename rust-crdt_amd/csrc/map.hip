@@ -59,8 +59,8 @@ constexpr uint32_t kMdStage = 128;
 // empty map: merge(m, empty) = m for a canonical m), both absent: no task.
 constexpr uint64_t kMpNone = ~0ull;
 
-template <bool VS, int NS, bool G = false>
-__global__ __launch_bounds__(kMpW, 7) void map_mvreg_merge_kernel(crdt_map_mvreg_slab S, crdt_map_mvreg_slab O,
+template <bool VS, int NS, bool G = false, int MINW = 7>
+__global__ __launch_bounds__(kMpW, MINW) void map_mvreg_merge_kernel(crdt_map_mvreg_slab S, crdt_map_mvreg_slab O,
                                                                crdt_map_mvreg_slab Rout, uint64_t n_obj, uint32_t A,
                                                                int* __restrict__ status, uint32_t* __restrict__ ctl,
                                                                const uint64_t* __restrict__ tsrc = nullptr,
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_truncate_kernel(crdt_map_mvreg
 }  // namespace
 
 int launch_map_mvreg_merge(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_slab& O, const crdt_map_mvreg_slab& R,
-                           uint64_t n_obj, uint32_t A, int* status, uint32_t* ctl, hipStream_t stream) {
+                           uint64_t n_obj, uint32_t A, int* status, uint32_t* ctl, hipStream_t stream, int variant) {
   if (n_obj == 0) return CRDT_OK;
   if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;  // ctl[3]: tickets
   int dev = 0, cus = 256;
@@ -412,6 +412,9 @@ int launch_map_mvreg_merge(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_sl
   if (A > 64u)  // 65-128 actors: two slots per lane
     hipLaunchKernelGGL((map_mvreg_merge_kernel<false, 2>), dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A,
                        status, ctl);
+  else if (vs && variant == 501)  // (diag: no register bound, 5 waves/SIMD, no spill)
+    hipLaunchKernelGGL((map_mvreg_merge_kernel<true, 1, false, 1>), dim3(blocks), dim3(kMpW), 0, stream, S, O, R,
+                       n_obj, A, status, ctl);
   else if (vs)
     hipLaunchKernelGGL((map_mvreg_merge_kernel<true, 1>), dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A,
                        status, ctl);

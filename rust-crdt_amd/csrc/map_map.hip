@@ -36,6 +36,7 @@ using namespace maprow;
 
 constexpr uint32_t kMmW = 64;
 constexpr uint32_t kMmComb = 128;  // combined outer deferred entries (<= dcap_self + dcap_other, dcap <= 64)
+constexpr uint32_t kMmStage = 128;  // u64: the map deferred sets staged per object when both sides fit
 constexpr uint64_t kMmNone = ~0ull;
 
 __device__ __forceinline__ void mm_sync() {
@@ -58,6 +59,8 @@ __global__ __launch_bounds__(kMmW) void map_map_outer_kernel(crdt_map_map_slab S
                                                              uint64_t* __restrict__ tsrc, uint64_t* __restrict__ Tb,
                                                              int* __restrict__ status, uint32_t* __restrict__ ctl) {
   __shared__ uint32_t comb[kMmComb];  // (self deferred idx + 1) | (other deferred idx + 1) << 8
+  __shared__ uint64_t md[kMmStage];    // the object's map deferred sets, used entries (when they fit)
+  __shared__ uint32_t mdn[2][64];      // their sizes (dcap <= 64), self / other
   const uint32_t lane = threadIdx.x;
   BlockTickets<4> sched(n_obj, ctl + 3, lane);  // (sched.h)
   for (uint64_t i = sched.first(); i < n_obj; i = sched.next(i)) {
@@ -70,12 +73,34 @@ __global__ __launch_bounds__(kMmW) void map_map_outer_kernel(crdt_map_map_slab S
     if (nS > S.kcap || nO > O.kcap || dS > S.dcap || dO > O.dcap) {
       if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
     } else {
-      bool bad = false;
-      for (uint32_t k = lane; k < dS; k += kMmW) bad = bad || S.dset_n[i * S.dcap + k] > S.scap;
-      for (uint32_t k = lane; k < dO; k += kMmW) bad = bad || O.dset_n[i * O.dcap + k] > O.scap;
-      if (__ballot(bad) != 0ull) {
+      // lane k: key k (k < 64) and map deferred entry k's set size (dcap <= 64)
+      const uint64_t kregS = lane < nS ? S.keys[i * S.kcap + lane] : 0ull;
+      const uint64_t kregO = lane < nO ? O.keys[i * O.kcap + lane] : 0ull;
+      const uint32_t dnS = lane < dS ? S.dset_n[i * S.dcap + lane] : 0u, dnO = lane < dO ? O.dset_n[i * O.dcap + lane] : 0u;
+      if (__ballot(dnS > S.scap || dnO > O.scap) != 0ull) {
         if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
       } else {
+        // the map deferred sets staged in LDS when they fit (map.hip)
+        const uint32_t sS = S.scap, sO = O.scap;
+        const bool st = (uint64_t)dS * sS + (uint64_t)dO * sO <= kMmStage;
+        mm_sync();  // the previous object's readers of md / mdn are done
+        mdn[0][lane] = dnS;
+        mdn[1][lane] = dnO;
+        mm_sync();
+        if (st) {
+          for (uint32_t e = lane; e < dS * sS; e += kMmW) {
+            const uint32_t d = e / sS;
+            if (e - d * sS < mdn[0][d]) md[e] = S.dset[i * S.dcap * sS + e];
+          }
+          for (uint32_t e = lane; e < dO * sO; e += kMmW) {
+            const uint32_t d = e / sO;
+            if (e - d * sO < mdn[1][d]) md[dS * sS + e] = O.dset[i * O.dcap * sO + e];
+          }
+        }
+        auto dset_of = [&](uint32_t x, uint32_t d) -> const uint64_t* {
+          if (x == 0u) return st ? md + d * sS : S.dset + (i * S.dcap + d) * sS;
+          return st ? md + dS * sS + d * sO : O.dset + (i * O.dcap + d) * sO;
+        };
         // ---- combined deferred list (map.hip): self's, plus other's that self's clock does not cover
         uint32_t nc = 0;
         {
@@ -97,7 +122,8 @@ __global__ __launch_bounds__(kMmW) void map_map_outer_kernel(crdt_map_map_slab S
         // ---- entries, key by key in ascending order
         uint32_t a = 0, b = 0;
         while (a < nS || b < nO) {
-          const uint64_t ka = a < nS ? S.keys[i * S.kcap + a] : ~0ull, kb = b < nO ? O.keys[i * O.kcap + b] : ~0ull;
+          const uint64_t ka = a < nS ? (a < kMmW ? lane64(kregS, a) : S.keys[i * S.kcap + a]) : ~0ull;
+          const uint64_t kb = b < nO ? (b < kMmW ? lane64(kregO, b) : O.keys[i * O.kcap + b]) : ~0ull;
           const bool hs = a < nS && (b >= nO || ka <= kb), ho = b < nO && (a >= nS || kb <= ka);
           const uint64_t key = hs ? ka : kb;
           const uint64_t ia = i * S.kcap + a, ib = i * O.kcap + b;
@@ -122,14 +148,8 @@ __global__ __launch_bounds__(kMmW) void map_map_outer_kernel(crdt_map_map_slab S
               const uint32_t e = comb[c];
               const uint32_t sa = e & 255u, sb = e >> 8;
               bool named = false;
-              if (sa) {
-                const uint64_t di = i * S.dcap + sa - 1u;
-                named = set_has(S.dset + di * S.scap, S.dset_n[di], key, lane);
-              }
-              if (!named && sb) {
-                const uint64_t di = i * O.dcap + sb - 1u;
-                named = set_has(O.dset + di * O.scap, O.dset_n[di], key, lane);
-              }
+              if (sa) named = set_has(dset_of(0u, sa - 1u), mdn[0][sa - 1u], key, lane);
+              if (!named && sb) named = set_has(dset_of(1u, sb - 1u), mdn[1][sb - 1u], key, lane);
               if (!named) continue;
               const Row<NS> D = sa ? rowv<NS>(S.dclock, i * S.dcap + sa - 1u, A, lane)
                                    : rowv<NS>(O.dclock, i * O.dcap + sb - 1u, A, lane);
@@ -171,9 +191,9 @@ __global__ __launch_bounds__(kMmW) void map_map_outer_kernel(crdt_map_map_slab S
           strow<NS>(R.dclock + dr * A, D, A, lane);
           uint32_t cnt = 0;
           if (lane == 0u) {  // sorted union of the two key sets
-            const uint64_t* xs = sa ? S.dset + (i * S.dcap + sa - 1u) * S.scap : nullptr;
-            const uint64_t* ys = sb ? O.dset + (i * O.dcap + sb - 1u) * O.scap : nullptr;
-            const uint32_t nx = sa ? S.dset_n[i * S.dcap + sa - 1u] : 0u, ny = sb ? O.dset_n[i * O.dcap + sb - 1u] : 0u;
+            const uint64_t* xs = sa ? dset_of(0u, sa - 1u) : nullptr;
+            const uint64_t* ys = sb ? dset_of(1u, sb - 1u) : nullptr;
+            const uint32_t nx = sa ? mdn[0][sa - 1u] : 0u, ny = sb ? mdn[1][sb - 1u] : 0u;
             uint32_t p = 0, q = 0;
             while (p < nx || q < ny) {
               const uint64_t kx = p < nx ? xs[p] : ~0ull, ky = q < ny ? ys[q] : ~0ull;
