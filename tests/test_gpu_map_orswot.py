@@ -159,3 +159,21 @@ def test_map_orswot_200_keys_100_actors(gpu, oracle):
         for f in exp.a:
             bad = np.nonzero((np.asarray(got.a[f]) != np.asarray(exp.a[f])).reshape(S.n, -1).any(axis=1))[0]
             assert bad.size == 0, f"{f}: {bad.size} objects differ, first {bad[:5].tolist()}"
+
+
+@pytest.mark.parametrize("scap", [16, 64])
+def test_map_orswot_many_keys_16_actors(gpu, oracle, scap):
+    """Past 64 keys per map at 16 actors (one slot per lane): the key walk
+    reads keys and counts past the first 64 from the slab, and the map
+    deferred sets are staged in LDS per object (scap 16: 4 KB, the staging
+    limit) or read from HBM (scap 64); both orientations, slab-row exact."""
+    A = 16
+    caps = dict(kcap=256, mcap=16, vdcap=8, vscap=16, dcap=16, scap=scap)
+    L, R = oracle.map_orswot_generate(0x3A1, 64, A, keys=120, members=6, ops=160, pct_future=20, caps=caps)
+    assert (L.a["n_keys"] > 64).sum() > 10 and L.a["n_def"].sum() > 10
+    for S, O in ((L, R), (R, L)):
+        exp = oracle.map_orswot_merge(S, O, A).canonical()
+        got = gpu.map_orswot_merge(S.to("cuda"), O.to("cuda"), A).canonical()
+        for f in exp.a:
+            bad = np.nonzero((np.asarray(got.a[f]) != np.asarray(exp.a[f])).reshape(S.n, -1).any(axis=1))[0]
+            assert bad.size == 0, f"{f}: {bad.size} objects differ, first {bad[:5].tolist()}"

@@ -207,3 +207,17 @@ def test_gpu_map_slab_limits(gpu, oracle):
         with pytest.raises(crdts_hip.CrdtError) as e:
             run(A, **kw)
         assert e.value.code == CRDT_EINVAL, (A, kw)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scap", [8, 32])
+def test_gpu_map_many_keys_16_actors(gpu, oracle, scap):
+    """Past 64 keys per map at 16 actors (the value-row stage, one slot per
+    lane): keys past the first 64 read from the slab; the map deferred sets
+    staged in LDS per object (scap 8) or read from HBM (scap 32: past the
+    staging limit); both orientations, slab-row exact."""
+    A = 16
+    L, R = oracle.map_generate(0x3B0 + scap, 400, A, 200, 300, (256, 4, 16, scap))
+    assert (L.a["n_keys"] > 64).sum() > 10 and L.a["n_def"].sum() > 10
+    for S, O in ((L, R), (R, L)):
+        _exact(gpu, oracle, S, O, A)
