@@ -291,8 +291,8 @@ __device__ bool ws_store(const Ws& W, Row<NS> clk, const crdt_map_orswot_slab& R
   return true;
 }
 
-template <int NS>
-__global__ __launch_bounds__(kMoW, 4) void map_orswot_merge_kernel(crdt_map_orswot_slab S, crdt_map_orswot_slab O,
+template <int NS, int MINW = 4>
+__global__ __launch_bounds__(kMoW, MINW) void map_orswot_merge_kernel(crdt_map_orswot_slab S, crdt_map_orswot_slab O,
                                                                 crdt_map_orswot_slab R, uint64_t n_obj, uint32_t A,
                                                                 uint32_t md_cap, int* __restrict__ status,
                                                                 uint32_t* __restrict__ ctl) {
@@ -561,7 +561,10 @@ int launch_map_orswot_merge(const crdt_map_orswot_slab& S, const crdt_map_orswot
   const size_t md = 8 * ((size_t)S.dcap * S.scap + (size_t)O.dcap * O.scap);
   const size_t md_bytes = (variant == 401 || md > kMoStageMax || lds + md > kMoLdsMax) ? 0 : md;
   const uint32_t md_cap = (uint32_t)(md_bytes / 8);
-  const void* fn = A > 64u ? (const void*)map_orswot_merge_kernel<2> : (const void*)map_orswot_merge_kernel<1>;
+  // (diag variant 402: no register bound — 3 waves/SIMD, no spill)
+  const void* fn = A > 64u ? (const void*)map_orswot_merge_kernel<2>
+                   : variant == 402 ? (const void*)map_orswot_merge_kernel<1, 1>
+                                    : (const void*)map_orswot_merge_kernel<1>;
   int dev = 0, cus = 256, occ = 0;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   // one single-wave block per resident slot (LDS-bound: the workspace sizes it)
