@@ -737,8 +737,11 @@ def run_orswot_csr(args, rank, world, local, eng=None):
         "config": {"workload": f"orswot_csr config5 (BASELINE.json configs[4]): {n} objects x {R} replicas, "
                                "CSR top clocks, fold ((r0 ⊔ r1) ⊔ r2) ...",
                    "replicas": R, "n_obj": n, "gen_s": round(gen_s, 2),
-                   "parallelism": ("owner-sharded RCCL join: slices of range j -> rank j (send/recv), rank-order "
-                                   "fold of n/N objects, folded ranges all-gathered (crdt_orswot_replica_join)")
+                   "parallelism": (("owner-sharded join over the gloo transport (crdt_orswot_replica_join_transport): "
+                                    "slices of range j -> rank j, rank-order fold of n/N objects, folded ranges "
+                                    "all-gathered") if args.rehearse else
+                                   ("owner-sharded RCCL join: slices of range j -> rank j (send/recv), rank-order "
+                                    "fold of n/N objects, folded ranges all-gathered (crdt_orswot_replica_join)"))
                    if world > 1 else "local fold"},
     }
     if world > 1:
@@ -818,7 +821,7 @@ def run_gcounter_ae(args, rank, world, local, eng=None):
     stream = torch.cuda.Stream(device=local)
     torch.cuda.synchronize()  # generated on torch's stream; the joins run on `stream`
     check = None
-    ae_eng = None if args.rehearse else eng  # rehearsal: the gloo path of replica.dense_allreduce_max
+    ae_eng = None if args.rehearse else eng  # rehearsal: the gloo path of replica.dense_reduce_scatter_max
     if world > 1:
         if not args.rehearse and not eng.has_comm:
             replica.init_comm(eng)  # the context's own RCCL communicator (crdt_comm_init)
@@ -832,8 +835,15 @@ def run_gcounter_ae(args, rank, world, local, eng=None):
         expect = torch.stack(parts).amax(0)  # counters < 2^41: signed max == u64 max here
         del parts
 
-        def step():
-            replica.dense_allreduce_max(base, engine=ae_eng, stream=stream)
+        if args.rehearse:  # the product's all-reduce over the gloo transport (crdt_replica_allreduce_max_transport)
+            T = replica.GlooTransport()
+            flat_rows = base.view(-1)
+
+            def step():
+                eng.replica_allreduce_max_transport(flat_rows, T, stream=stream)
+        else:
+            def step():
+                replica.dense_allreduce_max(base, engine=ae_eng, stream=stream)
     else:
         other = base.clone()
         other[:, (mine_slot + 1) % A] += 1
@@ -851,8 +861,10 @@ def run_gcounter_ae(args, rank, world, local, eng=None):
         "data": "synthetic: U[0,2^40) base + per-replica increments of its own slot",
         "config": {"workload": f"gcounter_ae config4 (BASELINE.json configs[3]): {n} GCounters x {A} slots per GPU",
                    "bytes_per_gpu": bytes_per_gpu,
-                   "parallelism": (f"RCCL all-reduce(max) over {world} GPUs, native u64 "
-                                   "(crdt_replica_allreduce_max)") if world > 1
+                   "parallelism": ((f"all-reduce(max) over {world} ranks through the gloo transport "
+                                    "(crdt_replica_allreduce_max_transport)") if args.rehearse else
+                                   (f"RCCL all-reduce(max) over {world} GPUs, native u64 "
+                                    "(crdt_replica_allreduce_max)")) if world > 1
                    else "local replica join (dense_max_kernel)"},
     }
     if world > 1:

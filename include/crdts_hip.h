@@ -380,6 +380,15 @@ int crdt_orswot_replica_join_transport(crdt_ctx* ctx, const crdt_transport* tran
                                        const crdt_orswot_batch* mine, uint32_t n_actors, uint32_t flags,
                                        uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes, size_t* h_out_used,
                                        void* stream);
+/* crdt_replica_allreduce_max over a transport of the caller's (above; no
+ * communicator needed): rank j owns words [j n/N, (j+1) n/N) (the remainder
+ * spread over the first ranks); each rank sends every peer its range, folds
+ * the received copies of its own range with the dense max kernel, and sends
+ * the result to every peer — the same bits as the RCCL all-reduce on every
+ * rank (a pointwise max, src/vclock.rs:131-137). Uses the context's arena
+ * for (N - 1) / N of the rows; synchronous: returns when d_rows is complete. */
+int crdt_replica_allreduce_max_transport(crdt_ctx* ctx, const crdt_transport* transport, uint64_t* d_rows,
+                                         size_t n_words, void* stream);
 /* The same owner-sharded join over n_replicas (<= 64) replicas resident on
  * this context's device: each replica is a virtual rank (a host thread with
  * its own context and stream) and device copies are the transport; the code

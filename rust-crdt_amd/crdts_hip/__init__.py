@@ -685,6 +685,16 @@ class Engine:
               "orswot_replica_join_transport")
         return OrswotBatch(out.base, out.off, B.n_actors, max(16, used.value), B.flags)
 
+    def replica_allreduce_max_transport(self, rows, transport, stream=None):
+        """rows (a device int64 tensor read as u64) := its max over ranks, in
+        place, over a caller transport (crdt_replica_allreduce_max_transport:
+        owner-sharded reduce-scatter with the dense max kernel + all-gather;
+        `transport` has a `.c` TransportC, e.g. replica.GlooTransport)."""
+        check(lib.crdt_replica_allreduce_max_transport(self.ctx, C.byref(transport.c), C.c_void_p(rows.data_ptr()),
+                                                       rows.numel(), self._stream(stream)),
+              "replica_allreduce_max_transport")
+        return rows
+
     def orswot_replica_join_local(self, batches, stream=None):
         """The same owner-sharded join with every replica a virtual rank on this
         device (crdt_orswot_replica_join_local)."""

@@ -605,6 +605,53 @@ int crdt_replica_reduce_scatter_max(crdt_ctx* ctx, const uint64_t* d_rows, size_
                                    (ncclComm_t)ctx->comm, S(stream)));
 }
 
+// Dense rows over a caller transport (config 4 without RCCL): ring-free
+// owner-sharded all-reduce — rank j owns words [lo(j), lo(j+1)); every rank
+// sends each peer that peer's range (reduce-scatter), folds the R - 1
+// received copies of its own range with dense_max_kernel, then sends its range
+// to every peer (all-gather). Per rank 2(R - 1)/R of the rows sent and
+// received; the max is order-free, so the result is bit-identical to
+// ncclAllReduce(ncclMax) on every rank.
+int dense_allreduce_rank(crdt_ctx* ctx, Transport& T, uint64_t* d_rows, size_t n, hipStream_t st) {
+  const int R = T.R, me = T.me;
+  if (R == 1 || n == 0) return CRDT_OK;
+  auto lo = [&](int j) -> size_t { return (n / (size_t)R) * (size_t)j + std::min((size_t)j, n % (size_t)R); };
+  const size_t my0 = lo(me), myn = lo(me + 1) - my0;
+  int rc = ensure_arena(ctx, al256(8 * myn * (size_t)(R - 1)) + 256);
+  if (rc) return rc;
+  uint64_t* scratch = (uint64_t*)ctx->d_arena;
+  std::vector<Xfer> sends, recvs;
+  for (int p = 0, k = 0; p < R; ++p) {
+    if (p == me) continue;
+    sends.push_back(Xfer{p, d_rows + lo(p), nullptr, 8 * (lo(p + 1) - lo(p))});
+    recvs.push_back(Xfer{p, nullptr, scratch + (size_t)k * myn, 8 * myn});
+    ++k;
+  }
+  if ((rc = T.exchange(sends, recvs, st))) return rc;
+  for (int k = 0; k < R - 1 && !rc; ++k) rc = launch_dense_max(d_rows + my0, scratch + (size_t)k * myn, myn, st);
+  if (rc) return rc;
+  sends.clear();
+  recvs.clear();
+  for (int p = 0; p < R; ++p) {
+    if (p == me) continue;
+    sends.push_back(Xfer{p, d_rows + my0, nullptr, 8 * myn});
+    recvs.push_back(Xfer{p, nullptr, d_rows + lo(p), 8 * (lo(p + 1) - lo(p))});
+  }
+  if ((rc = T.exchange(sends, recvs, st))) return rc;
+  return hipStreamSynchronize(st) == hipSuccess ? CRDT_OK : CRDT_EHIP;  // the arena is free again
+}
+
+int crdt_replica_allreduce_max_transport(crdt_ctx* ctx, const crdt_transport* transport, uint64_t* d_rows,
+                                         size_t n_words, void* stream) {
+  if (!ctx || !transport || !transport->allgather || !transport->exchange || transport->n_ranks < 1 ||
+      transport->rank < 0 || transport->rank >= transport->n_ranks || (n_words && !d_rows))
+    return CRDT_EINVAL;
+  int rc = set_dev(ctx);
+  if (rc) return rc;
+  CallbackTransport T(transport);
+  return dense_allreduce_rank(ctx, T, d_rows, n_words, S(stream));
+}
+
 int crdt_orswot_replica_join_bound(crdt_ctx* ctx, const crdt_orswot_batch* mine, size_t* h_bound, void* stream) {
   if (!ctx || !ctx->comm || !mine || !h_bound) return CRDT_EINVAL;
   int rc = set_dev(ctx);

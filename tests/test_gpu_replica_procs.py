@@ -12,7 +12,9 @@ over RCCL. Checked: every rank ends with the oracle's rank-order fold
 ((r0 ⊔ r1) ⊔ r2) (src/orswot.rs:87-157, order fixed by :98-103 vs :132-138)
 byte for byte; a non-canonical record in the middle of a slice makes EVERY
 rank return the same error (none left in a collective), and the next join on
-the same contexts succeeds.
+the same contexts succeeds. Config 4's dense all-reduce (max) over the same
+transport (crdt_replica_allreduce_max_transport) equals the pointwise max of
+every rank's rows on every rank.
 """
 import os
 import socket
@@ -92,6 +94,21 @@ def _worker(rank, world, port, q):
     res["after_ok"] = replica.digest(out2) == res["dense_digest"]
     eng.status()  # nothing left latched
     res["calls"] = dict(T.calls)
+    # 5. config 4: dense u64 rows (VClock / GCounter rows) all-reduced (max) by
+    #    the product over the transport (crdt_replica_allreduce_max_transport);
+    #    a length no rank count divides, counters >= 2^63 and zeros
+    import torch
+
+    def rows_of(r):
+        g = np.random.default_rng(300 + r)
+        x = g.integers(0, np.iinfo(np.uint64).max, size=16 * 1000 + 7, dtype=np.uint64, endpoint=True)
+        x[g.random(x.shape) < 0.25] = 0
+        return x
+
+    exp = np.maximum.reduce([rows_of(r) for r in range(world)])
+    t = torch.from_numpy(rows_of(rank).view(np.int64).copy()).to("cuda:0")
+    eng.replica_allreduce_max_transport(t, T)
+    res["ar_ok"] = bool(np.array_equal(t.cpu().numpy().view(np.uint64), exp))
     q.put(res)
     dist.destroy_process_group()
 
@@ -139,3 +156,4 @@ def test_product_join_across_processes(world):
     assert len({r["bad_code"] for r in res}) == 1, [r["bad_code"] for r in res]
     for r in res:  # 2 exchanges per completed join; the failed one stops after the first
         assert r["calls"]["exchange"] == 2 + 2 + 1 + 2, r["calls"]
+        assert r["ar_ok"], f"rank {r['rank']}: the transport all-reduce differs from the pointwise max"
