@@ -70,6 +70,12 @@ int crdt_ctx_set_list_cap(crdt_ctx* ctx, uint32_t cap);
  * joins have made so far (crdt_orswot_replica_join*: 3 per call in the steady
  * state). A counter for callers that profile the join's per-step cost. */
 uint64_t crdt_ctx_host_syncs(const crdt_ctx* ctx);
+/* Largest device arena (bytes) the context may allocate for the replica
+ * exchanges (crdt_orswot_replica_join*, crdt_replica_allreduce_max_transport);
+ * 0 (the default) = no limit. A call whose arena would exceed it returns
+ * CRDT_ECAPACITY on every rank of the exchange (the verdict is all-gathered
+ * before any data moves), and the context keeps the arena it had. */
+int crdt_ctx_set_arena_limit(crdt_ctx* ctx, size_t max_bytes);
 
 /* ------------------------------------------------------------------------ *
  * Dense clocks and counters.
@@ -345,7 +351,9 @@ int crdt_replica_reduce_scatter_max(crdt_ctx* ctx, const uint64_t* d_rows, size_
  * record i at d_out + d_out_off[i], *h_out_used = its extent in bytes;
  * out_bytes >= crdt_orswot_replica_join_bound() suffices (the sum of every
  * rank's replica bytes, a collective). Synchronous: returns when the output
- * is complete on `stream`. */
+ * is complete on `stream`. A status an earlier launch on a rank's context
+ * latched and the caller has not read (crdt_ctx_status) is that rank's error
+ * in the join: every rank returns it, and the status is cleared. */
 int crdt_orswot_replica_join_bound(crdt_ctx* ctx, const crdt_orswot_batch* mine, size_t* h_bound, void* stream);
 int crdt_orswot_replica_join(crdt_ctx* ctx, const crdt_orswot_batch* mine, uint32_t n_actors, uint32_t flags,
                              uint8_t* d_out, uint64_t* d_out_off, size_t out_bytes, size_t* h_out_used,

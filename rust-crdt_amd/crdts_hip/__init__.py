@@ -625,6 +625,10 @@ class Engine:
               "replica_reduce_scatter_max")
         return out
 
+    def set_arena_limit(self, max_bytes):
+        """Largest replica-exchange arena the context may allocate (0: no limit; crdt_ctx_set_arena_limit)."""
+        check(lib.crdt_ctx_set_arena_limit(self.ctx, int(max_bytes)), "set_arena_limit")
+
     def host_syncs(self):
         """Host synchronisations the context's replica joins made so far (crdt_ctx_host_syncs)."""
         return int(lib.crdt_ctx_host_syncs(self.ctx))

@@ -71,7 +71,7 @@ EXPORTS = [
     "crdt_orswot_replica_join_bound", "crdt_orswot_replica_join", "crdt_orswot_replica_join_local",
     "crdt_comm_count", "crdt_orswot_replica_join_transport", "crdt_orswot_generate_replicas_subset",
     "crdt_dense_merge_host", "crdt_vclock_csr_merge", "crdt_gcounter_csr_merge", "crdt_pncounter_csr_merge",
-    "crdt_orswot_truncate", "crdt_ctx_host_syncs", "crdt_orswot_fold",
+    "crdt_orswot_truncate", "crdt_ctx_host_syncs", "crdt_orswot_fold", "crdt_ctx_set_arena_limit",
     "crdt_map_map_merge_scratch_bytes", "crdt_map_map_merge", "crdt_replica_allreduce_max_transport",
 ]
 
@@ -177,6 +177,7 @@ def _load():
         "crdt_ctx_set_blocks_per_cu": (I, [P, I]),
         "crdt_ctx_set_list_cap": (I, [P, U32]),
         "crdt_ctx_host_syncs": (U64, [P]),
+        "crdt_ctx_set_arena_limit": (I, [P, SZ]),
         "crdt_orswot_fold": (I, [P, BP, U32, U32, U32, P, P, SZ, P]),
         "crdt_ctx_set_variant": (I, [P, I]),
         "crdt_ctx_debug_read": (I, [P, P, SZ, P]),

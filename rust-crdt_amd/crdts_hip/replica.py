@@ -199,7 +199,11 @@ class GlooTransport:
     ABI's owner-sharded join (crdt_orswot_replica_join_transport) with every
     rank a process, RCCL not involved. Device data is staged through host
     memory (hipMemcpy), so this is a test / fallback transport — the product
-    multi-GPU path is RCCL (crdt_orswot_replica_join)."""
+    multi-GPU path is RCCL (crdt_orswot_replica_join). Any transport failure
+    (a torch.distributed error, a self transfer that does not pair up) ends
+    the process with exit code 70 instead of returning CRDT_ECOMM: its peers
+    may already have posted their side, and only a closed connection releases
+    them."""
 
     def __init__(self, group=None):
         import ctypes as C
@@ -250,8 +254,10 @@ class GlooTransport:
         os._exit(70)
 
     def _exchange(self, user, sends, ns, recvs, nr, stream):
-        # the local checks first: a mismatch found before any request is
-        # posted is returned as a failure (the C side reports CRDT_ECOMM)
+        # the local checks first. A mismatch ends the process as any other
+        # transport failure does (_abandon): the peers post their side of this
+        # exchange concurrently, so returning an error here would leave them
+        # waiting for transfers this rank never makes
         S = [sends[k] for k in range(ns)]
         Rv = [recvs[k] for k in range(nr)]
         me = self.rank

@@ -124,6 +124,12 @@ int crdt_ctx_status(crdt_ctx* ctx, void* stream) {
   return st;
 }
 
+int crdt_ctx_set_arena_limit(crdt_ctx* ctx, size_t max_bytes) {
+  if (!ctx) return CRDT_EINVAL;
+  ctx->arena_limit = max_bytes;
+  return CRDT_OK;
+}
+
 int crdt_ctx_set_list_cap(crdt_ctx* ctx, uint32_t cap) {
   if (!ctx || cap > kDefaultListCap) return CRDT_EINVAL;
   ctx->list_cap = cap;

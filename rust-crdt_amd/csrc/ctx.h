@@ -42,6 +42,7 @@ struct crdt_ctx {
   uint64_t* d_comm_stage = nullptr;  // device staging of the small all-gathers
   uint8_t* d_arena = nullptr;
   size_t arena_bytes = 0;
+  size_t arena_limit = 0;  // largest arena the context may allocate (0: no limit; crdt_ctx_set_arena_limit)
   // HBM scratch of the large-object paths (bincode ingest, apply), allocated
   // on first use
   uint8_t* d_big = nullptr;

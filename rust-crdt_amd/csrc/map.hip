@@ -58,6 +58,9 @@ constexpr uint32_t kMdStage = 128;
 // with O row tsrc[2t + 1] into R row t; kMpNone marks an absent side (an
 // empty map: merge(m, empty) = m for a canonical m), both absent: no task.
 constexpr uint64_t kMpNone = ~0ull;
+// a task the merge rejected (a latched CRDT_ENONCANON) marks its Tmp row so:
+// the truncation then neither reads the row's (unwritten) counts nor writes R
+constexpr uint32_t kMpRejected = ~0u;
 
 template <bool VS, int NS, bool G = false, int MINW = 7>
 __global__ __launch_bounds__(kMpW, MINW) void map_mvreg_merge_kernel(crdt_map_mvreg_slab S, crdt_map_mvreg_slab O,
@@ -90,7 +93,10 @@ __global__ __launch_bounds__(kMpW, MINW) void map_mvreg_merge_kernel(crdt_map_mv
     const uint32_t dS = hasS ? __builtin_amdgcn_readfirstlane(S.n_def[si]) : 0u;
     const uint32_t dO = hasO ? __builtin_amdgcn_readfirstlane(O.n_def[oi]) : 0u;
     if (nS > S.kcap || nO > O.kcap || dS > S.dcap || dO > O.dcap) {
-      if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
+      if (lane == 0u) {
+        atomicCAS(status, 0, CRDT_ENONCANON);
+        if (to_tmp) Tmp.n_keys[ri] = kMpRejected;  // map_mvreg_truncate_kernel skips the row
+      }
       continue;
     }
     // every value count within mcap and deferred set size within scap (the
@@ -106,7 +112,10 @@ __global__ __launch_bounds__(kMpW, MINW) void map_mvreg_merge_kernel(crdt_map_mv
     for (uint32_t k = lane + kMpW; k < nS; k += kMpW) bad = bad || S.mv_n[si * S.kcap + k] > S.mcap;
     for (uint32_t k = lane + kMpW; k < nO; k += kMpW) bad = bad || O.mv_n[oi * O.kcap + k] > O.mcap;
     if (__ballot(bad) != 0ull) {
-      if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
+      if (lane == 0u) {
+        atomicCAS(status, 0, CRDT_ENONCANON);
+        if (to_tmp) Tmp.n_keys[ri] = kMpRejected;
+      }
       continue;
     }
     // the map deferred sets (used entries) staged in LDS when they fit
@@ -336,8 +345,24 @@ __global__ __launch_bounds__(kMpW) void map_mvreg_truncate_kernel(crdt_map_mvreg
     if (tsrc[2 * t] == kMpNone && tsrc[2 * t + 1] == kMpNone) continue;
     const Row<NS> c = rowv<NS>(Tb, t, A, lane);
     if (!vany(c)) continue;  // (written to R by the merge)
-    strow<NS>(R.clock + t * A, vsub(rowv<NS>(Tmp.clock, t, A, lane), c), A, lane);
     const uint32_t nk = __builtin_amdgcn_readfirstlane(Tmp.n_keys[t]);
+    if (nk == kMpRejected) continue;  // the merge rejected the task (status latched there)
+    // every count this pass reads is bounded by the slabs it indexes (the
+    // merge never writes past them; a count past them is not its output)
+    const uint32_t kb = Tmp.kcap < R.kcap ? Tmp.kcap : R.kcap, mb = Tmp.mcap < R.mcap ? Tmp.mcap : R.mcap;
+    const uint32_t db0 = Tmp.dcap < R.dcap ? Tmp.dcap : R.dcap, db = db0 < kMpComb ? db0 : kMpComb;
+    const uint32_t sb = Tmp.scap < R.scap ? Tmp.scap : R.scap;
+    bool bad = nk > kb || __builtin_amdgcn_readfirstlane(Tmp.n_def[t]) > db;
+    for (uint32_t k = lane; k < (nk <= kb ? nk : 0u); k += kMpW) bad = bad || Tmp.mv_n[t * Tmp.kcap + k] > mb;
+    {
+      const uint32_t nd0 = __builtin_amdgcn_readfirstlane(Tmp.n_def[t]);
+      for (uint32_t d = lane; d < (nd0 <= db ? nd0 : 0u); d += kMpW) bad = bad || Tmp.dset_n[t * Tmp.dcap + d] > sb;
+    }
+    if (__ballot(bad) != 0ull) {
+      if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
+      continue;
+    }
+    strow<NS>(R.clock + t * A, vsub(rowv<NS>(Tmp.clock, t, A, lane), c), A, lane);
     uint32_t out = 0;
     for (uint32_t k = 0; k < nk; ++k) {
       const uint64_t ik = t * Tmp.kcap + k;

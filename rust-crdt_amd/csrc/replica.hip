@@ -296,6 +296,7 @@ struct ThreadTransport : Transport {
 // ---------------------------------------------------------------- per-rank join
 int ensure_arena(crdt_ctx* ctx, size_t bytes) {
   if (ctx->arena_bytes >= bytes) return CRDT_OK;
+  if (ctx->arena_limit && bytes > ctx->arena_limit) return CRDT_ECAPACITY;
   (void)hipFree(ctx->d_arena);
   ctx->d_arena = nullptr;
   ctx->arena_bytes = 0;
@@ -350,8 +351,10 @@ int orswot_join_rank_body(crdt_ctx* ctx, Transport& T, const crdt_orswot_batch* 
   const size_t W = 2 * (size_t)R + 4;
 
   // 1. my byte extents of every range + (n, error, want, arena capacity),
-  //    all-gathered straight from the device. A status latched by an earlier
-  //    launch on this context belongs to that launch: it is cleared here.
+  //    all-gathered straight from the device. A status an earlier launch on
+  //    this context latched and the caller has not read goes out as this
+  //    rank's error word (slice_bounds_kernel reads and clears it): every rank
+  //    fails this join with that code (include/crdts_hip.h).
   int err = ensure_arena(ctx, plan_head(R));
   if (!err && n && (!mine->base || !mine->off)) err = CRDT_EINVAL;
   if (err) {
@@ -614,11 +617,24 @@ int crdt_replica_reduce_scatter_max(crdt_ctx* ctx, const uint64_t* d_rows, size_
 // ncclAllReduce(ncclMax) on every rank.
 int dense_allreduce_rank(crdt_ctx* ctx, Transport& T, uint64_t* d_rows, size_t n, hipStream_t st) {
   const int R = T.R, me = T.me;
-  if (R == 1 || n == 0) return CRDT_OK;
+  if (R == 1) return CRDT_OK;
   auto lo = [&](int j) -> size_t { return (n / (size_t)R) * (size_t)j + std::min((size_t)j, n % (size_t)R); };
   const size_t my0 = lo(me), myn = lo(me + 1) - my0;
-  int rc = ensure_arena(ctx, al256(8 * myn * (size_t)(R - 1)) + 256);
-  if (rc) return rc;
+  // 0. every rank's (row count, arena verdict), all-gathered: every rank
+  //    takes the same decision before any data moves (a rank that left here
+  //    alone would leave its peers waiting in the exchange)
+  int rc = n ? ensure_arena(ctx, al256(8 * myn * (size_t)(R - 1)) + 256) : CRDT_OK;
+  {
+    uint64_t mine[2] = {(uint64_t)n, (uint64_t)-rc};
+    std::vector<uint64_t> G(2 * (size_t)R);
+    const int trc = T.allgather(mine, 2, G.data(), st);
+    if (trc) return trc;
+    for (int p = 0; p < R; ++p) {
+      if (G[2 * p] != n) return CRDT_EINVAL;  // the same row count on every rank
+      if (G[2 * p + 1]) return -(int)G[2 * p + 1];
+    }
+  }
+  if (n == 0) return CRDT_OK;
   uint64_t* scratch = (uint64_t*)ctx->d_arena;
   std::vector<Xfer> sends, recvs;
   for (int p = 0, k = 0; p < R; ++p) {
@@ -629,7 +645,16 @@ int dense_allreduce_rank(crdt_ctx* ctx, Transport& T, uint64_t* d_rows, size_t n
   }
   if ((rc = T.exchange(sends, recvs, st))) return rc;
   for (int k = 0; k < R - 1 && !rc; ++k) rc = launch_dense_max(d_rows + my0, scratch + (size_t)k * myn, myn, st);
-  if (rc) return rc;
+  // 1. the fold's launch verdict, all-gathered: no rank enters the all-gather
+  //    exchange while a peer has left with an error
+  {
+    uint64_t e = (uint64_t)-rc;
+    std::vector<uint64_t> E((size_t)R);
+    const int trc = T.allgather(&e, 1, E.data(), st);
+    if (trc) return trc;
+    for (int p = 0; p < R; ++p)
+      if (E[p]) return -(int)E[p];
+  }
   sends.clear();
   recvs.clear();
   for (int p = 0; p < R; ++p) {

@@ -116,3 +116,42 @@ def test_nested_map_limits(gpu):
     with pytest.raises(crdts_hip.CrdtError) as e:
         gpu.map_map_merge(S, S, 8, out=small)
     assert e.value.code == CRDT_EINVAL
+
+
+def test_nested_map_malformed_inner_under_truncation(gpu):
+    """A malformed nested map (n_keys past its kcap) in tasks whose merged
+    nested map is truncated afterwards: the task merge latches CRDT_ENONCANON
+    and marks the task's scratch row, so the truncation reads no count from
+    it and writes nothing for it (the scratch holds garbage counts from the
+    start); the well-formed objects of the batch still merge exactly."""
+    import crdts_hip
+    from crdts_hip._lib import CRDT_ENONCANON
+
+    A, n = 16, 200
+    rng = random.Random(5)
+    pool = list(range(A))
+    pairs = [nested_gen.pair(rng, pool) for _ in range(n)]
+    S = crdts_hip.MapMapSlab.alloc(n, A, inner_caps=INNER, **CAPS)
+    O = crdts_hip.MapMapSlab.alloc(n, A, inner_caps=INNER, **CAPS)
+    for i, (x, y) in enumerate(pairs):
+        map_slab.nested_map_to_row(x, S, i, A)
+        map_slab.nested_map_to_row(y, O, i, A)
+    gpu.map_map_merge(S.to("cuda"), O.to("cuda"), A)  # (allocates the engine's scratch)
+    bad_objs = [i for i in range(0, n, 3) if S.a["n_keys"][i] > 0]
+    kc = S.inner.kcap
+    for i in bad_objs:  # every used key slot's nested map claims kcap + 1 keys
+        for k in range(int(S.a["n_keys"][i])):
+            S.inner.a["n_keys"][i * S.kcap + k] = kc + 1
+    gpu._map_map_scratch.fill_(0x7F)  # garbage counts in the task scratch
+    R = gpu.map_map_merge(S.to("cuda"), O.to("cuda"), A, check_status=False)
+    with pytest.raises(crdts_hip.CrdtError) as e:
+        gpu.status()
+    assert e.value.code == CRDT_ENONCANON
+    R = R.host()
+    bad = set(bad_objs)
+    for i, (x, y) in enumerate(pairs):
+        if i in bad:
+            continue
+        exp = x.clone()
+        exp.merge(y)
+        assert map_slab.nested_map_from_row(R, i) == exp, f"pair {i}"

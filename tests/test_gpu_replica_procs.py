@@ -14,7 +14,9 @@ byte for byte; a non-canonical record in the middle of a slice makes EVERY
 rank return the same error (none left in a collective), and the next join on
 the same contexts succeeds. Config 4's dense all-reduce (max) over the same
 transport (crdt_replica_allreduce_max_transport) equals the pointwise max of
-every rank's rows on every rank.
+every rank's rows on every rank. One rank whose arena cannot grow
+(crdt_ctx_set_arena_limit) makes every rank of either exchange return
+CRDT_ECAPACITY before any data moves.
 """
 import os
 import socket
@@ -42,6 +44,9 @@ def _oracle_fold(oracle_ffi, reps, A, flags=0):
     for b, o in reps[1:]:
         acc = oracle_ffi.orswot_merge_batch(acc[0], acc[1], b, o, A, threads=4, flags=flags)
     return records.unpack_batch(*acc)
+
+
+CRDT_ECAPACITY, CRDT_ENONCANON = -4, -2  # include/crdts_hip.h
 
 
 def _worker(rank, world, port, q):
@@ -109,6 +114,45 @@ def _worker(rank, world, port, q):
     t = torch.from_numpy(rows_of(rank).view(np.int64).copy()).to("cuda:0")
     eng.replica_allreduce_max_transport(t, T)
     res["ar_ok"] = bool(np.array_equal(t.cpu().numpy().view(np.uint64), exp))
+    # 6. one rank's arena cannot grow (a fresh context with a 1 KB arena limit
+    #    on the last rank): every rank returns CRDT_ECAPACITY before any data
+    #    moves (the verdicts are all-gathered first; nobody waits in an
+    #    exchange), the rows are untouched, and the same contexts succeed once
+    #    the limit is lifted — for the dense all-reduce and the Orswot join
+    eng2 = crdts_hip.Engine(0)
+    if rank == world - 1:
+        eng2.set_arena_limit(1024)
+    t2 = torch.from_numpy(rows_of(rank).view(np.int64).copy()).to("cuda:0")
+    codes = []
+    for call in (lambda: eng2.replica_allreduce_max_transport(t2, T), lambda: eng2.orswot_replica_join_transport(B, T)):
+        try:
+            call()
+            codes.append(0)
+        except crdts_hip.CrdtError as e:
+            codes.append(e.code)
+    res["limit_codes"] = codes
+    res["limit_rows_kept"] = bool(np.array_equal(t2.cpu().numpy().view(np.uint64), rows_of(rank)))
+    eng2.set_arena_limit(0)
+    eng2.replica_allreduce_max_transport(t2, T)
+    res["limit_after_ok"] = bool(np.array_equal(t2.cpu().numpy().view(np.uint64), exp)) and \
+        replica.digest(eng2.orswot_replica_join_transport(B, T)) == res["dense_digest"]
+    eng2.status()
+    # 7. a status latched on rank 0's context by an earlier launch (a rejected
+    #    record, merged with check_status=False) and never read is that rank's
+    #    error in the next join: every rank returns it; the join after that
+    #    succeeds (the status was cleared)
+    if rank == 0:
+        bb = reps[0][0].copy()
+        o0 = int(reps[0][1][0])
+        bb[o0 + 4:o0 + 8] = np.frombuffer(np.uint32(17).tobytes(), np.uint8)
+        Bb = crdts_hip.OrswotBatch.from_host(bb, reps[0][1], 16)
+        eng2.orswot_merge(Bb, Bb, check_status=False)
+    try:
+        eng2.orswot_replica_join_transport(B, T)
+        res["latched_code"] = 0
+    except crdts_hip.CrdtError as e:
+        res["latched_code"] = e.code
+    res["latched_after_ok"] = replica.digest(eng2.orswot_replica_join_transport(B, T)) == res["dense_digest"]
     q.put(res)
     dist.destroy_process_group()
 
@@ -157,3 +201,8 @@ def test_product_join_across_processes(world):
     for r in res:  # 2 exchanges per completed join; the failed one stops after the first
         assert r["calls"]["exchange"] == 2 + 2 + 1 + 2, r["calls"]
         assert r["ar_ok"], f"rank {r['rank']}: the transport all-reduce differs from the pointwise max"
+        assert r["limit_codes"] == ([0, CRDT_ECAPACITY] if world == 1 else [CRDT_ECAPACITY, CRDT_ECAPACITY]), r["limit_codes"]
+        assert r["limit_rows_kept"] or world == 1
+        assert r["limit_after_ok"], f"rank {r['rank']}: the calls after the arena failure differ"
+        assert r["latched_code"] == CRDT_ENONCANON, r["latched_code"]
+        assert r["latched_after_ok"], f"rank {r['rank']}: the join after the latched status differs"

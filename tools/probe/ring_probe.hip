@@ -1,0 +1,200 @@
+// LDS-DMA ring skeleton (diagnostic, not product): the data flow of the
+// Orswot join with the record prefetch moved from registers to a per-wave
+// LDS ring filled by global_load_lds_dwordx4 and sized by the records' real
+// bytes, and NO join (a synthetic dependent chain of `spin` steps over the
+// slot stands in for it). Sizes come from the offset gaps (compact batches:
+// gap == record size), so no header line is read before the record itself.
+//   RB    ring bytes per wave (a pair is <= 4 KB, so RB >= 4096)
+//   DMAX  most objects in flight per wave (the one being consumed included)
+//   PACK  0: output record i at lo[i] + ro[i]; 1: back to back per chunk
+//   WPB   waves per block
+//   NT    non-temporal record loads
+// The output stands in with the self record (its size ~ the merged size).
+//   hipcc --offload-arch=gfx950 -O3 -shared -fPIC ring_probe.hip -o libring.so
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../rust-crdt_amd/csrc/sched.h"
+
+namespace {
+constexpr int kWave = 64;
+constexpr uint32_t kScr = 2560;  // the product's per-wave join scratch, reserved (unused here)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t lane_of(uint32_t v, uint32_t t) { return __builtin_amdgcn_readlane(v, t); }
+__device__ __forceinline__ uint64_t lane_of64(uint64_t v, uint32_t t) {
+  return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), t) << 32) | __builtin_amdgcn_readlane((uint32_t)v, t);
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// one 1 KB piece: lane i's 16 B from gsrc land at LDS byte m0 + 16 i
+template <bool NT>
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t m0) {
+  uint32_t keep;
+  if (NT)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(m0) : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(m0) : "memory");
+}
+
+// s_waitcnt vmcnt(n) for a run-time n (an immediate per case); n past the
+// table waits for 40 (an over-wait, never an under-wait)
+__device__ __forceinline__ void wait_vm(uint32_t n) {
+#define W(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+  switch (n) {
+    W(0) W(1) W(2) W(3) W(4) W(5) W(6) W(7) W(8) W(9) W(10) W(11) W(12) W(13) W(14) W(15) W(16) W(17) W(18) W(19)
+    W(20) W(21) W(22) W(23) W(24) W(25) W(26) W(27) W(28) W(29) W(30) W(31) W(32) W(33) W(34) W(35) W(36) W(37)
+    W(38) W(39)
+    default: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+  }
+#undef W
+}
+
+template <uint32_t RB, uint32_t DMAX, int PACK, uint32_t WPB, int MINW, bool NT>
+__global__ __launch_bounds__(kWave* WPB, MINW) void ring_kernel(const uint8_t* __restrict__ Lb,
+                                                                 const uint64_t* __restrict__ Loff, uint64_t Lbytes,
+                                                                 const uint8_t* __restrict__ Rb,
+                                                                 const uint64_t* __restrict__ Roff, uint64_t Rbytes,
+                                                                 uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff,
+                                                                 uint64_t n_obj, uint32_t* ctl, uint32_t* sinkp) {
+  static_assert(RB >= 4096u && RB % 16u == 0u, "a pair of 2 KB records fits");
+  __shared__ u32x4 lds[WPB][(RB + kScr) / 16];
+  const uint32_t lane = threadIdx.x & 63u, wave = uni(threadIdx.x / 64u);
+  const uint32_t ring = uni(lds_addr(lds[wave]));
+  const uint64_t wave_id = (uint64_t)blockIdx.x * WPB + wave, n_waves = (uint64_t)gridDim.x * WPB;
+  const uint32_t spin = sinkp[1];
+  uint32_t sink = 0u, vmops = 0u;  // vmops: vector-memory instructions this wave issued (mod 2^32)
+  crdts_hip::GuidedSplit<20u, 5u> gs(n_obj, wave_id, n_waves);
+  uint64_t cbase, cend;
+  while (gs.next(cbase, cend, ctl, lane)) {
+    const uint64_t obj = cbase + lane;
+    const bool valid = obj < cend;
+    uint64_t lo = 0, ro = 0, nlo = Lbytes, nro = Rbytes;
+    if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
+    if (valid && obj + 1u < n_obj) { nlo = Loff[obj + 1u]; nro = Roff[obj + 1u]; }
+    nlo = nlo < Lbytes ? nlo : Lbytes;
+    nro = nro < Rbytes ? nro : Rbytes;
+    const uint64_t gl = nlo > lo ? nlo - lo : 0u, gr = nro > ro ? nro - ro : 0u;
+    const bool ok = valid && gl >= 32u && gr >= 32u && gl <= 2048u && gr <= 2048u && (lo & 15u) == 0u && (ro & 15u) == 0u;
+    const uint32_t n16 = ok ? (uint32_t)(gl / 16u) | ((uint32_t)(gr / 16u) << 16) : 0u;
+    uint64_t toissue = __ballot(ok), tocons = toissue;
+    if (!tocons) continue;
+    uint64_t cur = lane_of64(lo, 0) + lane_of64(ro, 0);  // PACK: the next record's place
+    uint32_t head = 0u, tail = 0u, inflight = 0u;
+    uint32_t posv = 0u, markv = 0u;  // lane t: object t's ring slot, vmops after its last piece
+    while (tocons) {
+      // ---- issue: as many of the chunk's next objects as the ring takes
+      while (toissue && inflight < DMAX) {
+        const uint32_t u = (uint32_t)__builtin_ctzll(toissue);
+        const uint32_t nu = lane_of(n16, u), nl = nu & 0xFFFFu, nr = nu >> 16;
+        const uint32_t B = 16u * (nl + nr);
+        uint32_t pos;
+        if (inflight == 0u) {
+          pos = 0u;
+        } else if (head > tail) {  // live [tail, head)
+          if (head + B <= RB) pos = head;
+          else if (B <= tail) pos = 0u;
+          else break;
+        } else {  // wrapped: live [tail, end) + [0, head)
+          if (head + B <= tail) pos = head;
+          else break;
+        }
+        if (inflight == 0u) tail = pos;
+        head = pos + B;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the freed slot's LDS reads are done
+        const uint8_t* const ls = Lb + lane_of64(lo, u);
+        const uint8_t* const rs = Rb + lane_of64(ro, u);
+        const uint32_t base = ring + pos;
+        for (uint32_t k = 0; k < nl; k += 64u) {
+          if (k + lane < nl) glds16<NT>(ls + 16u * (k + lane), uni(base + 16u * k));
+          ++vmops;
+        }
+        for (uint32_t k = 0; k < nr; k += 64u) {
+          if (k + lane < nr) glds16<NT>(rs + 16u * (k + lane), uni(base + 16u * (nl + k)));
+          ++vmops;
+        }
+        posv = lane == u ? pos : posv;
+        markv = lane == u ? vmops : markv;
+        toissue &= toissue - 1u;
+        ++inflight;
+      }
+      // ---- consume the oldest object in flight
+      const uint32_t c = (uint32_t)__builtin_ctzll(tocons);
+      wait_vm(vmops - lane_of(markv, c));
+      const uint32_t nc = lane_of(n16, c), nl = nc & 0xFFFFu, nr = nc >> 16;
+      const uint32_t slot = ring + lane_of(posv, c);
+      {  // synthetic join: a dependent LDS read + VALU chain over the pair
+        const __attribute__((address_space(3))) uint32_t* s = (const __attribute__((address_space(3))) uint32_t*)(size_t)slot;
+        uint32_t h = s[lane] ^ s[4u * nl + lane];
+        for (uint32_t q = 0; q < spin; ++q) h = h * 0x9e3779b1u + (h >> 7);
+        sink += h;
+      }
+      // copy-out of the stand-in output (the self record): two 16-B stores per
+      // lane, clamped to its last piece
+      const uint64_t oo = PACK ? cur : lane_of64(lo, c) + lane_of64(ro, c);
+      cur += 16u * nl;
+      {
+        const uint32_t lastb = 16u * (nl - 1u);
+        const uint32_t b0 = 16u * lane, b1 = 16u * (lane + 64u);
+        const uint32_t o0 = b0 < lastb ? b0 : lastb, o1 = b1 < lastb ? b1 : lastb;
+        const u32x4 p0 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(slot + o0);
+        const u32x4 p1 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(slot + o1);
+        __builtin_nontemporal_store(p0, (u32x4*)(Ob + oo + o0));
+        __builtin_nontemporal_store(p1, (u32x4*)(Ob + oo + o1));
+        vmops += 2u;
+      }
+      if (lane == 0u) Ooff[cbase + c] = oo;
+      ++vmops;
+      tocons &= tocons - 1u;
+      --inflight;
+      if (inflight == 0u) {
+        head = tail = 0u;
+      } else {
+        tail = lane_of(posv, (uint32_t)__builtin_ctzll(tocons));
+      }
+    }
+  }
+  if (sink == 0x9e3779b9u) sinkp[0] = sink;
+}
+
+template <uint32_t RB, uint32_t DMAX, int PACK, uint32_t WPB, int MINW, bool NT>
+const void* kfn() { return (const void*)ring_kernel<RB, DMAX, PACK, WPB, MINW, NT>; }
+
+struct Var { int id; const void* fn; uint32_t wpb; };
+}  // namespace
+
+// variant ids: RB(KB) * 100 + DMAX * 10 + PACK (+ 10000: non-temporal loads, + 20000: 1-wave blocks)
+extern "C" int ring_launch(int variant, const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
+                           const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t n_obj,
+                           uint32_t* ctl, uint32_t* sink, void* stream) {
+  static const Var vars[] = {
+      {420, kfn<4096, 2, 0, 4, 6, false>(), 4},   {430, kfn<4096, 3, 0, 4, 6, false>(), 4},
+      {421, kfn<4096, 2, 1, 4, 6, false>(), 4},   {431, kfn<4096, 3, 1, 4, 6, false>(), 4},
+      {530, kfn<5120, 3, 0, 4, 5, false>(), 4},   {540, kfn<5120, 4, 0, 4, 5, false>(), 4},
+      {630, kfn<6656, 3, 0, 4, 4, false>(), 4},   {640, kfn<6656, 4, 0, 4, 4, false>(), 4},
+      {641, kfn<6656, 4, 1, 4, 4, false>(), 4},   {860, kfn<8704, 6, 0, 4, 3, false>(), 4},
+      {10430, kfn<4096, 3, 0, 4, 6, true>(), 4},  {10640, kfn<6656, 4, 0, 4, 4, true>(), 4},
+      {20630, kfn<6144, 3, 0, 1, 1, false>(), 1}, {20640, kfn<6144, 4, 0, 1, 1, false>(), 1},
+      {20540, kfn<5120, 4, 0, 1, 1, false>(), 1},
+  };
+  const Var* v = nullptr;
+  for (const Var& x : vars)
+    if (x.id == variant) v = &x;
+  if (!v) return -1;
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, v->fn, kWave * v->wpb, 0) != hipSuccess || occ < 1) return -3;
+  const uint64_t chunks = (n_obj + 63) / 64;
+  uint64_t blocks = 256ull * occ;
+  if (blocks > (chunks + v->wpb - 1) / v->wpb) blocks = (chunks + v->wpb - 1) / v->wpb;
+  if (hipMemsetAsync(ctl, 0, 16, (hipStream_t)stream) != hipSuccess) return -4;
+  void* args[] = {&Lb, &Loff, &Lbytes, &Rb, &Roff, &Rbytes, &Ob, &Ooff, &n_obj, &ctl, &sink};
+  return hipLaunchKernel(v->fn, dim3((uint32_t)blocks), dim3(kWave * v->wpb), args, 0, (hipStream_t)stream) ==
+                 hipSuccess
+             ? occ * (int)v->wpb
+             : -2;
+}
