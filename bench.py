@@ -565,27 +565,38 @@ def settle(args, stream, fn, world=1):
     of calls (a step may hold collectives)."""
     if args.settle_ms <= 0:
         return
+    # one probe call first: a step that alone outlasts the budget (the 64 GB
+    # all-reduce of config 4 at N = 8) settles nothing more by repetition
     t0 = time.perf_counter()
-    for _ in range(8):
-        fn()
+    fn()
     stream.synchronize()
-    per = max_over_ranks((time.perf_counter() - t0) / 8.0, world)
-    n = min(4096, max(0, int(args.settle_ms * 1e-3 / max(per, 1e-6)) - 8))
+    per = max_over_ranks(time.perf_counter() - t0, world)
+    probes = 1
+    if 8.0 * per < args.settle_ms * 1e-3:  # short steps: the per-call time over 8 calls
+        t1 = time.perf_counter()
+        for _ in range(7):
+            fn()
+        stream.synchronize()
+        per = max_over_ranks((time.perf_counter() - t1) / 7.0, world)
+        probes = 8
+    spent = time.perf_counter() - t0
+    n = min(4096, max(0, int((args.settle_ms * 1e-3 - spent) / max(per, 1e-6))))
     for k in range(n):
         fn()
         if k % 64 == 63:
             stream.synchronize()  # bounded queue depth
     stream.synchronize()
-    SETTLE.update({"ms": round((time.perf_counter() - t0) * 1e3, 1), "launches": 8 + n,
+    SETTLE.update({"ms": round((time.perf_counter() - t0) * 1e3, 1), "launches": probes + n,
                    "note": "untimed calls of the timed step before the W warmup steps (the clock ramp, DESIGN.md §9)"})
 
 
-def _timed_steps(args, world, stream, fn):
-    """settle + W warmup + K timed calls of fn(); returns (wall_s over ranks (max), mean event ms on `stream`)."""
-    import numpy as np
-    import torch
-
+def _timed_steps(args, world, stream, fn, on_settled=None):
+    """settle + W warmup + K timed calls of fn(); returns (wall_s over ranks (max), mean event ms on `stream`).
+    on_settled() runs between the settle phase and the warmup steps (counters
+    per warmup + timed step start there)."""
     settle(args, stream, fn, world)
+    if on_settled is not None:
+        on_settled()
     for _ in range(args.warmup):
         fn()
     ev = TimingEvents(args.steps)
@@ -689,9 +700,9 @@ def run_orswot_csr(args, rank, world, local, eng=None):
 
     final = step()
     eng.status(stream)
-    syncs0 = eng.host_syncs()
-    wall, ev_ms = _timed_steps(args, world, stream, step)
-    syncs_per_step = (eng.host_syncs() - syncs0) / float(args.warmup + args.steps)
+    syncs0 = {}
+    wall, ev_ms = _timed_steps(args, world, stream, step, on_settled=lambda: syncs0.update(n=eng.host_syncs()))
+    syncs_per_step = (eng.host_syncs() - syncs0["n"]) / float(args.warmup + args.steps)
     eng.status(stream)
     if world > 1:
         # self-check (outside the timed region): identical bytes on every rank,
@@ -821,7 +832,6 @@ def run_gcounter_ae(args, rank, world, local, eng=None):
     stream = torch.cuda.Stream(device=local)
     torch.cuda.synchronize()  # generated on torch's stream; the joins run on `stream`
     check = None
-    ae_eng = None if args.rehearse else eng  # rehearsal: the gloo path of replica.dense_reduce_scatter_max
     if world > 1:
         if not args.rehearse and not eng.has_comm:
             replica.init_comm(eng)  # the context's own RCCL communicator (crdt_comm_init)
@@ -843,7 +853,7 @@ def run_gcounter_ae(args, rank, world, local, eng=None):
                 eng.replica_allreduce_max_transport(flat_rows, T, stream=stream)
         else:
             def step():
-                replica.dense_allreduce_max(base, engine=ae_eng, stream=stream)
+                replica.dense_allreduce_max(base, engine=eng, stream=stream)
     else:
         other = base.clone()
         other[:, (mine_slot + 1) % A] += 1
@@ -886,8 +896,13 @@ def run_gcounter_ae(args, rank, world, local, eng=None):
         # the owner-shard variant: reduce-scatter(max),
         # each rank keeps its 1/N of the joined counters (crdt_replica_reduce_scatter_max)
         flat = base.reshape(-1)[: (base.numel() // world) * world]
-        _, rs_ms = _timed_steps(args, world, stream,
-                                lambda: replica.dense_reduce_scatter_max(flat, engine=ae_eng, stream=stream))
+        if args.rehearse:  # the product's reduce-scatter over the gloo transport
+            def rs_step():
+                return eng.replica_reduce_scatter_max_transport(flat, T, stream=stream)
+        else:
+            def rs_step():
+                return replica.dense_reduce_scatter_max(flat, engine=eng, stream=stream)
+        _, rs_ms = _timed_steps(args, world, stream, rs_step)
         res["comm"]["reduce_scatter"] = {"ms": rs_ms, "algbw_GBps": bytes_per_gpu / (rs_ms * 1e-3) / 1e9,
                                          "busbw_GBps": (world - 1) / world * bytes_per_gpu / (rs_ms * 1e-3) / 1e9}
     else:

@@ -71,7 +71,7 @@ int crdt_ctx_set_list_cap(crdt_ctx* ctx, uint32_t cap);
  * state). A counter for callers that profile the join's per-step cost. */
 uint64_t crdt_ctx_host_syncs(const crdt_ctx* ctx);
 /* Largest device arena (bytes) the context may allocate for the replica
- * exchanges (crdt_orswot_replica_join*, crdt_replica_allreduce_max_transport);
+ * exchanges (crdt_orswot_replica_join*, crdt_replica_*_max_transport);
  * 0 (the default) = no limit. A call whose arena would exceed it returns
  * CRDT_ECAPACITY on every rank of the exchange (the verdict is all-gathered
  * before any data moves), and the context keeps the arena it had. */
@@ -397,6 +397,13 @@ int crdt_orswot_replica_join_transport(crdt_ctx* ctx, const crdt_transport* tran
  * for (N - 1) / N of the rows; synchronous: returns when d_rows is complete. */
 int crdt_replica_allreduce_max_transport(crdt_ctx* ctx, const crdt_transport* transport, uint64_t* d_rows,
                                          size_t n_words, void* stream);
+/* crdt_replica_reduce_scatter_max over a caller transport: rank r receives in
+ * d_shard the max over ranks of words [r n/N, (r+1) n/N) of d_rows (n_words a
+ * multiple of N) — its own copy of the range maxed with the N - 1 copies its
+ * peers send it (the dense max kernel). Synchronous. */
+int crdt_replica_reduce_scatter_max_transport(crdt_ctx* ctx, const crdt_transport* transport,
+                                              const uint64_t* d_rows, size_t n_words, uint64_t* d_shard,
+                                              void* stream);
 /* The same owner-sharded join over n_replicas (<= 64) replicas resident on
  * this context's device: each replica is a virtual rank (a host thread with
  * its own context and stream) and device copies are the transport; the code

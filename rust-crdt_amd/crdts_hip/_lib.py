@@ -73,6 +73,7 @@ EXPORTS = [
     "crdt_dense_merge_host", "crdt_vclock_csr_merge", "crdt_gcounter_csr_merge", "crdt_pncounter_csr_merge",
     "crdt_orswot_truncate", "crdt_ctx_host_syncs", "crdt_orswot_fold", "crdt_ctx_set_arena_limit",
     "crdt_map_map_merge_scratch_bytes", "crdt_map_map_merge", "crdt_replica_allreduce_max_transport",
+    "crdt_replica_reduce_scatter_max_transport",
 ]
 
 CRDT_COMM_ID_BYTES = 128
@@ -241,6 +242,7 @@ def _load():
         "crdt_orswot_replica_join_transport": (I, [P, C.POINTER(TransportC), BP, U32, U32, P, P, SZ, C.POINTER(SZ),
                                                    P]),
         "crdt_replica_allreduce_max_transport": (I, [P, C.POINTER(TransportC), P, SZ, P]),
+        "crdt_replica_reduce_scatter_max_transport": (I, [P, C.POINTER(TransportC), P, SZ, P, P]),
     }
     for name, (res, args) in sig.items():
         if name in DIAG_SYMBOLS and not hasattr(L, name):

@@ -666,6 +666,56 @@ int dense_allreduce_rank(crdt_ctx* ctx, Transport& T, uint64_t* d_rows, size_t n
   return hipStreamSynchronize(st) == hipSuccess ? CRDT_OK : CRDT_EHIP;  // the arena is free again
 }
 
+// The owner-shard variant over a caller transport: the reduce-scatter half
+// of dense_allreduce_rank. Rank j's shard is words [j n/R, (j+1) n/R) (n a
+// multiple of R, as ncclReduceScatter): its own copy is the fold's start, the
+// R - 1 received copies are maxed into it.
+int dense_reduce_scatter_rank(crdt_ctx* ctx, Transport& T, const uint64_t* d_rows, size_t n, uint64_t* d_shard,
+                              hipStream_t st) {
+  const int R = T.R, me = T.me;
+  const size_t w = n / (size_t)R;
+  int rc = w && R > 1 ? ensure_arena(ctx, al256(8 * w * (size_t)(R - 1)) + 256) : CRDT_OK;
+  if (R > 1) {  // every rank's (word count, arena verdict) before any data moves
+    uint64_t mine[2] = {(uint64_t)n, (uint64_t)-rc};
+    std::vector<uint64_t> G(2 * (size_t)R);
+    const int trc = T.allgather(mine, 2, G.data(), st);
+    if (trc) return trc;
+    for (int p = 0; p < R; ++p) {
+      if (G[2 * p] != n) return CRDT_EINVAL;
+      if (G[2 * p + 1]) return -(int)G[2 * p + 1];
+    }
+  }
+  if (w == 0) return CRDT_OK;
+  if (hipMemcpyAsync(d_shard, d_rows + w * (size_t)me, 8 * w, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return CRDT_EHIP;
+  if (R == 1) return hipStreamSynchronize(st) == hipSuccess ? CRDT_OK : CRDT_EHIP;
+  uint64_t* scratch = (uint64_t*)ctx->d_arena;
+  std::vector<Xfer> sends, recvs;
+  for (int p = 0, k = 0; p < R; ++p) {
+    if (p == me) continue;
+    sends.push_back(Xfer{p, d_rows + w * (size_t)p, nullptr, 8 * w});
+    recvs.push_back(Xfer{p, nullptr, scratch + (size_t)k * w, 8 * w});
+    ++k;
+  }
+  if ((rc = T.exchange(sends, recvs, st))) return rc;
+  for (int k = 0; k < R - 1 && !rc; ++k) rc = launch_dense_max(d_shard, scratch + (size_t)k * w, w, st);
+  if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = CRDT_EHIP;  // the arena is free again
+  return rc;  // (no exchange follows: a local launch failure is this rank's alone)
+}
+
+int crdt_replica_reduce_scatter_max_transport(crdt_ctx* ctx, const crdt_transport* transport,
+                                              const uint64_t* d_rows, size_t n_words, uint64_t* d_shard,
+                                              void* stream) {
+  if (!ctx || !transport || !transport->allgather || !transport->exchange || transport->n_ranks < 1 ||
+      transport->rank < 0 || transport->rank >= transport->n_ranks || n_words % (size_t)transport->n_ranks ||
+      (n_words && (!d_rows || !d_shard)))
+    return CRDT_EINVAL;
+  int rc = set_dev(ctx);
+  if (rc) return rc;
+  CallbackTransport T(transport);
+  return dense_reduce_scatter_rank(ctx, T, d_rows, n_words, d_shard, S(stream));
+}
+
 int crdt_replica_allreduce_max_transport(crdt_ctx* ctx, const crdt_transport* transport, uint64_t* d_rows,
                                          size_t n_words, void* stream) {
   if (!ctx || !transport || !transport->allgather || !transport->exchange || transport->n_ranks < 1 ||

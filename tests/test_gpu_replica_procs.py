@@ -14,7 +14,8 @@ byte for byte; a non-canonical record in the middle of a slice makes EVERY
 rank return the same error (none left in a collective), and the next join on
 the same contexts succeeds. Config 4's dense all-reduce (max) over the same
 transport (crdt_replica_allreduce_max_transport) equals the pointwise max of
-every rank's rows on every rank. One rank whose arena cannot grow
+every rank's rows on every rank, and its owner-shard variant
+(crdt_replica_reduce_scatter_max_transport) each rank's slice of it. One rank whose arena cannot grow
 (crdt_ctx_set_arena_limit) makes every rank of either exchange return
 CRDT_ECAPACITY before any data moves.
 """
@@ -114,6 +115,12 @@ def _worker(rank, world, port, q):
     t = torch.from_numpy(rows_of(rank).view(np.int64).copy()).to("cuda:0")
     eng.replica_allreduce_max_transport(t, T)
     res["ar_ok"] = bool(np.array_equal(t.cpu().numpy().view(np.uint64), exp))
+    # 5b. the owner-shard variant over the same transport
+    #     (crdt_replica_reduce_scatter_max_transport): rank r's 1/N of the max
+    w = 6000 // world
+    rs = eng.replica_reduce_scatter_max_transport(
+        torch.from_numpy(rows_of(rank)[:6000].view(np.int64).copy()).to("cuda:0"), T)
+    res["rs_ok"] = bool(np.array_equal(rs.cpu().numpy().view(np.uint64), exp[rank * w:(rank + 1) * w]))
     # 6. one rank's arena cannot grow (a fresh context with a 1 KB arena limit
     #    on the last rank): every rank returns CRDT_ECAPACITY before any data
     #    moves (the verdicts are all-gathered first; nobody waits in an
@@ -201,6 +208,7 @@ def test_product_join_across_processes(world):
     for r in res:  # 2 exchanges per completed join; the failed one stops after the first
         assert r["calls"]["exchange"] == 2 + 2 + 1 + 2, r["calls"]
         assert r["ar_ok"], f"rank {r['rank']}: the transport all-reduce differs from the pointwise max"
+        assert r["rs_ok"], f"rank {r['rank']}: the transport reduce-scatter differs from its slice of the max"
         assert r["limit_codes"] == ([0, CRDT_ECAPACITY] if world == 1 else [CRDT_ECAPACITY, CRDT_ECAPACITY]), r["limit_codes"]
         assert r["limit_rows_kept"] or world == 1
         assert r["limit_after_ok"], f"rank {r['rank']}: the calls after the arena failure differ"
