@@ -1576,16 +1576,19 @@ def run_map_map(args, rank, world, local):
                            "traffic": wl_traffic(args, "map_map", "map_map_outer_kernel", "map_mvreg_merge_kernel",
                                                  "map_mvreg_truncate_kernel")}
         if not args.no_cpu_baseline:
-            mm = 2000
-            t0 = _t.perf_counter()
-            for x, y in pairs[:mm]:
-                z = x.clone()
-                z.merge(y)
-            secs = _t.perf_counter() - t0
-            res["cpu_baseline"] = {"value": mm / secs, "unit": "merges/s", "cores": 1, "kind": "port",
+            import oracle_ffi
+
+            th = cpu_threads(args)
+            mm = min(n, 200_000)  # the tiled host slabs: the same pairs the GPU merged
+            Ls, Rs = (crdts_hip.MapMapSlab({f: v[: mm * (v.shape[0] // n)] for f, v in S.a.items()}, S.kcap, S.dcap,
+                                           S.scap, crdts_hip.MapSlab({f: v[: mm * (v.shape[0] // n)]
+                                                                       for f, v in S.inner.a.items()}, *S.inner_caps))
+                      for S in (L, R))
+            secs = oracle_ffi.map_map_bench(Ls, Rs, A, th)
+            res["cpu_baseline"] = {"value": mm / secs, "unit": "merges/s", "cores": th, "kind": "port",
                                    **cpu_cores_note(),
-                                   "sample": f"{mm} nested map merges, the Python restatement (oracle/crdts_ref.py), "
-                                             "1 thread"}
+                                   "sample": f"{mm} nested map merges, the C++ restatement (oracle/ref_cpu.cpp "
+                                             f"MapT<MapT<MVRegO>>, std::map containers), {th} threads, decode untimed"}
     return res
 
 

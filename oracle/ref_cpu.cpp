@@ -547,23 +547,28 @@ struct MVRegO {
   }
 };
 
-// Map<u64, MVReg<u64, A>, A> (src/map.rs:82-98): merge :191-268, apply :162-188,
-// apply_rm :336-349, apply_deferred :323-333. std::map<VClock, ...> orders
+// Map<u64, V, A> (src/map.rs:82-98) over a value V with merge and
+// Causal::truncate: merge :191-268, apply :162-188, apply_rm :336-349,
+// apply_deferred :323-333, truncate :131-158. std::map<VClock, ...> orders
 // deferred clocks lexicographically over (actor, counter): CLOCK ORDER.
-struct MapEntry {
+// MapO = Map<u64, MVReg>; MapMapO = Map<u64, Map<u64, MVReg>> (the reference's
+// TestMap, test/map.rs:4-8).
+template <class V>
+struct MapEntryT {
   VClock clock;
-  MVRegO val;
+  V val;
 };
-struct MapO {
+template <class V>
+struct MapT {
   VClock clock;
-  std::map<uint64_t, MapEntry> entries;
+  std::map<uint64_t, MapEntryT<V>> entries;
   std::map<std::map<Actor, Counter>, std::set<uint64_t>> deferred;
 
   void apply_rm(uint64_t key, const VClock& c) {
     if (!c.le(clock)) deferred[c.dots].insert(key);
     auto it = entries.find(key);
     if (it != entries.end()) {
-      MapEntry e = it->second;
+      MapEntryT<V> e = it->second;
       entries.erase(it);
       e.clock.subtract(c);
       if (!e.clock.is_empty()) {
@@ -581,9 +586,9 @@ struct MapO {
       for (uint64_t k : kv.second) apply_rm(k, c);
     }
   }
-  void apply_up(Actor a, Counter ctr, uint64_t key, const VClock& put_clock, uint64_t val) {
+  void apply_up(Actor a, Counter ctr, uint64_t key, const VClock& put_clock, uint64_t val) {  // (V = MVRegO)
     if (clock.get(a) >= ctr) return;
-    MapEntry e;
+    MapEntryT<V> e;
     auto it = entries.find(key);
     if (it != entries.end()) { e = it->second; entries.erase(it); }
     e.clock.witness(a, ctr);
@@ -592,10 +597,34 @@ struct MapO {
     clock.witness(a, ctr);
     apply_deferred();
   }
-  void merge(const MapO& other) {
-    std::map<uint64_t, MapEntry> keep;
+  // Causal::truncate (:131-158): entry clocks lose `c` (emptied entries
+  // dropped, the rest truncate their value), deferred clocks lose it
+  // (emptied ones dropped; two that become equal: the later in CLOCK ORDER
+  // replaces the earlier, as the reference's HashMap insert), clock loses it
+  void truncate(const VClock& c) {
+    for (auto it = entries.begin(); it != entries.end();) {
+      it->second.clock.subtract(c);
+      if (it->second.clock.is_empty()) {
+        it = entries.erase(it);
+      } else {
+        it->second.val.truncate(c);
+        ++it;
+      }
+    }
+    std::map<std::map<Actor, Counter>, std::set<uint64_t>> d;
+    for (const auto& kv : deferred) {
+      VClock rc;
+      rc.dots = kv.first;
+      rc.subtract(c);
+      if (!rc.is_empty()) d[rc.dots] = kv.second;
+    }
+    deferred.swap(d);
+    clock.subtract(c);
+  }
+  void merge(const MapT& other) {
+    std::map<uint64_t, MapEntryT<V>> keep;
     for (const auto& kv : entries) {
-      MapEntry entry = kv.second;
+      MapEntryT<V> entry = kv.second;
       auto oit = other.entries.find(kv.first);
       if (oit == other.entries.end()) {
         entry.clock.subtract(other.clock);
@@ -606,7 +635,7 @@ struct MapO {
           keep[kv.first] = entry;
         }
       } else {
-        MapEntry oe = oit->second;
+        MapEntryT<V> oe = oit->second;
         VClock common = entry.clock.intersection(oe.clock);
         entry.clock.subtract(common);
         oe.clock.subtract(common);
@@ -627,7 +656,7 @@ struct MapO {
     }
     for (const auto& kv : other.entries) {
       if (entries.count(kv.first)) continue;
-      MapEntry entry = kv.second;
+      MapEntryT<V> entry = kv.second;
       entry.clock.subtract(clock);
       if (!entry.clock.is_empty()) {
         VClock del = clock;
@@ -646,6 +675,9 @@ struct MapO {
     apply_deferred();
   }
 };
+using MapEntry = MapEntryT<MVRegO>;
+using MapO = MapT<MVRegO>;
+using MapMapO = MapT<MapO>;
 }  // namespace oracle
 
 extern "C" {
@@ -1146,6 +1178,100 @@ int orc_map_mvreg_merge_batch(const crdt_map_mvreg_slab* s, const crdt_map_mvreg
     if (!map_to_slab(m, *out, i, A)) return -4;
   }
   return 0;
+}
+
+// ---------------------------------------------------------------- Map<u64, Map<u64, MVReg>>
+// The nested map's slab (include/crdts_hip.h crdt_map_map_slab): the outer
+// map's arrays, key slot k of object i's nested map as object i*kcap + k of
+// the inner Map<u64, MVReg> slab.
+static MapMapO mapmap_from_slab(const crdt_map_map_slab& S, size_t i, uint32_t A) {
+  MapMapO m;
+  m.clock = row_to_vclock(S.clock + i * A, A);
+  for (uint32_t k = 0; k < S.n_keys[i]; ++k) {
+    const size_t ki = i * S.kcap + k;
+    MapEntryT<MapO> e;
+    e.clock = row_to_vclock(S.eclock + ki * A, A);
+    e.val = map_from_slab(S.inner, ki, A);
+    m.entries[S.keys[ki]] = e;
+  }
+  for (uint32_t d = 0; d < S.n_def[i]; ++d) {
+    const size_t di = i * S.dcap + d;
+    auto& set = m.deferred[row_to_vclock(S.dclock + di * A, A).dots];
+    for (uint32_t j = 0; j < S.dset_n[di]; ++j) set.insert(S.dset[di * S.scap + j]);
+  }
+  return m;
+}
+
+static bool mapmap_to_slab(const MapMapO& m, const crdt_map_map_slab& S, size_t i, uint32_t A) {
+  if (m.entries.size() > S.kcap || m.deferred.size() > S.dcap) return false;
+  vclock_to_row(m.clock, S.clock + i * A, A);
+  S.n_keys[i] = (uint32_t)m.entries.size();
+  const MapO empty;
+  for (uint32_t z = 0; z < S.kcap; ++z) {  // every key slot (its nested map emptied)
+    const size_t ki = i * S.kcap + z;
+    S.keys[ki] = 0;
+    std::fill(S.eclock + ki * A, S.eclock + (ki + 1) * A, 0ull);
+    if (!map_to_slab(empty, S.inner, ki, A)) return false;
+  }
+  uint32_t k = 0;
+  for (const auto& kv : m.entries) {
+    const size_t ki = i * S.kcap + k++;
+    S.keys[ki] = kv.first;
+    vclock_to_row(kv.second.clock, S.eclock + ki * A, A);
+    if (!map_to_slab(kv.second.val, S.inner, ki, A)) return false;
+  }
+  S.n_def[i] = (uint32_t)m.deferred.size();
+  for (uint32_t z = 0; z < S.dcap; ++z) {
+    const size_t di = i * S.dcap + z;
+    S.dset_n[di] = 0;
+    std::fill(S.dclock + di * A, S.dclock + (di + 1) * A, 0ull);
+    std::fill(S.dset + di * S.scap, S.dset + (di + 1) * S.scap, 0ull);
+  }
+  uint32_t d = 0;
+  for (const auto& kv : m.deferred) {
+    const size_t di = i * S.dcap + d++;
+    if (kv.second.size() > S.scap) return false;
+    VClock c;
+    c.dots = kv.first;
+    vclock_to_row(c, S.dclock + di * A, A);
+    S.dset_n[di] = (uint32_t)kv.second.size();
+    uint32_t j = 0;
+    for (uint64_t key : kv.second) S.dset[di * S.scap + j++] = key;
+  }
+  return true;
+}
+
+// out[i] = self[i].merge(&other[i]) for nested maps; 0, or -4 past an output capacity.
+int orc_map_map_merge_batch(const crdt_map_map_slab* s, const crdt_map_map_slab* o, const crdt_map_map_slab* out,
+                            size_t n, uint32_t A) {
+  for (size_t i = 0; i < n; ++i) {
+    MapMapO m = mapmap_from_slab(*s, i, A);
+    m.merge(mapmap_from_slab(*o, i, A));
+    if (!mapmap_to_slab(m, *out, i, A)) return -4;
+  }
+  return 0;
+}
+
+// CPU baseline of the nested map merge: the n pairs decoded (untimed), then
+// self.merge(&other) for every pair over `threads` std::threads; seconds.
+double orc_map_map_bench(const crdt_map_map_slab* s, const crdt_map_map_slab* o, size_t n, uint32_t A,
+                         int threads) {
+  std::vector<MapMapO> L(n), R(n);
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) {
+      L[i] = mapmap_from_slab(*s, i, A);
+      R[i] = mapmap_from_slab(*o, i, A);
+    }
+  });
+  auto t0 = std::chrono::steady_clock::now();
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) L[i].merge(R[i]);
+  });
+  auto t1 = std::chrono::steady_clock::now();
+  volatile size_t sink = 0;
+  for (size_t i = 0; i < n; i += 97) sink += L[i].entries.size();
+  (void)sink;
+  return std::chrono::duration<double>(t1 - t0).count();
 }
 
 // Replica pairs by op simulation (the reference's quickcheck shape,

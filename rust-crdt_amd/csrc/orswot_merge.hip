@@ -2802,6 +2802,180 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
 
 
 // ======================================================================
+// Ring join kernel (round 5): orswot_join_kernel's join with the record
+// prefetch moved from registers into a per-wave LDS ring filled by LDS-DMA
+// (global_load_lds_dwordx4: 64 lanes x 16 B land at M0 + 16 lane, no VGPR
+// destination). A pair slot is the two records back to back, sized by their
+// real bytes (config 3: ~1.9 KB of the 4 KB the register stage reserved), so
+// the ring holds up to DMAX objects in flight without the 16 prefetch VGPRs.
+// The chunk step reads only the offsets: each record's length is its offset
+// gap (== its size in a compact batch; at most the 2 KB fast stage), and the
+// header is validated from the ring when the object is consumed, so no
+// header line is fetched twice. The wait for an object is a counted
+// `s_waitcnt vmcnt(N)`, N = the vector-memory instructions this wave issued
+// after the object's last piece (loads and stores retire in issue order on
+// vmcnt; an instruction left uncounted only makes the wait stricter).
+// ======================================================================
+// one LDS-DMA piece: lane i's 16 B at gsrc land at LDS byte address m0 + 16 i
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t m0) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(m0)
+               : "memory");
+}
+// s_waitcnt vmcnt(n) for a run-time n: one immediate per case; past the
+// table the wait is for 31 (stricter, never weaker)
+__device__ __forceinline__ void wait_vm(uint32_t n) {
+#define CRDT_W(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+  switch (n) {
+    CRDT_W(0) CRDT_W(1) CRDT_W(2) CRDT_W(3) CRDT_W(4) CRDT_W(5) CRDT_W(6) CRDT_W(7) CRDT_W(8) CRDT_W(9) CRDT_W(10)
+    CRDT_W(11) CRDT_W(12) CRDT_W(13) CRDT_W(14) CRDT_W(15) CRDT_W(16) CRDT_W(17) CRDT_W(18) CRDT_W(19) CRDT_W(20)
+    CRDT_W(21) CRDT_W(22) CRDT_W(23) CRDT_W(24) CRDT_W(25) CRDT_W(26) CRDT_W(27) CRDT_W(28) CRDT_W(29) CRDT_W(30)
+    default: asm volatile("s_waitcnt vmcnt(31)" ::: "memory"); break;
+  }
+#undef CRDT_W
+}
+// a record's 32-B header read from LDS by every lane (a broadcast), wave-uniform
+__device__ __forceinline__ void lds_header(uint32_t a, u32x4& h0, u32x4& h1) {
+  const u32x4 x = *(const __attribute__((address_space(3))) u32x4*)(size_t)a;
+  const u32x4 y = *(const __attribute__((address_space(3))) u32x4*)(size_t)(a + 16u);
+  h0 = u32x4{uni(x.x), uni(x.y), uni(x.z), uni(x.w)};
+  h1 = u32x4{uni(y.x), uni(y.y), uni(y.z), uni(y.w)};
+}
+
+template <int MINW, int AW, uint32_t RB, uint32_t DMAX>
+__global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_ring_kernel(
+    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
+    const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
+    uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
+    int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
+  static_assert(RB >= 2u * kFastStage && RB % 16u == 0u, "a pair of fast-stage records fits the ring");
+  __shared__ u32x4 ring_s[kWavesPerBlock][RB / 16];
+  __shared__ u32x4 scr_s[kWavesPerBlock][M3Lay<AW>::Bytes / 16];
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t wave = uni(threadIdx.x / kWave);
+  const uint32_t ring = uni(lds_addr(ring_s[wave]));
+  const uint32_t uX = uni(lds_addr(scr_s[wave]));
+  const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
+  uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
+  GuidedSplit<20u, 5u, 0u> gs(n_obj, wave_id, n_waves);
+  uint32_t vmops = 0u;  // vector-memory instructions this wave issued and counted (mod 2^32)
+  uint64_t cbase, cend;
+  while (gs.next(cbase, cend, &ctl[3], lane)) {
+    // ---- chunk step: lane k <-> object cbase + k; offsets only
+    const uint64_t obj = cbase + lane;
+    const bool valid = obj < cend;
+    uint64_t lo = 0, ro = 0, nlo = Lbytes, nro = Rbytes;
+    if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
+    if (valid && obj + 1u < n_obj) { nlo = Loff[obj + 1u]; nro = Roff[obj + 1u]; }  // same lines: coalesced
+    // offsets that can hold a header: the record's bytes up to the next
+    // offset (at most the fast stage) go to the ring; the header decides
+    const bool pre = valid && (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes && ro + kHdrBytes <= Rbytes;
+    const uint64_t el = nlo < Lbytes ? nlo : Lbytes, er = nro < Rbytes ? nro : Rbytes;
+    const uint64_t gl = el > lo + kHdrBytes ? el - lo : kHdrBytes, gr = er > ro + kHdrBytes ? er - ro : kHdrBytes;
+    const uint32_t n16 = pre ? (uint32_t)((gl < kFastStage ? gl : kFastStage) / 16u) |
+                                   ((uint32_t)((gr < kFastStage ? gr : kFastStage) / 16u) << 16)
+                             : 0u;
+    // offsets that cannot: not canonical (as orswot_join_kernel: valid && !ok)
+    if (valid && !pre) Ooff[obj] = lo + ro;
+    if (__ballot(valid && !pre) != 0ull && lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
+    uint64_t toissue = __ballot(pre), tocons = toissue;
+    uint32_t head = 0u, tail = 0u, inflight = 0u;
+    uint32_t posv = 0u, markv = 0u;  // lane t: object t's ring slot, vmops after its last piece
+    while (tocons) {
+      // ---- issue: the chunk's next objects, as many as the ring takes
+      while (toissue && inflight < DMAX) {
+        const uint32_t u = (uint32_t)__builtin_ctzll(toissue);
+        const uint32_t nu = lane_of(n16, u), nl = nu & 0xFFFFu, nr = nu >> 16;
+        const uint32_t B = 16u * (nl + nr);
+        uint32_t pos;
+        if (inflight == 0u) {
+          pos = 0u;
+        } else if (head > tail) {  // live slots [tail, head)
+          if (head + B <= RB) pos = head;
+          else if (B <= tail) pos = 0u;
+          else break;
+        } else {  // wrapped: live [tail, end) and [0, head)
+          if (head + B <= tail) pos = head;
+          else break;
+        }
+        if (inflight == 0u) tail = pos;
+        head = pos + B;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS accesses to a freed slot are done
+        const uint8_t* const ls = Lb + lane_of64(lo, u);
+        const uint8_t* const rs = Rb + lane_of64(ro, u);
+        const uint32_t base = ring + pos;
+        for (uint32_t k = 0; k < nl; k += kWave) {
+          if (k + lane < nl) glds16(ls + 16u * (k + lane), uni(base + 16u * k));
+          ++vmops;
+        }
+        for (uint32_t k = 0; k < nr; k += kWave) {
+          if (k + lane < nr) glds16(rs + 16u * (k + lane), uni(base + 16u * (nl + k)));
+          ++vmops;
+        }
+        posv = lane == u ? pos : posv;
+        markv = lane == u ? vmops : markv;
+        toissue &= toissue - 1u;
+        ++inflight;
+      }
+      // ---- consume the oldest object in flight
+      const uint32_t t = (uint32_t)__builtin_ctzll(tocons);
+      wait_vm(vmops - lane_of(markv, t));
+      const uint32_t nt = lane_of(n16, t), nl = nt & 0xFFFFu, nr = nt >> 16;
+      const uint32_t uL = ring + lane_of(posv, t), uR = uL + 16u * nl;
+      const uint64_t l0 = lane_of64(lo, t), r0 = lane_of64(ro, t);
+      const uint64_t nl0 = lane_of64(nlo, t), nr0 = lane_of64(nro, t);
+      u32x4 hl0, hl1, hr0, hr1;
+      lds_header(uL, hl0, hl1);
+      lds_header(uR, hr0, hr1);
+      // the chunk step's verdicts of orswot_join_kernel, from the ring's headers
+      bool ok = header_ok(hl0, hl1, l0, Lbytes, A) && header_ok(hr0, hr1, r0, Rbytes, A) &&
+                l0 + r0 + (uint64_t)hl0.x + hr0.x <= Obytes;
+      const bool placed = !ok || (nl0 >= l0 + hl0.x && nr0 >= r0 + hr0.x);
+      if (!placed && lane == 0u) atomicCAS(status, 0, CRDT_EINVAL);
+      ok = ok && placed;
+      if (!ok && placed && lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
+      const bool fits = ok && hl0.x <= 16u * nl && hr0.x <= 16u * nr && A <= (uint32_t)AW && hl0.z <= 64u &&
+                        hr0.z <= 64u && hl0.w <= 64u && hr0.w <= 64u;
+      const bool has_def = (hl1.x | hr1.x) != 0u;
+      const bool hd = fits && has_def && hl1.x <= 32u && hr1.x <= 32u;
+      const bool fast = fits && (!has_def || hd);
+      const uint64_t oo = l0 + r0;
+      bool fbu = ok && !fast;  // (the general kernel's)
+      if (fast) {
+        bool big = false;
+        uint32_t r;
+        if (hd) {
+          r = mask3_object<0xFFFFFFFFu, 0, true, 0, true, 0, true, 1, AW>(uL, uR, uX, Ob + oo, A, hl0.z, hl0.w, hr0.z,
+                                                                         hr0.w, lane, big);
+        } else {
+          r = mask3_object<0xFFFFFFFFu, 3, false, 0, true, 0, true, 1, AW>(uL, uR, uX, Ob + oo, A, hl0.z, hl0.w,
+                                                                          hr0.z, hr0.w, lane, big, sink);
+        }
+        fbu = big || r == kLeanFallback;
+        if (!hd) {
+          wave_sync();
+          copy_io<7>(uL, Ob + oo, fbu ? 1u : r, lane);  // the record assembled over its slot
+          vmops += 2u;
+        }
+      }
+      *(Ooff + cbase + t) = oo | (fbu ? kPending : 0ull);
+      ++vmops;
+      if (fbu && lane == 0u) {  // the general kernel joins it
+        const uint32_t e = atomicAdd(&ctl[0], 1u);
+        if (e < list_cap) list[e] = cbase + t;
+      }
+      tocons &= tocons - 1u;
+      if (--inflight == 0u) head = tail = 0u;
+      else tail = lane_of(posv, (uint32_t)__builtin_ctzll(tocons));
+    }
+  }
+}
+
+// ======================================================================
 // General path: objects the fast kernel flagged (records larger than its
 // stage, > 128 union positions, > 32 deferred clocks on a side). The fast
 // kernel appends them to a list; a small fixed grid of single-wave blocks
@@ -3240,6 +3414,45 @@ int launch_product_join(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
 }
 }  // namespace
 
+namespace {
+// The ring join launch (orswot_ring_kernel, then the general kernel), with
+// launch_join_passes' alternating control-word sets (no memset before it).
+template <int MINW, int AW, uint32_t RB, uint32_t DMAX>
+int launch_ring_join(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
+                     const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
+                     uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list, uint32_t list_cap,
+                     hipStream_t stream, int blocks_per_cu, JoinSeq* js) {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const void* fn = (const void*)orswot_ring_kernel<MINW, AW, RB, DMAX>;
+  static std::atomic<int> occ_cache{0};  // per instantiation
+  int occ = occ_cache.load(std::memory_order_relaxed);
+  if (occ == 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)
+      occ = 4;
+    occ_cache.store(occ, std::memory_order_relaxed);
+  }
+  const uint64_t chunks = (n_obj + kWave - 1) / kWave;
+  const uint64_t want = (chunks + kWavesPerBlock - 1) / kWavesPerBlock;
+  const uint64_t cap = (uint64_t)cus * (blocks_per_cu > 0 ? blocks_per_cu : occ);
+  const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
+  uint32_t* set = ctl + 4u + 4u * (js->seq & 1u);
+  uint32_t* const other = ctl + 4u + 4u * (~js->seq & 1u);
+  if (js->dirty && hipMemsetAsync(ctl + 4, 0, 8 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
+  js->dirty = true;  // until both kernels are launched
+  void* args[] = {&Lb, &Loff, &Lbytes, &Rb, &Roff, &Rbytes, &Ob, &Ooff, &Obytes, &n_obj, &n_actors, &status,
+                  &set, &list, &list_cap};
+  if (hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) != hipSuccess)
+    return CRDT_EHIP;
+  hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff, Ob,
+                     Ooff, n_obj, n_actors, set, list, list_cap, other);
+  if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
+  ++js->seq;
+  js->dirty = false;
+  return CRDT_OK;
+}
+}  // namespace
+
 int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                         const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff,
                         uint64_t Obytes, uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl,
@@ -3267,6 +3480,14 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
     return go(launch_product_join<5, 64>);
   return go(launch_product_join<6, 32>);
 #else
+  // r05: the LDS-DMA ring join (orswot_ring_kernel<MINW, AW, ring bytes, objects in flight>)
+  if (variant == 300) return go(launch_ring_join<6, 32, 4096, 2>);
+  if (variant == 301) return go(launch_ring_join<6, 32, 4096, 3>);
+  if (variant == 302) return go(launch_ring_join<5, 32, 5632, 3>);
+  if (variant == 303) return go(launch_ring_join<5, 32, 5632, 4>);
+  if (variant == 304) return go(launch_ring_join<4, 32, 7680, 4>);
+  if (variant == 305) return go(launch_ring_join<4, 32, 7680, 5>);
+  if (variant == 306) return go(launch_ring_join<3, 32, 11072, 6>);
   if (n_actors > 32u && (variant == 0 || variant == 265)) return go(launch_product_join<5, 64>);
   if (variant == 134) return go(launch_join_passes<6, true, true, true, true, 1>);  // timing only: no kill
   if (variant == 135) return go(launch_join_passes<6, true, true, true, true, 2>);  // timing only: no deferred block

@@ -101,6 +101,10 @@ def lib():
     L.orc_vclock_partial_cmp.argtypes = [U32P, U64P, C.c_uint32, U32P, U64P, C.c_uint32]
     L.orc_map_orswot_merge_batch.restype = C.c_int
     L.orc_map_orswot_merge_batch.argtypes = [P, P, P, C.c_size_t, C.c_uint32]
+    L.orc_map_map_merge_batch.restype = C.c_int
+    L.orc_map_map_merge_batch.argtypes = [P, P, P, C.c_size_t, C.c_uint32]
+    L.orc_map_map_bench.restype = C.c_double
+    L.orc_map_map_bench.argtypes = [P, P, C.c_size_t, C.c_uint32, C.c_int]
     L.orc_map_orswot_order_outcomes.restype = C.c_int
     L.orc_map_orswot_order_outcomes.argtypes = [P, P, C.c_size_t, C.c_uint32, C.c_int, P]
     L.orc_map_orswot_generate.restype = C.c_int
@@ -431,6 +435,26 @@ def map_orswot_merge(S, O, A, out_caps=None):
     if rc:
         raise ValueError(f"oracle map-orswot merge rc={rc}")
     return R
+
+
+def map_map_merge(S, O, A):
+    """Oracle (C++) Map<u64, Map<u64, MVReg>>::merge of host MapMapSlabs ->
+    output MapMapSlab (outer and inner capacities summed)."""
+    import crdts_hip
+
+    R = crdts_hip.MapMapSlab.alloc(S.n, A, S.kcap + O.kcap, S.dcap + O.dcap, S.scap + O.scap,
+                                   tuple(x + y for x, y in zip(S.inner_caps, O.inner_caps)))
+    s, o, r = S.cstruct(), O.cstruct(), R.cstruct()
+    rc = lib().orc_map_map_merge_batch(C.byref(s), C.byref(o), C.byref(r), S.n, A)
+    if rc:
+        raise ValueError(f"oracle nested map merge rc={rc}")
+    return R
+
+
+def map_map_bench(S, O, A, threads):
+    """Seconds for the C++ restatement's nested-map merge of the slabs' pairs (decode untimed)."""
+    s, o = S.cstruct(), O.cstruct()
+    return lib().orc_map_map_bench(C.byref(s), C.byref(o), S.n, A, threads)
 
 
 def map_orswot_order_outcomes(S, O, A, max_k=6):

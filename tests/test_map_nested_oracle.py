@@ -153,3 +153,35 @@ def test_prop_truncate_with_empty_vclock_is_nop():  # test/map.rs:715-727
         s = m.clone()
         m.truncate(crdts_ref.VClock())
         assert m == s
+
+
+@pytest.mark.parametrize("A,n", [(16, 250), (100, 60)])
+def test_cpp_nested_map_merge_equals_restatement(A, n):
+    """The C++ restatement's Map<u64, Map<u64, MVReg>>::merge (oracle/ref_cpu.cpp
+    MapT<MapT<MVRegO>>, the CPU baseline of bench.py --workload map_map) equals
+    the Python restatement's — the one these KATs pin — on op-simulated pairs,
+    both orientations."""
+    import random
+
+    import crdts_hip
+    import map_slab
+    import nested_gen
+    import oracle_ffi
+
+    rng = random.Random(A + n)
+    pool = list(range(A))
+    pairs = [nested_gen.pair(rng, pool) for _ in range(n)]
+    caps, inner = dict(kcap=4, dcap=8, scap=4), (4, 8, 8, 4)
+    S = crdts_hip.MapMapSlab.alloc(n, A, inner_caps=inner, **caps)
+    O = crdts_hip.MapMapSlab.alloc(n, A, inner_caps=inner, **caps)
+    for i, (x, y) in enumerate(pairs):
+        map_slab.nested_map_to_row(x, S, i, A)
+        map_slab.nested_map_to_row(y, O, i, A)
+    assert S.inner.a["n_def"].sum() > 0 and S.a["n_def"].sum() > 0
+    for X, Y, flip in ((S, O, False), (O, S, True)):
+        R = oracle_ffi.map_map_merge(X, Y, A)
+        for i, (x, y) in enumerate(pairs):
+            a, b = (y, x) if flip else (x, y)
+            exp = a.clone()
+            exp.merge(b)
+            assert map_slab.nested_map_from_row(R, i) == exp, f"pair {i}"
