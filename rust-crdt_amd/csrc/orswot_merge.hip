@@ -2824,16 +2824,24 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t m0) {
                : "v"(gsrc), "s"(m0)
                : "memory");
 }
-// s_waitcnt vmcnt(n) for a run-time n: one immediate per case; past the
-// table the wait is for 31 (stricter, never weaker)
+// s_waitcnt vmcnt(n) for a run-time n. Past T the wait is for T (stricter,
+// never weaker): in the steady state the oldest instructions issued after an
+// object's last piece are the copy-out stores of two objects earlier, long
+// retired, so vmcnt(T) costs nothing over the exact count; the exact table
+// (a short branch tree) serves the chunk's first and last objects.
+template <uint32_t T>
 __device__ __forceinline__ void wait_vm(uint32_t n) {
+  static_assert(T <= 15u, "the exact table covers 0..15");
+  if (n >= T) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T) : "memory");
+    return;
+  }
 #define CRDT_W(k) \
   case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
   switch (n) {
     CRDT_W(0) CRDT_W(1) CRDT_W(2) CRDT_W(3) CRDT_W(4) CRDT_W(5) CRDT_W(6) CRDT_W(7) CRDT_W(8) CRDT_W(9) CRDT_W(10)
-    CRDT_W(11) CRDT_W(12) CRDT_W(13) CRDT_W(14) CRDT_W(15) CRDT_W(16) CRDT_W(17) CRDT_W(18) CRDT_W(19) CRDT_W(20)
-    CRDT_W(21) CRDT_W(22) CRDT_W(23) CRDT_W(24) CRDT_W(25) CRDT_W(26) CRDT_W(27) CRDT_W(28) CRDT_W(29) CRDT_W(30)
-    default: asm volatile("s_waitcnt vmcnt(31)" ::: "memory"); break;
+    CRDT_W(11) CRDT_W(12) CRDT_W(13) CRDT_W(14)
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
   }
 #undef CRDT_W
 }
@@ -2844,14 +2852,34 @@ __device__ __forceinline__ void lds_header(uint32_t a, u32x4& h0, u32x4& h1) {
   h0 = u32x4{uni(x.x), uni(x.y), uni(x.z), uni(x.w)};
   h1 = u32x4{uni(y.x), uni(y.y), uni(y.z), uni(y.w)};
 }
+// The fast path's header test in 32-bit arithmetic (every count bounded
+// first, so record_size64's formula cannot overflow): the width is the
+// batch's, flags clear, deferred fields consistent, the counts within the
+// mask join's limits, and the size matches the counts. Implies header_ok for
+// a record whose offset passed the chunk step and whose size fits the bytes
+// loaded for it (the offset gap).
+template <int AW>
+__device__ __forceinline__ bool fast_header(u32x4 h0, u32x4 h1, uint32_t A) {
+  const bool bnd = h0.y == A && h1.w == 0u && h0.z <= 64u && h0.w <= 64u && h1.x <= 32u && h1.y <= 4096u &&
+                   h1.z <= 4096u && (h1.x != 0u || (h1.y | h1.z) == 0u) && A <= (uint32_t)AW;
+  uint32_t b = ((kHdrBytes + 8u * A + 12u * (h0.z + h0.w)) + 7u) & ~7u;
+  b = (b + 12u * h1.y + 8u * h1.z + 8u * h1.x + 15u) & ~15u;
+  return bnd && b == h0.x;
+}
 
-template <int MINW, int AW, uint32_t RB, uint32_t DMAX>
+// HABL (timing only, -DCRDT_DIAG builds): 4 no join, the self record copied
+// out as the output; 7 as 4 after the header verdicts
+template <int MINW, int AW, uint32_t RB, uint32_t DMAX, int HABL = 0>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_ring_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
     uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
     int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
   static_assert(RB >= 2u * kFastStage && RB % 16u == 0u, "a pair of fast-stage records fits the ring");
+#ifndef CRDT_DIAG
+  static_assert(HABL == 0, "timing-only ablations exist in -DCRDT_DIAG builds only");
+#endif
+  constexpr uint32_t kVmT = 4u * (DMAX - 1u) < 15u ? 4u * (DMAX - 1u) : 15u;  // steady state: 2 pieces + 2 stores per object
   __shared__ u32x4 ring_s[kWavesPerBlock][RB / 16];
   __shared__ u32x4 scr_s[kWavesPerBlock][M3Lay<AW>::Bytes / 16];
   const uint32_t lane = threadIdx.x & (kWave - 1);
@@ -2861,6 +2889,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_ring_kern
   const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
   const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
   uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
+  // whole 128-B output lines (see the copy-out) only where the output base is 16-B aligned
+  const bool lines = ((uint64_t)Ob & 15u) == 0u;
   GuidedSplit<20u, 5u, 0u> gs(n_obj, wave_id, n_waves);
   uint32_t vmops = 0u;  // vector-memory instructions this wave issued and counted (mod 2^32)
   uint64_t cbase, cend;
@@ -2868,23 +2898,26 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_ring_kern
     // ---- chunk step: lane k <-> object cbase + k; offsets only
     const uint64_t obj = cbase + lane;
     const bool valid = obj < cend;
-    uint64_t lo = 0, ro = 0, nlo = Lbytes, nro = Rbytes;
+    uint64_t lo = 0, ro = 0, el = Lbytes, er = Rbytes;
     if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
-    if (valid && obj + 1u < n_obj) { nlo = Loff[obj + 1u]; nro = Roff[obj + 1u]; }  // same lines: coalesced
+    if (valid && obj + 1u < n_obj) { el = Loff[obj + 1u]; er = Roff[obj + 1u]; }  // same lines: coalesced
     // offsets that can hold a header: the record's bytes up to the next
     // offset (at most the fast stage) go to the ring; the header decides
     const bool pre = valid && (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes && ro + kHdrBytes <= Rbytes;
-    const uint64_t el = nlo < Lbytes ? nlo : Lbytes, er = nro < Rbytes ? nro : Rbytes;
+    el = el < Lbytes ? el : Lbytes;
+    er = er < Rbytes ? er : Rbytes;
     const uint64_t gl = el > lo + kHdrBytes ? el - lo : kHdrBytes, gr = er > ro + kHdrBytes ? er - ro : kHdrBytes;
     const uint32_t n16 = pre ? (uint32_t)((gl < kFastStage ? gl : kFastStage) / 16u) |
                                    ((uint32_t)((gr < kFastStage ? gr : kFastStage) / 16u) << 16)
                              : 0u;
     // offsets that cannot: not canonical (as orswot_join_kernel: valid && !ok)
-    if (valid && !pre) Ooff[obj] = lo + ro;
     if (__ballot(valid && !pre) != 0ull && lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
+    uint64_t oov = lo + ro;  // lane t: object t's output offset and flag, stored once per chunk (coalesced)
     uint64_t toissue = __ballot(pre), tocons = toissue;
     uint32_t head = 0u, tail = 0u, inflight = 0u;
     uint32_t posv = 0u, markv = 0u;  // lane t: object t's ring slot, vmops after its last piece
+    uint32_t prev_t = kWave;         // the last object whose record end in the output is known, and that end
+    uint64_t prev_end = 0u;
     while (tocons) {
       // ---- issue: the chunk's next objects, as many as the ring takes
       while (toissue && inflight < DMAX) {
@@ -2923,47 +2956,91 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_ring_kern
       }
       // ---- consume the oldest object in flight
       const uint32_t t = (uint32_t)__builtin_ctzll(tocons);
-      wait_vm(vmops - lane_of(markv, t));
+      wait_vm<kVmT>(vmops - lane_of(markv, t));
       const uint32_t nt = lane_of(n16, t), nl = nt & 0xFFFFu, nr = nt >> 16;
       const uint32_t uL = ring + lane_of(posv, t), uR = uL + 16u * nl;
       const uint64_t l0 = lane_of64(lo, t), r0 = lane_of64(ro, t);
-      const uint64_t nl0 = lane_of64(nlo, t), nr0 = lane_of64(nro, t);
-      u32x4 hl0, hl1, hr0, hr1;
-      lds_header(uL, hl0, hl1);
-      lds_header(uR, hr0, hr1);
-      // the chunk step's verdicts of orswot_join_kernel, from the ring's headers
-      bool ok = header_ok(hl0, hl1, l0, Lbytes, A) && header_ok(hr0, hr1, r0, Rbytes, A) &&
-                l0 + r0 + (uint64_t)hl0.x + hr0.x <= Obytes;
-      const bool placed = !ok || (nl0 >= l0 + hl0.x && nr0 >= r0 + hr0.x);
-      if (!placed && lane == 0u) atomicCAS(status, 0, CRDT_EINVAL);
-      ok = ok && placed;
-      if (!ok && placed && lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
-      const bool fits = ok && hl0.x <= 16u * nl && hr0.x <= 16u * nr && A <= (uint32_t)AW && hl0.z <= 64u &&
-                        hr0.z <= 64u && hl0.w <= 64u && hr0.w <= 64u;
-      const bool has_def = (hl1.x | hr1.x) != 0u;
-      const bool hd = fits && has_def && hl1.x <= 32u && hr1.x <= 32u;
-      const bool fast = fits && (!has_def || hd);
       const uint64_t oo = l0 + r0;
-      bool fbu = ok && !fast;  // (the general kernel's)
-      if (fast) {
-        bool big = false;
-        uint32_t r;
-        if (hd) {
-          r = mask3_object<0xFFFFFFFFu, 0, true, 0, true, 0, true, 1, AW>(uL, uR, uX, Ob + oo, A, hl0.z, hl0.w, hr0.z,
-                                                                         hr0.w, lane, big);
-        } else {
-          r = mask3_object<0xFFFFFFFFu, 3, false, 0, true, 0, true, 1, AW>(uL, uR, uX, Ob + oo, A, hl0.z, hl0.w,
-                                                                          hr0.z, hr0.w, lane, big, sink);
+      bool fast = false, hd = false, fbu = false;
+      uint32_t szl = 0u, szr = 0u, r = 0u;
+#ifdef CRDT_DIAG
+      if (HABL == 4) {  // (no header read either)
+        copy_io<7>(uL, Ob + oo, nl, lane);
+        vmops += 2u;
+      } else
+#endif
+      {
+        u32x4 hl0, hl1, hr0, hr1;
+        lds_header(uL, hl0, hl1);
+        lds_header(uR, hr0, hr1);
+        szl = hl0.x;
+        szr = hr0.x;
+        // the common case in 32-bit arithmetic: both headers pass the fast
+        // path's bounds and size test, and both records fit the bytes loaded
+        // (so they lie in their buffers and before the next offsets)
+        fast = fast_header<AW>(hl0, hl1, A) && fast_header<AW>(hr0, hr1, A) && szl <= 16u * nl && szr <= 16u * nr &&
+               oo + szl + szr <= Obytes;
+        if (!fast) {  // orswot_join_kernel's chunk-step verdicts, from the ring's headers
+          // (the next offsets again, wave-uniform loads: not kept in VGPRs for this rare path)
+          const uint64_t oi = cbase + t;
+          const uint64_t nl0 = oi + 1u < n_obj ? Loff[oi + 1u] : Lbytes, nr0 = oi + 1u < n_obj ? Roff[oi + 1u] : Rbytes;
+          bool ok = header_ok(hl0, hl1, l0, Lbytes, A) && header_ok(hr0, hr1, r0, Rbytes, A) &&
+                    oo + (uint64_t)szl + szr <= Obytes;
+          const bool placed = !ok || (nl0 >= l0 + szl && nr0 >= r0 + szr);
+          if (!placed && lane == 0u) atomicCAS(status, 0, CRDT_EINVAL);
+          ok = ok && placed;
+          if (!ok && placed && lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
+          const bool fits = ok && szl <= 16u * nl && szr <= 16u * nr && A <= (uint32_t)AW && hl0.z <= 64u &&
+                            hr0.z <= 64u && hl0.w <= 64u && hr0.w <= 64u;
+          fast = fits && ((hl1.x | hr1.x) == 0u || (hl1.x <= 32u && hr1.x <= 32u));
+          fbu = ok && !fast;  // (the general kernel's)
         }
-        fbu = big || r == kLeanFallback;
-        if (!hd) {
-          wave_sync();
-          copy_io<7>(uL, Ob + oo, fbu ? 1u : r, lane);  // the record assembled over its slot
-          vmops += 2u;
+        hd = fast && (hl1.x | hr1.x) != 0u;
+#ifdef CRDT_DIAG
+        if (HABL == 7) {
+          if (fast) {
+            copy_io<7>(uL, Ob + oo, nl, lane);
+            vmops += 2u;
+          }
+        } else
+#endif
+        if (fast) {
+          bool big = false;
+          if (hd) {
+            r = mask3_object<0xFFFFFFFFu, 0, true, 0, true, 0, true, 1, AW>(uL, uR, uX, Ob + oo, A, hl0.z, hl0.w, hr0.z,
+                                                                           hr0.w, lane, big);
+          } else {
+            r = mask3_object<0xFFFFFFFFu, 3, false, 0, true, 0, true, 1, AW>(uL, uR, uX, Ob + oo, A, hl0.z, hl0.w,
+                                                                            hr0.z, hr0.w, lane, big, sink);
+          }
+          fbu = big || r == kLeanFallback;
+          if (!hd) {
+            // The record assembled over its slot goes out with two 16-B stores
+            // per lane, widened to whole 128-B lines where that stays in bytes
+            // no record owns: the tail within this object's own slot (record
+            // i's slot is [off_i, off_i + |self_i| + |other_i|); a merged
+            // record is always shorter by at least a header and a clock), the
+            // head only after the previous object's record, when this wave
+            // wrote it and knows where it ends. A partial line would cost the
+            // memory side a read-modify-write.
+            uint64_t w0 = oo, w1 = oo + 16u * (fbu ? 1u : r);
+            if (lines && !fbu) {
+              const uint64_t e = (w1 + 127u) & ~127ull;
+              if (e <= oo + szl + szr) w1 = e;
+              const uint64_t h = oo & ~127ull;
+              if (prev_t + 1u == t && h >= prev_end && w1 - h <= 2u * 16u * kWave) w0 = h;
+            }
+            wave_sync();
+            copy_io<7>(uL - (uint32_t)(oo - w0), Ob + w0, (uint32_t)(w1 - w0) / 16u, lane);
+            vmops += 2u;
+          }
         }
       }
-      *(Ooff + cbase + t) = oo | (fbu ? kPending : 0ull);
-      ++vmops;
+      if (fast && !fbu) {
+        prev_t = t;
+        prev_end = oo + 16u * r;
+      }
+      oov = lane == t ? oo | (fbu ? kPending : 0ull) : oov;
       if (fbu && lane == 0u) {  // the general kernel joins it
         const uint32_t e = atomicAdd(&ctl[0], 1u);
         if (e < list_cap) list[e] = cbase + t;
@@ -2972,6 +3049,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_ring_kern
       if (--inflight == 0u) head = tail = 0u;
       else tail = lane_of(posv, (uint32_t)__builtin_ctzll(tocons));
     }
+    if (valid) Ooff[obj] = oov;  // every object of the chunk, one coalesced store
   }
 }
 
@@ -3417,14 +3495,14 @@ int launch_product_join(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
 namespace {
 // The ring join launch (orswot_ring_kernel, then the general kernel), with
 // launch_join_passes' alternating control-word sets (no memset before it).
-template <int MINW, int AW, uint32_t RB, uint32_t DMAX>
+template <int MINW, int AW, uint32_t RB, uint32_t DMAX, int HABL = 0>
 int launch_ring_join(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                      const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
                      uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list, uint32_t list_cap,
                      hipStream_t stream, int blocks_per_cu, JoinSeq* js) {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const void* fn = (const void*)orswot_ring_kernel<MINW, AW, RB, DMAX>;
+  const void* fn = (const void*)orswot_ring_kernel<MINW, AW, RB, DMAX, HABL>;
   static std::atomic<int> occ_cache{0};  // per instantiation
   int occ = occ_cache.load(std::memory_order_relaxed);
   if (occ == 0) {
@@ -3488,6 +3566,8 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   if (variant == 304) return go(launch_ring_join<4, 32, 7680, 4>);
   if (variant == 305) return go(launch_ring_join<4, 32, 7680, 5>);
   if (variant == 306) return go(launch_ring_join<3, 32, 11072, 6>);
+  if (variant == 307) return go(launch_ring_join<6, 32, 4096, 3, 4>);  // timing only: no join
+  if (variant == 308) return go(launch_ring_join<6, 32, 4096, 3, 7>);  // timing only: header verdicts, no join
   if (n_actors > 32u && (variant == 0 || variant == 265)) return go(launch_product_join<5, 64>);
   if (variant == 134) return go(launch_join_passes<6, true, true, true, true, 1>);  // timing only: no kill
   if (variant == 135) return go(launch_join_passes<6, true, true, true, true, 2>);  // timing only: no deferred block

@@ -55,7 +55,11 @@ __device__ __forceinline__ void wait_vm(uint32_t n) {
 #undef W
 }
 
-template <uint32_t RB, uint32_t DMAX, int PACK, uint32_t WPB, int MINW, bool NT>
+// IL > 0: interleaved schedule instead of the guided split — groups of IL
+// consecutive objects dealt round-robin to the waves (group g to wave
+// g mod n_waves), 64 / IL groups per chunk, so that at any time every wave
+// works inside one compact window of the batch (DRAM row locality)
+template <uint32_t RB, uint32_t DMAX, int PACK, uint32_t WPB, int MINW, bool NT, int OUTM = 0, uint32_t IL = 0>
 __global__ __launch_bounds__(kWave* WPB, MINW) void ring_kernel(const uint8_t* __restrict__ Lb,
                                                                  const uint64_t* __restrict__ Loff, uint64_t Lbytes,
                                                                  const uint8_t* __restrict__ Rb,
@@ -70,10 +74,21 @@ __global__ __launch_bounds__(kWave* WPB, MINW) void ring_kernel(const uint8_t* _
   const uint32_t spin = sinkp[1];
   uint32_t sink = 0u, vmops = 0u;  // vmops: vector-memory instructions this wave issued (mod 2^32)
   crdts_hip::GuidedSplit<20u, 5u> gs(n_obj, wave_id, n_waves);
-  uint64_t cbase, cend;
-  while (gs.next(cbase, cend, ctl, lane)) {
-    const uint64_t obj = cbase + lane;
-    const bool valid = obj < cend;
+  uint64_t cbase = 0, cend = 0, round = 0;
+  for (;;) {
+    uint64_t obj;
+    bool valid;
+    if (IL) {
+      const uint64_t g = wave_id + (round + lane / IL) * n_waves;
+      obj = g * IL + lane % IL;
+      valid = obj < n_obj;
+      if (wave_id + round * n_waves >= (n_obj + IL - 1) / IL) break;
+      round += 64u / IL;
+    } else {
+      if (!gs.next(cbase, cend, ctl, lane)) break;
+      obj = cbase + lane;
+      valid = obj < cend;
+    }
     uint64_t lo = 0, ro = 0, nlo = Lbytes, nro = Rbytes;
     if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
     if (valid && obj + 1u < n_obj) { nlo = Loff[obj + 1u]; nro = Roff[obj + 1u]; }
@@ -87,6 +102,8 @@ __global__ __launch_bounds__(kWave* WPB, MINW) void ring_kernel(const uint8_t* _
     uint64_t cur = lane_of64(lo, 0) + lane_of64(ro, 0);  // PACK: the next record's place
     uint32_t head = 0u, tail = 0u, inflight = 0u;
     uint32_t posv = 0u, markv = 0u;  // lane t: object t's ring slot, vmops after its last piece
+    uint64_t oov = 0;                 // lane t: object t's output offset (OUTM >= 5: stored per chunk)
+    const bool okl = ok;
     while (tocons) {
       // ---- issue: as many of the chunk's next objects as the ring takes
       while (toissue && inflight < DMAX) {
@@ -131,14 +148,20 @@ __global__ __launch_bounds__(kWave* WPB, MINW) void ring_kernel(const uint8_t* _
       {  // synthetic join: a dependent LDS read + VALU chain over the pair
         const __attribute__((address_space(3))) uint32_t* s = (const __attribute__((address_space(3))) uint32_t*)(size_t)slot;
         uint32_t h = s[lane] ^ s[4u * nl + lane];
-        for (uint32_t q = 0; q < spin; ++q) h = h * 0x9e3779b1u + (h >> 7);
+        if (spin >= 1000u) {  // an LDS-bound chain: dependent reads of the wave's scratch
+          const __attribute__((address_space(3))) uint32_t* x =
+              (const __attribute__((address_space(3))) uint32_t*)(size_t)(ring + RB);
+          for (uint32_t q = 1000u; q < spin; ++q) h = x[(h + lane) & 511u] + q;
+        } else {
+          for (uint32_t q = 0; q < spin; ++q) h = h * 0x9e3779b1u + (h >> 7);
+        }
         sink += h;
       }
       // copy-out of the stand-in output (the self record): two 16-B stores per
       // lane, clamped to its last piece
       const uint64_t oo = PACK ? cur : lane_of64(lo, c) + lane_of64(ro, c);
       cur += 16u * nl;
-      {
+      if (OUTM == 0 || OUTM == 5) {
         const uint32_t lastb = 16u * (nl - 1u);
         const uint32_t b0 = 16u * lane, b1 = 16u * (lane + 64u);
         const uint32_t o0 = b0 < lastb ? b0 : lastb, o1 = b1 < lastb ? b1 : lastb;
@@ -147,9 +170,40 @@ __global__ __launch_bounds__(kWave* WPB, MINW) void ring_kernel(const uint8_t* _
         __builtin_nontemporal_store(p0, (u32x4*)(Ob + oo + o0));
         __builtin_nontemporal_store(p1, (u32x4*)(Ob + oo + o1));
         vmops += 2u;
+      } else if (OUTM == 3 || OUTM == 6) {  // timing only: the stand-in written as whole 128-B lines at a line-aligned place
+        const uint64_t ob = ((uint64_t)(Ob + oo) + 127u) & ~127ull;
+        const uint32_t nw = (16u * nl + 127u) / 16u & ~7u;  // pieces of whole lines
+        const uint32_t lastb = 16u * (nw - 1u);
+        const uint32_t b0 = 16u * lane, b1 = 16u * (lane + 64u);
+        const uint32_t o0 = b0 < lastb ? b0 : lastb, o1 = b1 < lastb ? b1 : lastb;
+        const u32x4 p0 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(slot + o0);
+        const u32x4 p1 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(slot + o1);
+        __builtin_nontemporal_store(p0, (u32x4*)(ob + o0));
+        __builtin_nontemporal_store(p1, (u32x4*)(ob + o1));
+        vmops += 2u;
+      } else if (OUTM == 4) {  // timing only: natural place, default-policy stores
+        const uint32_t lastb = 16u * (nl - 1u);
+        const uint32_t b0 = 16u * lane, b1 = 16u * (lane + 64u);
+        const uint32_t o0 = b0 < lastb ? b0 : lastb, o1 = b1 < lastb ? b1 : lastb;
+        const u32x4 p0 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(slot + o0);
+        const u32x4 p1 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(slot + o1);
+        *(u32x4*)(Ob + oo + o0) = p0;
+        *(u32x4*)(Ob + oo + o1) = p1;
+        vmops += 2u;
+      } else if (OUTM == 2) {  // no writes: the pair folded into the sink
+        const u32x4 p0 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(slot + 16u * (lane % (nl + nr)));
+        sink += p0.x ^ p0.w;
       }
-      if (lane == 0u) Ooff[cbase + c] = oo;
-      ++vmops;
+      oov = lane == c ? oo : oov;
+      if (OUTM != 2 && OUTM < 5) {
+        if (IL) {
+          const uint64_t g = wave_id + (round - 64u / IL + c / IL) * n_waves;
+          if (lane == 0u) Ooff[g * IL + c % IL] = oo;
+        } else if (lane == 0u) {
+          Ooff[cbase + c] = oo;
+        }
+        ++vmops;
+      }
       tocons &= tocons - 1u;
       --inflight;
       if (inflight == 0u) {
@@ -158,12 +212,105 @@ __global__ __launch_bounds__(kWave* WPB, MINW) void ring_kernel(const uint8_t* _
         tail = lane_of(posv, (uint32_t)__builtin_ctzll(tocons));
       }
     }
+    if (OUTM >= 5 && okl) Ooff[obj] = oov;  // one coalesced store per chunk
   }
   if (sink == 0x9e3779b9u) sinkp[0] = sink;
 }
 
-template <uint32_t RB, uint32_t DMAX, int PACK, uint32_t WPB, int MINW, bool NT>
-const void* kfn() { return (const void*)ring_kernel<RB, DMAX, PACK, WPB, MINW, NT>; }
+template <uint32_t RB, uint32_t DMAX, int PACK, uint32_t WPB, int MINW, bool NT, int OUTM = 0, uint32_t IL = 0>
+const void* kfn() { return (const void*)ring_kernel<RB, DMAX, PACK, WPB, MINW, NT, OUTM, IL>; }
+
+// Group loads: G consecutive objects' records fetched as ONE contiguous range
+// per side (records of consecutive objects are contiguous in a compact
+// batch), in full 1 KB pieces: the read stream has partial lines only at the
+// group's ends. Slot = the G self records, then the G other records.
+template <uint32_t RB, uint32_t G, int OUTM>
+__global__ __launch_bounds__(kWave * 4, 1) void bulk_kernel(const uint8_t* __restrict__ Lb,
+                                                            const uint64_t* __restrict__ Loff, uint64_t Lbytes,
+                                                            const uint8_t* __restrict__ Rb,
+                                                            const uint64_t* __restrict__ Roff, uint64_t Rbytes,
+                                                            uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff,
+                                                            uint64_t n_obj, uint32_t* ctl, uint32_t* sinkp) {
+  __shared__ u32x4 lds[4][(RB + kScr) / 16];
+  const uint32_t lane = threadIdx.x & 63u, wave = uni(threadIdx.x / 64u);
+  const uint32_t ring = uni(lds_addr(lds[wave]));
+  const uint64_t wave_id = (uint64_t)blockIdx.x * 4 + wave, n_waves = (uint64_t)gridDim.x * 4;
+  uint32_t sink = 0u, vmops = 0u;
+  crdts_hip::GuidedSplit<20u, 5u> gs(n_obj, wave_id, n_waves);
+  uint64_t cbase, cend;
+  while (gs.next(cbase, cend, ctl, lane)) {
+    const uint64_t obj = cbase + lane;
+    const bool valid = obj < cend;
+    uint64_t lo = 0, ro = 0, nlo = Lbytes, nro = Rbytes;
+    if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
+    if (valid && obj + 1u < n_obj) { nlo = Loff[obj + 1u]; nro = Roff[obj + 1u]; }
+    const uint32_t n = (uint32_t)(cend - cbase < 64u ? cend - cbase : 64u);
+    const uint32_t ngr = (n + G - 1u) / G;
+    uint32_t head = 0u, tail = 0u, inflight = 0u, issued = 0u, consumed = 0u;
+    uint32_t posv = 0u, markv = 0u, lenv = 0u;  // lane g: group g's slot, vmops mark, L bytes
+    while (consumed < ngr) {
+      while (issued < ngr && inflight < 3u) {
+        const uint32_t f = issued * G, l = (issued + 1u) * G < n ? (issued + 1u) * G - 1u : n - 1u;
+        const uint64_t l0 = lane_of64(lo, f), r0 = lane_of64(ro, f);
+        const uint32_t bl = (uint32_t)(lane_of64(nlo, l) - l0), br = (uint32_t)(lane_of64(nro, l) - r0);
+        const uint32_t B = bl + br;
+        if (B > RB) { ++issued; continue; }  // (a group past the ring: skipped, probe only)
+        uint32_t pos;
+        if (inflight == 0u) pos = 0u;
+        else if (head > tail) { if (head + B <= RB) pos = head; else if (B <= tail) pos = 0u; else break; }
+        else { if (head + B <= tail) pos = head; else break; }
+        if (inflight == 0u) tail = pos;
+        head = pos + B;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint32_t nl = bl / 16u, nr = br / 16u;
+        for (uint32_t k = 0; k < nl; k += 64u) {
+          if (k + lane < nl) glds16<false>(Lb + l0 + 16u * (k + lane), uni(ring + pos + 16u * k));
+          ++vmops;
+        }
+        for (uint32_t k = 0; k < nr; k += 64u) {
+          if (k + lane < nr) glds16<false>(Rb + r0 + 16u * (k + lane), uni(ring + pos + bl + 16u * k));
+          ++vmops;
+        }
+        posv = lane == issued ? pos : posv;
+        markv = lane == issued ? vmops : markv;
+        lenv = lane == issued ? bl : lenv;
+        ++issued;
+        ++inflight;
+      }
+      if (inflight == 0u) { consumed = issued; continue; }
+      const uint32_t g = consumed;
+      wait_vm(vmops - lane_of(markv, g));
+      const uint32_t slot = ring + lane_of(posv, g);
+      const uint32_t f = g * G, l = (g + 1u) * G < n ? (g + 1u) * G - 1u : n - 1u;
+      const uint64_t l0 = lane_of64(lo, f);
+      for (uint32_t t = f; t <= l; ++t) {  // each object's output: its self record
+        const uint64_t lt = lane_of64(lo, t);
+        const uint32_t nt = (uint32_t)((lane_of64(nlo, t) - lt) / 16u);
+        const uint32_t src = slot + (uint32_t)(lt - l0);
+        const uint64_t oo = lt + lane_of64(ro, t);
+        if (OUTM == 0) {
+          const uint32_t lastb = 16u * (nt - 1u);
+          const uint32_t b0 = 16u * lane, b1 = 16u * (lane + 64u);
+          const uint32_t o0 = b0 < lastb ? b0 : lastb, o1 = b1 < lastb ? b1 : lastb;
+          const u32x4 p0 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(src + o0);
+          const u32x4 p1 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(src + o1);
+          __builtin_nontemporal_store(p0, (u32x4*)(Ob + oo + o0));
+          __builtin_nontemporal_store(p1, (u32x4*)(Ob + oo + o1));
+          vmops += 2u;
+          if (lane == 0u) Ooff[cbase + t] = oo;
+          ++vmops;
+        } else {
+          const u32x4 p0 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(src + 16u * (lane % nt));
+          sink += p0.x ^ p0.w;
+        }
+      }
+      ++consumed;
+      if (--inflight == 0u) head = tail = 0u;
+      else tail = lane_of(posv, consumed);
+    }
+  }
+  if (sink == 0x9e3779b9u) sinkp[0] = sink;
+}
 
 struct Var { int id; const void* fn; uint32_t wpb; };
 }  // namespace
@@ -181,6 +328,23 @@ extern "C" int ring_launch(int variant, const uint8_t* Lb, const uint64_t* Loff,
       {10430, kfn<4096, 3, 0, 4, 6, true>(), 4},  {10640, kfn<6656, 4, 0, 4, 4, true>(), 4},
       {20630, kfn<6144, 3, 0, 1, 1, false>(), 1}, {20640, kfn<6144, 4, 0, 1, 1, false>(), 1},
       {20540, kfn<5120, 4, 0, 1, 1, false>(), 1},
+      // OUTM 1: no copy-out (Ooff only), 2: nothing written
+      {40430, kfn<4096, 3, 0, 4, 6, false, 1>(), 4}, {50430, kfn<4096, 3, 0, 4, 6, false, 2>(), 4},
+      {50860, kfn<8704, 6, 0, 4, 3, false, 2>(), 4},
+      // interleaved schedule: 70000 + IL * 100 + OUTM (RB 4096, DMAX 3, 6 waves/SIMD)
+      {70100, kfn<4096, 3, 0, 4, 6, false, 0, 1>(), 4}, {70102, kfn<4096, 3, 0, 4, 6, false, 2, 1>(), 4},
+      {70400, kfn<4096, 3, 0, 4, 6, false, 0, 4>(), 4}, {70402, kfn<4096, 3, 0, 4, 6, false, 2, 4>(), 4},
+      {71600, kfn<4096, 3, 0, 4, 6, false, 0, 16>(), 4}, {71602, kfn<4096, 3, 0, 4, 6, false, 2, 16>(), 4},
+      {76400, kfn<4096, 3, 0, 4, 6, false, 0, 64>(), 4}, {76402, kfn<4096, 3, 0, 4, 6, false, 2, 64>(), 4},
+      {70403, kfn<4096, 3, 0, 4, 6, false, 3, 4>(), 4}, {70404, kfn<4096, 3, 0, 4, 6, false, 4, 4>(), 4},
+      {70405, kfn<4096, 3, 0, 4, 6, false, 5, 4>(), 4}, {70406, kfn<4096, 3, 0, 4, 6, false, 6, 4>(), 4},
+      {435, kfn<4096, 3, 0, 4, 6, false, 5>(), 4}, {436, kfn<4096, 3, 0, 4, 6, false, 6>(), 4},
+      {76405, kfn<4096, 3, 0, 4, 6, false, 5, 64>(), 4}, {76406, kfn<4096, 3, 0, 4, 6, false, 6, 64>(), 4},
+      {70401, kfn<4096, 3, 0, 4, 6, false, 1, 4>(), 4}, {70413, kfn<4096, 3, 1, 4, 6, false, 0, 4>(), 4},
+      // group loads: 60000 + RB(KB) * 100 + G * 10 + OUTM
+      {61020, (const void*)bulk_kernel<10240, 2, 0>, 4}, {61022, (const void*)bulk_kernel<10240, 2, 2>, 4},
+      {61640, (const void*)bulk_kernel<16384, 4, 0>, 4}, {61642, (const void*)bulk_kernel<16384, 4, 2>, 4},
+      {60610, (const void*)bulk_kernel<6144, 1, 0>, 4}, {60612, (const void*)bulk_kernel<6144, 1, 2>, 4},
   };
   const Var* v = nullptr;
   for (const Var& x : vars)

@@ -127,9 +127,14 @@ __global__ __launch_bounds__(kWave* kWpb, 6) void skel_kernel(const uint8_t* __r
       const uint32_t nu = lane_of(n16, u);
       prefetch(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
       prefetch(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
-      {  // synthetic join: a dependent LDS read + VALU chain
+      {  // synthetic join: a dependent LDS read + VALU chain (spin >= 1000: LDS-bound chain)
         uint32_t h = ((const uint32_t*)sR)[lane] ^ ((const uint32_t*)sL)[lane];
-        for (uint32_t q = 0; q < spin; ++q) h = h * 0x9e3779b1u + (h >> 7);
+        if (spin >= 1000u) {
+          const uint32_t* x = (const uint32_t*)(st[wave] + 2 * kPer * kWave);
+          for (uint32_t q = 1000u; q < spin; ++q) h = x[(h + lane) & 511u] + q;
+        } else {
+          for (uint32_t q = 0; q < spin; ++q) h = h * 0x9e3779b1u + (h >> 7);
+        }
         sink += h;
       }
       const uint32_t on16 = nt16 & 0xFFFFu;  // output stand-in: the self record
