@@ -323,7 +323,7 @@ def run_orswot(args, rank, world, local):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "orswot_join_kernel (+ orswot_merge_general_kernel in the same window)",
+            "kernel": "orswot_join5_kernel (+ orswot_merge_general_kernel in the same window)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

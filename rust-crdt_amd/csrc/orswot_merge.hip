@@ -2802,6 +2802,168 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
 
 
 // ======================================================================
+// The product join (round 5 form): orswot_join_kernel's product
+// instantiation written out with only the product's choices — one pass,
+// the guided split (5/8 static chunks, 20-object tickets), the saddr record
+// prefetch one object ahead into registers, mask3_object for every object
+// (its HD form with direct stores for the ~5 % with deferred removes), the
+// packed two-sided rank search and the bank-conflict scratch layout — and
+// two memory-side changes (FL):
+//  * the output record leaves as whole 128-B lines where that stays in
+//    bytes no record owns (a partial line costs the memory side a
+//    read-modify-write): the tail inside this object's own output slot
+//    (record i's slot is [off_i, off_i + |self_i| + |other_i|), and a
+//    merged record is shorter than it by at least a header and a clock),
+//    the head only past the previous object's record when this wave wrote
+//    it; the bytes between records are unspecified (include/crdts_hip.h);
+//  * the chunk's output offsets leave in one coalesced store at the chunk's
+//    end, not one 8-B store per object (each of which is a partial line).
+// ======================================================================
+template <int MINW, int AW, int FL>  // FL bits: 1 one Ooff store per chunk, 2 whole-line tails, 4 whole-line heads
+__global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join5_kernel(
+    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
+    const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
+    uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
+    int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
+  __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
+  __shared__ u32x4 scr_s[kWavesPerBlock][M3Lay<AW>::Bytes / 16];
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t wave = uni(threadIdx.x / kWave);  // wave-uniform: LDS bases in SGPRs
+  u32x4* const sL = stage_s[wave][0];
+  u32x4* const sR = stage_s[wave][1];
+  const uint32_t uX = lds_addr(scr_s[wave]);
+  const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
+  uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
+  const bool lines = (FL & 6) && ((uint64_t)Ob & 15u) == 0u;
+  GuidedSplit<20u, 5u, 0u> gs(n_obj, wave_id, n_waves);
+  uint64_t cbase, cend;
+  while (gs.next(cbase, cend, &ctl[3], lane)) {
+    // ---- chunk step: lane k <-> object cbase + k (offsets, headers, verdicts)
+    u32x4 pl[kPer], pr[kPer];  // record prefetch registers
+    const uint64_t obj = cbase + lane;
+    const bool valid = obj < cend;
+    uint64_t lo = 0, ro = 0;
+    u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
+    uint64_t nlo = Lbytes, nro = Rbytes;
+    if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
+    if (valid && obj + 1u < n_obj) { nlo = Loff[obj + 1u]; nro = Roff[obj + 1u]; }  // same lines: coalesced
+    bool ok = valid && (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes && ro + kHdrBytes <= Rbytes;
+    if (ok) {
+      hl0 = ((const u32x4*)(Lb + lo))[0]; hl1 = ((const u32x4*)(Lb + lo))[1];
+      hr0 = ((const u32x4*)(Rb + ro))[0]; hr1 = ((const u32x4*)(Rb + ro))[1];
+    }
+    ok = ok && header_ok(hl0, hl1, lo, Lbytes, A) && header_ok(hr0, hr1, ro, Rbytes, A) &&
+         lo + ro + (uint64_t)hl0.x + hr0.x <= Obytes;
+    // output placement precondition (out[i] at self.off[i] + other.off[i]):
+    // each side's records in increasing offset order, none overlapping the next
+    const bool placed = !ok || (nlo >= lo + hl0.x && nro >= ro + hr0.x);
+    if (__ballot(!placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_EINVAL);
+    ok = ok && placed;
+    const bool fits = ok && hl0.x <= kFastStage && hr0.x <= kFastStage && A <= (uint32_t)AW && hl0.z <= 64u &&
+                      hr0.z <= 64u && hl0.w <= 64u && hr0.w <= 64u;
+    const bool hd = fits && (hl1.x | hr1.x) != 0u && hl1.x <= 32u && hr1.x <= 32u;
+    const bool fast = (fits && (hl1.x | hr1.x) == 0u) || hd;
+    const uint64_t defs = __ballot(hd);
+    const bool gen = ok && !fast;
+    // objects the general kernel joins (listed here, or falling back in the
+    // loop): FL 1 keeps them as a wave mask and stores the chunk's offsets
+    // once, at its end (no per-lane 64-bit value kept across the loop)
+    uint64_t pendm = __ballot(gen);
+    if (!(FL & 1) && valid) Ooff[obj] = (lo + ro) | (gen ? kPending : 0ull);
+    if (gen) {  // hand the object to the general kernel
+      const uint32_t e = atomicAdd(&ctl[0], 1u);
+      if (e < list_cap) list[e] = obj;
+    }
+    if (__ballot(valid && !ok && placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
+    const uint64_t runs = __ballot(fast);
+    if (runs == 0ull) {
+      if ((FL & 1) && valid) Ooff[obj] = (lo + ro) | (gen ? kPending : 0ull);
+      continue;
+    }
+    const uint32_t n16 = fast ? (hl0.x / 16u) | ((hr0.x / 16u) << 16) : 0u;
+    const uint32_t nm = hl0.z | (hr0.z << 16), nd = hl0.w | (hr0.w << 16);
+
+    // ---- software pipeline: the next object's records are in flight while
+    // the current one is joined from LDS (loop rotated: the wait for a
+    // prefetch has one predecessor, the previous object's stores)
+    uint64_t pend = runs;
+    uint32_t t = (uint32_t)__builtin_ctzll(pend);
+    pend &= pend - 1;
+    {
+      const uint32_t nn = lane_of(n16, t);
+      prefetch_io<7>(pl, Lb + lane_of64(lo, t), nn & 0xFFFFu, lane);
+      prefetch_io<7>(pr, Rb + lane_of64(ro, t), nn >> 16, lane);
+    }
+    wave_sync();  // the previous chunk's last LDS reads are done
+    stage_all(sL, pl, lane);
+    stage_all(sR, pr, lane);
+    wave_sync();
+    uint32_t prev_t = kWave;  // FL: the last object whose output record end this wave knows, and that end
+    uint64_t prev_end = 0u;
+    for (;;) {
+      const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
+      const uint32_t m = lane_of(nm, t), d = lane_of(nd, t);
+      // the next object, or this one again after the chunk's last (a constant load count)
+      const uint32_t u = pend ? (uint32_t)__builtin_ctzll(pend) : t;
+      const uint32_t nu = lane_of(n16, u);
+      prefetch_io<7>(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
+      prefetch_io<7>(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
+      bool big = false;
+      uint32_t r;
+      const bool dt = (defs >> t) & 1ull;
+      if (dt) {
+        r = mask3_object<0xFFFFFFFFu, 0, true, 0, true, 0, true, 1, AW>(lds_addr(sL), lds_addr(sR), uX, Ob + oo, A,
+                                                                       m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16,
+                                                                       lane, big);
+      } else {
+        r = mask3_object<0xFFFFFFFFu, 3, false, 0, true, 0, true, 1, AW>(lds_addr(sL), lds_addr(sR), uX, Ob + oo, A,
+                                                                        m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16,
+                                                                        lane, big, sink);
+      }
+      const bool fbu = big || r == kLeanFallback;  // wave-uniform
+      wave_sync();
+      if (dt) {  // the same two stores, to the sink (a constant store count per object)
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        __builtin_nontemporal_store(z, (u32x4*)sink);
+        __builtin_nontemporal_store(z, (u32x4*)sink + 1);
+      } else {
+        uint64_t w0 = oo, w1 = oo + 16u * (fbu ? 1u : r);
+        if (lines && !fbu) {
+          const uint64_t e = (w1 + 127u) & ~127ull;
+          const uint32_t nt = lane_of(n16, t);  // the output slot: the inputs' bytes
+          if ((FL & 2) && e <= oo + 16u * ((nt & 0xFFFFu) + (nt >> 16))) w1 = e;
+          const uint64_t h = oo & ~127ull;
+          if ((FL & 4) && prev_t + 1u == t && h >= prev_end && w1 - h <= 2u * 16u * kWave) w0 = h;
+        }
+        copy_io<7>(lds_addr(sL) - (uint32_t)(oo - w0), Ob + w0, (uint32_t)(w1 - w0) / 16u, lane);
+      }
+      if ((FL & 4) && !fbu) {
+        prev_t = t;
+        prev_end = oo + 16u * r;
+      }
+      if (FL & 1) {
+        pendm |= fbu ? 1ull << t : 0ull;
+      } else {
+        *(Ooff + cbase + t) = oo | (fbu ? kPending : 0ull);
+      }
+      if (fbu && lane == 0u) {  // listed for the general kernel (rare)
+        const uint32_t e = atomicAdd(&ctl[0], 1u);
+        if (e < list_cap) list[e] = cbase + t;
+      }
+      if (pend == 0ull) break;
+      t = u;
+      pend &= pend - 1;
+      wave_sync();  // this object's LDS reads are done
+      stage_used(sL, pl, nu & 0xFFFFu, lane);
+      stage_used(sR, pr, nu >> 16, lane);
+      wave_sync();
+    }
+    if ((FL & 1) && valid) Ooff[obj] = (lo + ro) | ((pendm >> lane) & 1ull ? kPending : 0ull);  // one coalesced store
+  }
+}
+
+// ======================================================================
 // Ring join kernel (round 5): orswot_join_kernel's join with the record
 // prefetch moved from registers into a per-wave LDS ring filled by LDS-DMA
 // (global_load_lds_dwordx4: 64 lanes x 16 B land at M0 + 16 lane, no VGPR
@@ -3495,15 +3657,15 @@ int launch_product_join(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
 namespace {
 // The ring join launch (orswot_ring_kernel, then the general kernel), with
 // launch_join_passes' alternating control-word sets (no memset before it).
-template <int MINW, int AW, uint32_t RB, uint32_t DMAX, int HABL = 0>
-int launch_ring_join(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
-                     const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
-                     uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list, uint32_t list_cap,
-                     hipStream_t stream, int blocks_per_cu, JoinSeq* js) {
+template <const void* (*KF)()>
+int launch_join_kernel(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
+                       const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
+                       uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list, uint32_t list_cap,
+                       hipStream_t stream, int blocks_per_cu, JoinSeq* js) {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const void* fn = (const void*)orswot_ring_kernel<MINW, AW, RB, DMAX, HABL>;
-  static std::atomic<int> occ_cache{0};  // per instantiation
+  const void* fn = KF();
+  static std::atomic<int> occ_cache{0};  // per kernel
   int occ = occ_cache.load(std::memory_order_relaxed);
   if (occ == 0) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)
@@ -3529,6 +3691,14 @@ int launch_ring_join(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, c
   js->dirty = false;
   return CRDT_OK;
 }
+template <int MINW, int AW, uint32_t RB, uint32_t DMAX, int HABL>
+const void* ring_fn() { return (const void*)orswot_ring_kernel<MINW, AW, RB, DMAX, HABL>; }
+template <int MINW, int AW, int FL>
+const void* join5_fn() { return (const void*)orswot_join5_kernel<MINW, AW, FL>; }
+template <int MINW, int AW, uint32_t RB, uint32_t DMAX, int HABL = 0>
+constexpr auto launch_ring_join = launch_join_kernel<ring_fn<MINW, AW, RB, DMAX, HABL>>;
+template <int MINW, int AW, int FL>
+constexpr auto launch_join5 = launch_join_kernel<join5_fn<MINW, AW, FL>>;
 }  // namespace
 
 int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
@@ -3544,19 +3714,20 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
              stream, blocks_per_cu, js);
   };
 #ifndef CRDT_DIAG
-  // The product path: orswot_join_kernel in one pass (mask3_object for every
+  // The product path: orswot_join5_kernel — one pass (mask3_object for every
   // object; those with deferred removes take its HD form, direct stores) at 6
   // waves per SIMD with the guided split (5/8 of the objects in static chunks,
-  // the rest in 20-object ticket chunks), record prefetch in the saddr form
-  // and the copy-out clamped on byte offsets (IO 7), both sides' member ranks
-  // in one packed pass when nL + nR <= 64 (PK) and mask3's bank-conflict
-  // layout (BK), then the general kernel (measured best, tools/ab_bench.py;
-  // DESIGN.md §4). Other variants exist in -DCRDT_DIAG builds only.
+  // the rest in 20-object ticket chunks), record prefetch one object ahead in
+  // the saddr form and the copy-out clamped on byte offsets, both sides'
+  // member ranks in one packed pass when nL + nR <= 64 and mask3's
+  // bank-conflict layout, then the general kernel (measured best,
+  // tools/ab_bench.py). It is orswot_join_kernel's product
+  // instantiation written out (diag variants 265 / 310: 0.7396 / 0.7364 ms);
+  // the knob variants exist in -DCRDT_DIAG builds only.
   (void)variant;
-  // (packed output placement, PO, measured 1-1.5 % slower here: diag variant 270)
   if (n_actors > 32u)  // dense top clocks of 33-64 actors: the same join with 64-bit actor masks, 5 waves/SIMD
-    return go(launch_product_join<5, 64>);
-  return go(launch_product_join<6, 32>);
+    return go(launch_join5<5, 64, 0>);
+  return go(launch_join5<6, 32, 0>);
 #else
   // r05: the LDS-DMA ring join (orswot_ring_kernel<MINW, AW, ring bytes, objects in flight>)
   if (variant == 300) return go(launch_ring_join<6, 32, 4096, 2>);
@@ -3566,6 +3737,12 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   if (variant == 304) return go(launch_ring_join<4, 32, 7680, 4>);
   if (variant == 305) return go(launch_ring_join<4, 32, 7680, 5>);
   if (variant == 306) return go(launch_ring_join<3, 32, 11072, 6>);
+  // r05: the product join written out (join5), without (310) / with (311) whole-line copy-out + chunk Ooff store
+  if (variant == 310) return go(launch_join5<6, 32, 0>);
+  if (variant == 311) return go(launch_join5<6, 32, 7>);
+  if (variant == 312) return go(launch_join5<6, 32, 1>);  // one Ooff store per chunk
+  if (variant == 313) return go(launch_join5<6, 32, 2>);  // whole-line tails
+  if (variant == 314) return go(launch_join5<6, 32, 6>);  // whole-line tails and heads
   if (variant == 307) return go(launch_ring_join<6, 32, 4096, 3, 4>);  // timing only: no join
   if (variant == 308) return go(launch_ring_join<6, 32, 4096, 3, 7>);  // timing only: header verdicts, no join
   if (n_actors > 32u && (variant == 0 || variant == 265)) return go(launch_product_join<5, 64>);

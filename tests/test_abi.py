@@ -92,18 +92,15 @@ def test_device_entry_points_fail_cleanly_without_gpu():
 
 
 def test_product_has_only_the_product_join_instantiation():
-    """The timing-only ablations (HABL != 0) and the two-pass join modes exist
-    in the -DCRDT_DIAG build only: the product library's code objects hold
-    exactly one orswot_join_kernel, MODE 3 with HABL 0 (static_asserts in
-    orswot_merge.hip keep it that way) — one per actor-mask width: the 32-bit
-    form at 6 waves/SIMD and the 64-bit form (dense clocks of 33-64 actors) at 5."""
+    """The knob variants of the join (orswot_join_kernel's timing-only
+    ablations and two-pass modes, the LDS-DMA ring kernel, the join5 memory
+    knobs) exist in the -DCRDT_DIAG build only: the product library's code
+    objects hold orswot_join5_kernel<MINW, AW, 0> once per actor-mask width —
+    the 32-bit form at 6 waves/SIMD and the 64-bit form (dense clocks of
+    33-64 actors) at 5 — and no other join kernel."""
     import crdts_hip
 
     blob = open(crdts_hip.LIB_PATH, "rb").read()
-    names = set(re.findall(rb"orswot_join_kernelILi(\d+)ELi(\d+)ELi(\d+)ELb([01])ELb([01])ELb([01])ELi(\d+)E", blob))
-    assert names, "no orswot_join_kernel in the product library"
-    for minw, mode, out, hdd, dc, m3hd, habl in names:
-        assert mode == b"3" and habl == b"0", names
-    assert sorted(n[0] for n in names) == [b"5", b"6"], names
-    widths = set(re.findall(rb"orswot_join_kernelI\S*?ELi0ELi(32|64)EEEv", blob))
-    assert widths == {b"32", b"64"}, widths
+    names = set(re.findall(rb"orswot_join5_kernelILi(\d+)ELi(\d+)ELi(\d+)E", blob))
+    assert names == {(b"6", b"32", b"0"), (b"5", b"64", b"0")}, names
+    assert b"orswot_join_kernelI" not in blob and b"orswot_ring_kernelI" not in blob

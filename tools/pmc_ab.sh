@@ -12,9 +12,9 @@ mkdir -p $OUT
 G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
 G2="SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
 G3="SQ_LDS_UNALIGNED_STALL SQ_LDS_ADDR_CONFLICT SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM"
-if [ "$MODE" = short ]; then GROUPS=("$G1" "FETCH_SIZE" "WRITE_SIZE"); else GROUPS=("$G1" "$G2" "$G3" "FETCH_SIZE" "WRITE_SIZE"); fi
+if [ "$MODE" = short ]; then PMCG=("$G1" "FETCH_SIZE" "WRITE_SIZE"); else PMCG=("$G1" "$G2" "$G3" "FETCH_SIZE" "WRITE_SIZE"); fi
 i=0
-for grp in "${GROUPS[@]}"; do
+for grp in "${PMCG[@]}"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- python3 tools/ab_bench.py --variants $VARS --rounds $ROUNDS > $OUT/p$i.log 2>&1
 done

@@ -127,13 +127,15 @@ __global__ __launch_bounds__(kWave* WPB, MINW) void ring_kernel(const uint8_t* _
         const uint8_t* const ls = Lb + lane_of64(lo, u);
         const uint8_t* const rs = Rb + lane_of64(ro, u);
         const uint32_t base = ring + pos;
-        for (uint32_t k = 0; k < nl; k += 64u) {
-          if (k + lane < nl) glds16<NT>(ls + 16u * (k + lane), uni(base + 16u * k));
-          ++vmops;
-        }
-        for (uint32_t k = 0; k < nr; k += 64u) {
-          if (k + lane < nr) glds16<NT>(rs + 16u * (k + lane), uni(base + 16u * (nl + k)));
-          ++vmops;
+        if (OUTM != 7 && OUTM != 8 && OUTM != 11 && OUTM != 12) {  // (7, 8, 11, 12: write-only timing, no loads)
+          for (uint32_t k = 0; k < nl; k += 64u) {
+            if (k + lane < nl) glds16<NT>(ls + 16u * (k + lane), uni(base + 16u * k));
+            ++vmops;
+          }
+          for (uint32_t k = 0; k < nr; k += 64u) {
+            if (k + lane < nr) glds16<NT>(rs + 16u * (k + lane), uni(base + 16u * (nl + k)));
+            ++vmops;
+          }
         }
         posv = lane == u ? pos : posv;
         markv = lane == u ? vmops : markv;
@@ -161,7 +163,7 @@ __global__ __launch_bounds__(kWave* WPB, MINW) void ring_kernel(const uint8_t* _
       // lane, clamped to its last piece
       const uint64_t oo = PACK ? cur : lane_of64(lo, c) + lane_of64(ro, c);
       cur += 16u * nl;
-      if (OUTM == 0 || OUTM == 5) {
+      if (OUTM == 0 || OUTM == 5 || OUTM == 7) {
         const uint32_t lastb = 16u * (nl - 1u);
         const uint32_t b0 = 16u * lane, b1 = 16u * (lane + 64u);
         const uint32_t o0 = b0 < lastb ? b0 : lastb, o1 = b1 < lastb ? b1 : lastb;
@@ -170,7 +172,7 @@ __global__ __launch_bounds__(kWave* WPB, MINW) void ring_kernel(const uint8_t* _
         __builtin_nontemporal_store(p0, (u32x4*)(Ob + oo + o0));
         __builtin_nontemporal_store(p1, (u32x4*)(Ob + oo + o1));
         vmops += 2u;
-      } else if (OUTM == 3 || OUTM == 6) {  // timing only: the stand-in written as whole 128-B lines at a line-aligned place
+      } else if (OUTM == 3 || OUTM == 6 || OUTM == 8) {  // timing only: the stand-in written as whole 128-B lines at a line-aligned place
         const uint64_t ob = ((uint64_t)(Ob + oo) + 127u) & ~127ull;
         const uint32_t nw = (16u * nl + 127u) / 16u & ~7u;  // pieces of whole lines
         const uint32_t lastb = 16u * (nw - 1u);
@@ -189,6 +191,20 @@ __global__ __launch_bounds__(kWave* WPB, MINW) void ring_kernel(const uint8_t* _
         const u32x4 p1 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(slot + o1);
         *(u32x4*)(Ob + oo + o0) = p0;
         *(u32x4*)(Ob + oo + o1) = p1;
+        vmops += 2u;
+      } else if (OUTM >= 9 && OUTM <= 12) {  // natural place; lanes past the record store nothing
+        // 9/11: exec-masked stores; 10/12: buffer stores over the record's bytes (out-of-range lanes dropped)
+        const uint32_t b0 = 16u * lane, b1 = 16u * (lane + 64u), nb = 16u * nl;
+        const u32x4 p0 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(slot + b0);
+        const u32x4 p1 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(slot + b1);
+        if (OUTM == 9 || OUTM == 11) {
+          if (b0 < nb) __builtin_nontemporal_store(p0, (u32x4*)(Ob + oo + b0));
+          if (b1 < nb) __builtin_nontemporal_store(p1, (u32x4*)(Ob + oo + b1));
+        } else {
+          const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Ob + oo, (short)0, (int)nb, 0x00020000);
+          __builtin_amdgcn_raw_buffer_store_b128(p0, rs, (int)b0, 0, 2);
+          __builtin_amdgcn_raw_buffer_store_b128(p1, rs, (int)b1, 0, 2);
+        }
         vmops += 2u;
       } else if (OUTM == 2) {  // no writes: the pair folded into the sink
         const u32x4 p0 = *(const __attribute__((address_space(3))) u32x4*)(size_t)(slot + 16u * (lane % (nl + nr)));
@@ -338,6 +354,13 @@ extern "C" int ring_launch(int variant, const uint8_t* Lb, const uint64_t* Loff,
       {76400, kfn<4096, 3, 0, 4, 6, false, 0, 64>(), 4}, {76402, kfn<4096, 3, 0, 4, 6, false, 2, 64>(), 4},
       {70403, kfn<4096, 3, 0, 4, 6, false, 3, 4>(), 4}, {70404, kfn<4096, 3, 0, 4, 6, false, 4, 4>(), 4},
       {70405, kfn<4096, 3, 0, 4, 6, false, 5, 4>(), 4}, {70406, kfn<4096, 3, 0, 4, 6, false, 6, 4>(), 4},
+      {437, kfn<4096, 3, 0, 4, 6, false, 7>(), 4}, {438, kfn<4096, 3, 0, 4, 6, false, 8>(), 4},
+      {70407, kfn<4096, 3, 0, 4, 6, false, 7, 4>(), 4}, {70408, kfn<4096, 3, 0, 4, 6, false, 8, 4>(), 4},
+      {70417, kfn<4096, 3, 1, 4, 6, false, 7, 4>(), 4},
+      {439, kfn<4096, 3, 0, 4, 6, false, 9>(), 4}, {440, kfn<4096, 3, 0, 4, 6, false, 10>(), 4},
+      {441, kfn<4096, 3, 0, 4, 6, false, 11>(), 4}, {442, kfn<4096, 3, 0, 4, 6, false, 12>(), 4},
+      {70409, kfn<4096, 3, 0, 4, 6, false, 9, 4>(), 4}, {70410, kfn<4096, 3, 0, 4, 6, false, 10, 4>(), 4},
+      {70411, kfn<4096, 3, 0, 4, 6, false, 11, 4>(), 4},
       {435, kfn<4096, 3, 0, 4, 6, false, 5>(), 4}, {436, kfn<4096, 3, 0, 4, 6, false, 6>(), 4},
       {76405, kfn<4096, 3, 0, 4, 6, false, 5, 64>(), 4}, {76406, kfn<4096, 3, 0, 4, 6, false, 6, 64>(), 4},
       {70401, kfn<4096, 3, 0, 4, 6, false, 1, 4>(), 4}, {70413, kfn<4096, 3, 1, 4, 6, false, 0, 4>(), 4},

@@ -22,7 +22,7 @@ import os
 import shutil
 import sys
 
-KERNELS = {"orswot_join_kernel": "orswot_join_kernel<", "orswot_mask_kernel": "orswot_mask_kernel<",
+KERNELS = {"orswot_join_kernel": ("orswot_join_kernel<", "orswot_join5_kernel<"), "orswot_mask_kernel": "orswot_mask_kernel<",
            "orswot_merge_general_kernel": "orswot_merge_general_kernel", "dense_max_kernel": "dense_max_kernel"}
 # every other kernel of the library is summarised under its own name
 OTHER = ("orswot_apply_kernel", "orswot_sparse_mask_kernel", "orswot_sparse_general_kernel", "bincode_ingest_kernel",
@@ -33,7 +33,7 @@ OTHER = ("orswot_apply_kernel", "orswot_sparse_mask_kernel", "orswot_sparse_gene
 
 def short(name):
     for k, pat in KERNELS.items():
-        if pat in name:
+        if any(p in name for p in ((pat,) if isinstance(pat, str) else pat)):
             return k
     import re
     for k in OTHER:  # whole identifier: mvreg_merge_kernel must not match map_mvreg_merge_kernel
