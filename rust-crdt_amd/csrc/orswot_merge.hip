@@ -1910,27 +1910,42 @@ __device__ __forceinline__ uint32_t rank32(const uint8_t* b, uint32_t off, uint3
 // with 16-B stores, instead of scattered 4- / 8-B stores to HBM (as mask3's
 // OUT 2 does for the dense join); with O == nullptr it stays in the stage
 // (the fused fold's accumulator)
-template <bool HD, int ABL = 0, bool ASM = false>
+// DN (dense top clocks of 65..1024 actors, ncL = ncR = A): the clock union is
+// the set of actors with a non-zero counter on either side (a dense clock
+// stores 0 for an absent actor, src/vclock.rs:159-163), built from the rows
+// 64 actors per round; the joined top clock is written dense (pointwise max
+// of the rows, src/orswot.rs:153) and the record keeps the dense form.
+template <bool HD, int ABL = 0, bool ASM = false, bool DN = false>
 __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* X, uint8_t* O,
                                                        uint32_t A, uint32_t ncL, uint32_t nL, uint32_t dL,
                                                        uint32_t ncR, uint32_t nR, uint32_t dR, uint32_t lane,
                                                        Stamps* st = nullptr) {
-  const uint32_t keyL = kHdrBytes + clock_bytes(ncL, true), keyR = kHdrBytes + clock_bytes(ncR, true);
-  const uint32_t caL = kHdrBytes + 8u * ncL, caR = kHdrBytes + 8u * ncR;  // clock actor lists
+  static_assert(!(DN && ASM), "DN: direct stores");
+  const uint32_t keyL = kHdrBytes + clock_bytes(ncL, !DN), keyR = kHdrBytes + clock_bytes(ncR, !DN);
+  const uint32_t caL = kHdrBytes + 8u * ncL, caR = kHdrBytes + 8u * ncR;  // clock actor lists (CSR)
   const uint32_t ctrL = keyL + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
   const uint32_t ctrR = keyR + 8u * nR, actR = ctrR + 8u * dR, endR = actR + 4u * dR;
   const uint32_t tr = kSpTrash + 16u * lane;
 
   // ---- union of the two top clocks: an actor's union position is the
   // number of union-bitmap bits below it (both sides agree on a common actor)
-  const bool hcl = lane < ncL, hcr = lane < ncR;
-  const uint32_t cxl = ld32(Ls, caL + 4u * lane), cxr = ld32(Rs, caR + 4u * lane);
-  const uint64_t cvl = ld64(Ls, kHdrBytes + 8u * lane), cvr = ld64(Rs, kHdrBytes + 8u * lane);
-  if (__ballot((hcl && cxl >= kSpTableN) || (hcr && cxr >= kSpTableN)) != 0ull) return kLeanFallback;
+  const bool hcl = !DN && lane < ncL, hcr = !DN && lane < ncR;
+  const uint32_t cxl = DN ? 0u : ld32(Ls, caL + 4u * lane), cxr = DN ? 0u : ld32(Rs, caR + 4u * lane);
+  const uint64_t cvl = DN ? 0ull : ld64(Ls, kHdrBytes + 8u * lane), cvr = DN ? 0ull : ld64(Rs, kHdrBytes + 8u * lane);
+  if (!DN && __ballot((hcl && cxl >= kSpTableN) || (hcr && cxr >= kSpTableN)) != 0ull) return kLeanFallback;
   wave_sync();  // the previous object's readers of this scratch are done
-  if (lane < kSpTableN / 64u) *(uint64_t*)(X + kSpUbm + 8u * lane) = 0ull;
-  atomicOr((unsigned long long*)(X + (hcl ? kSpUbm + 8u * (cxl >> 6) : tr)), 1ull << (cxl & 63u));
-  atomicOr((unsigned long long*)(X + (hcr ? kSpUbm + 8u * (cxr >> 6) : tr)), 1ull << (cxr & 63u));
+  if (DN) {  // one bitmap word per 64 actors: lane a of round q <-> actor 64 q + a
+    for (uint32_t q = 0; q < kSpTableN / 64u; ++q) {
+      const uint32_t a = 64u * q + lane;
+      const bool p = a < A && (ld64(Ls, kHdrBytes + 8u * a) | ld64(Rs, kHdrBytes + 8u * a)) != 0ull;
+      const uint64_t w = __ballot(p);
+      if (lane == 0u) *(uint64_t*)(X + kSpUbm + 8u * q) = w;
+    }
+  } else {
+    if (lane < kSpTableN / 64u) *(uint64_t*)(X + kSpUbm + 8u * lane) = 0ull;
+    atomicOr((unsigned long long*)(X + (hcl ? kSpUbm + 8u * (cxl >> 6) : tr)), 1ull << (cxl & 63u));
+    atomicOr((unsigned long long*)(X + (hcr ? kSpUbm + 8u * (cxr >> 6) : tr)), 1ull << (cxr & 63u));
+  }
   wave_sync();
   const uint64_t bw = lane < kSpTableN / 64u ? *(const uint64_t*)(X + kSpUbm + 8u * lane) : 0ull;
   const uint32_t bpc = (uint32_t)__popcll(bw), bin = scan_incl(bpc);
@@ -1970,12 +1985,26 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
 
   wave_sync();  // the previous object's readers of this scratch are done
   // union clock entries (each side its own counter) + actor table
-  *(uint32_t*)(X + (hcl ? kSpUcAct + 4u * (ucl & 63u) : tr)) = cxl;
-  *(uint64_t*)(X + (hcl ? kSpUcL + 8u * (ucl & 63u) : tr)) = cvl;
-  X[hcl ? kSpTable + cxl : tr] = (uint8_t)ucl;
-  *(uint32_t*)(X + (hcr ? kSpUcAct + 4u * (ucr & 63u) : tr)) = cxr;
-  *(uint64_t*)(X + (hcr ? kSpUcR + 8u * (ucr & 63u) : tr)) = cvr;
-  X[hcr ? kSpTable + cxr : tr] = (uint8_t)ucr;
+  if (DN) {  // every present actor, round by round: its union position from the prefix table
+    for (uint32_t q = 0; q < (A + 63u) / 64u; ++q) {
+      const uint32_t a = 64u * q + lane;
+      const uint64_t l = a < A ? ld64(Ls, kHdrBytes + 8u * a) : 0ull, r = a < A ? ld64(Rs, kHdrBytes + 8u * a) : 0ull;
+      const u32x4 pw = *(const u32x4*)(X + kSpUpre + 16u * q);
+      const uint32_t u = pw.z + below64(((uint64_t)pw.y << 32) | pw.x, lane);
+      const bool p = (l | r) != 0ull;
+      *(uint32_t*)(X + (p ? kSpUcAct + 4u * (u & 63u) : tr)) = a;
+      *(uint64_t*)(X + (p ? kSpUcL + 8u * (u & 63u) : tr)) = l;
+      *(uint64_t*)(X + (p ? kSpUcR + 8u * (u & 63u) : tr)) = r;
+      X[p ? kSpTable + a : tr] = (uint8_t)u;
+    }
+  } else {
+    *(uint32_t*)(X + (hcl ? kSpUcAct + 4u * (ucl & 63u) : tr)) = cxl;
+    *(uint64_t*)(X + (hcl ? kSpUcL + 8u * (ucl & 63u) : tr)) = cvl;
+    X[hcl ? kSpTable + cxl : tr] = (uint8_t)ucl;
+    *(uint32_t*)(X + (hcr ? kSpUcAct + 4u * (ucr & 63u) : tr)) = cxr;
+    *(uint64_t*)(X + (hcr ? kSpUcR + 8u * (ucr & 63u) : tr)) = cvr;
+    X[hcr ? kSpTable + cxr : tr] = (uint8_t)ucr;
+  }
   // member masks (zeroed), run heads, descriptors
   *(u32x4*)(X + kSpMsL + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
   *(u32x4*)(X + kSpMsR + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
@@ -2116,10 +2145,10 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   if (ABL == 9) mark<ABL>(*st, 6);
   // survivors cached in the run-head area (free once the head ballots are taken; 64 entries)
   uint32_t* dcache = (uint32_t*)(X + kSpHeadL);
-  if (HD) deferred_pass_wave<true>(DL, DR, A, lane, nd, ndd, ndm, nullptr, dcache);
+  if (HD) deferred_pass_wave<!DN>(DL, DR, A, lane, nd, ndd, ndm, nullptr, dcache);
   if (ABL == 9) mark<ABL>(*st, 8);
   RecLayout OL;
-  rec_layout(OL, Uc, tot_mem, tot_dot, nd, ndd, ndm, true);
+  rec_layout(OL, DN ? A : Uc, tot_mem, tot_dot, nd, ndd, ndm, !DN);
   const uint32_t size = OL.size;
   const uint32_t d0 = cincl - c;
   if (ABL == 9) mark<ABL>(*st, 6);
@@ -2151,12 +2180,19 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
       *(uint32_t*)(O + OL.o_mdend + 4u * midx) = d0 + c;
     }
   }
-  if (lane < Uc) {  // top clock: the union list, pointwise max (src/orswot.rs:153)
-    const uint64_t a = *(const uint64_t*)(X + kSpUcL + 8u * lane), b = *(const uint64_t*)(X + kSpUcR + 8u * lane);
-    *(uint64_t*)(O + kHdrBytes + 8u * lane) = a > b ? a : b;
-    *(uint32_t*)(O + kHdrBytes + 8u * Uc + 4u * lane) = *(const uint32_t*)(X + kSpUcAct + 4u * lane);
+  if (DN) {  // top clock: dense, pointwise max of the rows (src/orswot.rs:153)
+    for (uint32_t a = lane; a < A; a += kWave) {
+      const uint64_t l = ld64(Ls, kHdrBytes + 8u * a), r = ld64(Rs, kHdrBytes + 8u * a);
+      *(uint64_t*)(O + kHdrBytes + 8u * a) = l > r ? l : r;
+    }
+  } else {
+    if (lane < Uc) {  // top clock: the union list, pointwise max (src/orswot.rs:153)
+      const uint64_t a = *(const uint64_t*)(X + kSpUcL + 8u * lane), b = *(const uint64_t*)(X + kSpUcR + 8u * lane);
+      *(uint64_t*)(O + kHdrBytes + 8u * lane) = a > b ? a : b;
+      *(uint32_t*)(O + kHdrBytes + 8u * Uc + 4u * lane) = *(const uint32_t*)(X + kSpUcAct + 4u * lane);
+    }
+    if (lane == 0u && (Uc & 1u)) *(uint32_t*)(O + kHdrBytes + 12u * Uc) = 0u;  // clock section pad to 8
   }
-  if (lane == 0u && (Uc & 1u)) *(uint32_t*)(O + kHdrBytes + 12u * Uc) = 0u;  // clock section pad to 8
   wave_sync();
   uint32_t* oact = (uint32_t*)(O + OL.o_dact);
   uint64_t* octr = (uint64_t*)(O + OL.o_dctr);
@@ -2191,15 +2227,15 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
              (uint32_t*)(O + OL.o_fdend), (uint32_t*)(O + OL.o_fmend)};
     wave_sync();
-    deferred_pass_wave<true>(DL, DR, A, lane, nd, ndd, ndm, &w, dcache, nd);
+    deferred_pass_wave<!DN>(DL, DR, A, lane, nd, ndd, ndm, &w, dcache, nd);
   }
   if (ABL == 9) mark<ABL>(*st, 9);
   if (lane == 0u && OL.o_def != OL.o_mpad) *(uint32_t*)(O + OL.o_mpad) = 0u;
   if (lane >= 1u && lane < 4u && OL.o_end + 4u * (lane - 1u) < size) *(uint32_t*)(O + OL.o_end + 4u * (lane - 1u)) = 0u;
   if (lane == 0u) {
     u32x4* h = (u32x4*)O;
-    h[0] = u32x4{size, Uc, tot_mem, tot_dot};
-    h[1] = u32x4{nd, ndd, ndm, kSparseClock};
+    h[0] = u32x4{size, DN ? A : Uc, tot_mem, tot_dot};
+    h[1] = u32x4{nd, ndd, ndm, DN ? 0u : kSparseClock};
   }
   if (ASM && O_ != nullptr) {  // the assembled record out of the stage: 16-B coalesced non-temporal stores
     wave_sync();
@@ -3371,7 +3407,9 @@ __device__ __forceinline__ void stage_pair(u32x4* dst, const u32x4 (&r)[kSpPer],
   for (uint32_t k = 0; k < kSpPer; ++k) dst[lane + k * kWave] = r[k];
 }
 
-template <int MINW, int ABL = 0, uint32_t DYN = 0, uint32_t SF = 5, bool SASM = false>  // ABL 9: phase stamps into the list buffer (no general path)
+// DN: dense batches of 65..1024 actors (sparse_mask_object's DN form; the
+// clock union of an object must have <= 64 actors, else the general kernel)
+template <int MINW, int ABL = 0, uint32_t DYN = 0, uint32_t SF = 5, bool SASM = false, bool DN = false>  // ABL 9: phase stamps into the list buffer (no general path)
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_mask_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
@@ -3410,12 +3448,13 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
       hl0 = ((const u32x4*)(Lb + lo))[0]; hl1 = ((const u32x4*)(Lb + lo))[1];
       hr0 = ((const u32x4*)(Rb + ro))[0]; hr1 = ((const u32x4*)(Rb + ro))[1];
     }
-    ok = ok && sparse_header_ok(hl0, hl1, lo, Lbytes, A) && sparse_header_ok(hr0, hr1, ro, Rbytes, A) &&
+    ok = ok && (DN ? header_ok(hl0, hl1, lo, Lbytes, A) && header_ok(hr0, hr1, ro, Rbytes, A)
+                   : sparse_header_ok(hl0, hl1, lo, Lbytes, A) && sparse_header_ok(hr0, hr1, ro, Rbytes, A)) &&
          lo + ro + (uint64_t)hl0.x + hr0.x <= Obytes;
     const bool placed = !ok || (nlo >= lo + hl0.x && nro >= ro + hr0.x);  // as in orswot_mask_kernel
     if (__ballot(!placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_EINVAL);
     ok = ok && placed;
-    const bool fast = ok && hl0.x + hr0.x <= kSpPair && A <= kSpTableN && hl0.y <= 64u && hr0.y <= 64u &&
+    const bool fast = ok && hl0.x + hr0.x <= kSpPair && A <= kSpTableN && (DN || (hl0.y <= 64u && hr0.y <= 64u)) &&
                       hl0.z <= 64u && hr0.z <= 64u && hl0.w <= 128u && hr0.w <= 128u && hl1.x <= 32u &&
                       hr1.x <= 32u;
     if (valid) Ooff[obj] = (lo + ro) | ((ok && !fast) ? kPending : 0ull);
@@ -3453,11 +3492,11 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
       const uint8_t* Rs = Ls + 16u * (nn & 0xFFFFu);
       uint32_t r;
       if ((defs >> t) & 1ull)
-        r = sparse_mask_object<true, ABL>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu, d & 0xFFFFu, c >> 16,
-                                          m >> 16, d >> 16, lane, &st);
+        r = sparse_mask_object<true, ABL, false, DN>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu, d & 0xFFFFu,
+                                                     c >> 16, m >> 16, d >> 16, lane, &st);
       else
-        r = sparse_mask_object<false, ABL, SASM>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu, d & 0xFFFFu, c >> 16,
-                                           m >> 16, d >> 16, lane, &st);
+        r = sparse_mask_object<false, ABL, SASM && !DN, DN>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu,
+                                                            d & 0xFFFFu, c >> 16, m >> 16, d >> 16, lane, &st);
       if (ABL != 9 && r == kLeanFallback && lane == 0u) {  // union clock / members > 64 or a foreign dot actor
         Ooff[cbase + t] |= kPending;
         const uint32_t e = atomicAdd(&ctl[0], 1u);
@@ -3699,6 +3738,10 @@ template <int MINW, int AW, uint32_t RB, uint32_t DMAX, int HABL = 0>
 constexpr auto launch_ring_join = launch_join_kernel<ring_fn<MINW, AW, RB, DMAX, HABL>>;
 template <int MINW, int AW, int FL>
 constexpr auto launch_join5 = launch_join_kernel<join5_fn<MINW, AW, FL>>;
+// dense top clocks of 65..1024 actors: the sparse mask join over the
+// per-object union of present actors (DN), then the dense general kernel
+const void* dense_wide_fn() { return (const void*)orswot_sparse_mask_kernel<3, 0, 16, 5, false, true>; }
+constexpr auto launch_dense_wide = launch_join_kernel<dense_wide_fn>;
 }  // namespace
 
 int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
@@ -3713,6 +3756,11 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
     return f(Lb, Loff, Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors, status, ctl, list, list_cap,
              stream, blocks_per_cu, js);
   };
+  // dense top clocks wider than the 64-bit actor masks (65..1024 actors):
+  // every object whose clock union holds <= 64 present actors takes the
+  // sparse mask join in its dense form (DN), the rest the general kernel
+  // (diag variant 320: every such object to the general kernel, as before)
+  if (n_actors > 64u && n_actors <= kSpTableN && variant != 320) return go(launch_dense_wide);
 #ifndef CRDT_DIAG
   // The product path: orswot_join5_kernel — one pass (mask3_object for every
   // object; those with deferred removes take its HD form, direct stores) at 6

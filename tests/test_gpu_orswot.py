@@ -479,3 +479,26 @@ def test_dense_33_to_64_actors(gpu, oracle, A, n):
     out = _gpu_merge(gpu, lb, lo, rb, ro, A)
     ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, A, threads=16)
     _compare(out, ob, oo, f"A={A}")
+
+
+# ------------------------------------------------------------------ 65-1024 dense actors
+@pytest.mark.parametrize("A,n,anc", [(100, 100_000, 32), (128, 100_000, 32), (200, 20_000, 100), (700, 5_000, 32)])
+def test_dense_wide_actors(gpu, oracle, A, n, anc):
+    """Dense top clocks wider than the 64-bit actor masks (65-1024 actors; the
+    reference clock has no actor bound, src/vclock.rs:54-57) take the sparse
+    mask join over each object's union of PRESENT actors (a dense clock stores
+    0 for an absent actor) in its dense form, and objects whose union passes
+    64 actors (A = 200 with 100 ancestor adds) or whose pair passes the 6 KB
+    stage (A = 700: 5.6 KB of clocks alone) the general kernel; config-3-shaped
+    pairs with deferred removes, byte-exact against the oracle (bench.py
+    --n-actors 128 times the same form)."""
+    import crdts_hip
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(n, threads=16, seed=0xC0FFEE03 + A,
+                                                   params={"n_actors": A, "ancestor_adds": anc})
+    recs = records.unpack_batch(lb, lo)
+    assert sum(1 for r in recs[:2000] if records.decode(r)["deferred"]) > 20  # deferred removes present
+    assert max(a for r in recs[:2000] for a in records.decode(r)["clock"]) >= 64  # actors past the 64-bit masks
+    out = _gpu_merge(gpu, lb, lo, rb, ro, A)
+    ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, A, threads=16)
+    _compare(out, ob, oo, f"A={A}")
