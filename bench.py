@@ -579,8 +579,10 @@ def settle(args, stream, fn, world=1):
         stream.synchronize()
         per = max_over_ranks((time.perf_counter() - t1) / 7.0, world)
         probes = 8
-    spent = time.perf_counter() - t0
-    n = min(4096, max(0, int((args.settle_ms * 1e-3 - spent) / max(per, 1e-6))))
+    # the count from all-reduced values only: every rank makes the same number
+    # of calls (a step may hold collectives; a locally measured elapsed time
+    # would differ between ranks)
+    n = min(4096, max(0, int(args.settle_ms * 1e-3 / max(per, 1e-6)) - probes))
     for k in range(n):
         fn()
         if k % 64 == 63:

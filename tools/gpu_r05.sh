@@ -6,8 +6,8 @@ TAG=${1:-r05}; K=${2:-}
 OUT=gpurun_out/chk_$TAG
 mkdir -p $OUT
 if [ -n "$K" ]; then KARG=(-k "$K"); else KARG=(); fi
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread "${KARG[@]}" > $OUT/gputests.log 2>&1 || { echo TESTS_FAILED; tail -60 $OUT/gputests.log; exit 1; }
-tail -2 $OUT/gputests.log
+[ -n "${SKIP_TESTS:-}" ] || timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread "${KARG[@]}" > $OUT/gputests.log 2>&1 || { echo TESTS_FAILED; tail -60 $OUT/gputests.log; exit 1; }
+[ -n "${SKIP_TESTS:-}" ] || tail -2 $OUT/gputests.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo SMOKE_FAILED; tail -20 $OUT/smoke.log; exit 1; }
 tail -1 $OUT/smoke.log
 timeout -k 10 300 python bench.py --gpus 2 --rehearse --n-obj 200000 --ae-n-obj 100000 --steps 3 --warmup 1 > $OUT/bench_rehearse2.json 2> $OUT/bench_rehearse2.err || { echo REHEARSE_FAILED; tail -30 $OUT/bench_rehearse2.err; exit 1; }
