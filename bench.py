@@ -64,7 +64,8 @@ def parse():
                             "mvreg", "map", "map_orswot", "map_map", "clock_csr", "truncate", "spawn_check"])
     p.add_argument("--replicas", type=int, default=8, help="orswot_csr at N=1: replicas folded locally")
     p.add_argument("--n-actors", type=int, default=16,
-                   help="orswot: dense top-clock actors (config 3: 16; 33-64 take the 64-bit actor-mask join)")
+                   help="orswot: dense top-clock actors (config 3: 16; 33-64 take the 64-bit actor-mask join, "
+                        "65-1024 the sparse mask join over each object's present actors)")
     p.add_argument("--n-obj", type=int, default=None, help="objects per GPU")
     p.add_argument("--threads", type=int, default=16, help="host threads for input generation")
     p.add_argument("--cpu-threads", type=int, default=None,
@@ -312,7 +313,9 @@ def run_orswot(args, rank, world, local):
         "config": {
             "workload": ("orswot_merge config3 (BASELINE.json configs[2]): 1M objects/GPU x ~31 members/side "
                          "x 16 dense actors incl. deferred removes") if A == 16 else
-                        (f"orswot_merge config3 shape over {A} dense actors (64-bit actor-mask join): "
+                        (f"orswot_merge config3 shape over {A} dense actors ("
+                         + ("64-bit actor-mask join" if A <= 64 else "sparse mask join over the present actors, DN form")
+                         + "): "
                          f"{n} objects/GPU incl. deferred removes"),
             "n_obj_per_gpu": n,
             "n_actors": A,
@@ -323,7 +326,8 @@ def run_orswot(args, rank, world, local):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "orswot_join5_kernel (+ orswot_merge_general_kernel in the same window)",
+            "kernel": ("orswot_join5_kernel" if A <= 64 else "orswot_sparse_mask_kernel<DN>")
+                      + " (+ orswot_merge_general_kernel in the same window)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

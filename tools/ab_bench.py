@@ -20,16 +20,19 @@ def main():
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--n-obj", type=int, default=1_000_000)
     ap.add_argument("--check", default="", help="variants >= 100 whose output is also compared byte for byte")
+    ap.add_argument("--n-actors", type=int, default=16, help="dense top-clock actors (config 3: 16)")
     a = ap.parse_args()
     import numpy as np
     import torch
 
     import crdts_hip
 
-    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(a.n_obj, threads=16)
+    A = a.n_actors
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(a.n_obj, threads=16, **({} if A == 16 else {
+        "seed": 0xC0FFEE03 + A, "params": {"n_actors": A}}))
     eng = crdts_hip.Engine(0)
-    L = crdts_hip.OrswotBatch.from_host(lb, lo, 16)
-    R = crdts_hip.OrswotBatch.from_host(rb, ro, 16)
+    L = crdts_hip.OrswotBatch.from_host(lb, lo, A)
+    R = crdts_hip.OrswotBatch.from_host(rb, ro, A)
     out = eng.orswot_alloc_out(L, R)
     s = torch.cuda.Stream()
     configs = [(int(v), int(b)) for v in a.variants.split(",") for b in a.bpc.split(",")]
