@@ -60,7 +60,7 @@ def parse():
     # (the driver's 5 x 0.75 ms) would otherwise time the ramp
     p.add_argument("--settle-ms", type=float, default=200.0)
     p.add_argument("--workload", default="orswot",
-                   choices=["orswot", "vclock", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply",
+                   choices=["orswot", "orswot_tail", "vclock", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply",
                             "mvreg", "map", "map_orswot", "map_map", "clock_csr", "truncate", "spawn_check"])
     p.add_argument("--replicas", type=int, default=8, help="orswot_csr at N=1: replicas folded locally")
     p.add_argument("--n-actors", type=int, default=16,
@@ -255,8 +255,13 @@ def run_orswot(args, rank, world, local):
     first = rank * n
     t0 = time.time()
     A = args.n_actors
-    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(n, first_obj=first, threads=args.threads,
-                                                   params=None if A == 16 else {"n_actors": A})
+    tail = args.workload == "orswot_tail"
+    if tail:  # config 3 with a heavy tail: 5 % of the objects at 100 / 300 / 1000 members per side
+        A = 16
+        (lb, lo), (rb, ro) = crdts_hip.generate_orswot_tail(n, first_obj=first, threads=args.threads)
+    else:
+        (lb, lo), (rb, ro) = crdts_hip.generate_orswot(n, first_obj=first, threads=args.threads,
+                                                       params=None if A == 16 else {"n_actors": A})
     gen_s = time.time() - t0
     eng = crdts_hip.Engine(local)
     L = crdts_hip.OrswotBatch.from_host(lb, lo, A, device=local)
@@ -296,7 +301,7 @@ def run_orswot(args, rank, world, local):
     # measured HBM bytes of one launch (both kernels of the timed window), from
     # the FETCH_SIZE / WRITE_SIZE passes of tools/profile.sh -> tools/traffic.py
     tk = [load_traffic(args.traffic_json, k) for k in ("orswot_join_kernel", "orswot_merge_general_kernel")]
-    traffic = None if args.n_obj is not None or A != 16 or tk[0] is None else tk[0] + (tk[1] or 0.0)
+    traffic = None if args.n_obj is not None or A != 16 or tail or tk[0] is None else tk[0] + (tk[1] or 0.0)
     res = {
         "metric": METRIC,
         "value": value,
@@ -311,7 +316,10 @@ def run_orswot(args, rank, world, local):
         "dtype": "u64",
         "data": "synthetic: op-simulated Orswot pairs (SplitMix64 seed 0xC0FFEE03 ^ object id)",
         "config": {
-            "workload": ("orswot_merge config3 (BASELINE.json configs[2]): 1M objects/GPU x ~31 members/side "
+            "workload": (f"orswot_tail: config 3 with a heavy tail, {n} objects/GPU, every 20th object at "
+                         f"{'/'.join(map(str, crdts_hip.TAIL_SIZES))} members per side in turn (the general / big-object "
+                         "path), the rest config-3 pairs") if tail else
+                        ("orswot_merge config3 (BASELINE.json configs[2]): 1M objects/GPU x ~31 members/side "
                          "x 16 dense actors incl. deferred removes") if A == 16 else
                         (f"orswot_merge config3 shape over {A} dense actors ("
                          + ("64-bit actor-mask join" if A <= 64 else "sparse mask join over the present actors, DN form")
@@ -383,7 +391,7 @@ def cpu_baseline_orswot(lb, lo, rb, ro, args):
         "unit": "objects/s",
         "cores": threads,
         "kind": "port", **cpu_cores_note(),
-        "sample": f"first {m} objects of the same config-3 batch, merge loop only (decode untimed), "
+        "sample": f"first {m} objects of the same batch, merge loop only (decode untimed), "
                   f"{threads} std::threads static partition",
         "value_1core": m1 / secs1,
     }
@@ -1676,7 +1684,7 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     if args.workload == "spawn_check":
         res = run_spawn_check(args, rank, world, local)
-    elif args.workload == "orswot":
+    elif args.workload in ("orswot", "orswot_tail"):
         res = run_orswot(args, rank, world, local)
     elif args.workload == "vclock":
         res = run_vclock(args, rank, world, local)

@@ -1003,6 +1003,68 @@ def generate_orswot(n_obj, first_obj=0, seed=CONFIG3_SEED, params=None, threads=
         lib.crdt_orswot_gen_free(g)
 
 
+TAIL_SEED = 0xC0FFEE06
+TAIL_SIZES = (100, 300, 1000)
+
+
+def generate_orswot_tail(n_obj, frac=0.05, sizes=TAIL_SIZES, first_obj=0, seed=CONFIG3_SEED, threads=8):
+    """Config 3 with a heavy tail (bench.py --workload orswot_tail): object i
+    is heavy iff (first_obj + i) % round(1 / frac) == 0; heavy objects take
+    the sizes in turn, an object of size m being op-simulated over a member
+    universe of m keys with m ancestor adds and m/8..m/4 divergent ops per
+    side (so ~m members per side: the reference's entries map is unbounded,
+    src/orswot.rs:26-30); the others are config-3 objects. The same object
+    index gets the same pair at any batch split. Returns ((L_base, L_off),
+    (R_base, R_off)) as numpy arrays."""
+    step = max(1, int(round(1.0 / frac)))
+    ids = np.arange(first_obj, first_obj + n_obj, dtype=np.int64)
+    heavy = ids % step == 0
+    kind = np.where(heavy, 1 + (ids // step) % len(sizes), 0)
+    parts = []  # per kind: (positions, (lb, lo), (rb, ro))
+    for k in range(len(sizes) + 1):
+        pos = np.nonzero(kind == k)[0]
+        if pos.size == 0:
+            continue
+        if k == 0:  # config-3 pairs of the objects' own ids (the heavy ids' pairs generated and dropped)
+            (lb, lo), (rb, ro) = generate_orswot(n_obj, first_obj=first_obj, seed=seed, threads=threads)
+            sides = []
+            for b, o in ((lb, lo), (rb, ro)):
+                end = np.append(o[1:], np.uint64(b.nbytes))
+                sides.append((b, o[pos], end[pos]))
+        else:  # heavy object g of size m: pair index (g // step) // len(sizes) of the size-m generator
+            m = sizes[k - 1]
+            sides = generate_orswot(int(pos.size), first_obj=int(ids[pos[0]] // step // len(sizes)),
+                                    seed=TAIL_SEED + m, threads=threads,
+                                    params={"member_universe": m, "ancestor_adds": m, "min_div_ops": max(4, m // 8),
+                                            "max_div_ops": max(8, m // 4)})
+        parts.append((pos, sides))
+    out = []
+    for side in (0, 1):
+        # gather every object's record (16-B units) into object order
+        srcs, starts, counts, order = [], [], [], []
+        base_units = 0
+        for pos, sides in parts:
+            b, o = sides[side][0], sides[side][1]
+            end = sides[side][2] if len(sides[side]) == 3 else np.append(o[1:], np.uint64(b.nbytes))
+            u = b.view(np.complex128) if b.nbytes % 16 == 0 else np.frombuffer(b.tobytes() + bytes(16 - b.nbytes % 16), np.complex128)
+            sz = end.astype(np.int64) - o.astype(np.int64)
+            srcs.append(u)
+            starts.append(o.astype(np.int64) // 16 + base_units)
+            counts.append(sz // 16)
+            order.append(pos)
+            base_units += u.size
+        src = np.concatenate(srcs)
+        pos_all = np.concatenate(order)
+        st = np.empty(n_obj, np.int64)
+        ct = np.empty(n_obj, np.int64)
+        st[pos_all] = np.concatenate(starts)
+        ct[pos_all] = np.concatenate(counts)
+        off_units = np.concatenate(([0], np.cumsum(ct)[:-1]))
+        idx = np.repeat(st - off_units, ct) + np.arange(int(ct.sum()), dtype=np.int64)
+        out.append((src[idx].view(np.uint8).copy(), (off_units * 16).astype(np.uint64)))
+    return out[0], out[1]
+
+
 def _copy_sides(g, n_sides, n_obj):
     sides = []
     for s in range(n_sides):

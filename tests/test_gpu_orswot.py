@@ -502,3 +502,22 @@ def test_dense_wide_actors(gpu, oracle, A, n, anc):
     out = _gpu_merge(gpu, lb, lo, rb, ro, A)
     ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, A, threads=16)
     _compare(out, ob, oo, f"A={A}")
+
+
+# ------------------------------------------------------------------ heavy-tailed batches
+def test_heavy_tail_100k(gpu, oracle):
+    """Config 3 with a heavy tail (bench.py --workload orswot_tail): every 20th
+    object op-simulated at 100 / 300 / 1000 members per side (the reference's
+    entries map is unbounded, src/orswot.rs:26-30) — records up to ~28 KB,
+    past the join kernel's 2 KB stage and 64-member masks — byte-exact against
+    the oracle, both orientations."""
+    import crdts_hip
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot_tail(100_000, threads=16)
+    recs = records.unpack_batch(lb, lo)
+    big = [i for i in range(0, 100_000, 20)]
+    assert max(len(recs[i]) for i in big) > 16_384 and min(len(records.decode(recs[i])["entries"]) for i in big) > 64
+    for a, b in (((lb, lo), (rb, ro)), ((rb, ro), (lb, lo))):
+        out = _gpu_merge(gpu, *a, *b, 16)
+        ob, oo = oracle.orswot_merge_batch(*a, *b, 16, threads=16)
+        _compare(out, ob, oo, "heavy tail")
