@@ -102,14 +102,14 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
 // Byte offsets of one record's sections (wave-uniform), relative to its base.
 struct RV {
   uint32_t clk, cact, key, dctr, dact, mdend, fctr, fkey, fact, fdend, fmend;
-  uint32_t n_mem, n_def, n_clk;
+  uint32_t n_mem, n_def, n_clk, n_dm;  // (n_dm: deferred member entries, all clocks)
 };
 
 __device__ __forceinline__ RV make_rv(const RecLayout& L) {
   RV v;
   v.clk = L.o_clk; v.cact = L.o_cact; v.n_clk = L.n_clk; v.key = L.o_key; v.dctr = L.o_dctr; v.dact = L.o_dact; v.mdend = L.o_mdend;
   v.fctr = L.o_fctr; v.fkey = L.o_fkey; v.fact = L.o_fact; v.fdend = L.o_fdend; v.fmend = L.o_fmend;
-  v.n_mem = L.n_mem; v.n_def = L.n_def;
+  v.n_mem = L.n_mem; v.n_def = L.n_def; v.n_dm = L.n_def_mem;
   return v;
 }
 
@@ -191,7 +191,8 @@ __device__ __forceinline__ bool def_has_member(const S& s, uint32_t k, uint64_t 
 // apply_remove subtracts D from entries[m] for every (D, m) — whether or not
 // D is re-deferred — dropping dot (x, v) iff D[x] >= v (VClock::subtract,
 // src/vclock.rs:236-242). Order-independent, and duplicates are harmless.
-__device__ __forceinline__ bool killed(const Side& L, const Side& R, uint64_t m, uint32_t x, uint64_t v) {
+template <class S>
+__device__ __forceinline__ bool killed(const S& L, const S& R, uint64_t m, uint32_t x, uint64_t v) {
   for (uint32_t k = 0; k < L.v.n_def; ++k)
     if (def_has_member(L, k, m) && def_get(L, k, x) >= v) return true;
   for (uint32_t k = 0; k < R.v.n_def; ++k)
@@ -199,11 +200,22 @@ __device__ __forceinline__ bool killed(const Side& L, const Side& R, uint64_t m,
   return false;
 }
 
+// Whether member m appears in any deferred clock's member set of either
+// side: a linear pass over both flat fkey arrays (independent loads; both are
+// short), so killed() runs only for the members it can hit.
+template <class S>
+__device__ __forceinline__ bool in_any_deferred(const S& L, const S& R, uint64_t m) {
+  bool hit = false;
+  for (uint32_t k = 0; k < L.v.n_dm; ++k) hit = hit || g64(L.b, L.v.fkey, k) == m;
+  for (uint32_t k = 0; k < R.v.n_dm; ++k) hit = hit || g64(R.b, R.v.fkey, k) == m;
+  return hit;
+}
+
 // Merge path: the candidate at union position p (self first on ties).
 // Branch-free binary search with a fixed trip count (no per-lane loop
 // control): i = number of self keys among the first p union positions.
-__device__ __forceinline__ uint32_t merge_path(const Side& L, const Side& R, uint32_t p, uint32_t& i,
-                                               uint32_t& j) {
+template <class S>
+__device__ __forceinline__ uint32_t merge_path(const S& L, const S& R, uint32_t p, uint32_t& i, uint32_t& j) {
   const uint32_t nL = L.v.n_mem, nR = R.v.n_mem;
   uint32_t lo = p > nR ? p - nR : 0, len = (p < nL ? p : nL) - lo;
   const uint32_t steps = 32u - __builtin_clz(uni(nL < nR ? nL : nR) | 1u);  // >= log2(len + 1)
@@ -226,8 +238,8 @@ __device__ __forceinline__ uint32_t merge_path(const Side& L, const Side& R, uin
 // captures the first output dot in (x0, v0); MODE 1 also stores the run at
 // oact/octr[d0..]. Lc/Rc are the PRE-merge top clocks. One loop step per
 // actor of the union of both runs, branch-free inside.
-template <int MODE, bool SP = false>
-__device__ __forceinline__ uint32_t join(const Side& L, const Side& R, uint32_t type, uint32_t i,
+template <int MODE, bool SP = false, class S>
+__device__ __forceinline__ uint32_t join(const S& L, const S& R, uint32_t type, uint32_t i,
                                          uint32_t j, uint32_t A, bool has_def, uint32_t& x0, uint64_t& v0,
                                          uint32_t* oact, uint64_t* octr, uint32_t d0) {
   uint32_t a = 0, ae = 0, b = 0, be = 0;
@@ -241,7 +253,11 @@ __device__ __forceinline__ uint32_t join(const Side& L, const Side& R, uint32_t 
     if (!any) ae = a;
   }
   uint64_t m = 0;
-  if (has_def) m = (type & kSelf) ? g64(L.b, L.v.key, i) : g64(R.b, R.v.key, j);
+  bool mk = false;  // m is in some deferred member set: its dots face the kill test
+  if (has_def) {
+    m = (type & kSelf) ? g64(L.b, L.v.key, i) : g64(R.b, R.v.key, j);
+    mk = in_any_deferred(L, R, m);
+  }
   uint32_t c = 0;
   while (a < ae || b < be) {
     const bool ha = a < ae, hb = b < be;
@@ -260,7 +276,7 @@ __device__ __forceinline__ uint32_t join(const Side& L, const Side& R, uint32_t 
     uint64_t v = (ta && tb && va == vb) ? va : (lp > rp ? lp : rp);
     a += ta ? 1u : 0u;
     b += tb ? 1u : 0u;
-    if (v != 0 && has_def && killed(L, R, m, x, v)) v = 0;
+    if (v != 0 && mk && killed(L, R, m, x, v)) v = 0;
     if (v != 0) {
       if (MODE == 1) {
         oact[d0 + c] = x;
@@ -577,23 +593,21 @@ __device__ __forceinline__ void merge_object(const uint8_t* Ls, const uint8_t* R
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   for (uint32_t base = 0; base < P; base += kWave) {
     const uint32_t p = base + lane;
-    uint32_t q, cnt, x;
-    uint64_t v;
-    if (base == 0) { q = q0; cnt = c0; x = x0; v = v0; }
-    else if (base == kWave) { q = q1; cnt = c1; x = x1; v = v1; }
-    else {
-      uint32_t type = kNone, i = 0, j = 0;
-      cnt = 0; x = 0; v = 0;
-      if (p < P) {
-        type = merge_path(L, R, p, i, j);
-        if (type != kNone) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0);
-      }
-      q = (type << 30) | (i << 15) | j;
+    // (cached chunks: positions < 128, so i, j fit the 15-bit fields of q;
+    // later chunks keep i, j whole — a side may hold 32 768+ members)
+    uint32_t type = kNone, i = 0, j = 0, cnt = 0, x = 0;
+    uint64_t v = 0;
+    if (base < 2u * kWave) {
+      const uint32_t q = base == 0 ? q0 : q1;
+      cnt = base == 0 ? c0 : c1; x = base == 0 ? x0 : x1; v = base == 0 ? v0 : v1;
+      type = q >> 30; i = (q >> 15) & 0x7FFFu; j = q & 0x7FFFu;
+    } else if (p < P) {
+      type = merge_path(L, R, p, i, j);
+      if (type != kNone) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0);
     }
     const uint64_t keep = __ballot(cnt != 0);
     const uint32_t incl = wave_incl_scan(cnt, lane);
     if (cnt != 0) {
-      const uint32_t type = q >> 30, i = (q >> 15) & 0x7FFFu, j = q & 0x7FFFu;
       const uint32_t midx = mem_base + (uint32_t)__popcll(keep & lt_mask);
       const uint32_t d0 = dot_base + incl - cnt;
       okey[midx] = (type & kSelf) ? g64(Ls, L.v.key, i) : g64(Rs, R.v.key, j);
@@ -3264,6 +3278,14 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_ring_kern
 constexpr uint32_t kGenStage = 8192;
 constexpr uint32_t kGenBlocks = 512;
 
+// (the big-object kernel's share of the general list: see orswot_big_kernel)
+constexpr uint32_t kBigW = 8;           // waves per block
+constexpr uint32_t kBigStage = 32768;   // LDS stage per record
+
+__device__ __forceinline__ bool is_big(u32x4 hl0, u32x4 hr0) {
+  return hl0.z + hr0.z > 2u * kWave || hl0.x > kGenStage || hr0.x > kGenStage;
+}
+
 __device__ __forceinline__ void general_one(const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb,
                                             const uint64_t* Roff, uint8_t* Ob, uint64_t* Ooff, uint64_t o, uint32_t A,
                                             u32x4* sl, u32x4* sr, u32x4* so, uint32_t lane) {
@@ -3273,6 +3295,7 @@ __device__ __forceinline__ void general_one(const uint8_t* Lb, const uint64_t* L
   const u32x4 hl0 = ((const u32x4*)lr)[0], hl1 = ((const u32x4*)lr)[1];
   const u32x4 hr0 = ((const u32x4*)rr)[0], hr1 = ((const u32x4*)rr)[1];
   const uint32_t szl = uni(hl0.x), szr = uni(hr0.x);
+  if (is_big(u32x4{szl, 0u, uni(hl0.z), 0u}, u32x4{szr, 0u, uni(hr0.z), 0u})) return;  // orswot_big_kernel's
   if (szl <= kGenStage && szr <= kGenStage) {
     wave_sync();
     // both records staged 4 KB per side at a time: every load of a round is
@@ -3337,6 +3360,303 @@ __device__ __forceinline__ void general_one(const uint8_t* Lb, const uint64_t* L
   if (lane == 0) Ooff[o] = oo;
 }
 
+// ======================================================================
+// Big objects (round 5): the general path's objects with more than 128 union
+// positions or a record past the general stage (kGenStage) — the heavy tail
+// of a batch (the reference's entries map is unbounded, src/orswot.rs:26-30)
+// — joined by a whole workgroup of kBigW waves per object instead of one
+// wave: merge_object's two passes with the 64-position chunks of the member
+// union dealt round-robin to the waves. Between them a block-wide exclusive
+// scan of the per-chunk member / dot totals. A boundary table (the self-key
+// count at every 64th union position, one full merge-path search per chunk)
+// narrows each position's search to a 65-entry window (7 steps), and pass 1
+// leaves each position's candidate and dot count in LDS for pass 2 (which
+// then runs only the joins of kept members). Both records are staged in LDS
+// when each fits kBigStage; larger ones are read from HBM, the tables then
+// carved from the unused stage. Same rules and output as merge_object
+// (src/orswot.rs:87-157 with apply_deferred).
+// ======================================================================
+constexpr uint32_t kBigChS = 96;     // chunk capacity, staged records (<= 86 possible: 12 B a member at least)
+constexpr uint32_t kBigChH = 4096;   // chunk capacity, records from HBM (P <= 262 144; past it: one wave)
+constexpr uint32_t kBigPos = 4096;   // positions whose candidate / count pass 1 keeps in LDS
+
+struct BigTabs {
+  uint32_t* tot;  // 2 x cap: per-chunk kept members, then dots (then their exclusive prefixes)
+  uint32_t* spl;  // cap + 1: self keys before each chunk's first position
+  uint16_t* pq;   // kBigPos: (type << 14) | i of each position
+  uint8_t* pc;    // kBigPos: its joined dot count (255: count again)
+  uint32_t* bc;   // 4: grand totals
+  uint32_t cap;
+};
+
+// merge_path with the answer known to lie in [ilo, ihi], ihi - ilo <= 64.
+template <class S>
+__device__ __forceinline__ uint32_t merge_path_in(const S& L, const S& R, uint32_t p, uint32_t ilo, uint32_t ihi,
+                                                  uint32_t& i, uint32_t& j) {
+  const uint32_t nL = L.v.n_mem, nR = R.v.n_mem;
+  uint32_t lo = p > nR ? p - nR : 0u, hi = p < nL ? p : nL;
+  lo = lo > ilo ? lo : ilo;
+  hi = hi < ihi ? hi : ihi;
+  uint32_t len = hi > lo ? hi - lo : 0u;
+#pragma unroll
+  for (uint32_t s = 0; s < 7u; ++s) {
+    const uint32_t half = len >> 1, mid = lo + half;
+    const bool go = len != 0 && g64(L.b, L.v.key, mid) <= g64(R.b, R.v.key, p - 1 - mid);
+    lo = go ? mid + 1 : lo;
+    len = len == 0 ? 0 : (go ? len - half - 1 : half);
+  }
+  i = lo;
+  j = p - lo;
+  const uint64_t kl = i < nL ? g64(L.b, L.v.key, i) : ~0ull;
+  const uint64_t kr = j < nR ? g64(R.b, R.v.key, j) : ~0ull;
+  if (i < nL && (j >= nR || kl <= kr)) return (j < nR && kl == kr) ? kBoth : kSelf;
+  if (i > 0 && g64(L.b, L.v.key, i - 1) == kr) return kNone;  // twin of a kBoth at p-1
+  return kOther;
+}
+
+// (ABL, timing only in diag variants: 1 no kill test, 2 no deferred block,
+// 3 no pass 2, 4 no pass 1 join)
+template <bool SP, int ABL = 0, class S>
+__device__ __forceinline__ void merge_object_block(const S& L, const S& R, uint8_t* O, uint32_t A, uint32_t lane,
+                                                   uint32_t wave, const BigTabs& T) {
+  const bool has_def = ABL != 1 && (L.v.n_def | R.v.n_def) != 0;
+  const uint32_t P = L.v.n_mem + R.v.n_mem;
+  const uint32_t nch = (P + kWave - 1) / kWave;
+  uint32_t n_clk = A;
+  if constexpr (SP) n_clk = uni(sparse_clock_join(L, R, nullptr, 0u, lane));
+  // ---- chunk boundaries: the merge-path split at every 64th position
+  for (uint32_t c = threadIdx.x; c <= nch; c += kWave * kBigW) {
+    const uint32_t p = kWave * c < P ? kWave * c : P;
+    uint32_t i, j;
+    merge_path(L, R, p, i, j);
+    T.spl[c] = i;
+  }
+  __syncthreads();
+  // ---- pass 1: per chunk (64 union positions) its kept members and dots;
+  // a wave's first two chunks stay in registers for pass 2, every position
+  // below kBigPos leaves its candidate and count in LDS
+  uint32_t q0 = 0, c0 = 0, x0 = 0, q1 = 0, c1 = 0, x1 = 0;
+  uint64_t v0 = 0, v1 = 0;
+  for (uint32_t ch = wave, k = 0; ch < nch; ch += kBigW, ++k) {
+    const uint32_t p = kWave * ch + lane;
+    const uint32_t ilo = uni(T.spl[ch]), ihi = uni(T.spl[ch + 1]);
+    uint32_t type = kNone, i = 0, j = 0, cnt = 0, x = 0;
+    uint64_t v = 0;
+    if (p < P) {
+      type = merge_path_in(L, R, p, ilo, ihi, i, j);
+      if (ABL == 4) cnt = type != kNone;
+      else if (type != kNone) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0);
+      if (p < kBigPos) {
+        T.pq[p] = (uint16_t)((type << 14) | i);
+        T.pc[p] = (uint8_t)(cnt < 255u ? cnt : 255u);
+      }
+    }
+    const uint32_t q = (type << 30) | (i << 15) | j;  // (k < 2: p < 1024)
+    if (k == 0) { q0 = q; c0 = cnt; x0 = x; v0 = v; }
+    else if (k == 1) { q1 = q; c1 = cnt; x1 = x; v1 = v; }
+    const uint32_t m = (uint32_t)__popcll(__ballot(cnt != 0)), d = wave_sum(cnt);
+    if (lane == 0u) { T.tot[ch] = m; T.tot[T.cap + ch] = d; }
+  }
+  __syncthreads();
+  // ---- exclusive prefix of the chunk totals (wave 0), and the grand totals
+  if (wave == 0u) {
+    uint32_t cm = 0, cd = 0;
+    for (uint32_t b = 0; b < nch; b += kWave) {
+      const uint32_t ch = b + lane;
+      const uint32_t m = ch < nch ? T.tot[ch] : 0u, d = ch < nch ? T.tot[T.cap + ch] : 0u;
+      const uint32_t im = wave_incl_scan(m, lane), id = wave_incl_scan(d, lane);
+      if (ch < nch) { T.tot[ch] = cm + im - m; T.tot[T.cap + ch] = cd + id - d; }
+      cm += lane_of(im, kWave - 1);
+      cd += lane_of(id, kWave - 1);
+    }
+    if (lane == 0u) { T.bc[0] = cm; T.bc[1] = cd; }
+  }
+  __syncthreads();
+  const uint32_t tot_mem = uni(T.bc[0]), tot_dot = uni(T.bc[1]);
+  const uint32_t o_key = kHdrBytes + clock_bytes(n_clk, SP);
+  const uint32_t o_dctr = o_key + 8u * tot_mem;
+  const uint32_t o_dact = o_dctr + 8u * tot_dot;
+  const uint32_t o_mdend = o_dact + 4u * tot_dot;
+  const uint32_t o_mpad = o_mdend + 4u * tot_mem;
+  const uint32_t o_def = (o_mpad + 7u) & ~7u;
+  uint64_t* okey = (uint64_t*)(O + o_key);
+  uint64_t* odctr = (uint64_t*)(O + o_dctr);
+  uint32_t* odact = (uint32_t*)(O + o_dact);
+  uint32_t* omdend = (uint32_t*)(O + o_mdend);
+  // top clock: pointwise max (src/orswot.rs:153 -> src/vclock.rs:131-137)
+  if constexpr (SP) {
+    if (wave == 0u) {
+      sparse_clock_join(L, R, O, n_clk, lane);
+      if (lane == 0u && (n_clk & 1u)) *(uint32_t*)(O + kHdrBytes + 12u * n_clk) = 0u;  // pad to 8
+    }
+  } else {
+    for (uint32_t a = wave * kWave + lane; a < A; a += kBigW * kWave) {
+      const uint64_t x = g64(L.b, L.v.clk, a), y = g64(R.b, R.v.clk, a);
+      ((uint64_t*)(O + kHdrBytes))[a] = x > y ? x : y;
+    }
+  }
+  // ---- pass 2: kept members and their joined dot runs at their chunk's base
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  for (uint32_t ch = wave, k = 0; ch < (ABL == 3 ? 0u : nch); ch += kBigW, ++k) {
+    const uint32_t p = kWave * ch + lane;
+    uint32_t type = kNone, i = 0, j = 0, cnt = 0, x = 0;
+    uint64_t v = 0;
+    bool xv = false;  // (x, v) hold the run's only dot
+    if (k < 2u) {
+      const uint32_t q = k == 0 ? q0 : q1;
+      cnt = k == 0 ? c0 : c1; x = k == 0 ? x0 : x1; v = k == 0 ? v0 : v1;
+      type = q >> 30; i = (q >> 15) & 0x7FFFu; j = q & 0x7FFFu;
+      xv = true;
+    } else if (p < P && p < kBigPos) {
+      const uint32_t u = T.pq[p];
+      type = u >> 14; i = u & 0x3FFFu; j = p - i;
+      cnt = T.pc[p];
+      if (cnt == 255u) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0);
+    } else if (p < P) {
+      type = merge_path_in(L, R, p, uni(T.spl[ch]), uni(T.spl[ch + 1]), i, j);
+      if (type != kNone) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0);
+      xv = true;
+    }
+    const uint64_t keep = __ballot(cnt != 0);
+    const uint32_t incl = wave_incl_scan(cnt, lane);
+    const uint32_t mem_base = uni(T.tot[ch]), dot_base = uni(T.tot[T.cap + ch]);
+    if (cnt != 0) {
+      const uint32_t midx = mem_base + (uint32_t)__popcll(keep & lt_mask);
+      const uint32_t d0 = dot_base + incl - cnt;
+      okey[midx] = (type & kSelf) ? g64(L.b, L.v.key, i) : g64(R.b, R.v.key, j);
+      if (cnt == 1 && xv) {
+        odact[d0] = x;
+        odctr[d0] = v;
+      } else {
+        join<1, SP>(L, R, type, i, j, A, has_def, x, v, odact, odctr, d0);
+      }
+      omdend[midx] = d0 + cnt;
+    }
+  }
+  // ---- deferred block + header + padding (wave 0; the deferred walk wave-cooperative)
+  if (wave == 0u) {
+    uint32_t nd = 0, ndd = 0, ndm = 0;
+    if (lane == 0u && o_def != o_mpad) *(uint32_t*)(O + o_mpad) = 0u;
+    if (ABL != 2 && has_def) {
+      deferred_pass_wave<SP>(L, R, A, lane, nd, ndd, ndm, nullptr);
+      RecLayout OL;
+      rec_layout(OL, n_clk, tot_mem, tot_dot, nd, ndd, ndm, SP);
+      DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
+               (uint32_t*)(O + OL.o_fdend), (uint32_t*)(O + OL.o_fmend)};
+      deferred_pass_wave<SP>(L, R, A, lane, nd, ndd, ndm, &w);
+    }
+    if (lane == 0u) {
+      RecLayout OL;
+      rec_layout(OL, n_clk, tot_mem, tot_dot, nd, ndd, ndm, SP);
+      for (uint32_t b = OL.o_end; b < OL.size; b += 4) *(uint32_t*)(O + b) = 0u;
+      u32x4* h = (u32x4*)O;
+      h[0] = u32x4{OL.size, n_clk, tot_mem, tot_dot};
+      h[1] = u32x4{nd, ndd, ndm, SP ? kSparseClock : 0u};
+    }
+  }
+  __syncthreads();  // the stages and the tables are free for the next object
+}
+
+template <bool SP, int ABL>
+__device__ __noinline__ void big_from_hbm(const uint8_t* lr, const uint8_t* rr, uint8_t* O, uint32_t A,
+                                          uint32_t lane, uint32_t wave, u32x4* st, uint32_t* bc) {
+  uint8_t* sb = (uint8_t*)st;
+  const BigTabs H{(uint32_t*)sb, (uint32_t*)(sb + 8u * kBigChH), (uint16_t*)(sb + 12u * kBigChH + 16u),
+                  (uint8_t*)(sb + 12u * kBigChH + 16u + 2u * kBigPos), bc, kBigChH};
+  static_assert(12u * kBigChH + 16u + 3u * kBigPos <= 2u * kBigStage, "HBM-path tables fit the stage");
+  const RecLayout LL = layout_at(lr), RL = layout_at(rr);
+  const Side L{lr, make_rv(LL)}, R{rr, make_rv(RL)};
+  merge_object_block<SP, ABL>(L, R, O, A, lane, wave, H);
+}
+template <bool SP>
+__device__ __noinline__ void huge_one_wave(const uint8_t* lr, const uint8_t* rr, uint8_t* O, uint32_t A,
+                                           uint32_t lane) {
+  merge_object<SP>(lr, rr, O, A, lane);
+}
+
+// One big object o (listed for the general path) joined by the whole block.
+// st: the 2 x kBigStage stage; T: the staged path's tables.
+template <bool SP, int ABL = 0>
+__device__ __forceinline__ void big_one(const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb,
+                                        const uint64_t* Roff, uint8_t* Ob, uint64_t* Ooff, uint64_t o, uint32_t A,
+                                        u32x4* st, const BigTabs& T, uint32_t lane, uint32_t wave) {
+  const uint64_t oo = Ooff[o] & ~kPending;
+  const uint8_t* lr = Lb + Loff[o];
+  const uint8_t* rr = Rb + Roff[o];
+  const RecLayout LL = layout_at(lr), RL = layout_at(rr);
+  const uint32_t szl = LL.size, szr = RL.size, P = LL.n_mem + RL.n_mem;
+  if (P > kWave * kBigChH) {  // (past the HBM tables: one wave, merge_object)
+    if (wave == 0u) huge_one_wave<SP>(lr, rr, Ob + oo, A, lane);
+  } else if (szl <= kBigStage && szr <= kBigStage && P <= kWave * kBigChS) {
+    // both records staged: every load of the thread issued before its stores
+    u32x4* sl = st;
+    u32x4* sr = st + kBigStage / 16u;
+    constexpr uint32_t kPer = kBigStage / 16u / (kWave * kBigW);
+    const uint32_t nl = szl / 16u, nr = szr / 16u;
+    u32x4 tl[kPer], tr[kPer];
+#pragma unroll
+    for (uint32_t u = 0; u < kPer; ++u) {
+      const uint32_t k = threadIdx.x + u * kWave * kBigW;
+      if (k < nl) tl[u] = ((const u32x4*)lr)[k];
+      if (k < nr) tr[u] = ((const u32x4*)rr)[k];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kPer; ++u) {
+      const uint32_t k = threadIdx.x + u * kWave * kBigW;
+      if (k < nl) sl[k] = tl[u];
+      if (k < nr) sr[k] = tr[u];
+    }
+    __syncthreads();
+    const SideL L{(lds_cu8*)(size_t)lds_addr(sl), make_rv(LL)}, R{(lds_cu8*)(size_t)lds_addr(sr), make_rv(RL)};
+    if constexpr (ABL != 5) merge_object_block<SP, ABL>(L, R, Ob + oo, A, lane, wave, T);  // (5: staging only)
+  } else {  // from HBM; the tables in the stage
+    big_from_hbm<SP, ABL>(lr, rr, Ob + oo, A, lane, wave, st, T.bc);
+  }
+  if (threadIdx.x == 0u) Ooff[o] = oo;
+  __syncthreads();
+}
+
+// The listed objects is_big() picks (the general kernel, launched before,
+// skipped them), one block per object. With an overflowed list every pending
+// flag left is one.
+template <bool SP, int MINW = 4, int ABL = 0>
+__global__ __launch_bounds__(kWave * kBigW, MINW) void orswot_big_kernel(
+    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, const uint8_t* __restrict__ Rb,
+    const uint64_t* __restrict__ Roff, uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t n_obj,
+    uint32_t A, uint32_t* __restrict__ ctl, const uint64_t* __restrict__ list, uint32_t list_cap) {
+  __shared__ u32x4 st_s[2 * kBigStage / 16];
+  __shared__ uint32_t tot_s[2 * kBigChS], spl_s[kBigChS + 4], bc_s[4];
+  __shared__ uint16_t pq_s[kBigPos];
+  __shared__ uint8_t pc_s[kBigPos];
+  const BigTabs T{tot_s, spl_s, pq_s, pc_s, bc_s, kBigChS};
+  const uint32_t lane = threadIdx.x & (kWave - 1), wave = uni(threadIdx.x / kWave);
+  const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const uint32_t scan = uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (n == 0u) return;
+  // listed: the list in 64-entry chunks dealt round-robin to the blocks (no
+  // ticket: every control word is some join variant's), each wave reading
+  // the chunk's headers; list overflow / unlisted flags: every pending object
+  // left is big. The block takes its chunk's big objects in order.
+  const bool listed = n <= list_cap && scan == 0u;
+  const uint64_t n_chunks = ((listed ? (uint64_t)n : n_obj) + kWave - 1) / kWave;
+  for (uint64_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+    const uint64_t e = c * kWave + lane;
+    bool big = false;
+    uint64_t o = e;
+    if (listed) {
+      if (e < n) {
+        o = list[e];
+        big = is_big(((const u32x4*)(Lb + Loff[o]))[0], ((const u32x4*)(Rb + Roff[o]))[0]);
+      }
+    } else {
+      big = e < n_obj && (Ooff[e] & kPending) != 0ull;
+    }
+    for (uint64_t m = __ballot(big); m; m &= m - 1)
+      big_one<SP, ABL>(Lb, Loff, Rb, Roff, Ob, Ooff, lane_of64(o, (uint32_t)__builtin_ctzll(m)), A, st_s, T, lane,
+                       wave);
+  }
+}
+
 __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, const uint8_t* __restrict__ Rb,
     const uint64_t* __restrict__ Roff, uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t n_obj,
@@ -3367,6 +3687,32 @@ __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
                     gen_s[1], gen_s[2], lane);
     }
   }
+}
+
+constexpr uint32_t kBigBlocks = 512;  // two 8-wave, 72 KB-LDS blocks per CU
+#ifdef CRDT_DIAG
+int g_big_variant = 0;  // diag variants 330..: the big kernel's knobs
+#endif
+
+// The big-object pass, queued after every general kernel launch (the objects
+// it leaves flagged are this kernel's).
+__host__ inline hipError_t launch_big(const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb, const uint64_t* Roff,
+                                      uint8_t* Ob, uint64_t* Ooff, uint64_t n_obj, uint32_t A, uint32_t* ctl,
+                                      const uint64_t* list, uint32_t list_cap, hipStream_t stream) {
+  const void* fn = (const void*)orswot_big_kernel<false, 4>;
+  uint32_t blocks = kBigBlocks;
+#ifdef CRDT_DIAG
+  if (g_big_variant == 1) { fn = (const void*)orswot_big_kernel<false, 1>; blocks = 256; }
+  if (g_big_variant == 2) { fn = (const void*)orswot_big_kernel<false, 2>; blocks = 256; }
+  if (g_big_variant == 3) blocks = 256;
+  if (g_big_variant == 4) fn = (const void*)orswot_big_kernel<false, 4, 1>;
+  if (g_big_variant == 5) fn = (const void*)orswot_big_kernel<false, 4, 2>;
+  if (g_big_variant == 6) fn = (const void*)orswot_big_kernel<false, 4, 3>;
+  if (g_big_variant == 7) fn = (const void*)orswot_big_kernel<false, 4, 4>;
+  if (g_big_variant == 8) fn = (const void*)orswot_big_kernel<false, 4, 5>;
+#endif
+  void* args[] = {&Lb, &Loff, &Rb, &Roff, &Ob, &Ooff, &n_obj, &A, &ctl, &list, &list_cap};
+  return hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kBigW), args, 0, stream);
 }
 
 // ======================================================================
@@ -3670,6 +4016,8 @@ int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
   hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
                      Ob, Ooff, n_obj, n_actors, set, list, list_cap, other);
   if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
+  if (launch_big(Lb, Loff, Rb, Roff, Ob, Ooff, n_obj, n_actors, set, list, list_cap, stream) != hipSuccess)
+    return CRDT_EHIP;
   if (NM) {
     ++js->seq;
     js->dirty = false;
@@ -3726,6 +4074,8 @@ int launch_join_kernel(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
   hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff, Ob,
                      Ooff, n_obj, n_actors, set, list, list_cap, other);
   if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
+  if (launch_big(Lb, Loff, Rb, Roff, Ob, Ooff, n_obj, n_actors, set, list, list_cap, stream) != hipSuccess)
+    return CRDT_EHIP;
   ++js->seq;
   js->dirty = false;
   return CRDT_OK;
@@ -3760,6 +4110,13 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // every object whose clock union holds <= 64 present actors takes the
   // sparse mask join in its dense form (DN), the rest the general kernel
   // (diag variant 320: every such object to the general kernel, as before)
+#ifdef CRDT_DIAG
+  g_big_variant = 0;
+  if (variant >= 330 && variant < 340) {  // the big-object kernel's knobs, after the join5 product
+    g_big_variant = variant - 330;
+    variant = 310;
+  }
+#endif
   if (n_actors > 64u && n_actors <= kSpTableN && variant != 320) return go(launch_dense_wide);
 #ifndef CRDT_DIAG
   // The product path: orswot_join5_kernel — one pass (mask3_object for every
@@ -3924,7 +4281,10 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   if (variant == 109 || variant == 14 || variant == 16) return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
   hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
                      Ob, Ooff, n_obj, n_actors, ctl, list, list_cap, nullptr);
-  return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
+  if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
+  return launch_big(Lb, Loff, Rb, Roff, Ob, Ooff, n_obj, n_actors, ctl, list, list_cap, stream) == hipSuccess
+             ? CRDT_OK
+             : CRDT_EHIP;
 #endif
 }
 

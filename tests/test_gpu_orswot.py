@@ -521,3 +521,61 @@ def test_heavy_tail_100k(gpu, oracle):
         out = _gpu_merge(gpu, *a, *b, 16)
         ob, oo = oracle.orswot_merge_batch(*a, *b, 16, threads=16)
         _compare(out, ob, oo, "heavy tail")
+
+
+def _synth_heavy_pair(rng, n, n_actors=16, n_def=4):
+    """One op-shaped pair of n-member Orswots from a common ancestor (one dot
+    per member, top clock = per-actor max): self adds / removes as actors
+    0-7, other as 8-15, and each side defers n_def removes whose context
+    runs ahead of it on the other side's actors — the reference's
+    remove-before-add case (src/orswot.rs:197-203). Built directly as records
+    (the op simulator takes minutes at 100k+ members)."""
+    pool = rng.choice(1 << 40, size=int(n * 1.25), replace=False).astype(np.uint64).tolist()
+    anc, fresh = pool[:n], pool[n:]
+    ctr = [0] * n_actors
+    ent = {}
+    for m, a in zip(anc, rng.integers(0, n_actors, size=n).tolist()):
+        ctr[a] += 1
+        ent[m] = {a: ctr[a]}
+    sides = []
+    for lo_a, hi_a in ((0, n_actors // 2), (n_actors // 2, n_actors)):
+        c = list(ctr)
+        e = {m: dict(d) for m, d in ent.items()}
+        n_add = n // 6
+        for m in rng.choice(anc, size=n_add, replace=False).tolist() + fresh[lo_a * 1000:lo_a * 1000 + n // 20]:
+            a = int(rng.integers(lo_a, hi_a))
+            c[a] += 1
+            e.setdefault(m, {})[a] = c[a]
+        for m in rng.choice(anc, size=n // 10, replace=False).tolist():
+            e.pop(m, None)
+        deferred = {}
+        for _ in range(n_def):
+            a = int(rng.integers(n_actors // 2 - lo_a, n_actors - lo_a)) % n_actors  # an actor of the other side
+            ctx = tuple(sorted({a: ctr[a] + int(rng.integers(1, n // 8 + 2))}.items()))
+            deferred[ctx] = set(rng.choice(anc, size=3, replace=False).tolist())
+        clock = {a: v for a, v in enumerate(c) if v}
+        sides.append(records.encode(clock, e, deferred, n_actors))
+    return sides
+
+
+def test_big_kernel_paths(gpu, oracle):
+    """orswot_big_kernel's three paths, byte-exact against the oracle, both
+    orientations: records staged in LDS (<= 32 KB a side), records joined
+    from HBM with the tables in the stage (P <= 262 144 union positions), and
+    past those tables one wave (merge_object), next to config-3 pairs."""
+    import crdts_hip
+
+    rng = np.random.default_rng(0xB16)
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(40, threads=4)
+    Ls, Rs = records.unpack_batch(lb, lo), records.unpack_batch(rb, ro)
+    for k, n in enumerate((150, 700, 1200, 3000, 20000, 150000)):
+        a, b = _synth_heavy_pair(rng, n, n_def=4 + 8 * (k % 2))
+        Ls[5 * k + 1], Rs[5 * k + 1] = a, b
+    sizes = sorted(len(r) for r in Ls)
+    assert sizes[-1] > 3_000_000 and sizes[-3] > 32768
+    lb, lo = records.pack_batch(Ls)
+    rb, ro = records.pack_batch(Rs)
+    for x, y in (((lb, lo), (rb, ro)), ((rb, ro), (lb, lo))):
+        out = _gpu_merge(gpu, *x, *y, 16)
+        ob, oo = oracle.orswot_merge_batch(*x, *y, 16, threads=8)
+        _compare(out, ob, oo, "big kernel paths")

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--n-obj", type=int, default=1_000_000)
     ap.add_argument("--check", default="", help="variants >= 100 whose output is also compared byte for byte")
     ap.add_argument("--n-actors", type=int, default=16, help="dense top-clock actors (config 3: 16)")
+    ap.add_argument("--tail", action="store_true", help="bench.py's orswot_tail batch (heavy-tailed config 3)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -28,8 +29,11 @@ def main():
     import crdts_hip
 
     A = a.n_actors
-    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(a.n_obj, threads=16, **({} if A == 16 else {
-        "seed": 0xC0FFEE03 + A, "params": {"n_actors": A}}))
+    if a.tail:
+        (lb, lo), (rb, ro) = crdts_hip.generate_orswot_tail(a.n_obj, threads=16)
+    else:
+        (lb, lo), (rb, ro) = crdts_hip.generate_orswot(a.n_obj, threads=16, **({} if A == 16 else {
+            "seed": 0xC0FFEE03 + A, "params": {"n_actors": A}}))
     eng = crdts_hip.Engine(0)
     L = crdts_hip.OrswotBatch.from_host(lb, lo, A)
     R = crdts_hip.OrswotBatch.from_host(rb, ro, A)
