@@ -300,8 +300,9 @@ def run_orswot(args, rank, world, local):
     achieved_rec = rec_bytes / (kernel_ms * 1e-3) / 1e9
     # measured HBM bytes of one launch (both kernels of the timed window), from
     # the FETCH_SIZE / WRITE_SIZE passes of tools/profile.sh -> tools/traffic.py
-    tk = [load_traffic(args.traffic_json, k) for k in ("orswot_join_kernel", "orswot_merge_general_kernel")]
-    traffic = None if args.n_obj is not None or A != 16 or tail or tk[0] is None else tk[0] + (tk[1] or 0.0)
+    tk = [load_traffic(args.traffic_json, k)
+          for k in ("orswot_join_kernel", "orswot_merge_general_kernel", "orswot_big_kernel")]
+    traffic = None if args.n_obj is not None or A != 16 or tail or tk[0] is None else tk[0] + sum(t or 0.0 for t in tk[1:])
     res = {
         "metric": METRIC,
         "value": value,
@@ -334,8 +335,9 @@ def run_orswot(args, rank, world, local):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": ("orswot_join5_kernel" if A <= 64 else "orswot_sparse_mask_kernel<DN>")
-                      + " (+ orswot_merge_general_kernel in the same window)",
+            "kernel": ("orswot_big_kernel (+ orswot_join5_kernel, orswot_merge_general_kernel in the same window)"
+                       if tail else ("orswot_join5_kernel" if A <= 64 else "orswot_sparse_mask_kernel<DN>")
+                       + " (+ orswot_merge_general_kernel, orswot_big_kernel in the same window)"),
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

@@ -35,9 +35,9 @@ namespace crdts_hip {
 namespace {
 
 constexpr uint32_t kMoW = 64;
-constexpr uint32_t kMoComb = 64;       // combined map deferred entries (<= dcap_self + dcap_other)
+constexpr uint32_t kMoComb = 64;       // the nested sets' deferred entries of a workspace (<= vdcap_s + vdcap_o)
 constexpr uint32_t kMoLdsMax = 65536;  // workspace limit per wave
-constexpr uint32_t kMoStageMax = 4096;  // map deferred staging area limit per wave
+constexpr uint32_t kMoStageMax = 16384;  // map deferred staging area limit per wave
 
 __device__ __forceinline__ void mo_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -297,9 +297,7 @@ __global__ __launch_bounds__(kMoW, MINW) void map_orswot_merge_kernel(crdt_map_o
                                                                 uint32_t md_cap, int* __restrict__ status,
                                                                 uint32_t* __restrict__ ctl) {
   extern __shared__ uint64_t mo_lds[];
-  __shared__ uint32_t comb[kMoComb];  // (self deferred idx + 1) | (other deferred idx + 1) << 8
   __shared__ uint32_t dn_s[3][kMoComb];  // the three workspaces' deferred set sizes
-  __shared__ uint32_t mdn[2][32];        // the object's map deferred set sizes (dcap <= 32), self / other
   const uint32_t lane = threadIdx.x;
   const Caps c{S.mcap + O.mcap, S.vdcap + O.vdcap, S.vscap + O.vscap, A};
   // workspaces: self's key slot (W0), other's (W2), their merge (W1); then the
@@ -325,6 +323,14 @@ __global__ __launch_bounds__(kMoW, MINW) void map_orswot_merge_kernel(crdt_map_o
     for (uint32_t j = lane; j < c.MW + c.DW; j += kMoW) mdead[j] = 0u;
     md = p + (c.MW + c.DW + 1u) / 2u;
   }
+  // the map deferred bookkeeping (dcap_s + dcap_o <= 512 entries each, after
+  // the staging area): the combined list, (self deferred idx + 1) | (other
+  // deferred idx + 1) << 16; both sides' set sizes; the entries naming a key
+  const uint32_t DC = S.dcap + O.dcap;
+  uint32_t* const comb = (uint32_t*)(md + md_cap);
+  uint32_t* const mdn0 = comb + DC;
+  uint32_t* const mdn1 = mdn0 + S.dcap;
+  uint32_t* const nl = mdn0 + DC;
   uint32_t* const ddead = mdead + c.MW;
   mo_sync();
   BlockTickets<4> sched(n_obj, ctl + 3, lane);  // (sched.h)
@@ -366,14 +372,21 @@ __global__ __launch_bounds__(kMoW, MINW) void map_orswot_merge_kernel(crdt_map_o
       bad = bad || O.vn_mem[ki] > O.mcap || O.vn_def[ki] > O.vdcap;
       for (uint32_t d = 0; !bad && d < O.vn_def[ki]; ++d) bad = O.vdset_n[ki * O.vdcap + d] > O.vscap;
     }
-    // (dS, dO <= dcap <= 32: one lane per deferred entry)
-    const uint32_t nsS = lane < dS ? S.dset_n[i * S.dcap + lane] : 0u, nsO = lane < dO ? O.dset_n[i * O.dcap + lane] : 0u;
-    bad = bad || nsS > S.scap || nsO > O.scap;
+    // the map deferred set sizes, one lane per entry
+    for (uint32_t d = lane; d < dS; d += kMoW) {
+      const uint32_t x = S.dset_n[i * S.dcap + d];
+      mdn0[d] = x;
+      bad = bad || x > S.scap;
+    }
+    for (uint32_t d = lane; d < dO; d += kMoW) {
+      const uint32_t x = O.dset_n[i * O.dcap + d];
+      mdn1[d] = x;
+      bad = bad || x > O.scap;
+    }
     if (__ballot(bad) != 0ull) {
       if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
       continue;
     }
-    if (lane < 32u) { mdn[0][lane] = nsS; mdn[1][lane] = nsO; }
     mo_sync();
     // the map deferred sets staged in LDS when they fit (md_cap words): the
     // key loop asks each of them about every key. (Staging their clocks too
@@ -385,11 +398,11 @@ __global__ __launch_bounds__(kMoW, MINW) void map_orswot_merge_kernel(crdt_map_o
     if (st) {  // the used entries of each set
       for (uint32_t e = lane; e < dS * sS; e += kMoW) {
         const uint32_t d = e / sS;
-        if (e - d * sS < mdn[0][d]) mdS[e] = S.dset[i * S.dcap * sS + e];
+        if (e - d * sS < mdn0[d]) mdS[e] = S.dset[i * S.dcap * sS + e];
       }
       for (uint32_t e = lane; e < dO * sO; e += kMoW) {
         const uint32_t d = e / sO;
-        if (e - d * sO < mdn[1][d]) mdO[e] = O.dset[i * O.dcap * sO + e];
+        if (e - d * sO < mdn1[d]) mdO[e] = O.dset[i * O.dcap * sO + e];
       }
     }
     mo_sync();
@@ -406,7 +419,7 @@ __global__ __launch_bounds__(kMoW, MINW) void map_orswot_merge_kernel(crdt_map_o
         if (a >= dS) o = 1;
         else if (b >= dO) o = -1;
         else o = vorder(sdc(a), odc(b), lane);
-        if (lane == 0u) comb[nc] = (o <= 0 ? a + 1u : 0u) | ((o >= 0 ? b + 1u : 0u) << 8);
+        if (lane == 0u) comb[nc] = (o <= 0 ? a + 1u : 0u) | ((o >= 0 ? b + 1u : 0u) << 16);
         ++nc;
         if (o <= 0) ++a;
         if (o >= 0) ++b;
@@ -414,22 +427,26 @@ __global__ __launch_bounds__(kMoW, MINW) void map_orswot_merge_kernel(crdt_map_o
     }
     mo_sync();
     auto comb_clock = [&](uint32_t e) -> Row<NS> {
-      const uint32_t sa = e & 255u, sb = e >> 8;
+      const uint32_t sa = e & 0xFFFFu, sb = e >> 16;
       return sa ? sdc(sa - 1u) : odc(sb - 1u);
     };
-    // the combined entries naming `key`, as a bit mask over the list
-    auto comb_named = [&](uint64_t key) -> uint64_t {
-      uint64_t named = 0ull;
+    // the combined entries naming `key`, ascending, into nl; returns their count
+    auto comb_named = [&](uint64_t key) -> uint32_t {
+      uint32_t nn = 0;
       for (uint32_t k = 0; k < nc; ++k) {
-        const uint32_t e = comb[k], sa = e & 255u, sb = e >> 8;
+        const uint32_t e = uni(comb[k]), sa = e & 0xFFFFu, sb = e >> 16;
         bool f = false;
         if (sa)
-          f = set_has(st ? mdS + (sa - 1u) * sS : S.dset + (i * S.dcap + sa - 1u) * sS, mdn[0][sa - 1u], key, lane);
+          f = set_has(st ? mdS + (sa - 1u) * sS : S.dset + (i * S.dcap + sa - 1u) * sS, uni(mdn0[sa - 1u]), key, lane);
         if (!f && sb)
-          f = set_has(st ? mdO + (sb - 1u) * sO : O.dset + (i * O.dcap + sb - 1u) * sO, mdn[1][sb - 1u], key, lane);
-        named |= f ? 1ull << k : 0ull;
+          f = set_has(st ? mdO + (sb - 1u) * sO : O.dset + (i * O.dcap + sb - 1u) * sO, uni(mdn1[sb - 1u]), key, lane);
+        if (f) {
+          if (lane == 0u) nl[nn] = k;
+          ++nn;
+        }
       }
-      return named;
+      mo_sync();
+      return nn;
     };
     // ---- entries, key by key in ascending order
     uint32_t nk = 0, a = 0, b = 0;
@@ -464,9 +481,9 @@ __global__ __launch_bounds__(kMoW, MINW) void map_orswot_merge_kernel(crdt_map_o
       bool keep = vany(ec);
       // apply_deferred: the entry clock loses every combined clock naming the key
       // (subtracts commute; an entry emptied at any step is gone for good)
-      const uint64_t named = keep && nc ? comb_named(ckey) : 0ull;
+      const uint32_t nn = keep && nc ? comb_named(ckey) : 0u;
       if (keep) {
-        for (uint64_t m = named; m; m &= m - 1) ec = vsub(ec, comb_clock(comb[__builtin_ctzll(m)]));
+        for (uint32_t t = 0; t < nn; ++t) ec = vsub(ec, comb_clock(uni(comb[uni(nl[t])])));
         keep = vany(ec);
       }
       if (keep && nk >= R.kcap) {
@@ -489,8 +506,8 @@ __global__ __launch_bounds__(kMoW, MINW) void map_orswot_merge_kernel(crdt_map_o
         // ... truncated by the removers' clock (Map::merge), then by each deferred
         // clock naming the key, in CLOCK ORDER (apply_deferred -> apply_rm)
         ws_truncate(Wk, vclk, del, mdead, ddead, c, lane);
-        for (uint64_t m = named; m; m &= m - 1)
-          ws_truncate(Wk, vclk, comb_clock(comb[__builtin_ctzll(m)]), mdead, ddead, c, lane);
+        for (uint32_t t = 0; t < nn; ++t)
+          ws_truncate(Wk, vclk, comb_clock(uni(comb[uni(nl[t])])), mdead, ddead, c, lane);
         const uint64_t ir = i * R.kcap + nk;
         if (ws_store(Wk, vclk, R, ir, c, lane)) {
           if (lane == 0u) R.keys[ir] = ckey;
@@ -507,8 +524,8 @@ __global__ __launch_bounds__(kMoW, MINW) void map_orswot_merge_kernel(crdt_map_o
     // ---- map deferred kept: the combined clocks the merged clock does not cover, sets united
     uint32_t nd = 0;
     for (uint32_t k = 0; k < nc; ++k) {
-      const uint32_t e = comb[k];
-      const uint32_t sa = e & 255u, sb = e >> 8;
+      const uint32_t e = uni(comb[k]);
+      const uint32_t sa = e & 0xFFFFu, sb = e >> 16;
       const Row<NS> D = comb_clock(e);
       if (vle(D, cM)) continue;
       if (nd >= R.dcap) { over = true; break; }
@@ -518,7 +535,7 @@ __global__ __launch_bounds__(kMoW, MINW) void map_orswot_merge_kernel(crdt_map_o
       if (lane == 0u) {  // sorted union of the two key sets
         const uint64_t* xs = sa ? (st ? mdS + (sa - 1u) * sS : S.dset + (i * S.dcap + sa - 1u) * sS) : nullptr;
         const uint64_t* ys = sb ? (st ? mdO + (sb - 1u) * sO : O.dset + (i * O.dcap + sb - 1u) * sO) : nullptr;
-        const uint32_t nx = sa ? mdn[0][sa - 1u] : 0u, ny = sb ? mdn[1][sb - 1u] : 0u;
+        const uint32_t nx = sa ? mdn0[sa - 1u] : 0u, ny = sb ? mdn1[sb - 1u] : 0u;
         uint32_t p = 0, q = 0;
         while (p < nx || q < ny) {
           const uint64_t kx = p < nx ? xs[p] : ~0ull, ky = q < ny ? ys[q] : ~0ull;
@@ -542,12 +559,14 @@ __global__ __launch_bounds__(kMoW, MINW) void map_orswot_merge_kernel(crdt_map_o
 }  // namespace
 
 // The kernel's dynamic workspace: self's and other's key slots and their
-// merge (W0, W2, W1), the drop flags (the deferred set sizes are static LDS).
-// This is the bound crdt_map_orswot_merge checks against 64 KB.
+// merge (W0, W2, W1), the drop flags, the map deferred bookkeeping (3 x
+// (dcap_s + dcap_o) u32; the nested deferred set sizes are static LDS). This
+// is the bound crdt_map_orswot_merge checks against 64 KB.
 size_t map_orswot_lds_bytes(const crdt_map_orswot_slab& S, const crdt_map_orswot_slab& O, uint32_t A) {
   auto per = [&](size_t m, size_t d, size_t s) { return 8 * (m + m * A + d * A + d * s); };
   const size_t MW = S.mcap + O.mcap, DW = S.vdcap + O.vdcap, SW = S.vscap + O.vscap;
-  return per(S.mcap, S.vdcap, S.vscap) + per(O.mcap, O.vdcap, O.vscap) + per(MW, DW, SW) + 8 * ((MW + DW + 1) / 2);
+  return per(S.mcap, S.vdcap, S.vscap) + per(O.mcap, O.vdcap, O.vscap) + per(MW, DW, SW) + 8 * ((MW + DW + 1) / 2) +
+         8 * ((3 * ((size_t)S.dcap + O.dcap) + 1) / 2);
 }
 
 int launch_map_orswot_merge(const crdt_map_orswot_slab& S, const crdt_map_orswot_slab& O,

@@ -177,3 +177,21 @@ def test_map_orswot_many_keys_16_actors(gpu, oracle, scap):
         for f in exp.a:
             bad = np.nonzero((np.asarray(got.a[f]) != np.asarray(exp.a[f])).reshape(S.n, -1).any(axis=1))[0]
             assert bad.size == 0, f"{f}: {bad.size} objects differ, first {bad[:5].tolist()}"
+
+
+def test_map_orswot_100_map_deferred_clocks(gpu, oracle):
+    """Past the round-4 map deferred cap (32 per side): maps holding 57-157
+    map-level deferred removes per side (dcap 160; the combined list up to
+    ~300 entries, key sets up to 40 keys, read from HBM past the staging
+    area), both orientations, slab-row exact against the oracle
+    (src/map.rs:255-260 deferral, :325-350 apply_deferred / apply_rm)."""
+    caps = dict(kcap=256, mcap=8, vdcap=8, vscap=8, dcap=160, scap=64)
+    L, R = oracle.map_orswot_generate(0x100D, 16, 16, keys=300, members=4, ops=800, pct_future=70, caps=caps)
+    assert L.a["n_def"].max() >= 100 and R.a["n_def"].max() >= 100 and (L.a["n_def"] >= 100).sum() >= 4
+    for S, O in ((L, R), (R, L)):
+        exp = oracle.map_orswot_merge(S, O, 16).canonical()
+        assert exp.a["n_def"].max() > 128
+        got = gpu.map_orswot_merge(S.to("cuda"), O.to("cuda"), 16).canonical()
+        for f in exp.a:
+            bad = np.nonzero((np.asarray(got.a[f]) != np.asarray(exp.a[f])).reshape(S.n, -1).any(axis=1))[0]
+            assert bad.size == 0, f"{f}: {bad.size} objects differ, first {bad[:5].tolist()}"

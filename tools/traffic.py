@@ -23,7 +23,8 @@ import shutil
 import sys
 
 KERNELS = {"orswot_join_kernel": ("orswot_join_kernel<", "orswot_join5_kernel<"), "orswot_mask_kernel": "orswot_mask_kernel<",
-           "orswot_merge_general_kernel": "orswot_merge_general_kernel", "dense_max_kernel": "dense_max_kernel"}
+           "orswot_merge_general_kernel": "orswot_merge_general_kernel", "orswot_big_kernel": "orswot_big_kernel<",
+           "dense_max_kernel": "dense_max_kernel"}
 # every other kernel of the library is summarised under its own name
 OTHER = ("orswot_apply_kernel", "orswot_sparse_mask_kernel", "orswot_sparse_general_kernel", "bincode_ingest_kernel",
          "clock_csr_merge_kernel", "orswot_truncate_kernel", "bincode_decode_big_kernel", "slice_bounds_kernel",
