@@ -440,6 +440,9 @@ int launch_map_mvreg_merge(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_sl
   else if (vs && variant == 501)  // (diag: no register bound, 5 waves/SIMD, no spill)
     hipLaunchKernelGGL((map_mvreg_merge_kernel<true, 1, false, 1>), dim3(blocks), dim3(kMpW), 0, stream, S, O, R,
                        n_obj, A, status, ctl);
+  else if (vs && variant == 502)  // (diag: 6 waves/SIMD)
+    hipLaunchKernelGGL((map_mvreg_merge_kernel<true, 1, false, 6>), dim3(blocks), dim3(kMpW), 0, stream, S, O, R,
+                       n_obj, A, status, ctl);
   else if (vs)
     hipLaunchKernelGGL((map_mvreg_merge_kernel<true, 1>), dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_obj, A,
                        status, ctl);
