@@ -529,7 +529,7 @@ int crdt_map_mvreg_merge(crdt_ctx* ctx, const crdt_map_mvreg_slab* self, const c
  * 128; output capacities (outer and inner) >= the sums of the inputs' (else
  * CRDT_EINVAL); a result past them latches CRDT_ECAPACITY. d_scratch needs
  * crdt_map_map_merge_scratch_bytes(out, n_obj, n_actors) bytes (the per-slot
- * merge tasks, truncating clocks and a scratch inner slab). Only used slots
+ * merge tasks and their truncating clocks). Only used slots
  * of the output are written. Where two deferred clocks of an inner map
  * become equal under truncation the later one's key set is kept (the
  * reference inserts into a HashMap there). */

@@ -78,12 +78,12 @@ int launch_mvreg_merge(const uint32_t* sn, const uint64_t* sclk, const uint64_t*
 int launch_map_mvreg_merge(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_slab& O, const crdt_map_mvreg_slab& R,
                            uint64_t n_obj, uint32_t A, int* status, uint32_t* ctl, hipStream_t stream, int variant = 0);
 // The nested map's inner pass (map_map.hip): task t merges S row tsrc[2t]
-// with O row tsrc[2t + 1] (~0: an absent side) into R row t, or into Tmp row
-// t when Tb row t is non-empty, and then Tmp row t truncated by Tb row t into R.
+// with O row tsrc[2t + 1] (~0: an absent side) into R row t, truncated by Tb
+// row t when it is non-empty (one pass: no intermediate slab).
 int launch_map_mvreg_merge_tasks(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_slab& O,
-                                 const crdt_map_mvreg_slab& R, const crdt_map_mvreg_slab& Tmp, const uint64_t* tsrc,
-                                 const uint64_t* Tb, uint64_t n_tasks, uint32_t slots, uint32_t A, int* status,
-                                 uint32_t* ctl, hipStream_t stream);
+                                 const crdt_map_mvreg_slab& R, const uint64_t* tsrc, const uint64_t* Tb,
+                                 uint64_t n_tasks, uint32_t slots, uint32_t A, int* status, uint32_t* ctl,
+                                 hipStream_t stream);
 size_t map_map_scratch_bytes(const crdt_map_map_slab& R, uint64_t n_obj, uint32_t A);
 int launch_map_map_merge(const crdt_map_map_slab& S, const crdt_map_map_slab& O, const crdt_map_map_slab& R,
                          uint64_t n_obj, uint32_t A, uint8_t* scratch, int* status, uint32_t* ctl,

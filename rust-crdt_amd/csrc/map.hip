@@ -58,18 +58,15 @@ constexpr uint32_t kMdStage = 128;
 // with O row tsrc[2t + 1] into R row t; kMpNone marks an absent side (an
 // empty map: merge(m, empty) = m for a canonical m), both absent: no task.
 constexpr uint64_t kMpNone = ~0ull;
-// a task the merge rejected (a latched CRDT_ENONCANON) marks its Tmp row so:
-// the truncation then neither reads the row's (unwritten) counts nor writes R
-constexpr uint32_t kMpRejected = ~0u;
 
 template <bool VS, int NS, bool G = false, int MINW = 7>
 __global__ __launch_bounds__(kMpW, MINW) void map_mvreg_merge_kernel(crdt_map_mvreg_slab S, crdt_map_mvreg_slab O,
                                                                crdt_map_mvreg_slab Rout, uint64_t n_obj, uint32_t A,
                                                                int* __restrict__ status, uint32_t* __restrict__ ctl,
                                                                const uint64_t* __restrict__ tsrc = nullptr,
-                                                               const uint64_t* __restrict__ Tb = nullptr,
-                                                               crdt_map_mvreg_slab Tmp = {}) {
+                                                               const uint64_t* __restrict__ Tb = nullptr) {
   __shared__ uint32_t comb[kMpComb];     // (self deferred idx + 1) | (other deferred idx + 1) << 8
+  __shared__ uint32_t tk[G ? kMpComb : 1];  // G: the truncated map's deferred survivors (comb index), CLOCK ORDER
   __shared__ uint32_t vals[kMpVals];     // kept value slots of the key: side << 8 | slot
   __shared__ uint64_t vr[2][VS ? kVsRows : 1];  // the key's value clock rows: self, other
   __shared__ uint64_t md[kMdStage];             // the object's map deferred sets (when they fit)
@@ -81,10 +78,12 @@ __global__ __launch_bounds__(kMpW, MINW) void map_mvreg_merge_kernel(crdt_map_mv
     const uint64_t si = G ? tsrc[2 * i] : i, oi = G ? tsrc[2 * i + 1] : i, ri = i;
     const bool hasS = !G || si != kMpNone, hasO = !G || oi != kMpNone;
     if (G && !hasS && !hasO) continue;
-    // G: a task whose merged map is truncated afterwards goes to Tmp (read by
-    // map_mvreg_truncate_kernel), the rest to the output
-    const bool to_tmp = G && Tb != nullptr && vany(rowv<NS>(Tb, i, A, lane));
-    const crdt_map_mvreg_slab& R = to_tmp ? Tmp : Rout;
+    // G: the merged map is then truncated by the task's row of Tb when it is
+    // non-empty (Causal::truncate, src/map.rs:131-158 — the nested map's
+    // removers' clock, from map_map_outer_kernel), fused into the writes below
+    const Row<NS> tc = G && Tb != nullptr ? rowv<NS>(Tb, i, A, lane) : zrow<NS>();
+    const bool trunc = G && Tb != nullptr && vany(tc);
+    const crdt_map_mvreg_slab& R = Rout;
     const Row<NS> cS = hasS ? rowv<NS>(S.clock, si, A, lane) : zrow<NS>();
     const Row<NS> cO = hasO ? rowv<NS>(O.clock, oi, A, lane) : zrow<NS>();
     const Row<NS> cM = vmax(cS, cO);  // VClock::merge
@@ -93,10 +92,7 @@ __global__ __launch_bounds__(kMpW, MINW) void map_mvreg_merge_kernel(crdt_map_mv
     const uint32_t dS = hasS ? __builtin_amdgcn_readfirstlane(S.n_def[si]) : 0u;
     const uint32_t dO = hasO ? __builtin_amdgcn_readfirstlane(O.n_def[oi]) : 0u;
     if (nS > S.kcap || nO > O.kcap || dS > S.dcap || dO > O.dcap) {
-      if (lane == 0u) {
-        atomicCAS(status, 0, CRDT_ENONCANON);
-        if (to_tmp) Tmp.n_keys[ri] = kMpRejected;  // map_mvreg_truncate_kernel skips the row
-      }
+      if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
       continue;
     }
     // every value count within mcap and deferred set size within scap (the
@@ -112,10 +108,7 @@ __global__ __launch_bounds__(kMpW, MINW) void map_mvreg_merge_kernel(crdt_map_mv
     for (uint32_t k = lane + kMpW; k < nS; k += kMpW) bad = bad || S.mv_n[si * S.kcap + k] > S.mcap;
     for (uint32_t k = lane + kMpW; k < nO; k += kMpW) bad = bad || O.mv_n[oi * O.kcap + k] > O.mcap;
     if (__ballot(bad) != 0ull) {
-      if (lane == 0u) {
-        atomicCAS(status, 0, CRDT_ENONCANON);
-        if (to_tmp) Tmp.n_keys[ri] = kMpRejected;
-      }
+      if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
       continue;
     }
     // the map deferred sets (used entries) staged in LDS when they fit
@@ -259,6 +252,14 @@ __global__ __launch_bounds__(kMpW, MINW) void map_mvreg_merge_kernel(crdt_map_mv
         }
         keep = vany(ec);
       }
+      // G: Map::truncate of the merged map — the entry clock loses tc (an
+      // emptied entry is dropped) and its register is truncated by tc too
+      // (subtracting del then tc = subtracting their max, slot by slot)
+      if (trunc && keep) {
+        ec = vsub(ec, tc);
+        keep = vany(ec);
+        del = vmax(del, tc);
+      }
       if (keep) {
         if (nk >= R.kcap) {
           over = true;
@@ -287,15 +288,54 @@ __global__ __launch_bounds__(kMpW, MINW) void map_mvreg_merge_kernel(crdt_map_mv
       if (ho) ++b;
     }
     if (lane == 0u) R.n_keys[ri] = nk;
-    strow<NS>(R.clock + ri * A, cM, A, lane);
-    // ---- deferred kept: the combined clocks the merged clock does not cover, sets united
-    uint32_t nd = 0;
-    for (uint32_t c = 0; c < nc; ++c) {
-      const uint32_t e = comb[c];
+    strow<NS>(R.clock + ri * A, trunc ? vsub(cM, tc) : cM, A, lane);
+    auto comb_row = [&](uint32_t e) -> Row<NS> {
       const uint32_t sa = e & 255u, sb = e >> 8;
-      const Row<NS> D = sa ? rowv<NS>(S.dclock, si * S.dcap + sa - 1u, A, lane)
-                           : rowv<NS>(O.dclock, oi * O.dcap + sb - 1u, A, lane);
-      if (vle(D, cM)) continue;
+      return sa ? rowv<NS>(S.dclock, si * S.dcap + sa - 1u, A, lane) : rowv<NS>(O.dclock, oi * O.dcap + sb - 1u, A, lane);
+    };
+    // ---- deferred kept: the combined clocks the merged clock does not cover, sets united
+    // (G, truncated: each loses tc, an emptied one is dropped, one that becomes
+    // equal to an earlier survivor replaces it — the reference's HashMap
+    // insert over the merge's CLOCK ORDER — and the survivors are written in
+    // the CLOCK ORDER of the truncated clocks)
+    uint32_t nw = nc;
+    if constexpr (G) {
+      if (trunc) {
+        uint32_t ns = 0;
+        for (uint32_t c = 0; c < nc; ++c) {
+          const Row<NS> D = comb_row(comb[c]);
+          if (vle(D, cM)) continue;
+          const Row<NS> Dt = vsub(D, tc);
+          if (!vany(Dt)) continue;
+          uint32_t at = ns, pos = ns;
+          for (uint32_t q = 0; q < ns; ++q) {
+            const int o = vorder(Dt, vsub(comb_row(comb[tk[q]]), tc), lane);
+            if (o == 0) { at = q; break; }    // equal: this (later) one replaces it
+            if (o < 0 && pos == ns) pos = q;  // insertion point
+          }
+          mp_sync();
+          if (at < ns) {
+            if (lane == 0u) tk[at] = c;
+          } else {
+            if (lane == 0u) {
+              for (uint32_t q = ns; q > pos; --q) tk[q] = tk[q - 1];
+              tk[pos] = c;
+            }
+            ++ns;
+          }
+          mp_sync();
+        }
+        nw = ns;
+      }
+    }
+    uint32_t nd = 0;
+    for (uint32_t w = 0; w < nw; ++w) {
+      const bool tl = G && trunc;
+      const uint32_t e = comb[tl ? tk[w] : w];
+      const uint32_t sa = e & 255u, sb = e >> 8;
+      const Row<NS> D0 = comb_row(e);
+      if (!tl && vle(D0, cM)) continue;
+      const Row<NS> D = tl ? vsub(D0, tc) : D0;
       if (nd >= R.dcap) { over = true; break; }
       const uint64_t dr = ri * R.dcap + nd;
       strow<NS>(R.dclock + dr * A, D, A, lane);
@@ -320,105 +360,6 @@ __global__ __launch_bounds__(kMpW, MINW) void map_mvreg_merge_kernel(crdt_map_mv
     }
     if (lane == 0u) R.n_def[ri] = nd;
     if (over && lane == 0u) atomicCAS(status, 0, CRDT_ECAPACITY);
-    mp_sync();
-  }
-}
-
-// Map<u64, MVReg>::truncate (Causal, src/map.rs:131-158, with
-// MVReg::truncate src/mvreg.rs:100-113 on every kept entry's register) of the
-// maps the task form wrote to Tmp, by their row of Tb, into R (same row):
-// entry clocks lose the clock (emptied entries dropped, the rest keep their
-// surviving values in order), deferred clocks lose it (emptied ones dropped;
-// two that become equal keep the later one's key set, as the reference's
-// HashMap insert does over the merge's CLOCK ORDER; output re-sorted in CLOCK
-// ORDER), and the map clock loses it.
-template <int NS>
-__global__ __launch_bounds__(kMpW) void map_mvreg_truncate_kernel(crdt_map_mvreg_slab Tmp, crdt_map_mvreg_slab R,
-                                                                  const uint64_t* __restrict__ Tb,
-                                                                  const uint64_t* __restrict__ tsrc, uint64_t n,
-                                                                  uint32_t A, int* __restrict__ status,
-                                                                  uint32_t* __restrict__ ctl) {
-  __shared__ uint32_t keep_d[kMpComb];  // surviving deferred (source index), CLOCK ORDER of the truncated clocks
-  const uint32_t lane = threadIdx.x;
-  GridStride sched(n, ctl + 3, lane);  // (most tasks are empty or not truncated)
-  for (uint64_t t = sched.first(); t < n; t = sched.next(t)) {
-    if (tsrc[2 * t] == kMpNone && tsrc[2 * t + 1] == kMpNone) continue;
-    const Row<NS> c = rowv<NS>(Tb, t, A, lane);
-    if (!vany(c)) continue;  // (written to R by the merge)
-    const uint32_t nk = __builtin_amdgcn_readfirstlane(Tmp.n_keys[t]);
-    if (nk == kMpRejected) continue;  // the merge rejected the task (status latched there)
-    // every count this pass reads is bounded by the slabs it indexes (the
-    // merge never writes past them; a count past them is not its output)
-    const uint32_t kb = Tmp.kcap < R.kcap ? Tmp.kcap : R.kcap, mb = Tmp.mcap < R.mcap ? Tmp.mcap : R.mcap;
-    const uint32_t db0 = Tmp.dcap < R.dcap ? Tmp.dcap : R.dcap, db = db0 < kMpComb ? db0 : kMpComb;
-    const uint32_t sb = Tmp.scap < R.scap ? Tmp.scap : R.scap;
-    bool bad = nk > kb || __builtin_amdgcn_readfirstlane(Tmp.n_def[t]) > db;
-    for (uint32_t k = lane; k < (nk <= kb ? nk : 0u); k += kMpW) bad = bad || Tmp.mv_n[t * Tmp.kcap + k] > mb;
-    {
-      const uint32_t nd0 = __builtin_amdgcn_readfirstlane(Tmp.n_def[t]);
-      for (uint32_t d = lane; d < (nd0 <= db ? nd0 : 0u); d += kMpW) bad = bad || Tmp.dset_n[t * Tmp.dcap + d] > sb;
-    }
-    if (__ballot(bad) != 0ull) {
-      if (lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
-      continue;
-    }
-    strow<NS>(R.clock + t * A, vsub(rowv<NS>(Tmp.clock, t, A, lane), c), A, lane);
-    uint32_t out = 0;
-    for (uint32_t k = 0; k < nk; ++k) {
-      const uint64_t ik = t * Tmp.kcap + k;
-      const Row<NS> e = vsub(rowv<NS>(Tmp.eclock, ik, A, lane), c);
-      if (!vany(e)) continue;
-      const uint64_t ok = t * R.kcap + out;
-      if (lane == 0u) R.keys[ok] = Tmp.keys[ik];
-      strow<NS>(R.eclock + ok * A, e, A, lane);
-      const uint32_t nv = __builtin_amdgcn_readfirstlane(Tmp.mv_n[ik]);
-      uint32_t nout = 0;
-      for (uint32_t v = 0; v < nv; ++v) {
-        const Row<NS> r = vsub(rowv<NS>(Tmp.mv_clock, ik * Tmp.mcap + v, A, lane), c);
-        if (!vany(r)) continue;
-        strow<NS>(R.mv_clock + (ok * R.mcap + nout) * A, r, A, lane);
-        if (lane == 0u) R.mv_val[ok * R.mcap + nout] = Tmp.mv_val[ik * Tmp.mcap + v];
-        ++nout;
-      }
-      if (lane == 0u) R.mv_n[ok] = nout;
-      ++out;
-    }
-    if (lane == 0u) R.n_keys[t] = out;
-    // deferred: survivors, later equal clocks replacing earlier ones, then CLOCK ORDER
-    const uint32_t nd = __builtin_amdgcn_readfirstlane(Tmp.n_def[t]);
-    uint32_t ns = 0;
-    for (uint32_t d = 0; d < nd; ++d) {
-      const Row<NS> D = vsub(rowv<NS>(Tmp.dclock, t * Tmp.dcap + d, A, lane), c);
-      if (!vany(D)) continue;
-      uint32_t at = ns, pos = ns;
-      for (uint32_t q = 0; q < ns; ++q) {
-        const uint32_t sq = keep_d[q];
-        const Row<NS> Q = vsub(rowv<NS>(Tmp.dclock, t * Tmp.dcap + sq, A, lane), c);
-        const int o = vorder(D, Q, lane);
-        if (o == 0) { at = q; break; }   // equal: this (later) one replaces it
-        if (o < 0 && pos == ns) pos = q; // insertion point
-      }
-      mp_sync();
-      if (at < ns) {
-        if (lane == 0u) keep_d[at] = d;
-      } else {
-        if (lane == 0u) {
-          for (uint32_t q = ns; q > pos; --q) keep_d[q] = keep_d[q - 1];
-          keep_d[pos] = d;
-        }
-        ++ns;
-      }
-      mp_sync();
-    }
-    for (uint32_t q = 0; q < ns; ++q) {
-      const uint32_t sq = keep_d[q];
-      const uint64_t src = t * Tmp.dcap + sq, dst = t * R.dcap + q;
-      strow<NS>(R.dclock + dst * A, vsub(rowv<NS>(Tmp.dclock, src, A, lane), c), A, lane);
-      const uint32_t m = __builtin_amdgcn_readfirstlane(Tmp.dset_n[src]);
-      for (uint32_t j = lane; j < m; j += kMpW) R.dset[dst * R.scap + j] = Tmp.dset[src * Tmp.scap + j];
-      if (lane == 0u) R.dset_n[dst] = m;
-    }
-    if (lane == 0u) R.n_def[t] = ns;
     mp_sync();
   }
 }
@@ -453,9 +394,9 @@ int launch_map_mvreg_merge(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_sl
 }
 
 int launch_map_mvreg_merge_tasks(const crdt_map_mvreg_slab& S, const crdt_map_mvreg_slab& O,
-                                 const crdt_map_mvreg_slab& R, const crdt_map_mvreg_slab& Tmp, const uint64_t* tsrc,
-                                 const uint64_t* Tb, uint64_t n_tasks, uint32_t slots, uint32_t A, int* status,
-                                 uint32_t* ctl, hipStream_t stream) {
+                                 const crdt_map_mvreg_slab& R, const uint64_t* tsrc, const uint64_t* Tb,
+                                 uint64_t n_tasks, uint32_t slots, uint32_t A, int* status, uint32_t* ctl,
+                                 hipStream_t stream) {
   if (n_tasks == 0) return CRDT_OK;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -472,18 +413,10 @@ int launch_map_mvreg_merge_tasks(const crdt_map_mvreg_slab& S, const crdt_map_mv
   if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
   if (A > 64u)
     hipLaunchKernelGGL((map_mvreg_merge_kernel<false, 2, true>), dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_tasks,
-                       A, status, ctl, tsrc, Tb, Tmp);
+                       A, status, ctl, tsrc, Tb);
   else
     hipLaunchKernelGGL((map_mvreg_merge_kernel<false, 1, true>), dim3(blocks), dim3(kMpW), 0, stream, S, O, R, n_tasks,
-                       A, status, ctl, tsrc, Tb, Tmp);
-  if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
-  if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
-  if (A > 64u)
-    hipLaunchKernelGGL((map_mvreg_truncate_kernel<2>), dim3(blocks), dim3(kMpW), 0, stream, Tmp, R, Tb, tsrc, n_tasks,
-                       A, status, ctl);
-  else
-    hipLaunchKernelGGL((map_mvreg_truncate_kernel<1>), dim3(blocks), dim3(kMpW), 0, stream, Tmp, R, Tb, tsrc, n_tasks,
-                       A, status, ctl);
+                       A, status, ctl, tsrc, Tb);
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 

@@ -14,14 +14,14 @@
 // with emptied rows dropped), so each kept key is truncated once, by the max
 // of its removal clock and the deferred clocks naming it.
 //
-// Three launches, batch-parallel: (1) the outer pass, one wave per map pair
+// Two launches, batch-parallel: (1) the outer pass, one wave per map pair
 // (lane = actor slot, NS slots per lane: map_rows.h): the outer entries,
 // clock and deferred removes, and per output key slot a task — which inner
 // map of each side (or none) and the truncating clock; (2) the inner maps
 // merged task by task (map.hip's Map<u64, MVReg> kernel in its task form: a
-// missing side is the empty map, merge(m, empty) = m for a reachable m), into
-// the output or, when the task truncates, into a scratch slab; (3) those
-// truncated into the output (map.hip's map_mvreg_truncate_kernel).
+// missing side is the empty map, merge(m, empty) = m for a reachable m) and
+// truncated by the task's clock as they are written to the output (round 5:
+// no scratch inner slab and no third pass over it).
 #include <hip/hip_runtime.h>
 
 #include "../../include/crdts_hip.h"
@@ -225,11 +225,7 @@ __global__ __launch_bounds__(kMmW) void map_map_outer_kernel(crdt_map_map_slab S
 
 size_t map_map_scratch_bytes(const crdt_map_map_slab& R, uint64_t n_obj, uint32_t A) {
   const uint64_t nt = n_obj * R.kcap;
-  const crdt_map_mvreg_slab& I = R.inner;
-  const uint64_t inner = 8ull * nt * A + 4ull * nt + 8ull * nt * I.kcap + 8ull * nt * I.kcap * A + 4ull * nt * I.kcap +
-                         8ull * nt * I.kcap * I.mcap * A + 8ull * nt * I.kcap * I.mcap + 4ull * nt +
-                         8ull * nt * I.dcap * A + 4ull * nt * I.dcap + 8ull * nt * I.dcap * I.scap;
-  return 16ull * nt + 8ull * nt * A + inner + 64u * 16u;  // tasks, truncating clocks, the scratch inner slab
+  return 16ull * nt + 8ull * nt * A + 2u * 16u;  // tasks, truncating clocks (each 16-B aligned)
 }
 
 int launch_map_map_merge(const crdt_map_map_slab& S, const crdt_map_map_slab& O, const crdt_map_map_slab& R,
@@ -237,7 +233,7 @@ int launch_map_map_merge(const crdt_map_map_slab& S, const crdt_map_map_slab& O,
                          hipStream_t stream) {
   if (n_obj == 0) return CRDT_OK;
   const uint64_t nt = n_obj * R.kcap;
-  // scratch: tasks [nt][2] u64, truncating clocks [nt][A], then the scratch inner slab (R.inner's capacities)
+  // scratch: tasks [nt][2] u64, then truncating clocks [nt][A]
   uint8_t* p = scratch;
   auto take = [&](uint64_t bytes) {
     uint8_t* q = p;
@@ -246,23 +242,6 @@ int launch_map_map_merge(const crdt_map_map_slab& S, const crdt_map_map_slab& O,
   };
   uint64_t* tsrc = (uint64_t*)take(16ull * nt);
   uint64_t* Tb = (uint64_t*)take(8ull * nt * A);
-  const crdt_map_mvreg_slab& I = R.inner;
-  crdt_map_mvreg_slab T{};
-  T.kcap = I.kcap;
-  T.mcap = I.mcap;
-  T.dcap = I.dcap;
-  T.scap = I.scap;
-  T.clock = (uint64_t*)take(8ull * nt * A);
-  T.n_keys = (uint32_t*)take(4ull * nt);
-  T.keys = (uint64_t*)take(8ull * nt * I.kcap);
-  T.eclock = (uint64_t*)take(8ull * nt * I.kcap * A);
-  T.mv_n = (uint32_t*)take(4ull * nt * I.kcap);
-  T.mv_clock = (uint64_t*)take(8ull * nt * I.kcap * I.mcap * A);
-  T.mv_val = (uint64_t*)take(8ull * nt * I.kcap * I.mcap);
-  T.n_def = (uint32_t*)take(4ull * nt);
-  T.dclock = (uint64_t*)take(8ull * nt * I.dcap * A);
-  T.dset_n = (uint32_t*)take(4ull * nt * I.dcap);
-  T.dset = (uint64_t*)take(8ull * nt * I.dcap * I.scap);
   if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;  // ctl[3]: tickets
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -275,7 +254,7 @@ int launch_map_map_merge(const crdt_map_map_slab& S, const crdt_map_map_slab& O,
     hipLaunchKernelGGL((map_map_outer_kernel<1>), dim3(blocks), dim3(kMmW), 0, stream, S, O, R, n_obj, A, tsrc, Tb,
                        status, ctl);
   if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
-  return launch_map_mvreg_merge_tasks(S.inner, O.inner, R.inner, T, tsrc, Tb, nt, R.kcap, A, status, ctl, stream);
+  return launch_map_mvreg_merge_tasks(S.inner, O.inner, R.inner, tsrc, Tb, nt, R.kcap, A, status, ctl, stream);
 }
 
 }  // namespace crdts_hip

@@ -83,8 +83,9 @@ def main():
             rd = 2.0 * cs["FETCH_SIZE"] * 1024.0
             wr = cs["WRITE_SIZE"] * 1024.0
             note = "per launch; FETCH_SIZE x2 (gfx950 16-B streaming-read correction), KiB->B"
-            if k.startswith(("mvreg_merge_kernel", "map_mvreg_merge_kernel", "vclock_cmp_kernel", "orswot_apply_kernel")):
-                note += "; 8-B/4-B accesses: absolute uncalibrated (MI355X_MICROARCH.md HBM section)"
+            if k.startswith(("mvreg_merge_kernel", "map_", "vclock_cmp_kernel", "orswot_apply_kernel")):
+                note += ("; partial-line 8-B / 4-B accesses: x2 FETCH_SIZE is the 128-B line traffic "
+                         "(calibrated, profiles/r05_fetch_calib_partial_lines.json)")
             traffic[k] = {"read_bytes": rd, "write_bytes": wr, "total_bytes": rd + wr, "note": note}
     json.dump({"pmc_avg_per_launch": pmc, "source": src}, open(dst + "_pmc.json", "w"), indent=1)
     tdir = os.path.dirname(dst) or "."
