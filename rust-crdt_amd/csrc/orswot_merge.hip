@@ -211,6 +211,14 @@ __device__ __forceinline__ bool in_any_deferred(const S& L, const S& R, uint64_t
   return hit;
 }
 
+// A 1024-bit filter over both sides' deferred member keys (big-object
+// kernel): a member whose bit is clear is in no deferred member set.
+__device__ __forceinline__ uint32_t dm_hash(uint64_t m) { return (uint32_t)((m * 0x9E3779B97F4A7C15ull) >> 54); }
+__device__ __forceinline__ bool dm_maybe(const uint32_t* bloom, uint64_t m) {
+  const uint32_t h = dm_hash(m);
+  return ((bloom[h >> 5] >> (h & 31u)) & 1u) != 0u;
+}
+
 // Merge path: the candidate at union position p (self first on ties).
 // Branch-free binary search with a fixed trip count (no per-lane loop
 // control): i = number of self keys among the first p union positions.
@@ -241,7 +249,8 @@ __device__ __forceinline__ uint32_t merge_path(const S& L, const S& R, uint32_t 
 template <int MODE, bool SP = false, class S>
 __device__ __forceinline__ uint32_t join(const S& L, const S& R, uint32_t type, uint32_t i,
                                          uint32_t j, uint32_t A, bool has_def, uint32_t& x0, uint64_t& v0,
-                                         uint32_t* oact, uint64_t* octr, uint32_t d0) {
+                                         uint32_t* oact, uint64_t* octr, uint32_t d0,
+                                         const uint32_t* bloom = nullptr) {
   uint32_t a = 0, ae = 0, b = 0, be = 0;
   if (type & kSelf) { a = run_begin(L.b, L.v.mdend, i); ae = g32(L.b, L.v.mdend, i); }
   if (type & kOther) { b = run_begin(R.b, R.v.mdend, j); be = g32(R.b, R.v.mdend, j); }
@@ -256,7 +265,7 @@ __device__ __forceinline__ uint32_t join(const S& L, const S& R, uint32_t type, 
   bool mk = false;  // m is in some deferred member set: its dots face the kill test
   if (has_def) {
     m = (type & kSelf) ? g64(L.b, L.v.key, i) : g64(R.b, R.v.key, j);
-    mk = in_any_deferred(L, R, m);
+    mk = (bloom == nullptr || dm_maybe(bloom, m)) && in_any_deferred(L, R, m);
   }
   uint32_t c = 0;
   while (a < ae || b < be) {
@@ -3387,6 +3396,7 @@ struct BigTabs {
   uint8_t* pc;    // kBigPos: its joined dot count (255: count again)
   uint32_t* bc;   // 4: grand totals
   uint32_t cap;
+  uint32_t* bloom;  // 32: the deferred member filter (dm_maybe)
 };
 
 // merge_path with the answer known to lie in [ilo, ihi], ihi - ilo <= 64.
@@ -3424,6 +3434,16 @@ __device__ __forceinline__ void merge_object_block(const S& L, const S& R, uint8
   const uint32_t nch = (P + kWave - 1) / kWave;
   uint32_t n_clk = A;
   if constexpr (SP) n_clk = uni(sparse_clock_join(L, R, nullptr, 0u, lane));
+  // ---- the deferred member filter (both sides' deferred member keys)
+  if (has_def) {
+    if (threadIdx.x < 32u) T.bloom[threadIdx.x] = 0u;
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < L.v.n_dm + R.v.n_dm; k += kWave * kBigW) {
+      const uint64_t m = k < L.v.n_dm ? g64(L.b, L.v.fkey, k) : g64(R.b, R.v.fkey, k - L.v.n_dm);
+      const uint32_t h = dm_hash(m);
+      atomicOr(&T.bloom[h >> 5], 1u << (h & 31u));
+    }
+  }
   // ---- chunk boundaries: the merge-path split at every 64th position
   for (uint32_t c = threadIdx.x; c <= nch; c += kWave * kBigW) {
     const uint32_t p = kWave * c < P ? kWave * c : P;
@@ -3445,7 +3465,7 @@ __device__ __forceinline__ void merge_object_block(const S& L, const S& R, uint8
     if (p < P) {
       type = merge_path_in(L, R, p, ilo, ihi, i, j);
       if (ABL == 4) cnt = type != kNone;
-      else if (type != kNone) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0);
+      else if (type != kNone) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0, T.bloom);
       if (p < kBigPos) {
         T.pq[p] = (uint16_t)((type << 14) | i);
         T.pc[p] = (uint8_t)(cnt < 255u ? cnt : 255u);
@@ -3495,46 +3515,10 @@ __device__ __forceinline__ void merge_object_block(const S& L, const S& R, uint8
       ((uint64_t*)(O + kHdrBytes))[a] = x > y ? x : y;
     }
   }
-  // ---- pass 2: kept members and their joined dot runs at their chunk's base
-  const uint64_t lt_mask = (1ull << lane) - 1ull;
-  for (uint32_t ch = wave, k = 0; ch < (ABL == 3 ? 0u : nch); ch += kBigW, ++k) {
-    const uint32_t p = kWave * ch + lane;
-    uint32_t type = kNone, i = 0, j = 0, cnt = 0, x = 0;
-    uint64_t v = 0;
-    bool xv = false;  // (x, v) hold the run's only dot
-    if (k < 2u) {
-      const uint32_t q = k == 0 ? q0 : q1;
-      cnt = k == 0 ? c0 : c1; x = k == 0 ? x0 : x1; v = k == 0 ? v0 : v1;
-      type = q >> 30; i = (q >> 15) & 0x7FFFu; j = q & 0x7FFFu;
-      xv = true;
-    } else if (p < P && p < kBigPos) {
-      const uint32_t u = T.pq[p];
-      type = u >> 14; i = u & 0x3FFFu; j = p - i;
-      cnt = T.pc[p];
-      if (cnt == 255u) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0);
-    } else if (p < P) {
-      type = merge_path_in(L, R, p, uni(T.spl[ch]), uni(T.spl[ch + 1]), i, j);
-      if (type != kNone) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0);
-      xv = true;
-    }
-    const uint64_t keep = __ballot(cnt != 0);
-    const uint32_t incl = wave_incl_scan(cnt, lane);
-    const uint32_t mem_base = uni(T.tot[ch]), dot_base = uni(T.tot[T.cap + ch]);
-    if (cnt != 0) {
-      const uint32_t midx = mem_base + (uint32_t)__popcll(keep & lt_mask);
-      const uint32_t d0 = dot_base + incl - cnt;
-      okey[midx] = (type & kSelf) ? g64(L.b, L.v.key, i) : g64(R.b, R.v.key, j);
-      if (cnt == 1 && xv) {
-        odact[d0] = x;
-        odctr[d0] = v;
-      } else {
-        join<1, SP>(L, R, type, i, j, A, has_def, x, v, odact, odctr, d0);
-      }
-      omdend[midx] = d0 + cnt;
-    }
-  }
-  // ---- deferred block + header + padding (wave 0; the deferred walk wave-cooperative)
-  if (wave == 0u) {
+  // ---- deferred block + header + padding: the last wave (the fewest pass-2
+  // chunks), before its chunks, while the others write theirs; the deferred
+  // walk wave-cooperative
+  if (wave == kBigW - 1u) {
     uint32_t nd = 0, ndd = 0, ndm = 0;
     if (lane == 0u && o_def != o_mpad) *(uint32_t*)(O + o_mpad) = 0u;
     if (ABL != 2 && has_def) {
@@ -3554,6 +3538,44 @@ __device__ __forceinline__ void merge_object_block(const S& L, const S& R, uint8
       h[1] = u32x4{nd, ndd, ndm, SP ? kSparseClock : 0u};
     }
   }
+  // ---- pass 2: kept members and their joined dot runs at their chunk's base
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  for (uint32_t ch = wave, k = 0; ch < (ABL == 3 ? 0u : nch); ch += kBigW, ++k) {
+    const uint32_t p = kWave * ch + lane;
+    uint32_t type = kNone, i = 0, j = 0, cnt = 0, x = 0;
+    uint64_t v = 0;
+    bool xv = false;  // (x, v) hold the run's only dot
+    if (k < 2u) {
+      const uint32_t q = k == 0 ? q0 : q1;
+      cnt = k == 0 ? c0 : c1; x = k == 0 ? x0 : x1; v = k == 0 ? v0 : v1;
+      type = q >> 30; i = (q >> 15) & 0x7FFFu; j = q & 0x7FFFu;
+      xv = true;
+    } else if (p < P && p < kBigPos) {
+      const uint32_t u = T.pq[p];
+      type = u >> 14; i = u & 0x3FFFu; j = p - i;
+      cnt = T.pc[p];
+      if (cnt == 255u) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0, T.bloom);
+    } else if (p < P) {
+      type = merge_path_in(L, R, p, uni(T.spl[ch]), uni(T.spl[ch + 1]), i, j);
+      if (type != kNone) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0, T.bloom);
+      xv = true;
+    }
+    const uint64_t keep = __ballot(cnt != 0);
+    const uint32_t incl = wave_incl_scan(cnt, lane);
+    const uint32_t mem_base = uni(T.tot[ch]), dot_base = uni(T.tot[T.cap + ch]);
+    if (cnt != 0) {
+      const uint32_t midx = mem_base + (uint32_t)__popcll(keep & lt_mask);
+      const uint32_t d0 = dot_base + incl - cnt;
+      okey[midx] = (type & kSelf) ? g64(L.b, L.v.key, i) : g64(R.b, R.v.key, j);
+      if (cnt == 1 && xv) {
+        odact[d0] = x;
+        odctr[d0] = v;
+      } else {
+        join<1, SP>(L, R, type, i, j, A, has_def, x, v, odact, odctr, d0, T.bloom);
+      }
+      omdend[midx] = d0 + cnt;
+    }
+  }
   __syncthreads();  // the stages and the tables are free for the next object
 }
 
@@ -3562,8 +3584,9 @@ __device__ __noinline__ void big_from_hbm(const uint8_t* lr, const uint8_t* rr, 
                                           uint32_t lane, uint32_t wave, u32x4* st, uint32_t* bc) {
   uint8_t* sb = (uint8_t*)st;
   const BigTabs H{(uint32_t*)sb, (uint32_t*)(sb + 8u * kBigChH), (uint16_t*)(sb + 12u * kBigChH + 16u),
-                  (uint8_t*)(sb + 12u * kBigChH + 16u + 2u * kBigPos), bc, kBigChH};
-  static_assert(12u * kBigChH + 16u + 3u * kBigPos <= 2u * kBigStage, "HBM-path tables fit the stage");
+                  (uint8_t*)(sb + 12u * kBigChH + 16u + 2u * kBigPos), bc, kBigChH,
+                  (uint32_t*)(sb + 12u * kBigChH + 16u + 3u * kBigPos)};
+  static_assert(12u * kBigChH + 16u + 3u * kBigPos + 128u <= 2u * kBigStage, "HBM-path tables fit the stage");
   const RecLayout LL = layout_at(lr), RL = layout_at(rr);
   const Side L{lr, make_rv(LL)}, R{rr, make_rv(RL)};
   merge_object_block<SP, ABL>(L, R, O, A, lane, wave, H);
@@ -3628,7 +3651,8 @@ __global__ __launch_bounds__(kWave * kBigW, MINW) void orswot_big_kernel(
   __shared__ uint32_t tot_s[2 * kBigChS], spl_s[kBigChS + 4], bc_s[4];
   __shared__ uint16_t pq_s[kBigPos];
   __shared__ uint8_t pc_s[kBigPos];
-  const BigTabs T{tot_s, spl_s, pq_s, pc_s, bc_s, kBigChS};
+  __shared__ uint32_t bloom_s[32];
+  const BigTabs T{tot_s, spl_s, pq_s, pc_s, bc_s, kBigChS, bloom_s};
   const uint32_t lane = threadIdx.x & (kWave - 1), wave = uni(threadIdx.x / kWave);
   const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   const uint32_t scan = uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
