@@ -40,7 +40,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "rust-crdt_amd"))
 
 HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md: 8.0 TB/s spec
-TRAFFIC_ROUNDS = ("r04", "r03q", "r03p", "r03n", "r03k", "r03j", "r03", "r02", "r01e")  # profiles/traffic_<round>[_<workload>].json, newest first
+TRAFFIC_ROUNDS = ("r05", "r04", "r03q", "r03p", "r03n", "r03k", "r03j", "r03", "r02", "r01e")  # profiles/traffic_<round>[_<workload>].json, newest first
 METRIC = "merged objects/sec (node) + achieved HBM GB/s % of peak, Orswot 1M×32 members"
 
 
