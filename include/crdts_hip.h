@@ -574,10 +574,11 @@ int crdt_map_map_merge(crdt_ctx* ctx, const crdt_map_map_slab* self, const crdt_
  * Only the used slots of the output are written: slots past a count keep
  * whatever the buffer held (a reader goes by the counts; zeroing them cost
  * ~10x the state's own bytes in writes). Per side kcap <= 4096, mcap <= 256,
- * vdcap, vscap <= 32, dcap <= 256, scap <= 4096, n_actors <= 128, and the
+ * vdcap, vscap, dcap <= 256, scap <= 4096, n_actors <= 128, and the
  * kernel's per-wave workspace — two nested sets of (mcap_s + mcap_o) member
- * rows and (vdcap_s + vdcap_o) deferred clocks of n_actors slots, plus
- * 12 B per map deferred slot (dcap_s + dcap_o) — within 64 KB
+ * rows and (vdcap_s + vdcap_o) deferred clocks of n_actors slots with their
+ * member sets, plus 12 B per map deferred slot (dcap_s + dcap_o) — within
+ * 64 KB
  * (else CRDT_EINVAL); output capacities must hold the result (else
  * CRDT_ECAPACITY is latched for that object). The map's deferred
  * removes are applied in CLOCK ORDER: the reference iterates a HashMap there

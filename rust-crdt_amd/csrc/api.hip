@@ -635,8 +635,8 @@ int crdt_map_orswot_merge(crdt_ctx* ctx, const crdt_map_orswot_slab* self, const
                           const crdt_map_orswot_slab* out, size_t n_obj, uint32_t n_actors, void* stream) {
   if (!ctx || !self || !other || !out || n_actors == 0 || n_actors > 128) return CRDT_EINVAL;
   for (const crdt_map_orswot_slab* x : {self, other})
-    if (x->kcap == 0 || x->kcap > 4096 || x->mcap == 0 || x->mcap > 256 || x->vdcap == 0 || x->vdcap > 32 ||
-        x->vscap == 0 || x->vscap > 32 || x->dcap == 0 || x->dcap > 256 || x->scap == 0 || x->scap > 4096)
+    if (x->kcap == 0 || x->kcap > 4096 || x->mcap == 0 || x->mcap > 256 || x->vdcap == 0 || x->vdcap > 256 ||
+        x->vscap == 0 || x->vscap > 256 || x->dcap == 0 || x->dcap > 256 || x->scap == 0 || x->scap > 4096)
       return CRDT_EINVAL;
   if (out->kcap == 0 || out->mcap == 0 || out->vdcap == 0 || out->vscap == 0 || out->dcap == 0 || out->scap == 0)
     return CRDT_EINVAL;

@@ -35,7 +35,6 @@ namespace crdts_hip {
 namespace {
 
 constexpr uint32_t kMoW = 64;
-constexpr uint32_t kMoComb = 64;       // the nested sets' deferred entries of a workspace (<= vdcap_s + vdcap_o)
 constexpr uint32_t kMoLdsMax = 65536;  // workspace limit per wave
 constexpr uint32_t kMoStageMax = 16384;  // map deferred staging area limit per wave
 
@@ -100,7 +99,7 @@ __device__ void ws_copy(Ws& W, const crdt_map_orswot_slab& X, uint64_t ki, const
   for (uint32_t j = lane; j < W.nm; j += kMoW) W.key[j] = X.vmem[ki * X.mcap + j];
   for (uint32_t e = lane; e < W.nm * c.A; e += kMoW) W.row[e] = X.vmclock[ki * X.mcap * c.A + e];
   for (uint32_t e = lane; e < W.nd * c.A; e += kMoW) W.dclk[e] = X.vdclock[ki * X.vdcap * c.A + e];
-  if (lane < W.nd) W.dn[lane] = X.vdset_n[ki * X.vdcap + lane];  // nd <= vdcap <= 32
+  for (uint32_t d = lane; d < W.nd; d += kMoW) W.dn[d] = X.vdset_n[ki * X.vdcap + d];
   const uint32_t vs = X.vscap;
   for (uint32_t e = lane; e < W.nd * vs; e += kMoW) {  // capacity-strided: no wait for the sizes
     const uint32_t d = e / vs;
@@ -159,11 +158,10 @@ __device__ void ws_apply_deferred(Ws& W, Row<NS> clk, uint32_t* mdead, uint32_t*
     if (k != d) {
       const Row<NS> D = ldrow<NS>(W.dclk + d * c.A, c.A, lane);
       const uint32_t n = uni(W.dn[d]);
-      uint64_t s0 = lane < n ? W.dset[d * W.sw + lane] : 0ull;
       mo_sync();
       strow(W.dclk + k * c.A, D, c.A, lane);
       if (lane == 0u) W.dn[k] = n;
-      if (lane < n) W.dset[k * W.sw + lane] = s0;  // sw <= 64
+      for (uint32_t j = lane; j < n; j += kMoW) W.dset[k * W.sw + j] = W.dset[d * W.sw + j];  // (rows k < d)
       mo_sync();
     }
     ++k;
@@ -297,7 +295,6 @@ __global__ __launch_bounds__(kMoW, MINW) void map_orswot_merge_kernel(crdt_map_o
                                                                 uint32_t md_cap, int* __restrict__ status,
                                                                 uint32_t* __restrict__ ctl) {
   extern __shared__ uint64_t mo_lds[];
-  __shared__ uint32_t dn_s[3][kMoComb];  // the three workspaces' deferred set sizes
   const uint32_t lane = threadIdx.x;
   const Caps c{S.mcap + O.mcap, S.vdcap + O.vdcap, S.vscap + O.vscap, A};
   // workspaces: self's key slot (W0), other's (W2), their merge (W1); then the
@@ -307,18 +304,17 @@ __global__ __launch_bounds__(kMoW, MINW) void map_orswot_merge_kernel(crdt_map_o
   uint64_t* md;
   {
     uint64_t* p = mo_lds;
-    const uint32_t caps[3][3] = {{S.mcap, S.vdcap, S.vscap}, {c.MW, c.DW, c.SW}, {O.mcap, O.vdcap, O.vscap}};
-    Ws* ws[3] = {&W0, &W1, &W2};
-    for (int w = 0; w < 3; ++w) {
-      const uint32_t m = caps[w][0], d = caps[w][1];
-      ws[w]->key = p; p += m;
-      ws[w]->row = p; p += m * A;
-      ws[w]->dclk = p; p += d * A;
-      ws[w]->dset = p; p += d * caps[w][2];
-      ws[w]->dn = dn_s[w];
-      ws[w]->sw = caps[w][2];
-      ws[w]->nm = ws[w]->nd = 0u;
-    }
+    auto carve = [&](Ws& W, uint32_t m, uint32_t d, uint32_t sw) {  // (no indexed array: W stays in registers)
+      W.key = p; p += m;
+      W.row = p; p += m * A;
+      W.dclk = p; p += d * A;
+      W.dset = p; p += d * sw;
+      W.sw = sw;
+      W.nm = W.nd = 0u;
+    };
+    carve(W0, S.mcap, S.vdcap, S.vscap);
+    carve(W1, c.MW, c.DW, c.SW);
+    carve(W2, O.mcap, O.vdcap, O.vscap);
     mdead = (uint32_t*)p;
     for (uint32_t j = lane; j < c.MW + c.DW; j += kMoW) mdead[j] = 0u;
     md = p + (c.MW + c.DW + 1u) / 2u;
@@ -331,6 +327,10 @@ __global__ __launch_bounds__(kMoW, MINW) void map_orswot_merge_kernel(crdt_map_o
   uint32_t* const mdn0 = comb + DC;
   uint32_t* const mdn1 = mdn0 + S.dcap;
   uint32_t* const nl = mdn0 + DC;
+  // then the three workspaces' nested deferred set sizes (vdcap_s, DW, vdcap_o)
+  W0.dn = nl + DC;
+  W1.dn = W0.dn + S.vdcap;
+  W2.dn = W1.dn + c.DW;
   uint32_t* const ddead = mdead + c.MW;
   mo_sync();
   BlockTickets<4> sched(n_obj, ctl + 3, lane);  // (sched.h)
@@ -350,18 +350,21 @@ __global__ __launch_bounds__(kMoW, MINW) void map_orswot_merge_kernel(crdt_map_o
     const uint32_t vmS = ls ? S.vn_mem[i * S.kcap + lane] : 0u, vdS = ls ? S.vn_def[i * S.kcap + lane] : 0u;
     const uint32_t vmO = lo ? O.vn_mem[i * O.kcap + lane] : 0u, vdO = lo ? O.vn_def[i * O.kcap + lane] : 0u;
     // every count the loops below trust, within its capacity (the nested
-    // deferred set sizes read capacity-wide, so their loads issue together)
+    // deferred set sizes up to the wave's largest count, so their loads
+    // issue together and no unused slot is read)
     bool bad = vmS > S.mcap || vdS > S.vdcap || vmO > O.mcap || vdO > O.vdcap;
-    if (ls)
-      for (uint32_t d = 0; d < S.vdcap; ++d) {
-        const uint32_t x = S.vdset_n[(i * S.kcap + lane) * S.vdcap + d];
-        bad |= (d < vdS) & (x > S.vscap);
-      }
-    if (lo)
-      for (uint32_t d = 0; d < O.vdcap; ++d) {
-        const uint32_t x = O.vdset_n[(i * O.kcap + lane) * O.vdcap + d];
-        bad |= (d < vdO) & (x > O.vscap);
-      }
+    uint32_t mvd = (vdS < S.vdcap ? vdS : S.vdcap) > (vdO < O.vdcap ? vdO : O.vdcap) ? (vdS < S.vdcap ? vdS : S.vdcap)
+                                                                                   : (vdO < O.vdcap ? vdO : O.vdcap);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const uint32_t t = __shfl_xor(mvd, off, kMoW);
+      mvd = t > mvd ? t : mvd;
+    }
+    mvd = uni(mvd);
+    for (uint32_t d = 0; d < mvd; ++d) {
+      if (ls && d < vdS) bad = bad || S.vdset_n[(i * S.kcap + lane) * S.vdcap + d] > S.vscap;
+      if (lo && d < vdO) bad = bad || O.vdset_n[(i * O.kcap + lane) * O.vdcap + d] > O.vscap;
+    }
     for (uint32_t k = kMoW + lane; k < nS; k += kMoW) {
       const uint64_t ki = i * S.kcap + k;
       bad = bad || S.vn_mem[ki] > S.mcap || S.vn_def[ki] > S.vdcap;
@@ -560,13 +563,14 @@ __global__ __launch_bounds__(kMoW, MINW) void map_orswot_merge_kernel(crdt_map_o
 
 // The kernel's dynamic workspace: self's and other's key slots and their
 // merge (W0, W2, W1), the drop flags, the map deferred bookkeeping (3 x
-// (dcap_s + dcap_o) u32; the nested deferred set sizes are static LDS). This
-// is the bound crdt_map_orswot_merge checks against 64 KB.
+// (dcap_s + dcap_o) u32) and the workspaces' nested deferred set sizes
+// (2 x (vdcap_s + vdcap_o) u32). This is the bound crdt_map_orswot_merge
+// checks against 64 KB.
 size_t map_orswot_lds_bytes(const crdt_map_orswot_slab& S, const crdt_map_orswot_slab& O, uint32_t A) {
   auto per = [&](size_t m, size_t d, size_t s) { return 8 * (m + m * A + d * A + d * s); };
   const size_t MW = S.mcap + O.mcap, DW = S.vdcap + O.vdcap, SW = S.vscap + O.vscap;
   return per(S.mcap, S.vdcap, S.vscap) + per(O.mcap, O.vdcap, O.vscap) + per(MW, DW, SW) + 8 * ((MW + DW + 1) / 2) +
-         8 * ((3 * ((size_t)S.dcap + O.dcap) + 1) / 2);
+         8 * ((3 * ((size_t)S.dcap + O.dcap) + 2 * DW + 1) / 2);
 }
 
 int launch_map_orswot_merge(const crdt_map_orswot_slab& S, const crdt_map_orswot_slab& O,

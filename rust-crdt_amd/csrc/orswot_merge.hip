@@ -3285,7 +3285,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_ring_kern
 // 512 same-address atomics serialised at the memory side cost ~50 us).
 // ======================================================================
 constexpr uint32_t kGenStage = 8192;
-constexpr uint32_t kGenBlocks = 512;
+constexpr uint32_t kGenBlocks = 1536;  // 6 resident 24 KB-LDS blocks per CU
 
 // (the big-object kernel's share of the general list: see orswot_big_kernel)
 constexpr uint32_t kBigW = 8;           // waves per block
@@ -3425,7 +3425,8 @@ __device__ __forceinline__ uint32_t merge_path_in(const S& L, const S& R, uint32
 }
 
 // (ABL, timing only in diag variants: 1 no kill test, 2 no deferred block,
-// 3 no pass 2, 4 no pass 1 join)
+// 3 no pass 2, 4 no pass 1 join; 6 — a real variant — no register cache of
+// the first two chunks, pass 2 from the LDS cache only)
 template <bool SP, int ABL = 0, class S>
 __device__ __forceinline__ void merge_object_block(const S& L, const S& R, uint8_t* O, uint32_t A, uint32_t lane,
                                                    uint32_t wave, const BigTabs& T) {
@@ -3472,8 +3473,8 @@ __device__ __forceinline__ void merge_object_block(const S& L, const S& R, uint8
       }
     }
     const uint32_t q = (type << 30) | (i << 15) | j;  // (k < 2: p < 1024)
-    if (k == 0) { q0 = q; c0 = cnt; x0 = x; v0 = v; }
-    else if (k == 1) { q1 = q; c1 = cnt; x1 = x; v1 = v; }
+    if (ABL != 6 && k == 0) { q0 = q; c0 = cnt; x0 = x; v0 = v; }
+    else if (ABL != 6 && k == 1) { q1 = q; c1 = cnt; x1 = x; v1 = v; }
     const uint32_t m = (uint32_t)__popcll(__ballot(cnt != 0)), d = wave_sum(cnt);
     if (lane == 0u) { T.tot[ch] = m; T.tot[T.cap + ch] = d; }
   }
@@ -3545,7 +3546,7 @@ __device__ __forceinline__ void merge_object_block(const S& L, const S& R, uint8
     uint32_t type = kNone, i = 0, j = 0, cnt = 0, x = 0;
     uint64_t v = 0;
     bool xv = false;  // (x, v) hold the run's only dot
-    if (k < 2u) {
+    if (ABL != 6 && k < 2u) {
       const uint32_t q = k == 0 ? q0 : q1;
       cnt = k == 0 ? c0 : c1; x = k == 0 ? x0 : x1; v = k == 0 ? v0 : v1;
       type = q >> 30; i = (q >> 15) & 0x7FFFu; j = q & 0x7FFFu;
@@ -3608,32 +3609,37 @@ __device__ __forceinline__ void big_one(const uint8_t* Lb, const uint64_t* Loff,
   const uint8_t* rr = Rb + Roff[o];
   const RecLayout LL = layout_at(lr), RL = layout_at(rr);
   const uint32_t szl = LL.size, szr = RL.size, P = LL.n_mem + RL.n_mem;
+  const bool staged = szl <= kBigStage && szr <= kBigStage && P <= kWave * kBigChS;
+  u32x4* sl = st;
+  u32x4* sr = st + kBigStage / 16u;
   if (P > kWave * kBigChH) {  // (past the HBM tables: one wave, merge_object)
     if (wave == 0u) huge_one_wave<SP>(lr, rr, Ob + oo, A, lane);
-  } else if (szl <= kBigStage && szr <= kBigStage && P <= kWave * kBigChS) {
-    // both records staged: every load of the thread issued before its stores
-    u32x4* sl = st;
-    u32x4* sr = st + kBigStage / 16u;
-    constexpr uint32_t kPer = kBigStage / 16u / (kWave * kBigW);
-    const uint32_t nl = szl / 16u, nr = szr / 16u;
-    u32x4 tl[kPer], tr[kPer];
+  } else {
+    if (staged) {
+      // both records staged: every load of the thread issued before its stores
+      constexpr uint32_t kPer = kBigStage / 16u / (kWave * kBigW);
+      const uint32_t nl = szl / 16u, nr = szr / 16u;
+      u32x4 tl[kPer], tr[kPer];
 #pragma unroll
-    for (uint32_t u = 0; u < kPer; ++u) {
-      const uint32_t k = threadIdx.x + u * kWave * kBigW;
-      if (k < nl) tl[u] = ((const u32x4*)lr)[k];
-      if (k < nr) tr[u] = ((const u32x4*)rr)[k];
-    }
+      for (uint32_t u = 0; u < kPer; ++u) {
+        const uint32_t k = threadIdx.x + u * kWave * kBigW;
+        if (k < nl) tl[u] = ((const u32x4*)lr)[k];
+        if (k < nr) tr[u] = ((const u32x4*)rr)[k];
+      }
 #pragma unroll
-    for (uint32_t u = 0; u < kPer; ++u) {
-      const uint32_t k = threadIdx.x + u * kWave * kBigW;
-      if (k < nl) sl[k] = tl[u];
-      if (k < nr) sr[k] = tr[u];
+      for (uint32_t u = 0; u < kPer; ++u) {
+        const uint32_t k = threadIdx.x + u * kWave * kBigW;
+        if (k < nl) sl[k] = tl[u];
+        if (k < nr) sr[k] = tr[u];
+      }
+      __syncthreads();
     }
-    __syncthreads();
-    const SideL L{(lds_cu8*)(size_t)lds_addr(sl), make_rv(LL)}, R{(lds_cu8*)(size_t)lds_addr(sr), make_rv(RL)};
-    if constexpr (ABL != 5) merge_object_block<SP, ABL>(L, R, Ob + oo, A, lane, wave, T);  // (5: staging only)
-  } else {  // from HBM; the tables in the stage
-    big_from_hbm<SP, ABL>(lr, rr, Ob + oo, A, lane, wave, st, T.bc);
+    if (staged) {
+      const SideL L{(lds_cu8*)(size_t)lds_addr(sl), make_rv(LL)}, R{(lds_cu8*)(size_t)lds_addr(sr), make_rv(RL)};
+      if constexpr (ABL != 5) merge_object_block<SP, ABL>(L, R, Ob + oo, A, lane, wave, T);  // (5: staging only)
+    } else {  // from HBM; the tables in the stage
+      big_from_hbm<SP, ABL>(lr, rr, Ob + oo, A, lane, wave, st, T.bc);
+    }
   }
   if (threadIdx.x == 0u) Ooff[o] = oo;
   __syncthreads();
@@ -3734,6 +3740,7 @@ __host__ inline hipError_t launch_big(const uint8_t* Lb, const uint64_t* Loff, c
   if (g_big_variant == 6) fn = (const void*)orswot_big_kernel<false, 4, 3>;
   if (g_big_variant == 7) fn = (const void*)orswot_big_kernel<false, 4, 4>;
   if (g_big_variant == 8) fn = (const void*)orswot_big_kernel<false, 4, 5>;
+  if (g_big_variant == 9) fn = (const void*)orswot_big_kernel<false, 4, 6>;
 #endif
   void* args[] = {&Lb, &Loff, &Rb, &Roff, &Ob, &Ooff, &n_obj, &A, &ctl, &list, &list_cap};
   return hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kBigW), args, 0, stream);
@@ -4136,7 +4143,7 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // (diag variant 320: every such object to the general kernel, as before)
 #ifdef CRDT_DIAG
   g_big_variant = 0;
-  if (variant >= 330 && variant < 340) {  // the big-object kernel's knobs, after the join5 product
+  if (variant >= 330 && variant < 345) {  // the big-object kernel's knobs, after the join5 product
     g_big_variant = variant - 330;
     variant = 310;
   }

@@ -195,3 +195,53 @@ def test_map_orswot_100_map_deferred_clocks(gpu, oracle):
         for f in exp.a:
             bad = np.nonzero((np.asarray(got.a[f]) != np.asarray(exp.a[f])).reshape(S.n, -1).any(axis=1))[0]
             assert bad.size == 0, f"{f}: {bad.size} objects differ, first {bad[:5].tolist()}"
+
+
+def _nested_deferred_map(seed, keys, n_mem, n_rm, me, other):
+    """Map<u64, Orswot> through the op path: per key, n_mem members added by
+    actor `me`, then n_rm member removes whose clocks run ahead on actor
+    `other` (a context from a replica this one has not heard from) — each
+    deferred inside the nested set (src/orswot.rs:190-203), n_rm distinct
+    clocks per key."""
+    import random
+
+    rng = random.Random(seed)
+    m = crdts_ref.Map(crdts_ref.Orswot)
+    for k in range(keys):
+        for j in range(n_mem):
+            add, _, _ = m.get(k)
+            dot = (me, add.get(me) + 1)
+            m.apply_up(dot, k, lambda s, d=dot, x=j: s.apply_add(d, x))
+        for j in range(n_rm):
+            add, _, _ = m.get(k)
+            dot = (me, add.get(me) + 1)
+            ctx = crdts_ref.VClock([(me, rng.randint(1, n_mem)), (other, 40 + 3 * j + rng.randint(0, 2))])
+            m.apply_up(dot, k, lambda s, c=ctx, x=rng.randrange(n_mem): s.apply_rm(c, x))
+    return m
+
+
+def test_map_orswot_nested_deferred_past_32(gpu, oracle):
+    """Past the round-4 nested deferred cap (32 per key per side): nested sets
+    holding 45-60 deferred removes per side (vdcap 64), both orientations,
+    GPU == oracle slab-row exact and == the Python restatement's merge."""
+    import crdts_hip
+
+    A8 = 4
+    a = _nested_deferred_map(1, 3, 24, 60, 0, 1)
+    b = _nested_deferred_map(2, 3, 24, 45, 1, 0)
+    assert max(len(v[1].deferred) for v in a.entries.values()) > 32
+    caps = dict(kcap=4, mcap=32, vdcap=64, vscap=4, dcap=4, scap=4)
+    for x, y in ((a, b), (b, a)):
+        S = crdts_hip.MapOrswotSlab.alloc(1, A8, **caps)
+        O = crdts_hip.MapOrswotSlab.alloc(1, A8, **caps)
+        map_slab.orswot_map_to_row(x, S, 0, A8)
+        map_slab.orswot_map_to_row(y, O, 0, A8)
+        exp = oracle.map_orswot_merge(S, O, A8)
+        got = gpu.map_orswot_merge(S.to("cuda"), O.to("cuda"), A8).host()
+        ce, cg = exp.canonical(), got.canonical()
+        for f in ce.a:
+            assert np.array_equal(np.asarray(cg.a[f]), np.asarray(ce.a[f])), f
+        py = x.clone()
+        py.merge(y)
+        assert map_slab.orswot_map_from_row(got, 0) == py
+        assert max(int(v) for v in np.asarray(ce.a["vn_def"]).reshape(-1)) > 32
