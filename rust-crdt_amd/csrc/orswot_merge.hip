@@ -3291,8 +3291,13 @@ constexpr uint32_t kGenBlocks = 1536;  // 6 resident 24 KB-LDS blocks per CU
 constexpr uint32_t kBigW = 8;           // waves per block
 constexpr uint32_t kBigStage = 32768;   // LDS stage per record
 
+#ifndef CRDT_BIG_MIN_POS
+#define CRDT_BIG_MIN_POS 128
+#endif
+constexpr uint32_t kBigMinPos = CRDT_BIG_MIN_POS;  // union positions past which an object takes the block join
+
 __device__ __forceinline__ bool is_big(u32x4 hl0, u32x4 hr0) {
-  return hl0.z + hr0.z > 2u * kWave || hl0.x > kGenStage || hr0.x > kGenStage;
+  return hl0.z + hr0.z > kBigMinPos || hl0.x > kGenStage || hr0.x > kGenStage;
 }
 
 __device__ __forceinline__ void general_one(const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb,
