@@ -75,6 +75,9 @@ def parse():
     p.add_argument("--no-anti-entropy", action="store_true",
                    help="N > 1: skip the config-4/5 anti-entropy sub-measurements of the headline line")
     p.add_argument("--ae-steps", type=int, default=3, help="timed steps of each anti-entropy sub-measurement")
+    p.add_argument("--ae-deadline", type=float, default=300.0,
+                   help="N > 1: seconds the anti-entropy sub-measurements may take; past it every rank ends the run "
+                        "and rank 0 prints the headline line with the anti-entropy part marked unfinished")
     p.add_argument("--ae-n-obj", type=int, default=None,
                    help="objects of the anti-entropy sub-measurements (default: the configs' own sizes)")
     p.add_argument("--rehearse", action="store_true",
@@ -363,16 +366,75 @@ def run_orswot(args, rank, world, local):
         if not args.no_anti_entropy:
             # configs 4 and 5 over the same ranks (the driver's multi-GPU run
             # measures and checks them with the headline), each with its own
-            # timed region, checked after it
+            # timed region, checked after it. A watchdog bounds them: the
+            # headline is measured already, and a collective that never
+            # returns must not cost it (_ae_watchdog)
             sub = argparse.Namespace(**vars(args))
             sub.steps, sub.warmup, sub.n_obj, sub.no_cpu_baseline = args.ae_steps, 1, args.ae_n_obj, True
             res["anti_entropy"] = {}
-            for key, fn in (("config4_gcounter", run_gcounter_ae), ("config5_orswot_csr", run_orswot_csr)):
-                r = fn(sub, rank, world, local, eng=eng)
-                res["anti_entropy"][key] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "steps",
-                                                              "config", "comm", "check") if k in r}
-                torch.cuda.empty_cache()
+            dog = _ae_watchdog(args, rank, res)
+            errored = False
+            try:
+                for key, fn in (("config4_gcounter", run_gcounter_ae), ("config5_orswot_csr", run_orswot_csr)):
+                    try:
+                        r = fn(sub, rank, world, local, eng=eng)
+                    except Exception as e:  # noqa: BLE001 — reported in the line; the headline stands
+                        # (peers may be left in a collective: the watchdog stays
+                        # armed so that every rank still ends by the deadline)
+                        res["anti_entropy"][key] = {"error": f"{type(e).__name__}: {e}"[:400]}
+                        errored = True
+                        break
+                    res["anti_entropy"][key] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "steps",
+                                                                  "config", "comm", "check") if k in r}
+                    torch.cuda.empty_cache()
+            finally:
+                if not errored:
+                    dog.cancel()
     return res
+
+
+_PRINT_LOCK = None
+
+
+def _emit(res):
+    """Rank 0's one JSON line, printed at most once (the main thread or the
+    anti-entropy watchdog, whichever comes first)."""
+    global _PRINT_LOCK
+    import threading
+
+    if _PRINT_LOCK is None:
+        _PRINT_LOCK = threading.Lock()
+    with _PRINT_LOCK:
+        if getattr(_emit, "done", False):
+            return False
+        _emit.done = True
+        print(json.dumps(res), flush=True)
+        return True
+
+
+def _ae_watchdog(args, rank, res):
+    """Past --ae-deadline seconds in the anti-entropy part, every rank ends
+    the process (exit 0: the headline was measured and checked before it);
+    rank 0 first prints the line, the unfinished sub-measurements marked.
+    os._exit, not exec: nothing replaces the process."""
+    import threading
+
+    def fire():
+        if rank == 0:
+            out = dict(res)
+            out["anti_entropy"] = dict(res.get("anti_entropy", {}))
+            out["anti_entropy"]["unfinished"] = f"stopped after {args.ae_deadline:.0f} s (--ae-deadline)"
+            if SETTLE:
+                out["settle"] = dict(SETTLE)
+            _emit(out)
+        sys.stderr.write(f"bench.py rank {rank}: anti-entropy past --ae-deadline, exiting\n")
+        sys.stderr.flush()
+        os._exit(0)
+
+    t = threading.Timer(args.ae_deadline, fire)
+    t.daemon = True
+    t.start()
+    return t
 
 
 def cpu_baseline_orswot(lb, lo, rb, ro, args):
@@ -1721,7 +1783,7 @@ def main():
             res["build"] = crdts_hip.build_record()  # the library this run loaded, vs __graft_entry__.build()'s record
         if SETTLE:
             res["settle"] = dict(SETTLE)
-        print(json.dumps(res), flush=True)
+        _emit(res)
     if failed:
         raise SystemExit(f"bench.py rank {rank}: cross-rank check failed: {failed}")
     if world > 1:
