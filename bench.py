@@ -360,9 +360,11 @@ def run_orswot(args, rank, world, local):
 
         del L, R, out, lb, lo, rb, ro
         torch.cuda.empty_cache()
+        dog0 = _ae_watchdog(args, rank, res)  # (the communicator's setup is bounded too)
         if not args.rehearse:
             replica.init_comm(eng)  # the context's RCCL communicator: its rank count is reported
             res["comm"] = {"rccl_ranks": eng.comm_count()}
+        dog0.cancel()
         if not args.no_anti_entropy:
             # configs 4 and 5 over the same ranks (the driver's multi-GPU run
             # measures and checks them with the headline), each with its own
