@@ -361,11 +361,17 @@ def run_orswot(args, rank, world, local):
         del L, R, out, lb, lo, rb, ro
         torch.cuda.empty_cache()
         dog0 = _ae_watchdog(args, rank, res)  # (the communicator's setup is bounded too)
+        comm_ok = True
         if not args.rehearse:
-            replica.init_comm(eng)  # the context's RCCL communicator: its rank count is reported
-            res["comm"] = {"rccl_ranks": eng.comm_count()}
-        dog0.cancel()
-        if not args.no_anti_entropy:
+            try:
+                replica.init_comm(eng)  # the context's RCCL communicator: its rank count is reported
+                res["comm"] = {"rccl_ranks": eng.comm_count()}
+            except Exception as e:  # noqa: BLE001 — reported; the headline stands, anti-entropy skipped
+                res["comm"] = {"error": f"{type(e).__name__}: {e}"[:400]}
+                comm_ok = False
+        if comm_ok:
+            dog0.cancel()
+        if comm_ok and not args.no_anti_entropy:
             # configs 4 and 5 over the same ranks (the driver's multi-GPU run
             # measures and checks them with the headline), each with its own
             # timed region, checked after it. A watchdog bounds them: the
