@@ -1957,8 +1957,9 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   const uint64_t cvl = DN ? 0ull : ld64(Ls, kHdrBytes + 8u * lane), cvr = DN ? 0ull : ld64(Rs, kHdrBytes + 8u * lane);
   if (!DN && __ballot((hcl && cxl >= kSpTableN) || (hcr && cxr >= kSpTableN)) != 0ull) return kLeanFallback;
   wave_sync();  // the previous object's readers of this scratch are done
-  if (DN) {  // one bitmap word per 64 actors: lane a of round q <-> actor 64 q + a
-    for (uint32_t q = 0; q < kSpTableN / 64u; ++q) {
+  if (DN) {  // one bitmap word per 64 actors: lane a of round q <-> actor 64 q + a (words past A stay 0)
+    if (lane < kSpTableN / 64u) *(uint64_t*)(X + kSpUbm + 8u * lane) = 0ull;
+    for (uint32_t q = 0; q < (A + 63u) / 64u; ++q) {
       const uint32_t a = 64u * q + lane;
       const bool p = a < A && (ld64(Ls, kHdrBytes + 8u * a) | ld64(Rs, kHdrBytes + 8u * a)) != 0ull;
       const uint64_t w = __ballot(p);
