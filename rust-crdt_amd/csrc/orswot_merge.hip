@@ -3301,16 +3301,42 @@ __device__ __forceinline__ bool is_big(u32x4 hl0, u32x4 hr0) {
   return hl0.z + hr0.z > kBigMinPos || hl0.x > kGenStage || hr0.x > kGenStage;
 }
 
-__device__ __forceinline__ void general_one(const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb,
-                                            const uint64_t* Roff, uint8_t* Ob, uint64_t* Ooff, uint64_t o, uint32_t A,
-                                            u32x4* sl, u32x4* sr, u32x4* so, uint32_t lane) {
-  const uint64_t oo = Ooff[o] & ~kPending;
-  const uint8_t* lr = Lb + Loff[o];
-  const uint8_t* rr = Rb + Roff[o];
-  const u32x4 hl0 = ((const u32x4*)lr)[0], hl1 = ((const u32x4*)lr)[1];
-  const u32x4 hr0 = ((const u32x4*)rr)[0], hr1 = ((const u32x4*)rr)[1];
+// A listed object's offsets and headers, loaded ahead of its join.
+struct GenPre {
+  uint64_t o, oo;
+  const uint8_t* lr;
+  const uint8_t* rr;
+  u32x4 hl0, hl1, hr0, hr1;
+};
+// the offsets (one round trip), then the header loads issued (not waited on)
+__device__ __forceinline__ void gen_pre(GenPre& g, const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb,
+                                        const uint64_t* Roff, const uint64_t* Ooff, uint64_t o) {
+  g.o = o;
+  g.oo = Ooff[o] & ~kPending;
+  g.lr = Lb + Loff[o];
+  g.rr = Rb + Roff[o];
+  g.hl0 = ((const u32x4*)g.lr)[0];
+  g.hl1 = ((const u32x4*)g.lr)[1];
+  g.hr0 = ((const u32x4*)g.rr)[0];
+  g.hr1 = ((const u32x4*)g.rr)[1];
+}
+
+// One listed object; `mid` runs once the records are staged (or at once for
+// an object this kernel leaves to orswot_big_kernel): the caller's loads for
+// the next object, in flight during this one's join.
+template <class Mid>
+__device__ __forceinline__ void general_one(const GenPre& g, uint8_t* Ob, uint64_t* Ooff, uint32_t A, u32x4* sl,
+                                            u32x4* sr, u32x4* so, uint32_t lane, Mid&& mid) {
+  const uint64_t o = g.o, oo = g.oo;
+  const uint8_t* lr = g.lr;
+  const uint8_t* rr = g.rr;
+  const u32x4 hl0 = g.hl0, hl1 = g.hl1, hr0 = g.hr0, hr1 = g.hr1;
   const uint32_t szl = uni(hl0.x), szr = uni(hr0.x);
-  if (is_big(u32x4{szl, 0u, uni(hl0.z), 0u}, u32x4{szr, 0u, uni(hr0.z), 0u})) return;  // orswot_big_kernel's
+  if (is_big(u32x4{szl, 0u, uni(hl0.z), 0u}, u32x4{szr, 0u, uni(hr0.z), 0u})) {  // orswot_big_kernel's
+    mid();
+    return;
+  }
+  if (szl > kGenStage || szr > kGenStage) mid();
   if (szl <= kGenStage && szr <= kGenStage) {
     wave_sync();
     // both records staged 4 KB per side at a time: every load of a round is
@@ -3334,22 +3360,29 @@ __device__ __forceinline__ void general_one(const uint8_t* Lb, const uint64_t* L
         }
       }
     }
+    mid();
     wave_sync();
     // the join kernel's mask3 join when its limits hold (<= 64 members and
-    // dots per side, <= 32 deferred clocks per side, A <= 32: in config 3 the
+    // dots per side, <= 32 deferred clocks per side, A <= 64: in config 3 the
     // objects sent here are records just past the join kernel's 2 KB stage),
     // else the older fast join, with the general kernel's larger stages
     uint32_t n16 = ~0u;
     const uint32_t nL = uni(hl0.z), nR = uni(hr0.z), dL = uni(hl0.w), dR = uni(hr0.w);
     bool done = false;
-    if (A <= 32u && nL <= 64u && nR <= 64u && dL <= 64u && dR <= 64u && uni(hl1.x) <= 32u && uni(hr1.x) <= 32u) {
+    if (A <= 64u && nL <= 64u && nR <= 64u && dL <= 64u && dR <= 64u && uni(hl1.x) <= 32u && uni(hr1.x) <= 32u) {
       bool big = false;
-      const uint32_t r =
-          (uni(hl1.x) | uni(hr1.x)) != 0u
-              ? mask3_object<0xFFFFFFFFu, 0, true>(lds_addr(sl), lds_addr(sr), lds_addr(so), Ob + oo, A, nL, dL, nR, dR,
-                                                   lane, big)
-              : mask3_object<0xFFFFFFFFu, 0, false>(lds_addr(sl), lds_addr(sr), lds_addr(so), Ob + oo, A, nL, dL, nR,
-                                                    dR, lane, big);
+      const bool hd = (uni(hl1.x) | uni(hr1.x)) != 0u;
+      uint32_t r;
+      if (A <= 32u)
+        r = hd ? mask3_object<0xFFFFFFFFu, 0, true>(lds_addr(sl), lds_addr(sr), lds_addr(so), Ob + oo, A, nL, dL, nR,
+                                                    dR, lane, big)
+               : mask3_object<0xFFFFFFFFu, 0, false>(lds_addr(sl), lds_addr(sr), lds_addr(so), Ob + oo, A, nL, dL, nR,
+                                                     dR, lane, big);
+      else  // 33-64 actors: the 64-bit actor-mask form of join5<5, 64> (M3Lay<64> fits the scratch)
+        r = hd ? mask3_object<0xFFFFFFFFu, 0, true, 0, true, 0, true, 1, 64>(lds_addr(sl), lds_addr(sr), lds_addr(so),
+                                                                             Ob + oo, A, nL, dL, nR, dR, lane, big)
+               : mask3_object<0xFFFFFFFFu, 0, false, 0, true, 0, true, 1, 64>(lds_addr(sl), lds_addr(sr), lds_addr(so),
+                                                                              Ob + oo, A, nL, dL, nR, dR, lane, big);
       done = r != kLeanFallback && !big;
       wave_sync();  // the scratch (so) is reused below
     }
@@ -3710,17 +3743,29 @@ __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
   // entry past the count is stale and not used)
   const uint64_t first = blockIdx.x < list_cap ? list[blockIdx.x] : 0ull;
   if (n <= list_cap && scan == 0u) {
-    for (uint32_t e = blockIdx.x; e < n; e += gridDim.x)
-      general_one(Lb, Loff, Rb, Roff, Ob, Ooff, e == blockIdx.x ? first : list[e], A, gen_s[0], gen_s[1], gen_s[2],
-                  lane);
+    // one object ahead: its list entry at the top of this one, its offsets
+    // and headers while this one's records are staged and joined
+    if (blockIdx.x >= n) return;
+    GenPre cur, nxt;
+    gen_pre(cur, Lb, Loff, Rb, Roff, Ooff, first);
+    for (uint32_t e = blockIdx.x; e < n; e += gridDim.x) {
+      const uint32_t en = e + gridDim.x;
+      const uint64_t on = en < n ? list[en] : 0ull;
+      general_one(cur, Ob, Ooff, A, gen_s[0], gen_s[1], gen_s[2], lane, [&]() {
+        if (en < n) gen_pre(nxt, Lb, Loff, Rb, Roff, Ooff, on);
+      });
+      cur = nxt;
+    }
   } else {  // list overflow, or objects flagged without a list entry: scan the flags
     const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
     for (uint64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
       const uint64_t obj = chunk * kWave + lane;
       const uint64_t oo = obj < n_obj ? Ooff[obj] : 0ull;
-      for (uint64_t pend = __ballot((oo & kPending) != 0ull); pend; pend &= pend - 1)
-        general_one(Lb, Loff, Rb, Roff, Ob, Ooff, chunk * kWave + (uint32_t)__builtin_ctzll(pend), A, gen_s[0],
-                    gen_s[1], gen_s[2], lane);
+      for (uint64_t pend = __ballot((oo & kPending) != 0ull); pend; pend &= pend - 1) {
+        GenPre g;
+        gen_pre(g, Lb, Loff, Rb, Roff, Ooff, chunk * kWave + (uint32_t)__builtin_ctzll(pend));
+        general_one(g, Ob, Ooff, A, gen_s[0], gen_s[1], gen_s[2], lane, []() {});
+      }
     }
   }
 }
