@@ -3428,6 +3428,24 @@ constexpr uint32_t kBigChS = 96;     // chunk capacity, staged records (<= 86 po
 constexpr uint32_t kBigChH = 4096;   // chunk capacity, records from HBM (P <= 262 144; past it: one wave)
 constexpr uint32_t kBigPos = 4096;   // positions whose candidate / count pass 1 keeps in LDS
 
+// ABL 8 (diag): wave 0's per-phase cycles of the big-object join, summed over
+// objects (crdt_debug_big_stamps reads and clears them)
+#ifdef CRDT_DIAG
+__device__ unsigned long long g_big_st[16];
+#endif
+template <int ABL>
+__device__ __forceinline__ void bst(uint64_t& last, uint32_t k, uint32_t wave, uint32_t lane) {
+#ifdef CRDT_DIAG
+  if constexpr (ABL == 8) {
+    if (wave == 0u) {
+      const uint64_t t = stamp();
+      if (lane == 0u) atomicAdd(&g_big_st[k], (unsigned long long)(t - last));
+      last = t;
+    }
+  }
+#endif
+}
+
 struct BigTabs {
   uint32_t* tot;  // 2 x cap: per-chunk kept members, then dots (then their exclusive prefixes)
   uint32_t* spl;  // cap + 1: self keys before each chunk's first position
@@ -3436,6 +3454,7 @@ struct BigTabs {
   uint32_t* bc;   // 4: grand totals
   uint32_t cap;
   uint32_t* bloom;  // 32: the deferred member filter (dm_maybe)
+  uint64_t* last;   // (ABL 8: wave 0's stamp)
 };
 
 // merge_path with the answer known to lie in [ilo, ihi], ihi - ilo <= 64.
@@ -3492,6 +3511,7 @@ __device__ __forceinline__ void merge_object_block(const S& L, const S& R, uint8
     T.spl[c] = i;
   }
   __syncthreads();
+  if (T.last) bst<ABL>(*T.last, 2, wave, lane);
   // ---- pass 1: per chunk (64 union positions) its kept members and dots;
   // a wave's first two chunks stay in registers for pass 2, every position
   // below kBigPos leaves its candidate and count in LDS
@@ -3518,7 +3538,10 @@ __device__ __forceinline__ void merge_object_block(const S& L, const S& R, uint8
     if (lane == 0u) { T.tot[ch] = m; T.tot[T.cap + ch] = d; }
   }
   __syncthreads();
+  if (T.last) bst<ABL>(*T.last, 3, wave, lane);
   // ---- exclusive prefix of the chunk totals (wave 0), and the grand totals
+  // (every wave scanning the table itself, no barrier, measured the same:
+  // the CU's two objects are bound by their joins, not by this wait)
   if (wave == 0u) {
     uint32_t cm = 0, cd = 0;
     for (uint32_t b = 0; b < nch; b += kWave) {
@@ -3533,6 +3556,7 @@ __device__ __forceinline__ void merge_object_block(const S& L, const S& R, uint8
   }
   __syncthreads();
   const uint32_t tot_mem = uni(T.bc[0]), tot_dot = uni(T.bc[1]);
+  if (T.last) bst<ABL>(*T.last, 4, wave, lane);
   const uint32_t o_key = kHdrBytes + clock_bytes(n_clk, SP);
   const uint32_t o_dctr = o_key + 8u * tot_mem;
   const uint32_t o_dact = o_dctr + 8u * tot_dot;
@@ -3616,7 +3640,9 @@ __device__ __forceinline__ void merge_object_block(const S& L, const S& R, uint8
       omdend[midx] = d0 + cnt;
     }
   }
+  if (T.last) bst<ABL>(*T.last, 5, wave, lane);
   __syncthreads();  // the stages and the tables are free for the next object
+  if (T.last) bst<ABL>(*T.last, 6, wave, lane);
 }
 
 template <bool SP, int ABL>
@@ -3625,7 +3651,7 @@ __device__ __noinline__ void big_from_hbm(const uint8_t* lr, const uint8_t* rr, 
   uint8_t* sb = (uint8_t*)st;
   const BigTabs H{(uint32_t*)sb, (uint32_t*)(sb + 8u * kBigChH), (uint16_t*)(sb + 12u * kBigChH + 16u),
                   (uint8_t*)(sb + 12u * kBigChH + 16u + 2u * kBigPos), bc, kBigChH,
-                  (uint32_t*)(sb + 12u * kBigChH + 16u + 3u * kBigPos)};
+                  (uint32_t*)(sb + 12u * kBigChH + 16u + 3u * kBigPos), nullptr};
   static_assert(12u * kBigChH + 16u + 3u * kBigPos + 128u <= 2u * kBigStage, "HBM-path tables fit the stage");
   const RecLayout LL = layout_at(lr), RL = layout_at(rr);
   const Side L{lr, make_rv(LL)}, R{rr, make_rv(RL)};
@@ -3643,12 +3669,14 @@ template <bool SP, int ABL = 0>
 __device__ __forceinline__ void big_one(const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb,
                                         const uint64_t* Roff, uint8_t* Ob, uint64_t* Ooff, uint64_t o, uint32_t A,
                                         u32x4* st, const BigTabs& T, uint32_t lane, uint32_t wave) {
+  if (T.last) bst<ABL>(*T.last, 8, wave, lane);  // (8: between objects: the list walk)
   const uint64_t oo = Ooff[o] & ~kPending;
   const uint8_t* lr = Lb + Loff[o];
   const uint8_t* rr = Rb + Roff[o];
   const RecLayout LL = layout_at(lr), RL = layout_at(rr);
   const uint32_t szl = LL.size, szr = RL.size, P = LL.n_mem + RL.n_mem;
   const bool staged = szl <= kBigStage && szr <= kBigStage && P <= kWave * kBigChS;
+  if (T.last) bst<ABL>(*T.last, 0, wave, lane);
   u32x4* sl = st;
   u32x4* sr = st + kBigStage / 16u;
   if (P > kWave * kBigChH) {  // (past the HBM tables: one wave, merge_object)
@@ -3672,6 +3700,7 @@ __device__ __forceinline__ void big_one(const uint8_t* Lb, const uint64_t* Loff,
         if (k < nr) sr[k] = tr[u];
       }
       __syncthreads();
+      if (T.last) bst<ABL>(*T.last, 1, wave, lane);
     }
     if (staged) {
       const SideL L{(lds_cu8*)(size_t)lds_addr(sl), make_rv(LL)}, R{(lds_cu8*)(size_t)lds_addr(sr), make_rv(RL)};
@@ -3682,6 +3711,10 @@ __device__ __forceinline__ void big_one(const uint8_t* Lb, const uint64_t* Loff,
   }
   if (threadIdx.x == 0u) Ooff[o] = oo;
   __syncthreads();
+  if (T.last) bst<ABL>(*T.last, 7, wave, lane);
+#ifdef CRDT_DIAG
+  if (ABL == 8 && threadIdx.x == 0u) atomicAdd(&g_big_st[15], 1ull);
+#endif
 }
 
 // The listed objects is_big() picks (the general kernel, launched before,
@@ -3697,7 +3730,9 @@ __global__ __launch_bounds__(kWave * kBigW, MINW) void orswot_big_kernel(
   __shared__ uint16_t pq_s[kBigPos];
   __shared__ uint8_t pc_s[kBigPos];
   __shared__ uint32_t bloom_s[32];
-  const BigTabs T{tot_s, spl_s, pq_s, pc_s, bc_s, kBigChS, bloom_s};
+  uint64_t last = 0;
+  if (ABL == 8) last = stamp();
+  const BigTabs T{tot_s, spl_s, pq_s, pc_s, bc_s, kBigChS, bloom_s, ABL == 8 ? &last : nullptr};
   const uint32_t lane = threadIdx.x & (kWave - 1), wave = uni(threadIdx.x / kWave);
   const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   const uint32_t scan = uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -3792,6 +3827,7 @@ __host__ inline hipError_t launch_big(const uint8_t* Lb, const uint64_t* Loff, c
   if (g_big_variant == 7) fn = (const void*)orswot_big_kernel<false, 4, 4>;
   if (g_big_variant == 8) fn = (const void*)orswot_big_kernel<false, 4, 5>;
   if (g_big_variant == 9) fn = (const void*)orswot_big_kernel<false, 4, 6>;
+  if (g_big_variant == 11) fn = (const void*)orswot_big_kernel<false, 4, 8>;
 #endif
   void* args[] = {&Lb, &Loff, &Rb, &Roff, &Ob, &Ooff, &n_obj, &A, &ctl, &list, &list_cap};
   return hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kBigW), args, 0, stream);
@@ -4440,3 +4476,16 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
 
 
 }  // namespace crdts_hip
+
+#ifdef CRDT_DIAG
+// Diagnostic build only: wave 0's per-phase cycle sums of orswot_big_kernel's
+// ABL 8 variant (diag variant 341), [15] = objects; read and cleared.
+extern "C" int crdt_debug_big_stamps(uint64_t* h16) {
+  unsigned long long z[16] = {};
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpyFromSymbol(h16, HIP_SYMBOL(crdts_hip::g_big_st), sizeof(z)) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(crdts_hip::g_big_st), z, sizeof(z)) != hipSuccess)
+    return CRDT_EHIP;
+  return CRDT_OK;
+}
+#endif
