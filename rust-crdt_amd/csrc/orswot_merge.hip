@@ -3277,13 +3277,14 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_ring_kern
 
 // ======================================================================
 // General path: objects the fast kernel flagged (records larger than its
-// stage, > 128 union positions, > 32 deferred clocks on a side). The fast
-// kernel appends them to a list; a small fixed grid of single-wave blocks
-// joins each one, staged through LDS when both records fit kGenStage, else
-// straight from HBM, and clears its flag. If the list overflowed, the blocks
-// scan every output offset for flags instead. The list counter is cleared by
-// an async memset queued before the fast kernel (no finishing-block ticket:
-// 512 same-address atomics serialised at the memory side cost ~50 us).
+// stage, > 64 members or dots on a side, > 32 deferred clocks on a side). The
+// fast kernel appends them to a list; a grid of single-wave blocks (6 per CU,
+// LDS-bound) joins each one from LDS stages of kGenStage per record, the next
+// listed object's offsets and headers in flight meanwhile, and clears its
+// flag. Objects past 128 union positions or the stage (is_big) are left
+// flagged for orswot_big_kernel, launched after it. If the list overflowed,
+// both kernels scan every output offset for flags instead. The list counter
+// is cleared by the alternating control-word sets (launch_join_passes).
 // ======================================================================
 constexpr uint32_t kGenStage = 8192;
 constexpr uint32_t kGenBlocks = 1536;  // 6 resident 24 KB-LDS blocks per CU
