@@ -3981,23 +3981,18 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
 // than the pair stage, or a union past 64 clock entries / members), staged
 // through LDS when both records fit kGenStage: joined by sparse_mask_object
 // when its limits hold, else by merge_object<true>.
-// One sparse join of the records at lr and rr into O (any sizes).
-__device__ void sparse_join_ptrs(const uint8_t* lr, const uint8_t* rr, uint8_t* O, uint32_t A, u32x4* sl, u32x4* sr,
-                                 uint8_t* X, uint32_t lane);
-
-__device__ __forceinline__ void sparse_general_one(const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb,
-                                                   const uint64_t* Roff, uint8_t* Ob, uint64_t* Ooff, uint64_t o,
-                                                   uint32_t A, u32x4* sl, u32x4* sr, uint8_t* X, uint32_t lane) {
-  const uint64_t oo = Ooff[o] & ~kPending;
-  sparse_join_ptrs(Lb + Loff[o], Rb + Roff[o], Ob + oo, A, sl, sr, X, lane);
-  if (lane == 0) Ooff[o] = oo;
-}
-
-__device__ void sparse_join_ptrs(const uint8_t* lr, const uint8_t* rr, uint8_t* O, uint32_t A, u32x4* sl, u32x4* sr,
-                                 uint8_t* X, uint32_t lane) {
-  const u32x4 hl0 = ((const u32x4*)lr)[0], hl1 = ((const u32x4*)lr)[1];
-  const u32x4 hr0 = ((const u32x4*)rr)[0], hr1 = ((const u32x4*)rr)[1];
+// One sparse join of the pre-loaded object g (GenPre: offsets, headers) into
+// its output place (any sizes); `mid` runs once the records are staged (the
+// caller's loads for the next listed object, in flight during this join).
+template <class Mid>
+__device__ __forceinline__ void sparse_general_one(const GenPre& g, uint8_t* Ob, uint64_t* Ooff, uint32_t A,
+                                                   u32x4* sl, u32x4* sr, uint8_t* X, uint32_t lane, Mid&& mid) {
+  const uint8_t* lr = g.lr;
+  const uint8_t* rr = g.rr;
+  uint8_t* O = Ob + g.oo;
+  const u32x4 hl0 = g.hl0, hl1 = g.hl1, hr0 = g.hr0, hr1 = g.hr1;
   const uint32_t szl = uni(hl0.x), szr = uni(hr0.x);
+  if (szl > kGenStage || szr > kGenStage) mid();
   if (szl <= kGenStage && szr <= kGenStage) {
     wave_sync();
     // both records staged 4 KB per side at a time: every load of a round is
@@ -4021,6 +4016,7 @@ __device__ void sparse_join_ptrs(const uint8_t* lr, const uint8_t* rr, uint8_t* 
         }
       }
     }
+    mid();
     wave_sync();
     uint32_t r = kLeanFallback;
     const uint32_t cL = uni(hl0.y), nL = uni(hl0.z), dL = uni(hl0.w), cR = uni(hr0.y), nR = uni(hr0.z),
@@ -4038,6 +4034,7 @@ __device__ void sparse_join_ptrs(const uint8_t* lr, const uint8_t* rr, uint8_t* 
   } else {
     merge_object<true>(lr, rr, O, A, lane);
   }
+  if (lane == 0) Ooff[g.o] = g.oo;
 }
 
 __global__ __launch_bounds__(kWave) void orswot_sparse_general_kernel(
@@ -4051,16 +4048,28 @@ __global__ __launch_bounds__(kWave) void orswot_sparse_general_kernel(
   if (zero4 && blockIdx.x == 0u && lane < 4u) zero4[lane] = 0u;  // (the next launch's words: as the dense path)
   const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (n <= list_cap) {
-    for (uint32_t e = blockIdx.x; e < n; e += gridDim.x)
-      sparse_general_one(Lb, Loff, Rb, Roff, Ob, Ooff, list[e], A, gen_s[0], gen_s[1], (uint8_t*)gx_s, lane);
+    // one object ahead, as the dense general kernel
+    if (blockIdx.x >= n) return;
+    GenPre cur, nxt;
+    gen_pre(cur, Lb, Loff, Rb, Roff, Ooff, list[blockIdx.x]);
+    for (uint32_t e = blockIdx.x; e < n; e += gridDim.x) {
+      const uint32_t en = e + gridDim.x;
+      const uint64_t on = en < n ? list[en] : 0ull;
+      sparse_general_one(cur, Ob, Ooff, A, gen_s[0], gen_s[1], (uint8_t*)gx_s, lane, [&]() {
+        if (en < n) gen_pre(nxt, Lb, Loff, Rb, Roff, Ooff, on);
+      });
+      cur = nxt;
+    }
   } else {  // list overflow: scan the flags
     const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
     for (uint64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
       const uint64_t obj = chunk * kWave + lane;
       const uint64_t oo = obj < n_obj ? Ooff[obj] : 0ull;
-      for (uint64_t pend = __ballot((oo & kPending) != 0ull); pend; pend &= pend - 1)
-        sparse_general_one(Lb, Loff, Rb, Roff, Ob, Ooff, chunk * kWave + (uint32_t)__builtin_ctzll(pend), A,
-                           gen_s[0], gen_s[1], (uint8_t*)gx_s, lane);
+      for (uint64_t pend = __ballot((oo & kPending) != 0ull); pend; pend &= pend - 1) {
+        GenPre g;
+        gen_pre(g, Lb, Loff, Rb, Roff, Ooff, chunk * kWave + (uint32_t)__builtin_ctzll(pend));
+        sparse_general_one(g, Ob, Ooff, A, gen_s[0], gen_s[1], (uint8_t*)gx_s, lane, []() {});
+      }
     }
   }
 }
