@@ -3325,8 +3325,9 @@ __device__ __forceinline__ void gen_pre(GenPre& g, const uint8_t* Lb, const uint
 // One listed object; `mid` runs once the records are staged (or at once for
 // an object this kernel leaves to orswot_big_kernel): the caller's loads for
 // the next object, in flight during this one's join.
+// (returns true for an object it leaves to orswot_big_kernel)
 template <class Mid>
-__device__ __forceinline__ void general_one(const GenPre& g, uint8_t* Ob, uint64_t* Ooff, uint32_t A, u32x4* sl,
+__device__ __forceinline__ bool general_one(const GenPre& g, uint8_t* Ob, uint64_t* Ooff, uint32_t A, u32x4* sl,
                                             u32x4* sr, u32x4* so, uint32_t lane, Mid&& mid) {
   const uint64_t o = g.o, oo = g.oo;
   const uint8_t* lr = g.lr;
@@ -3335,7 +3336,7 @@ __device__ __forceinline__ void general_one(const GenPre& g, uint8_t* Ob, uint64
   const uint32_t szl = uni(hl0.x), szr = uni(hr0.x);
   if (is_big(u32x4{szl, 0u, uni(hl0.z), 0u}, u32x4{szr, 0u, uni(hr0.z), 0u})) {  // orswot_big_kernel's
     mid();
-    return;
+    return true;
   }
   if (szl > kGenStage || szr > kGenStage) mid();
   if (szl <= kGenStage && szr <= kGenStage) {
@@ -3407,6 +3408,7 @@ __device__ __forceinline__ void general_one(const GenPre& g, uint8_t* Ob, uint64
     merge_object(lr, rr, Ob + oo, A, lane);
   }
   if (lane == 0) Ooff[o] = oo;
+  return false;
 }
 
 // ======================================================================
@@ -3737,7 +3739,11 @@ __global__ __launch_bounds__(kWave * kBigW, MINW) void orswot_big_kernel(
   const uint32_t lane = threadIdx.x & (kWave - 1), wave = uni(threadIdx.x / kWave);
   const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   const uint32_t scan = uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  if (n == 0u) return;
+  // ctl[2]: set by the general kernel when it left a big object (zeroed
+  // between launches, so 0 means none; the join variants that use the word
+  // otherwise only make it non-zero: a full walk, still exact)
+  const uint32_t nbig = uni(__hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (n == 0u || nbig == 0u) return;
   // listed: the list in 64-entry chunks dealt round-robin to the blocks (no
   // ticket: every control word is some join variant's), each wave reading
   // the chunk's headers; list overflow / unlisted flags: every pending object
@@ -3784,14 +3790,18 @@ __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
     if (blockIdx.x >= n) return;
     GenPre cur, nxt;
     gen_pre(cur, Lb, Loff, Rb, Roff, Ooff, first);
+    bool big = false;
     for (uint32_t e = blockIdx.x; e < n; e += gridDim.x) {
       const uint32_t en = e + gridDim.x;
       const uint64_t on = en < n ? list[en] : 0ull;
-      general_one(cur, Ob, Ooff, A, gen_s[0], gen_s[1], gen_s[2], lane, [&]() {
+      big |= general_one(cur, Ob, Ooff, A, gen_s[0], gen_s[1], gen_s[2], lane, [&]() {
         if (en < n) gen_pre(nxt, Lb, Loff, Rb, Roff, Ooff, on);
       });
       cur = nxt;
     }
+    // one store per wave that left a big object (not one atomic per object:
+    // same-address atomics serialise at the memory side)
+    if (big && lane == 0u) __hip_atomic_store(&ctl[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {  // list overflow, or objects flagged without a list entry: scan the flags
     const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
     for (uint64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
@@ -3800,7 +3810,8 @@ __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
       for (uint64_t pend = __ballot((oo & kPending) != 0ull); pend; pend &= pend - 1) {
         GenPre g;
         gen_pre(g, Lb, Loff, Rb, Roff, Ooff, chunk * kWave + (uint32_t)__builtin_ctzll(pend));
-        general_one(g, Ob, Ooff, A, gen_s[0], gen_s[1], gen_s[2], lane, []() {});
+        if (general_one(g, Ob, Ooff, A, gen_s[0], gen_s[1], gen_s[2], lane, []() {}) && lane == 0u)
+          __hip_atomic_store(&ctl[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
