@@ -2310,6 +2310,7 @@ __device__ __forceinline__ void prefetch_buf(u32x4 (&r)[kPer], const uint8_t* sr
 // prefetch_all with the record base and its last piece made wave-uniform
 // (SGPRs): each load is the SGPR base + a 32-bit lane offset (saddr form),
 // so the per-load VALU is the clamp and the shift, no 64-bit address add
+template <bool NT = true>  // (NT: non-temporal loads; false: default policy)
 __device__ __forceinline__ void prefetch_sa(u32x4 (&r)[kPer], const uint8_t* src, uint32_t n16, uint32_t lane) {
   const uint64_t b = (uint64_t)src;
   typedef const __attribute__((address_space(1))) u32x4 gu32x4;
@@ -2320,7 +2321,8 @@ __device__ __forceinline__ void prefetch_sa(u32x4 (&r)[kPer], const uint8_t* src
 #pragma unroll
   for (uint32_t k = 0; k < kPer; ++k) {
     const uint32_t idx = lane + k * kWave;
-    r[k] = __builtin_nontemporal_load((gu32x4*)(s + 16u * (idx < last ? idx : last)));
+    if constexpr (NT) r[k] = __builtin_nontemporal_load((gu32x4*)(s + 16u * (idx < last ? idx : last)));
+    else r[k] = *(gu32x4*)(s + 16u * (idx < last ? idx : last));
   }
 }
 // prefetch_sa with the clamp done on byte offsets (one v_min per load: the
@@ -2952,8 +2954,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join5_ker
     pend &= pend - 1;
     {
       const uint32_t nn = lane_of(n16, t);
-      prefetch_io<7>(pl, Lb + lane_of64(lo, t), nn & 0xFFFFu, lane);
-      prefetch_io<7>(pr, Rb + lane_of64(ro, t), nn >> 16, lane);
+      prefetch_sa<!(FL & 8)>(pl, Lb + lane_of64(lo, t), nn & 0xFFFFu, lane);
+      prefetch_sa<!(FL & 8)>(pr, Rb + lane_of64(ro, t), nn >> 16, lane);
     }
     wave_sync();  // the previous chunk's last LDS reads are done
     stage_all(sL, pl, lane);
@@ -2967,8 +2969,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join5_ker
       // the next object, or this one again after the chunk's last (a constant load count)
       const uint32_t u = pend ? (uint32_t)__builtin_ctzll(pend) : t;
       const uint32_t nu = lane_of(n16, u);
-      prefetch_io<7>(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
-      prefetch_io<7>(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
+      prefetch_sa<!(FL & 8)>(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
+      prefetch_sa<!(FL & 8)>(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
       bool big = false;
       uint32_t r;
       const bool dt = (defs >> t) & 1ull;
@@ -4287,6 +4289,7 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   if (variant == 312) return go(launch_join5<6, 32, 1>);  // one Ooff store per chunk
   if (variant == 313) return go(launch_join5<6, 32, 2>);  // whole-line tails
   if (variant == 314) return go(launch_join5<6, 32, 6>);  // whole-line tails and heads
+  if (variant == 315) return go(launch_join5<6, 32, 8>);  // record loads with the default (temporal) policy
   if (variant == 307) return go(launch_ring_join<6, 32, 4096, 3, 4>);  // timing only: no join
   if (variant == 308) return go(launch_ring_join<6, 32, 4096, 3, 7>);  // timing only: header verdicts, no join
   if (n_actors > 32u && (variant == 0 || variant == 265)) return go(launch_product_join<5, 64>);
