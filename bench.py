@@ -402,6 +402,7 @@ def run_orswot(args, rank, world, local):
 
 
 _PRINT_LOCK = None
+AE_TIMEOUT_EXIT = 3  # exit code of every rank the anti-entropy watchdog ends
 
 
 def _emit(res):
@@ -422,9 +423,11 @@ def _emit(res):
 
 def _ae_watchdog(args, rank, res):
     """Past --ae-deadline seconds in the anti-entropy part, every rank ends
-    the process (exit 0: the headline was measured and checked before it);
-    rank 0 first prints the line, the unfinished sub-measurements marked.
-    os._exit, not exec: nothing replaces the process."""
+    the process with exit code AE_TIMEOUT_EXIT (non-zero: a hung or failed
+    collective must not look like a clean run to the launcher); rank 0 first
+    prints the line — the headline was measured and checked before it — with
+    the unfinished sub-measurements marked. os._exit, not exec: nothing
+    replaces the process."""
     import threading
 
     def fire():
@@ -437,7 +440,7 @@ def _ae_watchdog(args, rank, res):
             _emit(out)
         sys.stderr.write(f"bench.py rank {rank}: anti-entropy past --ae-deadline, exiting\n")
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(AE_TIMEOUT_EXIT)
 
     t = threading.Timer(args.ae_deadline, fire)
     t.daemon = True

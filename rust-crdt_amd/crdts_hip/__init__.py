@@ -702,17 +702,18 @@ class Engine:
     def replica_reduce_scatter_max_transport(self, rows, transport, stream=None):
         """The owner shard of the u64 max over ranks over a caller transport
         (crdt_replica_reduce_scatter_max_transport): rank r gets words
-        [r n/N, (r+1) n/N). Returns a new int64 device tensor of n/N words."""
+        [r n/N, (r+1) n/N). Returns a new int64 device tensor of n/N words.
+        A word count N does not divide is CRDT_EINVAL on EVERY rank: the C ABI
+        checks it with the peers (a local early return here would leave them
+        waiting in the exchange)."""
         torch = _torch()
         flat = rows.reshape(-1)
-        if flat.numel() % transport.world:
-            raise CrdtError(-1, "reduce_scatter: word count not a multiple of the rank count")
-        out = torch.empty(flat.numel() // transport.world, dtype=torch.int64, device=flat.device)
+        out = torch.empty(max(1, flat.numel() // transport.world), dtype=torch.int64, device=flat.device)
         check(lib.crdt_replica_reduce_scatter_max_transport(self.ctx, C.byref(transport.c),
                                                             C.c_void_p(flat.data_ptr()), flat.numel(),
                                                             C.c_void_p(out.data_ptr()), self._stream(stream)),
               "replica_reduce_scatter_max_transport")
-        return out
+        return out[: flat.numel() // transport.world]
 
     def orswot_replica_join_local(self, batches, stream=None):
         """The same owner-sharded join with every replica a virtual rank on this

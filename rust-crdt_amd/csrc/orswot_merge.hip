@@ -177,7 +177,11 @@ __device__ __forceinline__ uint64_t def_get(const S& s, uint32_t k, uint32_t x) 
 
 template <class S>
 __device__ __forceinline__ bool def_has_member(const S& s, uint32_t k, uint64_t m) {
-  uint32_t lo = run_begin(s.b, s.v.fmend, k), hi = g32(s.b, s.v.fmend, k);
+  // the run is clamped to the n_dm keys in_any_deferred scans, so the two
+  // agree on a record whose member run ends overrun n_dm (not canonical)
+  uint32_t hi = g32(s.b, s.v.fmend, k), lo = run_begin(s.b, s.v.fmend, k);
+  hi = hi < s.v.n_dm ? hi : s.v.n_dm;
+  lo = lo < hi ? lo : hi;
   while (lo < hi) {
     uint32_t mid = (lo + hi) >> 1;
     uint64_t km = g64(s.b, s.v.fkey, mid);
@@ -978,20 +982,6 @@ constexpr uint32_t kLeanFallback = 0xFFFFFFFFu;
 // Scratch: kMask1Scratch bytes of LDS per wave. Returns output 16-B pieces,
 // or kLeanFallback (union > 64 members, or an actor id >= 32).
 // ======================================================================
-// mask_object scratch byte offsets (2 048 B used)
-constexpr uint32_t kMsL = 0;       // u32x2 [64]: L member i -> {actor mask, survives mask}
-constexpr uint32_t kMsR = 512;     // u32x2 [64]: R member j
-constexpr uint32_t kOut = 0;       // u32x4[64]: union member u -> {keep, useA, out dot base, -}; overlays
-                                   // msL/msR, which are dead once every union lane has read its masks
-constexpr uint32_t kEqGe = 1024;   // u32x2 [64]: union member u -> {equal mask, self>=other mask}
-constexpr uint32_t kDesc = 1536;   // u32  [64]: union member u -> type << 16 | i << 8 | j
-constexpr uint32_t kHeadL = 1792;  // u8   [64]: 1 at the first dot of each L member
-constexpr uint32_t kHeadR = 1856;  // u8   [64]
-constexpr uint32_t kUofI = 1920;   // u8   [64]: L member i -> union member
-constexpr uint32_t kUofJ = 1984;   // u8   [64]: R member j -> union member
-constexpr uint32_t kTrash = 2048;  // u64  [64]: per-lane sink for predicated stores / atomics
-constexpr uint32_t kMask1Scratch = 2560;
-
 // LDS hand-off between lanes of one wave with every LDS op drained (lgkmcnt(0)).
 __device__ __forceinline__ void lds_sync() {
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
@@ -1032,201 +1022,9 @@ __device__ __forceinline__ uint32_t rank_below(const uint8_t* b, uint32_t off, u
   return base;
 }
 
-// HD: the object has deferred removes (<= 32 deferred clocks per side):
-// kept dots are checked against the deferred clocks listing their member
-// (apply_deferred -> apply_remove, src/orswot.rs:235-243, 195-211) and the
-// deferred block is the wave-cooperative union + filter (:141-148, :197).
-template <uint32_t OUTCAP, bool HD = false, int ABL = 0, bool DC = false>
-__device__ __forceinline__ uint32_t mask_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* X, u32x4* Os,
-                                                uint32_t A, uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR,
-                                                uint32_t lane, bool& big, Stamps* stp = nullptr) {
-  big = false;
-  const uint32_t key = kHdrBytes + 8u * A;
-  const uint32_t ctrL = key + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
-  const uint32_t ctrR = key + 8u * nR, actR = ctrR + 8u * dR, endR = actR + 4u * dR;
-
-  // ---- dots of both sides in registers: actor, counter
-  const bool hdl = lane < dL, hdr = lane < dR;
-  const uint32_t xl = ld32(Ls, actL + 4u * lane), xr = ld32(Rs, actR + 4u * lane);
-  const uint64_t vl = ld64(Ls, ctrL + 8u * lane), vr = ld64(Rs, ctrR + 8u * lane);
-  if (__ballot((hdl && xl >= 32u) || (hdr && xr >= 32u)) != 0ull) return kLeanFallback;
-
-  // ---- 2. member alignment by rank (self first on equal keys)
-  const bool hml = lane < nL, hmr = lane < nR;
-  const uint64_t kl = ld64(Ls, key + 8u * lane), kr = ld64(Rs, key + 8u * lane);
-  uint32_t rl, rr;  // # other keys < my self key, # self keys < my other key
-  rank_both(Ls, Rs, key, nL, nR, kl, kr, rl, rr);
-  const bool eql = hml && rl < nR && ld64(Rs, key + 8u * rl) == kl;
-  const bool eqr = hmr && rr < nL && ld64(Ls, key + 8u * rr) == kr;
-  const uint64_t EL = __ballot(eql), ER = __ballot(eqr);
-  const uint32_t U = nL + nR - (uint32_t)__popcll(EL);
-  if (U > (uint32_t)kWave) return kLeanFallback;
-  const uint32_t ul = lane + rl - mbcnt64(EL);  // # union keys below my self key
-  const uint32_t ur = lane + rr - mbcnt64(ER);
-  if (ABL == 9) mark<ABL>(*stp, 4);  // dot loads + rank search
-
-  // ---- 1. per-member masks (LDS atomic OR) and run heads. Lane-conditional
-  // LDS stores are predicated by address (a lane with nothing to store writes
-  // its slot of the trash area) and atomics by value (OR 0): no exec-mask
-  // branches on this path.
-  uint32_t* msL = (uint32_t*)(X + kMsL);
-  const uint32_t tr = kTrash + 8u * lane;  // distinct per lane: no same-address serialisation
-  wave_sync();
-  *(uint64_t*)(X + kMsL + 8u * lane) = 0ull;
-  *(uint64_t*)(X + kMsR + 8u * lane) = 0ull;
-  *(uint64_t*)(X + kEqGe + 8u * lane) = 0ull;
-  X[kHeadL + lane] = 0u;
-  X[kHeadR + lane] = 0u;
-  const uint32_t el0 = ld32(Ls, endL + 4u * lane - 4u), er0 = ld32(Rs, endR + 4u * lane - 4u);
-  const uint32_t sl = lane ? el0 : 0u, sr = lane ? er0 : 0u;  // run starts
-  X[(hml && sl < 64u) ? kHeadL + sl : tr] = 1u;
-  X[(hmr && sr < 64u) ? kHeadR + sr : tr] = 1u;
-  *(uint32_t*)(X + (hml ? kDesc + 4u * (ul & 63u) : tr)) =
-      ((eql ? kBoth : kSelf) << 16) | (lane << 8) | (eql ? rl : 0u);
-  *(uint32_t*)(X + ((hmr && !eqr) ? kDesc + 4u * (ur & 63u) : tr)) = (kOther << 16) | (rr << 8) | lane;
-  X[kUofI + lane] = (uint8_t)ul;  // slots of lanes without a member are never read
-  X[kUofJ + lane] = (uint8_t)ur;
-  wave_sync();
-  const uint64_t HL = __ballot(hdl && X[kHeadL + lane] != 0u), HR = __ballot(hdr && X[kHeadR + lane] != 0u);
-  const uint32_t ml = mbcnt64(HL) + ((HL >> lane) & 1ull ? 1u : 0u) - 1u;  // member of my self dot
-  const uint32_t mr = mbcnt64(HR) + ((HR >> lane) & 1ull ? 1u : 0u) - 1u;
-  {
-    const uint64_t tl = ld64(Rs, kHdrBytes + 8u * (xl < A ? xl : 0u)), trr = ld64(Ls, kHdrBytes + 8u * (xr < A ? xr : 0u));
-    const uint64_t bl = hdl ? 1ull << (xl & 31u) : 0ull, br = hdr ? 1ull << (xr & 31u) : 0ull;
-    const bool upl = vl > (xl < A ? tl : 0ull), upr = vr > (xr < A ? trr : 0ull);
-    // {actor mask, survives mask} of the dot's member in one 64-bit OR
-    atomicOr((unsigned long long*)(X + (hdl ? kMsL + 8u * (ml & 63u) : tr)), (unsigned long long)(bl | (upl ? bl << 32 : 0ull)));
-    atomicOr((unsigned long long*)(X + (hdr ? kMsR + 8u * (mr & 63u) : tr)), (unsigned long long)(br | (upr ? br << 32 : 0ull)));
-  }
-  wave_sync();
-  if (ABL == 9) mark<ABL>(*stp, 5);  // heads + mask atomics
-  // ---- 3. actors on both sides of a shared member: equal / self >= other
-  {
-    const uint32_t j = mr & 63u;
-    const uint32_t u = X[kUofJ + j] & 63u;
-    const uint32_t d = *(const uint32_t*)(X + kDesc + 4u * u);
-    const uint32_t i = (d >> 8) & 63u;
-    const uint32_t ML = msL[2u * i];
-    const uint32_t x = xr & 31u;
-    const bool sh = hdr && (d >> 16) == kBoth && ((ML >> x) & 1u);
-    const uint32_t a0 = i ? ld32(Ls, endL + 4u * i - 4u) : 0u;
-    const uint64_t va = ld64(Ls, ctrL + 8u * ((a0 + below(ML, x)) & 63u));
-    const uint64_t b = sh ? ((va == vr ? 1ull : 0ull) | (va >= vr ? 1ull << 32 : 0ull)) << x : 0ull;
-    atomicOr((unsigned long long*)(X + (sh ? kEqGe + 8u * u : tr)), (unsigned long long)b);
-  }
-  wave_sync();
-  if (ABL == 9) mark<ABL>(*stp, 6);  // equal / >= pass
-  // ---- 4. per union member: mask join
-  const bool hu = lane < U;
-  const uint32_t d = hu ? *(const uint32_t*)(X + kDesc + 4u * lane) : 0u;
-  const uint32_t ty = d >> 16, mi = (d >> 8) & 0xFFu, mj = d & 0xFFu;
-  const u32x4 zero = {0u, 0u, 0u, 0u};
-  const uint64_t pl = *(const uint64_t*)(X + kMsL + 8u * mi), pr = *(const uint64_t*)(X + kMsR + 8u * mj);
-  const uint64_t pe = *(const uint64_t*)(X + kEqGe + 8u * lane);
-  const uint32_t ML = (ty & kSelf) ? (uint32_t)pl : 0u, FL = (ty & kSelf) ? (uint32_t)(pl >> 32) : 0u;
-  const uint32_t MR = (ty & kOther) ? (uint32_t)pr : 0u, FR = (ty & kOther) ? (uint32_t)(pr >> 32) : 0u;
-  const uint32_t EQ = ty == kBoth ? (uint32_t)pe : 0u, GE = ty == kBoth ? (uint32_t)(pe >> 32) : 0u;
-  const bool self_only = ty == kSelf;
-  const uint32_t lp = self_only ? ML : (ML & FL), rp = MR & FR;
-  const uint32_t useA = (ML & MR & EQ) | (lp & (~rp | GE));
-  uint32_t keep = useA | rp;
-  keep = (self_only && (ML & FL) == 0u) ? 0u : keep;
-  keep = hu ? keep : 0u;
-  uint32_t useK = useA & keep;  // a dropped self-only entry writes nothing
-  Side DL{Ls, RV{}}, DR{Rs, RV{}};
-  if (HD) {
-    // deferred removes: a kept dot (x, v) of member k dies if a deferred clock
-    // listing k has D[x] >= v; the dot lanes clear their bit in the keep mask
-    DL = side_of(Ls);
-    DR = side_of(Rs);
-    *(u32x4*)(X + kOut + 16u * lane) = u32x4{keep, useK, 0u, 0u};
-    wave_sync();
-    if (hdl) {
-      uint32_t* ok = (uint32_t*)(X + kOut + 16u * X[kUofI + (ml & 63u)]);
-      if ((ok[1] >> xl) & 1u) {
-        const uint64_t mk = dmask_of(DL, DR, ld64(Ls, key + 8u * (ml & 63u)));
-        if (mk && dkilled(DL, DR, mk, xl, vl)) atomicAnd(ok, ~(1u << xl));
-      }
-    }
-    if (hdr) {
-      uint32_t* ok = (uint32_t*)(X + kOut + 16u * X[kUofJ + (mr & 63u)]);
-      if (((ok[0] & ~ok[1]) >> xr) & 1u) {
-        const uint64_t mk = dmask_of(DL, DR, ld64(Rs, key + 8u * (mr & 63u)));
-        if (mk && dkilled(DL, DR, mk, xr, vr)) atomicAnd(ok, ~(1u << xr));
-      }
-    }
-    wave_sync();
-    keep = *(const uint32_t*)(X + kOut + 16u * lane);
-    useK &= keep;
-  }
-  const uint32_t c = __popc(keep);
-
-  // ---- 5. output layout
-  const uint64_t keepm = __ballot(c != 0u);
-  const uint32_t tot_mem = (uint32_t)__popcll(keepm);
-  const uint32_t cincl = scan_incl(c);
-  const uint32_t tot_dot = lane_of(cincl, kWave - 1);
-  uint32_t nd = 0, ndd = 0, ndm = 0;
-  // DC: the counting walk records its survivors (in the equal / >= area, read
-  // into registers above) and the writing walk replays them
-  uint32_t* const dcache = DC ? (uint32_t*)(X + kEqGe) : nullptr;
-  if (HD) deferred_pass_wave(DL, DR, A, lane, nd, ndd, ndm, nullptr, dcache);
-  const uint32_t nd_counted = nd;
-  RecLayout OL;
-  rec_layout(OL, A, tot_mem, tot_dot, nd, ndd, ndm);
-  const uint32_t size = OL.size;
-  if (size > OUTCAP) {
-    big = true;
-    return 0u;
-  }
-  const uint32_t d0 = cincl - c;
-  wave_sync();
-  *(u32x4*)(X + kOut + 16u * lane) = hu ? u32x4{keep, useK, d0, 0u} : zero;
-  uint8_t* O = (uint8_t*)Os;
-  if (c != 0u) {
-    const uint32_t midx = mbcnt64(keepm);
-    const uint64_t kk = (ty & kSelf) ? ld64(Ls, key + 8u * mi) : ld64(Rs, key + 8u * mj);
-    *(uint64_t*)(O + OL.o_key + 8u * midx) = kk;
-    *(uint32_t*)(O + OL.o_mdend + 4u * midx) = d0 + c;
-  }
-  for (uint32_t x = lane; x < A; x += kWave) {  // top clock: pointwise max (src/orswot.rs:153)
-    const uint64_t l = ld64(Ls, kHdrBytes + 8u * x), r = ld64(Rs, kHdrBytes + 8u * x);
-    *(uint64_t*)(O + kHdrBytes + 8u * x) = l > r ? l : r;
-  }
-  wave_sync();
-  uint32_t* oact = (uint32_t*)(O + OL.o_dact);
-  uint64_t* octr = (uint64_t*)(O + OL.o_dctr);
-  if (hdl) {  // self dots that survive, at their member's base + actor rank
-    const u32x4 o = *(const u32x4*)(X + kOut + 16u * X[kUofI + (ml & 63u)]);
-    if ((o.y >> xl) & 1u) {
-      const uint32_t idx = o.z + below(o.x, xl);
-      oact[idx] = xl;
-      octr[idx] = vl;
-    }
-  }
-  if (hdr) {  // other dots kept and not covered by a self dot
-    const u32x4 o = *(const u32x4*)(X + kOut + 16u * X[kUofJ + (mr & 63u)]);
-    if (((o.x & ~o.y) >> xr) & 1u) {
-      const uint32_t idx = o.z + below(o.x, xr);
-      oact[idx] = xr;
-      octr[idx] = vr;
-    }
-  }
-  if (HD) {  // deferred union keyed by clock (:141-148), kept iff !(D <= clock) (:197)
-    DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
-             (uint32_t*)(O + OL.o_fdend), (uint32_t*)(O + OL.o_fmend)};
-    deferred_pass_wave(DL, DR, A, lane, nd, ndd, ndm, &w, dcache, nd_counted);
-  }
-  // zero padding: member block to 8 (<= 4 B) and record to 16 (<= 12 B)
-  if (lane == 0u && OL.o_def != OL.o_mpad) *(uint32_t*)(O + OL.o_mpad) = 0u;
-  if (lane >= 1u && lane < 4u && OL.o_end + 4u * (lane - 1u) < size) *(uint32_t*)(O + OL.o_end + 4u * (lane - 1u)) = 0u;
-  if (lane == 0u) {
-    u32x4* h = (u32x4*)O;
-    h[0] = u32x4{size, A, tot_mem, tot_dot};
-    h[1] = u32x4{nd, ndd, ndm, 0u};
-  }
-  return size / 16u;
-}
+#ifdef CRDT_DIAG
+#include "diag/orswot_mask_diag.inc"  // mask_object (the v6 join): diagnostic kernels only
+#endif
 
 
 // ======================================================================
@@ -2394,473 +2192,9 @@ __device__ __forceinline__ void stage_used(u32x4* dst, const u32x4 (&r)[kPer], u
 }
 
 
-// ======================================================================
-// Mask kernel (v6): every object that fits the mask path (records <= 2 KB,
-// A <= 32, <= 64 members / dots per side, <= 32 deferred clocks per side)
-// is joined by mask_object and written straight to HBM; everything else is
-// flagged for the general kernel. Only the mask path lives here, which keeps
-// the register budget low enough for 5 waves per SIMD.
-// ======================================================================
-// ABL 9: phase stamps; M3: mask3_object for the objects without deferred removes
-template <int MINW, int ABL = 0, bool M3 = false, bool SINK = false>
-__global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_mask_kernel(
-    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
-    const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
-    uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
-    int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
-  __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
-  __shared__ u32x4 scr_s[kWavesPerBlock][kMask1Scratch / 16];
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint32_t wave = threadIdx.x / kWave;
-  u32x4* const sL = stage_s[wave][0];
-  u32x4* const sR = stage_s[wave][1];
-  uint8_t* const X = (uint8_t*)scr_s[wave];
-  const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
-  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint64_t rounds = (n_obj + n_waves * kWave - 1) / (n_waves * kWave);
-  const uint64_t cs = (n_obj + n_waves * rounds - 1) / (n_waves * rounds);
-  // the wave's store sink: after the list in the context's scratch (ctx.h)
-  uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
-  Stamps st{};
-  if (ABL == 9) st.last = stamp();
-  for (uint64_t cbase = wave_id * cs; cbase < n_obj; cbase += n_waves * cs) {
-    // ---- chunk state: lane k <-> object cbase + k
-    const uint64_t obj = cbase + lane;
-    const bool valid = lane < cs && obj < n_obj;
-    uint64_t lo = 0, ro = 0, nlo = Lbytes, nro = Rbytes;
-    if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
-    if (valid && obj + 1u < n_obj) { nlo = Loff[obj + 1u]; nro = Roff[obj + 1u]; }  // same lines: coalesced
-    u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
-    bool ok = valid && (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes && ro + kHdrBytes <= Rbytes;
-    if (ok) {
-      hl0 = ((const u32x4*)(Lb + lo))[0]; hl1 = ((const u32x4*)(Lb + lo))[1];
-      hr0 = ((const u32x4*)(Rb + ro))[0]; hr1 = ((const u32x4*)(Rb + ro))[1];
-    }
-    ok = ok && header_ok(hl0, hl1, lo, Lbytes, A) && header_ok(hr0, hr1, ro, Rbytes, A) &&
-         lo + ro + (uint64_t)hl0.x + hr0.x <= Obytes;
-    // output placement precondition (out[i] at self.off[i] + other.off[i]):
-    // each side's records in increasing offset order, none overlapping the next
-    const bool placed = !ok || (nlo >= lo + hl0.x && nro >= ro + hr0.x);
-    if (__ballot(!placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_EINVAL);
-    ok = ok && placed;
-    const bool fast = ok && hl0.x <= kFastStage && hr0.x <= kFastStage && A <= 32u && hl0.z <= 64u &&
-                      hr0.z <= 64u && hl0.w <= 64u && hr0.w <= 64u && hl1.x <= 32u && hr1.x <= 32u;
-    if (valid) Ooff[obj] = (lo + ro) | ((ok && !fast) ? kPending : 0ull);
-    if (ok && !fast) {  // hand the object to the general kernel
-      const uint32_t e = atomicAdd(&ctl[0], 1u);
-      if (e < list_cap) list[e] = obj;
-    }
-    if (__ballot(valid && !ok && placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
-    const uint64_t runs = __ballot(fast);
-    if (runs == 0ull) continue;
-    const uint32_t n16 = fast ? (hl0.x / 16u) | ((hr0.x / 16u) << 16) : 0u;
-    const uint32_t nm = hl0.z | (hr0.z << 16), nd = hl0.w | (hr0.w << 16);
-    const uint64_t defs = __ballot(fast && (hl1.x | hr1.x) != 0u);
-
-    // ---- software pipeline: the next object's records are in flight while
-    // the current one is joined from LDS
-    uint64_t pend = runs;
-    uint32_t t = (uint32_t)__builtin_ctzll(pend);
-    u32x4 pl[kPer], pr[kPer];
-    uint32_t nn = lane_of(n16, t);
-    prefetch_all(pl, Lb + lane_of64(lo, t), nn & 0xFFFFu, lane);
-    prefetch_all(pr, Rb + lane_of64(ro, t), nn >> 16, lane);
-    mark<ABL>(st, 7);  // chunk state
-    while (pend) {
-      t = (uint32_t)__builtin_ctzll(pend);
-      pend &= pend - 1;
-      nn = lane_of(n16, t);
-      wave_sync();  // previous object's LDS reads are done
-      stage_all(sL, pl, lane);
-      stage_all(sR, pr, lane);
-      wave_sync();
-      mark<ABL>(st, 0);  // wait for the prefetched records + stage them
-      const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
-      const uint32_t m = lane_of(nm, t), d = lane_of(nd, t);
-      if (pend) {
-        const uint32_t u = (uint32_t)__builtin_ctzll(pend);
-        const uint32_t nu = lane_of(n16, u);
-        prefetch_all(pl, Lb + lane_of64(lo, u), nu & 0xFFFFu, lane);
-        prefetch_all(pr, Rb + lane_of64(ro, u), nu >> 16, lane);
-      }
-      mark<ABL>(st, 1);  // issue the next prefetch
-      bool big = false;
-      uint32_t r;
-      if (M3 && !((defs >> t) & 1ull)) {
-        r = mask3_object<0xFFFFFFFFu, SINK ? 1 : 0>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
-                                            d & 0xFFFFu, m >> 16, d >> 16, lane, big, sink);
-      } else if ((defs >> t) & 1ull) {
-        r = mask_object<0xFFFFFFFFu, true, ABL>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
-                                                 m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, &st);
-      } else {
-        r = mask_object<0xFFFFFFFFu, false, ABL>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
-                                                  m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, &st);
-      }
-      if (r == kLeanFallback && lane == 0u) {  // union > 64 members or actor >= 32: general kernel
-        Ooff[cbase + t] |= kPending;
-        const uint32_t e = atomicAdd(&ctl[0], 1u);
-        if (e < list_cap) list[e] = cbase + t;
-      }
-      mark<ABL>(st, (defs >> t) & 1ull ? 3 : 2);  // join (2: plain, 3: with deferred removes)
-    }
-  }
-  if (ABL == 9 && lane < 8u) {  // per-wave phase sums -> the context's list buffer
-    uint64_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v = lane == (uint32_t)k ? st.acc[k] : v;
-    list[wave_id * 8u + lane] = v;
-  }
-}
-
-// ======================================================================
-// Join kernel: the product path (orswot_join_kernel, MODE 3). One pass over
-// the batch, one wave per chunk of objects (the guided split, sched.h): the
-// chunk step validates the 64 objects' headers lane-parallel and lists what
-// the mask join cannot take (records past the 2 KB stage, > 64 members or
-// dots, A > AW, > 32 deferred clocks) for orswot_merge_general_kernel; the
-// wave then joins its objects one by one from the LDS pair stage while the
-// next object's records are in flight in registers — mask3_object for every
-// object, its HD form (direct stores) for the 7 % with deferred removes
-// (src/orswot.rs:87-157 with apply_deferred) — and copies the assembled record
-// out. Every path issues the same vector-memory operations per object (the
-// deferred form's tail stores go to the wave's sink), so the compiler's
-// vmcnt accounting at the loop head waits for the prefetch and not for the
-// previous object's store acknowledgements (loads and stores share vmcnt in
-// issue order on gfx9). A fallback inside the loop (a union past 64 members,
-// a dot actor >= A) sets kPending and lists the object for the general kernel.
-//
-// Template knobs and the product's values (launch_product_join below; every
-// other value exists for the diagnostic A/B variants of -DCRDT_DIAG builds,
-// DESIGN.md §4 / §8 / §9 give the measurements):
-//   MINW 6 (5 for AW 64)  waves per SIMD (launch bound)
-//   MODE 3                one pass (1 / 2: the earlier two-pass split)
-//   OUT 2, HDD, DC, M3HD  deferred objects through mask3_object's HD form, direct stores
-//   HABL 0                timing-only ablations off
-//   RT                    member ranks by register search
-//   DYN 20, SF 5, GMIN 0  guided split: 5/8 of the objects in static chunks, then 20-object tickets
-//   SPEC false            no speculative first-object prefetch
-//   IO 7                  saddr record prefetch, copy-out clamped on byte offsets
-//   HK 0, PK, BK 1        packed two-sided rank search, bank-conflict scratch layout
-//   PO false, TCH 0       natural output placement, no touch prefetch
-//   AW 32 / 64            actor-mask width (dense top clocks of <= 32 / 33-64 actors)
-// ======================================================================
-constexpr uint64_t kPendingHD = 1ull << 62;  // Ooff flag: object left for the deferred pass
-
-// The join of an object with deferred removes (mask_object<HD>, output
-// assembled in the wave's LDS output stage), kept out of line: its register
-// demand then stays out of the join kernel's loop (7 % of config-3 objects
-// pay for the call; the other 93 % keep the lean loop's occupancy).
-__attribute__((noinline)) __device__ uint32_t hd_join(const uint8_t* Ls, const uint8_t* Rs, uint8_t* X, u32x4* Os,
-                                                      uint32_t A, uint32_t m, uint32_t d, uint32_t lane,
-                                                      bool* big) {
-  bool b = false;
-  const uint32_t r = mask_object<kFastStage, true>(Ls, Rs, X, Os, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16,
-                                                   lane, b);
-  *big = b;
-  return r;
-}
-
-// HDD (MODE 3): the deferred objects' join writes straight to HBM
-// (mask_object<HD>) and is followed by the same tail stores as the other
-// path, redirected to the sink: every path issues at least as many stores
-// after the prefetch as the lean one, so its loop-head wait stays exact
-// IO: 0 record prefetch and copy-out by global loads / stores with clamped
-// lane addresses; 1 prefetch through a buffer resource (prefetch_buf); 2 and
-// the copy-out too (copy_record_buf)
-// PO (MODE 3): packed output — a chunk's consecutive joined objects are
-// written back to back (each record right after the previous one's end, never
-// past its own self.off + other.off, so the capacity rule is unchanged): whole
-// 128-B lines instead of a partial line at both ends of every record, which
-// the memory side completes by read-modify-write (tools/probe/skel_probe.hip:
-// the record stream with a synthetic join, 1.08 -> 0.87 ms). An object after
-// one the pass did not join (listed for the general kernel at the chunk step,
-// or not valid) starts at its own self.off + other.off again; an object that
-// falls back inside the loop keeps its two inputs' bytes for the general kernel.
-template <int MINW, int MODE, int OUT = 2, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
-          bool RT = true, uint32_t DYN = 0, uint32_t SF = 6, bool SPEC = false, uint32_t GMIN = 0, int IO = 0,
-          int HK = 0, bool PK = false, int BK = 0, bool PO = false, int TCH = 0, int AW = 32>
-__global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kernel(
-    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
-    const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
-    uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
-    int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
-#ifndef CRDT_DIAG
-  // the product kernel: one pass (MODE 3), no timing-only ablation
-  static_assert(HABL == 0 && MODE == 3 && !TCH, "ablations and the two-pass modes exist in -DCRDT_DIAG builds only");
-#endif
-  static_assert(!PO || MODE == 3, "packed output: the one-pass join");
-  __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
-  static_assert(M3Lay<32>::Bytes == kMask1Scratch, "mask3's AW 32 scratch is the kernel's");
-  static_assert(AW == 32 || (MODE == 3 && HDD && M3HD), "AW 64: the one-pass product form");
-  __shared__ u32x4 scr_s[kWavesPerBlock][(MODE == 1 ? k3Scratch : M3Lay<AW>::Bytes) / 16];
-  __shared__ u32x4 out_s[kWavesPerBlock][MODE == 3 && !HDD ? kFastStage / 16 : 1];  // assembled outputs (deferred objects)
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint32_t wave = uni(threadIdx.x / kWave);  // wave-uniform: LDS bases in SGPRs
-  u32x4* const sL = stage_s[wave][0];
-  u32x4* const sR = stage_s[wave][1];
-  uint8_t* const X = (uint8_t*)scr_s[wave];
-  const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
-  const uint64_t ts0 = HABL == 6 ? __builtin_amdgcn_s_memrealtime() : 0ull;  // (HABL 6: wave start / end times)
-  uint32_t n_joined = 0u, n_hd = 0u, n_chunk = 0u;                                  // (HABL 6: per-wave counts)
-  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint64_t rounds = (n_obj + n_waves * kWave - 1) / (n_waves * kWave);
-  const uint64_t cs = (n_obj + n_waves * rounds - 1) / (n_waves * rounds);
-  uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
-  [[maybe_unused]] uint32_t tacc = 0u;  // TCH: the touch loads' values (kept live, stored never in practice)
-  uint64_t* const dlist = (uint64_t*)((uint8_t*)(list + kDefaultListCap) + kTrashBytes);  // deferred objects
-  // MODE 2 reads the deferred list in chunks of 64 entries when it did not
-  // overflow, else scans every object's flag
-  const uint32_t n_def = MODE == 2 ? uni(__hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : 0u;
-  const bool listed = MODE == 2 && n_def <= kDeferListCap;
-  const uint64_t n_items = listed ? n_def : n_obj;
-  const uint64_t cs2 = listed ? (M3HD ? 1u : kWave) : cs;  // M3HD: one listed object per wave (parallelism)
-  // DYN: the guided split (GuidedSplit); else static rounds of cs2-object chunks
-  GuidedSplit<DYN ? DYN : 1u, SF, GMIN> gs(n_items, wave_id, n_waves);
-  uint32_t it = 0u;
-  uint64_t cbase = wave_id * cs2, cend = n_items;
-  for (;;) {
-    if (DYN) {
-      if (!gs.next(cbase, cend, &ctl[3], lane)) break;
-    } else {
-      if (it++ > 0u) cbase += n_waves * cs2;
-      if (cbase >= n_items) break;
-    }
-    // ---- chunk state: lane k <-> object cbase + k (MODE 2 listed: entry cbase + k)
-    u32x4 pl[kPer], pr[kPer];  // record prefetch registers
-    const uint64_t item = cbase + lane;
-    const bool valid = DYN ? item < cend : lane < cs2 && item < n_items;
-    const uint64_t obj = listed ? (valid ? dlist[item] : 0ull) : item;
-    uint64_t lo = 0, ro = 0;
-    u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
-    bool fast;
-    uint64_t defs = 0ull;  // MODE 3: the chunk's objects with deferred removes
-    if (MODE != 2) {
-      uint64_t nlo = Lbytes, nro = Rbytes;
-      if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
-      if (valid && obj + 1u < n_obj) { nlo = Loff[obj + 1u]; nro = Roff[obj + 1u]; }  // same lines: coalesced
-      if (SPEC) {
-        // the chunk's first object's records are loaded with the headers
-        // (one round trip less per chunk): up to the next object's offset (a
-        // record never extends past it), at most the 2 KB stage; offsets
-        // that cannot hold a record read the wave's sink line instead
-        const uint64_t l0 = lane_of64(lo, 0), r0 = lane_of64(ro, 0), nl0 = lane_of64(nlo, 0), nr0 = lane_of64(nro, 0);
-        const bool okp = (l0 & 15u) == 0 && (r0 & 15u) == 0 && nl0 >= l0 + kHdrBytes && nr0 >= r0 + kHdrBytes &&
-                         nl0 <= Lbytes && nr0 <= Rbytes;
-        const uint64_t nl = (nl0 - l0) / 16u, nr = (nr0 - r0) / 16u;
-        prefetch_all(pl, okp ? Lb + l0 : sink, okp ? (uint32_t)(nl < 2u * kWave ? nl : 2u * kWave) : 1u, lane);
-        prefetch_all(pr, okp ? Rb + r0 : sink, okp ? (uint32_t)(nr < 2u * kWave ? nr : 2u * kWave) : 1u, lane);
-      }
-      bool ok = valid && (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes && ro + kHdrBytes <= Rbytes;
-      if (ok) {
-        hl0 = ((const u32x4*)(Lb + lo))[0]; hl1 = ((const u32x4*)(Lb + lo))[1];
-        hr0 = ((const u32x4*)(Rb + ro))[0]; hr1 = ((const u32x4*)(Rb + ro))[1];
-      }
-      ok = ok && header_ok(hl0, hl1, lo, Lbytes, A) && header_ok(hr0, hr1, ro, Rbytes, A) &&
-           lo + ro + (uint64_t)hl0.x + hr0.x <= Obytes;
-      // output placement precondition (out[i] at self.off[i] + other.off[i]):
-      // each side's records in increasing offset order, none overlapping the next
-      const bool placed = !ok || (nlo >= lo + hl0.x && nro >= ro + hr0.x);
-      if (__ballot(!placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_EINVAL);
-      ok = ok && placed;
-      const bool fits = ok && hl0.x <= kFastStage && hr0.x <= kFastStage && A <= (uint32_t)AW && hl0.z <= 64u &&
-                        hr0.z <= 64u && hl0.w <= 64u && hr0.w <= 64u;
-      const bool hd = fits && (hl1.x | hr1.x) != 0u && hl1.x <= 32u && hr1.x <= 32u;
-      fast = fits && (hl1.x | hr1.x) == 0u;
-      if (MODE == 3) {  // one pass: deferred objects joined here too
-        defs = __ballot(hd);
-        fast = fast || hd;
-      }
-      const bool gen = ok && !fast && !hd;
-      if (valid) Ooff[obj] = (lo + ro) | (gen ? kPending : 0ull) | (MODE == 1 && hd ? kPendingHD : 0ull);
-      if (MODE == 1) {  // list the deferred objects for the deferred pass
-        const uint64_t hm = __ballot(hd);
-        if (hm != 0ull) {
-          uint32_t base = 0;
-          if (lane == 0u) base = atomicAdd(&ctl[2], (uint32_t)__popcll(hm));
-          base = uni(base) + mbcnt64(hm);
-          if (hd && base < kDeferListCap) dlist[base] = obj;
-        }
-      }
-      if (gen) {  // hand the object to the general kernel
-        const uint32_t e = atomicAdd(&ctl[0], 1u);
-        if (e < list_cap) list[e] = obj;
-      }
-      if (__ballot(valid && !ok && placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
-    } else {  // the deferred pass: objects the join pass flagged kPendingHD (validated there)
-      const uint64_t fo = valid ? Ooff[obj] : 0ull;
-      fast = valid && (fo & kPendingHD) != 0ull;
-      if (fast) {
-        lo = Loff[obj];
-        ro = Roff[obj];
-        hl0 = ((const u32x4*)(Lb + lo))[0]; hl1 = ((const u32x4*)(Lb + lo))[1];
-        hr0 = ((const u32x4*)(Rb + ro))[0]; hr1 = ((const u32x4*)(Rb + ro))[1];
-      }
-    }
-    const uint64_t runs = __ballot(fast);
-    if (HABL == 6) ++n_chunk;
-    if (runs == 0ull) continue;
-    const uint32_t n16 = fast ? (hl0.x / 16u) | ((hr0.x / 16u) << 16) : 0u;
-    const uint32_t nm = hl0.z | (hr0.z << 16), nd = hl0.w | (hr0.w << 16);
-
-    // ---- software pipeline: the next object's records are in flight while
-    // the current one is joined from LDS. The loop is rotated so the wait for
-    // a prefetch (stage) has one predecessor, the previous object's stores:
-    // the compiler then lets those stores stay outstanding (vmcnt counts them
-    // as younger) instead of draining them at a merge with the prologue.
-    uint64_t pend = runs;
-    uint32_t t = (uint32_t)__builtin_ctzll(pend);
-    pend &= pend - 1;
-    // (HABL 3, timing only: every object of the chunk without deferred
-    // removes joins the records of the chunk's first such object)
-    const uint64_t nhd = runs & ~defs;
-    const uint32_t t0 = nhd ? (uint32_t)__builtin_ctzll(nhd) : t;
-    auto dsel = [&](uint32_t x) -> uint32_t { return HABL == 3 && !((defs >> x) & 1ull) ? t0 : x; };
-    {
-      const uint32_t ts = dsel(t);
-      if (!SPEC || ts != 0u) {  // (SPEC: object 0's records are already in flight)
-        const uint32_t nn = lane_of(n16, ts);
-        prefetch_io<IO>(pl, Lb + lane_of64(lo, ts), nn & 0xFFFFu, lane);
-        prefetch_io<IO>(pr, Rb + lane_of64(ro, ts), nn >> 16, lane);
-      }
-    }
-    wave_sync();  // the previous chunk's last LDS reads are done
-    stage_all(sL, pl, lane);
-    stage_all(sR, pr, lane);
-    wave_sync();
-    uint64_t cur = 0;         // PO: where the next record goes if it follows the last one joined
-    uint32_t tnext = kWave;   // PO: the object that record would be (none yet in this chunk)
-    uint32_t tv = 0u;         // TCH: the last touch load's value (consumed one object later)
-    for (;;) {
-      const uint64_t nat = HABL == 5 ? lane_of64(lo, t) : lane_of64(lo, t) + lane_of64(ro, t);
-      const uint64_t oo = PO && t == tnext ? (cur < nat ? cur : nat) : nat;
-      const uint32_t td = dsel(t);
-      const uint32_t m = lane_of(nm, td), d = lane_of(nd, td);
-      // the next object, or this one again after the chunk's last (a constant load count)
-      const uint32_t u = pend ? (uint32_t)__builtin_ctzll(pend) : t;
-      const uint32_t us = dsel(u);
-      const uint32_t nu = lane_of(n16, us);
-      prefetch_io<IO>(pl, Lb + lane_of64(lo, us), nu & 0xFFFFu, lane);
-      prefetch_io<IO>(pr, Rb + lane_of64(ro, us), nu >> 16, lane);
-      if (TCH) {
-        // TCH: one dword per 128-B line of the object after the next (lanes
-        // 0-15: its self record, 16-31: its other record; 32-63 repeat them),
-        // so that its record prefetch, one object later, finds the lines in
-        // the caches: the wave has two objects' bytes in flight for the price
-        // of one VGPR. The loaded value is consumed (folded into tacc) only
-        // when the next touch is issued, so no wait is placed on it sooner.
-        const uint64_t pend2 = pend ? pend & (pend - 1ull) : 0ull;
-        const uint32_t v = pend2 ? (uint32_t)__builtin_ctzll(pend2) : u;
-        const uint32_t nv = lane_of(n16, v);
-        const bool rs = (lane & 16u) != 0u;
-        const uint32_t last = 16u * (rs ? nv >> 16 : nv & 0xFFFFu) - 4u;
-        const uint32_t ob = 128u * (lane & 15u);
-        const uint8_t* const tb = rs ? Rb + lane_of64(ro, v) : Lb + lane_of64(lo, v);
-        tacc ^= tv;
-        tv = *(const uint32_t*)(tb + (ob < last ? ob : last));
-      }
-      bool big = false;
-      uint32_t r;
-      if (MODE == 1) {
-        r = mask3_object<0xFFFFFFFFu, OUT>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
-                                            d & 0xFFFFu, m >> 16, d >> 16, lane, big, sink);
-        // fallback (union past 64 members / dot actor >= A): the general
-        // kernel, which finds it by its flag. Both stores are issued for every
-        // object (the store count stays fixed): the offset is rewritten with
-        // or without the flag, and the scan request goes to ctl[1] or to the
-        // wave's sink word (wave-uniform addresses and values)
-        const bool fbu = r == kLeanFallback;
-        *(Ooff + cbase + t) = oo | (fbu ? kPending : 0ull);
-        *(fbu ? ctl + 1 : (uint32_t*)sink) = 1u;  // the wave's own sink word: no shared line
-      } else if (MODE == 3) {
-        // both joins assemble the record in LDS (mask3_object over its input
-        // stage, mask_object<HD> in the wave's output stage); one copy-out
-        // and the fallback stores follow either: the same vector-memory
-        // operations for every object
-        uint32_t src;
-        bool direct = false;
 #ifdef CRDT_DIAG
-        if (HABL == 4 || HABL == 5) {  // timing only: no join, the self record copied out as the output (5: densely)
-          r = lane_of(n16, t) & 0xFFFFu;
-          src = lds_addr(sL);
-        } else
+#include "diag/orswot_kernels_diag.inc"  // the v6 mask kernel, orswot_join_kernel<...>
 #endif
-        if ((defs >> td) & 1ull) {
-          if (HDD) {
-            if (M3HD)
-              r = mask3_object<0xFFFFFFFFu, 0, true, HABL, RT, HK, PK, BK ? 1 : 0, AW>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
-                                                     d & 0xFFFFu, m >> 16, d >> 16, lane, big);
-            else
-              r = mask_object<0xFFFFFFFFu, true, 0, DC>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo),
-                                                        A, m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big);
-            direct = true;
-          } else {
-            r = hd_join((const uint8_t*)sL, (const uint8_t*)sR, X, out_s[wave], A, m, d, lane, &big);
-          }
-          src = lds_addr(out_s[wave]);
-        } else {
-          r = mask3_object<0xFFFFFFFFu, 3, false, 0, RT, 0, PK, BK, AW>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A,
-                                                         m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big, sink);
-          src = lds_addr(sL);
-        }
-        const bool fbu = big || r == kLeanFallback;  // wave-uniform
-        if (HABL == 6) { ++n_joined; n_hd += (defs >> td) & 1ull ? 1u : 0u; }
-        wave_sync();
-        if (HDD && direct) {  // the same two stores, to the sink
-          const u32x4 z = {0u, 0u, 0u, 0u};
-          __builtin_nontemporal_store(z, (u32x4*)sink);
-          __builtin_nontemporal_store(z, (u32x4*)sink + 1);
-        } else {
-          copy_io<IO>(src, Ob + oo, fbu ? 1u : r, lane);
-        }
-        *(Ooff + cbase + t) = oo | (fbu ? kPending : 0ull);
-        if (fbu) {  // listed for the general kernel (a rare path: its extra memory operations
-                    // only add to the count the loop-head wait sees)
-          if (lane == 0u) {
-            const uint32_t e = atomicAdd(&ctl[0], 1u);
-            if (e < list_cap) list[e] = cbase + t;
-          }
-        }
-        if (PO) {  // the next record's place: after this one (a fallback keeps both inputs' bytes)
-          const uint32_t nt = lane_of(n16, td);
-          cur = oo + 16ull * (fbu ? (nt & 0xFFFFu) + (nt >> 16) : uni(r));
-          tnext = t + 1u;
-        }
-      } else {
-        if (M3HD)
-          r = mask3_object<0xFFFFFFFFu, 0, true>(lds_addr(sL), lds_addr(sR), lds_addr(X), Ob + oo, A, m & 0xFFFFu,
-                                                 d & 0xFFFFu, m >> 16, d >> 16, lane, big);
-        else
-          r = mask_object<0xFFFFFFFFu, true>((const uint8_t*)sL, (const uint8_t*)sR, X, (u32x4*)(Ob + oo), A,
-                                             m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane, big);
-        if (lane == 0u) {
-          Ooff[lane_of64(obj, t)] = oo | (r == kLeanFallback ? kPending : 0ull);  // clears kPendingHD
-          if (r == kLeanFallback) ctl[1] = 1u;
-        }
-      }
-      if (pend == 0ull) break;
-      t = u;
-      pend &= pend - 1;
-      wave_sync();  // this object's LDS reads are done
-      stage_used(sL, pl, nu & 0xFFFFu, lane);
-      stage_used(sR, pr, nu >> 16, lane);
-      wave_sync();
-    }
-    if (TCH) tacc ^= tv;
-  }
-  if (TCH && tacc == A + 0x9e3779b9u) *(uint32_t*)sink = tacc;  // (keeps the touches; a value no record word has here)
-#ifdef CRDT_DIAG
-  if (HABL == 6 && lane == 0u && wave_id < 10922u) {  // timing only: the list's upper half holds the stamps
-    list[32768u + 3u * wave_id] = ts0;
-    list[32768u + 3u * wave_id + 1u] = __builtin_amdgcn_s_memrealtime();
-    list[32768u + 3u * wave_id + 2u] = ((uint64_t)n_joined << 32) | (n_hd << 16) | n_chunk;
-  }
-#else
-  (void)ts0;
-  (void)n_joined;
-  (void)n_hd;
-  (void)n_chunk;
-#endif
-}
 
 
 // ======================================================================
@@ -2869,24 +2203,21 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join_kern
 // the guided split (5/8 static chunks, 20-object tickets), the saddr record
 // prefetch one object ahead into registers, mask3_object for every object
 // (its HD form with direct stores for the ~5 % with deferred removes), the
-// packed two-sided rank search and the bank-conflict scratch layout — and
-// two memory-side changes (FL):
-//  * the output record leaves as whole 128-B lines where that stays in
-//    bytes no record owns (a partial line costs the memory side a
-//    read-modify-write): the tail inside this object's own output slot
-//    (record i's slot is [off_i, off_i + |self_i| + |other_i|), and a
-//    merged record is shorter than it by at least a header and a clock),
-//    the head only past the previous object's record when this wave wrote
-//    it; the bytes between records are unspecified (include/crdts_hip.h);
-//  * the chunk's output offsets leave in one coalesced store at the chunk's
-//    end, not one 8-B store per object (each of which is a partial line).
+// packed two-sided rank search and the bank-conflict scratch layout.
+// FL (diagnostic knobs, measured and not kept): 1 the chunk's
+// output offsets in one coalesced store at its end; 8 record loads with the
+// default (temporal) cache policy. (Whole-line output heads / tails, FL 2 / 4
+// in round 5, were removed: 0.739-0.784 vs 0.736 ms.)
 // ======================================================================
-template <int MINW, int AW, int FL>  // FL bits: 1 one Ooff store per chunk, 2 whole-line tails, 4 whole-line heads
+template <int MINW, int AW, int FL>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join5_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
     uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
     int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
+#ifndef CRDT_DIAG
+  static_assert(FL == 0, "FL knobs exist in -DCRDT_DIAG builds only");
+#endif
   __shared__ u32x4 stage_s[kWavesPerBlock][2][kFastStage / 16];
   __shared__ u32x4 scr_s[kWavesPerBlock][M3Lay<AW>::Bytes / 16];
   const uint32_t lane = threadIdx.x & (kWave - 1);
@@ -2897,7 +2228,6 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join5_ker
   const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
   const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
   uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
-  const bool lines = (FL & 6) && ((uint64_t)Ob & 15u) == 0u;
   GuidedSplit<20u, 5u, 0u> gs(n_obj, wave_id, n_waves);
   uint64_t cbase, cend;
   while (gs.next(cbase, cend, &ctl[3], lane)) {
@@ -2961,8 +2291,6 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join5_ker
     stage_all(sL, pl, lane);
     stage_all(sR, pr, lane);
     wave_sync();
-    uint32_t prev_t = kWave;  // FL: the last object whose output record end this wave knows, and that end
-    uint64_t prev_end = 0u;
     for (;;) {
       const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
       const uint32_t m = lane_of(nm, t), d = lane_of(nd, t);
@@ -2990,19 +2318,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join5_ker
         __builtin_nontemporal_store(z, (u32x4*)sink);
         __builtin_nontemporal_store(z, (u32x4*)sink + 1);
       } else {
-        uint64_t w0 = oo, w1 = oo + 16u * (fbu ? 1u : r);
-        if (lines && !fbu) {
-          const uint64_t e = (w1 + 127u) & ~127ull;
-          const uint32_t nt = lane_of(n16, t);  // the output slot: the inputs' bytes
-          if ((FL & 2) && e <= oo + 16u * ((nt & 0xFFFFu) + (nt >> 16))) w1 = e;
-          const uint64_t h = oo & ~127ull;
-          if ((FL & 4) && prev_t + 1u == t && h >= prev_end && w1 - h <= 2u * 16u * kWave) w0 = h;
-        }
-        copy_io<7>(lds_addr(sL) - (uint32_t)(oo - w0), Ob + w0, (uint32_t)(w1 - w0) / 16u, lane);
-      }
-      if ((FL & 4) && !fbu) {
-        prev_t = t;
-        prev_end = oo + 16u * r;
+        copy_io<7>(lds_addr(sL), Ob + oo, fbu ? 1u : r, lane);
       }
       if (FL & 1) {
         pendm |= fbu ? 1ull << t : 0ull;
@@ -3025,257 +2341,9 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join5_ker
   }
 }
 
-// ======================================================================
-// Ring join kernel (round 5): orswot_join_kernel's join with the record
-// prefetch moved from registers into a per-wave LDS ring filled by LDS-DMA
-// (global_load_lds_dwordx4: 64 lanes x 16 B land at M0 + 16 lane, no VGPR
-// destination). A pair slot is the two records back to back, sized by their
-// real bytes (config 3: ~1.9 KB of the 4 KB the register stage reserved), so
-// the ring holds up to DMAX objects in flight without the 16 prefetch VGPRs.
-// The chunk step reads only the offsets: each record's length is its offset
-// gap (== its size in a compact batch; at most the 2 KB fast stage), and the
-// header is validated from the ring when the object is consumed, so no
-// header line is fetched twice. The wait for an object is a counted
-// `s_waitcnt vmcnt(N)`, N = the vector-memory instructions this wave issued
-// after the object's last piece (loads and stores retire in issue order on
-// vmcnt; an instruction left uncounted only makes the wait stricter).
-// ======================================================================
-// one LDS-DMA piece: lane i's 16 B at gsrc land at LDS byte address m0 + 16 i
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t m0) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(m0)
-               : "memory");
-}
-// s_waitcnt vmcnt(n) for a run-time n. Past T the wait is for T (stricter,
-// never weaker): in the steady state the oldest instructions issued after an
-// object's last piece are the copy-out stores of two objects earlier, long
-// retired, so vmcnt(T) costs nothing over the exact count; the exact table
-// (a short branch tree) serves the chunk's first and last objects.
-template <uint32_t T>
-__device__ __forceinline__ void wait_vm(uint32_t n) {
-  static_assert(T <= 15u, "the exact table covers 0..15");
-  if (n >= T) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T) : "memory");
-    return;
-  }
-#define CRDT_W(k) \
-  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-  switch (n) {
-    CRDT_W(0) CRDT_W(1) CRDT_W(2) CRDT_W(3) CRDT_W(4) CRDT_W(5) CRDT_W(6) CRDT_W(7) CRDT_W(8) CRDT_W(9) CRDT_W(10)
-    CRDT_W(11) CRDT_W(12) CRDT_W(13) CRDT_W(14)
-    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-  }
-#undef CRDT_W
-}
-// a record's 32-B header read from LDS by every lane (a broadcast), wave-uniform
-__device__ __forceinline__ void lds_header(uint32_t a, u32x4& h0, u32x4& h1) {
-  const u32x4 x = *(const __attribute__((address_space(3))) u32x4*)(size_t)a;
-  const u32x4 y = *(const __attribute__((address_space(3))) u32x4*)(size_t)(a + 16u);
-  h0 = u32x4{uni(x.x), uni(x.y), uni(x.z), uni(x.w)};
-  h1 = u32x4{uni(y.x), uni(y.y), uni(y.z), uni(y.w)};
-}
-// The fast path's header test in 32-bit arithmetic (every count bounded
-// first, so record_size64's formula cannot overflow): the width is the
-// batch's, flags clear, deferred fields consistent, the counts within the
-// mask join's limits, and the size matches the counts. Implies header_ok for
-// a record whose offset passed the chunk step and whose size fits the bytes
-// loaded for it (the offset gap).
-template <int AW>
-__device__ __forceinline__ bool fast_header(u32x4 h0, u32x4 h1, uint32_t A) {
-  const bool bnd = h0.y == A && h1.w == 0u && h0.z <= 64u && h0.w <= 64u && h1.x <= 32u && h1.y <= 4096u &&
-                   h1.z <= 4096u && (h1.x != 0u || (h1.y | h1.z) == 0u) && A <= (uint32_t)AW;
-  uint32_t b = ((kHdrBytes + 8u * A + 12u * (h0.z + h0.w)) + 7u) & ~7u;
-  b = (b + 12u * h1.y + 8u * h1.z + 8u * h1.x + 15u) & ~15u;
-  return bnd && b == h0.x;
-}
-
-// HABL (timing only, -DCRDT_DIAG builds): 4 no join, the self record copied
-// out as the output; 7 as 4 after the header verdicts
-template <int MINW, int AW, uint32_t RB, uint32_t DMAX, int HABL = 0>
-__global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_ring_kernel(
-    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
-    const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
-    uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
-    int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
-  static_assert(RB >= 2u * kFastStage && RB % 16u == 0u, "a pair of fast-stage records fits the ring");
-#ifndef CRDT_DIAG
-  static_assert(HABL == 0, "timing-only ablations exist in -DCRDT_DIAG builds only");
-#endif
-  constexpr uint32_t kVmT = 4u * (DMAX - 1u) < 15u ? 4u * (DMAX - 1u) : 15u;  // steady state: 2 pieces + 2 stores per object
-  __shared__ u32x4 ring_s[kWavesPerBlock][RB / 16];
-  __shared__ u32x4 scr_s[kWavesPerBlock][M3Lay<AW>::Bytes / 16];
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint32_t wave = uni(threadIdx.x / kWave);
-  const uint32_t ring = uni(lds_addr(ring_s[wave]));
-  const uint32_t uX = uni(lds_addr(scr_s[wave]));
-  const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
-  const uint64_t n_waves = (uint64_t)gridDim.x * kWavesPerBlock;
-  uint8_t* const sink = (uint8_t*)(list + kDefaultListCap) + 64u * (uint32_t)(wave_id % kTrashWaves);
-  // whole 128-B output lines (see the copy-out) only where the output base is 16-B aligned
-  const bool lines = ((uint64_t)Ob & 15u) == 0u;
-  GuidedSplit<20u, 5u, 0u> gs(n_obj, wave_id, n_waves);
-  uint32_t vmops = 0u;  // vector-memory instructions this wave issued and counted (mod 2^32)
-  uint64_t cbase, cend;
-  while (gs.next(cbase, cend, &ctl[3], lane)) {
-    // ---- chunk step: lane k <-> object cbase + k; offsets only
-    const uint64_t obj = cbase + lane;
-    const bool valid = obj < cend;
-    uint64_t lo = 0, ro = 0, el = Lbytes, er = Rbytes;
-    if (valid) { lo = Loff[obj]; ro = Roff[obj]; }
-    if (valid && obj + 1u < n_obj) { el = Loff[obj + 1u]; er = Roff[obj + 1u]; }  // same lines: coalesced
-    // offsets that can hold a header: the record's bytes up to the next
-    // offset (at most the fast stage) go to the ring; the header decides
-    const bool pre = valid && (lo & 15u) == 0 && (ro & 15u) == 0 && lo + kHdrBytes <= Lbytes && ro + kHdrBytes <= Rbytes;
-    el = el < Lbytes ? el : Lbytes;
-    er = er < Rbytes ? er : Rbytes;
-    const uint64_t gl = el > lo + kHdrBytes ? el - lo : kHdrBytes, gr = er > ro + kHdrBytes ? er - ro : kHdrBytes;
-    const uint32_t n16 = pre ? (uint32_t)((gl < kFastStage ? gl : kFastStage) / 16u) |
-                                   ((uint32_t)((gr < kFastStage ? gr : kFastStage) / 16u) << 16)
-                             : 0u;
-    // offsets that cannot: not canonical (as orswot_join_kernel: valid && !ok)
-    if (__ballot(valid && !pre) != 0ull && lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
-    uint64_t oov = lo + ro;  // lane t: object t's output offset and flag, stored once per chunk (coalesced)
-    uint64_t toissue = __ballot(pre), tocons = toissue;
-    uint32_t head = 0u, tail = 0u, inflight = 0u;
-    uint32_t posv = 0u, markv = 0u;  // lane t: object t's ring slot, vmops after its last piece
-    uint32_t prev_t = kWave;         // the last object whose record end in the output is known, and that end
-    uint64_t prev_end = 0u;
-    while (tocons) {
-      // ---- issue: the chunk's next objects, as many as the ring takes
-      while (toissue && inflight < DMAX) {
-        const uint32_t u = (uint32_t)__builtin_ctzll(toissue);
-        const uint32_t nu = lane_of(n16, u), nl = nu & 0xFFFFu, nr = nu >> 16;
-        const uint32_t B = 16u * (nl + nr);
-        uint32_t pos;
-        if (inflight == 0u) {
-          pos = 0u;
-        } else if (head > tail) {  // live slots [tail, head)
-          if (head + B <= RB) pos = head;
-          else if (B <= tail) pos = 0u;
-          else break;
-        } else {  // wrapped: live [tail, end) and [0, head)
-          if (head + B <= tail) pos = head;
-          else break;
-        }
-        if (inflight == 0u) tail = pos;
-        head = pos + B;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS accesses to a freed slot are done
-        const uint8_t* const ls = Lb + lane_of64(lo, u);
-        const uint8_t* const rs = Rb + lane_of64(ro, u);
-        const uint32_t base = ring + pos;
-        for (uint32_t k = 0; k < nl; k += kWave) {
-          if (k + lane < nl) glds16(ls + 16u * (k + lane), uni(base + 16u * k));
-          ++vmops;
-        }
-        for (uint32_t k = 0; k < nr; k += kWave) {
-          if (k + lane < nr) glds16(rs + 16u * (k + lane), uni(base + 16u * (nl + k)));
-          ++vmops;
-        }
-        posv = lane == u ? pos : posv;
-        markv = lane == u ? vmops : markv;
-        toissue &= toissue - 1u;
-        ++inflight;
-      }
-      // ---- consume the oldest object in flight
-      const uint32_t t = (uint32_t)__builtin_ctzll(tocons);
-      wait_vm<kVmT>(vmops - lane_of(markv, t));
-      const uint32_t nt = lane_of(n16, t), nl = nt & 0xFFFFu, nr = nt >> 16;
-      const uint32_t uL = ring + lane_of(posv, t), uR = uL + 16u * nl;
-      const uint64_t l0 = lane_of64(lo, t), r0 = lane_of64(ro, t);
-      const uint64_t oo = l0 + r0;
-      bool fast = false, hd = false, fbu = false;
-      uint32_t szl = 0u, szr = 0u, r = 0u;
 #ifdef CRDT_DIAG
-      if (HABL == 4) {  // (no header read either)
-        copy_io<7>(uL, Ob + oo, nl, lane);
-        vmops += 2u;
-      } else
+#include "diag/orswot_ring_diag.inc"  // the LDS-DMA ring kernel (r05, not kept)
 #endif
-      {
-        u32x4 hl0, hl1, hr0, hr1;
-        lds_header(uL, hl0, hl1);
-        lds_header(uR, hr0, hr1);
-        szl = hl0.x;
-        szr = hr0.x;
-        // the common case in 32-bit arithmetic: both headers pass the fast
-        // path's bounds and size test, and both records fit the bytes loaded
-        // (so they lie in their buffers and before the next offsets)
-        fast = fast_header<AW>(hl0, hl1, A) && fast_header<AW>(hr0, hr1, A) && szl <= 16u * nl && szr <= 16u * nr &&
-               oo + szl + szr <= Obytes;
-        if (!fast) {  // orswot_join_kernel's chunk-step verdicts, from the ring's headers
-          // (the next offsets again, wave-uniform loads: not kept in VGPRs for this rare path)
-          const uint64_t oi = cbase + t;
-          const uint64_t nl0 = oi + 1u < n_obj ? Loff[oi + 1u] : Lbytes, nr0 = oi + 1u < n_obj ? Roff[oi + 1u] : Rbytes;
-          bool ok = header_ok(hl0, hl1, l0, Lbytes, A) && header_ok(hr0, hr1, r0, Rbytes, A) &&
-                    oo + (uint64_t)szl + szr <= Obytes;
-          const bool placed = !ok || (nl0 >= l0 + szl && nr0 >= r0 + szr);
-          if (!placed && lane == 0u) atomicCAS(status, 0, CRDT_EINVAL);
-          ok = ok && placed;
-          if (!ok && placed && lane == 0u) atomicCAS(status, 0, CRDT_ENONCANON);
-          const bool fits = ok && szl <= 16u * nl && szr <= 16u * nr && A <= (uint32_t)AW && hl0.z <= 64u &&
-                            hr0.z <= 64u && hl0.w <= 64u && hr0.w <= 64u;
-          fast = fits && ((hl1.x | hr1.x) == 0u || (hl1.x <= 32u && hr1.x <= 32u));
-          fbu = ok && !fast;  // (the general kernel's)
-        }
-        hd = fast && (hl1.x | hr1.x) != 0u;
-#ifdef CRDT_DIAG
-        if (HABL == 7) {
-          if (fast) {
-            copy_io<7>(uL, Ob + oo, nl, lane);
-            vmops += 2u;
-          }
-        } else
-#endif
-        if (fast) {
-          bool big = false;
-          if (hd) {
-            r = mask3_object<0xFFFFFFFFu, 0, true, 0, true, 0, true, 1, AW>(uL, uR, uX, Ob + oo, A, hl0.z, hl0.w, hr0.z,
-                                                                           hr0.w, lane, big);
-          } else {
-            r = mask3_object<0xFFFFFFFFu, 3, false, 0, true, 0, true, 1, AW>(uL, uR, uX, Ob + oo, A, hl0.z, hl0.w,
-                                                                            hr0.z, hr0.w, lane, big, sink);
-          }
-          fbu = big || r == kLeanFallback;
-          if (!hd) {
-            // The record assembled over its slot goes out with two 16-B stores
-            // per lane, widened to whole 128-B lines where that stays in bytes
-            // no record owns: the tail within this object's own slot (record
-            // i's slot is [off_i, off_i + |self_i| + |other_i|); a merged
-            // record is always shorter by at least a header and a clock), the
-            // head only after the previous object's record, when this wave
-            // wrote it and knows where it ends. A partial line would cost the
-            // memory side a read-modify-write.
-            uint64_t w0 = oo, w1 = oo + 16u * (fbu ? 1u : r);
-            if (lines && !fbu) {
-              const uint64_t e = (w1 + 127u) & ~127ull;
-              if (e <= oo + szl + szr) w1 = e;
-              const uint64_t h = oo & ~127ull;
-              if (prev_t + 1u == t && h >= prev_end && w1 - h <= 2u * 16u * kWave) w0 = h;
-            }
-            wave_sync();
-            copy_io<7>(uL - (uint32_t)(oo - w0), Ob + w0, (uint32_t)(w1 - w0) / 16u, lane);
-            vmops += 2u;
-          }
-        }
-      }
-      if (fast && !fbu) {
-        prev_t = t;
-        prev_end = oo + 16u * r;
-      }
-      oov = lane == t ? oo | (fbu ? kPending : 0ull) : oov;
-      if (fbu && lane == 0u) {  // the general kernel joins it
-        const uint32_t e = atomicAdd(&ctl[0], 1u);
-        if (e < list_cap) list[e] = cbase + t;
-      }
-      tocons &= tocons - 1u;
-      if (--inflight == 0u) head = tail = 0u;
-      else tail = lane_of(posv, (uint32_t)__builtin_ctzll(tocons));
-    }
-    if (valid) Ooff[obj] = oov;  // every object of the chunk, one coalesced store
-  }
-}
 
 // ======================================================================
 // General path: objects the fast kernel flagged (records larger than its
@@ -4090,97 +3158,9 @@ __global__ __launch_bounds__(kWave) void orswot_sparse_general_kernel(
 
 }  // namespace
 
-namespace {
-// The join launch: MODE 3 (one pass) or the two passes MODE 1 + MODE 2,
-// then the general kernel.
-template <int MINW, bool ONE = true, bool HDD = false, bool DC = false, bool M3HD = false, int HABL = 0,
-          bool RT = true, uint32_t DYN = 0, bool DK_ = false, uint32_t SF = 6, bool V10_ = false, bool SPEC = false,
-          uint32_t GMIN = 0, int IO = 0, int HK = 0, bool PK = false, int BK = 0, bool NM = false, bool PO = false,
-          int TCH = 0, int AW = 32>
-int launch_join_passes(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
-                       const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
-                       uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
-                       uint32_t list_cap, hipStream_t stream, int blocks_per_cu, JoinSeq* js) {
-#ifndef CRDT_DIAG
-  static_assert(HABL == 0 && ONE && !TCH, "the product launch: one pass, no timing-only ablation");
-#endif
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const void* f1;
-  const void* f2 = nullptr;
-  if constexpr (ONE) {
-    f1 = (const void*)orswot_join_kernel<MINW, 3, 2, HDD, DC, M3HD, HABL, RT, DYN, SF, SPEC, GMIN, IO, HK, PK, BK, PO,
-                                         TCH, AW>;
-  } else {
 #ifdef CRDT_DIAG
-    f1 = (const void*)orswot_join_kernel<MINW, 1>;
-    f2 = (const void*)orswot_join_kernel<MINW, 2, 2, false, false, M3HD>;
+#include "diag/orswot_launch_diag.inc"  // their launchers
 #endif
-  }
-  static std::atomic<int> occ_cache[2][10];  // per (pass, MINW; slot 9: the v9 kernel); HDD variants share one per MINW
-  constexpr int slot = AW == 64 ? 8 : MINW;
-  int occ[2];
-  const void* fs[2] = {f1, f2};
-  const int passes = ONE ? 1 : 2;
-  for (int k = 0; k < passes; ++k) {
-    occ[k] = occ_cache[ONE ? 1 - k : k][slot].load(std::memory_order_relaxed);
-    if (occ[k] == 0) {
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[k], fs[k], kWave * kWavesPerBlock, 0) != hipSuccess ||
-          occ[k] < 1)
-        occ[k] = 4;
-      occ_cache[ONE ? 1 - k : k][slot].store(occ[k], std::memory_order_relaxed);
-    }
-  }
-  const uint64_t chunks = (n_obj + kWave - 1) / kWave;
-  const uint64_t want = (chunks + kWavesPerBlock - 1) / kWavesPerBlock;
-  // NM: two sets of the four control words after the shared ones (ctl[4..7],
-  // ctl[8..11]), used by alternate launches of this context; the general
-  // kernel of a launch zeroes the other set, which the next launch uses, so
-  // no memset (a runtime fill kernel plus a ~10 us dispatch gap, r03k trace)
-  // precedes the join. After a failed launch the context zeroes both first.
-  uint32_t* set = NM ? ctl + 4u + 4u * (js->seq & 1u) : ctl;
-  uint32_t* const other = NM ? ctl + 4u + 4u * (~js->seq & 1u) : nullptr;
-  void* args[] = {&Lb, &Loff, &Lbytes, &Rb, &Roff, &Rbytes, &Ob, &Ooff, &Obytes, &n_obj, &n_actors, &status,
-                  &set, &list, &list_cap};
-  if (NM) {
-    if (js->dirty && hipMemsetAsync(ctl + 4, 0, 8 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
-    js->dirty = true;  // until both kernels are launched
-  } else if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) {
-    return CRDT_EHIP;
-  }
-  for (int k = 0; k < passes; ++k) {
-    const uint64_t cap = (uint64_t)cus * (blocks_per_cu > 0 ? blocks_per_cu : occ[k]);
-    const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
-    if (hipLaunchKernel(fs[k], dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) != hipSuccess)
-      return CRDT_EHIP;
-  }
-  hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
-                     Ob, Ooff, n_obj, n_actors, set, list, list_cap, other);
-  if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
-  if (launch_big(Lb, Loff, Rb, Roff, Ob, Ooff, n_obj, n_actors, set, list, list_cap, stream) != hipSuccess)
-    return CRDT_EHIP;
-  if (NM) {
-    ++js->seq;
-    js->dirty = false;
-  }
-  return CRDT_OK;
-}
-}  // namespace
-
-namespace {
-// The product join launch (the knob list above), named once.
-template <int MINW, int AW>
-int launch_product_join(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
-                        const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
-                        uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
-                        uint32_t list_cap, hipStream_t stream, int blocks_per_cu, JoinSeq* js) {
-  return launch_join_passes<MINW, /*ONE*/ true, /*HDD*/ true, /*DC*/ true, /*M3HD*/ true, /*HABL*/ 0, /*RT*/ true,
-                            /*DYN*/ 20, /*DK_*/ false, /*SF*/ 5, /*V10_*/ false, /*SPEC*/ false, /*GMIN*/ 0,
-                            /*IO*/ 7, /*HK*/ 0, /*PK*/ true, /*BK*/ 1, /*NM*/ true, /*PO*/ false, /*TCH*/ 0, AW>(
-      Lb, Loff, Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors, status, ctl, list, list_cap, stream,
-      blocks_per_cu, js);
-}
-}  // namespace
 
 namespace {
 // The ring join launch (orswot_ring_kernel, then the general kernel), with
@@ -4221,12 +3201,8 @@ int launch_join_kernel(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
   js->dirty = false;
   return CRDT_OK;
 }
-template <int MINW, int AW, uint32_t RB, uint32_t DMAX, int HABL>
-const void* ring_fn() { return (const void*)orswot_ring_kernel<MINW, AW, RB, DMAX, HABL>; }
 template <int MINW, int AW, int FL>
 const void* join5_fn() { return (const void*)orswot_join5_kernel<MINW, AW, FL>; }
-template <int MINW, int AW, uint32_t RB, uint32_t DMAX, int HABL = 0>
-constexpr auto launch_ring_join = launch_join_kernel<ring_fn<MINW, AW, RB, DMAX, HABL>>;
 template <int MINW, int AW, int FL>
 constexpr auto launch_join5 = launch_join_kernel<join5_fn<MINW, AW, FL>>;
 // dense top clocks of 65..1024 actors: the sparse mask join over the
@@ -4234,6 +3210,9 @@ constexpr auto launch_join5 = launch_join_kernel<join5_fn<MINW, AW, FL>>;
 const void* dense_wide_fn() { return (const void*)orswot_sparse_mask_kernel<3, 0, 16, 5, false, true>; }
 constexpr auto launch_dense_wide = launch_join_kernel<dense_wide_fn>;
 }  // namespace
+#ifdef CRDT_DIAG
+#include "diag/orswot_variants_diag.inc"  // the diagnostic variant table
+#endif
 
 int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                         const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff,
@@ -4252,14 +3231,18 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // sparse mask join in its dense form (DN), the rest the general kernel
   // (diag variant 320: every such object to the general kernel, as before)
 #ifdef CRDT_DIAG
+  // diagnostic builds: the kernel variants of tools/ (csrc/diag/orswot_variants_diag.inc);
+  // variant 0 is the product path below
   g_big_variant = 0;
-  if (variant >= 330 && variant < 345) {  // the big-object kernel's knobs, after the join5 product
-    g_big_variant = variant - 330;
-    variant = 310;
-  }
+  if (variant != 0)
+    return launch_orswot_merge_diag(go, Lb, Loff, Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors,
+                                    status, ctl, list, list_cap, stream, blocks_per_cu, variant);
 #endif
-  if (n_actors > 64u && n_actors <= kSpTableN && variant != 320) return go(launch_dense_wide);
-#ifndef CRDT_DIAG
+  (void)variant;
+  // dense top clocks wider than the 64-bit actor masks (65..1024 actors):
+  // every object whose clock union holds <= 64 present actors takes the
+  // sparse mask join in its dense form (DN), the rest the general kernel
+  if (n_actors > 64u && n_actors <= kSpTableN) return go(launch_dense_wide);
   // The product path: orswot_join5_kernel — one pass (mask3_object for every
   // object; those with deferred removes take its HD form, direct stores) at 6
   // waves per SIMD with the guided split (5/8 of the objects in static chunks,
@@ -4267,167 +3250,10 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
   // the saddr form and the copy-out clamped on byte offsets, both sides'
   // member ranks in one packed pass when nL + nR <= 64 and mask3's
   // bank-conflict layout, then the general kernel (measured best,
-  // tools/ab_bench.py). It is orswot_join_kernel's product
-  // instantiation written out (diag variants 265 / 310: 0.7396 / 0.7364 ms);
-  // the knob variants exist in -DCRDT_DIAG builds only.
-  (void)variant;
+  // tools/ab_bench.py).
   if (n_actors > 32u)  // dense top clocks of 33-64 actors: the same join with 64-bit actor masks, 5 waves/SIMD
     return go(launch_join5<5, 64, 0>);
   return go(launch_join5<6, 32, 0>);
-#else
-  // r05: the LDS-DMA ring join (orswot_ring_kernel<MINW, AW, ring bytes, objects in flight>)
-  if (variant == 300) return go(launch_ring_join<6, 32, 4096, 2>);
-  if (variant == 301) return go(launch_ring_join<6, 32, 4096, 3>);
-  if (variant == 302) return go(launch_ring_join<5, 32, 5632, 3>);
-  if (variant == 303) return go(launch_ring_join<5, 32, 5632, 4>);
-  if (variant == 304) return go(launch_ring_join<4, 32, 7680, 4>);
-  if (variant == 305) return go(launch_ring_join<4, 32, 7680, 5>);
-  if (variant == 306) return go(launch_ring_join<3, 32, 11072, 6>);
-  // r05: the product join written out (join5), without (310) / with (311) whole-line copy-out + chunk Ooff store
-  if (variant == 310) return go(launch_join5<6, 32, 0>);
-  if (variant == 311) return go(launch_join5<6, 32, 7>);
-  if (variant == 312) return go(launch_join5<6, 32, 1>);  // one Ooff store per chunk
-  if (variant == 313) return go(launch_join5<6, 32, 2>);  // whole-line tails
-  if (variant == 314) return go(launch_join5<6, 32, 6>);  // whole-line tails and heads
-  if (variant == 315) return go(launch_join5<6, 32, 8>);  // record loads with the default (temporal) policy
-  if (variant == 307) return go(launch_ring_join<6, 32, 4096, 3, 4>);  // timing only: no join
-  if (variant == 308) return go(launch_ring_join<6, 32, 4096, 3, 7>);  // timing only: header verdicts, no join
-  if (n_actors > 32u && (variant == 0 || variant == 265)) return go(launch_product_join<5, 64>);
-  if (variant == 134) return go(launch_join_passes<6, true, true, true, true, 1>);  // timing only: no kill
-  if (variant == 135) return go(launch_join_passes<6, true, true, true, true, 2>);  // timing only: no deferred block
-  if (variant == 136) return go(launch_join_passes<6, true, true, true, true, 3>);  // timing only: join without HBM
-  if (variant == 137) return go(launch_join_passes<6, true, true, true, true, 4>);  // timing only: HBM without join
-  if (variant == 138) return go(launch_join_passes<6, true, true, true, true, 5>);  // timing only: as 137, output dense
-  if (variant == 142) return go(launch_join_passes<6, true, true, true, true, 0, false>);  // r02e: clamped rank probes
-  if (variant == 143) return go(launch_join_passes<6, true, true, true, true, 6>);  // product + wave start / end stamps
-  // guided split: SF/8 static, the rest in DYN-object ticket chunks
-  if (variant == 150) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 6>);
-  if (variant == 151) return go(launch_join_passes<6, true, true, true, true, 0, true, 32, false, 6>);
-  if (variant == 152) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 4>);
-  if (variant == 153) return go(launch_join_passes<6, true, true, true, true, 0, true, 8, false, 6>);
-  if (variant == 154) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 7>);
-  if (variant == 155) return go(launch_join_passes<6, true, true, true, true, 6, true, 16, false, 6>);  // + stamps
-  if (variant == 180) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 2>);
-  if (variant == 181) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 3>);
-  if (variant == 182) return go(launch_join_passes<6, true, true, true, true, 0, true, 24, false, 4>);
-  if (variant == 183) return go(launch_join_passes<6, true, true, true, true, 0, true, 12, false, 4>);
-  if (variant == 184) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5>);
-  if (variant == 185) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 5>);
-  if (variant == 186) return go(launch_join_passes<6, true, true, true, true, 0, true, 24, false, 5>);
-  if (variant == 187) return go(launch_join_passes<6, true, true, true, true, 0, true, 24, false, 6>);
-  if (variant == 188) return go(launch_join_passes<6, true, true, true, true, 0, true, 28, false, 5>);
-  if (variant == 189) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 6>);
-  if (variant == 190) return go(launch_join_passes<6, true, true, true, true, 6, true, 20, false, 5>);  // + stamps
-  // + the chunk's first object prefetched with the headers
-  if (variant == 191) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, true>);
-  if (variant == 192) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 5, false, true>);
-  if (variant == 193) return go(launch_join_passes<6, true, true, true, true, 0, true, 12, false, 5, false, true>);
-  if (variant == 194) return go(launch_join_passes<6, true, true, true, true, 0, true, 16, false, 4, false, true>);
-  if (variant == 195) return go(launch_join_passes<6, true, true, true, true, 6, true, 16, false, 5, false, true>);  // + stamps
-  // shrinking ticket chunks (DYN = largest, GMIN = smallest)
-  if (variant == 200) return go(launch_join_passes<6, true, true, true, true, 0, true, 32, false, 5, false, false, 8>);
-  if (variant == 201) return go(launch_join_passes<6, true, true, true, true, 0, true, 24, false, 5, false, false, 8>);
-  if (variant == 202) return go(launch_join_passes<6, true, true, true, true, 0, true, 32, false, 5, false, false, 12>);
-  if (variant == 203) return go(launch_join_passes<6, true, true, true, true, 0, true, 32, false, 4, false, false, 8>);
-  if (variant == 204) return go(launch_join_passes<6, true, true, true, true, 0, true, 40, false, 4, false, false, 10>);
-  if (variant == 205) return go(launch_join_passes<6, true, true, true, true, 6, true, 32, false, 5, false, false, 8>);  // + stamps
-  // timing only, on the guided split: 244 no deferred kill, 245 no deferred block, 246 join without HBM, 247 HBM without join
-  // r03: record prefetch (250) and also the copy-out (251) through buffer resources
-  if (variant == 250) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 1>);
-  if (variant == 251) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 2>);
-  // r03: both sides' member ranks in one packed pass when nL + nR <= 64 (PK)
-  if (variant == 259) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true>);
-  // r03: + BK (mask3's LDS bank-conflict layout: dword descriptors, 4-B sink stride, header under exec)
-  if (variant == 264) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1>);
-  // r03: + NM (no memset before the join: alternating control-word sets, zeroed by the general kernel)
-  if (variant == 265) return go(launch_product_join<6, 32>);
-  // r04: + PO (packed output: consecutive records back to back): 0.750 vs 0.741 ms (265, the product)
-  if (variant == 270) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true, true>);
-  // r04: + TCH (a one-dword-per-line touch of the object after the next), with (271) and without (272) PO
-  if (variant == 271) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true, true, 1>);
-  if (variant == 272) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7, 0, true, 1, true, false, 1>);
-
-  if (variant == 256) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 6>);
-  if (variant == 257) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 7>);
-  if (variant == 255) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 5>);
-  if (variant == 254) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 4>);
-  if (variant == 253) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 3>);
-  // r03: the kill pass by a union key table and per-clock actor masks (HK 1)
-  if (variant == 252) return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5, false, false, 0, 0, 1>);
-  if (variant == 244) return go(launch_join_passes<6, true, true, true, true, 1, true, 20, false, 5>);
-  if (variant == 245) return go(launch_join_passes<6, true, true, true, true, 2, true, 20, false, 5>);
-  if (variant == 246) return go(launch_join_passes<6, true, true, true, true, 3, true, 20, false, 5>);
-  if (variant == 247) return go(launch_join_passes<6, true, true, true, true, 4, true, 20, false, 5>);
-  if (variant == 210) return go(launch_join_passes<6, true, true, true, true, 0, true, 32, false, 3>);
-  if (variant == 211) return go(launch_join_passes<6, true, true, true, true, 0, true, 40, false, 2>);
-  if (variant == 212) return go(launch_join_passes<6, true, true, true, true, 0, true, 32, false, 4>);
-  if (variant == 213) return go(launch_join_passes<6, true, true, true, true, 0, true, 24, false, 3>);
-  if (variant == 214) return go(launch_join_passes<6, true, true, true, true, 0, true, 48, false, 2>);
-  if (variant == 0 || (variant >= 25 && variant <= 35)) {
-    switch (variant) {
-      case 25: return go(launch_join_passes<4, false>);
-      case 26: return go(launch_join_passes<5, false>);
-      case 27: return go(launch_join_passes<6, false>);
-      case 28: return go(launch_join_passes<8, false>);
-      case 29: return go(launch_join_passes<4, true>);
-      case 30: return go(launch_join_passes<5, true, true>);
-      case 32: return go(launch_join_passes<6, true, true, true>);
-      case 33: return go(launch_join_passes<6, true, true, true, true>);
-      case 34: return go(launch_join_passes<6, false, false, false, true>);
-      case 0: return go(launch_join_passes<6, true, true, true, true, 0, true, 20, false, 5>);  // the product path
-      case 35: return go(launch_join_passes<6, true, true, true, true>);  // r02e product: static split
-      default: return go(launch_join_passes<6, true, true>);  // 31: round-2 v8
-    }
-  }
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess)
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  // round-1 and experimental kernels (101..103: timing-only ablations whose
-  // output is invalid); 11 = the round-1 product (orswot_mask_kernel<6>)
-  const void* fn = (const void*)orswot_mask_kernel<6>;
-  switch (variant) {
-    case 10: fn = (const void*)orswot_mask_kernel<5>; break;
-    case 11: fn = (const void*)orswot_mask_kernel<6>; break;
-    case 12: fn = (const void*)orswot_mask_kernel<4>; break;
-    case 14: fn = (const void*)orswot_mask_kernel<5, 9>; break;
-    case 18: fn = (const void*)orswot_mask_kernel<6, 0, true>; break;
-    case 19: fn = (const void*)orswot_mask_kernel<7, 0, true>; break;
-    case 20: fn = (const void*)orswot_mask_kernel<5, 0, true>; break;
-    case 21: fn = (const void*)orswot_mask_kernel<4, 0, true>; break;
-    case 22: fn = (const void*)orswot_mask_kernel<7, 0, true, true>; break;
-    case 23: fn = (const void*)orswot_mask_kernel<5, 0, true, true>; break;
-    case 24: fn = (const void*)orswot_mask_kernel<6, 0, true, true>; break;
-    default: break;
-  }
-  // Resident grid: the kernel's occupancy in 4-wave blocks per CU
-  // (blocks_per_cu overrides), no more blocks than 64-object chunks need.
-  static std::atomic<int> occ_cache[256];  // per variant, 0 = not yet queried
-  const int slot = variant & 255;
-  int occ = occ_cache[slot].load(std::memory_order_relaxed);
-  if (occ == 0) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWave * kWavesPerBlock, 0) != hipSuccess || occ < 1)
-      occ = 4;
-    occ_cache[slot].store(occ, std::memory_order_relaxed);
-  }
-  const uint64_t chunks = (n_obj + kWave - 1) / kWave;
-  const uint64_t want = (chunks + kWavesPerBlock - 1) / kWavesPerBlock;
-  const uint64_t cap = (uint64_t)cus * (blocks_per_cu > 0 ? blocks_per_cu : occ);
-  const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
-  void* args[] = {&Lb, &Loff, &Lbytes, &Rb, &Roff, &Rbytes, &Ob, &Ooff, &Obytes, &n_obj, &n_actors, &status,
-                  &ctl, &list, &list_cap};
-  if (hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
-  if (hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) != hipSuccess)
-    return CRDT_EHIP;
-  // diagnostic stamp variants reuse the object list for their phase sums:
-  // no general pass after them (their output is not a valid batch anyway)
-  if (variant == 109 || variant == 14 || variant == 16) return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
-  hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff,
-                     Ob, Ooff, n_obj, n_actors, ctl, list, list_cap, nullptr);
-  if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
-  return launch_big(Lb, Loff, Rb, Roff, Ob, Ooff, n_obj, n_actors, ctl, list, list_cap, stream) == hipSuccess
-             ? CRDT_OK
-             : CRDT_EHIP;
-#endif
 }
 
 int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,

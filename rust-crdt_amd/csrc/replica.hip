@@ -674,8 +674,14 @@ int dense_reduce_scatter_rank(crdt_ctx* ctx, Transport& T, const uint64_t* d_row
                               hipStream_t st) {
   const int R = T.R, me = T.me;
   const size_t w = n / (size_t)R;
-  int rc = w && R > 1 ? ensure_arena(ctx, al256(8 * w * (size_t)(R - 1)) + 256) : CRDT_OK;
-  if (R > 1) {  // every rank's (word count, arena verdict) before any data moves
+  // a word count that does not split into R shards fails on every rank: it is
+  // part of the all-gathered verdict, not a local early return that would
+  // leave the peers waiting in the all-gather
+  int rc = n % (size_t)R ? CRDT_EINVAL
+           : w && R > 1  ? ensure_arena(ctx, al256(8 * w * (size_t)(R - 1)) + 256)
+                         : CRDT_OK;
+  if (R == 1 && rc) return rc;
+  if (R > 1) {  // every rank's (word count, verdict) before any data moves
     uint64_t mine[2] = {(uint64_t)n, (uint64_t)-rc};
     std::vector<uint64_t> G(2 * (size_t)R);
     const int trc = T.allgather(mine, 2, G.data(), st);
@@ -707,9 +713,8 @@ int crdt_replica_reduce_scatter_max_transport(crdt_ctx* ctx, const crdt_transpor
                                               const uint64_t* d_rows, size_t n_words, uint64_t* d_shard,
                                               void* stream) {
   if (!ctx || !transport || !transport->allgather || !transport->exchange || transport->n_ranks < 1 ||
-      transport->rank < 0 || transport->rank >= transport->n_ranks || n_words % (size_t)transport->n_ranks ||
-      (n_words && (!d_rows || !d_shard)))
-    return CRDT_EINVAL;
+      transport->rank < 0 || transport->rank >= transport->n_ranks || (n_words && (!d_rows || !d_shard)))
+    return CRDT_EINVAL;  // (n_words % n_ranks is checked with the peers, dense_reduce_scatter_rank)
   int rc = set_dev(ctx);
   if (rc) return rc;
   CallbackTransport T(transport);

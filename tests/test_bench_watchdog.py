@@ -1,5 +1,6 @@
 """bench.py's anti-entropy watchdog (N > 1): past --ae-deadline every rank
-ends the process with exit 0, and rank 0 first prints its one JSON line with
+ends the process with exit code bench.AE_TIMEOUT_EXIT (3, non-zero: a hung
+collective must not read as a clean run), and rank 0 first prints its one JSON line with
 the unfinished part marked — a collective that never returns cannot cost the
 measured headline. CPU only: the watchdog is exercised on a sleeping process."""
 import json
@@ -25,9 +26,12 @@ def _run(rank):
                           timeout=60)
 
 
-def test_rank0_prints_once_and_exits_zero():
+AE_TIMEOUT_EXIT = 3  # bench.AE_TIMEOUT_EXIT (checked below)
+
+
+def test_rank0_prints_once_and_exits_nonzero():
     p = _run(0)
-    assert p.returncode == 0, p.stderr
+    assert p.returncode == AE_TIMEOUT_EXIT, p.stderr
     lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1
     d = json.loads(lines[0])
@@ -35,9 +39,16 @@ def test_rank0_prints_once_and_exits_zero():
     assert "unfinished" in d["anti_entropy"]
 
 
-def test_other_ranks_exit_zero_silently():
+def test_other_ranks_exit_nonzero_silently():
     p = _run(1)
-    assert p.returncode == 0 and p.stdout.strip() == ""
+    assert p.returncode == AE_TIMEOUT_EXIT and p.stdout.strip() == ""
+
+
+def test_exit_code_constant():
+    sys.path.insert(0, REPO)
+    import bench
+
+    assert bench.AE_TIMEOUT_EXIT == AE_TIMEOUT_EXIT != 0
 
 
 def test_emit_prints_at_most_once(capsys):

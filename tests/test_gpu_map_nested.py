@@ -119,11 +119,14 @@ def test_nested_map_limits(gpu):
 
 
 def test_nested_map_malformed_inner_under_truncation(gpu):
-    """A malformed nested map (n_keys past its kcap) in tasks whose merged
-    nested map is truncated afterwards: the task merge latches CRDT_ENONCANON
-    and marks the task's scratch row, so the truncation reads no count from
-    it and writes nothing for it (the scratch holds garbage counts from the
-    start); the well-formed objects of the batch still merge exactly."""
+    """A malformed nested map (n_keys past its kcap) in the tasks of the fused
+    merge-and-truncate kernel (map_mvreg_merge_kernel<G>: each task merges one
+    output key's nested maps and applies Map::truncate as it writes,
+    src/map.rs:131-158). The scratch now holds only the tasks and their
+    truncating clocks (map_map_scratch_bytes); it is filled with garbage
+    first. A task whose nested map is malformed latches CRDT_ENONCANON and
+    writes no row from the bad counts; the well-formed objects of the same
+    batch still merge and truncate exactly (against the Python restatement)."""
     import crdts_hip
     from crdts_hip._lib import CRDT_ENONCANON
 

@@ -47,7 +47,7 @@ def _oracle_fold(oracle_ffi, reps, A, flags=0):
     return records.unpack_batch(*acc)
 
 
-CRDT_ECAPACITY, CRDT_ENONCANON = -4, -2  # include/crdts_hip.h
+CRDT_EINVAL, CRDT_ECAPACITY, CRDT_ENONCANON = -1, -4, -2  # include/crdts_hip.h
 
 
 def _worker(rank, world, port, q):
@@ -121,6 +121,16 @@ def _worker(rank, world, port, q):
     rs = eng.replica_reduce_scatter_max_transport(
         torch.from_numpy(rows_of(rank)[:6000].view(np.int64).copy()).to("cuda:0"), T)
     res["rs_ok"] = bool(np.array_equal(rs.cpu().numpy().view(np.uint64), exp[rank * w:(rank + 1) * w]))
+    # 5c. rank 0 passes a word count no rank count > 1 divides, the others a
+    #     divisible one: every rank returns CRDT_EINVAL (the count is part of
+    #     the all-gathered verdict), none is left in the exchange
+    n5c = 6000 * world + (1 if rank == 0 else 0)
+    try:
+        eng.replica_reduce_scatter_max_transport(
+            torch.from_numpy(np.resize(rows_of(rank), n5c).view(np.int64).copy()).to("cuda:0"), T)
+        res["rs_bad_code"] = 0
+    except crdts_hip.CrdtError as e:
+        res["rs_bad_code"] = e.code
     # 6. one rank's arena cannot grow (a fresh context with a 1 KB arena limit
     #    on the last rank): every rank returns CRDT_ECAPACITY before any data
     #    moves (the verdicts are all-gathered first; nobody waits in an
@@ -209,6 +219,7 @@ def test_product_join_across_processes(world):
         assert r["calls"]["exchange"] == 2 + 2 + 1 + 2, r["calls"]
         assert r["ar_ok"], f"rank {r['rank']}: the transport all-reduce differs from the pointwise max"
         assert r["rs_ok"], f"rank {r['rank']}: the transport reduce-scatter differs from its slice of the max"
+        assert r["rs_bad_code"] == (0 if world == 1 else CRDT_EINVAL), r["rs_bad_code"]
         assert r["limit_codes"] == ([0, CRDT_ECAPACITY] if world == 1 else [CRDT_ECAPACITY, CRDT_ECAPACITY]), r["limit_codes"]
         assert r["limit_rows_kept"] or world == 1
         assert r["limit_after_ok"], f"rank {r['rank']}: the calls after the arena failure differ"
