@@ -60,7 +60,7 @@ def parse():
     # (the driver's 5 x 0.75 ms) would otherwise time the ramp
     p.add_argument("--settle-ms", type=float, default=200.0)
     p.add_argument("--workload", default="orswot",
-                   choices=["orswot", "orswot_tail", "vclock", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply",
+                   choices=["orswot", "orswot_tail", "orswot_csr_tail", "vclock", "gcounter", "pncounter", "orswot_csr", "gcounter_ae", "bincode", "apply",
                             "mvreg", "map", "map_orswot", "map_map", "clock_csr", "truncate", "spawn_check"])
     p.add_argument("--replicas", type=int, default=8, help="orswot_csr at N=1: replicas folded locally")
     p.add_argument("--n-actors", type=int, default=16,
@@ -258,8 +258,13 @@ def run_orswot(args, rank, world, local):
     first = rank * n
     t0 = time.time()
     A = args.n_actors
-    tail = args.workload == "orswot_tail"
-    if tail:  # config 3 with a heavy tail: 5 % of the objects at 100 / 300 / 1000 members per side
+    tail = args.workload in ("orswot_tail", "orswot_csr_tail")
+    csr = args.workload == "orswot_csr_tail"
+    flags = crdts_hip.SPARSE_CLOCK if csr else 0
+    if csr:  # config 5's CSR records (replicas 0 and 1) with the same heavy tail
+        A = crdts_hip.CONFIG5["universe"]
+        (lb, lo), (rb, ro) = crdts_hip.generate_orswot_csr_tail(n, first_obj=first, threads=args.threads)
+    elif tail:  # config 3 with a heavy tail: 5 % of the objects at 100 / 300 / 1000 members per side
         A = 16
         (lb, lo), (rb, ro) = crdts_hip.generate_orswot_tail(n, first_obj=first, threads=args.threads)
     else:
@@ -267,8 +272,8 @@ def run_orswot(args, rank, world, local):
                                                        params=None if A == 16 else {"n_actors": A})
     gen_s = time.time() - t0
     eng = crdts_hip.Engine(local)
-    L = crdts_hip.OrswotBatch.from_host(lb, lo, A, device=local)
-    R = crdts_hip.OrswotBatch.from_host(rb, ro, A, device=local)
+    L = crdts_hip.OrswotBatch.from_host(lb, lo, A, device=local, flags=flags)
+    R = crdts_hip.OrswotBatch.from_host(rb, ro, A, device=local, flags=flags)
     out = eng.orswot_alloc_out(L, R)
     stream = torch.cuda.Stream(device=local)
     # one checked launch, then algorithmic bytes from the real output sizes
@@ -318,9 +323,14 @@ def run_orswot(args, rank, world, local):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u64",
-        "data": "synthetic: op-simulated Orswot pairs (SplitMix64 seed 0xC0FFEE03 ^ object id)",
+        "data": ("synthetic: op-simulated Orswot replica pairs (SplitMix64 seed 0xC0FFEE05 ^ object id)" if csr else
+                 "synthetic: op-simulated Orswot pairs (SplitMix64 seed 0xC0FFEE03 ^ object id)"),
         "config": {
-            "workload": (f"orswot_tail: config 3 with a heavy tail, {n} objects/GPU, every 20th object at "
+            "workload": (f"orswot_csr_tail: config 5's CSR records (replicas 0 and 1, 1024-actor universe) with a "
+                         f"heavy tail, {n} objects/GPU, every 20th object at "
+                         f"{'/'.join(map(str, crdts_hip.TAIL_SIZES))} members per side in turn (the sparse general / "
+                         "big-object path), the rest config-5 pairs") if csr else
+                        (f"orswot_tail: config 3 with a heavy tail, {n} objects/GPU, every 20th object at "
                          f"{'/'.join(map(str, crdts_hip.TAIL_SIZES))} members per side in turn (the general / big-object "
                          "path), the rest config-3 pairs") if tail else
                         ("orswot_merge config3 (BASELINE.json configs[2]): 1M objects/GPU x ~31 members/side "
@@ -338,7 +348,9 @@ def run_orswot(args, rank, world, local):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": ("orswot_big_kernel (+ orswot_join5_kernel, orswot_merge_general_kernel in the same window)"
+            "kernel": ("orswot_big_kernel<CSR> (+ orswot_sparse_mask_kernel, orswot_sparse_general_kernel in the "
+                       "same window)" if csr else
+                       "orswot_big_kernel (+ orswot_join5_kernel, orswot_merge_general_kernel in the same window)"
                        if tail else ("orswot_join5_kernel" if A <= 64 else "orswot_sparse_mask_kernel<DN>")
                        + " (+ orswot_merge_general_kernel, orswot_big_kernel in the same window)"),
             "achieved": achieved,
@@ -1758,7 +1770,7 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     if args.workload == "spawn_check":
         res = run_spawn_check(args, rank, world, local)
-    elif args.workload in ("orswot", "orswot_tail"):
+    elif args.workload in ("orswot", "orswot_tail", "orswot_csr_tail"):
         res = run_orswot(args, rank, world, local)
     elif args.workload == "vclock":
         res = run_vclock(args, rank, world, local)

@@ -1017,6 +1017,40 @@ def generate_orswot_tail(n_obj, frac=0.05, sizes=TAIL_SIZES, first_obj=0, seed=C
     src/orswot.rs:26-30); the others are config-3 objects. The same object
     index gets the same pair at any batch split. Returns ((L_base, L_off),
     (R_base, R_off)) as numpy arrays."""
+    def base(n, first):
+        return generate_orswot(n, first_obj=first, seed=seed, threads=threads)
+
+    def heavy_gen(n, first, m, params):
+        return generate_orswot(n, first_obj=first, seed=TAIL_SEED + m, threads=threads, params=params)
+
+    return _tail_batch(n_obj, frac, sizes, first_obj, base, heavy_gen)
+
+
+def generate_orswot_csr_tail(n_obj, frac=0.05, sizes=TAIL_SIZES, first_obj=0, seed=CONFIG5_SEED, threads=8):
+    """Config 5's record form with a heavy tail (bench.py --workload
+    orswot_csr_tail): replicas 0 and 1 of the config-5 replica generator (CSR
+    top clocks over the 1 024-actor universe) as the self and other batches,
+    object i heavy iff (first_obj + i) % round(1 / frac) == 0, heavy objects
+    at the sizes in turn (member universe m, m ancestor adds, m/8..m/4
+    divergent ops per replica: ~m members per side; the reference's entries
+    map and clock are unbounded, src/orswot.rs:26-30, src/vclock.rs:54-57).
+    Split-invariant like generate_orswot_tail. Returns ((L_base, L_off),
+    (R_base, R_off)) as numpy arrays, every record with the sparse-clock flag."""
+    def base(n, first):
+        return tuple(generate_replicas(n, 2, first_obj=first, seed=seed, threads=threads))
+
+    def heavy_gen(n, first, m, params):
+        return tuple(generate_replicas(n, 2, first_obj=first, seed=TAIL_SEED + 0x5000 + m, threads=threads,
+                                       params=params))
+
+    return _tail_batch(n_obj, frac, sizes, first_obj, base, heavy_gen)
+
+
+def _tail_batch(n_obj, frac, sizes, first_obj, base, heavy_gen):
+    """The heavy-tail batch assembly shared by generate_orswot_tail and
+    generate_orswot_csr_tail: base(n, first) -> the ordinary pairs of objects
+    [first, first + n); heavy_gen(n, first, m, params) -> n heavy pairs of size
+    m (pair index first..)."""
     step = max(1, int(round(1.0 / frac)))
     ids = np.arange(first_obj, first_obj + n_obj, dtype=np.int64)
     heavy = ids % step == 0
@@ -1026,18 +1060,17 @@ def generate_orswot_tail(n_obj, frac=0.05, sizes=TAIL_SIZES, first_obj=0, seed=C
         pos = np.nonzero(kind == k)[0]
         if pos.size == 0:
             continue
-        if k == 0:  # config-3 pairs of the objects' own ids (the heavy ids' pairs generated and dropped)
-            (lb, lo), (rb, ro) = generate_orswot(n_obj, first_obj=first_obj, seed=seed, threads=threads)
+        if k == 0:  # base pairs of the objects' own ids (the heavy ids' pairs generated and dropped)
+            (lb, lo), (rb, ro) = base(n_obj, first_obj)
             sides = []
             for b, o in ((lb, lo), (rb, ro)):
                 end = np.append(o[1:], np.uint64(b.nbytes))
                 sides.append((b, o[pos], end[pos]))
         else:  # heavy object g of size m: pair index (g // step) // len(sizes) of the size-m generator
             m = sizes[k - 1]
-            sides = generate_orswot(int(pos.size), first_obj=int(ids[pos[0]] // step // len(sizes)),
-                                    seed=TAIL_SEED + m, threads=threads,
-                                    params={"member_universe": m, "ancestor_adds": m, "min_div_ops": max(4, m // 8),
-                                            "max_div_ops": max(8, m // 4)})
+            sides = heavy_gen(int(pos.size), int(ids[pos[0]] // step // len(sizes)), m,
+                              {"member_universe": m, "ancestor_adds": m, "min_div_ops": max(4, m // 8),
+                               "max_div_ops": max(8, m // 4)})
         parts.append((pos, sides))
     out = []
     for side in (0, 1):

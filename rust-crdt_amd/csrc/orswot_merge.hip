@@ -151,6 +151,16 @@ __device__ __forceinline__ uint64_t topv(P b, const RV& v, uint32_t a, uint32_t 
   const uint32_t k = clk_lower_bound(b, v, a);
   return (k < v.n_clk && g32(b, v.cact, k) == a) ? g64(b, v.clk, k) : 0ull;
 }
+// The same with an actor -> rank table of the clock (u8 k + 1 per actor id
+// < kRankTab, 0 = absent; orswot_big_kernel<true>'s per-object LDS table):
+// two dependent LDS reads instead of the binary search.
+constexpr uint32_t kRankTab = 1024;
+template <bool SP, class P>
+__device__ __forceinline__ uint64_t topr(P b, const RV& v, uint32_t a, uint32_t A, lds_cu8* rk) {
+  if (!SP || rk == nullptr || a >= kRankTab) return topv<SP>(b, v, a, A);
+  const uint32_t k = rk[a];
+  return k ? g64(b, v.clk, k - 1u) : 0ull;
+}
 template <class P>
 __device__ __forceinline__ uint32_t run_begin(P b, uint32_t off, uint32_t k) {
   return k ? g32(b, off, k - 1) : 0u;
@@ -254,7 +264,10 @@ template <int MODE, bool SP = false, class S>
 __device__ __forceinline__ uint32_t join(const S& L, const S& R, uint32_t type, uint32_t i,
                                          uint32_t j, uint32_t A, bool has_def, uint32_t& x0, uint64_t& v0,
                                          uint32_t* oact, uint64_t* octr, uint32_t d0,
-                                         const uint32_t* bloom = nullptr) {
+                                         const uint32_t* bloom = nullptr, lds_cu8* crank = nullptr) {
+  // crank (SP): actor -> rank tables of L's and R's top clocks (topr), or null
+  lds_cu8* const rkL = crank;
+  lds_cu8* const rkR = crank ? crank + kRankTab : nullptr;
   uint32_t a = 0, ae = 0, b = 0, be = 0;
   if (type & kSelf) { a = run_begin(L.b, L.v.mdend, i); ae = g32(L.b, L.v.mdend, i); }
   if (type & kOther) { b = run_begin(R.b, R.v.mdend, j); be = g32(R.b, R.v.mdend, j); }
@@ -262,7 +275,7 @@ __device__ __forceinline__ uint32_t join(const S& L, const S& R, uint32_t type, 
     // a self-only entry is kept UNCHANGED iff !(clock <= other.clock) (:98-103)
     bool any = false;
     for (uint32_t d = a; d < ae && !any; ++d)
-      any = g64(L.b, L.v.dctr, d) > topv<SP>(R.b, R.v, g32(L.b, L.v.dact, d), A);
+      any = g64(L.b, L.v.dctr, d) > topr<SP>(R.b, R.v, g32(L.b, L.v.dact, d), A, rkR);
     if (!any) ae = a;
   }
   uint64_t m = 0;
@@ -280,7 +293,7 @@ __device__ __forceinline__ uint32_t join(const S& L, const S& R, uint32_t type, 
     const uint32_t x = ta ? xa : xb;
     const uint64_t va = ta ? g64(L.b, L.v.dctr, a) : 0ull;
     const uint64_t vb = tb ? g64(R.b, R.v.dctr, b) : 0ull;
-    const uint64_t rc = topv<SP>(R.b, R.v, x, A), lc = topv<SP>(L.b, L.v, x, A);
+    const uint64_t rc = topr<SP>(R.b, R.v, x, A, rkR), lc = topr<SP>(L.b, L.v, x, A, rkL);
     // self-only: the whole run (kept); otherwise L[x] survives iff > Rc[x]
     // (:112, :133 analogue), R[x] iff > Lc[x] (:113, :133); a dot equal on
     // both sides is common (:109) and survives as is; result = max (:115-116)
@@ -502,7 +515,8 @@ __device__ __forceinline__ RecLayout layout_at(const uint8_t* rec) {
 // (src/vclock.rs:131-137): the sorted union of both actor lists, max on
 // common actors. Counts the union (every lane gets it); with O != nullptr
 // also writes ctr/act at O's clock section for a union of n_out entries.
-__device__ __forceinline__ uint32_t sparse_clock_join(const Side& L, const Side& R, uint8_t* O, uint32_t n_out,
+template <class S>
+__device__ __forceinline__ uint32_t sparse_clock_join(const S& L, const S& R, uint8_t* O, uint32_t n_out,
                                                       uint32_t lane) {
   // union index of actor x = #L acts < x + #R acts < x - #common acts < x;
   // the common count below an entry is a running wave prefix over its side.
@@ -2528,6 +2542,7 @@ struct BigTabs {
   uint32_t cap;
   uint32_t* bloom;  // 32: the deferred member filter (dm_maybe)
   uint64_t* last;   // (ABL 8: wave 0's stamp)
+  uint8_t* crank;   // SP: 2 x kRankTab actor -> rank tables of both top clocks (topr), or null
 };
 
 // merge_path with the answer known to lie in [ilo, ihi], ihi - ilo <= 64.
@@ -2566,6 +2581,21 @@ __device__ __forceinline__ void merge_object_block(const S& L, const S& R, uint8
   const uint32_t nch = (P + kWave - 1) / kWave;
   uint32_t n_clk = A;
   if constexpr (SP) n_clk = uni(sparse_clock_join(L, R, nullptr, 0u, lane));
+  // SP: both top clocks' actor -> rank tables (clocks of <= 255 entries over
+  // actor ids < kRankTab; others keep the binary search)
+  lds_cu8* crank = nullptr;
+  if (SP && T.crank != nullptr && L.v.n_clk <= 255u && R.v.n_clk <= 255u) {
+    uint32_t* z = (uint32_t*)T.crank;
+    for (uint32_t k = threadIdx.x; k < 2u * kRankTab / 4u; k += kWave * kBigW) z[k] = 0u;
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < L.v.n_clk + R.v.n_clk; k += kWave * kBigW) {
+      const bool isL = k < L.v.n_clk;
+      const uint32_t e = isL ? k : k - L.v.n_clk;
+      const uint32_t x = isL ? g32(L.b, L.v.cact, e) : g32(R.b, R.v.cact, e);
+      if (x < kRankTab) T.crank[(isL ? 0u : kRankTab) + x] = (uint8_t)(e + 1u);
+    }
+    crank = (lds_cu8*)(size_t)lds_addr(T.crank);
+  }
   // ---- the deferred member filter (both sides' deferred member keys)
   if (has_def) {
     if (threadIdx.x < 32u) T.bloom[threadIdx.x] = 0u;
@@ -2598,7 +2628,7 @@ __device__ __forceinline__ void merge_object_block(const S& L, const S& R, uint8
     if (p < P) {
       type = merge_path_in(L, R, p, ilo, ihi, i, j);
       if (ABL == 4) cnt = type != kNone;
-      else if (type != kNone) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0, T.bloom);
+      else if (type != kNone) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0, T.bloom, crank);
       if (p < kBigPos) {
         T.pq[p] = (uint16_t)((type << 14) | i);
         T.pc[p] = (uint8_t)(cnt < 255u ? cnt : 255u);
@@ -2691,10 +2721,10 @@ __device__ __forceinline__ void merge_object_block(const S& L, const S& R, uint8
       const uint32_t u = T.pq[p];
       type = u >> 14; i = u & 0x3FFFu; j = p - i;
       cnt = T.pc[p];
-      if (cnt == 255u) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0, T.bloom);
+      if (cnt == 255u) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0, T.bloom, crank);
     } else if (p < P) {
       type = merge_path_in(L, R, p, uni(T.spl[ch]), uni(T.spl[ch + 1]), i, j);
-      if (type != kNone) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0, T.bloom);
+      if (type != kNone) cnt = join<0, SP>(L, R, type, i, j, A, has_def, x, v, nullptr, nullptr, 0, T.bloom, crank);
       xv = true;
     }
     const uint64_t keep = __ballot(cnt != 0);
@@ -2708,7 +2738,7 @@ __device__ __forceinline__ void merge_object_block(const S& L, const S& R, uint8
         odact[d0] = x;
         odctr[d0] = v;
       } else {
-        join<1, SP>(L, R, type, i, j, A, has_def, x, v, odact, odctr, d0, T.bloom);
+        join<1, SP>(L, R, type, i, j, A, has_def, x, v, odact, odctr, d0, T.bloom, crank);
       }
       omdend[midx] = d0 + cnt;
     }
@@ -2720,11 +2750,11 @@ __device__ __forceinline__ void merge_object_block(const S& L, const S& R, uint8
 
 template <bool SP, int ABL>
 __device__ __noinline__ void big_from_hbm(const uint8_t* lr, const uint8_t* rr, uint8_t* O, uint32_t A,
-                                          uint32_t lane, uint32_t wave, u32x4* st, uint32_t* bc) {
+                                          uint32_t lane, uint32_t wave, u32x4* st, uint32_t* bc, uint8_t* crank) {
   uint8_t* sb = (uint8_t*)st;
   const BigTabs H{(uint32_t*)sb, (uint32_t*)(sb + 8u * kBigChH), (uint16_t*)(sb + 12u * kBigChH + 16u),
                   (uint8_t*)(sb + 12u * kBigChH + 16u + 2u * kBigPos), bc, kBigChH,
-                  (uint32_t*)(sb + 12u * kBigChH + 16u + 3u * kBigPos), nullptr};
+                  (uint32_t*)(sb + 12u * kBigChH + 16u + 3u * kBigPos), nullptr, crank};
   static_assert(12u * kBigChH + 16u + 3u * kBigPos + 128u <= 2u * kBigStage, "HBM-path tables fit the stage");
   const RecLayout LL = layout_at(lr), RL = layout_at(rr);
   const Side L{lr, make_rv(LL)}, R{rr, make_rv(RL)};
@@ -2779,7 +2809,7 @@ __device__ __forceinline__ void big_one(const uint8_t* Lb, const uint64_t* Loff,
       const SideL L{(lds_cu8*)(size_t)lds_addr(sl), make_rv(LL)}, R{(lds_cu8*)(size_t)lds_addr(sr), make_rv(RL)};
       if constexpr (ABL != 5) merge_object_block<SP, ABL>(L, R, Ob + oo, A, lane, wave, T);  // (5: staging only)
     } else {  // from HBM; the tables in the stage
-      big_from_hbm<SP, ABL>(lr, rr, Ob + oo, A, lane, wave, st, T.bc);
+      big_from_hbm<SP, ABL>(lr, rr, Ob + oo, A, lane, wave, st, T.bc, T.crank);
     }
   }
   if (threadIdx.x == 0u) Ooff[o] = oo;
@@ -2805,7 +2835,8 @@ __global__ __launch_bounds__(kWave * kBigW, MINW) void orswot_big_kernel(
   __shared__ uint32_t bloom_s[32];
   uint64_t last = 0;
   if (ABL == 8) last = stamp();
-  const BigTabs T{tot_s, spl_s, pq_s, pc_s, bc_s, kBigChS, bloom_s, ABL == 8 ? &last : nullptr};
+  __shared__ uint8_t crank_s[SP ? 2u * kRankTab : 4u];  // (SP: the top clocks' actor -> rank tables)
+  const BigTabs T{tot_s, spl_s, pq_s, pc_s, bc_s, kBigChS, bloom_s, ABL == 8 ? &last : nullptr, SP ? crank_s : nullptr};
   const uint32_t lane = threadIdx.x & (kWave - 1), wave = uni(threadIdx.x / kWave);
   const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   const uint32_t scan = uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -2894,12 +2925,15 @@ int g_big_variant = 0;  // diag variants 330..: the big kernel's knobs
 
 // The big-object pass, queued after every general kernel launch (the objects
 // it leaves flagged are this kernel's).
+// SP: CSR top clocks (after the sparse general kernel)
+template <bool SP = false>
 __host__ inline hipError_t launch_big(const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb, const uint64_t* Roff,
                                       uint8_t* Ob, uint64_t* Ooff, uint64_t n_obj, uint32_t A, uint32_t* ctl,
                                       const uint64_t* list, uint32_t list_cap, hipStream_t stream) {
-  const void* fn = (const void*)orswot_big_kernel<false, 4>;
+  const void* fn = (const void*)orswot_big_kernel<SP, 4>;
   uint32_t blocks = kBigBlocks;
 #ifdef CRDT_DIAG
+  if (!SP) {
   if (g_big_variant == 1) { fn = (const void*)orswot_big_kernel<false, 1>; blocks = 256; }
   if (g_big_variant == 2) { fn = (const void*)orswot_big_kernel<false, 2>; blocks = 256; }
   if (g_big_variant == 3) blocks = 256;
@@ -2910,6 +2944,7 @@ __host__ inline hipError_t launch_big(const uint8_t* Lb, const uint64_t* Loff, c
   if (g_big_variant == 8) fn = (const void*)orswot_big_kernel<false, 4, 5>;
   if (g_big_variant == 9) fn = (const void*)orswot_big_kernel<false, 4, 6>;
   if (g_big_variant == 11) fn = (const void*)orswot_big_kernel<false, 4, 8>;
+  }
 #endif
   void* args[] = {&Lb, &Loff, &Rb, &Roff, &Ob, &Ooff, &n_obj, &A, &ctl, &list, &list_cap};
   return hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kBigW), args, 0, stream);
@@ -3065,14 +3100,20 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
 // One sparse join of the pre-loaded object g (GenPre: offsets, headers) into
 // its output place (any sizes); `mid` runs once the records are staged (the
 // caller's loads for the next listed object, in flight during this join).
+// (returns true for an object it leaves to orswot_big_kernel<true>: past
+// kBigMinPos union positions or the general stage, as general_one)
 template <class Mid>
-__device__ __forceinline__ void sparse_general_one(const GenPre& g, uint8_t* Ob, uint64_t* Ooff, uint32_t A,
+__device__ __forceinline__ bool sparse_general_one(const GenPre& g, uint8_t* Ob, uint64_t* Ooff, uint32_t A,
                                                    u32x4* sl, u32x4* sr, uint8_t* X, uint32_t lane, Mid&& mid) {
   const uint8_t* lr = g.lr;
   const uint8_t* rr = g.rr;
   uint8_t* O = Ob + g.oo;
   const u32x4 hl0 = g.hl0, hl1 = g.hl1, hr0 = g.hr0, hr1 = g.hr1;
   const uint32_t szl = uni(hl0.x), szr = uni(hr0.x);
+  if (is_big(u32x4{szl, 0u, uni(hl0.z), 0u}, u32x4{szr, 0u, uni(hr0.z), 0u})) {  // orswot_big_kernel<true>'s
+    mid();
+    return true;
+  }
   if (szl > kGenStage || szr > kGenStage) mid();
   if (szl <= kGenStage && szr <= kGenStage) {
     wave_sync();
@@ -3116,6 +3157,7 @@ __device__ __forceinline__ void sparse_general_one(const GenPre& g, uint8_t* Ob,
     merge_object<true>(lr, rr, O, A, lane);
   }
   if (lane == 0) Ooff[g.o] = g.oo;
+  return false;
 }
 
 __global__ __launch_bounds__(kWave) void orswot_sparse_general_kernel(
@@ -3133,25 +3175,30 @@ __global__ __launch_bounds__(kWave) void orswot_sparse_general_kernel(
     if (blockIdx.x >= n) return;
     GenPre cur, nxt;
     gen_pre(cur, Lb, Loff, Rb, Roff, Ooff, list[blockIdx.x]);
+    bool big = false;
     for (uint32_t e = blockIdx.x; e < n; e += gridDim.x) {
       const uint32_t en = e + gridDim.x;
       const uint64_t on = en < n ? list[en] : 0ull;
-      sparse_general_one(cur, Ob, Ooff, A, gen_s[0], gen_s[1], (uint8_t*)gx_s, lane, [&]() {
+      big |= sparse_general_one(cur, Ob, Ooff, A, gen_s[0], gen_s[1], (uint8_t*)gx_s, lane, [&]() {
         if (en < n) gen_pre(nxt, Lb, Loff, Rb, Roff, Ooff, on);
       });
       cur = nxt;
     }
+    // one store per wave that left a big object (as the dense general kernel)
+    if (big && lane == 0u) __hip_atomic_store(&ctl[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {  // list overflow: scan the flags
     const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
+    bool big = false;
     for (uint64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
       const uint64_t obj = chunk * kWave + lane;
       const uint64_t oo = obj < n_obj ? Ooff[obj] : 0ull;
       for (uint64_t pend = __ballot((oo & kPending) != 0ull); pend; pend &= pend - 1) {
         GenPre g;
         gen_pre(g, Lb, Loff, Rb, Roff, Ooff, chunk * kWave + (uint32_t)__builtin_ctzll(pend));
-        sparse_general_one(g, Ob, Ooff, A, gen_s[0], gen_s[1], (uint8_t*)gx_s, lane, []() {});
+        big |= sparse_general_one(g, Ob, Ooff, A, gen_s[0], gen_s[1], (uint8_t*)gx_s, lane, []() {});
       }
     }
+    if (big && lane == 0u) __hip_atomic_store(&ctl[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -3317,6 +3364,10 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
   hipLaunchKernelGGL(orswot_sparse_general_kernel, dim3((uint32_t)cus * 6u), dim3(kWave), 0, stream, Lb, Loff, Rb,
                      Roff, Ob, Ooff, n_obj, n_actors, set, list, list_cap, other);
   if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
+  // objects past 128 union positions or the general stage: one block each
+  // (orswot_big_kernel<true>; it exits at once when the general kernel left none)
+  if (launch_big<true>(Lb, Loff, Rb, Roff, Ob, Ooff, n_obj, n_actors, set, list, list_cap, stream) != hipSuccess)
+    return CRDT_EHIP;
   if (nm) {
     ++js->seq;
     js->dirty = false;

@@ -174,3 +174,39 @@ def test_dense_and_sparse_launches_alternate_on_one_context(gpu, oracle):
             _compare(gpu.orswot_merge(L, R).records(), *dexp, f"dense launch {k}")
         else:
             _compare(_merge(gpu, sa, sao, sb, sbo).records(), *sexp, f"sparse launch {k}")
+
+
+# ------------------------------------------------------------------ heavy CSR objects
+def test_csr_heavy_tail_100k(gpu, oracle):
+    """Config 5's record form with a heavy tail (bench.py --workload
+    orswot_csr_tail): every 20th object at ~100 / 300 / 1000 members per side
+    (the reference's entries map and clock are unbounded, src/orswot.rs:26-30,
+    src/vclock.rs:54-57). Objects past 128 union positions or the general
+    stage take orswot_big_kernel<true> (one workgroup per object, CSR top
+    clock); byte-exact against the oracle, both orientations."""
+    import crdts_hip
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot_csr_tail(100_000, threads=16)
+    recs = records.unpack_batch(lb, lo)
+    heavy = list(range(0, 100_000, 20))
+    sizes = [len(records.decode(recs[i])["entries"]) for i in heavy]
+    assert sum(s > 128 for s in sizes) > len(heavy) // 2 and max(len(recs[i]) for i in heavy) > 16_384
+    for a, b in (((lb, lo), (rb, ro)), ((rb, ro), (lb, lo))):
+        got = _merge(gpu, *a, *b).records()
+        ob, oo = oracle.orswot_merge_batch(*a, *b, U, threads=16, flags=SPARSE)
+        _compare(got, ob, oo, "CSR heavy tail")
+
+
+def test_csr_big_kernel_hbm_path(gpu, oracle):
+    """CSR objects of ~3 000 members per side (records past the big kernel's
+    32 KB LDS stage: its HBM-table path) mixed 1:1 with config-5 objects,
+    byte-exact against the oracle, both orientations."""
+    import crdts_hip
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot_csr_tail(400, frac=0.5, sizes=(3000,), threads=16)
+    recs = records.unpack_batch(lb, lo)
+    assert max(len(recs[i]) for i in range(0, 400, 2)) > 32_768
+    for a, b in (((lb, lo), (rb, ro)), ((rb, ro), (lb, lo))):
+        got = _merge(gpu, *a, *b).records()
+        ob, oo = oracle.orswot_merge_batch(*a, *b, U, threads=16, flags=SPARSE)
+        _compare(got, ob, oo, "CSR big HBM path")
