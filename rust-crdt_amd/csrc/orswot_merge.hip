@@ -76,6 +76,10 @@ __device__ __forceinline__ void mark(Stamps& st, int k) {
 }
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+}
 __device__ __forceinline__ uint32_t lane_of(uint32_t v, uint32_t t) { return __builtin_amdgcn_readlane(v, t); }
 __device__ __forceinline__ uint64_t lane_of64(uint64_t v, uint32_t t) {
   // readlane yields int: widen through uint32_t, or a low half with bit 31
@@ -2211,6 +2215,43 @@ __device__ __forceinline__ void stage_used(u32x4* dst, const u32x4 (&r)[kPer], u
 #endif
 
 
+constexpr uint32_t kGenStage = 8192;
+constexpr uint32_t kGenBlocks = 1536;  // 6 resident 24 KB-LDS blocks per CU
+
+// (the big-object kernel's share of the general list: see orswot_big_kernel)
+constexpr uint32_t kBigW = 8;           // waves per block
+constexpr uint32_t kBigStage = 32768;   // LDS stage per record
+
+#ifndef CRDT_BIG_MIN_POS
+#define CRDT_BIG_MIN_POS 128
+#endif
+constexpr uint32_t kBigMinPos = CRDT_BIG_MIN_POS;  // union positions past which an object takes the block join
+
+__device__ __forceinline__ bool is_big(u32x4 hl0, u32x4 hr0) {
+  return hl0.z + hr0.z > kBigMinPos || hl0.x > kGenStage || hr0.x > kGenStage;
+}
+
+
+// ---- the object lists behind a join launch. The context's list buffer is
+// split in two halves of list_cap entries each (the launchers halve the
+// context's capacity): [0, list_cap) the general kernel's list (count ctl[0]),
+// [list_cap, 2 list_cap) the big-object list (count ctl[2] & kBigCount).
+// Objects are appended with one atomic per wave and list (a per-lane atomic
+// on one address serialises at the memory side: 49k of them cost the join
+// ~80 us, r06). Past a half's capacity the consumers scan the pending flags.
+constexpr uint32_t kBigCount = 0x7FFFFFFFu;  // ctl[2]: big-list count; bit 31: the general kernel left big objects
+constexpr uint32_t kBigLeft = 0x80000000u;
+__device__ __forceinline__ void list_append(bool put, uint64_t obj, uint32_t* ctr, uint64_t* dst, uint32_t cap,
+                                            uint32_t lane) {
+  const uint64_t m = __ballot(put);
+  if (m == 0ull) return;
+  uint32_t base = 0u;
+  if (lane == 0u) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+  base = (uint32_t)__builtin_amdgcn_readfirstlane(base);
+  const uint32_t e = base + mbcnt64(m);
+  if (put && e < cap) dst[e] = obj;
+}
+
 // ======================================================================
 // The product join (round 5 form): orswot_join_kernel's product
 // instantiation written out with only the product's choices — one pass,
@@ -2277,10 +2318,11 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join5_ker
     // once, at its end (no per-lane 64-bit value kept across the loop)
     uint64_t pendm = __ballot(gen);
     if (!(FL & 1) && valid) Ooff[obj] = (lo + ro) | (gen ? kPending : 0ull);
-    if (gen) {  // hand the object to the general kernel
-      const uint32_t e = atomicAdd(&ctl[0], 1u);
-      if (e < list_cap) list[e] = obj;
-    }
+    // hand the object to the general kernel, or straight to orswot_big_kernel
+    // when its headers already say it is big (is_big)
+    const bool bigo = gen && is_big(hl0, hr0);
+    list_append(gen && !bigo, obj, &ctl[0], list, list_cap, lane);
+    list_append(bigo, obj, &ctl[2], list + list_cap, list_cap, lane);
     if (__ballot(valid && !ok && placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
     const uint64_t runs = __ballot(fast);
     if (runs == 0ull) {
@@ -2370,22 +2412,6 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join5_ker
 // both kernels scan every output offset for flags instead. The list counter
 // is cleared by the alternating control-word sets (launch_join_passes).
 // ======================================================================
-constexpr uint32_t kGenStage = 8192;
-constexpr uint32_t kGenBlocks = 1536;  // 6 resident 24 KB-LDS blocks per CU
-
-// (the big-object kernel's share of the general list: see orswot_big_kernel)
-constexpr uint32_t kBigW = 8;           // waves per block
-constexpr uint32_t kBigStage = 32768;   // LDS stage per record
-
-#ifndef CRDT_BIG_MIN_POS
-#define CRDT_BIG_MIN_POS 128
-#endif
-constexpr uint32_t kBigMinPos = CRDT_BIG_MIN_POS;  // union positions past which an object takes the block join
-
-__device__ __forceinline__ bool is_big(u32x4 hl0, u32x4 hr0) {
-  return hl0.z + hr0.z > kBigMinPos || hl0.x > kGenStage || hr0.x > kGenStage;
-}
-
 // A listed object's offsets and headers, loaded ahead of its join.
 struct GenPre {
   uint64_t o, oo;
@@ -2773,7 +2799,11 @@ __device__ __forceinline__ void big_one(const uint8_t* Lb, const uint64_t* Loff,
                                         const uint64_t* Roff, uint8_t* Ob, uint64_t* Ooff, uint64_t o, uint32_t A,
                                         u32x4* st, const BigTabs& T, uint32_t lane, uint32_t wave) {
   if (T.last) bst<ABL>(*T.last, 8, wave, lane);  // (8: between objects: the list walk)
-  const uint64_t oo = Ooff[o] & ~kPending;
+  const uint64_t ow = Ooff[o];
+  // only a pending object is this kernel's: after the general kernel every
+  // pending object of either list is big (the general kernel cleared the rest)
+  if ((ow & kPending) == 0ull) return;
+  const uint64_t oo = ow & ~kPending;
   const uint8_t* lr = Lb + Loff[o];
   const uint8_t* rr = Rb + Roff[o];
   const RecLayout LL = layout_at(lr), RL = layout_at(rr);
@@ -2820,9 +2850,10 @@ __device__ __forceinline__ void big_one(const uint8_t* Lb, const uint64_t* Loff,
 #endif
 }
 
-// The listed objects is_big() picks (the general kernel, launched before,
-// skipped them), one block per object. With an overflowed list every pending
-// flag left is one.
+// The big objects, one block per object: the join's big list (objects whose
+// headers already said big) and the general list's objects is_big() picks
+// (the general kernel, launched before, skipped them). With an overflowed
+// list every pending flag left is one.
 template <bool SP, int MINW = 4, int ABL = 0>
 __global__ __launch_bounds__(kWave * kBigW, MINW) void orswot_big_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, const uint8_t* __restrict__ Rb,
@@ -2840,25 +2871,32 @@ __global__ __launch_bounds__(kWave * kBigW, MINW) void orswot_big_kernel(
   const uint32_t lane = threadIdx.x & (kWave - 1), wave = uni(threadIdx.x / kWave);
   const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   const uint32_t scan = uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  // ctl[2]: set by the general kernel when it left a big object (zeroed
-  // between launches, so 0 means none; the join variants that use the word
-  // otherwise only make it non-zero: a full walk, still exact)
-  const uint32_t nbig = uni(__hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  if (n == 0u || nbig == 0u) return;
-  // listed: the list in 64-entry chunks dealt round-robin to the blocks (no
-  // ticket: every control word is some join variant's), each wave reading
-  // the chunk's headers; list overflow / unlisted flags: every pending object
-  // left is big. The block takes its chunk's big objects in order.
-  const bool listed = n <= list_cap && scan == 0u;
-  const uint64_t n_chunks = ((listed ? (uint64_t)n : n_obj) + kWave - 1) / kWave;
-  for (uint64_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
-    const uint64_t e = c * kWave + lane;
+  // ctl[2] (list_append): the big list's count, | kBigLeft when the general
+  // kernel left big objects in its own list (zeroed between launches, so 0
+  // means none)
+  const uint32_t w2 = uni(__hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const uint32_t nb = w2 & kBigCount, ng = (w2 & kBigLeft) ? n : 0u;
+  if (nb == 0u && ng == 0u) return;
+  // listed: the big list, then (when the general kernel left some) the
+  // general list, one entry at a time dealt round-robin to the blocks (an
+  // entry is one object: a block's share differs by at most one object; the
+  // next entry is loaded while the current object is joined); big_one takes
+  // only pending objects. A list past its half's capacity / a scan request:
+  // every pending object left is big, found by a walk of the flags.
+  const bool listed = n <= list_cap && nb <= list_cap && scan == 0u;
+  const uint64_t units = listed ? (uint64_t)nb + ng : n_obj;
+  // listed: entry e goes to block e % grid (rounds of 64 of the block's
+  // entries: the block's share differs from another's by at most one
+  // object); the flag walk: 64-object chunks round-robin
+  for (uint64_t k0 = 0;; k0 += kWave) {
+    const uint64_t e = listed ? (k0 + lane) * gridDim.x + blockIdx.x : (k0 / kWave * gridDim.x + blockIdx.x) * kWave + lane;
+    if (uni64(e) >= units) break;  // (lane 0's is the round's smallest)
     bool big = false;
     uint64_t o = e;
     if (listed) {
-      if (e < n) {
-        o = list[e];
-        big = is_big(((const u32x4*)(Lb + Loff[o]))[0], ((const u32x4*)(Rb + Roff[o]))[0]);
+      if (e < units) {
+        o = e < nb ? list[list_cap + e] : list[e - nb];
+        big = o < n_obj;  // (big_one takes only pending objects)
       }
     } else {
       big = e < n_obj && (Ooff[e] & kPending) != 0ull;
@@ -2902,7 +2940,7 @@ __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
     }
     // one store per wave that left a big object (not one atomic per object:
     // same-address atomics serialise at the memory side)
-    if (big && lane == 0u) __hip_atomic_store(&ctl[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (big && lane == 0u) __hip_atomic_fetch_or(&ctl[2], kBigLeft, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {  // list overflow, or objects flagged without a list entry: scan the flags
     const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
     for (uint64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
@@ -2912,7 +2950,7 @@ __global__ __launch_bounds__(kWave) void orswot_merge_general_kernel(
         GenPre g;
         gen_pre(g, Lb, Loff, Rb, Roff, Ooff, chunk * kWave + (uint32_t)__builtin_ctzll(pend));
         if (general_one(g, Ob, Ooff, A, gen_s[0], gen_s[1], gen_s[2], lane, []() {}) && lane == 0u)
-          __hip_atomic_store(&ctl[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_or(&ctl[2], kBigLeft, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -3039,9 +3077,10 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
                       hl0.z <= 64u && hr0.z <= 64u && hl0.w <= 128u && hr0.w <= 128u && hl1.x <= 32u &&
                       hr1.x <= 32u;
     if (valid) Ooff[obj] = (lo + ro) | ((ok && !fast) ? kPending : 0ull);
-    if (ABL != 9 && ok && !fast) {
-      const uint32_t e = atomicAdd(&ctl[0], 1u);
-      if (e < list_cap) list[e] = obj;
+    if (ABL != 9) {  // the general kernel's objects, big ones straight to orswot_big_kernel<true>
+      const bool bigo = ok && !fast && is_big(hl0, hr0);
+      list_append(ok && !fast && !bigo, obj, &ctl[0], list, list_cap, lane);
+      list_append(bigo, obj, &ctl[2], list + list_cap, list_cap, lane);
     }
     if (__ballot(valid && !ok && placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_ENONCANON);
     uint64_t pend = __ballot(fast);
@@ -3185,7 +3224,7 @@ __global__ __launch_bounds__(kWave) void orswot_sparse_general_kernel(
       cur = nxt;
     }
     // one store per wave that left a big object (as the dense general kernel)
-    if (big && lane == 0u) __hip_atomic_store(&ctl[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (big && lane == 0u) __hip_atomic_fetch_or(&ctl[2], kBigLeft, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {  // list overflow: scan the flags
     const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
     bool big = false;
@@ -3198,7 +3237,7 @@ __global__ __launch_bounds__(kWave) void orswot_sparse_general_kernel(
         big |= sparse_general_one(g, Ob, Ooff, A, gen_s[0], gen_s[1], (uint8_t*)gx_s, lane, []() {});
       }
     }
-    if (big && lane == 0u) __hip_atomic_store(&ctl[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (big && lane == 0u) __hip_atomic_fetch_or(&ctl[2], kBigLeft, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -3267,6 +3306,7 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
                         uint64_t* list, uint32_t list_cap, hipStream_t stream, int blocks_per_cu, int variant,
                         JoinSeq* js) {
   if (n_obj == 0) return CRDT_OK;
+  list_cap /= 2u;  // the context's list: the general half, then the big half (list_append)
   JoinSeq local{0u, true};
   if (!js) js = &local;  // (no context state: the words are zeroed first)
   auto go = [&](auto f) {
@@ -3308,6 +3348,7 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
                                uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list,
                                uint32_t list_cap, hipStream_t stream, int sparse_variant, JoinSeq* js) {
   if (n_obj == 0) return CRDT_OK;
+  list_cap /= 2u;  // the context's list: the general half, then the big half (list_append)
   JoinSeq local{0u, true};
   if (!js) js = &local;
   int dev = 0, cus = 256, occ = 0;

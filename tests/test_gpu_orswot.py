@@ -579,3 +579,22 @@ def test_big_kernel_paths(gpu, oracle):
         out = _gpu_merge(gpu, *x, *y, 16)
         ob, oo = oracle.orswot_merge_batch(*x, *y, 16, threads=8)
         _compare(out, ob, oo, "big kernel paths")
+
+
+def test_heavy_tail_list_caps(gpu, oracle):
+    """The heavy tail's objects reach orswot_big_kernel by the join's big list
+    (headers already big), the general list, or — when a half of the
+    context's list is full — the pending flags: caps that overflow neither
+    half, only the big half (1 500: halves of 750 < 1 000 heavy objects),
+    both (8), and none at all (0); byte-exact every time, alternating with the
+    unlimited cap on one context."""
+    import crdts_hip
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot_tail(20_000, threads=16)
+    ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, 16, threads=16)
+    try:
+        for cap in (65536, 1500, 8, 0, 65536):
+            gpu.set_list_cap(cap)
+            _compare(_gpu_merge(gpu, lb, lo, rb, ro, 16), ob, oo, f"tail, cap {cap}")
+    finally:
+        gpu.set_list_cap(65536)

@@ -210,3 +210,19 @@ def test_csr_big_kernel_hbm_path(gpu, oracle):
         got = _merge(gpu, *a, *b).records()
         ob, oo = oracle.orswot_merge_batch(*a, *b, U, threads=16, flags=SPARSE)
         _compare(got, ob, oo, "CSR big HBM path")
+
+
+def test_csr_heavy_tail_list_caps(gpu, oracle):
+    """CSR heavy tail with list caps that overflow the big half, both halves,
+    or leave no list at all: the big objects still reach
+    orswot_big_kernel<true> (by the pending flags), byte-exact."""
+    import crdts_hip
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot_csr_tail(20_000, threads=16)
+    ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, U, threads=16, flags=SPARSE)
+    try:
+        for cap in (65536, 1500, 8, 0, 65536):
+            gpu.set_list_cap(cap)
+            _compare(_merge(gpu, lb, lo, rb, ro).records(), ob, oo, f"CSR tail, cap {cap}")
+    finally:
+        gpu.set_list_cap(65536)
