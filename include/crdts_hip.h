@@ -62,9 +62,11 @@ int crdt_ctx_status(crdt_ctx* ctx, void* stream);
 const char* crdt_strerror(int code);
 int crdt_abi_version(void);
 /* Capacity (<= 65536, the default) of the context's list of objects handed
- * from the fast Orswot / apply kernels to their general kernels. Past it the
- * general kernels scan every output offset instead; results are identical.
- * Lowering it exercises that overflow path (tests). */
+ * from the fast Orswot / apply kernels to their general kernels (an Orswot
+ * merge splits it in two halves: the general kernel's objects and the big
+ * objects the join hands straight to the block-per-object kernel). Past a
+ * list's capacity the kernels scan every output offset instead; results are
+ * identical. Lowering it exercises that overflow path (tests). */
 int crdt_ctx_set_list_cap(crdt_ctx* ctx, uint32_t cap);
 /* Host synchronisations with the device (stream waits) the context's replica
  * joins have made so far (crdt_orswot_replica_join*: 3 per call in the steady
