@@ -32,6 +32,7 @@
 #include "../../include/crdts_hip.h"
 #include "kernels.h"
 #include "record_layout.h"
+#include "sched.h"
 
 namespace crdts_hip {
 namespace {
@@ -714,6 +715,11 @@ __device__ void truncate_lds(const TruncArgs& g, const Rec& R, uint64_t o, uint3
 // records are truncated one by one with the next one's record and clock in
 // flight in registers, and the others (CSR top clocks, records past the LDS
 // limits or not canonical here) in the HBM form.
+// FLAGGED (after orswot_truncate_fast_kernel): only the records whose output
+// offset the fast kernel left flagged (kTPend) are this kernel's; the flag is
+// cleared when the record is written here.
+constexpr uint64_t kTPend = 1ull << 63;
+template <bool FLAGGED>
 __global__ __launch_bounds__(kW * kTWaves, 4) void orswot_truncate_kernel(TruncArgs g) {
   __shared__ TWs ws[kTWaves];
   const uint32_t lane = threadIdx.x & (kW - 1u), wv = threadIdx.x / kW;
@@ -723,7 +729,8 @@ __global__ __launch_bounds__(kW * kTWaves, 4) void orswot_truncate_kernel(TruncA
   const bool sparse = (g.flags & kSparseClock) != 0u;
   for (uint64_t cb = wave * kW; cb < g.n_obj; cb += n_waves * kW) {
     const uint64_t obj = cb + lane;
-    const bool valid = obj < g.n_obj;
+    const bool valid = obj < g.n_obj && (!FLAGGED || (g.out_off[obj] & kTPend) != 0ull);
+    if (FLAGGED && __ballot(valid) == 0ull) continue;
     uint64_t o = 0, c0 = 0;
     uint32_t cn = 0;
     if (valid) {
@@ -804,27 +811,216 @@ __global__ __launch_bounds__(kW * kTWaves, 4) void orswot_truncate_kernel(TruncA
   }
 }
 
+
+// ---------------------------------------------------------------- fast form
+// The common record — dense top clock over A <= 32 actors, no deferred
+// removes, <= 64 members and <= 64 dots, <= 2 KB, a truncating clock run of
+// <= 64 entries — as a streaming filter, with the join kernel's skeleton
+// (orswot_join5_kernel): a resident grid with the guided split, the chunk's
+// offsets, clock runs and headers in one step (lane = object), the next
+// record and clock run prefetched into registers while the current one is
+// filtered from LDS, the output assembled over the stage and copied out with
+// 16-B stores. Without deferred removes truncate is a filter (src/orswot.rs
+// :159-172 with the empty set's merge :94-104 and VClock::subtract
+// src/vclock.rs:236-242): a dot (x, v) survives iff v > c[x], a member is
+// kept iff one of its dots survives (then it keeps exactly those: never an
+// empty clock), the top clock keeps T[x] iff T[x] > c[x]. Every other record
+// is flagged (kTPend on its output offset) for orswot_truncate_kernel<true>.
+constexpr uint32_t kTFStage = 2048;               // record bytes staged per wave
+constexpr uint32_t kTFPer = kTFStage / 16u / kW;  // 16-B pieces per lane
+struct TFWs {
+  tu32x4 stage[kTFStage / 16];
+  uint64_t ct[kTA];  // the truncating clock, dense
+};
+__device__ __forceinline__ void tf_sync() { tsync(); }
+__device__ __forceinline__ uint64_t lane64(uint64_t v, uint32_t t) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), t) << 32) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, t);
+}
+
+__global__ __launch_bounds__(kW * kTWaves, 8) void orswot_truncate_fast_kernel(TruncArgs g, uint32_t* ctl) {
+  __shared__ TFWs ws[kTWaves];
+  const uint32_t lane = threadIdx.x & (kW - 1u), wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kW);
+  TFWs& w = ws[wv];
+  const uint64_t wave_id = (uint64_t)blockIdx.x * kTWaves + wv, n_waves = (uint64_t)gridDim.x * kTWaves;
+  const uint32_t A = g.A;
+  GuidedSplit<20u, 5u> gs(g.n_obj, wave_id, n_waves);
+  uint64_t cbase, cend;
+  while (gs.next(cbase, cend, &ctl[3], lane)) {
+    // ---- chunk step: lane k <-> object cbase + k
+    const uint64_t obj = cbase + lane;
+    const bool valid = obj < cend;
+    uint64_t o = 0, c0 = 0;
+    uint32_t cn = 0;
+    if (valid) {
+      o = g.off[obj];
+      c0 = g.coff[obj];
+      cn = g.clen[obj];
+    }
+    bool ok = valid && (o & 15u) == 0u && o <= g.bytes && g.bytes - o >= kHdrBytes;
+    tu32x4 h0 = {0u, 0u, 0u, 0u}, h1 = h0;
+    if (ok) {
+      h0 = ((const tu32x4*)(g.base + o))[0];
+      h1 = ((const tu32x4*)(g.base + o))[1];
+    }
+    // the fast form's own verdict (the rest, well-formed or not, is the
+    // general kernel's: it latches the errors)
+    const bool fast = ok && h0.y == A && A <= kTA && h0.z <= kW && h0.w <= kW && h1.x == 0u && h1.y == 0u &&
+                      h1.z == 0u && (h1.w & ~kEmptyClockFlag) == 0u && h0.x <= kTFStage &&
+                      h0.x == (((kHdrBytes + 8u * A + 12u * (h0.z + h0.w)) + 15u) & ~15u) &&
+                      h0.x <= g.bytes - o && o + h0.x <= g.out_bytes && c0 <= g.c_entries &&
+                      cn <= g.c_entries - c0 && cn <= kW;
+    if (valid) g.out_off[obj] = o | (fast ? 0ull : kTPend);
+    uint64_t pend = __ballot(fast);
+    if (pend == 0ull) continue;
+    const uint32_t n16 = fast ? h0.x / 16u : 1u;
+    const uint32_t nmd = h0.z | (h0.w << 16);
+    // ---- one record ahead in registers: its pieces and its clock run
+    tu32x4 pr[kTFPer];
+    uint32_t pa;
+    uint64_t pc;
+    auto fetch = [&](uint32_t t) {
+      const uint8_t* rec = g.base + lane64(o, t);
+      const uint32_t n = (uint32_t)__builtin_amdgcn_readlane(n16, t);
+#pragma unroll
+      for (uint32_t k = 0; k < kTFPer; ++k) {
+        const uint32_t i = lane + k * kW;
+        pr[k] = __builtin_nontemporal_load((const tu32x4*)rec + (i < n ? i : n - 1u));
+      }
+      const uint64_t ct0 = lane64(c0, t);
+      const uint32_t cnt = (uint32_t)__builtin_amdgcn_readlane(cn, t);
+      pa = lane < cnt ? g.cact[ct0 + lane] : 0xFFFFFFFFu;
+      pc = lane < cnt ? g.cctr[ct0 + lane] : 0ull;
+    };
+    uint32_t t = (uint32_t)__builtin_ctzll(pend);
+    pend &= pend - 1u;
+    fetch(t);
+    for (;;) {
+      // ---- stage the record and the dense clock row (the previous record's
+      // LDS reads are done: its copy-out waited for them)
+      const uint32_t n = (uint32_t)__builtin_amdgcn_readlane(n16, t);
+#pragma unroll
+      for (uint32_t k = 0; k < kTFPer; ++k)
+        if (lane + k * kW < n) w.stage[lane + k * kW] = pr[k];
+      if (lane < kTA) w.ct[lane] = 0ull;
+      const uint32_t ra = pa;
+      const uint64_t rc = pc;
+      const uint32_t prev = __shfl_up(ra, 1);
+      const uint32_t cnt = (uint32_t)__builtin_amdgcn_readlane(cn, t);
+      // canonical run: actors strictly increasing, counters > 0
+      const bool cbad = lane < cnt && (rc == 0ull || (lane > 0u && ra <= prev));
+      tf_sync();
+      if (lane < cnt && ra < kTA) w.ct[ra] = rc;
+      const uint64_t oo = lane64(o, t);
+      const uint32_t md = (uint32_t)__builtin_amdgcn_readlane(nmd, t);
+      const uint32_t nM = md & 0xFFFFu, nD = md >> 16;
+      // the next record's loads, in flight while this one is filtered
+      const bool more = pend != 0ull;
+      const uint32_t u = more ? (uint32_t)__builtin_ctzll(pend) : t;
+      pend &= pend - 1u;
+      fetch(u);
+      tf_sync();
+      // ---- the filter (record sections at their dense offsets)
+      const uint8_t* S = (const uint8_t*)w.stage;
+      const uint32_t o_key = kHdrBytes + 8u * A, o_dctr = o_key + 8u * nM, o_dact = o_dctr + 8u * nD,
+                     o_mdend = o_dact + 4u * nD;
+      const bool hm = lane < nM, hd = lane < nD;
+      const uint64_t km = hm ? ((const uint64_t*)(S + o_key))[lane] : 0ull;
+      const uint32_t em = hm ? ((const uint32_t*)(S + o_mdend))[lane] : 0u;
+      const uint32_t xd = hd ? ((const uint32_t*)(S + o_dact))[lane] : 0u;
+      const uint64_t vd = hd ? ((const uint64_t*)(S + o_dctr))[lane] : 0ull;
+      const uint64_t tx = lane < A ? ((const uint64_t*)(S + kHdrBytes))[lane] : 0ull;
+      const uint64_t cx = lane < A ? w.ct[lane] : 0ull;
+      const uint64_t cd = hd ? w.ct[xd & (kTA - 1u)] : 0ull;
+      // run ends within [prev end, n_dot] and dot actors < A: else not
+      // canonical here (the general kernel decides)
+      const uint32_t emp = __shfl_up(em, 1);
+      const bool rbad = (hm && (em > nD || (lane > 0u && em < emp) || (lane + 1u == nM && em != nD))) ||
+                        (hd && xd >= A) || (lane == 0u && nM == 0u && nD != 0u);
+      const uint64_t Sv = __ballot(hd && vd > cd);  // surviving dots
+      const uint64_t lt_em = em >= 64u ? ~0ull : (1ull << em) - 1ull;
+      const uint32_t ne = (uint32_t)__popcll(Sv & lt_em);  // survivors before this member's run end
+      const uint32_t nb = __shfl_up(ne, 1);
+      const bool kept = hm && ne > (lane > 0u ? nb : 0u);
+      const uint64_t K = __ballot(kept);
+      const uint32_t n_mem = (uint32_t)__popcll(K), n_dot = (uint32_t)__popcll(Sv);
+      const bool bad = __ballot(cbad || rbad) != 0ull;
+      RecLayout O;
+      rec_layout(O, A, n_mem, n_dot, 0u, 0u, 0u, false);
+      tf_sync();  // every read of the stage is done: the output is assembled over it
+      if (!bad) {
+        uint8_t* W = (uint8_t*)w.stage;
+        if (lane < A) ((uint64_t*)(W + kHdrBytes))[lane] = tx > cx ? tx : 0ull;
+        if (kept) {
+          const uint32_t pm = (uint32_t)__popcll(K & ((1ull << lane) - 1ull));
+          ((uint64_t*)(W + O.o_key))[pm] = km;
+          ((uint32_t*)(W + O.o_mdend))[pm] = ne;
+        }
+        if ((Sv >> lane) & 1ull) {
+          const uint32_t pd = (uint32_t)__popcll(Sv & ((1ull << lane) - 1ull));
+          ((uint64_t*)(W + O.o_dctr))[pd] = vd;
+          ((uint32_t*)(W + O.o_dact))[pd] = xd;
+        }
+        if (lane == 0u && O.o_def != O.o_mpad) *(uint32_t*)(W + O.o_mpad) = 0u;
+        if (lane >= 1u && lane < 4u && O.o_end + 4u * (lane - 1u) < O.size) *(uint32_t*)(W + O.o_end + 4u * (lane - 1u)) = 0u;
+        if (lane < 8u) {
+          const uint32_t hv = lane == 0u ? O.size : lane == 1u ? A : lane == 2u ? n_mem : lane == 3u ? n_dot
+                              : lane == 7u ? g.flags : 0u;
+          ((uint32_t*)W)[lane] = hv;
+        }
+        tf_sync();
+        const uint32_t n16o = O.size / 16u;  // <= the input's pieces: at most 2 per lane
+        const uint32_t i0 = lane < n16o ? lane : n16o - 1u, i1 = lane + kW < n16o ? lane + kW : n16o - 1u;
+        const tu32x4 q0 = w.stage[i0], q1 = w.stage[i1];
+        __builtin_nontemporal_store(q0, (tu32x4*)(g.out + oo) + i0);
+        __builtin_nontemporal_store(q1, (tu32x4*)(g.out + oo) + i1);
+      } else if (lane == 0u) {  // the general kernel takes it (and latches the error)
+        g.out_off[cbase + t] = oo | kTPend;
+      }
+      tf_sync();  // the copy-out's reads of the stage are done
+      if (!more) break;
+      t = u;
+    }
+  }
+}
 }  // namespace
 
 int launch_orswot_truncate(const crdt_orswot_batch& self, const crdt_clock_csr& clocks, uint32_t A, uint32_t flags,
-                           uint8_t* out, uint64_t* out_off, uint64_t out_bytes, int* status, hipStream_t stream) {
+                           uint8_t* out, uint64_t* out_off, uint64_t out_bytes, int* status, uint32_t* ctl,
+                           hipStream_t stream) {
   if (self.n_obj == 0) return CRDT_OK;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  static std::atomic<int> occ{0};
-  int o = occ.load(std::memory_order_relaxed);
-  if (o == 0) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (const void*)orswot_truncate_kernel, kW * kTWaves, 0) !=
-            hipSuccess || o < 1)
-      o = 2;
-    occ.store(o, std::memory_order_relaxed);
-  }
+  // dense batches of <= 32 actors: the fast form first (resident grid, its
+  // ticket counter ctl[3] zeroed), then the general form over the records it
+  // flagged; other batches: the general form over every record
+  const bool fast = (flags & kSparseClock) == 0u && A <= kTA && ctl != nullptr;
+  static std::atomic<int> occ[3];
+  auto occupancy = [&](int k, const void* fn) {
+    int o = occ[k].load(std::memory_order_relaxed);
+    if (o == 0) {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, fn, kW * kTWaves, 0) != hipSuccess || o < 1) o = 2;
+      occ[k].store(o, std::memory_order_relaxed);
+    }
+    return o;
+  };
   const uint64_t want = (self.n_obj + kTWaves - 1) / kTWaves;
-  const uint64_t cap = (uint64_t)cus * (uint64_t)o;
-  const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
   const TruncArgs g{self.base, self.off, (uint64_t)self.bytes, (uint64_t)self.n_obj, clocks.off, clocks.len,
                     clocks.act, clocks.ctr, (uint64_t)clocks.n_entries, A, flags, out, out_off, out_bytes, status};
-  hipLaunchKernelGGL(orswot_truncate_kernel, dim3(blocks), dim3(kW * kTWaves), 0, stream, g);
+  if (fast) {
+    const uint64_t chunks = (self.n_obj + kW - 1) / kW;
+    const uint64_t fwant = (chunks + kTWaves - 1) / kTWaves;
+    const uint64_t fcap = (uint64_t)cus * (uint64_t)occupancy(2, (const void*)orswot_truncate_fast_kernel);
+    if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
+    hipLaunchKernelGGL(orswot_truncate_fast_kernel, dim3((uint32_t)(fwant < fcap ? fwant : fcap)), dim3(kW * kTWaves),
+                       0, stream, g, ctl);
+    if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
+  }
+  const void* fn = fast ? (const void*)orswot_truncate_kernel<true> : (const void*)orswot_truncate_kernel<false>;
+  const uint64_t cap = (uint64_t)cus * (uint64_t)occupancy(fast ? 1 : 0, fn);
+  const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
+  void* args[] = {(void*)&g};
+  if (hipLaunchKernel(fn, dim3(blocks), dim3(kW * kTWaves), args, 0, stream) != hipSuccess) return CRDT_EHIP;
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }
 
