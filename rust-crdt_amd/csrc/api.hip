@@ -229,7 +229,7 @@ int crdt_orswot_truncate(crdt_ctx* ctx, const crdt_orswot_batch* self, const crd
   int rc = set_device(ctx);
   if (rc) return rc;
   return launch_orswot_truncate(*self, *clocks, n_actors, flags, d_out, d_out_off, out_bytes, ctx->d_status,
-                                ctx->d_ctl, S(stream));
+                                ctx->d_ctl, ctx->d_list, ctx->list_cap, S(stream));
 }
 
 int crdt_dense_merge_host(crdt_ctx* ctx, uint64_t* h_self, const uint64_t* h_other, size_t n_obj, uint32_t n_slots) {

@@ -30,7 +30,7 @@ int launch_clock_csr_merge(const crdt_clock_csr* const* self, const crdt_clock_c
 
 int launch_orswot_truncate(const crdt_orswot_batch& self, const crdt_clock_csr& clocks, uint32_t A, uint32_t flags,
                            uint8_t* out, uint64_t* out_off, uint64_t out_bytes, int* status, uint32_t* ctl,
-                           hipStream_t stream);
+                           uint64_t* list, uint32_t list_cap, hipStream_t stream);
 
 int launch_dense_max(uint64_t* self, const uint64_t* other, uint64_t n_words, hipStream_t stream);
 

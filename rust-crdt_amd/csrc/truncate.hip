@@ -720,15 +720,27 @@ __device__ void truncate_lds(const TruncArgs& g, const Rec& R, uint64_t o, uint3
 // cleared when the record is written here.
 constexpr uint64_t kTPend = 1ull << 63;
 template <bool FLAGGED>
-__global__ __launch_bounds__(kW * kTWaves, 4) void orswot_truncate_kernel(TruncArgs g) {
+__global__ __launch_bounds__(kW * kTWaves, 4) void orswot_truncate_kernel(TruncArgs g, const uint32_t* flagged,
+                                                                          const uint64_t* list, uint32_t list_cap) {
+  // FLAGGED: flagged[0] counts the records the fast kernel left (none: done),
+  // listed at list[0, count) unless the count passed list_cap (then every
+  // output offset's flag is scanned)
+  const uint32_t nfl =
+      FLAGGED ? __builtin_amdgcn_readfirstlane(__hip_atomic_load(flagged, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : 0u;
+  if (FLAGGED && nfl == 0u) return;
+  const bool listed = FLAGGED && nfl <= list_cap;
+  const uint64_t n_units = listed ? (uint64_t)nfl : g.n_obj;
   __shared__ TWs ws[kTWaves];
   const uint32_t lane = threadIdx.x & (kW - 1u), wv = threadIdx.x / kW;
   TWs& w = ws[wv];
   const uint64_t wave = (uint64_t)blockIdx.x * kTWaves + wv;
   const uint64_t n_waves = (uint64_t)gridDim.x * kTWaves;
   const bool sparse = (g.flags & kSparseClock) != 0u;
-  for (uint64_t cb = wave * kW; cb < g.n_obj; cb += n_waves * kW) {
-    const uint64_t obj = cb + lane;
+  // listed: one entry per wave at a time (the few listed records spread over
+  // every wave, not 64 to a wave); else 64-record chunks
+  const uint64_t per = listed ? 1u : kW;
+  for (uint64_t cb = wave * per; cb < n_units; cb += n_waves * per) {
+    const uint64_t obj = listed ? (lane == 0u ? list[cb] : g.n_obj) : cb + lane;
     const bool valid = obj < g.n_obj && (!FLAGGED || (g.out_off[obj] & kTPend) != 0ull);
     if (FLAGGED && __ballot(valid) == 0ull) continue;
     uint64_t o = 0, c0 = 0;
@@ -813,37 +825,52 @@ __global__ __launch_bounds__(kW * kTWaves, 4) void orswot_truncate_kernel(TruncA
 
 
 // ---------------------------------------------------------------- fast form
-// The common record — dense top clock over A <= 32 actors, no deferred
-// removes, <= 64 members and <= 64 dots, <= 2 KB, a truncating clock run of
-// <= 64 entries — as a streaming filter, with the join kernel's skeleton
-// (orswot_join5_kernel): a resident grid with the guided split, the chunk's
-// offsets, clock runs and headers in one step (lane = object), the next
-// record and clock run prefetched into registers while the current one is
-// filtered from LDS, the output assembled over the stage and copied out with
-// 16-B stores. Without deferred removes truncate is a filter (src/orswot.rs
-// :159-172 with the empty set's merge :94-104 and VClock::subtract
-// src/vclock.rs:236-242): a dot (x, v) survives iff v > c[x], a member is
-// kept iff one of its dots survives (then it keeps exactly those: never an
-// empty clock), the top clock keeps T[x] iff T[x] > c[x]. Every other record
-// is flagged (kTPend on its output offset) for orswot_truncate_kernel<true>.
+// The common record — dense top clock over A <= 32 actors, <= 64 members, <= 64
+// dots, <= 8 deferred clocks of <= 64 entries and <= 64 named members in
+// total, <= 2 KB, a truncating clock run of <= 64 entries — with the join
+// kernel's skeleton (orswot_join5_kernel): a resident grid with the guided
+// split, the chunk's offsets, clock runs and headers in one step (lane =
+// object), the next record and clock run prefetched into registers while the
+// current one is done from LDS, the output assembled over the stage and
+// copied out with 16-B stores. Lane = dot / member / deferred entry; every
+// per-member and per-clock quantity is a ballot over run masks.
+// Truncate (src/orswot.rs:159-172: merge with the empty set :94-104 +
+// apply_deferred :235-243, then VClock::subtract src/vclock.rs:236-242), with
+// M = max(T, c):
+//  - a dot (x, v) is above iff v > c[x], killed iff a deferred clock naming
+//    its member has D[x] >= v;
+//  - a member is kept iff one of its dots is above and one is not killed; it
+//    keeps its dots that are above and not killed (possibly none: an empty
+//    clock, header flag bit 1, as the reference keeps it);
+//  - a deferred clock is kept (entries and member set unchanged) iff one of
+//    its entries (x, d) has d > M[x];
+//  - the top clock keeps T[x] iff T[x] > c[x].
+// Every other record is flagged (kTPend on its output offset) for
+// orswot_truncate_kernel<true>, which also latches every error.
 constexpr uint32_t kTFStage = 2048;               // record bytes staged per wave
 constexpr uint32_t kTFPer = kTFStage / 16u / kW;  // 16-B pieces per lane
+constexpr uint32_t kTFDef = 8;                    // deferred clocks
 struct TFWs {
   tu32x4 stage[kTFStage / 16];
-  uint64_t ct[kTA];  // the truncating clock, dense
+  uint64_t ct[kTA];            // the truncating clock, dense
+  uint64_t drow[kTFDef][kTA];  // the deferred clocks, dense
+  uint32_t names[kW];          // per member: the deferred clocks naming it
 };
 __device__ __forceinline__ void tf_sync() { tsync(); }
 __device__ __forceinline__ uint64_t lane64(uint64_t v, uint32_t t) {
   return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), t) << 32) |
          (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, t);
 }
+__device__ __forceinline__ uint64_t below_mask(uint32_t n) { return n >= 64u ? ~0ull : (1ull << n) - 1ull; }
 
-__global__ __launch_bounds__(kW * kTWaves, 8) void orswot_truncate_fast_kernel(TruncArgs g, uint32_t* ctl) {
+__global__ __launch_bounds__(kW * kTWaves, 8) void orswot_truncate_fast_kernel(TruncArgs g, uint32_t* ctl,
+                                                                               uint64_t* list, uint32_t list_cap) {
   __shared__ TFWs ws[kTWaves];
   const uint32_t lane = threadIdx.x & (kW - 1u), wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kW);
   TFWs& w = ws[wv];
   const uint64_t wave_id = (uint64_t)blockIdx.x * kTWaves + wv, n_waves = (uint64_t)gridDim.x * kTWaves;
   const uint32_t A = g.A;
+  const uint64_t lt = (1ull << lane) - 1ull;
   GuidedSplit<20u, 5u> gs(g.n_obj, wave_id, n_waves);
   uint64_t cbase, cend;
   while (gs.next(cbase, cend, &ctl[3], lane)) {
@@ -864,17 +891,33 @@ __global__ __launch_bounds__(kW * kTWaves, 8) void orswot_truncate_fast_kernel(T
       h1 = ((const tu32x4*)(g.base + o))[1];
     }
     // the fast form's own verdict (the rest, well-formed or not, is the
-    // general kernel's: it latches the errors)
-    const bool fast = ok && h0.y == A && A <= kTA && h0.z <= kW && h0.w <= kW && h1.x == 0u && h1.y == 0u &&
-                      h1.z == 0u && (h1.w & ~kEmptyClockFlag) == 0u && h0.x <= kTFStage &&
-                      h0.x == (((kHdrBytes + 8u * A + 12u * (h0.z + h0.w)) + 15u) & ~15u) &&
-                      h0.x <= g.bytes - o && o + h0.x <= g.out_bytes && c0 <= g.c_entries &&
-                      cn <= g.c_entries - c0 && cn <= kW;
+    // general kernel's: it latches the errors). A record with empty member
+    // clocks takes it only without deferred removes.
+    const bool lim = h0.y == A && A <= kTA && h0.z <= kW && h0.w <= kW && h1.x <= kTFDef && h1.y <= kW && h1.z <= kW &&
+                     h0.x <= kTFStage && (h1.w == 0u || (h1.w == kEmptyClockFlag && h1.x == 0u));
+    uint32_t want = 0u;
+    if (lim) {
+      RecLayout L;
+      rec_layout(L, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, false);
+      want = L.size;
+    }
+    const bool fast = ok && lim && h0.x == want && h0.x <= g.bytes - o && o + h0.x <= g.out_bytes &&
+                      c0 <= g.c_entries && cn <= g.c_entries - c0 && cn <= kW;
     if (valid) g.out_off[obj] = o | (fast ? 0ull : kTPend);
+    // listed for the general kernel (one atomic per wave)
+    const uint64_t left = __ballot(valid && !fast);
+    if (left != 0ull) {
+      uint32_t base = 0u;
+      if (lane == 0u) base = atomicAdd(&ctl[0], (uint32_t)__popcll(left));
+      base = __builtin_amdgcn_readfirstlane(base);
+      const uint32_t e = base + (uint32_t)__popcll(left & lt);
+      if (valid && !fast && e < list_cap) list[e] = obj;
+    }
     uint64_t pend = __ballot(fast);
     if (pend == 0ull) continue;
     const uint32_t n16 = fast ? h0.x / 16u : 1u;
     const uint32_t nmd = h0.z | (h0.w << 16);
+    const uint32_t nf = h1.x | (h1.y << 8) | (h1.z << 16) | (h1.w << 24);  // (each <= 64; flags <= 2)
     // ---- one record ahead in registers: its pieces and its clock run
     tu32x4 pr[kTFPer];
     uint32_t pa;
@@ -896,13 +939,20 @@ __global__ __launch_bounds__(kW * kTWaves, 8) void orswot_truncate_fast_kernel(T
     pend &= pend - 1u;
     fetch(t);
     for (;;) {
-      // ---- stage the record and the dense clock row (the previous record's
-      // LDS reads are done: its copy-out waited for them)
+      // ---- stage the record, zero the tables (the previous record's LDS
+      // reads are done: its copy-out waited for them)
       const uint32_t n = (uint32_t)__builtin_amdgcn_readlane(n16, t);
 #pragma unroll
       for (uint32_t k = 0; k < kTFPer; ++k)
         if (lane + k * kW < n) w.stage[lane + k * kW] = pr[k];
+      const uint32_t fw = (uint32_t)__builtin_amdgcn_readlane(nf, t);
+      const uint32_t nF = fw & 0xFFu, nFD = (fw >> 8) & 0xFFu, nFM = (fw >> 16) & 0xFFu, iflags = fw >> 24;
       if (lane < kTA) w.ct[lane] = 0ull;
+      if (nF) {
+#pragma unroll
+        for (uint32_t k = 0; k < kTFDef * kTA / kW; ++k) (&w.drow[0][0])[lane + k * kW] = 0ull;
+        w.names[lane] = 0u;
+      }
       const uint32_t ra = pa;
       const uint64_t rc = pc;
       const uint32_t prev = __shfl_up(ra, 1);
@@ -914,58 +964,144 @@ __global__ __launch_bounds__(kW * kTWaves, 8) void orswot_truncate_fast_kernel(T
       const uint64_t oo = lane64(o, t);
       const uint32_t md = (uint32_t)__builtin_amdgcn_readlane(nmd, t);
       const uint32_t nM = md & 0xFFFFu, nD = md >> 16;
-      // the next record's loads, in flight while this one is filtered
+      RecLayout L;
+      rec_layout(L, A, nM, nD, nF, nFD, nFM, false);
+      const uint8_t* S = (const uint8_t*)w.stage;
+      // the deferred clocks into their dense rows; the members they name
+      uint32_t fx = 0u, fk = 0u, gk = 0u;
+      uint64_t fd = 0ull, fm = 0ull;
+      bool dbad = false;
+      if (nF) {
+        const uint32_t* fdend = (const uint32_t*)(S + L.o_fdend);
+        const uint32_t* fmend = (const uint32_t*)(S + L.o_fmend);
+        uint32_t pd = 0u, pm = 0u;
+        for (uint32_t k = 0; k < nF; ++k) {  // clock of entry e: # run ends <= e
+          const uint32_t ed = fdend[k], emk = fmend[k];
+          fk += lane >= ed ? 1u : 0u;
+          gk += lane >= emk ? 1u : 0u;
+          dbad = dbad || ed <= pd || emk <= pm;  // canonical: no empty clock or member set
+          pd = ed;
+          pm = emk;
+        }
+        dbad = dbad || pd != nFD || pm != nFM;
+        if (lane < nFD) {
+          fx = ((const uint32_t*)(S + L.o_fact))[lane];
+          fd = ((const uint64_t*)(S + L.o_fctr))[lane];
+          dbad = dbad || fx >= A || fk >= nF;
+          if (fx < kTA && fk < kTFDef) w.drow[fk][fx] = fd;
+        }
+        if (lane < nFM) {
+          fm = ((const uint64_t*)(S + L.o_fkey))[lane];
+          uint32_t lo = 0, len = nM;  // the named member's index (absent: no member to name)
+          const uint64_t* key = (const uint64_t*)(S + L.o_key);
+          while (len) {
+            const uint32_t h = len >> 1;
+            if (key[lo + h] < fm) { lo += h + 1u; len -= h + 1u; } else { len = h; }
+          }
+          if (lo < nM && key[lo] == fm && gk < kTFDef) atomicOr(&w.names[lo], 1u << gk);
+        }
+      }
+      // the next record's loads, in flight while this one is done
       const bool more = pend != 0ull;
       const uint32_t u = more ? (uint32_t)__builtin_ctzll(pend) : t;
       pend &= pend - 1u;
       fetch(u);
       tf_sync();
-      // ---- the filter (record sections at their dense offsets)
-      const uint8_t* S = (const uint8_t*)w.stage;
-      const uint32_t o_key = kHdrBytes + 8u * A, o_dctr = o_key + 8u * nM, o_dact = o_dctr + 8u * nD,
-                     o_mdend = o_dact + 4u * nD;
+      // ---- members and dots
       const bool hm = lane < nM, hd = lane < nD;
-      const uint64_t km = hm ? ((const uint64_t*)(S + o_key))[lane] : 0ull;
-      const uint32_t em = hm ? ((const uint32_t*)(S + o_mdend))[lane] : 0u;
-      const uint32_t xd = hd ? ((const uint32_t*)(S + o_dact))[lane] : 0u;
-      const uint64_t vd = hd ? ((const uint64_t*)(S + o_dctr))[lane] : 0ull;
+      const uint64_t km = hm ? ((const uint64_t*)(S + L.o_key))[lane] : 0ull;
+      const uint32_t em = hm ? ((const uint32_t*)(S + L.o_mdend))[lane] : 0u;
+      const uint32_t xd = hd ? ((const uint32_t*)(S + L.o_dact))[lane] : 0u;
+      const uint64_t vd = hd ? ((const uint64_t*)(S + L.o_dctr))[lane] : 0ull;
       const uint64_t tx = lane < A ? ((const uint64_t*)(S + kHdrBytes))[lane] : 0ull;
       const uint64_t cx = lane < A ? w.ct[lane] : 0ull;
       const uint64_t cd = hd ? w.ct[xd & (kTA - 1u)] : 0ull;
-      // run ends within [prev end, n_dot] and dot actors < A: else not
-      // canonical here (the general kernel decides)
+      // run ends within [previous end, n_dot], the last one n_dot; strictly
+      // increasing with deferred clocks (no empty clock among the inputs
+      // then); dot actors < A: else not canonical here (the general kernel)
       const uint32_t emp = __shfl_up(em, 1);
-      const bool rbad = (hm && (em > nD || (lane > 0u && em < emp) || (lane + 1u == nM && em != nD))) ||
+      const bool rbad = (hm && (em > nD || (lane > 0u && (nF ? em <= emp : em < emp)) || (lane == 0u && nF && em == 0u) ||
+                                (lane + 1u == nM && em != nD))) ||
                         (hd && xd >= A) || (lane == 0u && nM == 0u && nD != 0u);
-      const uint64_t Sv = __ballot(hd && vd > cd);  // surviving dots
-      const uint64_t lt_em = em >= 64u ? ~0ull : (1ull << em) - 1ull;
-      const uint32_t ne = (uint32_t)__popcll(Sv & lt_em);  // survivors before this member's run end
-      const uint32_t nb = __shfl_up(ne, 1);
-      const bool kept = hm && ne > (lane > 0u ? nb : 0u);
+      // the member of each dot: run starts marked by ds_permute (a start is
+      // the previous member's run end; runs are non-empty here)
+      bool dk = false;
+      if (nF) {
+        const uint32_t h = (uint32_t)__builtin_amdgcn_ds_permute((int)((hm && lane + 1u < nM ? em : 0u) << 2), 1);
+        const uint64_t HD = (__ballot(h != 0u) | 1ull) & below_mask(nD);
+        const uint32_t mem = (uint32_t)__popcll(HD & lt) + (uint32_t)((HD >> lane) & 1ull) - 1u;
+        const uint32_t nm = hd ? w.names[mem & (kW - 1u)] : 0u;
+        for (uint32_t b = nm; b; b &= b - 1u) dk = dk || w.drow[__builtin_ctz(b)][xd & (kTA - 1u)] >= vd;
+      }
+      const uint64_t G = __ballot(hd && vd > cd), NK = __ballot(hd && !dk), F = G & NK;
+      const uint32_t s_m = hm ? (lane ? emp : 0u) : 0u;
+      const uint64_t run = hm ? below_mask(em) & ~below_mask(s_m) : 0ull;
+      const bool kept = (G & run) != 0ull && (NK & run) != 0ull;
+      const uint32_t ne = (uint32_t)__popcll(F & below_mask(em));  // kept dots before this run's end
       const uint64_t K = __ballot(kept);
-      const uint32_t n_mem = (uint32_t)__popcll(K), n_dot = (uint32_t)__popcll(Sv);
-      const bool bad = __ballot(cbad || rbad) != 0ull;
+      const uint32_t n_mem = (uint32_t)__popcll(K), n_dot = (uint32_t)__popcll(F);
+      const bool empty = __ballot(kept && (F & run) == 0ull) != 0ull;
+      // deferred clocks kept: an entry above max(T, c)
+      uint32_t KD = 0u;
+      uint64_t FE = 0ull, ME = 0ull;
+      uint32_t n_fd = 0u, n_fm = 0u;
+      if (nF) {
+        const uint64_t mx = ((const uint64_t*)(S + kHdrBytes))[fx & (kTA - 1u)] > w.ct[fx & (kTA - 1u)]
+                                ? ((const uint64_t*)(S + kHdrBytes))[fx & (kTA - 1u)]
+                                : w.ct[fx & (kTA - 1u)];
+        const uint64_t AB = __ballot(lane < nFD && fd > mx);
+        const uint32_t* fdend = (const uint32_t*)(S + L.o_fdend);
+        for (uint32_t k = 0; k < nF; ++k) {
+          const uint32_t b0 = k ? fdend[k - 1u] : 0u, b1 = fdend[k];
+          KD |= (AB & below_mask(b1) & ~below_mask(b0)) != 0ull ? 1u << k : 0u;
+        }
+        KD = __builtin_amdgcn_readfirstlane(KD);
+        FE = __ballot(lane < nFD && fk < kTFDef && ((KD >> fk) & 1u));
+        ME = __ballot(lane < nFM && gk < kTFDef && ((KD >> gk) & 1u));
+        n_fd = (uint32_t)__popcll(FE);
+        n_fm = (uint32_t)__popcll(ME);
+      }
+      const uint32_t n_def = (uint32_t)__popcll(KD);
+      const bool bad = __ballot(cbad || rbad || dbad) != 0ull;
       RecLayout O;
-      rec_layout(O, A, n_mem, n_dot, 0u, 0u, 0u, false);
+      rec_layout(O, A, n_mem, n_dot, n_def, n_fd, n_fm, false);
+      // the kept clocks' cumulative ends (lane k: clock k)
+      uint32_t oe_d = 0u, oe_m = 0u;
+      if (nF && lane < nF) {
+        oe_d = (uint32_t)__popcll(FE & below_mask(((const uint32_t*)(S + L.o_fdend))[lane]));
+        oe_m = (uint32_t)__popcll(ME & below_mask(((const uint32_t*)(S + L.o_fmend))[lane]));
+      }
       tf_sync();  // every read of the stage is done: the output is assembled over it
       if (!bad) {
         uint8_t* W = (uint8_t*)w.stage;
         if (lane < A) ((uint64_t*)(W + kHdrBytes))[lane] = tx > cx ? tx : 0ull;
         if (kept) {
-          const uint32_t pm = (uint32_t)__popcll(K & ((1ull << lane) - 1ull));
+          const uint32_t pm = (uint32_t)__popcll(K & lt);
           ((uint64_t*)(W + O.o_key))[pm] = km;
           ((uint32_t*)(W + O.o_mdend))[pm] = ne;
         }
-        if ((Sv >> lane) & 1ull) {
-          const uint32_t pd = (uint32_t)__popcll(Sv & ((1ull << lane) - 1ull));
+        if ((F >> lane) & 1ull) {
+          const uint32_t pd = (uint32_t)__popcll(F & lt);
           ((uint64_t*)(W + O.o_dctr))[pd] = vd;
           ((uint32_t*)(W + O.o_dact))[pd] = xd;
+        }
+        if ((FE >> lane) & 1ull) {
+          const uint32_t q = (uint32_t)__popcll(FE & lt);
+          ((uint64_t*)(W + O.o_fctr))[q] = fd;
+          ((uint32_t*)(W + O.o_fact))[q] = fx;
+        }
+        if ((ME >> lane) & 1ull) ((uint64_t*)(W + O.o_fkey))[(uint32_t)__popcll(ME & lt)] = fm;
+        if (lane < nF && ((KD >> lane) & 1u)) {
+          const uint32_t q = (uint32_t)__popcll(KD & (uint32_t)lt);
+          ((uint32_t*)(W + O.o_fdend))[q] = oe_d;
+          ((uint32_t*)(W + O.o_fmend))[q] = oe_m;
         }
         if (lane == 0u && O.o_def != O.o_mpad) *(uint32_t*)(W + O.o_mpad) = 0u;
         if (lane >= 1u && lane < 4u && O.o_end + 4u * (lane - 1u) < O.size) *(uint32_t*)(W + O.o_end + 4u * (lane - 1u)) = 0u;
         if (lane < 8u) {
           const uint32_t hv = lane == 0u ? O.size : lane == 1u ? A : lane == 2u ? n_mem : lane == 3u ? n_dot
-                              : lane == 7u ? g.flags : 0u;
+                              : lane == 4u ? n_def : lane == 5u ? n_fd : lane == 6u ? n_fm
+                              : g.flags | (empty ? kEmptyClockFlag : 0u);
           ((uint32_t*)W)[lane] = hv;
         }
         tf_sync();
@@ -976,18 +1112,22 @@ __global__ __launch_bounds__(kW * kTWaves, 8) void orswot_truncate_fast_kernel(T
         __builtin_nontemporal_store(q1, (tu32x4*)(g.out + oo) + i1);
       } else if (lane == 0u) {  // the general kernel takes it (and latches the error)
         g.out_off[cbase + t] = oo | kTPend;
+        const uint32_t e = atomicAdd(&ctl[0], 1u);
+        if (e < list_cap) list[e] = cbase + t;
       }
+      (void)iflags;
       tf_sync();  // the copy-out's reads of the stage are done
       if (!more) break;
       t = u;
     }
   }
 }
+
 }  // namespace
 
 int launch_orswot_truncate(const crdt_orswot_batch& self, const crdt_clock_csr& clocks, uint32_t A, uint32_t flags,
                            uint8_t* out, uint64_t* out_off, uint64_t out_bytes, int* status, uint32_t* ctl,
-                           hipStream_t stream) {
+                           uint64_t* list, uint32_t list_cap, hipStream_t stream) {
   if (self.n_obj == 0) return CRDT_OK;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1013,13 +1153,15 @@ int launch_orswot_truncate(const crdt_orswot_batch& self, const crdt_clock_csr& 
     const uint64_t fcap = (uint64_t)cus * (uint64_t)occupancy(2, (const void*)orswot_truncate_fast_kernel);
     if (hipMemsetAsync(ctl, 0, 4 * sizeof(uint32_t), stream) != hipSuccess) return CRDT_EHIP;
     hipLaunchKernelGGL(orswot_truncate_fast_kernel, dim3((uint32_t)(fwant < fcap ? fwant : fcap)), dim3(kW * kTWaves),
-                       0, stream, g, ctl);
+                       0, stream, g, ctl, list, list_cap);
     if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
   }
   const void* fn = fast ? (const void*)orswot_truncate_kernel<true> : (const void*)orswot_truncate_kernel<false>;
   const uint64_t cap = (uint64_t)cus * (uint64_t)occupancy(fast ? 1 : 0, fn);
   const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
-  void* args[] = {(void*)&g};
+  const uint32_t* flagged = ctl;
+  const uint64_t* clist = list;
+  void* args[] = {(void*)&g, (void*)&flagged, (void*)&clist, (void*)&list_cap};
   if (hipLaunchKernel(fn, dim3(blocks), dim3(kW * kTWaves), args, 0, stream) != hipSuccess) return CRDT_EHIP;
   return hipGetLastError() == hipSuccess ? CRDT_OK : CRDT_EHIP;
 }

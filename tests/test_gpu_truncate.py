@@ -192,3 +192,26 @@ def test_out_aliasing_the_input_rejected(gpu):
         gpu.orswot_truncate(B, C, out=B)
     assert e.value.code == CRDT_EINVAL
     gpu.orswot_truncate(B, C)  # the context is still usable
+
+
+@pytest.mark.parametrize("A", [8, 16, 32])
+def test_fast_form_with_deferred_clocks(gpu, oracle, A):
+    """The streaming fast form (orswot_truncate_fast_kernel) takes dense
+    records of <= 64 members / dots with up to 8 deferred clocks: deferred
+    clocks that cover member dots (dots killed, members kept with an EMPTY
+    clock), clocks re-deferred or dropped against max(T, c) — mixed in one
+    batch with records past its limits (9-12 deferred clocks, 100+ members)
+    that the general form takes; byte-exact vs the oracle."""
+    shapes = [{"n_def": (1, 2, 3, 8)}, {}, {"n_def": (9, 12)}, {"members": 120}]
+    states, clocks, recs = T.cases(8_000, A=A, seed=61 + A, shapes=shapes)
+    n_def = [len(s[2]) for s in states]
+    assert sum(1 for d in n_def if 1 <= d <= 8) > 2000 and sum(1 for d in n_def if d > 8) > 500
+    lb, lo = records.pack_batch(recs)
+    exp = _check(gpu, oracle, lb, lo, T.clocks_csr(clocks), A)
+    assert sum(1 for r in exp if np.frombuffer(r[28:32], np.uint32)[0] & 2) > 100
+    try:  # the records the fast form leaves reach the general form listed, or (list full) by their flags
+        for cap in (8, 0):
+            gpu.set_list_cap(cap)
+            _check(gpu, oracle, lb, lo, T.clocks_csr(clocks), A)
+    finally:
+        gpu.set_list_cap(65536)
