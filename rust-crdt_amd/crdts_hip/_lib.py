@@ -16,6 +16,10 @@ LIB_PATH = os.path.join(ROOT, "lib", "libcrdts_hip.so")
 # variants, phase stamps, tuning knobs) with CRDTS_HIP_DIAG=1; never the product.
 if os.environ.get("CRDTS_HIP_DIAG") == "1":
     LIB_PATH = os.path.join(ROOT, "lib", "libcrdts_hip_diag.so")
+# A/B builds of a compile-time knob (tools/): CRDTS_HIP_AB=<tag> loads
+# lib/libcrdts_hip_ab_<tag>.so; never the product.
+if os.environ.get("CRDTS_HIP_AB"):
+    LIB_PATH = os.path.join(ROOT, "lib", f"libcrdts_hip_ab_{os.environ['CRDTS_HIP_AB']}.so")
 DIAG_SYMBOLS = {"crdt_ctx_set_blocks_per_cu", "crdt_ctx_set_variant", "crdt_ctx_debug_read"}
 
 CRDT_OK = 0
