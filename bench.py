@@ -66,6 +66,9 @@ def parse():
     p.add_argument("--n-actors", type=int, default=16,
                    help="orswot: dense top-clock actors (config 3: 16; 33-64 take the 64-bit actor-mask join, "
                         "65-1024 the sparse mask join over each object's present actors)")
+    p.add_argument("--gen-params", default=None,
+                   help="orswot: JSON overrides of the op-simulation generator's parameters (crdt_orswot_gen_params), "
+                        "e.g. the wide-union distribution of DESIGN.md §11")
     p.add_argument("--n-obj", type=int, default=None, help="objects per GPU")
     p.add_argument("--threads", type=int, default=16, help="host threads for input generation")
     p.add_argument("--cpu-threads", type=int, default=None,
@@ -248,6 +251,17 @@ def cpu_cores_note():
     return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_quota": cpu_quota()}
 
 
+def gen_params(args, A):
+    """The orswot generator's parameters: config 3's, with --n-actors and
+    --gen-params (JSON) applied; None for config 3 itself."""
+    if A == 16 and not args.gen_params:
+        return None
+    p = {"n_actors": A}
+    if args.gen_params:
+        p.update(json.loads(args.gen_params))
+    return p
+
+
 def run_orswot(args, rank, world, local):
     import numpy as np
     import torch
@@ -269,7 +283,7 @@ def run_orswot(args, rank, world, local):
         (lb, lo), (rb, ro) = crdts_hip.generate_orswot_tail(n, first_obj=first, threads=args.threads)
     else:
         (lb, lo), (rb, ro) = crdts_hip.generate_orswot(n, first_obj=first, threads=args.threads,
-                                                       params=None if A == 16 else {"n_actors": A})
+                                                       params=gen_params(args, A))
     gen_s = time.time() - t0
     eng = crdts_hip.Engine(local)
     L = crdts_hip.OrswotBatch.from_host(lb, lo, A, device=local, flags=flags)
@@ -338,7 +352,8 @@ def run_orswot(args, rank, world, local):
                         (f"orswot_merge config3 shape over {A} dense actors ("
                          + ("64-bit actor-mask join" if A <= 64 else "sparse mask join over the present actors, DN form")
                          + "): "
-                         f"{n} objects/GPU incl. deferred removes"),
+                         f"{n} objects/GPU incl. deferred removes"
+                         + (f", generator {json.loads(args.gen_params)}" if args.gen_params else "")),
             "n_obj_per_gpu": n,
             "n_actors": A,
             "alg_bytes_per_merge": alg_bytes / n,

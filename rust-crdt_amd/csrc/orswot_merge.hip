@@ -3089,6 +3089,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
     const uint32_t ncl = hl0.y | (hr0.y << 16), nm = hl0.z | (hr0.z << 16), nd = hl0.w | (hr0.w << 16);
     const uint64_t defs = __ballot(fast && (hl1.x | hr1.x) != 0u);
     uint32_t t = (uint32_t)__builtin_ctzll(pend);
+    uint64_t fbm = 0ull;  // the chunk's objects the join left (kLeanFallback)
     u32x4 pf[kSpPer];
     uint32_t nn = lane_of(n16, t);
     prefetch_pair(pf, Lb + lane_of64(lo, t), Rb + lane_of64(ro, t), nn & 0xFFFFu, nn >> 16, lane);
@@ -3117,11 +3118,15 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
       else
         r = sparse_mask_object<false, ABL, SASM && !DN, DN>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu,
                                                             d & 0xFFFFu, c >> 16, m >> 16, d >> 16, lane, &st);
-      if (ABL != 9 && r == kLeanFallback && lane == 0u) {  // union clock / members > 64 or a foreign dot actor
-        Ooff[cbase + t] |= kPending;
-        const uint32_t e = atomicAdd(&ctl[0], 1u);
-        if (e < list_cap) list[e] = cbase + t;
-      }
+      fbm |= r == kLeanFallback ? 1ull << t : 0ull;  // union clock / members > 64 or a foreign dot actor
+    }
+    // the chunk's fallbacks to the general kernel: flagged and listed with
+    // one atomic (a per-object atomic on one address serialises: the wide
+    // dense distribution lists nearly every object)
+    if (ABL != 9 && fbm != 0ull) {
+      const bool fb = (fbm >> lane) & 1ull;
+      if (fb) Ooff[obj] = (lo + ro) | kPending;
+      list_append(fb, obj, &ctl[0], list, list_cap, lane);
     }
   }
   if (ABL == 9 && lane < 16u) {  // per-wave phase sums -> the context's list buffer

@@ -504,6 +504,31 @@ def test_dense_wide_actors(gpu, oracle, A, n, anc):
     _compare(out, ob, oo, f"A={A}")
 
 
+WIDE_UNION = {"n_actors": 128, "ancestor_adds": 96, "member_universe": 32, "pct_add": 45, "max_div_ops": 20}
+
+
+def test_dense_wide_union(gpu, oracle):
+    """The wide-union distribution (bench.py --n-actors 128 --gen-params of
+    DESIGN.md §11): 128 dense actors with ~72 present per object pair — the
+    union of present actors passes 64 for ~98 % of the objects, with <= 64
+    members and ~80 dots per side — so nearly every object leaves the DN
+    mask join; byte-exact against the oracle, both orientations."""
+    import crdts_hip
+
+    (lb, lo), (rb, ro) = crdts_hip.generate_orswot(30_000, threads=16, seed=0xC0FFEE80, params=WIDE_UNION)
+    A = WIDE_UNION["n_actors"]
+    q = lb.view(np.uint64)
+    idx = (lo // 8 + 4).astype(np.int64)[:, None] + np.arange(A)[None, :]
+    qr = rb.view(np.uint64)
+    idr = (ro // 8 + 4).astype(np.int64)[:, None] + np.arange(A)[None, :]
+    union = ((q[idx] != 0) | (qr[idr] != 0)).sum(1)
+    assert (union > 64).mean() > 0.9
+    for a, b in (((lb, lo), (rb, ro)), ((rb, ro), (lb, lo))):
+        out = _gpu_merge(gpu, *a, *b, A)
+        ob, oo = oracle.orswot_merge_batch(*a, *b, A, threads=16)
+        _compare(out, ob, oo, "wide union")
+
+
 # ------------------------------------------------------------------ heavy-tailed batches
 def test_heavy_tail_100k(gpu, oracle):
     """Config 3 with a heavy tail (bench.py --workload orswot_tail): every 20th
