@@ -2085,6 +2085,296 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   return size / 16u;
 }
 
+// ======================================================================
+// Wide dense join: sparse_mask_object's DN form for objects whose union of
+// present actors holds 65..128 actors (the DN mask kernel leaves them; its
+// masks are 64-bit). Actor masks are 128-bit, two words (word b >> 6, bit
+// b & 63); an actor's rank is read from the union bitmap's prefix table (a
+// dense dot actor is in the union iff its bitmap bit is set, so no actor
+// table), and the other side's counter at a dot's actor from its dense row.
+// Same rules as mask_object (src/orswot.rs:94-138; apply_deferred
+// :235-243 -> apply_remove :195-211); members <= 64 per side and in the
+// union, dots <= 128 per side, deferred clocks <= 32 per side.
+// ======================================================================
+// scratch byte offsets (per wave; fits the sparse join's kSpScratch, so the
+// DN mask kernel runs it on its own scratch): member masks {M, F} x 128 bit
+// per member; the per-union-member {keep, useK, d0} (48 B) over them once
+// they are read, the deferred walk's survivor cache after it; the union
+// bitmap's prefix table over the equal / >= masks until the dots have their
+// ranks; run heads as bits (2 words per side); u16 union descriptors; an
+// 8-byte trash slot per lane for masked-off stores
+constexpr uint32_t kWdMsL = 0, kWdMsR = 2048, kWdOut = 0, kWdCache = 3072, kWdEq = 4096, kWdUpre = kWdEq,
+                   kWdDesc = 6144, kWdHeads = 6272, kWdUofI = 6304, kWdUofJ = 6368, kWdTrash = 6432;
+constexpr uint32_t kWdScratch = kWdTrash + 8u * kWave;  // 6 944 B per wave
+static_assert(kWdScratch <= kSpScratch, "the DN mask kernel's scratch holds the wide join's");
+constexpr uint32_t kWdOutStride = 48;
+
+__device__ __forceinline__ bool bit128(uint64_t lo, uint64_t hi, uint32_t b) {
+  return ((b < 64u ? lo : hi) >> (b & 63u)) & 1ull;
+}
+// # of set bits of the 128-bit mask below bit b (b < 128)
+__device__ __forceinline__ uint32_t below128(uint64_t lo, uint64_t hi, uint32_t b) {
+  return b < 64u ? below64(lo, b) : (uint32_t)__popcll(lo) + below64(hi, b - 64u);
+}
+__device__ __forceinline__ uint64_t ldm64(const uint8_t* X, uint32_t off) { return *(const uint64_t*)(X + off); }
+// bits [0, n) of a word (n as a signed count: <= 0 -> none, >= 64 -> all)
+__device__ __forceinline__ uint64_t lowmask64(uint32_t n) {
+  return (int32_t)n <= 0 ? 0ull : n >= 64u ? ~0ull : (1ull << n) - 1ull;
+}
+
+template <bool HD>
+__device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* X, uint8_t* O,
+                                                     uint32_t A, uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR,
+                                                     uint32_t lane) {
+  const uint32_t keyL = kHdrBytes + 8u * A, keyR = keyL;
+  const uint32_t ctrL = keyL + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
+  const uint32_t ctrR = keyR + 8u * nR, actR = ctrR + 8u * dR, endR = actR + 4u * dR;
+  const uint32_t tr = kWdTrash + 8u * lane;
+
+  // ---- union of present actors (a dense clock stores 0 for an absent
+  // actor, src/vclock.rs:159-163): lane q keeps bitmap word q (actors 64 q ..)
+  uint64_t bw = 0ull;
+  for (uint32_t q = 0; q < (A + 63u) / 64u; ++q) {
+    const uint32_t a = 64u * q + lane;
+    const bool p = a < A && (ld64(Ls, kHdrBytes + 8u * a) | ld64(Rs, kHdrBytes + 8u * a)) != 0ull;
+    const uint64_t w = __ballot(p);
+    bw = lane == q ? w : bw;
+  }
+  const uint32_t bpc = (uint32_t)__popcll(bw), bin = scan_incl(bpc);
+  const uint32_t Uc = lane_of(bin, kSpTableN / 64u - 1u);
+  if (Uc > 2u * kWave) return kLeanFallback;
+
+  // ---- members (as mask_object); dots in rounds of 64 (<= 128 per side)
+  const bool hml = lane < nL, hmr = lane < nR;
+  const uint32_t nrnd = (dL > dR ? dL : dR) > 64u ? 2u : 1u;
+  const uint64_t kl = ld64(Ls, keyL + 8u * lane), kr = ld64(Rs, keyR + 8u * lane);
+  uint32_t rl = 0, rr = 0;
+  {
+    const uint32_t n = nL > nR ? nL : nR;
+    for (uint32_t step = n ? 1u << (31u - __builtin_clz(n)) : 0u; step != 0u; step >>= 1) {
+      const uint32_t cl = rl + step, cr = rr + step;
+      const uint64_t kcl = ld64(Rs, keyR + 8u * (cl - 1u)), kcr = ld64(Ls, keyL + 8u * (cr - 1u));
+      rl = (cl <= nR && kcl < kl) ? cl : rl;
+      rr = (cr <= nL && kcr < kr) ? cr : rr;
+    }
+  }
+  const bool eql = hml && rl < nR && ld64(Rs, keyR + 8u * rl) == kl;
+  const bool eqr = hmr && rr < nL && ld64(Ls, keyL + 8u * rr) == kr;
+  const uint64_t EL = __ballot(eql), ER = __ballot(eqr);
+  const uint32_t U = nL + nR - (uint32_t)__popcll(EL);
+  if (U > (uint32_t)kWave) return kLeanFallback;
+  const uint32_t ul = lane + rl - mbcnt64(EL), ur = lane + rr - mbcnt64(ER);
+
+  wave_sync();  // the previous object's readers of this scratch are done
+  if (lane < kSpTableN / 64u)
+    *(u32x4*)(X + kWdUpre + 16u * lane) = u32x4{(uint32_t)bw, (uint32_t)(bw >> 32), bin - bpc, 0u};
+  const u32x4 z4{0u, 0u, 0u, 0u};
+  *(u32x4*)(X + kWdMsL + 32u * lane) = z4;
+  *(u32x4*)(X + kWdMsL + 32u * lane + 16u) = z4;
+  *(u32x4*)(X + kWdMsR + 32u * lane) = z4;
+  *(u32x4*)(X + kWdMsR + 32u * lane + 16u) = z4;
+  if (lane < 4u) *(uint64_t*)(X + kWdHeads + 8u * lane) = 0ull;
+  const uint32_t el0 = ld32(Ls, endL + 4u * lane - 4u), er0 = ld32(Rs, endR + 4u * lane - 4u);
+  const uint32_t sl = lane ? el0 : 0u, sr = lane ? er0 : 0u;
+  *(uint16_t*)(X + (hml ? kWdDesc + 2u * (ul & 63u) : tr)) =
+      (uint16_t)(((eql ? kBoth : kSelf) << 12) | (lane << 6) | (eql ? rl : 0u));
+  *(uint16_t*)(X + ((hmr && !eqr) ? kWdDesc + 2u * (ur & 63u) : tr)) = (uint16_t)((kOther << 12) | ((rr & 63u) << 6) | lane);
+  X[kWdUofI + lane] = (uint8_t)ul;
+  X[kWdUofJ + lane] = (uint8_t)ur;
+  wave_sync();
+  // run heads as bits: dot words 0 / 1 of each side (members' first dots)
+  atomicOr((unsigned long long*)(X + ((hml && sl < 128u) ? kWdHeads + 8u * (sl >> 6) : tr)), 1ull << (sl & 63u));
+  atomicOr((unsigned long long*)(X + ((hmr && sr < 128u) ? kWdHeads + 16u + 8u * (sr >> 6) : tr)), 1ull << (sr & 63u));
+  wave_sync();
+  // run-head masks of both rounds; the member of dot 64 r + lane is
+  // (#heads at or below it) - 1
+  const uint64_t HL0 = ldm64(X, kWdHeads) & lowmask64(dL), HL1 = ldm64(X, kWdHeads + 8u) & lowmask64(dL - 64u);
+  const uint64_t HR0 = ldm64(X, kWdHeads + 16u) & lowmask64(dR), HR1 = ldm64(X, kWdHeads + 24u) & lowmask64(dR - 64u);
+  bool foreign = false;
+  uint32_t rXL[2] = {0u, 0u}, rXR[2] = {0u, 0u}, rBL[2] = {0u, 0u}, rBR[2] = {0u, 0u};
+  uint32_t rML[2] = {0u, 0u}, rMR[2] = {0u, 0u};
+  uint64_t rVL[2] = {0ull, 0ull}, rVR[2] = {0ull, 0ull};
+#pragma unroll
+  for (uint32_t rd = 0; rd < 2u; ++rd) {  // dot -> union rank (its bitmap bit checked) -> member masks
+    if (rd >= nrnd) break;
+    const uint32_t d = 64u * rd + lane;
+    const bool hdl = d < dL, hdr = d < dR;
+    const uint32_t xl = ld32(Ls, actL + 4u * d), xr = ld32(Rs, actR + 4u * d);
+    const uint64_t vl = ld64(Ls, ctrL + 8u * d), vr = ld64(Rs, ctrR + 8u * d);
+    const uint64_t HL = rd ? HL1 : HL0, HR = rd ? HR1 : HR0;
+    const uint32_t ml = (rd ? (uint32_t)__popcll(HL0) : 0u) + mbcnt64(HL) + ((HL >> lane) & 1ull ? 1u : 0u) - 1u;
+    const uint32_t mr = (rd ? (uint32_t)__popcll(HR0) : 0u) + mbcnt64(HR) + ((HR >> lane) & 1ull ? 1u : 0u) - 1u;
+    const uint32_t xlc = xl < A ? xl : 0u, xrc = xr < A ? xr : 0u;
+    const u32x4 pwl = *(const u32x4*)(X + kWdUpre + 16u * (xlc >> 6)), pwr = *(const u32x4*)(X + kWdUpre + 16u * (xrc >> 6));
+    const uint64_t bwl = ((uint64_t)pwl.y << 32) | pwl.x, bwr = ((uint64_t)pwr.y << 32) | pwr.x;
+    const uint32_t bl = (pwl.z + below64(bwl, xlc & 63u)) & 127u, br = (pwr.z + below64(bwr, xrc & 63u)) & 127u;
+    rXL[rd] = xl; rXR[rd] = xr; rVL[rd] = vl; rVR[rd] = vr; rBL[rd] = bl; rBR[rd] = br; rML[rd] = ml; rMR[rd] = mr;
+    foreign = foreign || (hdl && (xl >= A || ((bwl >> (xlc & 63u)) & 1ull) == 0ull)) ||
+              (hdr && (xr >= A || ((bwr >> (xrc & 63u)) & 1ull) == 0ull));
+    const uint64_t rc = ld64(Rs, kHdrBytes + 8u * xlc), lc = ld64(Ls, kHdrBytes + 8u * xrc);
+    const uint64_t mbl = hdl ? 1ull << (bl & 63u) : 0ull, mbr = hdr ? 1ull << (br & 63u) : 0ull;
+    const uint32_t ol = kWdMsL + 32u * (ml & 63u) + 8u * (bl >> 6), orr = kWdMsR + 32u * (mr & 63u) + 8u * (br >> 6);
+    atomicOr((unsigned long long*)(X + (hdl ? ol : tr)), (unsigned long long)mbl);
+    atomicOr((unsigned long long*)(X + (hdl ? ol + 16u : tr)), (unsigned long long)(vl > rc ? mbl : 0ull));
+    atomicOr((unsigned long long*)(X + (hdr ? orr : tr)), (unsigned long long)mbr);
+    atomicOr((unsigned long long*)(X + (hdr ? orr + 16u : tr)), (unsigned long long)(vr > lc ? mbr : 0ull));
+  }
+  if (__ballot(foreign) != 0ull) return kLeanFallback;  // a dot actor absent from both top clocks
+  wave_sync();  // every dot has its rank: the prefix table's words are free
+  *(u32x4*)(X + kWdEq + 32u * lane) = z4;
+  *(u32x4*)(X + kWdEq + 32u * lane + 16u) = z4;
+  wave_sync();
+#pragma unroll
+  for (uint32_t rd = 0; rd < 2u; ++rd) {  // actors on both sides of a shared member: equal / self >= other
+    if (rd >= nrnd) break;
+    const bool hdr = 64u * rd + lane < dR;
+    const uint64_t vr = rVR[rd];
+    const uint32_t br = rBR[rd], mr = rMR[rd];
+    const uint32_t u = X[kWdUofJ + (mr & 63u)] & 63u;
+    const uint32_t d = *(const uint16_t*)(X + kWdDesc + 2u * u);
+    const uint32_t i = (d >> 6) & 63u;
+    const uint64_t mlo = ldm64(X, kWdMsL + 32u * i), mhi = ldm64(X, kWdMsL + 32u * i + 8u);
+    const bool sh = hdr && (d >> 12) == kBoth && bit128(mlo, mhi, br);
+    const uint32_t a0 = i ? ld32(Ls, endL + 4u * i - 4u) : 0u;
+    const uint64_t va = ld64(Ls, ctrL + 8u * ((a0 + below128(mlo, mhi, br)) & 127u));
+    const uint32_t oe = kWdEq + 32u * u + 8u * (br >> 6);
+    const uint64_t bb = 1ull << (br & 63u);
+    atomicOr((unsigned long long*)(X + (sh ? oe : tr)), (unsigned long long)(sh && va == vr ? bb : 0ull));
+    atomicOr((unsigned long long*)(X + (sh ? oe + 16u : tr)), (unsigned long long)(sh && va >= vr ? bb : 0ull));
+  }
+  wave_sync();
+  // ---- per union member: mask join (src/orswot.rs:94-138), word by word
+  const bool hu = lane < U;
+  const uint32_t dsc = hu ? *(const uint16_t*)(X + kWdDesc + 2u * lane) : 0u;
+  const uint32_t ty = dsc >> 12, mi = (dsc >> 6) & 63u, mj = dsc & 63u;
+  const bool self_only = ty == kSelf;
+  uint64_t keep[2], useK[2], lpf = 0ull;
+#pragma unroll
+  for (uint32_t w = 0; w < 2u; ++w) {
+    const uint64_t ML = (ty & kSelf) ? ldm64(X, kWdMsL + 32u * mi + 8u * w) : 0ull;
+    const uint64_t FL = (ty & kSelf) ? ldm64(X, kWdMsL + 32u * mi + 16u + 8u * w) : 0ull;
+    const uint64_t MR = (ty & kOther) ? ldm64(X, kWdMsR + 32u * mj + 8u * w) : 0ull;
+    const uint64_t FR = (ty & kOther) ? ldm64(X, kWdMsR + 32u * mj + 16u + 8u * w) : 0ull;
+    const uint64_t EQ = ty == kBoth ? ldm64(X, kWdEq + 32u * lane + 8u * w) : 0ull;
+    const uint64_t GE = ty == kBoth ? ldm64(X, kWdEq + 32u * lane + 16u + 8u * w) : 0ull;
+    const uint64_t lp = self_only ? ML : (ML & FL), rp = MR & FR;
+    const uint64_t useA = (ML & MR & EQ) | (lp & (~rp | GE));
+    keep[w] = useA | rp;
+    useK[w] = useA;
+    lpf |= ML & FL;
+  }
+#pragma unroll
+  for (uint32_t w = 0; w < 2u; ++w) {
+    keep[w] = (!hu || (self_only && lpf == 0ull)) ? 0ull : keep[w];
+    useK[w] &= keep[w];
+  }
+  SideL DL{(lds_cu8*)(size_t)lds_addr(Ls), RV{}}, DR{(lds_cu8*)(size_t)lds_addr(Rs), RV{}};  // LDS stages: ds_* reads
+  if (HD) {  // deferred removes (apply_deferred -> apply_remove, src/orswot.rs:235-243, 195-211)
+    DL.v = make_rv(layout_at(Ls));
+    DR.v = make_rv(layout_at(Rs));
+    wave_sync();
+    uint64_t* ow = (uint64_t*)(X + kWdOut + kWdOutStride * lane);
+    ow[0] = keep[0]; ow[1] = keep[1]; ow[2] = useK[0]; ow[3] = useK[1];
+    wave_sync();
+#pragma unroll
+    for (uint32_t rd = 0; rd < 2u; ++rd) {
+      if (rd >= nrnd) break;
+      const uint32_t d = 64u * rd + lane;
+      const bool hdl = d < dL, hdr = d < dR;
+      const uint32_t bl = rBL[rd], br = rBR[rd], ml = rML[rd], mr = rMR[rd];
+      if (hdl) {
+        unsigned long long* ok = (unsigned long long*)(X + kWdOut + kWdOutStride * X[kWdUofI + (ml & 63u)]);
+        if (bit128(ok[2], ok[3], bl)) {
+          const uint64_t mk = dmask_of(DL, DR, ld64(Ls, keyL + 8u * (ml & 63u)));
+          if (mk && dkilled(DL, DR, mk, rXL[rd], rVL[rd])) atomicAnd(ok + (bl >> 6), ~(1ull << (bl & 63u)));
+        }
+      }
+      if (hdr) {
+        unsigned long long* ok = (unsigned long long*)(X + kWdOut + kWdOutStride * X[kWdUofJ + (mr & 63u)]);
+        if (bit128(ok[0] & ~ok[2], ok[1] & ~ok[3], br)) {
+          const uint64_t mk = dmask_of(DL, DR, ld64(Rs, keyR + 8u * (mr & 63u)));
+          if (mk && dkilled(DL, DR, mk, rXR[rd], rVR[rd])) atomicAnd(ok + (br >> 6), ~(1ull << (br & 63u)));
+        }
+      }
+    }
+    wave_sync();
+    keep[0] = ow[0];
+    keep[1] = ow[1];
+    useK[0] &= keep[0];
+    useK[1] &= keep[1];
+  }
+  const uint32_t c = (uint32_t)__popcll(keep[0]) + (uint32_t)__popcll(keep[1]);
+  // ---- output layout (dense top clock of A entries)
+  const uint64_t keepm = __ballot(c != 0u);
+  const uint32_t tot_mem = (uint32_t)__popcll(keepm);
+  const uint32_t cincl = scan_incl(c);
+  const uint32_t tot_dot = lane_of(cincl, kWave - 1);
+  uint32_t nd = 0, ndd = 0, ndm = 0;
+  // survivors cached past the {keep, useK, d0} rows (64 entries)
+  uint32_t* dcache = (uint32_t*)(X + kWdCache);
+  if (HD) deferred_pass_wave<false>(DL, DR, A, lane, nd, ndd, ndm, nullptr, dcache);
+  RecLayout OL;
+  rec_layout(OL, A, tot_mem, tot_dot, nd, ndd, ndm, false);
+  const uint32_t size = OL.size;
+  const uint32_t d0 = cincl - c;
+  wave_sync();
+  {
+    uint64_t* ow = (uint64_t*)(X + kWdOut + kWdOutStride * lane);
+    ow[0] = keep[0]; ow[1] = keep[1]; ow[2] = useK[0]; ow[3] = useK[1];
+    *(uint32_t*)(ow + 4) = d0;
+  }
+  if (c != 0u) {
+    const uint32_t midx = mbcnt64(keepm);
+    const uint64_t kk = (ty & kSelf) ? ld64(Ls, keyL + 8u * mi) : ld64(Rs, keyR + 8u * mj);
+    *(uint64_t*)(O + OL.o_key + 8u * midx) = kk;
+    *(uint32_t*)(O + OL.o_mdend + 4u * midx) = d0 + c;
+  }
+  for (uint32_t a = lane; a < A; a += kWave) {  // top clock: dense, pointwise max of the rows (src/orswot.rs:153)
+    const uint64_t l = ld64(Ls, kHdrBytes + 8u * a), r = ld64(Rs, kHdrBytes + 8u * a);
+    *(uint64_t*)(O + kHdrBytes + 8u * a) = l > r ? l : r;
+  }
+  wave_sync();
+  uint32_t* oact = (uint32_t*)(O + OL.o_dact);
+  uint64_t* octr = (uint64_t*)(O + OL.o_dctr);
+#pragma unroll
+  for (uint32_t rd = 0; rd < 2u; ++rd) {  // every kept dot at its member's base + actor rank
+    if (rd >= nrnd) break;
+    const uint32_t d = 64u * rd + lane;
+    const bool hdl = d < dL, hdr = d < dR;
+    const uint32_t bl = rBL[rd], br = rBR[rd], ml = rML[rd], mr = rMR[rd];
+    if (hdl) {
+      const uint64_t* ob = (const uint64_t*)(X + kWdOut + kWdOutStride * X[kWdUofI + (ml & 63u)]);
+      if (bit128(ob[2], ob[3], bl)) {
+        const uint32_t idx = *(const uint32_t*)(ob + 4) + below128(ob[0], ob[1], bl);
+        oact[idx] = rXL[rd];
+        octr[idx] = rVL[rd];
+      }
+    }
+    if (hdr) {
+      const uint64_t* ob = (const uint64_t*)(X + kWdOut + kWdOutStride * X[kWdUofJ + (mr & 63u)]);
+      if (bit128(ob[0] & ~ob[2], ob[1] & ~ob[3], br)) {
+        const uint32_t idx = *(const uint32_t*)(ob + 4) + below128(ob[0], ob[1], br);
+        oact[idx] = rXR[rd];
+        octr[idx] = rVR[rd];
+      }
+    }
+  }
+  if (HD) {
+    DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
+             (uint32_t*)(O + OL.o_fdend), (uint32_t*)(O + OL.o_fmend)};
+    wave_sync();
+    deferred_pass_wave<false>(DL, DR, A, lane, nd, ndd, ndm, &w, dcache, nd);
+  }
+  if (lane == 0u && OL.o_def != OL.o_mpad) *(uint32_t*)(O + OL.o_mpad) = 0u;
+  if (lane >= 1u && lane < 4u && OL.o_end + 4u * (lane - 1u) < size) *(uint32_t*)(O + OL.o_end + 4u * (lane - 1u)) = 0u;
+  if (lane == 0u) {
+    u32x4* h = (u32x4*)O;
+    h[0] = u32x4{size, A, tot_mem, tot_dot};
+    h[1] = u32x4{nd, ndd, ndm, 0u};
+  }
+  return size / 16u;
+}
+
 // Copy an output record from its LDS stage to HBM: 16-B coalesced,
 // non-temporal stores (the output is not re-read by this kernel).
 __device__ __forceinline__ void copy_out(const u32x4* src, uint8_t* dst, uint32_t n16, uint32_t lane) {
@@ -2415,6 +2705,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_join5_ker
 // A listed object's offsets and headers, loaded ahead of its join.
 struct GenPre {
   uint64_t o, oo;
+  bool pend;  // still flagged (orswot_dense_wide_kernel clears the objects it joins)
   const uint8_t* lr;
   const uint8_t* rr;
   u32x4 hl0, hl1, hr0, hr1;
@@ -2423,7 +2714,9 @@ struct GenPre {
 __device__ __forceinline__ void gen_pre(GenPre& g, const uint8_t* Lb, const uint64_t* Loff, const uint8_t* Rb,
                                         const uint64_t* Roff, const uint64_t* Ooff, uint64_t o) {
   g.o = o;
-  g.oo = Ooff[o] & ~kPending;
+  const uint64_t f = Ooff[o];
+  g.oo = f & ~kPending;
+  g.pend = (f & kPending) != 0ull;
   g.lr = Lb + Loff[o];
   g.rr = Rb + Roff[o];
   g.hl0 = ((const u32x4*)g.lr)[0];
@@ -2444,6 +2737,10 @@ __device__ __forceinline__ bool general_one(const GenPre& g, uint8_t* Ob, uint64
   const uint8_t* rr = g.rr;
   const u32x4 hl0 = g.hl0, hl1 = g.hl1, hr0 = g.hr0, hr1 = g.hr1;
   const uint32_t szl = uni(hl0.x), szr = uni(hr0.x);
+  if (!uni((uint32_t)g.pend)) {  // listed, then joined by orswot_dense_wide_kernel
+    mid();
+    return false;
+  }
   if (is_big(u32x4{szl, 0u, uni(hl0.z), 0u}, u32x4{szr, 0u, uni(hr0.z), 0u})) {  // orswot_big_kernel's
     mid();
     return true;
@@ -3011,19 +3308,21 @@ __device__ __forceinline__ bool sparse_header_ok(u32x4 h0, u32x4 h1, uint64_t of
 constexpr uint32_t kSpPair = 6144;
 constexpr uint32_t kSpPer = kSpPair / 16 / kWave;
 
-__device__ __forceinline__ void prefetch_pair(u32x4 (&r)[kSpPer], const uint8_t* L, const uint8_t* R, uint32_t nl,
+template <uint32_t PER = kSpPer>
+__device__ __forceinline__ void prefetch_pair(u32x4 (&r)[PER], const uint8_t* L, const uint8_t* R, uint32_t nl,
                                               uint32_t nr, uint32_t lane) {
 #pragma unroll
-  for (uint32_t k = 0; k < kSpPer; ++k) {
+  for (uint32_t k = 0; k < PER; ++k) {
     const uint32_t idx = lane + k * kWave;
     const uint32_t j = idx - nl < nr ? idx - nl : nr - 1u;
     r[k] = __builtin_nontemporal_load(idx < nl ? (const u32x4*)L + idx : (const u32x4*)R + j);
   }
 }
 
-__device__ __forceinline__ void stage_pair(u32x4* dst, const u32x4 (&r)[kSpPer], uint32_t lane) {
+template <uint32_t PER = kSpPer>
+__device__ __forceinline__ void stage_pair(u32x4* dst, const u32x4 (&r)[PER], uint32_t lane) {
 #pragma unroll
-  for (uint32_t k = 0; k < kSpPer; ++k) dst[lane + k * kWave] = r[k];
+  for (uint32_t k = 0; k < PER; ++k) dst[lane + k * kWave] = r[k];
 }
 
 // DN: dense batches of 65..1024 actors (sparse_mask_object's DN form; the
@@ -3118,6 +3417,11 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
       else
         r = sparse_mask_object<false, ABL, SASM && !DN, DN>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu,
                                                             d & 0xFFFFu, c >> 16, m >> 16, d >> 16, lane, &st);
+      if (DN && r == kLeanFallback)  // a union of 65..128 present actors: the 128-bit form on the same stage
+        r = (defs >> t) & 1ull ? wide_mask_object<true>(Ls, Rs, X, Ob + oo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16,
+                                                        d >> 16, lane)
+                               : wide_mask_object<false>(Ls, Rs, X, Ob + oo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16,
+                                                         d >> 16, lane);
       fbm |= r == kLeanFallback ? 1ull << t : 0ull;  // union clock / members > 64 or a foreign dot actor
     }
     // the chunk's fallbacks to the general kernel: flagged and listed with
@@ -3134,6 +3438,82 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
 #pragma unroll
     for (int q = 0; q < 16; ++q) v = lane == (uint32_t)q ? st.acc[q] : v;
     list[wave_id * 16u + lane] = v;
+  }
+}
+
+// Wide dense kernel (dense batches of 65..1024 actors, after the DN mask
+// kernel): the objects it left flagged whose pair fits the pair stage with
+// <= 64 members, <= 128 dots and <= 32 deferred clocks per side are joined by
+// wide_mask_object (union of present actors <= 128) and their flag cleared;
+// the rest stay flagged for the general kernel (which skips a listed object
+// whose flag is clear). The flags are scanned 64 objects per chunk, the next
+// candidate's pair in flight in registers during a join; the kernel returns
+// at once when the DN kernel listed nothing.
+constexpr uint32_t kWdWaves = 2;
+constexpr uint32_t kWdPair = 16384, kWdPer = kWdPair / 16 / kWave;  // pairs the DN kernel's 6 KB stage cannot take
+constexpr int kWdMinW = 1;  // (LDS: 23.3 KB per wave, three 2-wave blocks per CU)
+template <int MINW>
+__global__ __launch_bounds__(kWave * kWdWaves, MINW) void orswot_dense_wide_kernel(
+    const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, const uint8_t* __restrict__ Rb,
+    const uint64_t* __restrict__ Roff, uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t n_obj,
+    uint32_t A, const uint32_t* __restrict__ ctl) {
+  __shared__ u32x4 pair_s[kWdWaves][kWdPair / 16];
+  __shared__ u32x4 scr_s[kWdWaves][kWdScratch / 16];
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t wave = threadIdx.x / kWave;
+  u32x4* const S = pair_s[wave];
+  uint8_t* const X = (uint8_t*)scr_s[wave];
+  if (uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) return;
+  const uint64_t wave_id = (uint64_t)blockIdx.x * kWdWaves + wave;
+  const uint64_t n_waves = (uint64_t)gridDim.x * kWdWaves;
+  const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
+  for (uint64_t chunk = wave_id; chunk < n_chunks; chunk += n_waves) {
+    const uint64_t obj = chunk * kWave + lane;
+    const bool pending = obj < n_obj && (Ooff[obj] & kPending) != 0ull;
+    if (__ballot(pending) == 0ull) continue;
+    uint64_t lo = 0, ro = 0;
+    u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
+    if (pending) {  // (the DN kernel flags only objects whose headers it checked)
+      lo = Loff[obj];
+      ro = Roff[obj];
+      hl0 = ((const u32x4*)(Lb + lo))[0]; hl1 = ((const u32x4*)(Lb + lo))[1];
+      hr0 = ((const u32x4*)(Rb + ro))[0]; hr1 = ((const u32x4*)(Rb + ro))[1];
+    }
+    const bool cand = pending && hl0.x + hr0.x <= kWdPair && hl0.z <= 64u && hr0.z <= 64u && hl0.w <= 128u &&
+                      hr0.w <= 128u && hl1.x <= 32u && hr1.x <= 32u;
+    uint64_t pend = __ballot(cand);
+    if (pend == 0ull) continue;
+    const uint32_t n16 = cand ? (hl0.x / 16u) | ((hr0.x / 16u) << 16) : 0u;
+    const uint32_t nm = hl0.z | (hr0.z << 16), nd = hl0.w | (hr0.w << 16);
+    const uint64_t defs = __ballot(cand && (hl1.x | hr1.x) != 0u);
+    uint64_t donem = 0ull;
+    u32x4 pf[kWdPer];
+    uint32_t t = (uint32_t)__builtin_ctzll(pend);
+    uint32_t nn = lane_of(n16, t);
+    prefetch_pair<kWdPer>(pf, Lb + lane_of64(lo, t), Rb + lane_of64(ro, t), nn & 0xFFFFu, nn >> 16, lane);
+    while (pend) {
+      t = (uint32_t)__builtin_ctzll(pend);
+      pend &= pend - 1;
+      nn = lane_of(n16, t);
+      wave_sync();  // previous object's LDS reads are done
+      stage_pair<kWdPer>(S, pf, lane);
+      wave_sync();
+      const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
+      const uint32_t m = lane_of(nm, t), d = lane_of(nd, t);
+      if (pend) {
+        const uint32_t u = (uint32_t)__builtin_ctzll(pend);
+        const uint32_t nu = lane_of(n16, u);
+        prefetch_pair<kWdPer>(pf, Lb + lane_of64(lo, u), Rb + lane_of64(ro, u), nu & 0xFFFFu, nu >> 16, lane);
+      }
+      const uint8_t* Ls = (const uint8_t*)S;
+      const uint8_t* Rs = Ls + 16u * (nn & 0xFFFFu);
+      const uint32_t r = (defs >> t) & 1ull
+                             ? wide_mask_object<true>(Ls, Rs, X, Ob + oo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane)
+                             : wide_mask_object<false>(Ls, Rs, X, Ob + oo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16,
+                                                       lane);
+      donem |= r != kLeanFallback ? 1ull << t : 0ull;
+    }
+    if ((donem >> lane) & 1ull) Ooff[obj] = lo + ro;  // joined: the flag cleared (one coalesced store)
   }
 }
 
@@ -3256,7 +3636,7 @@ __global__ __launch_bounds__(kWave) void orswot_sparse_general_kernel(
 namespace {
 // The ring join launch (orswot_ring_kernel, then the general kernel), with
 // launch_join_passes' alternating control-word sets (no memset before it).
-template <const void* (*KF)()>
+template <const void* (*KF)(), bool WIDE = false>
 int launch_join_kernel(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes, const uint8_t* Rb,
                        const uint64_t* Roff, uint64_t Rbytes, uint8_t* Ob, uint64_t* Ooff, uint64_t Obytes,
                        uint64_t n_obj, uint32_t n_actors, int* status, uint32_t* ctl, uint64_t* list, uint32_t list_cap,
@@ -3283,6 +3663,22 @@ int launch_join_kernel(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
                   &set, &list, &list_cap};
   if (hipLaunchKernel(fn, dim3(blocks), dim3(kWave * kWavesPerBlock), args, 0, stream) != hipSuccess)
     return CRDT_EHIP;
+  if (WIDE) {  // dense-wide: unions of 65..128 present actors before the general kernel
+    const void* wf = (const void*)orswot_dense_wide_kernel<kWdMinW>;
+    static std::atomic<int> wocc_cache{0};
+    int wocc = wocc_cache.load(std::memory_order_relaxed);
+    if (wocc == 0) {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&wocc, wf, kWave * kWdWaves, 0) != hipSuccess || wocc < 1)
+        wocc = 2;
+      wocc_cache.store(wocc, std::memory_order_relaxed);
+    }
+    const uint64_t wwant = ((n_obj + kWave - 1) / kWave + kWdWaves - 1) / kWdWaves;
+    const uint64_t wcap = (uint64_t)cus * wocc;
+    const uint32_t wblocks = (uint32_t)(wwant < wcap ? wwant : wcap);
+    const uint32_t* cset = set;
+    void* wargs[] = {&Lb, &Loff, &Rb, &Roff, &Ob, &Ooff, &n_obj, &n_actors, &cset};
+    if (hipLaunchKernel(wf, dim3(wblocks), dim3(kWave * kWdWaves), wargs, 0, stream) != hipSuccess) return CRDT_EHIP;
+  }
   hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff, Ob,
                      Ooff, n_obj, n_actors, set, list, list_cap, other);
   if (hipGetLastError() != hipSuccess) return CRDT_EHIP;
@@ -3299,7 +3695,7 @@ constexpr auto launch_join5 = launch_join_kernel<join5_fn<MINW, AW, FL>>;
 // dense top clocks of 65..1024 actors: the sparse mask join over the
 // per-object union of present actors (DN), then the dense general kernel
 const void* dense_wide_fn() { return (const void*)orswot_sparse_mask_kernel<3, 0, 16, 5, false, true>; }
-constexpr auto launch_dense_wide = launch_join_kernel<dense_wide_fn>;
+constexpr auto launch_dense_wide = launch_join_kernel<dense_wide_fn, true>;
 }  // namespace
 #ifdef CRDT_DIAG
 #include "diag/orswot_variants_diag.inc"  // the diagnostic variant table

@@ -7,8 +7,11 @@ export TMPDIR=/tmp
 OUT=gpurun_out/wide_${1:-a}
 mkdir -p $OUT
 GP='{"ancestor_adds": 96, "member_universe": 32, "pct_add": 45, "max_div_ops": 20}'
-timeout -k 10 300 python bench.py --n-actors 128 --gen-params "$GP" ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err || { echo BENCH_FAILED; tail -20 $OUT/bench.err; exit 1; }
-python3 -c "import json; d=json.loads(open('$OUT/bench.json').read().strip().split(chr(10))[-1]); print('wide', round(d['value']/1e6,2), round(d['ms_per_step'],4), d['roofline']['frac'])"
+# AB="tag1 tag2": also time lib/libcrdts_hip_ab_<tag>.so (CRDTS_HIP_AB) on the same box
+for tag in "" ${AB:-}; do
+  timeout -k 10 300 env CRDTS_HIP_AB=$tag python bench.py --n-actors 128 --gen-params "$GP" ${BENCH_ARGS:-} > $OUT/bench$tag.json 2> $OUT/bench$tag.err || { echo BENCH_FAILED $tag; tail -20 $OUT/bench$tag.err; exit 1; }
+  python3 -c "import json; d=json.loads(open('$OUT/bench$tag.json').read().strip().split(chr(10))[-1]); print('wide${tag:+ ab }$tag', round(d['value']/1e6,2), round(d['ms_per_step'],4), d['roofline']['frac'])"
+done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --n-actors 128 --gen-params "$GP" --no-cpu-baseline --steps 5 --warmup 2 > $OUT/prof.log 2>&1 || { echo PROF_FAILED; exit 1; }
 python3 -c "
 import csv, re
