@@ -3446,9 +3446,10 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
 // <= 64 members, <= 128 dots and <= 32 deferred clocks per side are joined by
 // wide_mask_object (union of present actors <= 128) and their flag cleared;
 // the rest stay flagged for the general kernel (which skips a listed object
-// whose flag is clear). The flags are scanned 64 objects per chunk, the next
-// candidate's pair in flight in registers during a join; the kernel returns
-// at once when the DN kernel listed nothing.
+// whose flag is clear). The DN kernel's list is dealt in chunks of up to 64
+// entries per wave (past its capacity: every object's flag is scanned, 64
+// objects per chunk), the next candidate's pair in flight in registers during
+// a join; the kernel returns at once when the DN kernel listed nothing.
 constexpr uint32_t kWdWaves = 2;
 constexpr uint32_t kWdPair = 16384, kWdPer = kWdPair / 16 / kWave;  // pairs the DN kernel's 6 KB stage cannot take
 constexpr int kWdMinW = 1;  // (LDS: 23.3 KB per wave, three 2-wave blocks per CU)
@@ -3456,20 +3457,26 @@ template <int MINW>
 __global__ __launch_bounds__(kWave * kWdWaves, MINW) void orswot_dense_wide_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, const uint8_t* __restrict__ Rb,
     const uint64_t* __restrict__ Roff, uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t n_obj,
-    uint32_t A, const uint32_t* __restrict__ ctl) {
+    uint32_t A, const uint32_t* __restrict__ ctl, const uint64_t* __restrict__ list, uint32_t list_cap) {
   __shared__ u32x4 pair_s[kWdWaves][kWdPair / 16];
   __shared__ u32x4 scr_s[kWdWaves][kWdScratch / 16];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wave = threadIdx.x / kWave;
   u32x4* const S = pair_s[wave];
   uint8_t* const X = (uint8_t*)scr_s[wave];
-  if (uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) return;
+  const uint32_t n = uni(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (n == 0u) return;
+  const bool listed = n <= list_cap;
   const uint64_t wave_id = (uint64_t)blockIdx.x * kWdWaves + wave;
   const uint64_t n_waves = (uint64_t)gridDim.x * kWdWaves;
-  const uint64_t n_chunks = (n_obj + kWave - 1) / kWave;
+  // listed: chunks of `per` list entries (the list spread over every wave)
+  const uint64_t per = listed ? (n + n_waves - 1) / n_waves < kWave ? (n + n_waves - 1) / n_waves : kWave : kWave;
+  const uint64_t n_chunks = ((listed ? n : n_obj) + per - 1) / per;
   for (uint64_t chunk = wave_id; chunk < n_chunks; chunk += n_waves) {
-    const uint64_t obj = chunk * kWave + lane;
-    const bool pending = obj < n_obj && (Ooff[obj] & kPending) != 0ull;
+    const uint64_t e = chunk * per + lane;
+    const bool in = lane < per && e < (listed ? (uint64_t)n : n_obj);
+    const uint64_t obj = !in ? 0ull : listed ? list[e] : e;
+    const bool pending = in && (Ooff[obj] & kPending) != 0ull;
     if (__ballot(pending) == 0ull) continue;
     uint64_t lo = 0, ro = 0;
     u32x4 hl0 = {0, 0, 0, 0}, hl1 = hl0, hr0 = hl0, hr1 = hl0;
@@ -3665,6 +3672,7 @@ int launch_join_kernel(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
     return CRDT_EHIP;
   if (WIDE) {  // dense-wide: unions of 65..128 present actors before the general kernel
     const void* wf = (const void*)orswot_dense_wide_kernel<kWdMinW>;
+    const uint64_t* wlist = list;
     static std::atomic<int> wocc_cache{0};
     int wocc = wocc_cache.load(std::memory_order_relaxed);
     if (wocc == 0) {
@@ -3676,7 +3684,7 @@ int launch_join_kernel(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes,
     const uint64_t wcap = (uint64_t)cus * wocc;
     const uint32_t wblocks = (uint32_t)(wwant < wcap ? wwant : wcap);
     const uint32_t* cset = set;
-    void* wargs[] = {&Lb, &Loff, &Rb, &Roff, &Ob, &Ooff, &n_obj, &n_actors, &cset};
+    void* wargs[] = {&Lb, &Loff, &Rb, &Roff, &Ob, &Ooff, &n_obj, &n_actors, &cset, &wlist, &list_cap};
     if (hipLaunchKernel(wf, dim3(wblocks), dim3(kWave * kWdWaves), wargs, 0, stream) != hipSuccess) return CRDT_EHIP;
   }
   hipLaunchKernelGGL(orswot_merge_general_kernel, dim3(kGenBlocks), dim3(kWave), 0, stream, Lb, Loff, Rb, Roff, Ob,

@@ -527,6 +527,16 @@ def test_dense_wide_union(gpu, oracle):
         out = _gpu_merge(gpu, *a, *b, A)
         ob, oo = oracle.orswot_merge_batch(*a, *b, A, threads=16)
         _compare(out, ob, oo, "wide union")
+    # orswot_dense_wide_kernel (pairs past the DN kernel's 6 KB stage, ~5 %)
+    # from the DN kernel's list, and from the flags when the list overflows
+    # (cap 8: halves of 4) or is absent (0)
+    ob, oo = oracle.orswot_merge_batch(lb, lo, rb, ro, A, threads=16)
+    try:
+        for cap in (8, 0):
+            gpu.set_list_cap(cap)
+            _compare(_gpu_merge(gpu, lb, lo, rb, ro, A), ob, oo, f"wide union, cap {cap}")
+    finally:
+        gpu.set_list_cap(65536)
 
 
 # ------------------------------------------------------------------ heavy-tailed batches

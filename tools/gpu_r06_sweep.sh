@@ -17,6 +17,9 @@ if [ "$PART" = bench ]; then
   done
   timeout -k 10 300 python bench.py --n-actors 64 > $OUT/bench_orswot_a64.json 2> $OUT/bench_orswot_a64.err || { echo BENCH_FAILED a64; exit 1; }
   timeout -k 10 300 python bench.py --n-actors 128 > $OUT/bench_orswot_a128.json 2> $OUT/bench_orswot_a128.err || { echo BENCH_FAILED a128; exit 1; }
+  timeout -k 10 300 python bench.py --n-actors 128 --gen-params '{"ancestor_adds": 96, "member_universe": 32, "pct_add": 45, "max_div_ops": 20}' > $OUT/bench_orswot_wide.json 2> $OUT/bench_orswot_wide.err || { echo BENCH_FAILED wide; exit 1; }
+  python3 -c "import json; d=json.loads(open('$OUT/bench_orswot_wide.json').read().strip().split(chr(10))[-1]); print('wide', round(d['value']/1e6,2), round(d['ms_per_step'],4), d['roofline']['frac'])"
+  python3 -c "import json; d=json.loads(open('$OUT/bench_orswot_a128.json').read().strip().split(chr(10))[-1]); print('a128', round(d['value']/1e6,2), round(d['ms_per_step'],4), d['roofline']['frac'])"
   timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $OUT/bench_orswot_w5.json 2> $OUT/bench_orswot_w5.err || { echo BENCH_FAILED w5; exit 1; }
   cut -c1-400 $OUT/bench_orswot_w5.json
   timeout -k 10 300 python bench.py --gpus 2 --rehearse --n-obj 200000 --ae-n-obj 100000 --steps 3 --warmup 1 > $OUT/bench_rehearse2.json 2> $OUT/bench_rehearse2.err || { echo REHEARSE_FAILED; tail -20 $OUT/bench_rehearse2.err; exit 1; }
