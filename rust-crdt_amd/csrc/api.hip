@@ -275,7 +275,7 @@ int crdt_orswot_merge_ex(crdt_ctx* ctx, const crdt_orswot_batch* self, const crd
     return launch_orswot_merge_sparse(self->base, self->off, self->bytes, other->base, other->off, other->bytes,
                                       d_out_base, d_out_off, out_bytes, self->n_obj, n_actors, ctx->d_status,
                                       ctx->d_ctl, ctx->d_list, ctx->list_cap, S(stream),
-                                      ctx->variant >= 201 && ctx->variant <= 213 ? ctx->variant - 200 : 0,
+                                      ctx->variant >= 201 && ctx->variant <= 211 ? ctx->variant - 200 : 0,
                                       &ctx->join_seq);
   return launch_orswot_merge(self->base, self->off, self->bytes, other->base, other->off,
                              other->bytes, d_out_base, d_out_off, out_bytes, self->n_obj, n_actors,

@@ -1728,20 +1728,7 @@ constexpr uint32_t kSpMsL = 0, kSpMsR = 1024, kSpOut = 0, kSpEq = 2048, kSpDesc 
 // (zeroed only after the union positions are read)
 constexpr uint32_t kSpUbm = kSpEq, kSpUpre = kSpEq + 256u;
 constexpr uint32_t kSpScratch = kSpTable + kSpTableN;  // 7 040 B per wave
-// LN: the lean CSR layout (5 120 B) of the 4-waves/SIMD config-5 kernel: no
-// actor table (an actor's rank is the union bitmap's bits below it, read from
-// the prefix table, which stays in the equal / >= mask words until the dots
-// have their ranks), run heads as bits there too, u16 descriptors, an 8-B
-// trash slot per lane; the deferred walk's cache over the mask words after
-// the join
-constexpr uint32_t kLnMsR = 1024, kLnEq = 2048, kLnDesc = 3072, kLnUofI = 3200, kLnUofJ = 3264, kLnUcAct = 3328,
-                   kLnUcL = 3584, kLnUcR = 4096, kLnTrash = 4608;
-constexpr uint32_t kSpScratchLn = kLnTrash + 8u * kWave;  // 5 120 B per wave
 
-// bits [0, n) of a word (n as a signed count: <= 0 -> none, >= 64 -> all)
-__device__ __forceinline__ uint64_t lowmask64(uint32_t n) {
-  return (int32_t)n <= 0 ? 0ull : n >= 64u ? ~0ull : (1ull << n) - 1ull;
-}
 __device__ __forceinline__ uint32_t below64(uint64_t mask, uint32_t b) {
   return (uint32_t)__popcll(mask & ((1ull << b) - 1ull));
 }
@@ -1767,25 +1754,17 @@ __device__ __forceinline__ uint32_t rank32(const uint8_t* b, uint32_t off, uint3
 // stores 0 for an absent actor, src/vclock.rs:159-163), built from the rows
 // 64 actors per round; the joined top clock is written dense (pointwise max
 // of the rows, src/orswot.rs:153) and the record keeps the dense form.
-template <bool HD, int ABL = 0, bool ASM = false, bool DN = false, bool LN = false>
+template <bool HD, int ABL = 0, bool ASM = false, bool DN = false>
 __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* X, uint8_t* O,
                                                        uint32_t A, uint32_t ncL, uint32_t nL, uint32_t dL,
                                                        uint32_t ncR, uint32_t nR, uint32_t dR, uint32_t lane,
                                                        Stamps* st = nullptr) {
   static_assert(!(DN && ASM), "DN: direct stores");
-  static_assert(!(LN && DN), "LN: CSR top clocks");
-  // scratch offsets: the 7 040-B layout, or LN's 5 120 B (kSpScratchLn)
-  constexpr uint32_t oMsL = kSpMsL, oMsR = LN ? kLnMsR : kSpMsR, oOut = kSpOut, oEq = LN ? kLnEq : kSpEq;
-  constexpr uint32_t oDesc = LN ? kLnDesc : kSpDesc, oHeadL = kSpHeadL, oHeadR = kSpHeadR;
-  constexpr uint32_t oUofI = LN ? kLnUofI : kSpUofI, oUofJ = LN ? kLnUofJ : kSpUofJ, oUcAct = LN ? kLnUcAct : kSpUcAct;
-  constexpr uint32_t oUcL = LN ? kLnUcL : kSpUcL, oUcR = LN ? kLnUcR : kSpUcR, oTrash = LN ? kLnTrash : kSpTrash;
-  constexpr uint32_t oTable = kSpTable, oUbm = LN ? kLnEq : kSpUbm, oUpre = LN ? kLnEq + 256u : kSpUpre;
-  constexpr uint32_t oHeads = kLnEq + 640u;  // (LN)
   const uint32_t keyL = kHdrBytes + clock_bytes(ncL, !DN), keyR = kHdrBytes + clock_bytes(ncR, !DN);
   const uint32_t caL = kHdrBytes + 8u * ncL, caR = kHdrBytes + 8u * ncR;  // clock actor lists (CSR)
   const uint32_t ctrL = keyL + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
   const uint32_t ctrR = keyR + 8u * nR, actR = ctrR + 8u * dR, endR = actR + 4u * dR;
-  const uint32_t tr = oTrash + (LN ? 8u : 16u) * lane;
+  const uint32_t tr = kSpTrash + 16u * lane;
 
   // ---- union of the two top clocks: an actor's union position is the
   // number of union-bitmap bits below it (both sides agree on a common actor)
@@ -1795,30 +1774,30 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   if (!DN && __ballot((hcl && cxl >= kSpTableN) || (hcr && cxr >= kSpTableN)) != 0ull) return kLeanFallback;
   wave_sync();  // the previous object's readers of this scratch are done
   if (DN) {  // one bitmap word per 64 actors: lane a of round q <-> actor 64 q + a (words past A stay 0)
-    if (lane < kSpTableN / 64u) *(uint64_t*)(X + oUbm + 8u * lane) = 0ull;
+    if (lane < kSpTableN / 64u) *(uint64_t*)(X + kSpUbm + 8u * lane) = 0ull;
     for (uint32_t q = 0; q < (A + 63u) / 64u; ++q) {
       const uint32_t a = 64u * q + lane;
       const bool p = a < A && (ld64(Ls, kHdrBytes + 8u * a) | ld64(Rs, kHdrBytes + 8u * a)) != 0ull;
       const uint64_t w = __ballot(p);
-      if (lane == 0u) *(uint64_t*)(X + oUbm + 8u * q) = w;
+      if (lane == 0u) *(uint64_t*)(X + kSpUbm + 8u * q) = w;
     }
   } else {
-    if (lane < kSpTableN / 64u) *(uint64_t*)(X + oUbm + 8u * lane) = 0ull;
-    atomicOr((unsigned long long*)(X + (hcl ? oUbm + 8u * (cxl >> 6) : tr)), 1ull << (cxl & 63u));
-    atomicOr((unsigned long long*)(X + (hcr ? oUbm + 8u * (cxr >> 6) : tr)), 1ull << (cxr & 63u));
+    if (lane < kSpTableN / 64u) *(uint64_t*)(X + kSpUbm + 8u * lane) = 0ull;
+    atomicOr((unsigned long long*)(X + (hcl ? kSpUbm + 8u * (cxl >> 6) : tr)), 1ull << (cxl & 63u));
+    atomicOr((unsigned long long*)(X + (hcr ? kSpUbm + 8u * (cxr >> 6) : tr)), 1ull << (cxr & 63u));
   }
   wave_sync();
-  const uint64_t bw = lane < kSpTableN / 64u ? *(const uint64_t*)(X + oUbm + 8u * lane) : 0ull;
+  const uint64_t bw = lane < kSpTableN / 64u ? *(const uint64_t*)(X + kSpUbm + 8u * lane) : 0ull;
   const uint32_t bpc = (uint32_t)__popcll(bw), bin = scan_incl(bpc);
   const uint32_t Uc = lane_of(bin, kSpTableN / 64u - 1u);
   if (Uc > (uint32_t)kWave) return kLeanFallback;
   if (lane < kSpTableN / 64u)
-    *(u32x4*)(X + oUpre + 16u * lane) = u32x4{(uint32_t)bw, (uint32_t)(bw >> 32), bin - bpc, 0u};
-  *(uint64_t*)(X + oUcL + 8u * lane) = 0ull;
-  *(uint64_t*)(X + oUcR + 8u * lane) = 0ull;
+    *(u32x4*)(X + kSpUpre + 16u * lane) = u32x4{(uint32_t)bw, (uint32_t)(bw >> 32), bin - bpc, 0u};
+  *(uint64_t*)(X + kSpUcL + 8u * lane) = 0ull;
+  *(uint64_t*)(X + kSpUcR + 8u * lane) = 0ull;
   wave_sync();
-  const u32x4 pwl = *(const u32x4*)(X + oUpre + 16u * (cxl >> 6 & 15u));
-  const u32x4 pwr = *(const u32x4*)(X + oUpre + 16u * (cxr >> 6 & 15u));
+  const u32x4 pwl = *(const u32x4*)(X + kSpUpre + 16u * (cxl >> 6 & 15u));
+  const u32x4 pwr = *(const u32x4*)(X + kSpUpre + 16u * (cxr >> 6 & 15u));
   const uint32_t ucl = pwl.z + below64(((uint64_t)pwl.y << 32) | pwl.x, cxl & 63u);
   const uint32_t ucr = pwr.z + below64(((uint64_t)pwr.y << 32) | pwr.x, cxr & 63u);
   if (ABL == 9) mark<ABL>(*st, 2);
@@ -1850,61 +1829,46 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     for (uint32_t q = 0; q < (A + 63u) / 64u; ++q) {
       const uint32_t a = 64u * q + lane;
       const uint64_t l = a < A ? ld64(Ls, kHdrBytes + 8u * a) : 0ull, r = a < A ? ld64(Rs, kHdrBytes + 8u * a) : 0ull;
-      const u32x4 pw = *(const u32x4*)(X + oUpre + 16u * q);
+      const u32x4 pw = *(const u32x4*)(X + kSpUpre + 16u * q);
       const uint32_t u = pw.z + below64(((uint64_t)pw.y << 32) | pw.x, lane);
       const bool p = (l | r) != 0ull;
-      *(uint32_t*)(X + (p ? oUcAct + 4u * (u & 63u) : tr)) = a;
-      *(uint64_t*)(X + (p ? oUcL + 8u * (u & 63u) : tr)) = l;
-      *(uint64_t*)(X + (p ? oUcR + 8u * (u & 63u) : tr)) = r;
-      X[p ? oTable + a : tr] = (uint8_t)u;
+      *(uint32_t*)(X + (p ? kSpUcAct + 4u * (u & 63u) : tr)) = a;
+      *(uint64_t*)(X + (p ? kSpUcL + 8u * (u & 63u) : tr)) = l;
+      *(uint64_t*)(X + (p ? kSpUcR + 8u * (u & 63u) : tr)) = r;
+      X[p ? kSpTable + a : tr] = (uint8_t)u;
     }
   } else {
-    *(uint32_t*)(X + (hcl ? oUcAct + 4u * (ucl & 63u) : tr)) = cxl;
-    *(uint64_t*)(X + (hcl ? oUcL + 8u * (ucl & 63u) : tr)) = cvl;
-    if (!LN) X[hcl ? oTable + cxl : tr] = (uint8_t)ucl;
-    *(uint32_t*)(X + (hcr ? oUcAct + 4u * (ucr & 63u) : tr)) = cxr;
-    *(uint64_t*)(X + (hcr ? oUcR + 8u * (ucr & 63u) : tr)) = cvr;
-    if (!LN) X[hcr ? oTable + cxr : tr] = (uint8_t)ucr;
+    *(uint32_t*)(X + (hcl ? kSpUcAct + 4u * (ucl & 63u) : tr)) = cxl;
+    *(uint64_t*)(X + (hcl ? kSpUcL + 8u * (ucl & 63u) : tr)) = cvl;
+    X[hcl ? kSpTable + cxl : tr] = (uint8_t)ucl;
+    *(uint32_t*)(X + (hcr ? kSpUcAct + 4u * (ucr & 63u) : tr)) = cxr;
+    *(uint64_t*)(X + (hcr ? kSpUcR + 8u * (ucr & 63u) : tr)) = cvr;
+    X[hcr ? kSpTable + cxr : tr] = (uint8_t)ucr;
   }
   // member masks (zeroed), run heads, descriptors
-  *(u32x4*)(X + oMsL + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
-  *(u32x4*)(X + oMsR + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
+  *(u32x4*)(X + kSpMsL + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
+  *(u32x4*)(X + kSpMsR + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
+  *(u32x4*)(X + kSpEq + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
+  X[kSpHeadL + lane] = 0u;
+  X[kSpHeadL + 64u + lane] = 0u;
+  X[kSpHeadR + lane] = 0u;
+  X[kSpHeadR + 64u + lane] = 0u;
   const uint32_t el0 = ld32(Ls, endL + 4u * lane - 4u), er0 = ld32(Rs, endR + 4u * lane - 4u);
   const uint32_t sl = lane ? el0 : 0u, sr = lane ? er0 : 0u;
-  if (LN) {  // the equal / >= masks are zeroed once the dots have their ranks (the prefix table is there)
-    if (lane < 4u) *(uint64_t*)(X + oHeads + 8u * lane) = 0ull;
-    *(uint16_t*)(X + (hml ? oDesc + 2u * (ul & 63u) : tr)) =
-        (uint16_t)(((eql ? kBoth : kSelf) << 12) | (lane << 6) | (eql ? rl : 0u));
-    *(uint16_t*)(X + ((hmr && !eqr) ? oDesc + 2u * (ur & 63u) : tr)) = (uint16_t)((kOther << 12) | ((rr & 63u) << 6) | lane);
-  } else {
-    *(u32x4*)(X + oEq + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
-    X[oHeadL + lane] = 0u;
-    X[oHeadL + 64u + lane] = 0u;
-    X[oHeadR + lane] = 0u;
-    X[oHeadR + 64u + lane] = 0u;
-    X[(hml && sl < 128u) ? oHeadL + sl : tr] = 1u;
-    X[(hmr && sr < 128u) ? oHeadR + sr : tr] = 1u;
-    *(uint32_t*)(X + (hml ? oDesc + 4u * (ul & 63u) : tr)) = ((eql ? kBoth : kSelf) << 16) | (lane << 8) | (eql ? rl : 0u);
-    *(uint32_t*)(X + ((hmr && !eqr) ? oDesc + 4u * (ur & 63u) : tr)) = (kOther << 16) | (rr << 8) | lane;
-  }
-  X[oUofI + lane] = (uint8_t)ul;
-  X[oUofJ + lane] = (uint8_t)ur;
-  if (LN) {  // run heads as bits: dot words 0 / 1 of each side
-    wave_sync();
-    atomicOr((unsigned long long*)(X + ((hml && sl < 128u) ? oHeads + 8u * (sl >> 6) : tr)), 1ull << (sl & 63u));
-    atomicOr((unsigned long long*)(X + ((hmr && sr < 128u) ? oHeads + 16u + 8u * (sr >> 6) : tr)), 1ull << (sr & 63u));
-  }
+  X[(hml && sl < 128u) ? kSpHeadL + sl : tr] = 1u;
+  X[(hmr && sr < 128u) ? kSpHeadR + sr : tr] = 1u;
+  *(uint32_t*)(X + (hml ? kSpDesc + 4u * (ul & 63u) : tr)) = ((eql ? kBoth : kSelf) << 16) | (lane << 8) | (eql ? rl : 0u);
+  *(uint32_t*)(X + ((hmr && !eqr) ? kSpDesc + 4u * (ur & 63u) : tr)) = (kOther << 16) | (rr << 8) | lane;
+  X[kSpUofI + lane] = (uint8_t)ul;
+  X[kSpUofJ + lane] = (uint8_t)ur;
   wave_sync();
   if (ABL == 9) mark<ABL>(*st, 3);
   // run-head masks of both rounds; the member of dot 64r + lane is
   // (#heads at or below it) - 1
-  const uint64_t HL0 = LN ? *(const uint64_t*)(X + oHeads) & lowmask64(dL) : __ballot(lane < dL && X[oHeadL + lane] != 0u);
-  const uint64_t HL1 = LN ? *(const uint64_t*)(X + oHeads + 8u) & lowmask64(dL - 64u)
-                          : __ballot(64u + lane < dL && X[oHeadL + 64u + lane] != 0u);
-  const uint64_t HR0 = LN ? *(const uint64_t*)(X + oHeads + 16u) & lowmask64(dR)
-                          : __ballot(lane < dR && X[oHeadR + lane] != 0u);
-  const uint64_t HR1 = LN ? *(const uint64_t*)(X + oHeads + 24u) & lowmask64(dR - 64u)
-                          : __ballot(64u + lane < dR && X[oHeadR + 64u + lane] != 0u);
+  const uint64_t HL0 = __ballot(lane < dL && X[kSpHeadL + lane] != 0u);
+  const uint64_t HL1 = __ballot(64u + lane < dL && X[kSpHeadL + 64u + lane] != 0u);
+  const uint64_t HR0 = __ballot(lane < dR && X[kSpHeadR + lane] != 0u);
+  const uint64_t HR1 = __ballot(64u + lane < dR && X[kSpHeadR + 64u + lane] != 0u);
   bool foreign = false;
   // each dot's actor, counter, union-clock bit and member, per round, kept in
   // registers for the later passes (two rounds at most)
@@ -1921,37 +1885,21 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     const uint64_t HL = rd ? HL1 : HL0, HR = rd ? HR1 : HR0;
     const uint32_t ml = (rd ? (uint32_t)__popcll(HL0) : 0u) + mbcnt64(HL) + ((HL >> lane) & 1ull ? 1u : 0u) - 1u;
     const uint32_t mr = (rd ? (uint32_t)__popcll(HR0) : 0u) + mbcnt64(HR) + ((HR >> lane) & 1ull ? 1u : 0u) - 1u;
-    uint32_t bl, br;
-    if (LN) {  // rank = the union bitmap's bits below the actor; in the union iff its bit is set
-      const u32x4 pwl = *(const u32x4*)(X + oUpre + 16u * ((xl >> 6) & 15u));
-      const u32x4 pwr = *(const u32x4*)(X + oUpre + 16u * ((xr >> 6) & 15u));
-      const uint64_t bwl = ((uint64_t)pwl.y << 32) | pwl.x, bwr = ((uint64_t)pwr.y << 32) | pwr.x;
-      bl = (pwl.z + below64(bwl, xl & 63u)) & 63u;
-      br = (pwr.z + below64(bwr, xr & 63u)) & 63u;
-      foreign = foreign || (hdl && (xl >= kSpTableN || ((bwl >> (xl & 63u)) & 1ull) == 0ull)) ||
-                (hdr && (xr >= kSpTableN || ((bwr >> (xr & 63u)) & 1ull) == 0ull));
-    } else {
-      bl = X[oTable + (xl & (kSpTableN - 1u))] & 63u;
-      br = X[oTable + (xr & (kSpTableN - 1u))] & 63u;
-      foreign = foreign || (hdl && (xl >= kSpTableN || bl >= Uc || *(const uint32_t*)(X + oUcAct + 4u * bl) != xl)) ||
-                (hdr && (xr >= kSpTableN || br >= Uc || *(const uint32_t*)(X + oUcAct + 4u * br) != xr));
-    }
+    const uint32_t bl = X[kSpTable + (xl & (kSpTableN - 1u))] & 63u, br = X[kSpTable + (xr & (kSpTableN - 1u))] & 63u;
     rXL[rd] = xl; rXR[rd] = xr; rVL[rd] = vl; rVR[rd] = vr; rBL[rd] = bl; rBR[rd] = br; rML[rd] = ml; rMR[rd] = mr;
-    const uint64_t rc = *(const uint64_t*)(X + oUcR + 8u * bl), lc = *(const uint64_t*)(X + oUcL + 8u * br);
+    foreign = foreign || (hdl && (xl >= kSpTableN || bl >= Uc || *(const uint32_t*)(X + kSpUcAct + 4u * bl) != xl)) ||
+              (hdr && (xr >= kSpTableN || br >= Uc || *(const uint32_t*)(X + kSpUcAct + 4u * br) != xr));
+    const uint64_t rc = *(const uint64_t*)(X + kSpUcR + 8u * bl), lc = *(const uint64_t*)(X + kSpUcL + 8u * br);
     const uint64_t mbl = hdl ? 1ull << bl : 0ull, mbr = hdr ? 1ull << br : 0ull;
-    unsigned long long* pl = (unsigned long long*)(X + (hdl ? oMsL + 16u * (ml & 63u) : tr));
-    unsigned long long* pr = (unsigned long long*)(X + (hdr ? oMsR + 16u * (mr & 63u) : tr));
+    unsigned long long* pl = (unsigned long long*)(X + (hdl ? kSpMsL + 16u * (ml & 63u) : tr));
+    unsigned long long* pr = (unsigned long long*)(X + (hdr ? kSpMsR + 16u * (mr & 63u) : tr));
     atomicOr(pl, (unsigned long long)mbl);
-    atomicOr(LN && !hdl ? pl : pl + 1, (unsigned long long)(vl > rc ? mbl : 0ull));  // (LN: an 8-B trash slot)
+    atomicOr(pl + 1, (unsigned long long)(vl > rc ? mbl : 0ull));
     atomicOr(pr, (unsigned long long)mbr);
-    atomicOr(LN && !hdr ? pr : pr + 1, (unsigned long long)(vr > lc ? mbr : 0ull));
+    atomicOr(pr + 1, (unsigned long long)(vr > lc ? mbr : 0ull));
   }
   if (__ballot(foreign) != 0ull) return kLeanFallback;  // a dot actor outside both top clocks
   wave_sync();
-  if (LN) {  // every dot has its rank: the prefix table's words become the equal / >= masks
-    *(u32x4*)(X + oEq + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
-    wave_sync();
-  }
   if (ABL == 9) mark<ABL>(*st, 4);
 #pragma unroll
   for (uint32_t rd = 0; rd < 2u; ++rd) {  // actors on both sides of a shared member: equal / self >= other
@@ -1960,26 +1908,25 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     const bool hdr = dd < dR;
     const uint64_t vr = rVR[rd];
     const uint32_t br = rBR[rd], mr = rMR[rd];
-    const uint32_t u = X[oUofJ + (mr & 63u)] & 63u;
-    const uint32_t d = LN ? (uint32_t) * (const uint16_t*)(X + oDesc + 2u * u) : *(const uint32_t*)(X + oDesc + 4u * u);
-    const uint32_t i = (d >> (LN ? 6 : 8)) & 63u;
-    const uint64_t ML = *(const uint64_t*)(X + oMsL + 16u * i);
-    const bool sh = hdr && (d >> (LN ? 12 : 16)) == kBoth && ((ML >> br) & 1ull);
+    const uint32_t u = X[kSpUofJ + (mr & 63u)] & 63u;
+    const uint32_t d = *(const uint32_t*)(X + kSpDesc + 4u * u);
+    const uint32_t i = (d >> 8) & 63u;
+    const uint64_t ML = *(const uint64_t*)(X + kSpMsL + 16u * i);
+    const bool sh = hdr && (d >> 16) == kBoth && ((ML >> br) & 1ull);
     const uint32_t a0 = i ? ld32(Ls, endL + 4u * i - 4u) : 0u;
     const uint64_t va = ld64(Ls, ctrL + 8u * ((a0 + below64(ML, br)) & 127u));
-    unsigned long long* pe = (unsigned long long*)(X + (sh ? oEq + 16u * u : tr));
+    unsigned long long* pe = (unsigned long long*)(X + (sh ? kSpEq + 16u * u : tr));
     atomicOr(pe, (unsigned long long)(sh && va == vr ? 1ull << br : 0ull));
-    atomicOr(LN && !sh ? pe : pe + 1, (unsigned long long)(sh && va >= vr ? 1ull << br : 0ull));
+    atomicOr(pe + 1, (unsigned long long)(sh && va >= vr ? 1ull << br : 0ull));
   }
   wave_sync();
   if (ABL == 9) mark<ABL>(*st, 5);
   // ---- per union member: mask join (src/orswot.rs:94-138)
   const bool hu = lane < U;
-  const uint32_t dsc = !hu ? 0u : LN ? (uint32_t) * (const uint16_t*)(X + oDesc + 2u * lane)
-                                     : *(const uint32_t*)(X + oDesc + 4u * lane);
-  const uint32_t ty = dsc >> (LN ? 12 : 16), mi = (dsc >> (LN ? 6 : 8)) & 63u, mj = dsc & 63u;
-  const u32x4 pl4 = *(const u32x4*)(X + oMsL + 16u * mi), pr4 = *(const u32x4*)(X + oMsR + 16u * mj);
-  const u32x4 pe4 = *(const u32x4*)(X + oEq + 16u * lane);
+  const uint32_t dsc = hu ? *(const uint32_t*)(X + kSpDesc + 4u * lane) : 0u;
+  const uint32_t ty = dsc >> 16, mi = (dsc >> 8) & 63u, mj = dsc & 63u;
+  const u32x4 pl4 = *(const u32x4*)(X + kSpMsL + 16u * mi), pr4 = *(const u32x4*)(X + kSpMsR + 16u * mj);
+  const u32x4 pe4 = *(const u32x4*)(X + kSpEq + 16u * lane);
   const uint64_t zl = ((uint64_t)pl4.y << 32) | pl4.x, zfl = ((uint64_t)pl4.w << 32) | pl4.z;
   const uint64_t zr = ((uint64_t)pr4.y << 32) | pr4.x, zfr = ((uint64_t)pr4.w << 32) | pr4.z;
   const uint64_t ML = (ty & kSelf) ? zl : 0ull, FL = (ty & kSelf) ? zfl : 0ull;
@@ -1998,8 +1945,8 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     DL.v = make_rv(layout_at(Ls));
     DR.v = make_rv(layout_at(Rs));
     wave_sync();
-    *(uint64_t*)(X + oOut + 32u * lane) = keep;
-    *(uint64_t*)(X + oOut + 32u * lane + 8u) = useK;
+    *(uint64_t*)(X + kSpOut + 32u * lane) = keep;
+    *(uint64_t*)(X + kSpOut + 32u * lane + 8u) = useK;
     wave_sync();
 #pragma unroll
     for (uint32_t rd = 0; rd < 2u; ++rd) {
@@ -2009,14 +1956,14 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
       const uint32_t xl = rXL[rd], xr = rXR[rd], bl = rBL[rd], br = rBR[rd], ml = rML[rd], mr = rMR[rd];
       const uint64_t vl = rVL[rd], vr = rVR[rd];
       if (hdl) {
-        unsigned long long* ok = (unsigned long long*)(X + oOut + 32u * X[oUofI + (ml & 63u)]);
+        unsigned long long* ok = (unsigned long long*)(X + kSpOut + 32u * X[kSpUofI + (ml & 63u)]);
         if ((ok[1] >> bl) & 1ull) {
           const uint64_t mk = dmask_of(DL, DR, ld64(Ls, keyL + 8u * (ml & 63u)));
           if (mk && dkilled(DL, DR, mk, xl, vl)) atomicAnd(ok, ~(1ull << bl));
         }
       }
       if (hdr) {
-        unsigned long long* ok = (unsigned long long*)(X + oOut + 32u * X[oUofJ + (mr & 63u)]);
+        unsigned long long* ok = (unsigned long long*)(X + kSpOut + 32u * X[kSpUofJ + (mr & 63u)]);
         if (((ok[0] & ~ok[1]) >> br) & 1ull) {
           const uint64_t mk = dmask_of(DL, DR, ld64(Rs, keyR + 8u * (mr & 63u)));
           if (mk && dkilled(DL, DR, mk, xr, vr)) atomicAnd(ok, ~(1ull << br));
@@ -2024,7 +1971,7 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
       }
     }
     wave_sync();
-    keep = *(const uint64_t*)(X + oOut + 32u * lane);
+    keep = *(const uint64_t*)(X + kSpOut + 32u * lane);
     useK &= keep;
     if (ABL == 9) mark<ABL>(*st, 10);
   }
@@ -2037,7 +1984,7 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   uint32_t nd = 0, ndd = 0, ndm = 0;
   if (ABL == 9) mark<ABL>(*st, 6);
   // survivors cached in the run-head area (free once the head ballots are taken; 64 entries)
-  uint32_t* dcache = (uint32_t*)(X + (LN ? oEq : oHeadL));  // (LN: the equal / >= masks, read by now)
+  uint32_t* dcache = (uint32_t*)(X + kSpHeadL);
   if (HD) deferred_pass_wave<!DN>(DL, DR, A, lane, nd, ndd, ndm, nullptr, dcache);
   if (ABL == 9) mark<ABL>(*st, 8);
   RecLayout OL;
@@ -2053,9 +2000,9 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     const uint64_t kk = c != 0u ? ((ty & kSelf) ? ld64(Ls, keyL + 8u * mi) : ld64(Rs, keyR + 8u * mj)) : 0ull;
     wave_sync();
     O = const_cast<uint8_t*>(Ls);
-    *(uint64_t*)(X + oOut + 32u * lane) = hu ? keep : 0ull;
-    *(uint64_t*)(X + oOut + 32u * lane + 8u) = hu ? useK : 0ull;
-    *(uint32_t*)(X + oOut + 32u * lane + 16u) = d0;
+    *(uint64_t*)(X + kSpOut + 32u * lane) = hu ? keep : 0ull;
+    *(uint64_t*)(X + kSpOut + 32u * lane + 8u) = hu ? useK : 0ull;
+    *(uint32_t*)(X + kSpOut + 32u * lane + 16u) = d0;
     if (c != 0u) {
       const uint32_t midx = mbcnt64(keepm);
       *(uint64_t*)(O + OL.o_key + 8u * midx) = kk;
@@ -2063,9 +2010,9 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     }
   } else {
     wave_sync();
-    *(uint64_t*)(X + oOut + 32u * lane) = hu ? keep : 0ull;
-    *(uint64_t*)(X + oOut + 32u * lane + 8u) = hu ? useK : 0ull;
-    *(uint32_t*)(X + oOut + 32u * lane + 16u) = d0;
+    *(uint64_t*)(X + kSpOut + 32u * lane) = hu ? keep : 0ull;
+    *(uint64_t*)(X + kSpOut + 32u * lane + 8u) = hu ? useK : 0ull;
+    *(uint32_t*)(X + kSpOut + 32u * lane + 16u) = d0;
     if (c != 0u) {
       const uint32_t midx = mbcnt64(keepm);
       const uint64_t kk = (ty & kSelf) ? ld64(Ls, keyL + 8u * mi) : ld64(Rs, keyR + 8u * mj);
@@ -2080,9 +2027,9 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     }
   } else {
     if (lane < Uc) {  // top clock: the union list, pointwise max (src/orswot.rs:153)
-      const uint64_t a = *(const uint64_t*)(X + oUcL + 8u * lane), b = *(const uint64_t*)(X + oUcR + 8u * lane);
+      const uint64_t a = *(const uint64_t*)(X + kSpUcL + 8u * lane), b = *(const uint64_t*)(X + kSpUcR + 8u * lane);
       *(uint64_t*)(O + kHdrBytes + 8u * lane) = a > b ? a : b;
-      *(uint32_t*)(O + kHdrBytes + 8u * Uc + 4u * lane) = *(const uint32_t*)(X + oUcAct + 4u * lane);
+      *(uint32_t*)(O + kHdrBytes + 8u * Uc + 4u * lane) = *(const uint32_t*)(X + kSpUcAct + 4u * lane);
     }
     if (lane == 0u && (Uc & 1u)) *(uint32_t*)(O + kHdrBytes + 12u * Uc) = 0u;  // clock section pad to 8
   }
@@ -2097,7 +2044,7 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     const uint32_t xl = rXL[rd], xr = rXR[rd], bl = rBL[rd], br = rBR[rd], ml = rML[rd], mr = rMR[rd];
     const uint64_t vl = rVL[rd], vr = rVR[rd];
     if (hdl) {
-      const uint8_t* ob = X + oOut + 32u * X[oUofI + (ml & 63u)];
+      const uint8_t* ob = X + kSpOut + 32u * X[kSpUofI + (ml & 63u)];
       const uint64_t k = *(const uint64_t*)ob, ua = *(const uint64_t*)(ob + 8);
       if ((ua >> bl) & 1ull) {
         const uint32_t idx = *(const uint32_t*)(ob + 16) + below64(k, bl);
@@ -2106,7 +2053,7 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
       }
     }
     if (hdr) {
-      const uint8_t* ob = X + oOut + 32u * X[oUofJ + (mr & 63u)];
+      const uint8_t* ob = X + kSpOut + 32u * X[kSpUofJ + (mr & 63u)];
       const uint64_t k = *(const uint64_t*)ob, ua = *(const uint64_t*)(ob + 8);
       if (((k & ~ua) >> br) & 1ull) {
         const uint32_t idx = *(const uint32_t*)(ob + 16) + below64(k, br);
@@ -2170,6 +2117,10 @@ __device__ __forceinline__ uint32_t below128(uint64_t lo, uint64_t hi, uint32_t 
   return b < 64u ? below64(lo, b) : (uint32_t)__popcll(lo) + below64(hi, b - 64u);
 }
 __device__ __forceinline__ uint64_t ldm64(const uint8_t* X, uint32_t off) { return *(const uint64_t*)(X + off); }
+// bits [0, n) of a word (n as a signed count: <= 0 -> none, >= 64 -> all)
+__device__ __forceinline__ uint64_t lowmask64(uint32_t n) {
+  return (int32_t)n <= 0 ? 0ull : n >= 64u ? ~0ull : (1ull << n) - 1ull;
+}
 
 template <bool HD>
 __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* X, uint8_t* O,
@@ -3356,7 +3307,6 @@ __device__ __forceinline__ bool sparse_header_ok(u32x4 h0, u32x4 h1, uint64_t of
 // flagged and listed for orswot_sparse_general_kernel.
 constexpr uint32_t kSpPair = 6144;
 constexpr uint32_t kSpPer = kSpPair / 16 / kWave;
-constexpr uint32_t kSpPairLn = 5120;  // LN: 5 KB + 5 KB of LDS per wave, 4 four-wave blocks per CU
 
 template <uint32_t PER = kSpPer>
 __device__ __forceinline__ void prefetch_pair(u32x4 (&r)[PER], const uint8_t* L, const uint8_t* R, uint32_t nl,
@@ -3377,19 +3327,14 @@ __device__ __forceinline__ void stage_pair(u32x4* dst, const u32x4 (&r)[PER], ui
 
 // DN: dense batches of 65..1024 actors (sparse_mask_object's DN form; the
 // clock union of an object must have <= 64 actors, else the general kernel)
-// LN: the lean scratch and a 5 KB pair stage (CSR batches; pairs past it to
-// the sparse general kernel)
-template <int MINW, int ABL = 0, uint32_t DYN = 0, uint32_t SF = 5, bool SASM = false, bool DN = false,
-          bool LN = false>  // ABL 9: phase stamps into the list buffer (no general path)
+template <int MINW, int ABL = 0, uint32_t DYN = 0, uint32_t SF = 5, bool SASM = false, bool DN = false>  // ABL 9: phase stamps into the list buffer (no general path)
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_mask_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
     uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
     int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
-  static_assert(!(LN && DN), "LN: CSR batches");
-  constexpr uint32_t PAIR = LN ? kSpPairLn : kSpPair, PER = PAIR / 16 / kWave;
-  __shared__ u32x4 pair_s[kWavesPerBlock][PAIR / 16];
-  __shared__ u32x4 scr_s[kWavesPerBlock][(LN ? kSpScratchLn : kSpScratch) / 16];
+  __shared__ u32x4 pair_s[kWavesPerBlock][kSpPair / 16];
+  __shared__ u32x4 scr_s[kWavesPerBlock][kSpScratch / 16];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wave = threadIdx.x / kWave;
   u32x4* const S = pair_s[wave];
@@ -3427,7 +3372,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
     const bool placed = !ok || (nlo >= lo + hl0.x && nro >= ro + hr0.x);  // as in orswot_mask_kernel
     if (__ballot(!placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_EINVAL);
     ok = ok && placed;
-    const bool fast = ok && hl0.x + hr0.x <= PAIR && A <= kSpTableN && (DN || (hl0.y <= 64u && hr0.y <= 64u)) &&
+    const bool fast = ok && hl0.x + hr0.x <= kSpPair && A <= kSpTableN && (DN || (hl0.y <= 64u && hr0.y <= 64u)) &&
                       hl0.z <= 64u && hr0.z <= 64u && hl0.w <= 128u && hr0.w <= 128u && hl1.x <= 32u &&
                       hr1.x <= 32u;
     if (valid) Ooff[obj] = (lo + ro) | ((ok && !fast) ? kPending : 0ull);
@@ -3444,15 +3389,15 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
     const uint64_t defs = __ballot(fast && (hl1.x | hr1.x) != 0u);
     uint32_t t = (uint32_t)__builtin_ctzll(pend);
     uint64_t fbm = 0ull;  // the chunk's objects the join left (kLeanFallback)
-    u32x4 pf[PER];
+    u32x4 pf[kSpPer];
     uint32_t nn = lane_of(n16, t);
-    prefetch_pair<PER>(pf, Lb + lane_of64(lo, t), Rb + lane_of64(ro, t), nn & 0xFFFFu, nn >> 16, lane);
+    prefetch_pair(pf, Lb + lane_of64(lo, t), Rb + lane_of64(ro, t), nn & 0xFFFFu, nn >> 16, lane);
     while (pend) {
       t = (uint32_t)__builtin_ctzll(pend);
       pend &= pend - 1;
       nn = lane_of(n16, t);
       wave_sync();  // previous object's LDS reads are done
-      stage_pair<PER>(S, pf, lane);
+      stage_pair(S, pf, lane);
       wave_sync();
       mark<ABL>(st, 0);
       const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
@@ -3460,18 +3405,18 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
       if (pend) {
         const uint32_t u = (uint32_t)__builtin_ctzll(pend);
         const uint32_t nu = lane_of(n16, u);
-        prefetch_pair<PER>(pf, Lb + lane_of64(lo, u), Rb + lane_of64(ro, u), nu & 0xFFFFu, nu >> 16, lane);
+        prefetch_pair(pf, Lb + lane_of64(lo, u), Rb + lane_of64(ro, u), nu & 0xFFFFu, nu >> 16, lane);
       }
       mark<ABL>(st, 1);
       const uint8_t* Ls = (const uint8_t*)S;
       const uint8_t* Rs = Ls + 16u * (nn & 0xFFFFu);
       uint32_t r;
       if ((defs >> t) & 1ull)
-        r = sparse_mask_object<true, ABL, false, DN, LN>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu, d & 0xFFFFu,
-                                                         c >> 16, m >> 16, d >> 16, lane, &st);
+        r = sparse_mask_object<true, ABL, false, DN>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu, d & 0xFFFFu,
+                                                     c >> 16, m >> 16, d >> 16, lane, &st);
       else
-        r = sparse_mask_object<false, ABL, SASM && !DN, DN, LN>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu,
-                                                                d & 0xFFFFu, c >> 16, m >> 16, d >> 16, lane, &st);
+        r = sparse_mask_object<false, ABL, SASM && !DN, DN>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu,
+                                                            d & 0xFFFFu, c >> 16, m >> 16, d >> 16, lane, &st);
       if (DN && r == kLeanFallback)  // a union of 65..128 present actors: the 128-bit form on the same stage
         r = (defs >> t) & 1ull ? wide_mask_object<true>(Ls, Rs, X, Ob + oo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16,
                                                         d >> 16, lane)
@@ -3827,8 +3772,6 @@ int launch_orswot_merge_sparse(const uint8_t* Lb, const uint64_t* Loff, uint64_t
                    : sparse_variant == 9 ? (const void*)orswot_sparse_mask_kernel<3, 0, 12, 5>
                    : sparse_variant == 10 ? (const void*)orswot_sparse_mask_kernel<3>  // r02e: static split
                    : sparse_variant == 11 ? (const void*)orswot_sparse_mask_kernel<3, 0, 16, 5, true>  // r04: + SASM
-                   : sparse_variant == 12 ? (const void*)orswot_sparse_mask_kernel<4, 0, 16, 5, false, false, true>  // r06: LN
-                   : sparse_variant == 13 ? (const void*)orswot_sparse_mask_kernel<3, 0, 16, 5, false, false, true>
                                         : (const void*)orswot_sparse_mask_kernel<3, 0, 16, 5>;
 #else
   sparse_variant = 0;
