@@ -1749,18 +1749,13 @@ __device__ __forceinline__ uint32_t rank32(const uint8_t* b, uint32_t off, uint3
 // with 16-B stores, instead of scattered 4- / 8-B stores to HBM (as mask3's
 // OUT 2 does for the dense join); with O == nullptr it stays in the stage
 // (the fused fold's accumulator)
-// DN (dense top clocks of 65..1024 actors, ncL = ncR = A): the clock union is
-// the set of actors with a non-zero counter on either side (a dense clock
-// stores 0 for an absent actor, src/vclock.rs:159-163), built from the rows
-// 64 actors per round; the joined top clock is written dense (pointwise max
-// of the rows, src/orswot.rs:153) and the record keeps the dense form.
-template <bool HD, int ABL = 0, bool ASM = false, bool DN = false>
+// (Dense top clocks of 65..1 024 actors take wide_mask_object, below.)
+template <bool HD, int ABL = 0, bool ASM = false>
 __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* X, uint8_t* O,
                                                        uint32_t A, uint32_t ncL, uint32_t nL, uint32_t dL,
                                                        uint32_t ncR, uint32_t nR, uint32_t dR, uint32_t lane,
                                                        Stamps* st = nullptr) {
-  static_assert(!(DN && ASM), "DN: direct stores");
-  const uint32_t keyL = kHdrBytes + clock_bytes(ncL, !DN), keyR = kHdrBytes + clock_bytes(ncR, !DN);
+  const uint32_t keyL = kHdrBytes + clock_bytes(ncL, true), keyR = kHdrBytes + clock_bytes(ncR, true);
   const uint32_t caL = kHdrBytes + 8u * ncL, caR = kHdrBytes + 8u * ncR;  // clock actor lists (CSR)
   const uint32_t ctrL = keyL + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
   const uint32_t ctrR = keyR + 8u * nR, actR = ctrR + 8u * dR, endR = actR + 4u * dR;
@@ -1768,24 +1763,14 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
 
   // ---- union of the two top clocks: an actor's union position is the
   // number of union-bitmap bits below it (both sides agree on a common actor)
-  const bool hcl = !DN && lane < ncL, hcr = !DN && lane < ncR;
-  const uint32_t cxl = DN ? 0u : ld32(Ls, caL + 4u * lane), cxr = DN ? 0u : ld32(Rs, caR + 4u * lane);
-  const uint64_t cvl = DN ? 0ull : ld64(Ls, kHdrBytes + 8u * lane), cvr = DN ? 0ull : ld64(Rs, kHdrBytes + 8u * lane);
-  if (!DN && __ballot((hcl && cxl >= kSpTableN) || (hcr && cxr >= kSpTableN)) != 0ull) return kLeanFallback;
+  const bool hcl = lane < ncL, hcr = lane < ncR;
+  const uint32_t cxl = ld32(Ls, caL + 4u * lane), cxr = ld32(Rs, caR + 4u * lane);
+  const uint64_t cvl = ld64(Ls, kHdrBytes + 8u * lane), cvr = ld64(Rs, kHdrBytes + 8u * lane);
+  if (__ballot((hcl && cxl >= kSpTableN) || (hcr && cxr >= kSpTableN)) != 0ull) return kLeanFallback;
   wave_sync();  // the previous object's readers of this scratch are done
-  if (DN) {  // one bitmap word per 64 actors: lane a of round q <-> actor 64 q + a (words past A stay 0)
-    if (lane < kSpTableN / 64u) *(uint64_t*)(X + kSpUbm + 8u * lane) = 0ull;
-    for (uint32_t q = 0; q < (A + 63u) / 64u; ++q) {
-      const uint32_t a = 64u * q + lane;
-      const bool p = a < A && (ld64(Ls, kHdrBytes + 8u * a) | ld64(Rs, kHdrBytes + 8u * a)) != 0ull;
-      const uint64_t w = __ballot(p);
-      if (lane == 0u) *(uint64_t*)(X + kSpUbm + 8u * q) = w;
-    }
-  } else {
-    if (lane < kSpTableN / 64u) *(uint64_t*)(X + kSpUbm + 8u * lane) = 0ull;
-    atomicOr((unsigned long long*)(X + (hcl ? kSpUbm + 8u * (cxl >> 6) : tr)), 1ull << (cxl & 63u));
-    atomicOr((unsigned long long*)(X + (hcr ? kSpUbm + 8u * (cxr >> 6) : tr)), 1ull << (cxr & 63u));
-  }
+  if (lane < kSpTableN / 64u) *(uint64_t*)(X + kSpUbm + 8u * lane) = 0ull;
+  atomicOr((unsigned long long*)(X + (hcl ? kSpUbm + 8u * (cxl >> 6) : tr)), 1ull << (cxl & 63u));
+  atomicOr((unsigned long long*)(X + (hcr ? kSpUbm + 8u * (cxr >> 6) : tr)), 1ull << (cxr & 63u));
   wave_sync();
   const uint64_t bw = lane < kSpTableN / 64u ? *(const uint64_t*)(X + kSpUbm + 8u * lane) : 0ull;
   const uint32_t bpc = (uint32_t)__popcll(bw), bin = scan_incl(bpc);
@@ -1825,26 +1810,12 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
 
   wave_sync();  // the previous object's readers of this scratch are done
   // union clock entries (each side its own counter) + actor table
-  if (DN) {  // every present actor, round by round: its union position from the prefix table
-    for (uint32_t q = 0; q < (A + 63u) / 64u; ++q) {
-      const uint32_t a = 64u * q + lane;
-      const uint64_t l = a < A ? ld64(Ls, kHdrBytes + 8u * a) : 0ull, r = a < A ? ld64(Rs, kHdrBytes + 8u * a) : 0ull;
-      const u32x4 pw = *(const u32x4*)(X + kSpUpre + 16u * q);
-      const uint32_t u = pw.z + below64(((uint64_t)pw.y << 32) | pw.x, lane);
-      const bool p = (l | r) != 0ull;
-      *(uint32_t*)(X + (p ? kSpUcAct + 4u * (u & 63u) : tr)) = a;
-      *(uint64_t*)(X + (p ? kSpUcL + 8u * (u & 63u) : tr)) = l;
-      *(uint64_t*)(X + (p ? kSpUcR + 8u * (u & 63u) : tr)) = r;
-      X[p ? kSpTable + a : tr] = (uint8_t)u;
-    }
-  } else {
-    *(uint32_t*)(X + (hcl ? kSpUcAct + 4u * (ucl & 63u) : tr)) = cxl;
-    *(uint64_t*)(X + (hcl ? kSpUcL + 8u * (ucl & 63u) : tr)) = cvl;
-    X[hcl ? kSpTable + cxl : tr] = (uint8_t)ucl;
-    *(uint32_t*)(X + (hcr ? kSpUcAct + 4u * (ucr & 63u) : tr)) = cxr;
-    *(uint64_t*)(X + (hcr ? kSpUcR + 8u * (ucr & 63u) : tr)) = cvr;
-    X[hcr ? kSpTable + cxr : tr] = (uint8_t)ucr;
-  }
+  *(uint32_t*)(X + (hcl ? kSpUcAct + 4u * (ucl & 63u) : tr)) = cxl;
+  *(uint64_t*)(X + (hcl ? kSpUcL + 8u * (ucl & 63u) : tr)) = cvl;
+  X[hcl ? kSpTable + cxl : tr] = (uint8_t)ucl;
+  *(uint32_t*)(X + (hcr ? kSpUcAct + 4u * (ucr & 63u) : tr)) = cxr;
+  *(uint64_t*)(X + (hcr ? kSpUcR + 8u * (ucr & 63u) : tr)) = cvr;
+  X[hcr ? kSpTable + cxr : tr] = (uint8_t)ucr;
   // member masks (zeroed), run heads, descriptors
   *(u32x4*)(X + kSpMsL + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
   *(u32x4*)(X + kSpMsR + 16u * lane) = u32x4{0u, 0u, 0u, 0u};
@@ -1985,10 +1956,10 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
   if (ABL == 9) mark<ABL>(*st, 6);
   // survivors cached in the run-head area (free once the head ballots are taken; 64 entries)
   uint32_t* dcache = (uint32_t*)(X + kSpHeadL);
-  if (HD) deferred_pass_wave<!DN>(DL, DR, A, lane, nd, ndd, ndm, nullptr, dcache);
+  if (HD) deferred_pass_wave<true>(DL, DR, A, lane, nd, ndd, ndm, nullptr, dcache);
   if (ABL == 9) mark<ABL>(*st, 8);
   RecLayout OL;
-  rec_layout(OL, DN ? A : Uc, tot_mem, tot_dot, nd, ndd, ndm, !DN);
+  rec_layout(OL, Uc, tot_mem, tot_dot, nd, ndd, ndm, true);
   const uint32_t size = OL.size;
   const uint32_t d0 = cincl - c;
   if (ABL == 9) mark<ABL>(*st, 6);
@@ -2020,19 +1991,12 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
       *(uint32_t*)(O + OL.o_mdend + 4u * midx) = d0 + c;
     }
   }
-  if (DN) {  // top clock: dense, pointwise max of the rows (src/orswot.rs:153)
-    for (uint32_t a = lane; a < A; a += kWave) {
-      const uint64_t l = ld64(Ls, kHdrBytes + 8u * a), r = ld64(Rs, kHdrBytes + 8u * a);
-      *(uint64_t*)(O + kHdrBytes + 8u * a) = l > r ? l : r;
-    }
-  } else {
-    if (lane < Uc) {  // top clock: the union list, pointwise max (src/orswot.rs:153)
-      const uint64_t a = *(const uint64_t*)(X + kSpUcL + 8u * lane), b = *(const uint64_t*)(X + kSpUcR + 8u * lane);
-      *(uint64_t*)(O + kHdrBytes + 8u * lane) = a > b ? a : b;
-      *(uint32_t*)(O + kHdrBytes + 8u * Uc + 4u * lane) = *(const uint32_t*)(X + kSpUcAct + 4u * lane);
-    }
-    if (lane == 0u && (Uc & 1u)) *(uint32_t*)(O + kHdrBytes + 12u * Uc) = 0u;  // clock section pad to 8
+  if (lane < Uc) {  // top clock: the union list, pointwise max (src/orswot.rs:153)
+    const uint64_t a = *(const uint64_t*)(X + kSpUcL + 8u * lane), b = *(const uint64_t*)(X + kSpUcR + 8u * lane);
+    *(uint64_t*)(O + kHdrBytes + 8u * lane) = a > b ? a : b;
+    *(uint32_t*)(O + kHdrBytes + 8u * Uc + 4u * lane) = *(const uint32_t*)(X + kSpUcAct + 4u * lane);
   }
+  if (lane == 0u && (Uc & 1u)) *(uint32_t*)(O + kHdrBytes + 12u * Uc) = 0u;  // clock section pad to 8
   wave_sync();
   uint32_t* oact = (uint32_t*)(O + OL.o_dact);
   uint64_t* octr = (uint64_t*)(O + OL.o_dctr);
@@ -2067,15 +2031,15 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
     DefOut w{(uint64_t*)(O + OL.o_fctr), (uint64_t*)(O + OL.o_fkey), (uint32_t*)(O + OL.o_fact),
              (uint32_t*)(O + OL.o_fdend), (uint32_t*)(O + OL.o_fmend)};
     wave_sync();
-    deferred_pass_wave<!DN>(DL, DR, A, lane, nd, ndd, ndm, &w, dcache, nd);
+    deferred_pass_wave<true>(DL, DR, A, lane, nd, ndd, ndm, &w, dcache, nd);
   }
   if (ABL == 9) mark<ABL>(*st, 9);
   if (lane == 0u && OL.o_def != OL.o_mpad) *(uint32_t*)(O + OL.o_mpad) = 0u;
   if (lane >= 1u && lane < 4u && OL.o_end + 4u * (lane - 1u) < size) *(uint32_t*)(O + OL.o_end + 4u * (lane - 1u)) = 0u;
   if (lane == 0u) {
     u32x4* h = (u32x4*)O;
-    h[0] = u32x4{size, DN ? A : Uc, tot_mem, tot_dot};
-    h[1] = u32x4{nd, ndd, ndm, DN ? 0u : kSparseClock};
+    h[0] = u32x4{size, Uc, tot_mem, tot_dot};
+    h[1] = u32x4{nd, ndd, ndm, kSparseClock};
   }
   if (ASM && O_ != nullptr) {  // the assembled record out of the stage: 16-B coalesced non-temporal stores
     wave_sync();
@@ -2086,19 +2050,21 @@ __device__ __forceinline__ uint32_t sparse_mask_object(const uint8_t* Ls, const 
 }
 
 // ======================================================================
-// Wide dense join: sparse_mask_object's DN form for objects whose union of
-// present actors holds 65..128 actors (the DN mask kernel leaves them; its
-// masks are 64-bit). Actor masks are 128-bit, two words (word b >> 6, bit
-// b & 63); an actor's rank is read from the union bitmap's prefix table (a
-// dense dot actor is in the union iff its bitmap bit is set, so no actor
-// table), and the other side's counter at a dot's actor from its dense row.
+// Dense-wide join (dense top clocks of 65..1 024 actors): the mask join over
+// each object's union of PRESENT actors (a dense clock stores 0 for an absent
+// actor, src/vclock.rs:159-163), W words of actor masks: W = 1 for a union of
+// <= 64 actors, W = 2 (word b >> 6, bit b & 63) for 65..128. An actor's rank
+// is read from the union bitmap's prefix table (a dense dot actor is in the
+// union iff its bitmap bit is set, so no actor table and no union clock
+// lists), the other side's counter at a dot's actor from its dense row, and
+// the joined top clock is written dense (pointwise max, src/orswot.rs:153).
 // Same rules as mask_object (src/orswot.rs:94-138; apply_deferred
 // :235-243 -> apply_remove :195-211); members <= 64 per side and in the
 // union, dots <= 128 per side, deferred clocks <= 32 per side.
 // ======================================================================
-// scratch byte offsets (per wave; fits the sparse join's kSpScratch, so the
-// DN mask kernel runs it on its own scratch): member masks {M, F} x 128 bit
-// per member; the per-union-member {keep, useK, d0} (48 B) over them once
+// scratch byte offsets (per wave, laid out for W = 2; fits the sparse join's
+// kSpScratch): member masks {M, F} of W words per member; the
+// per-union-member {keep, useK, d0} (48 B; W = 1: 32) over them once
 // they are read, the deferred walk's survivor cache after it; the union
 // bitmap's prefix table over the equal / >= masks until the dots have their
 // ranks; run heads as bits (2 words per side); u16 union descriptors; an
@@ -2122,7 +2088,7 @@ __device__ __forceinline__ uint64_t lowmask64(uint32_t n) {
   return (int32_t)n <= 0 ? 0ull : n >= 64u ? ~0ull : (1ull << n) - 1ull;
 }
 
-template <bool HD>
+template <bool HD, uint32_t W = 2>
 __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const uint8_t* Rs, uint8_t* X, uint8_t* O,
                                                      uint32_t A, uint32_t nL, uint32_t dL, uint32_t nR, uint32_t dR,
                                                      uint32_t lane) {
@@ -2130,6 +2096,10 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
   const uint32_t ctrL = keyL + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
   const uint32_t ctrR = keyR + 8u * nR, actR = ctrR + 8u * dR, endR = actR + 4u * dR;
   const uint32_t tr = kWdTrash + 8u * lane;
+  static_assert(W == 1u || W == 2u, "64- or 128-bit actor masks");
+  // per member: {M, F} of W words; per union member: {EQ, GE} of W words,
+  // then {keep, useK, d0} over the member masks
+  constexpr uint32_t MS = 16u * W, OS = W == 2u ? kWdOutStride : 32u;
 
   // ---- union of present actors (a dense clock stores 0 for an absent
   // actor, src/vclock.rs:159-163): lane q keeps bitmap word q (actors 64 q ..)
@@ -2142,7 +2112,7 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
   }
   const uint32_t bpc = (uint32_t)__popcll(bw), bin = scan_incl(bpc);
   const uint32_t Uc = lane_of(bin, kSpTableN / 64u - 1u);
-  if (Uc > 2u * kWave) return kLeanFallback;
+  if (Uc > W * kWave) return kLeanFallback;
 
   // ---- members (as mask_object); dots in rounds of 64 (<= 128 per side)
   const bool hml = lane < nL, hmr = lane < nR;
@@ -2169,10 +2139,11 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
   if (lane < kSpTableN / 64u)
     *(u32x4*)(X + kWdUpre + 16u * lane) = u32x4{(uint32_t)bw, (uint32_t)(bw >> 32), bin - bpc, 0u};
   const u32x4 z4{0u, 0u, 0u, 0u};
-  *(u32x4*)(X + kWdMsL + 32u * lane) = z4;
-  *(u32x4*)(X + kWdMsL + 32u * lane + 16u) = z4;
-  *(u32x4*)(X + kWdMsR + 32u * lane) = z4;
-  *(u32x4*)(X + kWdMsR + 32u * lane + 16u) = z4;
+#pragma unroll
+  for (uint32_t q = 0; q < W; ++q) {
+    *(u32x4*)(X + kWdMsL + MS * lane + 16u * q) = z4;
+    *(u32x4*)(X + kWdMsR + MS * lane + 16u * q) = z4;
+  }
   if (lane < 4u) *(uint64_t*)(X + kWdHeads + 8u * lane) = 0ull;
   const uint32_t el0 = ld32(Ls, endL + 4u * lane - 4u), er0 = ld32(Rs, endR + 4u * lane - 4u);
   const uint32_t sl = lane ? el0 : 0u, sr = lane ? er0 : 0u;
@@ -2213,16 +2184,16 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
               (hdr && (xr >= A || ((bwr >> (xrc & 63u)) & 1ull) == 0ull));
     const uint64_t rc = ld64(Rs, kHdrBytes + 8u * xlc), lc = ld64(Ls, kHdrBytes + 8u * xrc);
     const uint64_t mbl = hdl ? 1ull << (bl & 63u) : 0ull, mbr = hdr ? 1ull << (br & 63u) : 0ull;
-    const uint32_t ol = kWdMsL + 32u * (ml & 63u) + 8u * (bl >> 6), orr = kWdMsR + 32u * (mr & 63u) + 8u * (br >> 6);
+    const uint32_t ol = kWdMsL + MS * (ml & 63u) + 8u * (bl >> 6), orr = kWdMsR + MS * (mr & 63u) + 8u * (br >> 6);
     atomicOr((unsigned long long*)(X + (hdl ? ol : tr)), (unsigned long long)mbl);
-    atomicOr((unsigned long long*)(X + (hdl ? ol + 16u : tr)), (unsigned long long)(vl > rc ? mbl : 0ull));
+    atomicOr((unsigned long long*)(X + (hdl ? ol + 8u * W : tr)), (unsigned long long)(vl > rc ? mbl : 0ull));
     atomicOr((unsigned long long*)(X + (hdr ? orr : tr)), (unsigned long long)mbr);
-    atomicOr((unsigned long long*)(X + (hdr ? orr + 16u : tr)), (unsigned long long)(vr > lc ? mbr : 0ull));
+    atomicOr((unsigned long long*)(X + (hdr ? orr + 8u * W : tr)), (unsigned long long)(vr > lc ? mbr : 0ull));
   }
   if (__ballot(foreign) != 0ull) return kLeanFallback;  // a dot actor absent from both top clocks
   wave_sync();  // every dot has its rank: the prefix table's words are free
-  *(u32x4*)(X + kWdEq + 32u * lane) = z4;
-  *(u32x4*)(X + kWdEq + 32u * lane + 16u) = z4;
+#pragma unroll
+  for (uint32_t q = 0; q < W; ++q) *(u32x4*)(X + kWdEq + MS * lane + 16u * q) = z4;
   wave_sync();
 #pragma unroll
   for (uint32_t rd = 0; rd < 2u; ++rd) {  // actors on both sides of a shared member: equal / self >= other
@@ -2233,14 +2204,14 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
     const uint32_t u = X[kWdUofJ + (mr & 63u)] & 63u;
     const uint32_t d = *(const uint16_t*)(X + kWdDesc + 2u * u);
     const uint32_t i = (d >> 6) & 63u;
-    const uint64_t mlo = ldm64(X, kWdMsL + 32u * i), mhi = ldm64(X, kWdMsL + 32u * i + 8u);
+    const uint64_t mlo = ldm64(X, kWdMsL + MS * i), mhi = W == 2u ? ldm64(X, kWdMsL + MS * i + 8u) : 0ull;
     const bool sh = hdr && (d >> 12) == kBoth && bit128(mlo, mhi, br);
     const uint32_t a0 = i ? ld32(Ls, endL + 4u * i - 4u) : 0u;
     const uint64_t va = ld64(Ls, ctrL + 8u * ((a0 + below128(mlo, mhi, br)) & 127u));
-    const uint32_t oe = kWdEq + 32u * u + 8u * (br >> 6);
+    const uint32_t oe = kWdEq + MS * u + 8u * (br >> 6);
     const uint64_t bb = 1ull << (br & 63u);
     atomicOr((unsigned long long*)(X + (sh ? oe : tr)), (unsigned long long)(sh && va == vr ? bb : 0ull));
-    atomicOr((unsigned long long*)(X + (sh ? oe + 16u : tr)), (unsigned long long)(sh && va >= vr ? bb : 0ull));
+    atomicOr((unsigned long long*)(X + (sh ? oe + 8u * W : tr)), (unsigned long long)(sh && va >= vr ? bb : 0ull));
   }
   wave_sync();
   // ---- per union member: mask join (src/orswot.rs:94-138), word by word
@@ -2248,15 +2219,15 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
   const uint32_t dsc = hu ? *(const uint16_t*)(X + kWdDesc + 2u * lane) : 0u;
   const uint32_t ty = dsc >> 12, mi = (dsc >> 6) & 63u, mj = dsc & 63u;
   const bool self_only = ty == kSelf;
-  uint64_t keep[2], useK[2], lpf = 0ull;
+  uint64_t keep[2] = {0ull, 0ull}, useK[2] = {0ull, 0ull}, lpf = 0ull;
 #pragma unroll
-  for (uint32_t w = 0; w < 2u; ++w) {
-    const uint64_t ML = (ty & kSelf) ? ldm64(X, kWdMsL + 32u * mi + 8u * w) : 0ull;
-    const uint64_t FL = (ty & kSelf) ? ldm64(X, kWdMsL + 32u * mi + 16u + 8u * w) : 0ull;
-    const uint64_t MR = (ty & kOther) ? ldm64(X, kWdMsR + 32u * mj + 8u * w) : 0ull;
-    const uint64_t FR = (ty & kOther) ? ldm64(X, kWdMsR + 32u * mj + 16u + 8u * w) : 0ull;
-    const uint64_t EQ = ty == kBoth ? ldm64(X, kWdEq + 32u * lane + 8u * w) : 0ull;
-    const uint64_t GE = ty == kBoth ? ldm64(X, kWdEq + 32u * lane + 16u + 8u * w) : 0ull;
+  for (uint32_t w = 0; w < W; ++w) {
+    const uint64_t ML = (ty & kSelf) ? ldm64(X, kWdMsL + MS * mi + 8u * w) : 0ull;
+    const uint64_t FL = (ty & kSelf) ? ldm64(X, kWdMsL + MS * mi + 8u * W + 8u * w) : 0ull;
+    const uint64_t MR = (ty & kOther) ? ldm64(X, kWdMsR + MS * mj + 8u * w) : 0ull;
+    const uint64_t FR = (ty & kOther) ? ldm64(X, kWdMsR + MS * mj + 8u * W + 8u * w) : 0ull;
+    const uint64_t EQ = ty == kBoth ? ldm64(X, kWdEq + MS * lane + 8u * w) : 0ull;
+    const uint64_t GE = ty == kBoth ? ldm64(X, kWdEq + MS * lane + 8u * W + 8u * w) : 0ull;
     const uint64_t lp = self_only ? ML : (ML & FL), rp = MR & FR;
     const uint64_t useA = (ML & MR & EQ) | (lp & (~rp | GE));
     keep[w] = useA | rp;
@@ -2264,7 +2235,7 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
     lpf |= ML & FL;
   }
 #pragma unroll
-  for (uint32_t w = 0; w < 2u; ++w) {
+  for (uint32_t w = 0; w < W; ++w) {
     keep[w] = (!hu || (self_only && lpf == 0ull)) ? 0ull : keep[w];
     useK[w] &= keep[w];
   }
@@ -2273,8 +2244,9 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
     DL.v = make_rv(layout_at(Ls));
     DR.v = make_rv(layout_at(Rs));
     wave_sync();
-    uint64_t* ow = (uint64_t*)(X + kWdOut + kWdOutStride * lane);
-    ow[0] = keep[0]; ow[1] = keep[1]; ow[2] = useK[0]; ow[3] = useK[1];
+    uint64_t* ow = (uint64_t*)(X + kWdOut + OS * lane);
+    ow[0] = keep[0]; ow[W] = useK[0];
+    if (W == 2u) { ow[1] = keep[1]; ow[3] = useK[1]; }
     wave_sync();
 #pragma unroll
     for (uint32_t rd = 0; rd < 2u; ++rd) {
@@ -2283,15 +2255,15 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
       const bool hdl = d < dL, hdr = d < dR;
       const uint32_t bl = rBL[rd], br = rBR[rd], ml = rML[rd], mr = rMR[rd];
       if (hdl) {
-        unsigned long long* ok = (unsigned long long*)(X + kWdOut + kWdOutStride * X[kWdUofI + (ml & 63u)]);
-        if (bit128(ok[2], ok[3], bl)) {
+        unsigned long long* ok = (unsigned long long*)(X + kWdOut + OS * X[kWdUofI + (ml & 63u)]);
+        if (bit128(ok[W], W == 2u ? ok[3] : 0ull, bl)) {
           const uint64_t mk = dmask_of(DL, DR, ld64(Ls, keyL + 8u * (ml & 63u)));
           if (mk && dkilled(DL, DR, mk, rXL[rd], rVL[rd])) atomicAnd(ok + (bl >> 6), ~(1ull << (bl & 63u)));
         }
       }
       if (hdr) {
-        unsigned long long* ok = (unsigned long long*)(X + kWdOut + kWdOutStride * X[kWdUofJ + (mr & 63u)]);
-        if (bit128(ok[0] & ~ok[2], ok[1] & ~ok[3], br)) {
+        unsigned long long* ok = (unsigned long long*)(X + kWdOut + OS * X[kWdUofJ + (mr & 63u)]);
+        if (bit128(ok[0] & ~ok[W], W == 2u ? ok[1] & ~ok[3] : 0ull, br)) {
           const uint64_t mk = dmask_of(DL, DR, ld64(Rs, keyR + 8u * (mr & 63u)));
           if (mk && dkilled(DL, DR, mk, rXR[rd], rVR[rd])) atomicAnd(ok + (br >> 6), ~(1ull << (br & 63u)));
         }
@@ -2299,7 +2271,7 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
     }
     wave_sync();
     keep[0] = ow[0];
-    keep[1] = ow[1];
+    keep[1] = W == 2u ? ow[1] : 0ull;
     useK[0] &= keep[0];
     useK[1] &= keep[1];
   }
@@ -2319,9 +2291,10 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
   const uint32_t d0 = cincl - c;
   wave_sync();
   {
-    uint64_t* ow = (uint64_t*)(X + kWdOut + kWdOutStride * lane);
-    ow[0] = keep[0]; ow[1] = keep[1]; ow[2] = useK[0]; ow[3] = useK[1];
-    *(uint32_t*)(ow + 4) = d0;
+    uint64_t* ow = (uint64_t*)(X + kWdOut + OS * lane);
+    ow[0] = keep[0]; ow[W] = useK[0];
+    if (W == 2u) { ow[1] = keep[1]; ow[3] = useK[1]; }
+    *(uint32_t*)(ow + 2u * W) = d0;
   }
   if (c != 0u) {
     const uint32_t midx = mbcnt64(keepm);
@@ -2343,17 +2316,19 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
     const bool hdl = d < dL, hdr = d < dR;
     const uint32_t bl = rBL[rd], br = rBR[rd], ml = rML[rd], mr = rMR[rd];
     if (hdl) {
-      const uint64_t* ob = (const uint64_t*)(X + kWdOut + kWdOutStride * X[kWdUofI + (ml & 63u)]);
-      if (bit128(ob[2], ob[3], bl)) {
-        const uint32_t idx = *(const uint32_t*)(ob + 4) + below128(ob[0], ob[1], bl);
+      const uint64_t* ob = (const uint64_t*)(X + kWdOut + OS * X[kWdUofI + (ml & 63u)]);
+      const uint64_t k0 = ob[0], k1 = W == 2u ? ob[1] : 0ull, u0 = ob[W], u1 = W == 2u ? ob[3] : 0ull;
+      if (bit128(u0, u1, bl)) {
+        const uint32_t idx = *(const uint32_t*)(ob + 2u * W) + below128(k0, k1, bl);
         oact[idx] = rXL[rd];
         octr[idx] = rVL[rd];
       }
     }
     if (hdr) {
-      const uint64_t* ob = (const uint64_t*)(X + kWdOut + kWdOutStride * X[kWdUofJ + (mr & 63u)]);
-      if (bit128(ob[0] & ~ob[2], ob[1] & ~ob[3], br)) {
-        const uint32_t idx = *(const uint32_t*)(ob + 4) + below128(ob[0], ob[1], br);
+      const uint64_t* ob = (const uint64_t*)(X + kWdOut + OS * X[kWdUofJ + (mr & 63u)]);
+      const uint64_t k0 = ob[0], k1 = W == 2u ? ob[1] : 0ull, u0 = ob[W], u1 = W == 2u ? ob[3] : 0ull;
+      if (bit128(k0 & ~u0, k1 & ~u1, br)) {
+        const uint32_t idx = *(const uint32_t*)(ob + 2u * W) + below128(k0, k1, br);
         oact[idx] = rXR[rd];
         octr[idx] = rVR[rd];
       }
@@ -3325,8 +3300,8 @@ __device__ __forceinline__ void stage_pair(u32x4* dst, const u32x4 (&r)[PER], ui
   for (uint32_t k = 0; k < PER; ++k) dst[lane + k * kWave] = r[k];
 }
 
-// DN: dense batches of 65..1024 actors (sparse_mask_object's DN form; the
-// clock union of an object must have <= 64 actors, else the general kernel)
+// DN: dense batches of 65..1024 actors (wide_mask_object, 64- then 128-bit
+// masks; a union of > 128 present actors goes to the general kernel)
 template <int MINW, int ABL = 0, uint32_t DYN = 0, uint32_t SF = 5, bool SASM = false, bool DN = false>  // ABL 9: phase stamps into the list buffer (no general path)
 __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_mask_kernel(
     const uint8_t* __restrict__ Lb, const uint64_t* __restrict__ Loff, uint64_t Lbytes,
@@ -3411,17 +3386,21 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
       const uint8_t* Ls = (const uint8_t*)S;
       const uint8_t* Rs = Ls + 16u * (nn & 0xFFFFu);
       uint32_t r;
-      if ((defs >> t) & 1ull)
-        r = sparse_mask_object<true, ABL, false, DN>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu, d & 0xFFFFu,
-                                                     c >> 16, m >> 16, d >> 16, lane, &st);
-      else
-        r = sparse_mask_object<false, ABL, SASM && !DN, DN>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu,
-                                                            d & 0xFFFFu, c >> 16, m >> 16, d >> 16, lane, &st);
-      if (DN && r == kLeanFallback)  // a union of 65..128 present actors: the 128-bit form on the same stage
-        r = (defs >> t) & 1ull ? wide_mask_object<true>(Ls, Rs, X, Ob + oo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16,
-                                                        d >> 16, lane)
-                               : wide_mask_object<false>(Ls, Rs, X, Ob + oo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16,
-                                                         d >> 16, lane);
+      if (DN) {  // dense-wide: 64-bit actor masks, then 128-bit for a union of 65..128 present actors
+        const bool hd = (defs >> t) & 1ull;
+        r = hd ? wide_mask_object<true, 1>(Ls, Rs, X, Ob + oo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane)
+               : wide_mask_object<false, 1>(Ls, Rs, X, Ob + oo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane);
+        if (r == kLeanFallback)  // (on the same stage)
+          r = hd ? wide_mask_object<true, 2>(Ls, Rs, X, Ob + oo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16, lane)
+                 : wide_mask_object<false, 2>(Ls, Rs, X, Ob + oo, A, m & 0xFFFFu, d & 0xFFFFu, m >> 16, d >> 16,
+                                              lane);
+      } else if ((defs >> t) & 1ull) {
+        r = sparse_mask_object<true, ABL>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu, d & 0xFFFFu, c >> 16,
+                                          m >> 16, d >> 16, lane, &st);
+      } else {
+        r = sparse_mask_object<false, ABL, SASM>(Ls, Rs, X, Ob + oo, A, c & 0xFFFFu, m & 0xFFFFu, d & 0xFFFFu,
+                                                 c >> 16, m >> 16, d >> 16, lane, &st);
+      }
       fbm |= r == kLeanFallback ? 1ull << t : 0ull;  // union clock / members > 64 or a foreign dot actor
     }
     // the chunk's fallbacks to the general kernel: flagged and listed with
@@ -3700,8 +3679,9 @@ template <int MINW, int AW, int FL>
 const void* join5_fn() { return (const void*)orswot_join5_kernel<MINW, AW, FL>; }
 template <int MINW, int AW, int FL>
 constexpr auto launch_join5 = launch_join_kernel<join5_fn<MINW, AW, FL>>;
-// dense top clocks of 65..1024 actors: the sparse mask join over the
-// per-object union of present actors (DN), then the dense general kernel
+// dense top clocks of 65..1024 actors: the mask join over the per-object
+// union of present actors (DN: wide_mask_object), orswot_dense_wide_kernel
+// for pairs past its stage, then the dense general kernel
 const void* dense_wide_fn() { return (const void*)orswot_sparse_mask_kernel<3, 0, 16, 5, false, true>; }
 constexpr auto launch_dense_wide = launch_join_kernel<dense_wide_fn, true>;
 }  // namespace
@@ -3722,10 +3702,6 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
     return f(Lb, Loff, Lbytes, Rb, Roff, Rbytes, Ob, Ooff, Obytes, n_obj, n_actors, status, ctl, list, list_cap,
              stream, blocks_per_cu, js);
   };
-  // dense top clocks wider than the 64-bit actor masks (65..1024 actors):
-  // every object whose clock union holds <= 64 present actors takes the
-  // sparse mask join in its dense form (DN), the rest the general kernel
-  // (diag variant 320: every such object to the general kernel, as before)
 #ifdef CRDT_DIAG
   // diagnostic builds: the kernel variants of tools/ (csrc/diag/orswot_variants_diag.inc);
   // variant 0 is the product path below
@@ -3736,8 +3712,8 @@ int launch_orswot_merge(const uint8_t* Lb, const uint64_t* Loff, uint64_t Lbytes
 #endif
   (void)variant;
   // dense top clocks wider than the 64-bit actor masks (65..1024 actors):
-  // every object whose clock union holds <= 64 present actors takes the
-  // sparse mask join in its dense form (DN), the rest the general kernel
+  // every object whose union of present actors holds <= 128 actors takes the
+  // dense-wide mask join (DN), the rest the general kernel
   if (n_actors > 64u && n_actors <= kSpTableN) return go(launch_dense_wide);
   // The product path: orswot_join5_kernel — one pass (mask3_object for every
   // object; those with deferred removes take its HD form, direct stores) at 6
