@@ -2074,6 +2074,12 @@ constexpr uint32_t kWdMsL = 0, kWdMsR = 2048, kWdOut = 0, kWdCache = 3072, kWdEq
 constexpr uint32_t kWdScratch = kWdTrash + 8u * kWave;  // 6 944 B per wave
 static_assert(kWdScratch <= kSpScratch, "the DN mask kernel's scratch holds the wide join's");
 constexpr uint32_t kWdOutStride = 48;
+// W = 1 (64-bit masks): {M, F} 16 B per member, {keep, useK, d0} 32 B per
+// union member, the survivor cache over the equal / >= masks after the join
+constexpr uint32_t kWd1MsR = 1024, kWd1Eq = 2048, kWd1Desc = 3072, kWd1Heads = 3200, kWd1UofI = 3232, kWd1UofJ = 3296,
+                   kWd1Trash = 3360;
+constexpr uint32_t kWd1Scratch = kWd1Trash + 8u * kWave;  // 3 872 B per wave
+static_assert(kWd1Scratch <= kWdScratch, "W = 1 fits the W = 2 scratch");
 
 __device__ __forceinline__ bool bit128(uint64_t lo, uint64_t hi, uint32_t b) {
   return ((b < 64u ? lo : hi) >> (b & 63u)) & 1ull;
@@ -2095,8 +2101,13 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
   const uint32_t keyL = kHdrBytes + 8u * A, keyR = keyL;
   const uint32_t ctrL = keyL + 8u * nL, actL = ctrL + 8u * dL, endL = actL + 4u * dL;
   const uint32_t ctrR = keyR + 8u * nR, actR = ctrR + 8u * dR, endR = actR + 4u * dR;
-  const uint32_t tr = kWdTrash + 8u * lane;
   static_assert(W == 1u || W == 2u, "64- or 128-bit actor masks");
+  // scratch offsets: kWd* (W = 2), or the 3 872-B W = 1 layout (kWd1*)
+  constexpr uint32_t oMsL = kWdMsL, oOut = kWdOut, oMsR = W == 2u ? kWdMsR : kWd1MsR, oEq = W == 2u ? kWdEq : kWd1Eq;
+  constexpr uint32_t oCache = W == 2u ? kWdCache : kWd1Eq, oUpre = W == 2u ? kWdUpre : kWd1Eq, oDesc = W == 2u ? kWdDesc : kWd1Desc;
+  constexpr uint32_t oHeads = W == 2u ? kWdHeads : kWd1Heads, oUofI = W == 2u ? kWdUofI : kWd1UofI;
+  constexpr uint32_t oUofJ = W == 2u ? kWdUofJ : kWd1UofJ, oTrash = W == 2u ? kWdTrash : kWd1Trash;
+  const uint32_t tr = oTrash + 8u * lane;
   // per member: {M, F} of W words; per union member: {EQ, GE} of W words,
   // then {keep, useK, d0} over the member masks
   constexpr uint32_t MS = 16u * W, OS = W == 2u ? kWdOutStride : 32u;
@@ -2137,30 +2148,30 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
 
   wave_sync();  // the previous object's readers of this scratch are done
   if (lane < kSpTableN / 64u)
-    *(u32x4*)(X + kWdUpre + 16u * lane) = u32x4{(uint32_t)bw, (uint32_t)(bw >> 32), bin - bpc, 0u};
+    *(u32x4*)(X + oUpre + 16u * lane) = u32x4{(uint32_t)bw, (uint32_t)(bw >> 32), bin - bpc, 0u};
   const u32x4 z4{0u, 0u, 0u, 0u};
 #pragma unroll
   for (uint32_t q = 0; q < W; ++q) {
-    *(u32x4*)(X + kWdMsL + MS * lane + 16u * q) = z4;
-    *(u32x4*)(X + kWdMsR + MS * lane + 16u * q) = z4;
+    *(u32x4*)(X + oMsL + MS * lane + 16u * q) = z4;
+    *(u32x4*)(X + oMsR + MS * lane + 16u * q) = z4;
   }
-  if (lane < 4u) *(uint64_t*)(X + kWdHeads + 8u * lane) = 0ull;
+  if (lane < 4u) *(uint64_t*)(X + oHeads + 8u * lane) = 0ull;
   const uint32_t el0 = ld32(Ls, endL + 4u * lane - 4u), er0 = ld32(Rs, endR + 4u * lane - 4u);
   const uint32_t sl = lane ? el0 : 0u, sr = lane ? er0 : 0u;
-  *(uint16_t*)(X + (hml ? kWdDesc + 2u * (ul & 63u) : tr)) =
+  *(uint16_t*)(X + (hml ? oDesc + 2u * (ul & 63u) : tr)) =
       (uint16_t)(((eql ? kBoth : kSelf) << 12) | (lane << 6) | (eql ? rl : 0u));
-  *(uint16_t*)(X + ((hmr && !eqr) ? kWdDesc + 2u * (ur & 63u) : tr)) = (uint16_t)((kOther << 12) | ((rr & 63u) << 6) | lane);
-  X[kWdUofI + lane] = (uint8_t)ul;
-  X[kWdUofJ + lane] = (uint8_t)ur;
+  *(uint16_t*)(X + ((hmr && !eqr) ? oDesc + 2u * (ur & 63u) : tr)) = (uint16_t)((kOther << 12) | ((rr & 63u) << 6) | lane);
+  X[oUofI + lane] = (uint8_t)ul;
+  X[oUofJ + lane] = (uint8_t)ur;
   wave_sync();
   // run heads as bits: dot words 0 / 1 of each side (members' first dots)
-  atomicOr((unsigned long long*)(X + ((hml && sl < 128u) ? kWdHeads + 8u * (sl >> 6) : tr)), 1ull << (sl & 63u));
-  atomicOr((unsigned long long*)(X + ((hmr && sr < 128u) ? kWdHeads + 16u + 8u * (sr >> 6) : tr)), 1ull << (sr & 63u));
+  atomicOr((unsigned long long*)(X + ((hml && sl < 128u) ? oHeads + 8u * (sl >> 6) : tr)), 1ull << (sl & 63u));
+  atomicOr((unsigned long long*)(X + ((hmr && sr < 128u) ? oHeads + 16u + 8u * (sr >> 6) : tr)), 1ull << (sr & 63u));
   wave_sync();
   // run-head masks of both rounds; the member of dot 64 r + lane is
   // (#heads at or below it) - 1
-  const uint64_t HL0 = ldm64(X, kWdHeads) & lowmask64(dL), HL1 = ldm64(X, kWdHeads + 8u) & lowmask64(dL - 64u);
-  const uint64_t HR0 = ldm64(X, kWdHeads + 16u) & lowmask64(dR), HR1 = ldm64(X, kWdHeads + 24u) & lowmask64(dR - 64u);
+  const uint64_t HL0 = ldm64(X, oHeads) & lowmask64(dL), HL1 = ldm64(X, oHeads + 8u) & lowmask64(dL - 64u);
+  const uint64_t HR0 = ldm64(X, oHeads + 16u) & lowmask64(dR), HR1 = ldm64(X, oHeads + 24u) & lowmask64(dR - 64u);
   bool foreign = false;
   uint32_t rXL[2] = {0u, 0u}, rXR[2] = {0u, 0u}, rBL[2] = {0u, 0u}, rBR[2] = {0u, 0u};
   uint32_t rML[2] = {0u, 0u}, rMR[2] = {0u, 0u};
@@ -2176,7 +2187,7 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
     const uint32_t ml = (rd ? (uint32_t)__popcll(HL0) : 0u) + mbcnt64(HL) + ((HL >> lane) & 1ull ? 1u : 0u) - 1u;
     const uint32_t mr = (rd ? (uint32_t)__popcll(HR0) : 0u) + mbcnt64(HR) + ((HR >> lane) & 1ull ? 1u : 0u) - 1u;
     const uint32_t xlc = xl < A ? xl : 0u, xrc = xr < A ? xr : 0u;
-    const u32x4 pwl = *(const u32x4*)(X + kWdUpre + 16u * (xlc >> 6)), pwr = *(const u32x4*)(X + kWdUpre + 16u * (xrc >> 6));
+    const u32x4 pwl = *(const u32x4*)(X + oUpre + 16u * (xlc >> 6)), pwr = *(const u32x4*)(X + oUpre + 16u * (xrc >> 6));
     const uint64_t bwl = ((uint64_t)pwl.y << 32) | pwl.x, bwr = ((uint64_t)pwr.y << 32) | pwr.x;
     const uint32_t bl = (pwl.z + below64(bwl, xlc & 63u)) & 127u, br = (pwr.z + below64(bwr, xrc & 63u)) & 127u;
     rXL[rd] = xl; rXR[rd] = xr; rVL[rd] = vl; rVR[rd] = vr; rBL[rd] = bl; rBR[rd] = br; rML[rd] = ml; rMR[rd] = mr;
@@ -2184,7 +2195,7 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
               (hdr && (xr >= A || ((bwr >> (xrc & 63u)) & 1ull) == 0ull));
     const uint64_t rc = ld64(Rs, kHdrBytes + 8u * xlc), lc = ld64(Ls, kHdrBytes + 8u * xrc);
     const uint64_t mbl = hdl ? 1ull << (bl & 63u) : 0ull, mbr = hdr ? 1ull << (br & 63u) : 0ull;
-    const uint32_t ol = kWdMsL + MS * (ml & 63u) + 8u * (bl >> 6), orr = kWdMsR + MS * (mr & 63u) + 8u * (br >> 6);
+    const uint32_t ol = oMsL + MS * (ml & 63u) + 8u * (bl >> 6), orr = oMsR + MS * (mr & 63u) + 8u * (br >> 6);
     atomicOr((unsigned long long*)(X + (hdl ? ol : tr)), (unsigned long long)mbl);
     atomicOr((unsigned long long*)(X + (hdl ? ol + 8u * W : tr)), (unsigned long long)(vl > rc ? mbl : 0ull));
     atomicOr((unsigned long long*)(X + (hdr ? orr : tr)), (unsigned long long)mbr);
@@ -2193,7 +2204,7 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
   if (__ballot(foreign) != 0ull) return kLeanFallback;  // a dot actor absent from both top clocks
   wave_sync();  // every dot has its rank: the prefix table's words are free
 #pragma unroll
-  for (uint32_t q = 0; q < W; ++q) *(u32x4*)(X + kWdEq + MS * lane + 16u * q) = z4;
+  for (uint32_t q = 0; q < W; ++q) *(u32x4*)(X + oEq + MS * lane + 16u * q) = z4;
   wave_sync();
 #pragma unroll
   for (uint32_t rd = 0; rd < 2u; ++rd) {  // actors on both sides of a shared member: equal / self >= other
@@ -2201,14 +2212,14 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
     const bool hdr = 64u * rd + lane < dR;
     const uint64_t vr = rVR[rd];
     const uint32_t br = rBR[rd], mr = rMR[rd];
-    const uint32_t u = X[kWdUofJ + (mr & 63u)] & 63u;
-    const uint32_t d = *(const uint16_t*)(X + kWdDesc + 2u * u);
+    const uint32_t u = X[oUofJ + (mr & 63u)] & 63u;
+    const uint32_t d = *(const uint16_t*)(X + oDesc + 2u * u);
     const uint32_t i = (d >> 6) & 63u;
-    const uint64_t mlo = ldm64(X, kWdMsL + MS * i), mhi = W == 2u ? ldm64(X, kWdMsL + MS * i + 8u) : 0ull;
+    const uint64_t mlo = ldm64(X, oMsL + MS * i), mhi = W == 2u ? ldm64(X, oMsL + MS * i + 8u) : 0ull;
     const bool sh = hdr && (d >> 12) == kBoth && bit128(mlo, mhi, br);
     const uint32_t a0 = i ? ld32(Ls, endL + 4u * i - 4u) : 0u;
     const uint64_t va = ld64(Ls, ctrL + 8u * ((a0 + below128(mlo, mhi, br)) & 127u));
-    const uint32_t oe = kWdEq + MS * u + 8u * (br >> 6);
+    const uint32_t oe = oEq + MS * u + 8u * (br >> 6);
     const uint64_t bb = 1ull << (br & 63u);
     atomicOr((unsigned long long*)(X + (sh ? oe : tr)), (unsigned long long)(sh && va == vr ? bb : 0ull));
     atomicOr((unsigned long long*)(X + (sh ? oe + 8u * W : tr)), (unsigned long long)(sh && va >= vr ? bb : 0ull));
@@ -2216,18 +2227,18 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
   wave_sync();
   // ---- per union member: mask join (src/orswot.rs:94-138), word by word
   const bool hu = lane < U;
-  const uint32_t dsc = hu ? *(const uint16_t*)(X + kWdDesc + 2u * lane) : 0u;
+  const uint32_t dsc = hu ? *(const uint16_t*)(X + oDesc + 2u * lane) : 0u;
   const uint32_t ty = dsc >> 12, mi = (dsc >> 6) & 63u, mj = dsc & 63u;
   const bool self_only = ty == kSelf;
   uint64_t keep[2] = {0ull, 0ull}, useK[2] = {0ull, 0ull}, lpf = 0ull;
 #pragma unroll
   for (uint32_t w = 0; w < W; ++w) {
-    const uint64_t ML = (ty & kSelf) ? ldm64(X, kWdMsL + MS * mi + 8u * w) : 0ull;
-    const uint64_t FL = (ty & kSelf) ? ldm64(X, kWdMsL + MS * mi + 8u * W + 8u * w) : 0ull;
-    const uint64_t MR = (ty & kOther) ? ldm64(X, kWdMsR + MS * mj + 8u * w) : 0ull;
-    const uint64_t FR = (ty & kOther) ? ldm64(X, kWdMsR + MS * mj + 8u * W + 8u * w) : 0ull;
-    const uint64_t EQ = ty == kBoth ? ldm64(X, kWdEq + MS * lane + 8u * w) : 0ull;
-    const uint64_t GE = ty == kBoth ? ldm64(X, kWdEq + MS * lane + 8u * W + 8u * w) : 0ull;
+    const uint64_t ML = (ty & kSelf) ? ldm64(X, oMsL + MS * mi + 8u * w) : 0ull;
+    const uint64_t FL = (ty & kSelf) ? ldm64(X, oMsL + MS * mi + 8u * W + 8u * w) : 0ull;
+    const uint64_t MR = (ty & kOther) ? ldm64(X, oMsR + MS * mj + 8u * w) : 0ull;
+    const uint64_t FR = (ty & kOther) ? ldm64(X, oMsR + MS * mj + 8u * W + 8u * w) : 0ull;
+    const uint64_t EQ = ty == kBoth ? ldm64(X, oEq + MS * lane + 8u * w) : 0ull;
+    const uint64_t GE = ty == kBoth ? ldm64(X, oEq + MS * lane + 8u * W + 8u * w) : 0ull;
     const uint64_t lp = self_only ? ML : (ML & FL), rp = MR & FR;
     const uint64_t useA = (ML & MR & EQ) | (lp & (~rp | GE));
     keep[w] = useA | rp;
@@ -2244,7 +2255,7 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
     DL.v = make_rv(layout_at(Ls));
     DR.v = make_rv(layout_at(Rs));
     wave_sync();
-    uint64_t* ow = (uint64_t*)(X + kWdOut + OS * lane);
+    uint64_t* ow = (uint64_t*)(X + oOut + OS * lane);
     ow[0] = keep[0]; ow[W] = useK[0];
     if (W == 2u) { ow[1] = keep[1]; ow[3] = useK[1]; }
     wave_sync();
@@ -2255,14 +2266,14 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
       const bool hdl = d < dL, hdr = d < dR;
       const uint32_t bl = rBL[rd], br = rBR[rd], ml = rML[rd], mr = rMR[rd];
       if (hdl) {
-        unsigned long long* ok = (unsigned long long*)(X + kWdOut + OS * X[kWdUofI + (ml & 63u)]);
+        unsigned long long* ok = (unsigned long long*)(X + oOut + OS * X[oUofI + (ml & 63u)]);
         if (bit128(ok[W], W == 2u ? ok[3] : 0ull, bl)) {
           const uint64_t mk = dmask_of(DL, DR, ld64(Ls, keyL + 8u * (ml & 63u)));
           if (mk && dkilled(DL, DR, mk, rXL[rd], rVL[rd])) atomicAnd(ok + (bl >> 6), ~(1ull << (bl & 63u)));
         }
       }
       if (hdr) {
-        unsigned long long* ok = (unsigned long long*)(X + kWdOut + OS * X[kWdUofJ + (mr & 63u)]);
+        unsigned long long* ok = (unsigned long long*)(X + oOut + OS * X[oUofJ + (mr & 63u)]);
         if (bit128(ok[0] & ~ok[W], W == 2u ? ok[1] & ~ok[3] : 0ull, br)) {
           const uint64_t mk = dmask_of(DL, DR, ld64(Rs, keyR + 8u * (mr & 63u)));
           if (mk && dkilled(DL, DR, mk, rXR[rd], rVR[rd])) atomicAnd(ok + (br >> 6), ~(1ull << (br & 63u)));
@@ -2283,7 +2294,7 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
   const uint32_t tot_dot = lane_of(cincl, kWave - 1);
   uint32_t nd = 0, ndd = 0, ndm = 0;
   // survivors cached past the {keep, useK, d0} rows (64 entries)
-  uint32_t* dcache = (uint32_t*)(X + kWdCache);
+  uint32_t* dcache = (uint32_t*)(X + oCache);
   if (HD) deferred_pass_wave<false>(DL, DR, A, lane, nd, ndd, ndm, nullptr, dcache);
   RecLayout OL;
   rec_layout(OL, A, tot_mem, tot_dot, nd, ndd, ndm, false);
@@ -2291,7 +2302,7 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
   const uint32_t d0 = cincl - c;
   wave_sync();
   {
-    uint64_t* ow = (uint64_t*)(X + kWdOut + OS * lane);
+    uint64_t* ow = (uint64_t*)(X + oOut + OS * lane);
     ow[0] = keep[0]; ow[W] = useK[0];
     if (W == 2u) { ow[1] = keep[1]; ow[3] = useK[1]; }
     *(uint32_t*)(ow + 2u * W) = d0;
@@ -2316,7 +2327,7 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
     const bool hdl = d < dL, hdr = d < dR;
     const uint32_t bl = rBL[rd], br = rBR[rd], ml = rML[rd], mr = rMR[rd];
     if (hdl) {
-      const uint64_t* ob = (const uint64_t*)(X + kWdOut + OS * X[kWdUofI + (ml & 63u)]);
+      const uint64_t* ob = (const uint64_t*)(X + oOut + OS * X[oUofI + (ml & 63u)]);
       const uint64_t k0 = ob[0], k1 = W == 2u ? ob[1] : 0ull, u0 = ob[W], u1 = W == 2u ? ob[3] : 0ull;
       if (bit128(u0, u1, bl)) {
         const uint32_t idx = *(const uint32_t*)(ob + 2u * W) + below128(k0, k1, bl);
@@ -2325,7 +2336,7 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
       }
     }
     if (hdr) {
-      const uint64_t* ob = (const uint64_t*)(X + kWdOut + OS * X[kWdUofJ + (mr & 63u)]);
+      const uint64_t* ob = (const uint64_t*)(X + oOut + OS * X[oUofJ + (mr & 63u)]);
       const uint64_t k0 = ob[0], k1 = W == 2u ? ob[1] : 0ull, u0 = ob[W], u1 = W == 2u ? ob[3] : 0ull;
       if (bit128(k0 & ~u0, k1 & ~u1, br)) {
         const uint32_t idx = *(const uint32_t*)(ob + 2u * W) + below128(k0, k1, br);
