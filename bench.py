@@ -65,7 +65,7 @@ def parse():
     p.add_argument("--replicas", type=int, default=8, help="orswot_csr at N=1: replicas folded locally")
     p.add_argument("--n-actors", type=int, default=16,
                    help="orswot: dense top-clock actors (config 3: 16; 33-64 take the 64-bit actor-mask join, "
-                        "65-1024 the sparse mask join over each object's present actors)")
+                        "65-1024 the dense-wide mask join over each object's present actors)")
     p.add_argument("--gen-params", default=None,
                    help="orswot: JSON overrides of the op-simulation generator's parameters (crdt_orswot_gen_params), "
                         "e.g. the wide-union distribution of DESIGN.md §11")

@@ -28,8 +28,11 @@ if [ "$PART" = bench ]; then
   tail -1 $OUT/smoke.log
 elif [ "$PART" = prof ]; then
   bash tools/profile.sh $TAG || { echo PROFILE_FAILED; exit 1; }
-  for wl in truncate orswot_tail orswot_csr_tail; do
+  for wl in truncate orswot_tail orswot_csr_tail orswot_csr; do
     bash tools/profile_workload.sh $TAG $wl || { echo PROFILE_WL_FAILED $wl; exit 1; }
   done
+  bash tools/profile_workload.sh ${TAG}_a128 orswot --n-actors 128 || { echo PROFILE_WL_FAILED a128; exit 1; }
+  bash tools/profile_workload.sh ${TAG}_wide orswot --n-actors 128 \
+    --gen-params '{"ancestor_adds":96,"member_universe":32,"pct_add":45,"max_div_ops":20}' || { echo PROFILE_WL_FAILED wide; exit 1; }
 fi
 echo SWEEP_OK
