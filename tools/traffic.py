@@ -27,7 +27,7 @@ KERNELS = {"orswot_join_kernel": ("orswot_join_kernel<", "orswot_join5_kernel<")
            "dense_max_kernel": "dense_max_kernel"}
 # every other kernel of the library is summarised under its own name
 OTHER = ("orswot_apply_kernel", "orswot_sparse_mask_kernel", "orswot_sparse_general_kernel", "bincode_ingest_kernel",
-         "clock_csr_merge_kernel", "orswot_truncate_kernel", "orswot_truncate_fast_kernel", "bincode_decode_big_kernel", "slice_bounds_kernel",
+         "clock_csr_merge_kernel", "orswot_truncate_kernel", "orswot_truncate_fast_kernel", "bincode_decode_big_kernel", "slice_bounds_kernel", "orswot_dense_wide_kernel",
          "bincode_egest_kernel", "bincode_decode_kernel", "bincode_sizes_lane_kernel", "bincode_bounds_kernel", "mvreg_merge_kernel",
          "vclock_cmp_kernel", "map_mvreg_merge_kernel", "map_orswot_merge_kernel", "map_map_outer_kernel", "map_mvreg_truncate_kernel", "validate_kernel", "sizes_kernel", "copy_kernel")
 
