@@ -2114,7 +2114,8 @@ __device__ __forceinline__ uint32_t wide_mask_object(const uint8_t* Ls, const ui
   static_assert(W == 1u || W == 2u, "64- or 128-bit actor masks");
   // scratch offsets: kWd* (W = 2), or the 3 872-B W = 1 layout (kWd1*)
   constexpr uint32_t oMsL = kWdMsL, oOut = kWdOut, oMsR = W == 2u ? kWdMsR : kWd1MsR, oEq = W == 2u ? kWdEq : kWd1Eq;
-  constexpr uint32_t oCache = W == 2u ? kWdCache : kWd1Eq, oUpre = W == 2u ? kWdUpre : kWd1Eq, oDesc = W == 2u ? kWdDesc : kWd1Desc;
+  constexpr uint32_t oCache = W == 2u ? kWdCache : kWd1Eq, oUpre = W == 2u ? kWdUpre : kWd1Eq;
+  constexpr uint32_t oDesc = W == 2u ? kWdDesc : kWd1Desc;
   constexpr uint32_t oHeads = W == 2u ? kWdHeads : kWd1Heads, oUofI = W == 2u ? kWdUofI : kWd1UofI;
   constexpr uint32_t oUofJ = W == 2u ? kWdUofJ : kWd1UofJ, oTrash = W == 2u ? kWdTrash : kWd1Trash;
   const uint32_t tr = oTrash + 8u * lane;
