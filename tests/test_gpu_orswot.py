@@ -539,6 +539,52 @@ def test_dense_wide_union(gpu, oracle):
         gpu.set_list_cap(65536)
 
 
+@pytest.mark.parametrize("U", [63, 64, 65, 127, 128, 129])
+def test_dense_wide_union_boundaries(gpu, oracle, U):
+    """Object pairs whose top clocks hold exactly U present actors between
+    them, at 160 dense actors: the dense-wide join's 64-bit masks up to 64,
+    its 128-bit masks up to 128, the general kernel past 128 — in the DN
+    kernel for pairs within its 6 KB stage (10-55 % of them here) and in
+    orswot_dense_wide_kernel for the larger ones. Shared and one-sided
+    actors, removes through the whole clock (read context) and
+    future-context removes left deferred; byte-exact against the oracle in
+    both orientations (src/orswot.rs:87-157, src/vclock.rs:54-57)."""
+    import crdts_hip
+
+    rng = random.Random(0xB0 + U)
+    A, n = 160, 160
+    L, R = [], []
+    for _ in range(n):
+        acts = rng.sample(range(A), U)
+        ns = rng.randrange(U // 4, U // 2 + 1)
+        shared, rest = acts[:ns], acts[ns:]
+        cut = rng.randrange(len(rest) + 1)
+        for side, dst in ((shared + rest[:cut], L), (shared + rest[cut:], R)):
+            h, clk = crdts_hip.HostOrswot(), {}
+            for a in side:  # every actor of the side in its top clock
+                clk[a] = clk.get(a, 0) + 1
+                h.apply_add(a, clk[a], rng.randrange(24))
+            for _ in range(rng.randrange(0, 30)):
+                a, m, r = rng.choice(side), rng.randrange(24), rng.random()
+                if r < 0.6:
+                    clk[a] += 1
+                    h.apply_add(a, clk[a], m)
+                elif r < 0.85:
+                    h.apply_rm(m, sorted(clk.items()))
+                else:  # a context past the clock: left deferred
+                    h.apply_rm(m, sorted({**clk, a: clk[a] + rng.randrange(1, 4)}.items()))
+            dst.append(h.encode(A))
+    union = [len(set(records.decode(x)["clock"]) | set(records.decode(y)["clock"])) for x, y in zip(L, R)]
+    assert set(union) == {U}
+    assert sum(1 for r in L if records.decode(r)["deferred"]) > n // 10
+    lb, lo = records.pack_batch(L)
+    rb, ro = records.pack_batch(R)
+    for a, b in (((lb, lo), (rb, ro)), ((rb, ro), (lb, lo))):
+        out = _gpu_merge(gpu, *a, *b, A)
+        ob, oo = oracle.orswot_merge_batch(*a, *b, A, threads=16)
+        _compare(out, ob, oo, f"union of {U}")
+
+
 # ------------------------------------------------------------------ heavy-tailed batches
 def test_heavy_tail_100k(gpu, oracle):
     """Config 3 with a heavy tail (bench.py --workload orswot_tail): every 20th
