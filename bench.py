@@ -366,8 +366,10 @@ def run_orswot(args, rank, world, local):
             "kernel": ("orswot_big_kernel<CSR> (+ orswot_sparse_mask_kernel, orswot_sparse_general_kernel in the "
                        "same window)" if csr else
                        "orswot_big_kernel (+ orswot_join5_kernel, orswot_merge_general_kernel in the same window)"
-                       if tail else ("orswot_join5_kernel" if A <= 64 else "orswot_sparse_mask_kernel<DN>")
-                       + " (+ orswot_merge_general_kernel, orswot_big_kernel in the same window)"),
+                       if tail else ("orswot_join5_kernel (+ orswot_merge_general_kernel, orswot_big_kernel in the "
+                                     "same window)" if A <= 64 else
+                                     "orswot_sparse_mask_kernel<DN> (the dense-wide join; + orswot_dense_wide_kernel, "
+                                     "orswot_merge_general_kernel, orswot_big_kernel in the same window)")),
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
