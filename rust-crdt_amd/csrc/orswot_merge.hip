@@ -3304,6 +3304,9 @@ __device__ __forceinline__ bool sparse_header_ok(u32x4 h0, u32x4 h1, uint64_t of
 // flagged and listed for orswot_sparse_general_kernel.
 constexpr uint32_t kSpPair = 6144;
 constexpr uint32_t kSpPer = kSpPair / 16 / kWave;
+// CSR batches: the join's 6 016-B scratch leaves room for a 7 KB pair stage
+// at the same 3 four-wave blocks per CU (the DN kernel keeps 6 KB + 7 040 B)
+constexpr uint32_t kSpPairCsr = 7168, kSpScratchCsr = kSpTrash + 16u * kWave;
 
 template <uint32_t PER = kSpPer>
 __device__ __forceinline__ void prefetch_pair(u32x4 (&r)[PER], const uint8_t* L, const uint8_t* R, uint32_t nl,
@@ -3330,8 +3333,9 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
     const uint8_t* __restrict__ Rb, const uint64_t* __restrict__ Roff, uint64_t Rbytes,
     uint8_t* __restrict__ Ob, uint64_t* __restrict__ Ooff, uint64_t Obytes, uint64_t n_obj, uint32_t A,
     int* __restrict__ status, uint32_t* __restrict__ ctl, uint64_t* __restrict__ list, uint32_t list_cap) {
-  __shared__ u32x4 pair_s[kWavesPerBlock][kSpPair / 16];
-  __shared__ u32x4 scr_s[kWavesPerBlock][kSpScratch / 16];
+  constexpr uint32_t PAIR = DN ? kSpPair : kSpPairCsr, PER = PAIR / 16 / kWave;
+  __shared__ u32x4 pair_s[kWavesPerBlock][PAIR / 16];
+  __shared__ u32x4 scr_s[kWavesPerBlock][(DN ? kSpScratch : kSpScratchCsr) / 16];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wave = threadIdx.x / kWave;
   u32x4* const S = pair_s[wave];
@@ -3369,7 +3373,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
     const bool placed = !ok || (nlo >= lo + hl0.x && nro >= ro + hr0.x);  // as in orswot_mask_kernel
     if (__ballot(!placed) != 0ull && lane == 0) atomicCAS(status, 0, CRDT_EINVAL);
     ok = ok && placed;
-    const bool fast = ok && hl0.x + hr0.x <= kSpPair && A <= kSpTableN && (DN || (hl0.y <= 64u && hr0.y <= 64u)) &&
+    const bool fast = ok && hl0.x + hr0.x <= PAIR && A <= kSpTableN && (DN || (hl0.y <= 64u && hr0.y <= 64u)) &&
                       hl0.z <= 64u && hr0.z <= 64u && hl0.w <= 128u && hr0.w <= 128u && hl1.x <= 32u &&
                       hr1.x <= 32u;
     if (valid) Ooff[obj] = (lo + ro) | ((ok && !fast) ? kPending : 0ull);
@@ -3386,15 +3390,15 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
     const uint64_t defs = __ballot(fast && (hl1.x | hr1.x) != 0u);
     uint32_t t = (uint32_t)__builtin_ctzll(pend);
     uint64_t fbm = 0ull;  // the chunk's objects the join left (kLeanFallback)
-    u32x4 pf[kSpPer];
+    u32x4 pf[PER];
     uint32_t nn = lane_of(n16, t);
-    prefetch_pair(pf, Lb + lane_of64(lo, t), Rb + lane_of64(ro, t), nn & 0xFFFFu, nn >> 16, lane);
+    prefetch_pair<PER>(pf, Lb + lane_of64(lo, t), Rb + lane_of64(ro, t), nn & 0xFFFFu, nn >> 16, lane);
     while (pend) {
       t = (uint32_t)__builtin_ctzll(pend);
       pend &= pend - 1;
       nn = lane_of(n16, t);
       wave_sync();  // previous object's LDS reads are done
-      stage_pair(S, pf, lane);
+      stage_pair<PER>(S, pf, lane);
       wave_sync();
       mark<ABL>(st, 0);
       const uint64_t oo = lane_of64(lo, t) + lane_of64(ro, t);
@@ -3402,7 +3406,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, MINW) void orswot_sparse_ma
       if (pend) {
         const uint32_t u = (uint32_t)__builtin_ctzll(pend);
         const uint32_t nu = lane_of(n16, u);
-        prefetch_pair(pf, Lb + lane_of64(lo, u), Rb + lane_of64(ro, u), nu & 0xFFFFu, nu >> 16, lane);
+        prefetch_pair<PER>(pf, Lb + lane_of64(lo, u), Rb + lane_of64(ro, u), nu & 0xFFFFu, nu >> 16, lane);
       }
       mark<ABL>(st, 1);
       const uint8_t* Ls = (const uint8_t*)S;
